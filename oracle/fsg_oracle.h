@@ -1,0 +1,90 @@
+/*
+ * fsg_oracle.h — CPU ORACLE for the SmartModule record-transform path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is a plain-C restatement of the reference
+ * algorithm (deem0n/fluvio: fluvio-protocol codec, fluvio-smartmodule derive
+ * semantics, fluvio-smartengine chain, fluvio-spu process_batch).  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it, and only
+ * as the checker / the timed CPU baseline — never as the product path.
+ *
+ * Parity pinning: see oracle/README.md and tests/golden/ (KATs transcribed
+ * from the reference's own tests; reference is Rust, unbuildable here).
+ */
+#ifndef FSG_ORACLE_H
+#define FSG_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes — same numeric space as include/fsg.h */
+#define ORC_OK 0
+#define ORC_E_UNKNOWN -1                 /* SmartModuleTransformErrorStatus::UnknownError */
+#define ORC_E_INIT -2                    /* SmartModuleInitErrorStatus::InitError */
+#define ORC_E_DECODING_BASE_INPUT -11
+#define ORC_E_DECODING_RECORDS -22
+#define ORC_E_ENCODING_OUTPUT -33
+#define ORC_E_UNKNOWN_SM -100            /* EngineError::UnknownSmartModule */
+#define ORC_E_INSTANTIATE -101
+#define ORC_E_STORE_MEMORY -102
+#define ORC_E_UNSUPPORTED -103
+#define ORC_E_IO -104                    /* io::Error surfaced by FileBatchIterator / empty-chain decode */
+#define ORC_E_INVALID_ARG -105
+
+typedef struct orc_result {
+  int status;
+  /* process(): encoded Vec<Record> (u32 BE count + records)
+   * process_batch(): encoded Batch (file format: 12-B preamble + 45-B header + records, CRC32C set) */
+  uint8_t *bytes;
+  size_t bytes_len;
+  uint32_t n_records;
+  int64_t base_offset;
+  int32_t last_offset_delta;
+  /* Option<SmartModuleTransformRuntimeError> */
+  int has_error;
+  char *hint;
+  size_t hint_len;
+  int64_t err_offset;
+  int32_t err_kind;
+  int has_key;
+  uint8_t *key;
+  size_t key_len;
+  uint8_t *value;
+  size_t value_len;
+  /* infra error message (init errors etc.) */
+  char *message;
+  /* metrics deltas of this call */
+  uint64_t m_bytes_in, m_records_out, m_invocations;
+} orc_result;
+
+typedef struct orc_chain orc_chain;
+
+uint32_t orc_crc32c(const uint8_t *p, size_t n);
+size_t orc_varint_encode(int64_t v, uint8_t *out);
+size_t orc_varint_size(int64_t v);
+int orc_varint_decode(const uint8_t *p, size_t n, int64_t *v, size_t *used);
+
+orc_chain *orc_chain_new(void);
+void orc_chain_free(orc_chain *c);
+/* add a built-in SmartModule by reference module name; runs init().
+ * returns ORC_OK or an error (message in *msg_out, malloc'd, may be NULL) */
+int orc_chain_add(orc_chain *c, const char *module, const char **keys, const char **vals,
+                  size_t n_params, const uint8_t *acc, size_t acc_len, int has_acc, char **msg_out);
+int orc_chain_process(orc_chain *c, const uint8_t *raw, size_t raw_len, int64_t base_offset,
+                      int64_t base_ts, orc_result *out);
+int orc_process_batch(orc_chain *c, const uint8_t *slice, size_t slice_len, uint64_t max_bytes,
+                      orc_result *out);
+int orc_chain_accumulator(orc_chain *c, size_t stage, uint8_t **acc, size_t *len);
+void orc_result_free(orc_result *r);
+void orc_free(void *p);
+
+/* regex oracle exposed for cross-checks with an independent engine */
+int orc_regex_is_match(const char *pattern, const uint8_t *text, size_t n, int *is_match);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,205 @@
+"""Writes tests/golden/kats.json: known-answer vectors for the SmartModule path.
+
+Every EXPECTED value below is transcribed from an assertion in the reference's
+own tests (file:line cited next to it, paths relative to /root/reference), or
+from the output of the reference's compiled guest recorded in SURVEY.md §8c.
+The INPUT bytes are built here with the host codec (fluvio_amd/protocol.py) to
+reproduce the inputs those tests construct (BatchProducer, Record::new, ...).
+Nothing here is computed by the oracle or by the product.
+
+Run:  python tests/golden/make_golden.py
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+from fluvio_amd.protocol import (Batch, BatchHeader, Record, encode_records)  # noqa: E402
+
+OUT = os.path.join(os.path.dirname(__file__), "kats.json")
+
+
+def recs(values, offset_deltas=True):
+    rs = [Record.new(v) for v in values]
+    if offset_deltas:
+        for i, r in enumerate(rs):
+            r.preamble.offset_delta = i
+    return rs
+
+
+def producer_batch(base_offset, values, producer_id=0, ts_delta=False):
+    """fluvio-protocol/src/fixture.rs:42-54 (BatchProducer::generate_batch), with the
+    base offset assigned by the replica on write (offsets are consecutive)."""
+    b = Batch(base_offset=base_offset, header=BatchHeader(magic=2, producer_id=producer_id,
+                                                         producer_epoch=-1))
+    for i, v in enumerate(values):
+        r = Record.new(v)
+        if ts_delta:
+            r.preamble.timestamp_delta = i
+        b.add_record(r)
+    return b.encode()
+
+
+def filter_values(n):
+    """fluvio-spu/src/services/public/tests/mod.rs:25-45 (create_filter_records)."""
+    return [("b" * 100 if i == 0 else "a" * 100 if i == 1 else "z" * 100) for i in range(n)]
+
+
+def main():
+    k = {}
+    k["varint"] = {
+        "source": "crates/fluvio-protocol/src/core/varint.rs:93-103,126-136",
+        "cases": [[0, "00"], [-1, "01"], [1, "02"], [63, "7e"], [7, "0e"], [10, "14"], [4, "08"],
+                  [8191, "fe7f"], [-134217729, "8180808001"]],
+    }
+    k["record_dog"] = {
+        "source": "crates/fluvio-protocol/src/record/data.rs:653-666",
+        "bytes": bytes([0x12, 0x0, 0x0, 0x2, 0x0, 0x6, 0x64, 0x6F, 0x67, 0x0]).hex(),
+        "offset_delta": 1, "value": "dog", "write_size": 10,
+    }
+    # batch.rs:548-575: one record "test" pushed directly (last_offset_delta stays -1)
+    b = Batch(header=BatchHeader(first_timestamp=1555478494747, max_time_stamp=1555478494747))
+    b.records.append(Record.new(b"test"))
+    b2 = Batch(header=BatchHeader(first_timestamp=1555478494747, max_time_stamp=1555478494747))
+    b2.records.append(Record.new(b"test"))
+    b2.header.attributes |= 0x10
+    b2.schema_id = 42
+    k["crc"] = {
+        "source": "crates/fluvio-protocol/src/record/batch.rs:574,627",
+        "cases": [{"batch": b.encode().hex(), "crc": 1430948200},
+                  {"batch": b2.encode().hex(), "crc": 2943551365}],
+    }
+    k["produce_records"] = {
+        "source": "crates/fluvio-spu/src/smartengine/produce_batch.rs:124,128",
+        "cases": [{"records": encode_records(recs(["soup"])).hex(),
+                   "expect": b"\0\0\0\x01\x14\0\0\0\0\x08soup\0".hex()},
+                  {"records": encode_records(recs(["fries"])).hex(),
+                   "expect": b"\0\0\0\x01\x16\0\0\0\0\nfries\0".hex()}],
+    }
+
+    # --- SmartModuleChainInstance::process cases (SmartEngine unit tests) -----
+    chain = []
+
+    def case(name, source, modules, calls):
+        chain.append({"name": name, "source": source, "modules": modules, "calls": calls})
+
+    # inputs are SmartModuleInput::try_from_records(vec![Record::new(..)]) -> offset_delta 0
+    case("filter", "crates/fluvio-smartengine/src/engine/wasmtime/transforms/filter.rs:37-58",
+         [["filter", {}, None]],
+         [{"values": ["hello world"], "expect": []},
+          {"values": ["apple", "fruit"], "expect": ["apple"]}])
+    case("map", "crates/fluvio-smartengine/src/engine/wasmtime/transforms/map.rs:18-41",
+         [["map", {}, None]],
+         [{"values": ["apple", "fruit"], "expect": ["APPLE", "FRUIT"]}])
+    case("filter_map", "crates/fluvio-smartengine/src/engine/wasmtime/transforms/filter_map.rs:21-43",
+         [["filter_map", {}, None]],
+         [{"values": ["10", "11"], "expect": ["5"]}])
+    case("chain_filter_map", "crates/fluvio-smartengine/src/engine/wasmtime/engine.rs:259-311",
+         [["filter_init", {"key": "a"}, None], ["map", {}, None]],
+         [{"values": ["hello world"], "expect": []},
+          {"values": ["apple", "fruit", "banana"], "expect": ["APPLE", "BANANA"]}])
+    case("chain_filter_aggregate", "crates/fluvio-smartengine/src/engine/wasmtime/engine.rs:315-384",
+         [["filter_init", {"key": "a"}, None], ["aggregate", {}, "zero"]],
+         [{"values": ["apple", "fruit", "banana"], "expect": ["zeroapple", "zeroapplebanana"]},
+          {"values": ["nothing"], "expect": []},
+          {"values": ["elephant"], "expect": ["zeroapplebananaelephant"]}])
+    case("aggregate_ok", "crates/fluvio-smartengine/src/engine/wasmtime/transforms/aggregate.rs:124-221",
+         [["aggregate", {}, None]],
+         [{"values": ["a"], "expect": ["a"], "acc": "a"},
+          {"values": ["b"], "expect": ["ab"], "acc": "ab"},
+          {"values": [], "expect": [], "acc": "ab"},
+          {"values": ["c"], "expect": ["abc"]}])
+    case("aggregate_with_initial", "crates/fluvio-smartengine/src/engine/wasmtime/transforms/aggregate.rs:223-255",
+         [["aggregate", {}, "a"]],
+         [{"values": ["b"], "expect": ["ab"]}])
+    case("empty_chain", "crates/fluvio-smartengine/src/engine/wasmtime/engine.rs:477-498",
+         [], [{"values": ["input"], "expect": ["input"]}])
+    k["chain"] = chain
+    k["init_errors"] = [
+        {"source": "crates/fluvio-smartengine/src/engine/wasmtime/transforms/filter.rs:62-81",
+         "module": "filter_init", "params": {}, "message": "Missing param key"},
+        {"source": "smartmodule/regex-filter/src/lib.rs:13-22",
+         "module": "regex-filter", "params": {}, "message": "Missing param regex"},
+    ]
+
+    # --- reference guest output recorded in SURVEY.md §8c (compiled reference
+    # fixture crates/fluvio-smartmodule/fixtures/smartmodule.wasm = contains('a'))
+    k["survey_guest"] = {
+        "source": "SURVEY.md §8c (reference compiled guest, recorded during the survey)",
+        "module": "filter",
+        "ok": {"values": ["apple", "fruit", "banana", "hello world"], "base_offset": 0,
+               "expect_successes": "0000000216000000000a6170706c650018000004000c62616e616e6100",
+               "expect_error_tag": "00"},
+        "utf8": {"values_hex": ["6170706c65", "ff61"], "base_offset": 100,
+                 "expect_values": ["apple"],
+                 "error": {"hint": "invalid utf-8 sequence of 1 bytes from index 0", "offset": 101,
+                           "kind": 0, "key": None, "value": "ff61"}},
+    }
+
+    # --- SPU process_batch over stored batches ----------------------------
+    spu = []
+    # stream_fetch.rs:441-476: 2 filter records at offset 0 -> 1 record, offset_delta 1
+    s1 = producer_batch(0, filter_values(2))
+    spu.append({"name": "filter_first_fetch",
+                "source": "crates/fluvio-spu/src/services/public/tests/stream_fetch.rs:441-476",
+                "modules": [["filter", {}, None]], "slice": s1.hex(), "max_bytes": 10000,
+                "expect": {"base_offset": 0, "n_records": 1, "values": ["a" * 100],
+                           "offset_deltas": [1]}})
+    # stream_fetch.rs:480-537: fetch from offset 2 over [raw(2)@2, filter(3)@4, filter(3)@7]
+    s2 = (producer_batch(2, [bytes([10, 20])] * 2, producer_id=12) + producer_batch(4, filter_values(3))
+          + producer_batch(7, filter_values(3)))
+    spu.append({"name": "filter_across_batches",
+                "source": "crates/fluvio-spu/src/services/public/tests/stream_fetch.rs:480-537",
+                "modules": [["filter", {}, None]], "slice": s2.hex(), "max_bytes": 10000,
+                "expect": {"base_offset": 4, "n_records": 2, "values": ["a" * 100, "a" * 100],
+                           "next_offset": 10}})
+    # stream_fetch.rs:839-969: three batches of 10 filter records, max_bytes 250
+    s3 = b"".join(producer_batch(10 * i, filter_values(10)) for i in range(3))
+    spu.append({"name": "filter_max_bytes",
+                "source": "crates/fluvio-spu/src/services/public/tests/stream_fetch.rs:870-920",
+                "modules": [["filter", {}, None]], "slice": s3.hex(), "max_bytes": 250,
+                "expect": {"base_offset": 0, "n_records": 2, "values": ["a" * 100, "a" * 100],
+                           "next_offset": 20}})
+    s3b = producer_batch(20, filter_values(10))
+    spu.append({"name": "filter_max_bytes_second_fetch",
+                "source": "crates/fluvio-spu/src/services/public/tests/stream_fetch.rs:922-960",
+                "modules": [["filter", {}, None]], "slice": s3b.hex(), "max_bytes": 250,
+                "expect": {"base_offset": 20, "n_records": 1, "values": ["a" * 100],
+                           "next_offset": 30}})
+    # stream_fetch.rs:704-803: filter_odd over "0".."9","ten" -> 5 records + error at offset 10
+    s4 = producer_batch(0, [str(i) for i in range(10)] + ["ten"])
+    spu.append({"name": "filter_odd_error",
+                "source": "crates/fluvio-spu/src/services/public/tests/stream_fetch.rs:744-795",
+                "modules": [["filter_odd", {}, None]], "slice": s4.hex(), "max_bytes": 10000,
+                "expect": {"base_offset": 0, "n_records": 5, "values": ["0", "2", "4", "6", "8"],
+                           "error": {"offset": 10, "key": None, "value": "ten", "kind": 0,
+                                     "hint": "Oops something went wrong\n\nCaused by:\n   0: Failed to parse int\n   1: invalid digit found in string"}}})
+    # stream_fetch.rs:1438-1530: aggregate (concat, initial "A") over "0".."4"
+    s5 = producer_batch(0, [str(i) for i in range(5)])
+    spu.append({"name": "aggregate_single_batch",
+                "source": "crates/fluvio-spu/src/services/public/tests/stream_fetch.rs:1481-1528",
+                "modules": [["aggregate", {}, "A"]], "slice": s5.hex(), "max_bytes": 10000,
+                "expect": {"base_offset": 0, "n_records": 5,
+                           "values": ["A0", "A01", "A012", "A0123", "A01234"]}})
+    # stream_fetch.rs:1551-1709: aggregate over two batches "0".."2" @0 and "3".."5" @3
+    s5b = producer_batch(0, ["0", "1", "2"]) + producer_batch(3, ["3", "4", "5"])
+    spu.append({"name": "aggregate_multi_batch",
+                "source": "crates/fluvio-spu/src/services/public/tests/stream_fetch.rs:1672-1693",
+                "modules": [["aggregate", {}, "A"]], "slice": s5b.hex(), "max_bytes": 10000,
+                "expect": {"base_offset": 0, "n_records": 6, "next_offset": 6,
+                           "values": ["A0", "A01", "A012", "A0123", "A01234", "A012345"]}})
+    # stream_fetch.rs:1933-2020: filter_map over 11,22,33,44,55 -> "11","22"
+    s6 = producer_batch(0, ["11", "22", "33", "44", "55"])
+    spu.append({"name": "filter_map",
+                "source": "crates/fluvio-spu/src/services/public/tests/stream_fetch.rs:1933-2020",
+                "modules": [["filter_map", {}, None]], "slice": s6.hex(), "max_bytes": 10000,
+                "expect": {"base_offset": 0, "n_records": 2, "values": ["11", "22"]}})
+    k["process_batch"] = spu
+
+    with open(OUT, "w") as f:
+        json.dump(k, f, indent=1, sort_keys=True)
+    print("wrote", OUT)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,160 @@
+"""Pins the CPU oracle (oracle/) against the reference's own known answers
+(tests/golden/kats.json, every expected value cited to a reference test).
+
+CPU only: no GPU, no product library involved.
+"""
+import re
+import struct
+
+import pytest
+
+from fluvio_amd import protocol as P
+from oracle import oracle as O
+
+
+def _vals(raw):
+    return [r.value for r in P.decode_records(raw)]
+
+
+def test_varint_table(kats):
+    for v, hx in kats["varint"]["cases"]:
+        assert O.varint_encode(v).hex() == hx
+        assert P.varint_encode(v).hex() == hx
+        assert P.varint_decode(bytes.fromhex(hx)) == (v, len(hx) // 2)
+
+
+def test_record_dog(kats):
+    k = kats["record_dog"]
+    raw = bytes.fromhex(k["bytes"])
+    recs = P.decode_records(struct.pack(">I", 1) + raw)
+    assert recs[0].preamble.offset_delta == k["offset_delta"]
+    assert recs[0].value == k["value"].encode()
+    assert recs[0].write_size() == k["write_size"]
+    # oracle decode -> encode round trip through the empty chain
+    out = O.OracleChain().process(struct.pack(">I", 1) + raw)
+    assert out["bytes"] == struct.pack(">I", 1) + raw
+
+
+def test_crc_kats(kats):
+    for c in kats["crc"]["cases"]:
+        b = bytes.fromhex(c["batch"])
+        crc_field = struct.unpack(">I", b[17:21])[0]
+        assert crc_field == c["crc"]  # host codec reproduces the KAT
+        assert O.crc32c(b[21:]) == c["crc"]  # oracle CRC over attributes..records
+
+
+def test_produce_records(kats):
+    for c in kats["produce_records"]["cases"]:
+        assert c["records"] == c["expect"]
+        out = O.OracleChain().process(bytes.fromhex(c["records"]))
+        assert out["bytes"].hex() == c["expect"]
+
+
+def _records_input(values, base_offset=0):
+    return P.encode_records([P.Record.new(v) for v in values])
+
+
+@pytest.mark.parametrize("case_idx", range(8))
+def test_chain_cases(kats, case_idx):
+    case = kats["chain"][case_idx]
+    chain = O.OracleChain([(m, p, a.encode() if a is not None else None)
+                           for m, p, a in case["modules"]])
+    agg_stage = next((i for i, m in enumerate(case["modules"]) if m[0].startswith("aggregate")), None)
+    for call in case["calls"]:
+        out = chain.process(_records_input(call["values"]))
+        assert out["status"] == 0
+        assert out["error"] is None
+        assert _vals(out["bytes"]) == [v.encode() for v in call["expect"]], case["name"]
+        if "acc" in call:
+            assert chain.accumulator(agg_stage) == call["acc"].encode()
+
+
+def test_init_errors(kats):
+    for c in kats["init_errors"]:
+        with pytest.raises(O.OracleError) as e:
+            O.OracleChain([(c["module"], c["params"], None)])
+        assert e.value.status == -2
+        assert e.value.message == c["message"]
+
+
+def test_survey_guest_vectors(kats):
+    g = kats["survey_guest"]
+    ok = g["ok"]
+    recs = [P.Record.new(v) for v in ok["values"]]
+    for i, r in enumerate(recs):
+        r.preamble.offset_delta = i
+    out = O.OracleChain([(g["module"], {}, None)]).process(P.encode_records(recs), ok["base_offset"])
+    assert out["bytes"].hex() == ok["expect_successes"]
+    assert out["error"] is None
+    u = g["utf8"]
+    recs = [P.Record.new(bytes.fromhex(v)) for v in u["values_hex"]]
+    for i, r in enumerate(recs):
+        r.preamble.offset_delta = i
+    out = O.OracleChain([(g["module"], {}, None)]).process(P.encode_records(recs), u["base_offset"])
+    assert _vals(out["bytes"]) == [v.encode() for v in u["expect_values"]]
+    e = out["error"]
+    assert e["hint"] == u["error"]["hint"]
+    assert e["offset"] == u["error"]["offset"]
+    assert e["kind"] == u["error"]["kind"]
+    assert e["key"] is None
+    assert e["value"].hex() == u["error"]["value"]
+
+
+def test_process_batch_cases(kats):
+    for case in kats["process_batch"]:
+        chain = O.OracleChain([(m, p, a.encode() if a is not None else None)
+                               for m, p, a in case["modules"]])
+        out = chain.process_batch(bytes.fromhex(case["slice"]), case["max_bytes"])
+        exp = case["expect"]
+        assert out["status"] == 0, case["name"]
+        b, end = P.decode_batch(out["bytes"])
+        assert end == len(out["bytes"])
+        assert b.base_offset == exp["base_offset"], case["name"]
+        recs = b.memory_records()
+        assert len(recs) == exp["n_records"], case["name"]
+        assert [r.value for r in recs] == [v.encode() for v in exp["values"]], case["name"]
+        if "offset_deltas" in exp:
+            assert [r.preamble.offset_delta for r in recs] == exp["offset_deltas"]
+        if "next_offset" in exp:
+            # stream_fetch.rs:487-492: next_filter_offset = base_offset + last_offset_delta + 1
+            assert b.base_offset + b.header.last_offset_delta + 1 == exp["next_offset"], case["name"]
+        # CRC is over attributes..records and batch_len matches
+        assert b.header.crc == P.crc32c(out["bytes"][21:])
+        assert b.batch_len == len(out["bytes"]) - 12
+        if "error" in exp:
+            e = out["error"]
+            assert e is not None
+            for f in ("offset", "kind", "hint"):
+                assert e[f] == exp["error"][f], (case["name"], f)
+            assert e["key"] is None
+            assert e["value"] == exp["error"]["value"].encode()
+        else:
+            assert out["error"] is None
+
+
+@pytest.mark.parametrize("pattern,texts", [
+    (r"\d{3}-\d{2}-\d{4}", ["my ssn is 123-45-6789 ok", "123-45-678", "x1234-56-78901", "", "12-345-6789"]),
+    (r"[A-Z]", ["AA", "aa", "a1b2", "zZ"]),
+    (r"^ab|cd$", ["abx", "xab", "xcd", "cdx", "ab", ""]),
+    (r"a(b|c)*d", ["ad", "abcbd", "abxd", "zzabbbbbccd"]),
+    (r"colou?r\s+\w+", ["color red", "colour  blue", "colr x", "color"]),
+    (r"[^a-c]x", ["ax", "dx", "x", "abcx"]),
+    (r"a.c", ["abc", "a\nc", "aéc", "ac"]),
+    (r"x{2,3}y", ["xy", "xxy", "xxxxy"]),
+    (r"", ["", "anything"]),
+])
+def test_regex_oracle_vs_python_re(pattern, texts):
+    """Cross-check the oracle's regex engine with Python's independent `re` on
+    inputs where Rust regex and Python re agree (no `$` before a trailing \\n,
+    ASCII \\w).  Pins the restatement of regex is_match (third-party crate
+    regex 1.6.0/1.8.1, absent from /root/reference)."""
+    for t in texts:
+        assert O.regex_is_match(pattern, t.encode()) == (re.search(pattern, t) is not None), (pattern, t)
+
+
+def test_regex_unicode_classes():
+    # \d is Unicode Nd in Rust regex (Arabic-Indic digits match), '.' is a scalar value
+    assert O.regex_is_match(r"\d\d\d", "١٢٣".encode())
+    assert O.regex_is_match(r"^.$", "é".encode())
+    assert not O.regex_is_match(r"^..$", "é".encode())
+    assert O.regex_is_match(r"\s", "a　b".encode())
