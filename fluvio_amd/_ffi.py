@@ -1,0 +1,140 @@
+"""ctypes binding of libfsg.so (include/fsg.h).
+
+This is the Python analogue of the reference-side FFI crate a maintainer would
+add (INTEGRATION.md shows the Rust `extern "C"` block).  Loading fails loudly if
+the HIP library has not been built: there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libfsg.so")
+CSRC = os.path.join(_HERE, "csrc")
+
+FSG_OK = 0
+FSG_E_UNKNOWN = -1
+FSG_E_INIT = -2
+FSG_E_DECODING_BASE_INPUT = -11
+FSG_E_DECODING_RECORDS = -22
+FSG_E_ENCODING_OUTPUT = -33
+FSG_E_UNKNOWN_SM = -100
+FSG_E_INSTANTIATE = -101
+FSG_E_STORE_MEMORY = -102
+FSG_E_UNSUPPORTED = -103
+FSG_E_IO = -104
+FSG_E_INVALID_ARG = -105
+FSG_E_DEVICE = -200
+
+
+class fsg_param(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_char_p), ("value", ctypes.c_char_p)]
+
+
+class fsg_metrics(ctypes.Structure):
+    _fields_ = [("bytes_in", ctypes.c_uint64), ("records_out", ctypes.c_uint64),
+                ("invocation_count", ctypes.c_uint64), ("fuel_used", ctypes.c_uint64)]
+
+
+class fsg_runtime_error(ctypes.Structure):
+    _fields_ = [("hint", ctypes.POINTER(ctypes.c_char)), ("hint_len", ctypes.c_size_t),
+                ("offset", ctypes.c_int64), ("kind", ctypes.c_int32), ("has_key", ctypes.c_int32),
+                ("key", ctypes.POINTER(ctypes.c_uint8)), ("key_len", ctypes.c_size_t),
+                ("value", ctypes.POINTER(ctypes.c_uint8)), ("value_len", ctypes.c_size_t)]
+
+
+class fsg_output(ctypes.Structure):
+    _fields_ = [("records", ctypes.POINTER(ctypes.c_uint8)), ("records_len", ctypes.c_size_t),
+                ("n_records", ctypes.c_uint32), ("has_error", ctypes.c_int32),
+                ("error", fsg_runtime_error)]
+
+
+class fsg_batch_output(ctypes.Structure):
+    _fields_ = [("batch", ctypes.POINTER(ctypes.c_uint8)), ("batch_len", ctypes.c_size_t),
+                ("base_offset", ctypes.c_int64), ("last_offset_delta", ctypes.c_int32),
+                ("n_records", ctypes.c_uint32), ("has_error", ctypes.c_int32),
+                ("error", fsg_runtime_error)]
+
+
+class fsg_timings(ctypes.Structure):
+    _fields_ = [("eval_ms", ctypes.c_float), ("plan_ms", ctypes.c_float), ("write_ms", ctypes.c_float),
+                ("crc_ms", ctypes.c_float), ("total_ms", ctypes.c_float), ("in_bytes", ctypes.c_uint64),
+                ("out_bytes", ctypes.c_uint64), ("n_batches", ctypes.c_uint64),
+                ("n_records_in", ctypes.c_uint64)]
+
+
+VP = ctypes.c_void_p
+PP = ctypes.POINTER(ctypes.c_void_p)
+U8P = ctypes.c_char_p
+SZ = ctypes.c_size_t
+
+# every symbol include/fsg.h declares, with (restype, argtypes)
+SIGNATURES = {
+    "fsg_last_error_message": (ctypes.c_char_p, []),
+    "fsg_abi_version": (ctypes.c_int, []),
+    "fsg_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "fsg_engine_new": (ctypes.c_int, [ctypes.c_int, PP]),
+    "fsg_engine_free": (None, [VP]),
+    "fsg_chain_builder_new": (ctypes.c_int, [PP]),
+    "fsg_chain_builder_set_store_memory_limit": (ctypes.c_int, [VP, SZ]),
+    "fsg_chain_builder_add_smart_module": (ctypes.c_int, [VP, ctypes.POINTER(fsg_param), SZ, ctypes.c_int16,
+                                                          U8P, SZ, ctypes.c_int32, U8P, SZ]),
+    "fsg_chain_builder_initialize": (ctypes.c_int, [VP, VP, PP]),
+    "fsg_chain_builder_free": (None, [VP]),
+    "fsg_chain_process": (ctypes.c_int, [VP, U8P, SZ, ctypes.c_int64, ctypes.c_int64,
+                                         ctypes.POINTER(fsg_metrics), ctypes.POINTER(ctypes.POINTER(fsg_output))]),
+    "fsg_chain_process_batch": (ctypes.c_int, [VP, U8P, SZ, ctypes.c_uint64, ctypes.POINTER(fsg_metrics),
+                                               ctypes.POINTER(ctypes.POINTER(fsg_batch_output))]),
+    "fsg_chain_look_back": (ctypes.c_int, [VP, ctypes.POINTER(fsg_metrics)]),
+    "fsg_chain_get_accumulator": (ctypes.c_int, [VP, SZ, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
+                                                 ctypes.POINTER(SZ)]),
+    "fsg_chain_last_timings": (ctypes.c_int, [VP, ctypes.POINTER(fsg_timings)]),
+    "fsg_chain_free": (None, [VP]),
+    "fsg_output_free": (None, [ctypes.POINTER(fsg_output)]),
+    "fsg_batch_output_free": (None, [ctypes.POINTER(fsg_batch_output)]),
+    "fsg_free": (None, [VP]),
+    "fsg_slice_upload": (ctypes.c_int, [VP, U8P, SZ, PP]),
+    "fsg_slice_info": (ctypes.c_int, [VP, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                      ctypes.POINTER(ctypes.c_uint64)]),
+    "fsg_slice_free": (None, [VP]),
+    "fsg_chain_process_slice": (ctypes.c_int, [VP, VP, ctypes.c_uint64, ctypes.POINTER(fsg_metrics),
+                                               ctypes.POINTER(ctypes.POINTER(fsg_batch_output))]),
+    "fsg_chain_output_device": (ctypes.c_int, [VP, PP, ctypes.POINTER(SZ)]),
+    "fsg_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
+    "fsg_engine_comm_init": (ctypes.c_int, [VP, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]),
+    "fsg_allreduce_i32": (ctypes.c_int, [VP, VP, SZ]),
+}
+
+_lib = None
+
+
+def build() -> str:
+    """Compile libfsg.so for gfx950 (hipcc cross-compiles without a GPU)."""
+    env = dict(os.environ)
+    subprocess.run(["make", "-s", "-j8", "-C", CSRC], check=True, env=env)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libfsg.so not built ({LIB_PATH}); run fluvio_amd._ffi.build() "
+                               "— the GPU engine has no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        L.fsg_debug_regex_match.restype = ctypes.c_int
+        L.fsg_debug_regex_match.argtypes = [ctypes.c_char_p, ctypes.c_char_p, SZ, ctypes.POINTER(ctypes.c_int),
+                                            ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    m = lib().fsg_last_error_message()
+    return m.decode("utf-8", "replace") if m else ""

@@ -1,0 +1,230 @@
+// fsg_device.h — data layout shared by the host runtime and the CDNA4 kernels.
+//
+// HBM layout of one process_batch call (see DESIGN.md "Data layout"):
+//   slice     : the stored batches exactly as FileBatchIterator reads them
+//               (57-byte file header + record section per batch), padded to
+//               a 16-byte multiple plus kSlicePad bytes of zeros
+//   bpos[]    : u64 byte offset of each batch in the slice (ingest framing)
+//   rbase[]   : u64 exclusive prefix of the record counts (descriptor base)
+//   bstat[]   : BatchStat per batch (written by k_eval)
+//   desc[]    : KeptRec per kept record, at rbase[b] + k
+//   rows[]    : ScanRow per batch (k_size), scanned in place
+//   out       : the output batch (61-byte header + records)
+#pragma once
+#include <stdint.h>
+
+namespace fsg {
+
+constexpr int kWave = 64;
+constexpr int kWin = 17408;     // LDS record window per wave (bytes)
+constexpr int kMaxR = 128;      // records per window
+constexpr int kMaxStages = 8;
+constexpr int kSlicePad = 256;  // zero padding behind the slice (over-read guard)
+constexpr int kCrcChunk = 65536;
+
+// stage operations (built-in GPU SmartModules)
+enum StageOp : uint8_t {
+  OP_CONTAINS = 0,     // filter / filter_init / filter_with_param: from_utf8 + contains(needle)
+  OP_REGEX = 1,        // regex-filter (keep match) / filter_regex (keep non-match)
+  OP_FILTER_ODD = 2,   // filter_odd: from_utf8 + parse::<i32> + keep even
+  OP_MAP_UPPER = 3,    // map: make_ascii_uppercase
+  OP_MAP_DOUBLE = 4,   // map_double: from_utf8 + parse::<i32> * 2
+  OP_FILTER_MAP = 5,   // filter_map: from_utf8_lossy + parse::<i32>, even -> /2
+  OP_AGG_SUM = 6,      // aggregate-sum (last stage only)
+};
+
+// value representation entering a stage (static per chain position)
+enum ValType : uint8_t { VT_SRC = 0, VT_SRC_UPPER = 1, VT_I32 = 2 };
+
+// error detail codes stored in BatchStat::err_code
+enum ErrCode : uint32_t {
+  EC_NONE = 0,
+  EC_UTF8 = 1,        // aux = valid_up_to, aux2 = error_len (0 = None)
+  EC_PARSE = 2,       // aux = ParseIntError kind (1 Empty, 2 InvalidDigit, 3 PosOverflow, 4 NegOverflow)
+  EC_ACC_UTF8 = 3,    // aggregate accumulator is not UTF-8 (aux/aux2 as EC_UTF8)
+};
+
+struct DfaDesc {
+  // ASCII DFA: every class restricted to ASCII; exact on ASCII-only values.
+  // <= 255 states, u8 transitions, staged in LDS when it fits.
+  uint32_t nstates;
+  uint32_t nclasses;
+  uint32_t s_bot;      // start state at value start (^ satisfied)
+  uint32_t s_mid;      // restart state inside a value
+  int32_t max_len;     // longest match in bytes, -1 = unbounded
+  uint32_t classmap;   // blob offset: u8[256]
+  uint32_t classmap_up;// blob offset: u8[256], classmap of toupper(byte)
+  uint32_t trans;      // blob offset: u8[nstates * nclasses]
+  uint32_t accept;     // blob offset: u8[256] (bit0 accept, bit1 accept at end of value)
+  // full Unicode DFA for values with non-ASCII bytes: u16 transitions (global)
+  uint32_t f_nstates;
+  uint32_t f_nclasses;
+  uint32_t f_s_bot;
+  uint32_t f_classmap;
+  uint32_t f_classmap_up;
+  uint32_t f_trans;    // blob offset: u16[f_nstates * f_nclasses]
+  uint32_t f_accept;   // blob offset: u8[f_nstates]
+  uint32_t unicode_word;
+  uint32_t pad;
+};
+
+struct StageDesc {
+  uint8_t op;
+  uint8_t kind;        // SmartModuleKind tag (FSG_KIND_*)
+  uint8_t in_type;     // ValType
+  uint8_t keep_match;  // OP_REGEX: 1 keep matching, 0 keep non-matching
+  uint32_t needle;     // blob offset (OP_CONTAINS)
+  uint32_t needle_len;
+  uint32_t acc_bad;    // OP_AGG_SUM: initial accumulator is invalid UTF-8
+  uint32_t acc_vut;    //   its Utf8Error valid_up_to
+  uint32_t acc_elen;   //   its Utf8Error error_len
+  DfaDesc dfa;
+};
+
+struct ChainDesc {
+  uint32_t nstages;
+  uint32_t out_type;   // ValType of the value after the last stage
+  uint32_t has_agg;
+  uint32_t pad;
+  StageDesc st[kMaxStages];
+};
+
+// per-batch result of k_eval
+enum BatchFlags : uint32_t {
+  BF_ERR = 1u,         // a record-level SmartModule error (SmartModuleTransformRuntimeError)
+  BF_DECODE = 2u,      // Vec<Record> decode failed -> the process() call returns Err
+  BF_UNSUPPORTED = 4u, // input needs a feature the GPU path does not implement
+  BF_LAST_STAGE = 8u,  // the error (if any) happened in the last stage -> records_out counted
+};
+
+struct BatchStat {
+  int64_t base_offset;
+  int64_t first_ts;
+  int32_t lod_in;      // header.last_offset_delta
+  uint32_t flags;
+  uint32_t nkeep;      // records in the stage output (before the error record)
+  uint32_t sec_len;    // record-section length = bytes_in of this process() call
+  uint32_t err_stage;
+  uint32_t err_code;
+  uint64_t err_pos;    // absolute slice offset of the failing record
+  int64_t err_od;      // its offset_delta
+  int32_t err_ival;    // VT_I32 value entering the failing stage
+  uint32_t err_aux;
+  uint32_t err_aux2;
+  uint32_t pad;
+  int64_t agg_sum;     // wrapping i32 sum of the aggregate inputs of this batch
+};
+
+// one kept output record (a compaction descriptor, 64 bytes): enough to
+// re-encode the record canonically without re-parsing the source
+enum KeepMode : uint8_t { KM_COPY = 0, KM_UPPER = 1, KM_I32 = 2, KM_AGG = 3 };
+struct KeptRec {
+  uint64_t src;        // absolute slice offset of the source record (its length varint)
+  uint64_t vpos;       // absolute slice offset of the source value bytes
+  uint64_t kpos;       // absolute slice offset of the key bytes
+  int64_t od;          // source offset_delta
+  int64_t ts;          // timestamp_delta
+  int64_t hdr;         // headers varint
+  uint32_t vlen;       // source value length (KM_COPY / KM_UPPER)
+  uint32_t klen;
+  int32_t ival;        // KM_I32 value / KM_AGG batch-local inclusive sum
+  uint8_t mode;        // KeepMode
+  uint8_t has_key;
+  uint8_t attr;
+  uint8_t pad;
+};
+static_assert(sizeof(KeptRec) == 64, "KeptRec is one 64-byte line");
+
+// per-batch row of the cross-batch scan (in place: exclusive prefix afterwards)
+struct ScanRow {
+  uint64_t rec_bytes;  // Σ output record sizes of this batch (after offset fix-up)
+  uint64_t nonempty;   // 1 if the batch contributes records
+  uint64_t lod;        // input last_offset_delta + 1 for batches >= first surviving batch
+  uint64_t nrec;       // records contributed
+  uint64_t bytes_in;   // record-section bytes (metrics.bytes_in)
+  uint64_t recs_out;   // last-stage output records (metrics.records_out)
+  int64_t agg;         // aggregate sum (wrapping i32 in the low bits)
+  uint64_t pad;
+};
+
+// cross-batch minima found with atomics (reset to 0xFFFFFFFF per call)
+struct Mins {
+  uint32_t first_keep;
+  uint32_t first_err;
+  uint32_t first_dec;
+  uint32_t first_unsup;
+  uint32_t cut;
+  uint32_t pad[3];
+};
+
+struct Plan {
+  int32_t status;      // 0, FSG_E_DECODING_BASE_INPUT, FSG_E_IO, FSG_E_UNSUPPORTED
+  int32_t err_batch;   // batch whose error is returned, -1 none
+  int32_t first;       // first surviving batch, -1 none
+  int32_t last;        // last batch whose records are included
+  int32_t stop;        // last processed batch (-1 none)
+  int32_t lod;
+  int64_t base_offset;
+  uint64_t n_records;
+  uint64_t rec_bytes;
+  uint64_t bytes_in;
+  uint64_t invocations;
+  uint64_t records_out;
+  int64_t agg_prefix_first;  // aggregate prefix (exclusive) at `first` — unused unless has_agg
+  int64_t acc_final;         // aggregate accumulator after the stop batch
+  int32_t acc_touched;       // accumulator changed by this call
+  int32_t pad;
+};
+
+struct EvalArgs {
+  const uint8_t* slice;
+  uint64_t slice_len;
+  const uint64_t* bpos;
+  const uint64_t* rbase;
+  uint32_t nbatches;
+  uint32_t pad;
+  const ChainDesc* chain;
+  const uint8_t* blob;
+  BatchStat* bstat;
+  KeptRec* desc;
+  Mins* mins;
+};
+
+struct SizeArgs {
+  const BatchStat* bstat;
+  const KeptRec* desc;
+  const uint64_t* rbase;
+  const Mins* mins;
+  const ScanRow* agg_pre;  // exclusive aggregate prefix (nullptr if no aggregate)
+  ScanRow* rows;
+  uint32_t nbatches;
+  uint32_t agg_only;       // 1: only fill rows[].agg (first pass of an aggregate chain)
+  int64_t acc0;
+};
+
+struct PlanArgs {
+  const BatchStat* bstat;
+  const ScanRow* rows;
+  const ScanRow* pre;
+  const Mins* mins;
+  Plan* plan;
+  uint32_t nbatches;
+  int32_t tail_status;  // framing status of the batch after the last framed one (0 = clean end)
+  int32_t empty_chain;
+  int32_t has_agg;
+  int64_t acc0;
+};
+
+struct WriteArgs {
+  const uint8_t* slice;
+  const BatchStat* bstat;
+  const KeptRec* desc;
+  const uint64_t* rbase;
+  const ScanRow* pre;
+  const ScanRow* agg_pre;
+  const Plan* plan;
+  uint8_t* out;
+  int64_t acc0;
+};
+
+}  // namespace fsg

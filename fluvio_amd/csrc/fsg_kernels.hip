@@ -1,0 +1,1477 @@
+// fsg_kernels.hip — CDNA4 (gfx950) kernels of the SmartModule record-transform path.
+//
+// Pipeline of one process_batch call over an HBM-resident slice:
+//   k_eval     one wave per stored batch: header decode, LDS-staged record
+//              windows, record framing (Record::decode, data.rs:534-562), the
+//              fused SmartModule chain per record, first-error semantics
+//              (engine.rs:135-185 + derive generator loops), compaction
+//              descriptors of the surviving records
+//   k_size     one wave per batch: output record sizes after the offset fix-up
+//              (spu batch.rs:95-105)
+//   k_scan_*   cross-batch exclusive scan (bytes, offsets, metrics, aggregate)
+//              + max_bytes cut detection (batch.rs:101-111)
+//   k_plan     one thread: the process_batch stop rules (batch.rs:41-142)
+//   k_header   output Batch header (batch.rs:398-430, Batch::default 482-497)
+//   k_write    one wave per included batch: canonical record re-encode
+//              (data.rs:504-532, varint.rs:43-66) into the output batch
+//   k_crc_*    CRC32C over attributes..records, chunked + GF(2) combine
+#include <hip/hip_runtime.h>
+
+#include "fsg_device.h"
+
+namespace fsg {
+
+// ---------------------------------------------------------------------------
+// small device helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t rd_be(const uint8_t* p, int n) {
+  uint64_t v = 0;
+  for (int i = 0; i < n; i++) v = (v << 8) | p[i];
+  return v;
+}
+
+// varint size with the encoder quirk (varint.rs:68-80)
+__device__ __forceinline__ uint32_t vsize(int64_t num) {
+  int64_t v = (int64_t)(((uint64_t)num << 1) ^ (uint64_t)(num >> 31));
+  uint32_t n = 1;
+  while (v & (int64_t)0xffffff80) {
+    n++;
+    v >>= 7;
+  }
+  return n;
+}
+// variant_encode (varint.rs:43-66); returns bytes written
+__device__ __forceinline__ uint32_t venc(int64_t num, uint8_t* out) {
+  int64_t v = (int64_t)(((uint64_t)num << 1) ^ (uint64_t)(num >> 31));
+  uint32_t k = 0;
+  while (v & (int64_t)0xffffff80) {
+    out[k++] = (uint8_t)((v & 0x7f) | 0x80);
+    v >>= 7;
+  }
+  out[k++] = (uint8_t)v;
+  return k;
+}
+
+__device__ __forceinline__ uint32_t dec_len_i32(int32_t v) {
+  uint32_t u = v < 0 ? (uint32_t)(-(int64_t)v) : (uint32_t)v;
+  uint32_t n = 1;
+  while (u >= 10) {
+    u /= 10;
+    n++;
+  }
+  return n + (v < 0 ? 1 : 0);
+}
+__device__ __forceinline__ uint32_t fmt_i32(int32_t v, uint8_t* out) {
+  uint8_t t[12];
+  uint32_t n = 0;
+  uint32_t u = v < 0 ? (uint32_t)(-(int64_t)v) : (uint32_t)v;
+  do {
+    t[n++] = (uint8_t)('0' + u % 10);
+    u /= 10;
+  } while (u);
+  uint32_t k = 0;
+  if (v < 0) out[k++] = '-';
+  while (n) out[k++] = t[--n];
+  return k;
+}
+
+__device__ __forceinline__ uint8_t up(uint8_t c) { return (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c; }
+
+// wave helpers (64 lanes)
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ uint32_t lanemask_lt() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
+  const int l = lane_id();
+  for (int o = 1; o < 64; o <<= 1) {
+    T t = __shfl_up(v, o, 64);
+    if (l >= o) v += t;
+  }
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Rust core::str::from_utf8 (run_utf8_validation) — serial, one lane per value
+// returns 1 valid; else 0 with valid_up_to and error_len (0 = None)
+// ---------------------------------------------------------------------------
+template <typename P>
+__device__ int utf8_check(P s, uint32_t n, uint32_t* vut, uint32_t* elen) {
+  uint32_t i = 0;
+  while (i < n) {
+    uint32_t f = s[i];
+    if (f < 0x80) {
+      i++;
+      continue;
+    }
+    int w = (f >= 0xC2 && f <= 0xDF) ? 2 : (f >= 0xE0 && f <= 0xEF) ? 3 : (f >= 0xF0 && f <= 0xF4) ? 4 : 0;
+    if (w == 0) { *vut = i; *elen = 1; return 0; }
+    if (i + 1 >= n) { *vut = i; *elen = 0; return 0; }
+    uint32_t b1 = s[i + 1];
+    if (w == 2) {
+      if ((b1 & 0xC0) != 0x80) { *vut = i; *elen = 1; return 0; }
+      i += 2;
+      continue;
+    }
+    bool ok1;
+    if (w == 3)
+      ok1 = (f == 0xE0 && b1 >= 0xA0 && b1 <= 0xBF) || (f >= 0xE1 && f <= 0xEC && b1 >= 0x80 && b1 <= 0xBF) ||
+            (f == 0xED && b1 >= 0x80 && b1 <= 0x9F) || (f >= 0xEE && f <= 0xEF && b1 >= 0x80 && b1 <= 0xBF);
+    else
+      ok1 = (f == 0xF0 && b1 >= 0x90 && b1 <= 0xBF) || (f >= 0xF1 && f <= 0xF3 && b1 >= 0x80 && b1 <= 0xBF) ||
+            (f == 0xF4 && b1 >= 0x80 && b1 <= 0x8F);
+    if (!ok1) { *vut = i; *elen = 1; return 0; }
+    if (i + 2 >= n) { *vut = i; *elen = 0; return 0; }
+    if ((s[i + 2] & 0xC0) != 0x80) { *vut = i; *elen = 2; return 0; }
+    if (w == 3) {
+      i += 3;
+      continue;
+    }
+    if (i + 3 >= n) { *vut = i; *elen = 0; return 0; }
+    if ((s[i + 3] & 0xC0) != 0x80) { *vut = i; *elen = 3; return 0; }
+    i += 4;
+  }
+  return 1;
+}
+
+// char::is_whitespace on a code point
+__device__ __forceinline__ bool cp_ws(uint32_t c) {
+  return (c >= 0x09 && c <= 0x0D) || c == 0x20 || c == 0x85 || c == 0xA0 || c == 0x1680 ||
+         (c >= 0x2000 && c <= 0x200A) || c == 0x2028 || c == 0x2029 || c == 0x202F || c == 0x205F ||
+         c == 0x3000;
+}
+template <typename P>
+__device__ __forceinline__ uint32_t cp_at(P s, uint32_t i, uint32_t* w) {
+  uint32_t f = s[i];
+  if (f < 0x80) { *w = 1; return f; }
+  if (f < 0xE0) { *w = 2; return ((f & 0x1F) << 6) | (s[i + 1] & 0x3F); }
+  if (f < 0xF0) { *w = 3; return ((f & 0x0F) << 12) | ((uint32_t)(s[i + 1] & 0x3F) << 6) | (s[i + 2] & 0x3F); }
+  *w = 4;
+  return ((f & 0x07) << 18) | ((uint32_t)(s[i + 1] & 0x3F) << 12) | ((uint32_t)(s[i + 2] & 0x3F) << 6) |
+         (s[i + 3] & 0x3F);
+}
+// str::trim on valid UTF-8 -> [b, e)
+template <typename P>
+__device__ void utf8_trim(P s, uint32_t n, uint32_t* b, uint32_t* e) {
+  uint32_t i = 0, w;
+  while (i < n) {
+    uint32_t c = cp_at(s, i, &w);
+    if (!cp_ws(c)) break;
+    i += w;
+  }
+  uint32_t j = n;
+  while (j > i) {
+    uint32_t k = j - 1;
+    while (k > i && (s[k] & 0xC0) == 0x80) k--;
+    uint32_t c = cp_at(s, k, &w);
+    if (!cp_ws(c)) break;
+    j = k;
+  }
+  *b = i;
+  *e = j;
+}
+
+// <i32 as FromStr>::from_str — 0 ok, 1 Empty, 2 InvalidDigit, 3 PosOverflow, 4 NegOverflow
+template <typename P>
+__device__ int parse_i32(P s, uint32_t n, int32_t* out) {
+  if (n == 0) return 1;
+  uint32_t i = 0;
+  bool pos = true;
+  uint8_t c0 = s[0];
+  if ((c0 == '+' || c0 == '-') && n == 1) return 2;
+  if (c0 == '+')
+    i = 1;
+  else if (c0 == '-') {
+    pos = false;
+    i = 1;
+  }
+  int64_t acc = 0;
+  for (; i < n; i++) {
+    uint32_t c = s[i];
+    if (c < '0' || c > '9') return 2;
+    int d = (int)c - '0';
+    if (pos) {
+      acc = acc * 10 + d;
+      if (acc > 2147483647LL) return 3;
+    } else {
+      acc = acc * 10 - d;
+      if (acc < -2147483648LL) return 4;
+    }
+  }
+  *out = (int32_t)acc;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// k_eval: per-wave LDS state
+// ---------------------------------------------------------------------------
+enum RecFlags : uint32_t {
+  RF_ALIVE = 1u,
+  RF_MATCH = 2u,
+  RF_NONASCII = 4u,
+  RF_UTF8_DONE = 8u,
+  RF_UTF8_BAD = 16u,
+};
+
+constexpr int kDfaLds = 4096;
+
+struct __attribute__((aligned(16))) WaveLds {
+  uint8_t win[kWin + 64];
+  uint32_t r_vs[kMaxR];     // value start (window offset)
+  uint32_t r_vl[kMaxR];     // value length
+  uint32_t r_start[kMaxR];  // record start (window offset)
+  uint32_t r_kpos[kMaxR];   // key bytes (window offset)
+  uint32_t r_klen[kMaxR];
+  uint32_t r_flags[kMaxR];
+  uint32_t r_aux[kMaxR];    // utf8 valid_up_to / parse kind
+  uint32_t r_aux2[kMaxR];   // utf8 error_len
+  int32_t r_ival[kMaxR];    // VT_I32 value
+  int32_t r_ival_in[kMaxR]; // value entering the erroring stage
+  uint8_t r_es[kMaxR];      // first error stage (0xFF none)
+  uint8_t r_ec[kMaxR];      // error code
+  uint8_t r_attr[kMaxR];
+  uint8_t r_haskey[kMaxR];
+  int64_t r_od[kMaxR];
+  int64_t r_ts[kMaxR];
+  int64_t r_hdr[kMaxR];
+  uint8_t dfa_cls[256];
+  uint8_t dfa_clsu[256];
+  uint8_t dfa_acc[256];
+  uint8_t dfa_trans[kDfaLds];
+  // wave-uniform scalars
+  int32_t nr;
+  int32_t walk_status;      // 0 ok, 1 decode error, 2 window incomplete (need next window)
+  uint32_t next_cursor_lo, next_cursor_hi;
+};
+
+// decode a varint from window bytes [q, lim); lim_sec tells whether running
+// out of window bytes means "incomplete" (more section bytes) or EOF
+template <typename P>
+__device__ __forceinline__ int wvarint(P w, uint32_t& q, uint32_t wlim, int64_t* out) {
+  uint64_t num = 0;
+  uint32_t shift = 0;
+  for (;;) {
+    if (q >= wlim) return -1;
+    uint8_t b = w[q++];
+    num |= ((uint64_t)(b & 0x7f)) << (shift & 63);
+    shift += 7;
+    if (!(b & 0x80)) break;
+  }
+  int64_t sn = (int64_t)num;
+  *out = (int64_t)((uint64_t)(sn >> 1) ^ (uint64_t)(-(sn & 1)));
+  return 0;
+}
+
+// Serial exact walk of records (lane 0).  Window bytes w[0..wlen) map to
+// absolute offsets wbase..; the record section ends at absolute sec_end.
+// Record::decode semantics (data.rs:534-562): fields parsed in order, the next
+// record starts where the headers varint ends.
+template <typename P>
+__device__ void walk_records(WaveLds& L, P w, uint64_t wbase, uint32_t wlen, uint64_t sec_end, uint64_t cursor,
+                             uint32_t rec_remaining, int max_recs) {
+  // window limit in window offsets; section limit in window offsets (may exceed wlen)
+  const uint64_t sec_lim64 = sec_end - wbase;
+  const uint32_t wlim = wlen;
+  uint32_t q = (uint32_t)(cursor - wbase);
+  int nr = 0;
+  int status = 0;
+  const int lim = max_recs < kMaxR ? max_recs : kMaxR;
+  while (nr < lim && (uint32_t)nr < rec_remaining) {
+    const uint32_t start = q;
+    const uint32_t have = wlim < sec_lim64 ? wlim : (uint32_t)sec_lim64;  // readable bytes in window
+    const bool win_short = (uint64_t)wlim < sec_lim64;                        // more section bytes exist
+#define WALK_FAIL()            \
+  do {                         \
+    status = win_short ? 2 : 1; \
+    goto done;                 \
+  } while (0)
+    int64_t len;
+    if (wvarint(w, q, have, &len)) WALK_FAIL();
+    if ((int64_t)(sec_lim64 - q) < len) {  // "not enough for record" (remaining is section-relative)
+      status = 1;
+      goto done;
+    }
+    if (q >= have) WALK_FAIL();
+    uint8_t attr = w[q++];
+    int64_t ts, od;
+    if (wvarint(w, q, have, &ts)) WALK_FAIL();
+    if (wvarint(w, q, have, &od)) WALK_FAIL();
+    if (q >= have) WALK_FAIL();
+    uint8_t tag = w[q++];
+    if (tag > 1) {
+      status = 1;
+      goto done;
+    }
+    uint32_t kpos = 0, klen = 0;
+    if (tag == 1) {
+      int64_t kl;
+      if (wvarint(w, q, have, &kl)) WALK_FAIL();
+      uint64_t want = (uint64_t)kl, rem = sec_lim64 - q;
+      uint64_t take = want < rem ? want : rem;
+      if ((uint64_t)q + take > have) {
+        status = 2;  // bytes exist in the section but not in the window
+        goto done;
+      }
+      kpos = q;
+      klen = (uint32_t)take;
+      q += (uint32_t)take;
+    }
+    int64_t vl;
+    if (wvarint(w, q, have, &vl)) WALK_FAIL();
+    {
+      uint64_t want = (uint64_t)vl, rem = sec_lim64 - q;
+      uint64_t take = want < rem ? want : rem;
+      if ((uint64_t)q + take > have) {
+        status = 2;
+        goto done;
+      }
+      L.r_vs[nr] = q;
+      L.r_vl[nr] = (uint32_t)take;
+      q += (uint32_t)take;
+    }
+    int64_t hdr;
+    if (wvarint(w, q, have, &hdr)) WALK_FAIL();
+#undef WALK_FAIL
+    L.r_start[nr] = start;
+    L.r_kpos[nr] = kpos;
+    L.r_klen[nr] = klen;
+    L.r_haskey[nr] = tag;
+    L.r_attr[nr] = attr;
+    L.r_od[nr] = od;
+    L.r_ts[nr] = ts;
+    L.r_hdr[nr] = hdr;
+    L.r_flags[nr] = RF_ALIVE;
+    L.r_es[nr] = 0xFF;
+    L.r_ec[nr] = 0;
+    L.r_ival[nr] = 0;
+    nr++;
+  }
+done:
+  if (status == 2 && nr > 0) status = 0;  // stop the window before the incomplete record
+  L.nr = nr;
+  L.walk_status = status;
+  const uint64_t nc = wbase + (nr > 0 ? (uint64_t)(L.r_vs[nr - 1] + L.r_vl[nr - 1]) : (cursor - wbase));
+  // next record starts after the headers varint of the last record: recompute
+  uint64_t nxt = cursor;
+  if (nr > 0) {
+    uint32_t qq = L.r_vs[nr - 1] + L.r_vl[nr - 1];
+    int64_t h;
+    wvarint(w, qq, wlen, &h);
+    nxt = wbase + qq;
+  }
+  (void)nc;
+  L.next_cursor_lo = (uint32_t)nxt;
+  L.next_cursor_hi = (uint32_t)(nxt >> 32);
+}
+
+// find the record whose [start, ...) region contains window offset p (largest r with r_vs[r] <= p)
+__device__ __forceinline__ int find_rec(const WaveLds& L, int nr, uint32_t p) {
+  int lo = 0, hi = nr - 1, r = -1;
+  while (lo <= hi) {
+    int m = (lo + hi) >> 1;
+    if (L.r_vs[m] <= p) {
+      r = m;
+      lo = m + 1;
+    } else
+      hi = m - 1;
+  }
+  return r;
+}
+
+// exact zero-byte mask: 0x80 in each byte of x that is zero
+__device__ __forceinline__ uint32_t zbytes(uint32_t x) {
+  return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+}
+
+// Data-parallel substring scan + non-ASCII marking over the values of the window.
+// Marks RF_MATCH on records whose (optionally uppercased) value contains needle.
+template <bool kLds, typename P>
+__device__ void scan_contains(WaveLds& L, P w, uint32_t wlen, int nr, const uint8_t* needle, uint32_t m, bool upper,
+                              bool mark_nonascii) {
+  if (nr == 0) return;
+  const uint32_t lo = L.r_vs[0];
+  const uint32_t hi = L.r_vs[nr - 1] + L.r_vl[nr - 1];
+  const uint32_t l = lane_id();
+  const uint8_t n0 = m ? needle[0] : 0;
+  const uint32_t N0 = 0x01010101u * n0;
+  const bool alt = upper && n0 >= 'A' && n0 <= 'Z';
+  const uint32_t N1 = 0x01010101u * (uint32_t)(n0 + 32);
+  for (uint32_t c = (lo & ~15u) + l * 16; c < hi; c += 64 * 16) {
+    uint32_t wd[4];
+    if constexpr (kLds) {
+      const uint4 v = *(const uint4*)(&L.win[c]);
+      wd[0] = v.x;
+      wd[1] = v.y;
+      wd[2] = v.z;
+      wd[3] = v.w;
+    } else {
+      for (int k = 0; k < 4; k++)
+        wd[k] = (uint32_t)w[c + 4 * k] | ((uint32_t)w[c + 4 * k + 1] << 8) | ((uint32_t)w[c + 4 * k + 2] << 16) |
+                ((uint32_t)w[c + 4 * k + 3] << 24);
+    }
+    for (int k = 0; k < 4; k++) {
+      uint32_t x = wd[k];
+      if (mark_nonascii && (x & 0x80808080u)) {
+        for (int j = 0; j < 4; j++) {
+          uint32_t p = c + 4 * k + j;
+          if (((x >> (8 * j)) & 0x80) && p >= lo && p < hi) {
+            int r = find_rec(L, nr, p);
+            if (r >= 0 && p < L.r_vs[r] + L.r_vl[r]) atomicOr(&L.r_flags[r], RF_NONASCII);
+          }
+        }
+      }
+      if (m == 0) continue;
+      uint32_t cand = zbytes(x ^ N0);
+      if (alt) cand |= zbytes(x ^ N1);
+      while (cand) {
+        int j = __builtin_ctz(cand) >> 3;
+        cand &= cand - 1;
+        cand &= ~(0x80u << (8 * j));
+        uint32_t p = c + 4 * k + j;
+        if (p < lo || p >= hi) continue;
+        int r = find_rec(L, nr, p);
+        if (r < 0) continue;
+        const uint32_t ve = L.r_vs[r] + L.r_vl[r];
+        if (p + m > ve) continue;
+        if (L.r_flags[r] & RF_MATCH) continue;
+        bool ok = true;
+        for (uint32_t t = 1; t < m; t++) {
+          uint8_t y = w[p + t];
+          if (upper) y = up(y);
+          if (y != needle[t]) {
+            ok = false;
+            break;
+          }
+        }
+        if (ok) atomicOr(&L.r_flags[r], RF_MATCH);
+      }
+    }
+  }
+  (void)wlen;
+}
+
+// records with an empty value never get a scan hit; an empty needle matches all
+// Data-parallel non-ASCII marking only
+template <bool kLds, typename P>
+__device__ void scan_nonascii(WaveLds& L, P w, uint32_t wlen, int nr) {
+  scan_contains<kLds>(L, w, wlen, nr, nullptr, 0, false, true);
+}
+
+// DFA helpers
+struct DfaView {
+  const uint8_t* cls;
+  const uint8_t* trans;
+  const uint8_t* acc;
+  uint32_t ncls;
+};
+
+// Bounded-length regex: each lane scans its 16-byte chunks plus max_len bytes of
+// overlap, restarting at value starts; any match inside a value marks RF_MATCH.
+template <typename P>
+__device__ void scan_regex_bounded(WaveLds& L, P w, int nr, const DfaView& d, uint32_t s_bot, uint32_t s_mid,
+                                   uint32_t max_len) {
+  if (nr == 0) return;
+  const uint32_t lo = L.r_vs[0];
+  const uint32_t hi = L.r_vs[nr - 1] + L.r_vl[nr - 1];
+  const uint32_t l = lane_id();
+  for (uint32_t c0 = (lo & ~15u) + l * 16; c0 < hi; c0 += 64 * 16) {
+    uint32_t c = c0 < lo ? lo : c0;
+    int r = find_rec(L, nr, c);
+    if (r < 0) r = 0;
+    uint32_t send = c0 + 16 + max_len;
+    if (send > hi) send = hi;
+    uint32_t q = c;
+    bool have_state = false;
+    uint32_t st = 0;
+    while (q < send && r < nr) {
+      const uint32_t vs = L.r_vs[r], ve = vs + L.r_vl[r];
+      if (q >= ve) {
+        if (have_state && (d.acc[st] & 2)) atomicOr(&L.r_flags[r], RF_MATCH);
+        have_state = false;
+        r++;
+        continue;
+      }
+      if (q < vs) {
+        q = vs;
+        have_state = false;
+        continue;
+      }
+      if (!have_state) {
+        st = (q == vs) ? s_bot : s_mid;
+        have_state = true;
+        if (d.acc[st] & 1) {
+          atomicOr(&L.r_flags[r], RF_MATCH);
+          q = ve;
+          continue;
+        }
+      }
+      st = d.trans[st * d.ncls + d.cls[w[q]]];
+      q++;
+      if (d.acc[st] & 1) {
+        atomicOr(&L.r_flags[r], RF_MATCH);
+        q = ve;  // value decided; skip its remainder
+        have_state = false;
+        r++;
+        continue;
+      }
+    }
+    // a value that ends exactly at send: check end-of-text acceptance
+    if (have_state && r < nr && q == L.r_vs[r] + L.r_vl[r] && (d.acc[st] & 2)) atomicOr(&L.r_flags[r], RF_MATCH);
+  }
+}
+
+// serial DFA over one byte sequence (unbounded patterns / short values)
+template <typename P>
+__device__ bool dfa_run(P s, uint32_t n, const DfaView& d, uint32_t s_bot) {
+  uint32_t st = s_bot;
+  if (d.acc[st] & 1) return true;
+  for (uint32_t i = 0; i < n; i++) {
+    st = d.trans[st * d.ncls + d.cls[s[i]]];
+    if (d.acc[st] & 1) return true;
+  }
+  return (d.acc[st] & 2) != 0;
+}
+
+// serial full (Unicode) DFA: u16 transitions read through L1/L2
+template <typename P>
+__device__ bool dfa_run_full(P s, uint32_t n, const uint8_t* blob, const DfaDesc& f, bool upper) {
+  const uint8_t* cls = blob + (upper ? f.f_classmap_up : f.f_classmap);
+  const uint16_t* tr = (const uint16_t*)(blob + f.f_trans);
+  const uint8_t* acc = blob + f.f_accept;
+  uint32_t st = f.f_s_bot;
+  if (acc[st] & 1) return true;
+  for (uint32_t i = 0; i < n; i++) {
+    st = tr[st * f.f_nclasses + cls[s[i]]];
+    if (acc[st] & 1) return true;
+  }
+  return (acc[st] & 2) != 0;
+}
+
+// ---------------------------------------------------------------------------
+// evaluate the chain (stages [0, nst)) over the records of one window
+// ---------------------------------------------------------------------------
+template <bool kLds, typename P>
+__device__ void eval_window(WaveLds& L, P w, uint32_t wlen, int nr, const ChainDesc& ch, const uint8_t* blob,
+                            int nst, bool& unsupported) {
+  const uint32_t l = lane_id();
+  bool nonascii_done = false;
+  for (int s = 0; s < nst; s++) {
+    const StageDesc& sd = ch.st[s];
+    const uint8_t op = sd.op;
+    const bool src = sd.in_type != VT_I32;
+    const bool upper = sd.in_type == VT_SRC_UPPER;
+    if (op == OP_MAP_UPPER) continue;  // value representation changes statically
+    const bool need_utf8 = src && (op == OP_CONTAINS || op == OP_REGEX || op == OP_FILTER_ODD ||
+                                   op == OP_MAP_DOUBLE || op == OP_AGG_SUM);
+    // ---- data-parallel phase over window bytes
+    for (int r = l; r < nr; r += 64) L.r_flags[r] &= ~RF_MATCH;
+    __syncthreads();
+    if (src && op == OP_CONTAINS) {
+      scan_contains<kLds>(L, w, wlen, nr, blob + sd.needle, sd.needle_len, upper, !nonascii_done);
+      nonascii_done = true;
+    } else if (need_utf8 && !nonascii_done) {
+      scan_nonascii<kLds>(L, w, wlen, nr);
+      nonascii_done = true;
+    }
+    DfaView dv;
+    if (op == OP_REGEX) {
+      const bool in_lds = sd.dfa.nstates * sd.dfa.nclasses <= (uint32_t)kDfaLds;
+      dv.cls = in_lds ? (upper ? L.dfa_clsu : L.dfa_cls) : blob + (upper ? sd.dfa.classmap_up : sd.dfa.classmap);
+      dv.trans = in_lds ? L.dfa_trans : blob + sd.dfa.trans;
+      dv.acc = in_lds ? L.dfa_acc : blob + sd.dfa.accept;
+      dv.ncls = sd.dfa.nclasses;
+      if (src && sd.dfa.max_len >= 0)
+        scan_regex_bounded(L, w, nr, dv, sd.dfa.s_bot, sd.dfa.s_mid, (uint32_t)sd.dfa.max_len);
+    }
+    __syncthreads();
+    // ---- per-record phase (lane per record)
+    for (int r = l; r < nr; r += 64) {
+      uint32_t f = L.r_flags[r];
+      if (!(f & RF_ALIVE)) continue;
+      const uint32_t vs = L.r_vs[r], vl = L.r_vl[r];
+      if (need_utf8 && (f & RF_NONASCII) && !(f & RF_UTF8_DONE)) {
+        uint32_t vut = 0, el = 0;
+        if (!utf8_check(w + vs, vl, &vut, &el)) {
+          f |= RF_UTF8_BAD;
+          L.r_aux[r] = vut;
+          L.r_aux2[r] = el;
+        }
+        f |= RF_UTF8_DONE;
+      }
+      bool err = false;
+      uint8_t ec = 0;
+      const int32_t ival_in = L.r_ival[r];
+      if (op == OP_AGG_SUM && sd.acc_bad) {
+        err = true;
+        ec = EC_ACC_UTF8;
+        L.r_aux[r] = sd.acc_vut;
+        L.r_aux2[r] = sd.acc_elen;
+      } else if (need_utf8 && (f & RF_UTF8_BAD)) {
+        err = true;
+        ec = EC_UTF8;
+      } else {
+        switch (op) {
+          case OP_CONTAINS: {
+            bool keep;
+            if (src) {
+              keep = (f & RF_MATCH) || sd.needle_len == 0;
+            } else {
+              uint8_t t[12];
+              uint32_t n = fmt_i32(ival_in, t);
+              keep = sd.needle_len == 0;
+              const uint8_t* nd = blob + sd.needle;
+              for (uint32_t i = 0; !keep && i + sd.needle_len <= n; i++) {
+                uint32_t k = 0;
+                while (k < sd.needle_len && t[i + k] == nd[k]) k++;
+                keep = k == sd.needle_len;
+              }
+            }
+            if (!keep) f &= ~RF_ALIVE;
+            break;
+          }
+          case OP_REGEX: {
+            bool m;
+            if (src) {
+              if (f & RF_NONASCII) {
+                if (sd.dfa.unicode_word) unsupported = true;
+                m = dfa_run_full(w + vs, vl, blob, sd.dfa, upper);
+              } else if (sd.dfa.max_len >= 0) {
+                m = (f & RF_MATCH) != 0;
+                // an empty value is never visited by the chunk scan
+                if (vl == 0) m = dfa_run(w + vs, 0u, dv, sd.dfa.s_bot);
+              } else {
+                m = dfa_run(w + vs, vl, dv, sd.dfa.s_bot);
+              }
+            } else {
+              uint8_t t[12];
+              uint32_t n = fmt_i32(ival_in, t);
+              m = dfa_run((const uint8_t*)t, n, dv, sd.dfa.s_bot);
+            }
+            bool keep = sd.keep_match ? m : !m;
+            if (!keep) f &= ~RF_ALIVE;
+            break;
+          }
+          case OP_FILTER_ODD:
+          case OP_MAP_DOUBLE:
+          case OP_FILTER_MAP:
+          case OP_AGG_SUM: {
+            int32_t x = 0;
+            int pk = 0;
+            if (src) {
+              uint32_t b = 0, e = vl;
+              if (op == OP_AGG_SUM) utf8_trim(w + vs, vl, &b, &e);
+              pk = parse_i32(w + vs + b, e - b, &x);
+            } else {
+              x = ival_in;
+            }
+            if (pk) {
+              err = true;
+              ec = EC_PARSE;
+              L.r_aux[r] = (uint32_t)pk;
+              break;
+            }
+            if (op == OP_FILTER_ODD) {
+              if (x % 2 != 0) f &= ~RF_ALIVE;
+            } else if (op == OP_MAP_DOUBLE) {
+              L.r_ival[r] = (int32_t)((uint32_t)x * 2u);
+            } else if (op == OP_FILTER_MAP) {
+              if (x % 2 == 0)
+                L.r_ival[r] = x / 2;
+              else
+                f &= ~RF_ALIVE;
+            } else {
+              L.r_ival[r] = x;  // aggregate input; running sum formed by the cross-batch scan
+            }
+            break;
+          }
+          default: break;
+        }
+      }
+      if (err) {
+        f &= ~RF_ALIVE;
+        L.r_es[r] = (uint8_t)s;
+        L.r_ec[r] = ec;
+        L.r_ival_in[r] = ival_in;
+      }
+      L.r_flags[r] = f;
+    }
+    __syncthreads();
+  }
+}
+
+// stage window bytes [al, al+wlen) into LDS with 16-byte coalesced loads
+__device__ __forceinline__ void load_window(WaveLds& L, const uint8_t* slice, uint64_t al, uint32_t wlen) {
+  const uint32_t l = lane_id();
+  const uint4* src = (const uint4*)(slice + al);
+  uint4* dst = (uint4*)L.win;
+  const uint32_t n16 = (wlen + 15) / 16;
+  for (uint32_t i = l; i < n16; i += 64) dst[i] = src[i];
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// k_eval — one 64-lane workgroup per stored batch
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_eval(EvalArgs a) {
+  __shared__ WaveLds L;
+  const uint32_t b = blockIdx.x;
+  const uint32_t l = lane_id();
+  const ChainDesc& ch = *a.chain;
+  const uint8_t* S = a.slice;
+  const uint64_t pos = a.bpos[b];
+  // ---- batch header (file format, batch.rs:163-180)
+  const uint8_t* h = S + pos;
+  const int64_t base_offset = (int64_t)rd_be(h, 8);
+  const int32_t batch_len = (int32_t)rd_be(h + 8, 4);
+  const int32_t lod_in = (int32_t)rd_be(h + 23, 4);
+  const int64_t first_ts = (int64_t)rd_be(h + 27, 8);
+  const uint64_t sec0 = pos + 57;
+  const uint64_t sec_end = pos + 12 + (uint64_t)(uint32_t)batch_len;  // framing validated at ingest
+  const uint32_t sec_len = (uint32_t)(sec_end - sec0);
+  // ---- stage the DFA of a regex stage into LDS (first one only)
+  for (int s = 0; s < (int)ch.nstages; s++) {
+    const StageDesc& sd = ch.st[s];
+    if (sd.op == OP_REGEX && sd.dfa.nstates * sd.dfa.nclasses <= (uint32_t)kDfaLds) {
+      for (uint32_t i = l; i < 256; i += 64) {
+        L.dfa_cls[i] = a.blob[sd.dfa.classmap + i];
+        L.dfa_clsu[i] = a.blob[sd.dfa.classmap_up + i];
+        L.dfa_acc[i] = i < sd.dfa.nstates ? a.blob[sd.dfa.accept + i] : 0;
+      }
+      for (uint32_t i = l; i < sd.dfa.nstates * sd.dfa.nclasses; i += 64) L.dfa_trans[i] = a.blob[sd.dfa.trans + i];
+      break;
+    }
+  }
+  // ---- Vec<Record> count (decoder.rs:43-55)
+  uint32_t flags = 0;
+  int32_t count = 0;
+  if (sec_len < 4) {
+    flags |= BF_DECODE;
+  } else {
+    count = (int32_t)rd_be(S + sec0, 4);
+  }
+  const uint32_t nrec_total = count > 0 ? (uint32_t)count : 0u;
+  const uint64_t rb = a.rbase[b];
+  // phase A: full chain; phase B (only if a record error occurred): truncated chain
+  int nst = (int)ch.nstages;
+  uint32_t err_stage = 0xFFFFFFFFu, err_idx = 0xFFFFFFFFu;
+  uint32_t err_code = 0, err_aux = 0, err_aux2 = 0;
+  int32_t err_ival = 0;
+  uint64_t err_pos = 0;
+  int64_t err_od = 0;
+  bool unsupported = false;
+  uint32_t kcount = 0;
+  int64_t aggsum = 0;
+  for (int phase = 0; phase < 2 && !(flags & BF_DECODE); phase++) {
+    if (phase == 1) {
+      if (err_stage == 0xFFFFFFFFu) break;
+      nst = (int)err_stage + 1;
+    }
+    kcount = 0;
+    aggsum = 0;
+    uint64_t cursor = sec0 + 4;
+    uint32_t done_recs = 0;
+    const uint32_t rec_cap = phase == 1 ? err_idx : nrec_total;
+    const bool agg_on = ch.has_agg && (phase == 0 || err_stage + 1 == ch.nstages);
+    const int last = nst - 1;
+    const uint8_t out_type = (nst == (int)ch.nstages) ? (uint8_t)ch.out_type : ch.st[nst].in_type;
+    while (done_recs < nrec_total && done_recs < (phase == 1 ? rec_cap + 1 : nrec_total)) {
+      // window [al, al + wlen)
+      const uint64_t al = cursor & ~15ull;
+      uint64_t wend = al + kWin;
+      const uint64_t sec_end16 = (sec_end + 15) & ~15ull;
+      if (wend > sec_end16) wend = sec_end16;
+      const uint32_t wlen = (uint32_t)(wend - al);
+      __syncthreads();
+      load_window(L, S, al, wlen);
+      if (l == 0) walk_records(L, (const uint8_t*)L.win, al, wlen, sec_end, cursor, nrec_total - done_recs, kMaxR);
+      __syncthreads();
+      int nr = L.nr;
+      const int ws = L.walk_status;
+      bool global_mode = false;
+      uint64_t gbase = 0;
+      if (nr == 0) {
+        if (ws == 1) {
+          flags |= BF_DECODE;
+          break;
+        }
+        // a record larger than the window: evaluate it from global memory
+        global_mode = true;
+        gbase = cursor;
+        __syncthreads();
+        if (l == 0) walk_records(L, S + gbase, gbase, (uint32_t)(sec_end - gbase), sec_end, cursor, 1, 1);
+        __syncthreads();
+        nr = L.nr;
+        if (nr == 0) {
+          flags |= BF_DECODE;
+          break;
+        }
+      }
+      // phase B: only records before the error record
+      int nr_eval = nr;
+      if (phase == 1 && done_recs + (uint32_t)nr > err_idx + 1) nr_eval = (int)(err_idx + 1 - done_recs);
+      if (global_mode)
+        eval_window<false>(L, S + gbase, (uint32_t)(sec_end - gbase), nr_eval, ch, a.blob, nst, unsupported);
+      else
+        eval_window<true>(L, (const uint8_t*)L.win, wlen, nr_eval, ch, a.blob, nst, unsupported);
+      const uint64_t wbase = global_mode ? gbase : al;
+      // ---- error tracking (phase A) and descriptor emission
+      for (int r0 = 0; r0 < nr_eval; r0 += 64) {
+        const int r = r0 + (int)l;
+        const bool valid = r < nr_eval;
+        const uint32_t gidx = done_recs + (uint32_t)r;
+        bool is_err = false;
+        uint32_t es = 0xFFu;
+        if (valid) {
+          es = L.r_es[r];
+          is_err = es != 0xFFu;
+        }
+        if (phase == 0) {
+          // lexicographic min (stage, index) over the wave
+          uint64_t key = is_err ? (((uint64_t)es << 32) | gidx) : ~0ull;
+          for (int o = 32; o > 0; o >>= 1) {
+            uint64_t t = __shfl_xor(key, o, 64);
+            key = t < key ? t : key;
+          }
+          if (key != ~0ull) {
+            const uint32_t ks = (uint32_t)(key >> 32), ki = (uint32_t)key;
+            if (ks < err_stage || (ks == err_stage && ki < err_idx)) {
+              err_stage = ks;
+              err_idx = ki;
+              const int rr = (int)(ki - done_recs);
+              err_code = L.r_ec[rr];
+              err_aux = L.r_aux[rr];
+              err_aux2 = L.r_aux2[rr];
+              err_ival = L.r_ival_in[rr];
+              err_pos = wbase + L.r_start[rr];
+              err_od = L.r_od[rr];
+            }
+          }
+        }
+        bool kept = valid && !is_err && (L.r_flags[r] & RF_ALIVE);
+        if (phase == 1 && gidx >= err_idx) kept = false;
+        const uint64_t bal = ballot(kept);
+        const uint32_t pre = (uint32_t)__popcll(bal & ((1ull << l) - 1ull));
+        int32_t local = 0;
+        if (agg_on) {
+          int32_t v = kept ? L.r_ival[r] : 0;
+          // wrapping i32 inclusive scan
+          uint32_t uv = (uint32_t)v;
+          for (int o = 1; o < 64; o <<= 1) {
+            uint32_t t = __shfl_up(uv, o, 64);
+            if ((int)l >= o) uv += t;
+          }
+          local = (int32_t)((uint32_t)aggsum + uv);
+          aggsum = (int64_t)(int32_t)((uint32_t)aggsum + (uint32_t)__shfl(uv, 63, 64));
+        }
+        if (kept) {
+          KeptRec d;
+          d.src = wbase + L.r_start[r];
+          d.od = L.r_od[r];
+          const uint32_t klen = L.r_klen[r];
+          d.kpos = L.r_haskey[r] ? (wbase + L.r_kpos[r]) : 0;
+          d.klen = klen;
+          d.has_key = L.r_haskey[r];
+          d.attr = L.r_attr[r];
+          d.ts = L.r_ts[r];
+          d.hdr = L.r_hdr[r];
+          d.vpos = wbase + L.r_vs[r];
+          d.vlen = L.r_vl[r];
+          if (agg_on) {
+            d.mode = KM_AGG;
+            d.ival = local;
+          } else if (out_type == VT_I32) {
+            d.mode = KM_I32;
+            d.ival = L.r_ival[r];
+          } else {
+            d.mode = out_type == VT_SRC_UPPER ? KM_UPPER : KM_COPY;
+            d.ival = 0;
+          }
+          a.desc[rb + kcount + pre] = d;
+        }
+        kcount += (uint32_t)__popcll(bal);
+      }
+      done_recs += (uint32_t)nr;
+      cursor = ((uint64_t)L.next_cursor_hi << 32) | L.next_cursor_lo;
+      (void)last;
+    }
+    if (phase == 0 && err_stage == 0xFFFFFFFFu) break;
+  }
+  if (!(flags & BF_DECODE) && err_stage != 0xFFFFFFFFu) flags |= BF_ERR;
+  if (err_stage == 0xFFFFFFFFu || err_stage + 1 == ch.nstages) flags |= BF_LAST_STAGE;
+  if (unsupported) flags |= BF_UNSUPPORTED;
+  if (l == 0) {
+    BatchStat st;
+    st.base_offset = base_offset;
+    st.first_ts = first_ts;
+    st.lod_in = lod_in;
+    st.flags = flags;
+    st.nkeep = kcount;
+    st.sec_len = sec_len;
+    st.err_stage = err_stage;
+    st.err_code = err_code;
+    st.err_pos = err_pos;
+    st.err_od = err_od;
+    st.err_ival = err_ival;
+    st.err_aux = err_aux;
+    st.err_aux2 = err_aux2;
+    st.pad = 0;
+    st.agg_sum = (ch.has_agg && (err_stage == 0xFFFFFFFFu || err_stage + 1 == ch.nstages)) ? aggsum : 0;
+    a.bstat[b] = st;
+    if (flags & BF_DECODE) atomicMin(&a.mins->first_dec, b);
+    if (flags & BF_UNSUPPORTED) atomicMin(&a.mins->first_unsup, b);
+    if (!(flags & BF_DECODE)) {
+      if (kcount) atomicMin(&a.mins->first_keep, b);
+      if (flags & BF_ERR) atomicMin(&a.mins->first_err, b);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// output record size of a descriptor after the offset fix-up
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t out_vlen(const KeptRec& d, int32_t agg_base) {
+  if (d.mode == KM_I32) return dec_len_i32(d.ival);
+  if (d.mode == KM_AGG) return dec_len_i32((int32_t)((uint32_t)agg_base + (uint32_t)d.ival));
+  return d.vlen;
+}
+__device__ __forceinline__ uint32_t rec_out_size(const KeptRec& d, int64_t rel, int32_t agg_base) {
+  const uint32_t vl = out_vlen(d, agg_base);
+  uint32_t inner = 1 + vsize(d.ts) + vsize(d.od + rel) + 1 + (d.has_key ? vsize((int64_t)d.klen) + d.klen : 0) +
+                   vsize((int64_t)vl) + vl + vsize(d.hdr);
+  return vsize((int64_t)inner) + inner;
+}
+
+
+
+// k_size: one wave per batch (4 batches per 256-thread block)
+__global__ __launch_bounds__(256) void k_size(SizeArgs a) {
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t l = lane_id();
+  if (b >= a.nbatches) return;
+  const BatchStat st = a.bstat[b];
+  const uint32_t f = a.mins->first_keep;
+  ScanRow row = {};
+  if (a.agg_only) {
+    row.agg = st.agg_sum;
+    if (l == 0) a.rows[b] = row;
+    return;
+  }
+  row.bytes_in = st.sec_len;
+  row.recs_out = (st.flags & BF_LAST_STAGE) ? st.nkeep : 0;
+  row.agg = st.agg_sum;
+  if (f != 0xFFFFFFFFu && b >= f && !(st.flags & BF_DECODE)) {
+    const int64_t rel = a.bstat[f].base_offset - st.base_offset;
+    const int32_t agg_base = a.agg_pre ? (int32_t)((uint64_t)a.acc0 + (uint64_t)a.agg_pre[b].agg) : 0;
+    uint64_t sum = 0;
+    const KeptRec* d = a.desc + a.rbase[b];
+    for (uint32_t k = l; k < st.nkeep; k += 64) sum += rec_out_size(d[k], rel, agg_base);
+    sum = wave_sum(sum);
+    row.rec_bytes = sum;
+    row.nonempty = st.nkeep ? 1 : 0;
+    row.lod = (uint64_t)(int64_t)(st.lod_in + 1);
+    row.nrec = st.nkeep;
+  }
+  if (l == 0) a.rows[b] = row;
+}
+
+// ---------------------------------------------------------------------------
+// cross-batch exclusive scan of ScanRow (3 kernels)
+// ---------------------------------------------------------------------------
+constexpr int kScanBlock = 256;
+constexpr int kScanPer = 8;  // rows per thread
+constexpr int kScanTile = kScanBlock * kScanPer;
+
+__device__ __forceinline__ void row_add(ScanRow& a, const ScanRow& b) {
+  a.rec_bytes += b.rec_bytes;
+  a.nonempty += b.nonempty;
+  a.lod += b.lod;
+  a.nrec += b.nrec;
+  a.bytes_in += b.bytes_in;
+  a.recs_out += b.recs_out;
+  a.agg = (int64_t)(int32_t)((uint32_t)a.agg + (uint32_t)b.agg);
+}
+
+__device__ void block_excl_scan(ScanRow& v, ScanRow* sh, ScanRow& total) {
+  // Hillis-Steele over 256 threads through LDS (rows are 64 B)
+  const int t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  for (int o = 1; o < kScanBlock; o <<= 1) {
+    ScanRow x = sh[t];
+    if (t >= o) row_add(x, sh[t - o]);
+    __syncthreads();
+    sh[t] = x;
+    __syncthreads();
+  }
+  total = sh[kScanBlock - 1];
+  ScanRow ex = {};
+  if (t > 0) ex = sh[t - 1];
+  v = ex;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void k_scan_reduce(const ScanRow* rows, uint32_t n, ScanRow* tile_sums) {
+  __shared__ ScanRow sh[kScanBlock];
+  const uint32_t base = blockIdx.x * kScanTile;
+  ScanRow acc = {};
+  for (int k = 0; k < kScanPer; k++) {
+    uint32_t i = base + threadIdx.x * kScanPer + k;
+    if (i < n) row_add(acc, rows[i]);
+  }
+  ScanRow total;
+  block_excl_scan(acc, sh, total);
+  if (threadIdx.x == 0) tile_sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void k_scan_top(ScanRow* tile_sums, uint32_t ntiles, ScanRow* grand) {
+  __shared__ ScanRow sh[kScanBlock];
+  ScanRow carry = {};
+  for (uint32_t base = 0; base < ntiles; base += kScanBlock) {
+    uint32_t i = base + threadIdx.x;
+    ScanRow v = {};
+    if (i < ntiles) v = tile_sums[i];
+    ScanRow total;
+    block_excl_scan(v, sh, total);
+    row_add(v, carry);
+    if (i < ntiles) tile_sums[i] = v;
+    row_add(carry, total);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *grand = carry;
+}
+
+struct ScanDownArgs {
+  const ScanRow* rows;
+  ScanRow* pre;
+  const ScanRow* tile_sums;
+  uint32_t n;
+  uint32_t detect_cut;
+  uint64_t max_bytes;
+  Mins* mins;
+  const BatchStat* bstat;
+};
+
+__global__ __launch_bounds__(256) void k_scan_down(ScanDownArgs a) {
+  __shared__ ScanRow sh[kScanBlock];
+  const uint32_t base = blockIdx.x * kScanTile;
+  ScanRow acc = {};
+  for (int k = 0; k < kScanPer; k++) {
+    uint32_t i = base + threadIdx.x * kScanPer + k;
+    if (i < a.n) row_add(acc, a.rows[i]);
+  }
+  ScanRow total;
+  block_excl_scan(acc, sh, total);
+  ScanRow run = a.tile_sums[blockIdx.x];
+  row_add(run, acc);
+  const uint32_t f = a.mins->first_keep;
+  for (int k = 0; k < kScanPer; k++) {
+    uint32_t i = base + threadIdx.x * kScanPer + k;
+    if (i >= a.n) break;
+    const ScanRow v = a.rows[i];
+    a.pre[i] = run;
+    row_add(run, v);
+    // max_bytes cut (batch.rs:101-111): total + records.write_size(0) > max_bytes
+    if (a.detect_cut && f != 0xFFFFFFFFu && i >= f && v.nonempty) {
+      const uint64_t incl = run.rec_bytes + 4ull * run.nonempty;
+      if (incl > a.max_bytes) atomicMin(&a.mins->cut, i);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_plan: the process_batch stop rules (batch.rs:41-142), one thread
+// ---------------------------------------------------------------------------
+
+
+__device__ __forceinline__ ScanRow incl_at(const PlanArgs& a, uint32_t i) {
+  ScanRow r = a.pre[i];
+  row_add(r, a.rows[i]);
+  return r;
+}
+
+__global__ void k_plan(PlanArgs a) {
+  if (threadIdx.x != 0) return;
+  const uint32_t NONE = 0xFFFFFFFFu;
+  const uint32_t n = a.nbatches;
+  const uint32_t f = a.mins->first_keep, e = a.mins->first_err, d = a.mins->first_dec, u = a.mins->first_unsup;
+  const uint32_t c = a.mins->cut;
+  Plan p = {};
+  p.err_batch = -1;
+  p.first = -1;
+  p.last = -1;
+  p.stop = -1;
+  p.lod = -1;
+  p.base_offset = -1;
+  // stop batch: min(error batch, cut batch); the cut batch was processed too
+  uint32_t stop = n ? n - 1 : NONE;
+  bool cut = false, err = false;
+  if (c != NONE && (e == NONE || c <= e)) {
+    stop = c;
+    cut = true;
+    err = (c == e);
+  } else if (e != NONE) {
+    stop = e;
+    err = true;
+  }
+  int status = 0;
+  uint32_t fail_at = NONE;
+  if (d != NONE && (stop == NONE || d <= stop)) {
+    status = a.empty_chain ? -104 : -11;  // FSG_E_IO / FSG_E_DECODING_BASE_INPUT
+    fail_at = d;
+  }
+  if (u != NONE && (stop == NONE || u <= stop) && (fail_at == NONE || u < fail_at)) {
+    status = -103;  // FSG_E_UNSUPPORTED
+    fail_at = u;
+  }
+  if (status == 0 && a.tail_status != 0 && !cut && !err) {
+    status = a.tail_status;  // the iterator hit a bad batch after the last framed one
+  }
+  if (status != 0) {
+    p.status = status;
+    const uint32_t m = fail_at != NONE ? fail_at : (n ? n - 1 : NONE);
+    if (m != NONE) {
+      ScanRow r = incl_at(a, m);
+      p.bytes_in = r.bytes_in;
+      p.invocations = m + 1;
+    }
+    *a.plan = p;
+    return;
+  }
+  if (stop == NONE) {  // no batches at all
+    *a.plan = p;
+    return;
+  }
+  p.stop = (int32_t)stop;
+  const ScanRow rs = incl_at(a, stop);
+  p.bytes_in = rs.bytes_in;
+  p.invocations = stop + 1;
+  p.records_out = rs.recs_out;
+  if (a.has_agg) {
+    p.acc_final = (int64_t)(int32_t)((uint64_t)a.acc0 + (uint64_t)rs.agg);
+    p.acc_touched = rs.recs_out > 0;  // aggregate emits one record per aggregated input
+  }
+  const int64_t last = cut ? (int64_t)c - 1 : (int64_t)stop;
+  if (err) p.err_batch = (int32_t)e;
+  if (f != NONE && f <= stop) {
+    p.first = (int32_t)f;
+    p.base_offset = a.bstat[f].base_offset;  // set before the max_bytes check (batch.rs:85-91)
+    if ((int64_t)f <= last) {
+      p.last = (int32_t)last;
+      const ScanRow rl = incl_at(a, (uint32_t)last);
+      const ScanRow rf = a.pre[f];
+      p.lod = (int32_t)(-1 + (int64_t)(rl.lod - rf.lod));
+      p.n_records = rl.nrec - rf.nrec;
+      p.rec_bytes = rl.rec_bytes - rf.rec_bytes;
+    }
+  }
+  *a.plan = p;
+}
+
+// ---------------------------------------------------------------------------
+// k_header: output batch header (Batch::default() + base offset, lod, count)
+// ---------------------------------------------------------------------------
+__global__ void k_header(const Plan* plan, uint8_t* out) {
+  if (threadIdx.x != 0) return;
+  const Plan p = *plan;
+  uint8_t h[61];
+  auto be = [&](int off, uint64_t v, int nb) {
+    for (int i = 0; i < nb; i++) h[off + i] = (uint8_t)(v >> (8 * (nb - 1 - i)));
+  };
+  be(0, (uint64_t)p.base_offset, 8);
+  be(8, (uint32_t)(45 + 4 + p.rec_bytes), 4);
+  be(12, (uint32_t)-1, 4);  // partition_leader_epoch
+  h[16] = 2;                // magic
+  be(17, 0, 4);             // crc placeholder
+  be(21, 0, 2);             // attributes: compression None of the first surviving batch
+  be(23, (uint32_t)p.lod, 4);
+  be(27, (uint64_t)-1, 8);  // first_timestamp
+  be(35, (uint64_t)-1, 8);  // max_time_stamp
+  be(43, (uint64_t)-1, 8);  // producer_id
+  be(51, (uint16_t)-1, 2);  // producer_epoch
+  be(53, (uint32_t)-1, 4);  // first_sequence
+  be(57, (uint32_t)p.n_records, 4);
+  for (int i = 0; i < 61; i++) out[i] = h[i];
+}
+
+// ---------------------------------------------------------------------------
+// k_write: canonical re-encode of the kept records, one wave per included batch
+// ---------------------------------------------------------------------------
+
+
+__global__ __launch_bounds__(64) void k_write(WriteArgs a) {
+  const Plan p = *a.plan;
+  const int32_t b = p.first + (int32_t)blockIdx.x;
+  if (p.first < 0 || b > p.last) return;
+  const uint32_t l = lane_id();
+  const BatchStat st = a.bstat[b];
+  const int64_t rel = a.bstat[p.first].base_offset - st.base_offset;
+  const int32_t agg_base = a.agg_pre ? (int32_t)((uint64_t)a.acc0 + (uint64_t)a.agg_pre[b].agg) : 0;
+  const KeptRec* d = a.desc + a.rbase[b];
+  uint8_t* o = a.out + 61 + (a.pre[b].rec_bytes - a.pre[p.first].rec_bytes);
+  uint64_t run = 0;
+  for (uint32_t k0 = 0; k0 < st.nkeep; k0 += 64) {
+    const uint32_t k = k0 + l;
+    const bool v = k < st.nkeep;
+    KeptRec r = {};
+    uint32_t sz = 0;
+    if (v) {
+      r = d[k];
+      sz = rec_out_size(r, rel, agg_base);
+    }
+    const uint64_t incl = wave_incl_scan((uint64_t)sz);
+    const uint64_t my = run + incl - sz;
+    run += __shfl(incl, 63, 64);
+    // each lane writes its record's varint header and small fields
+    uint32_t vstart = 0, vl = 0, kstart = 0;
+    if (v) {
+      uint8_t* q = o + my;
+      vl = out_vlen(r, agg_base);
+      uint32_t inner = 1 + vsize(r.ts) + vsize(r.od + rel) + 1 +
+                       (r.has_key ? vsize((int64_t)r.klen) + r.klen : 0) + vsize((int64_t)vl) + vl + vsize(r.hdr);
+      uint8_t t[16];
+      uint32_t n = venc((int64_t)inner, t), w = 0;
+      for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
+      q[w++] = r.attr;
+      n = venc(r.ts, t);
+      for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
+      n = venc(r.od + rel, t);
+      for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
+      q[w++] = r.has_key ? 1 : 0;
+      if (r.has_key) {
+        n = venc((int64_t)r.klen, t);
+        for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
+        kstart = w;
+        w += r.klen;
+      }
+      n = venc((int64_t)vl, t);
+      for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
+      vstart = w;
+      if (r.mode == KM_I32 || r.mode == KM_AGG) {
+        const int32_t x = r.mode == KM_I32 ? r.ival : (int32_t)((uint32_t)agg_base + (uint32_t)r.ival);
+        w += fmt_i32(x, q + w);
+      } else {
+        w += vl;
+      }
+      n = venc(r.hdr, t);
+      for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
+    }
+    // cooperative copy of key and value bytes, one record at a time
+    const uint32_t nv = st.nkeep - k0 < 64 ? st.nkeep - k0 : 64;
+    for (uint32_t j = 0; j < nv; j++) {
+      const uint64_t pos = __shfl(my, (int)j, 64);
+      const uint32_t ks = __shfl(kstart, (int)j, 64);
+      const uint32_t vs = __shfl(vstart, (int)j, 64);
+      const KeptRec& rj = d[k0 + j];
+      uint8_t* q = o + pos;
+      if (rj.has_key) {
+        const uint8_t* ksrc = a.slice + rj.kpos;
+        for (uint32_t i = l; i < rj.klen; i += 64) q[ks + i] = ksrc[i];
+      }
+      if (rj.mode == KM_COPY || rj.mode == KM_UPPER) {
+        const uint8_t* vsrc = a.slice + rj.vpos;
+        const bool upc = rj.mode == KM_UPPER;
+        for (uint32_t i = l; i < rj.vlen; i += 64) {
+          uint8_t c = vsrc[i];
+          q[vs + i] = upc ? up(c) : c;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// CRC32C (reflected 0x82F63B78) over [off, off + n): chunked raw CRCs + combine
+// ---------------------------------------------------------------------------
+__constant__ uint32_t c_crc_tab[8][256];
+__constant__ uint32_t c_x2n[32];  // x^(2^k) mod P (zlib x2n_table, Castagnoli)
+
+__device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
+  uint32_t m = 1u << 31, p = 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = (b & 1) ? (b >> 1) ^ 0x82F63B78u : b >> 1;
+  }
+  return p;
+}
+// x^(8*len) mod P
+__device__ __forceinline__ uint32_t xpow8(uint64_t len) {
+  uint32_t p = 1u << 31;
+  unsigned k = 3;
+  while (len) {
+    if (len & 1) p = multmodp(c_x2n[k & 31], p);
+    len >>= 1;
+    k++;
+  }
+  return p;
+}
+
+constexpr int kCrcThreads = 256;
+constexpr int kCrcPerThread = kCrcChunk / kCrcThreads;  // 256 bytes
+
+// raw CRC (init 0, no final xor) of each kCrcChunk-byte chunk
+__global__ __launch_bounds__(256) void k_crc_chunks(const uint8_t* buf, uint64_t off, uint64_t n, uint32_t* parts) {
+  __shared__ uint32_t tab[8][256];
+  __shared__ uint32_t sh[kCrcThreads];
+  __shared__ uint32_t shl[kCrcThreads];
+  for (int i = threadIdx.x; i < 8 * 256; i += 256) tab[i >> 8][i & 255] = c_crc_tab[i >> 8][i & 255];
+  __syncthreads();
+  const uint64_t c0 = (uint64_t)blockIdx.x * kCrcChunk;
+  const uint64_t t0 = c0 + (uint64_t)threadIdx.x * kCrcPerThread;
+  uint32_t len = 0;
+  if (t0 < n) len = (uint32_t)((n - t0) < (uint64_t)kCrcPerThread ? (n - t0) : kCrcPerThread);
+  const uint8_t* p = buf + off + t0;
+  uint32_t c = 0;
+  uint32_t i = 0;
+  for (; i + 8 <= len; i += 8) {
+    uint32_t lo = (uint32_t)p[i] | ((uint32_t)p[i + 1] << 8) | ((uint32_t)p[i + 2] << 16) | ((uint32_t)p[i + 3] << 24);
+    uint32_t hi =
+        (uint32_t)p[i + 4] | ((uint32_t)p[i + 5] << 8) | ((uint32_t)p[i + 6] << 16) | ((uint32_t)p[i + 7] << 24);
+    lo ^= c;
+    c = tab[7][lo & 0xff] ^ tab[6][(lo >> 8) & 0xff] ^ tab[5][(lo >> 16) & 0xff] ^ tab[4][lo >> 24] ^
+        tab[3][hi & 0xff] ^ tab[2][(hi >> 8) & 0xff] ^ tab[1][(hi >> 16) & 0xff] ^ tab[0][hi >> 24];
+  }
+  for (; i < len; i++) c = tab[0][(c ^ p[i]) & 0xff] ^ (c >> 8);
+  sh[threadIdx.x] = c;
+  shl[threadIdx.x] = len;
+  __syncthreads();
+  // tree combine: (A, B) -> shift(A, |B|) ^ B
+  for (int s = 1; s < kCrcThreads; s <<= 1) {
+    if ((threadIdx.x % (2 * s)) == 0 && threadIdx.x + s < kCrcThreads) {
+      const uint32_t lb = shl[threadIdx.x + s];
+      uint32_t a = sh[threadIdx.x];
+      if (lb) a = multmodp(xpow8(lb), a);
+      sh[threadIdx.x] = a ^ sh[threadIdx.x + s];
+      shl[threadIdx.x] += lb;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) parts[blockIdx.x] = sh[0];
+}
+
+// fold the chunk CRCs in order with init 0xFFFFFFFF, write BE CRC at out[17..21)
+__global__ __launch_bounds__(1024) void k_crc_fold(const uint32_t* parts, uint32_t nparts, uint64_t n, uint8_t* out) {
+  __shared__ uint32_t sh[1024];
+  __shared__ uint64_t shl[1024];
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (nparts + 1023) / 1024;
+  const uint32_t i0 = t * per;
+  uint32_t c = 0;
+  uint64_t len = 0;
+  const uint32_t kfull = xpow8(kCrcChunk);
+  for (uint32_t i = i0; i < i0 + per && i < nparts; i++) {
+    const uint64_t clen = (uint64_t)(i + 1) * kCrcChunk <= n ? (uint64_t)kCrcChunk : n - (uint64_t)i * kCrcChunk;
+    const uint32_t sft = clen == (uint64_t)kCrcChunk ? kfull : xpow8(clen);
+    c = multmodp(sft, c) ^ parts[i];
+    len += clen;
+  }
+  sh[t] = c;
+  shl[t] = len;
+  __syncthreads();
+  for (int s = 1; s < 1024; s <<= 1) {
+    if ((t % (2 * s)) == 0 && t + s < 1024) {
+      const uint64_t lb = shl[t + s];
+      uint32_t a = sh[t];
+      if (lb) a = multmodp(xpow8(lb), a);
+      sh[t] = a ^ sh[t + s];
+      shl[t] += lb;
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    // register init 0xFFFFFFFF contributes shift(0xFFFFFFFF, n); final xor
+    uint32_t crc = sh[0] ^ multmodp(xpow8(n), 0xFFFFFFFFu);
+    crc ^= 0xFFFFFFFFu;
+    out[17] = (uint8_t)(crc >> 24);
+    out[18] = (uint8_t)(crc >> 16);
+    out[19] = (uint8_t)(crc >> 8);
+    out[20] = (uint8_t)crc;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host-side launch wrappers (called from fsg_runtime.cpp)
+// ---------------------------------------------------------------------------
+}  // namespace fsg
+
+#include "fsg_launch.h"
+
+namespace fsg {
+
+static bool g_tabs_ready = false;
+
+hipError_t upload_crc_tables() {
+  if (g_tabs_ready) return hipSuccess;
+  static uint32_t tab[8][256];
+  for (uint32_t i = 0; i < 256; i++) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : c >> 1;
+    tab[0][i] = c;
+  }
+  for (int t = 1; t < 8; t++)
+    for (uint32_t i = 0; i < 256; i++) tab[t][i] = (tab[t - 1][i] >> 8) ^ tab[0][tab[t - 1][i] & 0xff];
+  uint32_t x2n[32];
+  // host multmodp
+  auto mm = [](uint32_t a, uint32_t b) {
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+      if (a & m) {
+        p ^= b;
+        if ((a & (m - 1)) == 0) break;
+      }
+      m >>= 1;
+      b = (b & 1) ? (b >> 1) ^ 0x82F63B78u : b >> 1;
+    }
+    return p;
+  };
+  uint32_t p = 1u << 30;  // x^1
+  x2n[0] = p;
+  for (int n = 1; n < 32; n++) x2n[n] = p = mm(p, p);
+  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_crc_tab), tab, sizeof tab);
+  if (e != hipSuccess) return e;
+  e = hipMemcpyToSymbol(HIP_SYMBOL(c_x2n), x2n, sizeof x2n);
+  if (e == hipSuccess) g_tabs_ready = true;
+  return e;
+}
+
+void launch_eval(const EvalArgs& a, hipStream_t s) {
+  if (a.nbatches) hipLaunchKernelGGL(k_eval, dim3(a.nbatches), dim3(64), 0, s, a);
+}
+void launch_size(const SizeArgs& a, hipStream_t s) {
+  if (a.nbatches) hipLaunchKernelGGL(k_size, dim3((a.nbatches + 3) / 4), dim3(256), 0, s, a);
+}
+uint32_t scan_tiles(uint32_t n) { return (n + kScanTile - 1) / kScanTile; }
+void launch_scan(const ScanRow* rows, ScanRow* pre, ScanRow* tile_sums, ScanRow* grand, uint32_t n, bool cut,
+                 uint64_t max_bytes, Mins* mins, const BatchStat* bstat, hipStream_t s) {
+  if (!n) return;
+  const uint32_t nt = scan_tiles(n);
+  hipLaunchKernelGGL(k_scan_reduce, dim3(nt), dim3(kScanBlock), 0, s, rows, n, tile_sums);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanBlock), 0, s, tile_sums, nt, grand);
+  ScanDownArgs d{rows, pre, tile_sums, n, cut ? 1u : 0u, max_bytes, mins, bstat};
+  hipLaunchKernelGGL(k_scan_down, dim3(nt), dim3(kScanBlock), 0, s, d);
+}
+void launch_plan(const PlanArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_plan, dim3(1), dim3(64), 0, s, a); }
+void launch_header(const Plan* plan, uint8_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_header, dim3(1), dim3(64), 0, s, plan, out);
+}
+void launch_write(const WriteArgs& a, uint32_t nblocks, hipStream_t s) {
+  if (nblocks) hipLaunchKernelGGL(k_write, dim3(nblocks), dim3(64), 0, s, a);
+}
+uint32_t crc_parts(uint64_t n) { return (uint32_t)((n + kCrcChunk - 1) / kCrcChunk); }
+void launch_crc(const uint8_t* buf, uint64_t off, uint64_t n, uint32_t* parts, uint8_t* out, hipStream_t s) {
+  const uint32_t np = crc_parts(n);
+  if (np) hipLaunchKernelGGL(k_crc_chunks, dim3(np), dim3(kCrcThreads), 0, s, buf, off, n, parts);
+  hipLaunchKernelGGL(k_crc_fold, dim3(1), dim3(1024), 0, s, parts, np, n, out);
+}
+
+}  // namespace fsg

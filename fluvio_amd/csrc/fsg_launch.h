@@ -1,0 +1,19 @@
+// fsg_launch.h — host-side launch wrappers of the kernels in fsg_kernels.hip
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "fsg_device.h"
+
+namespace fsg {
+hipError_t upload_crc_tables();
+void launch_eval(const EvalArgs& a, hipStream_t s);
+void launch_size(const SizeArgs& a, hipStream_t s);
+uint32_t scan_tiles(uint32_t n);
+void launch_scan(const ScanRow* rows, ScanRow* pre, ScanRow* tile_sums, ScanRow* grand, uint32_t n, bool cut,
+                 uint64_t max_bytes, Mins* mins, const BatchStat* bstat, hipStream_t s);
+void launch_plan(const PlanArgs& a, hipStream_t s);
+void launch_header(const Plan* plan, uint8_t* out, hipStream_t s);
+void launch_write(const WriteArgs& a, uint32_t nblocks, hipStream_t s);
+uint32_t crc_parts(uint64_t n);
+void launch_crc(const uint8_t* buf, uint64_t off, uint64_t n, uint32_t* parts, uint8_t* out, hipStream_t s);
+}  // namespace fsg

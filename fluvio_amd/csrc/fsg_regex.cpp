@@ -1,0 +1,775 @@
+// fsg_regex.cpp — chain-build-time compiler: Rust-regex pattern -> UTF-8 byte DFA.
+//
+// The reference compiles `Regex::new(param "regex")` inside the guest's init()
+// (smartmodule/regex-filter/src/lib.rs:13-22) and calls `Regex::is_match` per
+// record (lib.rs:24-28; filter_regex: examples/filter_regex/src/lib.rs).  The
+// regex crate (1.6.0 / 1.8.1) is a third-party dependency that is not in the
+// reference tree; we restate its published semantics for the supported subset:
+// unanchored is_match over valid UTF-8, Unicode-aware `.` (any scalar but \n),
+// `\d` (Unicode Nd), `\s` (White_Space), `^`/`$` at value start/end (no
+// multi-line flag).  `\w`/`\W` are exact on ASCII values only (the kernel
+// reports FSG_E_UNSUPPORTED for a non-ASCII value); \b, \p{..}, inline flags,
+// nested classes and class set operations are rejected at init (FSG_E_UNSUPPORTED).
+//
+// Output: a DFA over bytes with unanchored restart folded in, byte classes,
+// sticky acceptance, an end-of-value acceptance bit and the longest possible
+// match length (used by the kernel's chunk-parallel scan).
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "fsg_regex.h"
+
+namespace fsg {
+namespace {
+
+struct Range {
+  uint32_t lo, hi;
+};
+
+const Range kNd[] = {
+    {0x30, 0x39},       {0x660, 0x669},     {0x6F0, 0x6F9},     {0x7C0, 0x7C9},     {0x966, 0x96F},
+    {0x9E6, 0x9EF},     {0xA66, 0xA6F},     {0xAE6, 0xAEF},     {0xB66, 0xB6F},     {0xBE6, 0xBEF},
+    {0xC66, 0xC6F},     {0xCE6, 0xCEF},     {0xD66, 0xD6F},     {0xDE6, 0xDEF},     {0xE50, 0xE59},
+    {0xED0, 0xED9},     {0xF20, 0xF29},     {0x1040, 0x1049},   {0x1090, 0x1099},   {0x17E0, 0x17E9},
+    {0x1810, 0x1819},   {0x1946, 0x194F},   {0x19D0, 0x19D9},   {0x1A80, 0x1A89},   {0x1A90, 0x1A99},
+    {0x1B50, 0x1B59},   {0x1BB0, 0x1BB9},   {0x1C40, 0x1C49},   {0x1C50, 0x1C59},   {0xA620, 0xA629},
+    {0xA8D0, 0xA8D9},   {0xA900, 0xA909},   {0xA9D0, 0xA9D9},   {0xA9F0, 0xA9F9},   {0xAA50, 0xAA59},
+    {0xABF0, 0xABF9},   {0xFF10, 0xFF19},   {0x104A0, 0x104A9}, {0x10D30, 0x10D39}, {0x11066, 0x1106F},
+    {0x110F0, 0x110F9}, {0x11136, 0x1113F}, {0x111D0, 0x111D9}, {0x112F0, 0x112F9}, {0x11450, 0x11459},
+    {0x114D0, 0x114D9}, {0x11650, 0x11659}, {0x116C0, 0x116C9}, {0x11730, 0x11739}, {0x118E0, 0x118E9},
+    {0x11950, 0x11959}, {0x11C50, 0x11C59}, {0x11D50, 0x11D59}, {0x11DA0, 0x11DA9}, {0x11F50, 0x11F59},
+    {0x16A60, 0x16A69}, {0x16AC0, 0x16AC9}, {0x16B50, 0x16B59}, {0x1D7CE, 0x1D7FF}, {0x1E140, 0x1E149},
+    {0x1E2F0, 0x1E2F9}, {0x1E4F0, 0x1E4F9}, {0x1E950, 0x1E959}, {0x1FBF0, 0x1FBF9}};
+const Range kWs[] = {{0x09, 0x0D}, {0x20, 0x20},     {0x85, 0x85},     {0xA0, 0xA0},     {0x1680, 0x1680},
+                     {0x2000, 0x200A}, {0x2028, 0x2029}, {0x202F, 0x202F}, {0x205F, 0x205F}, {0x3000, 0x3000}};
+const Range kWordAscii[] = {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}};
+
+using Set = std::vector<Range>;
+
+Set norm(Set s) {
+  std::sort(s.begin(), s.end(), [](const Range& a, const Range& b) { return a.lo < b.lo; });
+  Set o;
+  for (auto& r : s) {
+    if (!o.empty() && r.lo <= o.back().hi + 1)
+      o.back().hi = std::max(o.back().hi, r.hi);
+    else
+      o.push_back(r);
+  }
+  return o;
+}
+Set negate(const Set& s0) {
+  Set s = norm(s0), o;
+  uint32_t next = 0;
+  for (auto& r : s) {
+    if (r.lo > next) o.push_back({next, r.lo - 1});
+    next = r.hi + 1;
+  }
+  if (next <= 0x10FFFF) o.push_back({next, 0x10FFFF});
+  return o;
+}
+template <size_t N>
+Set table(const Range (&t)[N], bool neg) {
+  Set s(t, t + N);
+  return neg ? negate(s) : s;
+}
+
+// ---------------- AST
+enum NodeT { N_EMPTY, N_SET, N_CAT, N_ALT, N_REP, N_BOL, N_EOL };
+struct Node {
+  NodeT t = N_EMPTY;
+  Set set;
+  std::vector<std::unique_ptr<Node>> kids;
+  std::unique_ptr<Node> sub;
+  int mn = 0, mx = 0;  // mx < 0: unbounded
+};
+using NodeP = std::unique_ptr<Node>;
+
+struct Parser {
+  std::vector<uint32_t> p;
+  size_t i = 0;
+  bool err = false, unsup = false, word = false;
+  int depth = 0;
+
+  bool at(uint32_t c) const { return i < p.size() && p[i] == c; }
+  static bool hex(uint32_t c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'); }
+  static uint32_t hv(uint32_t c) { return c <= '9' ? c - '0' : (c | 0x20) - 'a' + 10; }
+
+  // 1: single code point in *c; 2: set in *s; 0: failure (err/unsup set)
+  int escape(uint32_t* c, Set* s) {
+    if (i >= p.size()) {
+      err = true;
+      return 0;
+    }
+    uint32_t e = p[i++];
+    switch (e) {
+      case 'd': *s = table(kNd, false); return 2;
+      case 'D': *s = table(kNd, true); return 2;
+      case 's': *s = table(kWs, false); return 2;
+      case 'S': *s = table(kWs, true); return 2;
+      case 'w': *s = table(kWordAscii, false); word = true; return 2;
+      case 'W': *s = table(kWordAscii, true); word = true; return 2;
+      case 'n': *c = '\n'; return 1;
+      case 't': *c = '\t'; return 1;
+      case 'r': *c = '\r'; return 1;
+      case 'f': *c = '\f'; return 1;
+      case 'v': *c = '\v'; return 1;
+      case 'a': *c = 7; return 1;
+      case 'x': {
+        uint32_t v = 0;
+        if (at('{')) {
+          i++;
+          int nd = 0;
+          while (i < p.size() && hex(p[i]) && nd <= 8) {
+            v = v * 16 + hv(p[i++]);
+            nd++;
+          }
+          if (!at('}') || nd == 0 || v > 0x10FFFF || (v >= 0xD800 && v <= 0xDFFF)) {
+            err = true;
+            return 0;
+          }
+          i++;
+        } else {
+          for (int k = 0; k < 2; k++) {
+            if (i >= p.size() || !hex(p[i])) {
+              err = true;
+              return 0;
+            }
+            v = v * 16 + hv(p[i++]);
+          }
+        }
+        *c = v;
+        return 1;
+      }
+      case 'b': case 'B': case 'A': case 'z': case 'p': case 'P': case 'u': case 'U':
+        unsup = true;
+        return 0;
+      default:
+        if (e < 0x80 && !((e >= '0' && e <= '9') || (e >= 'a' && e <= 'z') || (e >= 'A' && e <= 'Z'))) {
+          *c = e;
+          return 1;
+        }
+        err = true;
+        return 0;
+    }
+  }
+
+  NodeP cls() {
+    auto n = std::make_unique<Node>();
+    n->t = N_SET;
+    bool neg = false;
+    if (at('^')) {
+      neg = true;
+      i++;
+    }
+    bool first = true;
+    for (;;) {
+      if (i >= p.size()) {
+        err = true;
+        return n;
+      }
+      uint32_t c = p[i];
+      if (c == ']' && !first) {
+        i++;
+        break;
+      }
+      if (c == '[') {
+        unsup = true;
+        return n;
+      }
+      if ((c == '&' || c == '-' || c == '~') && i + 1 < p.size() && p[i + 1] == c && !first) {
+        unsup = true;
+        return n;
+      }
+      first = false;
+      i++;
+      uint32_t lo;
+      if (c == '\\') {
+        Set s;
+        int k = escape(&lo, &s);
+        if (k == 2) {
+          n->set.insert(n->set.end(), s.begin(), s.end());
+          continue;
+        }
+        if (k == 0) return n;
+      } else {
+        lo = c;
+      }
+      uint32_t hi = lo;
+      if (i + 1 < p.size() && p[i] == '-' && p[i + 1] != ']') {
+        i++;
+        uint32_t c2 = p[i++];
+        if (c2 == '\\') {
+          Set s;
+          int k = escape(&hi, &s);
+          if (k != 1) {
+            if (k == 2) err = true;
+            return n;
+          }
+        } else {
+          hi = c2;
+        }
+        if (hi < lo) {
+          err = true;
+          return n;
+        }
+      }
+      n->set.push_back({lo, hi});
+    }
+    n->set = neg ? negate(n->set) : norm(n->set);
+    return n;
+  }
+
+  bool num(int* v) {
+    int nd = 0;
+    long x = 0;
+    while (i < p.size() && p[i] >= '0' && p[i] <= '9') {
+      x = std::min(100000L, x * 10 + (long)(p[i++] - '0'));
+      nd++;
+    }
+    *v = (int)x;
+    return nd > 0;
+  }
+
+  NodeP atom() {
+    uint32_t c = p[i++];
+    auto n = std::make_unique<Node>();
+    if (c == '(') {
+      if (at('?')) {
+        i++;
+        if (at(':')) {
+          i++;
+        } else if (at('P') || at('<')) {
+          if (at('P')) i++;
+          if (!at('<')) {
+            err = true;
+            return n;
+          }
+          while (i < p.size() && p[i] != '>') i++;
+          if (i >= p.size()) {
+            err = true;
+            return n;
+          }
+          i++;
+        } else {
+          unsup = true;
+          return n;
+        }
+      }
+      if (++depth > 200) {
+        err = true;
+        return n;
+      }
+      NodeP g = alt();
+      depth--;
+      if (!at(')')) {
+        err = true;
+        return g;
+      }
+      i++;
+      return g;
+    }
+    if (c == '[') return cls();
+    if (c == '.') {
+      n->t = N_SET;
+      n->set = {{0, '\n' - 1}, {'\n' + 1, 0x10FFFF}};
+      return n;
+    }
+    if (c == '^') {
+      n->t = N_BOL;
+      return n;
+    }
+    if (c == '$') {
+      n->t = N_EOL;
+      return n;
+    }
+    if (c == '\\') {
+      uint32_t cp = 0;
+      Set s;
+      int k = escape(&cp, &s);
+      n->t = N_SET;
+      if (k == 2)
+        n->set = norm(s);
+      else if (k == 1)
+        n->set = {{cp, cp}};
+      return n;
+    }
+    if (c == '*' || c == '+' || c == '?' || c == ')' || c == '|' || c == '{') {
+      err = true;
+      return n;
+    }
+    n->t = N_SET;
+    n->set = {{c, c}};
+    return n;
+  }
+
+  NodeP cat() {
+    auto n = std::make_unique<Node>();
+    n->t = N_CAT;
+    while (i < p.size() && p[i] != '|' && p[i] != ')' && !err && !unsup) {
+      NodeP a = atom();
+      for (;;) {
+        if (i >= p.size()) break;
+        uint32_t q = p[i];
+        int mn, mx;
+        if (q == '*') {
+          mn = 0;
+          mx = -1;
+          i++;
+        } else if (q == '+') {
+          mn = 1;
+          mx = -1;
+          i++;
+        } else if (q == '?') {
+          mn = 0;
+          mx = 1;
+          i++;
+        } else if (q == '{') {
+          i++;
+          if (!num(&mn)) {
+            err = true;
+            break;
+          }
+          mx = mn;
+          if (at(',')) {
+            i++;
+            if (!num(&mx)) mx = -1;
+          }
+          if (!at('}') || (mx >= 0 && mx < mn)) {
+            err = true;
+            break;
+          }
+          i++;
+          if (mn > 1000 || mx > 1000) {
+            unsup = true;
+            break;
+          }
+        } else {
+          break;
+        }
+        if (at('?')) i++;  // lazy: same language for is_match
+        auto r = std::make_unique<Node>();
+        r->t = N_REP;
+        r->mn = mn;
+        r->mx = mx;
+        r->sub = std::move(a);
+        a = std::move(r);
+      }
+      n->kids.push_back(std::move(a));
+    }
+    return n;
+  }
+
+  NodeP alt() {
+    auto n = std::make_unique<Node>();
+    n->t = N_ALT;
+    n->kids.push_back(cat());
+    while (at('|') && !err && !unsup) {
+      i++;
+      n->kids.push_back(cat());
+    }
+    return n;
+  }
+};
+
+// ---------------- max match length in bytes (-1 unbounded)
+int utf8_len(uint32_t c) { return c < 0x80 ? 1 : c < 0x800 ? 2 : c < 0x10000 ? 3 : 4; }
+int64_t max_len(const Node* n, bool ascii) {
+  switch (n->t) {
+    case N_EMPTY: case N_BOL: case N_EOL: return 0;
+    case N_SET: {
+      int m = 0;
+      for (auto& r : n->set) {
+        if (ascii && r.lo > 0x7F) continue;
+        m = std::max(m, ascii ? 1 : utf8_len(r.hi));
+      }
+      return m;
+    }
+    case N_CAT: {
+      int64_t s = 0;
+      for (auto& k : n->kids) {
+        int64_t v = max_len(k.get(), ascii);
+        if (v < 0) return -1;
+        s += v;
+      }
+      return s;
+    }
+    case N_ALT: {
+      int64_t m = 0;
+      for (auto& k : n->kids) {
+        int64_t v = max_len(k.get(), ascii);
+        if (v < 0) return -1;
+        m = std::max(m, v);
+      }
+      return m;
+    }
+    case N_REP: {
+      int64_t v = max_len(n->sub.get(), ascii);
+      if (v < 0) return -1;
+      if (n->mx < 0) return v == 0 ? 0 : -1;
+      return v * n->mx;
+    }
+  }
+  return -1;
+}
+
+// ---------------- byte NFA
+enum NfaT { F_BYTE, F_SPLIT, F_EPS, F_BOT, F_EOT, F_MATCH };
+struct NState {
+  NfaT t;
+  uint8_t lo, hi;
+  int a, b;  // next states
+};
+struct Nfa {
+  std::vector<NState> st;
+  int add(NfaT t, uint8_t lo = 0, uint8_t hi = 0) {
+    st.push_back({t, lo, hi, -1, -1});
+    return (int)st.size() - 1;
+  }
+};
+// fragment: start state + list of dangling out-pointers (state index, which: 0 a / 1 b)
+struct Frag {
+  int start;
+  std::vector<std::pair<int, int>> outs;
+};
+void patch(Nfa& g, const Frag& f, int to) {
+  for (auto& o : f.outs) (o.second ? g.st[o.first].b : g.st[o.first].a) = to;
+}
+Frag eps(Nfa& g) {
+  int s = g.add(F_EPS);
+  return {s, {{s, 0}}};
+}
+Frag cat2(Nfa& g, Frag a, Frag b) {
+  patch(g, a, b.start);
+  return {a.start, b.outs};
+}
+Frag alt2(Nfa& g, Frag a, Frag b) {
+  int s = g.add(F_SPLIT);
+  g.st[s].a = a.start;
+  g.st[s].b = b.start;
+  Frag f{s, a.outs};
+  f.outs.insert(f.outs.end(), b.outs.begin(), b.outs.end());
+  return f;
+}
+Frag bytes_seq(Nfa& g, const std::vector<std::pair<uint8_t, uint8_t>>& seq) {
+  Frag f{-1, {}};
+  int prev = -1;
+  for (auto& br : seq) {
+    int s = g.add(F_BYTE, br.first, br.second);
+    if (prev < 0)
+      f.start = s;
+    else
+      g.st[prev].a = s;
+    prev = s;
+  }
+  f.outs = {{prev, 0}};
+  return f;
+}
+// UTF-8 byte-range sequences of a code point range (surrogates excluded)
+void utf8_seqs(uint32_t lo, uint32_t hi, std::vector<std::vector<std::pair<uint8_t, uint8_t>>>& out) {
+  if (lo > hi) return;
+  if (lo <= 0xDFFF && hi >= 0xD800) {
+    if (lo < 0xD800) utf8_seqs(lo, 0xD7FF, out);
+    if (hi > 0xDFFF) utf8_seqs(0xE000, hi, out);
+    return;
+  }
+  static const uint32_t bounds[] = {0x7F, 0x7FF, 0xFFFF};
+  for (uint32_t bd : bounds)
+    if (lo <= bd && hi > bd) {
+      utf8_seqs(lo, bd, out);
+      utf8_seqs(bd + 1, hi, out);
+      return;
+    }
+  if (hi <= 0x7F) {
+    out.push_back({{(uint8_t)lo, (uint8_t)hi}});
+    return;
+  }
+  int n = utf8_len(lo);
+  for (int k = 1; k < n; k++) {
+    uint32_t m = (1u << (6 * k)) - 1;
+    if ((lo & ~m) != (hi & ~m)) {
+      if ((lo & m) != 0) {
+        utf8_seqs(lo, lo | m, out);
+        utf8_seqs((lo | m) + 1, hi, out);
+        return;
+      }
+      if ((hi & m) != m) {
+        utf8_seqs(lo, (hi & ~m) - 1, out);
+        utf8_seqs(hi & ~m, hi, out);
+        return;
+      }
+    }
+  }
+  auto enc = [](uint32_t c, uint8_t* b) {
+    int n = utf8_len(c);
+    if (n == 1) {
+      b[0] = (uint8_t)c;
+    } else if (n == 2) {
+      b[0] = 0xC0 | (c >> 6);
+      b[1] = 0x80 | (c & 0x3F);
+    } else if (n == 3) {
+      b[0] = 0xE0 | (c >> 12);
+      b[1] = 0x80 | ((c >> 6) & 0x3F);
+      b[2] = 0x80 | (c & 0x3F);
+    } else {
+      b[0] = 0xF0 | (c >> 18);
+      b[1] = 0x80 | ((c >> 12) & 0x3F);
+      b[2] = 0x80 | ((c >> 6) & 0x3F);
+      b[3] = 0x80 | (c & 0x3F);
+    }
+    return n;
+  };
+  uint8_t a[4], b[4];
+  enc(lo, a);
+  enc(hi, b);
+  std::vector<std::pair<uint8_t, uint8_t>> seq;
+  for (int k = 0; k < n; k++) seq.push_back({a[k], b[k]});
+  out.push_back(seq);
+}
+
+Frag build(Nfa& g, const Node* n, bool ascii) {
+  switch (n->t) {
+    case N_EMPTY: return eps(g);
+    case N_BOL: {
+      int s = g.add(F_BOT);
+      return {s, {{s, 0}}};
+    }
+    case N_EOL: {
+      int s = g.add(F_EOT);
+      return {s, {{s, 0}}};
+    }
+    case N_SET: {
+      std::vector<std::vector<std::pair<uint8_t, uint8_t>>> seqs;
+      for (auto& r : n->set) {
+        if (ascii && r.lo > 0x7F) continue;
+        utf8_seqs(r.lo, ascii ? std::min<uint32_t>(r.hi, 0x7F) : r.hi, seqs);
+      }
+      if (seqs.empty()) {
+        // empty class: matches nothing — a byte range that is never taken
+        int s = g.add(F_SPLIT);  // dead: both edges unset -> no progress
+        g.st[s].a = -2;
+        g.st[s].b = -2;
+        return {s, {}};
+      }
+      Frag f = bytes_seq(g, seqs[0]);
+      for (size_t k = 1; k < seqs.size(); k++) f = alt2(g, f, bytes_seq(g, seqs[k]));
+      return f;
+    }
+    case N_CAT: {
+      Frag f = eps(g);
+      for (auto& k : n->kids) f = cat2(g, f, build(g, k.get(), ascii));
+      return f;
+    }
+    case N_ALT: {
+      Frag f = build(g, n->kids[0].get(), ascii);
+      for (size_t k = 1; k < n->kids.size(); k++) f = alt2(g, f, build(g, n->kids[k].get(), ascii));
+      return f;
+    }
+    case N_REP: {
+      Frag f = eps(g);
+      for (int k = 0; k < n->mn; k++) f = cat2(g, f, build(g, n->sub.get(), ascii));
+      if (n->mx < 0) {
+        int s = g.add(F_SPLIT);
+        Frag body = build(g, n->sub.get(), ascii);
+        g.st[s].a = body.start;
+        patch(g, body, s);
+        patch(g, f, s);
+        return {f.start, {{s, 1}}};
+      }
+      for (int k = n->mn; k < n->mx; k++) {
+        int s = g.add(F_SPLIT);
+        Frag body = build(g, n->sub.get(), ascii);
+        g.st[s].a = body.start;
+        patch(g, f, s);
+        Frag nf{f.start, body.outs};
+        nf.outs.push_back({s, 1});
+        f = nf;
+      }
+      return f;
+    }
+  }
+  return eps(g);
+}
+
+struct Closure {
+  const Nfa& g;
+  std::vector<int> mark;
+  int gen = 0;
+  explicit Closure(const Nfa& n) : g(n), mark(n.st.size(), 0) {}
+  // closure of `seeds`; keeps BYTE, MATCH and (unfollowed) EOT states
+  std::vector<int> run(const std::vector<int>& seeds, bool bot, bool eot) {
+    gen++;
+    std::vector<int> out, stack(seeds.rbegin(), seeds.rend());
+    while (!stack.empty()) {
+      int s = stack.back();
+      stack.pop_back();
+      if (s < 0 || mark[s] == gen) continue;
+      mark[s] = gen;
+      const NState& x = g.st[s];
+      switch (x.t) {
+        case F_BYTE: case F_MATCH: out.push_back(s); break;
+        case F_EPS: stack.push_back(x.a); break;
+        case F_SPLIT:
+          stack.push_back(x.b);
+          stack.push_back(x.a);
+          break;
+        case F_BOT:
+          if (bot) stack.push_back(x.a);
+          break;
+        case F_EOT:
+          if (eot)
+            stack.push_back(x.a);
+          else
+            out.push_back(s);
+          break;
+      }
+    }
+    std::sort(out.begin(), out.end());
+    return out;
+  }
+};
+
+}  // namespace
+
+static int determinize(const Node* rootp, bool ascii, bool word, Dfa& out, std::string& msg);
+
+int compile_regex(const std::string& pattern, Dfa& out, Dfa& full, std::string& msg) {
+  // pattern -> code points (must be valid UTF-8; Rust &str)
+  Parser P;
+  {
+    const uint8_t* s = (const uint8_t*)pattern.data();
+    size_t n = pattern.size(), i = 0;
+    while (i < n) {
+      uint32_t c = s[i];
+      int w = c < 0x80 ? 1 : c < 0xE0 ? 2 : c < 0xF0 ? 3 : 4;
+      if (i + w > n) {
+        msg = "regex parse error";
+        return -2;
+      }
+      uint32_t cp = w == 1 ? c : w == 2 ? (c & 0x1F) : w == 3 ? (c & 0x0F) : (c & 0x07);
+      for (int k = 1; k < w; k++) cp = (cp << 6) | (s[i + k] & 0x3F);
+      P.p.push_back(cp);
+      i += w;
+    }
+  }
+  NodeP root = P.alt();
+  if (P.unsup) {
+    msg = "unsupported regex syntax";
+    return -103;
+  }
+  if (P.err || P.i != P.p.size()) {
+    msg = "regex parse error";
+    return -2;
+  }
+  if (int rc = determinize(root.get(), true, P.word, out, msg)) return rc;
+  return determinize(root.get(), false, P.word, full, msg);
+}
+
+int determinize(const Node* rootp, bool ascii, bool word, Dfa& out, std::string& msg) {
+  const int64_t ml = max_len(rootp, ascii);
+  Nfa g;
+  Frag f = build(g, rootp, ascii);
+  int m = g.add(F_MATCH);
+  patch(g, f, m);
+  const int start = f.start;
+  // byte classes from all byte-range boundaries
+  std::vector<int> cut(257, 0);
+  cut[0] = cut[256] = 1;
+  for (auto& s : g.st)
+    if (s.t == F_BYTE) {
+      cut[s.lo] = 1;
+      cut[s.hi + 1] = 1;
+    }
+  std::vector<uint8_t> cls(256);
+  std::vector<int> rep;
+  int nc = -1;
+  for (int b = 0; b < 256; b++) {
+    if (cut[b]) {
+      nc++;
+      rep.push_back(b);
+    }
+    cls[b] = (uint8_t)nc;
+  }
+  const int ncls = nc + 1;
+  Closure C(g);
+  std::map<std::vector<int>, int> ids;
+  std::vector<std::vector<int>> sets;
+  std::vector<uint8_t> bot_flag;
+  auto intern = [&](const std::vector<int>& s, bool is_bot) {
+    auto key = s;
+    if (is_bot) key.push_back(-7);  // the BOT state is distinct (EOT acceptance with ^ satisfied)
+    auto it = ids.find(key);
+    if (it != ids.end()) return it->second;
+    int id = (int)sets.size();
+    ids[key] = id;
+    sets.push_back(s);
+    bot_flag.push_back(is_bot);
+    return id;
+  };
+  const int s_bot = intern(C.run({start}, true, false), true);
+  const int s_mid = intern(C.run({start}, false, false), false);
+  std::vector<std::vector<int>> trans;
+  std::vector<uint8_t> acc;
+  for (size_t k = 0; k < sets.size(); k++) {
+    if (sets.size() > (ascii ? 255u : 65535u)) {
+      msg = "regex too large for the GPU DFA";
+      return -103;
+    }
+    const auto cur = sets[k];
+    const bool is_acc = std::find_if(cur.begin(), cur.end(), [&](int s) { return g.st[s].t == F_MATCH; }) != cur.end();
+    uint8_t a = is_acc ? 1 : 0;
+    {
+      auto ce = C.run(cur, bot_flag[k], true);
+      if (is_acc || std::find_if(ce.begin(), ce.end(), [&](int s) { return g.st[s].t == F_MATCH; }) != ce.end())
+        a |= 2;
+    }
+    acc.push_back(a);
+    std::vector<int> row(ncls);
+    for (int c = 0; c < ncls; c++) {
+      if (is_acc) {
+        row[c] = (int)k;  // sticky: is_match is decided
+        continue;
+      }
+      const int byte = rep[c];
+      std::vector<int> nxt;
+      for (int s : cur) {
+        const NState& x = g.st[s];
+        if (x.t == F_BYTE && byte >= x.lo && byte <= x.hi) nxt.push_back(x.a);
+      }
+      nxt.push_back(start);  // unanchored restart at the next position
+      row[c] = intern(C.run(nxt, false, false), false);
+    }
+    trans.push_back(row);
+  }
+  out.nstates = (uint32_t)sets.size();
+  out.nclasses = (uint32_t)ncls;
+  out.s_bot = (uint32_t)s_bot;
+  out.s_mid = (uint32_t)s_mid;
+  out.max_len = ml < 0 || ml > (1 << 20) ? -1 : (int32_t)ml;
+  out.unicode_word = word;
+  out.classmap = cls;
+  out.classmap_up.resize(256);
+  for (int b = 0; b < 256; b++) out.classmap_up[b] = cls[(b >= 'a' && b <= 'z') ? b - 32 : b];
+  out.trans.resize(out.nstates * out.nclasses);
+  for (uint32_t s = 0; s < out.nstates; s++)
+    for (uint32_t c = 0; c < out.nclasses; c++) out.trans[s * out.nclasses + c] = (uint16_t)trans[s][c];
+  out.accept = acc;
+  return 0;
+}
+
+bool dfa_is_match(const Dfa& d, const uint8_t* s, size_t n) {
+  uint32_t st = d.s_bot;
+  if (d.accept[st] & 1) return true;
+  for (size_t i = 0; i < n; i++) {
+    st = d.trans[st * d.nclasses + d.classmap[s[i]]];
+    if (d.accept[st] & 1) return true;
+  }
+  return (d.accept[st] & 2) != 0;
+}
+
+}  // namespace fsg

@@ -1,0 +1,25 @@
+// fsg_regex.h — Rust-regex subset -> UTF-8 byte DFA (chain-build time)
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace fsg {
+
+struct Dfa {
+  uint32_t nstates = 0, nclasses = 0, s_bot = 0, s_mid = 0;
+  int32_t max_len = -1;  // longest match in bytes, -1 unbounded
+  bool unicode_word = false;
+  std::vector<uint8_t> classmap, classmap_up, accept;
+  std::vector<uint16_t> trans;
+};
+
+// Two DFAs of one pattern: `ascii` with every class restricted to ASCII (exact
+// on ASCII-only values; <= 255 states, staged in LDS) and `full` over all of
+// Unicode (<= 65535 states, read through L1/L2 for values with non-ASCII bytes).
+// 0 ok; -2 (FSG_E_INIT) syntax error; -103 (FSG_E_UNSUPPORTED) outside the supported subset
+int compile_regex(const std::string& pattern, Dfa& ascii, Dfa& full, std::string& msg);
+// host walk of the compiled DFA — used only by the compiler's unit tests
+bool dfa_is_match(const Dfa& d, const uint8_t* s, size_t n);
+
+}  // namespace fsg

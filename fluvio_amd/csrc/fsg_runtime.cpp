@@ -1,0 +1,918 @@
+// fsg_runtime.cpp — host runtime of the MI355X SmartModule engine behind the C ABI
+// (include/fsg.h).  C++ restatement of the fluvio-smartengine surface:
+//
+//   SmartEngine                  crates/fluvio-smartengine/src/engine/wasmtime/engine.rs:26-41
+//   SmartModuleChainBuilder      engine.rs:49-111 (+ create_transform, transforms/mod.rs:24-52)
+//   SmartModuleChainInstance     engine.rs:118-218
+//   SmartModuleChainMetrics      crates/fluvio-smartengine/src/engine/metrics.rs:6-41
+//   SPU process_batch            crates/fluvio-spu/src/smartengine/batch.rs:41-142
+//   FileBatchIterator framing    crates/fluvio-storage/src/iterators.rs:55-160
+//
+// The runtime owns device buffers and one HIP stream per chain instance, builds
+// the chain descriptor (built-in GPU SmartModules selected at initialize()),
+// frames ingested slices and launches the kernels of fsg_kernels.hip.  No record
+// is transformed on the host: the only host-side record work is formatting the
+// single SmartModuleTransformRuntimeError a call may return.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "fsg.h"
+#include "fsg_device.h"
+#include "fsg_launch.h"
+#include "fsg_regex.h"
+
+using namespace fsg;
+
+// ---------------------------------------------------------------------------
+// error plumbing
+// ---------------------------------------------------------------------------
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) return fail(FSG_E_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+extern "C" const char* fsg_last_error_message(void) { return g_err.c_str(); }
+extern "C" int fsg_abi_version(void) { return FSG_ABI_VERSION; }
+extern "C" void fsg_free(void* p) { free(p); }
+
+// ---------------------------------------------------------------------------
+// small host helpers (config parsing / error formatting only)
+// ---------------------------------------------------------------------------
+namespace {
+
+uint64_t rd_be(const uint8_t* p, int n) {
+  uint64_t v = 0;
+  for (int i = 0; i < n; i++) v = (v << 8) | p[i];
+  return v;
+}
+
+// Rust from_utf8 (for config data and error hints)
+bool utf8_ok(const uint8_t* s, size_t n, uint32_t* vut, uint32_t* elen) {
+  size_t i = 0;
+  while (i < n) {
+    uint32_t f = s[i];
+    if (f < 0x80) {
+      i++;
+      continue;
+    }
+    int w = (f >= 0xC2 && f <= 0xDF) ? 2 : (f >= 0xE0 && f <= 0xEF) ? 3 : (f >= 0xF0 && f <= 0xF4) ? 4 : 0;
+    auto bad = [&](uint32_t l) {
+      *vut = (uint32_t)i;
+      *elen = l;
+      return false;
+    };
+    if (w == 0) return bad(1);
+    if (i + 1 >= n) return bad(0);
+    uint32_t b1 = s[i + 1];
+    if (w == 2) {
+      if ((b1 & 0xC0) != 0x80) return bad(1);
+      i += 2;
+      continue;
+    }
+    bool ok1 = w == 3 ? ((f == 0xE0 && b1 >= 0xA0 && b1 <= 0xBF) || (f >= 0xE1 && f <= 0xEC && b1 >= 0x80 && b1 <= 0xBF) ||
+                         (f == 0xED && b1 >= 0x80 && b1 <= 0x9F) || (f >= 0xEE && f <= 0xEF && b1 >= 0x80 && b1 <= 0xBF))
+                      : ((f == 0xF0 && b1 >= 0x90 && b1 <= 0xBF) || (f >= 0xF1 && f <= 0xF3 && b1 >= 0x80 && b1 <= 0xBF) ||
+                         (f == 0xF4 && b1 >= 0x80 && b1 <= 0x8F));
+    if (!ok1) return bad(1);
+    if (i + 2 >= n) return bad(0);
+    if ((s[i + 2] & 0xC0) != 0x80) return bad(2);
+    if (w == 3) {
+      i += 3;
+      continue;
+    }
+    if (i + 3 >= n) return bad(0);
+    if ((s[i + 3] & 0xC0) != 0x80) return bad(3);
+    i += 4;
+  }
+  return true;
+}
+std::string utf8_hint(uint32_t vut, uint32_t elen) {
+  char b[96];
+  if (elen)
+    snprintf(b, sizeof b, "invalid utf-8 sequence of %u bytes from index %u", elen, vut);
+  else
+    snprintf(b, sizeof b, "incomplete utf-8 byte sequence from index %u", vut);
+  return b;
+}
+const char* parse_hint(uint32_t kind) {
+  switch (kind) {
+    case 1: return "cannot parse integer from empty string";
+    case 2: return "invalid digit found in string";
+    case 3: return "number too large to fit in target type";
+    default: return "number too small to fit in target type";
+  }
+}
+bool is_ws(uint32_t c) {
+  return (c >= 0x09 && c <= 0x0D) || c == 0x20 || c == 0x85 || c == 0xA0 || c == 0x1680 ||
+         (c >= 0x2000 && c <= 0x200A) || c == 0x2028 || c == 0x2029 || c == 0x202F || c == 0x205F || c == 0x3000;
+}
+// aggregate-sum's `acc.trim().parse::<i32>().unwrap_or(0)` on a valid UTF-8 accumulator
+int32_t acc_value(const std::vector<uint8_t>& a) {
+  std::vector<uint32_t> cps;
+  std::vector<size_t> at;
+  for (size_t i = 0; i < a.size();) {
+    uint32_t f = a[i];
+    int w = f < 0x80 ? 1 : f < 0xE0 ? 2 : f < 0xF0 ? 3 : 4;
+    uint32_t cp = w == 1 ? f : w == 2 ? (f & 0x1F) : w == 3 ? (f & 0x0F) : (f & 0x07);
+    for (int k = 1; k < w && i + k < a.size(); k++) cp = (cp << 6) | (a[i + k] & 0x3F);
+    cps.push_back(cp);
+    at.push_back(i);
+    i += w;
+  }
+  size_t b = 0, e = cps.size();
+  while (b < e && is_ws(cps[b])) b++;
+  while (e > b && is_ws(cps[e - 1])) e--;
+  const size_t bb = b < at.size() ? at[b] : a.size();
+  const size_t eb = e < at.size() ? at[e] : a.size();
+  if (bb >= eb) return 0;
+  const uint8_t* s = a.data() + bb;
+  size_t n = eb - bb, i = 0;
+  bool pos = true;
+  if ((s[0] == '+' || s[0] == '-') && n == 1) return 0;
+  if (s[0] == '+')
+    i = 1;
+  else if (s[0] == '-') {
+    pos = false;
+    i = 1;
+  }
+  int64_t acc = 0;
+  for (; i < n; i++) {
+    if (s[i] < '0' || s[i] > '9') return 0;
+    acc = pos ? acc * 10 + (s[i] - '0') : acc * 10 - (s[i] - '0');
+    if (acc > 2147483647LL || acc < -2147483648LL) return 0;
+  }
+  return (int32_t)acc;
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t c = std::max<size_t>(n + n / 4, 4096);
+    hipError_t e = hipMalloc(&p, c);
+    if (e == hipSuccess) cap = c;
+    return e;
+  }
+  template <typename T>
+  T* as() const {
+    return (T*)p;
+  }
+};
+
+struct ModuleSpec {
+  std::vector<uint8_t> bytes;
+  std::map<std::string, std::string> params;  // SmartModuleExtraParams (BTreeMap)
+  int16_t version = 22;                       // DEFAULT_SMARTENGINE_VERSION
+  bool has_acc = false;
+  std::vector<uint8_t> acc;
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// objects
+// ---------------------------------------------------------------------------
+struct fsg_engine {
+  int device = 0;
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+};
+
+struct fsg_chain_builder {
+  std::vector<ModuleSpec> mods;
+  size_t limit = 1000000000;  // DEFAULT_STORE_MEMORY_LIMIT (engine.rs:24)
+};
+
+struct fsg_slice {
+  fsg_engine* eng = nullptr;
+  DevBuf data, bpos, rbase;
+  size_t len = 0;
+  uint32_t nb = 0;
+  uint64_t nrec = 0;
+  int tail_status = 0;
+  uint64_t header_bytes = 0;  // 57 B per framed batch + the record sections
+};
+
+struct fsg_chain {
+  fsg_engine* eng = nullptr;
+  hipStream_t stream = nullptr;
+  size_t limit = 0;
+  ChainDesc hdesc{};
+  std::vector<uint8_t> hblob;
+  DevBuf d_desc, d_blob;
+  std::vector<std::string> names;
+  int agg_stage = -1;
+  std::vector<uint8_t> acc;  // aggregate accumulator bytes (SmartModuleAggregate.accumulator)
+  // scratch
+  DevBuf bstat, kept, rows, pre, aggpre, tiles, grand, mins, plan, out, crcparts;
+  Plan hplan{};
+  hipEvent_t ev[6] = {};
+  fsg_timings last{};
+  size_t out_len = 0;
+  ~fsg_chain() {
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+// ---------------------------------------------------------------------------
+// engine
+// ---------------------------------------------------------------------------
+extern "C" int fsg_device_count(int* count) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) n = 0;
+  *count = n;
+  return FSG_OK;
+}
+
+extern "C" int fsg_engine_new(int device, fsg_engine** out) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(FSG_E_DEVICE, "no HIP device available");
+  if (device < 0 || device >= n) return fail(FSG_E_INVALID_ARG, "device index out of range");
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(upload_crc_tables());
+  auto* e = new fsg_engine();
+  e->device = device;
+  *out = e;
+  return FSG_OK;
+}
+
+extern "C" void fsg_engine_free(fsg_engine* e) {
+  if (!e) return;
+  if (e->comm) ncclCommDestroy(e->comm);
+  delete e;
+}
+
+// ---------------------------------------------------------------------------
+// builder
+// ---------------------------------------------------------------------------
+extern "C" int fsg_chain_builder_new(fsg_chain_builder** out) {
+  *out = new fsg_chain_builder();
+  return FSG_OK;
+}
+extern "C" void fsg_chain_builder_free(fsg_chain_builder* b) { delete b; }
+extern "C" int fsg_chain_builder_set_store_memory_limit(fsg_chain_builder* b, size_t max_memory_bytes) {
+  b->limit = max_memory_bytes;
+  return FSG_OK;
+}
+extern "C" int fsg_chain_builder_add_smart_module(fsg_chain_builder* b, const fsg_param* params, size_t n_params,
+                                                  int16_t version, const uint8_t* initial_acc, size_t acc_len,
+                                                  int32_t has_initial_acc, const uint8_t* module, size_t module_len) {
+  ModuleSpec m;
+  m.bytes.assign(module, module + module_len);
+  for (size_t i = 0; i < n_params; i++) m.params[params[i].key] = params[i].value;  // BTreeMap insert
+  m.version = version;
+  m.has_acc = has_initial_acc != 0;
+  if (m.has_acc) m.acc.assign(initial_acc, initial_acc + acc_len);
+  b->mods.push_back(std::move(m));
+  return FSG_OK;
+}
+
+namespace {
+std::string init_error(const std::string& what) { return what + "\n\nSmartModule Init Error: \n"; }
+
+// one reference SmartModule -> one GPU stage (chain-build-time selection)
+int add_stage(fsg_chain* c, const ModuleSpec& m, const std::string& name, uint8_t& vt) {
+  if (c->hdesc.nstages >= (uint32_t)kMaxStages) return fail(FSG_E_UNSUPPORTED, "chain longer than 8 stages");
+  if (c->agg_stage >= 0) return fail(FSG_E_UNSUPPORTED, "stages after an aggregate are not implemented on the GPU");
+  StageDesc sd{};
+  sd.in_type = vt;
+  auto param = [&](const char* k) -> const std::string* {
+    auto it = m.params.find(k);
+    return it == m.params.end() ? nullptr : &it->second;
+  };
+  auto put_blob = [&](const void* p, size_t n) {
+    uint32_t off = (uint32_t)c->hblob.size();
+    c->hblob.insert(c->hblob.end(), (const uint8_t*)p, (const uint8_t*)p + n);
+    while (c->hblob.size() % 16) c->hblob.push_back(0);
+    return off;
+  };
+  if (name == "filter" || name == "filter_init" || name == "filter_with_param") {
+    std::string needle = "a";  // examples/filter: contains('a')
+    if (name != "filter") {
+      const std::string* k = param("key");
+      if (!k && name == "filter_init") return fail(FSG_E_INIT, init_error("Missing param key"));
+      if (k) needle = *k;
+    }
+    sd.op = OP_CONTAINS;
+    sd.kind = FSG_KIND_FILTER;
+    sd.needle = put_blob(needle.data(), needle.size());
+    sd.needle_len = (uint32_t)needle.size();
+  } else if (name == "regex-filter" || name == "filter_regex") {
+    std::string pat;
+    if (name == "regex-filter") {
+      const std::string* r = param("regex");
+      if (!r) return fail(FSG_E_INIT, init_error("Missing param regex"));
+      pat = *r;
+      sd.keep_match = 1;
+    } else {
+      pat = "\\d{3}-\\d{2}-\\d{4}";  // examples/filter_regex: keep records without an SSN
+      sd.keep_match = 0;
+    }
+    Dfa d, fd;
+    std::string msg;
+    int rc = compile_regex(pat, d, fd, msg);
+    if (rc == -2) return fail(FSG_E_INIT, init_error(msg));
+    if (rc) return fail(rc, msg);
+    sd.op = OP_REGEX;
+    sd.kind = FSG_KIND_FILTER;
+    sd.dfa.nstates = d.nstates;
+    sd.dfa.nclasses = d.nclasses;
+    sd.dfa.s_bot = d.s_bot;
+    sd.dfa.s_mid = d.s_mid;
+    sd.dfa.max_len = d.max_len;
+    sd.dfa.unicode_word = d.unicode_word;
+    sd.dfa.classmap = put_blob(d.classmap.data(), 256);
+    sd.dfa.classmap_up = put_blob(d.classmap_up.data(), 256);
+    std::vector<uint8_t> t8(d.trans.begin(), d.trans.end());
+    sd.dfa.trans = put_blob(t8.data(), t8.size());
+    std::vector<uint8_t> acc(256, 0);
+    std::copy(d.accept.begin(), d.accept.end(), acc.begin());
+    sd.dfa.accept = put_blob(acc.data(), 256);
+    sd.dfa.f_nstates = fd.nstates;
+    sd.dfa.f_nclasses = fd.nclasses;
+    sd.dfa.f_s_bot = fd.s_bot;
+    sd.dfa.f_classmap = put_blob(fd.classmap.data(), 256);
+    sd.dfa.f_classmap_up = put_blob(fd.classmap_up.data(), 256);
+    sd.dfa.f_trans = put_blob(fd.trans.data(), fd.trans.size() * 2);
+    sd.dfa.f_accept = put_blob(fd.accept.data(), fd.accept.size());
+  } else if (name == "filter_odd") {
+    sd.op = OP_FILTER_ODD;
+    sd.kind = FSG_KIND_FILTER;
+  } else if (name == "map") {
+    sd.op = OP_MAP_UPPER;
+    sd.kind = FSG_KIND_MAP;
+    if (vt == VT_SRC) vt = VT_SRC_UPPER;
+  } else if (name == "map_double") {
+    sd.op = OP_MAP_DOUBLE;
+    sd.kind = FSG_KIND_MAP;
+    vt = VT_I32;
+  } else if (name == "filter_map") {
+    sd.op = OP_FILTER_MAP;
+    sd.kind = FSG_KIND_FILTER_MAP;
+    vt = VT_I32;
+  } else if (name == "aggregate-sum") {
+    sd.op = OP_AGG_SUM;
+    sd.kind = FSG_KIND_AGGREGATE;
+    c->agg_stage = (int)c->hdesc.nstages;
+    c->acc = m.has_acc ? m.acc : std::vector<uint8_t>();
+    vt = VT_I32;
+  } else if (name == "aggregate") {
+    return fail(FSG_E_UNSUPPORTED, "the string-concatenating aggregate example is not implemented on the GPU");
+  } else {
+    return fail(FSG_E_UNKNOWN_SM, "No valid smartmodule found");
+  }
+  c->hdesc.st[c->hdesc.nstages++] = sd;
+  c->names.push_back(name);
+  return FSG_OK;
+}
+}  // namespace
+
+extern "C" int fsg_chain_builder_initialize(fsg_chain_builder* b, fsg_engine* e, fsg_chain** out) {
+  std::unique_ptr<fsg_chain_builder> own(b);
+  if (!e) return fail(FSG_E_INVALID_ARG, "null engine");
+  HIPCHK(hipSetDevice(e->device));
+  auto c = std::make_unique<fsg_chain>();
+  c->eng = e;
+  c->limit = b->limit;
+  uint8_t vt = VT_SRC;
+  for (auto& m : b->mods) {
+    const auto& by = m.bytes;
+    if (by.size() >= 4 && !memcmp(by.data(), "\0asm", 4))
+      return fail(FSG_E_UNKNOWN_SM, "No valid smartmodule found (wasm modules do not run on the GPU engine)");
+    if (by.size() < 4 || memcmp(by.data(), "\0fsg", 4))
+      return fail(FSG_E_INSTANTIATE, "Failed to instantiate: module bytes are neither wasm nor a GPU built-in descriptor");
+    std::string name(by.begin() + 4, by.end());
+    int rc = add_stage(c.get(), m, name, vt);
+    if (rc) return rc;
+  }
+  c->hdesc.out_type = vt;
+  c->hdesc.has_agg = c->agg_stage >= 0;
+  if (c->agg_stage >= 0) {
+    StageDesc& sd = c->hdesc.st[c->agg_stage];
+    uint32_t vut = 0, el = 0;
+    sd.acc_bad = !utf8_ok(c->acc.data(), c->acc.size(), &vut, &el);
+    sd.acc_vut = vut;
+    sd.acc_elen = el;
+  }
+  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  for (auto& ev : c->ev) HIPCHK(hipEventCreate(&ev));
+  HIPCHK(c->d_desc.ensure(sizeof(ChainDesc)));
+  HIPCHK(hipMemcpy(c->d_desc.p, &c->hdesc, sizeof(ChainDesc), hipMemcpyHostToDevice));
+  if (c->hblob.empty()) c->hblob.resize(16, 0);
+  HIPCHK(c->d_blob.ensure(c->hblob.size()));
+  HIPCHK(hipMemcpy(c->d_blob.p, c->hblob.data(), c->hblob.size(), hipMemcpyHostToDevice));
+  *out = c.release();
+  return FSG_OK;
+}
+
+extern "C" void fsg_chain_free(fsg_chain* c) { delete c; }
+
+// ---------------------------------------------------------------------------
+// slices (ingest)
+// ---------------------------------------------------------------------------
+namespace {
+// FileBatchIterator framing (iterators.rs:55-160): header -> batch_len -> record section
+int frame(const uint8_t* s, size_t len, std::vector<uint64_t>& bpos, std::vector<uint64_t>& rbase, uint64_t& nrec,
+          int& tail, uint64_t& hdr_bytes) {
+  size_t pos = 0;
+  nrec = 0;
+  tail = 0;
+  hdr_bytes = 0;
+  while (pos < len) {
+    if (len - pos < 57) {
+      tail = FSG_E_IO;  // "not enough for batch header"
+      break;
+    }
+    const int32_t batch_len = (int32_t)rd_be(s + pos + 8, 4);
+    const int16_t attrs = (int16_t)rd_be(s + pos + 21, 2);
+    if (batch_len < 45) {
+      tail = FSG_E_IO;
+      break;
+    }
+    const size_t rem = (size_t)batch_len - 45;
+    if (len - pos - 57 < rem) {
+      tail = FSG_E_IO;  // "not enough for batch records"
+      break;
+    }
+    const int comp = attrs & 7;
+    if (comp != 0) {
+      tail = comp <= 4 ? FSG_E_UNSUPPORTED : FSG_E_IO;  // compressed sections: not on the GPU path yet
+      break;
+    }
+    uint64_t cnt = 0;
+    if (rem >= 4) {
+      int32_t c = (int32_t)rd_be(s + pos + 57, 4);
+      cnt = c > 0 ? (uint64_t)c : 0;
+      cnt = std::min<uint64_t>(cnt, (rem - 4) / 7);  // a record is at least 7 bytes
+    }
+    bpos.push_back(pos);
+    rbase.push_back(nrec);
+    nrec += cnt;
+    hdr_bytes += 57 + rem;
+    pos += 57 + rem;
+  }
+  return 0;
+}
+
+int upload_slice(fsg_engine* e, const uint8_t* s, size_t len, fsg_slice* sl, hipStream_t stream) {
+  std::vector<uint64_t> bpos, rbase;
+  frame(s, len, bpos, rbase, sl->nrec, sl->tail_status, sl->header_bytes);
+  sl->eng = e;
+  sl->len = len;
+  sl->nb = (uint32_t)bpos.size();
+  const size_t alloc = ((len + 15) & ~(size_t)15) + kSlicePad + kWin;
+  HIPCHK(sl->data.ensure(alloc));
+  HIPCHK(hipMemsetAsync((uint8_t*)sl->data.p + (len & ~(size_t)15), 0, alloc - (len & ~(size_t)15), stream));
+  if (len) HIPCHK(hipMemcpyAsync(sl->data.p, s, len, hipMemcpyHostToDevice, stream));
+  HIPCHK(sl->bpos.ensure(std::max<size_t>(1, bpos.size()) * 8));
+  HIPCHK(sl->rbase.ensure(std::max<size_t>(1, rbase.size()) * 8));
+  if (!bpos.empty()) {
+    HIPCHK(hipMemcpyAsync(sl->bpos.p, bpos.data(), bpos.size() * 8, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(sl->rbase.p, rbase.data(), rbase.size() * 8, hipMemcpyHostToDevice, stream));
+  }
+  HIPCHK(hipStreamSynchronize(stream));
+  return FSG_OK;
+}
+}  // namespace
+
+extern "C" int fsg_slice_upload(fsg_engine* e, const uint8_t* s, size_t len, fsg_slice** out) {
+  HIPCHK(hipSetDevice(e->device));
+  auto sl = std::make_unique<fsg_slice>();
+  int rc = upload_slice(e, s, len, sl.get(), 0);
+  if (rc) return rc;
+  *out = sl.release();
+  return FSG_OK;
+}
+extern "C" int fsg_slice_info(const fsg_slice* s, uint64_t* n_batches, uint64_t* n_records, uint64_t* bytes) {
+  if (n_batches) *n_batches = s->nb;
+  if (n_records) *n_records = s->nrec;
+  if (bytes) *bytes = s->header_bytes;
+  return FSG_OK;
+}
+extern "C" void fsg_slice_free(fsg_slice* s) { delete s; }
+
+// ---------------------------------------------------------------------------
+// process_batch over a resident slice
+// ---------------------------------------------------------------------------
+namespace {
+
+void free_error(fsg_runtime_error& e) {
+  free((void*)e.hint);
+  free((void*)e.key);
+  free((void*)e.value);
+  memset(&e, 0, sizeof e);
+}
+
+// Build SmartModuleTransformRuntimeError (link/smartmodule.rs:26-43) for the
+// error record of batch eb: hint, offset = base_offset + offset_delta, kind,
+// and the record's key/value as they entered the failing stage.
+int build_error(fsg_chain* c, const fsg_slice* s, const BatchStat& st, fsg_runtime_error& err) {
+  memset(&err, 0, sizeof err);
+  // fetch the failing record's bytes (header first, then the full record)
+  uint8_t head[16] = {0};
+  const size_t avail = s->len - st.err_pos;
+  HIPCHK(hipMemcpy(head, (uint8_t*)s->data.p + st.err_pos, std::min<size_t>(16, avail), hipMemcpyDeviceToHost));
+  uint64_t num = 0;
+  unsigned shift = 0;
+  size_t i = 0;
+  for (;;) {
+    uint8_t bb = head[i++];
+    num |= (uint64_t)(bb & 0x7f) << (shift & 63);
+    shift += 7;
+    if (!(bb & 0x80) || i >= 10) break;
+  }
+  const int64_t len = (int64_t)((num >> 1) ^ (~(num & 1) + 1));
+  const size_t rlen = std::min<size_t>(avail, i + (size_t)std::max<int64_t>(len, 0) + 16);
+  std::vector<uint8_t> rec(rlen);
+  HIPCHK(hipMemcpy(rec.data(), (uint8_t*)s->data.p + st.err_pos, rlen, hipMemcpyDeviceToHost));
+  // parse the record fields (Record::decode) to recover key and value
+  size_t q = 0;
+  auto var = [&](int64_t* v) {
+    uint64_t n = 0;
+    unsigned sh = 0;
+    for (;;) {
+      if (q >= rec.size()) return false;
+      uint8_t bb = rec[q++];
+      n |= (uint64_t)(bb & 0x7f) << (sh & 63);
+      sh += 7;
+      if (!(bb & 0x80)) break;
+    }
+    *v = (int64_t)((n >> 1) ^ (~(n & 1) + 1));
+    return true;
+  };
+  int64_t t;
+  var(&t);   // len
+  q++;       // attributes
+  var(&t);   // timestamp_delta
+  var(&t);   // offset_delta
+  const uint8_t tag = q < rec.size() ? rec[q++] : 0;
+  std::vector<uint8_t> key, val;
+  if (tag == 1) {
+    int64_t kl;
+    var(&kl);
+    size_t take = std::min<size_t>((size_t)kl, rec.size() - q);
+    key.assign(rec.begin() + q, rec.begin() + q + take);
+    q += take;
+  }
+  int64_t vl;
+  var(&vl);
+  size_t take = std::min<size_t>((size_t)vl, rec.size() - q);
+  val.assign(rec.begin() + q, rec.begin() + q + take);
+  const StageDesc& sd = c->hdesc.st[st.err_stage];
+  if (sd.in_type == VT_SRC_UPPER)
+    for (auto& ch : val)
+      if (ch >= 'a' && ch <= 'z') ch -= 32;
+  if (sd.in_type == VT_I32) {
+    char b[16];
+    int n = snprintf(b, sizeof b, "%d", st.err_ival);
+    val.assign(b, b + n);
+  }
+  std::string hint;
+  if (st.err_code == EC_UTF8 || st.err_code == EC_ACC_UTF8) {
+    hint = utf8_hint(st.err_aux, st.err_aux2);
+  } else if (st.err_code == EC_PARSE) {
+    hint = parse_hint(st.err_aux);
+    if (sd.op == OP_FILTER_ODD)
+      hint = "Oops something went wrong\n\nCaused by:\n   0: Failed to parse int\n   1: " + hint;
+  }
+  err.hint = (const char*)malloc(hint.size() + 1);
+  memcpy((void*)err.hint, hint.c_str(), hint.size() + 1);
+  err.hint_len = hint.size();
+  err.offset = st.base_offset + st.err_od;
+  err.kind = sd.kind;
+  err.has_key = tag == 1;
+  if (tag == 1) {
+    err.key = (const uint8_t*)malloc(std::max<size_t>(1, key.size()));
+    memcpy((void*)err.key, key.data(), key.size());
+    err.key_len = key.size();
+  }
+  err.value = (const uint8_t*)malloc(std::max<size_t>(1, val.size()));
+  memcpy((void*)err.value, val.data(), val.size());
+  err.value_len = val.size();
+  return FSG_OK;
+}
+
+int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics* m, fsg_batch_output* res,
+              bool empty_chain_io) {
+  hipStream_t st = c->stream;
+  const uint32_t nb = s->nb;
+  memset(res, 0, sizeof *res);
+  // scratch (StoreMemoryExceeded past the store limit, limiter.rs:18-35)
+  const size_t need = (size_t)std::max<uint32_t>(nb, 1) * (sizeof(BatchStat) + 3 * sizeof(ScanRow)) +
+                      (size_t)std::max<uint64_t>(s->nrec, 1) * sizeof(KeptRec);
+  if (need > c->limit) {
+    char b[160];
+    snprintf(b, sizeof b, "Requested memory %zub exceeded max allowed %zub", need, c->limit);
+    return fail(FSG_E_STORE_MEMORY, b);
+  }
+  HIPCHK(c->bstat.ensure(std::max<uint32_t>(nb, 1) * sizeof(BatchStat)));
+  HIPCHK(c->kept.ensure(std::max<uint64_t>(s->nrec, 1) * sizeof(KeptRec)));
+  HIPCHK(c->rows.ensure(std::max<uint32_t>(nb, 1) * sizeof(ScanRow)));
+  HIPCHK(c->pre.ensure(std::max<uint32_t>(nb, 1) * sizeof(ScanRow)));
+  HIPCHK(c->aggpre.ensure(std::max<uint32_t>(nb, 1) * sizeof(ScanRow)));
+  HIPCHK(c->tiles.ensure(std::max<uint32_t>(scan_tiles(nb), 1) * sizeof(ScanRow)));
+  HIPCHK(c->grand.ensure(sizeof(ScanRow)));
+  HIPCHK(c->mins.ensure(sizeof(Mins)));
+  HIPCHK(c->plan.ensure(sizeof(Plan)));
+  const bool has_agg = c->agg_stage >= 0;
+  const int64_t acc0 = has_agg ? acc_value(c->acc) : 0;
+
+  HIPCHK(hipMemsetAsync(c->mins.p, 0xFF, sizeof(Mins), st));
+  HIPCHK(hipEventRecord(c->ev[0], st));
+  EvalArgs ea{};
+  ea.slice = (const uint8_t*)s->data.p;
+  ea.slice_len = s->len;
+  ea.bpos = s->bpos.as<uint64_t>();
+  ea.rbase = s->rbase.as<uint64_t>();
+  ea.nbatches = nb;
+  ea.chain = c->d_desc.as<ChainDesc>();
+  ea.blob = c->d_blob.as<uint8_t>();
+  ea.bstat = c->bstat.as<BatchStat>();
+  ea.desc = c->kept.as<KeptRec>();
+  ea.mins = c->mins.as<Mins>();
+  launch_eval(ea, st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev[1], st));
+  SizeArgs sa{};
+  sa.bstat = ea.bstat;
+  sa.desc = ea.desc;
+  sa.rbase = ea.rbase;
+  sa.mins = ea.mins;
+  sa.rows = c->rows.as<ScanRow>();
+  sa.nbatches = nb;
+  sa.acc0 = acc0;
+  if (has_agg) {
+    sa.agg_only = 1;
+    launch_size(sa, st);
+    launch_scan(sa.rows, c->aggpre.as<ScanRow>(), c->tiles.as<ScanRow>(), c->grand.as<ScanRow>(), nb, false, 0,
+                ea.mins, ea.bstat, st);
+    sa.agg_only = 0;
+    sa.agg_pre = c->aggpre.as<ScanRow>();
+  }
+  launch_size(sa, st);
+  launch_scan(sa.rows, c->pre.as<ScanRow>(), c->tiles.as<ScanRow>(), c->grand.as<ScanRow>(), nb, true, max_bytes,
+              ea.mins, ea.bstat, st);
+  PlanArgs pa{};
+  pa.bstat = ea.bstat;
+  pa.rows = sa.rows;
+  pa.pre = c->pre.as<ScanRow>();
+  pa.mins = ea.mins;
+  pa.plan = c->plan.as<Plan>();
+  pa.nbatches = nb;
+  pa.tail_status = s->tail_status;
+  pa.empty_chain = empty_chain_io ? 1 : 0;
+  pa.has_agg = has_agg;
+  pa.acc0 = acc0;
+  launch_plan(pa, st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev[2], st));
+  HIPCHK(hipMemcpyAsync(&c->hplan, c->plan.p, sizeof(Plan), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const Plan p = c->hplan;
+  if (m) {
+    m->bytes_in += p.bytes_in;
+    m->invocation_count += p.invocations;
+    m->records_out += p.records_out;
+  }
+  if (p.status != 0) {
+    const char* why = p.status == FSG_E_UNSUPPORTED ? "input needs a feature the GPU path does not implement"
+                      : p.status == FSG_E_IO        ? "io error while decoding batches"
+                                                    : "failed to decode SmartModule base input";
+    return fail(p.status, why);
+  }
+  // output batch: 61-byte header + records
+  const size_t out_len = 61 + p.rec_bytes;
+  HIPCHK(c->out.ensure(out_len + 64));
+  HIPCHK(c->crcparts.ensure((crc_parts(out_len) + 1) * sizeof(uint32_t)));
+  WriteArgs wa{};
+  wa.slice = ea.slice;
+  wa.bstat = ea.bstat;
+  wa.desc = ea.desc;
+  wa.rbase = ea.rbase;
+  wa.pre = pa.pre;
+  wa.agg_pre = has_agg ? c->aggpre.as<ScanRow>() : nullptr;
+  wa.plan = pa.plan;
+  wa.out = c->out.as<uint8_t>();
+  wa.acc0 = acc0;
+  launch_header(pa.plan, wa.out, st);
+  HIPCHK(hipEventRecord(c->ev[3], st));
+  launch_write(wa, p.last >= p.first && p.first >= 0 ? (uint32_t)(p.last - p.first + 1) : 0u, st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev[4], st));
+  launch_crc(wa.out, 21, out_len - 21, c->crcparts.as<uint32_t>(), wa.out, st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev[5], st));
+  HIPCHK(hipStreamSynchronize(st));
+  c->out_len = out_len;
+  // timings
+  float t[5] = {0};
+  for (int k = 0; k < 5; k++) HIPCHK(hipEventElapsedTime(&t[k], c->ev[k], c->ev[k + 1]));
+  c->last.eval_ms = t[0];
+  c->last.plan_ms = t[1];
+  c->last.write_ms = t[3];
+  c->last.crc_ms = t[4];
+  c->last.total_ms = t[0] + t[1] + t[2] + t[3] + t[4];
+  c->last.in_bytes = s->header_bytes;
+  c->last.out_bytes = out_len;
+  c->last.n_batches = nb;
+  c->last.n_records_in = s->nrec;
+  // result
+  res->base_offset = p.base_offset;
+  res->last_offset_delta = p.lod;
+  res->n_records = (uint32_t)p.n_records;
+  if (p.err_batch >= 0) {
+    BatchStat bs;
+    HIPCHK(hipMemcpy(&bs, ea.bstat + p.err_batch, sizeof bs, hipMemcpyDeviceToHost));
+    int rc = build_error(c, s, bs, res->error);
+    if (rc) return rc;
+    res->has_error = 1;
+  }
+  if (has_agg && p.acc_touched) {
+    char b[16];
+    int n = snprintf(b, sizeof b, "%d", (int32_t)p.acc_final);
+    c->acc.assign(b, b + n);
+  }
+  return FSG_OK;
+}
+
+int download_output(fsg_chain* c, fsg_batch_output* res) {
+  uint8_t* h = (uint8_t*)malloc(c->out_len);
+  if (!h) return fail(FSG_E_DEVICE, "host allocation failed");
+  hipError_t e = hipMemcpy(h, c->out.p, c->out_len, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) {
+    free(h);
+    return fail(FSG_E_DEVICE, hipGetErrorString(e));
+  }
+  res->batch = h;
+  res->batch_len = c->out_len;
+  return FSG_OK;
+}
+
+}  // namespace
+
+extern "C" int fsg_chain_process_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics* m,
+                                       fsg_batch_output** out) {
+  HIPCHK(hipSetDevice(c->eng->device));
+  auto res = std::make_unique<fsg_batch_output>();
+  int rc = run_slice(c, s, max_bytes, m, res.get(), c->hdesc.nstages == 0);
+  if (rc) {
+    free_error(res->error);
+    return rc;
+  }
+  if (out) {
+    rc = download_output(c, res.get());
+    if (rc) {
+      free_error(res->error);
+      return rc;
+    }
+    *out = res.release();
+  } else {
+    free_error(res->error);
+  }
+  return FSG_OK;
+}
+
+extern "C" int fsg_chain_output_device(fsg_chain* c, const void** dptr, size_t* len) {
+  *dptr = c->out.p;
+  *len = c->out_len;
+  return FSG_OK;
+}
+
+extern "C" int fsg_chain_process_batch(fsg_chain* c, const uint8_t* slice, size_t len, uint64_t max_bytes,
+                                       fsg_metrics* m, fsg_batch_output** out) {
+  HIPCHK(hipSetDevice(c->eng->device));
+  fsg_slice s;
+  int rc = upload_slice(c->eng, slice, len, &s, c->stream);
+  if (rc) return rc;
+  return fsg_chain_process_slice(c, &s, max_bytes, m, out);
+}
+
+// SmartModuleChainInstance::process: one SmartModuleInput{base_offset, raw_bytes,
+// base_timestamp} is one batch of the same pipeline (no offset fix-up applies).
+extern "C" int fsg_chain_process(fsg_chain* c, const uint8_t* raw, size_t len, int64_t base_offset,
+                                 int64_t base_timestamp, fsg_metrics* m, fsg_output** out) {
+  HIPCHK(hipSetDevice(c->eng->device));
+  std::vector<uint8_t> b(57 + len);
+  auto be = [&](size_t off, uint64_t v, int n) {
+    for (int i = 0; i < n; i++) b[off + i] = (uint8_t)(v >> (8 * (n - 1 - i)));
+  };
+  be(0, (uint64_t)base_offset, 8);
+  be(8, (uint32_t)(45 + len), 4);
+  be(12, (uint32_t)-1, 4);
+  b[16] = 2;
+  be(21, 0, 2);
+  be(23, 0, 4);
+  be(27, (uint64_t)base_timestamp, 8);
+  if (len) memcpy(b.data() + 57, raw, len);
+  fsg_slice s;
+  int rc = upload_slice(c->eng, b.data(), b.size(), &s, c->stream);
+  if (rc) return rc;
+  fsg_batch_output r;
+  rc = run_slice(c, &s, ~0ull, m, &r, c->hdesc.nstages == 0);
+  if (rc) {
+    free_error(r.error);
+    return rc;
+  }
+  auto o = std::make_unique<fsg_output>();
+  memset(o.get(), 0, sizeof(fsg_output));
+  const size_t rl = c->out_len - 57;  // u32 count + records
+  uint8_t* h = (uint8_t*)malloc(std::max<size_t>(rl, 1));
+  hipError_t e = hipMemcpy(h, (uint8_t*)c->out.p + 57, rl, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) {
+    free(h);
+    free_error(r.error);
+    return fail(FSG_E_DEVICE, hipGetErrorString(e));
+  }
+  o->records = h;
+  o->records_len = rl;
+  o->n_records = r.n_records;
+  o->has_error = r.has_error;
+  o->error = r.error;
+  *out = o.release();
+  return FSG_OK;
+}
+
+extern "C" int fsg_chain_look_back(fsg_chain* c, fsg_metrics* m) {
+  (void)c;
+  (void)m;
+  return FSG_OK;  // no built-in GPU module has a look_back stage
+}
+
+extern "C" int fsg_chain_get_accumulator(fsg_chain* c, size_t stage, uint8_t** acc, size_t* len) {
+  if ((int)stage != c->agg_stage) return fail(FSG_E_INVALID_ARG, "stage is not an aggregate");
+  *acc = (uint8_t*)malloc(std::max<size_t>(1, c->acc.size()));
+  memcpy(*acc, c->acc.data(), c->acc.size());
+  *len = c->acc.size();
+  return FSG_OK;
+}
+
+extern "C" int fsg_chain_last_timings(fsg_chain* c, fsg_timings* t) {
+  *t = c->last;
+  return FSG_OK;
+}
+
+extern "C" void fsg_output_free(fsg_output* o) {
+  if (!o) return;
+  free((void*)o->records);
+  free_error(o->error);
+  delete o;
+}
+extern "C" void fsg_batch_output_free(fsg_batch_output* o) {
+  if (!o) return;
+  free((void*)o->batch);
+  free_error(o->error);
+  delete o;
+}
+
+// ---------------------------------------------------------------------------
+// RCCL: aggregate state merge across GPUs (partitions sharded p -> GPU p mod n)
+// ---------------------------------------------------------------------------
+extern "C" int fsg_comm_unique_id(uint8_t id[FSG_UNIQUE_ID_BYTES]) {
+  static_assert(sizeof(ncclUniqueId) == FSG_UNIQUE_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return fail(FSG_E_DEVICE, "ncclGetUniqueId failed");
+  memcpy(id, &u, sizeof u);
+  return FSG_OK;
+}
+extern "C" int fsg_engine_comm_init(fsg_engine* e, const uint8_t id[FSG_UNIQUE_ID_BYTES], int nranks, int rank) {
+  HIPCHK(hipSetDevice(e->device));
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof u);
+  ncclResult_t r = ncclCommInitRank(&e->comm, nranks, u, rank);
+  if (r != ncclSuccess) return fail(FSG_E_DEVICE, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  e->nranks = nranks;
+  e->rank = rank;
+  return FSG_OK;
+}
+extern "C" int fsg_allreduce_i32(fsg_engine* e, void* dev_state, size_t count) {
+  if (!e->comm) return fail(FSG_E_INVALID_ARG, "engine has no communicator");
+  HIPCHK(hipSetDevice(e->device));
+  ncclResult_t r = ncclAllReduce(dev_state, dev_state, count, ncclInt32, ncclSum, e->comm, 0);
+  if (r != ncclSuccess) return fail(FSG_E_DEVICE, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  HIPCHK(hipStreamSynchronize(0));
+  return FSG_OK;
+}

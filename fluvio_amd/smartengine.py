@@ -1,0 +1,441 @@
+"""Host-side mirror of the fluvio-smartengine API over the MI355X C ABI.
+
+Same names, argument meaning and error behaviour as the reference (paths
+relative to /root/reference):
+
+  SmartEngine                 crates/fluvio-smartengine/src/engine/wasmtime/engine.rs:26-41
+  SmartModuleChainBuilder     engine.rs:49-111
+  SmartModuleChainInstance    engine.rs:118-218 (process, look_back)
+  SmartModuleConfig(+Builder) crates/fluvio-smartengine/src/engine/config.rs:33-74
+  SmartModuleInitialData      config.rs:11-28
+  SmartModuleChainMetrics     crates/fluvio-smartengine/src/engine/metrics.rs:6-41
+  SmartModuleInput/Output     crates/fluvio-smartmodule/src/input.rs:82-184, output.rs:12-42
+  SmartModuleTransformRuntimeError  crates/fluvio-protocol/src/link/smartmodule.rs:12-72
+  EngineError                 crates/fluvio-smartengine/src/engine/error.rs:1-13
+  process_batch               crates/fluvio-spu/src/smartengine/batch.rs:41-142
+
+SmartModule bytes are chosen at chain-build time: ``builtin("regex-filter")``
+returns the ``b"\\0fsg"`` descriptor of a GPU built-in; real wasm (``b"\\0asm"``)
+is rejected with ``UnknownSmartModule`` exactly where the reference's
+``create_transform`` would fail for a module it cannot run.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Tuple
+
+from . import _ffi
+from .protocol import Batch, Record, decode_batch, decode_records, encode_records
+
+DEFAULT_SMARTENGINE_VERSION = 22  # input.rs:14 SMARTMODULE_TIMESTAMPS_VERSION
+
+BUILTINS = ("filter", "filter_init", "filter_with_param", "regex-filter", "filter_regex", "filter_odd",
+            "map", "map_double", "filter_map", "aggregate-sum")
+
+
+def builtin(name: str) -> bytes:
+    """Module bytes selecting a GPU built-in SmartModule by its reference name."""
+    return b"\0fsg" + name.encode()
+
+
+# ---------------------------------------------------------------------------
+# errors (EngineError + guest status enums)
+# ---------------------------------------------------------------------------
+class EngineError(Exception):
+    code = _ffi.FSG_E_UNKNOWN
+
+    def __init__(self, message: str = "", code: Optional[int] = None):
+        super().__init__(message)
+        if code is not None:
+            self.code = code
+
+
+class UnknownSmartModule(EngineError):
+    code = _ffi.FSG_E_UNKNOWN_SM
+
+
+class Instantiate(EngineError):
+    code = _ffi.FSG_E_INSTANTIATE
+
+
+class StoreMemoryExceeded(EngineError):
+    code = _ffi.FSG_E_STORE_MEMORY
+
+
+class SmartModuleInitError(EngineError):
+    """SmartModuleInitRuntimeError surfaced by initialize() (init.rs:42-66)."""
+    code = _ffi.FSG_E_INIT
+
+
+class SmartModuleTransformErrorStatus(EngineError):
+    """A negative guest return code (error.rs:17-34): DecodingBaseInput, ..."""
+
+
+class Unsupported(EngineError):
+    code = _ffi.FSG_E_UNSUPPORTED
+
+
+class IoError(EngineError):
+    code = _ffi.FSG_E_IO
+
+
+class DeviceError(EngineError):
+    code = _ffi.FSG_E_DEVICE
+
+
+_ERRORS = {
+    _ffi.FSG_E_UNKNOWN_SM: UnknownSmartModule, _ffi.FSG_E_INSTANTIATE: Instantiate,
+    _ffi.FSG_E_STORE_MEMORY: StoreMemoryExceeded, _ffi.FSG_E_INIT: SmartModuleInitError,
+    _ffi.FSG_E_DECODING_BASE_INPUT: SmartModuleTransformErrorStatus,
+    _ffi.FSG_E_DECODING_RECORDS: SmartModuleTransformErrorStatus,
+    _ffi.FSG_E_ENCODING_OUTPUT: SmartModuleTransformErrorStatus,
+    _ffi.FSG_E_UNKNOWN: SmartModuleTransformErrorStatus,
+    _ffi.FSG_E_UNSUPPORTED: Unsupported, _ffi.FSG_E_IO: IoError, _ffi.FSG_E_DEVICE: DeviceError,
+}
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        cls = _ERRORS.get(rc, EngineError)
+        raise cls(_ffi.last_error(), rc)
+
+
+# ---------------------------------------------------------------------------
+# config
+# ---------------------------------------------------------------------------
+@dataclass
+class SmartModuleInitialData:
+    accumulator: Optional[bytes] = None
+
+    @staticmethod
+    def none() -> "SmartModuleInitialData":
+        return SmartModuleInitialData(None)
+
+    @staticmethod
+    def with_aggregate(accumulator: bytes) -> "SmartModuleInitialData":
+        return SmartModuleInitialData(bytes(accumulator))
+
+
+@dataclass
+class SmartModuleConfig:
+    params: Dict[str, str] = field(default_factory=dict)
+    initial_data: SmartModuleInitialData = field(default_factory=SmartModuleInitialData)
+    version: Optional[int] = None
+    lookback: Optional[object] = None
+
+    @staticmethod
+    def builder() -> "SmartModuleConfigBuilder":
+        return SmartModuleConfigBuilder()
+
+    def get_version(self) -> int:
+        return DEFAULT_SMARTENGINE_VERSION if self.version is None else self.version
+
+
+class SmartModuleConfigBuilder:
+    def __init__(self):
+        self._c = SmartModuleConfig()
+
+    def param(self, key: str, value: str) -> "SmartModuleConfigBuilder":
+        self._c.params[key] = value
+        return self
+
+    def params(self, params: Dict[str, str]) -> "SmartModuleConfigBuilder":
+        self._c.params = dict(params)
+        return self
+
+    def initial_data(self, data: SmartModuleInitialData) -> "SmartModuleConfigBuilder":
+        self._c.initial_data = data
+        return self
+
+    def version(self, v: int) -> "SmartModuleConfigBuilder":
+        self._c.version = v
+        return self
+
+    def lookback(self, lb) -> "SmartModuleConfigBuilder":
+        self._c.lookback = lb
+        return self
+
+    def build(self) -> SmartModuleConfig:
+        return self._c
+
+
+class SmartModuleChainMetrics:
+    def __init__(self):
+        self._m = _ffi.fsg_metrics()
+
+    def bytes_in(self) -> int:
+        return self._m.bytes_in
+
+    def records_out(self) -> int:
+        return self._m.records_out
+
+    def invocation_count(self) -> int:
+        return self._m.invocation_count
+
+    def fuel_used(self) -> int:
+        return self._m.fuel_used
+
+
+# ---------------------------------------------------------------------------
+# input / output
+# ---------------------------------------------------------------------------
+@dataclass
+class SmartModuleInput:
+    raw_bytes: bytes
+    base_offset: int = 0
+    base_timestamp: int = 0
+
+    @staticmethod
+    def new(raw_bytes: bytes, base_offset: int, base_timestamp: int) -> "SmartModuleInput":
+        return SmartModuleInput(bytes(raw_bytes), base_offset, base_timestamp)
+
+    @staticmethod
+    def try_from_records(records: List[Record], version: int = DEFAULT_SMARTENGINE_VERSION) -> "SmartModuleInput":
+        return SmartModuleInput(encode_records(records), 0, 0)
+
+    def set_base_offset(self, v: int) -> None:
+        self.base_offset = v
+
+    def set_base_timestamp(self, v: int) -> None:
+        self.base_timestamp = v
+
+
+@dataclass
+class SmartModuleTransformRuntimeError(Exception):
+    hint: str
+    offset: int
+    kind: int
+    record_key: Optional[bytes]
+    record_value: bytes
+
+    KIND_NAMES = {0: "Filter", 1: "Map", 2: "ArrayMap", 3: "Aggregate", 4: "FilterMap"}
+
+    def __str__(self) -> str:  # Display (link/smartmodule.rs:46-64)
+        def disp(b: Optional[bytes]) -> str:
+            if b is None:
+                return "NULL"
+            try:
+                return b.decode("utf-8")
+            except UnicodeDecodeError:
+                return f"Binary: {len(b)} bytes"
+        return (f"{self.hint}\n\nSmartModule Info: \n    Type: {self.KIND_NAMES.get(self.kind, self.kind)}\n"
+                f"    Offset: {self.offset}\n    Key: {disp(self.record_key)}\n    Value: {disp(self.record_value)}")
+
+
+def _runtime_error(e: _ffi.fsg_runtime_error) -> SmartModuleTransformRuntimeError:
+    return SmartModuleTransformRuntimeError(
+        hint=ctypes.string_at(e.hint, e.hint_len).decode("utf-8", "replace") if e.hint_len else "",
+        offset=e.offset, kind=e.kind,
+        record_key=ctypes.string_at(e.key, e.key_len) if e.has_key else None,
+        record_value=ctypes.string_at(e.value, e.value_len) if e.value_len else b"")
+
+
+@dataclass
+class SmartModuleOutput:
+    raw_successes: bytes  # encoded Vec<Record>
+    error: Optional[SmartModuleTransformRuntimeError] = None
+
+    @property
+    def successes(self) -> List[Record]:
+        return decode_records(self.raw_successes)
+
+
+@dataclass
+class BatchOutput:
+    """(Batch, Option<SmartModuleTransformRuntimeError>) of SPU process_batch."""
+    raw: bytes
+    base_offset: int
+    last_offset_delta: int
+    n_records: int
+    error: Optional[SmartModuleTransformRuntimeError] = None
+
+    def batch(self):
+        return decode_batch(self.raw)[0]
+
+    def records(self) -> List[Record]:
+        return self.batch().memory_records()
+
+
+# ---------------------------------------------------------------------------
+# engine / builder / chain
+# ---------------------------------------------------------------------------
+class SmartEngine:
+    """SmartEngine::new — binds one MI355X (default: LOCAL_RANK or 0)."""
+
+    def __init__(self, device: Optional[int] = None):
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        h = ctypes.c_void_p()
+        _check(_ffi.lib().fsg_engine_new(device, ctypes.byref(h)))
+        self._h = h
+        self.device = device
+
+    @staticmethod
+    def new() -> "SmartEngine":
+        return SmartEngine()
+
+    def comm_init(self, unique_id: bytes, nranks: int, rank: int) -> None:
+        _check(_ffi.lib().fsg_engine_comm_init(self._h, unique_id, nranks, rank))
+
+    def allreduce_i32(self, dev_ptr: int, count: int) -> None:
+        _check(_ffi.lib().fsg_allreduce_i32(self._h, ctypes.c_void_p(dev_ptr), count))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and h.value and _ffi._lib is not None:
+            _ffi.lib().fsg_engine_free(h)
+            self._h = None
+
+
+def comm_unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    _check(_ffi.lib().fsg_comm_unique_id(buf))
+    return buf.raw
+
+
+class SmartModuleChainBuilder:
+    def __init__(self):
+        self._mods: List[Tuple[SmartModuleConfig, bytes]] = []
+        self._limit: Optional[int] = None
+
+    @staticmethod
+    def default() -> "SmartModuleChainBuilder":
+        return SmartModuleChainBuilder()
+
+    @staticmethod
+    def from_pair(config: SmartModuleConfig, module: bytes) -> "SmartModuleChainBuilder":
+        b = SmartModuleChainBuilder()
+        b.add_smart_module(config, module)
+        return b
+
+    def add_smart_module(self, config: SmartModuleConfig, module: bytes) -> None:
+        self._mods.append((config, bytes(module)))
+
+    def set_store_memory_limit(self, max_memory_bytes: int) -> None:
+        self._limit = max_memory_bytes
+
+    def initialize(self, engine: SmartEngine) -> "SmartModuleChainInstance":
+        L = _ffi.lib()
+        b = ctypes.c_void_p()
+        _check(L.fsg_chain_builder_new(ctypes.byref(b)))
+        if self._limit is not None:
+            L.fsg_chain_builder_set_store_memory_limit(b, self._limit)
+        for cfg, module in self._mods:
+            items = list(cfg.params.items())
+            arr = (_ffi.fsg_param * max(1, len(items)))()
+            for i, (k, v) in enumerate(items):
+                arr[i].key = k.encode()
+                arr[i].value = v.encode()
+            acc = cfg.initial_data.accumulator
+            _check(L.fsg_chain_builder_add_smart_module(
+                b, arr, len(items), cfg.get_version(), acc or b"", len(acc or b""), 1 if acc is not None else 0,
+                module, len(module)))
+        c = ctypes.c_void_p()
+        _check(L.fsg_chain_builder_initialize(b, engine._h, ctypes.byref(c)))  # consumes the builder
+        return SmartModuleChainInstance(c, engine, len(self._mods))
+
+
+class SmartModuleChainInstance:
+    def __init__(self, handle: ctypes.c_void_p, engine: SmartEngine, n: int):
+        self._h = handle
+        self._engine = engine  # keep the engine alive
+        self.n_instances = n
+
+    def process(self, input: SmartModuleInput,
+                metrics: Optional[SmartModuleChainMetrics] = None) -> SmartModuleOutput:
+        m = metrics._m if metrics is not None else None
+        out = ctypes.POINTER(_ffi.fsg_output)()
+        _check(_ffi.lib().fsg_chain_process(self._h, input.raw_bytes, len(input.raw_bytes), input.base_offset,
+                                            input.base_timestamp, ctypes.byref(m) if m is not None else None,
+                                            ctypes.byref(out)))
+        try:
+            o = out.contents
+            raw = ctypes.string_at(o.records, o.records_len) if o.records_len else b"\0\0\0\0"
+            err = _runtime_error(o.error) if o.has_error else None
+            return SmartModuleOutput(raw, err)
+        finally:
+            _ffi.lib().fsg_output_free(out)
+
+    def look_back(self, read_fn: Callable, metrics: Optional[SmartModuleChainMetrics] = None) -> None:
+        _check(_ffi.lib().fsg_chain_look_back(self._h, ctypes.byref(metrics._m) if metrics else None))
+
+    def accumulator(self, stage: int) -> bytes:
+        p = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_size_t()
+        _check(_ffi.lib().fsg_chain_get_accumulator(self._h, stage, ctypes.byref(p), ctypes.byref(n)))
+        data = ctypes.string_at(p, n.value) if n.value else b""
+        _ffi.lib().fsg_free(p)
+        return data
+
+    def last_timings(self) -> Dict[str, float]:
+        t = _ffi.fsg_timings()
+        _check(_ffi.lib().fsg_chain_last_timings(self._h, ctypes.byref(t)))
+        return {k: getattr(t, k) for k, _ in _ffi.fsg_timings._fields_}
+
+    def _batch_result(self, out) -> BatchOutput:
+        try:
+            o = out.contents
+            raw = ctypes.string_at(o.batch, o.batch_len)
+            err = _runtime_error(o.error) if o.has_error else None
+            return BatchOutput(raw, o.base_offset, o.last_offset_delta, o.n_records, err)
+        finally:
+            _ffi.lib().fsg_batch_output_free(out)
+
+    def process_batch(self, slice_bytes: bytes, max_bytes: int = (1 << 64) - 1,
+                      metrics: Optional[SmartModuleChainMetrics] = None) -> BatchOutput:
+        out = ctypes.POINTER(_ffi.fsg_batch_output)()
+        _check(_ffi.lib().fsg_chain_process_batch(self._h, slice_bytes, len(slice_bytes), max_bytes,
+                                                  ctypes.byref(metrics._m) if metrics else None,
+                                                  ctypes.byref(out)))
+        return self._batch_result(out)
+
+    def process_slice(self, sl: "ResidentSlice", max_bytes: int = (1 << 64) - 1,
+                      metrics: Optional[SmartModuleChainMetrics] = None, download: bool = True):
+        out = ctypes.POINTER(_ffi.fsg_batch_output)()
+        _check(_ffi.lib().fsg_chain_process_slice(self._h, sl._h, max_bytes,
+                                                  ctypes.byref(metrics._m) if metrics else None,
+                                                  ctypes.byref(out) if download else None))
+        return self._batch_result(out) if download else None
+
+    def output_device(self) -> Tuple[int, int]:
+        p = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        _check(_ffi.lib().fsg_chain_output_device(self._h, ctypes.byref(p), ctypes.byref(n)))
+        return p.value or 0, n.value
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and h.value and _ffi._lib is not None:
+            _ffi.lib().fsg_chain_free(h)
+            self._h = None
+
+
+class ResidentSlice:
+    """A fetch slice of stored batches ingested into HBM once (FileBatchIterator framing)."""
+
+    def __init__(self, engine: SmartEngine, slice_bytes: bytes):
+        h = ctypes.c_void_p()
+        _check(_ffi.lib().fsg_slice_upload(engine._h, slice_bytes, len(slice_bytes), ctypes.byref(h)))
+        self._h = h
+        self._engine = engine
+        nb, nr, by = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _ffi.lib().fsg_slice_info(h, ctypes.byref(nb), ctypes.byref(nr), ctypes.byref(by))
+        self.n_batches, self.n_records, self.bytes = nb.value, nr.value, by.value
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and h.value and _ffi._lib is not None:
+            _ffi.lib().fsg_slice_free(h)
+            self._h = None
+
+
+def process_batch(chain: SmartModuleChainInstance, slice_bytes: bytes, max_bytes: int,
+                  metrics: Optional[SmartModuleChainMetrics] = None
+                  ) -> Tuple[Batch, Optional[SmartModuleTransformRuntimeError]]:
+    """fluvio-spu process_batch (batch.rs:41-142): returns (Batch, Option<error>)."""
+    out = chain.process_batch(slice_bytes, max_bytes, metrics)
+    b = out.batch()
+    batch = Batch(base_offset=b.base_offset, header=b.header, records=b.memory_records())
+    return batch, out.error

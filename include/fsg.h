@@ -1,0 +1,195 @@
+/*
+ * fsg.h — C ABI of the MI355X SmartModule engine (libfsg.so).
+ *
+ * Drop-in boundary for Fluvio's SmartModule record-transform path.  Each entry
+ * point replaces one reference interface (paths relative to the reference
+ * deem0n/fluvio tree):
+ *
+ *   fsg_engine_new                      SmartEngine::new
+ *                                         crates/fluvio-smartengine/src/engine/wasmtime/engine.rs:31
+ *   fsg_chain_builder_new               SmartModuleChainBuilder::default            engine.rs:94-103
+ *   fsg_chain_builder_set_store_memory_limit
+ *                                       SmartModuleChainBuilder::set_store_memory_limit  engine.rs:60
+ *   fsg_chain_builder_add_smart_module  SmartModuleChainBuilder::add_smart_module   engine.rs:56
+ *                                         (+ SmartModuleConfig, config.rs:33-74)
+ *   fsg_chain_builder_initialize        SmartModuleChainBuilder::initialize         engine.rs:65-91
+ *                                         (+ create_transform, transforms/mod.rs:24-52)
+ *   fsg_chain_process                   SmartModuleChainInstance::process           engine.rs:135-185
+ *   fsg_chain_look_back                 SmartModuleChainInstance::look_back         engine.rs:187-218
+ *   fsg_chain_process_batch             fluvio-spu process_batch                    crates/fluvio-spu/src/smartengine/batch.rs:41-142
+ *                                         over a FileBatchIterator slice           crates/fluvio-storage/src/iterators.rs:55-160
+ *   fsg_chain_get_accumulator           SmartModuleAggregate accumulator            transforms/aggregate.rs:22-25,95
+ *   fsg_metrics                         SmartModuleChainMetrics                     crates/fluvio-smartengine/src/engine/metrics.rs:6-41
+ *   fsg_runtime_error                   SmartModuleTransformRuntimeError            crates/fluvio-protocol/src/link/smartmodule.rs:12-43
+ *
+ * SmartModule selection happens at chain-build time: `module` bytes are either a
+ * wasm binary ("\0asm" magic -> FSG_E_UNKNOWN_SM: this library runs no wasm) or a
+ * built-in descriptor "\0fsg" + <reference module name>, e.g. "\0fsgregex-filter".
+ * Transform configuration travels in `params` exactly as the reference passes it
+ * to `init` (wasmtime/instance.rs:69-78): key="..." for filter_init, regex="..."
+ * for regex-filter, etc.
+ *
+ * Conventions: the caller owns input buffers (borrowed for the call); the
+ * library owns output objects until the matching *_free.  Every function
+ * returns 0 on success or a negative FSG_E_* code; fsg_last_error_message()
+ * gives the text of the last failure on the calling thread.  A record-level
+ * SmartModule error is data (has_error in the output), not a return code,
+ * exactly like SmartModuleOutput.error.  A chain is single-threaded (&mut self
+ * in the reference); an engine may be shared by chains.  Everything runs on the
+ * GPU: there is no CPU fallback, and with no usable HIP device fsg_engine_new
+ * fails with FSG_E_DEVICE.
+ */
+#ifndef FSG_H
+#define FSG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FSG_ABI_VERSION 1
+
+/* ---- status codes (mirror EngineError and the guest status enums) ---- */
+#define FSG_OK 0
+#define FSG_E_UNKNOWN -1             /* SmartModuleTransformErrorStatus::UnknownError (error.rs:20) */
+#define FSG_E_INIT -2                /* SmartModuleInitErrorStatus::InitError (error.rs:41) */
+#define FSG_E_DECODING_BASE_INPUT -11 /* SmartModuleTransformErrorStatus::DecodingBaseInput */
+#define FSG_E_DECODING_RECORDS -22
+#define FSG_E_ENCODING_OUTPUT -33
+#define FSG_E_UNKNOWN_SM -100        /* EngineError::UnknownSmartModule (error.rs:3) */
+#define FSG_E_INSTANTIATE -101       /* EngineError::Instantiate */
+#define FSG_E_STORE_MEMORY -102      /* EngineError::StoreMemoryExceeded */
+#define FSG_E_UNSUPPORTED -103       /* valid for the reference, not implemented on the GPU path */
+#define FSG_E_IO -104                /* io::Error from batch framing / empty-chain record decode */
+#define FSG_E_INVALID_ARG -105
+#define FSG_E_DEVICE -200            /* HIP runtime failure / no device */
+
+/* SmartModuleKind tags (link/smartmodule.rs:80-95) */
+#define FSG_KIND_FILTER 0
+#define FSG_KIND_MAP 1
+#define FSG_KIND_ARRAY_MAP 2
+#define FSG_KIND_AGGREGATE 3
+#define FSG_KIND_FILTER_MAP 4
+
+typedef struct fsg_engine fsg_engine;
+typedef struct fsg_chain_builder fsg_chain_builder;
+typedef struct fsg_chain fsg_chain;
+typedef struct fsg_slice fsg_slice;
+
+typedef struct fsg_param {
+  const char *key;
+  const char *value;
+} fsg_param;
+
+typedef struct fsg_metrics {
+  uint64_t bytes_in;
+  uint64_t records_out;
+  uint64_t invocation_count;
+  uint64_t fuel_used; /* always 0: no fuel metering on the GPU */
+} fsg_metrics;
+
+typedef struct fsg_runtime_error {
+  const char *hint; /* UTF-8, hint_len bytes (not NUL-terminated in general) */
+  size_t hint_len;
+  int64_t offset;
+  int32_t kind;     /* FSG_KIND_* */
+  int32_t has_key;
+  const uint8_t *key;
+  size_t key_len;
+  const uint8_t *value;
+  size_t value_len;
+} fsg_runtime_error;
+
+/* SmartModuleOutput: successes encoded as Vec<Record> (u32 BE count + records) */
+typedef struct fsg_output {
+  const uint8_t *records;
+  size_t records_len;
+  uint32_t n_records;
+  int32_t has_error;
+  fsg_runtime_error error;
+} fsg_output;
+
+/* (Batch, Option<SmartModuleTransformRuntimeError>) returned by SPU process_batch.
+ * `batch` is the file-format encoding (12-byte preamble + 45-byte header + u32
+ * count + records) with CRC32C computed, as Batch::encode writes it. */
+typedef struct fsg_batch_output {
+  const uint8_t *batch;
+  size_t batch_len;
+  int64_t base_offset;
+  int32_t last_offset_delta;
+  uint32_t n_records;
+  int32_t has_error;
+  fsg_runtime_error error;
+} fsg_batch_output;
+
+/* per-call device timings of the last process call (HIP events on the chain stream) */
+typedef struct fsg_timings {
+  float eval_ms;    /* decode + transform kernel */
+  float plan_ms;    /* size + scan + plan kernels */
+  float write_ms;   /* compaction / re-encode kernel */
+  float crc_ms;     /* CRC32C kernels */
+  float total_ms;   /* first kernel start to last kernel end */
+  uint64_t in_bytes;      /* algorithmic bytes read (batch headers + record sections) */
+  uint64_t out_bytes;     /* algorithmic bytes written (output batch) */
+  uint64_t n_batches;
+  uint64_t n_records_in;
+} fsg_timings;
+
+const char *fsg_last_error_message(void);
+int fsg_abi_version(void);
+
+/* ---- engine ------------------------------------------------------------ */
+int fsg_device_count(int *count);
+int fsg_engine_new(int device, fsg_engine **out);
+void fsg_engine_free(fsg_engine *engine);
+
+/* ---- chain builder ----------------------------------------------------- */
+int fsg_chain_builder_new(fsg_chain_builder **out);
+int fsg_chain_builder_set_store_memory_limit(fsg_chain_builder *b, size_t max_memory_bytes);
+/* SmartModuleConfig{params, version, initial_data} + module bytes.
+ * has_initial_acc=0 means SmartModuleInitialData::None. */
+int fsg_chain_builder_add_smart_module(fsg_chain_builder *b, const fsg_param *params, size_t n_params,
+                                       int16_t version, const uint8_t *initial_acc, size_t acc_len,
+                                       int32_t has_initial_acc, const uint8_t *module, size_t module_len);
+/* consumes the builder (initialize(self)) whether or not it succeeds */
+int fsg_chain_builder_initialize(fsg_chain_builder *b, fsg_engine *engine, fsg_chain **out);
+void fsg_chain_builder_free(fsg_chain_builder *b);
+
+/* ---- chain ------------------------------------------------------------- */
+int fsg_chain_process(fsg_chain *c, const uint8_t *raw_records, size_t len, int64_t base_offset,
+                      int64_t base_timestamp, fsg_metrics *metrics, fsg_output **out);
+int fsg_chain_process_batch(fsg_chain *c, const uint8_t *slice, size_t len, uint64_t max_bytes,
+                            fsg_metrics *metrics, fsg_batch_output **out);
+int fsg_chain_look_back(fsg_chain *c, fsg_metrics *metrics); /* no look_back stages: Ok */
+int fsg_chain_get_accumulator(fsg_chain *c, size_t stage, uint8_t **acc, size_t *len);
+int fsg_chain_last_timings(fsg_chain *c, fsg_timings *t);
+void fsg_chain_free(fsg_chain *c);
+void fsg_output_free(fsg_output *o);
+void fsg_batch_output_free(fsg_batch_output *o);
+void fsg_free(void *p);
+
+/* ---- HBM-resident path (batches ingested once, processed many times) --- */
+/* Ingest: copies the slice to HBM and frames its batches (FileBatchIterator). */
+int fsg_slice_upload(fsg_engine *engine, const uint8_t *slice, size_t len, fsg_slice **out);
+int fsg_slice_info(const fsg_slice *s, uint64_t *n_batches, uint64_t *n_records, uint64_t *bytes);
+void fsg_slice_free(fsg_slice *s);
+/* process_batch over a resident slice; the output batch stays in HBM until
+ * fsg_chain_download_output (out may be NULL to keep it resident). */
+int fsg_chain_process_slice(fsg_chain *c, const fsg_slice *s, uint64_t max_bytes, fsg_metrics *metrics,
+                            fsg_batch_output **out);
+/* device pointer + size of the last resident output batch (valid until the next call) */
+int fsg_chain_output_device(fsg_chain *c, const void **dptr, size_t *len);
+
+/* ---- multi-GPU aggregate state merge (RCCL over xGMI) ------------------- */
+#define FSG_UNIQUE_ID_BYTES 128
+int fsg_comm_unique_id(uint8_t id[FSG_UNIQUE_ID_BYTES]);
+int fsg_engine_comm_init(fsg_engine *engine, const uint8_t id[FSG_UNIQUE_ID_BYTES], int nranks, int rank);
+/* all-reduce (sum, wrapping i32) of aggregate state in HBM across the engine's communicator */
+int fsg_allreduce_i32(fsg_engine *engine, void *dev_state, size_t count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FSG_H */

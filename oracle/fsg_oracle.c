@@ -1165,7 +1165,7 @@ int orc_chain_add(orc_chain *c, const char *module, const char **keys, const cha
   } else if (!strcmp(module, "filter_init")) { /* key required */
     v = param_get(keys, vals, n_params, "key");
     if (!v) {
-      if (msg_out) *msg_out = dup_str("Missing param key");
+      if (msg_out) *msg_out = dup_str("Missing param key\n\nSmartModule Init Error: \n");
       return ORC_E_INIT;
     }
     s.mod = M_FILTER_CONTAINS;
@@ -1184,7 +1184,7 @@ int orc_chain_add(orc_chain *c, const char *module, const char **keys, const cha
     if (!strcmp(module, "regex-filter")) {
       pat = param_get(keys, vals, n_params, "regex");
       if (!pat) {
-        if (msg_out) *msg_out = dup_str("Missing param regex");
+        if (msg_out) *msg_out = dup_str("Missing param regex\n\nSmartModule Init Error: \n");
         return ORC_E_INIT;
       }
       s.rx_keep_match = 1;

@@ -117,9 +117,9 @@ def main():
     k["chain"] = chain
     k["init_errors"] = [
         {"source": "crates/fluvio-smartengine/src/engine/wasmtime/transforms/filter.rs:62-81",
-         "module": "filter_init", "params": {}, "message": "Missing param key"},
+         "module": "filter_init", "params": {}, "message": "Missing param key\n\nSmartModule Init Error: \n"},
         {"source": "smartmodule/regex-filter/src/lib.rs:13-22",
-         "module": "regex-filter", "params": {}, "message": "Missing param regex"},
+         "module": "regex-filter", "params": {}, "message": "Missing param regex\n\nSmartModule Init Error: \n"},
     ]
 
     # --- reference guest output recorded in SURVEY.md §8c (compiled reference

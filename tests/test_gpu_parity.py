@@ -1,0 +1,299 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the
+reference's own known answers.  Bit-exact on output batch bytes (incl. CRC32C),
+error records, metrics and aggregate state.
+
+Every test here needs an MI355X (marked gpu).
+"""
+import struct
+
+import pytest
+
+from fluvio_amd import protocol as P
+from fluvio_amd import synth
+from fluvio_amd.smartengine import (IoError, SmartEngine, SmartModuleChainBuilder, SmartModuleChainMetrics,
+                                    SmartModuleConfig, SmartModuleInitError, SmartModuleInitialData,
+                                    SmartModuleInput, SmartModuleTransformErrorStatus, UnknownSmartModule,
+                                    Unsupported, ResidentSlice, StoreMemoryExceeded, builtin)
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    return SmartEngine(0)
+
+
+def gpu_chain(engine, modules, limit=None):
+    b = SmartModuleChainBuilder.default()
+    if limit is not None:
+        b.set_store_memory_limit(limit)
+    for name, params, acc in modules:
+        cb = SmartModuleConfig.builder().params(params or {})
+        if acc is not None:
+            cb.initial_data(SmartModuleInitialData.with_aggregate(acc))
+        b.add_smart_module(cb.build(), builtin(name))
+    return b.initialize(engine)
+
+
+def orc_chain(modules):
+    return O.OracleChain([(n, p or {}, a) for n, p, a in modules])
+
+
+def mods(spec):
+    return [(m[0], m[1], m[2].encode() if isinstance(m[2], str) else m[2]) for m in spec]
+
+
+def assert_same_error(ge, oe):
+    if oe is None:
+        assert ge is None
+        return
+    assert ge is not None
+    assert ge.hint == oe["hint"]
+    assert ge.offset == oe["offset"]
+    assert ge.kind == oe["kind"]
+    assert ge.record_key == oe["key"]
+    assert ge.record_value == oe["value"]
+
+
+def check_batch(engine, modules, slice_bytes, max_bytes=(1 << 64) - 1, calls=1):
+    g = gpu_chain(engine, modules)
+    o = orc_chain(modules)
+    for _ in range(calls):
+        gm = SmartModuleChainMetrics()
+        try:
+            gout = g.process_batch(slice_bytes, max_bytes, gm)
+            gerr = None
+        except Exception as e:  # noqa: BLE001
+            gout, gerr = None, e
+        oout = o.process_batch(slice_bytes, max_bytes)
+        if oout["status"] != 0:
+            assert gerr is not None, f"oracle status {oout['status']}, gpu succeeded"
+            assert getattr(gerr, "code", None) == oout["status"], (gerr, oout["status"])
+            continue
+        assert gerr is None, gerr
+        assert gout.raw == oout["bytes"], "output batch bytes differ"
+        assert gout.base_offset == oout["base_offset"]
+        assert gout.last_offset_delta == oout["last_offset_delta"]
+        assert gout.n_records == oout["n_records"]
+        assert_same_error(gout.error, oout["error"])
+        om = oout["metrics"]
+        assert gm.bytes_in() == om["bytes_in"]
+        assert gm.invocation_count() == om["invocation_count"]
+        assert gm.records_out() == om["records_out"]
+        assert gm.fuel_used() == 0
+    for i, m in enumerate(modules):
+        if m[0] == "aggregate-sum":
+            assert g.accumulator(i) == o.accumulator(i)
+    return gout
+
+
+# ---------------------------------------------------------------------------
+# reference known answers
+# ---------------------------------------------------------------------------
+def test_kat_chain_cases(engine, kats):
+    for case in kats["chain"]:
+        modules = mods(case["modules"])
+        if any(m[0] == "aggregate" for m in modules):
+            with pytest.raises(Unsupported):
+                gpu_chain(engine, modules)
+            continue
+        g = gpu_chain(engine, modules)
+        for call in case["calls"]:
+            inp = SmartModuleInput.try_from_records([P.Record.new(v) for v in call["values"]])
+            out = g.process(inp)
+            assert out.error is None
+            assert [r.value for r in out.successes] == [v.encode() for v in call["expect"]], case["name"]
+
+
+def test_kat_init_errors(engine, kats):
+    for c in kats["init_errors"]:
+        with pytest.raises(SmartModuleInitError) as e:
+            gpu_chain(engine, [(c["module"], c["params"], None)])
+        assert str(e.value) == c["message"]
+
+
+def test_kat_survey_guest(engine, kats):
+    g = kats["survey_guest"]
+    ch = gpu_chain(engine, [(g["module"], {}, None)])
+    recs = [P.Record.new(v) for v in g["ok"]["values"]]
+    for i, r in enumerate(recs):
+        r.preamble.offset_delta = i
+    out = ch.process(SmartModuleInput(P.encode_records(recs), g["ok"]["base_offset"], 0))
+    assert out.raw_successes.hex() == g["ok"]["expect_successes"]
+    assert out.error is None
+    u = g["utf8"]
+    recs = [P.Record.new(bytes.fromhex(v)) for v in u["values_hex"]]
+    for i, r in enumerate(recs):
+        r.preamble.offset_delta = i
+    out = ch.process(SmartModuleInput(P.encode_records(recs), u["base_offset"], 0))
+    assert [r.value for r in out.successes] == [v.encode() for v in u["expect_values"]]
+    e = out.error
+    assert (e.hint, e.offset, e.kind, e.record_key, e.record_value.hex()) == (
+        u["error"]["hint"], u["error"]["offset"], u["error"]["kind"], None, u["error"]["value"])
+
+
+def test_kat_process_batch(engine, kats):
+    for case in kats["process_batch"]:
+        modules = mods(case["modules"])
+        if any(m[0] == "aggregate" for m in modules):
+            continue
+        out = check_batch(engine, modules, bytes.fromhex(case["slice"]), case["max_bytes"])
+        exp = case["expect"]
+        b = out.batch()
+        recs = b.memory_records()
+        assert b.base_offset == exp["base_offset"]
+        assert [r.value for r in recs] == [v.encode() for v in exp["values"]], case["name"]
+        if "next_offset" in exp:
+            assert b.base_offset + b.header.last_offset_delta + 1 == exp["next_offset"]
+        if "error" in exp:
+            assert out.error.hint == exp["error"]["hint"]
+            assert out.error.offset == exp["error"]["offset"]
+
+
+def test_unknown_module(engine):
+    b = SmartModuleChainBuilder.default()
+    b.add_smart_module(SmartModuleConfig.builder().build(), b"\0asm\x01\0\0\0")
+    with pytest.raises(UnknownSmartModule):
+        b.initialize(engine)
+    b = SmartModuleChainBuilder.default()
+    b.add_smart_module(SmartModuleConfig.builder().build(), builtin("no-such-module"))
+    with pytest.raises(UnknownSmartModule):
+        b.initialize(engine)
+
+
+# ---------------------------------------------------------------------------
+# randomized parity over synthetic slices
+# ---------------------------------------------------------------------------
+CHAINS = {
+    "filter": [("filter", {}, None)],
+    "filter_init_timeout": [("filter_init", {"key": "timeout"}, None)],
+    "filter_with_param": [("filter_with_param", {}, None)],
+    "regex_ssn": [("regex-filter", {"regex": r"\d{3}-\d{2}-\d{4}"}, None)],
+    "filter_regex": [("filter_regex", {}, None)],
+    "regex_level": [("regex-filter", {"regex": r'^\{"level":"(warn|error)"'}, None)],
+    "regex_unbounded": [("regex-filter", {"regex": r"a.*c\d+$"}, None)],
+    "regex_unicode": [("regex-filter", {"regex": r"é|\d\d"}, None)],
+    "map": [("map", {}, None)],
+    "filter_then_map": [("filter_init", {"key": "timeout"}, None), ("map", {}, None)],
+    "map_then_filter": [("map", {}, None), ("filter_init", {"key": "TIMEOUT"}, None)],
+    "map_then_lower_filter": [("map", {}, None), ("filter_init", {"key": "timeout"}, None)],
+    "filter_odd": [("filter_odd", {}, None)],
+    "map_double": [("map_double", {}, None)],
+    "filter_map": [("filter_map", {}, None)],
+    "map_double_filter_map": [("map_double", {}, None), ("filter_map", {}, None)],
+    "agg_sum": [("aggregate-sum", {}, b"7")],
+    "filter_agg_sum": [("filter_with_param", {"key": "1"}, None), ("aggregate-sum", {}, None)],
+    "empty": [],
+}
+
+
+@pytest.mark.parametrize("kind,n", [(1, 3000), (2, 2000), (3, 5000), (4, 4000)])
+@pytest.mark.parametrize("chain", sorted(CHAINS))
+def test_random_parity(engine, chain, kind, n):
+    sl = synth.make_slice(kind, n, base_offset=1000)
+    check_batch(engine, CHAINS[chain], sl)
+
+
+@pytest.mark.parametrize("max_bytes", [0, 1, 100, 5000, 40000, 300000])
+@pytest.mark.parametrize("chain", ["filter_init_timeout", "filter_then_map", "filter_map", "agg_sum"])
+def test_max_bytes_cut(engine, chain, max_bytes):
+    kind = 3 if chain in ("filter_map", "agg_sum") else 2
+    sl = synth.make_slice(kind, 1500, base_offset=77)
+    check_batch(engine, CHAINS[chain], sl, max_bytes)
+
+
+def test_aggregate_state_across_calls(engine):
+    sl = synth.make_slice(3, 3000)
+    check_batch(engine, CHAINS["agg_sum"], sl, calls=3)
+    check_batch(engine, [("aggregate-sum", {}, b"\xff\xfe")], sl)  # invalid UTF-8 accumulator
+    check_batch(engine, [("aggregate-sum", {}, b" 2147483647\n")], sl)  # wrapping sum
+
+
+def test_process_parity(engine):
+    """SmartModuleChainInstance::process on single inputs (per-batch API)."""
+    for chain in ("filter_init_timeout", "regex_ssn", "filter_odd", "filter_then_map", "filter_map", "empty"):
+        modules = CHAINS[chain]
+        g, o = gpu_chain(engine, modules), orc_chain(modules)
+        for kind in (1, 2, 4):
+            sl = synth.make_slice(kind, 300)
+            for b in P.decode_batches(sl):
+                gm = SmartModuleChainMetrics()
+                gout = g.process(SmartModuleInput(b.records_bytes, b.base_offset, b.header.first_timestamp), gm)
+                oout = o.process(b.records_bytes, b.base_offset, b.header.first_timestamp)
+                assert oout["status"] == 0
+                assert gout.raw_successes == oout["bytes"], chain
+                assert_same_error(gout.error, oout["error"])
+                assert gm.bytes_in() == oout["metrics"]["bytes_in"]
+                assert gm.records_out() == oout["metrics"]["records_out"]
+
+
+def test_large_records_beyond_window(engine):
+    """Records larger than the 17 KB LDS window take the global-memory path."""
+    batches = b""
+    base = 0
+    for size in (100, 20000, 17380, 17400, 70000, 5):
+        b = P.Batch(base_offset=base, header=P.BatchHeader(producer_id=0))
+        for j in range(3):
+            v = (b"x" * (size - 9)) + (b"timeout" if j != 1 else b"nothing") + b"\xc3\xa9"
+            b.add_record(P.Record.new(v))
+        batches += b.encode()
+        base += 3
+    for chain in ("filter_init_timeout", "map", "regex_unbounded", "filter_then_map"):
+        check_batch(engine, CHAINS[chain], batches)
+
+
+def test_edge_slices(engine):
+    chain = CHAINS["filter_init_timeout"]
+    good = synth.make_slice(2, 100)
+    # empty slice
+    check_batch(engine, chain, b"")
+    # batch with zero records, negative count
+    e = P.Batch(base_offset=5).encode()
+    check_batch(engine, chain, e + good)
+    neg = bytearray(e)
+    neg[57:61] = struct.pack(">i", -3)
+    check_batch(engine, chain, bytes(neg))
+    # truncated slice -> io error after processing the good batches
+    check_batch(engine, chain, good + good[:100])
+    # compressed batch (gzip bits) -> unsupported on the GPU path
+    comp = bytearray(P.decode_batches(good) and good)
+    comp[22] |= 1
+    with pytest.raises(Unsupported):
+        gpu_chain(engine, chain).process_batch(bytes(comp))
+    # a record whose length claims more than the section -> decoding error (-11)
+    bad = bytearray(good)
+    bad[61] = 0x7E
+    check_batch(engine, chain, bytes(bad))
+    # count larger than the records present -> decoding error
+    more = bytearray(e)
+    more[57:61] = struct.pack(">i", 2)
+    check_batch(engine, chain, bytes(more))
+    # empty chain on a malformed section -> io error
+    check_batch(engine, [], bytes(more))
+
+
+def test_unicode_word_is_loud(engine):
+    sl = synth.make_slice(4, 500)
+    ch = gpu_chain(engine, [("regex-filter", {"regex": r"\w+"}, None)])
+    with pytest.raises(Unsupported):
+        ch.process_batch(sl)
+
+
+def test_store_memory_limit(engine):
+    ch = gpu_chain(engine, CHAINS["filter"], limit=1000)
+    with pytest.raises(StoreMemoryExceeded):
+        ch.process_batch(synth.make_slice(2, 100))
+
+
+def test_resident_slice_matches_process_batch(engine):
+    sl = synth.make_slice(2, 4000)
+    ch = gpu_chain(engine, CHAINS["filter_then_map"])
+    rs = ResidentSlice(engine, sl)
+    a = ch.process_slice(rs)
+    b = ch.process_batch(sl)
+    assert a.raw == b.raw
+    o = orc_chain(CHAINS["filter_then_map"]).process_batch(sl)
+    assert a.raw == o["bytes"]
+    t = ch.last_timings()
+    assert t["eval_ms"] > 0 and t["out_bytes"] == len(a.raw)
