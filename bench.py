@@ -71,7 +71,7 @@ def main():
 
     # partition slice of this rank (p -> rank), ingested into HBM once
     t0 = time.time()
-    sl_bytes = synth.make_slice(kind, nrec, seed=synth.SEEDS[kind] + rank, base_offset=0)
+    sl_bytes = synth.make_slice_array(kind, nrec, seed=synth.SEEDS[kind] + rank, base_offset=0)
     gen_s = time.time() - t0
     t0 = time.time()
     rs = ResidentSlice(engine, sl_bytes)
@@ -120,12 +120,13 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle.oracle import OracleChain
         # the sample is a batch-aligned prefix of this rank's own slice
-        from fluvio_amd.protocol import decode_batch
         pos, n_s = 0, 0
         while pos < len(sl_bytes) and n_s < a.cpu_sample:
-            bh, pos = decode_batch(sl_bytes, pos)
-            n_s += int.from_bytes(bh.records_bytes[:4], "big")
-        sample = sl_bytes[:pos]
+            hdr = sl_bytes[pos:pos + 61].tobytes()
+            blen = int.from_bytes(hdr[8:12], "big")
+            n_s += int.from_bytes(hdr[57:61], "big")
+            pos += 12 + blen
+        sample = sl_bytes[:pos].tobytes()
         oc = OracleChain(modules)
         t1 = time.perf_counter()
         r = oc.process_batch(sample)

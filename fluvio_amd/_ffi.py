@@ -95,7 +95,7 @@ SIGNATURES = {
     "fsg_output_free": (None, [ctypes.POINTER(fsg_output)]),
     "fsg_batch_output_free": (None, [ctypes.POINTER(fsg_batch_output)]),
     "fsg_free": (None, [VP]),
-    "fsg_slice_upload": (ctypes.c_int, [VP, U8P, SZ, PP]),
+    "fsg_slice_upload": (ctypes.c_int, [VP, VP, SZ, PP]),
     "fsg_slice_info": (ctypes.c_int, [VP, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                       ctypes.POINTER(ctypes.c_uint64)]),
     "fsg_slice_free": (None, [VP]),
@@ -133,6 +133,16 @@ def lib():
                                             ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         _lib = L
     return _lib
+
+
+def buf_ptr(data):
+    """(pointer, length) of a bytes-like object without copying (bytes or numpy uint8)."""
+    if isinstance(data, (bytes, bytearray)):
+        b = bytes(data)
+        return ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p), len(b), b
+    import numpy as np
+    a = np.ascontiguousarray(data, dtype=np.uint8)
+    return ctypes.c_void_p(a.ctypes.data), a.nbytes, a
 
 
 def last_error() -> str:

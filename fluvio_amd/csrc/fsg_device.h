@@ -42,6 +42,7 @@ enum ErrCode : uint32_t {
   EC_UTF8 = 1,        // aux = valid_up_to, aux2 = error_len (0 = None)
   EC_PARSE = 2,       // aux = ParseIntError kind (1 Empty, 2 InvalidDigit, 3 PosOverflow, 4 NegOverflow)
   EC_ACC_UTF8 = 3,    // aggregate accumulator is not UTF-8 (aux/aux2 as EC_UTF8)
+  EC_UNSUP = 4,       // the record needs a feature the GPU path lacks (reached in stream order)
 };
 
 struct DfaDesc {

@@ -559,7 +559,7 @@ __device__ bool dfa_run_full(P s, uint32_t n, const uint8_t* blob, const DfaDesc
 // ---------------------------------------------------------------------------
 template <bool kLds, typename P>
 __device__ void eval_window(WaveLds& L, P w, uint32_t wlen, int nr, const ChainDesc& ch, const uint8_t* blob,
-                            int nst, bool& unsupported) {
+                            int nst, int lds_stage, bool& unsupported) {
   const uint32_t l = lane_id();
   bool nonascii_done = false;
   for (int s = 0; s < nst; s++) {
@@ -582,7 +582,7 @@ __device__ void eval_window(WaveLds& L, P w, uint32_t wlen, int nr, const ChainD
     }
     DfaView dv;
     if (op == OP_REGEX) {
-      const bool in_lds = sd.dfa.nstates * sd.dfa.nclasses <= (uint32_t)kDfaLds;
+      const bool in_lds = s == lds_stage;
       dv.cls = in_lds ? (upper ? L.dfa_clsu : L.dfa_cls) : blob + (upper ? sd.dfa.classmap_up : sd.dfa.classmap);
       dv.trans = in_lds ? L.dfa_trans : blob + sd.dfa.trans;
       dv.acc = in_lds ? L.dfa_acc : blob + sd.dfa.accept;
@@ -640,7 +640,11 @@ __device__ void eval_window(WaveLds& L, P w, uint32_t wlen, int nr, const ChainD
             bool m;
             if (src) {
               if (f & RF_NONASCII) {
-                if (sd.dfa.unicode_word) unsupported = true;
+                if (sd.dfa.unicode_word) {
+                  err = true;  // \w on a non-ASCII value: surfaces only if this record is reached
+                  ec = EC_UNSUP;
+                  break;
+                }
                 m = dfa_run_full(w + vs, vl, blob, sd.dfa, upper);
               } else if (sd.dfa.max_len >= 0) {
                 m = (f & RF_MATCH) != 0;
@@ -735,10 +739,12 @@ __global__ __launch_bounds__(64) void k_eval(EvalArgs a) {
   const uint64_t sec0 = pos + 57;
   const uint64_t sec_end = pos + 12 + (uint64_t)(uint32_t)batch_len;  // framing validated at ingest
   const uint32_t sec_len = (uint32_t)(sec_end - sec0);
-  // ---- stage the DFA of a regex stage into LDS (first one only)
+  // ---- stage the DFA of a regex stage into LDS (first one that fits)
+  int lds_stage = -1;
   for (int s = 0; s < (int)ch.nstages; s++) {
     const StageDesc& sd = ch.st[s];
     if (sd.op == OP_REGEX && sd.dfa.nstates * sd.dfa.nclasses <= (uint32_t)kDfaLds) {
+      lds_stage = s;
       for (uint32_t i = l; i < 256; i += 64) {
         L.dfa_cls[i] = a.blob[sd.dfa.classmap + i];
         L.dfa_clsu[i] = a.blob[sd.dfa.classmap_up + i];
@@ -817,9 +823,10 @@ __global__ __launch_bounds__(64) void k_eval(EvalArgs a) {
       int nr_eval = nr;
       if (phase == 1 && done_recs + (uint32_t)nr > err_idx + 1) nr_eval = (int)(err_idx + 1 - done_recs);
       if (global_mode)
-        eval_window<false>(L, S + gbase, (uint32_t)(sec_end - gbase), nr_eval, ch, a.blob, nst, unsupported);
+        eval_window<false>(L, S + gbase, (uint32_t)(sec_end - gbase), nr_eval, ch, a.blob, nst, lds_stage,
+                           unsupported);
       else
-        eval_window<true>(L, (const uint8_t*)L.win, wlen, nr_eval, ch, a.blob, nst, unsupported);
+        eval_window<true>(L, (const uint8_t*)L.win, wlen, nr_eval, ch, a.blob, nst, lds_stage, unsupported);
       const uint64_t wbase = global_mode ? gbase : al;
       // ---- error tracking (phase A) and descriptor emission
       for (int r0 = 0; r0 < nr_eval; r0 += 64) {
@@ -903,7 +910,7 @@ __global__ __launch_bounds__(64) void k_eval(EvalArgs a) {
     }
     if (phase == 0 && err_stage == 0xFFFFFFFFu) break;
   }
-  if (!(flags & BF_DECODE) && err_stage != 0xFFFFFFFFu) flags |= BF_ERR;
+  if (!(flags & BF_DECODE) && err_stage != 0xFFFFFFFFu) flags |= (err_code == EC_UNSUP) ? BF_UNSUPPORTED : BF_ERR;
   if (err_stage == 0xFFFFFFFFu || err_stage + 1 == ch.nstages) flags |= BF_LAST_STAGE;
   if (unsupported) flags |= BF_UNSUPPORTED;
   if (l == 0) {

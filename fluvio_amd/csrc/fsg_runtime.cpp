@@ -696,7 +696,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   if (m) {
     m->bytes_in += p.bytes_in;
     m->invocation_count += p.invocations;
-    m->records_out += p.records_out;
+    if (c->hdesc.nstages) m->records_out += p.records_out;  // the empty chain adds none (engine.rs:179-184)
   }
   if (p.status != 0) {
     const char* why = p.status == FSG_E_UNSUPPORTED ? "input needs a feature the GPU path does not implement"

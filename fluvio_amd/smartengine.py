@@ -417,7 +417,9 @@ class ResidentSlice:
 
     def __init__(self, engine: SmartEngine, slice_bytes: bytes):
         h = ctypes.c_void_p()
-        _check(_ffi.lib().fsg_slice_upload(engine._h, slice_bytes, len(slice_bytes), ctypes.byref(h)))
+        ptr, n, keep = _ffi.buf_ptr(slice_bytes)
+        _check(_ffi.lib().fsg_slice_upload(engine._h, ptr, n, ctypes.byref(h)))
+        del keep
         self._h = h
         self._engine = engine
         nb, nr, by = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()

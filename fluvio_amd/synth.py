@@ -8,6 +8,8 @@ kind 4: edge cases (empty values, keys, invalid UTF-8, multi-byte UTF-8)
 import ctypes
 import os
 
+import numpy as np
+
 from . import _ffi
 
 _LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libfsg_synth.so")
@@ -30,12 +32,19 @@ def _l():
     return _lib
 
 
-def make_slice(kind: int, nrec: int, seed: int = None, base_offset: int = 0, max_section: int = 16384) -> bytes:
-    """Returns the encoded batches (file format) holding `nrec` records."""
+def make_slice_array(kind: int, nrec: int, seed: int = None, base_offset: int = 0,
+                     max_section: int = 16384) -> np.ndarray:
+    """The encoded batches (file format) holding `nrec` records, as a uint8 array
+    (no copy; for the multi-GB bench slices)."""
     seed = SEEDS[kind] if seed is None else seed
     cap = nrec * REC_BYTES[kind] + (nrec // 4 + 16) * 64 + (1 << 16)
-    buf = ctypes.create_string_buffer(cap)
-    n = _l().synth_slice(kind, nrec, seed, base_offset, buf, cap, max_section)
+    buf = np.empty(cap, dtype=np.uint8)
+    n = _l().synth_slice(kind, nrec, seed, base_offset, buf.ctypes.data, cap, max_section)
     if n == 0 and nrec:
         raise RuntimeError("synth buffer too small")
-    return buf.raw[:n]
+    return buf[:n]
+
+
+def make_slice(kind: int, nrec: int, seed: int = None, base_offset: int = 0, max_section: int = 16384) -> bytes:
+    """Returns the encoded batches (file format) holding `nrec` records."""
+    return make_slice_array(kind, nrec, seed, base_offset, max_section).tobytes()

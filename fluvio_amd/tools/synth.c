@@ -90,26 +90,54 @@ static size_t gen_c1(uint8_t *v) {
   }
   return n;
 }
+static size_t put(char *o, size_t k, const char *s) {
+  size_t n = strlen(s);
+  memcpy(o + k, s, n);
+  return k + n;
+}
+static size_t put_u(char *o, size_t k, uint32_t v, int width) {
+  char t[12];
+  int n = 0;
+  do {
+    t[n++] = (char)('0' + v % 10);
+    v /= 10;
+  } while (v);
+  while (n < width) t[n++] = '0';
+  while (n) o[k++] = t[--n];
+  return k;
+}
 static size_t gen_c2(uint8_t *v) {
   static const char *LV[] = {"debug", "info", "warn", "error"};
+  static size_t wl[NWORDS];
+  if (!wl[0])
+    for (size_t i = 0; i < NWORDS; i++) wl[i] = strlen(WORDS[i]);
   char *o = (char *)v;
   size_t k = 0;
-  const char *lv = LV[rnd_n(4)];
-  k += (size_t)sprintf(o + k, "{\"level\":\"%s\",\"message\":\"", lv);
+  k = put(o, k, "{\"level\":\"");
+  k = put(o, k, LV[rnd_n(4)]);
+  k = put(o, k, "\",\"message\":\"");
   const int timeout = (int)(rnd() & 1);
   const size_t target = 1024 - 80;
   int placed = 0;
   while (k < target) {
     if (timeout && !placed && k > 100 && rnd_n(8) == 0) {
-      k += (size_t)sprintf(o + k, "timeout ");
+      k = put(o, k, "timeout ");
       placed = 1;
       continue;
     }
-    k += (size_t)sprintf(o + k, "%s ", WORDS[rnd_n(NWORDS)]);
+    const uint32_t w = rnd_n(NWORDS);
+    memcpy(o + k, WORDS[w], wl[w]);
+    k += wl[w];
+    o[k++] = ' ';
   }
-  if (timeout && !placed) k += (size_t)sprintf(o + k, "timeout ");
-  k += (size_t)sprintf(o + k, "\",\"service\":\"svc-%02u\",\"host\":\"h-%04u\",\"ts\":%u}", rnd_n(100),
-                       rnd_n(10000), rnd_n(1000000000));
+  if (timeout && !placed) k = put(o, k, "timeout ");
+  k = put(o, k, "\",\"service\":\"svc-");
+  k = put_u(o, k, rnd_n(100), 2);
+  k = put(o, k, "\",\"host\":\"h-");
+  k = put_u(o, k, rnd_n(10000), 4);
+  k = put(o, k, "\",\"ts\":");
+  k = put_u(o, k, rnd_n(1000000000), 1);
+  o[k++] = '}';
   return k;
 }
 static size_t gen_c3(uint8_t *v) {

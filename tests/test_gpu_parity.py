@@ -274,10 +274,16 @@ def test_edge_slices(engine):
 
 
 def test_unicode_word_is_loud(engine):
-    sl = synth.make_slice(4, 500)
-    ch = gpu_chain(engine, [("regex-filter", {"regex": r"\w+"}, None)])
+    """\\w on a non-ASCII value is outside the GPU subset: FSG_E_UNSUPPORTED when
+    (and only when) such a record is reached in stream order, like the oracle."""
+    chain = [("regex-filter", {"regex": r"\w+"}, None)]
+    check_batch(engine, chain, synth.make_slice(4, 500))
+    b = P.Batch()
+    for v in ("abc", "caf\u00e9", "xyz"):
+        b.add_record(P.Record.new(v))
     with pytest.raises(Unsupported):
-        ch.process_batch(sl)
+        gpu_chain(engine, chain).process_batch(b.encode())
+    check_batch(engine, chain, b.encode())
 
 
 def test_store_memory_limit(engine):
