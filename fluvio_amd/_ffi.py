@@ -11,7 +11,7 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libfsg.so")
+LIB_PATH = os.environ.get("FSG_LIB") or os.path.join(_HERE, "_lib", "libfsg.so")
 CSRC = os.path.join(_HERE, "csrc")
 
 FSG_OK = 0

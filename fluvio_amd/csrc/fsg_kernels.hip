@@ -210,6 +210,35 @@ __device__ int parse_i32(P s, uint32_t n, int32_t* out) {
 }
 
 // ---------------------------------------------------------------------------
+// diagnostic phase stamps (built only with -DFSG_STAMPS; never in the product)
+// ---------------------------------------------------------------------------
+#ifdef FSG_STAMPS
+__device__ unsigned long long g_stamps[16];
+#define STAMP_DECL unsigned long long st_acc[16] = {0}; unsigned long long st_t = __builtin_amdgcn_s_memtime();
+#define STAMP(i)                                                 \
+  do {                                                           \
+    unsigned long long t_ = __builtin_amdgcn_s_memtime();        \
+    st_acc[i] += t_ - st_t;                                      \
+    st_t = t_;                                                   \
+  } while (0)
+#define STAMP_COUNT(i, v) st_acc[i] += (v)
+#define STAMP_PARAMS , unsigned long long* st_acc, unsigned long long& st_t
+#define STAMP_ARGS , st_acc, st_t
+#define STAMP_FLUSH()                                                        \
+  do {                                                                       \
+    if (threadIdx.x == 0)                                                    \
+      for (int i_ = 0; i_ < 16; i_++) if (st_acc[i_]) atomicAdd(&g_stamps[i_], st_acc[i_]); \
+  } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(i)
+#define STAMP_COUNT(i, v)
+#define STAMP_PARAMS
+#define STAMP_ARGS
+#define STAMP_FLUSH()
+#endif
+
+// ---------------------------------------------------------------------------
 // k_eval: per-wave LDS state
 // ---------------------------------------------------------------------------
 enum RecFlags : uint32_t {
@@ -221,6 +250,14 @@ enum RecFlags : uint32_t {
 };
 
 constexpr int kDfaLds = 4096;
+constexpr int kEvalThreads = 256;  // one 4-wave workgroup per stored batch
+// compile-time op sets of the k_eval variants
+constexpr uint32_t opbit(int op) { return 1u << op; }
+constexpr uint32_t kOpsContains = opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
+constexpr uint32_t kOpsRegex = opbit(OP_REGEX) | opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
+constexpr uint32_t kOpsAll = 0x7Fu;
+constexpr int kDfaDyn = 768 + kDfaLds;  // dynamic LDS of a chain with a regex stage
+extern __shared__ __attribute__((aligned(16))) uint8_t g_dyn_lds[];
 
 struct __attribute__((aligned(16))) WaveLds {
   uint8_t win[kWin + 64];
@@ -241,13 +278,11 @@ struct __attribute__((aligned(16))) WaveLds {
   int64_t r_od[kMaxR];
   int64_t r_ts[kMaxR];
   int64_t r_hdr[kMaxR];
-  uint8_t dfa_cls[256];
-  uint8_t dfa_clsu[256];
-  uint8_t dfa_acc[256];
-  uint8_t dfa_trans[kDfaLds];
+  uint32_t r_end[kMaxR];    // fast walk: record end (window offset)
   // wave-uniform scalars
   int32_t nr;
   int32_t walk_status;      // 0 ok, 1 decode error, 2 window incomplete (need next window)
+  uint32_t err_stage_b, err_idx_b;  // broadcast of the batch's first error (wave 0 -> all)
   uint32_t next_cursor_lo, next_cursor_hi;
 };
 
@@ -371,6 +406,89 @@ done:
   L.next_cursor_hi = (uint32_t)(nxt >> 32);
 }
 
+// Fast walk: lane 0 chases only the length varints (record i+1 starts at
+// start_i + varint_size + len when the record is well formed); then every lane
+// parses its own records exactly (Record::decode) and checks that the fields end
+// where the length said.  Any inconsistency -> caller runs the exact serial walk.
+// Returns true when the window was walked.
+__device__ bool walk_fast(WaveLds& L, const uint8_t* w, uint64_t wbase, uint32_t wlen, uint64_t sec_end,
+                          uint64_t cursor, uint32_t rec_remaining) {
+  const uint32_t tid = threadIdx.x;
+  const uint64_t sec_lim64 = sec_end - wbase;
+  const uint32_t have = wlen < sec_lim64 ? wlen : (uint32_t)sec_lim64;
+  if (tid == 0) {
+    uint32_t q = (uint32_t)(cursor - wbase);
+    int n = 0;
+    const int lim = (int)(rec_remaining < (uint32_t)kMaxR ? rec_remaining : (uint32_t)kMaxR);
+    while (n < lim) {
+      uint32_t q0 = q;
+      int64_t len;
+      if (wvarint(w, q, have, &len)) break;
+      if (len < 0 || (int64_t)(sec_lim64 - q) < len) break;
+      const uint64_t end = (uint64_t)q + (uint64_t)len;
+      if (end > have) break;
+      L.r_start[n] = q0;
+      L.r_end[n] = (uint32_t)end;
+      q = (uint32_t)end;
+      n++;
+    }
+    L.nr = n;
+  }
+  __syncthreads();
+  const int nr = L.nr;
+  if (nr == 0) return false;
+  bool ok = true;
+  for (int r = (int)tid; r < nr; r += kEvalThreads) {
+    uint32_t q = L.r_start[r];
+    const uint32_t lim = L.r_end[r];
+    int64_t len, ts, od, kl, vl, hdr;
+    bool g = !wvarint(w, q, lim, &len);
+    uint8_t attr = 0, tag = 0;
+    if (g && q < lim) attr = w[q++]; else g = false;
+    g = g && !wvarint(w, q, lim, &ts) && !wvarint(w, q, lim, &od);
+    if (g && q < lim) tag = w[q++]; else g = false;
+    g = g && tag <= 1;
+    uint32_t kpos = 0, klen = 0;
+    if (g && tag == 1) {
+      g = !wvarint(w, q, lim, &kl) && kl >= 0 && (uint64_t)q + (uint64_t)kl <= lim;
+      if (g) {
+        kpos = q;
+        klen = (uint32_t)kl;
+        q += klen;
+      }
+    }
+    g = g && !wvarint(w, q, lim, &vl) && vl >= 0 && (uint64_t)q + (uint64_t)vl <= lim;
+    uint32_t vs = q;
+    if (g) q += (uint32_t)vl;
+    g = g && !wvarint(w, q, lim, &hdr) && q == lim;
+    if (g) {
+      L.r_vs[r] = vs;
+      L.r_vl[r] = (uint32_t)vl;
+      L.r_kpos[r] = kpos;
+      L.r_klen[r] = klen;
+      L.r_haskey[r] = tag;
+      L.r_attr[r] = attr;
+      L.r_od[r] = od;
+      L.r_ts[r] = ts;
+      L.r_hdr[r] = hdr;
+      L.r_flags[r] = RF_ALIVE;
+      L.r_es[r] = 0xFF;
+      L.r_ec[r] = 0;
+      L.r_ival[r] = 0;
+    }
+    ok &= g;
+  }
+  ok = __syncthreads_and(ok);
+  if (ok && tid == 0) {
+    L.walk_status = 0;
+    const uint64_t nxt = wbase + L.r_end[nr - 1];
+    L.next_cursor_lo = (uint32_t)nxt;
+    L.next_cursor_hi = (uint32_t)(nxt >> 32);
+  }
+  __syncthreads();
+  return ok;
+}
+
 // find the record whose [start, ...) region contains window offset p (largest r with r_vs[r] <= p)
 __device__ __forceinline__ int find_rec(const WaveLds& L, int nr, uint32_t p) {
   int lo = 0, hi = nr - 1, r = -1;
@@ -390,60 +508,112 @@ __device__ __forceinline__ uint32_t zbytes(uint32_t x) {
   return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
 }
 
+// SWAR helpers (4 bytes per u32)
+__device__ __forceinline__ uint32_t swar_upper(uint32_t x) {
+  // make_ascii_uppercase on each byte: 'a'..'z' -> 'A'..'Z', other bytes unchanged
+  const uint32_t y = x & 0x7F7F7F7Fu;
+  const uint32_t ge_a = y + 0x1F1F1F1Fu;   // high bit set where y >= 'a'
+  const uint32_t gt_z = y + 0x05050505u;   // high bit set where y >= '{'
+  const uint32_t lower = ge_a & ~gt_z & ~x & 0x80808080u;
+  return x - (lower >> 2);
+}
+// bytes [t, t+4) of the little-endian byte stream held in w[] (t compile-time)
+template <int T>
+__device__ __forceinline__ uint32_t bytes_at(const uint32_t (&w)[8], int k) {
+  constexpr int q = T / 4, r = T % 4;
+  const uint32_t lo = w[k + q];
+  if constexpr (r == 0) {
+    return lo;
+  } else {
+    const uint32_t hi = w[k + q + 1];
+    return (lo >> (8 * r)) | (hi << (32 - 8 * r));
+  }
+}
+
+// match mask of needle byte T at positions 4k..4k+3 of the chunk
+template <int T>
+__device__ __forceinline__ void needle_step(const uint32_t (&w)[8], const uint32_t (&nb)[16], uint32_t m,
+                                            uint32_t (&acc)[4]) {
+  if ((uint32_t)T < m) {
+    const uint32_t N = nb[T];
+#pragma unroll
+    for (int k = 0; k < 4; k++) acc[k] &= zbytes(bytes_at<T>(w, k) ^ N);
+  }
+}
+
 // Data-parallel substring scan + non-ASCII marking over the values of the window.
 // Marks RF_MATCH on records whose (optionally uppercased) value contains needle.
+// LDS path: each lane takes 16-byte chunks; the needle's first 16 bytes are
+// matched branch-free in registers (32 bytes loaded with two ds_read_b128),
+// longer needles finish with LDS byte compares.
 template <bool kLds, typename P>
 __device__ void scan_contains(WaveLds& L, P w, uint32_t wlen, int nr, const uint8_t* needle, uint32_t m, bool upper,
                               bool mark_nonascii) {
   if (nr == 0) return;
   const uint32_t lo = L.r_vs[0];
   const uint32_t hi = L.r_vs[nr - 1] + L.r_vl[nr - 1];
-  const uint32_t l = lane_id();
-  const uint8_t n0 = m ? needle[0] : 0;
-  const uint32_t N0 = 0x01010101u * n0;
-  const bool alt = upper && n0 >= 'A' && n0 <= 'Z';
-  const uint32_t N1 = 0x01010101u * (uint32_t)(n0 + 32);
-  for (uint32_t c = (lo & ~15u) + l * 16; c < hi; c += 64 * 16) {
-    uint32_t wd[4];
+  const uint32_t l = threadIdx.x;
+  // the needle's first 16 bytes, broadcast, in registers (loaded once)
+  uint32_t nb[16];
+#pragma unroll
+  for (int t = 0; t < 16; t++) nb[t] = (uint32_t)t < m ? 0x01010101u * needle[t] : 0u;
+  for (uint32_t c = (lo & ~15u) + l * 16; c < hi; c += kEvalThreads * 16) {
+    uint32_t wd[8];
     if constexpr (kLds) {
-      const uint4 v = *(const uint4*)(&L.win[c]);
-      wd[0] = v.x;
-      wd[1] = v.y;
-      wd[2] = v.z;
-      wd[3] = v.w;
+      const uint4 v0 = *(const uint4*)(&L.win[c]);
+      const uint4 v1 = *(const uint4*)(&L.win[c + 16]);
+      wd[0] = v0.x; wd[1] = v0.y; wd[2] = v0.z; wd[3] = v0.w;
+      wd[4] = v1.x; wd[5] = v1.y; wd[6] = v1.z; wd[7] = v1.w;
     } else {
-      for (int k = 0; k < 4; k++)
+      for (int k = 0; k < 8; k++)
         wd[k] = (uint32_t)w[c + 4 * k] | ((uint32_t)w[c + 4 * k + 1] << 8) | ((uint32_t)w[c + 4 * k + 2] << 16) |
                 ((uint32_t)w[c + 4 * k + 3] << 24);
     }
-    for (int k = 0; k < 4; k++) {
-      uint32_t x = wd[k];
-      if (mark_nonascii && (x & 0x80808080u)) {
+    if (mark_nonascii && ((wd[0] | wd[1] | wd[2] | wd[3]) & 0x80808080u)) {
+      for (int k = 0; k < 4; k++)
         for (int j = 0; j < 4; j++) {
           uint32_t p = c + 4 * k + j;
-          if (((x >> (8 * j)) & 0x80) && p >= lo && p < hi) {
+          if (((wd[k] >> (8 * j)) & 0x80) && p >= lo && p < hi) {
             int r = find_rec(L, nr, p);
             if (r >= 0 && p < L.r_vs[r] + L.r_vl[r]) atomicOr(&L.r_flags[r], RF_NONASCII);
           }
         }
-      }
-      if (m == 0) continue;
-      uint32_t cand = zbytes(x ^ N0);
-      if (alt) cand |= zbytes(x ^ N1);
+    }
+    if (m == 0) continue;
+    if (upper)
+      for (int k = 0; k < 8; k++) wd[k] = swar_upper(wd[k]);
+    uint32_t acc[4] = {0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u};
+    needle_step<0>(wd, nb, m, acc);
+    needle_step<1>(wd, nb, m, acc);
+    if (!(acc[0] | acc[1] | acc[2] | acc[3])) continue;  // 2-byte prefilter
+    needle_step<2>(wd, nb, m, acc);
+    needle_step<3>(wd, nb, m, acc);
+    needle_step<4>(wd, nb, m, acc);
+    needle_step<5>(wd, nb, m, acc);
+    needle_step<6>(wd, nb, m, acc);
+    needle_step<7>(wd, nb, m, acc);
+    needle_step<8>(wd, nb, m, acc);
+    needle_step<9>(wd, nb, m, acc);
+    needle_step<10>(wd, nb, m, acc);
+    needle_step<11>(wd, nb, m, acc);
+    needle_step<12>(wd, nb, m, acc);
+    needle_step<13>(wd, nb, m, acc);
+    needle_step<14>(wd, nb, m, acc);
+    needle_step<15>(wd, nb, m, acc);
+    for (int k = 0; k < 4; k++) {
+      uint32_t cand = acc[k];
       while (cand) {
-        int j = __builtin_ctz(cand) >> 3;
+        const int j = __builtin_ctz(cand) >> 3;
         cand &= cand - 1;
-        cand &= ~(0x80u << (8 * j));
-        uint32_t p = c + 4 * k + j;
+        const uint32_t p = c + 4 * k + j;
         if (p < lo || p >= hi) continue;
-        int r = find_rec(L, nr, p);
+        const int r = find_rec(L, nr, p);
         if (r < 0) continue;
         const uint32_t ve = L.r_vs[r] + L.r_vl[r];
         if (p + m > ve) continue;
-        if (L.r_flags[r] & RF_MATCH) continue;
         bool ok = true;
-        for (uint32_t t = 1; t < m; t++) {
-          uint8_t y = w[p + t];
+        for (uint32_t t = 16; t < m; t++) {  // needles longer than 16 bytes
+          uint8_t y = kLds ? L.win[p + t] : w[p + t];
           if (upper) y = up(y);
           if (y != needle[t]) {
             ok = false;
@@ -480,8 +650,8 @@ __device__ void scan_regex_bounded(WaveLds& L, P w, int nr, const DfaView& d, ui
   if (nr == 0) return;
   const uint32_t lo = L.r_vs[0];
   const uint32_t hi = L.r_vs[nr - 1] + L.r_vl[nr - 1];
-  const uint32_t l = lane_id();
-  for (uint32_t c0 = (lo & ~15u) + l * 16; c0 < hi; c0 += 64 * 16) {
+  const uint32_t l = threadIdx.x;
+  for (uint32_t c0 = (lo & ~15u) + l * 16; c0 < hi; c0 += kEvalThreads * 16) {
     uint32_t c = c0 < lo ? lo : c0;
     int r = find_rec(L, nr, c);
     if (r < 0) r = 0;
@@ -557,13 +727,13 @@ __device__ bool dfa_run_full(P s, uint32_t n, const uint8_t* blob, const DfaDesc
 // ---------------------------------------------------------------------------
 // evaluate the chain (stages [0, nst)) over the records of one window
 // ---------------------------------------------------------------------------
-template <bool kLds, typename P>
+template <uint32_t kOps, bool kLds, typename P>
 __device__ void eval_window(WaveLds& L, P w, uint32_t wlen, int nr, const ChainDesc& ch, const uint8_t* blob,
-                            int nst, int lds_stage, bool& unsupported) {
-  const uint32_t l = lane_id();
+                            int nst, int lds_stage, bool& unsupported STAMP_PARAMS) {
+  const uint32_t l = threadIdx.x;
   bool nonascii_done = false;
   for (int s = 0; s < nst; s++) {
-    const StageDesc& sd = ch.st[s];
+    const StageDesc sd = ch.st[s];  // by value: one scalar load, no re-reads inside the loops
     const uint8_t op = sd.op;
     const bool src = sd.in_type != VT_I32;
     const bool upper = sd.in_type == VT_SRC_UPPER;
@@ -571,9 +741,10 @@ __device__ void eval_window(WaveLds& L, P w, uint32_t wlen, int nr, const ChainD
     const bool need_utf8 = src && (op == OP_CONTAINS || op == OP_REGEX || op == OP_FILTER_ODD ||
                                    op == OP_MAP_DOUBLE || op == OP_AGG_SUM);
     // ---- data-parallel phase over window bytes
-    for (int r = l; r < nr; r += 64) L.r_flags[r] &= ~RF_MATCH;
+    for (int r = l; r < nr; r += kEvalThreads) L.r_flags[r] &= ~RF_MATCH;
     __syncthreads();
-    if (src && op == OP_CONTAINS) {
+    STAMP(10);
+    if ((kOps & opbit(OP_CONTAINS)) && src && op == OP_CONTAINS) {
       scan_contains<kLds>(L, w, wlen, nr, blob + sd.needle, sd.needle_len, upper, !nonascii_done);
       nonascii_done = true;
     } else if (need_utf8 && !nonascii_done) {
@@ -581,18 +752,19 @@ __device__ void eval_window(WaveLds& L, P w, uint32_t wlen, int nr, const ChainD
       nonascii_done = true;
     }
     DfaView dv;
-    if (op == OP_REGEX) {
+    if ((kOps & opbit(OP_REGEX)) && op == OP_REGEX) {
       const bool in_lds = s == lds_stage;
-      dv.cls = in_lds ? (upper ? L.dfa_clsu : L.dfa_cls) : blob + (upper ? sd.dfa.classmap_up : sd.dfa.classmap);
-      dv.trans = in_lds ? L.dfa_trans : blob + sd.dfa.trans;
-      dv.acc = in_lds ? L.dfa_acc : blob + sd.dfa.accept;
+      dv.cls = in_lds ? (upper ? g_dyn_lds + 256 : g_dyn_lds) : blob + (upper ? sd.dfa.classmap_up : sd.dfa.classmap);
+      dv.trans = in_lds ? g_dyn_lds + 768 : blob + sd.dfa.trans;
+      dv.acc = in_lds ? g_dyn_lds + 512 : blob + sd.dfa.accept;
       dv.ncls = sd.dfa.nclasses;
       if (src && sd.dfa.max_len >= 0)
         scan_regex_bounded(L, w, nr, dv, sd.dfa.s_bot, sd.dfa.s_mid, (uint32_t)sd.dfa.max_len);
     }
     __syncthreads();
-    // ---- per-record phase (lane per record)
-    for (int r = l; r < nr; r += 64) {
+    STAMP(11);
+    // ---- per-record phase (thread per record)
+    for (int r = l; r < nr; r += kEvalThreads) {
       uint32_t f = L.r_flags[r];
       if (!(f & RF_ALIVE)) continue;
       const uint32_t vs = L.r_vs[r], vl = L.r_vl[r];
@@ -608,7 +780,7 @@ __device__ void eval_window(WaveLds& L, P w, uint32_t wlen, int nr, const ChainD
       bool err = false;
       uint8_t ec = 0;
       const int32_t ival_in = L.r_ival[r];
-      if (op == OP_AGG_SUM && sd.acc_bad) {
+      if ((kOps & opbit(OP_AGG_SUM)) && op == OP_AGG_SUM && sd.acc_bad) {
         err = true;
         ec = EC_ACC_UTF8;
         L.r_aux[r] = sd.acc_vut;
@@ -619,6 +791,7 @@ __device__ void eval_window(WaveLds& L, P w, uint32_t wlen, int nr, const ChainD
       } else {
         switch (op) {
           case OP_CONTAINS: {
+            if constexpr (!(kOps & opbit(OP_CONTAINS))) break;
             bool keep;
             if (src) {
               keep = (f & RF_MATCH) || sd.needle_len == 0;
@@ -637,6 +810,7 @@ __device__ void eval_window(WaveLds& L, P w, uint32_t wlen, int nr, const ChainD
             break;
           }
           case OP_REGEX: {
+            if constexpr (!(kOps & opbit(OP_REGEX))) break;
             bool m;
             if (src) {
               if (f & RF_NONASCII) {
@@ -666,6 +840,9 @@ __device__ void eval_window(WaveLds& L, P w, uint32_t wlen, int nr, const ChainD
           case OP_MAP_DOUBLE:
           case OP_FILTER_MAP:
           case OP_AGG_SUM: {
+            if constexpr (!(kOps & (opbit(OP_FILTER_ODD) | opbit(OP_MAP_DOUBLE) | opbit(OP_FILTER_MAP) |
+                                    opbit(OP_AGG_SUM))))
+              break;
             int32_t x = 0;
             int pk = 0;
             if (src) {
@@ -707,26 +884,37 @@ __device__ void eval_window(WaveLds& L, P w, uint32_t wlen, int nr, const ChainD
       L.r_flags[r] = f;
     }
     __syncthreads();
+    STAMP(12);
   }
 }
 
-// stage window bytes [al, al+wlen) into LDS with 16-byte coalesced loads
+// stage window bytes [al, al+wlen) into LDS: 1 KiB LDS-DMA pieces
+// (global_load_lds_dwordx4, one per wave instruction), all issued before one wait
 __device__ __forceinline__ void load_window(WaveLds& L, const uint8_t* slice, uint64_t al, uint32_t wlen) {
   const uint32_t l = lane_id();
-  const uint4* src = (const uint4*)(slice + al);
-  uint4* dst = (uint4*)L.win;
-  const uint32_t n16 = (wlen + 15) / 16;
-  for (uint32_t i = l; i < n16; i += 64) dst[i] = src[i];
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t npieces = (wlen + 1023) / 1024;
+  const uint8_t* src = slice + al + l * 16;
+  for (uint32_t k = wv; k < npieces; k += kEvalThreads / 64)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + k * 1024),
+                                     (__attribute__((address_space(3))) void*)(L.win + k * 1024), 16, 0, 0);
+  __builtin_amdgcn_s_waitcnt(0);  // all counters: the LDS-DMA pieces have landed
   __syncthreads();
 }
 
 // ---------------------------------------------------------------------------
-// k_eval — one 64-lane workgroup per stored batch
+// k_eval — one 256-thread (4-wave) workgroup per stored batch: the window is
+// shared, the scans and per-record work spread over the 4 waves, the serial
+// walk and the ordered emission run on wave 0
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_eval(EvalArgs a) {
+template <uint32_t kOps>
+__global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : 2) void k_eval(EvalArgs a) {
   __shared__ WaveLds L;
+  STAMP_DECL
   const uint32_t b = blockIdx.x;
   const uint32_t l = lane_id();
+  const uint32_t tid = threadIdx.x;
+  const bool wave0 = tid < 64;
   const ChainDesc& ch = *a.chain;
   const uint8_t* S = a.slice;
   const uint64_t pos = a.bpos[b];
@@ -745,12 +933,13 @@ __global__ __launch_bounds__(64) void k_eval(EvalArgs a) {
     const StageDesc& sd = ch.st[s];
     if (sd.op == OP_REGEX && sd.dfa.nstates * sd.dfa.nclasses <= (uint32_t)kDfaLds) {
       lds_stage = s;
-      for (uint32_t i = l; i < 256; i += 64) {
-        L.dfa_cls[i] = a.blob[sd.dfa.classmap + i];
-        L.dfa_clsu[i] = a.blob[sd.dfa.classmap_up + i];
-        L.dfa_acc[i] = i < sd.dfa.nstates ? a.blob[sd.dfa.accept + i] : 0;
+      for (uint32_t i = tid; i < 256; i += kEvalThreads) {
+        g_dyn_lds[i] = a.blob[sd.dfa.classmap + i];
+        g_dyn_lds[256 + i] = a.blob[sd.dfa.classmap_up + i];
+        g_dyn_lds[512 + i] = i < sd.dfa.nstates ? a.blob[sd.dfa.accept + i] : 0;
       }
-      for (uint32_t i = l; i < sd.dfa.nstates * sd.dfa.nclasses; i += 64) L.dfa_trans[i] = a.blob[sd.dfa.trans + i];
+      for (uint32_t i = tid; i < sd.dfa.nstates * sd.dfa.nclasses; i += kEvalThreads)
+        g_dyn_lds[768 + i] = a.blob[sd.dfa.trans + i];
       break;
     }
   }
@@ -784,7 +973,7 @@ __global__ __launch_bounds__(64) void k_eval(EvalArgs a) {
     uint64_t cursor = sec0 + 4;
     uint32_t done_recs = 0;
     const uint32_t rec_cap = phase == 1 ? err_idx : nrec_total;
-    const bool agg_on = ch.has_agg && (phase == 0 || err_stage + 1 == ch.nstages);
+    const bool agg_on = (kOps & opbit(OP_AGG_SUM)) && ch.has_agg && (phase == 0 || err_stage + 1 == ch.nstages);
     const int last = nst - 1;
     const uint8_t out_type = (nst == (int)ch.nstages) ? (uint8_t)ch.out_type : ch.st[nst].in_type;
     while (done_recs < nrec_total && done_recs < (phase == 1 ? rec_cap + 1 : nrec_total)) {
@@ -795,9 +984,17 @@ __global__ __launch_bounds__(64) void k_eval(EvalArgs a) {
       if (wend > sec_end16) wend = sec_end16;
       const uint32_t wlen = (uint32_t)(wend - al);
       __syncthreads();
+      STAMP(0);
       load_window(L, S, al, wlen);
-      if (l == 0) walk_records(L, (const uint8_t*)L.win, al, wlen, sec_end, cursor, nrec_total - done_recs, kMaxR);
-      __syncthreads();
+      STAMP(1);
+      STAMP_COUNT(8, 1);
+      if (!walk_fast(L, (const uint8_t*)L.win, al, wlen, sec_end, cursor, nrec_total - done_recs)) {
+        STAMP_COUNT(9, 1);
+        if (tid == 0)
+          walk_records(L, (const uint8_t*)L.win, al, wlen, sec_end, cursor, nrec_total - done_recs, kMaxR);
+        __syncthreads();
+      }
+      STAMP(2);
       int nr = L.nr;
       const int ws = L.walk_status;
       bool global_mode = false;
@@ -811,7 +1008,7 @@ __global__ __launch_bounds__(64) void k_eval(EvalArgs a) {
         global_mode = true;
         gbase = cursor;
         __syncthreads();
-        if (l == 0) walk_records(L, S + gbase, gbase, (uint32_t)(sec_end - gbase), sec_end, cursor, 1, 1);
+        if (tid == 0) walk_records(L, S + gbase, gbase, (uint32_t)(sec_end - gbase), sec_end, cursor, 1, 1);
         __syncthreads();
         nr = L.nr;
         if (nr == 0) {
@@ -823,13 +1020,15 @@ __global__ __launch_bounds__(64) void k_eval(EvalArgs a) {
       int nr_eval = nr;
       if (phase == 1 && done_recs + (uint32_t)nr > err_idx + 1) nr_eval = (int)(err_idx + 1 - done_recs);
       if (global_mode)
-        eval_window<false>(L, S + gbase, (uint32_t)(sec_end - gbase), nr_eval, ch, a.blob, nst, lds_stage,
-                           unsupported);
+        eval_window<kOps, false>(L, S + gbase, (uint32_t)(sec_end - gbase), nr_eval, ch, a.blob, nst, lds_stage,
+                           unsupported STAMP_ARGS);
       else
-        eval_window<true>(L, (const uint8_t*)L.win, wlen, nr_eval, ch, a.blob, nst, lds_stage, unsupported);
+        eval_window<kOps, true>(L, (const uint8_t*)L.win, wlen, nr_eval, ch, a.blob, nst, lds_stage,
+                          unsupported STAMP_ARGS);
       const uint64_t wbase = global_mode ? gbase : al;
-      // ---- error tracking (phase A) and descriptor emission
-      for (int r0 = 0; r0 < nr_eval; r0 += 64) {
+      STAMP(3);
+      // ---- error tracking (phase A) and descriptor emission: wave 0, in record order
+      for (int r0 = 0; wave0 && r0 < nr_eval; r0 += 64) {
         const int r = r0 + (int)l;
         const bool valid = r < nr_eval;
         const uint32_t gidx = done_recs + (uint32_t)r;
@@ -904,16 +1103,25 @@ __global__ __launch_bounds__(64) void k_eval(EvalArgs a) {
         }
         kcount += (uint32_t)__popcll(bal);
       }
+      if (tid == 0) {
+        L.err_stage_b = err_stage;
+        L.err_idx_b = err_idx;
+      }
+      __syncthreads();
+      err_stage = L.err_stage_b;  // every wave learns the first error (uniform control flow)
+      err_idx = L.err_idx_b;
       done_recs += (uint32_t)nr;
       cursor = ((uint64_t)L.next_cursor_hi << 32) | L.next_cursor_lo;
       (void)last;
+      STAMP(4);
     }
     if (phase == 0 && err_stage == 0xFFFFFFFFu) break;
   }
+  unsupported = __syncthreads_or(unsupported);
   if (!(flags & BF_DECODE) && err_stage != 0xFFFFFFFFu) flags |= (err_code == EC_UNSUP) ? BF_UNSUPPORTED : BF_ERR;
   if (err_stage == 0xFFFFFFFFu || err_stage + 1 == ch.nstages) flags |= BF_LAST_STAGE;
   if (unsupported) flags |= BF_UNSUPPORTED;
-  if (l == 0) {
+  if (tid == 0) {
     BatchStat st;
     st.base_offset = base_offset;
     st.first_ts = first_ts;
@@ -938,6 +1146,8 @@ __global__ __launch_bounds__(64) void k_eval(EvalArgs a) {
       if (flags & BF_ERR) atomicMin(&a.mins->first_err, b);
     }
   }
+  STAMP(5);
+  STAMP_FLUSH();
 }
 
 // ---------------------------------------------------------------------------
@@ -1212,6 +1422,24 @@ __global__ void k_header(const Plan* plan, uint8_t* out) {
 // ---------------------------------------------------------------------------
 
 
+// wave-cooperative byte copy with 8 loads in flight per lane
+__device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint32_t n, bool upc) {
+  const uint32_t l = lane_id();
+  for (uint32_t base = 0; base < n; base += 64 * 8) {
+    uint8_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t i = base + k * 64 + l;
+      v[k] = i < n ? src[i] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t i = base + k * 64 + l;
+      if (i < n) dst[i] = upc ? up(v[k]) : v[k];
+    }
+  }
+}
+
 __global__ __launch_bounds__(64) void k_write(WriteArgs a) {
   const Plan p = *a.plan;
   const int32_t b = p.first + (int32_t)blockIdx.x;
@@ -1277,18 +1505,8 @@ __global__ __launch_bounds__(64) void k_write(WriteArgs a) {
       const uint32_t vs = __shfl(vstart, (int)j, 64);
       const KeptRec& rj = d[k0 + j];
       uint8_t* q = o + pos;
-      if (rj.has_key) {
-        const uint8_t* ksrc = a.slice + rj.kpos;
-        for (uint32_t i = l; i < rj.klen; i += 64) q[ks + i] = ksrc[i];
-      }
-      if (rj.mode == KM_COPY || rj.mode == KM_UPPER) {
-        const uint8_t* vsrc = a.slice + rj.vpos;
-        const bool upc = rj.mode == KM_UPPER;
-        for (uint32_t i = l; i < rj.vlen; i += 64) {
-          uint8_t c = vsrc[i];
-          q[vs + i] = upc ? up(c) : c;
-        }
-      }
+      if (rj.has_key) copy_bytes(q + ks, a.slice + rj.kpos, rj.klen, false);
+      if (rj.mode == KM_COPY || rj.mode == KM_UPPER) copy_bytes(q + vs, a.slice + rj.vpos, rj.vlen, rj.mode == KM_UPPER);
     }
   }
 }
@@ -1451,8 +1669,15 @@ hipError_t upload_crc_tables() {
   return e;
 }
 
-void launch_eval(const EvalArgs& a, hipStream_t s) {
-  if (a.nbatches) hipLaunchKernelGGL(k_eval, dim3(a.nbatches), dim3(64), 0, s, a);
+void launch_eval(const EvalArgs& a, uint32_t ops, hipStream_t s) {
+  if (!a.nbatches) return;
+  const size_t dyn = (ops & opbit(OP_REGEX)) ? kDfaDyn : 0;
+  if ((ops & ~kOpsContains) == 0)
+    hipLaunchKernelGGL(k_eval<kOpsContains>, dim3(a.nbatches), dim3(kEvalThreads), dyn, s, a);
+  else if ((ops & ~kOpsRegex) == 0)
+    hipLaunchKernelGGL(k_eval<kOpsRegex>, dim3(a.nbatches), dim3(kEvalThreads), dyn, s, a);
+  else
+    hipLaunchKernelGGL(k_eval<kOpsAll>, dim3(a.nbatches), dim3(kEvalThreads), dyn, s, a);
 }
 void launch_size(const SizeArgs& a, hipStream_t s) {
   if (a.nbatches) hipLaunchKernelGGL(k_size, dim3((a.nbatches + 3) / 4), dim3(256), 0, s, a);
@@ -1482,3 +1707,14 @@ void launch_crc(const uint8_t* buf, uint64_t off, uint64_t n, uint32_t* parts, u
 }
 
 }  // namespace fsg
+
+#ifdef FSG_STAMPS
+extern "C" int fsg_debug_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fsg::g_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(fsg::g_stamps), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif

@@ -6,7 +6,7 @@
 
 namespace fsg {
 hipError_t upload_crc_tables();
-void launch_eval(const EvalArgs& a, hipStream_t s);
+void launch_eval(const EvalArgs& a, uint32_t ops, hipStream_t s);  // ops: bit per StageOp in the chain
 void launch_size(const SizeArgs& a, hipStream_t s);
 uint32_t scan_tiles(uint32_t n);
 void launch_scan(const ScanRow* rows, ScanRow* pre, ScanRow* tile_sums, ScanRow* grand, uint32_t n, bool cut,

@@ -654,7 +654,9 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   ea.bstat = c->bstat.as<BatchStat>();
   ea.desc = c->kept.as<KeptRec>();
   ea.mins = c->mins.as<Mins>();
-  launch_eval(ea, st);
+  uint32_t ops = 0;
+  for (uint32_t k = 0; k < c->hdesc.nstages; k++) ops |= 1u << c->hdesc.st[k].op;
+  launch_eval(ea, ops, st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[1], st));
   SizeArgs sa{};
