@@ -547,7 +547,7 @@ __device__ __forceinline__ void needle_step(const uint32_t (&w)[8], const uint32
 // matched branch-free in registers (32 bytes loaded with two ds_read_b128),
 // longer needles finish with LDS byte compares.
 template <bool kLds, typename P>
-__device__ void scan_contains(WaveLds& L, P w, uint32_t wlen, int nr, const uint8_t* needle, uint32_t m, bool upper,
+__device__ __forceinline__ void scan_contains(WaveLds& L, P w, uint32_t wlen, int nr, const uint8_t* needle, uint32_t m, bool upper,
                               bool mark_nonascii) {
   if (nr == 0) return;
   const uint32_t lo = L.r_vs[0];
@@ -630,7 +630,7 @@ __device__ void scan_contains(WaveLds& L, P w, uint32_t wlen, int nr, const uint
 // records with an empty value never get a scan hit; an empty needle matches all
 // Data-parallel non-ASCII marking only
 template <bool kLds, typename P>
-__device__ void scan_nonascii(WaveLds& L, P w, uint32_t wlen, int nr) {
+__device__ __forceinline__ void scan_nonascii(WaveLds& L, P w, uint32_t wlen, int nr) {
   scan_contains<kLds>(L, w, wlen, nr, nullptr, 0, false, true);
 }
 
@@ -728,7 +728,7 @@ __device__ bool dfa_run_full(P s, uint32_t n, const uint8_t* blob, const DfaDesc
 // evaluate the chain (stages [0, nst)) over the records of one window
 // ---------------------------------------------------------------------------
 template <uint32_t kOps, bool kLds, typename P>
-__device__ void eval_window(WaveLds& L, P w, uint32_t wlen, int nr, const ChainDesc& ch, const uint8_t* blob,
+__device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int nr, const ChainDesc& ch, const uint8_t* blob,
                             int nst, int lds_stage, bool& unsupported STAMP_PARAMS) {
   const uint32_t l = threadIdx.x;
   bool nonascii_done = false;
@@ -919,7 +919,11 @@ __global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : 2) void 
   const uint8_t* S = a.slice;
   const uint64_t pos = a.bpos[b];
   // ---- batch header (file format, batch.rs:163-180)
-  const uint8_t* h = S + pos;
+  // the first window starts at the batch header: one LDS-DMA burst brings the
+  // header, the record count and (for batches up to ~17 KB) every record
+  const uint64_t al0 = pos & ~15ull;
+  load_window(L, S, al0, kWin);
+  const uint8_t* h = L.win + (pos - al0);
   const int64_t base_offset = (int64_t)rd_be(h, 8);
   const int32_t batch_len = (int32_t)rd_be(h + 8, 4);
   const int32_t lod_in = (int32_t)rd_be(h + 23, 4);
@@ -949,8 +953,9 @@ __global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : 2) void 
   if (sec_len < 4) {
     flags |= BF_DECODE;
   } else {
-    count = (int32_t)rd_be(S + sec0, 4);
+    count = (int32_t)rd_be(L.win + (sec0 - al0), 4);
   }
+  bool first_window = true;  // the window at al0 is already resident
   const uint32_t nrec_total = count > 0 ? (uint32_t)count : 0u;
   const uint64_t rb = a.rbase[b];
   // phase A: full chain; phase B (only if a record error occurred): truncated chain
@@ -978,14 +983,15 @@ __global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : 2) void 
     const uint8_t out_type = (nst == (int)ch.nstages) ? (uint8_t)ch.out_type : ch.st[nst].in_type;
     while (done_recs < nrec_total && done_recs < (phase == 1 ? rec_cap + 1 : nrec_total)) {
       // window [al, al + wlen)
-      const uint64_t al = cursor & ~15ull;
+      const uint64_t al = first_window ? al0 : (cursor & ~15ull);
       uint64_t wend = al + kWin;
       const uint64_t sec_end16 = (sec_end + 15) & ~15ull;
       if (wend > sec_end16) wend = sec_end16;
       const uint32_t wlen = (uint32_t)(wend - al);
       __syncthreads();
       STAMP(0);
-      load_window(L, S, al, wlen);
+      if (!first_window) load_window(L, S, al, wlen);
+      first_window = false;
       STAMP(1);
       STAMP_COUNT(8, 1);
       if (!walk_fast(L, (const uint8_t*)L.win, al, wlen, sec_end, cursor, nrec_total - done_recs)) {
@@ -1138,16 +1144,45 @@ __global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : 2) void 
     st.err_aux2 = err_aux2;
     st.pad = 0;
     st.agg_sum = (ch.has_agg && (err_stage == 0xFFFFFFFFu || err_stage + 1 == ch.nstages)) ? aggsum : 0;
-    a.bstat[b] = st;
-    if (flags & BF_DECODE) atomicMin(&a.mins->first_dec, b);
-    if (flags & BF_UNSUPPORTED) atomicMin(&a.mins->first_unsup, b);
-    if (!(flags & BF_DECODE)) {
-      if (kcount) atomicMin(&a.mins->first_keep, b);
-      if (flags & BF_ERR) atomicMin(&a.mins->first_err, b);
-    }
+    a.bstat[b] = st;  // the cross-batch minima are reduced by k_mins
   }
   STAMP(5);
   STAMP_FLUSH();
+}
+
+// ---------------------------------------------------------------------------
+// k_mins: first surviving / erroring / undecodable / unsupported batch
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_mins(const BatchStat* bstat, uint32_t n, Mins* mins) {
+  __shared__ uint32_t sh[4][4];
+  uint32_t fk = 0xFFFFFFFFu, fe = 0xFFFFFFFFu, fd = 0xFFFFFFFFu, fu = 0xFFFFFFFFu;
+  for (uint32_t b = blockIdx.x * 256 + threadIdx.x; b < n; b += gridDim.x * 256) {
+    const uint32_t f = bstat[b].flags;
+    const uint32_t nk = bstat[b].nkeep;
+    if (f & BF_DECODE) fd = fd < b ? fd : b;
+    if (f & BF_UNSUPPORTED) fu = fu < b ? fu : b;
+    if (!(f & BF_DECODE)) {
+      if (nk) fk = fk < b ? fk : b;
+      if (f & BF_ERR) fe = fe < b ? fe : b;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    uint32_t t;
+    t = __shfl_xor(fk, o, 64); fk = t < fk ? t : fk;
+    t = __shfl_xor(fe, o, 64); fe = t < fe ? t : fe;
+    t = __shfl_xor(fd, o, 64); fd = t < fd ? t : fd;
+    t = __shfl_xor(fu, o, 64); fu = t < fu ? t : fu;
+  }
+  const uint32_t w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[w][0] = fk; sh[w][1] = fe; sh[w][2] = fd; sh[w][3] = fu;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    uint32_t m = sh[0][threadIdx.x];
+    for (int k = 1; k < 4; k++) m = sh[k][threadIdx.x] < m ? sh[k][threadIdx.x] : m;
+    if (m != 0xFFFFFFFFu) atomicMin(&((uint32_t*)mins)[threadIdx.x], m);  // first_keep, first_err, first_dec, first_unsup
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1422,37 +1457,88 @@ __global__ void k_header(const Plan* plan, uint8_t* out) {
 // ---------------------------------------------------------------------------
 
 
-// wave-cooperative byte copy with 8 loads in flight per lane
-__device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint32_t n, bool upc) {
-  const uint32_t l = lane_id();
-  for (uint32_t base = 0; base < n; base += 64 * 8) {
-    uint8_t v[8];
+// 256-thread exclusive scan of a u64 (returns exclusive prefix, *total = sum)
+__device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t* sh4, uint64_t* total) {
+  const uint32_t l = lane_id(), w = threadIdx.x >> 6;
+  const uint64_t incl = wave_incl_scan(v);
+  if (l == 63) sh4[w] = incl;
+  __syncthreads();
+  uint64_t base = 0, tot = 0;
+  for (uint32_t k = 0; k < 4; k++) {
+    const uint64_t x = sh4[k];
+    if (k < w) base += x;
+    tot += x;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + incl - v;
+}
+
+// one 16-byte aligned destination unit of a copy segment (dst offset d0 within
+// `out`, source offset s0 within `slice`, n bytes): built from 5 aligned source
+// dwords with alignbyte; whole units are one dwordx4 store, edge units byte stores
+__device__ __forceinline__ void copy_unit(uint8_t* __restrict__ out, const uint8_t* __restrict__ slice, uint64_t d0,
+                                          uint64_t s0, uint32_t n, uint32_t uu, bool upper) {
+  const uint64_t D = ((d0 >> 4) + uu) << 4;
+  const uint64_t A = s0 + D - d0;  // >= s0 - 15: the value sits >= 61 B into the slice
+  const uint32_t* w = (const uint32_t*)(slice + (A & ~3ull));
+  const uint32_t sh = (uint32_t)(A & 3);
+  uint32_t x[5];
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const uint32_t i = base + k * 64 + l;
-      v[k] = i < n ? src[i] : 0;
-    }
+  for (int k = 0; k < 5; k++) x[k] = w[k];
+  uint32_t v[4];
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const uint32_t i = base + k * 64 + l;
-      if (i < n) dst[i] = upc ? up(v[k]) : v[k];
-    }
+  for (int k = 0; k < 4; k++) {
+    v[k] = __builtin_amdgcn_alignbyte(x[k + 1], x[k], sh);
+    if (upper) v[k] = swar_upper(v[k]);
+  }
+  const uint64_t lo = D > d0 ? D : d0;
+  const uint64_t e = d0 + n, hi = D + 16 < e ? D + 16 : e;
+  if (lo == D && hi == D + 16) {
+    uint4 q;
+    q.x = v[0];
+    q.y = v[1];
+    q.z = v[2];
+    q.w = v[3];
+    *(uint4*)(out + D) = q;
+  } else {
+    const uint32_t jl = (uint32_t)(lo - D), jh = (uint32_t)(hi - D);
+#pragma unroll
+    for (int jj = 0; jj < 16; jj++)
+      if ((uint32_t)jj >= jl && (uint32_t)jj < jh) out[D + jj] = (uint8_t)(v[jj >> 2] >> (8 * (jj & 3)));
   }
 }
 
-__global__ __launch_bounds__(64) void k_write(WriteArgs a) {
+__device__ __forceinline__ uint32_t seg_units(uint64_t d0, uint32_t n) {
+  return n ? (uint32_t)(((d0 + n + 15) >> 4) - (d0 >> 4)) : 0u;
+}
+
+// k_write — one 256-thread workgroup per included batch.  Per chunk of up to 256
+// survivors: sizes -> block scan -> each thread writes its record's varint
+// header, small fields and i32 values; then the key/value payload segments of
+// all records are cut into 16-byte aligned destination units which the threads
+// copy round-robin (adjacent threads store adjacent units).
+constexpr int kWriteThreads = 256;
+__global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
+  __shared__ uint64_t sh4[4];
+  __shared__ uint32_t s_u[kWriteThreads + 1];  // unit prefix of the chunk
+  __shared__ uint64_t s_ks[kWriteThreads], s_vs[kWriteThreads];
+  __shared__ uint64_t s_kd[kWriteThreads], s_vd[kWriteThreads];
+  __shared__ uint32_t s_kl[kWriteThreads], s_vl[kWriteThreads], s_ku[kWriteThreads];
+  __shared__ uint8_t s_up[kWriteThreads];
   const Plan p = *a.plan;
   const int32_t b = p.first + (int32_t)blockIdx.x;
   if (p.first < 0 || b > p.last) return;
-  const uint32_t l = lane_id();
+  const uint32_t tid = threadIdx.x;
   const BatchStat st = a.bstat[b];
   const int64_t rel = a.bstat[p.first].base_offset - st.base_offset;
   const int32_t agg_base = a.agg_pre ? (int32_t)((uint64_t)a.acc0 + (uint64_t)a.agg_pre[b].agg) : 0;
   const KeptRec* d = a.desc + a.rbase[b];
-  uint8_t* o = a.out + 61 + (a.pre[b].rec_bytes - a.pre[p.first].rec_bytes);
+  const uint64_t obase = 61 + (a.pre[b].rec_bytes - a.pre[p.first].rec_bytes);
+  uint8_t* out = a.out;
   uint64_t run = 0;
-  for (uint32_t k0 = 0; k0 < st.nkeep; k0 += 64) {
-    const uint32_t k = k0 + l;
+  for (uint32_t k0 = 0; k0 < st.nkeep; k0 += kWriteThreads) {
+    const uint32_t k = k0 + tid;
     const bool v = k < st.nkeep;
     KeptRec r = {};
     uint32_t sz = 0;
@@ -1460,16 +1546,14 @@ __global__ __launch_bounds__(64) void k_write(WriteArgs a) {
       r = d[k];
       sz = rec_out_size(r, rel, agg_base);
     }
-    const uint64_t incl = wave_incl_scan((uint64_t)sz);
-    const uint64_t my = run + incl - sz;
-    run += __shfl(incl, 63, 64);
-    // each lane writes its record's varint header and small fields
-    uint32_t vstart = 0, vl = 0, kstart = 0;
+    uint64_t tot;
+    const uint64_t my = obase + run + block_excl_scan_u64(sz, sh4, &tot);
+    uint32_t units = 0;
     if (v) {
-      uint8_t* q = o + my;
-      vl = out_vlen(r, agg_base);
-      uint32_t inner = 1 + vsize(r.ts) + vsize(r.od + rel) + 1 +
-                       (r.has_key ? vsize((int64_t)r.klen) + r.klen : 0) + vsize((int64_t)vl) + vl + vsize(r.hdr);
+      uint8_t* q = out + my;
+      const uint32_t vl = out_vlen(r, agg_base);
+      const uint32_t inner = 1 + vsize(r.ts) + vsize(r.od + rel) + 1 +
+                             (r.has_key ? vsize((int64_t)r.klen) + r.klen : 0) + vsize((int64_t)vl) + vl + vsize(r.hdr);
       uint8_t t[16];
       uint32_t n = venc((int64_t)inner, t), w = 0;
       for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
@@ -1479,149 +1563,170 @@ __global__ __launch_bounds__(64) void k_write(WriteArgs a) {
       n = venc(r.od + rel, t);
       for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
       q[w++] = r.has_key ? 1 : 0;
+      uint32_t kl = 0, vc = 0;
       if (r.has_key) {
         n = venc((int64_t)r.klen, t);
         for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
-        kstart = w;
+        s_kd[tid] = my + w;
+        kl = r.klen;
         w += r.klen;
       }
       n = venc((int64_t)vl, t);
       for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
-      vstart = w;
+      s_vd[tid] = my + w;
       if (r.mode == KM_I32 || r.mode == KM_AGG) {
         const int32_t x = r.mode == KM_I32 ? r.ival : (int32_t)((uint32_t)agg_base + (uint32_t)r.ival);
         w += fmt_i32(x, q + w);
       } else {
+        vc = vl;
         w += vl;
       }
       n = venc(r.hdr, t);
       for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
+      const uint32_t ku = kl ? seg_units(s_kd[tid], kl) : 0u;
+      units = ku + (vc ? seg_units(s_vd[tid], vc) : 0u);
+      s_ks[tid] = r.kpos;
+      s_vs[tid] = r.vpos;
+      s_kl[tid] = kl;
+      s_vl[tid] = vc;
+      s_ku[tid] = ku;
+      s_up[tid] = r.mode == KM_UPPER;
     }
-    // cooperative copy of key and value bytes, one record at a time
-    const uint32_t nv = st.nkeep - k0 < 64 ? st.nkeep - k0 : 64;
-    for (uint32_t j = 0; j < nv; j++) {
-      const uint64_t pos = __shfl(my, (int)j, 64);
-      const uint32_t ks = __shfl(kstart, (int)j, 64);
-      const uint32_t vs = __shfl(vstart, (int)j, 64);
-      const KeptRec& rj = d[k0 + j];
-      uint8_t* q = o + pos;
-      if (rj.has_key) copy_bytes(q + ks, a.slice + rj.kpos, rj.klen, false);
-      if (rj.mode == KM_COPY || rj.mode == KM_UPPER) copy_bytes(q + vs, a.slice + rj.vpos, rj.vlen, rj.mode == KM_UPPER);
+    uint64_t utot;
+    const uint64_t uex = block_excl_scan_u64((uint64_t)units, sh4, &utot);
+    s_u[tid] = (uint32_t)uex;
+    if (tid == 0) s_u[kWriteThreads] = (uint32_t)utot;
+    __syncthreads();
+    const int nrec = (int)(st.nkeep - k0 < (uint32_t)kWriteThreads ? st.nkeep - k0 : (uint32_t)kWriteThreads);
+    for (uint32_t g = tid; g < (uint32_t)utot; g += kWriteThreads) {
+      // record owning unit g: last rr with s_u[rr] <= g
+      int lo = 0, hi = nrec - 1, rr = 0;
+      while (lo <= hi) {
+        const int m = (lo + hi) >> 1;
+        if (s_u[m] <= g) {
+          rr = m;
+          lo = m + 1;
+        } else {
+          hi = m - 1;
+        }
+      }
+      const uint32_t u = g - s_u[rr], ku = s_ku[rr];
+      if (u < ku)
+        copy_unit(out, a.slice, s_kd[rr], s_ks[rr], s_kl[rr], u, false);
+      else
+        copy_unit(out, a.slice, s_vd[rr], s_vs[rr], s_vl[rr], u - ku, s_up[rr] != 0);
     }
+    run += tot;
+    __syncthreads();
   }
 }
 
 // ---------------------------------------------------------------------------
 // CRC32C (reflected 0x82F63B78) over [off, off + n): chunked raw CRCs + combine
 // ---------------------------------------------------------------------------
-__constant__ uint32_t c_crc_tab[8][256];
-__constant__ uint32_t c_x2n[32];  // x^(2^k) mod P (zlib x2n_table, Castagnoli)
-
-__device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
-  uint32_t m = 1u << 31, p = 0;
-  for (;;) {
-    if (a & m) {
-      p ^= b;
-      if ((a & (m - 1)) == 0) break;
-    }
-    m >>= 1;
-    b = (b & 1) ? (b >> 1) ^ 0x82F63B78u : b >> 1;
-  }
-  return p;
-}
-// x^(8*len) mod P
-__device__ __forceinline__ uint32_t xpow8(uint64_t len) {
-  uint32_t p = 1u << 31;
-  unsigned k = 3;
-  while (len) {
-    if (len & 1) p = multmodp(c_x2n[k & 31], p);
-    len >>= 1;
-    k++;
-  }
-  return p;
-}
-
+// Tables (built on the host by upload_crc_tables):
+//   g_crc_z16[q][v]   raw CRC of byte v followed by q zero bytes (q = 0..15):
+//                     slice-by-16 of one 16-byte block
+//   g_crc_shift[k]    the linear map "append 2^k zero bytes" (x^(8*2^k) mod P),
+//                     as 4 byte-indexed tables: shift(c) = ^_i T[i][(c >> 8i) & 0xff]
+// The k_crc16 path: raw CRC (init 0) of the 16-byte-aligned region [16, Z) with
+// the bytes before the CRC start masked to zero (leading zeros leave a raw CRC
+// unchanged), every thread's blocks folded with the 4 KiB shift, per-thread
+// partials shifted to the chunk end, chunk CRCs shifted to the region end and
+// XOR-combined (exact: CRC is linear over GF(2)); k_crc_final appends the
+// unaligned tail bytewise and applies the 0xFFFFFFFF init / final xor.
+constexpr int kCrcShiftLevels = 48;
+__device__ uint32_t g_crc_z16[16][256];
+__device__ uint32_t g_crc_shift[kCrcShiftLevels][4][256];
 constexpr int kCrcThreads = 256;
-constexpr int kCrcPerThread = kCrcChunk / kCrcThreads;  // 256 bytes
+constexpr int kCrcIters = 16;                               // blocks per thread per chunk
+constexpr uint32_t kCrcChunkBlocks = kCrcThreads * kCrcIters;  // 4096 x 16 B = 64 KiB
 
-// raw CRC (init 0, no final xor) of each kCrcChunk-byte chunk
-__global__ __launch_bounds__(256) void k_crc_chunks(const uint8_t* buf, uint64_t off, uint64_t n, uint32_t* parts) {
-  __shared__ uint32_t tab[8][256];
-  __shared__ uint32_t sh[kCrcThreads];
-  __shared__ uint32_t shl[kCrcThreads];
-  for (int i = threadIdx.x; i < 8 * 256; i += 256) tab[i >> 8][i & 255] = c_crc_tab[i >> 8][i & 255];
-  __syncthreads();
-  const uint64_t c0 = (uint64_t)blockIdx.x * kCrcChunk;
-  const uint64_t t0 = c0 + (uint64_t)threadIdx.x * kCrcPerThread;
-  uint32_t len = 0;
-  if (t0 < n) len = (uint32_t)((n - t0) < (uint64_t)kCrcPerThread ? (n - t0) : kCrcPerThread);
-  const uint8_t* p = buf + off + t0;
-  uint32_t c = 0;
-  uint32_t i = 0;
-  for (; i + 8 <= len; i += 8) {
-    uint32_t lo = (uint32_t)p[i] | ((uint32_t)p[i + 1] << 8) | ((uint32_t)p[i + 2] << 16) | ((uint32_t)p[i + 3] << 24);
-    uint32_t hi =
-        (uint32_t)p[i + 4] | ((uint32_t)p[i + 5] << 8) | ((uint32_t)p[i + 6] << 16) | ((uint32_t)p[i + 7] << 24);
-    lo ^= c;
-    c = tab[7][lo & 0xff] ^ tab[6][(lo >> 8) & 0xff] ^ tab[5][(lo >> 16) & 0xff] ^ tab[4][lo >> 24] ^
-        tab[3][hi & 0xff] ^ tab[2][(hi >> 8) & 0xff] ^ tab[1][(hi >> 16) & 0xff] ^ tab[0][hi >> 24];
-  }
-  for (; i < len; i++) c = tab[0][(c ^ p[i]) & 0xff] ^ (c >> 8);
-  sh[threadIdx.x] = c;
-  shl[threadIdx.x] = len;
-  __syncthreads();
-  // tree combine: (A, B) -> shift(A, |B|) ^ B
-  for (int s = 1; s < kCrcThreads; s <<= 1) {
-    if ((threadIdx.x % (2 * s)) == 0 && threadIdx.x + s < kCrcThreads) {
-      const uint32_t lb = shl[threadIdx.x + s];
-      uint32_t a = sh[threadIdx.x];
-      if (lb) a = multmodp(xpow8(lb), a);
-      sh[threadIdx.x] = a ^ sh[threadIdx.x + s];
-      shl[threadIdx.x] += lb;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) parts[blockIdx.x] = sh[0];
+__device__ __forceinline__ uint32_t crc_shift_tab(const uint32_t (*T)[256], uint32_t c) {
+  return T[0][c & 0xff] ^ T[1][(c >> 8) & 0xff] ^ T[2][(c >> 16) & 0xff] ^ T[3][c >> 24];
+}
+// append `n` zero bytes to a raw CRC state (global tables, any n < 2^48)
+__device__ __forceinline__ uint32_t crc_shift_bytes(uint32_t c, uint64_t n) {
+  for (int k = 0; n; k++, n >>= 1)
+    if (n & 1) c = crc_shift_tab(g_crc_shift[k], c);
+  return c;
 }
 
-// fold the chunk CRCs in order with init 0xFFFFFFFF, write BE CRC at out[17..21)
-__global__ __launch_bounds__(1024) void k_crc_fold(const uint32_t* parts, uint32_t nparts, uint64_t n, uint8_t* out) {
-  __shared__ uint32_t sh[1024];
-  __shared__ uint64_t shl[1024];
+__global__ __launch_bounds__(kCrcThreads) void k_crc16(const uint8_t* __restrict__ out, uint64_t skip,
+                                                        uint64_t nblocks, uint32_t* acc) {
+  __shared__ uint32_t z[16][256];
+  __shared__ uint32_t sh[9][4][256];  // shifts by 16 B .. 4 KiB (2^4 .. 2^12 bytes)
+  __shared__ uint32_t red[kCrcThreads / 64];
   const uint32_t t = threadIdx.x;
-  const uint32_t per = (nparts + 1023) / 1024;
-  const uint32_t i0 = t * per;
-  uint32_t c = 0;
-  uint64_t len = 0;
-  const uint32_t kfull = xpow8(kCrcChunk);
-  for (uint32_t i = i0; i < i0 + per && i < nparts; i++) {
-    const uint64_t clen = (uint64_t)(i + 1) * kCrcChunk <= n ? (uint64_t)kCrcChunk : n - (uint64_t)i * kCrcChunk;
-    const uint32_t sft = clen == (uint64_t)kCrcChunk ? kfull : xpow8(clen);
-    c = multmodp(sft, c) ^ parts[i];
-    len += clen;
-  }
-  sh[t] = c;
-  shl[t] = len;
+  for (uint32_t i = t; i < 16 * 256; i += kCrcThreads) (&z[0][0])[i] = (&g_crc_z16[0][0])[i];
+  for (uint32_t i = t; i < 9 * 4 * 256; i += kCrcThreads) (&sh[0][0][0])[i] = (&g_crc_shift[4][0][0])[i];
   __syncthreads();
-  for (int s = 1; s < 1024; s <<= 1) {
-    if ((t % (2 * s)) == 0 && t + s < 1024) {
-      const uint64_t lb = shl[t + s];
-      uint32_t a = sh[t];
-      if (lb) a = multmodp(xpow8(lb), a);
-      sh[t] = a ^ sh[t + s];
-      shl[t] += lb;
+  const uint4* base = (const uint4*)(out + 16);
+  const uint64_t nchunks = (nblocks + kCrcChunkBlocks - 1) / kCrcChunkBlocks;
+  for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const uint64_t b0 = ch * kCrcChunkBlocks;
+    const uint32_t nb = (uint32_t)(nblocks - b0 < kCrcChunkBlocks ? nblocks - b0 : kCrcChunkBlocks);
+    uint4 v[kCrcIters];
+#pragma unroll
+    for (int i = 0; i < kCrcIters; i++) {
+      const uint32_t j = t + (uint32_t)i * kCrcThreads;
+      if (j < nb) v[i] = base[b0 + j];
+    }
+    if (b0 == 0 && t == 0) {  // bytes [16, 16 + skip) precede the CRC region
+      uint32_t w[4] = {v[0].x, v[0].y, v[0].z, v[0].w};
+#pragma unroll
+      for (int q = 0; q < 16; q++)
+        if ((uint64_t)q < skip) w[q >> 2] &= ~(0xffu << (8 * (q & 3)));
+      v[0].x = w[0];
+      v[0].y = w[1];
+      v[0].z = w[2];
+      v[0].w = w[3];
+    }
+    uint32_t c = 0;
+    int last = -1;
+#pragma unroll
+    for (int i = 0; i < kCrcIters; i++) {
+      const uint32_t j = t + (uint32_t)i * kCrcThreads;
+      if (j < nb) {
+        const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+        uint32_t r = 0;
+#pragma unroll
+        for (int q = 0; q < 16; q++) r ^= z[15 - q][(w[q >> 2] >> (8 * (q & 3))) & 0xff];
+        c = crc_shift_tab(sh[8], c) ^ r;  // previous blocks move 4 KiB further from the end
+        last = i;
+      }
+    }
+    // shift to the chunk end: (nb - 1 - j_last) blocks of 16 B
+    if (last >= 0) {
+      uint32_t d = nb - 1 - (t + (uint32_t)last * kCrcThreads);
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        if ((d >> k) & 1) c = crc_shift_tab(sh[k], c);
+    }
+    // workgroup XOR reduce
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c ^= __shfl_xor(c, o, 64);
+    if ((t & 63) == 0) red[t >> 6] = c;
+    __syncthreads();
+    if (t == 0) {
+      uint32_t x = red[0] ^ red[1] ^ red[2] ^ red[3];
+      x = crc_shift_bytes(x, (nblocks - b0 - nb) * 16ull);  // to the end of the aligned region
+      atomicXor(acc, x);
     }
     __syncthreads();
   }
-  if (t == 0) {
-    // register init 0xFFFFFFFF contributes shift(0xFFFFFFFF, n); final xor
-    uint32_t crc = sh[0] ^ multmodp(xpow8(n), 0xFFFFFFFFu);
-    crc ^= 0xFFFFFFFFu;
-    out[17] = (uint8_t)(crc >> 24);
-    out[18] = (uint8_t)(crc >> 16);
-    out[19] = (uint8_t)(crc >> 8);
-    out[20] = (uint8_t)crc;
-  }
+}
+
+// tail bytes [tail0, end) bytewise, init/xorout, big-endian CRC at out[17..21)
+__global__ void k_crc_final(uint8_t* out, const uint32_t* acc, uint64_t tail0, uint64_t end, uint64_t n) {
+  if (threadIdx.x != 0) return;
+  uint32_t c = *acc;
+  for (uint64_t i = tail0; i < end; i++) c = g_crc_z16[0][(c ^ out[i]) & 0xff] ^ (c >> 8);
+  uint32_t crc = c ^ crc_shift_bytes(0xFFFFFFFFu, n) ^ 0xFFFFFFFFu;
+  out[17] = (uint8_t)(crc >> 24);
+  out[18] = (uint8_t)(crc >> 16);
+  out[19] = (uint8_t)(crc >> 8);
+  out[20] = (uint8_t)crc;
 }
 
 // ---------------------------------------------------------------------------
@@ -1637,16 +1742,15 @@ static bool g_tabs_ready = false;
 
 hipError_t upload_crc_tables() {
   if (g_tabs_ready) return hipSuccess;
-  static uint32_t tab[8][256];
+  static uint32_t z16[16][256];
   for (uint32_t i = 0; i < 256; i++) {
     uint32_t c = i;
     for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : c >> 1;
-    tab[0][i] = c;
+    z16[0][i] = c;
   }
-  for (int t = 1; t < 8; t++)
-    for (uint32_t i = 0; i < 256; i++) tab[t][i] = (tab[t - 1][i] >> 8) ^ tab[0][tab[t - 1][i] & 0xff];
-  uint32_t x2n[32];
-  // host multmodp
+  for (int t = 1; t < 16; t++)
+    for (uint32_t i = 0; i < 256; i++) z16[t][i] = (z16[t - 1][i] >> 8) ^ z16[0][z16[t - 1][i] & 0xff];
+  // GF(2) multiply mod P (reflected)
   auto mm = [](uint32_t a, uint32_t b) {
     uint32_t m = 1u << 31, p = 0;
     for (;;) {
@@ -1659,12 +1763,19 @@ hipError_t upload_crc_tables() {
     }
     return p;
   };
-  uint32_t p = 1u << 30;  // x^1
-  x2n[0] = p;
-  for (int n = 1; n < 32; n++) x2n[n] = p = mm(p, p);
-  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_crc_tab), tab, sizeof tab);
+  // X[k] = x^(8 * 2^k) mod P by repeated squaring (x^(2^32) != x for this P,
+  // so no exponent wrap-around is assumed)
+  static uint32_t shift[kCrcShiftLevels][4][256];
+  uint32_t X = 1u << 30;  // x^1
+  for (int i = 0; i < 3; i++) X = mm(X, X);  // x^8
+  for (int k = 0; k < kCrcShiftLevels; k++) {
+    for (int b = 0; b < 4; b++)
+      for (uint32_t v = 0; v < 256; v++) shift[k][b][v] = mm(X, v << (8 * b));
+    X = mm(X, X);
+  }
+  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_crc_z16), z16, sizeof z16);
   if (e != hipSuccess) return e;
-  e = hipMemcpyToSymbol(HIP_SYMBOL(c_x2n), x2n, sizeof x2n);
+  e = hipMemcpyToSymbol(HIP_SYMBOL(g_crc_shift), shift, sizeof shift);
   if (e == hipSuccess) g_tabs_ready = true;
   return e;
 }
@@ -1678,6 +1789,12 @@ void launch_eval(const EvalArgs& a, uint32_t ops, hipStream_t s) {
     hipLaunchKernelGGL(k_eval<kOpsRegex>, dim3(a.nbatches), dim3(kEvalThreads), dyn, s, a);
   else
     hipLaunchKernelGGL(k_eval<kOpsAll>, dim3(a.nbatches), dim3(kEvalThreads), dyn, s, a);
+}
+void launch_mins(const BatchStat* bstat, uint32_t n, Mins* mins, hipStream_t s) {
+  if (!n) return;
+  uint32_t g = (n + 255) / 256;
+  if (g > 1024) g = 1024;
+  hipLaunchKernelGGL(k_mins, dim3(g), dim3(256), 0, s, bstat, n, mins);
 }
 void launch_size(const SizeArgs& a, hipStream_t s) {
   if (a.nbatches) hipLaunchKernelGGL(k_size, dim3((a.nbatches + 3) / 4), dim3(256), 0, s, a);
@@ -1697,13 +1814,20 @@ void launch_header(const Plan* plan, uint8_t* out, hipStream_t s) {
   hipLaunchKernelGGL(k_header, dim3(1), dim3(64), 0, s, plan, out);
 }
 void launch_write(const WriteArgs& a, uint32_t nblocks, hipStream_t s) {
-  if (nblocks) hipLaunchKernelGGL(k_write, dim3(nblocks), dim3(64), 0, s, a);
+  if (nblocks) hipLaunchKernelGGL(k_write, dim3(nblocks), dim3(kWriteThreads), 0, s, a);
 }
-uint32_t crc_parts(uint64_t n) { return (uint32_t)((n + kCrcChunk - 1) / kCrcChunk); }
-void launch_crc(const uint8_t* buf, uint64_t off, uint64_t n, uint32_t* parts, uint8_t* out, hipStream_t s) {
-  const uint32_t np = crc_parts(n);
-  if (np) hipLaunchKernelGGL(k_crc_chunks, dim3(np), dim3(kCrcThreads), 0, s, buf, off, n, parts);
-  hipLaunchKernelGGL(k_crc_fold, dim3(1), dim3(1024), 0, s, parts, np, n, out);
+// CRC32C of out[off, off + n) into out[17..21); `acc` is one u32 of scratch
+void launch_crc(uint8_t* out, uint64_t off, uint64_t n, uint32_t* acc, hipStream_t s) {
+  const uint64_t end = off + n;
+  const uint64_t zend = end & ~15ull;  // aligned blocks [16, zend); off >= 16
+  const uint64_t nblocks = zend > 16 ? (zend - 16) / 16 : 0;
+  (void)hipMemsetAsync(acc, 0, sizeof(uint32_t), s);
+  if (nblocks) {
+    const uint64_t nchunks = (nblocks + kCrcChunkBlocks - 1) / kCrcChunkBlocks;
+    const uint32_t grid = (uint32_t)(nchunks < 512 ? nchunks : 512);
+    hipLaunchKernelGGL(k_crc16, dim3(grid), dim3(kCrcThreads), 0, s, (const uint8_t*)out, off - 16, nblocks, acc);
+  }
+  hipLaunchKernelGGL(k_crc_final, dim3(1), dim3(64), 0, s, out, (const uint32_t*)acc, nblocks ? zend : off, end, n);
 }
 
 }  // namespace fsg

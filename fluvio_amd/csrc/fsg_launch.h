@@ -7,6 +7,7 @@
 namespace fsg {
 hipError_t upload_crc_tables();
 void launch_eval(const EvalArgs& a, uint32_t ops, hipStream_t s);  // ops: bit per StageOp in the chain
+void launch_mins(const BatchStat* bstat, uint32_t n, Mins* mins, hipStream_t s);
 void launch_size(const SizeArgs& a, hipStream_t s);
 uint32_t scan_tiles(uint32_t n);
 void launch_scan(const ScanRow* rows, ScanRow* pre, ScanRow* tile_sums, ScanRow* grand, uint32_t n, bool cut,
@@ -14,6 +15,5 @@ void launch_scan(const ScanRow* rows, ScanRow* pre, ScanRow* tile_sums, ScanRow*
 void launch_plan(const PlanArgs& a, hipStream_t s);
 void launch_header(const Plan* plan, uint8_t* out, hipStream_t s);
 void launch_write(const WriteArgs& a, uint32_t nblocks, hipStream_t s);
-uint32_t crc_parts(uint64_t n);
-void launch_crc(const uint8_t* buf, uint64_t off, uint64_t n, uint32_t* parts, uint8_t* out, hipStream_t s);
+void launch_crc(uint8_t* out, uint64_t off, uint64_t n, uint32_t* acc, hipStream_t s);
 }  // namespace fsg

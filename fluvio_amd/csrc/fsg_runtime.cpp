@@ -659,6 +659,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   launch_eval(ea, ops, st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[1], st));
+  launch_mins(ea.bstat, nb, ea.mins, st);
   SizeArgs sa{};
   sa.bstat = ea.bstat;
   sa.desc = ea.desc;
@@ -709,7 +710,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   // output batch: 61-byte header + records
   const size_t out_len = 61 + p.rec_bytes;
   HIPCHK(c->out.ensure(out_len + 64));
-  HIPCHK(c->crcparts.ensure((crc_parts(out_len) + 1) * sizeof(uint32_t)));
+  HIPCHK(c->crcparts.ensure(sizeof(uint32_t)));
   WriteArgs wa{};
   wa.slice = ea.slice;
   wa.bstat = ea.bstat;
@@ -725,7 +726,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   launch_write(wa, p.last >= p.first && p.first >= 0 ? (uint32_t)(p.last - p.first + 1) : 0u, st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[4], st));
-  launch_crc(wa.out, 21, out_len - 21, c->crcparts.as<uint32_t>(), wa.out, st);
+  launch_crc(wa.out, 21, out_len - 21, c->crcparts.as<uint32_t>(), st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[5], st));
   HIPCHK(hipStreamSynchronize(st));

@@ -303,3 +303,18 @@ def test_resident_slice_matches_process_batch(engine):
     assert a.raw == o["bytes"]
     t = ch.last_timings()
     assert t["eval_ms"] > 0 and t["out_bytes"] == len(a.raw)
+
+
+def test_large_output_crc(engine):
+    """An output batch above 512 MiB: the CRC combine shifts by more than 2^32
+    bits (x^(2^32) != x mod the Castagnoli polynomial, so no exponent wrap is
+    allowed).  Checked byte-for-byte against the oracle and by recomputing the
+    CRC32C of the returned batch."""
+    sl = synth.make_slice_array(2, 640_000)  # ~650 MB in, all records kept by `map`
+    rs = ResidentSlice(engine, sl)
+    ch = gpu_chain(engine, CHAINS["map"])
+    out = ch.process_slice(rs).raw
+    assert len(out) > (512 << 20)
+    assert struct.unpack(">I", out[17:21])[0] == O.crc32c(out[21:])
+    o = orc_chain(CHAINS["map"]).process_batch(sl.tobytes())
+    assert out == o["bytes"]
