@@ -28,6 +28,8 @@ WORKLOADS = {
                  "regex-filter \\d{3}-\\d{2}-\\d{4} on 256 B records"),
     "c3-filter-map": (2, [("filter_init", {"key": "timeout"}, None), ("map", {}, None)], 4_000_000,
                       "filter -> map (uppercase) chain with compaction, re-encode, CRC32C"),
+    "c2-json": (2, [("filter_json", {}, None)], 4_000_000,
+                "JSON-field filter (filter_json: serde_json StructuredLog, keep level > debug) on 1 KB JSON records"),
 }
 
 

@@ -31,6 +31,7 @@ enum StageOp : uint8_t {
   OP_MAP_DOUBLE = 4,   // map_double: from_utf8 + parse::<i32> * 2
   OP_FILTER_MAP = 5,   // filter_map: from_utf8_lossy + parse::<i32>, even -> /2
   OP_AGG_SUM = 6,      // aggregate-sum (last stage only)
+  OP_FILTER_JSON = 7,  // filter_json: serde_json::from_slice::<StructuredLog>, keep level > Debug
 };
 
 // value representation entering a stage (static per chain position)
@@ -43,6 +44,8 @@ enum ErrCode : uint32_t {
   EC_PARSE = 2,       // aux = ParseIntError kind (1 Empty, 2 InvalidDigit, 3 PosOverflow, 4 NegOverflow)
   EC_ACC_UTF8 = 3,    // aggregate accumulator is not UTF-8 (aux/aux2 as EC_UTF8)
   EC_UNSUP = 4,       // the record needs a feature the GPU path lacks (reached in stream order)
+  EC_JSON = 5,        // serde_json error: bits 8..15 JsonErr, 16..23 sub; aux = reader index,
+                      // aux2 / aux3 = span (fsg_json_dev.h)
 };
 
 struct DfaDesc {
@@ -112,7 +115,7 @@ struct BatchStat {
   int32_t err_ival;    // VT_I32 value entering the failing stage
   uint32_t err_aux;
   uint32_t err_aux2;
-  uint32_t pad;
+  uint32_t err_aux3;
   int64_t agg_sum;     // wrapping i32 sum of the aggregate inputs of this batch
 };
 

@@ -1,0 +1,796 @@
+// Device restatement of serde_json 1.0.96 `from_slice::<StructuredLog>` — the
+// filter of smartmodule/examples/filter_json/src/lib.rs:54-70 (LogLevel enum
+// debug < info < warn < error, rename_all lowercase; `message: String`; other
+// keys ignored).  One thread parses one record value.
+//
+// The routine structure follows serde_json (deserialize_struct, MapAccess,
+// SeqAccess, deserialize_enum, deserialize_str, peek_invalid_type,
+// ignore_value, SliceRead::parse_str / ignore_str) because the error position
+// ("at line L column C") depends on which routine detects an error and how far
+// the reader has advanced at that moment.  Strings are scanned four bytes per
+// step while they hold no '"', '\\', control byte or non-ASCII byte.
+//
+// Output: JRes {ok, level} or an error descriptor {code, sub, pos, a, b}; the
+// host renders the Display text from it (fsg_runtime.cpp json_hint).
+#pragma once
+#include <cstdint>
+
+namespace fsg {
+
+// serde_json ErrorCode (syntax errors carry a reader position)
+enum JsonErr : uint8_t {
+  JE_NONE = 0,
+  JE_EOF_LIST, JE_EOF_OBJECT, JE_EOF_STRING, JE_EOF_VALUE, JE_COLON, JE_LIST_COMMA, JE_OBJ_COMMA, JE_IDENT,
+  JE_VALUE, JE_ESCAPE, JE_NUMBER, JE_CODEPOINT, JE_CONTROL, JE_KEY, JE_SURROGATE, JE_TRAILING_COMMA,
+  JE_TRAILING, JE_HEX_END, JE_RECURSION,
+  // serde custom errors (position fixed by serde_json's fix_position)
+  JE_DUP_FIELD,        // a = field index
+  JE_MISSING_FIELD,    // a = field index
+  JE_INVALID_LENGTH,   // a = elements seen
+  JE_UNKNOWN_VARIANT,  // [a, b) = raw string content (between the quotes)
+  JE_INVALID_TYPE,     // sub = unexpected kind | expected kind << 4; a, b = span (number digits / string)
+  JE_DEEP,             // ignored value nested deeper than the device frame stack (outside the restatement)
+};
+enum JsonUnexp : uint8_t { JU_UNIT = 0, JU_TRUE, JU_FALSE, JU_UINT, JU_NINT, JU_FLOAT, JU_STR, JU_SEQ, JU_MAP };
+enum JsonExp : uint8_t { JX_STRUCT = 0, JX_STRING, JX_VARIANT, JX_UNIT };
+
+struct JRes {
+  uint8_t ok;
+  uint8_t level;
+  uint8_t code;
+  uint8_t sub;
+  uint32_t pos;  // reader index the position is computed from
+  uint32_t a, b;
+};
+
+constexpr uint32_t kJsonFrames = 64;  // ignore_value frame stack: one u64 ('[' = 1, '{' = 0)
+
+template <typename P>
+struct JsonDev {
+  P s;
+  uint32_t n;
+  uint32_t i;
+  bool upper;  // the stage input is the ASCII-uppercased value (a `map` ran before)
+  int depth;
+  bool failed;
+  bool has_pos;
+  JRes r;
+
+  __device__ __forceinline__ int at(uint32_t k) const {
+    uint8_t c = s[k];
+    if (upper && c >= 'a' && c <= 'z') c -= 32;
+    return c;
+  }
+  __device__ __forceinline__ int peek() const { return i < n ? at(i) : -1; }
+  __device__ __forceinline__ void eat() { i++; }
+  __device__ __forceinline__ int next() { return i < n ? at(i++) : -1; }
+
+  __device__ __forceinline__ int fail_at(uint32_t idx, uint8_t code) {
+    failed = true;
+    has_pos = true;
+    r.code = code;
+    r.pos = idx;
+    return -1;
+  }
+  __device__ __forceinline__ int error(uint8_t code) { return fail_at(i, code); }
+  __device__ __forceinline__ int peek_error(uint8_t code) { return fail_at(i + 1 < n ? i + 1 : n, code); }
+  __device__ __forceinline__ int custom(uint8_t code, uint32_t a, uint32_t b, uint8_t sub) {
+    failed = true;
+    has_pos = false;
+    r.code = code;
+    r.a = a;
+    r.b = b;
+    r.sub = sub;
+    return -1;
+  }
+  __device__ __forceinline__ void fix_position() {
+    if (failed && !has_pos) {
+      has_pos = true;
+      r.pos = i;
+    }
+  }
+
+  __device__ __forceinline__ int ws() {
+    for (;;) {
+      const int c = peek();
+      if (c == ' ' || c == '\n' || c == '\t' || c == '\r')
+        eat();
+      else
+        return c;
+    }
+  }
+  __device__ __forceinline__ int ident(const char* id, int len) {
+    for (int k = 0; k < len; k++) {
+      const int c = next();
+      if (c < 0) return error(JE_EOF_VALUE);
+      if (c != id[k]) return error(JE_IDENT);
+    }
+    return 0;
+  }
+
+  // ---- strings
+  static __device__ __forceinline__ bool esc(int c) { return c == '"' || c == '\\' || (c >= 0 && c < 0x20); }
+  static __device__ __forceinline__ int hexv(int c) {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+  }
+  __device__ __forceinline__ int hex4(uint32_t* out) {
+    if (i + 4 > n) {
+      i = n;
+      return error(JE_EOF_STRING);
+    }
+    uint32_t v = 0;
+    for (int k = 0; k < 4; k++) {
+      const int h = hexv(at(i));
+      i++;
+      if (h < 0) return error(JE_ESCAPE);
+      v = (v << 4) + (uint32_t)h;
+    }
+    *out = v;
+    return 0;
+  }
+  // skip a run of plain bytes: 4 at a time while no escape/control/quote and
+  // (when `ascii`) no byte >= 0x80; returns with i at the first byte that needs
+  // individual treatment (or n)
+  __device__ __forceinline__ void skip_plain(bool ascii) {
+    while (i + 4 <= n) {
+      const uint32_t w = (uint32_t)at(i) | ((uint32_t)at(i + 1) << 8) | ((uint32_t)at(i + 2) << 16) |
+                         ((uint32_t)at(i + 3) << 24);
+      // bytes == '"' (0x22), '\\' (0x5C), < 0x20, or >= 0x80 (when ascii)
+      const uint32_t q = w ^ 0x22222222u, bs = w ^ 0x5C5C5C5Cu;
+      const uint32_t zq = (q - 0x01010101u) & ~q, zb = (bs - 0x01010101u) & ~bs;
+      const uint32_t ctl = (w - 0x20202020u) & ~w;
+      uint32_t hit = (zq | zb | ctl) & 0x80808080u;
+      if (ascii) hit |= w & 0x80808080u;
+      if (hit) break;
+      i += 4;
+    }
+  }
+
+  // incremental UTF-8 validation of decoded string bytes
+  struct U8 {
+    uint8_t need, lo, hi;
+    bool bad;
+  };
+  static __device__ __forceinline__ void u8_feed(U8& u, uint32_t c) {
+    if (u.bad) return;
+    if (u.need) {
+      if (c < u.lo || c > u.hi) {
+        u.bad = true;
+        return;
+      }
+      u.need--;
+      u.lo = 0x80;
+      u.hi = 0xBF;
+      return;
+    }
+    if (c < 0x80) return;
+    u.lo = 0x80;
+    u.hi = 0xBF;
+    if (c >= 0xC2 && c <= 0xDF) {
+      u.need = 1;
+    } else if (c >= 0xE0 && c <= 0xEF) {
+      u.need = 2;
+      if (c == 0xE0) u.lo = 0xA0;
+      if (c == 0xED) u.hi = 0x9F;
+    } else if (c >= 0xF0 && c <= 0xF4) {
+      u.need = 3;
+      if (c == 0xF0) u.lo = 0x90;
+      if (c == 0xF4) u.hi = 0x8F;
+    } else {
+      u.bad = true;
+    }
+  }
+  // candidate-string matcher over the decoded bytes (keys / enum variants):
+  // up to 4 candidates of <= 8 bytes packed little-endian in u64 registers
+  struct Match {
+    uint64_t c[4];
+    uint32_t l[4];
+    uint32_t alive;  // bit per candidate
+    uint32_t len;    // decoded length so far
+  };
+  static __device__ __forceinline__ void m_feed(Match& m, uint32_t c) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const bool ok = m.len < m.l[k] && ((m.c[k] >> (8 * (m.len & 7))) & 0xFF) == c;
+      if (!ok) m.alive &= ~(1u << k);
+    }
+    m.len++;
+  }
+  __device__ __forceinline__ int m_hit(const Match& m) const {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (((m.alive >> k) & 1) && m.l[k] == m.len) return k;
+    return -1;
+  }
+  static __device__ __forceinline__ void feed(U8& u, Match* m, uint32_t c) {
+    u8_feed(u, c);
+    if (m) m_feed(*m, c);
+  }
+  static __device__ __forceinline__ void feed_cp(U8& u, Match* m, uint32_t c) {
+    if (c < 0x80) {
+      feed(u, m, c);
+    } else if (c < 0x800) {
+      feed(u, m, 0xC0 | (c >> 6));
+      feed(u, m, 0x80 | (c & 0x3F));
+    } else if (c < 0x10000) {
+      feed(u, m, 0xE0 | (c >> 12));
+      feed(u, m, 0x80 | ((c >> 6) & 0x3F));
+      feed(u, m, 0x80 | (c & 0x3F));
+    } else {
+      feed(u, m, 0xF0 | (c >> 18));
+      feed(u, m, 0x80 | ((c >> 12) & 0x3F));
+      feed(u, m, 0x80 | ((c >> 6) & 0x3F));
+      feed(u, m, 0x80 | (c & 0x3F));
+    }
+  }
+  // read.rs parse_escape (validate = true)
+  __device__ __forceinline__ int escape(U8& u, Match* m) {
+    const int ch = next();
+    if (ch < 0) return error(JE_EOF_STRING);
+    switch (ch) {
+      case '"': feed(u, m, '"'); return 0;
+      case '\\': feed(u, m, '\\'); return 0;
+      case '/': feed(u, m, '/'); return 0;
+      case 'b': feed(u, m, 0x08); return 0;
+      case 'f': feed(u, m, 0x0c); return 0;
+      case 'n': feed(u, m, '\n'); return 0;
+      case 'r': feed(u, m, '\r'); return 0;
+      case 't': feed(u, m, '\t'); return 0;
+      case 'u': {
+        uint32_t n1;
+        if (hex4(&n1)) return -1;
+        if (n1 >= 0xDC00 && n1 <= 0xDFFF) return error(JE_SURROGATE);
+        if (n1 >= 0xD800 && n1 <= 0xDBFF) {
+          int p = peek();
+          if (p < 0) return error(JE_EOF_STRING);
+          if (p != '\\') {
+            eat();
+            return error(JE_HEX_END);
+          }
+          eat();
+          p = peek();
+          if (p < 0) return error(JE_EOF_STRING);
+          if (p != 'u') {
+            eat();
+            return error(JE_HEX_END);
+          }
+          eat();
+          uint32_t n2;
+          if (hex4(&n2)) return -1;
+          if (n2 < 0xDC00 || n2 > 0xDFFF) return error(JE_SURROGATE);
+          feed_cp(u, m, (((n1 - 0xD800) << 10) | (n2 - 0xDC00)) + 0x10000);
+          return 0;
+        }
+        feed_cp(u, m, n1);
+        return 0;
+      }
+      default: return error(JE_ESCAPE);
+    }
+  }
+  // SliceRead::parse_str after the opening quote; [*b0, *b1) = raw content span
+  __device__ __forceinline__ int parse_str(Match* m, uint32_t* b0, uint32_t* b1) {
+    U8 u = {0, 0x80, 0xBF, false};
+    *b0 = i;
+    for (;;) {
+      if (!m || !m->alive) skip_plain(true);
+      if (i >= n) return error(JE_EOF_STRING);
+      const int c = at(i);
+      if (c == '"') {
+        *b1 = i;
+        i++;
+        if (u.bad || u.need) return error(JE_CODEPOINT);
+        return 0;
+      } else if (c == '\\') {
+        i++;
+        if (escape(u, m)) return -1;
+      } else if (c < 0x20) {
+        i++;
+        return error(JE_CONTROL);
+      } else {
+        i++;
+        feed(u, m, (uint32_t)c);
+      }
+    }
+  }
+  __device__ __forceinline__ int ignore_escape() {
+    const int ch = next();
+    if (ch < 0) return error(JE_EOF_STRING);
+    switch (ch) {
+      case '"': case '\\': case '/': case 'b': case 'f': case 'n': case 'r': case 't': return 0;
+      case 'u': {
+        uint32_t v;
+        return hex4(&v);
+      }
+      default: return error(JE_ESCAPE);
+    }
+  }
+  __device__ __forceinline__ int ignore_str() {
+    for (;;) {
+      skip_plain(false);
+      if (i >= n) return error(JE_EOF_STRING);
+      const int c = at(i);
+      if (c == '"') {
+        i++;
+        return 0;
+      } else if (c == '\\') {
+        i++;
+        if (ignore_escape()) return -1;
+      } else if (c < 0x20) {
+        return error(JE_CONTROL);
+      } else {
+        i++;
+      }
+    }
+  }
+
+  // ---- numbers
+  __device__ __forceinline__ int pnull() const { const int c = peek(); return c < 0 ? 0 : c; }
+  static __device__ __forceinline__ bool dig(int c) { return c >= '0' && c <= '9'; }
+  __device__ __forceinline__ int ignore_exponent() {
+    eat();
+    const int c = pnull();
+    if (c == '+' || c == '-') eat();
+    if (!dig(next())) return error(JE_NUMBER);
+    while (dig(pnull())) eat();
+    return 0;
+  }
+  __device__ __forceinline__ int ignore_decimal() {
+    eat();
+    bool any = false;
+    while (dig(pnull())) {
+      eat();
+      any = true;
+    }
+    if (!any) return peek_error(JE_NUMBER);
+    const int c = pnull();
+    if (c == 'e' || c == 'E') return ignore_exponent();
+    return 0;
+  }
+  __device__ __forceinline__ int ignore_integer() {
+    const int c = next();
+    if (c == '0') {
+      if (dig(pnull())) return peek_error(JE_NUMBER);
+    } else if (c >= '1' && c <= '9') {
+      while (dig(pnull())) eat();
+    } else {
+      return error(JE_NUMBER);
+    }
+    const int d = pnull();
+    if (d == '.') return ignore_decimal();
+    if (d == 'e' || d == 'E') return ignore_exponent();
+    return 0;
+  }
+  __device__ __forceinline__ int exponent_syn() {
+    eat();
+    const int c = pnull();
+    if (c == '+' || c == '-') eat();
+    const int nx = next();
+    if (nx < 0) return error(JE_EOF_VALUE);
+    if (!dig(nx)) return error(JE_NUMBER);
+    while (dig(pnull())) eat();
+    return 0;
+  }
+  __device__ __forceinline__ int decimal_syn() {
+    eat();
+    bool any = false;
+    while (dig(pnull())) {
+      eat();
+      any = true;
+    }
+    if (!any) return peek() >= 0 ? peek_error(JE_NUMBER) : peek_error(JE_EOF_VALUE);
+    const int c = pnull();
+    if (c == 'e' || c == 'E') return exponent_syn();
+    return 0;
+  }
+  // parse_integer + parse_number syntax; *kind = JU_UINT / JU_NINT / JU_FLOAT
+  __device__ __forceinline__ int parse_integer(bool positive, uint8_t* kind) {
+    const int c = next();
+    if (c < 0) return error(JE_EOF_VALUE);
+    uint64_t sig = 0;
+    bool flt = false;
+    if (c == '0') {
+      if (dig(pnull())) return peek_error(JE_NUMBER);
+    } else if (c >= '1' && c <= '9') {
+      sig = (uint64_t)(c - '0');
+      for (;;) {
+        const int p = pnull();
+        if (!dig(p)) break;
+        const uint64_t dg = (uint64_t)(p - '0');
+        if (sig > (~0ull - dg) / 10) {  // parse_long_integer
+          while (dig(pnull())) eat();
+          const int q = pnull();
+          *kind = JU_FLOAT;
+          if (q == '.') return decimal_syn();
+          if (q == 'e' || q == 'E') return exponent_syn();
+          return 0;
+        }
+        eat();
+        sig = sig * 10 + dg;
+      }
+    } else {
+      return error(JE_NUMBER);
+    }
+    const int t = pnull();
+    if (t == '.') {
+      flt = true;
+      if (decimal_syn()) return -1;
+    } else if (t == 'e' || t == 'E') {
+      flt = true;
+      if (exponent_syn()) return -1;
+    }
+    if (!positive && (sig == 0 || sig > 0x8000000000000000ull)) flt = true;  // -0 / below i64::MIN -> f64
+    *kind = flt ? JU_FLOAT : (positive ? JU_UINT : JU_NINT);
+    return 0;
+  }
+
+  // de.rs peek_invalid_type (expected kind `ex`)
+  __device__ __forceinline__ int invalid_type(uint8_t ex) {
+    int c = peek();
+    if (c < 0) c = 0;
+    uint8_t un;
+    uint32_t a = 0, b = 0;
+    switch (c) {
+      case 'n':
+        eat();
+        if (ident("ull", 3)) return -1;
+        un = JU_UNIT;
+        break;
+      case 't':
+        eat();
+        if (ident("rue", 3)) return -1;
+        un = JU_TRUE;
+        break;
+      case 'f':
+        eat();
+        if (ident("alse", 4)) return -1;
+        un = JU_FALSE;
+        break;
+      case '-':
+      case '0': case '1': case '2': case '3': case '4': case '5': case '6': case '7': case '8': case '9': {
+        const bool pos = c != '-';
+        if (!pos) eat();
+        a = i;
+        if (parse_integer(pos, &un)) return -1;
+        b = i;
+        break;
+      }
+      case '"': {
+        eat();
+        if (parse_str(nullptr, &a, &b)) return -1;
+        un = JU_STR;
+        break;
+      }
+      case '[': un = JU_SEQ; break;
+      case '{': un = JU_MAP; break;
+      default: return peek_error(JE_VALUE);
+    }
+    custom(JE_INVALID_TYPE, a, b, (uint8_t)(un | (ex << 4)));
+    fix_position();
+    return -1;
+  }
+
+  // de.rs ignore_value (frames as a bit stack: 1 = '[', 0 = '{')
+  __device__ __forceinline__ int ignore_value() {
+    uint64_t stk = 0;
+    uint32_t sn = 0;
+    int enclosing = 0;
+    for (;;) {
+      const int peek_c = ws();
+      if (peek_c < 0) return peek_error(JE_EOF_VALUE);
+      int frame = 0;
+      switch (peek_c) {
+        case 'n': eat(); if (ident("ull", 3)) return -1; break;
+        case 't': eat(); if (ident("rue", 3)) return -1; break;
+        case 'f': eat(); if (ident("alse", 4)) return -1; break;
+        case '-': eat(); if (ignore_integer()) return -1; break;
+        case '0': case '1': case '2': case '3': case '4': case '5': case '6': case '7': case '8': case '9':
+          if (ignore_integer()) return -1;
+          break;
+        case '"': eat(); if (ignore_str()) return -1; break;
+        case '[':
+        case '{':
+          if (enclosing) {
+            if (sn >= kJsonFrames) return fail_at(i, JE_DEEP);
+            const uint64_t bit = 1ull << sn;
+            if (enclosing == '[')
+              stk |= bit;
+            else
+              stk &= ~bit;
+            sn++;
+          }
+          enclosing = 0;
+          eat();
+          frame = peek_c;
+          break;
+        default: return peek_error(JE_VALUE);
+      }
+      bool accept_comma;
+      if (frame) {
+        accept_comma = false;
+      } else if (enclosing) {
+        frame = enclosing;
+        enclosing = 0;
+        accept_comma = true;
+      } else if (sn) {
+        sn--;
+        frame = ((stk >> sn) & 1) ? '[' : '{';
+        accept_comma = true;
+      } else {
+        return 0;
+      }
+      for (;;) {
+        const int c = ws();
+        if (c == ',' && accept_comma) {
+          eat();
+          break;
+        } else if ((c == ']' && frame == '[') || (c == '}' && frame == '{')) {
+          // close the frame below
+        } else if (c >= 0) {
+          if (accept_comma) return peek_error(frame == '[' ? JE_LIST_COMMA : JE_OBJ_COMMA);
+          break;
+        } else {
+          return peek_error(frame == '[' ? JE_EOF_LIST : JE_EOF_OBJECT);
+        }
+        eat();
+        if (!sn) return 0;
+        sn--;
+        frame = ((stk >> sn) & 1) ? '[' : '{';
+        accept_comma = true;
+      }
+      if (frame == '{') {
+        int c = ws();
+        if (c == '"')
+          eat();
+        else if (c >= 0)
+          return peek_error(JE_KEY);
+        else
+          return peek_error(JE_EOF_OBJECT);
+        if (ignore_str()) return -1;
+        c = ws();
+        if (c == ':')
+          eat();
+        else if (c >= 0)
+          return peek_error(JE_COLON);
+        else
+          return peek_error(JE_EOF_OBJECT);
+      }
+      enclosing = frame;
+    }
+  }
+
+  // deserialize_str for the `message: String` field (expected "a string")
+  __device__ __forceinline__ int de_string() {
+    const int p = ws();
+    if (p < 0) return peek_error(JE_EOF_VALUE);
+    if (p == '"') {
+      eat();
+      uint32_t a, b;
+      return parse_str(nullptr, &a, &b);
+    }
+    invalid_type(JX_STRING);
+    fix_position();
+    return -1;
+  }
+  // variant identifier of LogLevel (deserialize_identifier -> deserialize_str)
+  __device__ __forceinline__ int variant(int* var) {
+    const int p = ws();
+    if (p < 0) return peek_error(JE_EOF_VALUE);
+    if (p != '"') {
+      invalid_type(JX_VARIANT);
+      fix_position();
+      return -1;
+    }
+    eat();
+    // "debug", "info", "warn", "error" (little-endian packed)
+    Match m = {{0x6775626564ull, 0x6f666e69ull, 0x6e726177ull, 0x726f727265ull}, {5, 4, 4, 5}, 0xFu, 0};
+    uint32_t a, b;
+    if (parse_str(&m, &a, &b)) return -1;
+    const int k = m_hit(m);
+    if (k >= 0) {
+      *var = k;
+      return 0;
+    }
+    custom(JE_UNKNOWN_VARIANT, a, b, 0);
+    fix_position();
+    return -1;
+  }
+  __device__ __forceinline__ int de_unit() {
+    const int p = ws();
+    if (p < 0) return peek_error(JE_EOF_VALUE);
+    if (p == 'n') {
+      eat();
+      return ident("ull", 3);
+    }
+    invalid_type(JX_UNIT);
+    fix_position();
+    return -1;
+  }
+  __device__ __forceinline__ int de_enum(int* var) {
+    const int p = ws();
+    if (p == '{') {
+      if (--depth == 0) return peek_error(JE_RECURSION);
+      eat();
+      if (variant(var)) return -1;
+      int c = ws();
+      if (c == ':')
+        eat();
+      else if (c >= 0)
+        return peek_error(JE_COLON);
+      else
+        return peek_error(JE_EOF_OBJECT);
+      if (de_unit()) return -1;
+      depth++;
+      c = ws();
+      if (c == '}') {
+        eat();
+        return 0;
+      }
+      if (c >= 0) return error(JE_VALUE);
+      return error(JE_EOF_OBJECT);
+    }
+    if (p == '"') return variant(var);
+    if (p >= 0) return peek_error(JE_VALUE);
+    return peek_error(JE_EOF_VALUE);
+  }
+  __device__ __forceinline__ int field_value(int f, int* level) { return f == 0 ? de_enum(level) : de_string(); }
+
+  __device__ __forceinline__ int visit_map(int* level) {
+    bool seen0 = false, seen1 = false, first = true;
+    for (;;) {
+      int p = ws();
+      if (p == '}') break;
+      if (p == ',' && !first) {
+        eat();
+        p = ws();
+      } else if (p >= 0) {
+        if (first)
+          first = false;
+        else
+          return peek_error(JE_OBJ_COMMA);
+      } else {
+        return peek_error(JE_EOF_OBJECT);
+      }
+      if (p == '}') return peek_error(JE_TRAILING_COMMA);
+      if (p < 0) return peek_error(JE_EOF_VALUE);
+      if (p != '"') return peek_error(JE_KEY);
+      eat();
+      // "level", "message"
+      Match m = {{0x6c6576656cull, 0x6567617373656dull, 0, 0}, {5, 7, 0, 0}, 3u, 0};
+      uint32_t a, b;
+      if (parse_str(&m, &a, &b)) return -1;
+      const int f = m_hit(m);
+      if (f == 0 && seen0) return custom(JE_DUP_FIELD, 0, 0, 0);
+      if (f == 1 && seen1) return custom(JE_DUP_FIELD, 1, 0, 0);
+      const int c = ws();
+      if (c == ':')
+        eat();
+      else if (c >= 0)
+        return peek_error(JE_COLON);
+      else
+        return peek_error(JE_EOF_OBJECT);
+      if (f < 0) {
+        if (ignore_value()) return -1;
+      } else {
+        if (field_value(f, level)) return -1;
+        if (f == 0)
+          seen0 = true;
+        else
+          seen1 = true;
+      }
+    }
+    if (!seen0) return custom(JE_MISSING_FIELD, 0, 0, 0);
+    if (!seen1) return custom(JE_MISSING_FIELD, 1, 0, 0);
+    return 0;
+  }
+  __device__ __forceinline__ int visit_seq(int* level) {
+    bool first = true;
+    for (int k = 0; k < 2; k++) {
+      int p = ws();
+      if (p == ']') return custom(JE_INVALID_LENGTH, (uint32_t)k, 0, 0);
+      if (p == ',' && !first) {
+        eat();
+        p = ws();
+      } else if (p >= 0) {
+        if (first)
+          first = false;
+        else
+          return peek_error(JE_LIST_COMMA);
+      } else {
+        return peek_error(JE_EOF_LIST);
+      }
+      if (p == ']') return peek_error(JE_TRAILING_COMMA);
+      if (p < 0) return peek_error(JE_EOF_VALUE);
+      if (field_value(k, level)) return -1;
+    }
+    return 0;
+  }
+  __device__ __forceinline__ int end_map() {
+    const int c = ws();
+    if (c == '}') {
+      eat();
+      return 0;
+    }
+    if (c == ',') return peek_error(JE_TRAILING_COMMA);
+    if (c >= 0) return peek_error(JE_TRAILING);
+    return peek_error(JE_EOF_OBJECT);
+  }
+  __device__ __forceinline__ int end_seq() {
+    const int c = ws();
+    if (c == ']') {
+      eat();
+      return 0;
+    }
+    if (c == ',') {
+      eat();
+      const int p = ws();
+      if (p == ']') return peek_error(JE_TRAILING_COMMA);
+      return peek_error(JE_TRAILING);
+    }
+    if (c >= 0) return peek_error(JE_TRAILING);
+    return peek_error(JE_EOF_LIST);
+  }
+  // the end check after a failed visitor only moves the reader
+  __device__ __forceinline__ void end_probe(bool seq) {
+    const bool f0 = failed, h0 = has_pos;
+    const JRes r0 = r;
+    failed = false;
+    if (seq)
+      end_seq();
+    else
+      end_map();
+    failed = f0;
+    has_pos = h0;
+    r = r0;
+  }
+  __device__ __forceinline__ int de_struct(int* level) {
+    const int p = ws();
+    if (p < 0) return peek_error(JE_EOF_VALUE);
+    int rc;
+    if (p == '[' || p == '{') {
+      if (--depth == 0) return peek_error(JE_RECURSION);
+      eat();
+      rc = p == '[' ? visit_seq(level) : visit_map(level);
+      depth++;
+      if (rc)
+        end_probe(p == '[');
+      else
+        rc = p == '[' ? end_seq() : end_map();
+    } else {
+      invalid_type(JX_STRUCT);
+      rc = -1;
+    }
+    if (rc) fix_position();
+    return rc;
+  }
+  __device__ __forceinline__ JRes run() {
+    int level = 0;
+    r = JRes{0, 0, 0, 0, 0, 0, 0};
+    failed = false;
+    has_pos = false;
+    depth = 128;
+    i = 0;
+    int rc = de_struct(&level);
+    if (!rc && ws() >= 0) rc = peek_error(JE_TRAILING);  // Deserializer::end
+    if (!rc) {
+      r.ok = 1;
+      r.level = (uint8_t)level;
+    }
+    return r;
+  }
+};
+
+// one out-of-line copy over a generic pointer (LDS window, global slice or a
+// private i32 text buffer); the parser's helpers inline into it so its state
+// stays in registers, and k_eval keeps one call site per variant
+__device__ __noinline__ JRes json_structured_log(const uint8_t* s, uint32_t n, bool upper) {
+  JsonDev<const uint8_t*> d;
+  d.s = s;
+  d.n = n;
+  d.upper = upper;
+  return d.run();
+}
+
+}  // namespace fsg

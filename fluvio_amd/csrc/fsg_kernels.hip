@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include "fsg_device.h"
+#include "fsg_json_dev.h"
 
 namespace fsg {
 
@@ -255,7 +256,8 @@ constexpr int kEvalThreads = 256;  // one 4-wave workgroup per stored batch
 constexpr uint32_t opbit(int op) { return 1u << op; }
 constexpr uint32_t kOpsContains = opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
 constexpr uint32_t kOpsRegex = opbit(OP_REGEX) | opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
-constexpr uint32_t kOpsAll = 0x7Fu;
+constexpr uint32_t kOpsJson = opbit(OP_FILTER_JSON) | opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
+constexpr uint32_t kOpsAll = 0xFFu;
 constexpr int kDfaDyn = 768 + kDfaLds;  // dynamic LDS of a chain with a regex stage
 extern __shared__ __attribute__((aligned(16))) uint8_t g_dyn_lds[];
 
@@ -269,10 +271,11 @@ struct __attribute__((aligned(16))) WaveLds {
   uint32_t r_flags[kMaxR];
   uint32_t r_aux[kMaxR];    // utf8 valid_up_to / parse kind
   uint32_t r_aux2[kMaxR];   // utf8 error_len
+  uint32_t r_aux3[kMaxR];   // serde_json error span end
   int32_t r_ival[kMaxR];    // VT_I32 value
   int32_t r_ival_in[kMaxR]; // value entering the erroring stage
+  uint32_t r_ec[kMaxR];     // error code word (ErrCode | detail)
   uint8_t r_es[kMaxR];      // first error stage (0xFF none)
-  uint8_t r_ec[kMaxR];      // error code
   uint8_t r_attr[kMaxR];
   uint8_t r_haskey[kMaxR];
   int64_t r_od[kMaxR];
@@ -284,6 +287,7 @@ struct __attribute__((aligned(16))) WaveLds {
   int32_t walk_status;      // 0 ok, 1 decode error, 2 window incomplete (need next window)
   uint32_t err_stage_b, err_idx_b;  // broadcast of the batch's first error (wave 0 -> all)
   uint32_t next_cursor_lo, next_cursor_hi;
+  BatchStat bs;             // the batch's result, assembled by lane 0 (keeps long-lived state out of VGPRs)
 };
 
 // decode a varint from window bytes [q, lim); lim_sec tells whether running
@@ -517,46 +521,42 @@ __device__ __forceinline__ uint32_t swar_upper(uint32_t x) {
   const uint32_t lower = ge_a & ~gt_z & ~x & 0x80808080u;
   return x - (lower >> 2);
 }
-// bytes [t, t+4) of the little-endian byte stream held in w[] (t compile-time)
-template <int T>
-__device__ __forceinline__ uint32_t bytes_at(const uint32_t (&w)[8], int k) {
-  constexpr int q = T / 4, r = T % 4;
-  const uint32_t lo = w[k + q];
-  if constexpr (r == 0) {
-    return lo;
-  } else {
-    const uint32_t hi = w[k + q + 1];
-    return (lo >> (8 * r)) | (hi << (32 - 8 * r));
-  }
-}
-
-// match mask of needle byte T at positions 4k..4k+3 of the chunk
-template <int T>
-__device__ __forceinline__ void needle_step(const uint32_t (&w)[8], const uint32_t (&nb)[16], uint32_t m,
-                                            uint32_t (&acc)[4]) {
-  if ((uint32_t)T < m) {
-    const uint32_t N = nb[T];
-#pragma unroll
-    for (int k = 0; k < 4; k++) acc[k] &= zbytes(bytes_at<T>(w, k) ^ N);
-  }
-}
-
 // Data-parallel substring scan + non-ASCII marking over the values of the window.
 // Marks RF_MATCH on records whose (optionally uppercased) value contains needle.
-// LDS path: each lane takes 16-byte chunks; the needle's first 16 bytes are
-// matched branch-free in registers (32 bytes loaded with two ds_read_b128),
-// longer needles finish with LDS byte compares.
-template <bool kLds, typename P>
-__device__ __forceinline__ void scan_contains(WaveLds& L, P w, uint32_t wlen, int nr, const uint8_t* needle, uint32_t m, bool upper,
-                              bool mark_nonascii) {
-  if (nr == 0) return;
+// Each lane takes 16-byte chunks (32 bytes loaded with two ds_read_b128 from the
+// LDS window).  Filter: needle[0] at p AND needle[m-1] at p+m-1, four positions
+// per u32 with an exact SWAR zero-byte test (the last-byte view is one
+// v_alignbyte per word); surviving positions are verified byte by byte.  A wave
+// pays for its worst lane's candidate count only, not for a full-needle SWAR
+// evaluation of every chunk.
+// Q >= 0: compile-time word offset; Q < 0: runtime offset q (global-memory path)
+template <int Q>
+__device__ __forceinline__ uint32_t last_view(const uint32_t (&w)[8], int k, uint32_t sh, uint32_t q) {
+  if constexpr (Q >= 0) {
+    return __builtin_amdgcn_alignbyte(w[k + Q + 1], w[k + Q], sh);
+  } else {
+    uint32_t a = w[k], b = w[k + 1];
+    for (uint32_t t = 1; t <= 3; t++)
+      if (q >= t) {
+        a = w[k + t];
+        b = w[k + t + 1];
+      }
+    return __builtin_amdgcn_alignbyte(b, a, sh);
+  }
+}
+template <int Q, bool kLds, typename P>
+__device__ __forceinline__ void scan_contains_q(WaveLds& L, P w, int nr, const uint8_t* needle, uint32_t m,
+                                                bool upper, bool mark_nonascii) {
   const uint32_t lo = L.r_vs[0];
   const uint32_t hi = L.r_vs[nr - 1] + L.r_vl[nr - 1];
   const uint32_t l = threadIdx.x;
-  // the needle's first 16 bytes, broadcast, in registers (loaded once)
-  uint32_t nb[16];
-#pragma unroll
-  for (int t = 0; t < 16; t++) nb[t] = (uint32_t)t < m ? 0x01010101u * needle[t] : 0u;
+  const uint32_t nf = m ? 0x01010101u * needle[0] : 0u;
+  // filter bytes: needle[0] and needle[mf-1] (mf = min(m, 16): the 32-byte chunk
+  // holds positions p..p+15 of each of the 16 starts)
+  const uint32_t mf = m < 16 ? m : 16;
+  const uint32_t nl = m ? 0x01010101u * needle[mf - 1] : 0u;
+  const uint32_t sh = m ? (mf - 1) & 3 : 0;
+  const uint32_t vend = m > 16 ? m : (m ? m - 1 : 0);  // verify needle[1..vend)
   for (uint32_t c = (lo & ~15u) + l * 16; c < hi; c += kEvalThreads * 16) {
     uint32_t wd[8];
     if constexpr (kLds) {
@@ -580,26 +580,15 @@ __device__ __forceinline__ void scan_contains(WaveLds& L, P w, uint32_t wlen, in
         }
     }
     if (m == 0) continue;
+#if defined(FSG_EXP) && FSG_EXP == 1
+    continue;  // experiment: substring filter off (timing/counter attribution only)
+#endif
     if (upper)
       for (int k = 0; k < 8; k++) wd[k] = swar_upper(wd[k]);
-    uint32_t acc[4] = {0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u};
-    needle_step<0>(wd, nb, m, acc);
-    needle_step<1>(wd, nb, m, acc);
-    if (!(acc[0] | acc[1] | acc[2] | acc[3])) continue;  // 2-byte prefilter
-    needle_step<2>(wd, nb, m, acc);
-    needle_step<3>(wd, nb, m, acc);
-    needle_step<4>(wd, nb, m, acc);
-    needle_step<5>(wd, nb, m, acc);
-    needle_step<6>(wd, nb, m, acc);
-    needle_step<7>(wd, nb, m, acc);
-    needle_step<8>(wd, nb, m, acc);
-    needle_step<9>(wd, nb, m, acc);
-    needle_step<10>(wd, nb, m, acc);
-    needle_step<11>(wd, nb, m, acc);
-    needle_step<12>(wd, nb, m, acc);
-    needle_step<13>(wd, nb, m, acc);
-    needle_step<14>(wd, nb, m, acc);
-    needle_step<15>(wd, nb, m, acc);
+    uint32_t acc[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) acc[k] = zbytes(wd[k] ^ nf) & zbytes(last_view<Q>(wd, k, sh, (mf - 1) >> 2) ^ nl);
+    if (!(acc[0] | acc[1] | acc[2] | acc[3])) continue;
     for (int k = 0; k < 4; k++) {
       uint32_t cand = acc[k];
       while (cand) {
@@ -612,7 +601,7 @@ __device__ __forceinline__ void scan_contains(WaveLds& L, P w, uint32_t wlen, in
         const uint32_t ve = L.r_vs[r] + L.r_vl[r];
         if (p + m > ve) continue;
         bool ok = true;
-        for (uint32_t t = 16; t < m; t++) {  // needles longer than 16 bytes
+        for (uint32_t t = 1; t < vend; t++) {
           uint8_t y = kLds ? L.win[p + t] : w[p + t];
           if (upper) y = up(y);
           if (y != needle[t]) {
@@ -624,7 +613,27 @@ __device__ __forceinline__ void scan_contains(WaveLds& L, P w, uint32_t wlen, in
       }
     }
   }
+}
+
+template <bool kLds, typename P>
+__device__ __forceinline__ void scan_contains(WaveLds& L, P w, uint32_t wlen, int nr, const uint8_t* needle,
+                                              uint32_t m, bool upper, bool mark_nonascii) {
   (void)wlen;
+  if (nr == 0) return;
+  // the last-byte view reads words k + (mf-1)/4 and k + (mf-1)/4 + 1 of the
+  // 8-word chunk: wave-uniform dispatch on that word offset
+  const uint32_t mf = m < 16 ? m : 16;
+  const uint32_t q = mf ? ((mf - 1) >> 2) : 0;
+  if constexpr (!kLds) {
+    scan_contains_q<-1, kLds>(L, w, nr, needle, m, upper, mark_nonascii);
+    return;
+  }
+  switch (q) {
+    case 0: scan_contains_q<0, kLds>(L, w, nr, needle, m, upper, mark_nonascii); break;
+    case 1: scan_contains_q<1, kLds>(L, w, nr, needle, m, upper, mark_nonascii); break;
+    case 2: scan_contains_q<2, kLds>(L, w, nr, needle, m, upper, mark_nonascii); break;
+    default: scan_contains_q<3, kLds>(L, w, nr, needle, m, upper, mark_nonascii); break;
+  }
 }
 
 // records with an empty value never get a scan hit; an empty needle matches all
@@ -763,8 +772,10 @@ __device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int 
     }
     __syncthreads();
     STAMP(11);
-    // ---- per-record phase (thread per record)
-    for (int r = l; r < nr; r += kEvalThreads) {
+    // ---- per-record phase (thread per record; record r = 4 * lane + wave so
+    // that the records of a window are spread over the four waves)
+    static_assert(kMaxR <= kEvalThreads, "one pass covers every record");
+    for (int r = (int)(((l & 63u) << 2) | (l >> 6)); r < nr; r += kEvalThreads) {
       uint32_t f = L.r_flags[r];
       if (!(f & RF_ALIVE)) continue;
       const uint32_t vs = L.r_vs[r], vl = L.r_vl[r];
@@ -778,7 +789,7 @@ __device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int 
         f |= RF_UTF8_DONE;
       }
       bool err = false;
-      uint8_t ec = 0;
+      uint32_t ec = 0;
       const int32_t ival_in = L.r_ival[r];
       if ((kOps & opbit(OP_AGG_SUM)) && op == OP_AGG_SUM && sd.acc_bad) {
         err = true;
@@ -834,6 +845,27 @@ __device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int 
             }
             bool keep = sd.keep_match ? m : !m;
             if (!keep) f &= ~RF_ALIVE;
+            break;
+          }
+          case OP_FILTER_JSON: {
+            if constexpr (!(kOps & opbit(OP_FILTER_JSON))) break;
+            uint8_t t[12];
+            const uint8_t* js = (const uint8_t*)&w[vs];
+            uint32_t jn = vl;
+            if (!src) {
+              jn = fmt_i32(ival_in, t);
+              js = t;
+            }
+            const JRes jr = json_structured_log(js, jn, src && upper);
+            if (!jr.ok) {
+              err = true;
+              ec = EC_JSON | ((uint32_t)jr.code << 8) | ((uint32_t)jr.sub << 16);
+              L.r_aux[r] = jr.pos;
+              L.r_aux2[r] = jr.a;
+              L.r_aux3[r] = jr.b;
+            } else if (jr.level == 0) {
+              f &= ~RF_ALIVE;  // level > Debug keeps the record
+            }
             break;
           }
           case OP_FILTER_ODD:
@@ -924,10 +956,19 @@ __global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : 2) void 
   const uint64_t al0 = pos & ~15ull;
   load_window(L, S, al0, kWin);
   const uint8_t* h = L.win + (pos - al0);
-  const int64_t base_offset = (int64_t)rd_be(h, 8);
   const int32_t batch_len = (int32_t)rd_be(h + 8, 4);
-  const int32_t lod_in = (int32_t)rd_be(h + 23, 4);
-  const int64_t first_ts = (int64_t)rd_be(h + 27, 8);
+  if (tid == 0) {
+    L.bs.base_offset = (int64_t)rd_be(h, 8);
+    L.bs.lod_in = (int32_t)rd_be(h + 23, 4);
+    L.bs.first_ts = (int64_t)rd_be(h + 27, 8);
+    L.bs.err_code = 0;
+    L.bs.err_pos = 0;
+    L.bs.err_od = 0;
+    L.bs.err_ival = 0;
+    L.bs.err_aux = 0;
+    L.bs.err_aux2 = 0;
+    L.bs.err_aux3 = 0;
+  }
   const uint64_t sec0 = pos + 57;
   const uint64_t sec_end = pos + 12 + (uint64_t)(uint32_t)batch_len;  // framing validated at ingest
   const uint32_t sec_len = (uint32_t)(sec_end - sec0);
@@ -961,10 +1002,6 @@ __global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : 2) void 
   // phase A: full chain; phase B (only if a record error occurred): truncated chain
   int nst = (int)ch.nstages;
   uint32_t err_stage = 0xFFFFFFFFu, err_idx = 0xFFFFFFFFu;
-  uint32_t err_code = 0, err_aux = 0, err_aux2 = 0;
-  int32_t err_ival = 0;
-  uint64_t err_pos = 0;
-  int64_t err_od = 0;
   bool unsupported = false;
   uint32_t kcount = 0;
   int64_t aggsum = 0;
@@ -1057,12 +1094,15 @@ __global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : 2) void 
               err_stage = ks;
               err_idx = ki;
               const int rr = (int)(ki - done_recs);
-              err_code = L.r_ec[rr];
-              err_aux = L.r_aux[rr];
-              err_aux2 = L.r_aux2[rr];
-              err_ival = L.r_ival_in[rr];
-              err_pos = wbase + L.r_start[rr];
-              err_od = L.r_od[rr];
+              if (l == 0) {
+                L.bs.err_code = L.r_ec[rr];
+                L.bs.err_aux = L.r_aux[rr];
+                L.bs.err_aux2 = L.r_aux2[rr];
+                L.bs.err_aux3 = L.r_aux3[rr];
+                L.bs.err_ival = L.r_ival_in[rr];
+                L.bs.err_pos = wbase + L.r_start[rr];
+                L.bs.err_od = L.r_od[rr];
+              }
             }
           }
         }
@@ -1123,26 +1163,17 @@ __global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : 2) void 
     }
     if (phase == 0 && err_stage == 0xFFFFFFFFu) break;
   }
-  unsupported = __syncthreads_or(unsupported);
-  if (!(flags & BF_DECODE) && err_stage != 0xFFFFFFFFu) flags |= (err_code == EC_UNSUP) ? BF_UNSUPPORTED : BF_ERR;
-  if (err_stage == 0xFFFFFFFFu || err_stage + 1 == ch.nstages) flags |= BF_LAST_STAGE;
-  if (unsupported) flags |= BF_UNSUPPORTED;
+  unsupported = __syncthreads_or(unsupported);  // also orders lane 0's L.bs writes
   if (tid == 0) {
-    BatchStat st;
-    st.base_offset = base_offset;
-    st.first_ts = first_ts;
-    st.lod_in = lod_in;
+    if (!(flags & BF_DECODE) && err_stage != 0xFFFFFFFFu)
+      flags |= (L.bs.err_code == EC_UNSUP) ? BF_UNSUPPORTED : BF_ERR;
+    if (err_stage == 0xFFFFFFFFu || err_stage + 1 == ch.nstages) flags |= BF_LAST_STAGE;
+    if (unsupported) flags |= BF_UNSUPPORTED;
+    BatchStat st = L.bs;
     st.flags = flags;
     st.nkeep = kcount;
     st.sec_len = sec_len;
     st.err_stage = err_stage;
-    st.err_code = err_code;
-    st.err_pos = err_pos;
-    st.err_od = err_od;
-    st.err_ival = err_ival;
-    st.err_aux = err_aux;
-    st.err_aux2 = err_aux2;
-    st.pad = 0;
     st.agg_sum = (ch.has_agg && (err_stage == 0xFFFFFFFFu || err_stage + 1 == ch.nstages)) ? aggsum : 0;
     a.bstat[b] = st;  // the cross-batch minima are reduced by k_mins
   }
@@ -1787,6 +1818,8 @@ void launch_eval(const EvalArgs& a, uint32_t ops, hipStream_t s) {
     hipLaunchKernelGGL(k_eval<kOpsContains>, dim3(a.nbatches), dim3(kEvalThreads), dyn, s, a);
   else if ((ops & ~kOpsRegex) == 0)
     hipLaunchKernelGGL(k_eval<kOpsRegex>, dim3(a.nbatches), dim3(kEvalThreads), dyn, s, a);
+  else if ((ops & ~kOpsJson) == 0)
+    hipLaunchKernelGGL(k_eval<kOpsJson>, dim3(a.nbatches), dim3(kEvalThreads), dyn, s, a);
   else
     hipLaunchKernelGGL(k_eval<kOpsAll>, dim3(a.nbatches), dim3(kEvalThreads), dyn, s, a);
 }

@@ -26,6 +26,7 @@
 
 #include "fsg.h"
 #include "fsg_device.h"
+#include "fsg_json_dev.h"
 #include "fsg_launch.h"
 #include "fsg_regex.h"
 
@@ -359,6 +360,9 @@ int add_stage(fsg_chain* c, const ModuleSpec& m, const std::string& name, uint8_
     sd.dfa.f_classmap_up = put_blob(fd.classmap_up.data(), 256);
     sd.dfa.f_trans = put_blob(fd.trans.data(), fd.trans.size() * 2);
     sd.dfa.f_accept = put_blob(fd.accept.data(), fd.accept.size());
+  } else if (name == "filter_json") {  // examples/filter_json: StructuredLog.level > Debug
+    sd.op = OP_FILTER_JSON;
+    sd.kind = FSG_KIND_FILTER;
   } else if (name == "filter_odd") {
     sd.op = OP_FILTER_ODD;
     sd.kind = FSG_KIND_FILTER;
@@ -527,6 +531,134 @@ void free_error(fsg_runtime_error& e) {
   memset(&e, 0, sizeof e);
 }
 
+// serde_json::Error Display for the descriptor k_eval found (fsg_json_dev.h):
+// "<message> at line L column C" with serde's custom messages
+// (serde/src/de/mod.rs: invalid_type / invalid_length / unknown_variant /
+// duplicate_field / missing_field).  The GPU did the parse; this renders text
+// from its code, reader index and spans.  Returns false outside the restatement.
+static void json_unescape(const std::vector<uint8_t>& v, uint32_t a, uint32_t b, std::string& out) {
+  auto hexv = [](int c) {
+    return c <= '9' ? c - '0' : (c | 0x20) - 'a' + 10;
+  };
+  auto put = [&](uint32_t c) {
+    if (c < 0x80) {
+      out += (char)c;
+    } else if (c < 0x800) {
+      out += (char)(0xC0 | (c >> 6));
+      out += (char)(0x80 | (c & 0x3F));
+    } else if (c < 0x10000) {
+      out += (char)(0xE0 | (c >> 12));
+      out += (char)(0x80 | ((c >> 6) & 0x3F));
+      out += (char)(0x80 | (c & 0x3F));
+    } else {
+      out += (char)(0xF0 | (c >> 18));
+      out += (char)(0x80 | ((c >> 12) & 0x3F));
+      out += (char)(0x80 | ((c >> 6) & 0x3F));
+      out += (char)(0x80 | (c & 0x3F));
+    }
+  };
+  for (uint32_t i = a; i < b && i < v.size();) {
+    if (v[i] != '\\') {
+      out += (char)v[i++];
+      continue;
+    }
+    const uint8_t e = v[i + 1];
+    i += 2;
+    switch (e) {
+      case 'b': out += '\b'; break;
+      case 'f': out += '\f'; break;
+      case 'n': out += '\n'; break;
+      case 'r': out += '\r'; break;
+      case 't': out += '\t'; break;
+      case 'u': {
+        uint32_t c = 0;
+        for (int k = 0; k < 4; k++) c = (c << 4) | (uint32_t)hexv(v[i + k]);
+        i += 4;
+        if (c >= 0xD800 && c <= 0xDBFF) {  // validated pair \uD8xx\uDCxx
+          uint32_t c2 = 0;
+          for (int k = 0; k < 4; k++) c2 = (c2 << 4) | (uint32_t)hexv(v[i + 2 + k]);
+          i += 6;
+          c = (((c - 0xD800) << 10) | (c2 - 0xDC00)) + 0x10000;
+        }
+        put(c);
+        break;
+      }
+      default: out += (char)e; break;  // " \\ /
+    }
+  }
+}
+
+bool json_hint(uint32_t code_word, uint32_t pos, uint32_t a, uint32_t b, const std::vector<uint8_t>& v,
+               std::string& out) {
+  static const char* const kSyntax[] = {
+      "", "EOF while parsing a list", "EOF while parsing an object", "EOF while parsing a string",
+      "EOF while parsing a value", "expected `:`", "expected `,` or `]`", "expected `,` or `}`", "expected ident",
+      "expected value", "invalid escape", "invalid number", "invalid unicode code point",
+      "control character (\\u0000-\\u001F) found while parsing a string", "key must be a string",
+      "lone leading surrogate in hex escape", "trailing comma", "trailing characters",
+      "unexpected end of hex escape", "recursion limit exceeded"};
+  static const char* const kFields[] = {"level", "message"};
+  const uint32_t code = (code_word >> 8) & 0xFF, sub = (code_word >> 16) & 0xFF;
+  std::string msg;
+  if (code >= JE_EOF_LIST && code <= JE_RECURSION) {
+    msg = kSyntax[code];
+  } else if (code == JE_DUP_FIELD) {
+    msg = std::string("duplicate field `") + kFields[a & 1] + "`";
+  } else if (code == JE_MISSING_FIELD) {
+    msg = std::string("missing field `") + kFields[a & 1] + "`";
+  } else if (code == JE_INVALID_LENGTH) {
+    msg = "invalid length " + std::to_string(a) + ", expected struct StructuredLog with 2 elements";
+  } else if (code == JE_UNKNOWN_VARIANT) {
+    std::string val;
+    json_unescape(v, a, b, val);
+    msg = "unknown variant `" + val + "`, expected one of `debug`, `info`, `warn`, `error`";
+  } else if (code == JE_INVALID_TYPE) {
+    static const char* const kExp[] = {"struct StructuredLog", "a string", "variant identifier", "unit"};
+    std::string un;
+    switch (sub & 15) {
+      case JU_UNIT: un = "unit value"; break;
+      case JU_TRUE: un = "boolean `true`"; break;
+      case JU_FALSE: un = "boolean `false`"; break;
+      case JU_UINT: un = "integer `" + std::string(v.begin() + a, v.begin() + b) + "`"; break;
+      case JU_NINT: un = "integer `-" + std::string(v.begin() + a, v.begin() + b) + "`"; break;
+      case JU_STR: {
+        std::string raw;
+        json_unescape(v, a, b, raw);
+        un = "string \"";
+        for (unsigned char c : raw) {  // Rust str Debug, printable-ASCII subset
+          if (c == '"') un += "\\\"";
+          else if (c == '\\') un += "\\\\";
+          else if (c == '\n') un += "\\n";
+          else if (c == '\r') un += "\\r";
+          else if (c == '\t') un += "\\t";
+          else if (c == 0) un += "\\0";
+          else if (c >= 0x20 && c < 0x7f) un += (char)c;
+          else return false;
+        }
+        un += "\"";
+        break;
+      }
+      case JU_SEQ: un = "sequence"; break;
+      case JU_MAP: un = "map"; break;
+      default: return false;  // JU_FLOAT
+    }
+    msg = "invalid type: " + un + ", expected " + kExp[(sub >> 4) & 3];
+  } else {
+    return false;  // JE_DEEP
+  }
+  size_t line = 1, col = 0;
+  for (uint32_t i = 0; i < pos && i < v.size(); i++) {
+    if (v[i] == '\n') {
+      line++;
+      col = 0;
+    } else {
+      col++;
+    }
+  }
+  out = msg + " at line " + std::to_string(line) + " column " + std::to_string(col);
+  return out.find('\0') == std::string::npos;
+}
+
 // Build SmartModuleTransformRuntimeError (link/smartmodule.rs:26-43) for the
 // error record of batch eb: hint, offset = base_offset + offset_delta, kind,
 // and the record's key/value as they entered the failing stage.
@@ -592,7 +724,11 @@ int build_error(fsg_chain* c, const fsg_slice* s, const BatchStat& st, fsg_runti
     val.assign(b, b + n);
   }
   std::string hint;
-  if (st.err_code == EC_UTF8 || st.err_code == EC_ACC_UTF8) {
+  if ((st.err_code & 0xFF) == EC_JSON) {
+    if (!json_hint(st.err_code, st.err_aux, st.err_aux2, st.err_aux3, val, hint))
+      return fail(FSG_E_UNSUPPORTED, "serde_json error text outside the GPU restatement (float / non-ASCII Debug string / "
+                                     "deep ignored nesting)");
+  } else if (st.err_code == EC_UTF8 || st.err_code == EC_ACC_UTF8) {
     hint = utf8_hint(st.err_aux, st.err_aux2);
   } else if (st.err_code == EC_PARSE) {
     hint = parse_hint(st.err_aux);

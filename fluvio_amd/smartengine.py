@@ -32,7 +32,7 @@ from .protocol import Batch, Record, decode_batch, decode_records, encode_record
 DEFAULT_SMARTENGINE_VERSION = 22  # input.rs:14 SMARTMODULE_TIMESTAMPS_VERSION
 
 BUILTINS = ("filter", "filter_init", "filter_with_param", "regex-filter", "filter_regex", "filter_odd",
-            "map", "map_double", "filter_map", "aggregate-sum")
+            "map", "map_double", "filter_map", "aggregate-sum", "filter_json")
 
 
 def builtin(name: str) -> bytes:

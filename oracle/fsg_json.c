@@ -1,0 +1,1049 @@
+/* TEST INFRASTRUCTURE — CPU oracle (never linked into or called by the product path).
+ *
+ * Scalar restatement of serde_json 1.0.96 (crates.io; pinned in
+ * smartmodule/examples/Cargo.lock, absent from the reference tree) as used by
+ * smartmodule/examples/filter_json/src/lib.rs:54-70:
+ *     serde_json::from_slice::<StructuredLog>(record.value.as_ref())?
+ * with `#[derive(Deserialize)] struct StructuredLog { level: LogLevel,
+ * #[serde(rename = "message")] _message: String }` and the unit enum
+ * `LogLevel { Debug, Info, Warn, Error }` (rename_all = "lowercase").
+ *
+ * The functions below follow serde_json's call structure one to one, because
+ * the error text (and its "at line L column C" position) depends on which
+ * routine detects an error and how far the reader has advanced:
+ *   from_trait + Deserializer::end            (de.rs)
+ *   deserialize_struct / visit_map / visit_seq (de.rs + serde_derive output)
+ *   MapAccess::next_key_seed / next_value_seed, parse_object_colon, end_map
+ *   SeqAccess::next_element_seed, end_seq
+ *   deserialize_enum, UnitVariantAccess, VariantAccess, deserialize_unit
+ *   deserialize_str (fix_position), peek_invalid_type, parse_integer/number
+ *   ignore_value / ignore_integer / ignore_decimal / ignore_exponent
+ *   SliceRead::parse_str_bytes / ignore_str / decode_hex_escape, parse_escape
+ *   position_of_index (line = 1 + #'\n' before i, column = bytes since it)
+ * Error Display = "<msg> at line L column C" (line 0: "<msg>").  serde's
+ * messages: invalid type / invalid length / unknown variant / duplicate field /
+ * missing field (serde/src/de/mod.rs).
+ *
+ * Outside the restatement (status ORC_E_UNSUPPORTED, mirrored by the GPU path):
+ * an "invalid type: floating point `..`" message (needs serde_json's f64
+ * parse + Rust's shortest float Display), "invalid type: string ..." for a
+ * string holding a byte outside printable ASCII (Rust's str Debug escaping),
+ * an ignored value nested more than 64 levels below its first bracket, and an
+ * error text holding a NUL byte.
+ */
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "fsg_oracle.h"
+
+enum { JF_IGNORED = 0, JF_ENUM = 1, JF_STRING = 2 };
+
+typedef struct {
+  const char *name;
+  int type;                  /* JF_ENUM / JF_STRING */
+  const char *const *variants; /* JF_ENUM */
+  int nvariants;
+} jfield;
+
+typedef struct {
+  const char *name; /* struct name for "expected struct X" */
+  const jfield *fields;
+  int nfields;
+} jstruct;
+
+typedef struct {
+  const uint8_t *s;
+  size_t n;
+  size_t i;
+  int depth; /* remaining_depth */
+  /* error state */
+  int failed;
+  int unsupported;
+  int has_pos;
+  size_t err_index; /* reader index the position is computed from */
+  char *msg;        /* heap, msg_len bytes (may hold any byte) */
+  size_t msg_len;
+} jde;
+
+/* ---- reader primitives (SliceRead) */
+static int jpeek(jde *d) { return d->i < d->n ? d->s[d->i] : -1; }
+static void jeat(jde *d) { d->i++; }
+static int jnext(jde *d) { return d->i < d->n ? d->s[d->i++] : -1; }
+
+/* ---- errors */
+static void jset_msg(jde *d, const char *m, size_t n) {
+  free(d->msg);
+  d->msg = (char *)malloc(n + 1);
+  memcpy(d->msg, m, n);
+  d->msg[n] = 0;
+  d->msg_len = n;
+}
+static int jfail_at(jde *d, size_t idx, const char *msg) {
+  d->failed = 1;
+  d->has_pos = 1;
+  d->err_index = idx;
+  jset_msg(d, msg, strlen(msg));
+  return -1;
+}
+static int jerror(jde *d, const char *msg) { return jfail_at(d, d->i, msg); }
+static int jpeek_error(jde *d, const char *msg) { return jfail_at(d, d->i + 1 < d->n ? d->i + 1 : d->n, msg); }
+static int jcustom(jde *d, const char *fmt, ...) {
+  d->failed = 1;
+  d->has_pos = 0;
+  va_list ap;
+  va_start(ap, fmt);
+  int n = vsnprintf(NULL, 0, fmt, ap);
+  va_end(ap);
+  char *m = (char *)malloc((size_t)n + 1);
+  va_start(ap, fmt);
+  vsnprintf(m, (size_t)n + 1, fmt, ap);
+  va_end(ap);
+  free(d->msg);
+  d->msg = m;
+  d->msg_len = (size_t)n;
+  return -1;
+}
+/* custom message from binary pieces (strings may hold NUL or any byte) */
+static int jcustom_parts(jde *d, const char *a, const uint8_t *b, size_t bn, const char *c) {
+  size_t an = strlen(a), cn = strlen(c);
+  char *m = (char *)malloc(an + bn + cn + 1);
+  memcpy(m, a, an);
+  memcpy(m + an, b, bn);
+  memcpy(m + an + bn, c, cn);
+  m[an + bn + cn] = 0;
+  d->failed = 1;
+  d->has_pos = 0;
+  free(d->msg);
+  d->msg = m;
+  d->msg_len = an + bn + cn;
+  return -1;
+}
+static int junsupported(jde *d) {
+  d->failed = 1;
+  d->unsupported = 1;
+  return -1;
+}
+/* Error::fix_position: give a position-less (custom) error the current one */
+static void jfix_position(jde *d) {
+  if (d->failed && !d->has_pos && !d->unsupported) {
+    d->has_pos = 1;
+    d->err_index = d->i;
+  }
+}
+
+#define E_EOF_LIST "EOF while parsing a list"
+#define E_EOF_OBJECT "EOF while parsing an object"
+#define E_EOF_STRING "EOF while parsing a string"
+#define E_EOF_VALUE "EOF while parsing a value"
+#define E_COLON "expected `:`"
+#define E_LIST_COMMA "expected `,` or `]`"
+#define E_OBJ_COMMA "expected `,` or `}`"
+#define E_IDENT "expected ident"
+#define E_VALUE "expected value"
+#define E_ESCAPE "invalid escape"
+#define E_NUMBER "invalid number"
+#define E_CODEPOINT "invalid unicode code point"
+#define E_CONTROL "control character (\\u0000-\\u001F) found while parsing a string"
+#define E_KEY "key must be a string"
+#define E_SURROGATE "lone leading surrogate in hex escape"
+#define E_TRAILING_COMMA "trailing comma"
+#define E_TRAILING "trailing characters"
+#define E_HEX_END "unexpected end of hex escape"
+#define E_RECURSION "recursion limit exceeded"
+
+static int parse_whitespace(jde *d) {
+  for (;;) {
+    int c = jpeek(d);
+    if (c == ' ' || c == '\n' || c == '\t' || c == '\r')
+      jeat(d);
+    else
+      return c;
+  }
+}
+
+static int parse_ident(jde *d, const char *ident) {
+  for (const char *p = ident; *p; p++) {
+    int c = jnext(d);
+    if (c < 0) return jerror(d, E_EOF_VALUE);
+    if (c != (uint8_t)*p) return jerror(d, E_IDENT);
+  }
+  return 0;
+}
+
+/* ---- strings */
+static int ESC(int c) { return c == '"' || c == '\\' || (c >= 0 && c < 0x20); }
+
+static int hexval(int c) {
+  if (c >= '0' && c <= '9') return c - '0';
+  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+  if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+  return -1;
+}
+
+static int decode_hex_escape(jde *d, uint32_t *out) {
+  if (d->i + 4 > d->n) {
+    d->i = d->n;
+    return jerror(d, E_EOF_STRING);
+  }
+  uint32_t v = 0;
+  for (int k = 0; k < 4; k++) {
+    int h = hexval(d->s[d->i]);
+    d->i++;
+    if (h < 0) return jerror(d, E_ESCAPE);
+    v = (v << 4) + (uint32_t)h;
+  }
+  *out = v;
+  return 0;
+}
+
+typedef struct {
+  uint8_t *b;
+  size_t n, cap;
+} jbuf;
+static void jb_push(jbuf *b, const uint8_t *p, size_t n) {
+  if (b->n + n > b->cap) {
+    b->cap = (b->n + n) * 2 + 16;
+    b->b = (uint8_t *)realloc(b->b, b->cap);
+  }
+  memcpy(b->b + b->n, p, n);
+  b->n += n;
+}
+static void jb_byte(jbuf *b, uint8_t c) { jb_push(b, &c, 1); }
+
+static void push_utf8(jbuf *b, uint32_t c) {
+  uint8_t t[4];
+  size_t k;
+  if (c < 0x80) {
+    t[0] = (uint8_t)c;
+    k = 1;
+  } else if (c < 0x800) {
+    t[0] = (uint8_t)(0xC0 | (c >> 6));
+    t[1] = (uint8_t)(0x80 | (c & 0x3F));
+    k = 2;
+  } else if (c < 0x10000) {
+    t[0] = (uint8_t)(0xE0 | (c >> 12));
+    t[1] = (uint8_t)(0x80 | ((c >> 6) & 0x3F));
+    t[2] = (uint8_t)(0x80 | (c & 0x3F));
+    k = 3;
+  } else {
+    t[0] = (uint8_t)(0xF0 | (c >> 18));
+    t[1] = (uint8_t)(0x80 | ((c >> 12) & 0x3F));
+    t[2] = (uint8_t)(0x80 | ((c >> 6) & 0x3F));
+    t[3] = (uint8_t)(0x80 | (c & 0x3F));
+    k = 4;
+  }
+  jb_push(b, t, k);
+}
+
+/* read.rs parse_escape (validate = true: deserializing a str) */
+static int parse_escape(jde *d, jbuf *scratch) {
+  int ch = jnext(d);
+  if (ch < 0) return jerror(d, E_EOF_STRING);
+  switch (ch) {
+    case '"': jb_byte(scratch, '"'); return 0;
+    case '\\': jb_byte(scratch, '\\'); return 0;
+    case '/': jb_byte(scratch, '/'); return 0;
+    case 'b': jb_byte(scratch, 0x08); return 0;
+    case 'f': jb_byte(scratch, 0x0c); return 0;
+    case 'n': jb_byte(scratch, '\n'); return 0;
+    case 'r': jb_byte(scratch, '\r'); return 0;
+    case 't': jb_byte(scratch, '\t'); return 0;
+    case 'u': {
+      uint32_t n1;
+      if (decode_hex_escape(d, &n1)) return -1;
+      if (n1 >= 0xDC00 && n1 <= 0xDFFF) return jerror(d, E_SURROGATE);
+      if (n1 >= 0xD800 && n1 <= 0xDBFF) {
+        int p = jpeek(d);
+        if (p < 0) return jerror(d, E_EOF_STRING);
+        if (p != '\\') {
+          jeat(d);
+          return jerror(d, E_HEX_END);
+        }
+        jeat(d);
+        p = jpeek(d);
+        if (p < 0) return jerror(d, E_EOF_STRING);
+        if (p != 'u') {
+          jeat(d);
+          return jerror(d, E_HEX_END);
+        }
+        jeat(d);
+        uint32_t n2;
+        if (decode_hex_escape(d, &n2)) return -1;
+        if (n2 < 0xDC00 || n2 > 0xDFFF) return jerror(d, E_SURROGATE);
+        push_utf8(scratch, (((n1 - 0xD800) << 10) | (n2 - 0xDC00)) + 0x10000);
+        return 0;
+      }
+      push_utf8(scratch, n1);
+      return 0;
+    }
+    default: return jerror(d, E_ESCAPE);
+  }
+}
+
+static int utf8_valid(const uint8_t *s, size_t n) {
+  size_t i = 0;
+  while (i < n) {
+    uint8_t c = s[i];
+    if (c < 0x80) {
+      i++;
+      continue;
+    }
+    size_t w;
+    uint32_t lo = 0x80, hi = 0xBF;
+    if (c >= 0xC2 && c <= 0xDF)
+      w = 2;
+    else if (c >= 0xE0 && c <= 0xEF) {
+      w = 3;
+      if (c == 0xE0) lo = 0xA0;
+      if (c == 0xED) hi = 0x9F;
+    } else if (c >= 0xF0 && c <= 0xF4) {
+      w = 4;
+      if (c == 0xF0) lo = 0x90;
+      if (c == 0xF4) hi = 0x8F;
+    } else
+      return 0;
+    if (i + w > n) return 0;
+    if (s[i + 1] < lo || s[i + 1] > hi) return 0;
+    for (size_t k = 2; k < w; k++)
+      if (s[i + k] < 0x80 || s[i + k] > 0xBF) return 0;
+    i += w;
+  }
+  return 1;
+}
+
+/* SliceRead::parse_str (after the opening quote was eaten): decoded UTF-8 string
+ * in *out (scratch or borrowed copy), caller frees out->b */
+static int parse_str(jde *d, jbuf *out) {
+  memset(out, 0, sizeof *out);
+  size_t start = d->i;
+  for (;;) {
+    while (d->i < d->n && !ESC(d->s[d->i])) d->i++;
+    if (d->i == d->n) return jerror(d, E_EOF_STRING);
+    int c = d->s[d->i];
+    if (c == '"') {
+      jb_push(out, d->s + start, d->i - start);
+      d->i++;
+      if (!utf8_valid(out->b, out->n)) return jerror(d, E_CODEPOINT);
+      return 0;
+    } else if (c == '\\') {
+      jb_push(out, d->s + start, d->i - start);
+      d->i++;
+      if (parse_escape(d, out)) return -1;
+      start = d->i;
+    } else {
+      d->i++;
+      return jerror(d, E_CONTROL);
+    }
+  }
+}
+
+/* read.rs ignore_escape / SliceRead::ignore_str (no UTF-8 validation) */
+static int ignore_escape(jde *d) {
+  int ch = jnext(d);
+  if (ch < 0) return jerror(d, E_EOF_STRING);
+  switch (ch) {
+    case '"': case '\\': case '/': case 'b': case 'f': case 'n': case 'r': case 't': return 0;
+    case 'u': {
+      uint32_t v;
+      return decode_hex_escape(d, &v);
+    }
+    default: return jerror(d, E_ESCAPE);
+  }
+}
+static int ignore_str(jde *d) {
+  for (;;) {
+    while (d->i < d->n && !ESC(d->s[d->i])) d->i++;
+    if (d->i == d->n) return jerror(d, E_EOF_STRING);
+    int c = d->s[d->i];
+    if (c == '"') {
+      d->i++;
+      return 0;
+    } else if (c == '\\') {
+      d->i++;
+      if (ignore_escape(d)) return -1;
+    } else {
+      return jerror(d, E_CONTROL);
+    }
+  }
+}
+
+/* ---- numbers */
+static int peek_or_null(jde *d) { int c = jpeek(d); return c < 0 ? 0 : c; }
+static int isdig(int c) { return c >= '0' && c <= '9'; }
+
+static int ignore_exponent(jde *d) {
+  jeat(d);
+  int c = peek_or_null(d);
+  if (c == '+' || c == '-') jeat(d);
+  c = jnext(d);
+  if (!isdig(c)) return jerror(d, E_NUMBER);
+  while (isdig(peek_or_null(d))) jeat(d);
+  return 0;
+}
+static int ignore_decimal(jde *d) {
+  jeat(d);
+  int any = 0;
+  while (isdig(peek_or_null(d))) {
+    jeat(d);
+    any = 1;
+  }
+  if (!any) return jpeek_error(d, E_NUMBER);
+  int c = peek_or_null(d);
+  if (c == 'e' || c == 'E') return ignore_exponent(d);
+  return 0;
+}
+static int ignore_integer(jde *d) {
+  int c = jnext(d);
+  if (c == '0') {
+    if (isdig(peek_or_null(d))) return jpeek_error(d, E_NUMBER);
+  } else if (c >= '1' && c <= '9') {
+    while (isdig(peek_or_null(d))) jeat(d);
+  } else {
+    return jerror(d, E_NUMBER);
+  }
+  c = peek_or_null(d);
+  if (c == '.') return ignore_decimal(d);
+  if (c == 'e' || c == 'E') return ignore_exponent(d);
+  return 0;
+}
+
+/* parse_integer / parse_number / parse_decimal / parse_exponent: the syntax and
+ * the reader movement exactly; a value that is a float (or -0, or an integer
+ * beyond u64/i64) marks the number as float (message outside the restatement) */
+typedef struct {
+  int is_float;
+  int neg;
+  uint64_t mag;
+} jnum;
+
+static int parse_exponent_syn(jde *d) {
+  jeat(d);
+  int c = peek_or_null(d);
+  if (c == '+' || c == '-') jeat(d);
+  int nx = jnext(d);
+  if (nx < 0) return jerror(d, E_EOF_VALUE);
+  if (!isdig(nx)) return jerror(d, E_NUMBER);
+  while (isdig(peek_or_null(d))) jeat(d);
+  return 0;
+}
+static int parse_decimal_syn(jde *d) {
+  jeat(d);
+  int any = 0;
+  while (isdig(peek_or_null(d))) {
+    jeat(d);
+    any = 1;
+  }
+  if (!any) {
+    if (jpeek(d) >= 0) return jpeek_error(d, E_NUMBER);
+    return jpeek_error(d, E_EOF_VALUE);
+  }
+  int c = peek_or_null(d);
+  if (c == 'e' || c == 'E') return parse_exponent_syn(d);
+  return 0;
+}
+static int parse_number_tail(jde *d, jnum *o) {
+  int c = peek_or_null(d);
+  if (c == '.') {
+    o->is_float = 1;
+    return parse_decimal_syn(d);
+  }
+  if (c == 'e' || c == 'E') {
+    o->is_float = 1;
+    return parse_exponent_syn(d);
+  }
+  if (o->neg && (o->mag == 0 || o->mag > (uint64_t)INT64_MAX + 1ull)) o->is_float = 1; /* -0 / underflow -> f64 */
+  return 0;
+}
+static int parse_integer(jde *d, int positive, jnum *o) {
+  memset(o, 0, sizeof *o);
+  o->neg = !positive;
+  int c = jnext(d);
+  if (c < 0) return jerror(d, E_EOF_VALUE);
+  if (c == '0') {
+    if (isdig(peek_or_null(d))) return jpeek_error(d, E_NUMBER);
+    return parse_number_tail(d, o);
+  }
+  if (c >= '1' && c <= '9') {
+    uint64_t sig = (uint64_t)(c - '0');
+    for (;;) {
+      int p = peek_or_null(d);
+      if (!isdig(p)) break;
+      uint64_t dg = (uint64_t)(p - '0');
+      if (sig > (UINT64_MAX - dg) / 10) {
+        /* parse_long_integer: the rest of the digits, then . / e as a float */
+        o->is_float = 1;
+        while (isdig(peek_or_null(d))) jeat(d);
+        int q = peek_or_null(d);
+        if (q == '.') return parse_decimal_syn(d);
+        if (q == 'e' || q == 'E') return parse_exponent_syn(d);
+        return 0;
+      }
+      jeat(d);
+      sig = sig * 10 + dg;
+    }
+    o->mag = sig;
+    return parse_number_tail(d, o);
+  }
+  return jerror(d, E_NUMBER);
+}
+
+/* Rust `{:?}` of a str, restricted to printable ASCII plus the escapes Rust
+ * uses for \t \r \n \" \\ and \0 (anything else: unsupported) */
+static int str_debug(jde *d, const jbuf *s, jbuf *out) {
+  memset(out, 0, sizeof *out);
+  jb_byte(out, '"');
+  for (size_t i = 0; i < s->n; i++) {
+    uint8_t c = s->b[i];
+    const char *e = NULL;
+    if (c == '"') e = "\\\"";
+    else if (c == '\\') e = "\\\\";
+    else if (c == '\n') e = "\\n";
+    else if (c == '\r') e = "\\r";
+    else if (c == '\t') e = "\\t";
+    else if (c == 0) e = "\\0";
+    if (e)
+      jb_push(out, (const uint8_t *)e, strlen(e));
+    else if (c >= 0x20 && c < 0x7f)
+      jb_byte(out, c);
+    else
+      return junsupported(d);
+  }
+  jb_byte(out, '"');
+  return 0;
+}
+
+/* de.rs peek_invalid_type */
+static int peek_invalid_type(jde *d, const char *expected) {
+  int c = jpeek(d);
+  if (c < 0) c = 0;
+  char unexp[64];
+  jbuf dbg = {0};
+  switch (c) {
+    case 'n':
+      jeat(d);
+      if (parse_ident(d, "ull")) return -1;
+      snprintf(unexp, sizeof unexp, "unit value");
+      break;
+    case 't':
+      jeat(d);
+      if (parse_ident(d, "rue")) return -1;
+      snprintf(unexp, sizeof unexp, "boolean `true`");
+      break;
+    case 'f':
+      jeat(d);
+      if (parse_ident(d, "alse")) return -1;
+      snprintf(unexp, sizeof unexp, "boolean `false`");
+      break;
+    case '-':
+    case '0': case '1': case '2': case '3': case '4': case '5': case '6': case '7': case '8': case '9': {
+      int pos = c != '-';
+      if (!pos) jeat(d);
+      jnum num;
+      if (parse_integer(d, pos, &num)) return -1;
+      if (num.is_float) return junsupported(d);
+      if (num.neg)
+        snprintf(unexp, sizeof unexp, "integer `-%llu`", (unsigned long long)num.mag);
+      else
+        snprintf(unexp, sizeof unexp, "integer `%llu`", (unsigned long long)num.mag);
+      break;
+    }
+    case '"': {
+      jeat(d);
+      jbuf sb;
+      if (parse_str(d, &sb)) {
+        free(sb.b);
+        return -1;
+      }
+      int r = str_debug(d, &sb, &dbg);
+      free(sb.b);
+      if (r) {
+        free(dbg.b);
+        return -1;
+      }
+      snprintf(unexp, sizeof unexp, "string ");
+      break;
+    }
+    case '[': snprintf(unexp, sizeof unexp, "sequence"); break;
+    case '{': snprintf(unexp, sizeof unexp, "map"); break;
+    default: return jpeek_error(d, E_VALUE);
+  }
+  char tail[160];
+  snprintf(tail, sizeof tail, ", expected %s", expected);
+  char head[96];
+  snprintf(head, sizeof head, "invalid type: %s", unexp);
+  jcustom_parts(d, head, dbg.b, dbg.n, tail);
+  free(dbg.b);
+  jfix_position(d);
+  return -1;
+}
+
+/* de.rs ignore_value (explicit frame stack, no recursion limit) */
+static int ignore_value(jde *d) {
+  char *stack = NULL;
+  size_t sn = 0, scap = 0;
+  int enclosing = 0; /* 0 none */
+  int rc = -1;
+#define PUSH(f)                                          \
+  do {                                                   \
+    if (sn == scap) {                                    \
+      scap = scap * 2 + 16;                              \
+      stack = (char *)realloc(stack, scap);              \
+    }                                                    \
+    stack[sn++] = (char)(f);                             \
+  } while (0)
+  for (;;) {
+    int peek = parse_whitespace(d);
+    if (peek < 0) {
+      jpeek_error(d, E_EOF_VALUE);
+      goto out;
+    }
+    int frame = 0; /* 0: scalar consumed */
+    switch (peek) {
+      case 'n': jeat(d); if (parse_ident(d, "ull")) goto out; break;
+      case 't': jeat(d); if (parse_ident(d, "rue")) goto out; break;
+      case 'f': jeat(d); if (parse_ident(d, "alse")) goto out; break;
+      case '-': jeat(d); if (ignore_integer(d)) goto out; break;
+      case '0': case '1': case '2': case '3': case '4': case '5': case '6': case '7': case '8': case '9':
+        if (ignore_integer(d)) goto out;
+        break;
+      case '"': jeat(d); if (ignore_str(d)) goto out; break;
+      case '[':
+      case '{':
+        /* the device path keeps ignore_value's frames in a 256-entry bit stack:
+         * deeper nesting is outside both restatements */
+        if (enclosing && sn >= 64) {
+          junsupported(d);
+          goto out;
+        }
+        if (enclosing) PUSH(enclosing);
+        enclosing = 0;
+        jeat(d);
+        frame = peek;
+        break;
+      default: jpeek_error(d, E_VALUE); goto out;
+    }
+    int accept_comma;
+    if (frame) {
+      accept_comma = 0;
+    } else if (enclosing) {
+      frame = enclosing;
+      enclosing = 0;
+      accept_comma = 1;
+    } else if (sn) {
+      frame = stack[--sn];
+      accept_comma = 1;
+    } else {
+      rc = 0;
+      goto out;
+    }
+    for (;;) {
+      int c = parse_whitespace(d);
+      if (c == ',' && accept_comma) {
+        jeat(d);
+        break;
+      } else if ((c == ']' && frame == '[') || (c == '}' && frame == '{')) {
+        /* fallthrough to close */
+      } else if (c >= 0) {
+        if (accept_comma) {
+          jpeek_error(d, frame == '[' ? E_LIST_COMMA : E_OBJ_COMMA);
+          goto out;
+        }
+        break;
+      } else {
+        jpeek_error(d, frame == '[' ? E_EOF_LIST : E_EOF_OBJECT);
+        goto out;
+      }
+      jeat(d);
+      if (!sn) {
+        rc = 0;
+        goto out;
+      }
+      frame = stack[--sn];
+      accept_comma = 1;
+    }
+    if (frame == '{') {
+      int c = parse_whitespace(d);
+      if (c == '"')
+        jeat(d);
+      else if (c >= 0) {
+        jpeek_error(d, E_KEY);
+        goto out;
+      } else {
+        jpeek_error(d, E_EOF_OBJECT);
+        goto out;
+      }
+      if (ignore_str(d)) goto out;
+      c = parse_whitespace(d);
+      if (c == ':')
+        jeat(d);
+      else if (c >= 0) {
+        jpeek_error(d, E_COLON);
+        goto out;
+      } else {
+        jpeek_error(d, E_EOF_OBJECT);
+        goto out;
+      }
+    }
+    enclosing = frame;
+  }
+out:
+#undef PUSH
+  free(stack);
+  return rc;
+}
+
+/* deserialize_str with a visitor: parses a string; returns it in *out */
+static int deserialize_str(jde *d, const char *expected, jbuf *out) {
+  memset(out, 0, sizeof *out);
+  int peek = parse_whitespace(d);
+  if (peek < 0) return jpeek_error(d, E_EOF_VALUE);
+  if (peek == '"') {
+    jeat(d);
+    if (parse_str(d, out)) return -1;
+    return 0;
+  }
+  peek_invalid_type(d, expected);
+  jfix_position(d);
+  return -1;
+}
+
+static void one_of(char *o, size_t cap, const char *const *names, int n) {
+  size_t k = 0;
+  if (n == 1) {
+    snprintf(o, cap, "`%s`", names[0]);
+    return;
+  }
+  if (n == 2) {
+    snprintf(o, cap, "`%s` or `%s`", names[0], names[1]);
+    return;
+  }
+  k += (size_t)snprintf(o + k, cap - k, "one of ");
+  for (int i = 0; i < n; i++) k += (size_t)snprintf(o + k, cap - k, "%s`%s`", i ? ", " : "", names[i]);
+}
+
+/* the variant identifier (deserialize_identifier -> deserialize_str, visitor
+ * "variant identifier"; unknown -> serde unknown_variant, fixed at the
+ * position after the string) */
+static int variant_ident(jde *d, const jfield *f, int *var) {
+  jbuf s;
+  if (deserialize_str(d, "variant identifier", &s)) {
+    free(s.b);
+    return -1;
+  }
+  for (int v = 0; v < f->nvariants; v++)
+    if (strlen(f->variants[v]) == s.n && !memcmp(f->variants[v], s.b, s.n)) {
+      *var = v;
+      free(s.b);
+      return 0;
+    }
+  /* the unknown value is displayed as-is (Display of a str) */
+  char names[512];
+  one_of(names, sizeof names, f->variants, f->nvariants);
+  char tail[560];
+  snprintf(tail, sizeof tail, "`, expected %s", names);
+  jcustom_parts(d, "unknown variant `", s.b, s.n, tail);
+  free(s.b);
+  jfix_position(d);
+  return -1;
+}
+
+/* de.rs deserialize_unit (the `()` of VariantAccess::unit_variant) */
+static int deserialize_unit(jde *d) {
+  int peek = parse_whitespace(d);
+  if (peek < 0) return jpeek_error(d, E_EOF_VALUE);
+  if (peek == 'n') {
+    jeat(d);
+    return parse_ident(d, "ull");
+  }
+  peek_invalid_type(d, "unit");
+  jfix_position(d);
+  return -1;
+}
+
+/* de.rs deserialize_enum for a unit-variant enum */
+static int deserialize_enum(jde *d, const jfield *f, int *var) {
+  int peek = parse_whitespace(d);
+  if (peek == '{') {
+    if (--d->depth == 0) return jpeek_error(d, E_RECURSION);
+    jeat(d);
+    /* VariantAccess::variant_seed: identifier, then parse_object_colon */
+    if (variant_ident(d, f, var)) return -1;
+    int c = parse_whitespace(d);
+    if (c == ':')
+      jeat(d);
+    else if (c >= 0)
+      return jpeek_error(d, E_COLON);
+    else
+      return jpeek_error(d, E_EOF_OBJECT);
+    /* unit_variant: Deserialize for () */
+    if (deserialize_unit(d)) return -1;
+    d->depth++;
+    c = parse_whitespace(d);
+    if (c == '}') {
+      jeat(d);
+      return 0;
+    }
+    if (c >= 0) return jerror(d, E_VALUE);
+    return jerror(d, E_EOF_OBJECT);
+  }
+  if (peek == '"') return variant_ident(d, f, var); /* UnitVariantAccess */
+  if (peek >= 0) return jpeek_error(d, E_VALUE);
+  return jpeek_error(d, E_EOF_VALUE);
+}
+
+/* one field value (next_value_seed after parse_object_colon, or a seq element) */
+static int field_value(jde *d, const jfield *f, int *enum_out) {
+  if (f->type == JF_ENUM) return deserialize_enum(d, f, enum_out);
+  jbuf s;
+  int r = deserialize_str(d, "a string", &s);
+  free(s.b);
+  return r;
+}
+
+static int end_map(jde *d) {
+  int c = parse_whitespace(d);
+  if (c == '}') {
+    jeat(d);
+    return 0;
+  }
+  if (c == ',') return jpeek_error(d, E_TRAILING_COMMA);
+  if (c >= 0) return jpeek_error(d, E_TRAILING);
+  return jpeek_error(d, E_EOF_OBJECT);
+}
+static int end_seq(jde *d) {
+  int c = parse_whitespace(d);
+  if (c == ']') {
+    jeat(d);
+    return 0;
+  }
+  if (c == ',') {
+    jeat(d);
+    int p = parse_whitespace(d);
+    if (p == ']') return jpeek_error(d, E_TRAILING_COMMA);
+    return jpeek_error(d, E_TRAILING);
+  }
+  if (c >= 0) return jpeek_error(d, E_TRAILING);
+  return jpeek_error(d, E_EOF_LIST);
+}
+
+/* the derive's visit_map: fields by name, duplicates and missing fields are
+ * errors in declaration order, unknown keys are IgnoredAny */
+static int visit_map(jde *d, const jstruct *st, int *vals) {
+  int seen[8] = {0};
+  int first = 1;
+  for (;;) {
+    /* MapAccess::next_key_seed */
+    int peek = parse_whitespace(d);
+    if (peek == '}') break;
+    if (peek == ',' && !first) {
+      jeat(d);
+      peek = parse_whitespace(d);
+    } else if (peek >= 0) {
+      if (first)
+        first = 0;
+      else
+        return jpeek_error(d, E_OBJ_COMMA);
+    } else {
+      return jpeek_error(d, E_EOF_OBJECT);
+    }
+    if (peek == '}') return jpeek_error(d, E_TRAILING_COMMA);
+    if (peek < 0) return jpeek_error(d, E_EOF_VALUE);
+    if (peek != '"') return jpeek_error(d, E_KEY);
+    jeat(d); /* MapKey::deserialize_any */
+    jbuf key;
+    if (parse_str(d, &key)) {
+      free(key.b);
+      return -1;
+    }
+    int fi = -1;
+    for (int k = 0; k < st->nfields; k++)
+      if (strlen(st->fields[k].name) == key.n && !memcmp(st->fields[k].name, key.b, key.n)) fi = k;
+    free(key.b);
+    if (fi >= 0 && seen[fi]) return jcustom(d, "duplicate field `%s`", st->fields[fi].name);
+    /* MapAccess::next_value_seed */
+    int c = parse_whitespace(d);
+    if (c == ':')
+      jeat(d);
+    else if (c >= 0)
+      return jpeek_error(d, E_COLON);
+    else
+      return jpeek_error(d, E_EOF_OBJECT);
+    if (fi < 0) {
+      if (ignore_value(d)) return -1;
+    } else {
+      if (field_value(d, &st->fields[fi], &vals[fi])) return -1;
+      seen[fi] = 1;
+    }
+  }
+  for (int k = 0; k < st->nfields; k++)
+    if (!seen[k]) return jcustom(d, "missing field `%s`", st->fields[k].name);
+  return 0;
+}
+
+/* the derive's visit_seq: fields in order, a missing element is invalid_length */
+static int visit_seq(jde *d, const jstruct *st, int *vals) {
+  int first = 1;
+  for (int k = 0; k < st->nfields; k++) {
+    int peek = parse_whitespace(d);
+    int none = 0;
+    if (peek == ']')
+      none = 1;
+    else if (peek == ',' && !first) {
+      jeat(d);
+      peek = parse_whitespace(d);
+    } else if (peek >= 0) {
+      if (first)
+        first = 0;
+      else
+        return jpeek_error(d, E_LIST_COMMA);
+    } else {
+      return jpeek_error(d, E_EOF_LIST);
+    }
+    if (!none) {
+      if (peek == ']') return jpeek_error(d, E_TRAILING_COMMA);
+      if (peek < 0) return jpeek_error(d, E_EOF_VALUE);
+      if (field_value(d, &st->fields[k], &vals[k])) return -1;
+    } else {
+      return jcustom(d, "invalid length %d, expected struct %s with %d elements", k, st->name, st->nfields);
+    }
+  }
+  return 0;
+}
+
+static int deserialize_struct(jde *d, const jstruct *st, int *vals) {
+  int peek = parse_whitespace(d);
+  if (peek < 0) return jpeek_error(d, E_EOF_VALUE);
+  int r;
+  if (peek == '[' || peek == '{') {
+    if (--d->depth == 0) return jpeek_error(d, E_RECURSION);
+    jeat(d);
+    r = peek == '[' ? visit_seq(d, st, vals) : visit_map(d, st, vals);
+    d->depth++;
+    /* match (ret, self.end_seq()/end_map()): the end check runs either way;
+     * the visitor's error wins */
+    if (r) {
+      /* keep the visitor's error, but let the end check move the reader */
+      jde probe = *d;
+      probe.msg = NULL;
+      probe.msg_len = 0;
+      probe.failed = 0;
+      (void)(peek == '[' ? end_seq(&probe) : end_map(&probe));
+      free(probe.msg);
+      d->i = probe.i;
+    } else {
+      r = peek == '[' ? end_seq(d) : end_map(d);
+    }
+  } else {
+    char exp[128];
+    snprintf(exp, sizeof exp, "struct %s", st->name);
+    peek_invalid_type(d, exp);
+    r = -1;
+  }
+  if (r) jfix_position(d);
+  return r;
+}
+
+static char *render(jde *d, size_t *len) {
+  size_t line = 1, col = 0;
+  for (size_t i = 0; i < d->err_index && i < d->n; i++) {
+    if (d->s[i] == '\n') {
+      line++;
+      col = 0;
+    } else {
+      col++;
+    }
+  }
+  char *m = (char *)malloc(d->msg_len + 64);
+  memcpy(m, d->msg, d->msg_len);
+  size_t k = d->msg_len;
+  if (d->has_pos) k += (size_t)sprintf(m + k, " at line %zu column %zu", line, col);
+  m[k] = 0;
+  *len = k;
+  return m;
+}
+
+/* serde_json::from_slice::<struct>: 0 ok, 1 error (*msg), ORC_E_UNSUPPORTED */
+static int from_slice_struct(const uint8_t *s, size_t n, const jstruct *st, int *vals, char **msg,
+                             size_t *msg_len) {
+  jde d;
+  memset(&d, 0, sizeof d);
+  d.s = s;
+  d.n = n;
+  d.depth = 128;
+  *msg = NULL;
+  int r = deserialize_struct(&d, st, vals);
+  if (!r) {
+    /* Deserializer::end */
+    if (parse_whitespace(&d) >= 0) r = jpeek_error(&d, E_TRAILING);
+  }
+  if (!r) {
+    free(d.msg);
+    return 0;
+  }
+  if (d.unsupported) {
+    free(d.msg);
+    return ORC_E_UNSUPPORTED;
+  }
+  *msg = render(&d, msg_len);
+  free(d.msg);
+  if (memchr(*msg, 0, *msg_len)) { /* a NUL inside the text: the C-string hint plumbing cannot carry it */
+    free(*msg);
+    *msg = NULL;
+    return ORC_E_UNSUPPORTED;
+  }
+  return 1;
+}
+
+static const char *const LOG_LEVELS[] = {"debug", "info", "warn", "error"};
+static const jfield STRUCTURED_LOG_FIELDS[] = {
+    {"level", JF_ENUM, LOG_LEVELS, 4},
+    {"message", JF_STRING, NULL, 0},
+};
+static const jstruct STRUCTURED_LOG = {"StructuredLog", STRUCTURED_LOG_FIELDS, 2};
+
+int orc_json_structured_log(const uint8_t *s, size_t n, int *level, char **msg, size_t *msg_len) {
+  int vals[2] = {0, 0};
+  int r = from_slice_struct(s, n, &STRUCTURED_LOG, vals, msg, msg_len);
+  if (r == 0) *level = vals[0];
+  return r;
+}
+
+/* generic entry for pinning against other serde_json fixtures of the reference:
+ * fields as "name" (string) or "name=v1|v2|.." (unit enum) */
+int orc_json_struct(const uint8_t *s, size_t n, const char *name, const char **fields, int nfields, int *vals,
+                    char **msg, size_t *msg_len) {
+  jfield f[8];
+  char *vbuf[8] = {0};
+  const char *vars[8][16];
+  if (nfields > 8) return ORC_E_INVALID_ARG;
+  char *names[8];
+  for (int k = 0; k < nfields; k++) {
+    const char *eq = strchr(fields[k], '=');
+    if (!eq) {
+      names[k] = strdup(fields[k]);
+      f[k].name = names[k];
+      f[k].type = JF_STRING;
+      f[k].variants = NULL;
+      f[k].nvariants = 0;
+      continue;
+    }
+    names[k] = strndup(fields[k], (size_t)(eq - fields[k]));
+    f[k].name = names[k];
+    f[k].type = JF_ENUM;
+    vbuf[k] = strdup(eq + 1);
+    int nv = 0;
+    for (char *p = strtok(vbuf[k], "|"); p && nv < 16; p = strtok(NULL, "|")) vars[k][nv++] = p;
+    f[k].variants = vars[k];
+    f[k].nvariants = nv;
+  }
+  jstruct st = {name, f, nfields};
+  int r = from_slice_struct(s, n, &st, vals, msg, msg_len);
+  for (int k = 0; k < nfields; k++) {
+    free(names[k]);
+    free(vbuf[k]);
+  }
+  return r;
+}

@@ -1113,6 +1113,7 @@ enum {
   M_FILTER_MAP_EVEN_HALF,
   M_AGG_SUM,
   M_AGG_CONCAT,
+  M_FILTER_JSON, /* examples/filter_json: StructuredLog.level > Debug */
 };
 
 typedef struct {
@@ -1199,6 +1200,9 @@ int orc_chain_add(orc_chain *c, const char *module, const char **keys, const cha
       return rc;
     }
     s.mod = M_FILTER_REGEX;
+    s.kind = K_FILTER;
+  } else if (!strcmp(module, "filter_json")) {
+    s.mod = M_FILTER_JSON;
     s.kind = K_FILTER;
   } else if (!strcmp(module, "filter_odd")) {
     s.mod = M_FILTER_ODD;
@@ -1298,6 +1302,22 @@ static void stage_run(stage_t *s, recvec *in, int64_t base_offset, stage_out *o)
           return;
         }
         keep = s->rx_keep_match ? m : !m;
+        break;
+      }
+      case M_FILTER_JSON: {
+        int level = 0;
+        size_t ml = 0;
+        char *m = NULL;
+        int jr = orc_json_structured_log(r->val, r->val_len, &level, &m, &ml);
+        if (jr == ORC_E_UNSUPPORTED) {
+          o->unsupported = 1;
+          return;
+        }
+        if (jr) {
+          hint = m; /* serde_json::Error Display */
+          break;
+        }
+        keep = level > 0;
         break;
       }
       case M_FILTER_ODD: {

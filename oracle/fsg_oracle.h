@@ -84,6 +84,15 @@ void orc_free(void *p);
 /* regex oracle exposed for cross-checks with an independent engine */
 int orc_regex_is_match(const char *pattern, const uint8_t *text, size_t n, int *is_match);
 
+/* serde_json 1.0.96 from_slice::<StructuredLog> (fsg_json.c): 0 ok (*level =
+ * 0 debug .. 3 error), 1 error (*msg / *msg_len: Display text, free with
+ * orc_free), ORC_E_UNSUPPORTED */
+int orc_json_structured_log(const uint8_t *s, size_t n, int *level, char **msg, size_t *msg_len);
+/* generic derive(Deserialize) struct: fields "name" (String) or "name=a|b|c"
+ * (unit enum, rename_all lowercase names), for the reference's other fixtures */
+int orc_json_struct(const uint8_t *s, size_t n, const char *name, const char **fields, int nfields, int *vals,
+                    char **msg, size_t *msg_len);
+
 #ifdef __cplusplus
 }
 #endif

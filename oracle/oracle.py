@@ -70,6 +70,11 @@ def lib():
         L.orc_free.argtypes = [ctypes.c_void_p]
         L.orc_regex_is_match.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t,
                                          ctypes.POINTER(ctypes.c_int)]
+        L.orc_json_structured_log.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int),
+                                              ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]
+        L.orc_json_struct.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                      ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                      ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]
         L.orc_varint_encode.restype = ctypes.c_size_t
         L.orc_varint_encode.argtypes = [ctypes.c_int64, ctypes.c_char_p]
         _lib = L
@@ -92,6 +97,38 @@ def regex_is_match(pattern: str, text: bytes) -> bool:
     if rc:
         raise ValueError(f"oracle regex status {rc}")
     return bool(m.value)
+
+
+def _json_result(rc, msg, ml):
+    if rc == 0:
+        return None
+    if rc == 1:
+        text = ctypes.string_at(msg.value, ml.value)
+        lib().orc_free(msg)
+        return text.decode("utf-8", "replace") if isinstance(text, bytes) else text
+    raise OracleError(rc, "outside the serde_json restatement")
+
+
+def json_structured_log(value: bytes):
+    """serde_json::from_slice::<StructuredLog>: ("ok", level 0..3) or ("err", Display text)."""
+    lv = ctypes.c_int(0)
+    msg = ctypes.c_void_p()
+    ml = ctypes.c_size_t(0)
+    rc = lib().orc_json_structured_log(value, len(value), ctypes.byref(lv), ctypes.byref(msg), ctypes.byref(ml))
+    err = _json_result(rc, msg, ml)
+    return ("ok", lv.value) if err is None else ("err", err)
+
+
+def json_struct(value: bytes, name: str, fields):
+    """Generic derive(Deserialize) struct (fields "f" = String, "f=a|b" = unit enum)."""
+    arr = (ctypes.c_char_p * len(fields))(*[f.encode() for f in fields])
+    vals = (ctypes.c_int * len(fields))()
+    msg = ctypes.c_void_p()
+    ml = ctypes.c_size_t(0)
+    rc = lib().orc_json_struct(value, len(value), name.encode(), arr, len(fields), vals, ctypes.byref(msg),
+                               ctypes.byref(ml))
+    err = _json_result(rc, msg, ml)
+    return ("ok", list(vals)) if err is None else ("err", err)
 
 
 class OracleError(Exception):

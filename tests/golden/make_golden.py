@@ -196,6 +196,26 @@ def main():
                 "expect": {"base_offset": 0, "n_records": 2, "values": ["11", "22"]}})
     k["process_batch"] = spu
 
+    # serde / serde_json error texts asserted by the reference's own tests (the
+    # JSON-field filter's error hints are serde_json::Error Display strings)
+    k["serde_json"] = [
+        {"name": "missing_field_position",
+         "source": "crates/fluvio-version-manager/src/common/manifest.rs:88-101 (serde_json::from_str)",
+         "input": '{\n"foo": "bar",\n"hello": "world"\n}', "struct": "VersionManifest",
+         "fields": ["channel=stable|latest", "version"],
+         "expect": "missing field `channel` at line 4 column 1", "match": "exact"},
+        {"name": "unknown_variant_one_of",
+         "source": "crates/fluvio-connector-package/src/config/mod.rs:738-742 (serde::de::Error::unknown_variant)",
+         "input": '{"compression":"gzipaoeu"}', "struct": "ProducerParameters",
+         "fields": ["compression=none|gzip|snappy|lz4|zstd"],
+         "expect": "unknown variant `gzipaoeu`, expected one of `none`, `gzip`, `snappy`, `lz4`, `zstd`",
+         "match": "prefix"},
+        {"name": "unexpected_string_debug",
+         "source": "crates/fluvio-connector-package/src/config/mod.rs:746-750 (serde::de::Unexpected::Str)",
+         "input": '"1aoeu"', "struct": "Batch", "fields": ["size"],
+         "expect": 'string "1aoeu"', "match": "contains"},
+    ]
+
     with open(OUT, "w") as f:
         json.dump(k, f, indent=1, sort_keys=True)
     print("wrote", OUT)

@@ -175,6 +175,10 @@ CHAINS = {
     "regex_unbounded": [("regex-filter", {"regex": r"a.*c\d+$"}, None)],
     "regex_unicode": [("regex-filter", {"regex": r"é|\d\d"}, None)],
     "map": [("map", {}, None)],
+    "filter_json": [("filter_json", {}, None)],
+    "filter_json_then_map": [("filter_json", {}, None), ("map", {}, None)],
+    "map_then_filter_json": [("map", {}, None), ("filter_json", {}, None)],
+    "double_then_filter_json": [("map_double", {}, None), ("filter_json", {}, None)],
     "filter_then_map": [("filter_init", {"key": "timeout"}, None), ("map", {}, None)],
     "map_then_filter": [("map", {}, None), ("filter_init", {"key": "TIMEOUT"}, None)],
     "map_then_lower_filter": [("map", {}, None), ("filter_init", {"key": "timeout"}, None)],
@@ -318,3 +322,50 @@ def test_large_output_crc(engine):
     assert struct.unpack(">I", out[17:21])[0] == O.crc32c(out[21:])
     o = orc_chain(CHAINS["map"]).process_batch(sl.tobytes())
     assert out == o["bytes"]
+
+
+# ---------------------------------------------------------------------------
+# JSON-field filter (examples/filter_json): serde_json semantics incl. error hints
+# ---------------------------------------------------------------------------
+def _one_record_slice(value: bytes, base: int = 0) -> bytes:
+    b = P.Batch(base_offset=base)
+    b.add_record(P.Record.new(value))
+    return b.encode()
+
+
+def test_filter_json_fuzz_one_record(engine):
+    """Every document of the corpus (valid, mutated, hand-picked error cases) as a
+    one-record batch: output, error hint text, offset and value bit-exact."""
+    from tests import jsongen
+    for doc in jsongen.corpus(7, 150, 450):
+        check_batch(engine, CHAINS["filter_json"], _one_record_slice(doc))
+
+
+def test_filter_json_first_error_in_stream(engine):
+    from tests import jsongen
+    import random
+    rng = random.Random(11)
+    good = [jsongen.valid_doc(rng).encode() for _ in range(400)]
+    bad = [b'{"level":"info","message":5}', b'{"level":"nope","message":"m"}', b"[1,2",
+           b'{"level":"warn","message":"x"} trailing']
+    sl = b""
+    base = 0
+    for k in range(40):
+        b = P.Batch(base_offset=base)
+        for j in range(10):
+            v = good[k * 10 + j]
+            if k == 23 and j == 6:
+                v = bad[k % len(bad)]
+            b.add_record(P.Record.new(v))
+        sl += b.encode()
+        base += 10
+    for chain in ("filter_json", "filter_json_then_map", "map_then_filter_json"):
+        check_batch(engine, CHAINS[chain], sl)
+        check_batch(engine, CHAINS[chain], sl, max_bytes=20000)
+
+
+def test_filter_json_synthetic_logs(engine):
+    """C2 records are StructuredLog documents: keep level > debug."""
+    sl = synth.make_slice(2, 3000)
+    out = check_batch(engine, CHAINS["filter_json"], sl)
+    assert 0 < out.n_records < 3000

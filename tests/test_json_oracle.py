@@ -1,0 +1,123 @@
+"""The serde_json restatement in oracle/fsg_json.c (test infrastructure):
+pinned by the serde / serde_json error texts the reference's own tests assert,
+and cross-checked against Python's independent `json` parser on the
+accept/reject decision and the decoded level (error *texts* beyond the pinned
+fixtures follow serde_json 1.0.96's source)."""
+import json
+
+import pytest
+
+from oracle import oracle as O
+from tests import jsongen
+
+LEVELS = jsongen.LEVELS
+
+
+def test_reference_serde_fixtures(kats):
+    for case in kats["serde_json"]:
+        st, msg = O.json_struct(case["input"].encode(), case["struct"], case["fields"])
+        assert st == "err", case["name"]
+        if case["match"] == "exact":
+            assert msg == case["expect"], case["name"]
+        elif case["match"] == "prefix":
+            assert msg.startswith(case["expect"]), (case["name"], msg)
+        else:
+            assert case["expect"] in msg, (case["name"], msg)
+
+
+class Pairs(list):
+    pass
+
+
+def _lone_surrogate(s):
+    return isinstance(s, str) and any(0xD800 <= ord(c) <= 0xDFFF for c in s)
+
+
+def _level(v):
+    """LogLevel from a decoded JSON value: index, or None (error), or 'skip'."""
+    if isinstance(v, str):
+        if _lone_surrogate(v):
+            return "skip"
+        return LEVELS.index(v) if v in LEVELS else None
+    if isinstance(v, Pairs):  # {"variant": null}
+        if len(v) != 1:
+            return None
+        k, x = v[0]
+        if _lone_surrogate(k):
+            return "skip"
+        return LEVELS.index(k) if (k in LEVELS and x is None) else None
+    return None
+
+
+def python_verdict(doc: bytes):
+    """("ok", level) / ("err",) by Python's json, or None where the two libraries'
+    rules differ by design (non-ASCII, lone surrogates, NaN/Infinity)."""
+    if any(b >= 0x80 for b in doc) or b"NaN" in doc or b"Infinity" in doc:
+        return None
+    try:
+        v = json.loads(doc, object_pairs_hook=Pairs)
+    except RecursionError:
+        return None
+    except ValueError:
+        return ("err",)
+    if isinstance(v, Pairs):
+        seen = {}
+        for k, x in v:
+            if _lone_surrogate(k):
+                return None
+            if k in ("level", "message"):
+                if k in seen:
+                    return ("err",)  # duplicate field
+                seen[k] = x
+        if "level" not in seen or "message" not in seen:
+            return ("err",)
+        lv, msg = _level(seen["level"]), seen["message"]
+    elif isinstance(v, list):
+        if len(v) != 2:
+            return ("err",)
+        lv, msg = _level(v[0]), v[1]
+    else:
+        return ("err",)
+    if lv == "skip" or _lone_surrogate(msg):
+        return None
+    if lv is None or not isinstance(msg, str):
+        return ("err",)
+    return ("ok", lv)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_oracle_matches_python_json(seed):
+    checked = 0
+    for doc in jsongen.corpus(seed, 300, 900):
+        pv = python_verdict(doc)
+        if pv is None:
+            continue
+        try:
+            ov = O.json_structured_log(doc)
+        except O.OracleError:
+            continue  # outside the restatement (float / Debug-escaped text)
+        assert ov[0] == pv[0], (doc, ov, pv)
+        if pv[0] == "ok":
+            assert ov[1] == pv[1], (doc, ov, pv)
+        checked += 1
+    assert checked > 900
+
+
+def test_oracle_error_texts():
+    """serde_json Display strings for the error kinds (positions as serde_json's
+    position_of_index of the reader index when the error is raised)."""
+    cases = {
+        b'': "EOF while parsing a value at line 1 column 0",
+        b'{"level":"info"}': "missing field `message` at line 1 column 16",
+        b'{"level":"info","level":"warn","message":"x"}': "duplicate field `level` at line 1 column 23",
+        b'["warn"]': "invalid length 1, expected struct StructuredLog with 2 elements at line 1 column 8",
+        b'{"level":"INFO","message":"m"}':
+            "unknown variant `INFO`, expected one of `debug`, `info`, `warn`, `error` at line 1 column 15",
+        b'"hello"': 'invalid type: string "hello", expected struct StructuredLog at line 1 column 7',
+        b'{"level":"info","message":5}': "invalid type: integer `5`, expected a string at line 1 column 27",
+        b'{"level":"info","message":"x"} x': "trailing characters at line 1 column 32",
+        b'{"level":"info","message":"x",}': "trailing comma at line 1 column 31",
+        b'\n\n  {"level"\n:\n"info"}': "missing field `message` at line 5 column 7",
+    }
+    for doc, want in cases.items():
+        assert O.json_structured_log(doc) == ("err", want), doc
