@@ -523,40 +523,29 @@ __device__ __forceinline__ uint32_t swar_upper(uint32_t x) {
 }
 // Data-parallel substring scan + non-ASCII marking over the values of the window.
 // Marks RF_MATCH on records whose (optionally uppercased) value contains needle.
-// Each lane takes 16-byte chunks (32 bytes loaded with two ds_read_b128 from the
-// LDS window).  Filter: needle[0] at p AND needle[m-1] at p+m-1, four positions
-// per u32 with an exact SWAR zero-byte test (the last-byte view is one
-// v_alignbyte per word); surviving positions are verified byte by byte.  A wave
-// pays for its worst lane's candidate count only, not for a full-needle SWAR
-// evaluation of every chunk.
-// Q >= 0: compile-time word offset; Q < 0: runtime offset q (global-memory path)
-template <int Q>
-__device__ __forceinline__ uint32_t last_view(const uint32_t (&w)[8], int k, uint32_t sh, uint32_t q) {
-  if constexpr (Q >= 0) {
-    return __builtin_amdgcn_alignbyte(w[k + Q + 1], w[k + Q], sh);
-  } else {
-    uint32_t a = w[k], b = w[k + 1];
-    for (uint32_t t = 1; t <= 3; t++)
-      if (q >= t) {
-        a = w[k + t];
-        b = w[k + t + 1];
-      }
-    return __builtin_amdgcn_alignbyte(b, a, sh);
-  }
+// Each lane takes 16-byte chunks (32 bytes from two ds_read_b128 of the LDS
+// window).  Filter: the 4-byte window at each of the 16 positions is compared
+// with the needle's first min(m, 4) bytes (one v_alignbyte + one compare per
+// position); the compares are OR-ed as wave ballots on the scalar unit, so a
+// wave with no 4-gram hit anywhere pays ~2 VALU per position and moves on.
+// Lanes with a hit rebuild their position mask and verify the rest of the
+// needle byte by byte.
+__device__ __forceinline__ uint32_t win_at(const uint32_t (&w)[8], int j) {
+  const int k = j >> 2, a = j & 3;
+  return a ? __builtin_amdgcn_alignbyte(w[k + 1], w[k], (uint32_t)a) : w[k];
 }
-template <int Q, bool kLds, typename P>
-__device__ __forceinline__ void scan_contains_q(WaveLds& L, P w, int nr, const uint8_t* needle, uint32_t m,
-                                                bool upper, bool mark_nonascii) {
+template <bool kLds, typename P>
+__device__ __forceinline__ void scan_contains(WaveLds& L, P w, uint32_t wlen, int nr, const uint8_t* needle,
+                                              uint32_t m, bool upper, bool mark_nonascii) {
+  (void)wlen;
+  if (nr == 0) return;
   const uint32_t lo = L.r_vs[0];
   const uint32_t hi = L.r_vs[nr - 1] + L.r_vl[nr - 1];
   const uint32_t l = threadIdx.x;
-  const uint32_t nf = m ? 0x01010101u * needle[0] : 0u;
-  // filter bytes: needle[0] and needle[mf-1] (mf = min(m, 16): the 32-byte chunk
-  // holds positions p..p+15 of each of the 16 starts)
-  const uint32_t mf = m < 16 ? m : 16;
-  const uint32_t nl = m ? 0x01010101u * needle[mf - 1] : 0u;
-  const uint32_t sh = m ? (mf - 1) & 3 : 0;
-  const uint32_t vend = m > 16 ? m : (m ? m - 1 : 0);  // verify needle[1..vend)
+  const uint32_t m4 = m < 4 ? m : 4;
+  uint32_t n4 = 0;
+  for (uint32_t t = 0; t < m4; t++) n4 |= (uint32_t)needle[t] << (8 * t);
+  const uint32_t k4 = m4 == 4 ? 0xFFFFFFFFu : ((1u << (8 * m4)) - 1u);
   for (uint32_t c = (lo & ~15u) + l * 16; c < hi; c += kEvalThreads * 16) {
     uint32_t wd[8];
     if constexpr (kLds) {
@@ -585,54 +574,32 @@ __device__ __forceinline__ void scan_contains_q(WaveLds& L, P w, int nr, const u
 #endif
     if (upper)
       for (int k = 0; k < 8; k++) wd[k] = swar_upper(wd[k]);
-    uint32_t acc[4];
+    uint64_t any = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) acc[k] = zbytes(wd[k] ^ nf) & zbytes(last_view<Q>(wd, k, sh, (mf - 1) >> 2) ^ nl);
-    if (!(acc[0] | acc[1] | acc[2] | acc[3])) continue;
-    for (int k = 0; k < 4; k++) {
-      uint32_t cand = acc[k];
-      while (cand) {
-        const int j = __builtin_ctz(cand) >> 3;
-        cand &= cand - 1;
-        const uint32_t p = c + 4 * k + j;
-        if (p < lo || p >= hi) continue;
-        const int r = find_rec(L, nr, p);
-        if (r < 0) continue;
-        const uint32_t ve = L.r_vs[r] + L.r_vl[r];
-        if (p + m > ve) continue;
-        bool ok = true;
-        for (uint32_t t = 1; t < vend; t++) {
-          uint8_t y = kLds ? L.win[p + t] : w[p + t];
-          if (upper) y = up(y);
-          if (y != needle[t]) {
-            ok = false;
-            break;
-          }
+    for (int j = 0; j < 16; j++) any |= __ballot(((win_at(wd, j) ^ n4) & k4) == 0);
+    if (!any) continue;                    // wave-uniform: no 4-gram hit in any lane
+    if (!((any >> (l & 63)) & 1)) continue;  // this lane has no hit
+    uint32_t cand = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) cand |= (uint32_t)(((win_at(wd, j) ^ n4) & k4) == 0) << j;
+    while (cand) {
+      const uint32_t p = c + (uint32_t)__builtin_ctz(cand);
+      cand &= cand - 1;
+      if (p < lo || p >= hi) continue;
+      const int r = find_rec(L, nr, p);
+      if (r < 0) continue;
+      if (p + m > L.r_vs[r] + L.r_vl[r]) continue;
+      bool ok = true;
+      for (uint32_t t = 4; t < m; t++) {
+        uint8_t y = kLds ? L.win[p + t] : w[p + t];
+        if (upper) y = up(y);
+        if (y != needle[t]) {
+          ok = false;
+          break;
         }
-        if (ok) atomicOr(&L.r_flags[r], RF_MATCH);
       }
+      if (ok) atomicOr(&L.r_flags[r], RF_MATCH);
     }
-  }
-}
-
-template <bool kLds, typename P>
-__device__ __forceinline__ void scan_contains(WaveLds& L, P w, uint32_t wlen, int nr, const uint8_t* needle,
-                                              uint32_t m, bool upper, bool mark_nonascii) {
-  (void)wlen;
-  if (nr == 0) return;
-  // the last-byte view reads words k + (mf-1)/4 and k + (mf-1)/4 + 1 of the
-  // 8-word chunk: wave-uniform dispatch on that word offset
-  const uint32_t mf = m < 16 ? m : 16;
-  const uint32_t q = mf ? ((mf - 1) >> 2) : 0;
-  if constexpr (!kLds) {
-    scan_contains_q<-1, kLds>(L, w, nr, needle, m, upper, mark_nonascii);
-    return;
-  }
-  switch (q) {
-    case 0: scan_contains_q<0, kLds>(L, w, nr, needle, m, upper, mark_nonascii); break;
-    case 1: scan_contains_q<1, kLds>(L, w, nr, needle, m, upper, mark_nonascii); break;
-    case 2: scan_contains_q<2, kLds>(L, w, nr, needle, m, upper, mark_nonascii); break;
-    default: scan_contains_q<3, kLds>(L, w, nr, needle, m, upper, mark_nonascii); break;
   }
 }
 
