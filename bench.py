@@ -118,6 +118,15 @@ def main():
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     pipe_gbps = (in_bytes + out_bytes) / (per["total_ms"] * 1e-3) / 1e9
 
+    traffic, traffic_src = None, None
+    tpath = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tpath):  # PMC HBM bytes per launch of the same command (scripts/traffic_from_pmc.py)
+        db = json.load(open(tpath)).get(a.workload)
+        if db:
+            for kname, v in db["kernels"].items():
+                if kname.split("<")[0] == "fsg::" + dom:
+                    traffic, traffic_src = v["total"], db["source"]
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle.oracle import OracleChain
@@ -161,7 +170,7 @@ def main():
             "gbps_pipeline": pipe_gbps,
             "gbps_input": in_bytes * world * steps / elapsed / 1e9,
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": peak, "unit": "GB/s",
-                         "frac": achieved / peak, "traffic": None,
+                         "frac": achieved / peak, "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": dom_ms},
             "kernel_ms": per,
             "cpu_baseline": cpu,

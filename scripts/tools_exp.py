@@ -2,7 +2,7 @@
 library build (FSG_LIB) and print the kernel timings (for rocprofv3 counter
 attribution between experiment builds)."""
 import json, os, sys
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fluvio_amd import synth
 from fluvio_amd.smartengine import *
 kind = int(sys.argv[1]); mod = sys.argv[2]; params = json.loads(sys.argv[3]); n = int(sys.argv[4])

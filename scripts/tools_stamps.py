@@ -1,7 +1,7 @@
 """Diagnostic: per-phase cycle shares of k_eval (stamped build, FSG_LIB=libfsg_stamps.so)."""
 import ctypes, os, sys, json
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-os.environ["FSG_LIB"] = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fluvio_amd", "_lib", "libfsg_stamps.so")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ["FSG_LIB"] = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "fluvio_amd", "_lib", "libfsg_stamps.so")
 from fluvio_amd import _ffi, synth
 from fluvio_amd.smartengine import *
 kind = int(sys.argv[1]) if len(sys.argv) > 1 else 2
