@@ -192,6 +192,7 @@ struct EvalArgs {
   BatchStat* bstat;
   KeptRec* desc;
   Mins* mins;
+  uint32_t* list;      // deferred batches: list[0] = count, list[1..] = indices (k_eval_lean -> k_eval)
 };
 
 struct SizeArgs {

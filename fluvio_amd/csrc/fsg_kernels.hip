@@ -907,10 +907,8 @@ __device__ __forceinline__ void load_window(WaveLds& L, const uint8_t* slice, ui
 // walk and the ordered emission run on wave 0
 // ---------------------------------------------------------------------------
 template <uint32_t kOps>
-__global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : 2) void k_eval(EvalArgs a) {
-  __shared__ WaveLds L;
+__device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const uint32_t b) {
   STAMP_DECL
-  const uint32_t b = blockIdx.x;
   const uint32_t l = lane_id();
   const uint32_t tid = threadIdx.x;
   const bool wave0 = tid < 64;
@@ -1143,6 +1141,413 @@ __global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : 2) void 
     st.err_stage = err_stage;
     st.agg_sum = (ch.has_agg && (err_stage == 0xFFFFFFFFu || err_stage + 1 == ch.nstages)) ? aggsum : 0;
     a.bstat[b] = st;  // the cross-batch minima are reduced by k_mins
+  }
+  STAMP(5);
+  STAMP_FLUSH();
+}
+
+// k_eval: batches blockIdx.x (direct mode) or the deferred list written by
+// k_eval_lean (list mode: a.list[0] = count, a.list[1..] = batch indices)
+template <uint32_t kOps>
+__global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : 2) void k_eval(EvalArgs a) {
+  __shared__ WaveLds L;
+  const uint32_t n = a.list ? a.list[0] : a.nbatches;
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    eval_batch<kOps>(a, L, a.list ? a.list[1 + i] : i);
+    __syncthreads();  // the window is reused by the next batch
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_eval_lean — one wave per stored batch for chains of substring filters and
+// ASCII-uppercase maps (filter / filter_init / filter_with_param / map), the
+// C2/C3 hot path.  No barriers beyond the wave, ~17.5 KiB LDS per batch so nine
+// batches are in flight per CU.  A batch takes this path only when its records
+// can neither error nor decode unusually: record section inside the 16 KiB
+// window, 1..64 records that frame exactly, every value ASCII (then
+// from_utf8 cannot fail, filter.rs / derive filter.rs:14-40).  Any other batch
+// is appended to a.list and evaluated exactly by k_eval (list mode).
+//   1. LDS-DMA the batch (header + record section) into the window
+//   2. lane 0 chases the record length varints; lane r parses record r exactly
+//      (Record::decode, data.rs:534-562) and checks it ends where its length says
+//   3. per contains stage, a data-parallel 4-gram scan over the value bytes
+//      (16 B + 4 B look-ahead per lane, ballot-filtered); 4-gram hits are parked
+//      in registers and resolved after the scan (record lookup + full needle);
+//      the first scan also counts bytes >= 0x80 in [first value, last value end)
+//      and compares with the count inside the inter-value gaps: equal <=> all
+//      values are ASCII
+//   4. survivors -> compaction descriptors (ballot prefix), BatchStat
+// ---------------------------------------------------------------------------
+constexpr int kLeanWin = 16464;  // 57-B header + 16 KiB section + 15 B alignment, 16-B multiple
+constexpr int kLeanMaxR = 64;    // one record per lane of wave 0
+constexpr int kLeanThreads = 128;  // two waves per batch: DMA issue and the scan are split over both
+constexpr int kLeanNeedle = 128; // longest needle of the lean path (longer: exact kernel)
+constexpr int kLeanBlk = (kLeanWin + 80) / 64 + 1;  // 64-byte blocks of the window
+struct __attribute__((aligned(16))) LeanLds {
+  uint8_t win[kLeanWin + 48];  // + look-ahead of the last scan chunk
+  uint32_t r_start[kLeanMaxR + 1];
+  uint32_t r_vs[kLeanMaxR];
+  uint32_t r_ve[kLeanMaxR];
+  uint32_t match[2];
+  uint32_t chase_bad;
+  uint32_t pad;
+  uint8_t needle[kLeanNeedle + 8];  // the scanned stage's needle
+  uint8_t blk[kLeanBlk + 1];        // blk[j] = last record whose value starts <= 64 j (0xFF none)
+};
+
+__device__ __forceinline__ uint32_t win5(const uint32_t (&w)[5], int j) {
+  const int k = j >> 2, al = j & 3;
+  return al ? __builtin_amdgcn_alignbyte(w[k + 1], w[k], (uint32_t)al) : w[k];
+}
+// 4 window bytes starting at any offset q (two aligned LDS dwords)
+__device__ __forceinline__ uint32_t lds_u32_at(const uint8_t* win, uint32_t q) {
+  const uint32_t* w = (const uint32_t*)(win + (q & ~3u));
+  return __builtin_amdgcn_alignbyte(w[1], w[0], q & 3u);
+}
+// record whose value region holds window offset p: the last r with r_vs[r] <= p
+__device__ __forceinline__ int lean_rec_of(const LeanLds& L, int nr, uint32_t p) {
+  int r = (int)(int8_t)L.blk[p >> 6];
+  while (r + 1 < nr && L.r_vs[r + 1] <= p) r++;
+  return r;
+}
+// m needle bytes at window offset p (4 bytes per compare)
+__device__ __forceinline__ bool lean_verify(const LeanLds& L, uint32_t p, uint32_t m, bool upper) {
+  for (uint32_t t = 0; t < m; t += 4) {
+    uint32_t x = lds_u32_at(L.win, p + t);
+    if (upper) x = swar_upper(x);
+    const uint32_t k = m - t >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (m - t))) - 1u);
+    if ((x ^ lds_u32_at(L.needle, t)) & k) return false;
+  }
+  return true;
+}
+// a 4-gram hit at window offset p: the whole needle inside one value -> record bit
+__device__ __forceinline__ void lean_resolve(const LeanLds& L, int nr, uint32_t p, uint32_t m, bool upper,
+                                             uint64_t& mask) {
+  const int r = lean_rec_of(L, nr, p);
+  if (r < 0 || p < L.r_vs[r] || p + m > L.r_ve[r]) return;
+  if (lean_verify(L, p, m, upper)) mask |= 1ull << r;
+}
+__device__ __forceinline__ void lean_push(const LeanLds& L, int nr, uint32_t p, uint32_t m, bool upper,
+                                          uint32_t& s0, uint32_t& s1, uint32_t& nh, uint64_t& mask) {
+  if (nh == 0) s0 = p;
+  else if (nh == 1) s0 |= p << 16;
+  else if (nh == 2) s1 = p;
+  else if (nh == 3) s1 |= p << 16;
+  else lean_resolve(L, nr, p, m, upper, mask);  // more than 4 hits in one lane: resolve now
+  nh++;
+}
+// One contains stage over the value bytes [lo, hi) of a window whose non-value
+// bytes in [lo & ~15, hi + 16) are zero.  Returns the OR of the scanned words
+// (bit 7 of a byte set <=> some value byte >= 0x80, i.e. a non-ASCII value).
+//   kMode 0 (m >= 7): every occurrence covers an aligned word, so each aligned
+//           word is compared with the needle's 4-grams at offsets 0..3 (one
+//           compare per byte, no byte shifting)
+//   kMode 1 (4 <= m <= 6): the 4-gram at each of the 16 positions (alignbyte)
+//   kMode 2 (1 <= m <= 3): masked compare of the first m bytes at each position
+//   kMode 3 (m == 0): OR only
+template <int kMode>
+__device__ __forceinline__ uint32_t lean_scan(LeanLds& L, int nr, uint32_t lo, uint32_t hi, const uint8_t* nd,
+                                              uint32_t m, bool upper) {
+  const uint32_t l = threadIdx.x, lane = l & 63u;
+  uint32_t rot[4] = {0, 0, 0, 0};
+  uint32_t k4 = 0xFFFFFFFFu;
+  if (kMode == 0) {
+    for (int d = 0; d < 4; d++)
+      for (int t = 0; t < 4; t++) rot[d] |= (uint32_t)L.needle[d + t] << (8 * t);
+  } else if (kMode != 3) {
+    const uint32_t m4 = m < 4 ? m : 4;
+    for (uint32_t t = 0; t < m4; t++) rot[0] |= (uint32_t)L.needle[t] << (8 * t);
+    if (kMode == 2) k4 = (1u << (8 * m4)) - 1u;
+  }
+  uint32_t acc = 0, s0 = 0, s1 = 0, nh = 0;
+  uint64_t mask = 0;  // records of this lane's verified hits
+  uint32_t c = (lo & ~15u) + l * 16;
+  uint4 nx = c < hi ? *(const uint4*)(&L.win[c]) : make_uint4(0, 0, 0, 0);
+  uint32_t nx4 = (kMode == 1 || kMode == 2) && c < hi ? *(const uint32_t*)(&L.win[c + 16]) : 0u;
+  constexpr uint32_t kStride = kLeanThreads * 16;
+  for (; c < hi; c += kStride) {
+    uint32_t wd[5] = {nx.x, nx.y, nx.z, nx.w, nx4};
+    if (c + kStride < hi) {  // next chunk's LDS read in flight during this one
+      nx = *(const uint4*)(&L.win[c + kStride]);
+      if (kMode == 1 || kMode == 2) nx4 = *(const uint32_t*)(&L.win[c + kStride + 16]);
+    }
+    acc |= wd[0] | wd[1] | wd[2] | wd[3];
+    if (kMode == 3) continue;
+    if (upper) {
+#pragma unroll
+      for (int k = 0; k < 5; k++) wd[k] = swar_upper(wd[k]);
+    }
+    uint64_t any = 0;
+    if (kMode == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int d = 0; d < 4; d++) any |= __ballot(wd[k] == rot[d]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; j++) any |= __ballot(((win5(wd, j) ^ rot[0]) & k4) == 0);
+    }
+#if defined(FSG_EXP) && FSG_EXP == 6
+    if (any != 1234567) continue;  // experiment: compares without the hit path
+#endif
+    if (!any) continue;               // wave-uniform: no 4-gram hit in any lane
+    if (!((any >> lane) & 1)) continue;  // none in this lane
+    if (kMode == 0) {
+      // rare hits: parked, resolved after the scan for all lanes at once
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int d = 0; d < 4; d++)
+          if (wd[k] == rot[d]) lean_push(L, nr, c + 4 * k - d, m, upper, s0, s1, nh, mask);
+    } else {
+      uint32_t cand = 0;
+#pragma unroll
+      for (int j = 0; j < 16; j++) cand |= (uint32_t)(((win5(wd, j) ^ rot[0]) & k4) == 0) << j;
+      if (kMode == 1) {
+        while (cand) {
+          lean_push(L, nr, c + (uint32_t)__builtin_ctz(cand), m, upper, s0, s1, nh, mask);
+          cand &= cand - 1;
+        }
+      } else {
+        // m <= 3: the masked compare is the whole needle and hits are dense;
+        // one record lookup per chunk, then register compares per hit
+        uint32_t p = c + (uint32_t)__builtin_ctz(cand);
+        int r = lean_rec_of(L, nr, p);
+        uint32_t rvs = r >= 0 ? L.r_vs[r] : 0u, rve = r >= 0 ? L.r_ve[r] : 0u;
+        uint32_t nvs = r + 1 < nr ? L.r_vs[r + 1] : 0xFFFFFFFFu;
+        while (cand) {
+          p = c + (uint32_t)__builtin_ctz(cand);
+          cand &= cand - 1;
+          while (p >= nvs) {
+            r++;
+            rvs = nvs;
+            rve = L.r_ve[r];
+            nvs = r + 1 < nr ? L.r_vs[r + 1] : 0xFFFFFFFFu;
+          }
+          if (r >= 0 && p >= rvs && p + m <= rve) mask |= 1ull << r;
+        }
+      }
+    }
+  }
+  if (nh > 0) lean_resolve(L, nr, s0 & 0xFFFFu, m, upper, mask);
+  if (nh > 1) lean_resolve(L, nr, s0 >> 16, m, upper, mask);
+  if (nh > 2) lean_resolve(L, nr, s1 & 0xFFFFu, m, upper, mask);
+  if (nh > 3) lean_resolve(L, nr, s1 >> 16, m, upper, mask);
+  if (mask) {
+    atomicOr(&L.match[0], (uint32_t)mask);
+    atomicOr(&L.match[1], (uint32_t)(mask >> 32));
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(kLeanThreads) void k_eval_lean(EvalArgs a) {
+  __shared__ LeanLds L;
+  STAMP_DECL
+  const uint32_t b = blockIdx.x;
+  const uint32_t l = threadIdx.x;
+  const ChainDesc& ch = *a.chain;
+  const uint64_t pos = a.bpos[b];
+  const uint64_t nxt = b + 1 < a.nbatches ? a.bpos[b + 1] : a.slice_len;
+  const uint64_t rb = a.rbase[b];
+  const uint64_t al = pos & ~15ull;
+  uint64_t wl = nxt > al ? nxt - al : 0;
+  if (wl > (uint64_t)kLeanWin) wl = kLeanWin;
+  const uint32_t wlen = (uint32_t)((wl + 15) & ~15ull);
+  // 1. stage [al, al + wlen): 1 KiB LDS-DMA pieces, the last one partial
+  {
+    const uint32_t lane = l & 63u;
+    const uint8_t* src = a.slice + al + lane * 16;
+    for (uint32_t k = __builtin_amdgcn_readfirstlane(l >> 6); k * 1024 < wlen; k += kLeanThreads / 64)
+      if (k * 1024 + lane * 16 < wlen)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + k * 1024),
+                                         (__attribute__((address_space(3))) void*)(L.win + k * 1024), 16, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+  STAMP(0);
+#if defined(FSG_EXP) && FSG_EXP == 3
+  if (l == 0) a.bstat[b] = BatchStat{};  // experiment: DMA only (timing attribution)
+  return;
+#endif
+  // batch header (file format, batch.rs:163-180), read before the gaps are cleared
+  const uint8_t* h = L.win + (pos - al);
+  const int64_t base_offset = (int64_t)rd_be(h, 8);
+  const uint32_t batch_len = (uint32_t)rd_be(h + 8, 4);
+  const int32_t lod_in = (int32_t)rd_be(h + 23, 4);
+  const int64_t first_ts = (int64_t)rd_be(h + 27, 8);
+  const uint64_t sec0 = pos + 57;
+  const uint64_t sec_end = pos + 12 + (uint64_t)batch_len;  // framing validated at ingest
+  const uint32_t sec_len = (uint32_t)(sec_end - sec0);
+  const int32_t count = sec_len >= 4 ? (int32_t)rd_be(L.win + (sec0 - al), 4) : -1;
+  bool defer = sec_len < 4 || sec_end - al > (uint64_t)wlen || count < 0 || count > kLeanMaxR;
+  // 2. framing: lane 0 chases the lengths (one LDS round trip per record when
+  //    the length varint has <= 4 bytes), lane r parses record r
+  const uint32_t have = (uint32_t)(sec_end - al);
+  if (!defer && l == 0) {
+    uint32_t q = (uint32_t)(sec0 + 4 - al);
+    int n = 0;
+    for (; n < count; n++) {
+      const uint32_t q0 = q;
+      int64_t len;
+      const uint32_t x = lds_u32_at(L.win, q);
+      const uint32_t term = ~x & 0x80808080u;
+      const uint32_t nb = term ? (((uint32_t)__builtin_ctz(term)) >> 3) + 1 : 5u;
+      if (nb <= 4 && q + nb <= have) {
+        const uint32_t y = nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u));
+        const uint32_t v = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
+        len = (v & 1u) ? -(int64_t)(v >> 1) - 1 : (int64_t)(v >> 1);  // zigzag
+        q += nb;
+      } else if (wvarint((const uint8_t*)L.win, q, have, &len)) {
+        break;
+      }
+      if (len < 0 || (int64_t)(have - q) < len) break;
+      L.r_start[n] = q0;
+      q += (uint32_t)len;
+    }
+    L.r_start[n] = q;
+    L.chase_bad = n < count ? 1u : 0u;
+  }
+  __syncthreads();
+  // a failed chase leaves the lengths unverified: the exact walk decides
+  if (!defer) defer = __builtin_amdgcn_readfirstlane(L.chase_bad) != 0u;
+  STAMP(1);
+#if defined(FSG_EXP) && FSG_EXP == 4
+  if (l == 0) a.bstat[b] = BatchStat{};  // experiment: DMA + chase only
+  return;
+#endif
+  const int nr = defer ? 0 : count;
+  bool g = true;
+  int64_t ts = 0, od = 0, hdr = 0;
+  uint32_t vs = 0, vl = 0, kpos = 0, klen = 0;
+  uint8_t attr = 0, tag = 0;
+  if ((int)l < nr) {
+    uint32_t q = L.r_start[l];
+    const uint32_t lim = L.r_start[l + 1];
+    int64_t len, kl, vlen;
+    g = !wvarint((const uint8_t*)L.win, q, lim, &len);
+    if (g && q < lim) attr = L.win[q++]; else g = false;
+    g = g && !wvarint((const uint8_t*)L.win, q, lim, &ts) && !wvarint((const uint8_t*)L.win, q, lim, &od);
+    if (g && q < lim) tag = L.win[q++]; else g = false;
+    g = g && tag <= 1;
+    if (g && tag == 1) {
+      g = !wvarint((const uint8_t*)L.win, q, lim, &kl) && kl >= 0 && (uint64_t)q + (uint64_t)kl <= lim;
+      if (g) {
+        kpos = q;
+        klen = (uint32_t)kl;
+        q += klen;
+      }
+    }
+    g = g && !wvarint((const uint8_t*)L.win, q, lim, &vlen) && vlen >= 0 && (uint64_t)q + (uint64_t)vlen <= lim;
+    vs = q;
+    if (g) {
+      vl = (uint32_t)vlen;
+      q += vl;
+    }
+    g = g && !wvarint((const uint8_t*)L.win, q, lim, &hdr) && q == lim;
+    L.r_vs[l] = vs;
+    L.r_ve[l] = vs + vl;
+  }
+  defer = __syncthreads_or(defer || !g);  // a record that does not frame exactly
+  STAMP(2);
+  uint64_t alive = __ballot((int)l < nr);
+  // 3. stages.  Before the first scan every non-value byte of the scanned
+  //    range is cleared (record headers, keys, lengths): then the OR of the
+  //    scanned words has a high bit iff some value is non-ASCII.
+  bool checked = false;
+#if defined(FSG_EXP) && FSG_EXP == 2
+  checked = true;
+  for (uint32_t s = 0; false; s++) {  // experiment: no scan
+#else
+  for (uint32_t s = 0; !defer && s < ch.nstages; s++) {
+#endif
+    const StageDesc& sd = ch.st[s];
+    if (sd.op != OP_CONTAINS) continue;  // OP_MAP_UPPER: representation only
+    const uint32_t m = sd.needle_len;
+    if (m == 0 && checked) continue;     // an empty needle keeps every (UTF-8) value
+    if (nr == 0) break;
+    const uint32_t lo = L.r_vs[0], hi = L.r_ve[nr - 1];
+#if defined(FSG_EXP) && FSG_EXP == 7
+    if (false) {  // experiment: no gap clearing
+#else
+    if (!checked) {
+#endif
+      if ((int)l < nr) {
+        const uint32_t e = (int)l + 1 < nr ? L.r_vs[l + 1] : ((vs + vl + 15) & ~15u) + 16;
+        for (uint32_t p = vs + vl; p < e; p++) L.win[p] = 0;
+      }
+      if (l == 0)
+        for (uint32_t p = lo & ~15u; p < lo; p++) L.win[p] = 0;
+      // record lookup table over 64-byte blocks
+      if ((int)l < nr) {
+        const uint32_t e = (int)l + 1 < nr ? L.r_vs[l + 1] : hi + 80;
+        for (uint32_t j = (vs + 63) >> 6; (j << 6) < e; j++) L.blk[j] = (uint8_t)l;
+      }
+      if (l == 0)
+        for (uint32_t j = 0; (j << 6) < lo; j++) L.blk[j] = 0xFF;
+    }
+    const uint8_t* nd = a.blob + sd.needle;
+    if (l == 0) {
+      L.match[0] = 0;
+      L.match[1] = 0;
+    }
+    if (m > (uint32_t)kLeanNeedle) {
+      defer = true;  // long needle: exact kernel
+      break;
+    }
+    for (uint32_t t = l; t < m; t += kLeanThreads) L.needle[t] = nd[t];
+    __syncthreads();
+    const bool upper = sd.in_type == VT_SRC_UPPER;
+    uint32_t orw;
+#if defined(FSG_EXP) && FSG_EXP == 5
+    if (true) orw = lean_scan<3>(L, nr, lo, hi, nd, m, upper); else  // experiment: OR only
+#endif
+    if (m >= 7) orw = lean_scan<0>(L, nr, lo, hi, nd, m, upper);
+    else if (m >= 4) orw = lean_scan<1>(L, nr, lo, hi, nd, m, upper);
+    else if (m > 0) orw = lean_scan<2>(L, nr, lo, hi, nd, m, upper);
+    else orw = lean_scan<3>(L, nr, lo, hi, nd, m, upper);
+    STAMP(3);
+    const bool high = __syncthreads_or((orw & 0x80808080u) != 0u);  // also orders the match bits
+    if (!checked && high) defer = true;  // a non-ASCII value: exact UTF-8 path
+    checked = true;
+    if (m > 0) alive &= __ballot(l < 64 && ((L.match[(l >> 5) & 1] >> (l & 31)) & 1u));
+    STAMP(4);
+  }
+  if (defer) {
+    if (l == 0) {
+      const uint32_t i = atomicAdd(&a.list[0], 1u);
+      a.list[1 + i] = b;
+    }
+    return;
+  }
+  // 4. survivors -> descriptors
+  const bool kept = l < 64 && ((alive >> (l & 63)) & 1ull);
+  if (kept) {
+    KeptRec d;
+    d.src = al + L.r_start[l];
+    d.vpos = al + vs;
+    d.kpos = tag ? al + kpos : 0;
+    d.od = od;
+    d.ts = ts;
+    d.hdr = hdr;
+    d.vlen = vl;
+    d.klen = klen;
+    d.ival = 0;
+    d.mode = ch.out_type == VT_SRC_UPPER ? KM_UPPER : KM_COPY;
+    d.has_key = tag;
+    d.attr = attr;
+    d.pad = 0;
+    a.desc[rb + __popcll(alive & ((1ull << l) - 1ull))] = d;
+  }
+  if (l == 0) {
+    BatchStat st = {};
+    st.base_offset = base_offset;
+    st.lod_in = lod_in;
+    st.first_ts = first_ts;
+    st.flags = BF_LAST_STAGE;
+    st.nkeep = (uint32_t)__popcll(alive);
+    st.sec_len = sec_len;
+    st.err_stage = 0xFFFFFFFFu;
+    a.bstat[b] = st;
   }
   STAMP(5);
   STAMP_FLUSH();
@@ -1778,17 +2183,25 @@ hipError_t upload_crc_tables() {
   return e;
 }
 
-void launch_eval(const EvalArgs& a, uint32_t ops, hipStream_t s) {
+void launch_eval(const EvalArgs& a, uint32_t ops, bool lean, hipStream_t s) {
   if (!a.nbatches) return;
   const size_t dyn = (ops & opbit(OP_REGEX)) ? kDfaDyn : 0;
+  EvalArgs e = a;
+  uint32_t grid = a.nbatches;
+  if (lean) {
+    hipLaunchKernelGGL(k_eval_lean, dim3(a.nbatches), dim3(kLeanThreads), 0, s, a);
+    grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list
+  } else {
+    e.list = nullptr;
+  }
   if ((ops & ~kOpsContains) == 0)
-    hipLaunchKernelGGL(k_eval<kOpsContains>, dim3(a.nbatches), dim3(kEvalThreads), dyn, s, a);
+    hipLaunchKernelGGL(k_eval<kOpsContains>, dim3(grid), dim3(kEvalThreads), dyn, s, e);
   else if ((ops & ~kOpsRegex) == 0)
-    hipLaunchKernelGGL(k_eval<kOpsRegex>, dim3(a.nbatches), dim3(kEvalThreads), dyn, s, a);
+    hipLaunchKernelGGL(k_eval<kOpsRegex>, dim3(grid), dim3(kEvalThreads), dyn, s, e);
   else if ((ops & ~kOpsJson) == 0)
-    hipLaunchKernelGGL(k_eval<kOpsJson>, dim3(a.nbatches), dim3(kEvalThreads), dyn, s, a);
+    hipLaunchKernelGGL(k_eval<kOpsJson>, dim3(grid), dim3(kEvalThreads), dyn, s, e);
   else
-    hipLaunchKernelGGL(k_eval<kOpsAll>, dim3(a.nbatches), dim3(kEvalThreads), dyn, s, a);
+    hipLaunchKernelGGL(k_eval<kOpsAll>, dim3(grid), dim3(kEvalThreads), dyn, s, e);
 }
 void launch_mins(const BatchStat* bstat, uint32_t n, Mins* mins, hipStream_t s) {
   if (!n) return;

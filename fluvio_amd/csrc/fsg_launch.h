@@ -6,7 +6,8 @@
 
 namespace fsg {
 hipError_t upload_crc_tables();
-void launch_eval(const EvalArgs& a, uint32_t ops, hipStream_t s);  // ops: bit per StageOp in the chain
+// ops: bit per StageOp in the chain; lean: k_eval_lean first, k_eval over its deferred list
+void launch_eval(const EvalArgs& a, uint32_t ops, bool lean, hipStream_t s);
 void launch_mins(const BatchStat* bstat, uint32_t n, Mins* mins, hipStream_t s);
 void launch_size(const SizeArgs& a, hipStream_t s);
 uint32_t scan_tiles(uint32_t n);

@@ -226,7 +226,7 @@ struct fsg_chain {
   int agg_stage = -1;
   std::vector<uint8_t> acc;  // aggregate accumulator bytes (SmartModuleAggregate.accumulator)
   // scratch
-  DevBuf bstat, kept, rows, pre, aggpre, tiles, grand, mins, plan, out, crcparts;
+  DevBuf bstat, kept, rows, pre, aggpre, tiles, grand, mins, plan, out, crcparts, defer;
   Plan hplan{};
   hipEvent_t ev[6] = {};
   fsg_timings last{};
@@ -770,6 +770,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   HIPCHK(c->rows.ensure(std::max<uint32_t>(nb, 1) * sizeof(ScanRow)));
   HIPCHK(c->pre.ensure(std::max<uint32_t>(nb, 1) * sizeof(ScanRow)));
   HIPCHK(c->aggpre.ensure(std::max<uint32_t>(nb, 1) * sizeof(ScanRow)));
+  HIPCHK(c->defer.ensure(((size_t)nb + 1) * sizeof(uint32_t)));
   HIPCHK(c->tiles.ensure(std::max<uint32_t>(scan_tiles(nb), 1) * sizeof(ScanRow)));
   HIPCHK(c->grand.ensure(sizeof(ScanRow)));
   HIPCHK(c->mins.ensure(sizeof(Mins)));
@@ -790,9 +791,14 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   ea.bstat = c->bstat.as<BatchStat>();
   ea.desc = c->kept.as<KeptRec>();
   ea.mins = c->mins.as<Mins>();
+  ea.list = c->defer.as<uint32_t>();
   uint32_t ops = 0;
   for (uint32_t k = 0; k < c->hdesc.nstages; k++) ops |= 1u << c->hdesc.st[k].op;
-  launch_eval(ea, ops, st);
+  // substring filters + uppercase maps: the one-wave lean kernel first, the
+  // batches it defers then go through the exact kernel (list mode)
+  const bool lean = (ops & ~((1u << OP_CONTAINS) | (1u << OP_MAP_UPPER))) == 0 && !has_agg;
+  if (lean) HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
+  launch_eval(ea, ops, lean, st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[1], st));
   launch_mins(ea.bstat, nb, ea.mins, st);

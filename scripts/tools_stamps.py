@@ -19,8 +19,11 @@ ch.process_slice(rs, download=False)
 L.fsg_debug_stamps(buf, 1)
 ch.process_slice(rs, download=False)
 L.fsg_debug_stamps(buf, 0)
+lean = os.environ.get("LEAN_STAMPS") == "1"
 names = ["pre/loop", "load_window", "walk", "eval(rest)", "emit", "tail", "", "", "windows", "exact_walks", "ev.clear", "ev.scan", "ev.perrec"]
-tot = sum(buf[i] for i in range(6)) + sum(buf[i] for i in (10, 11, 12))
+if lean:
+    names = ["load", "chase", "parse", "scan", "gap+check", "emit", "", "", "", "", "", "", ""]
+tot = sum(buf[i] for i in range(6)) + (0 if lean else sum(buf[i] for i in (10, 11, 12)))
 print("kind", kind, mod, "timings", ch.last_timings())
 for i in range(13):
     if names[i]:

@@ -369,3 +369,55 @@ def test_filter_json_synthetic_logs(engine):
     sl = synth.make_slice(2, 3000)
     out = check_batch(engine, CHAINS["filter_json"], sl)
     assert 0 < out.n_records < 3000
+
+
+# ---------------------------------------------------------------------------
+# k_eval_lean (one wave per batch) vs the exact path: every needle-length mode,
+# upper-cased scans, keys, empty values, needles at value edges or spanning
+# into the next record, non-ASCII values and > 64 records (both deferred to the
+# exact kernel), mixed in one slice
+# ---------------------------------------------------------------------------
+def _lean_slice(seed=7, nbatches=40):
+    import random
+    rnd = random.Random(seed)
+    words = ["timeout", "time", "out", "info", "warn", "level", "a", "TIMEOUT", "tim", "eout", "xx", "é", "\xff"]
+    out = b""
+    base = 0
+    for bi in range(nbatches):
+        b = P.Batch(base_offset=base)
+        nrec = rnd.choice([1, 3, 15, 63, 64, 65]) if bi % 3 else rnd.randint(1, 20)
+        size = rnd.choice([0, 5, 40, 200, 900])
+        for _ in range(nrec):
+            parts = []
+            while sum(len(p) for p in parts) < size:
+                pool = words if bi >= nbatches - 2 else (words[:12] if bi % 5 == 0 else words[:11])
+                w = rnd.choice(pool)
+                parts.append(w)
+            v = "".join(parts)[: size or None] if rnd.random() < 0.5 else " ".join(parts)
+            enc = v.encode("utf-8") if "\xff" not in v else v.replace("\xff", "").encode() + b"\xff"
+            key = None if rnd.random() < 0.7 else rnd.choice([b"", b"timeout", b"k\x80y"])
+            r = P.Record.new_key_value(key, enc)
+            b.add_record(r)
+        enc_b = b.encode()
+        if len(enc_b) - 57 > 16384:
+            continue
+        out += enc_b
+        base += nrec + rnd.randint(0, 3)
+    return out
+
+
+@pytest.mark.parametrize("chain", [
+    [("filter_init", {"key": "timeout"}, None)],          # m >= 7: aligned 4-gram rotations
+    [("filter_init", {"key": "level"}, None)],            # 4 <= m <= 6
+    [("filter_init", {"key": "ti"}, None)],               # m < 4
+    [("filter", {}, None)],                               # 'a'
+    [("filter_init", {"key": ""}, None)],                 # empty needle: UTF-8 check only
+    [("map", {}, None), ("filter_init", {"key": "TIMEOUT"}, None)],
+    [("map", {}, None), ("filter_init", {"key": "LEVEL"}, None)],
+    [("filter_init", {"key": "out"}, None), ("map", {}, None), ("filter_init", {"key": "TIME"}, None)],
+    [("map", {}, None)],
+    [],
+])
+def test_lean_path_parity(engine, chain):
+    check_batch(engine, chain, _lean_slice())
+    check_batch(engine, chain, _lean_slice(seed=11, nbatches=25))
