@@ -1860,79 +1860,79 @@ __global__ void k_header(const Plan* plan, uint8_t* out) {
 // ---------------------------------------------------------------------------
 
 
-// 256-thread exclusive scan of a u64 (returns exclusive prefix, *total = sum)
-__device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t* sh4, uint64_t* total) {
-  const uint32_t l = lane_id(), w = threadIdx.x >> 6;
-  const uint64_t incl = wave_incl_scan(v);
-  if (l == 63) sh4[w] = incl;
-  __syncthreads();
-  uint64_t base = 0, tot = 0;
-  for (uint32_t k = 0; k < 4; k++) {
-    const uint64_t x = sh4[k];
-    if (k < w) base += x;
-    tot += x;
+// copy n source bytes at slice offset s0 to out offset d0 (ASCII-uppercased when
+// `upper`), all lanes of the wave: 16-byte aligned destination units, lane u
+// takes units u, u + 64, ...  Every unit of a segment has the same source
+// misalignment, so each unit is two aligned dwordx4 loads and four alignbytes
+// selected by a wave-uniform switch; interior units are one dwordx4 store,
+// the two edge units byte stores.
+__device__ __forceinline__ void copy_seg(uint8_t* __restrict__ out, const uint8_t* __restrict__ slice, uint64_t d0,
+                                         uint64_t s0, uint32_t n, bool upper) {
+  if (!n) return;
+  const uint32_t lane = lane_id();
+  const uint64_t u0 = d0 >> 4;
+  const uint32_t nunits = (uint32_t)(((d0 + n + 15) >> 4) - u0);
+  const uint32_t sh = (uint32_t)((s0 - d0) & 15);  // source offset of a destination unit start, mod 16
+  const uint64_t e = d0 + n;
+  for (uint32_t u = lane; u < nunits; u += 64) {
+    const uint64_t D = (u0 + u) << 4;
+    const uint64_t A = s0 + D - d0;  // >= s0 - 15: the value sits >= 61 B into the slice
+    const uint4* src = (const uint4*)(slice + (A & ~15ull));
+    const uint4 x0 = src[0], x1 = src[1];
+    const uint32_t w[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    const uint32_t bs = sh & 3u;
+    uint32_t v[4];
+    switch (sh >> 2) {  // wave-uniform
+      case 0:
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], bs);
+        break;
+      case 1:
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = __builtin_amdgcn_alignbyte(w[k + 2], w[k + 1], bs);
+        break;
+      case 2:
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = __builtin_amdgcn_alignbyte(w[k + 3], w[k + 2], bs);
+        break;
+      default:
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = __builtin_amdgcn_alignbyte(w[k + 4], w[k + 3], bs);
+        break;
+    }
+    if (upper) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) v[k] = swar_upper(v[k]);
+    }
+    const uint64_t lo = D > d0 ? D : d0;
+    const uint64_t hi = D + 16 < e ? D + 16 : e;
+    if (lo == D && hi == D + 16) {
+      *(uint4*)(out + D) = make_uint4(v[0], v[1], v[2], v[3]);
+    } else {
+      const uint32_t jl = (uint32_t)(lo - D), jh = (uint32_t)(hi - D);
+#pragma unroll
+      for (int jj = 0; jj < 16; jj++)
+        if ((uint32_t)jj >= jl && (uint32_t)jj < jh) out[D + jj] = (uint8_t)(v[jj >> 2] >> (8 * (jj & 3)));
+    }
   }
-  __syncthreads();
-  *total = tot;
-  return base + incl - v;
 }
 
-// one 16-byte aligned destination unit of a copy segment (dst offset d0 within
-// `out`, source offset s0 within `slice`, n bytes): built from 5 aligned source
-// dwords with alignbyte; whole units are one dwordx4 store, edge units byte stores
-__device__ __forceinline__ void copy_unit(uint8_t* __restrict__ out, const uint8_t* __restrict__ slice, uint64_t d0,
-                                          uint64_t s0, uint32_t n, uint32_t uu, bool upper) {
-  const uint64_t D = ((d0 >> 4) + uu) << 4;
-  const uint64_t A = s0 + D - d0;  // >= s0 - 15: the value sits >= 61 B into the slice
-  const uint32_t* w = (const uint32_t*)(slice + (A & ~3ull));
-  const uint32_t sh = (uint32_t)(A & 3);
-  uint32_t x[5];
-#pragma unroll
-  for (int k = 0; k < 5; k++) x[k] = w[k];
-  uint32_t v[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    v[k] = __builtin_amdgcn_alignbyte(x[k + 1], x[k], sh);
-    if (upper) v[k] = swar_upper(v[k]);
-  }
-  const uint64_t lo = D > d0 ? D : d0;
-  const uint64_t e = d0 + n, hi = D + 16 < e ? D + 16 : e;
-  if (lo == D && hi == D + 16) {
-    uint4 q;
-    q.x = v[0];
-    q.y = v[1];
-    q.z = v[2];
-    q.w = v[3];
-    *(uint4*)(out + D) = q;
-  } else {
-    const uint32_t jl = (uint32_t)(lo - D), jh = (uint32_t)(hi - D);
-#pragma unroll
-    for (int jj = 0; jj < 16; jj++)
-      if ((uint32_t)jj >= jl && (uint32_t)jj < jh) out[D + jj] = (uint8_t)(v[jj >> 2] >> (8 * (jj & 3)));
-  }
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t x, uint32_t lane) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, lane);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
 }
 
-__device__ __forceinline__ uint32_t seg_units(uint64_t d0, uint32_t n) {
-  return n ? (uint32_t)(((d0 + n + 15) >> 4) - (d0 >> 4)) : 0u;
-}
-
-// k_write — one 256-thread workgroup per included batch.  Per chunk of up to 256
-// survivors: sizes -> block scan -> each thread writes its record's varint
-// header, small fields and i32 values; then the key/value payload segments of
-// all records are cut into 16-byte aligned destination units which the threads
-// copy round-robin (adjacent threads store adjacent units).
+// k_write — one wave per included batch (four per 256-thread block).  Per chunk
+// of up to 64 survivors: lane = record: size, wave scan, varint header fields
+// and i32 values; then the wave walks the chunk's records in order and copies
+// each key/value payload with all 64 lanes (copy_seg).
 constexpr int kWriteThreads = 256;
 __global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
-  __shared__ uint64_t sh4[4];
-  __shared__ uint32_t s_u[kWriteThreads + 1];  // unit prefix of the chunk
-  __shared__ uint64_t s_ks[kWriteThreads], s_vs[kWriteThreads];
-  __shared__ uint64_t s_kd[kWriteThreads], s_vd[kWriteThreads];
-  __shared__ uint32_t s_kl[kWriteThreads], s_vl[kWriteThreads], s_ku[kWriteThreads];
-  __shared__ uint8_t s_up[kWriteThreads];
   const Plan p = *a.plan;
-  const int32_t b = p.first + (int32_t)blockIdx.x;
+  const int32_t b = p.first + (int32_t)(blockIdx.x * (kWriteThreads / 64) + (threadIdx.x >> 6));
   if (p.first < 0 || b > p.last) return;
-  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = lane_id();
   const BatchStat st = a.bstat[b];
   const int64_t rel = a.bstat[p.first].base_offset - st.base_offset;
   const int32_t agg_base = a.agg_pre ? (int32_t)((uint64_t)a.acc0 + (uint64_t)a.agg_pre[b].agg) : 0;
@@ -1940,8 +1940,8 @@ __global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
   const uint64_t obase = 61 + (a.pre[b].rec_bytes - a.pre[p.first].rec_bytes);
   uint8_t* out = a.out;
   uint64_t run = 0;
-  for (uint32_t k0 = 0; k0 < st.nkeep; k0 += kWriteThreads) {
-    const uint32_t k = k0 + tid;
+  for (uint32_t k0 = 0; k0 < st.nkeep; k0 += 64) {
+    const uint32_t k = k0 + lane;
     const bool v = k < st.nkeep;
     KeptRec r = {};
     uint32_t sz = 0;
@@ -1949,9 +1949,10 @@ __global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
       r = d[k];
       sz = rec_out_size(r, rel, agg_base);
     }
-    uint64_t tot;
-    const uint64_t my = obase + run + block_excl_scan_u64(sz, sh4, &tot);
-    uint32_t units = 0;
+    const uint64_t incl = wave_incl_scan((uint64_t)sz);
+    const uint64_t my = obase + run + incl - sz;
+    uint64_t kd = 0, vd = 0;
+    uint32_t kl = 0, vc = 0;
     if (v) {
       uint8_t* q = out + my;
       const uint32_t vl = out_vlen(r, agg_base);
@@ -1966,17 +1967,16 @@ __global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
       n = venc(r.od + rel, t);
       for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
       q[w++] = r.has_key ? 1 : 0;
-      uint32_t kl = 0, vc = 0;
       if (r.has_key) {
         n = venc((int64_t)r.klen, t);
         for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
-        s_kd[tid] = my + w;
+        kd = my + w;
         kl = r.klen;
         w += r.klen;
       }
       n = venc((int64_t)vl, t);
       for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
-      s_vd[tid] = my + w;
+      vd = my + w;
       if (r.mode == KM_I32 || r.mode == KM_AGG) {
         const int32_t x = r.mode == KM_I32 ? r.ival : (int32_t)((uint32_t)agg_base + (uint32_t)r.ival);
         w += fmt_i32(x, q + w);
@@ -1986,41 +1986,18 @@ __global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
       }
       n = venc(r.hdr, t);
       for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
-      const uint32_t ku = kl ? seg_units(s_kd[tid], kl) : 0u;
-      units = ku + (vc ? seg_units(s_vd[tid], vc) : 0u);
-      s_ks[tid] = r.kpos;
-      s_vs[tid] = r.vpos;
-      s_kl[tid] = kl;
-      s_vl[tid] = vc;
-      s_ku[tid] = ku;
-      s_up[tid] = r.mode == KM_UPPER;
     }
-    uint64_t utot;
-    const uint64_t uex = block_excl_scan_u64((uint64_t)units, sh4, &utot);
-    s_u[tid] = (uint32_t)uex;
-    if (tid == 0) s_u[kWriteThreads] = (uint32_t)utot;
-    __syncthreads();
-    const int nrec = (int)(st.nkeep - k0 < (uint32_t)kWriteThreads ? st.nkeep - k0 : (uint32_t)kWriteThreads);
-    for (uint32_t g = tid; g < (uint32_t)utot; g += kWriteThreads) {
-      // record owning unit g: last rr with s_u[rr] <= g
-      int lo = 0, hi = nrec - 1, rr = 0;
-      while (lo <= hi) {
-        const int m = (lo + hi) >> 1;
-        if (s_u[m] <= g) {
-          rr = m;
-          lo = m + 1;
-        } else {
-          hi = m - 1;
-        }
-      }
-      const uint32_t u = g - s_u[rr], ku = s_ku[rr];
-      if (u < ku)
-        copy_unit(out, a.slice, s_kd[rr], s_ks[rr], s_kl[rr], u, false);
-      else
-        copy_unit(out, a.slice, s_vd[rr], s_vs[rr], s_vl[rr], u - ku, s_up[rr] != 0);
+    // payloads, record by record, with the whole wave
+    const uint32_t nrec = st.nkeep - k0 < 64u ? st.nkeep - k0 : 64u;
+    for (uint32_t i = 0; i < nrec; i++) {
+      const uint32_t rkl = __builtin_amdgcn_readlane(kl, i);
+      const uint32_t rvc = __builtin_amdgcn_readlane(vc, i);
+      if (rkl) copy_seg(out, a.slice, readlane_u64(kd, i), readlane_u64(r.kpos, i), rkl, false);
+      if (rvc)
+        copy_seg(out, a.slice, readlane_u64(vd, i), readlane_u64(r.vpos, i), rvc,
+                 __builtin_amdgcn_readlane((uint32_t)r.mode, i) == KM_UPPER);
     }
-    run += tot;
-    __syncthreads();
+    run += readlane_u64(incl, 63);
   }
 }
 
@@ -2227,7 +2204,9 @@ void launch_header(const Plan* plan, uint8_t* out, hipStream_t s) {
   hipLaunchKernelGGL(k_header, dim3(1), dim3(64), 0, s, plan, out);
 }
 void launch_write(const WriteArgs& a, uint32_t nblocks, hipStream_t s) {
-  if (nblocks) hipLaunchKernelGGL(k_write, dim3(nblocks), dim3(kWriteThreads), 0, s, a);
+  // nblocks = included batches, one wave each
+  if (nblocks) hipLaunchKernelGGL(k_write, dim3((nblocks + kWriteThreads / 64 - 1) / (kWriteThreads / 64)),
+                                  dim3(kWriteThreads), 0, s, a);
 }
 // CRC32C of out[off, off + n) into out[17..21); `acc` is one u32 of scratch
 void launch_crc(uint8_t* out, uint64_t off, uint64_t n, uint32_t* acc, hipStream_t s) {
