@@ -125,9 +125,12 @@ def main():
     if os.path.exists(tpath):  # PMC HBM bytes per launch of the same command (scripts/traffic_from_pmc.py)
         db = json.load(open(tpath)).get(a.workload)
         if db:
-            for kname, v in db["kernels"].items():
-                if kname.split("<")[0] == "fsg::" + dom:
-                    traffic, traffic_src = v["total"], db["source"]
+            # the eval timing brackets k_eval_lean plus the deferred exact k_eval<N>
+            # (and crc brackets k_crc16 + k_crc_final): sum every launch in the bracket
+            hits = [v["total"] for kname, v in db["kernels"].items()
+                    if kname.split("<")[0].startswith("fsg::" + dom)]
+            if hits:
+                traffic, traffic_src = sum(hits), db["source"]
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
