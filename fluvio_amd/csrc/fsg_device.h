@@ -32,6 +32,8 @@ enum StageOp : uint8_t {
   OP_FILTER_MAP = 5,   // filter_map: from_utf8_lossy + parse::<i32>, even -> /2
   OP_AGG_SUM = 6,      // aggregate-sum (last stage only)
   OP_FILTER_JSON = 7,  // filter_json: serde_json::from_slice::<StructuredLog>, keep level > Debug
+  OP_ARRAY_MAP = 8,    // array_map_json_array: Vec<serde_json::Value> -> one record per element (last stage)
+  OP_AGG_CONCAT = 9,   // aggregate: String accumulator ++ value (last stage)
 };
 
 // value representation entering a stage (static per chain position)
@@ -85,11 +87,13 @@ struct StageDesc {
   DfaDesc dfa;
 };
 
+// ChainDesc::flags: what the last stage is
+enum ChainFlags : uint32_t { CF_AGG_SUM = 1u, CF_AGG_CAT = 2u, CF_ARRAY = 4u };
 struct ChainDesc {
   uint32_t nstages;
   uint32_t out_type;   // ValType of the value after the last stage
   uint32_t has_agg;
-  uint32_t pad;
+  uint32_t flags;      // ChainFlags
   StageDesc st[kMaxStages];
 };
 
@@ -117,11 +121,16 @@ struct BatchStat {
   uint32_t err_aux2;
   uint32_t err_aux3;
   int64_t agg_sum;     // wrapping i32 sum of the aggregate inputs of this batch
+  uint32_t nout;       // output records of the stage output (array_map: elements; else nkeep)
+  uint32_t pad;
+  uint64_t cat_sum;    // aggregate (concat): bytes appended to the accumulator by this batch
 };
 
 // one kept output record (a compaction descriptor, 64 bytes): enough to
 // re-encode the record canonically without re-parsing the source
-enum KeepMode : uint8_t { KM_COPY = 0, KM_UPPER = 1, KM_I32 = 2, KM_AGG = 3 };
+enum KeepMode : uint8_t { KM_COPY = 0, KM_UPPER = 1, KM_I32 = 2, KM_AGG = 3, KM_ARRAY = 4, KM_CONCAT = 5 };
+// KeptRec::pad bits for KM_ARRAY / KM_CONCAT
+enum KeepFlags : uint8_t { KF_UPPER = 1, KF_I32 = 2 };
 struct KeptRec {
   uint64_t src;        // absolute slice offset of the source record (its length varint)
   uint64_t vpos;       // absolute slice offset of the source value bytes
@@ -129,15 +138,27 @@ struct KeptRec {
   int64_t od;          // source offset_delta
   int64_t ts;          // timestamp_delta
   int64_t hdr;         // headers varint
-  uint32_t vlen;       // source value length (KM_COPY / KM_UPPER)
+  uint32_t vlen;       // source value length (KM_COPY / KM_UPPER / KM_CONCAT), i32 bits with KF_I32
   uint32_t klen;
-  int32_t ival;        // KM_I32 value / KM_AGG batch-local inclusive sum
+  int32_t ival;        // KM_I32 value / KM_AGG batch-local inclusive sum / KM_ARRAY element count /
+                       // KM_CONCAT batch-local inclusive byte count
   uint8_t mode;        // KeepMode
   uint8_t has_key;
   uint8_t attr;
-  uint8_t pad;
+  uint8_t pad;         // KeepFlags
 };
 static_assert(sizeof(KeptRec) == 64, "KeptRec is one 64-byte line");
+
+// one array_map output element: the source span of a JSON array element and
+// the length of its serde_json::to_string form.  The elements of a record with
+// value at slice offset v live at elem[(v >> 1) + j] (an element needs >= 2
+// value bytes with its separator, so records never overlap).
+struct ElemRec {
+  uint64_t pos;        // absolute slice offset of the element's first byte
+  uint32_t src_len;    // source span (whitespace inside included)
+  uint32_t out_len;    // canonical length; bit 31 = canonical bytes == source bytes
+};
+static_assert(sizeof(ElemRec) == 16, "ElemRec is 16 bytes");
 
 // per-batch row of the cross-batch scan (in place: exclusive prefix afterwards)
 struct ScanRow {
@@ -148,7 +169,7 @@ struct ScanRow {
   uint64_t bytes_in;   // record-section bytes (metrics.bytes_in)
   uint64_t recs_out;   // last-stage output records (metrics.records_out)
   int64_t agg;         // aggregate sum (wrapping i32 in the low bits)
-  uint64_t pad;
+  uint64_t cat;        // aggregate (concat): accumulator bytes appended
 };
 
 // cross-batch minima found with atomics (reset to 0xFFFFFFFF per call)
@@ -178,6 +199,7 @@ struct Plan {
   int64_t acc_final;         // aggregate accumulator after the stop batch
   int32_t acc_touched;       // accumulator changed by this call
   int32_t pad;
+  uint64_t cat_final;        // aggregate (concat): accumulator bytes appended through the stop batch
 };
 
 struct EvalArgs {
@@ -193,6 +215,7 @@ struct EvalArgs {
   KeptRec* desc;
   Mins* mins;
   uint32_t* list;      // deferred batches: list[0] = count, list[1..] = indices (k_eval_lean -> k_eval)
+  ElemRec* elem;       // array_map element descriptors (nullptr without an array_map stage)
 };
 
 struct SizeArgs {
@@ -205,6 +228,8 @@ struct SizeArgs {
   uint32_t nbatches;
   uint32_t agg_only;       // 1: only fill rows[].agg (first pass of an aggregate chain)
   int64_t acc0;
+  const ElemRec* elem;
+  uint64_t acc_len;        // aggregate (concat): initial accumulator bytes
 };
 
 struct PlanArgs {
@@ -230,6 +255,10 @@ struct WriteArgs {
   const Plan* plan;
   uint8_t* out;
   int64_t acc0;
+  const ElemRec* elem;
+  const uint8_t* cat;      // aggregate (concat): kCatOff + accumulator stream
+  uint64_t acc_len;
 };
+constexpr uint64_t kCatOff = 64;  // the concat stream starts this far into its buffer (copy_seg margin)
 
 }  // namespace fsg

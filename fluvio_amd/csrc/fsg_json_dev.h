@@ -15,6 +15,8 @@
 #pragma once
 #include <cstdint>
 
+#include "fsg_device.h"
+
 namespace fsg {
 
 // serde_json ErrorCode (syntax errors carry a reader position)
@@ -30,9 +32,10 @@ enum JsonErr : uint8_t {
   JE_UNKNOWN_VARIANT,  // [a, b) = raw string content (between the quotes)
   JE_INVALID_TYPE,     // sub = unexpected kind | expected kind << 4; a, b = span (number digits / string)
   JE_DEEP,             // ignored value nested deeper than the device frame stack (outside the restatement)
+  JE_UNSUP,            // valid input outside the device restatement (array_map: floats, unsorted keys)
 };
 enum JsonUnexp : uint8_t { JU_UNIT = 0, JU_TRUE, JU_FALSE, JU_UINT, JU_NINT, JU_FLOAT, JU_STR, JU_SEQ, JU_MAP };
-enum JsonExp : uint8_t { JX_STRUCT = 0, JX_STRING, JX_VARIANT, JX_UNIT };
+enum JsonExp : uint8_t { JX_STRUCT = 0, JX_STRING, JX_VARIANT, JX_UNIT, JX_SEQ };
 
 struct JRes {
   uint8_t ok;
@@ -765,6 +768,285 @@ struct JsonDev {
     if (rc) fix_position();
     return rc;
   }
+  // ------------------------------------------------------------------------
+  // array_map_json_array (smartmodule/examples/array_map_json_array/src/lib.rs:
+  // 38-55): from_slice::<Vec<Value>> then to_string of every element.  The
+  // parse follows de.rs deserialize_seq / SeqAccess / deserialize_any /
+  // MapAccess / parse_object_colon; instead of building Values it records,
+  // per element, its source span and the length of its canonical
+  // serialization (ser.rs: compact, format_escaped_str, itoa).  Objects must
+  // already be in BTreeMap order (strictly increasing keys) and numbers must
+  // be integers (serde_json turns floats, -0 and integers beyond u64/i64 into
+  // f64, whose ryu Display is outside the restatement): anything else is
+  // JE_UNSUP, which the engine reports as FSG_E_UNSUPPORTED if reached.
+  // ------------------------------------------------------------------------
+  uint32_t vcanon;  // canonical bytes of the element being parsed
+  bool vhas_u;      // a \u escape was decoded (canonical form may differ in bytes)
+  bool vhas_bs;     // the last string held a backslash
+  static __device__ __forceinline__ uint32_t canon_byte_len(uint32_t c) {
+    if (c == '"' || c == '\\' || c == 0x08 || c == 0x09 || c == 0x0A || c == 0x0C || c == 0x0D) return 2;
+    return c < 0x20 ? 6 : 1;
+  }
+  __device__ __forceinline__ void vfeed_cp(U8& u, uint32_t c) {
+    feed_cp(u, nullptr, c);
+    vcanon += c < 0x80 ? canon_byte_len(c) : c < 0x800 ? 2 : c < 0x10000 ? 3 : 4;
+  }
+  // read.rs parse_escape (validate = true) adding the canonical length
+  __device__ __forceinline__ int vescape(U8& u) {
+    const int ch = next();
+    if (ch < 0) return error(JE_EOF_STRING);
+    switch (ch) {
+      case '"': vfeed_cp(u, '"'); return 0;
+      case '\\': vfeed_cp(u, '\\'); return 0;
+      case '/': vfeed_cp(u, '/'); return 0;
+      case 'b': vfeed_cp(u, 0x08); return 0;
+      case 'f': vfeed_cp(u, 0x0c); return 0;
+      case 'n': vfeed_cp(u, '\n'); return 0;
+      case 'r': vfeed_cp(u, '\r'); return 0;
+      case 't': vfeed_cp(u, '\t'); return 0;
+      case 'u': {
+        vhas_u = true;
+        uint32_t n1;
+        if (hex4(&n1)) return -1;
+        if (n1 >= 0xDC00 && n1 <= 0xDFFF) return error(JE_SURROGATE);
+        if (n1 >= 0xD800 && n1 <= 0xDBFF) {
+          int p = peek();
+          if (p < 0) return error(JE_EOF_STRING);
+          if (p != '\\') {
+            eat();
+            return error(JE_HEX_END);
+          }
+          eat();
+          p = peek();
+          if (p < 0) return error(JE_EOF_STRING);
+          if (p != 'u') {
+            eat();
+            return error(JE_HEX_END);
+          }
+          eat();
+          uint32_t n2;
+          if (hex4(&n2)) return -1;
+          if (n2 < 0xDC00 || n2 > 0xDFFF) return error(JE_SURROGATE);
+          vfeed_cp(u, (((n1 - 0xD800) << 10) | (n2 - 0xDC00)) + 0x10000);
+          return 0;
+        }
+        vfeed_cp(u, n1);
+        return 0;
+      }
+      default: return error(JE_ESCAPE);
+    }
+  }
+  // SliceRead::parse_str after the opening quote (validating), adding the
+  // canonical length of the string (quotes included) to vcanon
+  __device__ __forceinline__ int vstr() {
+    U8 u = {0, 0x80, 0xBF, false};
+    vcanon += 2;
+    vhas_bs = false;
+    for (;;) {
+      const uint32_t i0 = i;
+      skip_plain(true);
+      vcanon += i - i0;
+      if (i >= n) return error(JE_EOF_STRING);
+      const int c = at(i);
+      if (c == '"') {
+        i++;
+        if (u.bad || u.need) return error(JE_CODEPOINT);
+        return 0;
+      } else if (c == '\\') {
+        i++;
+        vhas_bs = true;
+        if (vescape(u)) return -1;
+      } else if (c < 0x20) {
+        i++;
+        return error(JE_CONTROL);
+      } else {
+        i++;
+        feed(u, nullptr, (uint32_t)c);
+        vcanon += 1;
+      }
+    }
+  }
+  // raw key compare (keys without escapes): <0, 0, >0
+  __device__ __forceinline__ int key_cmp(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1) const {
+    const uint32_t la = a1 - a0, lb = b1 - b0, m = la < lb ? la : lb;
+    for (uint32_t k = 0; k < m; k++) {
+      const int x = at(a0 + k), y = at(b0 + k);
+      if (x != y) return x - y;
+    }
+    return (int)la - (int)lb;
+  }
+  static constexpr int kKeyFrames = 8;  // objects checked for key order at these nesting levels
+  // one Value (deserialize_any), iteratively over a 128-level frame bit stack
+  __device__ int any_value() {
+    uint64_t stk[2] = {0, 0};  // bit = 1: '[' frame, 0: '{' frame
+    uint32_t sn = 0;
+    uint32_t pk0[kKeyFrames], pk1[kKeyFrames];  // previous key (raw content span) per object level; pk1 = ~0: none
+    bool first = false;
+    int frame = 0;
+    for (;;) {
+      // ---- VALUE
+      int c = ws();
+      if (c < 0) return peek_error(JE_EOF_VALUE);
+      switch (c) {
+        case 'n': eat(); if (ident("ull", 3)) return -1; vcanon += 4; break;
+        case 't': eat(); if (ident("rue", 3)) return -1; vcanon += 4; break;
+        case 'f': eat(); if (ident("alse", 4)) return -1; vcanon += 5; break;
+        case '-':
+        case '0': case '1': case '2': case '3': case '4': case '5': case '6': case '7': case '8': case '9': {
+          const uint32_t i0 = i;
+          if (c == '-') eat();
+          uint8_t kind;
+          if (parse_integer(c != '-', &kind)) return -1;
+          if (kind == JU_FLOAT) return fail_at(i, JE_UNSUP);
+          vcanon += i - i0;  // an integer's canonical text is its source text (JSON has no + / leading 0)
+          break;
+        }
+        case '"': eat(); if (vstr()) return -1; break;
+        case '[':
+        case '{': {
+          if (--depth == 0) return peek_error(JE_RECURSION);
+          eat();
+          const uint64_t bit = 1ull << (sn & 63);
+          if (c == '[') stk[sn >> 6] |= bit; else stk[sn >> 6] &= ~bit;
+          if (c == '{' && sn < (uint32_t)kKeyFrames) pk1[sn] = 0xFFFFFFFFu;
+          sn++;
+          vcanon += 1;
+          first = true;
+          frame = c;
+          goto next_member;
+        }
+        default: return peek_error(JE_VALUE);
+      }
+    after_value:
+      if (sn == 0) return 0;
+      frame = ((stk[(sn - 1) >> 6] >> ((sn - 1) & 63)) & 1) ? '[' : '{';
+      first = false;
+    next_member:
+      c = ws();
+      if ((frame == '[' && c == ']') || (frame == '{' && c == '}')) {
+        eat();  // end_seq / end_map after the visitor saw the close
+        depth++;
+        vcanon += 1;
+        sn--;
+        goto after_value;
+      }
+      if (c == ',' && !first) {
+        eat();
+        c = ws();
+        vcanon += 1;
+      } else if (c >= 0) {
+        if (!first) return peek_error(frame == '[' ? JE_LIST_COMMA : JE_OBJ_COMMA);
+      } else {
+        return peek_error(frame == '[' ? JE_EOF_LIST : JE_EOF_OBJECT);
+      }
+      const bool first_member = first;
+      first = false;
+      if (frame == '[') {
+        if (c == ']') return peek_error(JE_TRAILING_COMMA);
+        if (c < 0) return peek_error(JE_EOF_VALUE);
+        continue;  // element value
+      }
+      if (c == '}') return peek_error(JE_TRAILING_COMMA);
+      if (c < 0) return peek_error(JE_EOF_VALUE);
+      if (c != '"') return peek_error(JE_KEY);
+      eat();
+      const uint32_t k0 = i;
+      if (vstr()) return -1;
+      const uint32_t k1 = i - 1;
+      {  // BTreeMap order: keys must arrive strictly increasing (else re-sorting / dedup needed)
+        const uint32_t lv = sn - 1;
+        if (lv >= (uint32_t)kKeyFrames) {
+          // deeper objects: only a single-member object is known to be in order
+          if (!first_member) return fail_at(i, JE_UNSUP);
+        } else {
+          if (pk1[lv] != 0xFFFFFFFFu) {
+            const bool esc_prev = (pk0[lv] >> 31) != 0;
+            if (esc_prev || vhas_bs) return fail_at(i, JE_UNSUP);
+            if (key_cmp(pk0[lv] & 0x7FFFFFFFu, pk1[lv], k0, k1) >= 0) return fail_at(i, JE_UNSUP);
+          }
+          pk0[lv] = k0 | (vhas_bs ? 0x80000000u : 0u);
+          pk1[lv] = k1;
+        }
+      }
+      c = ws();  // parse_object_colon
+      if (c == ':') {
+        eat();
+      } else if (c >= 0) {
+        return peek_error(JE_COLON);
+      } else {
+        return peek_error(JE_EOF_OBJECT);
+      }
+      vcanon += 1;
+    }
+  }
+  // from_slice::<Vec<Value>>: elements -> out[0..*count) (pos absolute, canonical
+  // length, bit 31 = canonical bytes equal the source bytes)
+  __device__ __forceinline__ JRes run_array(ElemRec* out, uint64_t abs0, uint32_t* count) {
+    r = JRes{0, 0, 0, 0, 0, 0, 0};
+    failed = false;
+    has_pos = false;
+    depth = 128;
+    i = 0;
+    uint32_t k = 0;
+    int rc = 0;
+    int c = ws();
+    if (c < 0) {
+      rc = peek_error(JE_EOF_VALUE);
+    } else if (c == '[') {
+      --depth;  // 127: cannot reach 0
+      eat();
+      bool first = true;
+      for (;;) {  // SeqAccess::next_element_seed
+        int p = ws();
+        if (p == ']') break;
+        if (p == ',' && !first) {
+          eat();
+          p = ws();
+        } else if (p >= 0) {
+          if (!first) {
+            rc = peek_error(JE_LIST_COMMA);
+            break;
+          }
+          first = false;
+        } else {
+          rc = peek_error(JE_EOF_LIST);
+          break;
+        }
+        if (p == ']') {
+          rc = peek_error(JE_TRAILING_COMMA);
+          break;
+        }
+        if (p < 0) {
+          rc = peek_error(JE_EOF_VALUE);
+          break;
+        }
+        const uint32_t e0 = i;
+        vcanon = 0;
+        vhas_u = false;
+        if (any_value()) {
+          rc = -1;
+          break;
+        }
+        const uint32_t span = i - e0;
+        const bool verb = span == vcanon && !vhas_u;
+        out[k].pos = abs0 + e0;
+        out[k].src_len = span;
+        out[k].out_len = vcanon | (verb ? 0x80000000u : 0u);
+        k++;
+      }
+      depth++;
+      if (!rc) rc = end_seq();
+    } else {
+      invalid_type(JX_SEQ);
+      rc = -1;
+    }
+    if (rc) fix_position();
+    if (!rc && ws() >= 0) rc = peek_error(JE_TRAILING);  // Deserializer::end
+    *count = k;
+    if (!rc) r.ok = 1;
+    return r;
+  }
+
   __device__ __forceinline__ JRes run() {
     int level = 0;
     r = JRes{0, 0, 0, 0, 0, 0, 0};
@@ -791,6 +1073,15 @@ __device__ __noinline__ JRes json_structured_log(const uint8_t* s, uint32_t n, b
   d.n = n;
   d.upper = upper;
   return d.run();
+}
+// array_map_json_array over one value: element descriptors to out[0..*count)
+__device__ __noinline__ JRes json_array_explode(const uint8_t* s, uint32_t n, bool upper, ElemRec* out, uint64_t abs0,
+                                               uint32_t* count) {
+  JsonDev<const uint8_t*> d;
+  d.s = s;
+  d.n = n;
+  d.upper = upper;
+  return d.run_array(out, abs0, count);
 }
 
 }  // namespace fsg

@@ -257,7 +257,7 @@ constexpr uint32_t opbit(int op) { return 1u << op; }
 constexpr uint32_t kOpsContains = opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
 constexpr uint32_t kOpsRegex = opbit(OP_REGEX) | opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
 constexpr uint32_t kOpsJson = opbit(OP_FILTER_JSON) | opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
-constexpr uint32_t kOpsAll = 0xFFu;
+constexpr uint32_t kOpsAll = 0x3FFu;
 constexpr int kDfaDyn = 768 + kDfaLds;  // dynamic LDS of a chain with a regex stage
 extern __shared__ __attribute__((aligned(16))) uint8_t g_dyn_lds[];
 
@@ -705,7 +705,7 @@ __device__ bool dfa_run_full(P s, uint32_t n, const uint8_t* blob, const DfaDesc
 // ---------------------------------------------------------------------------
 template <uint32_t kOps, bool kLds, typename P>
 __device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int nr, const ChainDesc& ch, const uint8_t* blob,
-                            int nst, int lds_stage, bool& unsupported STAMP_PARAMS) {
+                            int nst, int lds_stage, bool& unsupported, uint64_t wbase, ElemRec* elem STAMP_PARAMS) {
   const uint32_t l = threadIdx.x;
   bool nonascii_done = false;
   for (int s = 0; s < nst; s++) {
@@ -715,7 +715,7 @@ __device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int 
     const bool upper = sd.in_type == VT_SRC_UPPER;
     if (op == OP_MAP_UPPER) continue;  // value representation changes statically
     const bool need_utf8 = src && (op == OP_CONTAINS || op == OP_REGEX || op == OP_FILTER_ODD ||
-                                   op == OP_MAP_DOUBLE || op == OP_AGG_SUM);
+                                   op == OP_MAP_DOUBLE || op == OP_AGG_SUM || op == OP_AGG_CONCAT);
     // ---- data-parallel phase over window bytes
     for (int r = l; r < nr; r += kEvalThreads) L.r_flags[r] &= ~RF_MATCH;
     __syncthreads();
@@ -758,7 +758,8 @@ __device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int 
       bool err = false;
       uint32_t ec = 0;
       const int32_t ival_in = L.r_ival[r];
-      if ((kOps & opbit(OP_AGG_SUM)) && op == OP_AGG_SUM && sd.acc_bad) {
+      if ((kOps & (opbit(OP_AGG_SUM) | opbit(OP_AGG_CONCAT))) && (op == OP_AGG_SUM || op == OP_AGG_CONCAT) &&
+          sd.acc_bad) {
         err = true;
         ec = EC_ACC_UTF8;
         L.r_aux[r] = sd.acc_vut;
@@ -833,6 +834,41 @@ __device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int 
             } else if (jr.level == 0) {
               f &= ~RF_ALIVE;  // level > Debug keeps the record
             }
+            break;
+          }
+          case OP_ARRAY_MAP: {
+            // array_map_json_array: serde_json::from_slice::<Vec<Value>> (no from_utf8 first)
+            if constexpr (!(kOps & opbit(OP_ARRAY_MAP))) break;
+            uint8_t t[12];
+            const uint8_t* js = (const uint8_t*)&w[vs];
+            uint32_t jn = vl;
+            if (!src) {
+              jn = fmt_i32(ival_in, t);
+              js = t;
+            }
+            const uint64_t av = wbase + vs;
+            uint32_t ne = 0;
+            const JRes jr = json_array_explode(js, jn, src && upper, elem + (av >> 1), av, &ne);
+            if (!jr.ok) {
+              err = true;
+              if (jr.code == JE_UNSUP) {
+                ec = EC_UNSUP;
+              } else {
+                ec = EC_JSON | ((uint32_t)jr.code << 8) | ((uint32_t)jr.sub << 16);
+                L.r_aux[r] = jr.pos;
+                L.r_aux2[r] = jr.a;
+                L.r_aux3[r] = jr.b;
+              }
+            } else {
+              L.r_ival[r] = (int32_t)ne;  // element count
+            }
+            break;
+          }
+          case OP_AGG_CONCAT: {
+            // aggregate: acc.push_str(from_utf8(value)?) — the bytes this record appends
+            if constexpr (!(kOps & opbit(OP_AGG_CONCAT))) break;
+            L.r_ival[r] = src ? (int32_t)vl : (int32_t)dec_len_i32(ival_in);
+            if (!src) L.r_ival_in[r] = ival_in;
             break;
           }
           case OP_FILTER_ODD:
@@ -968,19 +1004,26 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
   int nst = (int)ch.nstages;
   uint32_t err_stage = 0xFFFFFFFFu, err_idx = 0xFFFFFFFFu;
   bool unsupported = false;
-  uint32_t kcount = 0;
+  uint32_t kcount = 0, nout = 0;
   int64_t aggsum = 0;
+  uint64_t catsum = 0;
   for (int phase = 0; phase < 2 && !(flags & BF_DECODE); phase++) {
     if (phase == 1) {
       if (err_stage == 0xFFFFFFFFu) break;
       nst = (int)err_stage + 1;
     }
     kcount = 0;
+    nout = 0;
     aggsum = 0;
+    catsum = 0;
     uint64_t cursor = sec0 + 4;
     uint32_t done_recs = 0;
     const uint32_t rec_cap = phase == 1 ? err_idx : nrec_total;
-    const bool agg_on = (kOps & opbit(OP_AGG_SUM)) && ch.has_agg && (phase == 0 || err_stage + 1 == ch.nstages);
+    const bool full = nst == (int)ch.nstages;  // this phase's output is the last stage's
+    const bool agg_on = (kOps & opbit(OP_AGG_SUM)) && (ch.flags & CF_AGG_SUM) && full;
+    const bool cat_on = (kOps & opbit(OP_AGG_CONCAT)) && (ch.flags & CF_AGG_CAT) && full;
+    const bool arr_on = (kOps & opbit(OP_ARRAY_MAP)) && (ch.flags & CF_ARRAY) && full;
+    const uint8_t last_in = ch.st[ch.nstages - 1].in_type;
     const int last = nst - 1;
     const uint8_t out_type = (nst == (int)ch.nstages) ? (uint8_t)ch.out_type : ch.st[nst].in_type;
     while (done_recs < nrec_total && done_recs < (phase == 1 ? rec_cap + 1 : nrec_total)) {
@@ -1029,10 +1072,10 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
       if (phase == 1 && done_recs + (uint32_t)nr > err_idx + 1) nr_eval = (int)(err_idx + 1 - done_recs);
       if (global_mode)
         eval_window<kOps, false>(L, S + gbase, (uint32_t)(sec_end - gbase), nr_eval, ch, a.blob, nst, lds_stage,
-                           unsupported STAMP_ARGS);
+                           unsupported, gbase, a.elem STAMP_ARGS);
       else
         eval_window<kOps, true>(L, (const uint8_t*)L.win, wlen, nr_eval, ch, a.blob, nst, lds_stage,
-                          unsupported STAMP_ARGS);
+                          unsupported, al, a.elem STAMP_ARGS);
       const uint64_t wbase = global_mode ? gbase : al;
       STAMP(3);
       // ---- error tracking (phase A) and descriptor emission: wave 0, in record order
@@ -1076,6 +1119,20 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
         const uint64_t bal = ballot(kept);
         const uint32_t pre = (uint32_t)__popcll(bal & ((1ull << l) - 1ull));
         int32_t local = 0;
+        uint32_t cat_local = 0;
+        uint32_t outs = kept ? 1u : 0u;
+        if (arr_on) outs = kept ? (uint32_t)L.r_ival[r] : 0u;
+        if (cat_on) {
+          // u32 inclusive scan of the appended byte counts
+          uint32_t uv = kept ? (uint32_t)L.r_ival[r] : 0u;
+          for (int o = 1; o < 64; o <<= 1) {
+            uint32_t t = __shfl_up(uv, o, 64);
+            if ((int)l >= o) uv += t;
+          }
+          cat_local = (uint32_t)catsum + uv;
+          catsum += __shfl(uv, 63, 64);
+        }
+        nout += (uint32_t)wave_sum(outs);
         if (agg_on) {
           int32_t v = kept ? L.r_ival[r] : 0;
           // wrapping i32 inclusive scan
@@ -1100,9 +1157,23 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
           d.hdr = L.r_hdr[r];
           d.vpos = wbase + L.r_vs[r];
           d.vlen = L.r_vl[r];
+          d.pad = 0;
           if (agg_on) {
             d.mode = KM_AGG;
             d.ival = local;
+          } else if (arr_on) {
+            d.mode = KM_ARRAY;
+            d.ival = L.r_ival[r];
+            d.pad = last_in == VT_SRC_UPPER ? KF_UPPER : 0;
+          } else if (cat_on) {
+            d.mode = KM_CONCAT;
+            d.ival = (int32_t)cat_local;
+            if (last_in == VT_I32) {
+              d.pad = KF_I32;
+              d.vlen = (uint32_t)L.r_ival_in[r];
+            } else {
+              d.pad = last_in == VT_SRC_UPPER ? KF_UPPER : 0;
+            }
           } else if (out_type == VT_I32) {
             d.mode = KM_I32;
             d.ival = L.r_ival[r];
@@ -1139,7 +1210,11 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
     st.nkeep = kcount;
     st.sec_len = sec_len;
     st.err_stage = err_stage;
-    st.agg_sum = (ch.has_agg && (err_stage == 0xFFFFFFFFu || err_stage + 1 == ch.nstages)) ? aggsum : 0;
+    const bool agg_ran = err_stage == 0xFFFFFFFFu || err_stage + 1 == ch.nstages;
+    st.agg_sum = (ch.has_agg && agg_ran) ? aggsum : 0;
+    st.nout = nout;
+    st.pad = 0;
+    st.cat_sum = (ch.has_agg && agg_ran) ? catsum : 0;
     a.bstat[b] = st;  // the cross-batch minima are reduced by k_mins
   }
   STAMP(5);
@@ -1545,6 +1620,7 @@ __global__ __launch_bounds__(kLeanThreads) void k_eval_lean(EvalArgs a) {
     st.first_ts = first_ts;
     st.flags = BF_LAST_STAGE;
     st.nkeep = (uint32_t)__popcll(alive);
+    st.nout = st.nkeep;
     st.sec_len = sec_len;
     st.err_stage = 0xFFFFFFFFu;
     a.bstat[b] = st;
@@ -1561,7 +1637,7 @@ __global__ __launch_bounds__(256) void k_mins(const BatchStat* bstat, uint32_t n
   uint32_t fk = 0xFFFFFFFFu, fe = 0xFFFFFFFFu, fd = 0xFFFFFFFFu, fu = 0xFFFFFFFFu;
   for (uint32_t b = blockIdx.x * 256 + threadIdx.x; b < n; b += gridDim.x * 256) {
     const uint32_t f = bstat[b].flags;
-    const uint32_t nk = bstat[b].nkeep;
+    const uint32_t nk = bstat[b].nout;  // batches whose stage output is non-empty
     if (f & BF_DECODE) fd = fd < b ? fd : b;
     if (f & BF_UNSUPPORTED) fu = fu < b ? fu : b;
     if (!(f & BF_DECODE)) {
@@ -1591,19 +1667,34 @@ __global__ __launch_bounds__(256) void k_mins(const BatchStat* bstat, uint32_t n
 // ---------------------------------------------------------------------------
 // output record size of a descriptor after the offset fix-up
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t out_vlen(const KeptRec& d, int32_t agg_base) {
+__device__ __forceinline__ uint32_t out_vlen(const KeptRec& d, int32_t agg_base, uint64_t cat_base) {
   if (d.mode == KM_I32) return dec_len_i32(d.ival);
   if (d.mode == KM_AGG) return dec_len_i32((int32_t)((uint32_t)agg_base + (uint32_t)d.ival));
+  if (d.mode == KM_CONCAT) return (uint32_t)(cat_base + (uint32_t)d.ival);  // whole accumulator after this record
   return d.vlen;
 }
-__device__ __forceinline__ uint32_t rec_out_size(const KeptRec& d, int64_t rel, int32_t agg_base) {
-  const uint32_t vl = out_vlen(d, agg_base);
+__device__ __forceinline__ uint32_t rec_out_size(const KeptRec& d, int64_t rel, int32_t agg_base, uint64_t cat_base) {
+  const uint32_t vl = out_vlen(d, agg_base, cat_base);
   uint32_t inner = 1 + vsize(d.ts) + vsize(d.od + rel) + 1 + (d.has_key ? vsize((int64_t)d.klen) + d.klen : 0) +
                    vsize((int64_t)vl) + vl + vsize(d.hdr);
   return vsize((int64_t)inner) + inner;
 }
-
-
+// one array_map output record: Record::new_key_value(None, element) — default
+// preamble (attributes 0, timestamp_delta 0, offset_delta 0 + rel, no headers)
+__device__ __forceinline__ uint32_t elem_inner(uint32_t len, int64_t rel) {
+  return 1 + 1 + vsize(rel) + 1 + vsize((int64_t)len) + len + 1;
+}
+__device__ __forceinline__ uint32_t elem_out_size(uint32_t len, int64_t rel) {
+  const uint32_t inner = elem_inner(len, rel);
+  return vsize((int64_t)inner) + inner;
+}
+// Σ output record sizes of the elements of one KM_ARRAY record
+__device__ __forceinline__ uint64_t array_rec_bytes(const KeptRec& d, const ElemRec* elem, int64_t rel) {
+  const ElemRec* e = elem + (d.vpos >> 1);
+  uint64_t s = 0;
+  for (int32_t j = 0; j < d.ival; j++) s += elem_out_size(e[j].out_len & 0x7FFFFFFFu, rel);
+  return s;
+}
 
 // k_size: one wave per batch (4 batches per 256-thread block)
 __global__ __launch_bounds__(256) void k_size(SizeArgs a) {
@@ -1615,23 +1706,29 @@ __global__ __launch_bounds__(256) void k_size(SizeArgs a) {
   ScanRow row = {};
   if (a.agg_only) {
     row.agg = st.agg_sum;
+    row.cat = st.cat_sum;
     if (l == 0) a.rows[b] = row;
     return;
   }
   row.bytes_in = st.sec_len;
-  row.recs_out = (st.flags & BF_LAST_STAGE) ? st.nkeep : 0;
+  row.recs_out = (st.flags & BF_LAST_STAGE) ? st.nout : 0;
   row.agg = st.agg_sum;
+  row.cat = st.cat_sum;
   if (f != 0xFFFFFFFFu && b >= f && !(st.flags & BF_DECODE)) {
     const int64_t rel = a.bstat[f].base_offset - st.base_offset;
     const int32_t agg_base = a.agg_pre ? (int32_t)((uint64_t)a.acc0 + (uint64_t)a.agg_pre[b].agg) : 0;
+    const uint64_t cat_base = a.agg_pre ? a.acc_len + a.agg_pre[b].cat : 0;
     uint64_t sum = 0;
     const KeptRec* d = a.desc + a.rbase[b];
-    for (uint32_t k = l; k < st.nkeep; k += 64) sum += rec_out_size(d[k], rel, agg_base);
+    for (uint32_t k = l; k < st.nkeep; k += 64) {
+      const KeptRec r = d[k];
+      sum += r.mode == KM_ARRAY ? array_rec_bytes(r, a.elem, rel) : rec_out_size(r, rel, agg_base, cat_base);
+    }
     sum = wave_sum(sum);
     row.rec_bytes = sum;
-    row.nonempty = st.nkeep ? 1 : 0;
+    row.nonempty = st.nout ? 1 : 0;
     row.lod = (uint64_t)(int64_t)(st.lod_in + 1);
-    row.nrec = st.nkeep;
+    row.nrec = st.nout;
   }
   if (l == 0) a.rows[b] = row;
 }
@@ -1651,6 +1748,7 @@ __device__ __forceinline__ void row_add(ScanRow& a, const ScanRow& b) {
   a.bytes_in += b.bytes_in;
   a.recs_out += b.recs_out;
   a.agg = (int64_t)(int32_t)((uint32_t)a.agg + (uint32_t)b.agg);
+  a.cat += b.cat;
 }
 
 __device__ void block_excl_scan(ScanRow& v, ScanRow* sh, ScanRow& total) {
@@ -1810,6 +1908,7 @@ __global__ void k_plan(PlanArgs a) {
   p.records_out = rs.recs_out;
   if (a.has_agg) {
     p.acc_final = (int64_t)(int32_t)((uint64_t)a.acc0 + (uint64_t)rs.agg);
+    p.cat_final = rs.cat;
     p.acc_touched = rs.recs_out > 0;  // aggregate emits one record per aggregated input
   }
   const int64_t last = cut ? (int64_t)c - 1 : (int64_t)stop;
@@ -1923,10 +2022,187 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t x, uint32_t lane) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// serde_json::to_string of a validated JSON value whose objects are already in
+// key order (checked by json_array_explode): drop whitespace outside strings,
+// re-escape strings (ser.rs format_escaped_str: \" \\ \b \t \n \f \r, other
+// control bytes \u00xx, everything else raw).  One lane, rare path (elements
+// whose canonical bytes differ from their source bytes).
+__device__ void json_canon_write(const uint8_t* __restrict__ s, uint32_t n, bool upper, uint8_t* __restrict__ o) {
+  auto at = [&](uint32_t k) -> uint32_t {
+    uint8_t c = s[k];
+    if (upper && c >= 'a' && c <= 'z') c -= 32;
+    return c;
+  };
+  auto hexv = [](uint32_t c) -> uint32_t { return c <= '9' ? c - '0' : (c | 0x20) - 'a' + 10; };
+  auto put_esc = [&](uint32_t c) {  // one decoded byte c < 0x80
+    const char* hx = "0123456789abcdef";
+    switch (c) {
+      case '"': *o++ = '\\'; *o++ = '"'; return;
+      case '\\': *o++ = '\\'; *o++ = '\\'; return;
+      case 0x08: *o++ = '\\'; *o++ = 'b'; return;
+      case 0x09: *o++ = '\\'; *o++ = 't'; return;
+      case 0x0A: *o++ = '\\'; *o++ = 'n'; return;
+      case 0x0C: *o++ = '\\'; *o++ = 'f'; return;
+      case 0x0D: *o++ = '\\'; *o++ = 'r'; return;
+      default:
+        if (c < 0x20) {
+          *o++ = '\\'; *o++ = 'u'; *o++ = '0'; *o++ = '0';
+          *o++ = (uint8_t)hx[c >> 4];
+          *o++ = (uint8_t)hx[c & 15];
+        } else {
+          *o++ = (uint8_t)c;
+        }
+    }
+  };
+  uint32_t i = 0;
+  while (i < n) {
+    const uint32_t c = at(i);
+    if (c == ' ' || c == '\n' || c == '\t' || c == '\r') {
+      i++;
+      continue;
+    }
+    if (c != '"') {
+      *o++ = (uint8_t)c;
+      i++;
+      continue;
+    }
+    *o++ = '"';
+    i++;
+    for (;;) {
+      const uint32_t d = at(i++);
+      if (d == '"') break;
+      if (d != '\\') {
+        if (d < 0x80) put_esc(d); else *o++ = (uint8_t)d;
+        continue;
+      }
+      const uint32_t e = at(i++);
+      uint32_t cp;
+      switch (e) {
+        case 'b': cp = 0x08; break;
+        case 'f': cp = 0x0C; break;
+        case 'n': cp = 0x0A; break;
+        case 'r': cp = 0x0D; break;
+        case 't': cp = 0x09; break;
+        case 'u': {
+          cp = (hexv(at(i)) << 12) | (hexv(at(i + 1)) << 8) | (hexv(at(i + 2)) << 4) | hexv(at(i + 3));
+          i += 4;
+          if (cp >= 0xD800 && cp <= 0xDBFF) {  // validated pair
+            const uint32_t c2 = (hexv(at(i + 2)) << 12) | (hexv(at(i + 3)) << 8) | (hexv(at(i + 4)) << 4) | hexv(at(i + 5));
+            i += 6;
+            cp = (((cp - 0xD800) << 10) | (c2 - 0xDC00)) + 0x10000;
+          }
+          break;
+        }
+        default: cp = e; break;  // " \ /
+      }
+      if (cp < 0x80) {
+        put_esc(cp);
+      } else if (cp < 0x800) {
+        *o++ = (uint8_t)(0xC0 | (cp >> 6));
+        *o++ = (uint8_t)(0x80 | (cp & 0x3F));
+      } else if (cp < 0x10000) {
+        *o++ = (uint8_t)(0xE0 | (cp >> 12));
+        *o++ = (uint8_t)(0x80 | ((cp >> 6) & 0x3F));
+        *o++ = (uint8_t)(0x80 | (cp & 0x3F));
+      } else {
+        *o++ = (uint8_t)(0xF0 | (cp >> 18));
+        *o++ = (uint8_t)(0x80 | ((cp >> 12) & 0x3F));
+        *o++ = (uint8_t)(0x80 | ((cp >> 6) & 0x3F));
+        *o++ = (uint8_t)(0x80 | (cp & 0x3F));
+      }
+    }
+  }
+}
+
+constexpr uint32_t kElemLaneCopy = 48;  // array elements up to this size are copied by their own lane
+
+// array_map batch (derive generator/array_map.rs:17-42): the elements of the
+// batch's kept records, flattened 64 at a time over the wave.  Lane = element:
+// size, wave scan, record header (default preamble + offset fix-up), payload
+// (short verbatim elements by the lane, long ones by the whole wave, the rest
+// through the canonicalizer).
+__device__ void write_array_batch(const WriteArgs& a, const KeptRec* d, uint32_t nkeep, int64_t rel, uint64_t obase) {
+  const uint32_t lane = lane_id();
+  uint8_t* out = a.out;
+  uint64_t run = 0;
+  for (uint32_t k0 = 0; k0 < nkeep; k0 += 64) {
+    const uint32_t k = k0 + lane;
+    const bool v = k < nkeep;
+    uint32_t ne = 0, flg = 0;
+    uint64_t sb = 0;
+    if (v) {
+      const KeptRec r = d[k];
+      ne = (uint32_t)r.ival;
+      sb = r.vpos >> 1;
+      flg = r.pad;
+    }
+    const uint32_t eincl = wave_incl_scan(ne);
+    const uint32_t eex = eincl - ne;
+    const uint32_t tot = __builtin_amdgcn_readlane(eincl, 63);
+    for (uint32_t e0 = 0; e0 < tot; e0 += 64) {
+      const uint32_t e = e0 + lane;
+      const bool ev = e < tot;
+      // record of element e: the last lane whose exclusive prefix <= e
+      uint32_t rr = 0;
+#pragma unroll
+      for (uint32_t st = 32; st > 0; st >>= 1) {
+        const uint32_t c = rr + st;
+        const uint32_t pc = __shfl(eex, (int)(c & 63), 64);
+        if (c < 64 && pc <= e) rr = c;
+      }
+      const uint32_t rex = __shfl(eex, (int)rr, 64);
+      const uint64_t rsb = ((uint64_t)__shfl((uint32_t)(sb >> 32), (int)rr, 64) << 32) | __shfl((uint32_t)sb, (int)rr, 64);
+      const bool upper = (__shfl(flg, (int)rr, 64) & KF_UPPER) != 0;
+      ElemRec er = {0, 0, 0};
+      if (ev) er = a.elem[rsb + (e - rex)];
+      const uint32_t len = er.out_len & 0x7FFFFFFFu;
+      const bool verb = (er.out_len >> 31) != 0;
+      const uint32_t sz = ev ? elem_out_size(len, rel) : 0u;
+      const uint64_t incl = wave_incl_scan((uint64_t)sz);
+      const uint64_t my = obase + run + incl - sz;
+      bool wave_copy = false;
+      if (ev) {
+        uint8_t* q = out + my;
+        uint8_t t[16];
+        uint32_t w = 0;
+        uint32_t nn = venc((int64_t)elem_inner(len, rel), t);
+        for (uint32_t i = 0; i < nn; i++) q[w++] = t[i];
+        q[w++] = 0;  // attributes
+        q[w++] = 0;  // timestamp_delta
+        nn = venc(rel, t);
+        for (uint32_t i = 0; i < nn; i++) q[w++] = t[i];
+        q[w++] = 0;  // key: None
+        nn = venc((int64_t)len, t);
+        for (uint32_t i = 0; i < nn; i++) q[w++] = t[i];
+        if (!verb) {
+          json_canon_write(a.slice + er.pos, er.src_len, upper, q + w);
+        } else if (len <= kElemLaneCopy) {
+          const uint8_t* src = a.slice + er.pos;
+          for (uint32_t i = 0; i < len; i++) q[w + i] = upper ? up(src[i]) : src[i];
+        } else {
+          wave_copy = true;
+        }
+        q[w + len] = 0;  // headers
+      }
+      // long verbatim elements: whole-wave copies
+      uint64_t pend = __ballot(wave_copy);
+      while (pend) {
+        const uint32_t i = (uint32_t)__builtin_ctzll(pend);
+        pend &= pend - 1;
+        const uint32_t il = __builtin_amdgcn_readlane(len, i);
+        const uint64_t dst = readlane_u64(my, i) + elem_out_size(il, rel) - il - 1;
+        copy_seg(out, a.slice, dst, readlane_u64(er.pos, i), il, __builtin_amdgcn_readlane((uint32_t)upper, i) != 0);
+      }
+      run += readlane_u64(incl, 63);
+    }
+  }
+}
+
 // k_write — one wave per included batch (four per 256-thread block).  Per chunk
 // of up to 64 survivors: lane = record: size, wave scan, varint header fields
 // and i32 values; then the wave walks the chunk's records in order and copies
-// each key/value payload with all 64 lanes (copy_seg).
+// each key/value payload with all 64 lanes (copy_seg).  aggregate (concat)
+// values are prefixes of the accumulator stream built by k_cat.
 constexpr int kWriteThreads = 256;
 __global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
   const Plan p = *a.plan;
@@ -1936,9 +2212,14 @@ __global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
   const BatchStat st = a.bstat[b];
   const int64_t rel = a.bstat[p.first].base_offset - st.base_offset;
   const int32_t agg_base = a.agg_pre ? (int32_t)((uint64_t)a.acc0 + (uint64_t)a.agg_pre[b].agg) : 0;
+  const uint64_t cat_base = a.agg_pre ? a.acc_len + a.agg_pre[b].cat : 0;
   const KeptRec* d = a.desc + a.rbase[b];
   const uint64_t obase = 61 + (a.pre[b].rec_bytes - a.pre[p.first].rec_bytes);
   uint8_t* out = a.out;
+  if (st.nkeep && d[0].mode == KM_ARRAY) {  // a batch's descriptors share one mode
+    write_array_batch(a, d, st.nkeep, rel, obase);
+    return;
+  }
   uint64_t run = 0;
   for (uint32_t k0 = 0; k0 < st.nkeep; k0 += 64) {
     const uint32_t k = k0 + lane;
@@ -1947,15 +2228,15 @@ __global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
     uint32_t sz = 0;
     if (v) {
       r = d[k];
-      sz = rec_out_size(r, rel, agg_base);
+      sz = rec_out_size(r, rel, agg_base, cat_base);
     }
     const uint64_t incl = wave_incl_scan((uint64_t)sz);
     const uint64_t my = obase + run + incl - sz;
-    uint64_t kd = 0, vd = 0;
+    uint64_t kd = 0, vd = 0, vsrc = 0;
     uint32_t kl = 0, vc = 0;
     if (v) {
       uint8_t* q = out + my;
-      const uint32_t vl = out_vlen(r, agg_base);
+      const uint32_t vl = out_vlen(r, agg_base, cat_base);
       const uint32_t inner = 1 + vsize(r.ts) + vsize(r.od + rel) + 1 +
                              (r.has_key ? vsize((int64_t)r.klen) + r.klen : 0) + vsize((int64_t)vl) + vl + vsize(r.hdr);
       uint8_t t[16];
@@ -1982,6 +2263,7 @@ __global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
         w += fmt_i32(x, q + w);
       } else {
         vc = vl;
+        vsrc = r.mode == KM_CONCAT ? kCatOff : r.vpos;
         w += vl;
       }
       n = venc(r.hdr, t);
@@ -1989,15 +2271,52 @@ __global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
     }
     // payloads, record by record, with the whole wave
     const uint32_t nrec = st.nkeep - k0 < 64u ? st.nkeep - k0 : 64u;
+    const bool cat = st.nkeep && d[0].mode == KM_CONCAT;
     for (uint32_t i = 0; i < nrec; i++) {
       const uint32_t rkl = __builtin_amdgcn_readlane(kl, i);
       const uint32_t rvc = __builtin_amdgcn_readlane(vc, i);
       if (rkl) copy_seg(out, a.slice, readlane_u64(kd, i), readlane_u64(r.kpos, i), rkl, false);
       if (rvc)
-        copy_seg(out, a.slice, readlane_u64(vd, i), readlane_u64(r.vpos, i), rvc,
+        copy_seg(out, cat ? a.cat : a.slice, readlane_u64(vd, i), readlane_u64(vsrc, i), rvc,
                  __builtin_amdgcn_readlane((uint32_t)r.mode, i) == KM_UPPER);
     }
     run += readlane_u64(incl, 63);
+  }
+}
+
+// k_cat — aggregate (concat) accumulator stream: cat[kCatOff..] = initial
+// accumulator ++ the appended value of every aggregated record of batches
+// 0..stop, in stream order (smartmodule/examples/aggregate/src/lib.rs:7-13:
+// acc.push_str(value)).  One wave per batch; the initial accumulator was
+// copied by the host.
+__global__ __launch_bounds__(256) void k_cat(WriteArgs a, uint32_t nbatches) {
+  const Plan p = *a.plan;
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= nbatches || (int32_t)b > p.stop) return;
+  const uint32_t lane = lane_id();
+  const BatchStat st = a.bstat[b];
+  const KeptRec* d = a.desc + a.rbase[b];
+  if (!st.nkeep || d[0].mode != KM_CONCAT) return;
+  uint8_t* cat = (uint8_t*)a.cat;
+  const uint64_t base = kCatOff + a.acc_len + a.agg_pre[b].cat;
+  for (uint32_t k0 = 0; k0 < st.nkeep; k0 += 64) {
+    const uint32_t k = k0 + lane;
+    KeptRec r = {};
+    uint32_t n = 0;
+    uint64_t dst = 0;
+    if (k < st.nkeep) {
+      r = d[k];
+      n = (r.pad & KF_I32) ? dec_len_i32((int32_t)r.vlen) : r.vlen;
+      dst = base + (uint32_t)r.ival - n;
+      if (r.pad & KF_I32) fmt_i32((int32_t)r.vlen, cat + dst);
+    }
+    const uint32_t nrec = st.nkeep - k0 < 64u ? st.nkeep - k0 : 64u;
+    for (uint32_t i = 0; i < nrec; i++) {
+      const uint32_t rn = __builtin_amdgcn_readlane(n, i);
+      const uint32_t fl = __builtin_amdgcn_readlane((uint32_t)r.pad, i);
+      if (rn && !(fl & KF_I32))
+        copy_seg(cat, a.slice, readlane_u64(dst, i), readlane_u64(r.vpos, i), rn, (fl & KF_UPPER) != 0);
+    }
   }
 }
 
@@ -2202,6 +2521,9 @@ void launch_scan(const ScanRow* rows, ScanRow* pre, ScanRow* tile_sums, ScanRow*
 void launch_plan(const PlanArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_plan, dim3(1), dim3(64), 0, s, a); }
 void launch_header(const Plan* plan, uint8_t* out, hipStream_t s) {
   hipLaunchKernelGGL(k_header, dim3(1), dim3(64), 0, s, plan, out);
+}
+void launch_cat(const WriteArgs& a, uint32_t nbatches, hipStream_t s) {
+  if (nbatches) hipLaunchKernelGGL(k_cat, dim3((nbatches + 3) / 4), dim3(256), 0, s, a, nbatches);
 }
 void launch_write(const WriteArgs& a, uint32_t nblocks, hipStream_t s) {
   // nblocks = included batches, one wave each

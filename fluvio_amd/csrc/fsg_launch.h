@@ -16,5 +16,6 @@ void launch_scan(const ScanRow* rows, ScanRow* pre, ScanRow* tile_sums, ScanRow*
 void launch_plan(const PlanArgs& a, hipStream_t s);
 void launch_header(const Plan* plan, uint8_t* out, hipStream_t s);
 void launch_write(const WriteArgs& a, uint32_t nblocks, hipStream_t s);
+void launch_cat(const WriteArgs& a, uint32_t nbatches, hipStream_t s);
 void launch_crc(uint8_t* out, uint64_t off, uint64_t n, uint32_t* acc, hipStream_t s);
 }  // namespace fsg

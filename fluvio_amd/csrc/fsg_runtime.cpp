@@ -224,9 +224,10 @@ struct fsg_chain {
   DevBuf d_desc, d_blob;
   std::vector<std::string> names;
   int agg_stage = -1;
+  int array_stage = -1;
   std::vector<uint8_t> acc;  // aggregate accumulator bytes (SmartModuleAggregate.accumulator)
   // scratch
-  DevBuf bstat, kept, rows, pre, aggpre, tiles, grand, mins, plan, out, crcparts, defer;
+  DevBuf bstat, kept, rows, pre, aggpre, tiles, grand, mins, plan, out, crcparts, defer, elem, cat;
   Plan hplan{};
   hipEvent_t ev[6] = {};
   fsg_timings last{};
@@ -299,6 +300,7 @@ std::string init_error(const std::string& what) { return what + "\n\nSmartModule
 int add_stage(fsg_chain* c, const ModuleSpec& m, const std::string& name, uint8_t& vt) {
   if (c->hdesc.nstages >= (uint32_t)kMaxStages) return fail(FSG_E_UNSUPPORTED, "chain longer than 8 stages");
   if (c->agg_stage >= 0) return fail(FSG_E_UNSUPPORTED, "stages after an aggregate are not implemented on the GPU");
+  if (c->array_stage >= 0) return fail(FSG_E_UNSUPPORTED, "stages after an array_map are not implemented on the GPU");
   StageDesc sd{};
   sd.in_type = vt;
   auto param = [&](const char* k) -> const std::string* {
@@ -384,8 +386,15 @@ int add_stage(fsg_chain* c, const ModuleSpec& m, const std::string& name, uint8_
     c->agg_stage = (int)c->hdesc.nstages;
     c->acc = m.has_acc ? m.acc : std::vector<uint8_t>();
     vt = VT_I32;
-  } else if (name == "aggregate") {
-    return fail(FSG_E_UNSUPPORTED, "the string-concatenating aggregate example is not implemented on the GPU");
+  } else if (name == "aggregate") {  // examples/aggregate: acc.push_str(from_utf8(value)?)
+    sd.op = OP_AGG_CONCAT;
+    sd.kind = FSG_KIND_AGGREGATE;
+    c->agg_stage = (int)c->hdesc.nstages;
+    c->acc = m.has_acc ? m.acc : std::vector<uint8_t>();
+  } else if (name == "array_map_json_array") {  // examples/array_map_json_array: explode a JSON array
+    sd.op = OP_ARRAY_MAP;
+    sd.kind = FSG_KIND_ARRAY_MAP;
+    c->array_stage = (int)c->hdesc.nstages;
   } else {
     return fail(FSG_E_UNKNOWN_SM, "No valid smartmodule found");
   }
@@ -415,6 +424,9 @@ extern "C" int fsg_chain_builder_initialize(fsg_chain_builder* b, fsg_engine* e,
   }
   c->hdesc.out_type = vt;
   c->hdesc.has_agg = c->agg_stage >= 0;
+  if (c->agg_stage >= 0)
+    c->hdesc.flags |= c->hdesc.st[c->agg_stage].op == OP_AGG_SUM ? CF_AGG_SUM : CF_AGG_CAT;
+  if (c->array_stage >= 0) c->hdesc.flags |= CF_ARRAY;
   if (c->agg_stage >= 0) {
     StageDesc& sd = c->hdesc.st[c->agg_stage];
     uint32_t vut = 0, el = 0;
@@ -613,7 +625,8 @@ bool json_hint(uint32_t code_word, uint32_t pos, uint32_t a, uint32_t b, const s
     json_unescape(v, a, b, val);
     msg = "unknown variant `" + val + "`, expected one of `debug`, `info`, `warn`, `error`";
   } else if (code == JE_INVALID_TYPE) {
-    static const char* const kExp[] = {"struct StructuredLog", "a string", "variant identifier", "unit"};
+    static const char* const kExp[] = {"struct StructuredLog", "a string", "variant identifier", "unit",
+                                       "a sequence", "", "", ""};
     std::string un;
     switch (sub & 15) {
       case JU_UNIT: un = "unit value"; break;
@@ -642,7 +655,7 @@ bool json_hint(uint32_t code_word, uint32_t pos, uint32_t a, uint32_t b, const s
       case JU_MAP: un = "map"; break;
       default: return false;  // JU_FLOAT
     }
-    msg = "invalid type: " + un + ", expected " + kExp[(sub >> 4) & 3];
+    msg = "invalid type: " + un + ", expected " + kExp[(sub >> 4) & 7];
   } else {
     return false;  // JE_DEEP
   }
@@ -758,8 +771,10 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   const uint32_t nb = s->nb;
   memset(res, 0, sizeof *res);
   // scratch (StoreMemoryExceeded past the store limit, limiter.rs:18-35)
+  const bool has_array = c->array_stage >= 0;
+  const size_t elem_cap = has_array ? (s->len / 2 + 2) : 0;  // ElemRec slots (fsg_device.h)
   const size_t need = (size_t)std::max<uint32_t>(nb, 1) * (sizeof(BatchStat) + 3 * sizeof(ScanRow)) +
-                      (size_t)std::max<uint64_t>(s->nrec, 1) * sizeof(KeptRec);
+                      (size_t)std::max<uint64_t>(s->nrec, 1) * sizeof(KeptRec) + elem_cap * sizeof(ElemRec);
   if (need > c->limit) {
     char b[160];
     snprintf(b, sizeof b, "Requested memory %zub exceeded max allowed %zub", need, c->limit);
@@ -775,8 +790,10 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   HIPCHK(c->grand.ensure(sizeof(ScanRow)));
   HIPCHK(c->mins.ensure(sizeof(Mins)));
   HIPCHK(c->plan.ensure(sizeof(Plan)));
+  if (has_array) HIPCHK(c->elem.ensure(elem_cap * sizeof(ElemRec)));
   const bool has_agg = c->agg_stage >= 0;
-  const int64_t acc0 = has_agg ? acc_value(c->acc) : 0;
+  const bool has_cat = has_agg && (c->hdesc.flags & CF_AGG_CAT);
+  const int64_t acc0 = has_agg && !has_cat ? acc_value(c->acc) : 0;
 
   HIPCHK(hipMemsetAsync(c->mins.p, 0xFF, sizeof(Mins), st));
   HIPCHK(hipEventRecord(c->ev[0], st));
@@ -792,6 +809,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   ea.desc = c->kept.as<KeptRec>();
   ea.mins = c->mins.as<Mins>();
   ea.list = c->defer.as<uint32_t>();
+  ea.elem = has_array ? c->elem.as<ElemRec>() : nullptr;
   uint32_t ops = 0;
   for (uint32_t k = 0; k < c->hdesc.nstages; k++) ops |= 1u << c->hdesc.st[k].op;
   // substring filters + uppercase maps: the one-wave lean kernel first, the
@@ -810,6 +828,8 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   sa.rows = c->rows.as<ScanRow>();
   sa.nbatches = nb;
   sa.acc0 = acc0;
+  sa.elem = ea.elem;
+  sa.acc_len = has_cat ? c->acc.size() : 0;
   if (has_agg) {
     sa.agg_only = 1;
     launch_size(sa, st);
@@ -863,6 +883,15 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   wa.plan = pa.plan;
   wa.out = c->out.as<uint8_t>();
   wa.acc0 = acc0;
+  wa.elem = ea.elem;
+  wa.acc_len = sa.acc_len;
+  if (has_cat) {  // the accumulator stream: initial accumulator ++ appended values (k_cat)
+    HIPCHK(c->cat.ensure(kCatOff + c->acc.size() + p.cat_final + 64));
+    if (!c->acc.empty())
+      HIPCHK(hipMemcpyAsync(c->cat.as<uint8_t>() + kCatOff, c->acc.data(), c->acc.size(), hipMemcpyHostToDevice, st));
+    wa.cat = c->cat.as<uint8_t>();
+    launch_cat(wa, nb, st);
+  }
   launch_header(pa.plan, wa.out, st);
   HIPCHK(hipEventRecord(c->ev[3], st));
   launch_write(wa, p.last >= p.first && p.first >= 0 ? (uint32_t)(p.last - p.first + 1) : 0u, st);
@@ -897,9 +926,15 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     res->has_error = 1;
   }
   if (has_agg && p.acc_touched) {
-    char b[16];
-    int n = snprintf(b, sizeof b, "%d", (int32_t)p.acc_final);
-    c->acc.assign(b, b + n);
+    if (has_cat) {
+      std::vector<uint8_t> na(c->acc.size() + p.cat_final);
+      HIPCHK(hipMemcpy(na.data(), c->cat.as<uint8_t>() + kCatOff, na.size(), hipMemcpyDeviceToHost));
+      c->acc.swap(na);
+    } else {
+      char b[16];
+      int n = snprintf(b, sizeof b, "%d", (int32_t)p.acc_final);
+      c->acc.assign(b, b + n);
+    }
   }
   return FSG_OK;
 }

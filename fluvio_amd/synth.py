@@ -4,6 +4,7 @@ kind 1: C1 regex workload (256 B printable ASCII, ~50 % SSN), seed 0xF100
 kind 2: C2 JSON logs (~1 KB, ~50 % contain "timeout"), seed 0xF101
 kind 3: decimal i32 values (aggregate-sum / filter_map), seed 0xF105
 kind 4: edge cases (empty values, keys, invalid UTF-8, multi-byte UTF-8)
+kind 5: C4 JSON arrays of 1-16 ints / short ASCII strings (array_map), seed 0xF104
 """
 import ctypes
 import os
@@ -15,8 +16,8 @@ from . import _ffi
 _LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libfsg_synth.so")
 _lib = None
 
-SEEDS = {1: 0xF100, 2: 0xF101, 3: 0xF105, 4: 0xF1EE}
-REC_BYTES = {1: 272, 2: 1100, 3: 16, 4: 64}
+SEEDS = {1: 0xF100, 2: 0xF101, 3: 0xF105, 4: 0xF1EE, 5: 0xF104}
+REC_BYTES = {1: 272, 2: 1100, 3: 16, 4: 64, 5: 200}
 
 
 def _l():

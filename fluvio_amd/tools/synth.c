@@ -12,6 +12,8 @@
  *                messages contain the word "timeout"
  *   kind 3     : decimal i32 values in [-1000, 1000] (aggregate-sum / filter_map inputs)
  *   kind 4     : mixed short values incl. invalid UTF-8, empty values and keys (edge cases)
+ *   kind 5 (C4): JSON arrays of 1-16 elements, each an integer or a short ASCII string,
+ *                no whitespace (array_map_json_array input)
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -174,6 +176,26 @@ static size_t gen_c4(uint8_t *v, int *has_key, uint8_t *key, size_t *klen) {
   return n;
 }
 
+static size_t gen_c5(uint8_t *v) {
+  char *o = (char *)v;
+  size_t k = 0;
+  const uint32_t ne = 1 + rnd_n(16);
+  o[k++] = '[';
+  for (uint32_t e = 0; e < ne; e++) {
+    if (e) o[k++] = ',';
+    if (rnd() & 1) {
+      k += (size_t)sprintf(o + k, "%d", (int)rnd_n(200001) - 100000);
+    } else {
+      const uint32_t n = 1 + rnd_n(8);
+      o[k++] = '"';
+      for (uint32_t i = 0; i < n; i++) o[k++] = (char)('a' + rnd_n(26));
+      o[k++] = '"';
+    }
+  }
+  o[k++] = ']';
+  return k;
+}
+
 /* Generate `nrec` records of `kind` into out (capacity cap) starting at base offset
  * `base`.  Returns bytes written, or 0 if cap is too small. */
 size_t synth_slice(int kind, uint64_t nrec, uint64_t seed, int64_t base, uint8_t *out, size_t cap,
@@ -201,6 +223,7 @@ size_t synth_slice(int kind, uint64_t nrec, uint64_t seed, int64_t base, uint8_t
         case 1: vl = gen_c1(val); break;
         case 2: vl = gen_c2(val); break;
         case 3: vl = gen_c3(val); break;
+        case 5: vl = gen_c5(val); break;
         default: vl = gen_c4(val, &hk, key, &kl); break;
       }
       size_t inner = 1 + vsz(0) + vsz((int64_t)cnt) + 1 + (hk ? vsz((int64_t)kl) + kl : 0) + vsz((int64_t)vl) + vl + 1;

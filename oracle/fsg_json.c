@@ -1011,6 +1011,350 @@ int orc_json_structured_log(const uint8_t *s, size_t n, int *level, char **msg, 
   return r;
 }
 
+/* ------------------------------------------------------------------ */
+/* smartmodule/examples/array_map_json_array/src/lib.rs:38-55:           */
+/*   let array: Vec<serde_json::Value> = serde_json::from_slice(value)?; */
+/*   array.map(|v| serde_json::to_string(&v))                            */
+/* serde_json 1.0.96 without preserve_order (examples/Cargo.lock: deps   */
+/* itoa, ryu, serde only): objects are BTreeMap<String, Value>, so       */
+/* to_string emits members sorted by key bytes, a repeated key keeps its */
+/* last value (Map::insert).  Value parse = Deserializer::deserialize_any */
+/* (de.rs), serialization = ser.rs format_escaped_str + itoa.  Floats    */
+/* (and -0 / integers beyond u64/i64, which serde_json parses as f64)    */
+/* need ryu's shortest round-trip Display: ORC_E_UNSUPPORTED on both     */
+/* sides ("parity unpinned" beyond the restatement).                     */
+/* ------------------------------------------------------------------ */
+
+/* ser.rs format_escaped_str_contents: ESCAPE table — '"' '\\', the short
+ * escapes \b \t \n \f \r, every other byte < 0x20 as \u00XX (lowercase hex) */
+static void canon_str(jbuf *out, const uint8_t *s, size_t n) {
+  static const char HEX[] = "0123456789abcdef";
+  jb_byte(out, '"');
+  for (size_t i = 0; i < n; i++) {
+    uint8_t c = s[i];
+    switch (c) {
+      case '"': jb_push(out, (const uint8_t *)"\\\"", 2); break;
+      case '\\': jb_push(out, (const uint8_t *)"\\\\", 2); break;
+      case 0x08: jb_push(out, (const uint8_t *)"\\b", 2); break;
+      case 0x09: jb_push(out, (const uint8_t *)"\\t", 2); break;
+      case 0x0A: jb_push(out, (const uint8_t *)"\\n", 2); break;
+      case 0x0C: jb_push(out, (const uint8_t *)"\\f", 2); break;
+      case 0x0D: jb_push(out, (const uint8_t *)"\\r", 2); break;
+      default:
+        if (c < 0x20) {
+          uint8_t u[6] = {'\\', 'u', '0', '0', (uint8_t)HEX[c >> 4], (uint8_t)HEX[c & 15]};
+          jb_push(out, u, 6);
+        } else {
+          jb_byte(out, c);
+        }
+    }
+  }
+  jb_byte(out, '"');
+}
+
+typedef struct {
+  jbuf key; /* decoded key bytes */
+  jbuf val; /* canonical serialization of the value */
+} jmember;
+
+static int member_cmp(const void *a, const void *b) {
+  const jmember *x = (const jmember *)a, *y = (const jmember *)b;
+  size_t m = x->key.n < y->key.n ? x->key.n : y->key.n;
+  int c = m ? memcmp(x->key.b, y->key.b, m) : 0;
+  if (c) return c;
+  return x->key.n < y->key.n ? -1 : x->key.n > y->key.n ? 1 : 0;
+}
+
+static int value_canon(jde *d, jbuf *out);
+
+/* ValueVisitor::visit_seq via SeqAccess::next_element_seed (de.rs) */
+static int visit_seq_values(jde *d, jbuf *out, size_t *count) {
+  int first = 1;
+  size_t k = 0;
+  for (;;) {
+    int peek = parse_whitespace(d);
+    if (peek == ']') break;
+    if (peek == ',' && !first) {
+      jeat(d);
+      peek = parse_whitespace(d);
+    } else if (peek >= 0) {
+      if (first)
+        first = 0;
+      else
+        return jpeek_error(d, E_LIST_COMMA);
+    } else {
+      return jpeek_error(d, E_EOF_LIST);
+    }
+    if (peek == ']') return jpeek_error(d, E_TRAILING_COMMA);
+    if (peek < 0) return jpeek_error(d, E_EOF_VALUE);
+    if (out && k) jb_byte(out, ',');
+    if (value_canon(d, out)) return -1;
+    k++;
+  }
+  if (count) *count = k;
+  return 0;
+}
+
+/* ValueVisitor::visit_map via MapAccess (KeyClassifier keys, Map::insert) */
+static int visit_map_values(jde *d, jbuf *out) {
+  jmember *m = NULL;
+  size_t nm = 0, cap = 0;
+  int first = 1, rc = -1;
+  for (;;) {
+    int peek = parse_whitespace(d);
+    if (peek == '}') break;
+    if (peek == ',' && !first) {
+      jeat(d);
+      peek = parse_whitespace(d);
+    } else if (peek >= 0) {
+      if (first)
+        first = 0;
+      else {
+        jpeek_error(d, E_OBJ_COMMA);
+        goto out;
+      }
+    } else {
+      jpeek_error(d, E_EOF_OBJECT);
+      goto out;
+    }
+    if (peek == '}') { jpeek_error(d, E_TRAILING_COMMA); goto out; }
+    if (peek < 0) { jpeek_error(d, E_EOF_VALUE); goto out; }
+    if (peek != '"') { jpeek_error(d, E_KEY); goto out; }
+    jeat(d);
+    if (nm == cap) {
+      cap = cap * 2 + 8;
+      m = (jmember *)realloc(m, cap * sizeof(jmember));
+    }
+    memset(&m[nm], 0, sizeof(jmember));
+    nm++;
+    if (parse_str(d, &m[nm - 1].key)) goto out;
+    int c = parse_whitespace(d);
+    if (c == ':')
+      jeat(d);
+    else if (c >= 0) {
+      jpeek_error(d, E_COLON);
+      goto out;
+    } else {
+      jpeek_error(d, E_EOF_OBJECT);
+      goto out;
+    }
+    if (value_canon(d, &m[nm - 1].val)) goto out;
+  }
+  rc = 0;
+  if (out) {
+    /* BTreeMap: a later insert of the same key replaces the value -> keep the
+     * last occurrence of every key, then emit in key order */
+    size_t w = 0;
+    for (size_t i = 0; i < nm; i++) {
+      int dup = 0;
+      for (size_t j = i + 1; j < nm && !dup; j++)
+        dup = m[i].key.n == m[j].key.n && (!m[i].key.n || !memcmp(m[i].key.b, m[j].key.b, m[i].key.n));
+      if (dup) {
+        free(m[i].key.b);
+        free(m[i].val.b);
+      } else {
+        m[w++] = m[i];
+      }
+    }
+    nm = w;
+    qsort(m, nm, sizeof(jmember), member_cmp);
+    jb_byte(out, '{');
+    for (size_t i = 0; i < nm; i++) {
+      if (i) jb_byte(out, ',');
+      canon_str(out, m[i].key.b, m[i].key.n);
+      jb_byte(out, ':');
+      jb_push(out, m[i].val.b, m[i].val.n);
+    }
+    jb_byte(out, '}');
+  }
+out:
+  for (size_t i = 0; i < nm; i++) {
+    free(m[i].key.b);
+    free(m[i].val.b);
+  }
+  free(m);
+  return rc;
+}
+
+/* Deserializer::deserialize_any for Value, serialized with to_string */
+static int value_canon(jde *d, jbuf *out) {
+  int peek = parse_whitespace(d);
+  if (peek < 0) return jpeek_error(d, E_EOF_VALUE);
+  int r = 0;
+  switch (peek) {
+    case 'n':
+      jeat(d);
+      if (parse_ident(d, "ull")) return -1;
+      jb_push(out, (const uint8_t *)"null", 4);
+      break;
+    case 't':
+      jeat(d);
+      if (parse_ident(d, "rue")) return -1;
+      jb_push(out, (const uint8_t *)"true", 4);
+      break;
+    case 'f':
+      jeat(d);
+      if (parse_ident(d, "alse")) return -1;
+      jb_push(out, (const uint8_t *)"false", 5);
+      break;
+    case '-':
+    case '0': case '1': case '2': case '3': case '4': case '5': case '6': case '7': case '8': case '9': {
+      int pos = peek != '-';
+      if (!pos) jeat(d);
+      jnum num;
+      if (parse_integer(d, pos, &num)) return -1;
+      if (num.is_float) return junsupported(d);
+      char t[32];
+      int k = snprintf(t, sizeof t, "%s%llu", num.neg ? "-" : "", (unsigned long long)num.mag);
+      jb_push(out, (const uint8_t *)t, (size_t)k);
+      break;
+    }
+    case '"': {
+      jeat(d);
+      jbuf s;
+      if (parse_str(d, &s)) {
+        free(s.b);
+        return -1;
+      }
+      canon_str(out, s.b, s.n);
+      free(s.b);
+      break;
+    }
+    case '[':
+    case '{': {
+      /* check_recursion! */
+      if (--d->depth == 0) return jpeek_error(d, E_RECURSION);
+      jeat(d);
+      if (peek == '[') {
+        jb_byte(out, '[');
+        r = visit_seq_values(d, out, NULL);
+        if (!r) jb_byte(out, ']');
+      } else {
+        r = visit_map_values(d, out);
+      }
+      d->depth++;
+      if (r) {
+        jde probe = *d; /* (Err, _): the end check still moves the reader */
+        probe.msg = NULL;
+        probe.msg_len = 0;
+        probe.failed = 0;
+        (void)(peek == '[' ? end_seq(&probe) : end_map(&probe));
+        free(probe.msg);
+        d->i = probe.i;
+      } else {
+        r = peek == '[' ? end_seq(d) : end_map(d);
+      }
+      break;
+    }
+    default: return jpeek_error(d, E_VALUE);
+  }
+  if (r) jfix_position(d);
+  return r;
+}
+
+/* from_slice::<Vec<Value>> + to_string of each element.  0 ok (*elems: count
+ * malloc'd canonical strings), 1 error (*msg), ORC_E_UNSUPPORTED */
+int orc_json_array_map(const uint8_t *s, size_t n, uint8_t ***elems, size_t **lens, size_t *count, char **msg,
+                       size_t *msg_len) {
+  jde d;
+  memset(&d, 0, sizeof d);
+  d.s = s;
+  d.n = n;
+  d.depth = 128;
+  *msg = NULL;
+  *elems = NULL;
+  *lens = NULL;
+  *count = 0;
+  int r;
+  int peek = parse_whitespace(&d);
+  if (peek < 0) {
+    r = jpeek_error(&d, E_EOF_VALUE);
+  } else if (peek == '[') { /* deserialize_seq */
+    if (--d.depth == 0) {
+      r = jpeek_error(&d, E_RECURSION);
+    } else {
+      jeat(&d);
+      /* VecVisitor::visit_seq: each element parsed into its own buffer */
+      size_t cap = 0;
+      int first = 1;
+      r = 0;
+      for (;;) {
+        int p = parse_whitespace(&d);
+        if (p == ']') break;
+        if (p == ',' && !first) {
+          jeat(&d);
+          p = parse_whitespace(&d);
+        } else if (p >= 0) {
+          if (first)
+            first = 0;
+          else {
+            r = jpeek_error(&d, E_LIST_COMMA);
+            break;
+          }
+        } else {
+          r = jpeek_error(&d, E_EOF_LIST);
+          break;
+        }
+        if (p == ']') { r = jpeek_error(&d, E_TRAILING_COMMA); break; }
+        if (p < 0) { r = jpeek_error(&d, E_EOF_VALUE); break; }
+        jbuf v = {0};
+        if (value_canon(&d, &v)) {
+          free(v.b);
+          r = -1;
+          break;
+        }
+        if (*count == cap) {
+          cap = cap * 2 + 8;
+          *elems = (uint8_t **)realloc(*elems, cap * sizeof(uint8_t *));
+          *lens = (size_t *)realloc(*lens, cap * sizeof(size_t));
+        }
+        (*elems)[*count] = v.b ? v.b : (uint8_t *)malloc(1);
+        (*lens)[*count] = v.n;
+        (*count)++;
+      }
+      d.depth++;
+      if (r) {
+        jde probe = d;
+        probe.msg = NULL;
+        probe.msg_len = 0;
+        probe.failed = 0;
+        (void)end_seq(&probe);
+        free(probe.msg);
+        d.i = probe.i;
+      } else {
+        r = end_seq(&d);
+      }
+    }
+    if (r) jfix_position(&d);
+  } else {
+    r = peek_invalid_type(&d, "a sequence");
+    jfix_position(&d);
+  }
+  if (!r && parse_whitespace(&d) >= 0) r = jpeek_error(&d, E_TRAILING); /* Deserializer::end */
+  if (!r) {
+    free(d.msg);
+    return 0;
+  }
+  for (size_t i = 0; i < *count; i++) free((*elems)[i]);
+  free(*elems);
+  free(*lens);
+  *elems = NULL;
+  *lens = NULL;
+  *count = 0;
+  if (d.unsupported) {
+    free(d.msg);
+    return ORC_E_UNSUPPORTED;
+  }
+  *msg = render(&d, msg_len);
+  free(d.msg);
+  if (memchr(*msg, 0, *msg_len)) {
+    free(*msg);
+    *msg = NULL;
+    return ORC_E_UNSUPPORTED;
+  }
+  return 1;
+}
+
 /* generic entry for pinning against other serde_json fixtures of the reference:
  * fields as "name" (string) or "name=v1|v2|.." (unit enum) */
 int orc_json_struct(const uint8_t *s, size_t n, const char *name, const char **fields, int nfields, int *vals,

@@ -1114,6 +1114,7 @@ enum {
   M_AGG_SUM,
   M_AGG_CONCAT,
   M_FILTER_JSON, /* examples/filter_json: StructuredLog.level > Debug */
+  M_ARRAY_MAP,   /* examples/array_map_json_array: explode a JSON array */
 };
 
 typedef struct {
@@ -1222,6 +1223,9 @@ int orc_chain_add(orc_chain *c, const char *module, const char **keys, const cha
   } else if (!strcmp(module, "aggregate")) {
     s.mod = M_AGG_CONCAT;
     s.kind = K_AGGREGATE;
+  } else if (!strcmp(module, "array_map_json_array")) {
+    s.mod = M_ARRAY_MAP;
+    s.kind = K_ARRAY_MAP;
   } else {
     return ORC_E_UNKNOWN_SM;
   }
@@ -1333,6 +1337,33 @@ static void stage_run(stage_t *s, recvec *in, int64_t base_offset, stage_out *o)
           break;
         }
         keep = (x % 2) == 0;
+        break;
+      }
+      case M_ARRAY_MAP: {
+        /* array_map_json_array/src/lib.rs:38-55; derive generator/array_map.rs:17-42:
+         * every element -> Record::new_key_value(None, to_string(element)) with the
+         * default preamble (data.rs:465-472: attributes 0, deltas 0, no headers) */
+        uint8_t **el;
+        size_t *ln, cnt, ml;
+        char *m = NULL;
+        int jr = orc_json_array_map(r->val, r->val_len, &el, &ln, &cnt, &m, &ml);
+        if (jr == ORC_E_UNSUPPORTED) {
+          o->unsupported = 1;
+          return;
+        }
+        if (jr) {
+          hint = m;
+          break;
+        }
+        for (size_t k = 0; k < cnt; k++) {
+          rec_t nr;
+          memset(&nr, 0, sizeof nr);
+          nr.val = el[k];
+          nr.val_len = ln[k];
+          rv_push(&o->out, nr);
+        }
+        free(el);
+        free(ln);
         break;
       }
       case M_MAP_UPPER:

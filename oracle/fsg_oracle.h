@@ -90,6 +90,11 @@ int orc_regex_is_match(const char *pattern, const uint8_t *text, size_t n, int *
 int orc_json_structured_log(const uint8_t *s, size_t n, int *level, char **msg, size_t *msg_len);
 /* generic derive(Deserialize) struct: fields "name" (String) or "name=a|b|c"
  * (unit enum, rename_all lowercase names), for the reference's other fixtures */
+/* serde_json from_slice::<Vec<Value>> + to_string per element (array_map_json_array):
+* 0 ok (elems / lens: count malloc'd canonical strings; free each + arrays with orc_free),
+ * 1 error (*msg Display text), ORC_E_UNSUPPORTED (floats) */
+int orc_json_array_map(const uint8_t *s, size_t n, uint8_t ***elems, size_t **lens, size_t *count, char **msg,
+                       size_t *msg_len);
 int orc_json_struct(const uint8_t *s, size_t n, const char *name, const char **fields, int nfields, int *vals,
                     char **msg, size_t *msg_len);
 

@@ -75,6 +75,11 @@ def lib():
         L.orc_json_struct.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
                                       ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                       ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]
+        L.orc_json_array_map.argtypes = [ctypes.c_char_p, ctypes.c_size_t,
+                                         ctypes.POINTER(ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8))),
+                                         ctypes.POINTER(ctypes.POINTER(ctypes.c_size_t)),
+                                         ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_void_p),
+                                         ctypes.POINTER(ctypes.c_size_t)]
         L.orc_varint_encode.restype = ctypes.c_size_t
         L.orc_varint_encode.argtypes = [ctypes.c_int64, ctypes.c_char_p]
         _lib = L
@@ -117,6 +122,27 @@ def json_structured_log(value: bytes):
     rc = lib().orc_json_structured_log(value, len(value), ctypes.byref(lv), ctypes.byref(msg), ctypes.byref(ml))
     err = _json_result(rc, msg, ml)
     return ("ok", lv.value) if err is None else ("err", err)
+
+
+def json_array_map(value: bytes):
+    """array_map_json_array: ("ok", [canonical element bytes]) / ("err", Display text);
+    raises OracleError(-103) outside the restatement (floats)."""
+    el = ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8))()
+    ln = ctypes.POINTER(ctypes.c_size_t)()
+    cnt = ctypes.c_size_t()
+    msg = ctypes.c_void_p()
+    ml = ctypes.c_size_t(0)
+    rc = lib().orc_json_array_map(value, len(value), ctypes.byref(el), ctypes.byref(ln), ctypes.byref(cnt),
+                                  ctypes.byref(msg), ctypes.byref(ml))
+    if rc == 0:
+        out = [ctypes.string_at(el[i], ln[i]) for i in range(cnt.value)]
+        for i in range(cnt.value):
+            lib().orc_free(el[i])
+        lib().orc_free(el)
+        lib().orc_free(ln)
+        return "ok", out
+    err = _json_result(rc, msg, ml)
+    return "err", err
 
 
 def json_struct(value: bytes, name: str, fields):

@@ -112,6 +112,9 @@ def main():
     case("aggregate_with_initial", "crates/fluvio-smartengine/src/engine/wasmtime/transforms/aggregate.rs:223-255",
          [["aggregate", {}, "a"]],
          [{"values": ["b"], "expect": ["ab"]}])
+    case("array_map", "crates/fluvio-smartengine/src/engine/wasmtime/transforms/array_map.rs:41-52",
+         [["array_map_json_array", {}, None]],
+         [{"values": ['["Apple","Banana","Cranberry"]'], "expect": ['"Apple"', '"Banana"', '"Cranberry"']}])
     case("empty_chain", "crates/fluvio-smartengine/src/engine/wasmtime/engine.rs:477-498",
          [], [{"values": ["input"], "expect": ["input"]}])
     k["chain"] = chain
@@ -194,6 +197,12 @@ def main():
                 "source": "crates/fluvio-spu/src/services/public/tests/stream_fetch.rs:1933-2020",
                 "modules": [["filter_map", {}, None]], "slice": s6.hex(), "max_bytes": 10000,
                 "expect": {"base_offset": 0, "n_records": 2, "values": ["11", "22"]}})
+    # stream_fetch.rs:1838-1893: one record serde_json::to_string(&(0..10)) -> "0".."9"
+    s7 = producer_batch(0, ["[0,1,2,3,4,5,6,7,8,9]"])
+    spu.append({"name": "array_map_ints",
+                "source": "crates/fluvio-spu/src/services/public/tests/stream_fetch.rs:1838-1893",
+                "modules": [["array_map_json_array", {}, None]], "slice": s7.hex(), "max_bytes": 10000,
+                "expect": {"base_offset": 0, "n_records": 10, "values": [str(i) for i in range(10)]}})
     k["process_batch"] = spu
 
     # serde / serde_json error texts asserted by the reference's own tests (the

@@ -93,3 +93,54 @@ def corpus(seed: int, n_valid: int, n_mut: int):
              b'{"level":"debug","message":"x"}\n', b'\n\n  {"level"\n:\n"info"}',
              b'{"level":"info","message":"x","a":[1,2,{"b":[true,false,null,"s",-1.5e-3]}]}']
     return fixed + docs
+
+
+# ---------------------------------------------------------------------------
+# array_map_json_array inputs: JSON arrays of values
+# ---------------------------------------------------------------------------
+def am_value(rng, depth=0, sorted_keys=True, ints_only=True):
+    """A JSON value.  ints_only: integers within u64/i64 (serde_json keeps them
+    exact); sorted_keys: objects with strictly increasing keys (BTreeMap order)."""
+    r = rng.random()
+    if depth > 3 or r < 0.45:
+        nums = [str(rng.randrange(-10**6, 10**6)), "0", "18446744073709551615", "-9223372036854775808"]
+        if not ints_only:
+            nums += [f"{rng.randrange(1000)}.{rng.randrange(1000)}", "-0", "18446744073709551616", "1e3"]
+        return rng.choice([rand_str(rng), rand_str(rng, 3, False), rng.choice(nums), "true", "false", "null",
+                           '"\\u001f\\u0001\\u007F"', '"caf\\u00e9 \\ud83d\\ude00"', '"\\/\\b"', '"ü\x7f"'])
+    if r < 0.75:
+        return "[" + ",".join(ws(rng) + am_value(rng, depth + 1, sorted_keys, ints_only) + ws(rng)
+                              for _ in range(rng.randrange(4))) + "]"
+    keys = list({json.loads(rand_str(rng, 4, escapes=False)) for _ in range(rng.randrange(4))})
+    keys.sort(key=lambda k: k.encode())
+    if not sorted_keys and len(keys) > 1:
+        rng.shuffle(keys)
+        if rng.random() < 0.3:
+            keys.append(keys[0])
+    return "{" + ",".join(f"{ws(rng)}{json.dumps(k)}{ws(rng)}:{ws(rng)}{am_value(rng, depth + 1, sorted_keys, ints_only)}"
+                          for k in keys) + "}"
+
+
+def array_doc(rng, sorted_keys=True, ints_only=True):
+    n = rng.randrange(0, 12)
+    return ws(rng) + "[" + ",".join(ws(rng) + am_value(rng, 0, sorted_keys, ints_only) + ws(rng)
+                                    for _ in range(n)) + "]" + ws(rng)
+
+
+ARRAY_FIXED = [b"[]", b" [ ] ", b"[1]", b'["Apple","Banana","Cranberry"]', b"[0,1,2,3,4,5,6,7,8,9]",
+               b"[[[]]]", b'[{"a":1,"b":[2,{"c":null}]}]', b'["\\u0041\\/x"]', b'["\\u001F"]',
+               b'[true,false,null]', b"[-0]", b"[1.5]", b"[1e2]", b"[18446744073709551616]",
+               b"", b" ", b"{}", b'{"a":1}', b"5", b'"s"', b"null", b"[1,]", b"[,1]", b"[1 2]", b"[",
+               b"[1", b'["a', b'["\\x"]', b'["\\ud800"]', b'["\\udc00"]', b'["a\x01"]', b'["\xff"]',
+               b'["\xc3\xa9"]', b"[tru]", b"[nul", b"[01]", b"[1.]", b"[-]", b"[1e+]", b"[] x", b"[]]",
+               b'[{"a" 1}]', b'[{1:2}]', b'[{"a":1,}]', b'[{"a":1 "b":2}]', b'[{"a":1}', b"[" * 130 + b"]" * 130,
+               b"[" * 127 + b"]" * 127, b"[" * 128 + b"]" * 128, b'[{"b":1,"a":2}]', b'[{"a":1,"a":2}]',
+               b'[{"\\u0061":1,"b":2}]', b'[\n1\n,\n"x"\n]', b'["\\ud83d\\ude00","\\"\\\\\\b\\f\\n\\r\\t"]']
+
+
+def array_corpus(seed: int, n_valid: int, n_mut: int, sorted_keys=True, ints_only=True):
+    rng = random.Random(seed)
+    docs = [array_doc(rng, sorted_keys, ints_only).encode() for _ in range(n_valid)]
+    base = [array_doc(rng, sorted_keys, ints_only) for _ in range(max(1, n_mut // 4))]
+    docs += [mutate(rng, rng.choice(base)) for _ in range(n_mut)]
+    return docs

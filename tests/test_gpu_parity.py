@@ -83,7 +83,7 @@ def check_batch(engine, modules, slice_bytes, max_bytes=(1 << 64) - 1, calls=1):
         assert gm.records_out() == om["records_out"]
         assert gm.fuel_used() == 0
     for i, m in enumerate(modules):
-        if m[0] == "aggregate-sum":
+        if m[0] in ("aggregate-sum", "aggregate"):
             assert g.accumulator(i) == o.accumulator(i)
     return gout
 
@@ -94,16 +94,15 @@ def check_batch(engine, modules, slice_bytes, max_bytes=(1 << 64) - 1, calls=1):
 def test_kat_chain_cases(engine, kats):
     for case in kats["chain"]:
         modules = mods(case["modules"])
-        if any(m[0] == "aggregate" for m in modules):
-            with pytest.raises(Unsupported):
-                gpu_chain(engine, modules)
-            continue
+        agg = next((i for i, m in enumerate(modules) if m[0].startswith("aggregate")), None)
         g = gpu_chain(engine, modules)
         for call in case["calls"]:
             inp = SmartModuleInput.try_from_records([P.Record.new(v) for v in call["values"]])
             out = g.process(inp)
             assert out.error is None
             assert [r.value for r in out.successes] == [v.encode() for v in call["expect"]], case["name"]
+            if "acc" in call:  # transforms/aggregate.rs:157,185,207: the stored accumulator
+                assert g.accumulator(agg) == call["acc"].encode(), case["name"]
 
 
 def test_kat_init_errors(engine, kats):
@@ -136,8 +135,6 @@ def test_kat_survey_guest(engine, kats):
 def test_kat_process_batch(engine, kats):
     for case in kats["process_batch"]:
         modules = mods(case["modules"])
-        if any(m[0] == "aggregate" for m in modules):
-            continue
         out = check_batch(engine, modules, bytes.fromhex(case["slice"]), case["max_bytes"])
         exp = case["expect"]
         b = out.batch()
@@ -188,11 +185,22 @@ CHAINS = {
     "map_double_filter_map": [("map_double", {}, None), ("filter_map", {}, None)],
     "agg_sum": [("aggregate-sum", {}, b"7")],
     "filter_agg_sum": [("filter_with_param", {"key": "1"}, None), ("aggregate-sum", {}, None)],
+    "array_map": [("array_map_json_array", {}, None)],
+    "filter_array_map": [("filter_with_param", {"key": "1"}, None), ("array_map_json_array", {}, None)],
+    "map_array_map": [("map", {}, None), ("array_map_json_array", {}, None)],
     "empty": [],
+}
+# string-concatenating aggregate: output grows quadratically, small slices only
+CONCAT_CHAINS = {
+    "agg_concat": [("aggregate", {}, b"A")],
+    "filter_agg_concat": [("filter", {}, None), ("aggregate", {}, None)],
+    "map_agg_concat": [("map", {}, None), ("aggregate", {}, b"x")],
+    "filter_map_agg_concat": [("filter_map", {}, None), ("aggregate", {}, b"")],
+    "agg_concat_bad_acc": [("aggregate", {}, b"ok\xff")],
 }
 
 
-@pytest.mark.parametrize("kind,n", [(1, 3000), (2, 2000), (3, 5000), (4, 4000)])
+@pytest.mark.parametrize("kind,n", [(1, 3000), (2, 2000), (3, 5000), (4, 4000), (5, 3000)])
 @pytest.mark.parametrize("chain", sorted(CHAINS))
 def test_random_parity(engine, chain, kind, n):
     sl = synth.make_slice(kind, n, base_offset=1000)
@@ -421,3 +429,125 @@ def _lean_slice(seed=7, nbatches=40):
 def test_lean_path_parity(engine, chain):
     check_batch(engine, chain, _lean_slice())
     check_batch(engine, chain, _lean_slice(seed=11, nbatches=25))
+
+
+# ---------------------------------------------------------------------------
+# string-concatenating aggregate (examples/aggregate) and array_map
+# (examples/array_map_json_array): variable-size outputs
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("kind,n", [(1, 150), (3, 1500), (4, 900), (5, 600)])
+@pytest.mark.parametrize("chain", sorted(CONCAT_CHAINS))
+def test_aggregate_concat_parity(engine, chain, kind, n):
+    sl = synth.make_slice(kind, n, base_offset=5)
+    check_batch(engine, CONCAT_CHAINS[chain], sl, calls=2)
+
+
+@pytest.mark.parametrize("max_bytes", [0, 50, 4000, 200000])
+def test_aggregate_concat_max_bytes(engine, max_bytes):
+    check_batch(engine, CONCAT_CHAINS["agg_concat"], synth.make_slice(3, 900), max_bytes, calls=2)
+
+
+def _needs_reorder(doc: bytes) -> bool:
+    """True if some object of a valid JSON doc is not already in BTreeMap order
+    (keys strictly increasing), or orders keys holding escapes, or nests deeper
+    than the 8 levels whose order the device checks: the GPU reports those as
+    unsupported (fsg_json_dev.h any_value)."""
+    i, n = 0, len(doc)
+    stack = []  # per open container: None ('[') or list of raw keys ('{')
+    expect_key = False
+    while i < n:
+        c = doc[i:i + 1]
+        if c == b'"':
+            j = i + 1
+            while doc[j:j + 1] != b'"':
+                j += 2 if doc[j:j + 1] == b"\\" else 1
+            if expect_key and stack and stack[-1] is not None:
+                stack[-1].append(doc[i + 1:j])
+            expect_key = False
+            i = j + 1
+            continue
+        if c == b"{":
+            stack.append([])
+            expect_key = True
+        elif c == b"[":
+            stack.append(None)
+        elif c in (b"}", b"]"):
+            keys = stack.pop()
+            if keys is not None and len(keys) > 1:
+                if len(stack) > 8 or any(b"\\" in k for k in keys):
+                    return True
+                if any(keys[k] >= keys[k + 1] for k in range(len(keys) - 1)):
+                    return True
+        elif c == b",":
+            expect_key = bool(stack) and stack[-1] is not None
+        i += 1
+    return False
+
+
+def _check_array_doc(engine, doc):
+    sl = _one_record_slice(doc, base=3)
+    try:
+        check_batch(engine, CHAINS["array_map"], sl)
+    except AssertionError:
+        o = orc_chain(CHAINS["array_map"]).process_batch(sl)
+        if o["status"] != 0 or o["error"] is not None or not _needs_reorder(doc):
+            raise
+        with pytest.raises(Unsupported):
+            gpu_chain(engine, CHAINS["array_map"]).process_batch(sl)
+
+
+def test_array_map_fuzz_one_record(engine):
+    """Every document (valid, mutated, hand-picked errors) as a one-record batch:
+    exploded records bit-exact, or the serde_json error hint/offset/value."""
+    from tests import jsongen
+    docs = jsongen.ARRAY_FIXED + jsongen.array_corpus(3, 250, 350)
+    docs += jsongen.array_corpus(4, 60, 0, sorted_keys=False) + jsongen.array_corpus(6, 60, 0, ints_only=False)
+    for doc in docs:
+        _check_array_doc(engine, doc)
+
+
+def test_array_map_first_error_in_stream(engine):
+    from tests import jsongen
+    import random
+    rng = random.Random(21)
+    good = [jsongen.array_doc(rng).encode() for _ in range(600)]
+    sl, base = b"", 0
+    for k in range(60):
+        b = P.Batch(base_offset=base)
+        for j in range(10):
+            v = good[k * 10 + j]
+            if k == 37 and j == 4:
+                v = b'[1,"x",]'
+            b.add_record(P.Record.new(v))
+        sl += b.encode()
+        base += 10
+    for chain in ("array_map", "filter_array_map"):
+        check_batch(engine, CHAINS[chain], sl)
+        check_batch(engine, CHAINS[chain], sl, max_bytes=30000)
+
+
+def test_array_map_long_and_rewritten_elements(engine):
+    """Elements above the lane-copy size (whole-wave copies), elements whose
+    canonical form differs from the source (whitespace, \\u and \\/ escapes),
+    uppercased input (map -> array_map)."""
+    long_s = '"' + "x" * 3000 + '"'
+    docs = [f"[{long_s},1,{long_s}]", "[" + ",".join(['"' + "y" * k + '"' for k in range(0, 200, 7)]) + "]",
+            '[ "a\\u0041" , [ 1 , 2 ] , {"k" : "v\\/"} ]', "[" + ",".join(str(10**k) for k in range(19)) + "]",
+            '["' + "\\u00e9" * 40 + '"]', '[[' + "1," * 400 + '1]]', '["abc","def"]', '[true,"t"]']
+    sl, base = b"", 0
+    for d in docs:
+        b = P.Batch(base_offset=base)
+        b.add_record(P.Record.new(d.encode()))
+        b.add_record(P.Record.new(b'["tail"]'))
+        sl += b.encode()
+        base += 2
+    for chain in ("array_map", "map_array_map"):
+        check_batch(engine, CHAINS[chain], sl)
+
+
+def test_array_map_c4_synthetic(engine):
+    """C4 (BASELINE configs[3]): JSON arrays of 1-16 ints / short strings."""
+    sl = synth.make_slice(5, 20000)
+    out = check_batch(engine, CHAINS["array_map"], sl)
+    assert out.n_records > 5 * 20000
+    check_batch(engine, CHAINS["array_map"], sl, max_bytes=100000)

@@ -121,3 +121,51 @@ def test_oracle_error_texts():
     }
     for doc, want in cases.items():
         assert O.json_structured_log(doc) == ("err", want), doc
+
+
+# ---------------------------------------------------------------------------
+# array_map_json_array: from_slice::<Vec<Value>> + to_string per element
+# ---------------------------------------------------------------------------
+def _py_canon(v):
+    """serde_json::to_string of a Value as Python's json writes it: compact,
+    BTreeMap (sorted) keys, raw non-ASCII, \\u00xx lowercase for other controls."""
+    return json.dumps(v, separators=(",", ":"), ensure_ascii=False, sort_keys=True).encode()
+
+
+def test_array_map_reference_kat(kats):
+    case = next(c for c in kats["chain"] if c["name"] == "array_map")
+    st, els = O.json_array_map(case["calls"][0]["values"][0].encode())
+    assert st == "ok" and els == [e.encode() for e in case["calls"][0]["expect"]]
+
+
+@pytest.mark.parametrize("sorted_keys", [True, False])
+def test_array_map_oracle_vs_python_json(sorted_keys):
+    """Accept/reject and every canonical element against Python's independent
+    json module (valid documents: identical; Python is laxer on floats, which the
+    restatement leaves unsupported)."""
+    docs = jsongen.array_corpus(5, 400, 0, sorted_keys=sorted_keys, ints_only=True)
+    for d in docs:
+        st, els = O.json_array_map(d)
+        assert st == "ok", (d, els)
+        assert els == [_py_canon(v) for v in json.loads(d)], d
+
+
+def test_array_map_oracle_errors_and_floats():
+    for d in jsongen.ARRAY_FIXED + jsongen.array_corpus(9, 0, 300):
+        try:
+            st, res = O.json_array_map(d)
+        except O.OracleError as e:
+            assert e.status == -103  # a float / -0 / beyond-u64 integer
+            continue
+        try:
+            py = json.loads(d)
+            py_ok = isinstance(py, list)
+        except (ValueError, RecursionError):
+            py_ok = False
+        if st == "ok":
+            assert py_ok, d
+            assert res == [_py_canon(v) for v in py], d
+        else:
+            assert " at line " in res, (d, res)
+            if py_ok:  # Python accepts lone surrogates and deeper nesting than serde's limit 128
+                assert b"\\ud8" in d or b"\\udc" in d or d.count(b"[") >= 128, (d, res)

@@ -54,7 +54,7 @@ def _records_input(values, base_offset=0):
     return P.encode_records([P.Record.new(v) for v in values])
 
 
-@pytest.mark.parametrize("case_idx", range(8))
+@pytest.mark.parametrize("case_idx", range(9))
 def test_chain_cases(kats, case_idx):
     case = kats["chain"][case_idx]
     chain = O.OracleChain([(m, p, a.encode() if a is not None else None)
