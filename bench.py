@@ -1,36 +1,56 @@
-"""bench.py — SmartModule filter chain on MI355X (BASELINE.json metric).
+"""bench.py — SmartModule record-transform path on MI355X (BASELINE.json metric).
 
 One step = one SPU process_batch (fluvio-spu/src/smartengine/batch.rs:41-142)
 over an HBM-resident fetch slice of stored batches: decode, chain evaluation,
 compaction + offset fix-up, output batch re-encode and CRC32C — the whole path,
-output left in HBM.  Default workload = BASELINE.json configs[1] (C2):
-substring filter (filter_init, key="timeout") over ~1 KB JSON log records
+output left in HBM.  The headline line is BASELINE.json configs[1] (C2):
+substring filter (filter_init key="timeout") over ~1 KB JSON log records
 (synthetic, seed 0xF101, ~16 KB batches, one partition per GPU).
 
-Multi-GPU: one process per GPU (torch.distributed.run); topic partitions are
-sharded p -> rank, each rank filters its own partition slice, no data-path
-collective ("weak" scaling).  Rank 0 prints one JSON line.
+The same JSON line carries `workloads`, each timed in the same run with the
+same contract (warmup, barrier + sync, max over ranks):
+  c1-regex       regex-filter \\d{3}-\\d{2}-\\d{4} over 256 B records   (configs[0] shape)
+  c2-json        filter_json (serde_json StructuredLog, level > debug)  (configs[1])
+  c3-filter-map  filter -> map (uppercase), re-encode + CRC32C         (configs[2])
+  c4-array-map   array_map_json_array, 1-16 elements per record         (configs[3])
+  c5-keyed-agg   aggregate-sum over 64 partitions, per-partition state in
+                 HBM merged with an RCCL all-reduce                      (configs[4])
+
+Multi-GPU: one process per GPU (torch.distributed.run).  c1..c4: every rank
+filters its own partition (p -> rank, no data-path collective, "weak").
+c5: the 64 partitions are sharded p -> rank p mod N ("strong"), the state
+vector is all-reduced over RCCL each step.  Rank 0 prints ONE JSON line.
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+# name: (synth kind, chain modules, records per GPU, description)
 WORKLOADS = {
-    # name: (synth kind, chain modules, records per GPU, description)
     "c2-substring": (2, [("filter_init", {"key": "timeout"}, None)], 4_000_000,
                      "substring filter (filter_init key=timeout) on 1 KB JSON records"),
     "c1-regex": (1, [("regex-filter", {"regex": r"\d{3}-\d{2}-\d{4}"}, None)], 8_000_000,
                  "regex-filter \\d{3}-\\d{2}-\\d{4} on 256 B records"),
-    "c3-filter-map": (2, [("filter_init", {"key": "timeout"}, None), ("map", {}, None)], 4_000_000,
-                      "filter -> map (uppercase) chain with compaction, re-encode, CRC32C"),
     "c2-json": (2, [("filter_json", {}, None)], 4_000_000,
                 "JSON-field filter (filter_json: serde_json StructuredLog, keep level > debug) on 1 KB JSON records"),
+    "c3-filter-map": (2, [("filter_init", {"key": "timeout"}, None), ("map", {}, None)], 4_000_000,
+                      "filter -> map (uppercase) chain with compaction, re-encode, CRC32C"),
+    "c4-array-map": (5, [("array_map_json_array", {}, None)], 4_000_000,
+                     "array_map_json_array exploding JSON arrays of 1-16 ints / short strings"),
 }
+C5 = {"partitions": 64, "records_per_partition": 500_000,
+      "modules": [("aggregate-sum", {}, None)],
+      "description": "aggregate-sum over 64 partitions (decimal i32 records), per-partition accumulators in HBM, "
+                     "RCCL all-reduce of the partition state vector each step"}
+EXTRA = ["c1-regex", "c2-json", "c3-filter-map", "c4-array-map", "c5-keyed-agg"]
+PEAK_GBPS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -38,55 +58,182 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2-substring", choices=sorted(WORKLOADS))
-    ap.add_argument("--records", type=int, default=0, help="records per GPU (0 = workload default)")
-    ap.add_argument("--cpu-sample", type=int, default=1_500_000, help="records in the CPU-baseline sample")
+    ap.add_argument("--workload", default="c2-substring", choices=sorted(WORKLOADS) + ["c5-keyed-agg"])
+    ap.add_argument("--records", type=int, default=0, help="records per GPU of the headline workload (0 = default)")
+    ap.add_argument("--only", action="store_true", help="time the headline workload only (no `workloads`)")
+    ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="records per CPU-baseline process")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
     return ap.parse_args()
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    kind, modules, nrec_default, desc = WORKLOADS[a.workload]
-    nrec = a.records or nrec_default
+def lib_tag():
+    """Content hash of the HIP library: PMC traffic is quoted only for the build it was measured on."""
+    from fluvio_amd import _ffi
+    h = hashlib.sha256()
+    with open(_ffi.LIB_PATH, "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
 
-    # the engine (libfsg, HIP) is loaded before torch; torch is only the
-    # multi-process control plane (gloo barrier / max-reduce of timings)
+
+def pmc_traffic(workload, kernel, n_records, n_batches):
+    """Per-launch HBM bytes of the dominant kernel bracket from profiles/traffic.json
+    (scripts/traffic_from_pmc.py), only when measured on this build and shape."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None, None
+    db = json.load(open(path)).get(workload)
+    if not db or db.get("lib") != lib_tag() or db.get("n_records") != n_records or db.get("n_batches") != n_batches:
+        return None, None
+    # the eval bracket covers k_eval_lean + the deferred exact k_eval<N>; crc: k_crc16 + k_crc_final
+    hits = [v["total"] for k, v in db["kernels"].items() if k.split("<")[0].startswith("fsg::" + kernel)]
+    return (sum(hits), db["source"]) if hits else (None, None)
+
+
+class Ctx:
+    def __init__(self, a):
+        self.a = a
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def max_over_ranks(self, v):
+        if self.dist is None:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def broadcast_bytes(self, b, n):
+        if self.dist is None:
+            return b
+        import torch
+        t = torch.tensor(list(b) if self.rank == 0 else [0] * n, dtype=torch.uint8)
+        self.dist.broadcast(t, 0)
+        return bytes(t.tolist())
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_proc(args):
+    """One CPU-baseline process = one partition: its own synthetic slice through
+    the scalar C oracle (process_batch), timed inside the process."""
+    kind, modules, nrec, seed = args
     from fluvio_amd import synth
+    from oracle.oracle import OracleChain
+    sl = synth.make_slice(kind, nrec, seed=seed)
+    oc = OracleChain(modules)
+    t0 = time.perf_counter()
+    r = oc.process_batch(sl)
+    dt = time.perf_counter() - t0
+    assert r["status"] == 0
+    return nrec, dt
+
+
+def cpu_baseline(kind, modules, per_proc):
+    """Oracle CPU baseline, one process per partition on the host cores this box
+    grants (os.cpu_count() shows the whole machine; the GPU box's share is 16)."""
+    import multiprocessing as mp
+    cores = max(1, min(16, os.cpu_count() or 1, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 16))
+    jobs = [(kind, modules, per_proc, 0xC0DE + p) for p in range(cores)]
+    t0 = time.perf_counter()
+    with mp.get_context("spawn").Pool(cores) as pool:
+        res = pool.map(_cpu_proc, jobs)
+    wall = time.perf_counter() - t0
+    n = sum(r[0] for r in res)
+    busy = max(r[1] for r in res)  # slowest process's process_batch time (generation excluded)
+    return {"value": n / busy, "unit": "records/s", "cores": cores, "kind": "port",
+            "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "sample": f"{cores} processes x {per_proc} records (one partition each, synthetic, same generator) "
+                      f"through the scalar C oracle process_batch; value = all records / slowest process's time; "
+                      f"wasmtime itself is not available here (no Rust toolchain)",
+            "seconds": busy, "wall_s": wall}
+
+
+def roofline(per, t, workload, n_records, n_batches):
+    # algorithmic bytes per launch: k_eval reads the slice once; k_write reads the
+    # survivors' payloads (~ the output size) and writes the output batch once; the
+    # CRC reads the output once
+    kernels = {"k_eval": (per["eval_ms"], t["in_bytes"]), "k_write": (per["write_ms"], 2 * t["out_bytes"]),
+               "k_crc": (per["crc_ms"], t["out_bytes"])}
+    dom = max(kernels, key=lambda k: kernels[k][0])
+    dom_ms, dom_bytes = kernels[dom]
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    traffic, src = pmc_traffic(workload, dom, n_records, n_batches)
+    bound = "hbm"
+    return {"bound": bound, "kernel": dom, "achieved": achieved, "peak": PEAK_GBPS, "unit": "GB/s",
+            "frac": achieved / PEAK_GBPS, "traffic": traffic, "traffic_source": src,
+            "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": dom_ms}
+
+
+_SLICES = {}
+
+
+def get_slice(kind, nrec, rank):
+    from fluvio_amd import synth
+    key = (kind, nrec, rank)
+    if key not in _SLICES:
+        t0 = time.time()
+        _SLICES[key] = (synth.make_slice_array(kind, nrec, seed=synth.SEEDS[kind] + rank, base_offset=0),
+                        time.time() - t0)
+    return _SLICES[key]
+
+
+def cpu_baselines_first(ctx, names):
+    """CPU baselines run before this process touches the GPU (the pool's
+    processes are started from a GPU-free parent), rank 0 at N=1 only."""
+    a = ctx.a
+    if ctx.rank != 0 or ctx.world != 1 or a.no_cpu_baseline:
+        return {}
+    out = {}
+    for w in names:
+        if w == "c5-keyed-agg":
+            out[w] = cpu_baseline(3, C5["modules"], min(a.cpu_sample, C5["records_per_partition"]))
+        else:
+            kind, modules, nrec, _ = WORKLOADS[w]
+            out[w] = cpu_baseline(kind, modules, min(a.cpu_sample, nrec))
+    return out
+
+
+def run_filter(ctx, name, nrec, cpu):
+    """One workload: chain over this rank's resident partition slice."""
     from fluvio_amd.smartengine import (ResidentSlice, SmartEngine, SmartModuleChainBuilder,
                                         SmartModuleChainMetrics, SmartModuleConfig, builtin)
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
-
-    engine = SmartEngine(local)
+    a = ctx.a
+    kind, modules, nrec_default, desc = WORKLOADS[name]
+    nrec = nrec or nrec_default
+    engine = SmartEngine(ctx.local)
     b = SmartModuleChainBuilder.default()
     b.set_store_memory_limit(64 << 30)
-    for name, params, acc in modules:
-        b.add_smart_module(SmartModuleConfig.builder().params(params).build(), builtin(name))
+    for mname, params, acc in modules:
+        b.add_smart_module(SmartModuleConfig.builder().params(params).build(), builtin(mname))
     chain = b.initialize(engine)
-
-    # partition slice of this rank (p -> rank), ingested into HBM once
-    t0 = time.time()
-    sl_bytes = synth.make_slice_array(kind, nrec, seed=synth.SEEDS[kind] + rank, base_offset=0)
-    gen_s = time.time() - t0
+    sl_bytes, gen_s = get_slice(kind, nrec, ctx.rank)
     t0 = time.time()
     rs = ResidentSlice(engine, sl_bytes)
     ingest_s = time.time() - t0
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
     metrics = SmartModuleChainMetrics()
     for _ in range(a.warmup):
         chain.process_slice(rs, metrics=metrics, download=False)
-    barrier()
+    ctx.barrier()
     acc = {"eval_ms": 0.0, "plan_ms": 0.0, "write_ms": 0.0, "crc_ms": 0.0, "total_ms": 0.0}
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -94,96 +241,159 @@ def main():
         t = chain.last_timings()
         for k in acc:
             acc[k] += t[k]
-    barrier()
-    elapsed = time.perf_counter() - t0
+    ctx.barrier()
+    elapsed = ctx.max_over_ranks(time.perf_counter() - t0)
     t = chain.last_timings()
-    if dist is not None:
-        import torch
-        v = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(v, op=dist.ReduceOp.MAX)
-        elapsed = float(v.item())
-
-    steps = a.steps
-    ms_per_step = elapsed / steps * 1e3
-    in_bytes = t["in_bytes"]
-    out_bytes = t["out_bytes"]
+    per = {k: acc[k] / a.steps for k in acc}
     recs = rs.n_records
-    value = recs * world * steps / elapsed
-    per = {k: acc[k] / steps for k in acc}
-    # algorithmic bytes per launch: k_eval reads the slice once; k_write reads the
-    # survivors' payloads (~ the output size) and writes the output batch once
-    kernels = {"k_eval": (per["eval_ms"], in_bytes), "k_write": (per["write_ms"], 2 * out_bytes),
-               "k_crc": (per["crc_ms"], out_bytes)}
-    dom = max(kernels, key=lambda k: kernels[k][0])
-    dom_ms, dom_bytes = kernels[dom]
-    peak = 8000.0  # GB/s, MI355X HBM3E (MI355X_MICROARCH.md)
-    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    pipe_gbps = (in_bytes + out_bytes) / (per["total_ms"] * 1e-3) / 1e9
+    res = {"metric": "records/s", "value": recs * ctx.world * a.steps / elapsed, "unit": "records/s",
+           "ms_per_step": elapsed / a.steps * 1e3, "scaling": "weak", "dtype": "u8",
+           "config": {"workload": name, "description": desc, "records_per_gpu": recs,
+                      "batches_per_gpu": rs.n_batches, "slice_bytes_per_gpu": t["in_bytes"],
+                      "output_bytes_per_gpu": t["out_bytes"], "chain": [m[0] for m in modules]},
+           "gbps_input": t["in_bytes"] * ctx.world * a.steps / elapsed / 1e9,
+           "gbps_pipeline": (t["in_bytes"] + t["out_bytes"]) / (per["total_ms"] * 1e-3) / 1e9,
+           "roofline": roofline(per, t, name, recs, rs.n_batches),
+           "kernel_ms": per, "setup_s": {"generate": gen_s, "ingest_h2d": ingest_s}}
+    if not a.no_e2e:
+        # end to end: host slice -> H2D ingest + FileBatchIterator framing -> the
+        # same process_batch -> D2H of the output batch (fsg_chain_process_batch)
+        raw = sl_bytes.tobytes()
+        chain.process_batch(raw)
+        ctx.barrier()
+        reps = 2
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            out = chain.process_batch(raw)
+        ctx.barrier()
+        e2e = ctx.max_over_ranks(time.perf_counter() - t0) / reps
+        res["e2e"] = {"value": recs * ctx.world / e2e, "unit": "records/s", "ms_per_step": e2e * 1e3,
+                      "includes": "H2D of the slice (pageable host memory), host batch framing, the GPU "
+                                  "process_batch, D2H of the output batch",
+                      "output_bytes": len(out.raw)}
+        del raw, out
+    res["cpu_baseline"] = cpu.get(name)
+    del rs, chain
+    return res
 
-    traffic, traffic_src = None, None
-    tpath = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tpath):  # PMC HBM bytes per launch of the same command (scripts/traffic_from_pmc.py)
-        db = json.load(open(tpath)).get(a.workload)
-        if db:
-            # the eval timing brackets k_eval_lean plus the deferred exact k_eval<N>
-            # (and crc brackets k_crc16 + k_crc_final): sum every launch in the bracket
-            hits = [v["total"] for kname, v in db["kernels"].items()
-                    if kname.split("<")[0].startswith("fsg::" + dom)]
-            if hits:
-                traffic, traffic_src = sum(hits), db["source"]
 
-    cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        from oracle.oracle import OracleChain
-        # the sample is a batch-aligned prefix of this rank's own slice
-        pos, n_s = 0, 0
-        while pos < len(sl_bytes) and n_s < a.cpu_sample:
-            hdr = sl_bytes[pos:pos + 61].tobytes()
-            blen = int.from_bytes(hdr[8:12], "big")
-            n_s += int.from_bytes(hdr[57:61], "big")
-            pos += 12 + blen
-        sample = sl_bytes[:pos].tobytes()
-        oc = OracleChain(modules)
-        t1 = time.perf_counter()
-        r = oc.process_batch(sample)
-        cpu_s = time.perf_counter() - t1
-        assert r["status"] == 0
-        cpu = {"value": n_s / cpu_s, "unit": "records/s", "cores": 1, "kind": "port",
-               "sample": f"{n_s} records of the same workload (one process_batch over "
-                         f"{len(sample)} B) through the scalar C oracle on 1 host core; wasmtime "
-                         f"itself is not available here (no Rust)",
-               "seconds": cpu_s}
+def run_c5(ctx, cpu):
+    """C5: topic of 64 partitions, aggregate-sum per partition, partitions sharded
+    p -> rank p mod N; per-partition accumulators stay in HBM and are merged with
+    one RCCL all-reduce of the 64-slot state vector per step."""
+    from fluvio_amd import partitions as PT
+    from fluvio_amd import synth
+    from fluvio_amd.smartengine import (PartitionState, ResidentSlice, SmartEngine, SmartModuleChainBuilder,
+                                        SmartModuleConfig, builtin, comm_unique_id)
+    a = ctx.a
+    P, nrec = C5["partitions"], C5["records_per_partition"]
+    engine = SmartEngine(ctx.local)
+    uid = comm_unique_id() if ctx.rank == 0 else bytes(128)
+    engine.comm_init(ctx.broadcast_bytes(uid, 128), ctx.world, ctx.rank)
+    owned = PT.owned_partitions(P, ctx.world, ctx.rank)
+    t0 = time.time()
+    slices = {p: synth.make_slice_array(3, nrec, seed=synth.SEEDS[3] + p) for p in owned}
+    gen_s = time.time() - t0
+    chains, rsl = {}, {}
+    for p in owned:
+        b = SmartModuleChainBuilder.default()
+        for mname, params, acc in C5["modules"]:
+            b.add_smart_module(SmartModuleConfig.builder().params(params).build(), builtin(mname))
+        chains[p] = b.initialize(engine)
+        rsl[p] = ResidentSlice(engine, slices[p])
+    state = PartitionState(engine, P)
+    nthreads = min(16, len(owned)) or 1
+    groups = [owned[i::nthreads] for i in range(nthreads)]
+    kms = {"eval_ms": 0.0, "write_ms": 0.0, "crc_ms": 0.0, "total_ms": 0.0}
+    lock = threading.Lock()
 
-    if rank == 0:
-        line = {
+    def work(ps):  # one host thread drives a group of partitions, each on its own chain stream
+        for p in ps:
+            chains[p].process_slice(rsl[p], download=False)
+            state.collect(p, chains[p])
+            t = chains[p].last_timings()
+            with lock:
+                for k in kms:
+                    kms[k] += t[k]
+
+    def step():
+        th = [threading.Thread(target=work, args=(g,)) for g in groups if g]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        state.allreduce()  # RCCL sum over xGMI: the topic-wide per-partition table on every rank
+
+    for _ in range(a.warmup):
+        step()
+    ctx.barrier()
+    for k in kms:
+        kms[k] = 0.0
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    ctx.barrier()
+    elapsed = ctx.max_over_ranks(time.perf_counter() - t0)
+    total_recs = sum(rsl[p].n_records for p in owned)
+    if ctx.dist is not None:
+        import torch
+        tt = torch.tensor([total_recs], dtype=torch.float64)
+        ctx.dist.all_reduce(tt)
+        total_recs = int(tt.item())
+    in_bytes = sum(chains[p].last_timings()["in_bytes"] for p in owned)
+    vec = state.read()
+    per = {k: v / a.steps for k, v in kms.items()}
+    res = {"metric": "records/s", "value": total_recs * a.steps / elapsed, "unit": "records/s",
+           "ms_per_step": elapsed / a.steps * 1e3, "scaling": "strong", "dtype": "i32",
+           "config": {"workload": "c5-keyed-agg", "description": C5["description"], "partitions": P,
+                      "records_per_partition": nrec, "partitions_per_gpu": len(owned),
+                      "slice_bytes_this_gpu": in_bytes, "host_threads": nthreads,
+                      "parallelism": f"partitions sharded p -> rank p mod {ctx.world}"},
+           "kernel_ms_sum_over_partitions": per,
+           "gbps_input_per_gpu": in_bytes * a.steps / elapsed / 1e9,
+           "state_checksum": sum(vec) & 0xFFFFFFFF, "setup_s": {"generate": gen_s}}
+    res["cpu_baseline"] = cpu.get("c5-keyed-agg")
+    return res
+
+
+def main():
+    a = parse()
+    ctx = Ctx(a)
+    head = a.workload
+    extra = [] if a.only else [w for w in EXTRA if w != head]
+    cpu = cpu_baselines_first(ctx, [head] + extra)
+    if head == "c5-keyed-agg":
+        line = run_c5(ctx, cpu)
+    else:
+        line = run_filter(ctx, head, a.records, cpu)
+    line = dict(line)
+    workloads = {}
+    for w in extra:
+        workloads[w] = run_c5(ctx, cpu) if w == "c5-keyed-agg" else run_filter(ctx, w, 0, cpu)
+    if ctx.rank == 0:
+        out = {
             "metric": "records/sec + achieved HBM GB/s for SmartModule filter chain, 1/2/4/8 MI355X",
-            "value": value,
+            "value": line["value"],
             "unit": "records/s",
-            "n_gpus": world,
-            "steps": steps,
+            "n_gpus": ctx.world,
+            "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": ms_per_step,
+            "ms_per_step": line["ms_per_step"],
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": line["scaling"],
             "vs_baseline": None,
-            "dtype": "u8",
+            "dtype": line["dtype"],
             "data": "synthetic (fluvio_amd/tools/synth.c), HBM-resident batches",
-            "config": {"workload": a.workload, "description": desc, "records_per_gpu": recs,
-                       "batches_per_gpu": rs.n_batches, "slice_bytes_per_gpu": in_bytes,
-                       "output_bytes_per_gpu": out_bytes, "chain": [m[0] for m in modules],
-                       "parallelism": f"partitions sharded over {world} GPU(s)"},
-            "gbps_pipeline": pipe_gbps,
-            "gbps_input": in_bytes * world * steps / elapsed / 1e9,
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": peak, "unit": "GB/s",
-                         "frac": achieved / peak, "traffic": traffic, "traffic_source": traffic_src,
-                         "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": dom_ms},
-            "kernel_ms": per,
-            "cpu_baseline": cpu,
-            "setup_s": {"generate": gen_s, "ingest_h2d": ingest_s},
+            "config": dict(line["config"], parallelism=f"partitions sharded over {ctx.world} GPU(s)"),
         }
-        print(json.dumps(line))
-    if dist is not None:
-        dist.destroy_process_group()
+        for k, v in line.items():
+            if k not in out and k not in ("metric",):
+                out[k] = v
+        if workloads:
+            out["workloads"] = workloads
+        print(json.dumps(out))
+    if ctx.dist is not None:
+        ctx.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

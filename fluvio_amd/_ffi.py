@@ -104,8 +104,18 @@ SIGNATURES = {
     "fsg_chain_output_device": (ctypes.c_int, [VP, PP, ctypes.POINTER(SZ)]),
     "fsg_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "fsg_engine_comm_init": (ctypes.c_int, [VP, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]),
-    "fsg_allreduce_i32": (ctypes.c_int, [VP, VP, SZ]),
+    "fsg_allreduce_state": (ctypes.c_int, [VP, VP, SZ, ctypes.c_int]),
+    "fsg_chain_allreduce_state": (ctypes.c_int, [VP, VP, SZ, ctypes.c_int]),
+    "fsg_last_store_memory": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64)] * 3),
+    "fsg_state_new": (ctypes.c_int, [VP, SZ, ctypes.c_int, PP]),
+    "fsg_state_collect": (ctypes.c_int, [VP, SZ, VP]),
+    "fsg_state_allreduce": (ctypes.c_int, [VP]),
+    "fsg_state_read": (ctypes.c_int, [VP, VP, SZ]),
+    "fsg_state_device": (ctypes.c_int, [VP, PP]),
+    "fsg_state_free": (None, [VP]),
 }
+
+FSG_DTYPE_I32, FSG_DTYPE_U32, FSG_DTYPE_I64, FSG_DTYPE_U64, FSG_DTYPE_F64 = range(5)
 
 _lib = None
 

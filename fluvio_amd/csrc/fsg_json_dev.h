@@ -777,12 +777,16 @@ struct JsonDev {
   // serialization (ser.rs: compact, format_escaped_str, itoa).  Objects must
   // already be in BTreeMap order (strictly increasing keys) and numbers must
   // be integers (serde_json turns floats, -0 and integers beyond u64/i64 into
-  // f64, whose ryu Display is outside the restatement): anything else is
-  // JE_UNSUP, which the engine reports as FSG_E_UNSUPPORTED if reached.
+  // f64, whose ryu Display is outside the restatement): a float stops the
+  // parse with JE_UNSUP at once (as the oracle does), an object that needs
+  // re-ordering only once the whole document has parsed (a later syntax error
+  // is still reported exactly).  The engine reports JE_UNSUP as
+  // FSG_E_UNSUPPORTED if that record is reached in stream order.
   // ------------------------------------------------------------------------
   uint32_t vcanon;  // canonical bytes of the element being parsed
   bool vhas_u;      // a \u escape was decoded (canonical form may differ in bytes)
   bool vhas_bs;     // the last string held a backslash
+  bool vunsup;      // an object needs re-ordering: unsupported unless a later syntax error decides
   static __device__ __forceinline__ uint32_t canon_byte_len(uint32_t c) {
     if (c == '"' || c == '\\' || c == 0x08 || c == 0x09 || c == 0x0A || c == 0x0C || c == 0x0D) return 2;
     return c < 0x20 ? 6 : 1;
@@ -957,12 +961,11 @@ struct JsonDev {
         const uint32_t lv = sn - 1;
         if (lv >= (uint32_t)kKeyFrames) {
           // deeper objects: only a single-member object is known to be in order
-          if (!first_member) return fail_at(i, JE_UNSUP);
+          if (!first_member) vunsup = true;
         } else {
           if (pk1[lv] != 0xFFFFFFFFu) {
             const bool esc_prev = (pk0[lv] >> 31) != 0;
-            if (esc_prev || vhas_bs) return fail_at(i, JE_UNSUP);
-            if (key_cmp(pk0[lv] & 0x7FFFFFFFu, pk1[lv], k0, k1) >= 0) return fail_at(i, JE_UNSUP);
+            if (esc_prev || vhas_bs || key_cmp(pk0[lv] & 0x7FFFFFFFu, pk1[lv], k0, k1) >= 0) vunsup = true;
           }
           pk0[lv] = k0 | (vhas_bs ? 0x80000000u : 0u);
           pk1[lv] = k1;
@@ -987,6 +990,7 @@ struct JsonDev {
     has_pos = false;
     depth = 128;
     i = 0;
+    vunsup = false;
     uint32_t k = 0;
     int rc = 0;
     int c = ws();
@@ -1042,6 +1046,8 @@ struct JsonDev {
     }
     if (rc) fix_position();
     if (!rc && ws() >= 0) rc = peek_error(JE_TRAILING);  // Deserializer::end
+    // a valid document whose objects need re-ordering: outside the restatement
+    if (!rc && vunsup) rc = fail_at(i, JE_UNSUP);
     *count = k;
     if (!rc) r.ok = 1;
     return r;

@@ -17,6 +17,8 @@
 //   k_crc_*    CRC32C over attributes..records, chunked + GF(2) combine
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include "fsg_device.h"
 #include "fsg_json_dev.h"
 
@@ -209,35 +211,6 @@ __device__ int parse_i32(P s, uint32_t n, int32_t* out) {
   *out = (int32_t)acc;
   return 0;
 }
-
-// ---------------------------------------------------------------------------
-// diagnostic phase stamps (built only with -DFSG_STAMPS; never in the product)
-// ---------------------------------------------------------------------------
-#ifdef FSG_STAMPS
-__device__ unsigned long long g_stamps[16];
-#define STAMP_DECL unsigned long long st_acc[16] = {0}; unsigned long long st_t = __builtin_amdgcn_s_memtime();
-#define STAMP(i)                                                 \
-  do {                                                           \
-    unsigned long long t_ = __builtin_amdgcn_s_memtime();        \
-    st_acc[i] += t_ - st_t;                                      \
-    st_t = t_;                                                   \
-  } while (0)
-#define STAMP_COUNT(i, v) st_acc[i] += (v)
-#define STAMP_PARAMS , unsigned long long* st_acc, unsigned long long& st_t
-#define STAMP_ARGS , st_acc, st_t
-#define STAMP_FLUSH()                                                        \
-  do {                                                                       \
-    if (threadIdx.x == 0)                                                    \
-      for (int i_ = 0; i_ < 16; i_++) if (st_acc[i_]) atomicAdd(&g_stamps[i_], st_acc[i_]); \
-  } while (0)
-#else
-#define STAMP_DECL
-#define STAMP(i)
-#define STAMP_COUNT(i, v)
-#define STAMP_PARAMS
-#define STAMP_ARGS
-#define STAMP_FLUSH()
-#endif
 
 // ---------------------------------------------------------------------------
 // k_eval: per-wave LDS state
@@ -569,9 +542,6 @@ __device__ __forceinline__ void scan_contains(WaveLds& L, P w, uint32_t wlen, in
         }
     }
     if (m == 0) continue;
-#if defined(FSG_EXP) && FSG_EXP == 1
-    continue;  // experiment: substring filter off (timing/counter attribution only)
-#endif
     if (upper)
       for (int k = 0; k < 8; k++) wd[k] = swar_upper(wd[k]);
     uint64_t any = 0;
@@ -705,7 +675,7 @@ __device__ bool dfa_run_full(P s, uint32_t n, const uint8_t* blob, const DfaDesc
 // ---------------------------------------------------------------------------
 template <uint32_t kOps, bool kLds, typename P>
 __device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int nr, const ChainDesc& ch, const uint8_t* blob,
-                            int nst, int lds_stage, bool& unsupported, uint64_t wbase, ElemRec* elem STAMP_PARAMS) {
+                            int nst, int lds_stage, bool& unsupported, uint64_t wbase, ElemRec* elem) {
   const uint32_t l = threadIdx.x;
   bool nonascii_done = false;
   for (int s = 0; s < nst; s++) {
@@ -719,7 +689,6 @@ __device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int 
     // ---- data-parallel phase over window bytes
     for (int r = l; r < nr; r += kEvalThreads) L.r_flags[r] &= ~RF_MATCH;
     __syncthreads();
-    STAMP(10);
     if ((kOps & opbit(OP_CONTAINS)) && src && op == OP_CONTAINS) {
       scan_contains<kLds>(L, w, wlen, nr, blob + sd.needle, sd.needle_len, upper, !nonascii_done);
       nonascii_done = true;
@@ -738,7 +707,6 @@ __device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int 
         scan_regex_bounded(L, w, nr, dv, sd.dfa.s_bot, sd.dfa.s_mid, (uint32_t)sd.dfa.max_len);
     }
     __syncthreads();
-    STAMP(11);
     // ---- per-record phase (thread per record; record r = 4 * lane + wave so
     // that the records of a window are spread over the four waves)
     static_assert(kMaxR <= kEvalThreads, "one pass covers every record");
@@ -919,7 +887,6 @@ __device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int 
       L.r_flags[r] = f;
     }
     __syncthreads();
-    STAMP(12);
   }
 }
 
@@ -944,7 +911,6 @@ __device__ __forceinline__ void load_window(WaveLds& L, const uint8_t* slice, ui
 // ---------------------------------------------------------------------------
 template <uint32_t kOps>
 __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const uint32_t b) {
-  STAMP_DECL
   const uint32_t l = lane_id();
   const uint32_t tid = threadIdx.x;
   const bool wave0 = tid < 64;
@@ -1034,18 +1000,13 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
       if (wend > sec_end16) wend = sec_end16;
       const uint32_t wlen = (uint32_t)(wend - al);
       __syncthreads();
-      STAMP(0);
       if (!first_window) load_window(L, S, al, wlen);
       first_window = false;
-      STAMP(1);
-      STAMP_COUNT(8, 1);
       if (!walk_fast(L, (const uint8_t*)L.win, al, wlen, sec_end, cursor, nrec_total - done_recs)) {
-        STAMP_COUNT(9, 1);
         if (tid == 0)
           walk_records(L, (const uint8_t*)L.win, al, wlen, sec_end, cursor, nrec_total - done_recs, kMaxR);
         __syncthreads();
       }
-      STAMP(2);
       int nr = L.nr;
       const int ws = L.walk_status;
       bool global_mode = false;
@@ -1072,12 +1033,11 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
       if (phase == 1 && done_recs + (uint32_t)nr > err_idx + 1) nr_eval = (int)(err_idx + 1 - done_recs);
       if (global_mode)
         eval_window<kOps, false>(L, S + gbase, (uint32_t)(sec_end - gbase), nr_eval, ch, a.blob, nst, lds_stage,
-                           unsupported, gbase, a.elem STAMP_ARGS);
+                           unsupported, gbase, a.elem);
       else
         eval_window<kOps, true>(L, (const uint8_t*)L.win, wlen, nr_eval, ch, a.blob, nst, lds_stage,
-                          unsupported, al, a.elem STAMP_ARGS);
+                          unsupported, al, a.elem);
       const uint64_t wbase = global_mode ? gbase : al;
-      STAMP(3);
       // ---- error tracking (phase A) and descriptor emission: wave 0, in record order
       for (int r0 = 0; wave0 && r0 < nr_eval; r0 += 64) {
         const int r = r0 + (int)l;
@@ -1195,7 +1155,6 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
       done_recs += (uint32_t)nr;
       cursor = ((uint64_t)L.next_cursor_hi << 32) | L.next_cursor_lo;
       (void)last;
-      STAMP(4);
     }
     if (phase == 0 && err_stage == 0xFFFFFFFFu) break;
   }
@@ -1217,8 +1176,6 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
     st.cat_sum = (ch.has_agg && agg_ran) ? catsum : 0;
     a.bstat[b] = st;  // the cross-batch minima are reduced by k_mins
   }
-  STAMP(5);
-  STAMP_FLUSH();
 }
 
 // k_eval: batches blockIdx.x (direct mode) or the deferred list written by
@@ -1248,9 +1205,8 @@ __global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : 2) void 
 //   3. per contains stage, a data-parallel 4-gram scan over the value bytes
 //      (16 B + 4 B look-ahead per lane, ballot-filtered); 4-gram hits are parked
 //      in registers and resolved after the scan (record lookup + full needle);
-//      the first scan also counts bytes >= 0x80 in [first value, last value end)
-//      and compares with the count inside the inter-value gaps: equal <=> all
-//      values are ASCII
+//      before the first scan the bytes between values are cleared, so the OR
+//      of every scanned word has a high bit iff some value is non-ASCII
 //   4. survivors -> compaction descriptors (ballot prefix), BatchStat
 // ---------------------------------------------------------------------------
 constexpr int kLeanWin = 16464;  // 57-B header + 16 KiB section + 15 B alignment, 16-B multiple
@@ -1362,9 +1318,6 @@ __device__ __forceinline__ uint32_t lean_scan(LeanLds& L, int nr, uint32_t lo, u
 #pragma unroll
       for (int j = 0; j < 16; j++) any |= __ballot(((win5(wd, j) ^ rot[0]) & k4) == 0);
     }
-#if defined(FSG_EXP) && FSG_EXP == 6
-    if (any != 1234567) continue;  // experiment: compares without the hit path
-#endif
     if (!any) continue;               // wave-uniform: no 4-gram hit in any lane
     if (!((any >> lane) & 1)) continue;  // none in this lane
     if (kMode == 0) {
@@ -1417,7 +1370,6 @@ __device__ __forceinline__ uint32_t lean_scan(LeanLds& L, int nr, uint32_t lo, u
 
 __global__ __launch_bounds__(kLeanThreads) void k_eval_lean(EvalArgs a) {
   __shared__ LeanLds L;
-  STAMP_DECL
   const uint32_t b = blockIdx.x;
   const uint32_t l = threadIdx.x;
   const ChainDesc& ch = *a.chain;
@@ -1439,11 +1391,6 @@ __global__ __launch_bounds__(kLeanThreads) void k_eval_lean(EvalArgs a) {
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
   }
-  STAMP(0);
-#if defined(FSG_EXP) && FSG_EXP == 3
-  if (l == 0) a.bstat[b] = BatchStat{};  // experiment: DMA only (timing attribution)
-  return;
-#endif
   // batch header (file format, batch.rs:163-180), read before the gaps are cleared
   const uint8_t* h = L.win + (pos - al);
   const int64_t base_offset = (int64_t)rd_be(h, 8);
@@ -1485,11 +1432,6 @@ __global__ __launch_bounds__(kLeanThreads) void k_eval_lean(EvalArgs a) {
   __syncthreads();
   // a failed chase leaves the lengths unverified: the exact walk decides
   if (!defer) defer = __builtin_amdgcn_readfirstlane(L.chase_bad) != 0u;
-  STAMP(1);
-#if defined(FSG_EXP) && FSG_EXP == 4
-  if (l == 0) a.bstat[b] = BatchStat{};  // experiment: DMA + chase only
-  return;
-#endif
   const int nr = defer ? 0 : count;
   bool g = true;
   int64_t ts = 0, od = 0, hdr = 0;
@@ -1523,29 +1465,19 @@ __global__ __launch_bounds__(kLeanThreads) void k_eval_lean(EvalArgs a) {
     L.r_ve[l] = vs + vl;
   }
   defer = __syncthreads_or(defer || !g);  // a record that does not frame exactly
-  STAMP(2);
   uint64_t alive = __ballot((int)l < nr);
   // 3. stages.  Before the first scan every non-value byte of the scanned
   //    range is cleared (record headers, keys, lengths): then the OR of the
   //    scanned words has a high bit iff some value is non-ASCII.
   bool checked = false;
-#if defined(FSG_EXP) && FSG_EXP == 2
-  checked = true;
-  for (uint32_t s = 0; false; s++) {  // experiment: no scan
-#else
   for (uint32_t s = 0; !defer && s < ch.nstages; s++) {
-#endif
     const StageDesc& sd = ch.st[s];
     if (sd.op != OP_CONTAINS) continue;  // OP_MAP_UPPER: representation only
     const uint32_t m = sd.needle_len;
     if (m == 0 && checked) continue;     // an empty needle keeps every (UTF-8) value
     if (nr == 0) break;
     const uint32_t lo = L.r_vs[0], hi = L.r_ve[nr - 1];
-#if defined(FSG_EXP) && FSG_EXP == 7
-    if (false) {  // experiment: no gap clearing
-#else
     if (!checked) {
-#endif
       if ((int)l < nr) {
         const uint32_t e = (int)l + 1 < nr ? L.r_vs[l + 1] : ((vs + vl + 15) & ~15u) + 16;
         for (uint32_t p = vs + vl; p < e; p++) L.win[p] = 0;
@@ -1573,19 +1505,14 @@ __global__ __launch_bounds__(kLeanThreads) void k_eval_lean(EvalArgs a) {
     __syncthreads();
     const bool upper = sd.in_type == VT_SRC_UPPER;
     uint32_t orw;
-#if defined(FSG_EXP) && FSG_EXP == 5
-    if (true) orw = lean_scan<3>(L, nr, lo, hi, nd, m, upper); else  // experiment: OR only
-#endif
     if (m >= 7) orw = lean_scan<0>(L, nr, lo, hi, nd, m, upper);
     else if (m >= 4) orw = lean_scan<1>(L, nr, lo, hi, nd, m, upper);
     else if (m > 0) orw = lean_scan<2>(L, nr, lo, hi, nd, m, upper);
     else orw = lean_scan<3>(L, nr, lo, hi, nd, m, upper);
-    STAMP(3);
     const bool high = __syncthreads_or((orw & 0x80808080u) != 0u);  // also orders the match bits
     if (!checked && high) defer = true;  // a non-ASCII value: exact UTF-8 path
     checked = true;
     if (m > 0) alive &= __ballot(l < 64 && ((L.match[(l >> 5) & 1] >> (l & 31)) & 1u));
-    STAMP(4);
   }
   if (defer) {
     if (l == 0) {
@@ -1625,8 +1552,6 @@ __global__ __launch_bounds__(kLeanThreads) void k_eval_lean(EvalArgs a) {
     st.err_stage = 0xFFFFFFFFu;
     a.bstat[b] = st;
   }
-  STAMP(5);
-  STAMP_FLUSH();
 }
 
 // ---------------------------------------------------------------------------
@@ -1928,6 +1853,15 @@ __global__ void k_plan(PlanArgs a) {
   *a.plan = p;
 }
 
+// k_state: the aggregate-sum accumulator after this call, kept in HBM
+// (SmartModuleAggregate.accumulator, transforms/aggregate.rs:95): unchanged
+// unless the aggregate emitted records
+__global__ void k_state(const Plan* plan, int32_t* state) {
+  if (threadIdx.x != 0) return;
+  const Plan p = *plan;
+  if (p.status == 0 && p.acc_touched) *state = (int32_t)p.acc_final;
+}
+
 // ---------------------------------------------------------------------------
 // k_header: output batch header (Batch::default() + base offset, lod, count)
 // ---------------------------------------------------------------------------
@@ -2070,7 +2004,10 @@ __device__ void json_canon_write(const uint8_t* __restrict__ s, uint32_t n, bool
     i++;
     for (;;) {
       const uint32_t d = at(i++);
-      if (d == '"') break;
+      if (d == '"') {
+        *o++ = '"';
+        break;
+      }
       if (d != '\\') {
         if (d < 0x80) put_esc(d); else *o++ = (uint8_t)d;
         continue;
@@ -2437,10 +2374,16 @@ __global__ void k_crc_final(uint8_t* out, const uint32_t* acc, uint64_t tail0, u
 
 namespace fsg {
 
-static bool g_tabs_ready = false;
+// g_crc_z16 / g_crc_shift exist once per device: upload per device, under a lock
+static std::mutex g_tabs_mu;
+static uint64_t g_tabs_ready = 0;  // bit d: tables resident on device d
 
 hipError_t upload_crc_tables() {
-  if (g_tabs_ready) return hipSuccess;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lock(g_tabs_mu);
+  if (dev < 64 && ((g_tabs_ready >> dev) & 1)) return hipSuccess;
   static uint32_t z16[16][256];
   for (uint32_t i = 0; i < 256; i++) {
     uint32_t c = i;
@@ -2472,10 +2415,10 @@ hipError_t upload_crc_tables() {
       for (uint32_t v = 0; v < 256; v++) shift[k][b][v] = mm(X, v << (8 * b));
     X = mm(X, X);
   }
-  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_crc_z16), z16, sizeof z16);
+  e = hipMemcpyToSymbol(HIP_SYMBOL(g_crc_z16), z16, sizeof z16);
   if (e != hipSuccess) return e;
   e = hipMemcpyToSymbol(HIP_SYMBOL(g_crc_shift), shift, sizeof shift);
-  if (e == hipSuccess) g_tabs_ready = true;
+  if (e == hipSuccess && dev < 64) g_tabs_ready |= 1ull << dev;
   return e;
 }
 
@@ -2519,6 +2462,9 @@ void launch_scan(const ScanRow* rows, ScanRow* pre, ScanRow* tile_sums, ScanRow*
   hipLaunchKernelGGL(k_scan_down, dim3(nt), dim3(kScanBlock), 0, s, d);
 }
 void launch_plan(const PlanArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_plan, dim3(1), dim3(64), 0, s, a); }
+void launch_state(const Plan* plan, int32_t* state, hipStream_t s) {
+  hipLaunchKernelGGL(k_state, dim3(1), dim3(64), 0, s, plan, state);
+}
 void launch_header(const Plan* plan, uint8_t* out, hipStream_t s) {
   hipLaunchKernelGGL(k_header, dim3(1), dim3(64), 0, s, plan, out);
 }
@@ -2545,14 +2491,3 @@ void launch_crc(uint8_t* out, uint64_t off, uint64_t n, uint32_t* acc, hipStream
 }
 
 }  // namespace fsg
-
-#ifdef FSG_STAMPS
-extern "C" int fsg_debug_stamps(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fsg::g_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
-  if (reset) {
-    unsigned long long z[16] = {0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(fsg::g_stamps), z, sizeof z) != hipSuccess) return -1;
-  }
-  return 0;
-}
-#endif

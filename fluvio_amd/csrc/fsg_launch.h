@@ -14,6 +14,7 @@ uint32_t scan_tiles(uint32_t n);
 void launch_scan(const ScanRow* rows, ScanRow* pre, ScanRow* tile_sums, ScanRow* grand, uint32_t n, bool cut,
                  uint64_t max_bytes, Mins* mins, const BatchStat* bstat, hipStream_t s);
 void launch_plan(const PlanArgs& a, hipStream_t s);
+void launch_state(const Plan* plan, int32_t* state, hipStream_t s);
 void launch_header(const Plan* plan, uint8_t* out, hipStream_t s);
 void launch_write(const WriteArgs& a, uint32_t nblocks, hipStream_t s);
 void launch_cat(const WriteArgs& a, uint32_t nbatches, hipStream_t s);

@@ -36,9 +36,16 @@ using namespace fsg;
 // error plumbing
 // ---------------------------------------------------------------------------
 static thread_local std::string g_err;
+static thread_local uint64_t g_store_mem[3];  // current, requested, max of the last FSG_E_STORE_MEMORY
 static int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
+}
+extern "C" int fsg_last_store_memory(uint64_t* current, uint64_t* requested, uint64_t* max) {
+  if (current) *current = g_store_mem[0];
+  if (requested) *requested = g_store_mem[1];
+  if (max) *max = g_store_mem[2];
+  return FSG_OK;
 }
 #define HIPCHK(x)                                                                        \
   do {                                                                                   \
@@ -198,6 +205,7 @@ struct fsg_engine {
   int device = 0;
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  hipStream_t coll = nullptr;  // collective stream (state merges)
 };
 
 struct fsg_chain_builder {
@@ -228,6 +236,7 @@ struct fsg_chain {
   std::vector<uint8_t> acc;  // aggregate accumulator bytes (SmartModuleAggregate.accumulator)
   // scratch
   DevBuf bstat, kept, rows, pre, aggpre, tiles, grand, mins, plan, out, crcparts, defer, elem, cat;
+  DevBuf dstate;  // aggregate-sum accumulator (i32) after the last call, in HBM
   Plan hplan{};
   hipEvent_t ev[6] = {};
   fsg_timings last{};
@@ -256,8 +265,11 @@ extern "C" int fsg_engine_new(int device, fsg_engine** out) {
   if (device < 0 || device >= n) return fail(FSG_E_INVALID_ARG, "device index out of range");
   HIPCHK(hipSetDevice(device));
   HIPCHK(upload_crc_tables());
+  hipStream_t coll = nullptr;
+  HIPCHK(hipStreamCreateWithFlags(&coll, hipStreamNonBlocking));
   auto* e = new fsg_engine();
   e->device = device;
+  e->coll = coll;
   *out = e;
   return FSG_OK;
 }
@@ -265,6 +277,7 @@ extern "C" int fsg_engine_new(int device, fsg_engine** out) {
 extern "C" void fsg_engine_free(fsg_engine* e) {
   if (!e) return;
   if (e->comm) ncclCommDestroy(e->comm);
+  if (e->coll) (void)hipStreamDestroy(e->coll);
   delete e;
 }
 
@@ -441,6 +454,11 @@ extern "C" int fsg_chain_builder_initialize(fsg_chain_builder* b, fsg_engine* e,
   if (c->hblob.empty()) c->hblob.resize(16, 0);
   HIPCHK(c->d_blob.ensure(c->hblob.size()));
   HIPCHK(hipMemcpy(c->d_blob.p, c->hblob.data(), c->hblob.size(), hipMemcpyHostToDevice));
+  if (c->hdesc.flags & CF_AGG_SUM) {  // the accumulator's i32 value, resident in HBM
+    HIPCHK(c->dstate.ensure(sizeof(int32_t)));
+    const int32_t a0 = acc_value(c->acc);
+    HIPCHK(hipMemcpy(c->dstate.p, &a0, sizeof a0, hipMemcpyHostToDevice));
+  }
   *out = c.release();
   return FSG_OK;
 }
@@ -778,6 +796,9 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   if (need > c->limit) {
     char b[160];
     snprintf(b, sizeof b, "Requested memory %zub exceeded max allowed %zub", need, c->limit);
+    g_store_mem[0] = 0;  // nothing of this call is allocated yet
+    g_store_mem[1] = need;
+    g_store_mem[2] = c->limit;
     return fail(FSG_E_STORE_MEMORY, b);
   }
   HIPCHK(c->bstat.ensure(std::max<uint32_t>(nb, 1) * sizeof(BatchStat)));
@@ -853,6 +874,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   pa.has_agg = has_agg;
   pa.acc0 = acc0;
   launch_plan(pa, st);
+  if (c->hdesc.flags & CF_AGG_SUM) launch_state(pa.plan, c->dstate.as<int32_t>(), st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[2], st));
   HIPCHK(hipMemcpyAsync(&c->hplan, c->plan.p, sizeof(Plan), hipMemcpyDeviceToHost, st));
@@ -1088,11 +1110,87 @@ extern "C" int fsg_engine_comm_init(fsg_engine* e, const uint8_t id[FSG_UNIQUE_I
   e->rank = rank;
   return FSG_OK;
 }
-extern "C" int fsg_allreduce_i32(fsg_engine* e, void* dev_state, size_t count) {
-  if (!e->comm) return fail(FSG_E_INVALID_ARG, "engine has no communicator");
+namespace {
+bool nccl_type(int dtype, ncclDataType_t* t, size_t* sz) {
+  switch (dtype) {
+    case FSG_DTYPE_I32: *t = ncclInt32; *sz = 4; return true;
+    case FSG_DTYPE_U32: *t = ncclUint32; *sz = 4; return true;
+    case FSG_DTYPE_I64: *t = ncclInt64; *sz = 8; return true;
+    case FSG_DTYPE_U64: *t = ncclUint64; *sz = 8; return true;
+    case FSG_DTYPE_F64: *t = ncclFloat64; *sz = 8; return true;
+    default: return false;
+  }
+}
+int allreduce_on(fsg_engine* e, void* dev, size_t count, int dtype, hipStream_t st) {
+  if (!e->comm) return fail(FSG_E_INVALID_ARG, "engine has no communicator (fsg_engine_comm_init)");
+  ncclDataType_t t;
+  size_t sz;
+  if (!nccl_type(dtype, &t, &sz)) return fail(FSG_E_INVALID_ARG, "unknown state dtype");
   HIPCHK(hipSetDevice(e->device));
-  ncclResult_t r = ncclAllReduce(dev_state, dev_state, count, ncclInt32, ncclSum, e->comm, 0);
+  // integer sums wrap in two's complement, like the wasm guest's release-mode adds
+  ncclResult_t r = ncclAllReduce(dev, dev, count, t, ncclSum, e->comm, st);
   if (r != ncclSuccess) return fail(FSG_E_DEVICE, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
-  HIPCHK(hipStreamSynchronize(0));
+  HIPCHK(hipStreamSynchronize(st));
   return FSG_OK;
 }
+}  // namespace
+
+extern "C" int fsg_allreduce_state(fsg_engine* e, void* dev_state, size_t count, int dtype) {
+  return allreduce_on(e, dev_state, count, dtype, e->coll);
+}
+extern "C" int fsg_chain_allreduce_state(fsg_chain* c, void* dev_state, size_t count, int dtype) {
+  return allreduce_on(c->eng, dev_state, count, dtype, c->stream);
+}
+
+// ---------------------------------------------------------------------------
+// per-partition aggregate state vector in HBM
+// ---------------------------------------------------------------------------
+struct fsg_state {
+  fsg_engine* eng = nullptr;
+  DevBuf buf;
+  size_t count = 0, esize = 4;
+  int dtype = FSG_DTYPE_I32;
+};
+
+extern "C" int fsg_state_new(fsg_engine* e, size_t count, int dtype, fsg_state** out) {
+  ncclDataType_t t;
+  size_t sz;
+  if (!nccl_type(dtype, &t, &sz)) return fail(FSG_E_INVALID_ARG, "unknown state dtype");
+  HIPCHK(hipSetDevice(e->device));
+  auto s = std::make_unique<fsg_state>();
+  s->eng = e;
+  s->count = count;
+  s->esize = sz;
+  s->dtype = dtype;
+  HIPCHK(s->buf.ensure(std::max<size_t>(count, 1) * sz));
+  HIPCHK(hipMemsetAsync(s->buf.p, 0, std::max<size_t>(count, 1) * sz, e->coll));
+  HIPCHK(hipStreamSynchronize(e->coll));
+  *out = s.release();
+  return FSG_OK;
+}
+extern "C" int fsg_state_collect(fsg_state* s, size_t slot, fsg_chain* c) {
+  if (slot >= s->count) return fail(FSG_E_INVALID_ARG, "state slot out of range");
+  if (!(c->hdesc.flags & CF_AGG_SUM) || s->dtype != FSG_DTYPE_I32)
+    return fail(FSG_E_INVALID_ARG, "collect needs an aggregate-sum chain and an i32 state vector");
+  if (c->eng->device != s->eng->device) return fail(FSG_E_INVALID_ARG, "chain and state on different devices");
+  HIPCHK(hipSetDevice(s->eng->device));
+  // device to device on the chain's stream, after its last k_state; chains of
+  // different partitions may collect from different host threads at once
+  HIPCHK(hipMemcpyAsync((uint8_t*)s->buf.p + slot * s->esize, c->dstate.p, 4, hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return FSG_OK;
+}
+extern "C" int fsg_state_allreduce(fsg_state* s) {
+  return allreduce_on(s->eng, s->buf.p, s->count, s->dtype, s->eng->coll);
+}
+extern "C" int fsg_state_read(fsg_state* s, void* host, size_t bytes) {
+  HIPCHK(hipSetDevice(s->eng->device));
+  HIPCHK(hipStreamSynchronize(s->eng->coll));
+  HIPCHK(hipMemcpy(host, s->buf.p, std::min(bytes, s->count * s->esize), hipMemcpyDeviceToHost));
+  return FSG_OK;
+}
+extern "C" int fsg_state_device(fsg_state* s, void** dptr) {
+  *dptr = s->buf.p;
+  return FSG_OK;
+}
+extern "C" void fsg_state_free(fsg_state* s) { delete s; }

@@ -32,7 +32,8 @@ from .protocol import Batch, Record, decode_batch, decode_records, encode_record
 DEFAULT_SMARTENGINE_VERSION = 22  # input.rs:14 SMARTMODULE_TIMESTAMPS_VERSION
 
 BUILTINS = ("filter", "filter_init", "filter_with_param", "regex-filter", "filter_regex", "filter_odd",
-            "map", "map_double", "filter_map", "aggregate-sum", "filter_json")
+            "map", "map_double", "filter_map", "aggregate-sum", "aggregate", "filter_json",
+            "array_map_json_array")
 
 
 def builtin(name: str) -> bytes:
@@ -61,7 +62,14 @@ class Instantiate(EngineError):
 
 
 class StoreMemoryExceeded(EngineError):
+    """EngineError::StoreMemoryExceeded{current, requested, max} (error.rs:2-13)."""
     code = _ffi.FSG_E_STORE_MEMORY
+
+    def __init__(self, message: str = "", code: Optional[int] = None):
+        super().__init__(message, code)
+        c, r, m = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _ffi.lib().fsg_last_store_memory(ctypes.byref(c), ctypes.byref(r), ctypes.byref(m))
+        self.current, self.requested, self.max = c.value, r.value, m.value
 
 
 class SmartModuleInitError(EngineError):
@@ -279,13 +287,49 @@ class SmartEngine:
     def comm_init(self, unique_id: bytes, nranks: int, rank: int) -> None:
         _check(_ffi.lib().fsg_engine_comm_init(self._h, unique_id, nranks, rank))
 
-    def allreduce_i32(self, dev_ptr: int, count: int) -> None:
-        _check(_ffi.lib().fsg_allreduce_i32(self._h, ctypes.c_void_p(dev_ptr), count))
+    def allreduce_state(self, dev_ptr: int, count: int, dtype: int = _ffi.FSG_DTYPE_I32) -> None:
+        """RCCL sum of `count` state elements in HBM across the engine's communicator."""
+        _check(_ffi.lib().fsg_allreduce_state(self._h, ctypes.c_void_p(dev_ptr), count, dtype))
 
     def __del__(self):
         h = getattr(self, "_h", None)
         if h and h.value and _ffi._lib is not None:
             _ffi.lib().fsg_engine_free(h)
+            self._h = None
+
+
+class PartitionState:
+    """Per-partition aggregate state vector in HBM (fsg_state_*): one i32 slot
+    per topic partition, filled device-to-device from each partition's
+    aggregate-sum chain and merged across GPUs with an RCCL all-reduce."""
+
+    def __init__(self, engine: SmartEngine, count: int, dtype: int = _ffi.FSG_DTYPE_I32):
+        h = ctypes.c_void_p()
+        _check(_ffi.lib().fsg_state_new(engine._h, count, dtype, ctypes.byref(h)))
+        self._h, self._engine, self.count, self.dtype = h, engine, count, dtype
+
+    def collect(self, slot: int, chain: "SmartModuleChainInstance") -> None:
+        _check(_ffi.lib().fsg_state_collect(self._h, slot, chain._h))
+
+    def allreduce(self) -> None:
+        _check(_ffi.lib().fsg_state_allreduce(self._h))
+
+    def device_ptr(self) -> int:
+        p = ctypes.c_void_p()
+        _check(_ffi.lib().fsg_state_device(self._h, ctypes.byref(p)))
+        return p.value or 0
+
+    def read(self) -> List[int]:
+        import array
+        a = array.array("i" if self.dtype == _ffi.FSG_DTYPE_I32 else "q", [0] * self.count)
+        addr, _ = a.buffer_info()
+        _check(_ffi.lib().fsg_state_read(self._h, ctypes.c_void_p(addr), self.count * a.itemsize))
+        return list(a)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and h.value and _ffi._lib is not None:
+            _ffi.lib().fsg_state_free(h)
             self._h = None
 
 

@@ -21,6 +21,12 @@
  *   fsg_chain_get_accumulator           SmartModuleAggregate accumulator            transforms/aggregate.rs:22-25,95
  *   fsg_metrics                         SmartModuleChainMetrics                     crates/fluvio-smartengine/src/engine/metrics.rs:6-41
  *   fsg_runtime_error                   SmartModuleTransformRuntimeError            crates/fluvio-protocol/src/link/smartmodule.rs:12-43
+ *   fsg_last_store_memory               EngineError::StoreMemoryExceeded{current,requested,max}
+ *                                         crates/fluvio-smartengine/src/engine/error.rs:2-13
+ *   fsg_state_* / fsg_allreduce_state   per-partition aggregate state (SmartModuleAggregate.accumulator,
+ *                                         transforms/aggregate.rs:22-25) kept in HBM and merged across GPUs;
+ *                                         no reference counterpart (partitions never exchange state there:
+ *                                         crates/fluvio-spu/src/smartengine/context.rs:25-30)
  *
  * SmartModule selection happens at chain-build time: `module` bytes are either a
  * wasm binary ("\0asm" magic -> FSG_E_UNKNOWN_SM: this library runs no wasm) or a
@@ -49,7 +55,7 @@
 extern "C" {
 #endif
 
-#define FSG_ABI_VERSION 1
+#define FSG_ABI_VERSION 2
 
 /* ---- status codes (mirror EngineError and the guest status enums) ---- */
 #define FSG_OK 0
@@ -139,6 +145,9 @@ typedef struct fsg_timings {
 
 const char *fsg_last_error_message(void);
 int fsg_abi_version(void);
+/* the numbers of the last FSG_E_STORE_MEMORY on the calling thread
+ * (EngineError::StoreMemoryExceeded{current, requested, max}) */
+int fsg_last_store_memory(uint64_t *current, uint64_t *requested, uint64_t *max);
 
 /* ---- engine ------------------------------------------------------------ */
 int fsg_device_count(int *count);
@@ -184,10 +193,32 @@ int fsg_chain_output_device(fsg_chain *c, const void **dptr, size_t *len);
 
 /* ---- multi-GPU aggregate state merge (RCCL over xGMI) ------------------- */
 #define FSG_UNIQUE_ID_BYTES 128
+/* element types of aggregate state (sums wrap like the release-mode wasm guest) */
+#define FSG_DTYPE_I32 0
+#define FSG_DTYPE_U32 1
+#define FSG_DTYPE_I64 2
+#define FSG_DTYPE_U64 3
+#define FSG_DTYPE_F64 4
 int fsg_comm_unique_id(uint8_t id[FSG_UNIQUE_ID_BYTES]);
 int fsg_engine_comm_init(fsg_engine *engine, const uint8_t id[FSG_UNIQUE_ID_BYTES], int nranks, int rank);
-/* all-reduce (sum, wrapping i32) of aggregate state in HBM across the engine's communicator */
-int fsg_allreduce_i32(fsg_engine *engine, void *dev_state, size_t count);
+/* all-reduce (sum) of `count` dtype elements of aggregate state in HBM across the
+ * engine's communicator, on the engine's collective stream; returns when done */
+int fsg_allreduce_state(fsg_engine *engine, void *dev_state, size_t count, int dtype);
+/* the same on a chain's stream (ordered after the chain's kernels) */
+int fsg_chain_allreduce_state(fsg_chain *c, void *dev_state, size_t count, int dtype);
+
+/* Per-partition aggregate state vector in HBM (one slot per topic partition;
+ * partitions sharded p -> GPU p mod N).  collect copies a chain's aggregate-sum
+ * accumulator (i32, written by the GPU after every call) into a slot, device to
+ * device; allreduce merges the vectors of all ranks (slots owned by other ranks
+ * are zero locally, so the sum is the topic-wide table). */
+typedef struct fsg_state fsg_state;
+int fsg_state_new(fsg_engine *engine, size_t count, int dtype, fsg_state **out);
+int fsg_state_collect(fsg_state *s, size_t slot, fsg_chain *c);
+int fsg_state_allreduce(fsg_state *s);
+int fsg_state_read(fsg_state *s, void *host, size_t bytes);
+int fsg_state_device(fsg_state *s, void **dptr);
+void fsg_state_free(fsg_state *s);
 
 #ifdef __cplusplus
 }

@@ -1,8 +1,9 @@
 #!/bin/bash
-# Profile several bench workloads on one GPU box: bench line, rocprofv3 kernel
-# stats, PMC FETCH/WRITE passes and one SQ pass per workload.  Every GPU step
-# has its own time limit; the script stops at the first failing step.
-#   usage: scripts/gpu_prof.sh tag "wl1 wl2 ..." [tests]
+# One GPU-box pass: (optional) parity tests, the default bench line (headline +
+# workloads), then per workload a single-workload bench line, rocprofv3 kernel
+# stats, PMC FETCH/WRITE passes and one SQ pass.  Every GPU step has its own
+# time limit; the script stops at the first failing step.
+#   usage: scripts/gpu_prof.sh tag "wl1 wl2 ..." [tests] [full]
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -12,14 +13,17 @@ O=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p "$O"
 step() { echo "$1 rc=$2" >> "$O/steps.log"; [ "$2" -ne 0 ] && exit "$2"; return 0; }
 if [ -n "${3:-}" ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > "$O/gpu_tests.log" 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread > "$O/gpu_tests.log" 2>&1
   step tests $?
 fi
-rocprofv3 -L > "$O/counters.txt" 2>&1 || true
+if [ -n "${4:-}" ]; then
+  timeout -k 10 900 python -u bench.py > "$O/bench_full.log" 2>&1
+  step bench_full $?
+fi
 for WL in $WLS; do
-  timeout -k 10 300 python -u bench.py --workload "$WL" --steps 10 --warmup 2 > "$O/bench_$WL.log" 2>&1
+  timeout -k 10 300 python -u bench.py --workload "$WL" --only --steps 10 --warmup 2 --no-cpu-baseline > "$O/bench_$WL.log" 2>&1
   step "bench_$WL" $?
-  B="python3 $GRAFT_REPO_ROOT/bench.py --workload $WL --steps 5 --warmup 1 --no-cpu-baseline"
+  B="python3 $GRAFT_REPO_ROOT/bench.py --workload $WL --only --steps 5 --warmup 1 --no-cpu-baseline --no-e2e"
   cd /tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt_$WL" -o kt -- $B > "$O/kt_$WL.log" 2>&1
   step "kt_$WL" $?

@@ -3,9 +3,11 @@
 FETCH_SIZE is in KiB and reports half of the bytes of a wide coalesced read on
 gfx950 (x2); WRITE_SIZE is in KiB and exact for 16-B/lane streaming stores.
 
-usage: python scripts/traffic_from_pmc.py <gpurun_out/tag> <workload> [<round tag>]
-Updates profiles/traffic.json[workload] = {kernel: {read, write, total}} that
-bench.py quotes as roofline.traffic (with its source).
+usage: python scripts/traffic_from_pmc.py <pmc dir> <workload> <bench json line file> [<round tag>]
+  <pmc dir> holds fetch_<workload>/ and write_<workload>/ (scripts/gpu_prof.sh)
+Updates profiles/traffic.json[workload] = {kernel: {read, write, total}} plus
+the shape (records, batches) and the libfsg.so content tag it was measured on;
+bench.py quotes it as roofline.traffic only for that same build and shape.
 """
 import collections
 import csv
@@ -28,10 +30,13 @@ def per_kernel(d, counter):
 
 
 def main():
-    d, wl = sys.argv[1], sys.argv[2]
-    tag = sys.argv[3] if len(sys.argv) > 3 else os.path.basename(d.rstrip("/"))
-    fetch = per_kernel(os.path.join(d, "fetch"), "FETCH_SIZE")
-    write = per_kernel(os.path.join(d, "write"), "WRITE_SIZE")
+    d, wl, bj = sys.argv[1], sys.argv[2], sys.argv[3]
+    tag = sys.argv[4] if len(sys.argv) > 4 else os.path.basename(d.rstrip("/"))
+    fetch = per_kernel(os.path.join(d, "fetch_" + wl), "FETCH_SIZE")
+    write = per_kernel(os.path.join(d, "write_" + wl), "WRITE_SIZE")
+    line = json.loads(open(bj).read().strip().splitlines()[-1])
+    sys.path.insert(0, ROOT)
+    import bench
     out = {}
     for k in sorted(set(fetch) | set(write)):
         if "rocclr" in k:
@@ -42,7 +47,8 @@ def main():
     path = os.path.join(ROOT, "profiles", "traffic.json")
     db = json.load(open(path)) if os.path.exists(path) else {}
     db[wl] = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, {tag} (FETCH_SIZE x2 gfx950 correction)",
-              "kernels": out}
+              "kernels": out, "lib": bench.lib_tag(), "n_records": line["config"]["records_per_gpu"],
+              "n_batches": line["config"]["batches_per_gpu"]}
     json.dump(db, open(path, "w"), indent=1, sort_keys=True)
     for k, v in out.items():
         print(f"{k:32s} read {v['read']/1e9:8.3f} GB  write {v['write']/1e9:8.3f} GB")

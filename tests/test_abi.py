@@ -21,7 +21,7 @@ def test_header_declares_the_boundary():
     names = _declared()
     for must in ("fsg_engine_new", "fsg_chain_builder_add_smart_module", "fsg_chain_builder_initialize",
                  "fsg_chain_process", "fsg_chain_process_batch", "fsg_chain_process_slice",
-                 "fsg_allreduce_i32"):
+                 "fsg_allreduce_state", "fsg_state_collect", "fsg_state_allreduce"):
         assert must in names
 
 
@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _ffi.lib().fsg_abi_version() == 1
+    assert _ffi.lib().fsg_abi_version() == 2
 
 
 def test_gfx950_code_object_embedded():

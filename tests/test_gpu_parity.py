@@ -298,12 +298,6 @@ def test_unicode_word_is_loud(engine):
     check_batch(engine, chain, b.encode())
 
 
-def test_store_memory_limit(engine):
-    ch = gpu_chain(engine, CHAINS["filter"], limit=1000)
-    with pytest.raises(StoreMemoryExceeded):
-        ch.process_batch(synth.make_slice(2, 100))
-
-
 def test_resident_slice_matches_process_batch(engine):
     sl = synth.make_slice(2, 4000)
     ch = gpu_chain(engine, CHAINS["filter_then_map"])
@@ -488,10 +482,10 @@ def _check_array_doc(engine, doc):
     sl = _one_record_slice(doc, base=3)
     try:
         check_batch(engine, CHAINS["array_map"], sl)
-    except AssertionError:
+    except AssertionError as e:
         o = orc_chain(CHAINS["array_map"]).process_batch(sl)
         if o["status"] != 0 or o["error"] is not None or not _needs_reorder(doc):
-            raise
+            raise AssertionError(f"doc {doc!r}: {e}") from e
         with pytest.raises(Unsupported):
             gpu_chain(engine, CHAINS["array_map"]).process_batch(sl)
 
@@ -551,3 +545,54 @@ def test_array_map_c4_synthetic(engine):
     out = check_batch(engine, CHAINS["array_map"], sl)
     assert out.n_records > 5 * 20000
     check_batch(engine, CHAINS["array_map"], sl, max_bytes=100000)
+
+
+# ---------------------------------------------------------------------------
+# per-partition aggregate state in HBM + RCCL merge (one rank on this box;
+# the partition sharding / merge logic at world size 2 is tests/test_partitions.py)
+# ---------------------------------------------------------------------------
+def test_partition_state_rccl_one_rank():
+    from fluvio_amd.smartengine import PartitionState, comm_unique_id
+    eng = SmartEngine(0)
+    eng.comm_init(comm_unique_id(), 1, 0)
+    st = PartitionState(eng, 8)
+    expect = []
+    for p in range(8):
+        sl = synth.make_slice(3, 1500 + 200 * p, seed=0xF105 + p)
+        ch = gpu_chain(eng, [("aggregate-sum", {}, b"3" if p == 2 else None)])
+        for _ in range(1 + p % 2):
+            ch.process_batch(sl)
+        st.collect(p, ch)
+        expect.append(int(ch.accumulator(0)))
+        o = orc_chain([("aggregate-sum", {}, b"3" if p == 2 else None)])
+        for _ in range(1 + p % 2):
+            o.process_batch(sl)
+        assert ch.accumulator(0) == o.accumulator(0)
+    st.allreduce()
+    assert st.read() == expect
+    # the raw-pointer entry on the same HBM vector: a second all-reduce over one rank is the identity
+    eng.allreduce_state(st.device_ptr(), 8)
+    assert st.read() == expect
+
+
+def test_store_memory_exceeded_numbers(engine):
+    ch = gpu_chain(engine, CHAINS["filter"], limit=1000)
+    with pytest.raises(StoreMemoryExceeded) as e:
+        ch.process_batch(synth.make_slice(2, 100))
+    assert e.value.max == 1000 and e.value.requested > 1000
+
+
+def test_crc_tables_on_every_device():
+    """Engines on two devices in one process: each device gets its own CRC
+    tables (fsg_kernels.hip upload_crc_tables), so both output CRCs are right."""
+    import ctypes
+    from fluvio_amd import _ffi
+    n = ctypes.c_int(0)
+    _ffi.lib().fsg_device_count(ctypes.byref(n))
+    if n.value < 2:
+        pytest.skip("one GPU on this box")
+    sl = synth.make_slice(2, 500)
+    ref = orc_chain(CHAINS["map"]).process_batch(sl)["bytes"]
+    for d in (0, 1):
+        e = SmartEngine(d)
+        assert gpu_chain(e, CHAINS["map"]).process_batch(sl).raw == ref

@@ -1,0 +1,112 @@
+"""Partition sharding and the aggregate-state merge, CPU only.
+
+The producer's key routing (crates/fluvio/src/producer/partitioning.rs:51-83),
+rank ownership p -> rank p mod N, and the all-reduce merge of per-partition
+aggregate accumulators, run as two gloo ranks on the CPU.  Per-partition states
+come from the CPU oracle (aggregate-sum chains, one per partition, like the
+SPU's per-partition SmartModuleContext, context.rs:25-30); the merged vector
+must equal the single-process table over all partitions.
+"""
+import os
+import socket
+
+import pytest
+
+from fluvio_amd import partitions as PT
+from fluvio_amd import protocol as P
+
+N_PART = 8
+
+
+def test_siphash24_reference_vectors():
+    # SipHash paper, Appendix A (key 00..0f): empty input and the 15-byte 00..0e example
+    k0 = int.from_bytes(bytes(range(8)), "little")
+    k1 = int.from_bytes(bytes(range(8, 16)), "little")
+    assert PT.siphash24(b"", k0, k1) == 0x726FDB47DD0E0E31
+    assert PT.siphash24(bytes(range(15)), k0, k1) == 0xA129CA6149BE45E5
+
+
+def test_round_robin_like_reference():
+    # partitioning.rs:104-121 (test_round_robin_individual)
+    rr = PT.RoundRobin()
+    assert [rr.partition(None, 3) for _ in range(6)] == [0, 1, 2, 0, 1, 2]
+    # keyed records are stable per key, spread over the partitions
+    ps = {PT.partition_siphash(f"key-{i}".encode(), N_PART) for i in range(200)}
+    assert ps == set(range(N_PART))
+    assert PT.partition_siphash(b"abc", 64) == PT.partition_siphash(b"abc", 64)
+
+
+def test_ownership_covers_every_partition_once():
+    for world in (1, 2, 3, 8):
+        seen = sorted(p for r in range(world) for p in PT.owned_partitions(64, world, r))
+        assert seen == list(range(64))
+
+
+def topic_records(n=3000, seed=5):
+    import random
+    rng = random.Random(seed)
+    return [(f"user-{rng.randrange(500)}".encode(), str(rng.randrange(-1000, 1001)).encode()) for _ in range(n)]
+
+
+def partition_slice(recs, base=0):
+    """Stored batches of one partition (~16 KB record sections)."""
+    out, b, off = b"", P.Batch(base_offset=base), base
+    for k, v in recs:
+        b.add_record(P.Record.new_key_value(k, v))
+        if len(b.records) == 200:
+            out += b.encode()
+            off += len(b.records)
+            b = P.Batch(base_offset=off)
+    if b.records:
+        out += b.encode()
+    return out
+
+
+def partition_states(owned, routed):
+    from oracle.oracle import OracleChain
+    states = {}
+    for p in owned:
+        ch = OracleChain([("aggregate-sum", {}, None)])
+        r = ch.process_batch(partition_slice(routed[p]))
+        assert r["status"] == 0 and r["error"] is None
+        acc = ch.accumulator(0)
+        states[p] = int(acc) if acc else 0
+    return states
+
+
+def _rank_main(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    routed = PT.route(topic_records(), N_PART, key_of=lambda r: r[0])
+    owned = PT.owned_partitions(N_PART, world, rank)
+    vec = PT.local_state_vector(N_PART, partition_states(owned, routed))
+    merged = PT.merge_states_torch(vec)
+    with open(os.path.join(outdir, f"rank{rank}.txt"), "w") as f:
+        f.write(" ".join(map(str, merged)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(180)
+def test_two_rank_state_merge(tmp_path):
+    import torch.multiprocessing as mp
+    world = 2
+    mp.spawn(_rank_main, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    routed = PT.route(topic_records(), N_PART, key_of=lambda r: r[0])
+    expect = PT.local_state_vector(N_PART, partition_states(range(N_PART), routed))
+    assert any(expect)
+    for r in range(world):
+        got = [int(x) for x in open(tmp_path / f"rank{r}.txt").read().split()]
+        assert got == expect
+    # each partition's state is the running i32 sum of its own records only
+    for p in range(N_PART):
+        assert expect[p] == PT.wrap_i32(sum(int(v) for _, v in routed[p]))
