@@ -71,7 +71,14 @@ struct DfaDesc {
   uint32_t f_trans;    // blob offset: u16[f_nstates * f_nclasses]
   uint32_t f_accept;   // blob offset: u8[f_nstates]
   uint32_t unicode_word;
-  uint32_t pad;
+  // register-resident form for the lean kernel (ASCII DFA with <= 16 states):
+  // tt[b] = the row of byte b, next state of s in bits [4s, 4s+4); acc1/acc2 =
+  // states with accept bit0 / bit1
+  uint32_t lean;       // 1: tt / tt_up / acc1 / acc2 are valid
+  uint32_t tt;         // blob offset: u64[256]
+  uint32_t tt_up;      // blob offset: u64[256], rows of toupper(byte)
+  uint32_t acc1;
+  uint32_t acc2;
 };
 
 struct StageDesc {

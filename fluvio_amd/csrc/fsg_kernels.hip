@@ -1222,6 +1222,7 @@ struct __attribute__((aligned(16))) LeanLds {
   uint32_t match[2];
   uint32_t chase_bad;
   uint32_t pad;
+  uint64_t tt[256];                 // the scanned regex stage's byte rows (DfaDesc::tt)
   uint8_t needle[kLeanNeedle + 8];  // the scanned stage's needle
   uint8_t blk[kLeanBlk + 1];        // blk[j] = last record whose value starts <= 64 j (0xFF none)
 };
@@ -1368,6 +1369,55 @@ __device__ __forceinline__ uint32_t lean_scan(LeanLds& L, int nr, uint32_t lo, u
   return acc;
 }
 
+// One bounded-length regex stage over the value bytes [lo, hi) (regex-filter /
+// filter_regex with a <= 16-state ASCII DFA, smartmodule/regex-filter/src/lib.rs:
+// 24-28): the range is cut into one piece per thread; a thread runs the DFA
+// over its piece plus max_len - 1 bytes of overlap, so every match starting
+// in the piece ends inside the scan.  The DFA is register resident: the
+// state is 4 bits, one LDS read of tt[byte] gives the byte's whole row.
+// A value piece starts in s_bot at the value start and in s_mid elsewhere
+// (unanchored restart); accept bit0 is sticky (the DFA stays in an accepting
+// state), bit1 is checked where a value ends (`$`).  Returns the OR of every
+// scanned byte (bit 7 set <=> a non-ASCII value byte).
+__device__ __forceinline__ uint32_t lean_regex(LeanLds& L, int nr, uint32_t lo, uint32_t hi, uint32_t mlen,
+                                               uint32_t s_bot, uint32_t s_mid, uint32_t acc1, uint32_t acc2) {
+  const uint32_t l = threadIdx.x;
+  const uint32_t q_len = (hi - lo + kLeanThreads - 1) / kLeanThreads;
+  const uint32_t p0 = lo + l * q_len;
+  uint32_t orw = 0;
+  uint64_t mask = 0;
+  if (q_len && p0 < hi) {
+    const uint32_t p1 = p0 + q_len < hi ? p0 + q_len : hi;
+    const uint32_t pe = p1 + mlen - (mlen ? 1u : 0u);
+    const uint32_t pend = pe < hi ? pe : hi;
+    int r = lean_rec_of(L, nr, p0);
+    if (r < 0) r = 0;
+    for (; r < nr; r++) {
+      const uint32_t vs = L.r_vs[r], ve = L.r_ve[r];
+      if (vs >= p1) break;
+      uint32_t q = vs > p0 ? vs : p0;
+      if (q >= ve) continue;
+      uint32_t st = q == vs ? s_bot : s_mid;
+      const uint32_t end = ve < pend ? ve : pend;
+      while (q < end) {
+        const uint32_t w = lds_u32_at(L.win, q);
+        const uint32_t n = end - q < 4u ? end - q : 4u;
+        orw |= n == 4 ? w : (w & ((1u << (8 * n)) - 1u));
+        for (uint32_t k = 0; k < n; k++) st = (uint32_t)(L.tt[(w >> (8 * k)) & 0xFFu] >> (4 * st)) & 15u;
+        q += n;
+      }
+      if (((acc1 >> st) & 1u) || (end == ve && ((acc2 >> st) & 1u))) mask |= 1ull << r;
+    }
+  }
+  // empty values: decided by the start state alone
+  if ((int)l < nr && L.r_vs[l] == L.r_ve[l] && (((acc1 | acc2) >> s_bot) & 1u)) mask |= 1ull << l;
+  if (mask) {
+    atomicOr(&L.match[0], (uint32_t)mask);
+    atomicOr(&L.match[1], (uint32_t)(mask >> 32));
+  }
+  return orw;
+}
+
 __global__ __launch_bounds__(kLeanThreads) void k_eval_lean(EvalArgs a) {
   __shared__ LeanLds L;
   const uint32_t b = blockIdx.x;
@@ -1472,9 +1522,10 @@ __global__ __launch_bounds__(kLeanThreads) void k_eval_lean(EvalArgs a) {
   bool checked = false;
   for (uint32_t s = 0; !defer && s < ch.nstages; s++) {
     const StageDesc& sd = ch.st[s];
-    if (sd.op != OP_CONTAINS) continue;  // OP_MAP_UPPER: representation only
+    if (sd.op == OP_MAP_UPPER) continue;  // representation only
+    const bool rx = sd.op == OP_REGEX;
     const uint32_t m = sd.needle_len;
-    if (m == 0 && checked) continue;     // an empty needle keeps every (UTF-8) value
+    if (!rx && m == 0 && checked) continue;  // an empty needle keeps every (UTF-8) value
     if (nr == 0) break;
     const uint32_t lo = L.r_vs[0], hi = L.r_ve[nr - 1];
     if (!checked) {
@@ -1492,11 +1543,26 @@ __global__ __launch_bounds__(kLeanThreads) void k_eval_lean(EvalArgs a) {
       if (l == 0)
         for (uint32_t j = 0; (j << 6) < lo; j++) L.blk[j] = 0xFF;
     }
-    const uint8_t* nd = a.blob + sd.needle;
     if (l == 0) {
       L.match[0] = 0;
       L.match[1] = 0;
     }
+    if (rx) {
+      const bool upper = sd.in_type == VT_SRC_UPPER;
+      const uint64_t* tt = (const uint64_t*)(a.blob + (upper ? sd.dfa.tt_up : sd.dfa.tt));
+      for (uint32_t t = l; t < 256; t += kLeanThreads) L.tt[t] = tt[t];
+      __syncthreads();
+      const uint32_t orw = lean_regex(L, nr, lo, hi, (uint32_t)sd.dfa.max_len, sd.dfa.s_bot, sd.dfa.s_mid,
+                                      sd.dfa.acc1, sd.dfa.acc2);
+      const bool high = __syncthreads_or((orw & 0x80808080u) != 0u);  // also orders the match bits
+      if (!checked && high) defer = true;  // a non-ASCII value: exact UTF-8 / Unicode DFA path
+      checked = true;
+      const bool hit = l < 64 && ((L.match[(l >> 5) & 1] >> (l & 31)) & 1u);
+      alive &= __ballot(sd.keep_match ? hit : !hit);
+      __syncthreads();  // match / tt are rewritten by the next stage
+      continue;
+    }
+    const uint8_t* nd = a.blob + sd.needle;
     if (m > (uint32_t)kLeanNeedle) {
       defer = true;  // long needle: exact kernel
       break;
@@ -1513,6 +1579,7 @@ __global__ __launch_bounds__(kLeanThreads) void k_eval_lean(EvalArgs a) {
     if (!checked && high) defer = true;  // a non-ASCII value: exact UTF-8 path
     checked = true;
     if (m > 0) alive &= __ballot(l < 64 && ((L.match[(l >> 5) & 1] >> (l & 31)) & 1u));
+    __syncthreads();  // match / needle are rewritten by the next stage
   }
   if (defer) {
     if (l == 0) {

@@ -375,6 +375,21 @@ int add_stage(fsg_chain* c, const ModuleSpec& m, const std::string& name, uint8_
     sd.dfa.f_classmap_up = put_blob(fd.classmap_up.data(), 256);
     sd.dfa.f_trans = put_blob(fd.trans.data(), fd.trans.size() * 2);
     sd.dfa.f_accept = put_blob(fd.accept.data(), fd.accept.size());
+    if (d.nstates <= 16) {  // the lean kernel's byte-row tables (fsg_device.h DfaDesc)
+      std::vector<uint64_t> tt(256, 0), ttu(256, 0);
+      for (uint32_t b = 0; b < 256; b++)
+        for (uint32_t st = 0; st < d.nstates; st++) {
+          tt[b] |= (uint64_t)d.trans[st * d.nclasses + d.classmap[b]] << (4 * st);
+          ttu[b] |= (uint64_t)d.trans[st * d.nclasses + d.classmap_up[b]] << (4 * st);
+        }
+      sd.dfa.tt = put_blob(tt.data(), tt.size() * 8);
+      sd.dfa.tt_up = put_blob(ttu.data(), ttu.size() * 8);
+      for (uint32_t st = 0; st < d.nstates; st++) {
+        if (d.accept[st] & 1) sd.dfa.acc1 |= 1u << st;
+        if (d.accept[st] & 2) sd.dfa.acc2 |= 1u << st;
+      }
+      sd.dfa.lean = d.max_len >= 0 ? 1 : 0;
+    }
   } else if (name == "filter_json") {  // examples/filter_json: StructuredLog.level > Debug
     sd.op = OP_FILTER_JSON;
     sd.kind = FSG_KIND_FILTER;
@@ -832,10 +847,17 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   ea.list = c->defer.as<uint32_t>();
   ea.elem = has_array ? c->elem.as<ElemRec>() : nullptr;
   uint32_t ops = 0;
-  for (uint32_t k = 0; k < c->hdesc.nstages; k++) ops |= 1u << c->hdesc.st[k].op;
-  // substring filters + uppercase maps: the one-wave lean kernel first, the
-  // batches it defers then go through the exact kernel (list mode)
-  const bool lean = (ops & ~((1u << OP_CONTAINS) | (1u << OP_MAP_UPPER))) == 0 && !has_agg;
+  bool lean_stages = true;  // every stage has a lean form
+  for (uint32_t k = 0; k < c->hdesc.nstages; k++) {
+    const StageDesc& sd = c->hdesc.st[k];
+    ops |= 1u << sd.op;
+    if (sd.op == OP_CONTAINS && sd.needle_len > 128) lean_stages = false;  // kLeanNeedle
+    if (sd.op == OP_REGEX && !sd.dfa.lean) lean_stages = false;
+  }
+  // substring / bounded regex filters + uppercase maps: the lean kernel first,
+  // the batches it defers then go through the exact kernel (list mode)
+  const bool lean =
+      (ops & ~((1u << OP_CONTAINS) | (1u << OP_MAP_UPPER) | (1u << OP_REGEX))) == 0 && !has_agg && lean_stages;
   if (lean) HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
   launch_eval(ea, ops, lean, st);
   HIPCHK(hipGetLastError());

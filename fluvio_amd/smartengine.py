@@ -421,7 +421,12 @@ class SmartModuleChainInstance:
     def _batch_result(self, out) -> BatchOutput:
         try:
             o = out.contents
-            raw = ctypes.string_at(o.batch, o.batch_len)
+            n = o.batch_len
+            if n < (1 << 31):
+                raw = ctypes.string_at(o.batch, n)
+            else:  # string_at takes a C int size
+                raw = bytearray(n)
+                ctypes.memmove((ctypes.c_char * n).from_buffer(raw), o.batch, n)
             err = _runtime_error(o.error) if o.has_error else None
             return BatchOutput(raw, o.base_offset, o.last_offset_delta, o.n_records, err)
         finally:

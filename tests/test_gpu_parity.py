@@ -419,6 +419,15 @@ def _lean_slice(seed=7, nbatches=40):
     [("filter_init", {"key": "out"}, None), ("map", {}, None), ("filter_init", {"key": "TIME"}, None)],
     [("map", {}, None)],
     [],
+    [("regex-filter", {"regex": r"ti.e"}, None)],                        # lean regex: <= 16-state DFA
+    [("regex-filter", {"regex": r"^(time|level)"}, None)],
+    [("regex-filter", {"regex": r"out$|^a"}, None)],
+    [("regex-filter", {"regex": r"^$"}, None)],                           # empty values only
+    [("regex-filter", {"regex": r"(a|b)?"}, None)],                       # matches the empty string
+    [("filter_regex", {}, None)],
+    [("map", {}, None), ("regex-filter", {"regex": r"TI[M]E"}, None)],   # upper-cased rows
+    [("filter_init", {"key": "o"}, None), ("regex-filter", {"regex": r"t\w{2}e"}, None)],
+    [("regex-filter", {"regex": r"[a-z]{2}\d"}, None), ("filter_init", {"key": "out"}, None)],
 ])
 def test_lean_path_parity(engine, chain):
     check_batch(engine, chain, _lean_slice())
