@@ -18,9 +18,11 @@
 #include <hip/hip_runtime.h>
 
 #include <mutex>
+#include <type_traits>
 
 #include "fsg_device.h"
 #include "fsg_json_dev.h"
+#include "fsg_json_dfa.h"
 
 namespace fsg {
 
@@ -230,6 +232,9 @@ constexpr uint32_t opbit(int op) { return 1u << op; }
 constexpr uint32_t kOpsContains = opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
 constexpr uint32_t kOpsRegex = opbit(OP_REGEX) | opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
 constexpr uint32_t kOpsJson = opbit(OP_FILTER_JSON) | opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
+constexpr uint32_t kOpsArray = opbit(OP_ARRAY_MAP) | opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
+constexpr uint32_t kOpsInt = opbit(OP_FILTER_ODD) | opbit(OP_MAP_DOUBLE) | opbit(OP_FILTER_MAP) | opbit(OP_AGG_SUM) |
+                             opbit(OP_AGG_CONCAT) | opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
 constexpr uint32_t kOpsAll = 0x3FFu;
 constexpr int kDfaDyn = 768 + kDfaLds;  // dynamic LDS of a chain with a regex stage
 extern __shared__ __attribute__((aligned(16))) uint8_t g_dyn_lds[];
@@ -1226,6 +1231,18 @@ struct __attribute__((aligned(16))) LeanLds {
   uint8_t needle[kLeanNeedle + 8];  // the scanned stage's needle
   uint8_t blk[kLeanBlk + 1];        // blk[j] = last record whose value starts <= 64 j (0xFF none)
 };
+// the filter_json variant: per-chunk quote / in-string masks, the token list,
+// the token DFA (fsg_json_dfa.h)
+constexpr int kJsonChunks = (kLeanWin + 48) / 16 + 2;
+constexpr int kJsonEnt = 2048;  // token entries per batch (more: exact kernel)
+__device__ constexpr JsonDfaTables g_json_tables{};
+struct __attribute__((aligned(16))) LeanLdsJ : LeanLds {
+  uint32_t jm[kJsonChunks];      // quote16 | in-string16 << 16 (in-string: exclusive, batch-global parity)
+  uint32_t ent[kJsonEnt];        // pos | byte << 16 | token class << 24
+  uint32_t wsum[4];              // cross-wave scan carries
+  uint8_t dfa[kJsonStates * kJsonCls2];
+  uint8_t bcls[256];
+};
 
 __device__ __forceinline__ uint32_t win5(const uint32_t (&w)[5], int j) {
   const int k = j >> 2, al = j & 3;
@@ -1418,8 +1435,198 @@ __device__ __forceinline__ uint32_t lean_regex(LeanLds& L, int nr, uint32_t lo, 
   return orw;
 }
 
+// 4 bits: which of the 4 bytes of a SWAR mask word carry 0x80
+__device__ __forceinline__ uint32_t nib4(uint32_t m80) { return ((((m80 >> 7) & 0x01010101u) * 0x01020408u) >> 24) & 15u; }
+// 16-bit masks of one 16-byte chunk: bytes == c
+__device__ __forceinline__ uint32_t eq16(const uint4& v, uint32_t c4) {
+  return nib4(zbytes(v.x ^ c4)) | (nib4(zbytes(v.y ^ c4)) << 4) | (nib4(zbytes(v.z ^ c4)) << 8) |
+         (nib4(zbytes(v.w ^ c4)) << 12);
+}
+// bytes < 0x20, == '\\' or >= 0x80: anything the fast JSON path does not decide
+__device__ __forceinline__ uint32_t special16(const uint4& v) {
+  auto one = [](uint32_t w) {
+    return nib4(zbytes(w & 0xE0E0E0E0u) | zbytes(w ^ 0x5C5C5C5Cu) | (w & 0x80808080u));
+  };
+  return one(v.x) | (one(v.y) << 4) | (one(v.z) << 8) | (one(v.w) << 12);
+}
+template <typename LdsT>
+__device__ __forceinline__ bool lds_eq(const LdsT& L, uint32_t p, uint32_t n, const char* s, uint32_t sn) {
+  if (n != sn) return false;
+  for (uint32_t k = 0; k < n; k++)
+    if (L.win[p + k] != (uint8_t)s[k]) return false;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// filter_json in the lean kernel (smartmodule/examples/filter_json/src/lib.rs:
+// 54-70, serde_json::from_slice::<StructuredLog>), data-parallel:
+//   1. byte classes of every 16-byte chunk of the batch's values (quotes,
+//      spaces, "special" bytes: < 0x20, '\\', >= 0x80), one chunk per lane;
+//      the in-string mask from a prefix XOR of the quotes carried across the
+//      whole batch (a workgroup XOR scan)
+//   2. the token list: every quote, special byte and non-space byte outside
+//      strings, in order (workgroup prefix sum); opening quotes carry the class
+//      of their string ("level", "message", a LogLevel variant, other)
+//   3. one thread per record runs the table-driven token DFA of fsg_json_dfa.h
+//      over its tokens.  The DFA accepts exactly the flat objects whose
+//      outcome is certain: ASCII, no escapes / control bytes, level a variant
+//      string, message a string, other values strings / JSON numbers /
+//      literals, each field once.  Any other record (and any record starting
+//      inside an unbalanced string) sends the batch to the exact kernel.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t zero16(const uint4& v) {
+  return nib4(zbytes(v.x)) | (nib4(zbytes(v.y)) << 4) | (nib4(zbytes(v.z)) << 8) | (nib4(zbytes(v.w)) << 12);
+}
+__device__ __forceinline__ uint32_t pxor16(uint32_t q) {  // inclusive prefix XOR of 16 bits
+  uint32_t px = q ^ (q << 1);
+  px ^= px << 2;
+  px ^= px << 4;
+  px ^= px << 8;
+  return px & 0xFFFFu;
+}
+// workgroup (128 threads) exclusive prefix of v; returns the exclusive value, *total
+__device__ __forceinline__ uint32_t wg_excl_sum(uint32_t v, uint32_t* wsum, uint32_t* total) {
+  const uint32_t l = threadIdx.x, lane = l & 63u, w = l >> 6;
+  const uint32_t incl = wave_incl_scan(v);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  const uint32_t w0 = wsum[0];
+  *total = w0 + wsum[1];
+  __syncthreads();
+  return incl - v + (w ? w0 : 0u);
+}
+template <typename LdsT>
+__device__ __forceinline__ uint32_t json_str_class(const LdsT& L, uint32_t a, uint32_t n) {
+  auto eq = [&](const char* t, uint32_t tn) {
+    if (n != tn) return false;
+    for (uint32_t k = 0; k < n; k++)
+      if (L.win[a + k] != (uint8_t)t[k]) return false;
+    return true;
+  };
+  return eq("level", 5) ? JC_Q_LEVEL : eq("message", 7) ? JC_Q_MSG : eq("debug", 5) ? JC_Q_DEBUG
+       : eq("info", 4) ? JC_Q_INFO : eq("warn", 4) ? JC_Q_WARN : eq("error", 5) ? JC_Q_ERROR : JC_Q_OTHER;
+}
+// stages 1-3 for the records [0, nr); returns true if the batch must go to the
+// exact kernel; match bits of records whose level > Debug in L.match
+__device__ bool lean_json_stage(LeanLdsJ& L, int nr) {
+  const uint32_t l = threadIdx.x;
+  const uint32_t c0 = L.r_vs[0] & ~15u, c1 = L.r_ve[nr - 1];
+  const uint32_t nch = (c1 - c0 + 15) >> 4;
+  if (nch > (uint32_t)kJsonChunks) return true;
+  // 1. masks; thread t owns the contiguous chunks [t*per, (t+1)*per)
+  const uint32_t per = (nch + kLeanThreads - 1) / kLeanThreads;
+  const uint32_t k0 = l * per, k1 = k0 + per < nch ? k0 + per : nch;
+  uint32_t par = 0;
+  for (uint32_t k = k0; k < k1; k++) {
+    const uint4 v = *(const uint4*)(&L.win[c0 + 16 * k]);
+    const uint32_t q = eq16(v, 0x22222222u);
+    L.jm[k] = q;
+    par ^= __builtin_popcount(q) & 1u;
+  }
+  uint32_t tot;
+  uint32_t carry = wg_excl_sum(par, L.wsum, &tot) & 1u;  // parity of all quotes before my chunks
+  uint32_t cnt = 0;
+  for (uint32_t k = k0; k < k1; k++) {
+    const uint4 v = *(const uint4*)(&L.win[c0 + 16 * k]);
+    const uint32_t q = L.jm[k];
+    const uint32_t instr = (pxor16(q) ^ q ^ (carry ? 0xFFFFu : 0u)) & 0xFFFFu;
+    carry ^= __builtin_popcount(q) & 1u;
+    L.jm[k] = q | (instr << 16);
+    const uint32_t hot = q | special16(v) | zero16(v) | (~eq16(v, 0x20202020u) & ~instr & 0xFFFFu);
+    cnt += __builtin_popcount(hot);
+  }
+  // 2. token list
+  uint32_t ntok;
+  uint32_t e = wg_excl_sum(cnt, L.wsum, &ntok);
+  if (ntok > (uint32_t)kJsonEnt) return true;  // uniform: every thread saw the same total
+  for (uint32_t k = k0; k < k1; k++) {
+    const uint4 v = *(const uint4*)(&L.win[c0 + 16 * k]);
+    const uint32_t q = L.jm[k] & 0xFFFFu, instr = L.jm[k] >> 16;
+    uint32_t hot = q | special16(v) | zero16(v) | (~eq16(v, 0x20202020u) & ~instr & 0xFFFFu);
+    while (hot) {
+      const uint32_t j = (uint32_t)__builtin_ctz(hot);
+      hot &= hot - 1;
+      const uint32_t pos = c0 + 16 * k + j;
+      const uint32_t b = L.win[pos];
+      uint32_t cls = L.bcls[b];
+      if (b == '"') cls = ((instr >> j) & 1u) ? (uint32_t)JC_Q_CLOSE : (uint32_t)JC_Q_OTHER;
+      L.ent[e++] = pos | (b << 16) | (cls << 24);
+    }
+  }
+  __syncthreads();
+  // string classes of the opening quotes (the next token closes the string)
+  for (uint32_t t = l; t + 1 < ntok; t += kLeanThreads) {
+    const uint32_t en = L.ent[t];
+    if ((en >> 24) != JC_Q_OTHER) continue;
+    const uint32_t nx = L.ent[t + 1];
+    if ((nx >> 24) != JC_Q_CLOSE) continue;
+    const uint32_t a = (en & 0xFFFFu) + 1, n = (nx & 0xFFFFu) - a;
+    L.ent[t] = (en & 0x00FFFFFFu) | (json_str_class(L, a, n) << 24);
+  }
+  __syncthreads();
+  // 3. one thread per record, records spread over both waves
+  const uint32_t r = 2 * (l & 63u) + (l >> 6);
+  bool bad = false;
+  if ((int)r < nr) {
+    const uint32_t vs = L.r_vs[r], ve = L.r_ve[r];
+    // the record must start and end outside strings (balanced quotes before it)
+    auto instr_at = [&](uint32_t p) {
+      const uint32_t k = (p - c0) >> 4, j = (p - c0) & 15u;
+      if (k >= nch) return 0u;
+      return (L.jm[k] >> (16 + j)) & 1u;
+    };
+    if (instr_at(vs) || instr_at(ve)) bad = true;
+    // the record's tokens [t0, t1): binary search on positions
+    uint32_t lo = 0, hi = ntok;
+    while (lo < hi) {
+      const uint32_t m = (lo + hi) >> 1;
+      if ((L.ent[m] & 0xFFFFu) < vs) lo = m + 1; else hi = m;
+    }
+    uint32_t t = lo;
+    uint32_t st = JS_OBJ, prev = 0xFFFFu, flags = 0;
+    int lvl = -1;
+    for (; !bad && t < ntok; t++) {
+      const uint32_t en = L.ent[t];
+      const uint32_t pos = en & 0xFFFFu;
+      if (pos >= ve) break;
+      const uint32_t cls = en >> 24;
+      const uint32_t adj = pos == prev + 1 ? 1u : 0u;
+      prev = pos;
+      if (st >= JS_INV_D && st <= JS_INV_E) lvl = (int)(st - JS_INV_D);
+      st = L.dfa[st * kJsonCls2 + cls * 2 + adj];
+      // each field at most once (serde derive: duplicate field is an error)
+      const uint32_t fb = st == JS_INKEY_LV ? 1u : st == JS_INKEY_MSG ? 2u : 0u;
+      if (flags & fb) st = JS_FAIL;
+      flags |= fb;
+    }
+    if (st != JS_END || flags != 3u) bad = true;
+    if (!bad && lvl > 0) atomicOr(&L.match[r >> 5], 1u << (r & 31));
+  }
+  return __syncthreads_or(bad);
+}
+
+// zero every byte between values (record headers, keys, lengths) and build the
+// 64-byte block -> record table; thread l < nr owns record l (value [vs, vs+vl))
+__device__ __forceinline__ void clear_gaps(LeanLds& L, int nr, uint32_t vs, uint32_t vl) {
+  const uint32_t l = threadIdx.x;
+  const uint32_t lo = L.r_vs[0], hi = L.r_ve[nr - 1];
+  if ((int)l < nr) {
+    const uint32_t e = (int)l + 1 < nr ? L.r_vs[l + 1] : ((vs + vl + 15) & ~15u) + 16;
+    for (uint32_t p = vs + vl; p < e; p++) L.win[p] = 0;
+  }
+  if (l == 0)
+    for (uint32_t p = lo & ~15u; p < lo; p++) L.win[p] = 0;
+  if ((int)l < nr) {
+    const uint32_t e = (int)l + 1 < nr ? L.r_vs[l + 1] : hi + 80;
+    for (uint32_t j = (vs + 63) >> 6; (j << 6) < e; j++) L.blk[j] = (uint8_t)l;
+  }
+  if (l == 0)
+    for (uint32_t j = 0; (j << 6) < lo; j++) L.blk[j] = 0xFF;
+}
+
+template <bool kJson>
 __global__ __launch_bounds__(kLeanThreads) void k_eval_lean(EvalArgs a) {
-  __shared__ LeanLds L;
+  __shared__ typename std::conditional<kJson, LeanLdsJ, LeanLds>::type L;
   const uint32_t b = blockIdx.x;
   const uint32_t l = threadIdx.x;
   const ChainDesc& ch = *a.chain;
@@ -1519,29 +1726,39 @@ __global__ __launch_bounds__(kLeanThreads) void k_eval_lean(EvalArgs a) {
   // 3. stages.  Before the first scan every non-value byte of the scanned
   //    range is cleared (record headers, keys, lengths): then the OR of the
   //    scanned words has a high bit iff some value is non-ASCII.
-  bool checked = false;
+  bool checked = false;  // every value known ASCII (from_utf8 cannot fail)
+  bool cleared = false;  // gap bytes zeroed, record block table built
   for (uint32_t s = 0; !defer && s < ch.nstages; s++) {
     const StageDesc& sd = ch.st[s];
     if (sd.op == OP_MAP_UPPER) continue;  // representation only
+    if constexpr (kJson) if (sd.op == OP_FILTER_JSON) {
+      if (l == 0) {
+        L.match[0] = 0;
+        L.match[1] = 0;
+      }
+      for (uint32_t t = l; t < (uint32_t)(kJsonStates * kJsonCls2); t += kLeanThreads) L.dfa[t] = g_json_tables.t[t];
+      for (uint32_t t = l; t < 256; t += kLeanThreads) L.bcls[t] = g_json_tables.bcls[t];
+      if (!cleared && nr > 0) {
+        clear_gaps(L, nr, vs, vl);
+        cleared = true;
+      }
+      __syncthreads();
+      if (nr > 0 && lean_json_stage(L, nr)) {
+        defer = true;
+        break;
+      }
+      alive &= __ballot(l < 64 && ((L.match[(l >> 5) & 1] >> (l & 31)) & 1u));
+      __syncthreads();
+      continue;
+    }
     const bool rx = sd.op == OP_REGEX;
     const uint32_t m = sd.needle_len;
     if (!rx && m == 0 && checked) continue;  // an empty needle keeps every (UTF-8) value
     if (nr == 0) break;
     const uint32_t lo = L.r_vs[0], hi = L.r_ve[nr - 1];
-    if (!checked) {
-      if ((int)l < nr) {
-        const uint32_t e = (int)l + 1 < nr ? L.r_vs[l + 1] : ((vs + vl + 15) & ~15u) + 16;
-        for (uint32_t p = vs + vl; p < e; p++) L.win[p] = 0;
-      }
-      if (l == 0)
-        for (uint32_t p = lo & ~15u; p < lo; p++) L.win[p] = 0;
-      // record lookup table over 64-byte blocks
-      if ((int)l < nr) {
-        const uint32_t e = (int)l + 1 < nr ? L.r_vs[l + 1] : hi + 80;
-        for (uint32_t j = (vs + 63) >> 6; (j << 6) < e; j++) L.blk[j] = (uint8_t)l;
-      }
-      if (l == 0)
-        for (uint32_t j = 0; (j << 6) < lo; j++) L.blk[j] = 0xFF;
+    if (!cleared) {
+      clear_gaps(L, nr, vs, vl);
+      cleared = true;
     }
     if (l == 0) {
       L.match[0] = 0;
@@ -2495,7 +2712,11 @@ void launch_eval(const EvalArgs& a, uint32_t ops, bool lean, hipStream_t s) {
   EvalArgs e = a;
   uint32_t grid = a.nbatches;
   if (lean) {
-    hipLaunchKernelGGL(k_eval_lean, dim3(a.nbatches), dim3(kLeanThreads), 0, s, a);
+    // the JSON stage's exact fallback costs registers: its own variant
+    if (ops & opbit(OP_FILTER_JSON))
+      hipLaunchKernelGGL(k_eval_lean<true>, dim3(a.nbatches), dim3(kLeanThreads), 0, s, a);
+    else
+      hipLaunchKernelGGL(k_eval_lean<false>, dim3(a.nbatches), dim3(kLeanThreads), 0, s, a);
     grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list
   } else {
     e.list = nullptr;
@@ -2506,6 +2727,10 @@ void launch_eval(const EvalArgs& a, uint32_t ops, bool lean, hipStream_t s) {
     hipLaunchKernelGGL(k_eval<kOpsRegex>, dim3(grid), dim3(kEvalThreads), dyn, s, e);
   else if ((ops & ~kOpsJson) == 0)
     hipLaunchKernelGGL(k_eval<kOpsJson>, dim3(grid), dim3(kEvalThreads), dyn, s, e);
+  else if ((ops & ~kOpsArray) == 0)
+    hipLaunchKernelGGL(k_eval<kOpsArray>, dim3(grid), dim3(kEvalThreads), dyn, s, e);
+  else if ((ops & ~kOpsInt) == 0)
+    hipLaunchKernelGGL(k_eval<kOpsInt>, dim3(grid), dim3(kEvalThreads), dyn, s, e);
   else
     hipLaunchKernelGGL(k_eval<kOpsAll>, dim3(grid), dim3(kEvalThreads), dyn, s, e);
 }

@@ -853,11 +853,13 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     ops |= 1u << sd.op;
     if (sd.op == OP_CONTAINS && sd.needle_len > 128) lean_stages = false;  // kLeanNeedle
     if (sd.op == OP_REGEX && !sd.dfa.lean) lean_stages = false;
+    if (sd.op == OP_FILTER_JSON && sd.in_type != VT_SRC) lean_stages = false;
   }
   // substring / bounded regex filters + uppercase maps: the lean kernel first,
   // the batches it defers then go through the exact kernel (list mode)
-  const bool lean =
-      (ops & ~((1u << OP_CONTAINS) | (1u << OP_MAP_UPPER) | (1u << OP_REGEX))) == 0 && !has_agg && lean_stages;
+  const bool lean = (ops & ~((1u << OP_CONTAINS) | (1u << OP_MAP_UPPER) | (1u << OP_REGEX) |
+                             (1u << OP_FILTER_JSON))) == 0 &&
+                    !has_agg && lean_stages;
   if (lean) HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
   launch_eval(ea, ops, lean, st);
   HIPCHK(hipGetLastError());

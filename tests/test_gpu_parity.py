@@ -176,6 +176,8 @@ CHAINS = {
     "filter_json_then_map": [("filter_json", {}, None), ("map", {}, None)],
     "map_then_filter_json": [("map", {}, None), ("filter_json", {}, None)],
     "double_then_filter_json": [("map_double", {}, None), ("filter_json", {}, None)],
+    "filter_json_then_filter": [("filter_json", {}, None), ("filter_init", {"key": "timeout"}, None)],
+    "filter_then_filter_json": [("filter_init", {"key": "a"}, None), ("filter_json", {}, None)],
     "filter_then_map": [("filter_init", {"key": "timeout"}, None), ("map", {}, None)],
     "map_then_filter": [("map", {}, None), ("filter_init", {"key": "TIMEOUT"}, None)],
     "map_then_lower_filter": [("map", {}, None), ("filter_init", {"key": "timeout"}, None)],
@@ -361,9 +363,33 @@ def test_filter_json_first_error_in_stream(engine):
             b.add_record(P.Record.new(v))
         sl += b.encode()
         base += 10
-    for chain in ("filter_json", "filter_json_then_map", "map_then_filter_json"):
+    for chain in ("filter_json", "filter_json_then_map", "map_then_filter_json", "filter_json_then_filter",
+                  "filter_then_filter_json"):
         check_batch(engine, CHAINS[chain], sl)
         check_batch(engine, CHAINS[chain], sl, max_bytes=20000)
+
+
+def test_filter_json_lean_batches(engine):
+    """Batches of 1..64 records mixing documents the fast path decides, ones only
+    the exact restatement decides (escapes, nesting, whitespace, non-ASCII,
+    enum maps) and ones that fail: every batch bit-exact with the oracle."""
+    from tests import jsongen
+    import random
+    rng = random.Random(3)
+    docs = jsongen.corpus(13, 300, 120)
+    simple = [b'{"level":"%s","message":"m %d","n":-1.5e3,"t":true,"z":null,"s":"x"}' % (
+        rng.choice(jsongen.LEVELS).encode(), i) for i in range(200)]
+    sl, base = b"", 0
+    for k in range(60):
+        b = P.Batch(base_offset=base)
+        n = rng.choice([1, 7, 15, 40, 64])
+        for j in range(n):
+            pool = simple if k % 3 else docs
+            b.add_record(P.Record.new(rng.choice(pool)))
+        sl += b.encode()
+        base += n
+    for chain in ("filter_json", "filter_json_then_filter", "filter_then_filter_json"):
+        check_batch(engine, CHAINS[chain], sl)
 
 
 def test_filter_json_synthetic_logs(engine):

@@ -169,3 +169,54 @@ def test_array_map_oracle_errors_and_floats():
             assert " at line " in res, (d, res)
             if py_ok:  # Python accepts lone surrogates and deeper nesting than serde's limit 128
                 assert b"\\ud8" in d or b"\\udc" in d or d.count(b"[") >= 128, (d, res)
+
+
+# ---------------------------------------------------------------------------
+# the lean filter_json fast path's token DFA (fluvio_amd/csrc/fsg_json_dfa.h):
+# whatever it accepts, the serde_json restatement accepts with the same level
+# ---------------------------------------------------------------------------
+def _dfa_probe():
+    import ctypes
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = os.path.join(root, "oracle", "_build", "libjson_dfa_probe.so")
+    src = os.path.join(root, "tests", "native", "json_dfa_probe.cpp")
+    hdr = os.path.join(root, "fluvio_amd", "csrc", "fsg_json_dfa.h")
+    if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(src), os.path.getmtime(hdr)):
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-I", os.path.dirname(hdr), src, "-o", out],
+                       check=True)
+    L = ctypes.CDLL(out)
+    L.json_dfa_probe.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int)]
+
+    def probe(v):
+        lv = ctypes.c_int(-1)
+        return L.json_dfa_probe(v, len(v), ctypes.byref(lv)), lv.value
+    return probe
+
+
+def test_lean_json_dfa_only_accepts_what_serde_accepts():
+    from fluvio_amd import protocol as P
+    from fluvio_amd import synth
+    probe = _dfa_probe()
+    docs = jsongen.corpus(21, 600, 900)
+    docs += [b'{"level":"info","message":"m","n":%s}' % n for n in
+             (b"0", b"-0", b"01", b"1.", b"1.5", b"-", b"1e", b"1e+", b"1E-7", b"2e10", b"-12.5e+3", b"00", b"1 2")]
+    docs += [b'{"level":"info","message":"m","t":%s}' % t for t in
+             (b"true", b"tru", b"truee", b"false", b"fals", b"null", b"nul", b"nulll", b"t rue", b"True")]
+    docs += [b'{"level":"info","message":"x","level":"warn"}', b'{"message":"x"}', b'{ "level" : "warn" , "message" : "y" }',
+             b'{"level":"warn","message":"y"} ', b' {"level":"warn","message":"y"}', b'{"level":"warn","message":"y"}}',
+             b'{"level":"warn","message":"y",}', b'{"level":"warn" "message":"y"}', b'{"level":"warnx","message":"y"}']
+    accepted = 0
+    for d in docs:
+        ok, lv = probe(d)
+        if ok:
+            accepted += 1
+            assert O.json_structured_log(d) == ("ok", lv), d
+    assert accepted >= 10
+    # the bench's C2 documents are all decided by the fast path
+    for b in P.decode_batches(synth.make_slice(2, 300)):
+        for r in b.memory_records():
+            ok, lv = probe(r.value)
+            assert ok and O.json_structured_log(r.value) == ("ok", lv)
