@@ -11,7 +11,7 @@ The same JSON line carries `workloads`, each timed in the same run with the
 same contract (warmup, barrier + sync, max over ranks):
   c1-regex       regex-filter \\d{3}-\\d{2}-\\d{4} over 256 B records   (configs[0] shape)
   c2-json        filter_json (serde_json StructuredLog, level > debug)  (configs[1])
-  c3-filter-map  filter -> map (uppercase), re-encode + CRC32C         (configs[2])
+  c3-filter-map  filter -> projection -> uppercase, re-encode + CRC32C  (configs[2])
   c4-array-map   array_map_json_array, 1-16 elements per record         (configs[3])
   c5-keyed-agg   aggregate-sum over 64 partitions, per-partition state in
                  HBM merged with an RCCL all-reduce                      (configs[4])
@@ -40,8 +40,10 @@ WORKLOADS = {
                  "regex-filter \\d{3}-\\d{2}-\\d{4} on 256 B records"),
     "c2-json": (2, [("filter_json", {}, None)], 4_000_000,
                 "JSON-field filter (filter_json: serde_json StructuredLog, keep level > debug) on 1 KB JSON records"),
-    "c3-filter-map": (2, [("filter_init", {"key": "timeout"}, None), ("map", {}, None)], 4_000_000,
-                      "filter -> map (uppercase) chain with compaction, re-encode, CRC32C"),
+    "c3-filter-map": (2, [("filter_init", {"key": "timeout"}, None), ("map_json_project", {"field": "message"}, None),
+                          ("map", {}, None)], 4_000_000,
+                      "filter -> map (field projection of `message` + ASCII uppercase) with compaction, re-encode, "
+                      "CRC32C"),
     "c4-array-map": (5, [("array_map_json_array", {}, None)], 4_000_000,
                      "array_map_json_array exploding JSON arrays of 1-16 ints / short strings"),
 }

@@ -34,6 +34,7 @@ enum StageOp : uint8_t {
   OP_FILTER_JSON = 7,  // filter_json: serde_json::from_slice::<StructuredLog>, keep level > Debug
   OP_ARRAY_MAP = 8,    // array_map_json_array: Vec<serde_json::Value> -> one record per element (last stage)
   OP_AGG_CONCAT = 9,   // aggregate: String accumulator ++ value (last stage)
+  OP_PROJECT = 10,     // map_json_project: the value narrows to one JSON field's text (FilterMap)
 };
 
 // value representation entering a stage (static per chain position)
@@ -131,6 +132,9 @@ struct BatchStat {
   uint32_t nout;       // output records of the stage output (array_map: elements; else nkeep)
   uint32_t pad;
   uint64_t cat_sum;    // aggregate (concat): bytes appended to the accumulator by this batch
+  uint64_t err_vpos;   // the failing record's value as it entered the failing stage (byte views:
+  uint32_t err_vlen;   //   a projection narrows the view)
+  uint32_t pad2;
 };
 
 // one kept output record (a compaction descriptor, 64 bytes): enough to

@@ -35,7 +35,7 @@ enum JsonErr : uint8_t {
   JE_UNSUP,            // valid input outside the device restatement (array_map: floats, unsorted keys)
 };
 enum JsonUnexp : uint8_t { JU_UNIT = 0, JU_TRUE, JU_FALSE, JU_UINT, JU_NINT, JU_FLOAT, JU_STR, JU_SEQ, JU_MAP };
-enum JsonExp : uint8_t { JX_STRUCT = 0, JX_STRING, JX_VARIANT, JX_UNIT, JX_SEQ };
+enum JsonExp : uint8_t { JX_STRUCT = 0, JX_STRING, JX_VARIANT, JX_UNIT, JX_SEQ, JX_MAP };
 
 struct JRes {
   uint8_t ok;
@@ -1053,6 +1053,111 @@ struct JsonDev {
     return r;
   }
 
+  // map_json_project (C3 field projection; defined by the oracle, parity
+  // unpinned): from_slice::<Map<String, Value>> (de.rs deserialize_map /
+  // MapAccess), the last member whose key equals `field`.  *ps / *pl = its
+  // value's span, *found, *verb = the span is already serde_json::to_string's
+  // text (else the projection is JE_UNSUP).  Keys with escapes, floats and
+  // unsorted objects inside the projected value are JE_UNSUP.
+  __device__ __forceinline__ JRes run_project(const uint8_t* field, uint32_t fl, uint32_t* ps, uint32_t* pl,
+                                              bool* found) {
+    r = JRes{0, 0, 0, 0, 0, 0, 0};
+    failed = false;
+    has_pos = false;
+    depth = 128;
+    i = 0;
+    vunsup = false;
+    *found = false;
+    bool fverb = true, funsup = false;
+    int rc = 0;
+    int c = ws();
+    if (c < 0) {
+      rc = peek_error(JE_EOF_VALUE);
+    } else if (c == '{') {
+      --depth;  // 127: cannot reach 0
+      eat();
+      bool first = true;
+      for (;;) {
+        int p = ws();
+        if (p == '}') break;
+        if (p == ',' && !first) {
+          eat();
+          p = ws();
+        } else if (p >= 0) {
+          if (!first) {
+            rc = peek_error(JE_OBJ_COMMA);
+            break;
+          }
+          first = false;
+        } else {
+          rc = peek_error(JE_EOF_OBJECT);
+          break;
+        }
+        if (p == '}') {
+          rc = peek_error(JE_TRAILING_COMMA);
+          break;
+        }
+        if (p < 0) {
+          rc = peek_error(JE_EOF_VALUE);
+          break;
+        }
+        if (p != '"') {
+          rc = peek_error(JE_KEY);
+          break;
+        }
+        eat();
+        const uint32_t k0 = i;
+        vcanon = 0;
+        if (vstr()) {
+          rc = -1;
+          break;
+        }
+        const uint32_t k1 = i - 1;
+        bool hit = !vhas_bs && k1 - k0 == fl;
+        for (uint32_t k = 0; hit && k < fl; k++) hit = at(k0 + k) == field[k];
+        const bool maybe = vhas_bs;  // an escaped key could decode to the field name
+        c = ws();  // parse_object_colon
+        if (c == ':') {
+          eat();
+        } else if (c >= 0) {
+          rc = peek_error(JE_COLON);
+          break;
+        } else {
+          rc = peek_error(JE_EOF_OBJECT);
+          break;
+        }
+        const bool un0 = vunsup;
+        vunsup = false;
+        vcanon = 0;
+        vhas_u = false;
+        ws();
+        const uint32_t e0 = i;
+        if (any_value()) {
+          rc = -1;
+          break;
+        }
+        if (hit) {
+          *found = true;
+          *ps = e0;
+          *pl = i - e0;
+          fverb = i - e0 == vcanon && !vhas_u;
+          funsup = vunsup;
+        }
+        vunsup = un0 || maybe;
+      }
+      depth++;
+      if (!rc) rc = end_map();
+    } else {
+      invalid_type(JX_MAP);
+      rc = -1;
+    }
+    if (rc) fix_position();
+    if (!rc && ws() >= 0) rc = peek_error(JE_TRAILING);  // Deserializer::end
+    if (!rc && (vunsup || (*found && (funsup || !fverb)))) rc = fail_at(i, JE_UNSUP);
+    if (!rc) r.ok = 1;
+    return r;
+  }
+
   __device__ __forceinline__ JRes run() {
     int level = 0;
     r = JRes{0, 0, 0, 0, 0, 0, 0};
@@ -1079,6 +1184,15 @@ __device__ __noinline__ JRes json_structured_log(const uint8_t* s, uint32_t n, b
   d.n = n;
   d.upper = upper;
   return d.run();
+}
+// map_json_project over one value
+__device__ __noinline__ JRes json_project(const uint8_t* s, uint32_t n, bool upper, const uint8_t* field, uint32_t fl,
+                                          uint32_t* ps, uint32_t* pl, bool* found) {
+  JsonDev<const uint8_t*> d;
+  d.s = s;
+  d.n = n;
+  d.upper = upper;
+  return d.run_project(field, fl, ps, pl, found);
 }
 // array_map_json_array over one value: element descriptors to out[0..*count)
 __device__ __noinline__ JRes json_array_explode(const uint8_t* s, uint32_t n, bool upper, ElemRec* out, uint64_t abs0,

@@ -231,11 +231,12 @@ constexpr int kEvalThreads = 256;  // one 4-wave workgroup per stored batch
 constexpr uint32_t opbit(int op) { return 1u << op; }
 constexpr uint32_t kOpsContains = opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
 constexpr uint32_t kOpsRegex = opbit(OP_REGEX) | opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
-constexpr uint32_t kOpsJson = opbit(OP_FILTER_JSON) | opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
+constexpr uint32_t kOpsJson = opbit(OP_FILTER_JSON) | opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER) | opbit(OP_PROJECT) |
+                              opbit(OP_REGEX);
 constexpr uint32_t kOpsArray = opbit(OP_ARRAY_MAP) | opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
 constexpr uint32_t kOpsInt = opbit(OP_FILTER_ODD) | opbit(OP_MAP_DOUBLE) | opbit(OP_FILTER_MAP) | opbit(OP_AGG_SUM) |
                              opbit(OP_AGG_CONCAT) | opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
-constexpr uint32_t kOpsAll = 0x3FFu;
+constexpr uint32_t kOpsAll = 0x7FFu;
 constexpr int kDfaDyn = 768 + kDfaLds;  // dynamic LDS of a chain with a regex stage
 extern __shared__ __attribute__((aligned(16))) uint8_t g_dyn_lds[];
 
@@ -837,6 +838,39 @@ __device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int 
             }
             break;
           }
+          case OP_PROJECT: {
+            // map_json_project: the value becomes its field's JSON text (a view
+            // into the source value), a missing field drops the record
+            if constexpr (!(kOps & opbit(OP_PROJECT))) break;
+            uint8_t t[12];
+            const uint8_t* js = (const uint8_t*)&w[vs];
+            uint32_t jn = vl;
+            if (!src) {
+              jn = fmt_i32(ival_in, t);
+              js = t;
+            }
+            uint32_t ps = 0, pl = 0;
+            bool found = false;
+            const JRes jr = json_project(js, jn, src && upper, blob + sd.needle, sd.needle_len, &ps, &pl, &found);
+            if (!jr.ok) {
+              err = true;
+              if (jr.code == JE_UNSUP) {
+                ec = EC_UNSUP;
+              } else {
+                ec = EC_JSON | ((uint32_t)jr.code << 8) | ((uint32_t)jr.sub << 16);
+                L.r_aux[r] = jr.pos;
+                L.r_aux2[r] = jr.a;
+                L.r_aux3[r] = jr.b;
+              }
+            } else if (!found) {
+              f &= ~RF_ALIVE;
+            } else {
+              L.r_vs[r] = vs + ps;  // valid JSON text: valid UTF-8 from here on
+              L.r_vl[r] = pl;
+              f = (f | RF_UTF8_DONE) & ~RF_UTF8_BAD;
+            }
+            break;
+          }
           case OP_AGG_CONCAT: {
             // aggregate: acc.push_str(from_utf8(value)?) — the bytes this record appends
             if constexpr (!(kOps & opbit(OP_AGG_CONCAT))) break;
@@ -1075,6 +1109,8 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
                 L.bs.err_ival = L.r_ival_in[rr];
                 L.bs.err_pos = wbase + L.r_start[rr];
                 L.bs.err_od = L.r_od[rr];
+                L.bs.err_vpos = wbase + L.r_vs[rr];
+                L.bs.err_vlen = L.r_vl[rr];
               }
             }
           }
@@ -1237,7 +1273,8 @@ constexpr int kJsonChunks = (kLeanWin + 48) / 16 + 2;
 constexpr int kJsonEnt = 2048;  // token entries per batch (more: exact kernel)
 __device__ constexpr JsonDfaTables g_json_tables{};
 struct __attribute__((aligned(16))) LeanLdsJ : LeanLds {
-  uint32_t jm[kJsonChunks];      // quote16 | in-string16 << 16 (in-string: exclusive, batch-global parity)
+  uint32_t jm[kJsonChunks];      // pass 1: quote16 | special16 << 16; pass 2: in-string16 | hot16 << 16
+  uint16_t jn[kJsonChunks];      // non-space16
   uint32_t ent[kJsonEnt];        // pos | byte << 16 | token class << 24
   uint32_t wsum[4];              // cross-wave scan carries
   uint8_t dfa[kJsonStates * kJsonCls2];
@@ -1437,26 +1474,6 @@ __device__ __forceinline__ uint32_t lean_regex(LeanLds& L, int nr, uint32_t lo, 
 
 // 4 bits: which of the 4 bytes of a SWAR mask word carry 0x80
 __device__ __forceinline__ uint32_t nib4(uint32_t m80) { return ((((m80 >> 7) & 0x01010101u) * 0x01020408u) >> 24) & 15u; }
-// 16-bit masks of one 16-byte chunk: bytes == c
-__device__ __forceinline__ uint32_t eq16(const uint4& v, uint32_t c4) {
-  return nib4(zbytes(v.x ^ c4)) | (nib4(zbytes(v.y ^ c4)) << 4) | (nib4(zbytes(v.z ^ c4)) << 8) |
-         (nib4(zbytes(v.w ^ c4)) << 12);
-}
-// bytes < 0x20, == '\\' or >= 0x80: anything the fast JSON path does not decide
-__device__ __forceinline__ uint32_t special16(const uint4& v) {
-  auto one = [](uint32_t w) {
-    return nib4(zbytes(w & 0xE0E0E0E0u) | zbytes(w ^ 0x5C5C5C5Cu) | (w & 0x80808080u));
-  };
-  return one(v.x) | (one(v.y) << 4) | (one(v.z) << 8) | (one(v.w) << 12);
-}
-template <typename LdsT>
-__device__ __forceinline__ bool lds_eq(const LdsT& L, uint32_t p, uint32_t n, const char* s, uint32_t sn) {
-  if (n != sn) return false;
-  for (uint32_t k = 0; k < n; k++)
-    if (L.win[p + k] != (uint8_t)s[k]) return false;
-  return true;
-}
-
 // ---------------------------------------------------------------------------
 // filter_json in the lean kernel (smartmodule/examples/filter_json/src/lib.rs:
 // 54-70, serde_json::from_slice::<StructuredLog>), data-parallel:
@@ -1474,9 +1491,6 @@ __device__ __forceinline__ bool lds_eq(const LdsT& L, uint32_t p, uint32_t n, co
 //      literals, each field once.  Any other record (and any record starting
 //      inside an unbalanced string) sends the batch to the exact kernel.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t zero16(const uint4& v) {
-  return nib4(zbytes(v.x)) | (nib4(zbytes(v.y)) << 4) | (nib4(zbytes(v.z)) << 8) | (nib4(zbytes(v.w)) << 12);
-}
 __device__ __forceinline__ uint32_t pxor16(uint32_t q) {  // inclusive prefix XOR of 16 bits
   uint32_t px = q ^ (q << 1);
   px ^= px << 2;
@@ -1517,22 +1531,29 @@ __device__ bool lean_json_stage(LeanLdsJ& L, int nr) {
   const uint32_t per = (nch + kLeanThreads - 1) / kLeanThreads;
   const uint32_t k0 = l * per, k1 = k0 + per < nch ? k0 + per : nch;
   uint32_t par = 0;
-  for (uint32_t k = k0; k < k1; k++) {
+  for (uint32_t k = k0; k < k1; k++) {  // byte classes, once: quote, special (< 0x20 incl. 0, '\\', >= 0x80), non-space
     const uint4 v = *(const uint4*)(&L.win[c0 + 16 * k]);
-    const uint32_t q = eq16(v, 0x22222222u);
-    L.jm[k] = q;
+    uint32_t q = 0, sp = 0, ns = 0;
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      const uint32_t w = d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
+      q |= nib4(zbytes(w ^ 0x22222222u)) << (4 * d);
+      sp |= nib4(zbytes(w & 0xE0E0E0E0u) | zbytes(w ^ 0x5C5C5C5Cu) | (w & 0x80808080u)) << (4 * d);
+      ns |= nib4(zbytes(w ^ 0x20202020u)) << (4 * d);
+    }
+    L.jm[k] = q | (sp << 16);
+    L.jn[k] = (uint16_t)(~ns & 0xFFFFu);
     par ^= __builtin_popcount(q) & 1u;
   }
   uint32_t tot;
   uint32_t carry = wg_excl_sum(par, L.wsum, &tot) & 1u;  // parity of all quotes before my chunks
   uint32_t cnt = 0;
   for (uint32_t k = k0; k < k1; k++) {
-    const uint4 v = *(const uint4*)(&L.win[c0 + 16 * k]);
-    const uint32_t q = L.jm[k];
+    const uint32_t m = L.jm[k], q = m & 0xFFFFu, sp = m >> 16;
     const uint32_t instr = (pxor16(q) ^ q ^ (carry ? 0xFFFFu : 0u)) & 0xFFFFu;
     carry ^= __builtin_popcount(q) & 1u;
-    L.jm[k] = q | (instr << 16);
-    const uint32_t hot = q | special16(v) | zero16(v) | (~eq16(v, 0x20202020u) & ~instr & 0xFFFFu);
+    const uint32_t hot = q | sp | ((uint32_t)L.jn[k] & ~instr);
+    L.jm[k] = instr | (hot << 16);
     cnt += __builtin_popcount(hot);
   }
   // 2. token list
@@ -1540,9 +1561,8 @@ __device__ bool lean_json_stage(LeanLdsJ& L, int nr) {
   uint32_t e = wg_excl_sum(cnt, L.wsum, &ntok);
   if (ntok > (uint32_t)kJsonEnt) return true;  // uniform: every thread saw the same total
   for (uint32_t k = k0; k < k1; k++) {
-    const uint4 v = *(const uint4*)(&L.win[c0 + 16 * k]);
-    const uint32_t q = L.jm[k] & 0xFFFFu, instr = L.jm[k] >> 16;
-    uint32_t hot = q | special16(v) | zero16(v) | (~eq16(v, 0x20202020u) & ~instr & 0xFFFFu);
+    const uint32_t instr = L.jm[k] & 0xFFFFu;
+    uint32_t hot = L.jm[k] >> 16;
     while (hot) {
       const uint32_t j = (uint32_t)__builtin_ctz(hot);
       hot &= hot - 1;
@@ -1573,7 +1593,7 @@ __device__ bool lean_json_stage(LeanLdsJ& L, int nr) {
     auto instr_at = [&](uint32_t p) {
       const uint32_t k = (p - c0) >> 4, j = (p - c0) & 15u;
       if (k >= nch) return 0u;
-      return (L.jm[k] >> (16 + j)) & 1u;
+      return (L.jm[k] >> j) & 1u;
     };
     if (instr_at(vs) || instr_at(ve)) bad = true;
     // the record's tokens [t0, t1): binary search on positions

@@ -419,6 +419,14 @@ int add_stage(fsg_chain* c, const ModuleSpec& m, const std::string& name, uint8_
     sd.kind = FSG_KIND_AGGREGATE;
     c->agg_stage = (int)c->hdesc.nstages;
     c->acc = m.has_acc ? m.acc : std::vector<uint8_t>();
+  } else if (name == "map_json_project") {  // C3 field projection (parity unpinned: no reference module)
+    const std::string* f = param("field");
+    const std::string field = f ? *f : std::string("message");
+    sd.op = OP_PROJECT;
+    sd.kind = FSG_KIND_FILTER_MAP;
+    sd.needle = put_blob(field.data(), field.size());
+    sd.needle_len = (uint32_t)field.size();
+    if (vt == VT_I32) vt = VT_SRC;  // the text of an integer is parsed (always an error)
   } else if (name == "array_map_json_array") {  // examples/array_map_json_array: explode a JSON array
     sd.op = OP_ARRAY_MAP;
     sd.kind = FSG_KIND_ARRAY_MAP;
@@ -659,7 +667,7 @@ bool json_hint(uint32_t code_word, uint32_t pos, uint32_t a, uint32_t b, const s
     msg = "unknown variant `" + val + "`, expected one of `debug`, `info`, `warn`, `error`";
   } else if (code == JE_INVALID_TYPE) {
     static const char* const kExp[] = {"struct StructuredLog", "a string", "variant identifier", "unit",
-                                       "a sequence", "", "", ""};
+                                       "a sequence", "a map", "", ""};
     std::string un;
     switch (sub & 15) {
       case JU_UNIT: un = "unit value"; break;
@@ -761,6 +769,11 @@ int build_error(fsg_chain* c, const fsg_slice* s, const BatchStat& st, fsg_runti
   size_t take = std::min<size_t>((size_t)vl, rec.size() - q);
   val.assign(rec.begin() + q, rec.begin() + q + take);
   const StageDesc& sd = c->hdesc.st[st.err_stage];
+  if (sd.in_type != VT_I32) {  // the value's view as it entered the stage (a projection narrows it)
+    val.resize(st.err_vlen);
+    if (st.err_vlen)
+      HIPCHK(hipMemcpy(val.data(), (uint8_t*)s->data.p + st.err_vpos, st.err_vlen, hipMemcpyDeviceToHost));
+  }
   if (sd.in_type == VT_SRC_UPPER)
     for (auto& ch : val)
       if (ch >= 'a' && ch <= 'z') ch -= 32;

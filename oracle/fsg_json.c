@@ -1355,6 +1355,134 @@ int orc_json_array_map(const uint8_t *s, size_t n, uint8_t ***elems, size_t **le
   return 1;
 }
 
+/* ------------------------------------------------------------------ */
+/* map_json_project (C3 "field projection"; no reference module exists —  */
+/* BASELINE configs[2] names the transform, the reference ships it only   */
+/* as the hub's Jolt module, so this restatement DEFINES it: parity       */
+/* unpinned).  FilterMap semantics in serde_json terms:                   */
+/*   let m: Map<String, Value> = serde_json::from_slice(value)?;          */
+/*   m.get(field).map(|v| serde_json::to_string(v))                      */
+/* a missing field drops the record.  Map::insert: a repeated key keeps   */
+/* its last value.                                                        */
+/* ------------------------------------------------------------------ */
+int orc_json_project(const uint8_t *s, size_t n, const char *field, uint8_t **out, size_t *out_len, int *found,
+                     char **msg, size_t *msg_len) {
+  jde d;
+  memset(&d, 0, sizeof d);
+  d.s = s;
+  d.n = n;
+  d.depth = 128;
+  *msg = NULL;
+  *out = NULL;
+  *out_len = 0;
+  *found = 0;
+  const size_t fl = strlen(field);
+  jbuf val = {0};
+  int r = 0;
+  int peek = parse_whitespace(&d);
+  if (peek < 0) {
+    r = jpeek_error(&d, E_EOF_VALUE);
+  } else if (peek == '{') { /* deserialize_map */
+    --d.depth;
+    jeat(&d);
+    int first = 1;
+    for (;;) { /* MapAccess::next_key_seed / next_value_seed */
+      int p = parse_whitespace(&d);
+      if (p == '}') break;
+      if (p == ',' && !first) {
+        jeat(&d);
+        p = parse_whitespace(&d);
+      } else if (p >= 0) {
+        if (first)
+          first = 0;
+        else {
+          r = jpeek_error(&d, E_OBJ_COMMA);
+          break;
+        }
+      } else {
+        r = jpeek_error(&d, E_EOF_OBJECT);
+        break;
+      }
+      if (p == '}') { r = jpeek_error(&d, E_TRAILING_COMMA); break; }
+      if (p < 0) { r = jpeek_error(&d, E_EOF_VALUE); break; }
+      if (p != '"') { r = jpeek_error(&d, E_KEY); break; }
+      jeat(&d);
+      jbuf key;
+      if (parse_str(&d, &key)) {
+        free(key.b);
+        r = -1;
+        break;
+      }
+      const int hit = key.n == fl && (!fl || !memcmp(key.b, field, fl));
+      free(key.b);
+      int c = parse_whitespace(&d);
+      if (c == ':')
+        jeat(&d);
+      else if (c >= 0) {
+        r = jpeek_error(&d, E_COLON);
+        break;
+      } else {
+        r = jpeek_error(&d, E_EOF_OBJECT);
+        break;
+      }
+      jbuf v = {0};
+      if (value_canon(&d, &v)) {
+        free(v.b);
+        r = -1;
+        break;
+      }
+      if (hit) {
+        free(val.b);
+        val = v;
+        *found = 1;
+      } else {
+        free(v.b);
+      }
+    }
+    d.depth++;
+    if (r) {
+      jde probe = d;
+      probe.msg = NULL;
+      probe.msg_len = 0;
+      probe.failed = 0;
+      (void)end_map(&probe);
+      free(probe.msg);
+      d.i = probe.i;
+    } else {
+      r = end_map(&d);
+    }
+    if (r) jfix_position(&d);
+  } else {
+    r = peek_invalid_type(&d, "a map");
+    jfix_position(&d);
+  }
+  if (!r && parse_whitespace(&d) >= 0) r = jpeek_error(&d, E_TRAILING); /* Deserializer::end */
+  if (!r) {
+    free(d.msg);
+    if (*found) {
+      *out = val.b ? val.b : (uint8_t *)malloc(1);
+      *out_len = val.n;
+    } else {
+      free(val.b);
+    }
+    return 0;
+  }
+  free(val.b);
+  *found = 0;
+  if (d.unsupported) {
+    free(d.msg);
+    return ORC_E_UNSUPPORTED;
+  }
+  *msg = render(&d, msg_len);
+  free(d.msg);
+  if (memchr(*msg, 0, *msg_len)) {
+    free(*msg);
+    *msg = NULL;
+    return ORC_E_UNSUPPORTED;
+  }
+  return 1;
+}
+
 /* generic entry for pinning against other serde_json fixtures of the reference:
  * fields as "name" (string) or "name=v1|v2|.." (unit enum) */
 int orc_json_struct(const uint8_t *s, size_t n, const char *name, const char **fields, int nfields, int *vals,

@@ -1115,6 +1115,7 @@ enum {
   M_AGG_CONCAT,
   M_FILTER_JSON, /* examples/filter_json: StructuredLog.level > Debug */
   M_ARRAY_MAP,   /* examples/array_map_json_array: explode a JSON array */
+  M_PROJECT,     /* map_json_project: the value of one JSON field (C3 projection) */
 };
 
 typedef struct {
@@ -1226,6 +1227,14 @@ int orc_chain_add(orc_chain *c, const char *module, const char **keys, const cha
   } else if (!strcmp(module, "array_map_json_array")) {
     s.mod = M_ARRAY_MAP;
     s.kind = K_ARRAY_MAP;
+  } else if (!strcmp(module, "map_json_project")) { /* param field, default "message" */
+    v = param_get(keys, vals, n_params, "field");
+    if (!v) v = "message";
+    s.mod = M_PROJECT;
+    s.kind = K_FILTER_MAP;
+    s.needle_len = strlen(v);
+    s.needle = dup_bytes((const uint8_t *)v, s.needle_len + 1);
+    s.needle[s.needle_len] = 0;
   } else {
     return ORC_E_UNKNOWN_SM;
   }
@@ -1364,6 +1373,29 @@ static void stage_run(stage_t *s, recvec *in, int64_t base_offset, stage_out *o)
         }
         free(el);
         free(ln);
+        break;
+      }
+      case M_PROJECT: {
+        uint8_t *pv;
+        size_t pl, ml;
+        int found;
+        char *m = NULL;
+        int jr = orc_json_project(r->val, r->val_len, (const char *)s->needle, &pv, &pl, &found, &m, &ml);
+        if (jr == ORC_E_UNSUPPORTED) {
+          o->unsupported = 1;
+          return;
+        }
+        if (jr) {
+          hint = m;
+          break;
+        }
+        if (found) { /* filter_map: Some((key, projected)) keeps key and preamble */
+          outr = rec_clone(r);
+          free(outr.val);
+          outr.val = pv;
+          outr.val_len = pl;
+          emit = 1;
+        }
         break;
       }
       case M_MAP_UPPER:

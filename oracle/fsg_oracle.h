@@ -95,6 +95,10 @@ int orc_json_structured_log(const uint8_t *s, size_t n, int *level, char **msg, 
  * 1 error (*msg Display text), ORC_E_UNSUPPORTED (floats) */
 int orc_json_array_map(const uint8_t *s, size_t n, uint8_t ***elems, size_t **lens, size_t *count, char **msg,
                        size_t *msg_len);
+/* map_json_project: Map<String, Value> from_slice, to_string of the field's value.
+ * 0 ok (*found; *out canonical value when found), 1 error (*msg), ORC_E_UNSUPPORTED */
+int orc_json_project(const uint8_t *s, size_t n, const char *field, uint8_t **out, size_t *out_len, int *found,
+                     char **msg, size_t *msg_len);
 int orc_json_struct(const uint8_t *s, size_t n, const char *name, const char **fields, int nfields, int *vals,
                     char **msg, size_t *msg_len);
 

@@ -80,6 +80,10 @@ def lib():
                                          ctypes.POINTER(ctypes.POINTER(ctypes.c_size_t)),
                                          ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_void_p),
                                          ctypes.POINTER(ctypes.c_size_t)]
+        L.orc_json_project.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                       ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), ctypes.POINTER(ctypes.c_size_t),
+                                       ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_void_p),
+                                       ctypes.POINTER(ctypes.c_size_t)]
         L.orc_varint_encode.restype = ctypes.c_size_t
         L.orc_varint_encode.argtypes = [ctypes.c_int64, ctypes.c_char_p]
         _lib = L
@@ -143,6 +147,24 @@ def json_array_map(value: bytes):
         return "ok", out
     err = _json_result(rc, msg, ml)
     return "err", err
+
+
+def json_project(value: bytes, field: str = "message"):
+    """map_json_project: ("ok", canonical bytes or None if the field is absent) / ("err", text)."""
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    ol = ctypes.c_size_t()
+    found = ctypes.c_int()
+    msg = ctypes.c_void_p()
+    ml = ctypes.c_size_t(0)
+    rc = lib().orc_json_project(value, len(value), field.encode(), ctypes.byref(out), ctypes.byref(ol),
+                                ctypes.byref(found), ctypes.byref(msg), ctypes.byref(ml))
+    if rc == 0:
+        if not found.value:
+            return "ok", None
+        v = ctypes.string_at(out, ol.value)
+        lib().orc_free(out)
+        return "ok", v
+    return "err", _json_result(rc, msg, ml)
 
 
 def json_struct(value: bytes, name: str, fields):

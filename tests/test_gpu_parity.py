@@ -190,6 +190,10 @@ CHAINS = {
     "array_map": [("array_map_json_array", {}, None)],
     "filter_array_map": [("filter_with_param", {"key": "1"}, None), ("array_map_json_array", {}, None)],
     "map_array_map": [("map", {}, None), ("array_map_json_array", {}, None)],
+    "project": [("map_json_project", {}, None)],
+    "filter_project_map": [("filter_init", {"key": "timeout"}, None), ("map_json_project", {}, None), ("map", {}, None)],
+    "project_level_filter": [("map_json_project", {"field": "level"}, None), ("filter_init", {"key": "warn"}, None)],
+    "map_project_upper": [("map", {}, None), ("map_json_project", {"field": "MESSAGE"}, None)],
     "empty": [],
 }
 # string-concatenating aggregate: output grows quadratically, small slices only
@@ -631,3 +635,42 @@ def test_crc_tables_on_every_device():
     for d in (0, 1):
         e = SmartEngine(d)
         assert gpu_chain(e, CHAINS["map"]).process_batch(sl).raw == ref
+
+
+# ---------------------------------------------------------------------------
+# field projection (map_json_project, C3): parity unpinned by the reference
+# (no such module ships in it); checked against the oracle's definition
+# ---------------------------------------------------------------------------
+def test_project_fuzz_one_record(engine):
+    from tests import jsongen
+    for doc in jsongen.corpus(17, 150, 350):
+        sl = _one_record_slice(doc)
+        for chain in ("project", "project_level_filter"):
+            try:
+                check_batch(engine, CHAINS[chain], sl)
+            except AssertionError as e:
+                raise AssertionError(f"doc {doc!r}: {e}") from e
+
+
+def test_project_c3_chain_errors_in_stream(engine):
+    """C3: filter -> projection -> uppercase, with projection errors and an
+    error in a later stage after the value was narrowed (double_then... on text)."""
+    from tests import jsongen
+    import random
+    rng = random.Random(5)
+    good = [jsongen.valid_doc(rng).encode() for _ in range(500)]
+    sl, base = b"", 0
+    for k in range(50):
+        b = P.Batch(base_offset=base)
+        for j in range(10):
+            v = good[k * 10 + j]
+            if k == 31 and j == 2:
+                v = b'{"message": "timeout x", "level": 5, "message": [1, 2'
+            b.add_record(P.Record.new(v))
+        sl += b.encode()
+        base += 10
+    for chain in ("filter_project_map", "project", "map_project_upper"):
+        check_batch(engine, CHAINS[chain], sl)
+        check_batch(engine, CHAINS[chain], sl, max_bytes=5000)
+    # a stage erring on the projected (narrowed) value reports that value
+    check_batch(engine, [("map_json_project", {}, None), ("filter_odd", {}, None)], sl)

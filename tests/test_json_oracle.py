@@ -220,3 +220,37 @@ def test_lean_json_dfa_only_accepts_what_serde_accepts():
         for r in b.memory_records():
             ok, lv = probe(r.value)
             assert ok and O.json_structured_log(r.value) == ("ok", lv)
+
+
+# ---------------------------------------------------------------------------
+# map_json_project (C3 field projection, defined by the oracle: parity
+# unpinned by the reference) against Python's json on the accept/reject
+# decision and the projected text
+# ---------------------------------------------------------------------------
+def test_project_oracle_vs_python_json():
+    docs = jsongen.corpus(31, 300, 300) + [b'{"message":"a","message":"b"}', b'{"a":{"message":1}}', b"{}",
+                                           b'{"message":[3,{"b":1,"a":2}]}', b'{"message":null}']
+    seen_ok = seen_none = 0
+    for d in docs:
+        try:
+            st, v = O.json_project(d)
+        except O.OracleError as e:
+            assert e.status == -103
+            continue
+        try:
+            py = json.loads(d)
+        except (ValueError, RecursionError):
+            py = ValueError
+        if st == "ok":
+            assert isinstance(py, dict), d
+            if "message" in py:
+                assert v == _py_canon(py["message"]), d
+                seen_ok += 1
+            else:
+                assert v is None, d
+                seen_none += 1
+        else:
+            assert " at line " in v, (d, v)
+            if isinstance(py, dict):  # Python accepts lone surrogates / deeper nesting
+                assert b"\\ud8" in d or b"\\udc" in d or d.count(b"[") >= 60, (d, v)
+    assert seen_ok > 100 and seen_none > 0
