@@ -24,7 +24,8 @@ enum JsonTokCls : uint8_t {
   JC_D0, JC_D19, JC_MINUS, JC_DOT, JC_e, JC_E, JC_PLUS,
   JC_t, JC_r, JC_u, JC_f, JC_a, JC_l, JC_s, JC_n,
   JC_OTHER,
-  JC_COUNT
+  JC_COUNT,
+  JC_Q_FIELD = JC_COUNT  // projection: a string equal to the field name (taken as JC_Q_OTHER by the table)
 };
 enum JsonTokState : uint8_t {
   JS_OBJ, JS_KEY_OR_END, JS_KEY, JS_INKEY_LV, JS_INKEY_MSG, JS_INKEY_OTHER,

@@ -17,6 +17,7 @@
 //   k_crc_*    CRC32C over attributes..records, chunked + GF(2) combine
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <mutex>
 #include <type_traits>
 
@@ -1232,15 +1233,19 @@ __global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : 2) void 
 }
 
 // ---------------------------------------------------------------------------
-// k_eval_lean — one wave per stored batch for chains of substring filters and
-// ASCII-uppercase maps (filter / filter_init / filter_with_param / map), the
-// C2/C3 hot path.  No barriers beyond the wave, ~17.5 KiB LDS per batch so nine
-// batches are in flight per CU.  A batch takes this path only when its records
-// can neither error nor decode unusually: record section inside the 16 KiB
-// window, 1..64 records that frame exactly, every value ASCII (then
-// from_utf8 cannot fail, filter.rs / derive filter.rs:14-40).  Any other batch
-// is appended to a.list and evaluated exactly by k_eval (list mode).
-//   1. LDS-DMA the batch (header + record section) into the window
+// k_eval_lean — persistent workgroups of two waves for chains of substring /
+// bounded-regex / filter_json filters and ASCII-uppercase maps (filter /
+// filter_init / filter_with_param / regex-filter / filter_json / map), the
+// C1/C2 hot path.  Each workgroup walks the batches b = blockIdx.x + i * grid;
+// while batch i is evaluated, batch i + 1 is already streaming into a second
+// LDS window (LDS-DMA), so HBM latency hides behind the evaluation.  A batch
+// takes this path only when its records can neither error nor decode
+// unusually: record section inside the 16 KiB window, 1..64 records that frame
+// exactly, every value ASCII (then from_utf8 cannot fail, filter.rs / derive
+// filter.rs:14-40).  Any other batch is appended to a.list and evaluated
+// exactly by k_eval (list mode).
+//   1. LDS-DMA the batch (header + record section) into the prefetch window,
+//      copied to the evaluation window when its turn comes
 //   2. lane 0 chases the record length varints; lane r parses record r exactly
 //      (Record::decode, data.rs:534-562) and checks it ends where its length says
 //   3. per contains stage, a data-parallel 4-gram scan over the value bytes
@@ -1255,6 +1260,20 @@ constexpr int kLeanMaxR = 64;    // one record per lane of wave 0
 constexpr int kLeanThreads = 128;  // two waves per batch: DMA issue and the scan are split over both
 constexpr int kLeanNeedle = 128; // longest needle of the lean path (longer: exact kernel)
 constexpr int kLeanBlk = (kLeanWin + 80) / 64 + 1;  // 64-byte blocks of the window
+constexpr int kLeanNeedles = 256;  // resident needle bytes of all contains stages
+// a stage as the lean kernel needs it, copied to LDS once per workgroup (no
+// global reads while a prefetch is in flight)
+struct LeanStage {
+  uint8_t op;
+  uint8_t upper;       // in_type == VT_SRC_UPPER
+  uint8_t keep_match;
+  uint8_t pad;
+  uint32_t m;          // needle_len
+  uint32_t max_len, s_bot, s_mid, acc1, acc2;
+  uint32_t tt;         // blob offset of the regex rows (tt or tt_up by the input case)
+  uint32_t nd;         // blob offset of the needle
+  uint32_t nd_off;     // its offset in LeanLds::needles (when resident)
+};
 struct __attribute__((aligned(16))) LeanLds {
   uint8_t win[kLeanWin + 48];  // + look-ahead of the last scan chunk
   uint32_t r_start[kLeanMaxR + 1];
@@ -1262,11 +1281,35 @@ struct __attribute__((aligned(16))) LeanLds {
   uint32_t r_ve[kLeanMaxR];
   uint32_t match[2];
   uint32_t chase_bad;
-  uint32_t pad;
+  uint32_t nst;
+  uint32_t red[4];                  // workgroup OR (two alternating pairs)
+  uint32_t out_upper;
+  uint32_t tt_stage;                // stage whose rows sit in tt for the whole launch (0xFF: reloaded)
+  uint32_t nd_res;                  // 1: every needle sits in needles (LeanStage::nd_off)
+  LeanStage stg[kMaxStages];
   uint64_t tt[256];                 // the scanned regex stage's byte rows (DfaDesc::tt)
   uint8_t needle[kLeanNeedle + 8];  // the scanned stage's needle
-  uint8_t blk[kLeanBlk + 1];        // blk[j] = last record whose value starts <= 64 j (0xFF none)
+  uint8_t needles[kLeanNeedles];    // the contains stages' needles, back to back (when they fit)
+  alignas(4) uint8_t blk[kLeanBlk + 4];  // blk[j] = last record whose value starts <= 64 j (0xFF none)
 };
+// Workgroup barrier over LDS only: the LDS-DMA of the next batch stays in
+// flight (__syncthreads would also wait for every outstanding global access).
+__device__ __forceinline__ void lean_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+// workgroup OR of p over the two waves; `par` alternates the LDS pair so one
+// barrier suffices (a pair is rewritten two calls later, after a barrier that
+// every reader of it has passed)
+__device__ __forceinline__ bool lean_or(uint32_t* red, uint32_t& par, bool p) {
+  const uint64_t bl = __ballot(p);
+  uint32_t* r = red + 2 * par;
+  if ((threadIdx.x & 63u) == 0) r[threadIdx.x >> 6] = bl != 0 ? 1u : 0u;
+  lean_sync();
+  par ^= 1u;
+  return (r[0] | r[1]) != 0u;
+}
 // the filter_json variant: per-chunk quote / in-string masks, the token list,
 // the token DFA (fsg_json_dfa.h)
 constexpr int kJsonChunks = (kLeanWin + 48) / 16 + 2;
@@ -1334,7 +1377,7 @@ __device__ __forceinline__ void lean_push(const LeanLds& L, int nr, uint32_t p, 
 template <int kMode>
 __device__ __forceinline__ uint32_t lean_scan(LeanLds& L, int nr, uint32_t lo, uint32_t hi, const uint8_t* nd,
                                               uint32_t m, bool upper) {
-  const uint32_t l = threadIdx.x, lane = l & 63u;
+  const uint32_t l = threadIdx.x;
   uint32_t rot[4] = {0, 0, 0, 0};
   uint32_t k4 = 0xFFFFFFFFu;
   if (kMode == 0) {
@@ -1363,18 +1406,19 @@ __device__ __forceinline__ uint32_t lean_scan(LeanLds& L, int nr, uint32_t lo, u
 #pragma unroll
       for (int k = 0; k < 5; k++) wd[k] = swar_upper(wd[k]);
     }
-    uint64_t any = 0;
+    // min over the compare differences: zero iff some 4-gram hits (vector ops
+    // only; a ballot per compare would cost a scalar OR each)
+    uint32_t z = 0xFFFFFFFFu;
     if (kMode == 0) {
 #pragma unroll
-      for (int k = 0; k < 4; k++)
-#pragma unroll
-        for (int d = 0; d < 4; d++) any |= __ballot(wd[k] == rot[d]);
+      for (int k = 0; k < 4; k++) z = min(z, min(min(wd[k] ^ rot[0], wd[k] ^ rot[1]), min(wd[k] ^ rot[2], wd[k] ^ rot[3])));
     } else {
 #pragma unroll
-      for (int j = 0; j < 16; j++) any |= __ballot(((win5(wd, j) ^ rot[0]) & k4) == 0);
+      for (int j = 0; j < 16; j += 2) z = min(z, min((win5(wd, j) ^ rot[0]) & k4, (win5(wd, j + 1) ^ rot[0]) & k4));
     }
-    if (!any) continue;               // wave-uniform: no 4-gram hit in any lane
-    if (!((any >> lane) & 1)) continue;  // none in this lane
+    const bool hl = z == 0u;
+    if (!__ballot(hl)) continue;  // wave-uniform: no 4-gram hit in any lane
+    if (!hl) continue;            // none in this lane
     if (kMode == 0) {
       // rare hits: parked, resolved after the scan for all lanes at once
 #pragma unroll
@@ -1503,26 +1547,34 @@ __device__ __forceinline__ uint32_t wg_excl_sum(uint32_t v, uint32_t* wsum, uint
   const uint32_t l = threadIdx.x, lane = l & 63u, w = l >> 6;
   const uint32_t incl = wave_incl_scan(v);
   if (lane == 63) wsum[w] = incl;
-  __syncthreads();
+  lean_sync();
   const uint32_t w0 = wsum[0];
   *total = w0 + wsum[1];
-  __syncthreads();
+  lean_sync();
   return incl - v + (w ? w0 : 0u);
 }
+// the class of the string of n bytes at window offset a: its (up to 8) bytes
+// as one little-endian word against immediate constants (string literals would
+// be global loads)
 template <typename LdsT>
 __device__ __forceinline__ uint32_t json_str_class(const LdsT& L, uint32_t a, uint32_t n) {
-  auto eq = [&](const char* t, uint32_t tn) {
-    if (n != tn) return false;
-    for (uint32_t k = 0; k < n; k++)
-      if (L.win[a + k] != (uint8_t)t[k]) return false;
-    return true;
+  if (n < 4 || n > 7) return JC_Q_OTHER;
+  const uint64_t lo = lds_u32_at(L.win, a);
+  const uint64_t hi = lds_u32_at(L.win, a + 4);
+  const uint64_t w = (lo | (hi << 32)) & ((1ull << (8 * n)) - 1ull);
+  constexpr auto k = [](const char* t) {
+    uint64_t v = 0;
+    for (int i = 0; t[i]; i++) v |= (uint64_t)(uint8_t)t[i] << (8 * i);
+    return v;
   };
-  return eq("level", 5) ? JC_Q_LEVEL : eq("message", 7) ? JC_Q_MSG : eq("debug", 5) ? JC_Q_DEBUG
-       : eq("info", 4) ? JC_Q_INFO : eq("warn", 4) ? JC_Q_WARN : eq("error", 5) ? JC_Q_ERROR : JC_Q_OTHER;
+  if (n == 5) return w == k("level") ? JC_Q_LEVEL : w == k("debug") ? JC_Q_DEBUG : w == k("error") ? JC_Q_ERROR : JC_Q_OTHER;
+  if (n == 7) return w == k("message") ? JC_Q_MSG : JC_Q_OTHER;
+  if (n == 4) return w == k("info") ? JC_Q_INFO : w == k("warn") ? JC_Q_WARN : JC_Q_OTHER;
+  return JC_Q_OTHER;
 }
 // stages 1-3 for the records [0, nr); returns true if the batch must go to the
 // exact kernel; match bits of records whose level > Debug in L.match
-__device__ bool lean_json_stage(LeanLdsJ& L, int nr) {
+__device__ bool lean_json_stage(LeanLdsJ& L, int nr, uint32_t& orpar, bool proj, uint32_t fl) {
   const uint32_t l = threadIdx.x;
   const uint32_t c0 = L.r_vs[0] & ~15u, c1 = L.r_ve[nr - 1];
   const uint32_t nch = (c1 - c0 + 15) >> 4;
@@ -1573,7 +1625,7 @@ __device__ bool lean_json_stage(LeanLdsJ& L, int nr) {
       L.ent[e++] = pos | (b << 16) | (cls << 24);
     }
   }
-  __syncthreads();
+  lean_sync();
   // string classes of the opening quotes (the next token closes the string)
   for (uint32_t t = l; t + 1 < ntok; t += kLeanThreads) {
     const uint32_t en = L.ent[t];
@@ -1581,9 +1633,20 @@ __device__ bool lean_json_stage(LeanLdsJ& L, int nr) {
     const uint32_t nx = L.ent[t + 1];
     if ((nx >> 24) != JC_Q_CLOSE) continue;
     const uint32_t a = (en & 0xFFFFu) + 1, n = (nx & 0xFFFFu) - a;
-    L.ent[t] = (en & 0x00FFFFFFu) | (json_str_class(L, a, n) << 24);
+    uint32_t cls;
+    if (proj) {  // the projected field's name (L.needle) or another string
+      bool eq = n == fl;
+      for (uint32_t k = 0; eq && k < fl; k += 4) {
+        const uint32_t mk = fl - k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (fl - k))) - 1u);
+        eq = ((lds_u32_at(L.win, a + k) ^ lds_u32_at(L.needle, k)) & mk) == 0u;
+      }
+      cls = eq ? (uint32_t)JC_Q_FIELD : (uint32_t)JC_Q_OTHER;
+    } else {
+      cls = json_str_class(L, a, n);
+    }
+    L.ent[t] = (en & 0x00FFFFFFu) | (cls << 24);
   }
-  __syncthreads();
+  lean_sync();
   // 3. one thread per record, records spread over both waves
   const uint32_t r = 2 * (l & 63u) + (l >> 6);
   bool bad = false;
@@ -1605,24 +1668,67 @@ __device__ bool lean_json_stage(LeanLdsJ& L, int nr) {
     uint32_t t = lo;
     uint32_t st = JS_OBJ, prev = 0xFFFFu, flags = 0;
     int lvl = -1;
+    // projection (map_json_project, Map<String, Value>, last member wins): the
+    // value span of the last member whose key is the field; numbers whose
+    // serde_json text differs from the source (fractions, exponents, -0, more
+    // than 18 digits) are unsupported by the device restatement -> exact kernel
+    bool khit = false, inval = false, found = false, vneg = false;
+    uint32_t vstart = 0, ntv = 0, fs = 0, fe = 0;
     for (; !bad && t < ntok; t++) {
       const uint32_t en = L.ent[t];
       const uint32_t pos = en & 0xFFFFu;
       if (pos >= ve) break;
-      const uint32_t cls = en >> 24;
+      uint32_t cls = en >> 24;
       const uint32_t adj = pos == prev + 1 ? 1u : 0u;
+      const uint32_t st0 = st;
+      if (proj) {
+        const bool q = cls == JC_Q_FIELD;
+        if (q) cls = JC_Q_OTHER;  // every string takes the "other" paths of the table
+        else if (cls >= JC_Q_LEVEL && cls <= JC_Q_ERROR) cls = JC_Q_OTHER;
+        st = L.dfa[st * kJsonCls2 + cls * 2 + adj];
+        if (st == JS_INKEY_OTHER) khit = q;
+        if (st0 == JS_VAL_OTHER) {
+          inval = true;
+          vstart = pos;
+          ntv = 0;
+          vneg = cls == JC_MINUS;
+        }
+        if (inval) {
+          if (st == JS_KEY || st == JS_END) {  // ',' / '}' after the value
+            inval = false;
+            if (st0 == JS_N_ZERO && vneg && ntv == 2) bad = true;  // -0
+            if (khit) {
+              found = true;
+              fs = vstart;
+              fe = prev + 1;
+            }
+          } else {
+            ntv++;
+            if (st == JS_N_DOT || st == JS_N_E || ntv > 18) bad = true;
+          }
+        }
+      } else {
+        if (st >= JS_INV_D && st <= JS_INV_E) lvl = (int)(st - JS_INV_D);
+        st = L.dfa[st * kJsonCls2 + cls * 2 + adj];
+        // each field at most once (serde derive: duplicate field is an error)
+        const uint32_t fb = st == JS_INKEY_LV ? 1u : st == JS_INKEY_MSG ? 2u : 0u;
+        if (flags & fb) st = JS_FAIL;
+        flags |= fb;
+      }
       prev = pos;
-      if (st >= JS_INV_D && st <= JS_INV_E) lvl = (int)(st - JS_INV_D);
-      st = L.dfa[st * kJsonCls2 + cls * 2 + adj];
-      // each field at most once (serde derive: duplicate field is an error)
-      const uint32_t fb = st == JS_INKEY_LV ? 1u : st == JS_INKEY_MSG ? 2u : 0u;
-      if (flags & fb) st = JS_FAIL;
-      flags |= fb;
     }
-    if (st != JS_END || flags != 3u) bad = true;
-    if (!bad && lvl > 0) atomicOr(&L.match[r >> 5], 1u << (r & 31));
+    if (st != JS_END || (!proj && flags != 3u)) bad = true;
+    if (proj) {
+      if (!bad && found) {
+        atomicOr(&L.match[r >> 5], 1u << (r & 31));
+        L.r_vs[r] = fs;  // the value narrows to the field's text
+        L.r_ve[r] = fe;
+      }
+    } else if (!bad && lvl > 0) {
+      atomicOr(&L.match[r >> 5], 1u << (r & 31));
+    }
   }
-  return __syncthreads_or(bad);
+  return lean_or(L.red, orpar, bad);
 }
 
 // zero every byte between values (record headers, keys, lengths) and build the
@@ -1630,231 +1736,370 @@ __device__ bool lean_json_stage(LeanLdsJ& L, int nr) {
 __device__ __forceinline__ void clear_gaps(LeanLds& L, int nr, uint32_t vs, uint32_t vl) {
   const uint32_t l = threadIdx.x;
   const uint32_t lo = L.r_vs[0], hi = L.r_ve[nr - 1];
-  if ((int)l < nr) {
-    const uint32_t e = (int)l + 1 < nr ? L.r_vs[l + 1] : ((vs + vl + 15) & ~15u) + 16;
-    for (uint32_t p = vs + vl; p < e; p++) L.win[p] = 0;
-  }
-  if (l == 0)
-    for (uint32_t p = lo & ~15u; p < lo; p++) L.win[p] = 0;
+  // [s, e) <- 0: whole aligned dwords inside the range, bytes at its edges (a
+  // dword at an edge may hold another record's value bytes)
+  auto zero = [&](uint32_t s, uint32_t e) {
+    const uint32_t s4 = (s + 3) & ~3u, e4 = e & ~3u;
+    if (s4 >= e4) {
+      for (uint32_t p = s; p < e; p++) L.win[p] = 0;
+      return;
+    }
+    for (uint32_t p = s; p < s4; p++) L.win[p] = 0;
+    for (uint32_t p = s4; p < e4; p += 4) *(uint32_t*)(L.win + p) = 0u;
+    for (uint32_t p = e4; p < e; p++) L.win[p] = 0;
+  };
+  if ((int)l < nr) zero(vs + vl, (int)l + 1 < nr ? L.r_vs[l + 1] : ((vs + vl + 15) & ~15u) + 16);
+  if (l == 0) zero(lo & ~15u, lo);
+  // blk[j] = l for the 64-byte blocks j starting in [vs, next value start)
   if ((int)l < nr) {
     const uint32_t e = (int)l + 1 < nr ? L.r_vs[l + 1] : hi + 80;
-    for (uint32_t j = (vs + 63) >> 6; (j << 6) < e; j++) L.blk[j] = (uint8_t)l;
+    const uint32_t j0 = (vs + 63) >> 6, j1 = (e + 63) >> 6;
+    const uint32_t rep = l * 0x01010101u;
+    uint32_t j = j0;
+    for (; j < j1 && (j & 3u); j++) L.blk[j] = (uint8_t)l;
+    for (; j + 4 <= j1; j += 4) *(uint32_t*)(L.blk + j) = rep;
+    for (; j < j1; j++) L.blk[j] = (uint8_t)l;
   }
   if (l == 0)
     for (uint32_t j = 0; (j << 6) < lo; j++) L.blk[j] = 0xFF;
 }
 
-template <bool kJson>
-__global__ __launch_bounds__(kLeanThreads) void k_eval_lean(EvalArgs a) {
-  __shared__ typename std::conditional<kJson, LeanLdsJ, LeanLds>::type L;
-  const uint32_t b = blockIdx.x;
-  const uint32_t l = threadIdx.x;
-  const ChainDesc& ch = *a.chain;
-  const uint64_t pos = a.bpos[b];
+// the 16-byte aligned window [al, al + wlen) of batch b
+struct LeanWin {
+  uint64_t pos, al;
+  uint32_t wlen;
+};
+__device__ __forceinline__ LeanWin lean_window(const EvalArgs& a, uint32_t b) {
+  LeanWin w;
+  w.pos = a.bpos[b];
   const uint64_t nxt = b + 1 < a.nbatches ? a.bpos[b + 1] : a.slice_len;
-  const uint64_t rb = a.rbase[b];
-  const uint64_t al = pos & ~15ull;
-  uint64_t wl = nxt > al ? nxt - al : 0;
+  w.al = w.pos & ~15ull;
+  uint64_t wl = nxt > w.al ? nxt - w.al : 0;
   if (wl > (uint64_t)kLeanWin) wl = kLeanWin;
-  const uint32_t wlen = (uint32_t)((wl + 15) & ~15ull);
-  // 1. stage [al, al + wlen): 1 KiB LDS-DMA pieces, the last one partial
+  w.wlen = (uint32_t)((wl + 15) & ~15ull);
+  return w;
+}
+// 1 KiB LDS-DMA pieces (one 16-byte piece per lane), the last one partial;
+// the waves split the pieces
+__device__ __forceinline__ void lean_issue(const EvalArgs& a, const LeanWin& w, uint8_t* dst) {
+  const uint32_t l = threadIdx.x, lane = l & 63u;
+  const uint8_t* src = a.slice + w.al + lane * 16;
+  for (uint32_t k = __builtin_amdgcn_readfirstlane(l >> 6); k * 1024 < w.wlen; k += kLeanThreads / 64)
+    if (k * 1024 + lane * 16 < w.wlen)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + k * 1024),
+                                       (__attribute__((address_space(3))) void*)(dst + k * 1024), 16, 0, 0);
+}
+
+// four waves per SIMD (eight workgroups per CU, as many as the LDS holds)
+template <bool kJson>
+__global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJson ? 1 : 4))) void k_eval_lean(EvalArgs a) {
+  __shared__ typename std::conditional<kJson, LeanLdsJ, LeanLds>::type L;
+  const uint32_t l = threadIdx.x;
+  const uint32_t G = gridDim.x;
+  uint32_t b = blockIdx.x;
+  if (b >= a.nbatches) return;
+  // the chain's stages, needles, regex rows and JSON tables: LDS, once
   {
-    const uint32_t lane = l & 63u;
-    const uint8_t* src = a.slice + al + lane * 16;
-    for (uint32_t k = __builtin_amdgcn_readfirstlane(l >> 6); k * 1024 < wlen; k += kLeanThreads / 64)
-      if (k * 1024 + lane * 16 < wlen)
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + k * 1024),
-                                         (__attribute__((address_space(3))) void*)(L.win + k * 1024), 16, 0, 0);
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-  }
-  // batch header (file format, batch.rs:163-180), read before the gaps are cleared
-  const uint8_t* h = L.win + (pos - al);
-  const int64_t base_offset = (int64_t)rd_be(h, 8);
-  const uint32_t batch_len = (uint32_t)rd_be(h + 8, 4);
-  const int32_t lod_in = (int32_t)rd_be(h + 23, 4);
-  const int64_t first_ts = (int64_t)rd_be(h + 27, 8);
-  const uint64_t sec0 = pos + 57;
-  const uint64_t sec_end = pos + 12 + (uint64_t)batch_len;  // framing validated at ingest
-  const uint32_t sec_len = (uint32_t)(sec_end - sec0);
-  const int32_t count = sec_len >= 4 ? (int32_t)rd_be(L.win + (sec0 - al), 4) : -1;
-  bool defer = sec_len < 4 || sec_end - al > (uint64_t)wlen || count < 0 || count > kLeanMaxR;
-  // 2. framing: lane 0 chases the lengths (one LDS round trip per record when
-  //    the length varint has <= 4 bytes), lane r parses record r
-  const uint32_t have = (uint32_t)(sec_end - al);
-  if (!defer && l == 0) {
-    uint32_t q = (uint32_t)(sec0 + 4 - al);
-    int n = 0;
-    for (; n < count; n++) {
-      const uint32_t q0 = q;
-      int64_t len;
-      const uint32_t x = lds_u32_at(L.win, q);
-      const uint32_t term = ~x & 0x80808080u;
-      const uint32_t nb = term ? (((uint32_t)__builtin_ctz(term)) >> 3) + 1 : 5u;
-      if (nb <= 4 && q + nb <= have) {
-        const uint32_t y = nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u));
-        const uint32_t v = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
-        len = (v & 1u) ? -(int64_t)(v >> 1) - 1 : (int64_t)(v >> 1);  // zigzag
-        q += nb;
-      } else if (wvarint((const uint8_t*)L.win, q, have, &len)) {
-        break;
+    const ChainDesc& ch = *a.chain;
+    const uint32_t nst = ch.nstages;
+    uint32_t nrx = 0, rx = 0xFFu, ndo = 0;
+    for (uint32_t s = 0; s < nst; s++)
+      if (ch.st[s].op == OP_CONTAINS || ch.st[s].op == OP_PROJECT) ndo += ch.st[s].needle_len;
+    const bool nd_res = ndo <= (uint32_t)kLeanNeedles;
+    ndo = 0;
+    for (uint32_t s = 0; s < nst; s++) {
+      const StageDesc& sd = ch.st[s];
+      if (sd.op == OP_REGEX) {
+        nrx++;
+        rx = s;
       }
-      if (len < 0 || (int64_t)(have - q) < len) break;
-      L.r_start[n] = q0;
-      q += (uint32_t)len;
+      if (l == 0) {
+        LeanStage g;
+        g.op = sd.op;
+        g.upper = sd.in_type == VT_SRC_UPPER ? 1 : 0;
+        g.keep_match = sd.keep_match;
+        g.pad = 0;
+        g.m = sd.needle_len;
+        g.max_len = (uint32_t)sd.dfa.max_len;
+        g.s_bot = sd.dfa.s_bot;
+        g.s_mid = sd.dfa.s_mid;
+        g.acc1 = sd.dfa.acc1;
+        g.acc2 = sd.dfa.acc2;
+        g.tt = sd.in_type == VT_SRC_UPPER ? sd.dfa.tt_up : sd.dfa.tt;
+        g.nd = sd.needle;
+        g.nd_off = ndo;
+        L.stg[s] = g;
+      }
+      if ((sd.op == OP_CONTAINS || sd.op == OP_PROJECT) && nd_res) {
+        for (uint32_t t = l; t < sd.needle_len; t += kLeanThreads) L.needles[ndo + t] = a.blob[sd.needle + t];
+        ndo += sd.needle_len;
+      }
     }
-    L.r_start[n] = q;
-    L.chase_bad = n < count ? 1u : 0u;
+    if (nrx == 1) {  // one regex stage: its rows stay resident
+      const StageDesc& sd = ch.st[rx];
+      const uint64_t* tt = (const uint64_t*)(a.blob + (sd.in_type == VT_SRC_UPPER ? sd.dfa.tt_up : sd.dfa.tt));
+      for (uint32_t t = l; t < 256; t += kLeanThreads) L.tt[t] = tt[t];
+    }
+    if (l == 0) {
+      L.nst = nst;
+      L.out_upper = ch.out_type == VT_SRC_UPPER ? 1u : 0u;
+      L.tt_stage = nrx == 1 ? rx : 0xFFu;
+      L.nd_res = nd_res ? 1u : 0u;
+    }
+    if constexpr (kJson) {
+      for (uint32_t t = l; t < (uint32_t)(kJsonStates * kJsonCls2); t += kLeanThreads) L.dfa[t] = g_json_tables.t[t];
+      for (uint32_t t = l; t < 256; t += kLeanThreads) L.bcls[t] = g_json_tables.bcls[t];
+    }
   }
-  __syncthreads();
-  // a failed chase leaves the lengths unverified: the exact walk decides
-  if (!defer) defer = __builtin_amdgcn_readfirstlane(L.chase_bad) != 0u;
-  const int nr = defer ? 0 : count;
-  bool g = true;
-  int64_t ts = 0, od = 0, hdr = 0;
-  uint32_t vs = 0, vl = 0, kpos = 0, klen = 0;
-  uint8_t attr = 0, tag = 0;
-  if ((int)l < nr) {
-    uint32_t q = L.r_start[l];
-    const uint32_t lim = L.r_start[l + 1];
-    int64_t len, kl, vlen;
-    g = !wvarint((const uint8_t*)L.win, q, lim, &len);
-    if (g && q < lim) attr = L.win[q++]; else g = false;
-    g = g && !wvarint((const uint8_t*)L.win, q, lim, &ts) && !wvarint((const uint8_t*)L.win, q, lim, &od);
-    if (g && q < lim) tag = L.win[q++]; else g = false;
-    g = g && tag <= 1;
-    if (g && tag == 1) {
-      g = !wvarint((const uint8_t*)L.win, q, lim, &kl) && kl >= 0 && (uint64_t)q + (uint64_t)kl <= lim;
+  uint32_t par = 0;  // lean_or pair
+  // the previous batch's results, stored once the next window is in flight
+  // (a store issued right before the wait for the next window would be waited for too)
+  uint32_t p_b = 0xFFFFFFFFu;
+  bool p_defer = false, p_kept = false;
+  uint64_t p_idx = 0;
+  KeptRec p_d = {};
+  int64_t p_base = 0, p_ts0 = 0;
+  int32_t p_lod = 0;
+  uint32_t p_nkeep = 0, p_sec = 0;
+  auto flush = [&]() {
+    if (p_b == 0xFFFFFFFFu) return;
+    if (p_defer) {
+      if (l == 0) {
+        const uint32_t i = atomicAdd(&a.list[0], 1u);
+        a.list[1 + i] = p_b;
+      }
+    } else {
+      if (p_kept) a.desc[p_idx] = p_d;
+      if (l == 0) {
+        BatchStat st = {};
+        st.base_offset = p_base;
+        st.lod_in = p_lod;
+        st.first_ts = p_ts0;
+        st.flags = BF_LAST_STAGE;
+        st.nkeep = p_nkeep;
+        st.nout = p_nkeep;
+        st.sec_len = p_sec;
+        st.err_stage = 0xFFFFFFFFu;
+        a.bstat[p_b] = st;
+      }
+    }
+    p_b = 0xFFFFFFFFu;
+  };
+  for (;;) {
+    lean_sync();  // every lane is done with the previous batch's window
+    const LeanWin W = lean_window(a, b);
+    const uint64_t pos = W.pos, al = W.al;
+    const uint32_t wlen = W.wlen;
+    const uint64_t rb = a.rbase[b];
+    const uint32_t bn = b + G;
+    lean_issue(a, W, L.win);
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's pieces have landed
+    lean_sync();                    // ... and the other wave's
+    // batch header (file format, batch.rs:163-180), read before the gaps are cleared
+    const uint8_t* h = L.win + (pos - al);
+    const int64_t base_offset = (int64_t)rd_be(h, 8);
+    const uint32_t batch_len = (uint32_t)rd_be(h + 8, 4);
+    const int32_t lod_in = (int32_t)rd_be(h + 23, 4);
+    const int64_t first_ts = (int64_t)rd_be(h + 27, 8);
+    const uint64_t sec0 = pos + 57;
+    const uint64_t sec_end = pos + 12 + (uint64_t)batch_len;  // framing validated at ingest
+    const uint32_t sec_len = (uint32_t)(sec_end - sec0);
+    const int32_t count = sec_len >= 4 ? (int32_t)rd_be(L.win + (sec0 - al), 4) : -1;
+    bool defer = sec_len < 4 || sec_end - al > (uint64_t)wlen || count < 0 || count > kLeanMaxR;
+    // 2. framing: wave 0 chases the lengths with wave-uniform (scalar) values,
+    //    one LDS round trip per record when the length varint has <= 4 bytes;
+    //    lane n keeps the start of record n.  Lane r then parses record r.
+    const uint32_t have = (uint32_t)(sec_end - al);
+    if (!defer && l < 64) {
+      uint32_t q = (uint32_t)(sec0 + 4 - al);
+      uint32_t my = 0;
+      int n = 0;
+      for (; n < count; n++) {
+        const uint32_t q0 = q;
+        const uint32_t x = __builtin_amdgcn_readfirstlane(lds_u32_at(L.win, q));
+        const uint32_t term = ~x & 0x80808080u;
+        int64_t len;
+        if (term) {
+          const uint32_t nb = (((uint32_t)__builtin_ctz(term)) >> 3) + 1;
+          if (q + nb > have) break;
+          const uint32_t y = nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u));
+          const uint32_t v = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
+          len = (v & 1u) ? -(int64_t)(v >> 1) - 1 : (int64_t)(v >> 1);  // zigzag
+          q += nb;
+        } else if (wvarint((const uint8_t*)L.win, q, have, &len)) {
+          break;
+        }
+        if (len < 0 || (int64_t)(have - q) < len) break;
+        if ((int)l == n) my = q0;
+        q += (uint32_t)len;
+      }
+      if ((int)l < n) L.r_start[l] = my;
+      if (l == 0) {
+        L.r_start[n] = q;
+        L.chase_bad = n < count ? 1u : 0u;
+      }
+    }
+    lean_sync();
+    // a failed chase leaves the lengths unverified: the exact walk decides
+    if (!defer) defer = __builtin_amdgcn_readfirstlane(L.chase_bad) != 0u;
+    const int nr = defer ? 0 : count;
+    bool g = true;
+    int64_t ts = 0, od = 0, hdr = 0;
+    uint32_t vs = 0, vl = 0, kpos = 0, klen = 0;
+    uint8_t attr = 0, tag = 0;
+    if ((int)l < nr) {
+      uint32_t q = L.r_start[l];
+      const uint32_t lim = L.r_start[l + 1];
+      int64_t len, kl, vlen;
+      g = !wvarint((const uint8_t*)L.win, q, lim, &len);
+      if (g && q < lim) attr = L.win[q++]; else g = false;
+      g = g && !wvarint((const uint8_t*)L.win, q, lim, &ts) && !wvarint((const uint8_t*)L.win, q, lim, &od);
+      if (g && q < lim) tag = L.win[q++]; else g = false;
+      g = g && tag <= 1;
+      if (g && tag == 1) {
+        g = !wvarint((const uint8_t*)L.win, q, lim, &kl) && kl >= 0 && (uint64_t)q + (uint64_t)kl <= lim;
+        if (g) {
+          kpos = q;
+          klen = (uint32_t)kl;
+          q += klen;
+        }
+      }
+      g = g && !wvarint((const uint8_t*)L.win, q, lim, &vlen) && vlen >= 0 && (uint64_t)q + (uint64_t)vlen <= lim;
+      vs = q;
       if (g) {
-        kpos = q;
-        klen = (uint32_t)kl;
-        q += klen;
+        vl = (uint32_t)vlen;
+        q += vl;
       }
+      g = g && !wvarint((const uint8_t*)L.win, q, lim, &hdr) && q == lim;
+      L.r_vs[l] = vs;
+      L.r_ve[l] = vs + vl;
     }
-    g = g && !wvarint((const uint8_t*)L.win, q, lim, &vlen) && vlen >= 0 && (uint64_t)q + (uint64_t)vlen <= lim;
-    vs = q;
-    if (g) {
-      vl = (uint32_t)vlen;
-      q += vl;
-    }
-    g = g && !wvarint((const uint8_t*)L.win, q, lim, &hdr) && q == lim;
-    L.r_vs[l] = vs;
-    L.r_ve[l] = vs + vl;
-  }
-  defer = __syncthreads_or(defer || !g);  // a record that does not frame exactly
-  uint64_t alive = __ballot((int)l < nr);
-  // 3. stages.  Before the first scan every non-value byte of the scanned
-  //    range is cleared (record headers, keys, lengths): then the OR of the
-  //    scanned words has a high bit iff some value is non-ASCII.
-  bool checked = false;  // every value known ASCII (from_utf8 cannot fail)
-  bool cleared = false;  // gap bytes zeroed, record block table built
-  for (uint32_t s = 0; !defer && s < ch.nstages; s++) {
-    const StageDesc& sd = ch.st[s];
-    if (sd.op == OP_MAP_UPPER) continue;  // representation only
-    if constexpr (kJson) if (sd.op == OP_FILTER_JSON) {
+    defer = lean_or(L.red, par, defer || !g);  // a record that does not frame exactly
+    uint64_t alive = __ballot((int)l < nr);
+    // 3. stages.  Before the first scan every non-value byte of the scanned
+    //    range is cleared (record headers, keys, lengths): then the OR of the
+    //    scanned words has a high bit iff some value is non-ASCII.
+    bool checked = false;  // every value known ASCII (from_utf8 cannot fail)
+    bool cleared = false;  // gap bytes zeroed, record block table built
+    const uint32_t nst = __builtin_amdgcn_readfirstlane(L.nst);
+    for (uint32_t s = 0; !defer && s < nst; s++) {
+      const LeanStage sd = L.stg[s];
+      const uint32_t op = __builtin_amdgcn_readfirstlane((uint32_t)sd.op);
+      if (op == OP_MAP_UPPER) continue;  // representation only
+      if constexpr (kJson) if (op == OP_FILTER_JSON || op == OP_PROJECT) {
+        const bool proj = op == OP_PROJECT;
+        const uint32_t fl = proj ? __builtin_amdgcn_readfirstlane(sd.m) : 0u;
+        if (l == 0) {
+          L.match[0] = 0;
+          L.match[1] = 0;
+        }
+        if (proj) {  // the field name (<= kLeanNeedle bytes: the runtime checks)
+          if (__builtin_amdgcn_readfirstlane(L.nd_res)) {
+            const uint32_t o = __builtin_amdgcn_readfirstlane(sd.nd_off);
+            for (uint32_t t = l; t < fl; t += kLeanThreads) L.needle[t] = L.needles[o + t];
+          } else {
+            const uint8_t* nd = a.blob + __builtin_amdgcn_readfirstlane(sd.nd);
+            for (uint32_t t = l; t < fl; t += kLeanThreads) L.needle[t] = nd[t];
+          }
+        }
+        if (!cleared && nr > 0) {
+          clear_gaps(L, nr, vs, vl);
+          cleared = true;
+        }
+        lean_sync();
+        if (nr > 0 && lean_json_stage(L, nr, par, proj, fl)) {
+          defer = true;
+          break;
+        }
+        alive &= __ballot(l < 64 && ((L.match[(l >> 5) & 1] >> (l & 31)) & 1u));
+        if (proj && (int)l < nr) {  // lane l keeps record l's (narrowed) value span
+          vs = L.r_vs[l];
+          vl = L.r_ve[l] - vs;
+        }
+        lean_sync();
+        continue;
+      }
+      const bool rx = op == OP_REGEX;
+      const uint32_t m = __builtin_amdgcn_readfirstlane(sd.m);
+      if (!rx && m == 0 && checked) continue;  // an empty needle keeps every (UTF-8) value
+      if (nr == 0) break;
+      const uint32_t lo = L.r_vs[0], hi = L.r_ve[nr - 1];
+      if (!cleared) {
+        clear_gaps(L, nr, vs, vl);
+        cleared = true;
+      }
       if (l == 0) {
         L.match[0] = 0;
         L.match[1] = 0;
       }
-      for (uint32_t t = l; t < (uint32_t)(kJsonStates * kJsonCls2); t += kLeanThreads) L.dfa[t] = g_json_tables.t[t];
-      for (uint32_t t = l; t < 256; t += kLeanThreads) L.bcls[t] = g_json_tables.bcls[t];
-      if (!cleared && nr > 0) {
-        clear_gaps(L, nr, vs, vl);
-        cleared = true;
+      const bool upper = sd.upper != 0;
+      if (rx) {
+        if (__builtin_amdgcn_readfirstlane(L.tt_stage) != s) {  // several regex stages: rows per stage
+          const uint64_t* tt = (const uint64_t*)(a.blob + __builtin_amdgcn_readfirstlane(sd.tt));
+          lean_sync();  // every lane is done with the previous rows
+          for (uint32_t t = l; t < 256; t += kLeanThreads) L.tt[t] = tt[t];
+        }
+        lean_sync();
+        const uint32_t orw = lean_regex(L, nr, lo, hi, sd.max_len, sd.s_bot, sd.s_mid, sd.acc1, sd.acc2);
+        const bool high = lean_or(L.red, par, (orw & 0x80808080u) != 0u);  // also orders the match bits
+        if (!checked && high) defer = true;  // a non-ASCII value: exact UTF-8 / Unicode DFA path
+        checked = true;
+        const bool hit = l < 64 && ((L.match[(l >> 5) & 1] >> (l & 31)) & 1u);
+        alive &= __ballot(sd.keep_match ? hit : !hit);
+        lean_sync();  // match is rewritten by the next stage
+        continue;
       }
-      __syncthreads();
-      if (nr > 0 && lean_json_stage(L, nr)) {
-        defer = true;
+      if (m > (uint32_t)kLeanNeedle) {
+        defer = true;  // long needle: exact kernel
         break;
       }
-      alive &= __ballot(l < 64 && ((L.match[(l >> 5) & 1] >> (l & 31)) & 1u));
-      __syncthreads();
-      continue;
-    }
-    const bool rx = sd.op == OP_REGEX;
-    const uint32_t m = sd.needle_len;
-    if (!rx && m == 0 && checked) continue;  // an empty needle keeps every (UTF-8) value
-    if (nr == 0) break;
-    const uint32_t lo = L.r_vs[0], hi = L.r_ve[nr - 1];
-    if (!cleared) {
-      clear_gaps(L, nr, vs, vl);
-      cleared = true;
-    }
-    if (l == 0) {
-      L.match[0] = 0;
-      L.match[1] = 0;
-    }
-    if (rx) {
-      const bool upper = sd.in_type == VT_SRC_UPPER;
-      const uint64_t* tt = (const uint64_t*)(a.blob + (upper ? sd.dfa.tt_up : sd.dfa.tt));
-      for (uint32_t t = l; t < 256; t += kLeanThreads) L.tt[t] = tt[t];
-      __syncthreads();
-      const uint32_t orw = lean_regex(L, nr, lo, hi, (uint32_t)sd.dfa.max_len, sd.dfa.s_bot, sd.dfa.s_mid,
-                                      sd.dfa.acc1, sd.dfa.acc2);
-      const bool high = __syncthreads_or((orw & 0x80808080u) != 0u);  // also orders the match bits
-      if (!checked && high) defer = true;  // a non-ASCII value: exact UTF-8 / Unicode DFA path
+      if (__builtin_amdgcn_readfirstlane(L.nd_res)) {
+        const uint32_t o = __builtin_amdgcn_readfirstlane(sd.nd_off);
+        for (uint32_t t = l; t < m; t += kLeanThreads) L.needle[t] = L.needles[o + t];
+      } else {
+        const uint8_t* nd = a.blob + __builtin_amdgcn_readfirstlane(sd.nd);
+        for (uint32_t t = l; t < m; t += kLeanThreads) L.needle[t] = nd[t];
+      }
+      lean_sync();
+      uint32_t orw;
+      if (m >= 7) orw = lean_scan<0>(L, nr, lo, hi, nullptr, m, upper);
+      else if (m >= 4) orw = lean_scan<1>(L, nr, lo, hi, nullptr, m, upper);
+      else if (m > 0) orw = lean_scan<2>(L, nr, lo, hi, nullptr, m, upper);
+      else orw = lean_scan<3>(L, nr, lo, hi, nullptr, m, upper);
+      const bool high = lean_or(L.red, par, (orw & 0x80808080u) != 0u);  // also orders the match bits
+      if (!checked && high) defer = true;  // a non-ASCII value: exact UTF-8 path
       checked = true;
-      const bool hit = l < 64 && ((L.match[(l >> 5) & 1] >> (l & 31)) & 1u);
-      alive &= __ballot(sd.keep_match ? hit : !hit);
-      __syncthreads();  // match / tt are rewritten by the next stage
-      continue;
+      if (m > 0) alive &= __ballot(l < 64 && ((L.match[(l >> 5) & 1] >> (l & 31)) & 1u));
+      lean_sync();  // match / needle are rewritten by the next stage
     }
-    const uint8_t* nd = a.blob + sd.needle;
-    if (m > (uint32_t)kLeanNeedle) {
-      defer = true;  // long needle: exact kernel
-      break;
+    // 4. survivors -> descriptors (stored by the next iteration's flush)
+    p_b = b;
+    p_defer = defer;
+    p_kept = !defer && l < 64 && ((alive >> (l & 63)) & 1ull);
+    if (p_kept) {
+      p_idx = rb + __popcll(alive & ((1ull << l) - 1ull));
+      p_d.src = al + L.r_start[l];
+      p_d.vpos = al + vs;
+      p_d.kpos = tag ? al + kpos : 0;
+      p_d.od = od;
+      p_d.ts = ts;
+      p_d.hdr = hdr;
+      p_d.vlen = vl;
+      p_d.klen = klen;
+      p_d.ival = 0;
+      p_d.mode = L.out_upper ? KM_UPPER : KM_COPY;
+      p_d.has_key = tag;
+      p_d.attr = attr;
+      p_d.pad = 0;
     }
-    for (uint32_t t = l; t < m; t += kLeanThreads) L.needle[t] = nd[t];
-    __syncthreads();
-    const bool upper = sd.in_type == VT_SRC_UPPER;
-    uint32_t orw;
-    if (m >= 7) orw = lean_scan<0>(L, nr, lo, hi, nd, m, upper);
-    else if (m >= 4) orw = lean_scan<1>(L, nr, lo, hi, nd, m, upper);
-    else if (m > 0) orw = lean_scan<2>(L, nr, lo, hi, nd, m, upper);
-    else orw = lean_scan<3>(L, nr, lo, hi, nd, m, upper);
-    const bool high = __syncthreads_or((orw & 0x80808080u) != 0u);  // also orders the match bits
-    if (!checked && high) defer = true;  // a non-ASCII value: exact UTF-8 path
-    checked = true;
-    if (m > 0) alive &= __ballot(l < 64 && ((L.match[(l >> 5) & 1] >> (l & 31)) & 1u));
-    __syncthreads();  // match / needle are rewritten by the next stage
-  }
-  if (defer) {
-    if (l == 0) {
-      const uint32_t i = atomicAdd(&a.list[0], 1u);
-      a.list[1 + i] = b;
-    }
-    return;
-  }
-  // 4. survivors -> descriptors
-  const bool kept = l < 64 && ((alive >> (l & 63)) & 1ull);
-  if (kept) {
-    KeptRec d;
-    d.src = al + L.r_start[l];
-    d.vpos = al + vs;
-    d.kpos = tag ? al + kpos : 0;
-    d.od = od;
-    d.ts = ts;
-    d.hdr = hdr;
-    d.vlen = vl;
-    d.klen = klen;
-    d.ival = 0;
-    d.mode = ch.out_type == VT_SRC_UPPER ? KM_UPPER : KM_COPY;
-    d.has_key = tag;
-    d.attr = attr;
-    d.pad = 0;
-    a.desc[rb + __popcll(alive & ((1ull << l) - 1ull))] = d;
-  }
-  if (l == 0) {
-    BatchStat st = {};
-    st.base_offset = base_offset;
-    st.lod_in = lod_in;
-    st.first_ts = first_ts;
-    st.flags = BF_LAST_STAGE;
-    st.nkeep = (uint32_t)__popcll(alive);
-    st.nout = st.nkeep;
-    st.sec_len = sec_len;
-    st.err_stage = 0xFFFFFFFFu;
-    a.bstat[b] = st;
+    p_base = base_offset;
+    p_ts0 = first_ts;
+    p_lod = lod_in;
+    p_nkeep = (uint32_t)__popcll(alive);
+    p_sec = sec_len;
+    flush();
+    if (bn >= a.nbatches) break;
+    b = bn;
   }
 }
 
@@ -2592,26 +2837,40 @@ __device__ __forceinline__ uint32_t crc_shift_bytes(uint32_t c, uint64_t n) {
   return c;
 }
 
+// One 64 KiB chunk per workgroup iteration; the next chunk's blocks are loaded
+// (into registers) while this one is folded, and the barriers wait for LDS
+// only, so the loads stay in flight.
 __global__ __launch_bounds__(kCrcThreads) void k_crc16(const uint8_t* __restrict__ out, uint64_t skip,
                                                         uint64_t nblocks, uint32_t* acc) {
   __shared__ uint32_t z[16][256];
   __shared__ uint32_t sh[9][4][256];  // shifts by 16 B .. 4 KiB (2^4 .. 2^12 bytes)
-  __shared__ uint32_t red[kCrcThreads / 64];
+  __shared__ uint32_t red[2][kCrcThreads / 64];
   const uint32_t t = threadIdx.x;
+  const uint4* base = (const uint4*)(out + 16);
+  const uint64_t nchunks = (nblocks + kCrcChunkBlocks - 1) / kCrcChunkBlocks;
+  uint64_t ch = blockIdx.x;
+  if (ch >= nchunks) return;
+  // blocks of chunk c: unconditional loads, clamped to the last block (a
+  // conditional load would be waited for at once)
+  auto fetch = [&](uint64_t c, uint4 (&v)[kCrcIters]) {
+    const uint64_t b0 = c * kCrcChunkBlocks;
+#pragma unroll
+    for (int i = 0; i < kCrcIters; i++) {
+      const uint64_t j = b0 + t + (uint32_t)i * kCrcThreads;
+      v[i] = base[j < nblocks ? j : nblocks - 1];
+    }
+  };
+  uint4 v[kCrcIters], nv[kCrcIters];
+  fetch(ch, v);
   for (uint32_t i = t; i < 16 * 256; i += kCrcThreads) (&z[0][0])[i] = (&g_crc_z16[0][0])[i];
   for (uint32_t i = t; i < 9 * 4 * 256; i += kCrcThreads) (&sh[0][0][0])[i] = (&g_crc_shift[4][0][0])[i];
   __syncthreads();
-  const uint4* base = (const uint4*)(out + 16);
-  const uint64_t nchunks = (nblocks + kCrcChunkBlocks - 1) / kCrcChunkBlocks;
-  for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+  uint32_t par = 0;
+  for (;;) {
+    const uint64_t chn = ch + gridDim.x;
+    fetch(chn < nchunks ? chn : ch, nv);  // the last iteration re-reads its own chunk
     const uint64_t b0 = ch * kCrcChunkBlocks;
     const uint32_t nb = (uint32_t)(nblocks - b0 < kCrcChunkBlocks ? nblocks - b0 : kCrcChunkBlocks);
-    uint4 v[kCrcIters];
-#pragma unroll
-    for (int i = 0; i < kCrcIters; i++) {
-      const uint32_t j = t + (uint32_t)i * kCrcThreads;
-      if (j < nb) v[i] = base[b0 + j];
-    }
     if (b0 == 0 && t == 0) {  // bytes [16, 16 + skip) precede the CRC region
       uint32_t w[4] = {v[0].x, v[0].y, v[0].z, v[0].w};
 #pragma unroll
@@ -2643,17 +2902,21 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc16(const uint8_t* __restrict
       for (int k = 0; k < 8; k++)
         if ((d >> k) & 1) c = crc_shift_tab(sh[k], c);
     }
-    // workgroup XOR reduce
+    // workgroup XOR reduce (alternating slots: one LDS-only barrier)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) c ^= __shfl_xor(c, o, 64);
-    if ((t & 63) == 0) red[t >> 6] = c;
-    __syncthreads();
+    if ((t & 63) == 0) red[par][t >> 6] = c;
+    lean_sync();
     if (t == 0) {
-      uint32_t x = red[0] ^ red[1] ^ red[2] ^ red[3];
+      uint32_t x = red[par][0] ^ red[par][1] ^ red[par][2] ^ red[par][3];
       x = crc_shift_bytes(x, (nblocks - b0 - nb) * 16ull);  // to the end of the aligned region
       atomicXor(acc, x);
     }
-    __syncthreads();
+    par ^= 1u;
+    if (chn >= nchunks) break;
+    ch = chn;
+#pragma unroll
+    for (int i = 0; i < kCrcIters; i++) v[i] = nv[i];
   }
 }
 
@@ -2667,6 +2930,245 @@ __global__ void k_crc_final(uint8_t* out, const uint32_t* acc, uint64_t tail0, u
   out[18] = (uint8_t)(crc >> 16);
   out[19] = (uint8_t)(crc >> 8);
   out[20] = (uint8_t)crc;
+}
+
+// ---------------------------------------------------------------------------
+// k_write_lean: the output of one batch of verbatim records (KM_COPY /
+// KM_UPPER: filters, uppercase maps, projections) assembled in LDS and stored
+// with 16-byte stores, for batches of many small records (where k_write's
+// record-by-record wave copies leave the memory system idle).
+//   1. wave 0, lane = record: size, wave scan, the varint fields written into
+//      the staging buffer, the key / value segments into a table
+//   2. all threads: segment bytes global -> LDS in 16-byte units aligned like
+//      the output (interior units one LDS store, edge units bytewise), four
+//      units per round with every load in flight before the first use
+//   3. LDS -> HBM: interior units dwordx4 stores, the two edge units bytewise
+// A batch with more than 64 survivors or more bytes than the staging buffer
+// is written by the generic wave path (write_batch_wave).
+// (A CRC computed from the staging buffer was measured: 64-byte pieces
+// combined with GF(2) multiplies cost more VALU than the separate k_crc16 pass.)
+// ---------------------------------------------------------------------------
+constexpr int kWlThreads = 256;
+constexpr int kObuf = 17408;  // staging bytes (one 16 KiB batch + re-encoding growth + alignment)
+struct __attribute__((aligned(16))) WlLds {
+  uint8_t ob[kObuf + 16];
+  uint64_t s_src[128];   // segment source offsets (key and value of up to 64 records)
+  uint32_t s_dst[128];   // staging offset
+  uint32_t s_len[128];   // length | upper << 31
+  uint32_t s_upre[129];  // exclusive prefix of the segments' 16-byte units
+  uint32_t total, nunits, big;
+};
+
+// the generic writer of one batch (k_write's body), wave-wide
+__device__ void write_batch_wave(const WriteArgs& a, const KeptRec* d, uint32_t nkeep, int64_t rel, uint64_t obase) {
+  const uint32_t lane = lane_id();
+  uint8_t* out = a.out;
+  uint64_t run = 0;
+  for (uint32_t k0 = 0; k0 < nkeep; k0 += 64) {
+    const uint32_t k = k0 + lane;
+    const bool v = k < nkeep;
+    KeptRec r = {};
+    uint32_t sz = 0;
+    if (v) {
+      r = d[k];
+      sz = rec_out_size(r, rel, 0, 0);
+    }
+    const uint64_t incl = wave_incl_scan((uint64_t)sz);
+    const uint64_t my = obase + run + incl - sz;
+    uint64_t kd = 0, vd = 0;
+    uint32_t kl = 0, vc = 0;
+    if (v) {
+      uint8_t* q = out + my;
+      const uint32_t vl = r.vlen;
+      const uint32_t inner = 1 + vsize(r.ts) + vsize(r.od + rel) + 1 +
+                             (r.has_key ? vsize((int64_t)r.klen) + r.klen : 0) + vsize((int64_t)vl) + vl + vsize(r.hdr);
+      uint8_t t[16];
+      uint32_t n = venc((int64_t)inner, t), w = 0;
+      for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
+      q[w++] = r.attr;
+      n = venc(r.ts, t);
+      for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
+      n = venc(r.od + rel, t);
+      for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
+      q[w++] = r.has_key ? 1 : 0;
+      if (r.has_key) {
+        n = venc((int64_t)r.klen, t);
+        for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
+        kd = my + w;
+        kl = r.klen;
+        w += r.klen;
+      }
+      n = venc((int64_t)vl, t);
+      for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
+      vd = my + w;
+      vc = vl;
+      w += vl;
+      n = venc(r.hdr, t);
+      for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
+    }
+    const uint32_t nrec = nkeep - k0 < 64u ? nkeep - k0 : 64u;
+    for (uint32_t i = 0; i < nrec; i++) {
+      const uint32_t rkl = __builtin_amdgcn_readlane(kl, i);
+      const uint32_t rvc = __builtin_amdgcn_readlane(vc, i);
+      if (rkl) copy_seg(out, a.slice, readlane_u64(kd, i), readlane_u64(r.kpos, i), rkl, false);
+      if (rvc)
+        copy_seg(out, a.slice, readlane_u64(vd, i), readlane_u64(r.vpos, i), rvc,
+                 __builtin_amdgcn_readlane((uint32_t)r.mode, i) == KM_UPPER);
+    }
+    run += readlane_u64(incl, 63);
+  }
+}
+
+__global__ __launch_bounds__(kWlThreads) void k_write_lean(WriteArgs a) {
+  __shared__ WlLds L;
+  const Plan p = *a.plan;
+  const int32_t b = p.first + (int32_t)blockIdx.x;
+  if (p.first < 0 || b > p.last) return;
+  const uint32_t t = threadIdx.x, lane = t & 63u;
+  const BatchStat st = a.bstat[b];
+  const int64_t rel = a.bstat[p.first].base_offset - st.base_offset;
+  const KeptRec* d = a.desc + a.rbase[b];
+  const uint64_t obase = 61 + (a.pre[b].rec_bytes - a.pre[p.first].rec_bytes);
+  const uint32_t d0 = (uint32_t)(obase & 15);
+  const uint32_t nk = st.nkeep;
+  // 1. headers and segments
+  if (t < 64) {
+    const bool v = lane < nk && nk <= 64;
+    KeptRec r = {};
+    uint32_t sz = 0;
+    if (v) {
+      r = d[lane];
+      sz = rec_out_size(r, rel, 0, 0);
+    }
+    const uint32_t incl = wave_incl_scan(sz);
+    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+    const bool big = nk > 64 || d0 + total > (uint32_t)kObuf;
+    uint32_t uk = 0, uv = 0;
+    if (v && !big) {
+      const uint32_t off = d0 + incl - sz;
+      uint8_t* q = L.ob + off;
+      const uint32_t vl = r.vlen;
+      const uint32_t inner = 1 + vsize(r.ts) + vsize(r.od + rel) + 1 +
+                             (r.has_key ? vsize((int64_t)r.klen) + r.klen : 0) + vsize((int64_t)vl) + vl + vsize(r.hdr);
+      uint32_t w = venc((int64_t)inner, q);  // varints straight into the staging buffer
+      q[w++] = r.attr;
+      w += venc(r.ts, q + w);
+      w += venc(r.od + rel, q + w);
+      q[w++] = r.has_key ? 1 : 0;
+      uint32_t kdst = off + w;
+      if (r.has_key) {
+        w += venc((int64_t)r.klen, q + w);
+        kdst = off + w;
+        w += r.klen;
+      }
+      w += venc((int64_t)vl, q + w);
+      const uint32_t vdst = off + w;
+      w += vl;
+      w += venc(r.hdr, q + w);
+      const uint32_t kl = r.has_key ? r.klen : 0u;
+      L.s_src[2 * lane] = r.kpos;
+      L.s_dst[2 * lane] = kdst;
+      L.s_len[2 * lane] = kl;
+      L.s_src[2 * lane + 1] = r.vpos;
+      L.s_dst[2 * lane + 1] = vdst;
+      L.s_len[2 * lane + 1] = vl | (r.mode == KM_UPPER ? 0x80000000u : 0u);
+      uk = kl ? ((kdst + kl + 15) >> 4) - (kdst >> 4) : 0u;
+      uv = vl ? ((vdst + vl + 15) >> 4) - (vdst >> 4) : 0u;
+    }
+    const uint32_t ui = wave_incl_scan(uk + uv);
+    if (v && !big) {
+      L.s_upre[2 * lane] = ui - uk - uv;
+      L.s_upre[2 * lane + 1] = ui - uv;
+    }
+    if (lane == 0) {
+      L.total = total;
+      L.nunits = __builtin_amdgcn_readlane(ui, 63);
+      L.big = big ? 1u : 0u;
+    }
+    if (lane == 0 && !big) L.s_upre[2 * (nk < 64 ? nk : 64)] = __builtin_amdgcn_readlane(ui, 63);
+  }
+  __syncthreads();
+  if (L.big) {  // generic path for this batch
+    if (t < 64) write_batch_wave(a, d, nk, rel, obase);
+    return;
+  }
+  const uint32_t total = L.total, nunits = L.nunits, nseg = 2 * nk;
+  // 2. segments -> staging, thread t copies the contiguous units [u0, u1)
+  {
+    const uint32_t per = (nunits + kWlThreads - 1) / kWlThreads;
+    const uint32_t u0 = t * per, u1 = u0 + per < nunits ? u0 + per : nunits;
+    int s = 0;
+    if (u0 < u1) {  // last segment with s_upre <= u0
+      int lo = 0, hi = (int)nseg - 1;
+      while (lo < hi) {
+        const int m = (lo + hi + 1) >> 1;
+        if (L.s_upre[m] <= u0) lo = m; else hi = m - 1;
+      }
+      s = lo;
+    }
+    // four units per round: every load of the round is in flight before the first use
+    for (uint32_t u = u0; u < u1; u += 4) {
+      uint4 x0[4], x1[4];
+      uint32_t D[4], lo[4], hi[4], sh[4], up[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t uu = u + i < u1 ? u + i : u1 - 1;  // a clamped duplicate does no harm (same bytes)
+        while (L.s_upre[s + 1] <= uu) s++;
+        const uint32_t dst = L.s_dst[s], lw = L.s_len[s];
+        const uint32_t len = lw & 0x7FFFFFFFu;
+        up[i] = lw >> 31;
+        D[i] = ((dst >> 4) + (uu - L.s_upre[s])) << 4;      // staging unit start
+        const uint64_t A = L.s_src[s] + D[i] - dst;          // source of the unit's first byte (may precede the segment)
+        sh[i] = (uint32_t)(A & 15);
+        lo[i] = D[i] > dst ? D[i] : dst;
+        hi[i] = D[i] + 16 < dst + len ? D[i] + 16 : dst + len;
+        const uint4* src = (const uint4*)(a.slice + (A & ~15ull));
+        x0[i] = src[0];
+        x1[i] = src[1];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t w[8] = {x0[i].x, x0[i].y, x0[i].z, x0[i].w, x1[i].x, x1[i].y, x1[i].z, x1[i].w};
+        // words q .. q + 4 of w (q = sh / 4) by bit masks: a select on the
+        // index would become an indexed (scratch) access
+        const uint32_t m1 = 0u - ((sh[i] >> 2) & 1u), m2 = 0u - ((sh[i] >> 3) & 1u), bs = sh[i] & 3u;
+        uint32_t tw[5];
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+          const uint32_t a0 = (w[j] & ~m1) | (w[j + 1] & m1);
+          const uint32_t a1 = (w[j + 2] & ~m1) | (w[j + 3] & m1);
+          tw[j] = (a0 & ~m2) | (a1 & m2);
+        }
+        uint32_t v4[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          v4[j] = __builtin_amdgcn_alignbyte(tw[j + 1], tw[j], bs);
+          if (up[i]) v4[j] = swar_upper(v4[j]);
+        }
+        if (lo[i] == D[i] && hi[i] == D[i] + 16) {
+          *(uint4*)(L.ob + D[i]) = make_uint4(v4[0], v4[1], v4[2], v4[3]);
+        } else {
+#pragma unroll
+          for (uint32_t j = 0; j < 16; j++)
+            if (j >= lo[i] - D[i] && j < hi[i] - D[i]) L.ob[D[i] + j] = (uint8_t)(v4[j >> 2] >> (8 * (j & 3)));
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t E = d0 + total;
+  // 3. staging -> HBM
+  uint8_t* og = a.out + obase - d0;
+  const uint32_t nu = (E + 15) >> 4;
+  for (uint32_t u = t; u < nu; u += kWlThreads) {
+    const uint32_t D = u << 4;
+    if (D >= d0 && D + 16 <= E) {
+      *(uint4*)(og + D) = *(const uint4*)(L.ob + D);
+    } else {
+      const uint32_t lo = D > d0 ? D : d0, hi = D + 16 < E ? D + 16 : E;
+      for (uint32_t j = lo; j < hi; j++) og[j] = L.ob[j];
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2726,17 +3228,39 @@ hipError_t upload_crc_tables() {
   return e;
 }
 
+// resident workgroups of k_eval_lean on the current device (CUs x occupancy)
+static uint32_t lean_grid(bool json) {
+  static std::mutex mu;
+  static uint32_t cache[64][2];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  std::lock_guard<std::mutex> lock(mu);
+  uint32_t& c = cache[dev][json ? 1 : 0];
+  if (!c) {
+    int cus = 0, per = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (json)
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_eval_lean<true>, kLeanThreads, 0);
+    else
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_eval_lean<false>, kLeanThreads, 0);
+    c = (uint32_t)std::max(1, cus) * (uint32_t)std::max(1, per);
+  }
+  return c;
+}
+
 void launch_eval(const EvalArgs& a, uint32_t ops, bool lean, hipStream_t s) {
   if (!a.nbatches) return;
   const size_t dyn = (ops & opbit(OP_REGEX)) ? kDfaDyn : 0;
   EvalArgs e = a;
   uint32_t grid = a.nbatches;
   if (lean) {
-    // the JSON stage's exact fallback costs registers: its own variant
-    if (ops & opbit(OP_FILTER_JSON))
-      hipLaunchKernelGGL(k_eval_lean<true>, dim3(a.nbatches), dim3(kLeanThreads), 0, s, a);
+    // persistent: as many workgroups as fit on the device at once
+    const bool json = (ops & (opbit(OP_FILTER_JSON) | opbit(OP_PROJECT))) != 0;
+    const uint32_t g = std::min<uint32_t>(a.nbatches, lean_grid(json));
+    if (json)
+      hipLaunchKernelGGL(k_eval_lean<true>, dim3(g), dim3(kLeanThreads), 0, s, a);
     else
-      hipLaunchKernelGGL(k_eval_lean<false>, dim3(a.nbatches), dim3(kLeanThreads), 0, s, a);
+      hipLaunchKernelGGL(k_eval_lean<false>, dim3(g), dim3(kLeanThreads), 0, s, a);
     grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list
   } else {
     e.list = nullptr;
@@ -2788,6 +3312,9 @@ void launch_write(const WriteArgs& a, uint32_t nblocks, hipStream_t s) {
   if (nblocks) hipLaunchKernelGGL(k_write, dim3((nblocks + kWriteThreads / 64 - 1) / (kWriteThreads / 64)),
                                   dim3(kWriteThreads), 0, s, a);
 }
+void launch_write_lean(const WriteArgs& a, uint32_t nblocks, hipStream_t s) {
+  if (nblocks) hipLaunchKernelGGL(k_write_lean, dim3(nblocks), dim3(kWlThreads), 0, s, a);
+}
 // CRC32C of out[off, off + n) into out[17..21); `acc` is one u32 of scratch
 void launch_crc(uint8_t* out, uint64_t off, uint64_t n, uint32_t* acc, hipStream_t s) {
   const uint64_t end = off + n;
@@ -2796,7 +3323,7 @@ void launch_crc(uint8_t* out, uint64_t off, uint64_t n, uint32_t* acc, hipStream
   (void)hipMemsetAsync(acc, 0, sizeof(uint32_t), s);
   if (nblocks) {
     const uint64_t nchunks = (nblocks + kCrcChunkBlocks - 1) / kCrcChunkBlocks;
-    const uint32_t grid = (uint32_t)(nchunks < 512 ? nchunks : 512);
+    const uint32_t grid = (uint32_t)(nchunks < 768 ? nchunks : 768);  // 3 workgroups per CU (LDS)
     hipLaunchKernelGGL(k_crc16, dim3(grid), dim3(kCrcThreads), 0, s, (const uint8_t*)out, off - 16, nblocks, acc);
   }
   hipLaunchKernelGGL(k_crc_final, dim3(1), dim3(64), 0, s, out, (const uint32_t*)acc, nblocks ? zend : off, end, n);

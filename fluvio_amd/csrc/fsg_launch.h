@@ -19,4 +19,5 @@ void launch_header(const Plan* plan, uint8_t* out, hipStream_t s);
 void launch_write(const WriteArgs& a, uint32_t nblocks, hipStream_t s);
 void launch_cat(const WriteArgs& a, uint32_t nbatches, hipStream_t s);
 void launch_crc(uint8_t* out, uint64_t off, uint64_t n, uint32_t* acc, hipStream_t s);
+void launch_write_lean(const WriteArgs& a, uint32_t nblocks, hipStream_t s);
 }  // namespace fsg

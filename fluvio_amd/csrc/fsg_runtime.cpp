@@ -861,17 +861,24 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   ea.elem = has_array ? c->elem.as<ElemRec>() : nullptr;
   uint32_t ops = 0;
   bool lean_stages = true;  // every stage has a lean form
+  bool projected = false;  // a projection seen: only uppercase maps may follow on the lean path
   for (uint32_t k = 0; k < c->hdesc.nstages; k++) {
     const StageDesc& sd = c->hdesc.st[k];
     ops |= 1u << sd.op;
+    if (projected && sd.op != OP_MAP_UPPER) lean_stages = false;
     if (sd.op == OP_CONTAINS && sd.needle_len > 128) lean_stages = false;  // kLeanNeedle
     if (sd.op == OP_REGEX && !sd.dfa.lean) lean_stages = false;
-    if (sd.op == OP_FILTER_JSON && sd.in_type != VT_SRC) lean_stages = false;
+    if ((sd.op == OP_FILTER_JSON || sd.op == OP_PROJECT) && sd.in_type != VT_SRC) lean_stages = false;
+    if (sd.op == OP_PROJECT) {
+      projected = true;
+      if (sd.needle_len > 128) lean_stages = false;  // kLeanNeedle
+    }
   }
-  // substring / bounded regex filters + uppercase maps: the lean kernel first,
-  // the batches it defers then go through the exact kernel (list mode)
+  // substring / bounded regex / filter_json filters, a final field projection
+  // and uppercase maps: the lean kernel first, the batches it defers then go
+  // through the exact kernel (list mode)
   const bool lean = (ops & ~((1u << OP_CONTAINS) | (1u << OP_MAP_UPPER) | (1u << OP_REGEX) |
-                             (1u << OP_FILTER_JSON))) == 0 &&
+                             (1u << OP_FILTER_JSON) | (1u << OP_PROJECT))) == 0 &&
                     !has_agg && lean_stages;
   if (lean) HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
   launch_eval(ea, ops, lean, st);
@@ -953,7 +960,15 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   }
   launch_header(pa.plan, wa.out, st);
   HIPCHK(hipEventRecord(c->ev[3], st));
-  launch_write(wa, p.last >= p.first && p.first >= 0 ? (uint32_t)(p.last - p.first + 1) : 0u, st);
+  const uint32_t nblk = p.last >= p.first && p.first >= 0 ? (uint32_t)(p.last - p.first + 1) : 0u;
+  // verbatim records (filters, uppercase, projections) averaging under 512
+  // output bytes: staged in LDS (k_write_lean); larger records: k_write's
+  // record-by-record wave copies (one wave pass per ~1 KiB record)
+  const bool verbatim = !has_agg && !has_array && c->hdesc.out_type != VT_I32;
+  if (verbatim && nblk && p.n_records && p.rec_bytes < 512ull * p.n_records)
+    launch_write_lean(wa, nblk, st);
+  else
+    launch_write(wa, nblk, st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[4], st));
   launch_crc(wa.out, 21, out_len - 21, c->crcparts.as<uint32_t>(), st);

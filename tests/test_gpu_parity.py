@@ -396,6 +396,53 @@ def test_filter_json_lean_batches(engine):
         check_batch(engine, CHAINS[chain], sl)
 
 
+def test_project_lean_batches(engine):
+    """Field projection on the lean path (flat objects, fsg_kernels.hip
+    lean_json_stage): batches of 1..64 records mixing documents it decides
+    (string / integer / literal values, duplicate keys: last wins, missing
+    field: dropped) with ones only the exact restatement decides (floats,
+    -0, escapes, nesting) and ones that fail; every batch bit-exact with the
+    oracle or reported unsupported for a document the device defers to it."""
+    from tests import jsongen
+    import random
+    rng = random.Random(9)
+    docs = [d for d in jsongen.corpus(19, 300, 120) if not _project_may_be_unsupported(d)]
+    simple = []
+    for i in range(300):
+        k = rng.random()
+        if k < 0.2:
+            simple.append(b'{"level":"info","message":"m %d","n":%d,"t":true}' % (i, rng.randint(-10**12, 10**12)))
+        elif k < 0.4:
+            simple.append(b'{"message":%d,"x":null,"message":"last %d"}' % (i, i))  # duplicate: last wins
+        elif k < 0.6:
+            simple.append(b'{"a":"b","c":false}')                                   # no field: dropped
+        elif k < 0.8:
+            simple.append(b'{ "message" : -%d , "level" : "warn" }' % (i + 1))     # whitespace, integer
+        else:
+            simple.append(b'{"message":"%s"}' % (b"x" * rng.randint(0, 300)))
+    sl, base = b"", 0
+    for k in range(60):
+        b = P.Batch(base_offset=base)
+        n = rng.choice([1, 7, 15, 40, 64])
+        for j in range(n):
+            pool = simple if k % 3 else docs
+            b.add_record(P.Record.new(rng.choice(pool)))
+        sl += b.encode()
+        base += n
+    for chain in ("project", "filter_project_map", "project_level_filter"):
+        check_batch(engine, CHAINS[chain], sl)
+
+
+def test_project_synthetic_logs(engine):
+    """C3 on the bench's C2 documents: filter -> projection of `message` ->
+    uppercase, and projections of other fields, batch by batch."""
+    sl = synth.make_slice(2, 3000)
+    out = check_batch(engine, CHAINS["filter_project_map"], sl)
+    assert 0 < out.n_records < 3000
+    for f in ("level", "ts", "nope"):
+        check_batch(engine, [("map_json_project", {"field": f}, None)], sl)
+
+
 def test_filter_json_synthetic_logs(engine):
     """C2 records are StructuredLog documents: keep level > debug."""
     sl = synth.make_slice(2, 3000)
@@ -641,15 +688,31 @@ def test_crc_tables_on_every_device():
 # field projection (map_json_project, C3): parity unpinned by the reference
 # (no such module ships in it); checked against the oracle's definition
 # ---------------------------------------------------------------------------
+def _project_may_be_unsupported(doc: bytes) -> bool:
+    """Documents the device projection reports as unsupported
+    (fsg_json_dev.h run_project): a key with an escape (it could decode to the
+    field name), or a projected value that is not already serde_json's text
+    (escapes, floats, objects that need re-ordering).  A coarse superset: any
+    backslash, any fraction / exponent, any object inside an object."""
+    import re
+    return b"\\" in doc or re.search(rb"[0-9][.eE]", doc) is not None or \
+        re.search(rb":\s*[\[{]", doc) is not None
+
+
 def test_project_fuzz_one_record(engine):
     from tests import jsongen
+    n_unsup = 0
     for doc in jsongen.corpus(17, 150, 350):
         sl = _one_record_slice(doc)
         for chain in ("project", "project_level_filter"):
             try:
                 check_batch(engine, CHAINS[chain], sl)
             except AssertionError as e:
+                if "Unsupported" in str(e) and _project_may_be_unsupported(doc):
+                    n_unsup += 1
+                    continue
                 raise AssertionError(f"doc {doc!r}: {e}") from e
+    assert n_unsup < 150  # most documents take the device path
 
 
 def test_project_c3_chain_errors_in_stream(engine):
