@@ -13,13 +13,16 @@ same contract (warmup, barrier + sync, max over ranks):
   c2-json        filter_json (serde_json StructuredLog, level > debug)  (configs[1])
   c3-filter-map  filter -> projection -> uppercase, re-encode + CRC32C  (configs[2])
   c4-array-map   array_map_json_array, 1-16 elements per record         (configs[3])
-  c5-keyed-agg   aggregate-sum over 64 partitions, per-partition state in
-                 HBM merged with an RCCL all-reduce                      (configs[4])
+  c5-keyed-agg   aggregate-json (per-key u32 sums) over 64 partitions, keys
+                 routed by SipHash; each step every rank's keyed state is
+                 merged topic-wide (all_gather over RCCL)               (configs[4])
+  c5-agg-sum     aggregate-sum over 64 partitions, the 64-slot partition
+                 state vector all-reduced over RCCL each step
 
 Multi-GPU: one process per GPU (torch.distributed.run).  c1..c4: every rank
 filters its own partition (p -> rank, no data-path collective, "weak").
-c5: the 64 partitions are sharded p -> rank p mod N ("strong"), the state
-vector is all-reduced over RCCL each step.  Rank 0 prints ONE JSON line.
+c5: the 64 partitions are sharded p -> rank p mod N ("strong"), the state is
+merged over RCCL each step.  Rank 0 prints ONE JSON line.
 """
 import argparse
 import hashlib
@@ -51,7 +54,14 @@ C5 = {"partitions": 64, "records_per_partition": 500_000,
       "modules": [("aggregate-sum", {}, None)],
       "description": "aggregate-sum over 64 partitions (decimal i32 records), per-partition accumulators in HBM, "
                      "RCCL all-reduce of the partition state vector each step"}
-EXTRA = ["c1-regex", "c2-json", "c3-filter-map", "c4-array-map", "c5-keyed-agg"]
+C5K = {"partitions": 64, "records_per_partition": 50_000, "keys": 1024,
+       "modules": [("aggregate-json", {}, None)],
+       "description": "aggregate-json over 64 partitions: records {\"repo-NNNN\": n} keyed by the repo name "
+                      "(1024 keys routed by SipHash, ~16 per partition), per-key u32 sums, every record's output = "
+                      "the pretty-printed map; each step the ranks' keyed states are merged topic-wide "
+                      "(all_gather over RCCL + per-key sum on the GPU)"}
+EXTRA = ["c1-regex", "c2-json", "c3-filter-map", "c4-array-map", "c5-keyed-agg", "c5-agg-sum"]
+C5_ALL = ("c5-keyed-agg", "c5-agg-sum")
 PEAK_GBPS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
@@ -60,7 +70,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2-substring", choices=sorted(WORKLOADS) + ["c5-keyed-agg"])
+    ap.add_argument("--workload", default="c2-substring", choices=sorted(WORKLOADS) + list(C5_ALL))
     ap.add_argument("--records", type=int, default=0, help="records per GPU of the headline workload (0 = default)")
     ap.add_argument("--only", action="store_true", help="time the headline workload only (no `workloads`)")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="records per CPU-baseline process")
@@ -99,10 +109,21 @@ class Ctx:
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.dist = None
+        self._nccl = None
         if self.world > 1:
             import torch.distributed as dist
             dist.init_process_group("gloo")
             self.dist = dist
+
+    def nccl(self):
+        """RCCL group for GPU-tensor collectives (created on first use by every rank)."""
+        if self.dist is None:
+            return None
+        if self._nccl is None:
+            import torch
+            torch.cuda.set_device(self.local)
+            self._nccl = self.dist.new_group(backend="nccl")
+        return self._nccl
 
     def barrier(self):
         if self.dist is not None:
@@ -141,7 +162,11 @@ def _cpu_proc(args):
     kind, modules, nrec, seed = args
     from fluvio_amd import synth
     from oracle.oracle import OracleChain
-    sl = synth.make_slice(kind, nrec, seed=seed)
+    if kind == "keyed":
+        p = seed % C5K["partitions"]
+        sl = synth.make_keyed_slices(C5K["partitions"], nrec, C5K["keys"], owned=[p])[p]
+    else:
+        sl = synth.make_slice(kind, nrec, seed=seed)
     oc = OracleChain(modules)
     t0 = time.perf_counter()
     r = oc.process_batch(sl)
@@ -207,8 +232,10 @@ def cpu_baselines_first(ctx, names):
         return {}
     out = {}
     for w in names:
-        if w == "c5-keyed-agg":
+        if w == "c5-agg-sum":
             out[w] = cpu_baseline(3, C5["modules"], min(a.cpu_sample, C5["records_per_partition"]))
+        elif w == "c5-keyed-agg":
+            out[w] = cpu_baseline("keyed", C5K["modules"], min(a.cpu_sample, C5K["records_per_partition"]))
         else:
             kind, modules, nrec, _ = WORKLOADS[w]
             out[w] = cpu_baseline(kind, modules, min(a.cpu_sample, nrec))
@@ -347,15 +374,124 @@ def run_c5(ctx, cpu):
     per = {k: v / a.steps for k, v in kms.items()}
     res = {"metric": "records/s", "value": total_recs * a.steps / elapsed, "unit": "records/s",
            "ms_per_step": elapsed / a.steps * 1e3, "scaling": "strong", "dtype": "i32",
-           "config": {"workload": "c5-keyed-agg", "description": C5["description"], "partitions": P,
+           "config": {"workload": "c5-agg-sum", "description": C5["description"], "partitions": P,
                       "records_per_partition": nrec, "partitions_per_gpu": len(owned),
                       "slice_bytes_this_gpu": in_bytes, "host_threads": nthreads,
                       "parallelism": f"partitions sharded p -> rank p mod {ctx.world}"},
            "kernel_ms_sum_over_partitions": per,
            "gbps_input_per_gpu": in_bytes * a.steps / elapsed / 1e9,
            "state_checksum": sum(vec) & 0xFFFFFFFF, "setup_s": {"generate": gen_s}}
-    res["cpu_baseline"] = cpu.get("c5-keyed-agg")
+    res["cpu_baseline"] = cpu.get("c5-agg-sum")
     return res
+
+
+def run_c5k(ctx, cpu):
+    """C5 keyed: 64 partitions of {"repo-NNNN": n} records (key = repo name,
+    SipHash-routed), aggregate-json per partition (every output record = the
+    partition's whole map), partitions sharded p -> rank p mod N.  Per step:
+    every owned partition's slice through its chain, then the topic-wide
+    per-key totals: each chain's state as (FNV-1a 64 key fingerprint, u32)
+    pairs written straight into HBM (fsg_chain_keyed_state), one all_gather
+    over RCCL, and a per-key sum on the GPU (partitions.merge_keyed_torch)."""
+    import torch
+    from fluvio_amd import partitions as PT
+    from fluvio_amd import synth
+    from fluvio_amd.smartengine import ResidentSlice, SmartEngine, SmartModuleChainBuilder, SmartModuleConfig, builtin
+    a = ctx.a
+    P, nrec = C5K["partitions"], C5K["records_per_partition"]
+    engine = SmartEngine(ctx.local)
+    torch.cuda.set_device(ctx.local)
+    group = ctx.nccl()
+    owned = PT.owned_partitions(P, ctx.world, ctx.rank)
+    t0 = time.time()
+    raw = synth.make_keyed_slices(P, nrec, C5K["keys"], owned=owned)
+    gen_s = time.time() - t0
+    chains, rsl = {}, {}
+    for p in owned:
+        b = SmartModuleChainBuilder.default()
+        b.set_store_memory_limit(64 << 30)
+        for mname, params, acc in C5K["modules"]:
+            b.add_smart_module(SmartModuleConfig.builder().params(params).build(), builtin(mname))
+        chains[p] = b.initialize(engine)
+        rsl[p] = ResidentSlice(engine, raw[p])
+    del raw
+    cap = C5K["keys"] + 64
+    fp = torch.zeros(len(owned) * cap, dtype=torch.int64, device=f"cuda:{ctx.local}")
+    val = torch.zeros(len(owned) * cap, dtype=torch.int32, device=f"cuda:{ctx.local}")
+    nthreads = min(16, len(owned)) or 1
+    groups = [list(range(len(owned)))[i::nthreads] for i in range(nthreads)]
+    kms = {"eval_ms": 0.0, "plan_ms": 0.0, "write_ms": 0.0, "crc_ms": 0.0, "total_ms": 0.0}
+    out_bytes = [0]
+    lock = threading.Lock()
+    counts = [0] * len(owned)
+
+    def work(idx):  # one host thread drives a group of partitions, each on its own chain stream
+        for i in idx:
+            p = owned[i]
+            chains[p].process_slice(rsl[p], download=False)
+            counts[i] = chains[p].keyed_state(0, fp.data_ptr() + i * cap * 8, val.data_ptr() + i * cap * 4, cap)
+            t = chains[p].last_timings()
+            with lock:
+                for k in kms:
+                    kms[k] += t[k]
+                out_bytes[0] += t["out_bytes"]
+
+    merged = [None]
+
+    def step():
+        th = [threading.Thread(target=work, args=(g,)) for g in groups if g]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert max(counts) <= cap
+        sel = torch.cat([torch.arange(i * cap, i * cap + counts[i], device=fp.device) for i in range(len(owned))])
+        merged[0] = PT.merge_keyed_torch(fp[sel], val[sel].to(torch.int64) & 0xFFFFFFFF,
+                                         dist=ctx.dist, group=group)
+        torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        step()
+    ctx.barrier()
+    for k in kms:
+        kms[k] = 0.0
+    out_bytes[0] = 0
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    ctx.barrier()
+    elapsed = ctx.max_over_ranks(time.perf_counter() - t0)
+    total_recs = sum(rsl[p].n_records for p in owned)
+    if ctx.dist is not None:
+        tt = torch.tensor([total_recs], dtype=torch.float64)
+        ctx.dist.all_reduce(tt)
+        total_recs = int(tt.item())
+    in_bytes = sum(chains[p].last_timings()["in_bytes"] for p in owned)
+    keys, sums = merged[0]
+    per = {k: v / a.steps for k, v in kms.items()}
+    res = {"metric": "records/s", "value": total_recs * a.steps / elapsed, "unit": "records/s",
+           "ms_per_step": elapsed / a.steps * 1e3, "scaling": "strong", "dtype": "u32",
+           "config": {"workload": "c5-keyed-agg", "description": C5K["description"], "partitions": P,
+                      "records_per_partition": nrec, "keys": C5K["keys"], "partitions_per_gpu": len(owned),
+                      "slice_bytes_this_gpu": in_bytes, "output_bytes_this_gpu_per_step": out_bytes[0] / a.steps,
+                      "host_threads": nthreads, "chain": [m[0] for m in C5K["modules"]],
+                      "parallelism": f"partitions sharded p -> rank p mod {ctx.world}"},
+           "kernel_ms_sum_over_partitions": per,
+           "gbps_input_per_gpu": in_bytes * a.steps / elapsed / 1e9,
+           "gbps_output_per_gpu": out_bytes[0] / elapsed / 1e9,
+           "merged_keys": int(keys.numel()), "state_checksum": int(sums.sum().item()) & 0xFFFFFFFF,
+           "setup_s": {"generate": gen_s}}
+    res["cpu_baseline"] = cpu.get("c5-keyed-agg")
+    del rsl, chains
+    return res
+
+
+def run_workload(ctx, w, nrec, cpu):
+    if w == "c5-keyed-agg":
+        return run_c5k(ctx, cpu)
+    if w == "c5-agg-sum":
+        return run_c5(ctx, cpu)
+    return run_filter(ctx, w, nrec, cpu)
 
 
 def main():
@@ -364,14 +500,10 @@ def main():
     head = a.workload
     extra = [] if a.only else [w for w in EXTRA if w != head]
     cpu = cpu_baselines_first(ctx, [head] + extra)
-    if head == "c5-keyed-agg":
-        line = run_c5(ctx, cpu)
-    else:
-        line = run_filter(ctx, head, a.records, cpu)
-    line = dict(line)
+    line = dict(run_workload(ctx, head, a.records, cpu))
     workloads = {}
     for w in extra:
-        workloads[w] = run_c5(ctx, cpu) if w == "c5-keyed-agg" else run_filter(ctx, w, 0, cpu)
+        workloads[w] = run_workload(ctx, w, 0, cpu)
     if ctx.rank == 0:
         out = {
             "metric": "records/sec + achieved HBM GB/s for SmartModule filter chain, 1/2/4/8 MI355X",

@@ -90,6 +90,7 @@ SIGNATURES = {
     "fsg_chain_look_back": (ctypes.c_int, [VP, ctypes.POINTER(fsg_metrics)]),
     "fsg_chain_get_accumulator": (ctypes.c_int, [VP, SZ, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
                                                  ctypes.POINTER(SZ)]),
+    "fsg_chain_keyed_state": (ctypes.c_int, [VP, SZ, VP, VP, SZ, ctypes.POINTER(SZ)]),
     "fsg_chain_last_timings": (ctypes.c_int, [VP, ctypes.POINTER(fsg_timings)]),
     "fsg_chain_free": (None, [VP]),
     "fsg_output_free": (None, [ctypes.POINTER(fsg_output)]),

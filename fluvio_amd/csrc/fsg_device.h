@@ -35,6 +35,7 @@ enum StageOp : uint8_t {
   OP_ARRAY_MAP = 8,    // array_map_json_array: Vec<serde_json::Value> -> one record per element (last stage)
   OP_AGG_CONCAT = 9,   // aggregate: String accumulator ++ value (last stage)
   OP_PROJECT = 10,     // map_json_project: the value narrows to one JSON field's text (FilterMap)
+  OP_AGG_JSON = 11,    // aggregate-json: HashMap<String, u32> += per key, pretty JSON accumulator (last stage)
 };
 
 // value representation entering a stage (static per chain position)
@@ -96,7 +97,7 @@ struct StageDesc {
 };
 
 // ChainDesc::flags: what the last stage is
-enum ChainFlags : uint32_t { CF_AGG_SUM = 1u, CF_AGG_CAT = 2u, CF_ARRAY = 4u };
+enum ChainFlags : uint32_t { CF_AGG_SUM = 1u, CF_AGG_CAT = 2u, CF_ARRAY = 4u, CF_AGG_JSON = 8u };
 struct ChainDesc {
   uint32_t nstages;
   uint32_t out_type;   // ValType of the value after the last stage
@@ -139,7 +140,8 @@ struct BatchStat {
 
 // one kept output record (a compaction descriptor, 64 bytes): enough to
 // re-encode the record canonically without re-parsing the source
-enum KeepMode : uint8_t { KM_COPY = 0, KM_UPPER = 1, KM_I32 = 2, KM_AGG = 3, KM_ARRAY = 4, KM_CONCAT = 5 };
+enum KeepMode : uint8_t { KM_COPY = 0, KM_UPPER = 1, KM_I32 = 2, KM_AGG = 3, KM_ARRAY = 4, KM_CONCAT = 5,
+                         KM_AGGJ = 6 };  // KM_AGGJ: value = cat[vpos, vpos + vlen) (k_aggj's map text)
 // KeptRec::pad bits for KM_ARRAY / KM_CONCAT
 enum KeepFlags : uint8_t { KF_UPPER = 1, KF_I32 = 2 };
 struct KeptRec {
@@ -271,5 +273,63 @@ struct WriteArgs {
   uint64_t acc_len;
 };
 constexpr uint64_t kCatOff = 64;  // the concat stream starts this far into its buffer (copy_seg margin)
+
+// aggregate-json (k_aggj_*): the folded records in stream order (records of
+// batches up to the first error batch), their entries, the key dictionary
+// (insertion order = id order) with an open-addressing index in HBM, and the
+// per-block state table (the map's values at every block's first record).
+// Keys point at their bytes: the slice for keys met in records, the uploaded
+// initial accumulator otherwise.
+struct AggjArgs {
+  const uint8_t* slice;
+  const BatchStat* bstat;
+  KeptRec* desc;
+  const uint64_t* rbase;
+  const ElemRec* elem;
+  const Mins* mins;
+  uint32_t nbatches;
+  uint32_t write;          // text pass: 0 sizes, 1 writes the map text into cat
+  uint8_t* cat;            // text buffer (kCatOff margin)
+  // per batch
+  uint32_t* bcnt;          // folded records of batch b
+  uint64_t* brec;          // ... exclusive prefix (stream index of its first record)
+  // per folded record
+  uint64_t n_rec;
+  uint64_t* rdesc;         // KeptRec index
+  uint32_t* rne;           // entries (json_map_u32 pairs) of the record
+  uint64_t* rent;          // ... exclusive prefix (entry index of its first pair)
+  uint32_t* rnew;          // keys the record inserts into the map
+  uint64_t* rnewb;         // ... exclusive prefix
+  uint32_t* rlen;          // map text bytes after the record
+  uint64_t* roff;          // ... exclusive prefix (offset in cat after kCatOff)
+  // per entry: key id (kSkipEntry for a key the same record names again
+  // earlier) and the value the record contributes (the key's last value in it)
+  uint32_t* ekid;
+  uint32_t* eval;
+  // dictionary
+  unsigned long long* slot_ref;  // 0 empty; else the key's first occurrence: init key k -> k + 1,
+                                 // record r entry j -> (r + 1) << 32 | j
+  uint32_t* slot_id;
+  uint32_t cap;            // slots (power of two)
+  uint32_t n_init;         // keys of the initial accumulator (ids 0 .. n_init - 1)
+  const uint64_t* kptr;    // initial keys: match bytes
+  const uint32_t* klen;
+  const uint32_t* val_init;
+  uint64_t* tptr;          // per key id: text as serialized ("..." with escapes)
+  uint32_t* tlen;
+  uint32_t* kup;           // 1: read through the ASCII-uppercase view
+  uint32_t nkeys;          // K: keys after the call (host-known once the ids exist)
+  // blocks of `rb` consecutive records: state[b * K + k] = key k's value
+  // before block b's first record
+  uint32_t rb;
+  uint32_t nblk;
+  uint32_t* state;
+  unsigned long long* scal;  // [0] entries [1] records [2] new keys [3] text bytes
+  uint64_t* acc_off;       // per batch: the accumulator text after it (offset in cat) ...
+  uint32_t* acc_len;       // ... and its length (0xFFFFFFFF: no record aggregated yet)
+};
+constexpr uint32_t kSkipEntry = 0xFFFFFFFFu;
+constexpr uint32_t kAjLds = 4096;  // k_aggj_text keeps up to this many values in LDS
+
 
 }  // namespace fsg

@@ -33,9 +33,10 @@ enum JsonErr : uint8_t {
   JE_INVALID_TYPE,     // sub = unexpected kind | expected kind << 4; a, b = span (number digits / string)
   JE_DEEP,             // ignored value nested deeper than the device frame stack (outside the restatement)
   JE_UNSUP,            // valid input outside the device restatement (array_map: floats, unsorted keys)
+  JE_INVALID_VALUE,    // u32 visitor: sub = JU_UINT / JU_NINT, [a, b) = the digits ("invalid value: integer `N`, expected u32")
 };
 enum JsonUnexp : uint8_t { JU_UNIT = 0, JU_TRUE, JU_FALSE, JU_UINT, JU_NINT, JU_FLOAT, JU_STR, JU_SEQ, JU_MAP };
-enum JsonExp : uint8_t { JX_STRUCT = 0, JX_STRING, JX_VARIANT, JX_UNIT, JX_SEQ, JX_MAP };
+enum JsonExp : uint8_t { JX_STRUCT = 0, JX_STRING, JX_VARIANT, JX_UNIT, JX_SEQ, JX_MAP, JX_U32 };
 
 struct JRes {
   uint8_t ok;
@@ -1053,6 +1054,130 @@ struct JsonDev {
     return r;
   }
 
+  // aggregate-json (examples/aggregate-json/src/lib.rs:22-36):
+  // from_slice::<HashMap<String, u32>> (de.rs deserialize_map / MapAccess,
+  // keys deserialize_string, values deserialize_number with the u32 visitor).
+  // Entries (key content span, value) -> out[0..*count) in text order,
+  // duplicates included (the aggregation keeps the last value of a key).
+  // Keys with escapes and float values are JE_UNSUP.
+  __device__ __forceinline__ JRes run_map_u32(ElemRec* out, uint64_t abs0, uint32_t* count) {
+    r = JRes{0, 0, 0, 0, 0, 0, 0};
+    failed = false;
+    has_pos = false;
+    depth = 128;
+    i = 0;
+    vunsup = false;
+    uint32_t k = 0;
+    int rc = 0;
+    int c = ws();
+    if (c < 0) {
+      rc = peek_error(JE_EOF_VALUE);
+    } else if (c == '{') {
+      --depth;
+      eat();
+      bool first = true;
+      for (;;) {
+        int p = ws();
+        if (p == '}') break;
+        if (p == ',' && !first) {
+          eat();
+          p = ws();
+        } else if (p >= 0) {
+          if (!first) {
+            rc = peek_error(JE_OBJ_COMMA);
+            break;
+          }
+          first = false;
+        } else {
+          rc = peek_error(JE_EOF_OBJECT);
+          break;
+        }
+        if (p == '}') {
+          rc = peek_error(JE_TRAILING_COMMA);
+          break;
+        }
+        if (p < 0) {
+          rc = peek_error(JE_EOF_VALUE);
+          break;
+        }
+        if (p != '"') {
+          rc = peek_error(JE_KEY);
+          break;
+        }
+        eat();
+        const uint32_t k0 = i;
+        vcanon = 0;
+        if (vstr()) {
+          rc = -1;
+          break;
+        }
+        const uint32_t k1 = i - 1;
+        if (vhas_bs) vunsup = true;  // the decoded key differs from its source bytes
+        c = ws();  // parse_object_colon
+        if (c == ':') {
+          eat();
+        } else if (c >= 0) {
+          rc = peek_error(JE_COLON);
+          break;
+        } else {
+          rc = peek_error(JE_EOF_OBJECT);
+          break;
+        }
+        // deserialize_number -> PrimitiveVisitor<u32>
+        const int q = ws();
+        if (q < 0) {
+          rc = peek_error(JE_EOF_VALUE);
+          break;
+        }
+        uint32_t v = 0;
+        if (q == '-' || dig(q)) {
+          const bool pos = q != '-';
+          if (!pos) eat();
+          const uint32_t a = i;
+          uint8_t kind;
+          if (parse_integer(pos, &kind)) {
+            rc = -1;
+            break;
+          }
+          const uint32_t b = i;
+          if (kind == JU_FLOAT) {  // visit_f64: Rust float Display, outside the restatement
+            rc = fail_at(i, JE_UNSUP);
+            break;
+          }
+          uint64_t mag = 0;
+          const bool big = b - a > 10;
+          for (uint32_t t = a; !big && t < b; t++) mag = mag * 10 + (uint64_t)(at(t) - '0');
+          if (!pos || big || mag > 0xFFFFFFFFull) {  // visit_i64 / visit_u64 out of range
+            custom(JE_INVALID_VALUE, a, b, kind);
+            fix_position();
+            rc = -1;
+            break;
+          }
+          v = (uint32_t)mag;
+        } else {
+          invalid_type(JX_U32);
+          rc = -1;
+          break;
+        }
+        out[k].pos = abs0 + k0;
+        out[k].src_len = k1 - k0;
+        out[k].out_len = v;
+        k++;
+      }
+      depth++;
+      if (!rc) rc = end_map();
+    } else {
+      invalid_type(JX_MAP);
+      rc = -1;
+    }
+    if (rc) fix_position();
+    if (!rc && ws() >= 0) rc = peek_error(JE_TRAILING);  // Deserializer::end
+    if (!rc && vunsup) rc = fail_at(i, JE_UNSUP);
+    *count = k;
+    if (!rc) r.ok = 1;
+    return r;
+  }
+
   // map_json_project (C3 field projection; defined by the oracle, parity
   // unpinned): from_slice::<Map<String, Value>> (de.rs deserialize_map /
   // MapAccess), the last member whose key equals `field`.  *ps / *pl = its
@@ -1195,6 +1320,14 @@ __device__ __noinline__ JRes json_project(const uint8_t* s, uint32_t n, bool upp
   return d.run_project(field, fl, ps, pl, found);
 }
 // array_map_json_array over one value: element descriptors to out[0..*count)
+__device__ __noinline__ JRes json_map_u32(const uint8_t* s, uint32_t n, bool upper, ElemRec* out, uint64_t abs0,
+                                          uint32_t* count) {
+  JsonDev<const uint8_t*> d;
+  d.s = s;
+  d.n = n;
+  d.upper = upper;
+  return d.run_map_u32(out, abs0, count);
+}
 __device__ __noinline__ JRes json_array_explode(const uint8_t* s, uint32_t n, bool upper, ElemRec* out, uint64_t abs0,
                                                uint32_t* count) {
   JsonDev<const uint8_t*> d;

@@ -237,7 +237,7 @@ constexpr uint32_t kOpsJson = opbit(OP_FILTER_JSON) | opbit(OP_CONTAINS) | opbit
 constexpr uint32_t kOpsArray = opbit(OP_ARRAY_MAP) | opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
 constexpr uint32_t kOpsInt = opbit(OP_FILTER_ODD) | opbit(OP_MAP_DOUBLE) | opbit(OP_FILTER_MAP) | opbit(OP_AGG_SUM) |
                              opbit(OP_AGG_CONCAT) | opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
-constexpr uint32_t kOpsAll = 0x7FFu;
+constexpr uint32_t kOpsAll = 0xFFFu;
 constexpr int kDfaDyn = 768 + kDfaLds;  // dynamic LDS of a chain with a regex stage
 extern __shared__ __attribute__((aligned(16))) uint8_t g_dyn_lds[];
 
@@ -839,6 +839,36 @@ __device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int 
             }
             break;
           }
+          case OP_AGG_JSON: {
+            // aggregate-json: serde_json::from_slice::<HashMap<String, u32>> of the
+            // value (the accumulator side never fails: unwrap_or_default); the
+            // entries go to elem[], k_aggj folds them in stream order
+            if constexpr (!(kOps & opbit(OP_AGG_JSON))) break;
+            uint8_t t[12];
+            const uint8_t* js = (const uint8_t*)&w[vs];
+            uint32_t jn = vl;
+            if (!src) {
+              jn = fmt_i32(ival_in, t);
+              js = t;
+            }
+            const uint64_t av = wbase + vs;
+            uint32_t ne = 0;
+            const JRes jr = json_map_u32(js, jn, src && upper, elem + (av >> 1), av, &ne);
+            if (!jr.ok) {
+              err = true;
+              if (jr.code == JE_UNSUP) {
+                ec = EC_UNSUP;
+              } else {
+                ec = EC_JSON | ((uint32_t)jr.code << 8) | ((uint32_t)jr.sub << 16);
+                L.r_aux[r] = jr.pos;
+                L.r_aux2[r] = jr.a;
+                L.r_aux3[r] = jr.b;
+              }
+            } else {
+              L.r_ival[r] = (int32_t)ne;  // entry count
+            }
+            break;
+          }
           case OP_PROJECT: {
             // map_json_project: the value becomes its field's JSON text (a view
             // into the source value), a missing field drops the record
@@ -1029,6 +1059,7 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
     const bool agg_on = (kOps & opbit(OP_AGG_SUM)) && (ch.flags & CF_AGG_SUM) && full;
     const bool cat_on = (kOps & opbit(OP_AGG_CONCAT)) && (ch.flags & CF_AGG_CAT) && full;
     const bool arr_on = (kOps & opbit(OP_ARRAY_MAP)) && (ch.flags & CF_ARRAY) && full;
+    const bool aggj_on = (kOps & opbit(OP_AGG_JSON)) && (ch.flags & CF_AGG_JSON) && full;
     const uint8_t last_in = ch.st[ch.nstages - 1].in_type;
     const int last = nst - 1;
     const uint8_t out_type = (nst == (int)ch.nstages) ? (uint8_t)ch.out_type : ch.st[nst].in_type;
@@ -1165,6 +1196,10 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
             d.ival = local;
           } else if (arr_on) {
             d.mode = KM_ARRAY;
+            d.ival = L.r_ival[r];
+            d.pad = last_in == VT_SRC_UPPER ? KF_UPPER : 0;
+          } else if (aggj_on) {
+            d.mode = KM_AGGJ;  // vpos locates the entries; k_aggj sets src / vlen to the map text in cat
             d.ival = L.r_ival[r];
             d.pad = last_in == VT_SRC_UPPER ? KF_UPPER : 0;
           } else if (cat_on) {
@@ -2749,7 +2784,7 @@ __global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
         w += fmt_i32(x, q + w);
       } else {
         vc = vl;
-        vsrc = r.mode == KM_CONCAT ? kCatOff : r.vpos;
+        vsrc = r.mode == KM_CONCAT ? kCatOff : r.mode == KM_AGGJ ? r.src : r.vpos;  // KM_AGGJ: the map text in cat
         w += vl;
       }
       n = venc(r.hdr, t);
@@ -2757,7 +2792,7 @@ __global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
     }
     // payloads, record by record, with the whole wave
     const uint32_t nrec = st.nkeep - k0 < 64u ? st.nkeep - k0 : 64u;
-    const bool cat = st.nkeep && d[0].mode == KM_CONCAT;
+    const bool cat = st.nkeep && (d[0].mode == KM_CONCAT || d[0].mode == KM_AGGJ);
     for (uint32_t i = 0; i < nrec; i++) {
       const uint32_t rkl = __builtin_amdgcn_readlane(kl, i);
       const uint32_t rvc = __builtin_amdgcn_readlane(vc, i);
@@ -2803,6 +2838,373 @@ __global__ __launch_bounds__(256) void k_cat(WriteArgs a, uint32_t nbatches) {
       if (rn && !(fl & KF_I32))
         copy_seg(cat, a.slice, readlane_u64(dst, i), readlane_u64(r.vpos, i), rn, (fl & KF_UPPER) != 0);
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// aggregate-json (smartmodule/examples/aggregate-json/src/lib.rs:22-36): per
+// record, `accumulated + new` (`entry().and_modify(+=).or_insert()`, u32
+// wrapping as in the release wasm) and the record's value = serde_json::
+// to_vec_pretty of the whole map.  HashMap's iteration order is random per
+// process; the device (and the oracle) use insertion order: the accumulator's
+// keys, then new keys in the order a record first names them.
+//
+// The fold is sequential in the reference; here it is data-parallel:
+//   1. k_aggj_bcount / scan / k_aggj_flat: the folded records in stream order
+//      and their entries (exclusive scans give every record its stream index
+//      and its first entry index)
+//   2. k_aggj_insert: every record's distinct keys into one open-addressing
+//      index (CAS claim; atomicMin keeps the key's FIRST occurrence), value =
+//      the key's last value in the record (a JSON object's duplicate key)
+//   3. k_aggj_new / scan / k_aggj_ids / k_aggj_kid: a key's id = its rank by
+//      first occurrence (insertion order), entries resolved to ids
+//   4. k_aggj_bsum / k_aggj_colscan: per block of `rb` records, the sums per
+//      key, then per key an exclusive scan over blocks: the map's values at
+//      every block's first record
+//   5. k_aggj_text: one wave per block replays its records from that row
+//      (values in LDS), sizing (pass 0) or writing (pass 1) each record's text
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t dec_digits_u32(uint32_t v) {
+  uint32_t n = 1;
+  while (v >= 10u) {
+    v /= 10u;
+    n++;
+  }
+  return n;
+}
+__device__ __forceinline__ uint8_t key_byte(const uint8_t* p, uint32_t k, bool up) {
+  const uint8_t c = p[k];
+  return (up && c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c;
+}
+__device__ uint32_t aggj_hash(const uint8_t* p, uint32_t n, bool up) {  // FNV-1a
+  uint32_t h = 2166136261u;
+  for (uint32_t k = 0; k < n; k++) h = (h ^ key_byte(p, k, up)) * 16777619u;
+  return h;
+}
+__device__ bool aggj_key_eq(const uint8_t* a, uint32_t an, bool aup, const uint8_t* b, uint32_t bn, bool bup) {
+  if (an != bn) return false;
+  for (uint32_t k = 0; k < an; k++)
+    if (key_byte(a, k, aup) != key_byte(b, k, bup)) return false;
+  return true;
+}
+
+// generic exclusive scan u32 -> u64 (tiles of 2048, tile totals scanned by one
+// workgroup, added back); *tot = the sum
+constexpr int kXsThreads = 256, kXsPer = 8, kXsTile = kXsThreads * kXsPer;
+__device__ __forceinline__ uint64_t block_excl_u64(uint64_t x, uint64_t* sh, uint64_t& total) {
+  const uint64_t inc = wave_incl_scan(x);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane_id() == 63) sh[w] = inc;
+  __syncthreads();
+  uint64_t pre = 0, tot = 0;
+  for (int i = 0; i < nw; i++) {
+    const uint64_t v = sh[i];
+    if (i < w) pre += v;
+    tot += v;
+  }
+  __syncthreads();
+  total = tot;
+  return inc - x + pre;
+}
+__global__ __launch_bounds__(kXsThreads) void k_xscan_tiles(const uint32_t* in, uint64_t* out, uint64_t* tsum,
+                                                           uint64_t n) {
+  __shared__ uint64_t sh[kXsThreads / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kXsTile + (uint64_t)threadIdx.x * kXsPer;
+  uint32_t v[kXsPer];
+  uint64_t mine = 0;
+#pragma unroll
+  for (int i = 0; i < kXsPer; i++) {
+    v[i] = base + i < n ? in[base + i] : 0u;
+    mine += v[i];
+  }
+  uint64_t tot;
+  uint64_t run = block_excl_u64(mine, sh, tot);
+#pragma unroll
+  for (int i = 0; i < kXsPer; i++) {
+    if (base + i < n) out[base + i] = run;
+    run += v[i];
+  }
+  if (threadIdx.x == 0) tsum[blockIdx.x] = tot;
+}
+__global__ __launch_bounds__(1024) void k_xscan_top(uint64_t* tsum, uint32_t nt, unsigned long long* tot) {
+  __shared__ uint64_t sh[16];
+  uint64_t carry = 0;
+  for (uint32_t c0 = 0; c0 < nt; c0 += 1024) {
+    const uint32_t i = c0 + threadIdx.x;
+    const uint64_t x = i < nt ? tsum[i] : 0ull;
+    uint64_t t;
+    const uint64_t ex = block_excl_u64(x, sh, t);
+    if (i < nt) tsum[i] = carry + ex;
+    carry += t;
+  }
+  if (threadIdx.x == 0) *tot = carry;
+}
+__global__ __launch_bounds__(256) void k_xscan_add(uint64_t* out, const uint64_t* tsum, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+    out[i] += tsum[i / kXsTile];
+}
+
+// the batch of the first error bounds the fold (records after it never run)
+__device__ __forceinline__ uint32_t aggj_last(const AggjArgs& a) {
+  const uint32_t fe = a.mins->first_err;
+  return fe != 0xFFFFFFFFu && fe < a.nbatches ? fe : (a.nbatches ? a.nbatches - 1 : 0);
+}
+// per batch: folded records and their entries (scal[1], scal[0])
+__global__ __launch_bounds__(256) void k_aggj_bcount(AggjArgs a) {
+  const uint32_t last = aggj_last(a);
+  unsigned long long recs = 0, ents = 0;
+  for (uint32_t b = blockIdx.x * 256 + threadIdx.x; b < a.nbatches; b += gridDim.x * 256) {
+    const BatchStat st = a.bstat[b];
+    const uint32_t n = (b <= last && !(st.flags & BF_DECODE)) ? st.nkeep : 0u;
+    a.bcnt[b] = n;
+    const KeptRec* d = a.desc + a.rbase[b];
+    for (uint32_t k = 0; k < n; k++) ents += (uint32_t)d[k].ival;
+    recs += n;
+  }
+  recs = wave_sum(recs);
+  ents = wave_sum(ents);
+  if (lane_id() == 0 && recs) atomicAdd(&a.scal[1], recs);
+  if (lane_id() == 0 && ents) atomicAdd(&a.scal[0], ents);
+}
+// one wave per batch: the stream's record table
+__global__ __launch_bounds__(256) void k_aggj_flat(AggjArgs a) {
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= a.nbatches) return;
+  const uint32_t n = a.bcnt[b];
+  const uint64_t r0 = a.brec[b], d0 = a.rbase[b];
+  for (uint32_t k = lane_id(); k < n; k += 64) {
+    a.rdesc[r0 + k] = d0 + k;
+    a.rne[r0 + k] = (uint32_t)a.desc[d0 + k].ival;
+  }
+}
+struct AjKey {
+  const uint8_t* p;
+  uint32_t n;
+  bool up;
+};
+__device__ __forceinline__ AjKey aggj_key_of(const AggjArgs& a, unsigned long long ref) {
+  if ((ref >> 32) == 0) {  // initial key
+    const uint32_t k = (uint32_t)ref - 1u;
+    return {(const uint8_t*)a.kptr[k], a.klen[k], false};
+  }
+  const KeptRec& d = a.desc[a.rdesc[(ref >> 32) - 1]];
+  const ElemRec e = a.elem[(d.vpos >> 1) + (uint32_t)ref];
+  return {a.slice + e.pos, e.src_len, (d.pad & KF_UPPER) != 0};
+}
+// the key's slot (claimed if absent); `ref` becomes the slot's occurrence if earlier
+__device__ uint32_t aggj_insert(const AggjArgs& a, unsigned long long ref, const AjKey& me) {
+  uint32_t s = aggj_hash(me.p, me.n, me.up) & (a.cap - 1u);
+  for (;;) {
+    unsigned long long cur = __hip_atomic_load(&a.slot_ref[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == 0) {
+      cur = atomicCAS(&a.slot_ref[s], 0ull, ref);
+      if (cur == 0) return s;
+    }
+    const AjKey o = aggj_key_of(a, cur);
+    if (aggj_key_eq(o.p, o.n, o.up, me.p, me.n, me.up)) {
+      if (ref < cur) atomicMin(&a.slot_ref[s], ref);
+      return s;
+    }
+    s = (s + 1u) & (a.cap - 1u);
+  }
+}
+__global__ __launch_bounds__(256) void k_aggj_init(AggjArgs a) {
+  for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < a.n_init; k += gridDim.x * 256) {
+    const uint32_t s = aggj_insert(a, (unsigned long long)k + 1ull, {(const uint8_t*)a.kptr[k], a.klen[k], false});
+    a.slot_id[s] = k;
+  }
+}
+// one thread per record: its distinct keys into the index
+__global__ __launch_bounds__(256) void k_aggj_insert(AggjArgs a) {
+  for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < a.n_rec; r += (uint64_t)gridDim.x * 256) {
+    const KeptRec& d = a.desc[a.rdesc[r]];
+    const ElemRec* e = a.elem + (d.vpos >> 1);
+    const uint32_t ne = a.rne[r];
+    const uint64_t g0 = a.rent[r];
+    const bool up = (d.pad & KF_UPPER) != 0;
+    for (uint32_t j = 0; j < ne; j++) {
+      const uint8_t* kp = a.slice + e[j].pos;
+      const uint32_t kn = e[j].src_len;
+      bool before = false;  // the record's own map: a key's last value, at its first position
+      for (uint32_t i = 0; i < j && !before; i++) before = aggj_key_eq(a.slice + e[i].pos, e[i].src_len, up, kp, kn, up);
+      if (before) {
+        a.ekid[g0 + j] = kSkipEntry;
+        continue;
+      }
+      uint32_t v = e[j].out_len;
+      for (uint32_t i = j + 1; i < ne; i++)
+        if (aggj_key_eq(a.slice + e[i].pos, e[i].src_len, up, kp, kn, up)) v = e[i].out_len;
+      a.eval[g0 + j] = v;
+      a.ekid[g0 + j] = aggj_insert(a, ((unsigned long long)(r + 1) << 32) | j, {kp, kn, up});
+    }
+  }
+}
+// keys whose first occurrence is in the record
+__global__ __launch_bounds__(256) void k_aggj_new(AggjArgs a) {
+  for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < a.n_rec; r += (uint64_t)gridDim.x * 256) {
+    const uint32_t ne = a.rne[r];
+    const uint64_t g0 = a.rent[r];
+    uint32_t n = 0;
+    for (uint32_t j = 0; j < ne; j++) {
+      const uint32_t s = a.ekid[g0 + j];
+      if (s != kSkipEntry && a.slot_ref[s] == (((unsigned long long)(r + 1) << 32) | j)) n++;
+    }
+    a.rnew[r] = n;
+  }
+}
+__global__ __launch_bounds__(256) void k_aggj_ids(AggjArgs a) {
+  for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < a.n_rec; r += (uint64_t)gridDim.x * 256) {
+    if (!a.rnew[r]) continue;
+    const KeptRec& d = a.desc[a.rdesc[r]];
+    const ElemRec* e = a.elem + (d.vpos >> 1);
+    const uint32_t ne = a.rne[r];
+    const uint64_t g0 = a.rent[r];
+    uint32_t id = a.n_init + (uint32_t)a.rnewb[r];
+    for (uint32_t j = 0; j < ne; j++) {
+      const uint32_t s = a.ekid[g0 + j];
+      if (s == kSkipEntry || a.slot_ref[s] != (((unsigned long long)(r + 1) << 32) | j)) continue;
+      a.slot_id[s] = id;
+      a.tptr[id] = (uint64_t)(a.slice + e[j].pos - 1);  // the source key with its quotes: serde_json's text
+      a.tlen[id] = e[j].src_len + 2u;                   // of an unescaped key
+      a.kup[id] = (d.pad & KF_UPPER) ? 1u : 0u;
+      id++;
+    }
+  }
+}
+__global__ __launch_bounds__(256) void k_aggj_kid(AggjArgs a, uint64_t n_ent) {
+  for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < n_ent; g += (uint64_t)gridDim.x * 256) {
+    const uint32_t s = a.ekid[g];
+    if (s != kSkipEntry) a.ekid[g] = a.slot_id[s];
+  }
+}
+// per block, the sums its records contribute per key
+__global__ __launch_bounds__(256) void k_aggj_bsum(AggjArgs a) {
+  for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < a.n_rec; r += (uint64_t)gridDim.x * 256) {
+    uint32_t* row = a.state + (uint64_t)(r / a.rb) * a.nkeys;
+    const uint32_t ne = a.rne[r];
+    const uint64_t g0 = a.rent[r];
+    for (uint32_t j = 0; j < ne; j++) {
+      const uint32_t k = a.ekid[g0 + j];
+      if (k != kSkipEntry) atomicAdd(&row[k], a.eval[g0 + j]);  // u32 wrapping
+    }
+  }
+}
+// one workgroup per key: exclusive scan down its column, from the initial value
+__global__ __launch_bounds__(256) void k_aggj_colscan(AggjArgs a) {
+  __shared__ uint64_t sh[4];
+  const uint32_t k = blockIdx.x;
+  uint32_t carry = k < a.n_init ? a.val_init[k] : 0u;
+  for (uint32_t c0 = 0; c0 < a.nblk; c0 += 256) {
+    const uint32_t b = c0 + threadIdx.x;
+    uint32_t* p = a.state + (uint64_t)b * a.nkeys + k;
+    const uint32_t x = b < a.nblk ? *p : 0u;
+    uint64_t t;
+    const uint64_t ex = block_excl_u64(x, sh, t);
+    if (b < a.nblk) *p = carry + (uint32_t)ex;
+    carry += (uint32_t)t;
+  }
+}
+__device__ __forceinline__ uint32_t aggj_term(uint32_t k, uint32_t tl, uint32_t v) {
+  return (k ? 4u : 3u) + tl + 2u + dec_digits_u32(v);  // (k ? ",\n  " : "\n  ") key ": " digits
+}
+// one wave per block of records.  kLds: the values live in LDS (K <= kAjLds),
+// else in the block's own state row (agent-scope atomics: lanes of the wave
+// read what other lanes wrote)
+template <bool kLds>
+__global__ __launch_bounds__(64) void k_aggj_text(AggjArgs a) {
+  __shared__ uint32_t lds[kLds ? kAjLds : 1];
+  const uint32_t b = blockIdx.x, l = lane_id();
+  const uint64_t r0 = (uint64_t)b * a.rb, r1 = r0 + a.rb < a.n_rec ? r0 + a.rb : a.n_rec;
+  if (r0 >= r1) return;
+  uint32_t* row = a.state + (uint64_t)b * a.nkeys;
+  uint32_t* V = kLds ? lds : row;
+  auto vget = [&](uint32_t k) -> uint32_t {
+    return kLds ? V[k] : __hip_atomic_load(&V[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto vset = [&](uint32_t k, uint32_t x) {
+    if (kLds)
+      V[k] = x;
+    else
+      __hip_atomic_store(&V[k], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  const uint32_t nk_end = a.n_init + (uint32_t)(a.rnewb[r1 - 1] + a.rnew[r1 - 1]);
+  if (kLds)
+    for (uint32_t k = l; k < nk_end; k += 64) lds[k] = row[k];
+  uint32_t nk = a.n_init + (uint32_t)a.rnewb[r0];
+  uint64_t tot = 0;  // Σ terms of the keys so far
+  if (!a.write) {
+    for (uint32_t k = l; k < nk; k += 64) tot += aggj_term(k, a.tlen[k], vget(k));
+    tot = wave_sum(tot);
+  }
+  __syncthreads();
+  for (uint64_t r = r0; r < r1; r++) {
+    const uint32_t ne = a.rne[r];
+    const uint64_t g0 = a.rent[r];
+    int64_t delta = 0;
+    for (uint32_t j = l; j < ne; j += 64) {  // distinct keys within the record: no two lanes share one
+      const uint32_t k = a.ekid[g0 + j];
+      if (k == kSkipEntry) continue;
+      const uint32_t old = k < nk ? vget(k) : 0u;
+      const uint32_t nv = old + a.eval[g0 + j];
+      vset(k, nv);
+      if (!a.write)
+        delta += k < nk ? (int64_t)dec_digits_u32(nv) - (int64_t)dec_digits_u32(old)
+                        : (int64_t)aggj_term(k, a.tlen[k], nv);
+    }
+    nk += a.rnew[r];
+    __syncthreads();
+    if (!a.write) {
+      tot += (uint64_t)wave_sum(delta);
+      if (l == 0) a.rlen[r] = nk ? (uint32_t)(tot + 3u) : 2u;
+      continue;
+    }
+    // the text: "{" + terms + "\n}", or "{}"
+    uint8_t* o = a.cat + kCatOff + a.roff[r];
+    const uint32_t len = a.rlen[r];
+    if (l == 0) {
+      o[0] = '{';
+      o[len - 1] = '}';
+      if (nk) o[len - 2] = '\n';
+    }
+    uint64_t q0 = 1;
+    for (uint32_t c0 = 0; c0 < nk; c0 += 64) {
+      const uint32_t k = c0 + l;
+      uint32_t v = k < nk ? vget(k) : 0u, tl = k < nk ? a.tlen[k] : 0u;
+      const uint32_t t = k < nk ? aggj_term(k, tl, v) : 0u;
+      const uint32_t inc = wave_incl_scan(t);
+      if (k < nk) {
+        uint64_t q = q0 + inc - t;
+        if (k) o[q++] = ',';
+        o[q++] = '\n';
+        o[q++] = ' ';
+        o[q++] = ' ';
+        const uint8_t* tp = (const uint8_t*)a.tptr[k];
+        const bool up = a.kup[k] != 0;
+        for (uint32_t c = 0; c < tl; c++) o[q++] = key_byte(tp, c, up);
+        o[q++] = ':';
+        o[q++] = ' ';
+        const uint32_t nd = dec_digits_u32(v);
+        for (uint32_t c = 0; c < nd; c++) {
+          o[q + nd - 1 - c] = (uint8_t)('0' + v % 10u);
+          v /= 10u;
+        }
+      }
+      q0 += __shfl(inc, 63, 64);
+    }
+  }
+}
+// records' text offsets into their descriptors; the accumulator after each batch
+__global__ __launch_bounds__(256) void k_aggj_place(AggjArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < a.n_rec) {
+    KeptRec& d = a.desc[a.rdesc[i]];
+    d.src = kCatOff + a.roff[i];  // k_write reads the text from cat[src, src + vlen) (vpos still locates the entries)
+    d.vlen = a.rlen[i];
+  }
+  if (i < a.nbatches) {
+    const uint64_t n = a.brec[i] + a.bcnt[i];  // records folded up to and including batch i
+    a.acc_off[i] = n ? kCatOff + a.roff[n - 1] : 0;
+    a.acc_len[i] = n ? a.rlen[n - 1] : 0xFFFFFFFFu;
   }
 }
 
@@ -3306,6 +3708,67 @@ void launch_header(const Plan* plan, uint8_t* out, hipStream_t s) {
 }
 void launch_cat(const WriteArgs& a, uint32_t nbatches, hipStream_t s) {
   if (nbatches) hipLaunchKernelGGL(k_cat, dim3((nbatches + 3) / 4), dim3(256), 0, s, a, nbatches);
+}
+static uint32_t grid_for(uint64_t n, uint32_t per = 256, uint32_t cap = 8192) {
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + per - 1) / per, cap));
+}
+void launch_xscan(const uint32_t* in, uint64_t* out, uint64_t* tsum, uint64_t n, unsigned long long* tot,
+                  hipStream_t s) {
+  const uint64_t nt = (n + kXsTile - 1) / kXsTile;
+  if (nt) hipLaunchKernelGGL(k_xscan_tiles, dim3((uint32_t)nt), dim3(kXsThreads), 0, s, in, out, tsum, n);
+  hipLaunchKernelGGL(k_xscan_top, dim3(1), dim3(1024), 0, s, tsum, (uint32_t)nt, tot);
+  if (nt > 1) hipLaunchKernelGGL(k_xscan_add, dim3(grid_for(n)), dim3(256), 0, s, out, tsum, n);
+}
+uint64_t xscan_tiles(uint64_t n) { return (n + kXsTile - 1) / kXsTile + 1; }
+// phase 0: records / entries per batch (scal[0], scal[1])
+void launch_aggj_count(const AggjArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_aggj_bcount, dim3(grid_for(a.nbatches, 256, 1024)), dim3(256), 0, s, a);
+}
+// phase 1 (after the host sized the record / entry tables): record table, key
+// index, ids; scal[2] = new keys
+void launch_aggj_keys(const AggjArgs& a, uint64_t* tsum, hipStream_t s) {
+  launch_xscan(a.bcnt, a.brec, tsum, a.nbatches, a.scal + 4, s);
+  if (a.nbatches) hipLaunchKernelGGL(k_aggj_flat, dim3((a.nbatches + 3) / 4), dim3(256), 0, s, a);
+  launch_xscan(a.rne, a.rent, tsum, a.n_rec, a.scal + 5, s);
+  if (a.n_init) hipLaunchKernelGGL(k_aggj_init, dim3(grid_for(a.n_init)), dim3(256), 0, s, a);
+  if (a.n_rec) {
+    hipLaunchKernelGGL(k_aggj_insert, dim3(grid_for(a.n_rec)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_aggj_new, dim3(grid_for(a.n_rec)), dim3(256), 0, s, a);
+  }
+  launch_xscan(a.rnew, a.rnewb, tsum, a.n_rec, a.scal + 2, s);
+  if (a.n_rec) {
+    hipLaunchKernelGGL(k_aggj_ids, dim3(grid_for(a.n_rec)), dim3(256), 0, s, a);
+  }
+}
+void launch_aggj_kid(const AggjArgs& a, uint64_t n_ent, hipStream_t s) {
+  if (n_ent) hipLaunchKernelGGL(k_aggj_kid, dim3(grid_for(n_ent)), dim3(256), 0, s, a, n_ent);
+}
+// phase 2 (K known, state table zeroed): the block rows
+void launch_aggj_rows(const AggjArgs& a, hipStream_t s) {
+  if (!a.n_rec) return;
+  hipLaunchKernelGGL(k_aggj_bsum, dim3(grid_for(a.n_rec)), dim3(256), 0, s, a);
+  if (a.nkeys) hipLaunchKernelGGL(k_aggj_colscan, dim3(a.nkeys), dim3(256), 0, s, a);
+}
+// phase 3: pass 0 sizes, offsets, placement; scal[3] = text bytes.  With
+// K > kAjLds the pass replays on the rows in place: `a.state` is then a copy
+void launch_aggj_size(const AggjArgs& a, uint64_t* tsum, hipStream_t s) {
+  if (a.n_rec) {
+    if (a.nkeys <= kAjLds)
+      hipLaunchKernelGGL(k_aggj_text<true>, dim3(a.nblk), dim3(64), 0, s, a);
+    else
+      hipLaunchKernelGGL(k_aggj_text<false>, dim3(a.nblk), dim3(64), 0, s, a);
+  }
+  launch_xscan(a.rlen, a.roff, tsum, a.n_rec, a.scal + 3, s);
+  hipLaunchKernelGGL(k_aggj_place, dim3(grid_for(std::max<uint64_t>(a.n_rec, a.nbatches), 256, 1u << 30)), dim3(256),
+                     0, s, a);
+}
+// phase 4: the texts (pass 1), replayed from the block rows
+void launch_aggj_write(const AggjArgs& a, hipStream_t s) {
+  if (!a.n_rec) return;
+  if (a.nkeys <= kAjLds)
+    hipLaunchKernelGGL(k_aggj_text<true>, dim3(a.nblk), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_aggj_text<false>, dim3(a.nblk), dim3(64), 0, s, a);
 }
 void launch_write(const WriteArgs& a, uint32_t nblocks, hipStream_t s) {
   // nblocks = included batches, one wave each

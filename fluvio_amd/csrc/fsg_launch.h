@@ -20,4 +20,12 @@ void launch_write(const WriteArgs& a, uint32_t nblocks, hipStream_t s);
 void launch_cat(const WriteArgs& a, uint32_t nbatches, hipStream_t s);
 void launch_crc(uint8_t* out, uint64_t off, uint64_t n, uint32_t* acc, hipStream_t s);
 void launch_write_lean(const WriteArgs& a, uint32_t nblocks, hipStream_t s);
+// aggregate-json, in phases separated by host reads of AggjArgs::scal
+uint64_t xscan_tiles(uint64_t n);  // u64 scratch slots launch_xscan needs for n items
+void launch_aggj_count(const AggjArgs& a, hipStream_t s);
+void launch_aggj_keys(const AggjArgs& a, uint64_t* tsum, hipStream_t s);
+void launch_aggj_kid(const AggjArgs& a, uint64_t n_ent, hipStream_t s);
+void launch_aggj_rows(const AggjArgs& a, hipStream_t s);
+void launch_aggj_size(const AggjArgs& a, uint64_t* tsum, hipStream_t s);
+void launch_aggj_write(const AggjArgs& a, hipStream_t s);
 }  // namespace fsg

@@ -166,6 +166,172 @@ int32_t acc_value(const std::vector<uint8_t>& a) {
   return (int32_t)acc;
 }
 
+// aggregate-json's `serde_json::from_slice::<HashMap<String, u32>>(acc).unwrap_or_default()`
+// (the accumulator side, host): a JSON object of strings -> u32, whitespace
+// ' ' \t \n \r, string escapes decoded (UTF-8 validated), no sign / fraction /
+// exponent / leading zero / overflow; anything else -> the empty map.  Keys in
+// first-occurrence order, a duplicate key's last value wins.  `text` = the key
+// as serde_json writes it (format_escaped_str).
+struct AccMap {
+  std::vector<std::string> keys, text;
+  std::vector<uint32_t> vals;
+};
+bool parse_acc_map(const std::vector<uint8_t>& s, AccMap& m) {
+  size_t i = 0;
+  const size_t n = s.size();
+  auto ws = [&]() {
+    while (i < n && (s[i] == ' ' || s[i] == '\t' || s[i] == '\n' || s[i] == '\r')) i++;
+  };
+  auto hex4 = [&](uint32_t& v) {
+    if (i + 4 > n) return false;
+    v = 0;
+    for (int k = 0; k < 4; k++) {
+      const uint8_t c = s[i++];
+      const int h = c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'f' ? c - 'a' + 10 : c >= 'A' && c <= 'F' ? c - 'A' + 10 : -1;
+      if (h < 0) return false;
+      v = (v << 4) | (uint32_t)h;
+    }
+    return true;
+  };
+  auto put = [](std::string& o, uint32_t c) {
+    if (c < 0x80) {
+      o += (char)c;
+    } else if (c < 0x800) {
+      o += (char)(0xC0 | (c >> 6));
+      o += (char)(0x80 | (c & 0x3F));
+    } else if (c < 0x10000) {
+      o += (char)(0xE0 | (c >> 12));
+      o += (char)(0x80 | ((c >> 6) & 0x3F));
+      o += (char)(0x80 | (c & 0x3F));
+    } else {
+      o += (char)(0xF0 | (c >> 18));
+      o += (char)(0x80 | ((c >> 12) & 0x3F));
+      o += (char)(0x80 | ((c >> 6) & 0x3F));
+      o += (char)(0x80 | (c & 0x3F));
+    }
+  };
+  auto str = [&](std::string& o) {  // after the opening quote
+    const size_t raw0 = i;
+    (void)raw0;
+    for (;;) {
+      if (i >= n) return false;
+      const uint8_t c = s[i++];
+      if (c == '"') break;
+      if (c < 0x20) return false;
+      if (c != '\\') {
+        o += (char)c;
+        continue;
+      }
+      if (i >= n) return false;
+      const uint8_t e = s[i++];
+      switch (e) {
+        case '"': o += '"'; break;
+        case '\\': o += '\\'; break;
+        case '/': o += '/'; break;
+        case 'b': o += '\b'; break;
+        case 'f': o += '\f'; break;
+        case 'n': o += '\n'; break;
+        case 'r': o += '\r'; break;
+        case 't': o += '\t'; break;
+        case 'u': {
+          uint32_t c1;
+          if (!hex4(c1)) return false;
+          if (c1 >= 0xDC00 && c1 <= 0xDFFF) return false;
+          if (c1 >= 0xD800 && c1 <= 0xDBFF) {
+            uint32_t c2;
+            if (i + 2 > n || s[i] != '\\' || s[i + 1] != 'u') return false;
+            i += 2;
+            if (!hex4(c2) || c2 < 0xDC00 || c2 > 0xDFFF) return false;
+            c1 = (((c1 - 0xD800) << 10) | (c2 - 0xDC00)) + 0x10000;
+          }
+          put(o, c1);
+          break;
+        }
+        default: return false;
+      }
+    }
+    uint32_t vut = 0, el = 0;
+    return utf8_ok((const uint8_t*)o.data(), o.size(), &vut, &el);
+  };
+  auto fail = [&]() {
+    m = AccMap();
+    return false;
+  };
+  ws();
+  if (i >= n || s[i] != '{') return fail();
+  i++;
+  ws();
+  if (i < n && s[i] == '}') {
+    i++;
+  } else {
+    for (;;) {
+      ws();
+      if (i >= n || s[i] != '"') return fail();
+      i++;
+      std::string k;
+      if (!str(k)) return fail();
+      ws();
+      if (i >= n || s[i] != ':') return fail();
+      i++;
+      ws();
+      if (i >= n || s[i] < '0' || s[i] > '9') return fail();  // '-': negative or -0, both errors for u32
+      uint64_t v = 0;
+      const size_t d0 = i;
+      while (i < n && s[i] >= '0' && s[i] <= '9') {
+        v = v * 10 + (uint64_t)(s[i++] - '0');
+        if (v > 0xFFFFFFFFull) return fail();
+      }
+      if (s[d0] == '0' && i - d0 > 1) return fail();  // leading zero
+      if (i < n && (s[i] == '.' || s[i] == 'e' || s[i] == 'E')) return fail();  // a float: invalid type
+      size_t at = 0;
+      while (at < m.keys.size() && m.keys[at] != k) at++;
+      if (at < m.keys.size()) {
+        m.vals[at] = (uint32_t)v;
+      } else {
+        m.keys.push_back(k);
+        m.vals.push_back((uint32_t)v);
+      }
+      ws();
+      if (i < n && s[i] == ',') {
+        i++;
+        continue;
+      }
+      if (i < n && s[i] == '}') {
+        i++;
+        break;
+      }
+      return fail();
+    }
+  }
+  ws();
+  if (i != n) return fail();
+  for (const auto& k : m.keys) {  // format_escaped_str (ser.rs)
+    std::string t = "\"";
+    for (unsigned char c : k) {
+      switch (c) {
+        case '"': t += "\\\""; break;
+        case '\\': t += "\\\\"; break;
+        case '\b': t += "\\b"; break;
+        case '\f': t += "\\f"; break;
+        case '\n': t += "\\n"; break;
+        case '\r': t += "\\r"; break;
+        case '\t': t += "\\t"; break;
+        default:
+          if (c < 0x20) {
+            char b[8];
+            snprintf(b, sizeof b, "\\u%04x", c);
+            t += b;
+          } else {
+            t += (char)c;
+          }
+      }
+    }
+    t += "\"";
+    m.text.push_back(t);
+  }
+  return true;
+}
+
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -237,6 +403,10 @@ struct fsg_chain {
   // scratch
   DevBuf bstat, kept, rows, pre, aggpre, tiles, grand, mins, plan, out, crcparts, defer, elem, cat;
   DevBuf dstate;  // aggregate-sum accumulator (i32) after the last call, in HBM
+  // aggregate-json: key dictionary, index, initial keys, per-batch accumulator text
+  DevBuf aj_kptr, aj_klen, aj_tptr, aj_tlen, aj_kup, aj_vinit, aj_arena, aj_out, aj_accoff, aj_acclen;  // aggregate-json
+  DevBuf aj_bcnt, aj_brec, aj_rdesc, aj_rne, aj_rent, aj_rnew, aj_rnewb, aj_rlen, aj_roff, aj_ekid, aj_eval;
+  DevBuf aj_sref, aj_sid, aj_state, aj_state2, aj_tsum;
   Plan hplan{};
   hipEvent_t ev[6] = {};
   fsg_timings last{};
@@ -419,6 +589,12 @@ int add_stage(fsg_chain* c, const ModuleSpec& m, const std::string& name, uint8_
     sd.kind = FSG_KIND_AGGREGATE;
     c->agg_stage = (int)c->hdesc.nstages;
     c->acc = m.has_acc ? m.acc : std::vector<uint8_t>();
+  } else if (name == "aggregate-json") {  // examples/aggregate-json: HashMap<String, u32> += per key (C5 keyed)
+    sd.op = OP_AGG_JSON;
+    sd.kind = FSG_KIND_AGGREGATE;
+    c->agg_stage = (int)c->hdesc.nstages;
+    c->acc = m.has_acc ? m.acc : std::vector<uint8_t>();
+    vt = VT_SRC;  // the output value is the map's JSON text
   } else if (name == "map_json_project") {  // C3 field projection (parity unpinned: no reference module)
     const std::string* f = param("field");
     const std::string field = f ? *f : std::string("message");
@@ -461,7 +637,9 @@ extern "C" int fsg_chain_builder_initialize(fsg_chain_builder* b, fsg_engine* e,
   c->hdesc.out_type = vt;
   c->hdesc.has_agg = c->agg_stage >= 0;
   if (c->agg_stage >= 0)
-    c->hdesc.flags |= c->hdesc.st[c->agg_stage].op == OP_AGG_SUM ? CF_AGG_SUM : CF_AGG_CAT;
+    c->hdesc.flags |= c->hdesc.st[c->agg_stage].op == OP_AGG_SUM    ? CF_AGG_SUM
+                      : c->hdesc.st[c->agg_stage].op == OP_AGG_JSON ? CF_AGG_JSON
+                                                                     : CF_AGG_CAT;
   if (c->array_stage >= 0) c->hdesc.flags |= CF_ARRAY;
   if (c->agg_stage >= 0) {
     StageDesc& sd = c->hdesc.st[c->agg_stage];
@@ -665,9 +843,12 @@ bool json_hint(uint32_t code_word, uint32_t pos, uint32_t a, uint32_t b, const s
     std::string val;
     json_unescape(v, a, b, val);
     msg = "unknown variant `" + val + "`, expected one of `debug`, `info`, `warn`, `error`";
+  } else if (code == JE_INVALID_VALUE) {  // the u32 visitor (aggregate-json): visit_u64 / visit_i64 out of range
+    msg = std::string("invalid value: integer `") + ((sub & 15) == JU_NINT ? "-" : "") +
+          std::string(v.begin() + a, v.begin() + b) + "`, expected u32";
   } else if (code == JE_INVALID_TYPE) {
     static const char* const kExp[] = {"struct StructuredLog", "a string", "variant identifier", "unit",
-                                       "a sequence", "a map", "", ""};
+                                       "a sequence", "a map", "u32", ""};
     std::string un;
     switch (sub & 15) {
       case JU_UNIT: un = "unit value"; break;
@@ -818,7 +999,8 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   memset(res, 0, sizeof *res);
   // scratch (StoreMemoryExceeded past the store limit, limiter.rs:18-35)
   const bool has_array = c->array_stage >= 0;
-  const size_t elem_cap = has_array ? (s->len / 2 + 2) : 0;  // ElemRec slots (fsg_device.h)
+  const bool has_aggj = (c->hdesc.flags & CF_AGG_JSON) != 0;
+  const size_t elem_cap = (has_array || has_aggj) ? (s->len / 2 + 2) : 0;  // ElemRec slots (fsg_device.h)
   const size_t need = (size_t)std::max<uint32_t>(nb, 1) * (sizeof(BatchStat) + 3 * sizeof(ScanRow)) +
                       (size_t)std::max<uint64_t>(s->nrec, 1) * sizeof(KeptRec) + elem_cap * sizeof(ElemRec);
   if (need > c->limit) {
@@ -839,10 +1021,10 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   HIPCHK(c->grand.ensure(sizeof(ScanRow)));
   HIPCHK(c->mins.ensure(sizeof(Mins)));
   HIPCHK(c->plan.ensure(sizeof(Plan)));
-  if (has_array) HIPCHK(c->elem.ensure(elem_cap * sizeof(ElemRec)));
+  if (has_array || has_aggj) HIPCHK(c->elem.ensure(elem_cap * sizeof(ElemRec)));
   const bool has_agg = c->agg_stage >= 0;
   const bool has_cat = has_agg && (c->hdesc.flags & CF_AGG_CAT);
-  const int64_t acc0 = has_agg && !has_cat ? acc_value(c->acc) : 0;
+  const int64_t acc0 = has_agg && !has_cat && !has_aggj ? acc_value(c->acc) : 0;
 
   HIPCHK(hipMemsetAsync(c->mins.p, 0xFF, sizeof(Mins), st));
   HIPCHK(hipEventRecord(c->ev[0], st));
@@ -858,7 +1040,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   ea.desc = c->kept.as<KeptRec>();
   ea.mins = c->mins.as<Mins>();
   ea.list = c->defer.as<uint32_t>();
-  ea.elem = has_array ? c->elem.as<ElemRec>() : nullptr;
+  ea.elem = (has_array || has_aggj) ? c->elem.as<ElemRec>() : nullptr;
   uint32_t ops = 0;
   bool lean_stages = true;  // every stage has a lean form
   bool projected = false;  // a projection seen: only uppercase maps may follow on the lean path
@@ -885,6 +1067,150 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[1], st));
   launch_mins(ea.bstat, nb, ea.mins, st);
+  // aggregate-json: fold the entries in stream order, size every record's map text
+  AggjArgs aj{};
+  AccMap am;
+  if (has_aggj) {
+    parse_acc_map(c->acc, am);  // unwrap_or_default
+    const uint32_t n_init = (uint32_t)am.keys.size();
+    const size_t nbb = std::max<uint32_t>(nb, 1);
+    HIPCHK(c->aj_out.ensure(64));
+    HIPCHK(c->aj_bcnt.ensure(nbb * 4));
+    HIPCHK(c->aj_brec.ensure(nbb * 8));
+    HIPCHK(c->aj_accoff.ensure(nbb * 8));
+    HIPCHK(c->aj_acclen.ensure(nbb * 4));
+    HIPCHK(hipMemsetAsync(c->aj_out.p, 0, 64, st));
+    aj.slice = ea.slice;
+    aj.bstat = ea.bstat;
+    aj.desc = ea.desc;
+    aj.rbase = ea.rbase;
+    aj.elem = ea.elem;
+    aj.mins = ea.mins;
+    aj.nbatches = nb;
+    aj.bcnt = c->aj_bcnt.as<uint32_t>();
+    aj.brec = c->aj_brec.as<uint64_t>();
+    aj.scal = c->aj_out.as<unsigned long long>();
+    aj.acc_off = c->aj_accoff.as<uint64_t>();
+    aj.acc_len = c->aj_acclen.as<uint32_t>();
+    aj.n_init = n_init;
+    launch_aggj_count(aj, st);
+    unsigned long long sc[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(sc, c->aj_out.p, sizeof sc, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const uint64_t nent = sc[0], nrec = sc[1];
+    uint32_t cap = 16;
+    while (cap < 2 * (n_init + nent) + 1) cap <<= 1;
+    const size_t nkmax = (size_t)n_init + nent + 1;
+    const size_t dict = (size_t)nrec * 44 + (size_t)nent * 8 + (size_t)cap * 12 + nkmax * 28;
+    if (dict > c->limit) {
+      char b[160];
+      snprintf(b, sizeof b, "Requested memory %zub exceeded max allowed %zub", dict, c->limit);
+      g_store_mem[0] = 0;
+      g_store_mem[1] = dict;
+      g_store_mem[2] = c->limit;
+      return fail(FSG_E_STORE_MEMORY, b);
+    }
+    const size_t nr1 = std::max<uint64_t>(nrec, 1), ne1 = std::max<uint64_t>(nent, 1);
+    HIPCHK(c->aj_rdesc.ensure(nr1 * 8));
+    HIPCHK(c->aj_rne.ensure(nr1 * 4));
+    HIPCHK(c->aj_rent.ensure(nr1 * 8));
+    HIPCHK(c->aj_rnew.ensure(nr1 * 4));
+    HIPCHK(c->aj_rnewb.ensure(nr1 * 8));
+    HIPCHK(c->aj_rlen.ensure(nr1 * 4));
+    HIPCHK(c->aj_roff.ensure(nr1 * 8));
+    HIPCHK(c->aj_ekid.ensure(ne1 * 4));
+    HIPCHK(c->aj_eval.ensure(ne1 * 4));
+    HIPCHK(c->aj_sref.ensure((size_t)cap * 8));
+    HIPCHK(c->aj_sid.ensure((size_t)cap * 4));
+    HIPCHK(c->aj_tptr.ensure(nkmax * 8));
+    HIPCHK(c->aj_tlen.ensure(nkmax * 4));
+    HIPCHK(c->aj_kup.ensure(nkmax * 4));
+    HIPCHK(c->aj_kptr.ensure((size_t)(n_init + 1) * 8));
+    HIPCHK(c->aj_klen.ensure((size_t)(n_init + 1) * 4));
+    HIPCHK(c->aj_vinit.ensure((size_t)(n_init + 1) * 4));
+    HIPCHK(c->aj_tsum.ensure(xscan_tiles(std::max<uint64_t>(nrec, std::max<uint64_t>(nent, nb))) * 8));
+    HIPCHK(hipMemsetAsync(c->aj_sref.p, 0, (size_t)cap * 8, st));
+    if (n_init) {  // the initial accumulator's keys: match bytes and serialized text in one arena
+      std::vector<uint8_t> arena;
+      std::vector<uint64_t> ko(n_init), to(n_init);
+      std::vector<uint32_t> kl(n_init), tl(n_init), zero(n_init, 0);
+      for (uint32_t k = 0; k < n_init; k++) {
+        ko[k] = arena.size();
+        arena.insert(arena.end(), am.keys[k].begin(), am.keys[k].end());
+        to[k] = arena.size();
+        arena.insert(arena.end(), am.text[k].begin(), am.text[k].end());
+        kl[k] = (uint32_t)am.keys[k].size();
+        tl[k] = (uint32_t)am.text[k].size();
+      }
+      HIPCHK(c->aj_arena.ensure(arena.size() + 16));
+      const uint64_t base = (uint64_t)c->aj_arena.p;
+      for (uint32_t k = 0; k < n_init; k++) {
+        ko[k] += base;
+        to[k] += base;
+      }
+      HIPCHK(hipMemcpyAsync(c->aj_arena.p, arena.data(), arena.size(), hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(c->aj_kptr.p, ko.data(), n_init * 8, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(c->aj_tptr.p, to.data(), n_init * 8, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(c->aj_klen.p, kl.data(), n_init * 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(c->aj_tlen.p, tl.data(), n_init * 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(c->aj_kup.p, zero.data(), n_init * 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(c->aj_vinit.p, am.vals.data(), n_init * 4, hipMemcpyHostToDevice, st));
+    }
+    aj.n_rec = nrec;
+    aj.rdesc = c->aj_rdesc.as<uint64_t>();
+    aj.rne = c->aj_rne.as<uint32_t>();
+    aj.rent = c->aj_rent.as<uint64_t>();
+    aj.rnew = c->aj_rnew.as<uint32_t>();
+    aj.rnewb = c->aj_rnewb.as<uint64_t>();
+    aj.rlen = c->aj_rlen.as<uint32_t>();
+    aj.roff = c->aj_roff.as<uint64_t>();
+    aj.ekid = c->aj_ekid.as<uint32_t>();
+    aj.eval = c->aj_eval.as<uint32_t>();
+    aj.slot_ref = c->aj_sref.as<unsigned long long>();
+    aj.slot_id = c->aj_sid.as<uint32_t>();
+    aj.cap = cap;
+    aj.kptr = c->aj_kptr.as<uint64_t>();
+    aj.klen = c->aj_klen.as<uint32_t>();
+    aj.val_init = c->aj_vinit.as<uint32_t>();
+    aj.tptr = c->aj_tptr.as<uint64_t>();
+    aj.tlen = c->aj_tlen.as<uint32_t>();
+    aj.kup = c->aj_kup.as<uint32_t>();
+    launch_aggj_keys(aj, c->aj_tsum.as<uint64_t>(), st);
+    launch_aggj_kid(aj, nent, st);
+    unsigned long long nnew = 0;
+    HIPCHK(hipMemcpyAsync(&nnew, aj.scal + 2, sizeof nnew, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const uint64_t K = n_init + nnew;
+    // blocks of rb records: ~4096 blocks (one wave each), the row table
+    // nblk x K bounded to 64 Mi values
+    uint64_t rb = std::max<uint64_t>(32, (nrec + 4095) / 4096);
+    while (((nrec + rb - 1) / rb) * K > (64ull << 20) && rb < nrec) rb *= 2;
+    const uint64_t nblk = nrec ? (nrec + rb - 1) / rb : 0;
+    const size_t rows = (size_t)std::max<uint64_t>(nblk * K, 1) * 4;
+    if (dict + rows * (K > kAjLds ? 2 : 1) > c->limit) {
+      char b[160];
+      snprintf(b, sizeof b, "Requested memory %zub exceeded max allowed %zub", dict + rows, c->limit);
+      g_store_mem[0] = dict;
+      g_store_mem[1] = dict + rows;
+      g_store_mem[2] = c->limit;
+      return fail(FSG_E_STORE_MEMORY, b);
+    }
+    HIPCHK(c->aj_state.ensure(rows));
+    HIPCHK(hipMemsetAsync(c->aj_state.p, 0, rows, st));
+    aj.nkeys = (uint32_t)K;
+    aj.rb = (uint32_t)rb;
+    aj.nblk = (uint32_t)nblk;
+    aj.state = c->aj_state.as<uint32_t>();
+    launch_aggj_rows(aj, st);
+    AggjArgs a0 = aj;
+    if (K > kAjLds) {  // pass 0 replays in place: on a copy of the rows
+      HIPCHK(c->aj_state2.ensure(rows));
+      HIPCHK(hipMemcpyAsync(c->aj_state2.p, c->aj_state.p, rows, hipMemcpyDeviceToDevice, st));
+      a0.state = c->aj_state2.as<uint32_t>();
+    }
+    a0.write = 0;
+    launch_aggj_size(a0, c->aj_tsum.as<uint64_t>(), st);
+  }
   SizeArgs sa{};
   sa.bstat = ea.bstat;
   sa.desc = ea.desc;
@@ -958,6 +1284,23 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     wa.cat = c->cat.as<uint8_t>();
     launch_cat(wa, nb, st);
   }
+  if (has_aggj) {  // pass 1: the map texts into cat (sized by pass 0)
+    uint64_t aj_total = 0;
+    HIPCHK(hipMemcpy(&aj_total, aj.scal + 3, sizeof aj_total, hipMemcpyDeviceToHost));
+    if (aj_total + kCatOff > c->limit) {
+      char b[160];
+      snprintf(b, sizeof b, "Requested memory %zub exceeded max allowed %zub", (size_t)(aj_total + kCatOff), c->limit);
+      g_store_mem[0] = 0;
+      g_store_mem[1] = aj_total + kCatOff;
+      g_store_mem[2] = c->limit;
+      return fail(FSG_E_STORE_MEMORY, b);
+    }
+    HIPCHK(c->cat.ensure(kCatOff + aj_total + 64));
+    aj.cat = c->cat.as<uint8_t>();
+    aj.write = 1;
+    launch_aggj_write(aj, st);
+    wa.cat = aj.cat;
+  }
   launch_header(pa.plan, wa.out, st);
   HIPCHK(hipEventRecord(c->ev[3], st));
   const uint32_t nblk = p.last >= p.first && p.first >= 0 ? (uint32_t)(p.last - p.first + 1) : 0u;
@@ -999,7 +1342,18 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     if (rc) return rc;
     res->has_error = 1;
   }
-  if (has_agg && p.acc_touched) {
+  if (has_aggj && p.stop >= 0) {  // the accumulator text after the last processed batch
+    uint64_t off = 0;
+    uint32_t len = 0xFFFFFFFFu;
+    HIPCHK(hipMemcpy(&off, c->aj_accoff.as<uint64_t>() + p.stop, sizeof off, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&len, c->aj_acclen.as<uint32_t>() + p.stop, sizeof len, hipMemcpyDeviceToHost));
+    if (len != 0xFFFFFFFFu) {
+      std::vector<uint8_t> na(len);
+      if (len) HIPCHK(hipMemcpy(na.data(), c->cat.as<uint8_t>() + off, len, hipMemcpyDeviceToHost));
+      c->acc.swap(na);
+    }
+  }
+  if (has_agg && !has_aggj && p.acc_touched) {
     if (has_cat) {
       std::vector<uint8_t> na(c->acc.size() + p.cat_final);
       HIPCHK(hipMemcpy(na.data(), c->cat.as<uint8_t>() + kCatOff, na.size(), hipMemcpyDeviceToHost));
@@ -1121,6 +1475,29 @@ extern "C" int fsg_chain_get_accumulator(fsg_chain* c, size_t stage, uint8_t** a
   *acc = (uint8_t*)malloc(std::max<size_t>(1, c->acc.size()));
   memcpy(*acc, c->acc.data(), c->acc.size());
   *len = c->acc.size();
+  return FSG_OK;
+}
+
+extern "C" int fsg_chain_keyed_state(fsg_chain* c, size_t stage, uint64_t* dev_fp, uint32_t* dev_val, size_t cap,
+                                     size_t* n) {
+  if ((int)stage != c->agg_stage || !(c->hdesc.flags & CF_AGG_JSON))
+    return fail(FSG_E_INVALID_ARG, "stage is not an aggregate-json aggregate");
+  AccMap m;
+  parse_acc_map(c->acc, m);  // the accumulator as the next record would read it
+  std::vector<uint64_t> fp(m.keys.size());
+  for (size_t k = 0; k < m.keys.size(); k++) {  // FNV-1a 64 of the key's bytes
+    uint64_t h = 14695981039346656037ull;
+    for (unsigned char ch : m.keys[k]) h = (h ^ ch) * 1099511628211ull;
+    fp[k] = h;
+  }
+  *n = m.keys.size();
+  const size_t w = std::min(cap, m.keys.size());
+  HIPCHK(hipSetDevice(c->eng->device));
+  if (w) {
+    HIPCHK(hipMemcpyAsync(dev_fp, fp.data(), w * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(dev_val, m.vals.data(), w * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
   return FSG_OK;
 }
 

@@ -124,3 +124,42 @@ def merge_states_torch(vec: Sequence[int]) -> List[int]:
     t = torch.tensor(list(vec), dtype=torch.int32)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [int(x) for x in t.tolist()]
+
+
+def fnv1a64(key: bytes) -> int:
+    """The key fingerprint of fsg_chain_keyed_state (FNV-1a 64)."""
+    h = 14695981039346656037
+    for c in key:
+        h = ((h ^ c) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def merge_keyed_torch(fp, val, dist=None, group=None):
+    """Topic totals of aggregate-json states (C5 keyed): every rank's (key
+    fingerprint, u32 value) pairs gathered with one all_gather (RCCL on GPU
+    tensors, gloo on CPU ones), then summed per key (u32 wrapping) on the
+    tensors' device.  `fp` int64 (the u64 bits), `val` int64.  Returns
+    (fingerprints, sums) sorted by fingerprint, identical on every rank."""
+    import torch
+    if dist is not None and dist.is_initialized() and dist.get_world_size(group) > 1:
+        world = dist.get_world_size(group)
+        n = torch.tensor([fp.numel()], dtype=torch.int64, device=fp.device)
+        dist.all_reduce(n, op=dist.ReduceOp.MAX, group=group)
+        m = int(n.item())
+        pad = m - fp.numel()
+        fpp = torch.cat([fp, torch.zeros(pad, dtype=torch.int64, device=fp.device)])
+        valp = torch.cat([val, torch.zeros(pad, dtype=torch.int64, device=fp.device)])
+        okp = torch.cat([torch.ones(fp.numel(), dtype=torch.int64, device=fp.device),
+                         torch.zeros(pad, dtype=torch.int64, device=fp.device)])
+        packed = torch.stack([fpp, valp, okp])                   # one collective for the three rows
+        bufs = [torch.empty_like(packed) for _ in range(world)]
+        dist.all_gather(bufs, packed, group=group)
+        allp = torch.cat(bufs, dim=1)
+        keep = allp[2] == 1
+        fp, val = allp[0][keep], allp[1][keep]
+    if fp.numel() == 0:
+        return fp, val
+    keys, inv = torch.unique(fp, sorted=True, return_inverse=True)
+    sums = torch.zeros(keys.numel(), dtype=torch.int64, device=fp.device)
+    sums.index_add_(0, inv, val)
+    return keys, sums & 0xFFFFFFFF

@@ -32,8 +32,8 @@ from .protocol import Batch, Record, decode_batch, decode_records, encode_record
 DEFAULT_SMARTENGINE_VERSION = 22  # input.rs:14 SMARTMODULE_TIMESTAMPS_VERSION
 
 BUILTINS = ("filter", "filter_init", "filter_with_param", "regex-filter", "filter_regex", "filter_odd",
-            "map", "map_double", "filter_map", "aggregate-sum", "aggregate", "filter_json",
-            "array_map_json_array")
+            "map", "map_double", "filter_map", "aggregate-sum", "aggregate", "aggregate-json", "filter_json",
+            "array_map_json_array", "map_json_project")
 
 
 def builtin(name: str) -> bytes:
@@ -413,6 +413,15 @@ class SmartModuleChainInstance:
         _ffi.lib().fsg_free(p)
         return data
 
+
+    def keyed_state(self, stage: int, dev_fp: int, dev_val: int, cap: int) -> int:
+        """aggregate-json: write the accumulator's (FNV-1a 64 key fingerprint, u32
+        value) pairs into device buffers (raw pointers, `cap` pairs); returns the
+        number of pairs in the state (fsg_chain_keyed_state)."""
+        n = ctypes.c_size_t()
+        _check(_ffi.lib().fsg_chain_keyed_state(self._h, stage, ctypes.c_void_p(dev_fp), ctypes.c_void_p(dev_val),
+                                                cap, ctypes.byref(n)))
+        return n.value
     def last_timings(self) -> Dict[str, float]:
         t = _ffi.fsg_timings()
         _check(_ffi.lib().fsg_chain_last_timings(self._h, ctypes.byref(t)))

@@ -49,3 +49,33 @@ def make_slice_array(kind: int, nrec: int, seed: int = None, base_offset: int = 
 def make_slice(kind: int, nrec: int, seed: int = None, base_offset: int = 0, max_section: int = 16384) -> bytes:
     """Returns the encoded batches (file format) holding `nrec` records."""
     return make_slice_array(kind, nrec, seed, base_offset, max_section).tobytes()
+
+
+def make_keyed_slices(partitions: int = 64, nrec: int = 5000, nkeys: int = 10000, seed: int = 0xF106,
+                      owned=None) -> dict:
+    """C5 keyed: records `{"repo-NNNN": n}` (aggregate-json input), the record
+    key = the repo name, routed to partition SipHash(key) mod P exactly as
+    fluvio's producer does (partitioning.rs:70-83), so every key lives in one
+    partition.  ~16 KiB batches (tools/synth.c synth_keyed); returns
+    {partition: slice bytes} for `owned` (all partitions by default)."""
+    from . import partitions as PT
+    keys = [b"repo-%04d" % i for i in range(nkeys)]
+    by_p = {}
+    for k in keys:
+        by_p.setdefault(PT.partition_siphash(k, partitions), []).append(k)
+    L = _l()
+    L.synth_keyed.restype = ctypes.c_size_t
+    L.synth_keyed.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
+                              ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t]
+    out = {}
+    for p in (owned if owned is not None else range(partitions)):
+        ks = by_p.get(p) or [b"repo-none"]
+        blob = b"".join(ks)
+        off = np.zeros(len(ks) + 1, dtype=np.uint32)
+        off[1:] = np.cumsum([len(k) for k in ks])
+        cap = nrec * 80 + 65536
+        buf = np.zeros(cap, dtype=np.uint8)
+        n = L.synth_keyed(blob, off.ctypes.data, len(ks), nrec, seed * 1000003 + p, 0, buf.ctypes.data, cap)
+        assert n, "synth_keyed: buffer too small"
+        out[p] = buf[:n].tobytes()
+    return out

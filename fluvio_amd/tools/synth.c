@@ -271,3 +271,73 @@ size_t synth_slice(int kind, uint64_t nrec, uint64_t seed, int64_t base, uint8_t
   }
   return pos;
 }
+
+
+/* C5 keyed (aggregate-json input): records `{"<key>":n}` (n in 1..100) whose
+ * record key is the same <key>, picked uniformly from the caller's key list
+ * (the keys SipHash routes to this partition).  keys = concatenated key bytes,
+ * koff[k] .. koff[k + 1] = key k.  ~16 KiB record sections. */
+size_t synth_keyed(const uint8_t *keys, const uint32_t *koff, uint32_t nkeys, uint64_t nrec, uint64_t seed,
+                   int64_t base, uint8_t *out, size_t cap) {
+  rs = seed * 0x9E3779B97F4A7C15ull + 0x7654321ull;
+  if (!rs) rs = 1;
+  size_t pos = 0;
+  uint64_t done = 0;
+  static uint8_t val[256], rec[512];
+  while (done < nrec) {
+    if (pos + 61 > cap) return 0;
+    uint8_t *bh = out + pos;
+    size_t q = pos + 61;
+    uint32_t cnt = 0;
+    size_t sec = 4;
+    while (done + cnt < nrec) {
+      const uint32_t k = rnd_n(nkeys);
+      const uint8_t *kp = keys + koff[k];
+      const size_t kl = koff[k + 1] - koff[k];
+      if (kl > 64) return 0;
+      size_t vl = 0;
+      val[vl++] = '{';
+      val[vl++] = '"';
+      memcpy(val + vl, kp, kl);
+      vl += kl;
+      vl += (size_t)sprintf((char *)val + vl, "\":%u}", 1 + rnd_n(100));
+      size_t inner = 1 + vsz(0) + vsz((int64_t)cnt) + 1 + vsz((int64_t)kl) + kl + vsz((int64_t)vl) + vl + 1;
+      size_t rl = vsz((int64_t)inner) + inner;
+      if (cnt > 0 && sec + rl > 16384) break;
+      size_t w = venc((int64_t)inner, rec);
+      rec[w++] = 0;
+      w += venc(0, rec + w);
+      w += venc((int64_t)cnt, rec + w);
+      rec[w++] = 1;
+      w += venc((int64_t)kl, rec + w);
+      memcpy(rec + w, kp, kl);
+      w += kl;
+      w += venc((int64_t)vl, rec + w);
+      memcpy(rec + w, val, vl);
+      w += vl;
+      rec[w++] = 0;
+      if (q + w > cap) return 0;
+      memcpy(out + q, rec, w);
+      q += w;
+      sec += w;
+      cnt++;
+    }
+    const int64_t first_ts = 1700000000000LL + (int64_t)(done / 64);
+    be(bh + 0, (uint64_t)(base + (int64_t)done), 8);
+    be(bh + 8, (uint32_t)(45 + sec), 4);
+    be(bh + 12, 0, 4);
+    bh[16] = 2;
+    be(bh + 21, 0, 2);
+    be(bh + 23, cnt - 1, 4);
+    be(bh + 27, (uint64_t)first_ts, 8);
+    be(bh + 35, (uint64_t)first_ts, 8);
+    be(bh + 43, 0, 8);
+    be(bh + 51, (uint16_t)-1, 2);
+    be(bh + 53, (uint32_t)-1, 4);
+    be(bh + 57, cnt, 4);
+    be(bh + 17, crc32c(bh + 21, q - (pos + 21)), 4);
+    pos = q;
+    done += cnt;
+  }
+  return pos;
+}

@@ -173,6 +173,12 @@ int fsg_chain_process_batch(fsg_chain *c, const uint8_t *slice, size_t len, uint
                             fsg_metrics *metrics, fsg_batch_output **out);
 int fsg_chain_look_back(fsg_chain *c, fsg_metrics *metrics); /* no look_back stages: Ok */
 int fsg_chain_get_accumulator(fsg_chain *c, size_t stage, uint8_t **acc, size_t *len);
+/* aggregate-json (C5 keyed): the accumulator's (key fingerprint, u32 value)
+ * pairs for a cross-partition merge (FNV-1a 64 of each key's bytes) into device
+ * buffers of `cap` pairs; *n = pairs in the state.  Merging per-GPU tables is
+ * the caller's collective (RCCL all-gather + a keyed sum); no reference
+ * counterpart (each partition's own state is the reference's). */
+int fsg_chain_keyed_state(fsg_chain *c, size_t stage, uint64_t *dev_fp, uint32_t *dev_val, size_t cap, size_t *n);
 int fsg_chain_last_timings(fsg_chain *c, fsg_timings *t);
 void fsg_chain_free(fsg_chain *c);
 void fsg_output_free(fsg_output *o);

@@ -1519,3 +1519,176 @@ int orc_json_struct(const uint8_t *s, size_t n, const char *name, const char **f
   }
   return r;
 }
+
+/* ------------------------------------------------------------------------
+ * aggregate-json (smartmodule/examples/aggregate-json/src/lib.rs:1-36):
+ * serde_json::from_slice::<HashMap<String, u32>> of one value (de.rs
+ * deserialize_map + MapAccess, keys deserialize_string, values through the
+ * u32 PrimitiveVisitor of deserialize_number: visit_u64 / visit_i64 out of
+ * range -> "invalid value: integer `N`, expected u32", anything else ->
+ * "invalid type: ..., expected u32"; a float is outside the restatement).
+ * Entries come back in text order, duplicates included (HashMap::insert:
+ * the last value of a key wins).  0 = ok, ORC_E_UNSUPPORTED, or -1 with *msg.
+ * ---------------------------------------------------------------------- */
+static int deserialize_u32(jde *d, uint32_t *out) {
+  int peek = parse_whitespace(d);
+  if (peek < 0) return jpeek_error(d, E_EOF_VALUE);
+  if (peek == '-' || isdig(peek)) {
+    const int pos = peek != '-';
+    if (!pos) jeat(d);
+    jnum num;
+    if (parse_integer(d, pos, &num)) return -1;
+    if (num.is_float) return junsupported(d); /* visit_f64: float Display outside the restatement */
+    if (num.neg || num.mag > 0xFFFFFFFFull) {
+      if (num.neg)
+        jcustom(d, "invalid value: integer `-%llu`, expected u32", (unsigned long long)num.mag);
+      else
+        jcustom(d, "invalid value: integer `%llu`, expected u32", (unsigned long long)num.mag);
+      jfix_position(d);
+      return -1;
+    }
+    *out = (uint32_t)num.mag;
+    return 0;
+  }
+  return peek_invalid_type(d, "u32");
+}
+
+int orc_json_map_u32(const uint8_t *s, size_t n, uint8_t ***keys, size_t **klens, uint32_t **vals, size_t *count,
+                     char **msg, size_t *msg_len) {
+  jde d;
+  memset(&d, 0, sizeof d);
+  d.s = s;
+  d.n = n;
+  d.depth = 128;
+  *msg = NULL;
+  *keys = NULL;
+  *klens = NULL;
+  *vals = NULL;
+  *count = 0;
+  size_t cap = 0;
+  int r = 0;
+  int peek = parse_whitespace(&d);
+  if (peek < 0) {
+    r = jpeek_error(&d, E_EOF_VALUE);
+  } else if (peek == '{') { /* deserialize_map */
+    --d.depth;
+    jeat(&d);
+    int first = 1;
+    for (;;) {
+      int p = parse_whitespace(&d);
+      if (p == '}') break;
+      if (p == ',' && !first) {
+        jeat(&d);
+        p = parse_whitespace(&d);
+      } else if (p >= 0) {
+        if (first)
+          first = 0;
+        else {
+          r = jpeek_error(&d, E_OBJ_COMMA);
+          break;
+        }
+      } else {
+        r = jpeek_error(&d, E_EOF_OBJECT);
+        break;
+      }
+      if (p == '}') { r = jpeek_error(&d, E_TRAILING_COMMA); break; }
+      if (p < 0) { r = jpeek_error(&d, E_EOF_VALUE); break; }
+      if (p != '"') { r = jpeek_error(&d, E_KEY); break; }
+      jeat(&d);
+      jbuf key;
+      if (parse_str(&d, &key)) {
+        free(key.b);
+        r = -1;
+        break;
+      }
+      int c = parse_whitespace(&d);
+      if (c == ':')
+        jeat(&d);
+      else if (c >= 0) {
+        free(key.b);
+        r = jpeek_error(&d, E_COLON);
+        break;
+      } else {
+        free(key.b);
+        r = jpeek_error(&d, E_EOF_OBJECT);
+        break;
+      }
+      uint32_t v = 0;
+      if (deserialize_u32(&d, &v)) {
+        free(key.b);
+        r = -1;
+        break;
+      }
+      if (*count == cap) {
+        cap = cap * 2 + 8;
+        *keys = (uint8_t **)realloc(*keys, cap * sizeof(uint8_t *));
+        *klens = (size_t *)realloc(*klens, cap * sizeof(size_t));
+        *vals = (uint32_t *)realloc(*vals, cap * sizeof(uint32_t));
+      }
+      (*keys)[*count] = key.b ? key.b : (uint8_t *)malloc(1);
+      (*klens)[*count] = key.n;
+      (*vals)[*count] = v;
+      (*count)++;
+    }
+    d.depth++;
+    if (r) {
+      jde probe = d;
+      probe.msg = NULL;
+      probe.msg_len = 0;
+      probe.failed = 0;
+      (void)end_map(&probe);
+      free(probe.msg);
+      d.i = probe.i;
+    } else {
+      r = end_map(&d);
+    }
+    if (r) jfix_position(&d);
+  } else {
+    r = peek_invalid_type(&d, "a map");
+    jfix_position(&d);
+  }
+  if (!r && parse_whitespace(&d) >= 0) r = jpeek_error(&d, E_TRAILING); /* Deserializer::end */
+  if (!r) {
+    free(d.msg);
+    return 0;
+  }
+  for (size_t k = 0; k < *count; k++) free((*keys)[k]);
+  free(*keys);
+  free(*klens);
+  free(*vals);
+  *keys = NULL;
+  *klens = NULL;
+  *vals = NULL;
+  *count = 0;
+  if (d.unsupported) {
+    free(d.msg);
+    return ORC_E_UNSUPPORTED;
+  }
+  *msg = render(&d, msg_len);
+  free(d.msg);
+  if (memchr(*msg, 0, *msg_len)) {
+    free(*msg);
+    *msg = NULL;
+    return ORC_E_UNSUPPORTED;
+  }
+  return -1;
+}
+
+/* serde_json::to_vec_pretty of a map (ser.rs PrettyFormatter, two-space
+ * indent): "{}" when empty, else "{\n  \"k\": v,\n  ...\n}" */
+void orc_json_pretty_map(uint8_t *const *keys, const size_t *klens, const uint32_t *vals, size_t n, uint8_t **out,
+                         size_t *out_len) {
+  jbuf o = {0};
+  jb_byte(&o, '{');
+  for (size_t k = 0; k < n; k++) {
+    jb_push(&o, (const uint8_t *)(k ? ",\n  " : "\n  "), k ? 4 : 3);
+    canon_str(&o, keys[k], klens[k]);
+    char num[16];
+    int nl = snprintf(num, sizeof num, ": %u", vals[k]);
+    jb_push(&o, (const uint8_t *)num, (size_t)nl);
+  }
+  if (n) jb_push(&o, (const uint8_t *)"\n}", 2);
+  else jb_byte(&o, '}');
+  *out = o.b;
+  *out_len = o.n;
+}

@@ -1116,6 +1116,7 @@ enum {
   M_FILTER_JSON, /* examples/filter_json: StructuredLog.level > Debug */
   M_ARRAY_MAP,   /* examples/array_map_json_array: explode a JSON array */
   M_PROJECT,     /* map_json_project: the value of one JSON field (C3 projection) */
+  M_AGG_JSON,    /* examples/aggregate-json: HashMap<String, u32> += per key (C5 keyed) */
 };
 
 typedef struct {
@@ -1227,6 +1228,9 @@ int orc_chain_add(orc_chain *c, const char *module, const char **keys, const cha
   } else if (!strcmp(module, "array_map_json_array")) {
     s.mod = M_ARRAY_MAP;
     s.kind = K_ARRAY_MAP;
+  } else if (!strcmp(module, "aggregate-json")) {
+    s.mod = M_AGG_JSON;
+    s.kind = K_AGGREGATE;
   } else if (!strcmp(module, "map_json_project")) { /* param field, default "message" */
     v = param_get(keys, vals, n_params, "field");
     if (!v) v = "message";
@@ -1373,6 +1377,93 @@ static void stage_run(stage_t *s, recvec *in, int64_t base_offset, stage_out *o)
         }
         free(el);
         free(ln);
+        break;
+      }
+      case M_AGG_JSON: {
+        /* aggregate-json/src/lib.rs:22-36: accumulated = from_slice(acc).unwrap_or_default();
+         * new = from_slice(value)?; accumulated + new (per key `+=`, u32 wrapping in the
+         * release wasm); to_vec_pretty.  The map's iteration order is HashMap's (random per
+         * process): this restatement defines it as first insertion (the accumulator's keys
+         * first, then the record's new keys by first occurrence), the device does the same,
+         * and parity with the reference is on the map. */
+        uint8_t **ak = NULL, **nk = NULL;
+        size_t *al = NULL, *nl = NULL, an = 0, nn = 0, ml;
+        uint32_t *av = NULL, *nv = NULL;
+        char *m = NULL;
+        if (orc_json_map_u32(s->acc, s->acc_len, &ak, &al, &av, &an, &m, &ml)) { /* unwrap_or_default */
+          free(m);
+          m = NULL;
+          an = 0;
+        }
+        /* the accumulator's duplicate keys: the last value wins, at the first position */
+        size_t w = 0;
+        for (size_t k = 0; k < an; k++) {
+          size_t j = 0;
+          while (j < w && !(al[j] == al[k] && !memcmp(ak[j], ak[k], al[k]))) j++;
+          if (j < w) {
+            av[j] = av[k];
+            free(ak[k]);
+          } else {
+            ak[w] = ak[k];
+            al[w] = al[k];
+            av[w] = av[k];
+            w++;
+          }
+        }
+        an = w;
+        int jr = orc_json_map_u32(r->val, r->val_len, &nk, &nl, &nv, &nn, &m, &ml);
+        if (jr == ORC_E_UNSUPPORTED) {
+          for (size_t k = 0; k < an; k++) free(ak[k]);
+          free(ak); free(al); free(av);
+          o->unsupported = 1;
+          return;
+        }
+        if (jr) {
+          for (size_t k = 0; k < an; k++) free(ak[k]);
+          free(ak); free(al); free(av);
+          hint = m;
+          break;
+        }
+        /* the record's map: the last value of a key, at its first occurrence */
+        for (size_t k = 0; k < nn; k++) {
+          size_t last = k;
+          int seen_before = 0;
+          for (size_t j = 0; j < nn; j++) {
+            if (nl[j] != nl[k] || memcmp(nk[j], nk[k], nl[k])) continue;
+            if (j < k) seen_before = 1;
+            last = j;
+          }
+          if (seen_before) continue;
+          const uint32_t v = nv[last];
+          size_t j = 0;
+          while (j < an && !(al[j] == nl[k] && !memcmp(ak[j], nk[k], nl[k]))) j++;
+          if (j < an) {
+            av[j] = av[j] + v; /* wrapping */
+          } else {
+            ak = (uint8_t **)realloc(ak, (an + 1) * sizeof(uint8_t *));
+            al = (size_t *)realloc(al, (an + 1) * sizeof(size_t));
+            av = (uint32_t *)realloc(av, (an + 1) * sizeof(uint32_t));
+            ak[an] = dup_bytes(nk[k], nl[k]);
+            al[an] = nl[k];
+            av[an] = v;
+            an++;
+          }
+        }
+        for (size_t k = 0; k < nn; k++) free(nk[k]);
+        free(nk); free(nl); free(nv);
+        uint8_t *pb;
+        size_t pl;
+        orc_json_pretty_map(ak, al, av, an, &pb, &pl);
+        for (size_t k = 0; k < an; k++) free(ak[k]);
+        free(ak); free(al); free(av);
+        free(s->acc);
+        s->acc = pb;
+        s->acc_len = pl;
+        outr = rec_clone(r);
+        free(outr.val);
+        outr.val = dup_bytes(s->acc, s->acc_len);
+        outr.val_len = s->acc_len;
+        emit = 1;
         break;
       }
       case M_PROJECT: {

@@ -97,6 +97,11 @@ int orc_json_array_map(const uint8_t *s, size_t n, uint8_t ***elems, size_t **le
                        size_t *msg_len);
 /* map_json_project: Map<String, Value> from_slice, to_string of the field's value.
  * 0 ok (*found; *out canonical value when found), 1 error (*msg), ORC_E_UNSUPPORTED */
+/* aggregate-json: HashMap<String, u32> of one value (entries in text order) */
+int orc_json_map_u32(const uint8_t *s, size_t n, uint8_t ***keys, size_t **klens, uint32_t **vals, size_t *count,
+                     char **msg, size_t *msg_len);
+void orc_json_pretty_map(uint8_t *const *keys, const size_t *klens, const uint32_t *vals, size_t n, uint8_t **out,
+                         size_t *out_len);
 int orc_json_project(const uint8_t *s, size_t n, const char *field, uint8_t **out, size_t *out_len, int *found,
                      char **msg, size_t *msg_len);
 int orc_json_struct(const uint8_t *s, size_t n, const char *name, const char **fields, int nfields, int *vals,

@@ -83,7 +83,7 @@ def check_batch(engine, modules, slice_bytes, max_bytes=(1 << 64) - 1, calls=1):
         assert gm.records_out() == om["records_out"]
         assert gm.fuel_used() == 0
     for i, m in enumerate(modules):
-        if m[0] in ("aggregate-sum", "aggregate"):
+        if m[0] in ("aggregate-sum", "aggregate", "aggregate-json"):
             assert g.accumulator(i) == o.accumulator(i)
     return gout
 
@@ -737,3 +737,120 @@ def test_project_c3_chain_errors_in_stream(engine):
         check_batch(engine, CHAINS[chain], sl, max_bytes=5000)
     # a stage erring on the projected (narrowed) value reports that value
     check_batch(engine, [("map_json_project", {}, None), ("filter_odd", {}, None)], sl)
+
+
+# ---------------------------------------------------------------------------
+# aggregate-json (examples/aggregate-json: HashMap<String, u32> += per key,
+# the C5 keyed aggregate): every record's output = the pretty map after it
+# (insertion order, as the oracle defines it), the stored accumulator, errors
+# ---------------------------------------------------------------------------
+def _keyed_slice(seed, nbatches=30, nkeys=40, bad=0.0, escapes=False):
+    import json
+    import random
+    rng = random.Random(seed)
+    keys = ["repo-%04d" % i for i in range(nkeys)]
+    out, base = b"", 0
+    for _ in range(nbatches):
+        b = P.Batch(base_offset=base)
+        n = rng.choice([1, 5, 17, 64, 100])
+        for _ in range(n):
+            if rng.random() < bad:
+                v = rng.choice([b'{"a": -3}', b'{"a": "x"}', b"[1,2]", b'{"a": 4294967296}', b'{"a": 1', b"7"])
+            else:
+                d = {}
+                for _ in range(rng.randint(0, 3)):
+                    d[rng.choice(keys)] = rng.randint(0, 2 ** 32 - 1) if rng.random() < 0.1 else rng.randint(0, 1000)
+                v = json.dumps(d, separators=(",", ":") if rng.random() < 0.5 else (", ", ": ")).encode()
+                if rng.random() < 0.05:
+                    v = v.replace(b"}", b', "repo-0001": 2}') if len(d) else v  # duplicate key: last wins
+            key = None if rng.random() < 0.8 else b"k"
+            b.add_record(P.Record.new_key_value(key, v))
+        out += b.encode()
+        base += n
+    return out
+
+
+AGGJ_CHAINS = {
+    "aggj": [("aggregate-json", {}, None)],
+    "aggj_acc": [("aggregate-json", {}, b'{\n  "repo-0003": 10,\n  "z\\"q": 1\n}')],
+    "aggj_bad_acc": [("aggregate-json", {}, b"not json")],
+    "filter_aggj": [("filter_init", {"key": "repo-000"}, None), ("aggregate-json", {}, None)],
+    "map_aggj": [("map", {}, None), ("aggregate-json", {}, b'{"REPO-0001": 5}')],
+}
+
+
+@pytest.mark.parametrize("chain", sorted(AGGJ_CHAINS))
+@pytest.mark.parametrize("seed,bad", [(1, 0.0), (2, 0.0), (3, 0.01)])
+def test_aggregate_json_parity(engine, chain, seed, bad):
+    check_batch(engine, AGGJ_CHAINS[chain], _keyed_slice(seed, bad=bad), calls=2)
+
+
+@pytest.mark.parametrize("max_bytes", [0, 300, 20000])
+def test_aggregate_json_max_bytes(engine, max_bytes):
+    check_batch(engine, AGGJ_CHAINS["aggj"], _keyed_slice(5, nbatches=12), max_bytes, calls=2)
+
+
+def test_aggregate_json_many_blocks(engine):
+    """~15K records: hundreds of 32-record blocks, each replayed by its own wave
+    from the per-block rows (k_aggj_bsum / k_aggj_colscan / k_aggj_text)."""
+    check_batch(engine, AGGJ_CHAINS["aggj"], _keyed_slice(11, nbatches=400, nkeys=300), calls=2)
+
+
+def test_aggregate_json_large_dictionary(engine):
+    """More than kAjLds (4096) keys: the values replay in the block rows in HBM
+    instead of LDS; the second call starts from an accumulator of >4096 keys."""
+    import json
+    out, base = b"", 0
+    for bi in range(12):
+        b = P.Batch(base_offset=base)
+        for r in range(8):
+            d = {"k%05d" % (bi * 512 + r * 64 + j): bi + r + j for j in range(64)}
+            d["k00001"] = 7  # an old key again
+            b.add_record(P.Record.new(json.dumps(d).encode()))
+        out += b.encode()
+        base += 8
+    check_batch(engine, AGGJ_CHAINS["aggj"], out, calls=2)
+
+
+def test_keyed_state_merge_one_gpu(engine):
+    """C5 keyed at one rank: every partition's state as (FNV-1a 64, u32) pairs
+    written into HBM (fsg_chain_keyed_state), merged per key on the GPU
+    (partitions.merge_keyed_torch) == the oracle's accumulators summed per key."""
+    import json
+    import torch
+    from fluvio_amd import partitions as PT
+    nparts, cap = 8, 128
+    slices = synth.make_keyed_slices(nparts, 4000, 256)
+    fp = torch.zeros(nparts * cap, dtype=torch.int64, device="cuda:0")
+    val = torch.zeros(nparts * cap, dtype=torch.int32, device="cuda:0")
+    expect, counts = {}, []
+    for p in range(nparts):
+        g = gpu_chain(engine, AGGJ_CHAINS["aggj"])
+        o = orc_chain(AGGJ_CHAINS["aggj"])
+        for _ in range(2):
+            g.process_batch(slices[p])
+            o.process_batch(slices[p])
+        assert g.accumulator(0) == o.accumulator(0)
+        counts.append(g.keyed_state(0, fp.data_ptr() + p * cap * 8, val.data_ptr() + p * cap * 4, cap))
+        for k, v in json.loads(o.accumulator(0)).items():
+            f = PT.fnv1a64(k.encode())
+            assert f not in expect  # SipHash routing: a key lives in one partition
+            expect[f] = v
+        assert counts[-1] == len(json.loads(o.accumulator(0)))
+    sel = torch.cat([torch.arange(p * cap, p * cap + counts[p], device="cuda:0") for p in range(nparts)])
+    keys, sums = PT.merge_keyed_torch(fp[sel], val[sel].to(torch.int64) & 0xFFFFFFFF)
+    got = {k & 0xFFFFFFFFFFFFFFFF: v for k, v in zip(keys.tolist(), sums.tolist())}
+    assert got == expect
+
+
+def test_aggregate_json_process_kat(engine):
+    """One `process` call (engine.rs:135): the per-record pretty maps and the
+    stored accumulator, as the oracle has them."""
+    g = gpu_chain(engine, AGGJ_CHAINS["aggj"])
+    o = orc_chain(AGGJ_CHAINS["aggj"])
+    vals = [b'{"a":1}', b'{"b":2,"a":3}', b'{}', b'{"c": 1, "c": 7}']
+    out = g.process(SmartModuleInput.try_from_records([P.Record.new(v) for v in vals]))
+    ref = o.process(P.encode_records([P.Record.new(v) for v in vals]))
+    assert [r.value for r in out.successes] == [r.value for r in P.decode_records(ref["bytes"])]
+    assert out.successes[-1].value == b'{\n  "a": 4,\n  "b": 2,\n  "c": 7\n}'
+    assert g.accumulator(0) == o.accumulator(0)

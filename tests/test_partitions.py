@@ -110,3 +110,69 @@ def test_two_rank_state_merge(tmp_path):
     # each partition's state is the running i32 sum of its own records only
     for p in range(N_PART):
         assert expect[p] == PT.wrap_i32(sum(int(v) for _, v in routed[p]))
+
+
+# ---------------------------------------------------------------------------
+# C5 keyed (aggregate-json): per-key u32 sums, keys routed by SipHash so a key
+# lives in one partition; the topic-wide table = all ranks' (fingerprint, value)
+# pairs gathered and summed per key (partitions.merge_keyed_torch)
+# ---------------------------------------------------------------------------
+K_PART, K_REC, K_KEYS = 8, 1500, 64
+
+
+def keyed_pairs(owned):
+    """Per owned partition: the oracle's aggregate-json accumulator (the
+    pretty map after the partition's last record) as (FNV-1a 64, u32) pairs."""
+    import json
+    from fluvio_amd import synth
+    from oracle.oracle import OracleChain
+    slices = synth.make_keyed_slices(K_PART, K_REC, K_KEYS, owned=list(owned))
+    fps, vals = [], []
+    for p in owned:
+        ch = OracleChain([("aggregate-json", {}, None)])
+        r = ch.process_batch(slices[p])
+        assert r["status"] == 0 and r["error"] is None
+        for k, v in json.loads(ch.accumulator(0)).items():
+            fps.append(PT.fnv1a64(k.encode()))
+            vals.append(v)
+    return fps, vals
+
+
+def keyed_expect():
+    """Per-key totals straight from the generated records (all partitions)."""
+    import json
+    from fluvio_amd import synth
+    tot = {}
+    for p, sl in synth.make_keyed_slices(K_PART, K_REC, K_KEYS).items():
+        for b in P.decode_batches(sl):
+            for rec in b.memory_records():
+                for k, v in json.loads(rec.value).items():
+                    assert PT.partition_siphash(k.encode(), K_PART) == p  # routed by key
+                    tot[PT.fnv1a64(k.encode())] = (tot.get(PT.fnv1a64(k.encode()), 0) + v) & 0xFFFFFFFF
+    return tot
+
+
+def _keyed_rank_main(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    fps, vals = keyed_pairs(PT.owned_partitions(K_PART, world, rank))
+    fp = torch.tensor([f - (1 << 64) if f >= 1 << 63 else f for f in fps], dtype=torch.int64)
+    keys, sums = PT.merge_keyed_torch(fp, torch.tensor(vals, dtype=torch.int64), dist=dist)
+    with open(os.path.join(outdir, f"keyed{rank}.txt"), "w") as f:
+        f.write(" ".join(f"{k & 0xFFFFFFFFFFFFFFFF}:{v}" for k, v in zip(keys.tolist(), sums.tolist())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_two_rank_keyed_merge(tmp_path):
+    import torch.multiprocessing as mp
+    world = 2
+    mp.spawn(_keyed_rank_main, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    expect = keyed_expect()
+    assert len(expect) > K_PART
+    for r in range(world):
+        got = dict(tuple(map(int, x.split(":"))) for x in open(tmp_path / f"keyed{r}.txt").read().split())
+        assert got == expect
