@@ -229,6 +229,9 @@ struct EvalArgs {
   Mins* mins;
   uint32_t* list;      // deferred batches: list[0] = count, list[1..] = indices (k_eval_lean -> k_eval)
   ElemRec* elem;       // array_map element descriptors (nullptr without an array_map stage)
+  uint64_t nrec;       // records of the slice (rbase's total)
+  uint16_t* rstart;    // k_chase: record n of batch b starts at window offset rstart[rbase[b] + n] ...
+  uint16_t* rend;      // ... and the last one ends at rend[b] (0xFFFF: no lean framing, exact path)
 };
 
 struct SizeArgs {

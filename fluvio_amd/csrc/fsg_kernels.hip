@@ -1311,11 +1311,9 @@ struct LeanStage {
 };
 struct __attribute__((aligned(16))) LeanLds {
   uint8_t win[kLeanWin + 48];  // + look-ahead of the last scan chunk
-  uint32_t r_start[kLeanMaxR + 1];
   uint32_t r_vs[kLeanMaxR];
   uint32_t r_ve[kLeanMaxR];
   uint32_t match[2];
-  uint32_t chase_bad;
   uint32_t nst;
   uint32_t red[4];                  // workgroup OR (two alternating pairs)
   uint32_t out_upper;
@@ -1825,6 +1823,57 @@ __device__ __forceinline__ void lean_issue(const EvalArgs& a, const LeanWin& w, 
                                        (__attribute__((address_space(3))) void*)(dst + k * 1024), 16, 0, 0);
 }
 
+// k_chase — record framing of the lean path, one thread per batch: the chain
+// of record length varints (Record::decode's first field, data.rs:534-562)
+// walked with dependent global loads; thousands of batches in flight hide the
+// latency, and k_eval_lean gets every record's start with its window instead
+// of a serial walk through LDS.  Conservative: anything unusual (more than
+// kLeanMaxR records, a length varint over 4 bytes, a record past the window)
+// leaves rend[b] = 0xFFFF and the batch takes the exact path.
+__device__ __forceinline__ uint32_t ld_u32_at(const uint8_t* p) {  // 4 bytes at any address
+  const uint64_t a = (uint64_t)p;
+  const uint32_t* w = (const uint32_t*)(a & ~3ull);
+  return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3u));
+}
+__global__ __launch_bounds__(256) void k_chase(EvalArgs a) {
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= a.nbatches) return;
+  const uint64_t pos = a.bpos[b];
+  const uint64_t nxt = b + 1 < a.nbatches ? a.bpos[b + 1] : a.slice_len;
+  const uint64_t rb = a.rbase[b], rn = (b + 1 < a.nbatches ? a.rbase[b + 1] : a.nrec) - rb;
+  const uint64_t al = pos & ~15ull;
+  uint64_t wl = nxt > al ? nxt - al : 0;
+  if (wl > (uint64_t)kLeanWin) wl = kLeanWin;
+  const uint64_t wlen = (wl + 15) & ~15ull;
+  const uint8_t* base = a.slice + al;
+  const uint32_t batch_len = __builtin_bswap32(ld_u32_at(a.slice + pos + 8));
+  const uint64_t sec0 = pos + 57, sec_end = pos + 12 + (uint64_t)batch_len;
+  const uint64_t sec_len = sec_end - sec0;
+  const int32_t count = sec_len >= 4 ? (int32_t)__builtin_bswap32(ld_u32_at(a.slice + sec0)) : -1;
+  uint32_t end = 0xFFFFu;
+  if (sec_len >= 4 && sec_end - al <= wlen && count >= 0 && count <= kLeanMaxR && (uint64_t)count == rn) {
+    const uint32_t have = (uint32_t)(sec_end - al);
+    uint32_t q = (uint32_t)(sec0 + 4 - al);
+    int n = 0;
+    for (; n < count; n++) {
+      const uint32_t x = ld_u32_at(base + q);
+      const uint32_t term = ~x & 0x80808080u;
+      if (!term) break;
+      const uint32_t nb = (((uint32_t)__builtin_ctz(term)) >> 3) + 1;
+      if (q + nb > have) break;
+      const uint32_t y = nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u));
+      const uint32_t v = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
+      if (v & 1u) break;  // negative length (zigzag)
+      const uint32_t len = v >> 1;
+      if (have - (q + nb) < len) break;
+      a.rstart[rb + n] = (uint16_t)q;
+      q += nb + len;
+    }
+    if (n == count) end = q;
+  }
+  a.rend[b] = (uint16_t)end;
+}
+
 // four waves per SIMD (eight workgroups per CU, as many as the LDS holds)
 template <bool kJson>
 __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJson ? 1 : 4))) void k_eval_lean(EvalArgs a) {
@@ -1928,6 +1977,9 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
     const uint64_t rb = a.rbase[b];
     const uint32_t bn = b + G;
     lean_issue(a, W, L.win);
+    // the record starts (k_chase) ride along with the window
+    const uint32_t rs = l < 64 ? a.rstart[rb + l] : 0u;
+    const uint32_t re = a.rend[b];
     __builtin_amdgcn_s_waitcnt(0);  // this wave's pieces have landed
     lean_sync();                    // ... and the other wave's
     // batch header (file format, batch.rs:163-180), read before the gaps are cleared
@@ -1941,50 +1993,18 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
     const uint32_t sec_len = (uint32_t)(sec_end - sec0);
     const int32_t count = sec_len >= 4 ? (int32_t)rd_be(L.win + (sec0 - al), 4) : -1;
     bool defer = sec_len < 4 || sec_end - al > (uint64_t)wlen || count < 0 || count > kLeanMaxR;
-    // 2. framing: wave 0 chases the lengths with wave-uniform (scalar) values,
-    //    one LDS round trip per record when the length varint has <= 4 bytes;
-    //    lane n keeps the start of record n.  Lane r then parses record r.
-    const uint32_t have = (uint32_t)(sec_end - al);
-    if (!defer && l < 64) {
-      uint32_t q = (uint32_t)(sec0 + 4 - al);
-      uint32_t my = 0;
-      int n = 0;
-      for (; n < count; n++) {
-        const uint32_t q0 = q;
-        const uint32_t x = __builtin_amdgcn_readfirstlane(lds_u32_at(L.win, q));
-        const uint32_t term = ~x & 0x80808080u;
-        int64_t len;
-        if (term) {
-          const uint32_t nb = (((uint32_t)__builtin_ctz(term)) >> 3) + 1;
-          if (q + nb > have) break;
-          const uint32_t y = nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u));
-          const uint32_t v = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
-          len = (v & 1u) ? -(int64_t)(v >> 1) - 1 : (int64_t)(v >> 1);  // zigzag
-          q += nb;
-        } else if (wvarint((const uint8_t*)L.win, q, have, &len)) {
-          break;
-        }
-        if (len < 0 || (int64_t)(have - q) < len) break;
-        if ((int)l == n) my = q0;
-        q += (uint32_t)len;
-      }
-      if ((int)l < n) L.r_start[l] = my;
-      if (l == 0) {
-        L.r_start[n] = q;
-        L.chase_bad = n < count ? 1u : 0u;
-      }
-    }
-    lean_sync();
-    // a failed chase leaves the lengths unverified: the exact walk decides
-    if (!defer) defer = __builtin_amdgcn_readfirstlane(L.chase_bad) != 0u;
+    // 2. framing: the record starts k_chase found (rs, loaded with the window);
+    //    lane r parses record r.  No lean framing (rend 0xFFFF): exact path.
+    if (!defer) defer = re == 0xFFFFu;
     const int nr = defer ? 0 : count;
     bool g = true;
     int64_t ts = 0, od = 0, hdr = 0;
     uint32_t vs = 0, vl = 0, kpos = 0, klen = 0;
     uint8_t attr = 0, tag = 0;
+    const uint32_t rs_next = __shfl_down(rs, 1, 64);
     if ((int)l < nr) {
-      uint32_t q = L.r_start[l];
-      const uint32_t lim = L.r_start[l + 1];
+      uint32_t q = rs;
+      const uint32_t lim = (int)l + 1 == nr ? re : rs_next;
       int64_t len, kl, vlen;
       g = !wvarint((const uint8_t*)L.win, q, lim, &len);
       if (g && q < lim) attr = L.win[q++]; else g = false;
@@ -2113,7 +2133,7 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
     p_kept = !defer && l < 64 && ((alive >> (l & 63)) & 1ull);
     if (p_kept) {
       p_idx = rb + __popcll(alive & ((1ull << l) - 1ull));
-      p_d.src = al + L.r_start[l];
+      p_d.src = al + rs;
       p_d.vpos = al + vs;
       p_d.kpos = tag ? al + kpos : 0;
       p_d.od = od;
@@ -3659,6 +3679,7 @@ void launch_eval(const EvalArgs& a, uint32_t ops, bool lean, hipStream_t s) {
     // persistent: as many workgroups as fit on the device at once
     const bool json = (ops & (opbit(OP_FILTER_JSON) | opbit(OP_PROJECT))) != 0;
     const uint32_t g = std::min<uint32_t>(a.nbatches, lean_grid(json));
+    hipLaunchKernelGGL(k_chase, dim3((a.nbatches + 255) / 256), dim3(256), 0, s, a);
     if (json)
       hipLaunchKernelGGL(k_eval_lean<true>, dim3(g), dim3(kLeanThreads), 0, s, a);
     else

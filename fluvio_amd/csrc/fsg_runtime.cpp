@@ -407,6 +407,7 @@ struct fsg_chain {
   DevBuf aj_kptr, aj_klen, aj_tptr, aj_tlen, aj_kup, aj_vinit, aj_arena, aj_out, aj_accoff, aj_acclen;  // aggregate-json
   DevBuf aj_bcnt, aj_brec, aj_rdesc, aj_rne, aj_rent, aj_rnew, aj_rnewb, aj_rlen, aj_roff, aj_ekid, aj_eval;
   DevBuf aj_sref, aj_sid, aj_state, aj_state2, aj_tsum;
+  DevBuf rstart, rend;  // k_chase (lean path record starts)
   Plan hplan{};
   hipEvent_t ev[6] = {};
   fsg_timings last{};
@@ -1041,6 +1042,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   ea.mins = c->mins.as<Mins>();
   ea.list = c->defer.as<uint32_t>();
   ea.elem = (has_array || has_aggj) ? c->elem.as<ElemRec>() : nullptr;
+  ea.nrec = s->nrec;
   uint32_t ops = 0;
   bool lean_stages = true;  // every stage has a lean form
   bool projected = false;  // a projection seen: only uppercase maps may follow on the lean path
@@ -1062,7 +1064,13 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   const bool lean = (ops & ~((1u << OP_CONTAINS) | (1u << OP_MAP_UPPER) | (1u << OP_REGEX) |
                              (1u << OP_FILTER_JSON) | (1u << OP_PROJECT))) == 0 &&
                     !has_agg && lean_stages;
-  if (lean) HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
+  if (lean) {
+    HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
+    HIPCHK(c->rstart.ensure(((size_t)s->nrec + 64) * sizeof(uint16_t)));  // + a wave of over-read
+    HIPCHK(c->rend.ensure(((size_t)nb + 1) * sizeof(uint16_t)));
+    ea.rstart = c->rstart.as<uint16_t>();
+    ea.rend = c->rend.as<uint16_t>();
+  }
   launch_eval(ea, ops, lean, st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[1], st));
