@@ -1347,11 +1347,15 @@ __device__ __forceinline__ bool lean_or(uint32_t* red, uint32_t& par, bool p) {
 // the token DFA (fsg_json_dfa.h)
 constexpr int kJsonChunks = (kLeanWin + 48) / 16 + 2;
 constexpr int kJsonEnt = 2048;  // token entries per batch (more: exact kernel)
+constexpr int kJsonSeg = kJsonChunks;  // object members per batch (LeanLdsJ::jn; more: exact kernel)
 __device__ constexpr JsonDfaTables g_json_tables{};
 struct __attribute__((aligned(16))) LeanLdsJ : LeanLds {
   uint32_t jm[kJsonChunks];      // pass 1: quote16 | special16 << 16; pass 2: in-string16 | hot16 << 16
-  uint16_t jn[kJsonChunks];      // non-space16
-  uint32_t ent[kJsonEnt];        // pos | byte << 16 | token class << 24
+  uint16_t jn[kJsonChunks];      // non-space16; then the object members: first token | record start << 15
+  uint32_t ent[kJsonEnt];        // pos | in-string bit << 15 | byte << 16 | token class << 24
+  uint32_t racc[kLeanMaxR];      // per record: level fields | message fields << 8 | bad << 16
+  uint32_t rlvl[kLeanMaxR];      // per record: bit (LogLevel index) of its level value
+  uint32_t nseg;
   uint32_t wsum[4];              // cross-wave scan carries
   uint8_t dfa[kJsonStates * kJsonCls2];
   uint8_t bcls[256];
@@ -1399,7 +1403,7 @@ __device__ __forceinline__ void lean_push(const LeanLds& L, int nr, uint32_t p, 
   nh++;
 }
 // One contains stage over the value bytes [lo, hi) of a window whose non-value
-// bytes in [lo & ~15, hi + 16) are zero.  Returns the OR of the scanned words
+// bytes in [lo & ~15, hi + 16) are blanks (clear_gaps).  Returns the OR of the scanned words
 // (bit 7 of a byte set <=> some value byte >= 0x80, i.e. a non-ASCII value).
 //   kMode 0 (m >= 7): every occurrence covers an aligned word, so each aligned
 //           word is compared with the needle's 4-grams at offsets 0..3 (one
@@ -1645,62 +1649,140 @@ __device__ bool lean_json_stage(LeanLdsJ& L, int nr, uint32_t& orpar, bool proj,
   uint32_t ntok;
   uint32_t e = wg_excl_sum(cnt, L.wsum, &ntok);
   if (ntok > (uint32_t)kJsonEnt) return true;  // uniform: every thread saw the same total
+  // positions in order (ALU only: the token count per thread is uneven, the
+  // records' heads are dense), then classes strided over the tokens
   for (uint32_t k = k0; k < k1; k++) {
     const uint32_t instr = L.jm[k] & 0xFFFFu;
     uint32_t hot = L.jm[k] >> 16;
     while (hot) {
       const uint32_t j = (uint32_t)__builtin_ctz(hot);
       hot &= hot - 1;
-      const uint32_t pos = c0 + 16 * k + j;
-      const uint32_t b = L.win[pos];
-      uint32_t cls = L.bcls[b];
-      if (b == '"') cls = ((instr >> j) & 1u) ? (uint32_t)JC_Q_CLOSE : (uint32_t)JC_Q_OTHER;
-      L.ent[e++] = pos | (b << 16) | (cls << 24);
+      L.ent[e++] = (c0 + 16 * k + j) | (((instr >> j) & 1u) << 15);
     }
   }
+  if (l == 0) L.nseg = 0;
   lean_sync();
-  // string classes of the opening quotes (the next token closes the string)
-  for (uint32_t t = l; t + 1 < ntok; t += kLeanThreads) {
+  // classes; an opening quote takes the class of its string (the next token
+  // closes it).  Bits 0..15 never change here, so a neighbour's position and
+  // in-string bit can be read while it is being rewritten.
+  for (uint32_t t = l; t < ntok; t += kLeanThreads) {
     const uint32_t en = L.ent[t];
-    if ((en >> 24) != JC_Q_OTHER) continue;
-    const uint32_t nx = L.ent[t + 1];
-    if ((nx >> 24) != JC_Q_CLOSE) continue;
-    const uint32_t a = (en & 0xFFFFu) + 1, n = (nx & 0xFFFFu) - a;
-    uint32_t cls;
-    if (proj) {  // the projected field's name (L.needle) or another string
-      bool eq = n == fl;
-      for (uint32_t k = 0; eq && k < fl; k += 4) {
-        const uint32_t mk = fl - k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (fl - k))) - 1u);
-        eq = ((lds_u32_at(L.win, a + k) ^ lds_u32_at(L.needle, k)) & mk) == 0u;
+    const uint32_t pos = en & 0x7FFFu;
+    const uint32_t b = L.win[pos];
+    uint32_t cls = L.bcls[b];
+    if (b == '"') {
+      cls = (en & 0x8000u) ? (uint32_t)JC_Q_CLOSE : (uint32_t)JC_Q_OTHER;
+      if (cls == JC_Q_OTHER && t + 1 < ntok) {
+        const uint32_t nx = L.ent[t + 1];
+        const uint32_t np = nx & 0x7FFFu;
+        if ((nx & 0x8000u) && L.win[np] == '"') {
+          const uint32_t a = pos + 1, n = np - a;
+          if (proj) {  // the projected field's name (L.needle) or another string
+            bool eq = n == fl;
+            for (uint32_t k = 0; eq && k < fl; k += 4) {
+              const uint32_t mk = fl - k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (fl - k))) - 1u);
+              eq = ((lds_u32_at(L.win, a + k) ^ lds_u32_at(L.needle, k)) & mk) == 0u;
+            }
+            cls = eq ? (uint32_t)JC_Q_FIELD : (uint32_t)JC_Q_OTHER;
+          } else {
+            cls = json_str_class(L, a, n);
+          }
+        }
       }
-      cls = eq ? (uint32_t)JC_Q_FIELD : (uint32_t)JC_Q_OTHER;
-    } else {
-      cls = json_str_class(L, a, n);
     }
-    L.ent[t] = (en & 0x00FFFFFFu) | (cls << 24);
+    L.ent[t] = (en & 0xFFFFu) | (b << 16) | (cls << 24);
+    // members: the token after a comma starts one (of the comma's record)
+    if (!proj && cls == JC_COMMA) {
+      const uint32_t k = atomicAdd(&L.nseg, 1u);
+      if (k < (uint32_t)kJsonSeg) L.jn[k] = (uint16_t)(t + 1);
+    }
   }
   lean_sync();
-  // 3. one thread per record, records spread over both waves
+  // 3a. per record: balanced quotes at its ends, its first token (binary
+  //     search on positions) = the start of its first member
   const uint32_t r = 2 * (l & 63u) + (l >> 6);
+  auto instr_at = [&](uint32_t p) {
+    const uint32_t k = (p - c0) >> 4, j = (p - c0) & 15u;
+    if (k >= nch) return 0u;
+    return (L.jm[k] >> j) & 1u;
+  };
+  uint32_t t_first = 0;
   bool bad = false;
   if ((int)r < nr) {
     const uint32_t vs = L.r_vs[r], ve = L.r_ve[r];
-    // the record must start and end outside strings (balanced quotes before it)
-    auto instr_at = [&](uint32_t p) {
-      const uint32_t k = (p - c0) >> 4, j = (p - c0) & 15u;
-      if (k >= nch) return 0u;
-      return (L.jm[k] >> j) & 1u;
-    };
     if (instr_at(vs) || instr_at(ve)) bad = true;
-    // the record's tokens [t0, t1): binary search on positions
     uint32_t lo = 0, hi = ntok;
     while (lo < hi) {
       const uint32_t m = (lo + hi) >> 1;
-      if ((L.ent[m] & 0xFFFFu) < vs) lo = m + 1; else hi = m;
+      if ((L.ent[m] & 0x7FFFu) < vs) lo = m + 1; else hi = m;
     }
-    uint32_t t = lo;
-    uint32_t st = JS_OBJ, prev = 0xFFFFu, flags = 0;
-    int lvl = -1;
+    t_first = lo;
+    if (!proj) {
+      // no token inside the value: not an object (and no member may claim it)
+      if (lo >= ntok || (L.ent[lo] & 0x7FFFu) >= ve) bad = true;
+      L.racc[r] = bad ? 1u << 16 : 0u;
+      L.rlvl[r] = 0;
+      if (!bad) {
+        const uint32_t k = atomicAdd(&L.nseg, 1u);
+        if (k < (uint32_t)kJsonSeg) L.jn[k] = (uint16_t)(lo | 0x8000u);
+      }
+    }
+  }
+  if (!proj) {
+    lean_sync();
+    const uint32_t nseg = L.nseg;
+    if (nseg > (uint32_t)kJsonSeg) return lean_or(L.red, orpar, true);  // uniform
+    // 3b. the token DFA, one thread per object member: a member after a comma
+    //     starts in JS_KEY (the only state a comma leads to) and ends with the
+    //     next comma, which must lead to JS_KEY again, or at the record's end,
+    //     which must be JS_END.  Per record: each field exactly once, the
+    //     level value's variant.
+    for (uint32_t k = l; k < nseg; k += kLeanThreads) {
+      const uint32_t sg = L.jn[k];
+      const bool first = (sg & 0x8000u) != 0u;
+      uint32_t t = sg & 0x7FFFu;
+      // the member's record: that of its first token (a record start) or of the comma before it
+      const uint32_t anchor = L.ent[first ? t : t - 1] & 0x7FFFu;
+      const uint32_t rr = (uint32_t)lean_rec_of(L, nr, anchor);
+      const uint32_t ve = L.r_ve[rr];
+      uint32_t st = first ? (uint32_t)JS_OBJ : (uint32_t)JS_KEY;
+      uint32_t prev = first ? 0xFFFFu : anchor;
+      uint32_t nlv = 0, nmsg = 0, lv = 0;
+      bool ended = false;
+      for (; t < ntok; t++) {
+        const uint32_t en = L.ent[t];
+        const uint32_t pos = en & 0x7FFFu;
+        if (pos >= ve) break;
+        const uint32_t cls = en >> 24;
+        const uint32_t adj = pos == prev + 1 ? 1u : 0u;
+        if (st >= JS_INV_D && st <= JS_INV_E) lv = 1u << (st - JS_INV_D);
+        st = L.dfa[st * kJsonCls2 + cls * 2 + adj];
+        nlv += st == JS_INKEY_LV ? 1u : 0u;
+        nmsg += st == JS_INKEY_MSG ? 1u : 0u;
+        prev = pos;
+        if (cls == JC_COMMA || st == JS_FAIL) {
+          ended = true;
+          break;
+        }
+      }
+      const bool ok = ended ? st == JS_KEY : st == JS_END;
+      atomicAdd(&L.racc[rr], nlv | (nmsg << 8) | (ok ? 0u : 1u << 16));
+      if (lv) atomicOr(&L.rlvl[rr], lv);
+    }
+    lean_sync();
+    if ((int)r < nr) {
+      const uint32_t ac = L.racc[r];
+      // exactly one level and one message field (a duplicate is a serde error)
+      bad = (ac >> 16) != 0u || (ac & 0xFFu) != 1u || ((ac >> 8) & 0xFFu) != 1u;
+      if (!bad && (L.rlvl[r] & ~1u)) atomicOr(&L.match[r >> 5], 1u << (r & 31));
+    }
+    return lean_or(L.red, orpar, bad);
+  }
+  // 3c. projection: one thread per record runs the DFA over its tokens
+  if ((int)r < nr) {
+    const uint32_t ve = L.r_ve[r];
+    uint32_t t = t_first;
+    uint32_t st = JS_OBJ, prev = 0xFFFFu;
     // projection (map_json_project, Map<String, Value>, last member wins): the
     // value span of the last member whose key is the field; numbers whose
     // serde_json text differs from the source (fractions, exponents, -0, more
@@ -1709,77 +1791,67 @@ __device__ bool lean_json_stage(LeanLdsJ& L, int nr, uint32_t& orpar, bool proj,
     uint32_t vstart = 0, ntv = 0, fs = 0, fe = 0;
     for (; !bad && t < ntok; t++) {
       const uint32_t en = L.ent[t];
-      const uint32_t pos = en & 0xFFFFu;
+      const uint32_t pos = en & 0x7FFFu;
       if (pos >= ve) break;
       uint32_t cls = en >> 24;
       const uint32_t adj = pos == prev + 1 ? 1u : 0u;
       const uint32_t st0 = st;
-      if (proj) {
-        const bool q = cls == JC_Q_FIELD;
-        if (q) cls = JC_Q_OTHER;  // every string takes the "other" paths of the table
-        else if (cls >= JC_Q_LEVEL && cls <= JC_Q_ERROR) cls = JC_Q_OTHER;
-        st = L.dfa[st * kJsonCls2 + cls * 2 + adj];
-        if (st == JS_INKEY_OTHER) khit = q;
-        if (st0 == JS_VAL_OTHER) {
-          inval = true;
-          vstart = pos;
-          ntv = 0;
-          vneg = cls == JC_MINUS;
-        }
-        if (inval) {
-          if (st == JS_KEY || st == JS_END) {  // ',' / '}' after the value
-            inval = false;
-            if (st0 == JS_N_ZERO && vneg && ntv == 2) bad = true;  // -0
-            if (khit) {
-              found = true;
-              fs = vstart;
-              fe = prev + 1;
-            }
-          } else {
-            ntv++;
-            if (st == JS_N_DOT || st == JS_N_E || ntv > 18) bad = true;
+      const bool q = cls == JC_Q_FIELD;
+      if (q) cls = JC_Q_OTHER;  // every string takes the "other" paths of the table
+      else if (cls >= JC_Q_LEVEL && cls <= JC_Q_ERROR) cls = JC_Q_OTHER;
+      st = L.dfa[st * kJsonCls2 + cls * 2 + adj];
+      if (st == JS_INKEY_OTHER) khit = q;
+      if (st0 == JS_VAL_OTHER) {
+        inval = true;
+        vstart = pos;
+        ntv = 0;
+        vneg = cls == JC_MINUS;
+      }
+      if (inval) {
+        if (st == JS_KEY || st == JS_END) {  // ',' / '}' after the value
+          inval = false;
+          if (st0 == JS_N_ZERO && vneg && ntv == 2) bad = true;  // -0
+          if (khit) {
+            found = true;
+            fs = vstart;
+            fe = prev + 1;
           }
+        } else {
+          ntv++;
+          if (st == JS_N_DOT || st == JS_N_E || ntv > 18) bad = true;
         }
-      } else {
-        if (st >= JS_INV_D && st <= JS_INV_E) lvl = (int)(st - JS_INV_D);
-        st = L.dfa[st * kJsonCls2 + cls * 2 + adj];
-        // each field at most once (serde derive: duplicate field is an error)
-        const uint32_t fb = st == JS_INKEY_LV ? 1u : st == JS_INKEY_MSG ? 2u : 0u;
-        if (flags & fb) st = JS_FAIL;
-        flags |= fb;
       }
       prev = pos;
     }
-    if (st != JS_END || (!proj && flags != 3u)) bad = true;
-    if (proj) {
-      if (!bad && found) {
-        atomicOr(&L.match[r >> 5], 1u << (r & 31));
-        L.r_vs[r] = fs;  // the value narrows to the field's text
-        L.r_ve[r] = fe;
-      }
-    } else if (!bad && lvl > 0) {
+    if (st != JS_END) bad = true;
+    if (!bad && found) {
       atomicOr(&L.match[r >> 5], 1u << (r & 31));
+      L.r_vs[r] = fs;  // the value narrows to the field's text
+      L.r_ve[r] = fe;
     }
   }
   return lean_or(L.red, orpar, bad);
 }
 
-// zero every byte between values (record headers, keys, lengths) and build the
-// 64-byte block -> record table; thread l < nr owns record l (value [vs, vs+vl))
+// blank every byte between values (record headers, keys, lengths) with
+// spaces and build the 64-byte block -> record table; thread l < nr owns
+// record l (value [vs, vs+vl)).  A space has no high bit (the scans' OR stays
+// an ASCII test), is no JSON token (the token list holds value bytes only) and
+// a needle hit that reaches into a gap fails its record range check.
 __device__ __forceinline__ void clear_gaps(LeanLds& L, int nr, uint32_t vs, uint32_t vl) {
   const uint32_t l = threadIdx.x;
   const uint32_t lo = L.r_vs[0], hi = L.r_ve[nr - 1];
-  // [s, e) <- 0: whole aligned dwords inside the range, bytes at its edges (a
+  // [s, e) <- ' ': whole aligned dwords inside the range, bytes at its edges (a
   // dword at an edge may hold another record's value bytes)
   auto zero = [&](uint32_t s, uint32_t e) {
     const uint32_t s4 = (s + 3) & ~3u, e4 = e & ~3u;
     if (s4 >= e4) {
-      for (uint32_t p = s; p < e; p++) L.win[p] = 0;
+      for (uint32_t p = s; p < e; p++) L.win[p] = 0x20;
       return;
     }
-    for (uint32_t p = s; p < s4; p++) L.win[p] = 0;
-    for (uint32_t p = s4; p < e4; p += 4) *(uint32_t*)(L.win + p) = 0u;
-    for (uint32_t p = e4; p < e; p++) L.win[p] = 0;
+    for (uint32_t p = s; p < s4; p++) L.win[p] = 0x20;
+    for (uint32_t p = s4; p < e4; p += 4) *(uint32_t*)(L.win + p) = 0x20202020u;
+    for (uint32_t p = e4; p < e; p++) L.win[p] = 0x20;
   };
   if ((int)l < nr) zero(vs + vl, (int)l + 1 < nr ? L.r_vs[l + 1] : ((vs + vl + 15) & ~15u) + 16);
   if (l == 0) zero(lo & ~15u, lo);
@@ -1835,43 +1907,75 @@ __device__ __forceinline__ uint32_t ld_u32_at(const uint8_t* p) {  // 4 bytes at
   const uint32_t* w = (const uint32_t*)(a & ~3ull);
   return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3u));
 }
-__global__ __launch_bounds__(256) void k_chase(EvalArgs a) {
-  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-  if (b >= a.nbatches) return;
-  const uint64_t pos = a.bpos[b];
-  const uint64_t nxt = b + 1 < a.nbatches ? a.bpos[b + 1] : a.slice_len;
-  const uint64_t rb = a.rbase[b], rn = (b + 1 < a.nbatches ? a.rbase[b + 1] : a.nrec) - rb;
-  const uint64_t al = pos & ~15ull;
-  uint64_t wl = nxt > al ? nxt - al : 0;
-  if (wl > (uint64_t)kLeanWin) wl = kLeanWin;
-  const uint64_t wlen = (wl + 15) & ~15ull;
-  const uint8_t* base = a.slice + al;
-  const uint32_t batch_len = __builtin_bswap32(ld_u32_at(a.slice + pos + 8));
-  const uint64_t sec0 = pos + 57, sec_end = pos + 12 + (uint64_t)batch_len;
-  const uint64_t sec_len = sec_end - sec0;
-  const int32_t count = sec_len >= 4 ? (int32_t)__builtin_bswap32(ld_u32_at(a.slice + sec0)) : -1;
-  uint32_t end = 0xFFFFu;
-  if (sec_len >= 4 && sec_end - al <= wlen && count >= 0 && count <= kLeanMaxR && (uint64_t)count == rn) {
-    const uint32_t have = (uint32_t)(sec_end - al);
-    uint32_t q = (uint32_t)(sec0 + 4 - al);
-    int n = 0;
-    for (; n < count; n++) {
-      const uint32_t x = ld_u32_at(base + q);
-      const uint32_t term = ~x & 0x80808080u;
-      if (!term) break;
-      const uint32_t nb = (((uint32_t)__builtin_ctz(term)) >> 3) + 1;
-      if (q + nb > have) break;
-      const uint32_t y = nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u));
-      const uint32_t v = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
-      if (v & 1u) break;  // negative length (zigzag)
-      const uint32_t len = v >> 1;
-      if (have - (q + nb) < len) break;
-      a.rstart[rb + n] = (uint16_t)q;
-      q += nb + len;
+// The starts are staged in LDS and written back as one contiguous span per
+// workgroup (batches b0 .. b0 + 255 own consecutive record slots), so the
+// stores are coalesced instead of one partial line per record.
+constexpr int kChaseT = 256;
+__global__ __launch_bounds__(kChaseT) void k_chase(EvalArgs a) {
+  __shared__ uint16_t st[kChaseT * kLeanMaxR];
+  const uint32_t t = threadIdx.x;
+  const uint32_t b0 = blockIdx.x * kChaseT;
+  const uint32_t b = b0 + t;
+  const uint32_t bl = b0 + kChaseT < a.nbatches ? b0 + kChaseT : a.nbatches;  // first batch past the block
+  const uint64_t R0 = a.rbase[b0];
+  const uint64_t R1 = bl < a.nbatches ? a.rbase[bl] : a.nrec;
+  const bool stage = R1 - R0 <= (uint64_t)(kChaseT * kLeanMaxR);
+  if (b < a.nbatches) {
+    const uint64_t pos = a.bpos[b];
+    const uint64_t nxt = b + 1 < a.nbatches ? a.bpos[b + 1] : a.slice_len;
+    const uint64_t rb = a.rbase[b], rn = (b + 1 < a.nbatches ? a.rbase[b + 1] : a.nrec) - rb;
+    const uint64_t al = pos & ~15ull;
+    uint64_t wl = nxt > al ? nxt - al : 0;
+    if (wl > (uint64_t)kLeanWin) wl = kLeanWin;
+    const uint64_t wlen = (wl + 15) & ~15ull;
+    const uint8_t* base = a.slice + al;
+    const uint32_t batch_len = __builtin_bswap32(ld_u32_at(a.slice + pos + 8));
+    const uint64_t sec0 = pos + 57, sec_end = pos + 12 + (uint64_t)batch_len;
+    const uint64_t sec_len = sec_end - sec0;
+    const int32_t count = sec_len >= 4 ? (int32_t)__builtin_bswap32(ld_u32_at(a.slice + sec0)) : -1;
+    uint32_t end = 0xFFFFu;
+    if (sec_len >= 4 && sec_end - al <= wlen && count >= 0 && count <= kLeanMaxR && (uint64_t)count == rn) {
+      const uint32_t have = (uint32_t)(sec_end - al);
+      uint32_t q = (uint32_t)(sec0 + 4 - al);
+      int n = 0;
+      for (; n < count; n++) {
+        const uint32_t x = ld_u32_at(base + q);
+        const uint32_t term = ~x & 0x80808080u;
+        if (!term) break;
+        const uint32_t nb = (((uint32_t)__builtin_ctz(term)) >> 3) + 1;
+        if (q + nb > have) break;
+        const uint32_t y = nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u));
+        const uint32_t v = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
+        if (v & 1u) break;  // negative length (zigzag)
+        const uint32_t len = v >> 1;
+        if (have - (q + nb) < len) break;
+        if (stage)
+          st[rb - R0 + n] = (uint16_t)q;
+        else
+          a.rstart[rb + n] = (uint16_t)q;
+        q += nb + len;
+      }
+      if (n == count) end = q;
     }
-    if (n == count) end = q;
+    a.rend[b] = (uint16_t)end;
   }
-  a.rend[b] = (uint16_t)end;
+  if (!stage) return;  // uniform
+  __syncthreads();
+  // slots of failed chases hold garbage: the lean kernel never reads them (rend = 0xFFFF)
+  const uint64_t n = R1 - R0;
+  uint16_t* dst = a.rstart + R0;
+  const uint32_t head = (uint32_t)((8u - ((uintptr_t)dst & 15u) / 2u) & 7u);  // u16 slots to 16-B alignment
+  for (uint64_t i = t; i < n && i < head; i += kChaseT) dst[i] = st[i];
+  for (uint64_t i = head + 8ull * t; i + 8 <= n; i += 8ull * kChaseT) {
+    uint4 v;
+    v.x = st[i] | ((uint32_t)st[i + 1] << 16);
+    v.y = st[i + 2] | ((uint32_t)st[i + 3] << 16);
+    v.z = st[i + 4] | ((uint32_t)st[i + 5] << 16);
+    v.w = st[i + 6] | ((uint32_t)st[i + 7] << 16);
+    *(uint4*)(dst + i) = v;
+  }
+  const uint64_t tail0 = n > head ? head + ((n - head) & ~7ull) : n;
+  for (uint64_t i = tail0 + t; i < n; i += kChaseT) dst[i] = st[i];
 }
 
 // four waves per SIMD (eight workgroups per CU, as many as the LDS holds)
@@ -3679,7 +3783,7 @@ void launch_eval(const EvalArgs& a, uint32_t ops, bool lean, hipStream_t s) {
     // persistent: as many workgroups as fit on the device at once
     const bool json = (ops & (opbit(OP_FILTER_JSON) | opbit(OP_PROJECT))) != 0;
     const uint32_t g = std::min<uint32_t>(a.nbatches, lean_grid(json));
-    hipLaunchKernelGGL(k_chase, dim3((a.nbatches + 255) / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_chase, dim3((a.nbatches + kChaseT - 1) / kChaseT), dim3(kChaseT), 0, s, a);
     if (json)
       hipLaunchKernelGGL(k_eval_lean<true>, dim3(g), dim3(kLeanThreads), 0, s, a);
     else

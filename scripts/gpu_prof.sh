@@ -31,7 +31,7 @@ for WL in $WLS; do
   step "fetch_$WL" $?
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$O/write_$WL" -o write --output-format csv -- $B > "$O/write_$WL.log" 2>&1
   step "write_$WL" $?
-  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU -d "$O/sq_$WL" -o sq --output-format csv -- $B > "$O/sq_$WL.log" 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU -d "$O/sq_$WL" -o sq --output-format csv -- $B > "$O/sq_$WL.log" 2>&1
   step "sq_$WL" $?
   cd "$GRAFT_REPO_ROOT"
 done
