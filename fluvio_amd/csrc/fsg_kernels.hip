@@ -1355,6 +1355,7 @@ struct __attribute__((aligned(16))) LeanLdsJ : LeanLds {
   uint32_t ent[kJsonEnt];        // pos | in-string bit << 15 | byte << 16 | token class << 24
   uint32_t racc[kLeanMaxR];      // per record: level fields | message fields << 8 | bad << 16
   uint32_t rlvl[kLeanMaxR];      // per record: bit (LogLevel index) of its level value
+  unsigned long long rbest[kLeanMaxR];  // projection: (member + 1) << 32 | value span of the last matching member
   uint32_t nseg;
   uint32_t wsum[4];              // cross-wave scan carries
   uint8_t dfa[kJsonStates * kJsonCls2];
@@ -1611,6 +1612,76 @@ __device__ __forceinline__ uint32_t json_str_class(const LdsT& L, uint32_t a, ui
 }
 // stages 1-3 for the records [0, nr); returns true if the batch must go to the
 // exact kernel; match bits of records whose level > Debug in L.match
+// lean_json_stage step 3b for the members [0, nseg) of L.jn
+template <bool kProj>
+__device__ __forceinline__ void json_members(LeanLdsJ& L, int nr, uint32_t ntok, uint32_t nseg) {
+  for (uint32_t k = threadIdx.x; k < nseg; k += kLeanThreads) {
+    const uint32_t sg = L.jn[k];
+    const bool first = (sg & 0x8000u) != 0u;
+    const uint32_t t0 = sg & 0x7FFFu;
+    uint32_t t = t0;
+    // the member's record: that of its first token (a record start) or of the comma before it
+    const uint32_t anchor = L.ent[first ? t : t - 1] & 0x7FFFu;
+    const uint32_t rr = (uint32_t)lean_rec_of(L, nr, anchor);
+    const uint32_t ve = L.r_ve[rr];
+    uint32_t st = first ? (uint32_t)JS_OBJ : (uint32_t)JS_KEY;
+    uint32_t prev = first ? 0xFFFFu : anchor;
+    uint32_t nlv = 0, nmsg = 0, lv = 0;
+    bool ended = false, nbad = false;
+    bool khit = false, inval = false, found = false, vneg = false;
+    uint32_t vstart = 0, ntv = 0, fs = 0, fe = 0;
+    for (; t < ntok; t++) {
+      const uint32_t en = L.ent[t];
+      const uint32_t pos = en & 0x7FFFu;
+      if (pos >= ve) break;
+      uint32_t cls = en >> 24;
+      const uint32_t adj = pos == prev + 1 ? 1u : 0u;
+      const uint32_t st0 = st;
+      if constexpr (kProj) {
+        const bool q = cls == JC_Q_FIELD;
+        if (q) cls = JC_Q_OTHER;  // every string takes the "other" paths of the table
+        else if (cls >= JC_Q_LEVEL && cls <= JC_Q_ERROR) cls = JC_Q_OTHER;
+        st = L.dfa[st * kJsonCls2 + cls * 2 + adj];
+        if (st == JS_INKEY_OTHER) khit = q;
+        if (st0 == JS_VAL_OTHER) {
+          inval = true;
+          vstart = pos;
+          ntv = 0;
+          vneg = cls == JC_MINUS;
+        }
+        if (inval) {
+          if (st == JS_KEY || st == JS_END) {  // ',' / '}' after the value
+            inval = false;
+            if (st0 == JS_N_ZERO && vneg && ntv == 2) nbad = true;  // -0
+            if (khit) {
+              found = true;
+              fs = vstart;
+              fe = prev + 1;
+            }
+          } else {
+            ntv++;
+            if (st == JS_N_DOT || st == JS_N_E || ntv > 18) nbad = true;
+          }
+        }
+      } else {
+        if (st >= JS_INV_D && st <= JS_INV_E) lv = 1u << (st - JS_INV_D);
+        st = L.dfa[st * kJsonCls2 + cls * 2 + adj];
+        nlv += st == JS_INKEY_LV ? 1u : 0u;
+        nmsg += st == JS_INKEY_MSG ? 1u : 0u;
+      }
+      prev = pos;
+      if (cls == JC_COMMA || st == JS_FAIL) {
+        ended = true;
+        break;
+      }
+    }
+    const bool ok = !nbad && (ended ? st == JS_KEY : st == JS_END);
+    atomicAdd(&L.racc[rr], nlv | (nmsg << 8) | (ok ? 0u : 1u << 16));
+    if (lv) atomicOr(&L.rlvl[rr], lv);
+    if (found) atomicMax(&L.rbest[rr], ((unsigned long long)(t0 + 1) << 32) | (fs << 16) | fe);
+  }
+}
+
 __device__ bool lean_json_stage(LeanLdsJ& L, int nr, uint32_t& orpar, bool proj, uint32_t fl) {
   const uint32_t l = threadIdx.x;
   const uint32_t c0 = L.r_vs[0] & ~15u, c1 = L.r_ve[nr - 1];
@@ -1692,7 +1763,7 @@ __device__ bool lean_json_stage(LeanLdsJ& L, int nr, uint32_t& orpar, bool proj,
     }
     L.ent[t] = (en & 0xFFFFu) | (b << 16) | (cls << 24);
     // members: the token after a comma starts one (of the comma's record)
-    if (!proj && cls == JC_COMMA) {
+    if (cls == JC_COMMA) {
       const uint32_t k = atomicAdd(&L.nseg, 1u);
       if (k < (uint32_t)kJsonSeg) L.jn[k] = (uint16_t)(t + 1);
     }
@@ -1717,117 +1788,48 @@ __device__ bool lean_json_stage(LeanLdsJ& L, int nr, uint32_t& orpar, bool proj,
       if ((L.ent[m] & 0x7FFFu) < vs) lo = m + 1; else hi = m;
     }
     t_first = lo;
-    if (!proj) {
-      // no token inside the value: not an object (and no member may claim it)
-      if (lo >= ntok || (L.ent[lo] & 0x7FFFu) >= ve) bad = true;
-      L.racc[r] = bad ? 1u << 16 : 0u;
-      L.rlvl[r] = 0;
-      if (!bad) {
-        const uint32_t k = atomicAdd(&L.nseg, 1u);
-        if (k < (uint32_t)kJsonSeg) L.jn[k] = (uint16_t)(lo | 0x8000u);
-      }
+    // no token inside the value: not an object (and no member may claim it)
+    if (lo >= ntok || (L.ent[lo] & 0x7FFFu) >= ve) bad = true;
+    L.racc[r] = bad ? 1u << 16 : 0u;
+    L.rlvl[r] = 0;
+    L.rbest[r] = 0;
+    if (!bad) {
+      const uint32_t k = atomicAdd(&L.nseg, 1u);
+      if (k < (uint32_t)kJsonSeg) L.jn[k] = (uint16_t)(lo | 0x8000u);
     }
   }
-  if (!proj) {
-    lean_sync();
-    const uint32_t nseg = L.nseg;
-    if (nseg > (uint32_t)kJsonSeg) return lean_or(L.red, orpar, true);  // uniform
-    // 3b. the token DFA, one thread per object member: a member after a comma
-    //     starts in JS_KEY (the only state a comma leads to) and ends with the
-    //     next comma, which must lead to JS_KEY again, or at the record's end,
-    //     which must be JS_END.  Per record: each field exactly once, the
-    //     level value's variant.
-    for (uint32_t k = l; k < nseg; k += kLeanThreads) {
-      const uint32_t sg = L.jn[k];
-      const bool first = (sg & 0x8000u) != 0u;
-      uint32_t t = sg & 0x7FFFu;
-      // the member's record: that of its first token (a record start) or of the comma before it
-      const uint32_t anchor = L.ent[first ? t : t - 1] & 0x7FFFu;
-      const uint32_t rr = (uint32_t)lean_rec_of(L, nr, anchor);
-      const uint32_t ve = L.r_ve[rr];
-      uint32_t st = first ? (uint32_t)JS_OBJ : (uint32_t)JS_KEY;
-      uint32_t prev = first ? 0xFFFFu : anchor;
-      uint32_t nlv = 0, nmsg = 0, lv = 0;
-      bool ended = false;
-      for (; t < ntok; t++) {
-        const uint32_t en = L.ent[t];
-        const uint32_t pos = en & 0x7FFFu;
-        if (pos >= ve) break;
-        const uint32_t cls = en >> 24;
-        const uint32_t adj = pos == prev + 1 ? 1u : 0u;
-        if (st >= JS_INV_D && st <= JS_INV_E) lv = 1u << (st - JS_INV_D);
-        st = L.dfa[st * kJsonCls2 + cls * 2 + adj];
-        nlv += st == JS_INKEY_LV ? 1u : 0u;
-        nmsg += st == JS_INKEY_MSG ? 1u : 0u;
-        prev = pos;
-        if (cls == JC_COMMA || st == JS_FAIL) {
-          ended = true;
-          break;
-        }
+  (void)t_first;
+  lean_sync();
+  const uint32_t nseg = L.nseg;
+  if (nseg > (uint32_t)kJsonSeg) return lean_or(L.red, orpar, true);  // uniform
+  // 3b. the token DFA, one thread per object member: a member after a comma
+  //     starts in JS_KEY (the only state a comma leads to) and ends with the
+  //     next comma, which must lead to JS_KEY again, or at the record's end,
+  //     which must be JS_END.  filter_json, per record: each field exactly
+  //     once, the level value's variant.  Projection (map_json_project,
+  //     Map<String, Value>, last member wins): the value span of the last
+  //     member whose key is the field; numbers whose serde_json text differs
+  //     from the source (fractions, exponents, -0, more than 18 digits) are
+  //     unsupported by the device restatement -> exact kernel
+  if (proj)
+    json_members<true>(L, nr, ntok, nseg);
+  else
+    json_members<false>(L, nr, ntok, nseg);
+  lean_sync();
+  if ((int)r < nr) {
+    const uint32_t ac = L.racc[r];
+    if (proj) {
+      bad = (ac >> 16) != 0u;
+      const unsigned long long bst = L.rbest[r];
+      if (!bad && bst) {
+        atomicOr(&L.match[r >> 5], 1u << (r & 31));
+        L.r_vs[r] = (uint32_t)(bst >> 16) & 0xFFFFu;  // the value narrows to the field's text
+        L.r_ve[r] = (uint32_t)bst & 0xFFFFu;
       }
-      const bool ok = ended ? st == JS_KEY : st == JS_END;
-      atomicAdd(&L.racc[rr], nlv | (nmsg << 8) | (ok ? 0u : 1u << 16));
-      if (lv) atomicOr(&L.rlvl[rr], lv);
-    }
-    lean_sync();
-    if ((int)r < nr) {
-      const uint32_t ac = L.racc[r];
+    } else {
       // exactly one level and one message field (a duplicate is a serde error)
       bad = (ac >> 16) != 0u || (ac & 0xFFu) != 1u || ((ac >> 8) & 0xFFu) != 1u;
       if (!bad && (L.rlvl[r] & ~1u)) atomicOr(&L.match[r >> 5], 1u << (r & 31));
-    }
-    return lean_or(L.red, orpar, bad);
-  }
-  // 3c. projection: one thread per record runs the DFA over its tokens
-  if ((int)r < nr) {
-    const uint32_t ve = L.r_ve[r];
-    uint32_t t = t_first;
-    uint32_t st = JS_OBJ, prev = 0xFFFFu;
-    // projection (map_json_project, Map<String, Value>, last member wins): the
-    // value span of the last member whose key is the field; numbers whose
-    // serde_json text differs from the source (fractions, exponents, -0, more
-    // than 18 digits) are unsupported by the device restatement -> exact kernel
-    bool khit = false, inval = false, found = false, vneg = false;
-    uint32_t vstart = 0, ntv = 0, fs = 0, fe = 0;
-    for (; !bad && t < ntok; t++) {
-      const uint32_t en = L.ent[t];
-      const uint32_t pos = en & 0x7FFFu;
-      if (pos >= ve) break;
-      uint32_t cls = en >> 24;
-      const uint32_t adj = pos == prev + 1 ? 1u : 0u;
-      const uint32_t st0 = st;
-      const bool q = cls == JC_Q_FIELD;
-      if (q) cls = JC_Q_OTHER;  // every string takes the "other" paths of the table
-      else if (cls >= JC_Q_LEVEL && cls <= JC_Q_ERROR) cls = JC_Q_OTHER;
-      st = L.dfa[st * kJsonCls2 + cls * 2 + adj];
-      if (st == JS_INKEY_OTHER) khit = q;
-      if (st0 == JS_VAL_OTHER) {
-        inval = true;
-        vstart = pos;
-        ntv = 0;
-        vneg = cls == JC_MINUS;
-      }
-      if (inval) {
-        if (st == JS_KEY || st == JS_END) {  // ',' / '}' after the value
-          inval = false;
-          if (st0 == JS_N_ZERO && vneg && ntv == 2) bad = true;  // -0
-          if (khit) {
-            found = true;
-            fs = vstart;
-            fe = prev + 1;
-          }
-        } else {
-          ntv++;
-          if (st == JS_N_DOT || st == JS_N_E || ntv > 18) bad = true;
-        }
-      }
-      prev = pos;
-    }
-    if (st != JS_END) bad = true;
-    if (!bad && found) {
-      atomicOr(&L.match[r >> 5], 1u << (r & 31));
-      L.r_vs[r] = fs;  // the value narrows to the field's text
-      L.r_ve[r] = fe;
     }
   }
   return lean_or(L.red, orpar, bad);
