@@ -500,6 +500,13 @@ def main():
     head = a.workload
     extra = [] if a.only else [w for w in EXTRA if w != head]
     cpu = cpu_baselines_first(ctx, [head] + extra)
+    if "c5-keyed-agg" in [head] + extra:
+        # torch's HIP runtime (the keyed-state merge) starts before the engine's
+        # large allocations: started after them it can find no device
+        import torch
+        torch.cuda.set_device(ctx.local)
+        torch.zeros(1, device=f"cuda:{ctx.local}")
+        ctx.nccl()
     line = dict(run_workload(ctx, head, a.records, cpu))
     workloads = {}
     for w in extra:
