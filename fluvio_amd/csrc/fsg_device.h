@@ -331,6 +331,34 @@ struct AggjArgs {
   uint64_t* acc_off;       // per batch: the accumulator text after it (offset in cat) ...
   uint32_t* acc_len;       // ... and its length (0xFFFFFFFF: no record aggregated yet)
 };
+// device framing of a stored slice (FileBatchIterator, iterators.rs:55-160):
+// every position whose magic byte (offset 16) is 2 is a candidate batch start;
+// each candidate's successor (pos + 57 + batch_len - 45) is found among the
+// candidates, pointer doubling marks the chain from position 0.  A chain that
+// reaches a non-candidate (a batch without magic 2) goes back to the host walk.
+constexpr uint32_t kFrameChunk = 65536;  // bytes per candidate-collection workgroup
+constexpr uint32_t kFrameCap = 1024;     // candidates per chunk (more: host walk)
+// FN_END: the slice ends after this batch; FN_TAIL: a batch, then fewer than 57 bytes
+// (IO tail); FN_IO / FN_UNSUP: no batch here, the walk stops with that status
+enum FrameNext : uint32_t { FN_END = 0xFFFFFFF0u, FN_TAIL, FN_IO, FN_UNSUP, FN_NONCAND };
+struct FrameArgs {
+  const uint8_t* s;
+  uint64_t len;
+  uint16_t* cbuf;        // per chunk: candidate offsets in the chunk
+  uint32_t* ccnt;        // per chunk: candidates
+  uint64_t* coff;        // ... exclusive prefix
+  uint64_t* cand;        // candidate positions, ascending
+  uint64_t ncand;
+  uint32_t* jmp;         // levels x ncand: successor after 2^level batches (sink = ncand)
+  uint32_t* term;        // per candidate: FrameNext when the walk ends there, else its successor
+  uint32_t* mark;        // per candidate: on the chain from position 0
+  uint64_t* mpre;        // ... exclusive prefix (batch index)
+  uint32_t* nrec;        // per candidate: record count as framed
+  uint64_t* rpre;        // ... exclusive prefix (rbase)
+  uint64_t* bpos;        // out: batch positions
+  uint64_t* rbase;       // out
+  unsigned long long* scal;  // [0] overflow / fallback, [1] tail status, [2] header bytes, [3..] scan totals
+};
 constexpr uint32_t kSkipEntry = 0xFFFFFFFFu;
 constexpr uint32_t kAjLds = 4096;  // k_aggj_text keeps up to this many values in LDS
 

@@ -3335,6 +3335,152 @@ __global__ __launch_bounds__(256) void k_aggj_place(AggjArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// device framing (FileBatchIterator::next, crates/fluvio-storage/src/iterators.rs:
+// 55-160, restated on the host in fsg_runtime.cpp frame()).  See FrameArgs.
+// ---------------------------------------------------------------------------
+// 1. candidates: one workgroup per 64 KiB chunk, 16 coalesced 16-byte rounds;
+//    positions p with s[p + 16] == 2, kept in ascending order per chunk
+__global__ __launch_bounds__(256) void k_frame_cand(FrameArgs a) {
+  __shared__ uint64_t sh[4];
+  __shared__ uint32_t base;
+  const uint32_t t = threadIdx.x;
+  const uint64_t c0 = (uint64_t)blockIdx.x * kFrameChunk;
+  if (t == 0) base = 0;
+  __syncthreads();
+  for (uint32_t i = 0; i < kFrameChunk / (256 * 16); i++) {
+    const uint64_t u = c0 + ((uint64_t)i * 256 + t) * 16;  // the 16 bytes [u, u + 16) hold magic bytes of p = u - 16 + j
+    uint32_t m = 0;
+    if (u < a.len) {
+      const uint4 v = *(const uint4*)(a.s + u);  // the slice buffer is padded (kSlicePad)
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int d = 0; d < 4; d++) {
+        const uint32_t z = zbytes(w[d] ^ 0x02020202u);
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if ((z >> (8 * k + 7)) & 1u) m |= 1u << (4 * d + k);
+      }
+      // magic byte at u + j: candidate p = u + j - 16 (>= 0, inside the slice)
+      const uint32_t lo = u < 16 ? (uint32_t)(16 - u) : 0u;
+      const uint64_t lim = a.len + 16 - u;  // p < len
+      m &= (0xFFFFu << lo) & 0xFFFFu;
+      if (lim < 16) m &= (1u << lim) - 1u;
+    }
+    uint64_t tot;
+    const uint32_t ex = (uint32_t)block_excl_u64((uint64_t)__builtin_popcount(m), sh, tot);
+    uint32_t k = base + ex;
+    while (m) {
+      const uint32_t j = (uint32_t)__builtin_ctz(m);
+      m &= m - 1;
+      if (k < kFrameCap) a.cbuf[(uint64_t)blockIdx.x * kFrameCap + k] = (uint16_t)(u + j - 16 - c0 + 16);
+      k++;
+    }
+    __syncthreads();
+    if (t == 0) base += (uint32_t)tot;
+    __syncthreads();
+  }
+  if (t == 0) {
+    a.ccnt[blockIdx.x] = base < kFrameCap ? base : kFrameCap;
+    if (base > kFrameCap) atomicMax(&a.scal[0], 1ull);  // too dense: host walk
+  }
+}
+// 2. compaction: chunk offsets were stored relative to c0 - 16
+__global__ __launch_bounds__(256) void k_frame_compact(FrameArgs a, uint32_t nchunks) {
+  const uint32_t b = blockIdx.x;
+  if (b >= nchunks) return;
+  const uint32_t n = a.ccnt[b];
+  const uint64_t c0 = (uint64_t)b * kFrameChunk;
+  for (uint32_t k = threadIdx.x; k < n; k += 256)
+    a.cand[a.coff[b] + k] = c0 + a.cbuf[(uint64_t)b * kFrameCap + k] - 16;
+}
+__device__ __forceinline__ uint32_t be32_at(const uint8_t* p) { return __builtin_bswap32(ld_u32_at(p)); }
+// 3. each candidate's successor (the host walk's next step from it)
+__global__ __launch_bounds__(256) void k_frame_next(FrameArgs a) {
+  for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < a.ncand; c += (uint64_t)gridDim.x * 256) {
+    const uint64_t p = a.cand[c];
+    uint32_t nx, nrec = 0;
+    if (a.len - p < 57) {
+      nx = FN_IO;  // "not enough for batch header"
+    } else {
+      const int32_t batch_len = (int32_t)be32_at(a.s + p + 8);
+      const int16_t attrs = (int16_t)(be32_at(a.s + p + 19) & 0xFFFFu);  // bytes 21..22
+      const uint64_t rem = (uint64_t)(int64_t)batch_len - 45;
+      if (batch_len < 45 || a.len - p - 57 < rem) {
+        nx = FN_IO;
+      } else if (attrs & 7) {
+        nx = (attrs & 7) <= 4 ? FN_UNSUP : FN_IO;  // compressed sections: not on the GPU path yet
+      } else {
+        if (rem >= 4) {
+          const int32_t cnt = (int32_t)be32_at(a.s + p + 57);
+          uint64_t c64 = cnt > 0 ? (uint64_t)cnt : 0;
+          const uint64_t mx = (rem - 4) / 7;  // a record is at least 7 bytes
+          nrec = (uint32_t)(c64 < mx ? c64 : mx);
+        }
+        const uint64_t q = p + 57 + rem;
+        if (q == a.len) {
+          nx = FN_END;
+        } else if (a.len - q < 57) {
+          nx = FN_TAIL;  // "not enough for batch header" after this batch
+        } else {  // the candidate at q, if any
+          uint64_t lo = c + 1, hi = a.ncand;
+          while (lo < hi) {
+            const uint64_t m = (lo + hi) >> 1;
+            if (a.cand[m] < q) lo = m + 1; else hi = m;
+          }
+          nx = lo < a.ncand && a.cand[lo] == q ? (uint32_t)lo : FN_NONCAND;
+        }
+      }
+    }
+    a.term[c] = nx;
+    a.nrec[c] = nrec;
+    a.jmp[c] = nx < FN_END ? nx : (uint32_t)a.ncand;  // ends -> sink
+    a.mark[c] = c == 0 && p == 0 ? 1u : 0u;
+  }
+}
+__global__ __launch_bounds__(256) void k_frame_double(const uint32_t* src, uint32_t* dst, uint64_t n) {
+  for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < n; c += (uint64_t)gridDim.x * 256) {
+    const uint32_t x = src[c];
+    dst[c] = x < n ? src[x] : x;
+  }
+}
+// top-down: everything 2^level batches after a marked batch is on the chain
+__global__ __launch_bounds__(256) void k_frame_mark(const uint32_t* jl, uint32_t* mark, uint64_t n) {
+  for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < n; c += (uint64_t)gridDim.x * 256) {
+    if (!__hip_atomic_load(&mark[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) continue;
+    const uint32_t x = jl[c];
+    if (x < n) __hip_atomic_store(&mark[x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// 4. the chain's batches in order; tail status / fallback from its last batch
+__global__ __launch_bounds__(256) void k_frame_emit(FrameArgs a) {
+  unsigned long long hb = 0;
+  for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < a.ncand; c += (uint64_t)gridDim.x * 256) {
+    if (!a.mark[c]) continue;
+    const uint64_t i = a.mpre[c];
+    if (a.term[c] == FN_NONCAND) atomicMax(&a.scal[0], 1ull);  // a batch without magic 2 follows: host walk
+    const uint64_t p = a.cand[c];
+    a.bpos[i] = p;
+    a.rbase[i] = a.rpre[c];
+    hb += 57 + ((uint64_t)be32_at(a.s + p + 8) - 45);
+  }
+  hb = wave_sum(hb);
+  if (lane_id() == 0 && hb) atomicAdd(&a.scal[2], hb);
+}
+// record counts of the chain's batches only (the ends and tails count none)
+__global__ __launch_bounds__(256) void k_frame_counts(FrameArgs a) {
+  for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < a.ncand; c += (uint64_t)gridDim.x * 256) {
+    const uint32_t nx = a.term[c];
+    const bool on = a.mark[c] != 0;
+    if (on && (nx == FN_IO || nx == FN_UNSUP || nx == FN_TAIL))
+      a.scal[1] = nx == FN_UNSUP ? 2ull : 1ull;  // the walk stops here (FN_TAIL: after this batch)
+    if (!on || nx == FN_IO || nx == FN_UNSUP) {  // a tail position is no batch
+      a.nrec[c] = 0;
+      a.mark[c] = 0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // CRC32C (reflected 0x82F63B78) over [off, off + n): chunked raw CRCs + combine
 // ---------------------------------------------------------------------------
 // Tables (built on the host by upload_crc_tables):
@@ -3896,6 +4042,26 @@ void launch_aggj_write(const AggjArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_aggj_text<true>, dim3(a.nblk), dim3(64), 0, s, a);
   else
     hipLaunchKernelGGL(k_aggj_text<false>, dim3(a.nblk), dim3(64), 0, s, a);
+}
+// device framing, in phases separated by host reads of FrameArgs::scal
+void launch_frame_cand(const FrameArgs& a, uint32_t nchunks, uint64_t* tsum, hipStream_t s) {
+  hipLaunchKernelGGL(k_frame_cand, dim3(nchunks), dim3(256), 0, s, a);
+  launch_xscan(a.ccnt, a.coff, tsum, nchunks, a.scal + 3, s);  // scal[3] = candidates
+}
+void launch_frame_compact(const FrameArgs& a, uint32_t nchunks, hipStream_t s) {
+  hipLaunchKernelGGL(k_frame_compact, dim3(nchunks), dim3(256), 0, s, a, nchunks);
+}
+void launch_frame_chain(const FrameArgs& a, uint32_t levels, uint64_t* tsum, hipStream_t s) {
+  const uint64_t n = a.ncand;
+  const uint32_t g = grid_for(n);
+  hipLaunchKernelGGL(k_frame_next, dim3(g), dim3(256), 0, s, a);
+  for (uint32_t j = 1; j < levels; j++)
+    hipLaunchKernelGGL(k_frame_double, dim3(g), dim3(256), 0, s, a.jmp + (j - 1) * n, a.jmp + j * n, n);
+  for (uint32_t j = levels; j-- > 0;) hipLaunchKernelGGL(k_frame_mark, dim3(g), dim3(256), 0, s, a.jmp + j * n, a.mark, n);
+  hipLaunchKernelGGL(k_frame_counts, dim3(g), dim3(256), 0, s, a);
+  launch_xscan(a.mark, a.mpre, tsum, n, a.scal + 4, s);  // batches
+  launch_xscan(a.nrec, a.rpre, tsum, n, a.scal + 5, s);  // records
+  hipLaunchKernelGGL(k_frame_emit, dim3(g), dim3(256), 0, s, a);
 }
 void launch_write(const WriteArgs& a, uint32_t nblocks, hipStream_t s) {
   // nblocks = included batches, one wave each

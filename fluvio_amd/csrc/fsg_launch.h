@@ -28,4 +28,8 @@ void launch_aggj_kid(const AggjArgs& a, uint64_t n_ent, hipStream_t s);
 void launch_aggj_rows(const AggjArgs& a, hipStream_t s);
 void launch_aggj_size(const AggjArgs& a, uint64_t* tsum, hipStream_t s);
 void launch_aggj_write(const AggjArgs& a, hipStream_t s);
+// device framing (FrameArgs)
+void launch_frame_cand(const FrameArgs& a, uint32_t nchunks, uint64_t* tsum, hipStream_t s);
+void launch_frame_compact(const FrameArgs& a, uint32_t nchunks, hipStream_t s);
+void launch_frame_chain(const FrameArgs& a, uint32_t levels, uint64_t* tsum, hipStream_t s);
 }  // namespace fsg

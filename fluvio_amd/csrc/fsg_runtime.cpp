@@ -387,6 +387,7 @@ struct fsg_slice {
   uint64_t nrec = 0;
   int tail_status = 0;
   uint64_t header_bytes = 0;  // 57 B per framed batch + the record sections
+  bool device_framed = false; // framed by k_frame_* (else by the host walk)
 };
 
 struct fsg_chain {
@@ -714,22 +715,121 @@ int frame(const uint8_t* s, size_t len, std::vector<uint64_t>& bpos, std::vector
   return 0;
 }
 
-int upload_slice(fsg_engine* e, const uint8_t* s, size_t len, fsg_slice* sl, hipStream_t stream) {
-  std::vector<uint64_t> bpos, rbase;
-  frame(s, len, bpos, rbase, sl->nrec, sl->tail_status, sl->header_bytes);
+// Device framing (k_frame_*): the slice is copied as is and framed where it
+// lies; 0 = framed, 1 = the host walk must decide (a batch without magic 2
+// on the chain, or more than kFrameCap candidates in a 64 KiB chunk).
+int frame_on_device(fsg_slice* sl, hipStream_t st, int* fallback) {
+  const uint64_t len = sl->len;
+  *fallback = 0;
+  sl->nb = 0;
+  sl->nrec = 0;
+  sl->tail_status = 0;
+  sl->header_bytes = 0;
+  if (len == 0) return FSG_OK;
+  if (len < 57) {  // "not enough for batch header" at position 0
+    sl->tail_status = FSG_E_IO;
+    return FSG_OK;
+  }
+  const uint32_t nchunks = (uint32_t)((len + kFrameChunk - 1) / kFrameChunk);
+  DevBuf cbuf, ccnt, coff, tsum, scal;
+  HIPCHK(cbuf.ensure((size_t)nchunks * kFrameCap * 2));
+  HIPCHK(ccnt.ensure((size_t)nchunks * 4));
+  HIPCHK(coff.ensure((size_t)nchunks * 8));
+  HIPCHK(scal.ensure(64));
+  HIPCHK(hipMemsetAsync(scal.p, 0, 64, st));
+  FrameArgs a{};
+  a.s = sl->data.as<uint8_t>();
+  a.len = len;
+  a.cbuf = cbuf.as<uint16_t>();
+  a.ccnt = ccnt.as<uint32_t>();
+  a.coff = coff.as<uint64_t>();
+  a.scal = scal.as<unsigned long long>();
+  HIPCHK(tsum.ensure(xscan_tiles(nchunks) * 8));
+  launch_frame_cand(a, nchunks, tsum.as<uint64_t>(), st);
+  unsigned long long sc[8];
+  HIPCHK(hipMemcpyAsync(sc, scal.p, 64, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const uint64_t n = sc[3];
+  if (sc[0] || n == 0 || n >= 0xFFFFFFF0ull) {
+    *fallback = 1;
+    return FSG_OK;
+  }
+  DevBuf cand, jmp, term, mark, mpre, nrec, rpre;
+  uint32_t levels = 1;
+  while (levels < 40 && (1ull << (levels - 1)) < n) levels++;
+  HIPCHK(cand.ensure(n * 8));
+  HIPCHK(jmp.ensure((size_t)levels * n * 4));
+  HIPCHK(term.ensure(n * 4));
+  HIPCHK(mark.ensure(n * 4));
+  HIPCHK(mpre.ensure(n * 8));
+  HIPCHK(nrec.ensure(n * 4));
+  HIPCHK(rpre.ensure(n * 8));
+  HIPCHK(sl->bpos.ensure(n * 8));
+  HIPCHK(sl->rbase.ensure(n * 8));
+  HIPCHK(tsum.ensure(xscan_tiles(std::max<uint64_t>(n, nchunks)) * 8));
+  a.cand = cand.as<uint64_t>();
+  a.ncand = n;
+  a.jmp = jmp.as<uint32_t>();
+  a.term = term.as<uint32_t>();
+  a.mark = mark.as<uint32_t>();
+  a.mpre = mpre.as<uint64_t>();
+  a.nrec = nrec.as<uint32_t>();
+  a.rpre = rpre.as<uint64_t>();
+  a.bpos = sl->bpos.as<uint64_t>();
+  a.rbase = sl->rbase.as<uint64_t>();
+  launch_frame_compact(a, nchunks, st);
+  uint64_t first = 1;
+  HIPCHK(hipMemcpyAsync(&first, cand.p, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (first != 0) {  // position 0 has no magic 2: the host walk decides
+    *fallback = 1;
+    return FSG_OK;
+  }
+  launch_frame_chain(a, levels, tsum.as<uint64_t>(), st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(sc, scal.p, 64, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (sc[0]) {
+    *fallback = 1;
+    return FSG_OK;
+  }
+  sl->nb = (uint32_t)sc[4];
+  sl->nrec = sc[5];
+  sl->tail_status = sc[1] == 1 ? FSG_E_IO : sc[1] == 2 ? FSG_E_UNSUPPORTED : 0;
+  sl->header_bytes = sc[2];
+  return FSG_OK;
+}
+
+// device_frame: frame on the device (fsg_slice_upload, process_batch); the
+// host walk frames the one-batch slices process() builds itself
+int upload_slice(fsg_engine* e, const uint8_t* s, size_t len, fsg_slice* sl, hipStream_t stream,
+                 bool device_frame = true) {
   sl->eng = e;
   sl->len = len;
-  sl->nb = (uint32_t)bpos.size();
   const size_t alloc = ((len + 15) & ~(size_t)15) + kSlicePad + kWin;
   HIPCHK(sl->data.ensure(alloc));
   HIPCHK(hipMemsetAsync((uint8_t*)sl->data.p + (len & ~(size_t)15), 0, alloc - (len & ~(size_t)15), stream));
   if (len) HIPCHK(hipMemcpyAsync(sl->data.p, s, len, hipMemcpyHostToDevice, stream));
-  HIPCHK(sl->bpos.ensure(std::max<size_t>(1, bpos.size()) * 8));
-  HIPCHK(sl->rbase.ensure(std::max<size_t>(1, rbase.size()) * 8));
-  if (!bpos.empty()) {
-    HIPCHK(hipMemcpyAsync(sl->bpos.p, bpos.data(), bpos.size() * 8, hipMemcpyHostToDevice, stream));
-    HIPCHK(hipMemcpyAsync(sl->rbase.p, rbase.data(), rbase.size() * 8, hipMemcpyHostToDevice, stream));
+  int fallback = 1;
+  if (device_frame) {
+    int rc = frame_on_device(sl, stream, &fallback);
+    if (rc) return rc;
+    sl->device_framed = !fallback;
   }
+  if (fallback) {
+    sl->device_framed = false;
+    std::vector<uint64_t> bpos, rbase;
+    frame(s, len, bpos, rbase, sl->nrec, sl->tail_status, sl->header_bytes);
+    sl->nb = (uint32_t)bpos.size();
+    HIPCHK(sl->bpos.ensure(std::max<size_t>(1, bpos.size()) * 8));
+    HIPCHK(sl->rbase.ensure(std::max<size_t>(1, rbase.size()) * 8));
+    if (!bpos.empty()) {
+      HIPCHK(hipMemcpyAsync(sl->bpos.p, bpos.data(), bpos.size() * 8, hipMemcpyHostToDevice, stream));
+      HIPCHK(hipMemcpyAsync(sl->rbase.p, rbase.data(), rbase.size() * 8, hipMemcpyHostToDevice, stream));
+    }
+  }
+  HIPCHK(sl->bpos.ensure(8));
+  HIPCHK(sl->rbase.ensure(8));
   HIPCHK(hipStreamSynchronize(stream));
   return FSG_OK;
 }
@@ -743,6 +843,7 @@ extern "C" int fsg_slice_upload(fsg_engine* e, const uint8_t* s, size_t len, fsg
   *out = sl.release();
   return FSG_OK;
 }
+extern "C" int fsg_slice_device_framed(const fsg_slice* s) { return s->device_framed ? 1 : 0; }
 extern "C" int fsg_slice_info(const fsg_slice* s, uint64_t* n_batches, uint64_t* n_records, uint64_t* bytes) {
   if (n_batches) *n_batches = s->nb;
   if (n_records) *n_records = s->nrec;
@@ -1445,7 +1546,7 @@ extern "C" int fsg_chain_process(fsg_chain* c, const uint8_t* raw, size_t len, i
   be(27, (uint64_t)base_timestamp, 8);
   if (len) memcpy(b.data() + 57, raw, len);
   fsg_slice s;
-  int rc = upload_slice(c->eng, b.data(), b.size(), &s, c->stream);
+  int rc = upload_slice(c->eng, b.data(), b.size(), &s, c->stream, false);
   if (rc) return rc;
   fsg_batch_output r;
   rc = run_slice(c, &s, ~0ull, m, &r, c->hdesc.nstages == 0);

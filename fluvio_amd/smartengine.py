@@ -483,6 +483,7 @@ class ResidentSlice:
         nb, nr, by = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         _ffi.lib().fsg_slice_info(h, ctypes.byref(nb), ctypes.byref(nr), ctypes.byref(by))
         self.n_batches, self.n_records, self.bytes = nb.value, nr.value, by.value
+        self.device_framed = bool(_ffi.lib().fsg_slice_device_framed(h))
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -189,6 +189,11 @@ void fsg_free(void *p);
 /* Ingest: copies the slice to HBM and frames its batches (FileBatchIterator). */
 int fsg_slice_upload(fsg_engine *engine, const uint8_t *slice, size_t len, fsg_slice **out);
 int fsg_slice_info(const fsg_slice *s, uint64_t *n_batches, uint64_t *n_records, uint64_t *bytes);
+/* 1 if the slice was framed on the device (k_frame_*: magic-2 candidates,
+ * pointer doubling from position 0), 0 if the host walk framed it (a batch
+ * without magic 2 on the chain, or candidates too dense).  Same result either
+ * way (FileBatchIterator::next, crates/fluvio-storage/src/iterators.rs:55-160). */
+int fsg_slice_device_framed(const fsg_slice *s);
 void fsg_slice_free(fsg_slice *s);
 /* process_batch over a resident slice; the output batch stays in HBM until
  * fsg_chain_download_output (out may be NULL to keep it resident). */

@@ -291,6 +291,73 @@ def test_edge_slices(engine):
     check_batch(engine, [], bytes(more))
 
 
+def _frame_walk(sl):
+    """FileBatchIterator::next (crates/fluvio-storage/src/iterators.rs:55-160) as
+    a plain walk: (batches, records, header bytes, tail) — tail 'io' / 'unsup'."""
+    pos, nb, nrec, hb, tail = 0, 0, 0, 0, None
+    while pos < len(sl):
+        if len(sl) - pos < 57:
+            tail = "io"
+            break
+        blen, = struct.unpack_from(">i", sl, pos + 8)
+        attrs, = struct.unpack_from(">h", sl, pos + 21)
+        if blen < 45 or len(sl) - pos - 57 < blen - 45:
+            tail = "io"
+            break
+        if attrs & 7:
+            tail = "unsup" if (attrs & 7) <= 4 else "io"
+            break
+        rem = blen - 45
+        if rem >= 4:
+            c, = struct.unpack_from(">i", sl, pos + 57)
+            nrec += min(max(c, 0), (rem - 4) // 7)
+        nb += 1
+        hb += 57 + rem
+        pos += 57 + rem
+    return nb, nrec, hb, tail
+
+
+def test_device_framing(engine):
+    """The slice framed on the device (magic-2 candidates, pointer doubling from
+    position 0) equals the host walk; a batch without magic 2 on the chain
+    sends the slice to the host walk, with the same framing."""
+    import random
+    rng = random.Random(7)
+    good = synth.make_slice(2, 3000)
+    small = synth.make_slice(1, 2000)
+    nomagic = bytearray(good)
+    nomagic[16] = 1  # the first batch's magic byte
+    cases = [(good, True), (small, True), (good + small, True), (good + good[:40], True),
+             (good + good[:300], True), (P.Batch(base_offset=5).encode() + good, True), (bytes(nomagic), False)]
+    comp = bytearray(good)
+    # a compressed batch in the middle: the walk stops there (unsupported)
+    pos, k = 0, 0
+    while k < 20:
+        blen, = struct.unpack_from(">i", good, pos + 8)
+        pos += 12 + blen
+        k += 1
+    comp[pos + 22] |= 2
+    cases.append((bytes(comp), True))
+    # random bytes with magic-2 noise between batches are never on the chain
+    noisy = bytearray(good)
+    for _ in range(2000):
+        i = rng.randrange(len(noisy))
+        if noisy[i] == 0x20:
+            noisy[i] = 2
+    cases.append((bytes(noisy), True))
+    for sl, dev in cases:
+        rs = ResidentSlice(engine, sl)
+        nb, nrec, hb, tail = _frame_walk(sl)
+        assert (rs.n_batches, rs.n_records, rs.bytes) == (nb, nrec, hb)
+        assert rs.device_framed == dev
+    for sl, _ in cases:
+        if _frame_walk(sl)[3] == "unsup":
+            with pytest.raises(Unsupported):
+                gpu_chain(engine, CHAINS["filter_init_timeout"]).process_batch(sl)
+        else:
+            check_batch(engine, CHAINS["filter_init_timeout"], sl)
+
+
 def test_unicode_word_is_loud(engine):
     """\\w on a non-ASCII value is outside the GPU subset: FSG_E_UNSUPPORTED when
     (and only when) such a record is reached in stream order, like the oracle."""
