@@ -26,6 +26,8 @@ FSG_E_STORE_MEMORY = -102
 FSG_E_UNSUPPORTED = -103
 FSG_E_IO = -104
 FSG_E_INVALID_ARG = -105
+FSG_E_LOOKBACK = -106
+FSG_LOOKBACK_NONE, FSG_LOOKBACK_LAST, FSG_LOOKBACK_AGE = 0, 1, 2
 FSG_E_DEVICE = -200
 
 
@@ -58,6 +60,15 @@ class fsg_batch_output(ctypes.Structure):
                 ("error", fsg_runtime_error)]
 
 
+class fsg_lookback(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("stage", ctypes.c_uint32), ("last", ctypes.c_uint64),
+                ("age_ms", ctypes.c_uint64)]
+
+
+READ_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(fsg_lookback),
+                           ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t))
+
+
 class fsg_timings(ctypes.Structure):
     _fields_ = [("eval_ms", ctypes.c_float), ("plan_ms", ctypes.c_float), ("write_ms", ctypes.c_float),
                 ("crc_ms", ctypes.c_float), ("total_ms", ctypes.c_float), ("in_bytes", ctypes.c_uint64),
@@ -87,7 +98,10 @@ SIGNATURES = {
                                          ctypes.POINTER(fsg_metrics), ctypes.POINTER(ctypes.POINTER(fsg_output))]),
     "fsg_chain_process_batch": (ctypes.c_int, [VP, U8P, SZ, ctypes.c_uint64, ctypes.POINTER(fsg_metrics),
                                                ctypes.POINTER(ctypes.POINTER(fsg_batch_output))]),
-    "fsg_chain_look_back": (ctypes.c_int, [VP, ctypes.POINTER(fsg_metrics)]),
+    "fsg_chain_look_back": (ctypes.c_int, [VP, READ_FN, VP, ctypes.POINTER(fsg_metrics),
+                                           ctypes.POINTER(fsg_runtime_error)]),
+    "fsg_runtime_error_free": (None, [ctypes.POINTER(fsg_runtime_error)]),
+    "fsg_chain_builder_set_lookback": (ctypes.c_int, [VP, SZ, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint64]),
     "fsg_chain_get_accumulator": (ctypes.c_int, [VP, SZ, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
                                                  ctypes.POINTER(SZ)]),
     "fsg_chain_keyed_state": (ctypes.c_int, [VP, SZ, VP, VP, SZ, ctypes.POINTER(SZ)]),

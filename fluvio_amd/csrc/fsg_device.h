@@ -36,6 +36,8 @@ enum StageOp : uint8_t {
   OP_AGG_CONCAT = 9,   // aggregate: String accumulator ++ value (last stage)
   OP_PROJECT = 10,     // map_json_project: the value narrows to one JSON field's text (FilterMap)
   OP_AGG_JSON = 11,    // aggregate-json: HashMap<String, u32> += per key, pretty JSON accumulator (last stage)
+  OP_LB_MAX = 12,      // filter_look_back: from_utf8 + parse::<i32>, keep > PREV (stateful, last stage)
+  OP_DEDUP = 13,       // filter_hashset: from_utf8, keep values new to a BoundedHashSet (stateful, last stage)
 };
 
 // value representation entering a stage (static per chain position)
@@ -87,7 +89,7 @@ struct StageDesc {
   uint8_t op;
   uint8_t kind;        // SmartModuleKind tag (FSG_KIND_*)
   uint8_t in_type;     // ValType
-  uint8_t keep_match;  // OP_REGEX: 1 keep matching, 0 keep non-matching
+  uint8_t keep_match;  // OP_REGEX: 1 keep matching, 0 keep non-matching; OP_LB_MAX / OP_DEDUP: 1 = look_back mode
   uint32_t needle;     // blob offset (OP_CONTAINS)
   uint32_t needle_len;
   uint32_t acc_bad;    // OP_AGG_SUM: initial accumulator is invalid UTF-8
@@ -97,7 +99,7 @@ struct StageDesc {
 };
 
 // ChainDesc::flags: what the last stage is
-enum ChainFlags : uint32_t { CF_AGG_SUM = 1u, CF_AGG_CAT = 2u, CF_ARRAY = 4u, CF_AGG_JSON = 8u };
+enum ChainFlags : uint32_t { CF_AGG_SUM = 1u, CF_AGG_CAT = 2u, CF_ARRAY = 4u, CF_AGG_JSON = 8u, CF_STATEFUL = 16u };
 struct ChainDesc {
   uint32_t nstages;
   uint32_t out_type;   // ValType of the value after the last stage
@@ -211,7 +213,7 @@ struct Plan {
   int64_t agg_prefix_first;  // aggregate prefix (exclusive) at `first` — unused unless has_agg
   int64_t acc_final;         // aggregate accumulator after the stop batch
   int32_t acc_touched;       // accumulator changed by this call
-  int32_t pad;
+  int32_t done;              // last batch whose process() call completed (-1 none): state commits through it
   uint64_t cat_final;        // aggregate (concat): accumulator bytes appended through the stop batch
 };
 
@@ -358,6 +360,53 @@ struct FrameArgs {
   uint64_t* bpos;        // out: batch positions
   uint64_t* rbase;       // out
   unsigned long long* scal;  // [0] overflow / fallback, [1] tail status, [2] header bytes, [3..] scan totals
+};
+// stateful last stages (k_sf_*): filter_look_back (running max, PREV) and
+// filter_hashset (BoundedHashSet<String>: FIFO of distinct values, `limit`).
+// The stage runs on the records that reach it in batches b that
+// process_batch evaluates up to the stage (sf_ran); decisions in stream order,
+// descriptors compacted in place, state committed through plan.done.
+// Dedup state: entries (hash, arena bytes, last new-insertion index) persist
+// across calls; an open-addressing table over entries + this call's records is
+// rebuilt per call.  A value is in the set iff its last new-insertion index is
+// among the newest `limit` (the set holds the newest `limit` insertions).
+constexpr unsigned long long kSfEnt = 1ull << 63;  // table ref: entry id (else record index + 1)
+constexpr uint64_t kSfNone = ~0ull;
+struct SfArgs {
+  const uint8_t* slice;
+  BatchStat* bstat;
+  KeptRec* desc;
+  const uint64_t* rbase;
+  const Mins* mins;
+  const Plan* plan;
+  uint32_t nbatches;
+  uint32_t op;             // OP_LB_MAX / OP_DEDUP
+  uint32_t lookback;       // 1: look_back mode (no decisions, no compaction)
+  uint32_t fast;           // dedup: 1 = no eviction during this call (parallel decisions)
+  int64_t* bval;           // per batch: LB max of the values / dedup kept count
+  int64_t* bpre;           // ... exclusive prefix (LB: max with PREV, dedup: sum)
+  int32_t* prev;           // LB: PREV in HBM
+  // dedup
+  uint32_t* bn;            // per batch: records reaching the stage (0 where it did not run)
+  uint64_t* hv;            // per record (rbase index): value hash
+  uint64_t* vref;          // per record: value offset in the slice | kSfEnt for the uppercase view
+  uint32_t* vlen;          // per record: value length
+  uint32_t* slot;          // per record: table slot
+  uint8_t* keep;           // per record: decision
+  uint64_t* idx;           // per record: new-insertion index when kept
+  unsigned long long* sref;  // table: 0 empty, kSfEnt | entry, record index + 1
+  uint32_t* first;         // per slot: first record of this call
+  uint64_t* cur;           // per slot: last new-insertion index + 1 during the sequential walk
+  uint32_t cap;
+  uint64_t* ent_hash;
+  uint64_t* ent_pos;       // arena offset
+  uint32_t* ent_len;
+  uint64_t* ent_last;      // last new-insertion index + 1 (0: none)
+  uint8_t* arena;
+  uint64_t n_ent;          // entries at call start
+  uint64_t n0;             // new insertions before this call
+  uint64_t limit;
+  unsigned long long* scal;  // [0] entries after commit [1] arena bytes [2] N after commit [3] keeps
 };
 constexpr uint32_t kSkipEntry = 0xFFFFFFFFu;
 constexpr uint32_t kAjLds = 4096;  // k_aggj_text keeps up to this many values in LDS

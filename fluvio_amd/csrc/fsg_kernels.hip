@@ -236,8 +236,9 @@ constexpr uint32_t kOpsJson = opbit(OP_FILTER_JSON) | opbit(OP_CONTAINS) | opbit
                               opbit(OP_REGEX);
 constexpr uint32_t kOpsArray = opbit(OP_ARRAY_MAP) | opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
 constexpr uint32_t kOpsInt = opbit(OP_FILTER_ODD) | opbit(OP_MAP_DOUBLE) | opbit(OP_FILTER_MAP) | opbit(OP_AGG_SUM) |
-                             opbit(OP_AGG_CONCAT) | opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER);
-constexpr uint32_t kOpsAll = 0xFFFu;
+                             opbit(OP_AGG_CONCAT) | opbit(OP_CONTAINS) | opbit(OP_MAP_UPPER) | opbit(OP_LB_MAX) |
+                             opbit(OP_DEDUP);
+constexpr uint32_t kOpsAll = 0xFFFFu;
 constexpr int kDfaDyn = 768 + kDfaLds;  // dynamic LDS of a chain with a regex stage
 extern __shared__ __attribute__((aligned(16))) uint8_t g_dyn_lds[];
 
@@ -692,7 +693,8 @@ __device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int 
     const bool upper = sd.in_type == VT_SRC_UPPER;
     if (op == OP_MAP_UPPER) continue;  // value representation changes statically
     const bool need_utf8 = src && (op == OP_CONTAINS || op == OP_REGEX || op == OP_FILTER_ODD ||
-                                   op == OP_MAP_DOUBLE || op == OP_AGG_SUM || op == OP_AGG_CONCAT);
+                                   op == OP_MAP_DOUBLE || op == OP_AGG_SUM || op == OP_AGG_CONCAT ||
+                                   op == OP_LB_MAX || op == OP_DEDUP);
     // ---- data-parallel phase over window bytes
     for (int r = l; r < nr; r += kEvalThreads) L.r_flags[r] &= ~RF_MATCH;
     __syncthreads();
@@ -912,9 +914,10 @@ __device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int 
           case OP_FILTER_ODD:
           case OP_MAP_DOUBLE:
           case OP_FILTER_MAP:
-          case OP_AGG_SUM: {
+          case OP_AGG_SUM:
+          case OP_LB_MAX: {
             if constexpr (!(kOps & (opbit(OP_FILTER_ODD) | opbit(OP_MAP_DOUBLE) | opbit(OP_FILTER_MAP) |
-                                    opbit(OP_AGG_SUM))))
+                                    opbit(OP_AGG_SUM) | opbit(OP_LB_MAX))))
               break;
             int32_t x = 0;
             int pk = 0;
@@ -941,7 +944,9 @@ __device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int 
               else
                 f &= ~RF_ALIVE;
             } else {
-              L.r_ival[r] = x;  // aggregate input; running sum formed by the cross-batch scan
+              // aggregate input (running sum formed by the cross-batch scan) /
+              // filter_look_back value (kept or not by k_sf_compact)
+              L.r_ival[r] = x;
             }
             break;
           }
@@ -1216,7 +1221,7 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
             d.ival = L.r_ival[r];
           } else {
             d.mode = out_type == VT_SRC_UPPER ? KM_UPPER : KM_COPY;
-            d.ival = 0;
+            d.ival = L.r_ival[r];  // filter_look_back: the parsed value for k_sf_*
           }
           a.desc[rb + kcount + pre] = d;
         }
@@ -2495,6 +2500,7 @@ __global__ void k_plan(PlanArgs a) {
   p.first = -1;
   p.last = -1;
   p.stop = -1;
+  p.done = -1;
   p.lod = -1;
   p.base_offset = -1;
   // stop batch: min(error batch, cut batch); the cut batch was processed too
@@ -2523,6 +2529,9 @@ __global__ void k_plan(PlanArgs a) {
   }
   if (status != 0) {
     p.status = status;
+    // process() completed for the batches before the failing one (all of them
+    // when the iterator failed after the last framed batch)
+    p.done = fail_at != NONE ? (int32_t)fail_at - 1 : (int32_t)n - 1;
     const uint32_t m = fail_at != NONE ? fail_at : (n ? n - 1 : NONE);
     if (m != NONE) {
       ScanRow r = incl_at(a, m);
@@ -2537,6 +2546,7 @@ __global__ void k_plan(PlanArgs a) {
     return;
   }
   p.stop = (int32_t)stop;
+  p.done = (int32_t)stop;
   const ScanRow rs = incl_at(a, stop);
   p.bytes_in = rs.bytes_in;
   p.invocations = stop + 1;
@@ -3846,6 +3856,336 @@ __global__ __launch_bounds__(kWlThreads) void k_write_lean(WriteArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// stateful last stages (k_sf_*): filter_look_back (examples/filter_look_back:
+// keep a value above PREV, PREV = the kept value; look_back sets PREV to each
+// record) and filter_hashset (examples/filter_hashset: SET.insert(value) keeps
+// the record when the value was new; the BoundedHashSet holds the newest
+// `limit` insertions).  k_eval validated / parsed every record reaching the
+// stage and kept it; these kernels decide in stream order over the batches
+// process_batch ran the stage on (sf_ran), compact the descriptors in place,
+// and, after k_plan, commit the state through plan.done.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool sf_ran(const Mins& m, uint32_t b, uint32_t flags) {
+  if (b >= m.first_dec || b >= m.first_unsup) return false;  // (0xFFFFFFFF = none)
+  if (b < m.first_err) return true;
+  return b == m.first_err && (flags & BF_LAST_STAGE);  // the error was the stage's own
+}
+__device__ __forceinline__ uint32_t sf_word(const uint8_t* p, uint32_t i, uint32_t n, bool upper) {
+  uint32_t w = ld_u32_at(p + i);
+  if (upper) w = swar_upper(w);
+  if (n - i < 4) w &= (1u << (8 * (n - i))) - 1u;
+  return w;
+}
+// hash of a value's bytes as the stage sees them (the uppercase view after a map)
+__device__ uint64_t sf_hash(const uint8_t* p, uint32_t n, bool upper) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
+  for (uint32_t i = 0; i < n; i += 4) {
+    h = (h ^ sf_word(p, i, n, upper)) * 0x100000001B3ull;
+    h ^= h >> 29;
+  }
+  return h | 1ull;
+}
+__device__ bool sf_eq(const uint8_t* p, bool pu, const uint8_t* q, bool qu, uint32_t n) {
+  for (uint32_t i = 0; i < n; i += 4)
+    if (sf_word(p, i, n, pu) != sf_word(q, i, n, qu)) return false;
+  return true;
+}
+
+// per batch: LB: the max of the stage's values; dedup: value hashes and spans
+__global__ __launch_bounds__(256) void k_sf_prep(SfArgs a) {
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t l = lane_id();
+  if (b >= a.nbatches) return;
+  const BatchStat st = a.bstat[b];
+  const bool ran = sf_ran(*a.mins, b, st.flags);
+  const uint64_t rb = a.rbase[b];
+  const uint32_t nk = ran ? st.nkeep : 0u;
+  if (a.op == OP_LB_MAX) {
+    int64_t m = INT64_MIN;
+    for (uint32_t k = l; k < nk; k += 64) {
+      const int64_t v = a.desc[rb + k].ival;
+      m = v > m ? v : m;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const int64_t t = __shfl_xor(m, o, 64);
+      m = t > m ? t : m;
+    }
+    if (l == 0) a.bval[b] = m;
+    return;
+  }
+  for (uint32_t k = l; k < nk; k += 64) {
+    const KeptRec d = a.desc[rb + k];
+    a.hv[rb + k] = sf_hash(a.slice + d.vpos, d.vlen, d.mode == KM_UPPER);
+    a.vref[rb + k] = d.vpos | (d.mode == KM_UPPER ? kSfEnt : 0ull);  // the value's view, past the compaction
+    a.vlen[rb + k] = d.vlen;
+    a.keep[rb + k] = 0;
+  }
+  if (l == 0) a.bn[b] = nk;
+}
+
+__global__ __launch_bounds__(256) void k_sf_clear(SfArgs a) {
+  for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < a.cap; s += gridDim.x * 256) {
+    a.sref[s] = 0ull;
+    a.first[s] = 0xFFFFFFFFu;
+  }
+}
+// the persisted entries (distinct values) back into the table
+__global__ __launch_bounds__(256) void k_sf_rehash(SfArgs a) {
+  const uint32_t mask = a.cap - 1;
+  for (uint64_t e = blockIdx.x * 256ull + threadIdx.x; e < a.n_ent; e += gridDim.x * 256ull) {
+    uint32_t s = (uint32_t)a.ent_hash[e] & mask;
+    while (atomicCAS(&a.sref[s], 0ull, kSfEnt | e) != 0ull) s = (s + 1) & mask;
+  }
+}
+// every record of the stage: find or claim the slot of its value (exact byte
+// compare against the slot's entry or first claimant), note the first record
+__global__ __launch_bounds__(256) void k_sf_insert(SfArgs a) {
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t l = lane_id();
+  if (b >= a.nbatches) return;
+  const uint32_t n = a.bn[b];
+  const uint64_t rb = a.rbase[b];
+  const uint32_t mask = a.cap - 1;
+  for (uint32_t k = l; k < n; k += 64) {
+    const uint64_t t = rb + k;
+    const uint64_t vr = a.vref[t];
+    const uint32_t vl = a.vlen[t];
+    const uint8_t* v = a.slice + (vr & ~kSfEnt);
+    const bool up = (vr & kSfEnt) != 0;
+    const uint64_t h = a.hv[t];
+    uint32_t s = (uint32_t)h & mask;
+    for (;;) {
+      const unsigned long long cur = atomicCAS(&a.sref[s], 0ull, (unsigned long long)(t + 1));
+      if (cur == 0ull) break;  // claimed
+      bool same;
+      if (cur & kSfEnt) {
+        const uint64_t e = cur & ~kSfEnt;
+        same = a.ent_hash[e] == h && a.ent_len[e] == vl && sf_eq(v, up, a.arena + a.ent_pos[e], false, vl);
+      } else {
+        const uint64_t t2 = cur - 1;
+        const uint64_t vr2 = a.vref[t2];
+        same = a.hv[t2] == h && a.vlen[t2] == vl && sf_eq(v, up, a.slice + (vr2 & ~kSfEnt), (vr2 & kSfEnt) != 0, vl);
+      }
+      if (same) break;
+      s = (s + 1) & mask;
+    }
+    a.slot[t] = s;
+    atomicMin(&a.first[s], (uint32_t)t);
+  }
+}
+// no eviction can happen during the call: a record is new iff its value is
+// absent at the call's start (no entry, or an entry older than the newest
+// `limit` insertions) and it is the value's first record
+__global__ __launch_bounds__(256) void k_sf_decide(SfArgs a) {
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t l = lane_id();
+  if (b >= a.nbatches) return;
+  const uint32_t nk = a.bn[b];
+  const uint64_t rb = a.rbase[b];
+  uint64_t cnt = 0;
+  for (uint32_t k = l; k < nk; k += 64) {
+    const uint64_t t = rb + k;
+    const uint32_t s = a.slot[t];
+    const unsigned long long ref = a.sref[s];
+    bool present = false;
+    if (ref & kSfEnt) {  // last new-insertion index + 1 (0: none)
+      const uint64_t last1 = a.ent_last[ref & ~kSfEnt];
+      present = last1 != 0 && a.n0 - (last1 - 1) <= a.limit;
+    }
+    const bool kp = !present && a.first[s] == (uint32_t)t;
+    a.keep[t] = kp ? 1 : 0;
+    cnt += kp ? 1 : 0;
+  }
+  cnt = wave_sum(cnt);
+  if (l == 0) a.bval[b] = (int64_t)cnt;
+}
+// evictions possible: the BoundedHashSet walk in stream order, one thread
+// (a value is present iff its last new-insertion index is among the newest
+// `limit`); cur[] starts from the entries' indices
+__global__ __launch_bounds__(256) void k_sf_cur_init(SfArgs a) {
+  for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < a.cap; s += gridDim.x * 256) {
+    const unsigned long long ref = a.sref[s];
+    a.cur[s] = (ref & kSfEnt) ? a.ent_last[ref & ~kSfEnt] : 0ull;
+  }
+}
+__global__ void k_sf_seq(SfArgs a) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint64_t N = a.n0;
+  for (uint32_t b = 0; b < a.nbatches; b++) {
+    const uint32_t n = a.bn[b];
+    const uint64_t rb = a.rbase[b];
+    int64_t cnt = 0;
+    for (uint32_t k = 0; k < n; k++) {
+      const uint64_t t = rb + k;
+      const uint32_t s = a.slot[t];
+      const uint64_t last1 = a.cur[s];
+      const bool present = last1 != 0 && N - (last1 - 1) <= a.limit;
+      a.keep[t] = present ? 0 : 1;
+      if (!present) {
+        a.cur[s] = N + 1;
+        a.idx[t] = N;
+        N++;
+        cnt++;
+      }
+    }
+    a.bval[b] = cnt;
+  }
+}
+// exclusive scan of one int64 per batch (op 0: sum, 1: max) from `init`, one
+// workgroup; total = the inclusive value after the last batch
+__global__ __launch_bounds__(1024) void k_sf_scan(const int64_t* v, int64_t* out, uint32_t n, uint32_t op, int64_t init,
+                                                   const int32_t* init32, unsigned long long* total) {
+  __shared__ int64_t wsum[16];
+  __shared__ int64_t carry_s;
+  const uint32_t t = threadIdx.x, l = t & 63u, w = t >> 6;
+  auto comb = [op](int64_t x, int64_t y) { return op ? (x > y ? x : y) : x + y; };
+  const int64_t ident = op ? INT64_MIN : 0;
+  int64_t carry = init32 ? (int64_t)*init32 : init;  // LB: PREV from HBM
+  for (uint32_t base = 0; base < n; base += 1024) {
+    const uint32_t i = base + t;
+    int64_t x = i < n ? v[i] : ident;
+    for (int o = 1; o < 64; o <<= 1) {  // wave inclusive scan
+      const int64_t y = __shfl_up(x, o, 64);
+      if ((int)l >= o) x = comb(x, y);
+    }
+    if (l == 63) wsum[w] = x;
+    __syncthreads();
+    if (t == 0) {
+      int64_t c = carry;
+      for (int k = 0; k < 16; k++) {
+        const int64_t s = wsum[k];
+        wsum[k] = c;  // exclusive prefix of wave k
+        c = comb(c, s);
+      }
+      carry_s = c;
+    }
+    __syncthreads();
+    const int64_t ex = __shfl_up(x, 1, 64);
+    const int64_t pre = l == 0 ? wsum[w] : comb(wsum[w], ex);
+    if (i < n) out[i] = pre;
+    carry = carry_s;
+    __syncthreads();
+  }
+  if (t == 0 && total) *total = (unsigned long long)carry;
+}
+// decisions -> in-place compaction of each batch's descriptors (LB: keep a
+// value above the running max of PREV and the values before it)
+__global__ __launch_bounds__(256) void k_sf_compact(SfArgs a) {
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t l = lane_id();
+  if (b >= a.nbatches) return;
+  BatchStat st = a.bstat[b];
+  if (!sf_ran(*a.mins, b, st.flags)) return;
+  const uint64_t rb = a.rbase[b];
+  int64_t carry = a.bpre[b];  // LB: PREV and every value before the batch; dedup: kept before it
+  uint32_t w = 0;
+  for (uint32_t k0 = 0; k0 < st.nkeep; k0 += 64) {
+    const uint32_t k = k0 + l;
+    const bool valid = k < st.nkeep;
+    KeptRec d = {};
+    if (valid) d = a.desc[rb + k];
+    bool kp;
+    if (a.op == OP_LB_MAX) {
+      int64_t x = valid ? (int64_t)d.ival : INT64_MIN;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(x, o, 64);
+        if ((int)l >= o) x = x > y ? x : y;
+      }
+      int64_t ex = __shfl_up(x, 1, 64);
+      if (l == 0) ex = INT64_MIN;
+      const int64_t run = ex > carry ? ex : carry;
+      kp = valid && (int64_t)d.ival > run;
+      const int64_t top = __shfl(x, 63, 64);
+      carry = top > carry ? top : carry;
+    } else {
+      kp = valid && a.keep[rb + k];
+      if (a.fast) {
+        const uint64_t bal = ballot(kp);
+        if (kp) a.idx[rb + k] = a.n0 + (uint64_t)carry + (uint64_t)__popcll(bal & ((1ull << l) - 1ull));
+        carry += __popcll(bal);
+      }
+    }
+    const uint64_t bal = ballot(kp);
+    if (kp) a.desc[rb + w + __popcll(bal & ((1ull << l) - 1ull))] = d;
+    w += (uint32_t)__popcll(bal);
+  }
+  if (l == 0) {
+    a.bstat[b].nkeep = w;
+    a.bstat[b].nout = w;
+  }
+}
+// after k_plan: PREV through plan.done
+__global__ void k_sf_commit_lb(SfArgs a) {
+  if (threadIdx.x != 0) return;
+  const int32_t done = a.plan->done;
+  if (done < 0) return;
+  if (a.lookback) {  // look_back: PREV = the last record's value (stops at the first error)
+    const Mins m = *a.mins;
+    for (int32_t b = done; b >= 0; b--) {
+      const BatchStat st = a.bstat[b];
+      if (sf_ran(m, (uint32_t)b, st.flags) && st.nkeep) {
+        *a.prev = a.desc[a.rbase[b] + st.nkeep - 1].ival;
+        return;
+      }
+    }
+    return;
+  }
+  const int64_t bv = a.bval[done], bp = a.bpre[done];
+  *a.prev = (int32_t)(bv > bp ? bv : bp);
+}
+// dedup commit 1: a value first kept in this call (through plan.done) becomes
+// an entry (bytes copied to the arena as the stage saw them)
+__global__ __launch_bounds__(256) void k_sf_commit_new(SfArgs a) {
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t l = lane_id();
+  if (b >= a.nbatches || (int32_t)b > a.plan->done) return;
+  const uint64_t rb = a.rbase[b];
+  const uint32_t n = a.bn[b];  // 0 when the stage did not run on b
+  for (uint32_t k = l; k < n; k += 64) {
+    const uint64_t t = rb + k;
+    if (!a.keep[t]) continue;
+    const uint32_t s = a.slot[t];
+    if ((a.sref[s] & kSfEnt) || a.first[s] != (uint32_t)t) continue;
+    const uint64_t e = atomicAdd(&a.scal[0], 1ull);
+    const uint32_t len = a.vlen[t];
+    const uint64_t pos = atomicAdd(&a.scal[1], (unsigned long long)len);
+    const uint64_t vr = a.vref[t];
+    const uint8_t* src = a.slice + (vr & ~kSfEnt);
+    const bool up = (vr & kSfEnt) != 0;
+    for (uint32_t i = 0; i < len; i++) {
+      uint8_t c = src[i];
+      if (up && c >= 'a' && c <= 'z') c -= 32;
+      a.arena[pos + i] = c;
+    }
+    a.ent_hash[e] = a.hv[t];
+    a.ent_pos[e] = pos;
+    a.ent_len[e] = len;
+    a.ent_last[e] = 0;
+    a.sref[s] = kSfEnt | e;
+  }
+}
+// dedup commit 2: every entry's last new-insertion index (+1) through plan.done
+__global__ __launch_bounds__(256) void k_sf_commit_last(SfArgs a) {
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t l = lane_id();
+  if (b >= a.nbatches || (int32_t)b > a.plan->done) return;
+  const uint64_t rb = a.rbase[b];
+  const uint32_t n = a.bn[b];
+  for (uint32_t k = l; k < n; k += 64) {
+    const uint64_t t = rb + k;
+    if (!a.keep[t]) continue;
+    const unsigned long long ref = a.sref[a.slot[t]];
+    atomicMax((unsigned long long*)&a.ent_last[ref & ~kSfEnt], (unsigned long long)(a.idx[t] + 1));
+  }
+}
+// dedup commit 3: insertions through plan.done
+__global__ void k_sf_commit_n(SfArgs a) {
+  if (threadIdx.x != 0) return;
+  const int32_t done = a.plan->done;
+  a.scal[2] = a.n0 + (done >= 0 ? (uint64_t)(a.bpre[done] + a.bval[done]) : 0ull);
+}
+
+// ---------------------------------------------------------------------------
 // host-side launch wrappers (called from fsg_runtime.cpp)
 // ---------------------------------------------------------------------------
 }  // namespace fsg
@@ -4085,4 +4425,45 @@ void launch_crc(uint8_t* out, uint64_t off, uint64_t n, uint32_t* acc, hipStream
   hipLaunchKernelGGL(k_crc_final, dim3(1), dim3(64), 0, s, out, (const uint32_t*)acc, nblocks ? zend : off, end, n);
 }
 
+// stateful last stage (k_sf_*), between the eval and the size passes
+void launch_sf_lb(const SfArgs& a, hipStream_t s) {
+  if (!a.nbatches) return;
+  const uint32_t g = (a.nbatches + 3) / 4;
+  hipLaunchKernelGGL(k_sf_prep, dim3(g), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_sf_scan, dim3(1), dim3(1024), 0, s, (const int64_t*)a.bval, a.bpre, a.nbatches, 1u, (int64_t)0,
+                     (const int32_t*)a.prev, (unsigned long long*)nullptr);
+  if (!a.lookback) hipLaunchKernelGGL(k_sf_compact, dim3(g), dim3(256), 0, s, a);
+}
+void launch_sf_dedup(const SfArgs& a, hipStream_t s) {
+  if (!a.nbatches) return;
+  const uint32_t g = (a.nbatches + 3) / 4;
+  hipLaunchKernelGGL(k_sf_prep, dim3(g), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_sf_clear, dim3(grid_for(a.cap)), dim3(256), 0, s, a);
+  if (a.n_ent) hipLaunchKernelGGL(k_sf_rehash, dim3(grid_for(a.n_ent)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_sf_insert, dim3(g), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_sf_decide, dim3(g), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_sf_scan, dim3(1), dim3(1024), 0, s, (const int64_t*)a.bval, a.bpre, a.nbatches, 0u, (int64_t)0,
+                     (const int32_t*)nullptr, a.scal + 3);
+}
+void launch_sf_dedup_seq(const SfArgs& a, hipStream_t s) {
+  if (!a.nbatches) return;
+  hipLaunchKernelGGL(k_sf_cur_init, dim3(grid_for(a.cap)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_sf_seq, dim3(1), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(k_sf_scan, dim3(1), dim3(1024), 0, s, (const int64_t*)a.bval, a.bpre, a.nbatches, 0u, (int64_t)0,
+                     (const int32_t*)nullptr, a.scal + 3);
+}
+void launch_sf_compact(const SfArgs& a, hipStream_t s) {
+  if (a.nbatches) hipLaunchKernelGGL(k_sf_compact, dim3((a.nbatches + 3) / 4), dim3(256), 0, s, a);
+}
+void launch_sf_commit(const SfArgs& a, hipStream_t s) {
+  if (!a.nbatches) return;
+  if (a.op == OP_LB_MAX) {
+    hipLaunchKernelGGL(k_sf_commit_lb, dim3(1), dim3(64), 0, s, a);
+    return;
+  }
+  const uint32_t g = (a.nbatches + 3) / 4;
+  hipLaunchKernelGGL(k_sf_commit_new, dim3(g), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_sf_commit_last, dim3(g), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_sf_commit_n, dim3(1), dim3(64), 0, s, a);
+}
 }  // namespace fsg

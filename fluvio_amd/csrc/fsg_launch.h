@@ -28,6 +28,12 @@ void launch_aggj_kid(const AggjArgs& a, uint64_t n_ent, hipStream_t s);
 void launch_aggj_rows(const AggjArgs& a, hipStream_t s);
 void launch_aggj_size(const AggjArgs& a, uint64_t* tsum, hipStream_t s);
 void launch_aggj_write(const AggjArgs& a, hipStream_t s);
+// stateful last stages (SfArgs): filter_look_back / filter_hashset
+void launch_sf_lb(const SfArgs& a, hipStream_t s);
+void launch_sf_dedup(const SfArgs& a, hipStream_t s);      // decisions assuming no eviction; scal[3] = kept
+void launch_sf_dedup_seq(const SfArgs& a, hipStream_t s);  // the sequential BoundedHashSet walk
+void launch_sf_compact(const SfArgs& a, hipStream_t s);
+void launch_sf_commit(const SfArgs& a, hipStream_t s);     // after k_plan: state through plan.done
 // device framing (FrameArgs)
 void launch_frame_cand(const FrameArgs& a, uint32_t nchunks, uint64_t* tsum, hipStream_t s);
 void launch_frame_compact(const FrameArgs& a, uint32_t nchunks, hipStream_t s);

@@ -360,6 +360,16 @@ struct ModuleSpec {
   int16_t version = 22;                       // DEFAULT_SMARTENGINE_VERSION
   bool has_acc = false;
   std::vector<uint8_t> acc;
+  int32_t lb_kind = FSG_LOOKBACK_NONE;        // SmartModuleConfig.lookback
+  uint64_t lb_last = 0, lb_age_ms = 0;
+};
+
+// state of a stateful last stage, shared by the chain and its look_back-mode twin
+struct SfState {
+  uint64_t limit = 0xFFFFFFFEull;  // filter_hashset: usize::MAX - 1 (wasm32)
+  uint64_t n_ent = 0, arena_len = 0, n = 0;
+  DevBuf prev;                     // filter_look_back: PREV (i32)
+  DevBuf ent_hash, ent_pos, ent_len, ent_last, arena;
 };
 
 }  // namespace
@@ -409,6 +419,13 @@ struct fsg_chain {
   DevBuf aj_bcnt, aj_brec, aj_rdesc, aj_rne, aj_rent, aj_rnew, aj_rnewb, aj_rlen, aj_roff, aj_ekid, aj_eval;
   DevBuf aj_sref, aj_sid, aj_state, aj_state2, aj_tsum;
   DevBuf rstart, rend;  // k_chase (lean path record starts)
+  // stateful last stage (filter_look_back / filter_hashset)
+  int sf_stage = -1;
+  std::shared_ptr<SfState> sf;
+  fsg_lookback lookback{FSG_LOOKBACK_NONE, 0, 0, 0};
+  std::unique_ptr<fsg_chain> lbc;  // the stage in look_back mode (same state)
+  DevBuf sf_bval, sf_bpre, sf_bn, sf_hv, sf_vref, sf_vlen, sf_slot, sf_keep, sf_idx, sf_sref, sf_first, sf_cur,
+      sf_scal;
   Plan hplan{};
   hipEvent_t ev[6] = {};
   fsg_timings last{};
@@ -478,6 +495,17 @@ extern "C" int fsg_chain_builder_add_smart_module(fsg_chain_builder* b, const fs
   return FSG_OK;
 }
 
+extern "C" int fsg_chain_builder_set_lookback(fsg_chain_builder* b, size_t module_index, int32_t kind, uint64_t last,
+                                              uint64_t age_ms) {
+  if (module_index >= b->mods.size()) return fail(FSG_E_INVALID_ARG, "no such module");
+  if (kind < FSG_LOOKBACK_NONE || kind > FSG_LOOKBACK_AGE) return fail(FSG_E_INVALID_ARG, "bad lookback kind");
+  ModuleSpec& m = b->mods[module_index];
+  m.lb_kind = kind;
+  m.lb_last = last;
+  m.lb_age_ms = age_ms;
+  return FSG_OK;
+}
+
 namespace {
 std::string init_error(const std::string& what) { return what + "\n\nSmartModule Init Error: \n"; }
 
@@ -486,6 +514,8 @@ int add_stage(fsg_chain* c, const ModuleSpec& m, const std::string& name, uint8_
   if (c->hdesc.nstages >= (uint32_t)kMaxStages) return fail(FSG_E_UNSUPPORTED, "chain longer than 8 stages");
   if (c->agg_stage >= 0) return fail(FSG_E_UNSUPPORTED, "stages after an aggregate are not implemented on the GPU");
   if (c->array_stage >= 0) return fail(FSG_E_UNSUPPORTED, "stages after an array_map are not implemented on the GPU");
+  if (c->sf_stage >= 0)
+    return fail(FSG_E_UNSUPPORTED, "stages after a stateful filter (look_back) are not implemented on the GPU");
   StageDesc sd{};
   sd.in_type = vt;
   auto param = [&](const char* k) -> const std::string* {
@@ -609,6 +639,35 @@ int add_stage(fsg_chain* c, const ModuleSpec& m, const std::string& name, uint8_
     sd.op = OP_ARRAY_MAP;
     sd.kind = FSG_KIND_ARRAY_MAP;
     c->array_stage = (int)c->hdesc.nstages;
+  } else if (name == "filter_look_back" || name == "filter_hashset") {
+    // examples/filter_look_back (keep > PREV) / filter_hashset (dedup, BoundedHashSet)
+    auto st = std::make_shared<SfState>();
+    if (name == "filter_hashset") {
+      const std::string* cnt = param("count");  // init: count.parse::<usize>()? (usize = u32 on wasm32)
+      if (cnt) {
+        const std::string& t = *cnt;
+        size_t i = (!t.empty() && t[0] == '+') ? 1 : 0;
+        uint64_t v = 0;
+        uint32_t kind = t.empty() ? 1 : (i == t.size() ? 2 : 0);
+        for (; !kind && i < t.size(); i++) {
+          if (t[i] < '0' || t[i] > '9') kind = 2;
+          else if ((v = v * 10 + (uint64_t)(t[i] - '0')) > 0xFFFFFFFFull) kind = 3;
+        }
+        if (kind) return fail(FSG_E_INIT, init_error(parse_hint(kind)));
+        st->limit = v;
+      }
+      if (vt == VT_I32) return fail(FSG_E_UNSUPPORTED, "filter_hashset after an integer map is not implemented on the GPU");
+      sd.op = OP_DEDUP;
+    } else {
+      sd.op = OP_LB_MAX;
+    }
+    sd.kind = FSG_KIND_FILTER;
+    c->sf_stage = (int)c->hdesc.nstages;
+    c->sf = st;
+    c->lookback.kind = m.lb_kind;
+    c->lookback.stage = c->hdesc.nstages;
+    c->lookback.last = m.lb_last;
+    c->lookback.age_ms = m.lb_age_ms;
   } else {
     return fail(FSG_E_UNKNOWN_SM, "No valid smartmodule found");
   }
@@ -643,6 +702,7 @@ extern "C" int fsg_chain_builder_initialize(fsg_chain_builder* b, fsg_engine* e,
                       : c->hdesc.st[c->agg_stage].op == OP_AGG_JSON ? CF_AGG_JSON
                                                                      : CF_AGG_CAT;
   if (c->array_stage >= 0) c->hdesc.flags |= CF_ARRAY;
+  if (c->sf_stage >= 0) c->hdesc.flags |= CF_STATEFUL;
   if (c->agg_stage >= 0) {
     StageDesc& sd = c->hdesc.st[c->agg_stage];
     uint32_t vut = 0, el = 0;
@@ -657,6 +717,10 @@ extern "C" int fsg_chain_builder_initialize(fsg_chain_builder* b, fsg_engine* e,
   if (c->hblob.empty()) c->hblob.resize(16, 0);
   HIPCHK(c->d_blob.ensure(c->hblob.size()));
   HIPCHK(hipMemcpy(c->d_blob.p, c->hblob.data(), c->hblob.size(), hipMemcpyHostToDevice));
+  if (c->sf) {  // filter_look_back: PREV starts at 0 (static AtomicI32::new(0))
+    HIPCHK(c->sf->prev.ensure(sizeof(int32_t)));
+    HIPCHK(hipMemset(c->sf->prev.p, 0, sizeof(int32_t)));
+  }
   if (c->hdesc.flags & CF_AGG_SUM) {  // the accumulator's i32 value, resident in HBM
     HIPCHK(c->dstate.ensure(sizeof(int32_t)));
     const int32_t a0 = acc_value(c->acc);
@@ -1094,6 +1158,117 @@ int build_error(fsg_chain* c, const fsg_slice* s, const BatchStat& st, fsg_runti
   return FSG_OK;
 }
 
+// grow a persistent device buffer keeping its first `used` bytes
+hipError_t grow_keep(DevBuf& b, size_t need, size_t used, hipStream_t st) {
+  if (need <= b.cap) return hipSuccess;
+  void* np = nullptr;
+  const size_t cap = std::max<size_t>(need + need / 2, 4096);
+  hipError_t e = hipMalloc(&np, cap);
+  if (e != hipSuccess) return e;
+  if (used) {
+    e = hipMemcpyAsync(np, b.p, used, hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+      (void)hipFree(np);
+      return e;
+    }
+  }
+  if (b.p) (void)hipFree(b.p);
+  b.p = np;
+  b.cap = cap;
+  return hipSuccess;
+}
+
+// the stateful last stage (k_sf_*): decisions in stream order over the batches
+// it ran on, descriptors compacted; the commit follows k_plan (sf_commit)
+int sf_run(fsg_chain* c, const fsg_slice* s, const EvalArgs& ea, SfArgs& sa, hipStream_t st) {
+  SfState& S = *c->sf;
+  const StageDesc& sd = c->hdesc.st[c->sf_stage];
+  const uint32_t nb = s->nb;
+  const size_t nr = std::max<uint64_t>(s->nrec, 1);
+  sa = SfArgs{};
+  sa.slice = ea.slice;
+  sa.bstat = ea.bstat;
+  sa.desc = ea.desc;
+  sa.rbase = ea.rbase;
+  sa.mins = ea.mins;
+  sa.plan = c->plan.as<Plan>();
+  sa.nbatches = nb;
+  sa.op = sd.op;
+  sa.lookback = sd.keep_match;
+  HIPCHK(c->sf_bval.ensure(std::max<uint32_t>(nb, 1) * 8));
+  HIPCHK(c->sf_bpre.ensure(std::max<uint32_t>(nb, 1) * 8));
+  sa.bval = c->sf_bval.as<int64_t>();
+  sa.bpre = c->sf_bpre.as<int64_t>();
+  sa.prev = S.prev.as<int32_t>();
+  if (sd.op == OP_LB_MAX) {
+    launch_sf_lb(sa, st);
+    return FSG_OK;
+  }
+  // filter_hashset: the table holds the entries and this call's records
+  uint32_t cap = 1024;
+  while (cap < 2 * (S.n_ent + s->nrec) + 16) cap <<= 1;
+  const size_t state = (size_t)(S.n_ent + s->nrec) * 28 + S.arena_len + s->len;
+  const size_t scratch = nr * 41 + (size_t)cap * 20 + (size_t)std::max<uint32_t>(nb, 1) * 20;
+  if (state + scratch > c->limit) {
+    char b[160];
+    snprintf(b, sizeof b, "Requested memory %zub exceeded max allowed %zub", state + scratch, c->limit);
+    g_store_mem[0] = (size_t)S.n_ent * 28 + S.arena_len;
+    g_store_mem[1] = state + scratch;
+    g_store_mem[2] = c->limit;
+    return fail(FSG_E_STORE_MEMORY, b);
+  }
+  HIPCHK(grow_keep(S.ent_hash, (S.n_ent + nr) * 8, S.n_ent * 8, st));
+  HIPCHK(grow_keep(S.ent_pos, (S.n_ent + nr) * 8, S.n_ent * 8, st));
+  HIPCHK(grow_keep(S.ent_len, (S.n_ent + nr) * 4, S.n_ent * 4, st));
+  HIPCHK(grow_keep(S.ent_last, (S.n_ent + nr) * 8, S.n_ent * 8, st));
+  HIPCHK(grow_keep(S.arena, S.arena_len + s->len + 64, S.arena_len, st));
+  HIPCHK(c->sf_bn.ensure(std::max<uint32_t>(nb, 1) * 4));
+  HIPCHK(c->sf_hv.ensure(nr * 8));
+  HIPCHK(c->sf_vref.ensure(nr * 8));
+  HIPCHK(c->sf_vlen.ensure(nr * 4));
+  HIPCHK(c->sf_slot.ensure(nr * 4));
+  HIPCHK(c->sf_keep.ensure(nr));
+  HIPCHK(c->sf_idx.ensure(nr * 8));
+  HIPCHK(c->sf_sref.ensure((size_t)cap * 8));
+  HIPCHK(c->sf_first.ensure((size_t)cap * 4));
+  HIPCHK(c->sf_cur.ensure((size_t)cap * 8));
+  HIPCHK(c->sf_scal.ensure(64));
+  sa.bn = c->sf_bn.as<uint32_t>();
+  sa.hv = c->sf_hv.as<uint64_t>();
+  sa.vref = c->sf_vref.as<uint64_t>();
+  sa.vlen = c->sf_vlen.as<uint32_t>();
+  sa.slot = c->sf_slot.as<uint32_t>();
+  sa.keep = c->sf_keep.as<uint8_t>();
+  sa.idx = c->sf_idx.as<uint64_t>();
+  sa.sref = c->sf_sref.as<unsigned long long>();
+  sa.first = c->sf_first.as<uint32_t>();
+  sa.cur = c->sf_cur.as<uint64_t>();
+  sa.cap = cap;
+  sa.ent_hash = S.ent_hash.as<uint64_t>();
+  sa.ent_pos = S.ent_pos.as<uint64_t>();
+  sa.ent_len = S.ent_len.as<uint32_t>();
+  sa.ent_last = S.ent_last.as<uint64_t>();
+  sa.arena = S.arena.as<uint8_t>();
+  sa.n_ent = S.n_ent;
+  sa.n0 = S.n;
+  sa.limit = S.limit;
+  sa.scal = c->sf_scal.as<unsigned long long>();
+  const unsigned long long sc0[4] = {S.n_ent, S.arena_len, S.n, 0};
+  HIPCHK(hipMemcpyAsync(sa.scal, sc0, sizeof sc0, hipMemcpyHostToDevice, st));
+  launch_sf_dedup(sa, st);
+  unsigned long long kept = 0;
+  HIPCHK(hipMemcpyAsync(&kept, sa.scal + 3, sizeof kept, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  // no value leaves the set during the call when the set (the newest `limit`
+  // insertions) has room for every insertion the parallel pass found
+  const uint64_t live = std::min<uint64_t>(S.n, S.limit);
+  sa.fast = live + kept <= S.limit ? 1u : 0u;
+  if (!sa.fast) launch_sf_dedup_seq(sa, st);
+  launch_sf_compact(sa, st);
+  return FSG_OK;
+}
+
 int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics* m, fsg_batch_output* res,
               bool empty_chain_io) {
   hipStream_t st = c->stream;
@@ -1176,6 +1351,14 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[1], st));
   launch_mins(ea.bstat, nb, ea.mins, st);
+  SfArgs sfa{};
+  const bool has_sf = (c->hdesc.flags & CF_STATEFUL) != 0;
+  if (has_sf) {  // stateful last stage: decide + compact, then the minima again (first surviving batch)
+    int rc = sf_run(c, s, ea, sfa, st);
+    if (rc) return rc;
+    HIPCHK(hipMemsetAsync(c->mins.p, 0xFF, sizeof(Mins), st));
+    launch_mins(ea.bstat, nb, ea.mins, st);
+  }
   // aggregate-json: fold the entries in stream order, size every record's map text
   AggjArgs aj{};
   AccMap am;
@@ -1354,10 +1537,19 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   pa.acc0 = acc0;
   launch_plan(pa, st);
   if (c->hdesc.flags & CF_AGG_SUM) launch_state(pa.plan, c->dstate.as<int32_t>(), st);
+  if (has_sf) launch_sf_commit(sfa, st);  // the stage's state through plan.done
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[2], st));
   HIPCHK(hipMemcpyAsync(&c->hplan, c->plan.p, sizeof(Plan), hipMemcpyDeviceToHost, st));
+  unsigned long long sfs[3] = {0, 0, 0};
+  const bool dedup = has_sf && sfa.op == OP_DEDUP && nb;
+  if (dedup) HIPCHK(hipMemcpyAsync(sfs, sfa.scal, sizeof sfs, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  if (dedup) {
+    c->sf->n_ent = sfs[0];
+    c->sf->arena_len = sfs[1];
+    c->sf->n = sfs[2];
+  }
   const Plan p = c->hplan;
   if (m) {
     m->bytes_in += p.bytes_in;
@@ -1573,10 +1765,73 @@ extern "C" int fsg_chain_process(fsg_chain* c, const uint8_t* raw, size_t len, i
   return FSG_OK;
 }
 
-extern "C" int fsg_chain_look_back(fsg_chain* c, fsg_metrics* m) {
-  (void)c;
-  (void)m;
-  return FSG_OK;  // no built-in GPU module has a look_back stage
+extern "C" void fsg_runtime_error_free(fsg_runtime_error* e) {
+  if (e) free_error(*e);
+}
+
+namespace {
+// the stateful stage alone, in look_back mode (StageDesc::keep_match = 1),
+// sharing the chain's state
+int make_lookback_chain(fsg_chain* c) {
+  if (c->lbc) return FSG_OK;
+  auto l = std::make_unique<fsg_chain>();
+  l->eng = c->eng;
+  l->limit = c->limit;
+  StageDesc sd = c->hdesc.st[c->sf_stage];
+  sd.in_type = VT_SRC;  // look_back reads the records themselves
+  sd.keep_match = 1;
+  l->hdesc.nstages = 1;
+  l->hdesc.st[0] = sd;
+  l->hdesc.out_type = VT_SRC;
+  l->hdesc.flags = CF_STATEFUL;
+  l->hblob = c->hblob;
+  l->names.push_back(c->names[c->sf_stage]);
+  l->sf_stage = 0;
+  l->sf = c->sf;
+  HIPCHK(hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking));
+  for (auto& ev : l->ev) HIPCHK(hipEventCreate(&ev));
+  HIPCHK(l->d_desc.ensure(sizeof(ChainDesc)));
+  HIPCHK(hipMemcpy(l->d_desc.p, &l->hdesc, sizeof(ChainDesc), hipMemcpyHostToDevice));
+  HIPCHK(l->d_blob.ensure(l->hblob.size()));
+  HIPCHK(hipMemcpy(l->d_blob.p, l->hblob.data(), l->hblob.size(), hipMemcpyHostToDevice));
+  c->lbc = std::move(l);
+  return FSG_OK;
+}
+}  // namespace
+
+// SmartModuleChainInstance::look_back (engine.rs:187-218): a stage with a
+// look_back export (instance.rs:92-95) and a Lookback gets read_fn's records as
+// one SmartModuleInput (try_from_records: base offset 0), metrics.add_bytes_in,
+// and its look_back over them (derive generator/look_back.rs: stops at the
+// first Err with SmartModuleLookbackRuntimeError).
+extern "C" int fsg_chain_look_back(fsg_chain* c, fsg_read_fn read_fn, void* user, fsg_metrics* m,
+                                   fsg_runtime_error* error) {
+  if (error) memset(error, 0, sizeof *error);
+  if (c->sf_stage < 0 || c->lookback.kind == FSG_LOOKBACK_NONE) return FSG_OK;
+  if (!read_fn) return fail(FSG_E_INVALID_ARG, "look_back needs a read_fn");
+  HIPCHK(hipSetDevice(c->eng->device));
+  const uint8_t* recs = nullptr;
+  size_t len = 0;
+  if (read_fn(user, &c->lookback, &recs, &len) != 0) return fail(FSG_E_IO, "look_back read_fn failed");
+  if (m) {
+    m->bytes_in += len;
+    m->invocation_count += 1;
+  }
+  int rc = make_lookback_chain(c);
+  if (rc) return rc;
+  fsg_output* o = nullptr;
+  rc = fsg_chain_process(c->lbc.get(), recs, len, 0, -1, nullptr, &o);
+  if (rc) return rc;
+  if (o->has_error) {
+    if (error) {
+      *error = o->error;
+      memset(&o->error, 0, sizeof o->error);
+    }
+    fsg_output_free(o);
+    return fail(FSG_E_LOOKBACK, "look_back: SmartModule Lookback Error");
+  }
+  fsg_output_free(o);
+  return FSG_OK;
 }
 
 extern "C" int fsg_chain_get_accumulator(fsg_chain* c, size_t stage, uint8_t** acc, size_t* len) {

@@ -126,6 +126,41 @@ class SmartModuleInitialData:
         return SmartModuleInitialData(bytes(accumulator))
 
 
+@dataclass(frozen=True)
+class Lookback:
+    """Lookback (fluvio-smartengine engine/config.rs:45-49): Last(n) or Age{age, last}."""
+    last: int
+    age_ms: Optional[int] = None
+
+    @staticmethod
+    def Last(n: int) -> "Lookback":  # noqa: N802 (the reference's variant name)
+        return Lookback(n)
+
+    @staticmethod
+    def Age(age_ms: int, last: int) -> "Lookback":  # noqa: N802
+        return Lookback(last, age_ms)
+
+
+@dataclass
+class SmartModuleLookbackRuntimeError(Exception):
+    """SmartModuleLookbackRuntimeError (fluvio-protocol link/smartmodule.rs:150-176)."""
+    hint: str
+    offset: int
+    record_key: Optional[bytes]
+    record_value: bytes
+
+    def __str__(self) -> str:
+        def disp(b: Optional[bytes]) -> str:
+            if b is None:
+                return "NULL"
+            try:
+                return b.decode("utf-8")
+            except UnicodeDecodeError:
+                return f"Binary: {len(b)} bytes"
+        return (f"{self.hint}\n\nSmartModule Lookback Error: \n    Offset: {self.offset}\n"
+                f"    Key: {disp(self.record_key)}\n    Value: {disp(self.record_value)}")
+
+
 @dataclass
 class SmartModuleConfig:
     params: Dict[str, str] = field(default_factory=dict)
@@ -366,7 +401,7 @@ class SmartModuleChainBuilder:
         _check(L.fsg_chain_builder_new(ctypes.byref(b)))
         if self._limit is not None:
             L.fsg_chain_builder_set_store_memory_limit(b, self._limit)
-        for cfg, module in self._mods:
+        for idx, (cfg, module) in enumerate(self._mods):
             items = list(cfg.params.items())
             arr = (_ffi.fsg_param * max(1, len(items)))()
             for i, (k, v) in enumerate(items):
@@ -376,6 +411,10 @@ class SmartModuleChainBuilder:
             _check(L.fsg_chain_builder_add_smart_module(
                 b, arr, len(items), cfg.get_version(), acc or b"", len(acc or b""), 1 if acc is not None else 0,
                 module, len(module)))
+            lb = cfg.lookback
+            if lb is not None:
+                kind = _ffi.FSG_LOOKBACK_LAST if lb.age_ms is None else _ffi.FSG_LOOKBACK_AGE
+                _check(L.fsg_chain_builder_set_lookback(b, idx, kind, lb.last, lb.age_ms or 0))
         c = ctypes.c_void_p()
         _check(L.fsg_chain_builder_initialize(b, engine._h, ctypes.byref(c)))  # consumes the builder
         return SmartModuleChainInstance(c, engine, len(self._mods))
@@ -403,7 +442,34 @@ class SmartModuleChainInstance:
             _ffi.lib().fsg_output_free(out)
 
     def look_back(self, read_fn: Callable, metrics: Optional[SmartModuleChainMetrics] = None) -> None:
-        _check(_ffi.lib().fsg_chain_look_back(self._h, ctypes.byref(metrics._m) if metrics else None))
+        """SmartModuleChainInstance::look_back (engine.rs:187-218): read_fn(Lookback)
+        returns the records (a list of Record, or an encoded Vec<Record>) the
+        stage's look_back runs over; a record error raises
+        SmartModuleLookbackRuntimeError."""
+        keep = []
+
+        def _read(user, lbp, recs, ln):
+            try:
+                lb = lbp.contents
+                got = read_fn(Lookback(lb.last, None if lb.kind == _ffi.FSG_LOOKBACK_LAST else lb.age_ms))
+                raw = got if isinstance(got, (bytes, bytearray)) else encode_records(list(got))
+                buf = ctypes.create_string_buffer(bytes(raw), max(1, len(raw)))
+                keep.append(buf)
+                recs[0] = ctypes.cast(buf, ctypes.c_void_p)
+                ln[0] = len(raw)
+                return 0
+            except Exception:  # noqa: BLE001 (the read failed: io::Error for look_back)
+                return 1
+
+        cb = _ffi.READ_FN(_read)
+        err = _ffi.fsg_runtime_error()
+        rc = _ffi.lib().fsg_chain_look_back(self._h, cb, None, ctypes.byref(metrics._m) if metrics else None,
+                                            ctypes.byref(err))
+        if rc == _ffi.FSG_E_LOOKBACK:
+            e = _runtime_error(err)
+            _ffi.lib().fsg_runtime_error_free(ctypes.byref(err))
+            raise SmartModuleLookbackRuntimeError(e.hint, e.offset, e.record_key, e.record_value)
+        _check(rc)
 
     def accumulator(self, stage: int) -> bytes:
         p = ctypes.POINTER(ctypes.c_uint8)()

@@ -16,6 +16,8 @@
  *                                         (+ create_transform, transforms/mod.rs:24-52)
  *   fsg_chain_process                   SmartModuleChainInstance::process           engine.rs:135-185
  *   fsg_chain_look_back                 SmartModuleChainInstance::look_back         engine.rs:187-218
+ *                                         (read_fn = the SPU's read_records, smartengine/context.rs:46-60,117-160)
+ *   fsg_chain_builder_set_lookback      SmartModuleConfigBuilder::lookback          config.rs:45-73
  *   fsg_chain_process_batch             fluvio-spu process_batch                    crates/fluvio-spu/src/smartengine/batch.rs:41-142
  *                                         over a FileBatchIterator slice           crates/fluvio-storage/src/iterators.rs:55-160
  *   fsg_chain_get_accumulator           SmartModuleAggregate accumulator            transforms/aggregate.rs:22-25,95
@@ -55,7 +57,7 @@
 extern "C" {
 #endif
 
-#define FSG_ABI_VERSION 2
+#define FSG_ABI_VERSION 3
 
 /* ---- status codes (mirror EngineError and the guest status enums) ---- */
 #define FSG_OK 0
@@ -70,6 +72,7 @@ extern "C" {
 #define FSG_E_UNSUPPORTED -103       /* valid for the reference, not implemented on the GPU path */
 #define FSG_E_IO -104                /* io::Error from batch framing / empty-chain record decode */
 #define FSG_E_INVALID_ARG -105
+#define FSG_E_LOOKBACK -106          /* Err(SmartModuleLookbackRuntimeError) from look_back (link/smartmodule.rs:150-176) */
 #define FSG_E_DEVICE -200            /* HIP runtime failure / no device */
 
 /* SmartModuleKind tags (link/smartmodule.rs:80-95) */
@@ -78,6 +81,11 @@ extern "C" {
 #define FSG_KIND_ARRAY_MAP 2
 #define FSG_KIND_AGGREGATE 3
 #define FSG_KIND_FILTER_MAP 4
+
+/* Lookback (config.rs:45-49): Last(n) / Age{age, last} */
+#define FSG_LOOKBACK_NONE 0
+#define FSG_LOOKBACK_LAST 1
+#define FSG_LOOKBACK_AGE 2
 
 typedef struct fsg_engine fsg_engine;
 typedef struct fsg_chain_builder fsg_chain_builder;
@@ -116,6 +124,18 @@ typedef struct fsg_output {
   int32_t has_error;
   fsg_runtime_error error;
 } fsg_output;
+
+/* the Lookback a stage asks its look_back records for */
+typedef struct fsg_lookback {
+  int32_t kind;    /* FSG_LOOKBACK_LAST / FSG_LOOKBACK_AGE */
+  uint32_t stage;  /* chain position of the stage */
+  uint64_t last;
+  uint64_t age_ms;
+} fsg_lookback;
+/* look_back's read_fn: the records to feed (encoded Vec<Record>: u32 BE count +
+ * records), valid until read_fn is called again or look_back returns; nonzero
+ * return = the read failed (look_back returns FSG_E_IO) */
+typedef int (*fsg_read_fn)(void *user, const fsg_lookback *lb, const uint8_t **records, size_t *len);
 
 /* (Batch, Option<SmartModuleTransformRuntimeError>) returned by SPU process_batch.
  * `batch` is the file-format encoding (12-byte preamble + 45-byte header + u32
@@ -162,6 +182,9 @@ int fsg_chain_builder_set_store_memory_limit(fsg_chain_builder *b, size_t max_me
 int fsg_chain_builder_add_smart_module(fsg_chain_builder *b, const fsg_param *params, size_t n_params,
                                        int16_t version, const uint8_t *initial_acc, size_t acc_len,
                                        int32_t has_initial_acc, const uint8_t *module, size_t module_len);
+/* SmartModuleConfig.lookback of the module added `module_index`-th (0-based) */
+int fsg_chain_builder_set_lookback(fsg_chain_builder *b, size_t module_index, int32_t kind, uint64_t last,
+                                   uint64_t age_ms);
 /* consumes the builder (initialize(self)) whether or not it succeeds */
 int fsg_chain_builder_initialize(fsg_chain_builder *b, fsg_engine *engine, fsg_chain **out);
 void fsg_chain_builder_free(fsg_chain_builder *b);
@@ -171,7 +194,14 @@ int fsg_chain_process(fsg_chain *c, const uint8_t *raw_records, size_t len, int6
                       int64_t base_timestamp, fsg_metrics *metrics, fsg_output **out);
 int fsg_chain_process_batch(fsg_chain *c, const uint8_t *slice, size_t len, uint64_t max_bytes,
                             fsg_metrics *metrics, fsg_batch_output **out);
-int fsg_chain_look_back(fsg_chain *c, fsg_metrics *metrics); /* no look_back stages: Ok */
+/* look_back (engine.rs:187-218): for every stage with a look_back function
+ * (filter_look_back, filter_hashset) and a Lookback, read_fn gives the records and
+ * the stage's look_back runs over them on the GPU (metrics: bytes_in + one
+ * invocation per stage).  A record error returns FSG_E_LOOKBACK with *error set
+ * (free with fsg_runtime_error_free); no such stage: Ok without calling read_fn. */
+int fsg_chain_look_back(fsg_chain *c, fsg_read_fn read_fn, void *user, fsg_metrics *metrics,
+                        fsg_runtime_error *error);
+void fsg_runtime_error_free(fsg_runtime_error *e);
 int fsg_chain_get_accumulator(fsg_chain *c, size_t stage, uint8_t **acc, size_t *len);
 /* aggregate-json (C5 keyed): the accumulator's (key fingerprint, u32 value)
  * pairs for a cross-partition merge (FNV-1a 64 of each key's bytes) into device

@@ -1117,7 +1117,30 @@ enum {
   M_ARRAY_MAP,   /* examples/array_map_json_array: explode a JSON array */
   M_PROJECT,     /* map_json_project: the value of one JSON field (C3 projection) */
   M_AGG_JSON,    /* examples/aggregate-json: HashMap<String, u32> += per key (C5 keyed) */
+  M_FILTER_LOOKBACK, /* examples/filter_look_back: keep i32 values above the last kept (look_back sets it) */
+  M_FILTER_HASHSET,  /* examples/filter_hashset: dedup over a BoundedHashSet<String> (look_back inserts) */
 };
+
+/* examples/filter_hashset/src/lib.rs:46-80 BoundedHashSet<String>: BTreeMap<value,
+ * seq>, seq = seq.saturating_add(1) per insert (usize = u32 on wasm32), a vacant
+ * value is inserted with the current seq, and when len > limit the entry with the
+ * smallest seq is removed.  Entries are only ever removed that way and keep the
+ * seq of their insertion, so the min-seq entry is the oldest live insertion: the
+ * restatement keeps the live entries in insertion order (a FIFO) with a chained
+ * hash index for the lookups. */
+typedef struct {
+  uint8_t *b;
+  size_t n;
+  uint32_t seq;
+  int64_t next; /* bucket chain */
+} bhs_ent;
+typedef struct {
+  bhs_ent *e;
+  size_t ne, cap, head; /* live entries: [head, ne) */
+  int64_t *bucket;
+  size_t nbucket;
+  uint32_t limit, seq;
+} bhs_t;
 
 typedef struct {
   int mod;
@@ -1128,7 +1151,93 @@ typedef struct {
   int rx_keep_match;
   uint8_t *acc; /* aggregate accumulator */
   size_t acc_len;
+  int32_t prev; /* filter_look_back: static PREV (AtomicI32, starts at 0) */
+  bhs_t *set;   /* filter_hashset: static SET */
 } stage_t;
+
+static uint64_t bhs_hash(const uint8_t *b, size_t n) {
+  uint64_t h = 1469598103934665603ull;
+  for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
+  return h;
+}
+static void bhs_free(bhs_t *s) {
+  if (!s) return;
+  for (size_t i = s->head; i < s->ne; i++) free(s->e[i].b);
+  free(s->e);
+  free(s->bucket);
+  free(s);
+}
+static void bhs_rebuild(bhs_t *s, size_t nb) {
+  free(s->bucket);
+  s->nbucket = nb;
+  s->bucket = (int64_t *)malloc(nb * sizeof(int64_t));
+  for (size_t i = 0; i < nb; i++) s->bucket[i] = -1;
+  for (size_t i = s->head; i < s->ne; i++) {
+    size_t k = bhs_hash(s->e[i].b, s->e[i].n) & (nb - 1);
+    s->e[i].next = s->bucket[k];
+    s->bucket[k] = (int64_t)i;
+  }
+}
+/* BoundedHashSet::insert: true when the value was vacant */
+static int bhs_insert(bhs_t *s, const uint8_t *b, size_t n) {
+  s->seq = s->seq == 0xFFFFFFFFu ? s->seq : s->seq + 1; /* saturating_add */
+  if (!s->bucket) bhs_rebuild(s, 1024);
+  size_t k = bhs_hash(b, n) & (s->nbucket - 1);
+  for (int64_t i = s->bucket[k]; i >= 0; i = s->e[i].next)
+    if (s->e[i].n == n && !memcmp(s->e[i].b, b, n)) return 0; /* Occupied */
+  if (s->ne == s->cap) {
+    /* compact the evicted prefix away before growing */
+    size_t live = s->ne - s->head;
+    if (s->head > live) {
+      memmove(s->e, s->e + s->head, live * sizeof(bhs_ent));
+      s->ne = live;
+      s->head = 0;
+    } else {
+      s->cap = s->cap ? 2 * s->cap : 1024;
+      s->e = (bhs_ent *)realloc(s->e, s->cap * sizeof(bhs_ent));
+    }
+    bhs_rebuild(s, s->nbucket);
+  }
+  bhs_ent ne;
+  ne.b = dup_bytes(b, n);
+  ne.n = n;
+  ne.seq = s->seq;
+  s->e[s->ne] = ne;
+  s->ne++;
+  if ((s->ne - s->head) > 2 * s->nbucket) bhs_rebuild(s, 4 * s->nbucket);
+  else {
+    s->e[s->ne - 1].next = s->bucket[k];
+    s->bucket[k] = (int64_t)(s->ne - 1);
+  }
+  if ((uint64_t)(s->ne - s->head) > (uint64_t)s->limit) { /* remove_first: the smallest seq */
+    bhs_ent *h = &s->e[s->head];
+    size_t hk = bhs_hash(h->b, h->n) & (s->nbucket - 1);
+    int64_t *pp = &s->bucket[hk];
+    while (*pp != (int64_t)s->head) pp = &s->e[*pp].next;
+    *pp = h->next;
+    free(h->b);
+    h->b = NULL;
+    s->head++;
+  }
+  return 1;
+}
+/* usize::from_str on wasm32 (u32): optional '+', digits; 0 ok, else ParseIntError kind */
+static int parse_u32(const char *t, uint32_t *out) {
+  size_t n = strlen(t), i = 0;
+  if (n == 0) return 1;
+  if (t[0] == '+') {
+    i = 1;
+    if (n == 1) return 2;
+  }
+  uint64_t acc = 0;
+  for (; i < n; i++) {
+    if (t[i] < '0' || t[i] > '9') return 2;
+    acc = acc * 10 + (uint64_t)(t[i] - '0');
+    if (acc > 0xFFFFFFFFull) return 3;
+  }
+  *out = (uint32_t)acc;
+  return 0;
+}
 
 struct orc_chain {
   stage_t *st;
@@ -1141,6 +1250,7 @@ void orc_chain_free(orc_chain *c) {
   for (size_t i = 0; i < c->n; i++) {
     free(c->st[i].needle);
     free(c->st[i].acc);
+    bhs_free(c->st[i].set);
     rxprog_free(&c->st[i].rx);
   }
   free(c->st);
@@ -1239,6 +1349,24 @@ int orc_chain_add(orc_chain *c, const char *module, const char **keys, const cha
     s.needle_len = strlen(v);
     s.needle = dup_bytes((const uint8_t *)v, s.needle_len + 1);
     s.needle[s.needle_len] = 0;
+  } else if (!strcmp(module, "filter_look_back")) {
+    s.mod = M_FILTER_LOOKBACK;
+    s.kind = K_FILTER;
+  } else if (!strcmp(module, "filter_hashset")) {
+    /* init: count = params.get("count").parse()? else usize::MAX - 1 (lib.rs:28-37) */
+    uint32_t limit = 0xFFFFFFFEu;
+    v = param_get(keys, vals, n_params, "count");
+    if (v) {
+      int pk = parse_u32(v, &limit);
+      if (pk) {
+        if (msg_out) *msg_out = fmt_str("%s\n\nSmartModule Init Error: \n", parse_int_hint(pk));
+        return ORC_E_INIT;
+      }
+    }
+    s.mod = M_FILTER_HASHSET;
+    s.kind = K_FILTER;
+    s.set = (bhs_t *)calloc(1, sizeof(bhs_t));
+    s.set->limit = limit;
   } else {
     return ORC_E_UNKNOWN_SM;
   }
@@ -1489,6 +1617,28 @@ static void stage_run(stage_t *s, recvec *in, int64_t base_offset, stage_out *o)
         }
         break;
       }
+      case M_FILTER_LOOKBACK: { /* filter_look_back/src/lib.rs:7-18 */
+        if (!utf8_check(r->val, r->val_len, &vut, &el)) {
+          hint = utf8_hint(vut, el);
+          break;
+        }
+        int32_t x;
+        int pk = parse_i32(r->val, r->val_len, &x);
+        if (pk) {
+          hint = dup_str(parse_int_hint(pk));
+          break;
+        }
+        keep = x > s->prev;
+        if (keep) s->prev = x;
+        break;
+      }
+      case M_FILTER_HASHSET: /* filter_hashset/src/lib.rs:15-19: SET.insert(value.to_owned()) */
+        if (!utf8_check(r->val, r->val_len, &vut, &el)) {
+          hint = utf8_hint(vut, el);
+          break;
+        }
+        keep = bhs_insert(s->set, r->val, r->val_len);
+        break;
       case M_MAP_UPPER:
         outr = rec_clone(r);
         for (size_t k = 0; k < outr.val_len; k++)
@@ -1825,6 +1975,56 @@ int orc_process_batch(orc_chain *c, const uint8_t *slice, size_t slice_len, uint
   out->base_offset = sm_base;
   out->last_offset_delta = sm_lod;
   rv_free(&acc);
+  return 0;
+}
+
+/* SmartModuleChainInstance::look_back (engine.rs:187-218) for one stage: the
+ * records read_fn returned (SmartModuleInput::try_from_records: base offset 0)
+ * through the module's look_back (derive generator/look_back.rs: the first Err
+ * stops with SmartModuleLookbackRuntimeError{hint, offset = base + offset_delta,
+ * key, value}).  Stages without a look_back export are skipped (instance.rs:92-95). */
+int orc_chain_look_back(orc_chain *c, size_t stage, const uint8_t *raw, size_t raw_len, orc_result *out) {
+  memset(out, 0, sizeof *out);
+  if (stage >= c->n) return ORC_E_INVALID_ARG;
+  stage_t *s = &c->st[stage];
+  if (s->mod != M_FILTER_LOOKBACK && s->mod != M_FILTER_HASHSET) return 0;
+  out->m_bytes_in = raw_len; /* metrics.add_bytes_in: bytes + one invocation */
+  out->m_invocations = 1;
+  recvec rv;
+  if (recs_decode(raw, raw_len, &rv)) {
+    out->status = ORC_E_DECODING_BASE_INPUT;
+    return out->status;
+  }
+  for (size_t i = 0; i < rv.n; i++) {
+    rec_t *r = &rv.r[i];
+    size_t vut;
+    int el;
+    char *hint = NULL;
+    if (!utf8_check(r->val, r->val_len, &vut, &el)) {
+      hint = utf8_hint(vut, el);
+    } else if (s->mod == M_FILTER_LOOKBACK) { /* filter_look_back/src/lib.rs:20-26: PREV = parse()? */
+      int32_t x;
+      int pk = parse_i32(r->val, r->val_len, &x);
+      if (pk) hint = dup_str(parse_int_hint(pk));
+      else s->prev = x;
+    } else {
+      (void)bhs_insert(s->set, r->val, r->val_len); /* filter_hashset/src/lib.rs:21-26 */
+    }
+    if (hint) {
+      out->has_error = 1;
+      out->hint = hint;
+      out->hint_len = strlen(hint);
+      out->err_offset = r->off_delta; /* base_offset 0 */
+      out->has_key = r->has_key;
+      out->key = r->key;
+      out->key_len = r->key_len;
+      out->value = r->val;
+      out->value_len = r->val_len;
+      r->key = r->val = NULL;
+      break;
+    }
+  }
+  rv_free(&rv);
   return 0;
 }
 

@@ -78,6 +78,9 @@ int orc_chain_process(orc_chain *c, const uint8_t *raw, size_t raw_len, int64_t 
 int orc_process_batch(orc_chain *c, const uint8_t *slice, size_t slice_len, uint64_t max_bytes,
                       orc_result *out);
 int orc_chain_accumulator(orc_chain *c, size_t stage, uint8_t **acc, size_t *len);
+/* SmartModuleChainInstance::look_back for one stage: out->has_error carries the
+ * SmartModuleLookbackRuntimeError (hint, err_offset, key, value) */
+int orc_chain_look_back(orc_chain *c, size_t stage, const uint8_t *raw, size_t raw_len, orc_result *out);
 void orc_result_free(orc_result *r);
 void orc_free(void *p);
 

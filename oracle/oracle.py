@@ -66,6 +66,8 @@ def lib():
         L.orc_chain_accumulator.argtypes = [ctypes.c_void_p, ctypes.c_size_t,
                                             ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
                                             ctypes.POINTER(ctypes.c_size_t)]
+        L.orc_chain_look_back.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                                          ctypes.POINTER(_Result)]
         L.orc_result_free.argtypes = [ctypes.POINTER(_Result)]
         L.orc_free.argtypes = [ctypes.c_void_p]
         L.orc_regex_is_match.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t,
@@ -247,6 +249,16 @@ class OracleChain:
     def process_batch(self, slice_bytes: bytes, max_bytes: int = (1 << 64) - 1) -> Dict:
         r = _Result()
         lib().orc_process_batch(self._h, slice_bytes, len(slice_bytes), max_bytes, ctypes.byref(r))
+        try:
+            return _take(r)
+        finally:
+            lib().orc_result_free(ctypes.byref(r))
+
+    def look_back(self, stage: int, raw: bytes) -> Dict:
+        """look_back of one stage over encoded records (Vec<Record>); "error" is the
+        SmartModuleLookbackRuntimeError (hint, offset, key, value)."""
+        r = _Result()
+        lib().orc_chain_look_back(self._h, stage, raw, len(raw), ctypes.byref(r))
         try:
             return _take(r)
         finally:

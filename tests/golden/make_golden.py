@@ -225,6 +225,69 @@ def main():
          "expect": 'string "1aoeu"', "match": "contains"},
     ]
 
+    # stateful filters with look_back (f4).  A "chain" step list runs on one
+    # chain instance: look_back over the given records (Lookback::Last(n) read by
+    # the SPU from the replica's last n records), process of one input, or
+    # "new_chain" (the SPU builds a new SmartModuleContext per produce request /
+    # stream, and a recreated replica re-runs look_back).
+    lb = []
+    lb.append({"name": "chain_filter_look_back",
+               "source": "crates/fluvio-smartengine/src/engine/wasmtime/engine.rs:388-428",
+               "module": ["filter_look_back", {}], "lookback": ["last", 1, 0],
+               "steps": [{"look_back": ["2"]}, {"process": ["1", "2", "3"], "expect": ["3"]}],
+               "invocation_count": 2})
+    lb.append({"name": "chain_filter_look_back_error_propagated",
+               "source": "crates/fluvio-smartengine/src/engine/wasmtime/engine.rs:433-470",
+               "module": ["filter_look_back", {}], "lookback": ["last", 1, 0],
+               "steps": [{"look_back": ["wrong str"],
+                          "error": {"hint": "invalid digit found in string", "offset": 0, "key": None,
+                                    "value": "wrong str"}}],
+               "invocation_count": 1})
+    lb.append({"name": "bounded_hash_set",
+               "source": "smartmodule/examples/filter_hashset/src/lib.rs:83-104 (test_set, limit 3)",
+               "module": ["filter_hashset", {"count": "3"}], "lookback": None,
+               "steps": [{"process": ["1", "3", "2", "3", "1", "5", "1"], "expect": ["1", "3", "2", "5", "1"]}]})
+    # produce.rs:522-700: a chain per produce request, look_back over the replica's last record
+    stored = []
+    steps = []
+    for vals, last, exp in [(["1", "2", "3"], 1, ["1", "2", "3"]), (["1", "2", "3", "4", "5"], 1, ["4", "5"]),
+                            (["1", "2"], 0, ["1", "2"]), (["1", "2"], None, ["1", "2"])]:
+        steps.append({"new_chain": None if last is None else ["last", last, 0]})
+        if last is not None:
+            steps.append({"look_back": stored[len(stored) - last:] if last else []})
+        steps.append({"process": vals, "expect": exp})
+        stored += exp
+    assert stored == ["1", "2", "3", "4", "5", "1", "2", "1", "2"]  # produce.rs:656-700
+    lb.append({"name": "produce_basic_with_lookback",
+               "source": "crates/fluvio-spu/src/services/public/tests/produce.rs:522-700",
+               "module": ["filter_look_back", {}], "lookback": ["last", 1, 0], "steps": steps})
+    # produce.rs:840-1020: dedup (filter_hashset, count 6, Lookback::Last(6)) built once per
+    # replica with look_back at init (replica_state.rs:391-406); the replica is recreated once
+    stored = []
+    steps = [{"look_back": []}]
+    for vals, exp in [(["1", "2", "3", "1"], ["1", "2", "3"]), (["1", "2", "4", "5", "6"], ["4", "5", "6"]),
+                      (["7", "1", "2"], ["7", "1", "2"])]:
+        steps.append({"process": vals, "expect": exp})
+        stored += exp
+    steps.append({"new_chain": ["last", 6, 0]})
+    steps.append({"look_back": stored[-6:]})
+    steps.append({"process": ["7", "8"], "expect": ["8"]})
+    stored += ["8"]
+    assert stored == ["1", "2", "3", "4", "5", "6", "7", "1", "2", "8"]  # produce.rs:1014-1018
+    lb.append({"name": "produce_with_deduplication",
+               "source": "crates/fluvio-spu/src/services/public/tests/produce.rs:840-1020",
+               "module": ["filter_hashset", {"count": "6"}], "lookback": ["last", 6, 0], "steps": steps})
+    # stream_fetch.rs:2483-2605: a stream per fetch, look_back over the last record
+    steps = [{"look_back": ["3"]}, {"process": ["1", "10", "2", "11", "3"], "expect": ["10", "11"]},
+             {"new_chain": ["last", 1, 0]}, {"look_back": ["13"]},
+             {"process": ["1", "10", "2", "11", "3", "10", "14", "13"], "expect": ["14"]},
+             {"new_chain": ["last", 0, 0]}, {"look_back": []},
+             {"process": ["1", "10", "2", "11", "3", "10", "14", "13"], "expect": ["1", "10", "11", "14"]}]
+    lb.append({"name": "stream_fetch_filter_lookback",
+               "source": "crates/fluvio-spu/src/services/public/tests/stream_fetch.rs:2483-2605",
+               "module": ["filter_look_back", {}], "lookback": ["last", 1, 0], "steps": steps})
+    k["look_back"] = lb
+
     with open(OUT, "w") as f:
         json.dump(k, f, indent=1, sort_keys=True)
     print("wrote", OUT)

@@ -921,3 +921,143 @@ def test_aggregate_json_process_kat(engine):
     assert [r.value for r in out.successes] == [r.value for r in P.decode_records(ref["bytes"])]
     assert out.successes[-1].value == b'{\n  "a": 4,\n  "b": 2,\n  "c": 7\n}'
     assert g.accumulator(0) == o.accumulator(0)
+
+
+# ---------------------------------------------------------------------------
+# stateful filters with look_back: filter_look_back (keep above
+# PREV) and filter_hashset (dedup over a BoundedHashSet), last stage of a chain
+# ---------------------------------------------------------------------------
+def test_look_back_kats(engine, kats):
+    """engine.rs:388-470, filter_hashset test_set, SPU produce.rs:522-1020 (a
+    chain per produce request / per replica), stream_fetch.rs:2483-2605."""
+    from fluvio_amd.smartengine import Lookback, SmartModuleLookbackRuntimeError
+    from tests.lookback_steps import run_lookback_case
+
+    for case in kats["look_back"]:
+        name, params = case["module"]
+
+        def new_chain(lb, name=name, params=params):
+            b = SmartModuleChainBuilder.default()
+            cb = SmartModuleConfig.builder().params(params)
+            if lb:
+                cb.lookback(Lookback.Last(lb[1]) if lb[0] == "last" else Lookback.Age(lb[2], lb[1]))
+            b.add_smart_module(cb.build(), builtin(name))
+            return b.initialize(engine), SmartModuleChainMetrics()
+
+        def look_back(ch, values):
+            chain, m = ch
+            before = m.invocation_count()
+            seen = []
+            try:
+                chain.look_back(lambda lb: seen.append(lb) or [P.Record.new(v) for v in values], m)
+                err = None
+            except SmartModuleLookbackRuntimeError as e:
+                err = {"hint": e.hint, "offset": e.offset, "key": e.record_key, "value": e.record_value}
+            assert len(seen) == 1  # read_fn is asked once, for the stage's Lookback
+            return err, m.invocation_count() - before
+
+        def process(ch, values):
+            chain, m = ch
+            before = m.invocation_count()
+            out = chain.process(SmartModuleInput.try_from_records([P.Record.new(v) for v in values]), m)
+            assert out.error is None
+            return [r.value for r in out.successes], m.invocation_count() - before
+
+        run_lookback_case(case, new_chain, look_back, process)
+
+
+def test_look_back_not_configured(engine):
+    """No Lookback on the config, or a module without look_back: read_fn is never called."""
+    from fluvio_amd.smartengine import Lookback
+    for mods, lb in (([("filter_hashset", {}, None)], None), ([("filter", {}, None)], Lookback.Last(3))):
+        b = SmartModuleChainBuilder.default()
+        cb = SmartModuleConfig.builder().params(mods[0][1])
+        if lb:
+            cb.lookback(lb)
+        b.add_smart_module(cb.build(), builtin(mods[0][0]))
+        ch = b.initialize(engine)
+        m = SmartModuleChainMetrics()
+        ch.look_back(lambda _lb: pytest.fail("read_fn called"), m)
+        assert m.invocation_count() == 0 and m.bytes_in() == 0
+
+
+SF_CHAINS = {
+    "look_back": [("filter_look_back", {}, None)],
+    "map_double_look_back": [("map_double", {}, None), ("filter_look_back", {}, None)],
+    "dedup": [("filter_hashset", {}, None)],
+    "dedup_evicting": [("filter_hashset", {"count": "40"}, None)],
+    "dedup_zero": [("filter_hashset", {"count": "0"}, None)],
+    "map_dedup": [("map", {}, None), ("filter_hashset", {"count": "500"}, None)],
+    "filter_dedup": [("filter_with_param", {"key": "1"}, None), ("filter_hashset", {}, None)],
+}
+
+
+def check_sequence(engine, modules, calls, look_back=None):
+    """One GPU chain and one oracle chain through a sequence of process_batch
+    calls [(slice, max_bytes)], optionally after a look_back over `look_back`
+    (encoded records), compared call by call."""
+    from fluvio_amd.smartengine import Lookback, SmartModuleLookbackRuntimeError
+    b = SmartModuleChainBuilder.default()
+    for i, (name, params, acc) in enumerate(modules):
+        cb = SmartModuleConfig.builder().params(params or {})
+        if look_back is not None and i == len(modules) - 1:
+            cb.lookback(Lookback.Last(1000))
+        b.add_smart_module(cb.build(), builtin(name))
+    g = b.initialize(engine)
+    o = orc_chain(modules)
+    if look_back is not None:
+        ol = o.look_back(len(modules) - 1, look_back)
+        try:
+            g.look_back(lambda _lb: look_back)
+            assert ol["error"] is None
+        except SmartModuleLookbackRuntimeError as e:
+            oe = ol["error"]
+            assert oe is not None
+            assert (e.hint, e.offset, e.record_key, e.record_value) == (oe["hint"], oe["offset"], oe["key"],
+                                                                         oe["value"])
+    for sl, max_bytes in calls:
+        gm = SmartModuleChainMetrics()
+        oout = o.process_batch(sl, max_bytes)
+        if oout["status"] != 0:
+            with pytest.raises(Exception):
+                g.process_batch(sl, max_bytes, gm)
+            continue
+        gout = g.process_batch(sl, max_bytes, gm)
+        assert gout.raw == oout["bytes"], "output batch bytes differ"
+        assert gout.n_records == oout["n_records"]
+        assert_same_error(gout.error, oout["error"])
+        assert gm.records_out() == oout["metrics"]["records_out"]
+        assert gm.bytes_in() == oout["metrics"]["bytes_in"]
+
+
+@pytest.mark.parametrize("kind,n", [(3, 6000), (4, 3000), (1, 1500)])
+@pytest.mark.parametrize("chain", sorted(SF_CHAINS))
+def test_stateful_filter_parity(engine, chain, kind, n):
+    """Three different slices through one chain: the state carries across calls."""
+    calls = [(synth.make_slice(kind, n, seed=synth.SEEDS[kind] + k, base_offset=500 + 7 * n * k), (1 << 64) - 1)
+             for k in range(3)]
+    check_sequence(engine, SF_CHAINS[chain], calls)
+
+
+@pytest.mark.parametrize("max_bytes", [0, 100, 3000, 40000])
+@pytest.mark.parametrize("chain", ["look_back", "dedup", "dedup_evicting"])
+def test_stateful_filter_max_bytes(engine, chain, max_bytes):
+    """The batch cut by max_bytes was processed (its state kept), later ones not."""
+    calls = [(synth.make_slice(3, 4000, seed=0x51 + k, base_offset=100 + 5000 * k), max_bytes) for k in range(3)]
+    check_sequence(engine, SF_CHAINS[chain], calls)
+
+
+@pytest.mark.parametrize("chain", ["look_back", "dedup", "dedup_evicting"])
+def test_stateful_filter_after_look_back(engine, chain):
+    lb_ok = P.encode_records([P.Record.new(str(v)) for v in (5, -3, 700, 12, 12, 999, 40)])
+    calls = [(synth.make_slice(3, 5000, seed=0x77), (1 << 64) - 1)]
+    check_sequence(engine, SF_CHAINS[chain], calls, look_back=lb_ok)
+    lb_bad = P.encode_records([P.Record.new(v) for v in (b"5", b"900", b"x1", b"\xff")])  # stops at the first error
+    check_sequence(engine, SF_CHAINS[chain], calls, look_back=lb_bad)
+
+
+def test_dedup_large_sequential(engine):
+    """Evictions across many batches (the sequential BoundedHashSet walk)."""
+    calls = [(synth.make_slice(3, 40000, seed=0x99 + k), (1 << 64) - 1) for k in range(2)]
+    check_sequence(engine, [("filter_hashset", {"count": "1500"}, None)], calls)
+    check_sequence(engine, [("filter_hashset", {"count": "1000000"}, None)], calls)

@@ -158,3 +158,35 @@ def test_regex_unicode_classes():
     assert O.regex_is_match(r"^.$", "é".encode())
     assert not O.regex_is_match(r"^..$", "é".encode())
     assert O.regex_is_match(r"\s", "a　b".encode())
+
+
+def test_look_back_kats(kats):
+    """filter_look_back / filter_hashset with look_back: engine.rs:388-470,
+    filter_hashset test_set, SPU produce.rs:522-1020, stream_fetch.rs:2483-2605."""
+    from tests.lookback_steps import run_lookback_case
+
+    def new_chain(lb):
+        return O.OracleChain([tuple(case["module"]) + (None,)])
+
+    def look_back(ch, values):
+        r = ch.look_back(0, P.encode_records([P.Record.new(v) for v in values]))
+        assert r["status"] == 0
+        return r["error"], r["metrics"]["invocation_count"]
+
+    def process(ch, values):
+        r = ch.process(P.encode_records([P.Record.new(v) for v in values]))
+        assert r["status"] == 0 and r["error"] is None
+        return _vals(r["bytes"]), r["metrics"]["invocation_count"]
+
+    assert len(kats["look_back"]) >= 6
+    for case in kats["look_back"]:
+        run_lookback_case(case, new_chain, look_back, process)
+
+
+def test_hashset_init_count_param():
+    with pytest.raises(O.OracleError) as e:
+        O.OracleChain([("filter_hashset", {"count": "many"}, None)])
+    assert e.value.message == "invalid digit found in string\n\nSmartModule Init Error: \n"
+    O.OracleChain([("filter_hashset", {"count": "+7"}, None)])  # usize::from_str takes a leading '+'
+    with pytest.raises(O.OracleError):
+        O.OracleChain([("filter_hashset", {"count": "4294967296"}, None)])  # usize is u32 on wasm32
