@@ -259,6 +259,10 @@ def run_filter(ctx, name, nrec, cpu):
     t0 = time.time()
     rs = ResidentSlice(engine, sl_bytes)
     ingest_s = time.time() - t0
+    # CRC32C verify on ingest (north_star): every stored batch's CRC checked on
+    # the GPU against its header (report only, as the reference never checks)
+    rs.verify_crc()
+    vbad, _vfirst, vms = min((rs.verify_crc() for _ in range(3)), key=lambda r: r[2])
     metrics = SmartModuleChainMetrics()
     for _ in range(a.warmup):
         chain.process_slice(rs, metrics=metrics, download=False)
@@ -283,7 +287,11 @@ def run_filter(ctx, name, nrec, cpu):
            "gbps_input": t["in_bytes"] * ctx.world * a.steps / elapsed / 1e9,
            "gbps_pipeline": (t["in_bytes"] + t["out_bytes"]) / (per["total_ms"] * 1e-3) / 1e9,
            "roofline": roofline(per, t, name, recs, rs.n_batches),
-           "kernel_ms": per, "setup_s": {"generate": gen_s, "ingest_h2d": ingest_s}}
+           "kernel_ms": per, "setup_s": {"generate": gen_s, "ingest_h2d": ingest_s},
+           "crc_verify": {"ms": vms, "gbps": t["in_bytes"] / (vms * 1e-3) / 1e9 if vms > 0 else None,
+                          "mismatches": vbad,
+                          "note": "k_verify_crc: CRC32C of every stored batch vs its header, on ingest, outside "
+                                  "the timed step (the reference never verifies)"}}
     if not a.no_e2e:
         # end to end: host slice -> H2D ingest + FileBatchIterator framing -> the
         # same process_batch -> D2H of the output batch (fsg_chain_process_batch)

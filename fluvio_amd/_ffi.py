@@ -115,6 +115,8 @@ SIGNATURES = {
                                       ctypes.POINTER(ctypes.c_uint64)]),
     "fsg_slice_free": (None, [VP]),
     "fsg_slice_device_framed": (ctypes.c_int, [VP]),
+    "fsg_slice_verify_crc": (ctypes.c_int, [VP, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int64),
+                                            ctypes.POINTER(ctypes.c_float)]),
     "fsg_chain_process_slice": (ctypes.c_int, [VP, VP, ctypes.c_uint64, ctypes.POINTER(fsg_metrics),
                                                ctypes.POINTER(ctypes.POINTER(fsg_batch_output))]),
     "fsg_chain_output_device": (ctypes.c_int, [VP, PP, ctypes.POINTER(SZ)]),

@@ -3617,6 +3617,67 @@ __global__ void k_crc_final(uint8_t* out, const uint32_t* acc, uint64_t tail0, u
 }
 
 // ---------------------------------------------------------------------------
+// k_verify_crc: CRC32C of every stored batch checked against its header on
+// ingest (north_star "verify CRC32C").  The reference computes the CRC only on
+// encode and never checks it (protocol record/batch.rs:398-430), so this only
+// reports: process_batch never looks at the result.  One wave per batch
+// (persistent over the batches): 16-byte units counted back from the batch
+// end (the first unit zero-masked before the CRC start: leading zeros leave a
+// raw CRC unchanged), lane j takes units j, j + 64, ... (coalesced), folding
+// each round with the 1 KiB shift table, then its partial moves to the batch
+// end and the wave XORs the partials.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_verify_crc(const uint8_t* __restrict__ sl, const uint64_t* __restrict__ bpos,
+                                                    uint32_t nb, unsigned long long* bad, uint32_t* flags) {
+  __shared__ uint32_t z[16][256];
+  for (uint32_t i = threadIdx.x; i < 16 * 256; i += 256) (&z[0][0])[i] = (&g_crc_z16[0][0])[i];
+  __syncthreads();
+  const uint32_t l = lane_id();
+  const uint32_t W = gridDim.x * 4;
+  for (uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6); b < nb; b += W) {
+    const uint64_t pos = bpos[b];
+    const uint32_t blen = __builtin_bswap32(ld_u32_at(sl + pos + 8));
+    const uint32_t stored = __builtin_bswap32(ld_u32_at(sl + pos + 17));
+    const uint64_t a = pos + 21, e = pos + 12 + (uint64_t)blen;  // framing checked batch_len >= 45
+    const uint64_t n = e - a;
+    const uint32_t nu = (uint32_t)((n + 15) / 16);
+    const uint64_t b0 = e - 16ull * nu;  // unit u covers [b0 + 16u, b0 + 16u + 16)
+    uint32_t acc = 0, last = 0;
+    bool any = false;
+    for (uint32_t u = l; u < nu; u += 64) {
+      const uint8_t* p = sl + b0 + 16ull * u;
+      uint32_t w[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) w[q] = ld_u32_at(p + 4 * q);
+      if (u == 0 && b0 < a) {  // bytes before the CRC start
+        const uint32_t skip = (uint32_t)(a - b0);
+#pragma unroll
+        for (int q = 0; q < 16; q++)
+          if ((uint32_t)q < skip) w[q >> 2] &= ~(0xffu << (8 * (q & 3)));
+      }
+      uint32_t r = 0;
+#pragma unroll
+      for (int q = 0; q < 16; q++) r ^= z[15 - q][(w[q >> 2] >> (8 * (q & 3))) & 0xff];
+      acc = crc_shift_tab(g_crc_shift[10], acc) ^ r;  // earlier units of this lane: 1 KiB further back
+      last = u;
+      any = true;
+    }
+    if (any) acc = crc_shift_bytes(acc, 16ull * (nu - 1 - last));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc ^= __shfl_xor(acc, o, 64);
+    if (l == 0) {
+      const uint32_t crc = acc ^ crc_shift_bytes(0xFFFFFFFFu, n) ^ 0xFFFFFFFFu;
+      const bool ok = crc == stored;
+      if (flags) flags[b] = ok ? 0u : 1u;
+      if (!ok) {
+        atomicAdd(&bad[0], 1ull);
+        atomicMin(&bad[1], (unsigned long long)b);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_write_lean: the output of one batch of verbatim records (KM_COPY /
 // KM_UPPER: filters, uppercase maps, projections) assembled in LDS and stored
 // with 16-byte stores, for batches of many small records (where k_write's
@@ -4465,5 +4526,14 @@ void launch_sf_commit(const SfArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_sf_commit_new, dim3(g), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_sf_commit_last, dim3(g), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_sf_commit_n, dim3(1), dim3(64), 0, s, a);
+}
+void launch_verify_crc(const uint8_t* slice, const uint64_t* bpos, uint32_t nb, unsigned long long* bad,
+                       uint32_t* flags, hipStream_t s) {
+  if (!nb) return;
+  int dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const uint32_t g = std::min<uint32_t>((nb + 3) / 4, (uint32_t)std::max(1, cus) * 8u);
+  hipLaunchKernelGGL(k_verify_crc, dim3(g), dim3(256), 0, s, slice, bpos, nb, bad, flags);
 }
 }  // namespace fsg

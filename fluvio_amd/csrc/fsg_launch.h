@@ -34,6 +34,9 @@ void launch_sf_dedup(const SfArgs& a, hipStream_t s);      // decisions assuming
 void launch_sf_dedup_seq(const SfArgs& a, hipStream_t s);  // the sequential BoundedHashSet walk
 void launch_sf_compact(const SfArgs& a, hipStream_t s);
 void launch_sf_commit(const SfArgs& a, hipStream_t s);     // after k_plan: state through plan.done
+// CRC32C check of every stored batch (report only; bad[0] count, bad[1] first index)
+void launch_verify_crc(const uint8_t* slice, const uint64_t* bpos, uint32_t nb, unsigned long long* bad,
+                       uint32_t* flags, hipStream_t s);
 // device framing (FrameArgs)
 void launch_frame_cand(const FrameArgs& a, uint32_t nchunks, uint64_t* tsum, hipStream_t s);
 void launch_frame_compact(const FrameArgs& a, uint32_t nchunks, hipStream_t s);

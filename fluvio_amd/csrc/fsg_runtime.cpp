@@ -908,6 +908,36 @@ extern "C" int fsg_slice_upload(fsg_engine* e, const uint8_t* s, size_t len, fsg
   return FSG_OK;
 }
 extern "C" int fsg_slice_device_framed(const fsg_slice* s) { return s->device_framed ? 1 : 0; }
+// CRC32C of every framed batch against its header (report only: the reference
+// never verifies, protocol record/batch.rs:398-430, so nothing else changes)
+extern "C" int fsg_slice_verify_crc(const fsg_slice* s, uint64_t* n_bad, int64_t* first_bad, float* ms) {
+  HIPCHK(hipSetDevice(s->eng->device));
+  hipStream_t st = nullptr;
+  HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  DevBuf bad;
+  HIPCHK(bad.ensure(16));
+  const unsigned long long init[2] = {0, ~0ull};
+  HIPCHK(hipMemcpyAsync(bad.p, init, sizeof init, hipMemcpyHostToDevice, st));
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  HIPCHK(hipEventRecord(e0, st));
+  launch_verify_crc((const uint8_t*)s->data.p, s->bpos.as<uint64_t>(), s->nb, bad.as<unsigned long long>(), nullptr, st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(e1, st));
+  unsigned long long r[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(r, bad.p, sizeof r, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  float t = 0;
+  HIPCHK(hipEventElapsedTime(&t, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipStreamDestroy(st);
+  if (n_bad) *n_bad = r[0];
+  if (first_bad) *first_bad = r[0] ? (int64_t)r[1] : -1;
+  if (ms) *ms = t;
+  return FSG_OK;
+}
 extern "C" int fsg_slice_info(const fsg_slice* s, uint64_t* n_batches, uint64_t* n_records, uint64_t* bytes) {
   if (n_batches) *n_batches = s->nb;
   if (n_records) *n_records = s->nrec;

@@ -551,6 +551,14 @@ class ResidentSlice:
         self.n_batches, self.n_records, self.bytes = nb.value, nr.value, by.value
         self.device_framed = bool(_ffi.lib().fsg_slice_device_framed(h))
 
+    def verify_crc(self):
+        """CRC32C of every stored batch checked on the GPU (report only: the
+        reference never verifies).  Returns (mismatches, first bad batch or -1,
+        kernel ms)."""
+        nb, fb, ms = ctypes.c_uint64(), ctypes.c_int64(), ctypes.c_float()
+        _check(_ffi.lib().fsg_slice_verify_crc(self._h, ctypes.byref(nb), ctypes.byref(fb), ctypes.byref(ms)))
+        return nb.value, fb.value, ms.value
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h and h.value and _ffi._lib is not None:

@@ -224,6 +224,12 @@ int fsg_slice_info(const fsg_slice *s, uint64_t *n_batches, uint64_t *n_records,
  * without magic 2 on the chain, or candidates too dense).  Same result either
  * way (FileBatchIterator::next, crates/fluvio-storage/src/iterators.rs:55-160). */
 int fsg_slice_device_framed(const fsg_slice *s);
+/* CRC32C (Castagnoli) of every framed batch, computed on the GPU over header
+ * bytes 21.. + records and compared with the stored crc: *n_bad mismatches,
+ * *first_bad the first such batch (-1 none), *ms the kernel time.  Reports
+ * only — the reference never verifies (crates/fluvio-protocol/src/record/
+ * batch.rs:398-430 computes the CRC on encode only), so processing ignores it. */
+int fsg_slice_verify_crc(const fsg_slice *s, uint64_t *n_bad, int64_t *first_bad, float *ms);
 void fsg_slice_free(fsg_slice *s);
 /* process_batch over a resident slice; the output batch stays in HBM until
  * fsg_chain_download_output (out may be NULL to keep it resident). */

@@ -1061,3 +1061,49 @@ def test_dedup_large_sequential(engine):
     calls = [(synth.make_slice(3, 40000, seed=0x99 + k), (1 << 64) - 1) for k in range(2)]
     check_sequence(engine, [("filter_hashset", {"count": "1500"}, None)], calls)
     check_sequence(engine, [("filter_hashset", {"count": "1000000"}, None)], calls)
+
+
+# ---------------------------------------------------------------------------
+# CRC32C verify on ingest (north_star): report only, processing unchanged
+# ---------------------------------------------------------------------------
+def test_verify_crc_on_ingest(engine):
+    for kind, n in ((2, 3000), (1, 5000), (3, 20000), (4, 2000)):
+        sl = synth.make_slice(kind, n, base_offset=9)
+        batches = list(P.decode_batches(sl))
+        rs = ResidentSlice(engine, sl)
+        bad, first, _ms = rs.verify_crc()
+        assert (bad, first) == (0, -1), kind
+        # the oracle's CRC32C of each batch's covered bytes matches the stored one
+        pos = 0
+        for b in batches:
+            blen = struct.unpack(">i", sl[pos + 8:pos + 12])[0]
+            assert O.crc32c(sl[pos + 21:pos + 12 + blen]) == struct.unpack(">I", sl[pos + 17:pos + 21])[0]
+            pos += 12 + blen
+        # corrupt three batches (a record byte, a header byte in the CRC range, the stored CRC itself)
+        corrupt = bytearray(sl)
+        starts = []
+        pos = 0
+        while pos < len(sl):
+            starts.append(pos)
+            pos += 12 + struct.unpack(">i", sl[pos + 8:pos + 12])[0]
+        picks = sorted({1 % len(starts), len(starts) // 2, len(starts) - 1})
+        for j, bi in enumerate(picks):
+            p0 = starts[bi]
+            off = [p0 + 70, p0 + 30, p0 + 18][j % 3]
+            corrupt[off] ^= 0x40
+        rs2 = ResidentSlice(engine, bytes(corrupt))
+        bad, first, _ms = rs2.verify_crc()
+        assert (bad, first) == (len(picks), picks[0]), kind
+    # the reference never checks: a corrupted CRC field does not change process_batch
+    sl = synth.make_slice(2, 2000)
+    c = bytearray(sl)
+    c[17] ^= 0xFF
+    modules = [("filter_init", {"key": "timeout"}, None)]
+    assert gpu_chain(engine, modules).process_batch(bytes(c)).raw == orc_chain(modules).process_batch(bytes(c))["bytes"]
+
+
+def test_verify_crc_large_batches(engine):
+    """Batches beyond the 16 KiB window (one wave folds many 1 KiB rounds)."""
+    sl = synth.make_slice(2, 3000, max_section=300000)
+    rs = ResidentSlice(engine, sl)
+    assert rs.verify_crc()[:2] == (0, -1)
