@@ -7,9 +7,13 @@
 // reference tree; we restate its published semantics for the supported subset:
 // unanchored is_match over valid UTF-8, Unicode-aware `.` (any scalar but \n),
 // `\d` (Unicode Nd), `\s` (White_Space), `^`/`$` at value start/end (no
-// multi-line flag).  `\w`/`\W` are exact on ASCII values only (the kernel
-// reports FSG_E_UNSUPPORTED for a non-ASCII value); \b, \p{..}, inline flags,
-// nested classes and class set operations are rejected at init (FSG_E_UNSUPPORTED).
+// multi-line flag), `\A` / `\z`, `[[:name:]]` ASCII classes, inline flags i
+// (simple case folding, restated for ASCII letters + U+212A / U+017F), s and U.
+// `\w`, `\W`, `\b`, `\B` are exact on ASCII values only (the kernel reports
+// FSG_E_UNSUPPORTED for a non-ASCII value); word boundaries are DFA states that
+// remember whether the previous byte was a word byte.  \p{..}, the m / x / u
+// flags, nested classes and class set operations are rejected at init
+// (FSG_E_UNSUPPORTED).
 //
 // Output: a DFA over bytes with unanchored restart folded in, byte classes,
 // sticky acceptance, an end-of-value acceptance bit and the longest possible
@@ -80,7 +84,7 @@ Set table(const Range (&t)[N], bool neg) {
 }
 
 // ---------------- AST
-enum NodeT { N_EMPTY, N_SET, N_CAT, N_ALT, N_REP, N_BOL, N_EOL };
+enum NodeT { N_EMPTY, N_SET, N_CAT, N_ALT, N_REP, N_BOL, N_EOL, N_WB, N_NWB };
 struct Node {
   NodeT t = N_EMPTY;
   Set set;
@@ -93,15 +97,62 @@ using NodeP = std::unique_ptr<Node>;
 struct Parser {
   std::vector<uint32_t> p;
   size_t i = 0;
-  bool err = false, unsup = false, word = false;
+  bool err = false, unsup = false, word = false, wb = false;
+  bool fi = false, fs = false;  // inline flags i, s
   int depth = 0;
+
+  // (?i): simple case folding restated for ASCII letters (+ U+212A ~ k, U+017F ~ s);
+  // a literal outside ASCII under (?i) is unsupported
+  void add_folded(Set& st, uint32_t lo, uint32_t hi) {
+    st.push_back({lo, hi});
+    if (!fi) return;
+    if (hi >= 0x80) {
+      unsup = true;
+      return;
+    }
+    uint32_t a = std::max<uint32_t>(lo, 'a'), b = std::min<uint32_t>(hi, 'z');
+    if (a <= b) st.push_back({a - 32, b - 32});
+    a = std::max<uint32_t>(lo, 'A');
+    b = std::min<uint32_t>(hi, 'Z');
+    if (a <= b) st.push_back({a + 32, b + 32});
+    if ((lo <= 'k' && 'k' <= hi) || (lo <= 'K' && 'K' <= hi)) st.push_back({0x212A, 0x212A});
+    if ((lo <= 's' && 's' <= hi) || (lo <= 'S' && 'S' <= hi)) st.push_back({0x17F, 0x17F});
+  }
+  // [:name:] ASCII classes (regex-syntax ClassAsciiKind)
+  static bool posix(const std::vector<uint32_t>& name, Set& st) {
+    static const struct {
+      const char* n;
+      Range r[4];
+      int k;
+    } T[] = {{"alnum", {{'0', '9'}, {'A', 'Z'}, {'a', 'z'}}, 3},
+             {"alpha", {{'A', 'Z'}, {'a', 'z'}}, 2},
+             {"ascii", {{0, 0x7F}}, 1},
+             {"blank", {{'\t', '\t'}, {' ', ' '}}, 2},
+             {"cntrl", {{0, 0x1F}, {0x7F, 0x7F}}, 2},
+             {"digit", {{'0', '9'}}, 1},
+             {"graph", {{'!', '~'}}, 1},
+             {"lower", {{'a', 'z'}}, 1},
+             {"print", {{' ', '~'}}, 1},
+             {"punct", {{'!', '/'}, {':', '@'}, {'[', '`'}, {'{', '~'}}, 4},
+             {"space", {{'\t', '\r'}, {' ', ' '}}, 2},
+             {"upper", {{'A', 'Z'}}, 1},
+             {"word", {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}}, 4},
+             {"xdigit", {{'0', '9'}, {'A', 'F'}, {'a', 'f'}}, 3}};
+    for (auto& t : T) {
+      if (strlen(t.n) != name.size() || !std::equal(name.begin(), name.end(), t.n)) continue;
+      for (int q = 0; q < t.k; q++) st.push_back(t.r[q]);
+      return true;
+    }
+    return false;
+  }
 
   bool at(uint32_t c) const { return i < p.size() && p[i] == c; }
   static bool hex(uint32_t c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'); }
   static uint32_t hv(uint32_t c) { return c <= '9' ? c - '0' : (c | 0x20) - 'a' + 10; }
 
-  // 1: single code point in *c; 2: set in *s; 0: failure (err/unsup set)
-  int escape(uint32_t* c, Set* s) {
+  // 1: single code point in *c; 2: set in *s; 3 \b, 4 \B, 5 \A, 6 \z;
+  // 0: failure (err/unsup set)
+  int escape(uint32_t* c, Set* s, bool in_class = false) {
     if (i >= p.size()) {
       err = true;
       return 0;
@@ -146,7 +197,14 @@ struct Parser {
         *c = v;
         return 1;
       }
-      case 'b': case 'B': case 'A': case 'z': case 'p': case 'P': case 'u': case 'U':
+      case 'b': case 'B': case 'A': case 'z':
+        if (in_class) {
+          err = true;
+          return 0;
+        }
+        if (e == 'b' || e == 'B') word = wb = true;
+        return e == 'b' ? 3 : e == 'B' ? 4 : e == 'A' ? 5 : 6;
+      case 'p': case 'P': case 'u': case 'U':
         unsup = true;
         return 0;
       default:
@@ -178,6 +236,24 @@ struct Parser {
         i++;
         break;
       }
+      if (c == '[' && i + 1 < p.size() && p[i + 1] == ':') {  // [:name:] / [:^name:]
+        size_t j = i + 2;
+        bool pneg = false;
+        if (j < p.size() && p[j] == '^') {
+          pneg = true;
+          j++;
+        }
+        size_t k = j;
+        while (k + 1 < p.size() && !(p[k] == ':' && p[k + 1] == ']')) k++;
+        Set ps;
+        if (k + 1 < p.size() && posix(std::vector<uint32_t>(p.begin() + j, p.begin() + k), ps)) {
+          if (pneg) ps = negate(ps);
+          for (auto& r : ps) add_folded(n->set, r.lo, r.hi);
+          i = k + 2;
+          first = false;
+          continue;
+        }
+      }
       if (c == '[') {
         unsup = true;
         return n;
@@ -191,7 +267,7 @@ struct Parser {
       uint32_t lo;
       if (c == '\\') {
         Set s;
-        int k = escape(&lo, &s);
+        int k = escape(&lo, &s, true);
         if (k == 2) {
           n->set.insert(n->set.end(), s.begin(), s.end());
           continue;
@@ -219,9 +295,9 @@ struct Parser {
           return n;
         }
       }
-      n->set.push_back({lo, hi});
+      add_folded(n->set, lo, hi);
     }
-    n->set = neg ? negate(n->set) : norm(n->set);
+    n->set = neg ? negate(n->set) : norm(n->set);  // case folding applies before the negation
     return n;
   }
 
@@ -256,17 +332,78 @@ struct Parser {
             return n;
           }
           i++;
-        } else {
-          unsup = true;
-          return n;
+        } else {  // inline flags (?flags) / (?flags:re): i, s, U; m, x, u, R unsupported
+          int neg = 0, nflags = 0;
+          bool nfi = fi, nfs = fs;
+          for (;;) {
+            if (i >= p.size()) {
+              err = true;
+              return n;
+            }
+            const uint32_t f = p[i++];
+            if (f == ':' || f == ')') {
+              if (!nflags || neg == 1) {
+                err = true;
+                return n;
+              }
+              if (f == ')') {  // until the end of the enclosing group
+                fi = nfi;
+                fs = nfs;
+                return n;  // N_EMPTY
+              }
+              break;
+            }
+            if (f == '-') {
+              if (neg) {
+                err = true;
+                return n;
+              }
+              neg = 1;
+              continue;
+            }
+            if (f == 'i') {
+              nfi = !neg;
+            } else if (f == 's') {
+              nfs = !neg;
+            } else if (f == 'U') {  // greed only: same language for is_match
+            } else if (f == 'm' || f == 'x' || f == 'u' || f == 'R') {
+              unsup = true;
+              return n;
+            } else {
+              err = true;
+              return n;
+            }
+            nflags++;
+            if (neg) neg = 2;
+          }
+          const bool sfi = fi, sfs = fs;
+          fi = nfi;
+          fs = nfs;
+          if (++depth > 200) {
+            err = true;
+            return n;
+          }
+          NodeP g = alt();
+          depth--;
+          fi = sfi;
+          fs = sfs;
+          if (!at(')')) {
+            err = true;
+            return g;
+          }
+          i++;
+          return g;
         }
       }
       if (++depth > 200) {
         err = true;
         return n;
       }
+      const bool sfi = fi, sfs = fs;  // flags set inside a group end with it
       NodeP g = alt();
       depth--;
+      fi = sfi;
+      fs = sfs;
       if (!at(')')) {
         err = true;
         return g;
@@ -277,7 +414,10 @@ struct Parser {
     if (c == '[') return cls();
     if (c == '.') {
       n->t = N_SET;
-      n->set = {{0, '\n' - 1}, {'\n' + 1, 0x10FFFF}};
+      if (fs)
+        n->set = {{0, 0x10FFFF}};
+      else
+        n->set = {{0, '\n' - 1}, {'\n' + 1, 0x10FFFF}};
       return n;
     }
     if (c == '^') {
@@ -293,10 +433,14 @@ struct Parser {
       Set s;
       int k = escape(&cp, &s);
       n->t = N_SET;
-      if (k == 2)
+      if (k == 2) {
         n->set = norm(s);
-      else if (k == 1)
-        n->set = {{cp, cp}};
+      } else if (k == 1) {
+        add_folded(n->set, cp, cp);
+        n->set = norm(n->set);
+      } else if (k >= 3) {
+        n->t = k == 3 ? N_WB : k == 4 ? N_NWB : k == 5 ? N_BOL : N_EOL;
+      }
       return n;
     }
     if (c == '*' || c == '+' || c == '?' || c == ')' || c == '|' || c == '{') {
@@ -304,7 +448,8 @@ struct Parser {
       return n;
     }
     n->t = N_SET;
-    n->set = {{c, c}};
+    add_folded(n->set, c, c);
+    n->set = norm(n->set);
     return n;
   }
 
@@ -381,7 +526,7 @@ struct Parser {
 int utf8_len(uint32_t c) { return c < 0x80 ? 1 : c < 0x800 ? 2 : c < 0x10000 ? 3 : 4; }
 int64_t max_len(const Node* n, bool ascii) {
   switch (n->t) {
-    case N_EMPTY: case N_BOL: case N_EOL: return 0;
+    case N_EMPTY: case N_BOL: case N_EOL: case N_WB: case N_NWB: return 0;
     case N_SET: {
       int m = 0;
       for (auto& r : n->set) {
@@ -419,7 +564,7 @@ int64_t max_len(const Node* n, bool ascii) {
 }
 
 // ---------------- byte NFA
-enum NfaT { F_BYTE, F_SPLIT, F_EPS, F_BOT, F_EOT, F_MATCH };
+enum NfaT { F_BYTE, F_SPLIT, F_EPS, F_BOT, F_EOT, F_MATCH, F_WB, F_NWB };
 struct NState {
   NfaT t;
   uint8_t lo, hi;
@@ -543,6 +688,11 @@ Frag build(Nfa& g, const Node* n, bool ascii) {
       int s = g.add(F_EOT);
       return {s, {{s, 0}}};
     }
+    case N_WB:
+    case N_NWB: {
+      int s = g.add(n->t == N_WB ? F_WB : F_NWB);
+      return {s, {{s, 0}}};
+    }
     case N_SET: {
       std::vector<std::vector<std::pair<uint8_t, uint8_t>>> seqs;
       for (auto& r : n->set) {
@@ -601,8 +751,11 @@ struct Closure {
   std::vector<int> mark;
   int gen = 0;
   explicit Closure(const Nfa& n) : g(n), mark(n.st.size(), 0) {}
-  // closure of `seeds`; keeps BYTE, MATCH and (unfollowed) EOT states
-  std::vector<int> run(const std::vector<int>& seeds, bool bot, bool eot) {
+  // closure of `seeds`; keeps BYTE, MATCH and (unfollowed) EOT states; word
+  // boundaries are kept pending (resolve = false) or decided from the previous
+  // and next byte's word-ness (resolve = true)
+  std::vector<int> run(const std::vector<int>& seeds, bool bot, bool eot, bool resolve = false, bool pw = false,
+                       bool nw = false) {
     gen++;
     std::vector<int> out, stack(seeds.rbegin(), seeds.rend());
     while (!stack.empty()) {
@@ -627,6 +780,13 @@ struct Closure {
           else
             out.push_back(s);
           break;
+        case F_WB:
+        case F_NWB:
+          if (!resolve)
+            out.push_back(s);
+          else if ((pw != nw) == (x.t == F_WB))
+            stack.push_back(x.a);
+          break;
       }
     }
     std::sort(out.begin(), out.end());
@@ -636,7 +796,7 @@ struct Closure {
 
 }  // namespace
 
-static int determinize(const Node* rootp, bool ascii, bool word, Dfa& out, std::string& msg);
+static int determinize(const Node* rootp, bool ascii, bool word, bool wb, Dfa& out, std::string& msg);
 
 int compile_regex(const std::string& pattern, Dfa& out, Dfa& full, std::string& msg) {
   // pattern -> code points (must be valid UTF-8; Rust &str)
@@ -666,12 +826,15 @@ int compile_regex(const std::string& pattern, Dfa& out, Dfa& full, std::string& 
     msg = "regex parse error";
     return -2;
   }
-  if (int rc = determinize(root.get(), true, P.word, out, msg)) return rc;
-  return determinize(root.get(), false, P.word, full, msg);
+  if (int rc = determinize(root.get(), true, P.word, P.wb, out, msg)) return rc;
+  return determinize(root.get(), false, P.word, P.wb, full, msg);
 }
 
-int determinize(const Node* rootp, bool ascii, bool word, Dfa& out, std::string& msg) {
-  const int64_t ml = max_len(rootp, ascii);
+static bool word_byte(int b) { return (b >= '0' && b <= '9') || (b >= 'A' && b <= 'Z') || (b >= 'a' && b <= 'z') || b == '_'; }
+
+int determinize(const Node* rootp, bool ascii, bool word, bool wb, Dfa& out, std::string& msg) {
+  // word boundaries need the previous byte: no chunk-parallel restarts (max_len -1)
+  const int64_t ml = wb ? -1 : max_len(rootp, ascii);
   Nfa g;
   Frag f = build(g, rootp, ascii);
   int m = g.add(F_MATCH);
@@ -685,6 +848,9 @@ int determinize(const Node* rootp, bool ascii, bool word, Dfa& out, std::string&
       cut[s.lo] = 1;
       cut[s.hi + 1] = 1;
     }
+  if (wb)  // word bytes form their own classes
+    for (int b = 0; b < 256; b++)
+      if (word_byte(b) != (b > 0 && word_byte(b - 1))) cut[b] = 1;
   std::vector<uint8_t> cls(256);
   std::vector<int> rep;
   int nc = -1;
@@ -699,20 +865,23 @@ int determinize(const Node* rootp, bool ascii, bool word, Dfa& out, std::string&
   Closure C(g);
   std::map<std::vector<int>, int> ids;
   std::vector<std::vector<int>> sets;
-  std::vector<uint8_t> bot_flag;
-  auto intern = [&](const std::vector<int>& s, bool is_bot) {
+  std::vector<uint8_t> bot_flag, pw_flag;
+  auto intern = [&](const std::vector<int>& s, bool is_bot, bool pw) {
     auto key = s;
     if (is_bot) key.push_back(-7);  // the BOT state is distinct (EOT acceptance with ^ satisfied)
+    if (pw) key.push_back(-8);      // the previous byte was a word byte (word boundaries)
     auto it = ids.find(key);
     if (it != ids.end()) return it->second;
     int id = (int)sets.size();
     ids[key] = id;
     sets.push_back(s);
     bot_flag.push_back(is_bot);
+    pw_flag.push_back(pw);
     return id;
   };
-  const int s_bot = intern(C.run({start}, true, false), true);
-  const int s_mid = intern(C.run({start}, false, false), false);
+  const int s_bot = intern(C.run({start}, true, false), true, false);
+  const int s_mid = intern(C.run({start}, false, false), false, false);
+  int s_acc = -1;  // sticky accept reached through a word boundary decided at a transition
   std::vector<std::vector<int>> trans;
   std::vector<uint8_t> acc;
   for (size_t k = 0; k < sets.size(); k++) {
@@ -721,12 +890,15 @@ int determinize(const Node* rootp, bool ascii, bool word, Dfa& out, std::string&
       return -103;
     }
     const auto cur = sets[k];
-    const bool is_acc = std::find_if(cur.begin(), cur.end(), [&](int s) { return g.st[s].t == F_MATCH; }) != cur.end();
+    const bool pw = pw_flag[k];
+    auto has_match = [&](const std::vector<int>& v) {
+      return std::find_if(v.begin(), v.end(), [&](int s) { return g.st[s].t == F_MATCH; }) != v.end();
+    };
+    const bool is_acc = has_match(cur);
     uint8_t a = is_acc ? 1 : 0;
     {
-      auto ce = C.run(cur, bot_flag[k], true);
-      if (is_acc || std::find_if(ce.begin(), ce.end(), [&](int s) { return g.st[s].t == F_MATCH; }) != ce.end())
-        a |= 2;
+      auto ce = C.run(cur, bot_flag[k], true, wb, pw, false);  // at the end: no next byte
+      if (is_acc || has_match(ce)) a |= 2;
     }
     acc.push_back(a);
     std::vector<int> row(ncls);
@@ -736,13 +908,20 @@ int determinize(const Node* rootp, bool ascii, bool word, Dfa& out, std::string&
         continue;
       }
       const int byte = rep[c];
+      const bool nw = wb && word_byte(byte);
+      const std::vector<int> res = wb ? C.run(cur, bot_flag[k], false, true, pw, nw) : cur;
+      if (wb && has_match(res)) {  // a boundary before this byte completed the match
+        if (s_acc < 0) s_acc = intern({m}, false, false);
+        row[c] = s_acc;
+        continue;
+      }
       std::vector<int> nxt;
-      for (int s : cur) {
+      for (int s : res) {
         const NState& x = g.st[s];
         if (x.t == F_BYTE && byte >= x.lo && byte <= x.hi) nxt.push_back(x.a);
       }
       nxt.push_back(start);  // unanchored restart at the next position
-      row[c] = intern(C.run(nxt, false, false), false);
+      row[c] = intern(C.run(nxt, false, false), false, nw);
     }
     trans.push_back(row);
   }

@@ -556,7 +556,7 @@ static int cs_has(const cset *s, uint32_t c) {
   return 0;
 }
 
-enum { RX_CHAR, RX_CLASS, RX_SPLIT, RX_JMP, RX_BOL, RX_EOL, RX_MATCH };
+enum { RX_CHAR, RX_CLASS, RX_SPLIT, RX_JMP, RX_BOL, RX_EOL, RX_MATCH, RX_WB, RX_NWB };
 typedef struct {
   int op;
   uint32_t c;
@@ -572,7 +572,7 @@ typedef struct {
 } rxprog;
 
 /* AST */
-enum { A_EMPTY, A_CHAR, A_CLASS, A_CAT, A_ALT, A_REP, A_BOL, A_EOL };
+enum { A_EMPTY, A_CHAR, A_CLASS, A_CAT, A_ALT, A_REP, A_BOL, A_EOL, A_WB, A_NWB };
 typedef struct anode {
   int t;
   uint32_t c;
@@ -589,7 +589,58 @@ typedef struct {
   int err;
   int unsupported;
   int depth;
+  int fi, fs;   /* inline flags i (case-insensitive), s (. matches \n); U only swaps greed */
+  int word;     /* \w, \W, \b or \B used: exact on ASCII input only */
 } rxparser;
+
+/* (?i): regex-syntax's simple case folding, restated for ASCII letters: a-z <-> A-Z,
+ * plus the two non-ASCII code points that fold to ASCII letters (U+212A KELVIN SIGN
+ * ~ k, U+017F LONG S ~ s).  A literal outside ASCII under (?i) is unsupported. */
+static void cs_add_folded(rxparser *P, cset *s, uint32_t lo, uint32_t hi) {
+  cs_add(s, lo, hi);
+  if (!P->fi) return;
+  if (hi >= 0x80) {
+    P->unsupported = 1;
+    return;
+  }
+  uint32_t a = lo > 'a' ? lo : 'a', b = hi < 'z' ? hi : 'z';
+  if (a <= b) cs_add(s, a - 32, b - 32);
+  a = lo > 'A' ? lo : 'A';
+  b = hi < 'Z' ? hi : 'Z';
+  if (a <= b) cs_add(s, a + 32, b + 32);
+  if ((lo <= 'k' && 'k' <= hi) || (lo <= 'K' && 'K' <= hi)) cs_add(s, 0x212A, 0x212A);
+  if ((lo <= 's' && 's' <= hi) || (lo <= 'S' && 'S' <= hi)) cs_add(s, 0x17F, 0x17F);
+}
+/* [[:name:]] ASCII classes (regex-syntax ast ClassAsciiKind) */
+static int posix_class(const uint32_t *p, size_t n, cset *s) {
+  static const struct {
+    const char *name;
+    uint32_t r[5][2];
+  } T[] = {{"alnum", {{'0', '9'}, {'A', 'Z'}, {'a', 'z'}}},
+           {"alpha", {{'A', 'Z'}, {'a', 'z'}}},
+           {"ascii", {{0, 0x7F}}},
+           {"blank", {{'\t', '\t'}, {' ', ' '}}},
+           {"cntrl", {{0, 0x1F}, {0x7F, 0x7F}}},
+           {"digit", {{'0', '9'}}},
+           {"graph", {{'!', '~'}}},
+           {"lower", {{'a', 'z'}}},
+           {"print", {{' ', '~'}}},
+           {"punct", {{'!', '/'}, {':', '@'}, {'[', '`'}, {'{', '~'}}},
+           {"space", {{'\t', '\r'}, {' ', ' '}}},
+           {"upper", {{'A', 'Z'}}},
+           {"word", {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}}},
+           {"xdigit", {{'0', '9'}, {'A', 'F'}, {'a', 'f'}}}};
+  for (size_t k = 0; k < sizeof T / sizeof T[0]; k++) {
+    size_t L = strlen(T[k].name);
+    if (L != n) continue;
+    size_t j = 0;
+    while (j < L && p[j] == (uint32_t)T[k].name[j]) j++;
+    if (j < L) continue;
+    for (int q = 0; q < 5 && (q == 0 || T[k].r[q][1]); q++) cs_add(s, T[k].r[q][0], T[k].r[q][1]);
+    return 1;
+  }
+  return 0;
+}
 
 static anode *an_new(int t) {
   anode *a = (anode *)calloc(1, sizeof(anode));
@@ -628,6 +679,15 @@ static int rx_escape(rxparser *P, uint32_t *single, cset *set, int in_class) {
     case 'S': cs_add_tab(set, WS_TAB, sizeof WS_TAB / sizeof WS_TAB[0], 1); return 2;
     case 'w': cs_add_tab(set, WORD_ASCII, 4, 0); set->unicode_word = 1; return 2;
     case 'W': cs_add_tab(set, WORD_ASCII, 4, 1); set->unicode_word = 1; return 2;
+    case 'b': case 'B': /* word boundary assertions (Unicode \w: exact on ASCII input) */
+      if (in_class) {
+        P->err = 1;
+        return 0;
+      }
+      P->word = 1;
+      return c == 'b' ? 3 : 4;
+    case 'A': return in_class ? (P->err = 1, 0) : 5; /* start of text (= ^ without m) */
+    case 'z': return in_class ? (P->err = 1, 0) : 6; /* end of text (= $ without m) */
     case 'n': *single = '\n'; return 1;
     case 't': *single = '\t'; return 1;
     case 'r': *single = '\r'; return 1;
@@ -661,7 +721,7 @@ static int rx_escape(rxparser *P, uint32_t *single, cset *set, int in_class) {
       *single = v;
       return 1;
     }
-    case 'b': case 'B': case 'A': case 'z': case 'p': case 'P': case 'u': case 'U':
+    case 'p': case 'P': case 'u': case 'U':
       P->unsupported = 1;
       return 0;
     default:
@@ -669,7 +729,6 @@ static int rx_escape(rxparser *P, uint32_t *single, cset *set, int in_class) {
         *single = c; /* escaped punctuation / meta */
         return 1;
       }
-      (void)in_class;
       P->err = 1;
       return 0;
   }
@@ -694,8 +753,28 @@ static anode *rx_parse_class(rxparser *P) {
       P->i++;
       break;
     }
+    if (c == '[' && P->i + 1 < P->n && P->p[P->i + 1] == ':') { /* [:name:] / [:^name:] */
+      size_t j = P->i + 2;
+      int pneg = 0;
+      if (j < P->n && P->p[j] == '^') {
+        pneg = 1;
+        j++;
+      }
+      size_t k = j;
+      while (k + 1 < P->n && !(P->p[k] == ':' && P->p[k + 1] == ']')) k++;
+      cset tmp = {0};
+      if (k + 1 < P->n && posix_class(P->p + j, k - j, &tmp)) {
+        if (pneg) cs_negate(&tmp);
+        for (size_t q = 0; q < tmp.n; q++) cs_add_folded(P, &a->cls, tmp.r[q].lo, tmp.r[q].hi);
+        free(tmp.r);
+        P->i = k + 2;
+        first = 0;
+        continue;
+      }
+      free(tmp.r);
+    }
     if (c == '[') {
-      P->unsupported = 1; /* nested classes / POSIX classes */
+      P->unsupported = 1; /* nested classes */
       return a;
     }
     if ((c == '&' || c == '-' || c == '~') && P->i + 1 < P->n && P->p[P->i + 1] == c && !first) {
@@ -713,6 +792,11 @@ static anode *rx_parse_class(rxparser *P) {
         if (tmp.unicode_word) a->cls.unicode_word = 1;
         free(tmp.r);
         continue;
+      }
+      if (k >= 3) {
+        P->err = 1;
+        free(tmp.r);
+        return a;
       }
       free(tmp.r);
       if (k == 0) return a;
@@ -738,9 +822,9 @@ static anode *rx_parse_class(rxparser *P) {
         return a;
       }
     }
-    cs_add(&a->cls, lo, hi);
+    cs_add_folded(P, &a->cls, lo, hi);
   }
-  if (neg) cs_negate(&a->cls);
+  if (neg) cs_negate(&a->cls); /* case folding applies before the negation */
   cs_norm(&a->cls);
   return a;
 }
@@ -777,16 +861,75 @@ static anode *rx_parse_atom(rxparser *P) {
         }
         P->i++;
       } else {
-        P->unsupported = 1; /* inline flags */
-        return an_new(A_EMPTY);
+        /* inline flags (?flags) / (?flags:re): i, s, U supported; m, x, u, R not */
+        int neg = 0, nflags = 0, fi = P->fi, fs = P->fs;
+        for (;;) {
+          if (P->i >= P->n) {
+            P->err = 1;
+            return an_new(A_EMPTY);
+          }
+          uint32_t f = P->p[P->i++];
+          if (f == ':' || f == ')') {
+            if (!nflags || neg == 1) { /* "(?)" / "(?-)" / "(?i-)" are errors */
+              P->err = 1;
+              return an_new(A_EMPTY);
+            }
+            if (f == ')') { /* until the end of the enclosing group */
+              P->fi = fi;
+              P->fs = fs;
+              return an_new(A_EMPTY);
+            }
+            break;
+          }
+          if (f == '-') {
+            if (neg) {
+              P->err = 1;
+              return an_new(A_EMPTY);
+            }
+            neg = 1;
+            continue;
+          }
+          if (f == 'i') fi = !neg;
+          else if (f == 's') fs = !neg;
+          else if (f == 'U') { /* greed only: same language */ }
+          else if (f == 'm' || f == 'x' || f == 'u' || f == 'R') {
+            P->unsupported = 1;
+            return an_new(A_EMPTY);
+          } else {
+            P->err = 1;
+            return an_new(A_EMPTY);
+          }
+          nflags++;
+          if (neg) neg = 2;
+        }
+        int sfi = P->fi, sfs = P->fs;
+        P->fi = fi;
+        P->fs = fs;
+        if (++P->depth > 200) {
+          P->err = 1;
+          return an_new(A_EMPTY);
+        }
+        anode *g = rx_parse_alt(P);
+        P->depth--;
+        P->fi = sfi;
+        P->fs = sfs;
+        if (P->i >= P->n || P->p[P->i] != ')') {
+          P->err = 1;
+          return g;
+        }
+        P->i++;
+        return g;
       }
     }
     if (++P->depth > 200) {
       P->err = 1;
       return an_new(A_EMPTY);
     }
+    int sfi = P->fi, sfs = P->fs; /* flags set inside a group end with it */
     anode *g = rx_parse_alt(P);
     P->depth--;
+    P->fi = sfi;
+    P->fs = sfs;
     if (P->i >= P->n || P->p[P->i] != ')') {
       P->err = 1;
       return g;
@@ -797,8 +940,12 @@ static anode *rx_parse_atom(rxparser *P) {
   if (c == '[') return rx_parse_class(P);
   if (c == '.') {
     anode *a = an_new(A_CLASS);
-    cs_add(&a->cls, 0, '\n' - 1);
-    cs_add(&a->cls, '\n' + 1, 0x10FFFF);
+    if (P->fs) {
+      cs_add(&a->cls, 0, 0x10FFFF);
+    } else {
+      cs_add(&a->cls, 0, '\n' - 1);
+      cs_add(&a->cls, '\n' + 1, 0x10FFFF);
+    }
     return a;
   }
   if (c == '^') return an_new(A_BOL);
@@ -812,9 +959,17 @@ static anode *rx_parse_atom(rxparser *P) {
       a->t = A_CLASS;
       a->cls = tmp;
       cs_norm(&a->cls);
+    } else if (k >= 3) {
+      free(tmp.r);
+      a->t = k == 3 ? A_WB : k == 4 ? A_NWB : k == 5 ? A_BOL : A_EOL;
     } else {
       free(tmp.r);
       a->c = s;
+      if (P->fi && k == 1) {
+        a->t = A_CLASS;
+        cs_add_folded(P, &a->cls, s, s);
+        cs_norm(&a->cls);
+      }
     }
     return a;
   }
@@ -828,6 +983,11 @@ static anode *rx_parse_atom(rxparser *P) {
   }
   anode *a = an_new(A_CHAR);
   a->c = c;
+  if (P->fi) {
+    a->t = A_CLASS;
+    cs_add_folded(P, &a->cls, c, c);
+    cs_norm(&a->cls);
+  }
   return a;
 }
 
@@ -930,6 +1090,8 @@ static void rx_comp(rxprog *g, const anode *a) {
     case A_CLASS: rx_emit(g, RX_CLASS, (uint32_t)rx_addcls(g, &a->cls), 0, 0); break;
     case A_BOL: rx_emit(g, RX_BOL, 0, 0, 0); break;
     case A_EOL: rx_emit(g, RX_EOL, 0, 0, 0); break;
+    case A_WB: rx_emit(g, RX_WB, 0, 0, 0); break;
+    case A_NWB: rx_emit(g, RX_NWB, 0, 0, 0); break;
     case A_CAT:
       for (size_t i = 0; i < a->nk; i++) rx_comp(g, a->kids[i]);
       break;
@@ -995,8 +1157,12 @@ static int rx_compile(const char *pat, rxprog *g) {
   if (!utf8_check((const uint8_t *)pat, plen, &vut, &el)) return ORC_E_INIT;
   size_t ncp;
   uint32_t *cps = utf8_decode((const uint8_t *)pat, plen, &ncp);
-  rxparser P = {cps, ncp, 0, 0, 0, 0};
+  rxparser P;
+  memset(&P, 0, sizeof P);
+  P.p = cps;
+  P.n = ncp;
   anode *root = rx_parse_alt(&P);
+  if (P.word) g->unicode_word = 1;
   int rc = 0;
   if (P.unsupported)
     rc = ORC_E_UNSUPPORTED;
@@ -1016,7 +1182,11 @@ typedef struct {
   int *dense, *sparse;
   int n;
 } sset;
-static void ss_add(const rxprog *g, sset *s, int pc, size_t pos, size_t n, int *match, int *stack) {
+static int rx_is_word(uint32_t c) {
+  return (c >= '0' && c <= '9') || (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || c == '_';
+}
+static void ss_add(const rxprog *g, sset *s, int pc, size_t pos, size_t n, int *match, int *stack,
+                   const uint32_t *cp) {
   int sp = 0;
   stack[sp++] = pc;
   while (sp) {
@@ -1037,6 +1207,12 @@ static void ss_add(const rxprog *g, sset *s, int pc, size_t pos, size_t n, int *
       case RX_EOL:
         if (pos == n) stack[sp++] = p + 1;
         break;
+      case RX_WB:
+      case RX_NWB: {
+        const int pw = pos > 0 && rx_is_word(cp[pos - 1]), nw = pos < n && rx_is_word(cp[pos]);
+        if ((pw != nw) == (I->op == RX_WB)) stack[sp++] = p + 1;
+        break;
+      }
       case RX_MATCH: *match = 1; break;
       default: break;
     }
@@ -1053,7 +1229,7 @@ static int rx_run(const rxprog *g, const uint32_t *cp, size_t n) {
   int match = 0;
   sset *cur = &a, *nxt = &b;
   for (size_t i = 0;; i++) {
-    ss_add(g, cur, 0, i, n, &match, stack); /* unanchored: new thread at every position */
+    ss_add(g, cur, 0, i, n, &match, stack, cp); /* unanchored: new thread at every position */
     if (match || i == n) break;
     nxt->n = 0;
     for (int k = 0; k < cur->n; k++) {
@@ -1063,7 +1239,7 @@ static int rx_run(const rxprog *g, const uint32_t *cp, size_t n) {
         ok = I->c == cp[i];
       else if (I->op == RX_CLASS)
         ok = cs_has(&g->classes[I->c], cp[i]);
-      if (ok) ss_add(g, nxt, cur->dense[k] + 1, i + 1, n, &match, stack);
+      if (ok) ss_add(g, nxt, cur->dense[k] + 1, i + 1, n, &match, stack, cp);
       if (match) break;
     }
     if (match) break;

@@ -171,6 +171,10 @@ CHAINS = {
     "regex_level": [("regex-filter", {"regex": r'^\{"level":"(warn|error)"'}, None)],
     "regex_unbounded": [("regex-filter", {"regex": r"a.*c\d+$"}, None)],
     "regex_unicode": [("regex-filter", {"regex": r"é|\d\d"}, None)],
+    "regex_word_boundary": [("regex-filter", {"regex": r"\btimeout\b|\b\d{3}\b"}, None)],
+    "regex_case_insensitive": [("regex-filter", {"regex": r"(?i)TIMEOUT|(?i:ssn)\s"}, None)],
+    "regex_posix": [("regex-filter", {"regex": r"[[:digit:]]{3}-[[:digit:]]{2}|^[[:upper:]]"}, None)],
+    "map_then_regex_ci": [("map", {}, None), ("regex-filter", {"regex": r"(?i)error"}, None)],
     "map": [("map", {}, None)],
     "filter_json": [("filter_json", {}, None)],
     "filter_json_then_map": [("filter_json", {}, None), ("map", {}, None)],

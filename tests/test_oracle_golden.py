@@ -142,6 +142,18 @@ def test_process_batch_cases(kats):
     (r"a.c", ["abc", "a\nc", "aéc", "ac"]),
     (r"x{2,3}y", ["xy", "xxy", "xxxxy"]),
     (r"", ["", "anything"]),
+    # word boundaries (ASCII text: Unicode \b and Python's agree), inline flags, \A / \z
+    (r"\bfoo\b", ["a foo b", "afoo b", "foo", "foo_", "(foo)", ""]),
+    (r"\Bar\B", ["bars", "ar", "bar", "xarx"]),
+    (r"\b", ["", " ", "a"]),
+    (r"x\b|\by", ["x", "xa", "ay", "a y"]),
+    (r"(?i)timeout", ["TimeOut", "TIMEOUT", "time out", "timeouts"]),
+    (r"(?i)[a-f]{2}\d", ["AB1", "aB2", "ag3"]),
+    (r"(?i:ab)c", ["ABc", "abC", "aBc"]),
+    (r"(?i)[^k]", ["K", "k", "x"]),
+    (r"(?i)sk", ["SK", "\u017fK", "s\u212a", "sx"]),
+    (r"(?s)a.b", ["a\nb", "axb"]),
+    (r"\Aab", ["ab", "xab"]),
 ])
 def test_regex_oracle_vs_python_re(pattern, texts):
     """Cross-check the oracle's regex engine with Python's independent `re` on
@@ -149,7 +161,8 @@ def test_regex_oracle_vs_python_re(pattern, texts):
     ASCII \\w).  Pins the restatement of regex is_match (third-party crate
     regex 1.6.0/1.8.1, absent from /root/reference)."""
     for t in texts:
-        assert O.regex_is_match(pattern, t.encode()) == (re.search(pattern, t) is not None), (pattern, t)
+        py = pattern.replace(r"\z", r"\Z")
+        assert O.regex_is_match(pattern, t.encode()) == (re.search(py, t) is not None), (pattern, t)
 
 
 def test_regex_unicode_classes():
@@ -190,3 +203,13 @@ def test_hashset_init_count_param():
     O.OracleChain([("filter_hashset", {"count": "+7"}, None)])  # usize::from_str takes a leading '+'
     with pytest.raises(O.OracleError):
         O.OracleChain([("filter_hashset", {"count": "4294967296"}, None)])  # usize is u32 on wasm32
+
+
+def test_regex_posix_classes():
+    """[[:name:]] ASCII classes (regex-syntax ClassAsciiKind; Python re has none)."""
+    m = lambda p, t: O.regex_is_match(p, t.encode())  # noqa: E731
+    assert m(r"^[[:digit:]]{3}$", "123") and not m(r"^[[:digit:]]{3}$", "12a")
+    assert m(r"[[:^alpha:]]", "ab1") and not m(r"[[:^alpha:]]", "abc")
+    assert m(r"^[[:xdigit:][:space:]]+$", "fF 09\t") and not m(r"^[[:xdigit:]]+$", "fg")
+    assert m(r"[[:punct:]]", "a,b") and not m(r"[[:punct:]]", "ab")
+    assert m(r"(?i)^[[:upper:]]+$", "abC") and not m(r"^[[:upper:]]+$", "abC")
