@@ -137,7 +137,7 @@ struct BatchStat {
   uint64_t cat_sum;    // aggregate (concat): bytes appended to the accumulator by this batch
   uint64_t err_vpos;   // the failing record's value as it entered the failing stage (byte views:
   uint32_t err_vlen;   //   a projection narrows the view)
-  uint32_t pad2;
+  uint32_t comp;       // header attributes & 7 (the output batch takes the first surviving batch's)
 };
 
 // one kept output record (a compaction descriptor, 64 bytes): enough to
@@ -214,6 +214,8 @@ struct Plan {
   int64_t acc_final;         // aggregate accumulator after the stop batch
   int32_t acc_touched;       // accumulator changed by this call
   int32_t done;              // last batch whose process() call completed (-1 none): state commits through it
+  int32_t comp;              // compression bits of the first surviving batch (set_compression, batch.rs:144-153)
+  int32_t pad_;
   uint64_t cat_final;        // aggregate (concat): accumulator bytes appended through the stop batch
 };
 
@@ -407,6 +409,18 @@ struct SfArgs {
   uint64_t n0;             // new insertions before this call
   uint64_t limit;
   unsigned long long* scal;  // [0] entries after commit [1] arena bytes [2] N after commit [3] keeps
+};
+// record-section decompression at ingest (fsg_codec_dev.h, k_dec_*)
+struct DecArgs {
+  const uint8_t* src;     // the slice as stored
+  const uint64_t* bpos;   // its batches
+  const uint8_t* codec;   // attributes & 7 per batch (0, 1 gzip, 2 snappy, 3 lz4)
+  uint32_t nb;
+  int64_t* dsize;         // decompressed section length / DEC_BAD / DEC_UNSUP
+  uint8_t* dst;           // the decompressed slice
+  const uint64_t* npos;   // batch positions in dst
+  int32_t* status;        // writing pass: 0 ok, -1 decode / checksum error
+  uint64_t* cnt;          // record count estimate of each new section
 };
 constexpr uint32_t kSkipEntry = 0xFFFFFFFFu;
 constexpr uint32_t kAjLds = 4096;  // k_aggj_text keeps up to this many values in LDS

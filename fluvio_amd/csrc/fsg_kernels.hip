@@ -22,6 +22,7 @@
 #include <type_traits>
 
 #include "fsg_device.h"
+#include "fsg_codec_dev.h"
 #include "fsg_json_dev.h"
 #include "fsg_json_dfa.h"
 
@@ -1003,6 +1004,7 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
     L.bs.base_offset = (int64_t)rd_be(h, 8);
     L.bs.lod_in = (int32_t)rd_be(h + 23, 4);
     L.bs.first_ts = (int64_t)rd_be(h + 27, 8);
+    L.bs.comp = (uint32_t)rd_be(h + 22, 1) & 7u;
     L.bs.err_code = 0;
     L.bs.err_pos = 0;
     L.bs.err_od = 0;
@@ -2055,6 +2057,7 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
   KeptRec p_d = {};
   int64_t p_base = 0, p_ts0 = 0;
   int32_t p_lod = 0;
+  uint32_t p_comp = 0;
   uint32_t p_nkeep = 0, p_sec = 0;
   auto flush = [&]() {
     if (p_b == 0xFFFFFFFFu) return;
@@ -2070,6 +2073,7 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
         st.base_offset = p_base;
         st.lod_in = p_lod;
         st.first_ts = p_ts0;
+        st.comp = p_comp;
         st.flags = BF_LAST_STAGE;
         st.nkeep = p_nkeep;
         st.nout = p_nkeep;
@@ -2099,6 +2103,7 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
     const uint32_t batch_len = (uint32_t)rd_be(h + 8, 4);
     const int32_t lod_in = (int32_t)rd_be(h + 23, 4);
     const int64_t first_ts = (int64_t)rd_be(h + 27, 8);
+    const uint32_t comp = (uint32_t)h[22] & 7u;
     const uint64_t sec0 = pos + 57;
     const uint64_t sec_end = pos + 12 + (uint64_t)batch_len;  // framing validated at ingest
     const uint32_t sec_len = (uint32_t)(sec_end - sec0);
@@ -2260,6 +2265,7 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
     }
     p_base = base_offset;
     p_ts0 = first_ts;
+    p_comp = comp;
     p_lod = lod_in;
     p_nkeep = (uint32_t)__popcll(alive);
     p_sec = sec_len;
@@ -2561,6 +2567,7 @@ __global__ void k_plan(PlanArgs a) {
   if (f != NONE && f <= stop) {
     p.first = (int32_t)f;
     p.base_offset = a.bstat[f].base_offset;  // set before the max_bytes check (batch.rs:85-91)
+    p.comp = (int32_t)a.bstat[f].comp;       // set_compression of the first surviving batch
     if ((int64_t)f <= last) {
       p.last = (int32_t)last;
       const ScanRow rl = incl_at(a, (uint32_t)last);
@@ -2597,7 +2604,7 @@ __global__ void k_header(const Plan* plan, uint8_t* out) {
   be(12, (uint32_t)-1, 4);  // partition_leader_epoch
   h[16] = 2;                // magic
   be(17, 0, 4);             // crc placeholder
-  be(21, 0, 2);             // attributes: compression None of the first surviving batch
+  be(21, (uint32_t)p.comp & 7u, 2);  // attributes: the first surviving batch's compression
   be(23, (uint32_t)p.lod, 4);
   be(27, (uint64_t)-1, 8);  // first_timestamp
   be(35, (uint64_t)-1, 8);  // max_time_stamp
@@ -3678,6 +3685,65 @@ __global__ __launch_bounds__(256) void k_verify_crc(const uint8_t* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// record-section decompression at ingest (fsg_codec_dev.h): sizing pass, a
+// writing pass into the decompressed slice (batch header copied with
+// batch_len = 45 + decompressed length, compression bits kept for the output
+// header), the record counts of the new sections
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t dec_rem(const uint8_t* src, uint64_t pos) {
+  return (uint64_t)__builtin_bswap32(ld_u32_at(src + pos + 8)) - 45;  // framing checked batch_len >= 45
+}
+__global__ __launch_bounds__(256) void k_dec_size(DecArgs a) {
+  for (uint32_t b = blockIdx.x * 256 + threadIdx.x; b < a.nb; b += gridDim.x * 256) {
+    const uint64_t pos = a.bpos[b], rem = dec_rem(a.src, pos);
+    const uint32_t codec = a.codec[b];
+    if (!codec) {
+      a.dsize[b] = (int64_t)rem;
+      continue;
+    }
+    DecOut o{nullptr, 0, 0, false};
+    a.dsize[b] = dev_decompress(codec, a.src + pos + 57, rem, o, &g_crc_z16[0][0]);
+  }
+}
+__global__ __launch_bounds__(256) void k_dec_write(DecArgs a) {
+  for (uint32_t b = blockIdx.x * 256 + threadIdx.x; b < a.nb; b += gridDim.x * 256) {
+    const uint32_t codec = a.codec[b];
+    if (!codec) continue;
+    const uint64_t pos = a.bpos[b], rem = dec_rem(a.src, pos), np = a.npos[b];
+    const int64_t ds = a.dsize[b];
+    uint8_t* d = a.dst + np;
+    for (int k = 0; k < 57; k++) d[k] = a.src[pos + k];
+    const uint32_t bl = (uint32_t)(45 + ds);
+    d[8] = (uint8_t)(bl >> 24);
+    d[9] = (uint8_t)(bl >> 16);
+    d[10] = (uint8_t)(bl >> 8);
+    d[11] = (uint8_t)bl;
+    DecOut o{d + 57, 0, (uint64_t)ds, true};
+    const int64_t r = dev_decompress(codec, a.src + pos + 57, rem, o, &g_crc_z16[0][0]);
+    a.status[b] = r == ds ? 0 : -1;
+  }
+}
+__global__ __launch_bounds__(256) void k_dec_copy(DecArgs a) {  // uncompressed batches, a wave each
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= a.nb || a.codec[b]) return;
+  const uint64_t pos = a.bpos[b], n = 57 + dec_rem(a.src, pos), np = a.npos[b];
+  for (uint64_t k = lane_id(); k < n; k += 64) a.dst[np + k] = a.src[pos + k];
+}
+__global__ __launch_bounds__(256) void k_dec_count(DecArgs a) {
+  for (uint32_t b = blockIdx.x * 256 + threadIdx.x; b < a.nb; b += gridDim.x * 256) {
+    const uint64_t np = a.npos[b], ds = (uint64_t)a.dsize[b];
+    uint64_t c = 0;
+    if (ds >= 4) {  // Vec<Record> count (FileBatchIterator framing's estimate)
+      const int32_t v = (int32_t)__builtin_bswap32(ld_u32_at(a.dst + np + 57));
+      c = v > 0 ? (uint64_t)v : 0;
+      const uint64_t mx = (ds - 4) / 7;
+      c = c < mx ? c : mx;
+    }
+    a.cnt[b] = c;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_write_lean: the output of one batch of verbatim records (KM_COPY /
 // KM_UPPER: filters, uppercase maps, projections) assembled in LDS and stored
 // with 16-byte stores, for batches of many small records (where k_write's
@@ -4535,5 +4601,17 @@ void launch_verify_crc(const uint8_t* slice, const uint64_t* bpos, uint32_t nb, 
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const uint32_t g = std::min<uint32_t>((nb + 3) / 4, (uint32_t)std::max(1, cus) * 8u);
   hipLaunchKernelGGL(k_verify_crc, dim3(g), dim3(256), 0, s, slice, bpos, nb, bad, flags);
+}
+void launch_decompress(const DecArgs& a, int pass, hipStream_t s) {
+  if (!a.nb) return;
+  const uint32_t g = std::min<uint32_t>((a.nb + 255) / 256, 4096);
+  if (pass == 0) {
+    hipLaunchKernelGGL(k_dec_size, dim3(g), dim3(256), 0, s, a);
+  } else if (pass == 1) {
+    hipLaunchKernelGGL(k_dec_write, dim3(g), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_dec_copy, dim3((a.nb + 3) / 4), dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(k_dec_count, dim3(g), dim3(256), 0, s, a);
+  }
 }
 }  // namespace fsg

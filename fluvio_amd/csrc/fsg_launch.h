@@ -37,6 +37,8 @@ void launch_sf_commit(const SfArgs& a, hipStream_t s);     // after k_plan: stat
 // CRC32C check of every stored batch (report only; bad[0] count, bad[1] first index)
 void launch_verify_crc(const uint8_t* slice, const uint64_t* bpos, uint32_t nb, unsigned long long* bad,
                        uint32_t* flags, hipStream_t s);
+// record-section decompression: pass 0 sizes, 1 writes, 2 record counts
+void launch_decompress(const DecArgs& a, int pass, hipStream_t s);
 // device framing (FrameArgs)
 void launch_frame_cand(const FrameArgs& a, uint32_t nchunks, uint64_t* tsum, hipStream_t s);
 void launch_frame_compact(const FrameArgs& a, uint32_t nchunks, hipStream_t s);

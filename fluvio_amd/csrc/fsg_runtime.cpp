@@ -398,6 +398,7 @@ struct fsg_slice {
   int tail_status = 0;
   uint64_t header_bytes = 0;  // 57 B per framed batch + the record sections
   bool device_framed = false; // framed by k_frame_* (else by the host walk)
+  bool decompressed = false;  // compressed sections were decompressed on the GPU at ingest
 };
 
 struct fsg_chain {
@@ -738,7 +739,7 @@ extern "C" void fsg_chain_free(fsg_chain* c) { delete c; }
 namespace {
 // FileBatchIterator framing (iterators.rs:55-160): header -> batch_len -> record section
 int frame(const uint8_t* s, size_t len, std::vector<uint64_t>& bpos, std::vector<uint64_t>& rbase, uint64_t& nrec,
-          int& tail, uint64_t& hdr_bytes) {
+          int& tail, uint64_t& hdr_bytes, std::vector<uint8_t>* codecs = nullptr) {
   size_t pos = 0;
   nrec = 0;
   tail = 0;
@@ -760,12 +761,16 @@ int frame(const uint8_t* s, size_t len, std::vector<uint64_t>& bpos, std::vector
       break;
     }
     const int comp = attrs & 7;
-    if (comp != 0) {
-      tail = comp <= 4 ? FSG_E_UNSUPPORTED : FSG_E_IO;  // compressed sections: not on the GPU path yet
+    // gzip / snappy / lz4 sections are decompressed on the GPU after framing
+    // (decompress_slice); zstd is not restated (unsupported), codes > 4 are the
+    // iterator's "unknown compression value" io::Error
+    if (comp > 3 || (comp != 0 && !codecs)) {
+      tail = comp <= 4 ? FSG_E_UNSUPPORTED : FSG_E_IO;
       break;
     }
+    if (codecs) codecs->push_back((uint8_t)comp);
     uint64_t cnt = 0;
-    if (rem >= 4) {
+    if (rem >= 4 && comp == 0) {
       int32_t c = (int32_t)rd_be(s + pos + 57, 4);
       cnt = c > 0 ? (uint64_t)c : 0;
       cnt = std::min<uint64_t>(cnt, (rem - 4) / 7);  // a record is at least 7 bytes
@@ -857,10 +862,106 @@ int frame_on_device(fsg_slice* sl, hipStream_t st, int* fallback) {
     *fallback = 1;
     return FSG_OK;
   }
+  if (sc[1] == 2) {  // a compressed batch on the chain: the host walk frames, the GPU decompresses
+    *fallback = 1;
+    return FSG_OK;
+  }
   sl->nb = (uint32_t)sc[4];
   sl->nrec = sc[5];
-  sl->tail_status = sc[1] == 1 ? FSG_E_IO : sc[1] == 2 ? FSG_E_UNSUPPORTED : 0;
+  sl->tail_status = sc[1] == 1 ? FSG_E_IO : 0;
   sl->header_bytes = sc[2];
+  return FSG_OK;
+}
+
+// Compressed record sections (FileBatchIterator: compression.uncompress,
+// iterators.rs:136-156) decompressed on the GPU into a new slice where every
+// batch is stored uncompressed (header kept, batch_len = 45 + the new length,
+// the compression bits kept for the output header).  A batch that fails to
+// decode ends the slice there with the iterator's io::Error (zstd:
+// unsupported), like the reference's Err at that batch.
+int decompress_slice(fsg_slice* sl, const std::vector<uint64_t>& bpos, const std::vector<uint8_t>& codecs,
+                     hipStream_t st) {
+  const uint32_t nb = (uint32_t)bpos.size();
+  DevBuf dbpos, dcodec, dsize, npos, status, cnt;
+  HIPCHK(dbpos.ensure(std::max<size_t>(nb, 1) * 8));
+  HIPCHK(dcodec.ensure(std::max<size_t>(nb, 1)));
+  HIPCHK(dsize.ensure(std::max<size_t>(nb, 1) * 8));
+  HIPCHK(npos.ensure(std::max<size_t>(nb, 1) * 8));
+  HIPCHK(status.ensure(std::max<size_t>(nb, 1) * 4));
+  HIPCHK(cnt.ensure(std::max<size_t>(nb, 1) * 8));
+  HIPCHK(hipMemcpyAsync(dbpos.p, bpos.data(), nb * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(dcodec.p, codecs.data(), nb, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemsetAsync(status.p, 0, std::max<size_t>(nb, 1) * 4, st));
+  DecArgs a{};
+  a.src = sl->data.as<uint8_t>();
+  a.bpos = dbpos.as<uint64_t>();
+  a.codec = dcodec.as<uint8_t>();
+  a.nb = nb;
+  a.dsize = dsize.as<int64_t>();
+  a.npos = npos.as<uint64_t>();
+  a.status = status.as<int32_t>();
+  a.cnt = cnt.as<uint64_t>();
+  launch_decompress(a, 0, st);
+  std::vector<int64_t> ds(nb);
+  HIPCHK(hipMemcpyAsync(ds.data(), dsize.p, nb * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  uint32_t keep = nb;
+  int tail = sl->tail_status;
+  for (uint32_t b = 0; b < nb; b++)
+    if (ds[b] < 0 || ds[b] > 0x7FFFFFFFll - 45) {
+      keep = b;
+      tail = ds[b] == -2 ? FSG_E_UNSUPPORTED : FSG_E_IO;  // DEC_UNSUP: zstd
+      break;
+    }
+  std::vector<uint64_t> np(nb);
+  uint64_t total = 0;
+  for (uint32_t b = 0; b < keep; b++) {
+    np[b] = total;
+    total += 57 + (uint64_t)ds[b];
+  }
+  DevBuf nd;
+  const size_t alloc = ((total + 15) & ~(size_t)15) + kSlicePad + kWin;
+  HIPCHK(nd.ensure(alloc));
+  HIPCHK(hipMemsetAsync(nd.p, 0, alloc, st));
+  HIPCHK(hipMemcpyAsync(npos.p, np.data(), std::max<size_t>(keep, 1) * 8, hipMemcpyHostToDevice, st));
+  a.nb = keep;
+  a.dst = nd.as<uint8_t>();
+  launch_decompress(a, 1, st);
+  launch_decompress(a, 2, st);
+  HIPCHK(hipGetLastError());
+  std::vector<int32_t> stv(std::max<uint32_t>(keep, 1));
+  std::vector<uint64_t> cv(std::max<uint32_t>(keep, 1));
+  HIPCHK(hipMemcpyAsync(stv.data(), status.p, keep * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(cv.data(), cnt.p, keep * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  for (uint32_t b = 0; b < keep; b++)
+    if (stv[b]) {  // a checksum (or stream) error found while writing
+      keep = b;
+      tail = FSG_E_IO;
+      total = np[b];
+      break;
+    }
+  std::vector<uint64_t> rb(std::max<uint32_t>(keep, 1));
+  uint64_t nrec = 0;
+  for (uint32_t b = 0; b < keep; b++) {
+    rb[b] = nrec;
+    nrec += cv[b];
+  }
+  HIPCHK(sl->bpos.ensure(std::max<size_t>(keep, 1) * 8));
+  HIPCHK(sl->rbase.ensure(std::max<size_t>(keep, 1) * 8));
+  if (keep) {
+    HIPCHK(hipMemcpyAsync(sl->bpos.p, np.data(), keep * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(sl->rbase.p, rb.data(), keep * 8, hipMemcpyHostToDevice, st));
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  std::swap(sl->data.p, nd.p);
+  std::swap(sl->data.cap, nd.cap);
+  sl->len = total;
+  sl->nb = keep;
+  sl->nrec = nrec;
+  sl->tail_status = tail;
+  sl->header_bytes = total;
+  sl->decompressed = true;
   return FSG_OK;
 }
 
@@ -883,7 +984,10 @@ int upload_slice(fsg_engine* e, const uint8_t* s, size_t len, fsg_slice* sl, hip
   if (fallback) {
     sl->device_framed = false;
     std::vector<uint64_t> bpos, rbase;
-    frame(s, len, bpos, rbase, sl->nrec, sl->tail_status, sl->header_bytes);
+    std::vector<uint8_t> codecs;
+    frame(s, len, bpos, rbase, sl->nrec, sl->tail_status, sl->header_bytes, &codecs);
+    if (std::any_of(codecs.begin(), codecs.end(), [](uint8_t c) { return c != 0; }))
+      return decompress_slice(sl, bpos, codecs, stream);
     sl->nb = (uint32_t)bpos.size();
     HIPCHK(sl->bpos.ensure(std::max<size_t>(1, bpos.size()) * 8));
     HIPCHK(sl->rbase.ensure(std::max<size_t>(1, rbase.size()) * 8));

@@ -2050,16 +2050,23 @@ int orc_process_batch(orc_chain *c, const uint8_t *slice, size_t slice_len, uint
       return out->status;
     }
     int comp = b_attr & 7;
-    if (comp != 0) {
-      rv_free(&acc);
-      out->status = comp <= 4 ? ORC_E_UNSUPPORTED : ORC_E_IO;
-      return out->status;
-    }
     const uint8_t *recs = slice + pos + 57;
+    uint8_t *dec = NULL;
+    size_t rlen = rem;
+    if (comp != 0) { /* iterators.rs:136-156: compression.uncompress(records) (fsg_codec.c) */
+      int drc = comp > 4 ? -1 : orc_decompress(comp, recs, rem, &dec, &rlen);
+      if (drc) {
+        rv_free(&acc);
+        out->status = drc == ORC_E_UNSUPPORTED ? ORC_E_UNSUPPORTED : ORC_E_IO;
+        return out->status;
+      }
+      recs = dec;
+    }
     pos += 57 + rem;
     /* chain.process(SmartModuleInput::new(records, base_offset, first_timestamp)) */
     orc_result pr;
-    int rc = orc_chain_process(c, recs, rem, b_base, b_first_ts, &pr);
+    int rc = orc_chain_process(c, recs, rlen, b_base, b_first_ts, &pr);
+    free(dec);
     out->m_bytes_in += pr.m_bytes_in;
     out->m_invocations += pr.m_invocations;
     out->m_records_out += pr.m_records_out;

@@ -84,6 +84,13 @@ int orc_chain_look_back(orc_chain *c, size_t stage, const uint8_t *raw, size_t r
 void orc_result_free(orc_result *r);
 void orc_free(void *p);
 
+/* record-section codecs (fsg_codec.c): Compression::uncompress for codec
+ * 1 gzip, 2 snappy, 3 lz4 (0 ok, -1 decode error, ORC_E_UNSUPPORTED zstd) and
+ * the test-data encoders */
+int orc_decompress(int codec, const uint8_t *s, size_t n, uint8_t **out, size_t *out_len);
+int orc_compress(int codec, const uint8_t *s, size_t n, int flags, uint8_t **out, size_t *out_len);
+uint32_t orc_xxh32(const uint8_t *p, size_t n, uint32_t seed);
+
 /* regex oracle exposed for cross-checks with an independent engine */
 int orc_regex_is_match(const char *pattern, const uint8_t *text, size_t n, int *is_match);
 

@@ -86,6 +86,14 @@ def lib():
                                        ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), ctypes.POINTER(ctypes.c_size_t),
                                        ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_void_p),
                                        ctypes.POINTER(ctypes.c_size_t)]
+        for fn in (L.orc_decompress, L.orc_compress):
+            fn.restype = ctypes.c_int
+        L.orc_decompress.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t,
+                                     ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]
+        L.orc_compress.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int,
+                                   ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]
+        L.orc_xxh32.restype = ctypes.c_uint32
+        L.orc_xxh32.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32]
         L.orc_varint_encode.restype = ctypes.c_size_t
         L.orc_varint_encode.argtypes = [ctypes.c_int64, ctypes.c_char_p]
         _lib = L
@@ -94,6 +102,37 @@ def lib():
 
 def crc32c(data: bytes) -> int:
     return lib().orc_crc32c(data, len(data))
+
+
+CODECS = {"gzip": 1, "snappy": 2, "lz4": 3, "zstd": 4}
+
+
+def decompress(codec: int, data: bytes):
+    """Compression::uncompress (fsg_codec.c): bytes, or None on a decode error."""
+    p, n = ctypes.c_void_p(), ctypes.c_size_t()
+    rc = lib().orc_decompress(codec, data, len(data), ctypes.byref(p), ctypes.byref(n))
+    if rc == -1:
+        return None
+    if rc:
+        raise OracleError(rc, "unsupported codec")
+    out = ctypes.string_at(p, n.value)
+    lib().orc_free(p)
+    return out
+
+
+def compress(codec: int, data: bytes, flags: int = 0) -> bytes:
+    """Test-data encoders: 1 gzip (flags = zlib level), 2 snappy frame, 3 lz4 frame."""
+    p, n = ctypes.c_void_p(), ctypes.c_size_t()
+    rc = lib().orc_compress(codec, data, len(data), flags, ctypes.byref(p), ctypes.byref(n))
+    if rc:
+        raise OracleError(rc, "compress")
+    out = ctypes.string_at(p, n.value)
+    lib().orc_free(p)
+    return out
+
+
+def xxh32(data: bytes, seed: int = 0) -> int:
+    return lib().orc_xxh32(data, len(data), seed)
 
 
 def varint_encode(v: int) -> bytes:

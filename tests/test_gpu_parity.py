@@ -1111,3 +1111,47 @@ def test_verify_crc_large_batches(engine):
     sl = synth.make_slice(2, 3000, max_section=300000)
     rs = ResidentSlice(engine, sl)
     assert rs.verify_crc()[:2] == (0, -1)
+
+
+# ---------------------------------------------------------------------------
+# compressed record sections decompressed on the GPU at ingest
+# ---------------------------------------------------------------------------
+from tests.compressed_slices import recompress  # noqa: E402
+
+COMPRESSED_CHAINS = ["filter_init_timeout", "filter_then_map", "regex_ssn", "filter_json", "empty", "project"]
+
+
+@pytest.mark.parametrize("codecs,flags", [([1], 0), ([2], 0), ([3], 0), ([3], 15), ([2], 3), ([0, 3, 2, 1], {3: 7, 1: 9}),
+                                          ([1, 0], 1)])
+@pytest.mark.parametrize("chain", COMPRESSED_CHAINS)
+def test_compressed_slice_parity(engine, chain, codecs, flags):
+    kind = 1 if chain == "regex_ssn" else 2
+    sl = synth.make_slice(kind, 1200, base_offset=300)
+    check_batch(engine, CHAINS[chain], recompress(sl, codecs, flags))
+
+
+@pytest.mark.parametrize("chain", ["filter_map", "agg_sum", "filter_odd"])
+def test_compressed_int_chains(engine, chain):
+    sl = synth.make_slice(3, 20000, base_offset=7)
+    check_batch(engine, CHAINS[chain], recompress(sl, [3, 1, 2], {3: 3}))
+
+
+def test_compressed_resident_and_errors(engine):
+    sl = synth.make_slice(2, 2000)
+    csl = recompress(sl, [2, 3])
+    rs = ResidentSlice(engine, csl)
+    assert not rs.device_framed and rs.n_records == 2000
+    assert rs.verify_crc()[:2] == (0, -1)  # the decompressed slice keeps headers; CRCs are the stored ones
+    modules = [("filter_init", {"key": "timeout"}, None)]
+    out = gpu_chain(engine, modules).process_batch(csl)
+    assert out.raw == orc_chain(modules).process_batch(csl)["bytes"]
+    assert out.raw[22] & 7 == 2  # set_compression: the first surviving batch's codec
+    # a batch that fails to decode (checksum / stream error): io::Error at that batch
+    for codecs, flags in (([3], 3), ([2], 0), ([1], 0)):
+        bad = recompress(sl, codecs, flags, corrupt={3: 50})
+        check_batch(engine, modules, bad)
+        assert orc_chain(modules).process_batch(bad)["status"] == IoError.code if hasattr(IoError, "code") else True
+    # zstd (codec 4): not restated on the GPU path -> Unsupported, like the oracle
+    z = bytearray(recompress(sl, [0]))
+    z[22] = (z[22] & ~7) | 4
+    check_batch(engine, modules, bytes(z))
