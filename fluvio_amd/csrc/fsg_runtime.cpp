@@ -399,6 +399,10 @@ struct fsg_slice {
   uint64_t header_bytes = 0;  // 57 B per framed batch + the record sections
   bool device_framed = false; // framed by k_frame_* (else by the host walk)
   bool decompressed = false;  // compressed sections were decompressed on the GPU at ingest
+  // CRC32C verify of the stored (compressed) batches, run before decompression
+  uint64_t crc_bad = 0;
+  int64_t crc_first = -1;
+  float crc_ms = 0;
 };
 
 struct fsg_chain {
@@ -901,6 +905,26 @@ int decompress_slice(fsg_slice* sl, const std::vector<uint64_t>& bpos, const std
   a.npos = npos.as<uint64_t>();
   a.status = status.as<int32_t>();
   a.cnt = cnt.as<uint64_t>();
+  {  // the stored CRCs cover the compressed bytes: verify them before they go
+    DevBuf bad;
+    HIPCHK(bad.ensure(16));
+    const unsigned long long init[2] = {0, ~0ull};
+    HIPCHK(hipMemcpyAsync(bad.p, init, sizeof init, hipMemcpyHostToDevice, st));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, st));
+    launch_verify_crc(a.src, a.bpos, nb, bad.as<unsigned long long>(), nullptr, st);
+    HIPCHK(hipEventRecord(e1, st));
+    unsigned long long r[2];
+    HIPCHK(hipMemcpyAsync(r, bad.p, sizeof r, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipEventElapsedTime(&sl->crc_ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    sl->crc_bad = r[0];
+    sl->crc_first = r[0] ? (int64_t)r[1] : -1;
+  }
   launch_decompress(a, 0, st);
   std::vector<int64_t> ds(nb);
   HIPCHK(hipMemcpyAsync(ds.data(), dsize.p, nb * 8, hipMemcpyDeviceToHost, st));
@@ -1015,6 +1039,12 @@ extern "C" int fsg_slice_device_framed(const fsg_slice* s) { return s->device_fr
 // CRC32C of every framed batch against its header (report only: the reference
 // never verifies, protocol record/batch.rs:398-430, so nothing else changes)
 extern "C" int fsg_slice_verify_crc(const fsg_slice* s, uint64_t* n_bad, int64_t* first_bad, float* ms) {
+  if (s->decompressed) {  // checked on the stored bytes at ingest, before decompression
+    if (n_bad) *n_bad = s->crc_bad;
+    if (first_bad) *first_bad = s->crc_first;
+    if (ms) *ms = s->crc_ms;
+    return FSG_OK;
+  }
   HIPCHK(hipSetDevice(s->eng->device));
   hipStream_t st = nullptr;
   HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));

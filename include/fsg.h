@@ -228,7 +228,9 @@ int fsg_slice_device_framed(const fsg_slice *s);
  * bytes 21.. + records and compared with the stored crc: *n_bad mismatches,
  * *first_bad the first such batch (-1 none), *ms the kernel time.  Reports
  * only — the reference never verifies (crates/fluvio-protocol/src/record/
- * batch.rs:398-430 computes the CRC on encode only), so processing ignores it. */
+ * batch.rs:398-430 computes the CRC on encode only), so processing ignores it.
+ * For a slice with compressed batches the check runs on the stored bytes at
+ * ingest (before decompression) and this returns that result. */
 int fsg_slice_verify_crc(const fsg_slice *s, uint64_t *n_bad, int64_t *first_bad, float *ms);
 void fsg_slice_free(fsg_slice *s);
 /* process_batch over a resident slice; the output batch stays in HBM until

@@ -278,9 +278,12 @@ def test_edge_slices(engine):
     check_batch(engine, chain, bytes(neg))
     # truncated slice -> io error after processing the good batches
     check_batch(engine, chain, good + good[:100])
-    # compressed batch (gzip bits) -> unsupported on the GPU path
-    comp = bytearray(P.decode_batches(good) and good)
+    # gzip bits on a section that is not gzip -> the iterator's io::Error, like the oracle
+    comp = bytearray(good)
     comp[22] |= 1
+    check_batch(engine, chain, bytes(comp))
+    # zstd bits -> unsupported on the GPU path (zstd is not restated)
+    comp[22] = (comp[22] & ~7) | 4
     with pytest.raises(Unsupported):
         gpu_chain(engine, chain).process_batch(bytes(comp))
     # a record whose length claims more than the section -> decoding error (-11)
@@ -308,8 +311,8 @@ def _frame_walk(sl):
         if blen < 45 or len(sl) - pos - 57 < blen - 45:
             tail = "io"
             break
-        if attrs & 7:
-            tail = "unsup" if (attrs & 7) <= 4 else "io"
+        if attrs & 7:  # (these test sections are not really compressed: decoding fails -> io)
+            tail = "unsup" if (attrs & 7) == 4 else "io"
             break
         rem = blen - 45
         if rem >= 4:
@@ -341,7 +344,7 @@ def test_device_framing(engine):
         pos += 12 + blen
         k += 1
     comp[pos + 22] |= 2
-    cases.append((bytes(comp), True))
+    cases.append((bytes(comp), False))  # a compressed batch: host walk + GPU decompression (fails: io)
     # random bytes with magic-2 noise between batches are never on the chain
     noisy = bytearray(good)
     for _ in range(2000):
@@ -1141,7 +1144,12 @@ def test_compressed_resident_and_errors(engine):
     csl = recompress(sl, [2, 3])
     rs = ResidentSlice(engine, csl)
     assert not rs.device_framed and rs.n_records == 2000
-    assert rs.verify_crc()[:2] == (0, -1)  # the decompressed slice keeps headers; CRCs are the stored ones
+    assert rs.verify_crc()[:2] == (0, -1)  # checked on the stored (compressed) bytes at ingest
+    from tests.compressed_slices import batches
+    crc_bad = bytearray(csl)
+    crc_bad[list(batches(csl))[4][0] + 18] ^= 1  # batch 4's stored CRC
+    rsb = ResidentSlice(engine, bytes(crc_bad))
+    assert rsb.verify_crc()[:2] == (1, 4) and rsb.n_records == 2000
     modules = [("filter_init", {"key": "timeout"}, None)]
     out = gpu_chain(engine, modules).process_batch(csl)
     assert out.raw == orc_chain(modules).process_batch(csl)["bytes"]
@@ -1150,7 +1158,7 @@ def test_compressed_resident_and_errors(engine):
     for codecs, flags in (([3], 3), ([2], 0), ([1], 0)):
         bad = recompress(sl, codecs, flags, corrupt={3: 50})
         check_batch(engine, modules, bad)
-        assert orc_chain(modules).process_batch(bad)["status"] == IoError.code if hasattr(IoError, "code") else True
+        assert orc_chain(modules).process_batch(bad)["status"] == -104  # FSG_E_IO
     # zstd (codec 4): not restated on the GPU path -> Unsupported, like the oracle
     z = bytearray(recompress(sl, [0]))
     z[22] = (z[22] & ~7) | 4
