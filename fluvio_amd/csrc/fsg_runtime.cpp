@@ -1773,7 +1773,8 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   // output bytes: staged in LDS (k_write_lean); larger records: k_write's
   // record-by-record wave copies (one wave pass per ~1 KiB record)
   const bool verbatim = !has_agg && !has_array && c->hdesc.out_type != VT_I32;
-  if (verbatim && nblk && p.n_records && p.rec_bytes < 512ull * p.n_records)
+  static const bool force_lean = getenv("FSG_WRITE_LEAN") != nullptr;  // experiment toggle
+  if (verbatim && nblk && p.n_records && (force_lean || p.rec_bytes < 512ull * p.n_records))
     launch_write_lean(wa, nblk, st);
   else
     launch_write(wa, nblk, st);
