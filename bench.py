@@ -49,6 +49,10 @@ WORKLOADS = {
                       "CRC32C"),
     "c4-array-map": (5, [("array_map_json_array", {}, None)], 4_000_000,
                      "array_map_json_array exploding JSON arrays of 1-16 ints / short strings"),
+    "f4-dedup": (3, [("filter_hashset", {}, None)], 4_000_000,
+                 "filter_hashset dedup (BoundedHashSet, unbounded) over decimal i32 records in [-1000, 1000]; "
+                 "steady state: the state persists across steps, so after the first step every value is a "
+                 "duplicate (the decisions, table build and compaction still run over every record)"),
 }
 C5 = {"partitions": 64, "records_per_partition": 500_000,
       "modules": [("aggregate-sum", {}, None)],
@@ -60,7 +64,8 @@ C5K = {"partitions": 64, "records_per_partition": 50_000, "keys": 1024,
                       "(1024 keys routed by SipHash, ~16 per partition), per-key u32 sums, every record's output = "
                       "the pretty-printed map; each step the ranks' keyed states are merged topic-wide "
                       "(all_gather over RCCL + per-key sum on the GPU)"}
-EXTRA = ["c1-regex", "c2-json", "c3-filter-map", "c4-array-map", "c5-keyed-agg", "c5-agg-sum"]
+EXTRA = ["c1-regex", "c2-json", "c3-filter-map", "c4-array-map", "c5-keyed-agg", "c5-agg-sum", "f4-dedup",
+         "f3-one-record"]
 C5_ALL = ("c5-keyed-agg", "c5-agg-sum")
 PEAK_GBPS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
@@ -70,7 +75,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2-substring", choices=sorted(WORKLOADS) + list(C5_ALL))
+    ap.add_argument("--workload", default="c2-substring", choices=sorted(WORKLOADS) + list(C5_ALL) + ["f3-one-record"])
     ap.add_argument("--records", type=int, default=0, help="records per GPU of the headline workload (0 = default)")
     ap.add_argument("--only", action="store_true", help="time the headline workload only (no `workloads`)")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="records per CPU-baseline process")
@@ -232,6 +237,8 @@ def cpu_baselines_first(ctx, names):
         return {}
     out = {}
     for w in names:
+        if w == "f3-one-record":
+            continue
         if w == "c5-agg-sum":
             out[w] = cpu_baseline(3, C5["modules"], min(a.cpu_sample, C5["records_per_partition"]))
         elif w == "c5-keyed-agg":
@@ -494,7 +501,37 @@ def run_c5k(ctx, cpu):
     return res
 
 
+def run_one_record(ctx, cpu):
+    """f3: the producer's one-record path (crates/fluvio/src/producer/mod.rs:430-473
+    -> SmartModuleChainInstance::process of one SmartModuleInput): latency of one
+    fsg_chain_process call (upload, the kernel chain, download) per record."""
+    from fluvio_amd import protocol as P
+    from fluvio_amd.smartengine import (SmartEngine, SmartModuleChainBuilder, SmartModuleConfig,
+                                        SmartModuleInput, builtin)
+    engine = SmartEngine(ctx.local)
+    b = SmartModuleChainBuilder.default()
+    b.add_smart_module(SmartModuleConfig.builder().param("key", "timeout").build(), builtin("filter_init"))
+    chain = b.initialize(engine)
+    inp = SmartModuleInput.try_from_records([P.Record.new(b'{"level":"warn","message":"request timeout"}')])
+    for _ in range(20):
+        chain.process(inp)
+    n = 300
+    t0 = time.perf_counter()
+    for _ in range(n):
+        out = chain.process(inp)
+    dt = (time.perf_counter() - t0) / n
+    assert len(out.successes) == 1
+    return {"metric": "latency per one-record process() call", "value": dt * 1e6, "unit": "us",
+            "higher_is_better": False, "calls": n, "records_per_s": 1.0 / dt, "ms_per_step": dt * 1e3,
+            "scaling": "weak", "dtype": "u8",
+            "config": {"workload": "f3-one-record", "chain": ["filter_init"],
+                       "description": "fsg_chain_process of a one-record SmartModuleInput (H2D upload, eval, "
+                                      "plan with one host sync, write, CRC, D2H of the output)"}}
+
+
 def run_workload(ctx, w, nrec, cpu):
+    if w == "f3-one-record":
+        return run_one_record(ctx, cpu)
     if w == "c5-keyed-agg":
         return run_c5k(ctx, cpu)
     if w == "c5-agg-sum":

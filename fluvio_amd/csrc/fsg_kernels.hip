@@ -1265,7 +1265,7 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
 // k_eval: batches blockIdx.x (direct mode) or the deferred list written by
 // k_eval_lean (list mode: a.list[0] = count, a.list[1..] = batch indices)
 template <uint32_t kOps>
-__global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : 2) void k_eval(EvalArgs a) {
+__global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : (kOps == kOpsArray ? 3 : 2)) void k_eval(EvalArgs a) {
   __shared__ WaveLds L;
   const uint32_t n = a.list ? a.list[0] : a.nbatches;
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
