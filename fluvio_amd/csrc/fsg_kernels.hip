@@ -2084,27 +2084,18 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
     }
     p_b = 0xFFFFFFFFu;
   };
-  // the next batch's window and record base, loaded while this batch is
-  // evaluated: the window's LDS-DMA issues at the top of the loop without a
-  // dependent global load in front of it
-  LeanWin Wn = lean_window(a, b);
-  uint64_t rbn = a.rbase[b];
   for (;;) {
     lean_sync();  // every lane is done with the previous batch's window
-    const LeanWin W = Wn;
+    const LeanWin W = lean_window(a, b);
     const uint64_t pos = W.pos, al = W.al;
     const uint32_t wlen = W.wlen;
-    const uint64_t rb = rbn;
+    const uint64_t rb = a.rbase[b];
     const uint32_t bn = b + G;
     lean_issue(a, W, L.win);
     // the record starts (k_chase) ride along with the window
     const uint32_t rs = l < 64 ? a.rstart[rb + l] : 0u;
     const uint32_t re = a.rend[b];
     __builtin_amdgcn_s_waitcnt(0);  // this wave's pieces have landed
-    if (bn < a.nbatches) {          // in flight during this batch's evaluation
-      Wn = lean_window(a, bn);
-      rbn = a.rbase[bn];
-    }
     lean_sync();                    // ... and the other wave's
     // batch header (file format, batch.rs:163-180), read before the gaps are cleared
     const uint8_t* h = L.win + (pos - al);

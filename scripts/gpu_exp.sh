@@ -7,14 +7,10 @@ export TMPDIR=/tmp
 O=$GRAFT_REPO_ROOT/gpurun_out/$1
 mkdir -p "$O"
 step() { echo "$1 rc=$2" >> "$O/steps.log"; [ "$2" -ne 0 ] && exit "$2"; return 0; }
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "lean or random_parity or max_bytes" > "$O/gpu_tests.log" 2>&1
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "lean or random_parity or max_bytes or resident or edge or framing or compressed or project or filter_json" > "$O/gpu_tests.log" 2>&1
 step tests $?
-for WL in c2-substring c1-regex c2-json c3-filter-map c4-array-map f4-dedup f3-one-record; do
+for WL in c2-substring c1-regex c2-json c3-filter-map; do
   timeout -k 10 300 python -u bench.py --workload $WL --only --steps 10 --warmup 2 --no-cpu-baseline --no-e2e > "$O/bench_$WL.log" 2>&1
   step "bench_$WL" $?
 done
-FSG_WRITE_LEAN=1 timeout -k 10 300 python -u bench.py --workload c2-substring --only --steps 10 --warmup 2 --no-cpu-baseline --no-e2e > "$O/bench_c2_wlean.log" 2>&1
-step bench_wlean $?
-FSG_WRITE_LEAN=1 timeout -k 10 300 python -u bench.py --workload c3-filter-map --only --steps 10 --warmup 2 --no-cpu-baseline --no-e2e > "$O/bench_c3_wlean.log" 2>&1
-step bench_wlean3 $?
 exit 0
