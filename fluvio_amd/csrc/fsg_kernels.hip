@@ -398,11 +398,28 @@ done:
 // where the length said.  Any inconsistency -> caller runs the exact serial walk.
 // Returns true when the window was walked.
 __device__ bool walk_fast(WaveLds& L, const uint8_t* w, uint64_t wbase, uint32_t wlen, uint64_t sec_end,
-                          uint64_t cursor, uint32_t rec_remaining) {
+                          uint64_t cursor, uint32_t rec_remaining, const uint16_t* rsb = nullptr, uint64_t al0 = 0,
+                          uint32_t done = 0, uint32_t rend = 0) {
   const uint32_t tid = threadIdx.x;
   const uint64_t sec_lim64 = sec_end - wbase;
   const uint32_t have = wlen < sec_lim64 ? wlen : (uint32_t)sec_lim64;
-  if (tid == 0) {
+  if (rsb) {
+    // record starts precomputed by k_chase_x (offsets from al0): every lane
+    // takes its records' bounds; the records that end inside the window are a prefix
+    const uint32_t lim = rec_remaining < (uint32_t)kMaxR ? rec_remaining : (uint32_t)kMaxR;
+    bool in = false;
+    if (tid < lim) {
+      const uint64_t st = al0 + rsb[done + tid];
+      const uint64_t en = al0 + (tid + 1 < rec_remaining ? rsb[done + tid + 1] : rend);
+      in = st >= wbase && en - wbase <= have;
+      if (in) {
+        L.r_start[tid] = (uint32_t)(st - wbase);
+        L.r_end[tid] = (uint32_t)(en - wbase);
+      }
+    }
+    const int n = __syncthreads_count(in);
+    if (tid == 0) L.nr = n;
+  } else if (tid == 0) {
     uint32_t q = (uint32_t)(cursor - wbase);
     int n = 0;
     const int lim = (int)(rec_remaining < (uint32_t)kMaxR ? rec_remaining : (uint32_t)kMaxR);
@@ -1042,6 +1059,9 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
   }
   bool first_window = true;  // the window at al0 is already resident
   const uint32_t nrec_total = count > 0 ? (uint32_t)count : 0u;
+  // record starts from k_chase_x / k_chase when they framed this batch
+  const uint32_t rend_b = a.rend ? a.rend[b] : 0xFFFFu;
+  const uint16_t* rsb = (a.rstart && rend_b != 0xFFFFu) ? a.rstart + a.rbase[b] : nullptr;
   const uint64_t rb = a.rbase[b];
   // phase A: full chain; phase B (only if a record error occurred): truncated chain
   int nst = (int)ch.nstages;
@@ -1080,7 +1100,8 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
       __syncthreads();
       if (!first_window) load_window(L, S, al, wlen);
       first_window = false;
-      if (!walk_fast(L, (const uint8_t*)L.win, al, wlen, sec_end, cursor, nrec_total - done_recs)) {
+      if (!walk_fast(L, (const uint8_t*)L.win, al, wlen, sec_end, cursor, nrec_total - done_recs, rsb, al0, done_recs,
+                     rend_b)) {
         if (tid == 0)
           walk_records(L, (const uint8_t*)L.win, al, wlen, sec_end, cursor, nrec_total - done_recs, kMaxR);
         __syncthreads();
@@ -1985,6 +2006,43 @@ __global__ __launch_bounds__(kChaseT) void k_chase(EvalArgs a) {
   }
   const uint64_t tail0 = n > head ? head + ((n - head) & ~7ull) : n;
   for (uint64_t i = tail0 + t; i < n; i += kChaseT) dst[i] = st[i];
+}
+
+// k_chase_x — the same record framing for the exact kernel: any record count
+// (batch up to 64 KiB from its aligned start), starts stored directly
+__global__ __launch_bounds__(256) void k_chase_x(EvalArgs a) {
+  for (uint32_t b = blockIdx.x * 256 + threadIdx.x; b < a.nbatches; b += gridDim.x * 256) {
+    const uint64_t pos = a.bpos[b];
+    const uint64_t rb = a.rbase[b], rn = (b + 1 < a.nbatches ? a.rbase[b + 1] : a.nrec) - rb;
+    const uint64_t al = pos & ~15ull;
+    const uint8_t* base = a.slice + al;
+    const uint32_t batch_len = __builtin_bswap32(ld_u32_at(a.slice + pos + 8));
+    const uint64_t sec0 = pos + 57, sec_end = pos + 12 + (uint64_t)batch_len;
+    const uint64_t sec_len = sec_end - sec0;
+    const int32_t count = sec_len >= 4 ? (int32_t)__builtin_bswap32(ld_u32_at(a.slice + sec0)) : -1;
+    uint32_t end = 0xFFFFu;
+    if (sec_len >= 4 && sec_end - al < 0xFFFFu && count >= 0 && (uint64_t)count == rn) {
+      const uint32_t have = (uint32_t)(sec_end - al);
+      uint32_t q = (uint32_t)(sec0 + 4 - al);
+      int n = 0;
+      for (; n < count; n++) {
+        const uint32_t x = ld_u32_at(base + q);
+        const uint32_t term = ~x & 0x80808080u;
+        if (!term) break;
+        const uint32_t nb = (((uint32_t)__builtin_ctz(term)) >> 3) + 1;
+        if (q + nb > have) break;
+        const uint32_t y = nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u));
+        const uint32_t v = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
+        if (v & 1u) break;  // negative length (zigzag)
+        const uint32_t len = v >> 1;
+        if (have - (q + nb) < len) break;
+        a.rstart[rb + n] = (uint16_t)q;
+        q += nb + len;
+      }
+      if (n == count) end = q;
+    }
+    a.rend[b] = (uint16_t)end;
+  }
 }
 
 // four waves per SIMD (eight workgroups per CU, as many as the LDS holds)
@@ -4406,6 +4464,8 @@ void launch_eval(const EvalArgs& a, uint32_t ops, bool lean, hipStream_t s) {
     grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list
   } else {
     e.list = nullptr;
+    if (e.rstart)  // record starts for the exact kernel (no serial chase per window)
+      hipLaunchKernelGGL(k_chase_x, dim3(std::min<uint32_t>((a.nbatches + 255) / 256, 4096)), dim3(256), 0, s, e);
   }
   if ((ops & ~kOpsContains) == 0)
     hipLaunchKernelGGL(k_eval<kOpsContains>, dim3(grid), dim3(kEvalThreads), dyn, s, e);

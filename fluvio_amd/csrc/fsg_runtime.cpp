@@ -1504,13 +1504,12 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   const bool lean = (ops & ~((1u << OP_CONTAINS) | (1u << OP_MAP_UPPER) | (1u << OP_REGEX) |
                              (1u << OP_FILTER_JSON) | (1u << OP_PROJECT))) == 0 &&
                     !has_agg && lean_stages;
-  if (lean) {
-    HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
-    HIPCHK(c->rstart.ensure(((size_t)s->nrec + 64) * sizeof(uint16_t)));  // + a wave of over-read
-    HIPCHK(c->rend.ensure(((size_t)nb + 1) * sizeof(uint16_t)));
-    ea.rstart = c->rstart.as<uint16_t>();
-    ea.rend = c->rend.as<uint16_t>();
-  }
+  // record starts per batch (k_chase for the lean kernel, k_chase_x for the exact one)
+  HIPCHK(c->rstart.ensure(((size_t)s->nrec + 64) * sizeof(uint16_t)));  // + a wave of over-read
+  HIPCHK(c->rend.ensure(((size_t)nb + 1) * sizeof(uint16_t)));
+  ea.rstart = c->rstart.as<uint16_t>();
+  ea.rend = c->rend.as<uint16_t>();
+  if (lean) HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
   launch_eval(ea, ops, lean, st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[1], st));
