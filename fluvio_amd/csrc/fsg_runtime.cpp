@@ -15,8 +15,10 @@
 // single SmartModuleTransformRuntimeError a call may return.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <sys/mman.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -412,6 +414,9 @@ struct fsg_chain {
   ChainDesc hdesc{};
   std::vector<uint8_t> hblob;
   DevBuf d_desc, d_blob;
+  // ingest staging of process_batch / process: reused across calls, so a call
+  // pays no hipMalloc/hipFree (hipFree synchronises the device)
+  fsg_slice ingest;
   std::vector<std::string> names;
   int agg_stage = -1;
   int array_stage = -1;
@@ -995,6 +1000,15 @@ int upload_slice(fsg_engine* e, const uint8_t* s, size_t len, fsg_slice* sl, hip
                  bool device_frame = true) {
   sl->eng = e;
   sl->len = len;
+  sl->nb = 0;
+  sl->nrec = 0;
+  sl->tail_status = 0;
+  sl->header_bytes = 0;
+  sl->device_framed = false;
+  sl->decompressed = false;
+  sl->crc_bad = 0;
+  sl->crc_first = -1;
+  sl->crc_ms = 0;
   const size_t alloc = ((len + 15) & ~(size_t)15) + kSlicePad + kWin;
   HIPCHK(sl->data.ensure(alloc));
   HIPCHK(hipMemsetAsync((uint8_t*)sl->data.p + (len & ~(size_t)15), 0, alloc - (len & ~(size_t)15), stream));
@@ -1832,8 +1846,20 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   return FSG_OK;
 }
 
+// Host buffer for a downloaded batch, released with free(). Large outputs are
+// 2 MiB aligned and advised onto transparent huge pages: first touch of a
+// multi-GB malloc otherwise costs one page fault per 4 KiB inside the D2H copy.
+uint8_t* host_alloc(size_t n) {
+  constexpr size_t kHuge = 2u << 20;
+  if (n < 2 * kHuge) return (uint8_t*)malloc(std::max<size_t>(n, 1));
+  void* p = nullptr;
+  if (posix_memalign(&p, kHuge, n)) return nullptr;
+  (void)madvise(p, (n + kHuge - 1) & ~(kHuge - 1), MADV_HUGEPAGE);
+  return (uint8_t*)p;
+}
+
 int download_output(fsg_chain* c, fsg_batch_output* res) {
-  uint8_t* h = (uint8_t*)malloc(c->out_len);
+  uint8_t* h = host_alloc(c->out_len);
   if (!h) return fail(FSG_E_DEVICE, "host allocation failed");
   hipError_t e = hipMemcpy(h, c->out.p, c->out_len, hipMemcpyDeviceToHost);
   if (e != hipSuccess) {
@@ -1878,10 +1904,9 @@ extern "C" int fsg_chain_output_device(fsg_chain* c, const void** dptr, size_t* 
 extern "C" int fsg_chain_process_batch(fsg_chain* c, const uint8_t* slice, size_t len, uint64_t max_bytes,
                                        fsg_metrics* m, fsg_batch_output** out) {
   HIPCHK(hipSetDevice(c->eng->device));
-  fsg_slice s;
-  int rc = upload_slice(c->eng, slice, len, &s, c->stream);
+  int rc = upload_slice(c->eng, slice, len, &c->ingest, c->stream);
   if (rc) return rc;
-  return fsg_chain_process_slice(c, &s, max_bytes, m, out);
+  return fsg_chain_process_slice(c, &c->ingest, max_bytes, m, out);
 }
 
 // SmartModuleChainInstance::process: one SmartModuleInput{base_offset, raw_bytes,
@@ -1901,11 +1926,10 @@ extern "C" int fsg_chain_process(fsg_chain* c, const uint8_t* raw, size_t len, i
   be(23, 0, 4);
   be(27, (uint64_t)base_timestamp, 8);
   if (len) memcpy(b.data() + 57, raw, len);
-  fsg_slice s;
-  int rc = upload_slice(c->eng, b.data(), b.size(), &s, c->stream, false);
+  int rc = upload_slice(c->eng, b.data(), b.size(), &c->ingest, c->stream, false);
   if (rc) return rc;
   fsg_batch_output r;
-  rc = run_slice(c, &s, ~0ull, m, &r, c->hdesc.nstages == 0);
+  rc = run_slice(c, &c->ingest, ~0ull, m, &r, c->hdesc.nstages == 0);
   if (rc) {
     free_error(r.error);
     return rc;
@@ -1913,7 +1937,11 @@ extern "C" int fsg_chain_process(fsg_chain* c, const uint8_t* raw, size_t len, i
   auto o = std::make_unique<fsg_output>();
   memset(o.get(), 0, sizeof(fsg_output));
   const size_t rl = c->out_len - 57;  // u32 count + records
-  uint8_t* h = (uint8_t*)malloc(std::max<size_t>(rl, 1));
+  uint8_t* h = host_alloc(rl);
+  if (!h) {
+    free_error(r.error);
+    return fail(FSG_E_DEVICE, "host allocation failed");
+  }
   hipError_t e = hipMemcpy(h, (uint8_t*)c->out.p + 57, rl, hipMemcpyDeviceToHost);
   if (e != hipSuccess) {
     free(h);
