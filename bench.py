@@ -589,12 +589,12 @@ def main():
         out = {
             "metric": "records/sec + achieved HBM GB/s for SmartModule filter chain, 1/2/4/8 MI355X",
             "value": line["value"],
-            "unit": "records/s",
+            "unit": line.get("unit", "records/s"),
             "n_gpus": ctx.world,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": line["ms_per_step"],
-            "higher_is_better": True,
+            "higher_is_better": line.get("higher_is_better", True),
             "scaling": line["scaling"],
             "vs_baseline": None,
             "dtype": line["dtype"],
@@ -606,6 +606,8 @@ def main():
                 out[k] = v
         if workloads:
             out["workloads"] = workloads
+        if head == "f3-one-record":  # a latency line, not the headline metric
+            out["metric"] = line["metric"]
         print(json.dumps(out))
     if ctx.dist is not None:
         ctx.dist.destroy_process_group()

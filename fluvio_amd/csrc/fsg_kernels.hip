@@ -2525,7 +2525,7 @@ __global__ __launch_bounds__(256) void k_scan_down(ScanDownArgs a) {
   }
   ScanRow total;
   block_excl_scan(acc, sh, total);
-  ScanRow run = a.tile_sums[blockIdx.x];
+  ScanRow run = a.tile_sums ? a.tile_sums[blockIdx.x] : ScanRow{};  // null: the slice is one tile
   row_add(run, acc);
   const uint32_t f = a.mins->first_keep;
   for (int k = 0; k < kScanPer; k++) {
@@ -4468,8 +4468,8 @@ void launch_eval(const EvalArgs& a, uint32_t ops, bool lean, hipStream_t s) {
     // of dependent global loads per batch, so only where batches hold few
     // records (measured on MI355X: C4 ~240 records/batch eval 6.6 -> 5.5 ms;
     // ~2000 tiny records per batch over a few hundred batches is slower than the
-    // lane-0 chase through LDS)
-    if (e.rstart && a.nrec <= 256ull * a.nbatches)
+    // lane-0 chase through LDS; a handful of batches is not worth the launch)
+    if (e.rstart && a.nbatches >= 64 && a.nrec <= 256ull * a.nbatches)
       hipLaunchKernelGGL(k_chase_x, dim3(std::min<uint32_t>((a.nbatches + 255) / 256, 4096)), dim3(256), 0, s, e);
     else
       e.rstart = nullptr, e.rend = nullptr;
@@ -4501,9 +4501,14 @@ void launch_scan(const ScanRow* rows, ScanRow* pre, ScanRow* tile_sums, ScanRow*
                  uint64_t max_bytes, Mins* mins, const BatchStat* bstat, hipStream_t s) {
   if (!n) return;
   const uint32_t nt = scan_tiles(n);
+  ScanDownArgs d{rows, pre, nullptr, n, cut ? 1u : 0u, max_bytes, mins, bstat};
+  if (nt == 1) {  // up to kScanTile batches: one workgroup scans in place (one launch, not three)
+    hipLaunchKernelGGL(k_scan_down, dim3(1), dim3(kScanBlock), 0, s, d);
+    return;
+  }
   hipLaunchKernelGGL(k_scan_reduce, dim3(nt), dim3(kScanBlock), 0, s, rows, n, tile_sums);
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanBlock), 0, s, tile_sums, nt, grand);
-  ScanDownArgs d{rows, pre, tile_sums, n, cut ? 1u : 0u, max_bytes, mins, bstat};
+  d.tile_sums = tile_sums;
   hipLaunchKernelGGL(k_scan_down, dim3(nt), dim3(kScanBlock), 0, s, d);
 }
 void launch_plan(const PlanArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_plan, dim3(1), dim3(64), 0, s, a); }

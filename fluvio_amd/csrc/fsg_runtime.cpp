@@ -18,6 +18,7 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -356,6 +357,38 @@ struct DevBuf {
   }
 };
 
+// page-locked host memory (hipHostMalloc): D2H straight from the DMA engine,
+// no staging through HIP's pageable-copy path
+struct PinBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  ~PinBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
+    if (e == hipSuccess) cap = n;
+    return e;
+  }
+};
+
+// Host-side wait for a stream: spin on hipStreamQuery for up to ~200 us (the
+// one-record process() path's waits are tens of us, below the blocking
+// wait's wake-up latency), then block.
+hipError_t wait_stream(hipStream_t st) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    hipError_t e = hipStreamQuery(st);
+    if (e != hipErrorNotReady) return e;
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) break;
+  }
+  return hipStreamSynchronize(st);
+}
+
 struct ModuleSpec {
   std::vector<uint8_t> bytes;
   std::map<std::string, std::string> params;  // SmartModuleExtraParams (BTreeMap)
@@ -405,7 +438,11 @@ struct fsg_slice {
   uint64_t crc_bad = 0;
   int64_t crc_first = -1;
   float crc_ms = 0;
+  std::vector<uint64_t> hbpos, hrbase;  // host framing (kept: the H2D copies may still be reading them)
 };
+
+constexpr size_t kPinPlan = 256;           // pinned block: Plan, then the small output
+constexpr size_t kSmallOut = 1u << 20;    // outputs up to 1 MiB come back through it
 
 struct fsg_chain {
   fsg_engine* eng = nullptr;
@@ -437,6 +474,10 @@ struct fsg_chain {
   DevBuf sf_bval, sf_bpre, sf_bn, sf_hv, sf_vref, sf_vlen, sf_slot, sf_keep, sf_idx, sf_sref, sf_first, sf_cur,
       sf_scal;
   Plan hplan{};
+  // pinned: the plan read-back and, for outputs up to kSmallOut, the output
+  // batch itself (copied on the stream before run_slice's last wait)
+  PinBuf hpin;
+  bool out_pinned = false;
   hipEvent_t ev[6] = {};
   fsg_timings last{};
   size_t out_len = 0;
@@ -996,8 +1037,9 @@ int decompress_slice(fsg_slice* sl, const std::vector<uint64_t>& bpos, const std
 
 // device_frame: frame on the device (fsg_slice_upload, process_batch); the
 // host walk frames the one-batch slices process() builds itself
+// sync=false: the caller keeps `s` alive and synchronises the stream itself
 int upload_slice(fsg_engine* e, const uint8_t* s, size_t len, fsg_slice* sl, hipStream_t stream,
-                 bool device_frame = true) {
+                 bool device_frame = true, bool sync = true) {
   sl->eng = e;
   sl->len = len;
   sl->nb = 0;
@@ -1021,7 +1063,10 @@ int upload_slice(fsg_engine* e, const uint8_t* s, size_t len, fsg_slice* sl, hip
   }
   if (fallback) {
     sl->device_framed = false;
-    std::vector<uint64_t> bpos, rbase;
+    std::vector<uint64_t>& bpos = sl->hbpos;
+    std::vector<uint64_t>& rbase = sl->hrbase;
+    bpos.clear();
+    rbase.clear();
     std::vector<uint8_t> codecs;
     frame(s, len, bpos, rbase, sl->nrec, sl->tail_status, sl->header_bytes, &codecs);
     if (std::any_of(codecs.begin(), codecs.end(), [](uint8_t c) { return c != 0; }))
@@ -1036,7 +1081,7 @@ int upload_slice(fsg_engine* e, const uint8_t* s, size_t len, fsg_slice* sl, hip
   }
   HIPCHK(sl->bpos.ensure(8));
   HIPCHK(sl->rbase.ensure(8));
-  HIPCHK(hipStreamSynchronize(stream));
+  if (sync) HIPCHK(hipStreamSynchronize(stream));
   return FSG_OK;
 }
 }  // namespace
@@ -1517,7 +1562,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   // through the exact kernel (list mode)
   const bool lean = (ops & ~((1u << OP_CONTAINS) | (1u << OP_MAP_UPPER) | (1u << OP_REGEX) |
                              (1u << OP_FILTER_JSON) | (1u << OP_PROJECT))) == 0 &&
-                    !has_agg && lean_stages;
+                    !has_agg && lean_stages && nb > 1;  // one batch: the exact kernel alone (1 launch, not 3)
   // record starts per batch (k_chase for the lean kernel, k_chase_x for the exact one)
   HIPCHK(c->rstart.ensure(((size_t)s->nrec + 64) * sizeof(uint16_t)));  // + a wave of over-read
   HIPCHK(c->rend.ensure(((size_t)nb + 1) * sizeof(uint16_t)));
@@ -1717,11 +1762,13 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   if (has_sf) launch_sf_commit(sfa, st);  // the stage's state through plan.done
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[2], st));
-  HIPCHK(hipMemcpyAsync(&c->hplan, c->plan.p, sizeof(Plan), hipMemcpyDeviceToHost, st));
+  HIPCHK(c->hpin.ensure(kPinPlan + kSmallOut));
+  HIPCHK(hipMemcpyAsync(c->hpin.p, c->plan.p, sizeof(Plan), hipMemcpyDeviceToHost, st));
   unsigned long long sfs[3] = {0, 0, 0};
   const bool dedup = has_sf && sfa.op == OP_DEDUP && nb;
   if (dedup) HIPCHK(hipMemcpyAsync(sfs, sfa.scal, sizeof sfs, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  HIPCHK(wait_stream(st));
+  memcpy(&c->hplan, c->hpin.p, sizeof(Plan));
   if (dedup) {
     c->sf->n_ent = sfs[0];
     c->sf->arena_len = sfs[1];
@@ -1796,7 +1843,10 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   launch_crc(wa.out, 21, out_len - 21, c->crcparts.as<uint32_t>(), st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[5], st));
-  HIPCHK(hipStreamSynchronize(st));
+  c->out_pinned = out_len <= kSmallOut;
+  if (c->out_pinned)
+    HIPCHK(hipMemcpyAsync((uint8_t*)c->hpin.p + kPinPlan, wa.out, out_len, hipMemcpyDeviceToHost, st));
+  HIPCHK(wait_stream(st));
   c->out_len = out_len;
   // timings
   float t[5] = {0};
@@ -1861,7 +1911,11 @@ uint8_t* host_alloc(size_t n) {
 int download_output(fsg_chain* c, fsg_batch_output* res) {
   uint8_t* h = host_alloc(c->out_len);
   if (!h) return fail(FSG_E_DEVICE, "host allocation failed");
-  hipError_t e = hipMemcpy(h, c->out.p, c->out_len, hipMemcpyDeviceToHost);
+  hipError_t e = hipSuccess;
+  if (c->out_pinned)
+    memcpy(h, (const uint8_t*)c->hpin.p + kPinPlan, c->out_len);
+  else
+    e = hipMemcpy(h, c->out.p, c->out_len, hipMemcpyDeviceToHost);
   if (e != hipSuccess) {
     free(h);
     return fail(FSG_E_DEVICE, hipGetErrorString(e));
@@ -1926,11 +1980,13 @@ extern "C" int fsg_chain_process(fsg_chain* c, const uint8_t* raw, size_t len, i
   be(23, 0, 4);
   be(27, (uint64_t)base_timestamp, 8);
   if (len) memcpy(b.data() + 57, raw, len);
-  int rc = upload_slice(c->eng, b.data(), b.size(), &c->ingest, c->stream, false);
+  // no sync after the upload: `b` lives to the end of this call, which run_slice synchronises
+  int rc = upload_slice(c->eng, b.data(), b.size(), &c->ingest, c->stream, false, false);
   if (rc) return rc;
   fsg_batch_output r;
   rc = run_slice(c, &c->ingest, ~0ull, m, &r, c->hdesc.nstages == 0);
   if (rc) {
+    (void)hipStreamSynchronize(c->stream);  // an early error return may leave the upload in flight
     free_error(r.error);
     return rc;
   }
@@ -1942,7 +1998,11 @@ extern "C" int fsg_chain_process(fsg_chain* c, const uint8_t* raw, size_t len, i
     free_error(r.error);
     return fail(FSG_E_DEVICE, "host allocation failed");
   }
-  hipError_t e = hipMemcpy(h, (uint8_t*)c->out.p + 57, rl, hipMemcpyDeviceToHost);
+  hipError_t e = hipSuccess;
+  if (c->out_pinned)
+    memcpy(h, (const uint8_t*)c->hpin.p + kPinPlan + 57, rl);
+  else
+    e = hipMemcpy(h, (uint8_t*)c->out.p + 57, rl, hipMemcpyDeviceToHost);
   if (e != hipSuccess) {
     free(h);
     free_error(r.error);

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 O=$GRAFT_REPO_ROOT/gpurun_out/$1
 mkdir -p "$O"
 step() { echo "$1 rc=$2" >> "$O/steps.log"; [ "$2" -ne 0 ] && exit "$2"; return 0; }
-# timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > "$O/gpu_tests.log" 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > "$O/gpu_tests.log" 2>&1
 step tests $?
 timeout -k 10 300 python -u bench.py --workload c2-substring --only --steps 10 --warmup 2 --no-cpu-baseline > "$O/bench_c2.log" 2>&1
 step bench_c2 $?

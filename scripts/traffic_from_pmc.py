@@ -6,7 +6,7 @@ gfx950 (x2); WRITE_SIZE is in KiB and exact for 16-B/lane streaming stores.
 usage: python scripts/traffic_from_pmc.py <pmc dir> <workload> <bench json line file> [<round tag>]
   <pmc dir> holds fetch_<workload>/ and write_<workload>/ (scripts/gpu_prof.sh)
 Updates profiles/traffic.json[workload] = {kernel: {read, write, total}} plus
-the shape (records, batches) and the libfsg.so content tag it was measured on;
+the shape (records, batches) and the kernel-source tag (bench.lib_tag) it was measured on;
 bench.py quotes it as roofline.traffic only for that same build and shape.
 """
 import collections
