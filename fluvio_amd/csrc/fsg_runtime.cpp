@@ -1038,9 +1038,12 @@ int decompress_slice(fsg_slice* sl, const std::vector<uint64_t>& bpos, const std
 
 // device_frame: frame on the device (fsg_slice_upload, process_batch); the
 // host walk frames the one-batch slices process() builds itself
-// sync=false: the caller keeps `s` alive and synchronises the stream itself
+size_t slice_alloc(size_t len) { return ((len + 15) & ~(size_t)15) + kSlicePad + kWin; }
+
+// sync=false: the caller keeps `s` alive and synchronises the stream itself;
+// padded: `s` already holds slice_alloc(len) bytes, zeros behind the slice
 int upload_slice(fsg_engine* e, const uint8_t* s, size_t len, fsg_slice* sl, hipStream_t stream,
-                 bool device_frame = true, bool sync = true) {
+                 bool device_frame = true, bool sync = true, bool padded = false) {
   sl->eng = e;
   sl->len = len;
   sl->nb = 0;
@@ -1052,10 +1055,14 @@ int upload_slice(fsg_engine* e, const uint8_t* s, size_t len, fsg_slice* sl, hip
   sl->crc_bad = 0;
   sl->crc_first = -1;
   sl->crc_ms = 0;
-  const size_t alloc = ((len + 15) & ~(size_t)15) + kSlicePad + kWin;
+  const size_t alloc = slice_alloc(len);
   HIPCHK(sl->data.ensure(alloc));
-  HIPCHK(hipMemsetAsync((uint8_t*)sl->data.p + (len & ~(size_t)15), 0, alloc - (len & ~(size_t)15), stream));
-  if (len) HIPCHK(hipMemcpyAsync(sl->data.p, s, len, hipMemcpyHostToDevice, stream));
+  if (padded) {  // one copy carries the slice and its zero padding
+    HIPCHK(hipMemcpyAsync(sl->data.p, s, alloc, hipMemcpyHostToDevice, stream));
+  } else {
+    HIPCHK(hipMemsetAsync((uint8_t*)sl->data.p + (len & ~(size_t)15), 0, alloc - (len & ~(size_t)15), stream));
+    if (len) HIPCHK(hipMemcpyAsync(sl->data.p, s, len, hipMemcpyHostToDevice, stream));
+  }
   int fallback = 1;
   if (device_frame) {
     int rc = frame_on_device(sl, stream, &fallback);
@@ -1970,7 +1977,7 @@ extern "C" int fsg_chain_process_batch(fsg_chain* c, const uint8_t* slice, size_
 extern "C" int fsg_chain_process(fsg_chain* c, const uint8_t* raw, size_t len, int64_t base_offset,
                                  int64_t base_timestamp, fsg_metrics* m, fsg_output** out) {
   HIPCHK(hipSetDevice(c->eng->device));
-  std::vector<uint8_t> b(57 + len);
+  std::vector<uint8_t> b(slice_alloc(57 + len));  // zero-padded: uploaded in one copy
   auto be = [&](size_t off, uint64_t v, int n) {
     for (int i = 0; i < n; i++) b[off + i] = (uint8_t)(v >> (8 * (n - 1 - i)));
   };
@@ -1983,7 +1990,7 @@ extern "C" int fsg_chain_process(fsg_chain* c, const uint8_t* raw, size_t len, i
   be(27, (uint64_t)base_timestamp, 8);
   if (len) memcpy(b.data() + 57, raw, len);
   // no sync after the upload: `b` lives to the end of this call, which run_slice synchronises
-  int rc = upload_slice(c->eng, b.data(), b.size(), &c->ingest, c->stream, false, false);
+  int rc = upload_slice(c->eng, b.data(), 57 + len, &c->ingest, c->stream, false, false, true);
   if (rc) return rc;
   fsg_batch_output r;
   c->timed = false;  // 11 event calls are a tenth of a one-record call's latency
