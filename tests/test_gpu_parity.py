@@ -250,6 +250,34 @@ def test_process_parity(engine):
                 assert gm.records_out() == oout["metrics"]["records_out"]
 
 
+def test_ingest_slice_reused_across_calls(engine):
+    """process_batch / process stage their input in the chain's own ingest slice
+    (kept at the largest size seen): shrinking, growing, compressed, empty and
+    one-record inputs through ONE chain each match the oracle."""
+    from tests.compressed_slices import recompress
+    modules = CHAINS["filter_init_timeout"]
+    g, o = gpu_chain(engine, modules), orc_chain(modules)
+    big = synth.make_slice(2, 3000, base_offset=5)
+    small = synth.make_slice(2, 7, base_offset=90)
+    comp = recompress(synth.make_slice(2, 400, base_offset=3), [1, 2, 3, 0])
+    one = next(iter(P.decode_batches(synth.make_slice(2, 40))))
+    for step in ("big", "small", "one", "comp", "empty", "one", "big", "small", "comp", "one"):
+        if step == "one":
+            gout = g.process(SmartModuleInput(one.records_bytes, one.base_offset, one.header.first_timestamp))
+            oout = o.process(one.records_bytes, one.base_offset, one.header.first_timestamp)
+            assert oout["status"] == 0
+            assert gout.raw_successes == oout["bytes"], step
+            assert_same_error(gout.error, oout["error"])
+            continue
+        sl = {"big": big, "small": small, "comp": comp, "empty": b""}[step]
+        gout = g.process_batch(sl)
+        oout = o.process_batch(sl)
+        assert oout["status"] == 0, step
+        assert gout.raw == oout["bytes"], step
+        assert gout.n_records == oout["n_records"], step
+        assert_same_error(gout.error, oout["error"])
+
+
 def test_large_records_beyond_window(engine):
     """Records larger than the 17 KB LDS window take the global-memory path."""
     batches = b""
