@@ -25,6 +25,8 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "fsg.h"
@@ -479,11 +481,16 @@ struct fsg_chain {
   PinBuf hpin;
   bool out_pinned = false;
   bool timed = true;  // per-phase kernel timings (events); off for the one-record process()
+  // large-output download: two pinned chunks, DMA of one overlapping the host copy of the other
+  PinBuf hstage;
+  hipEvent_t dl_ev[2] = {};
   hipEvent_t ev[6] = {};
   fsg_timings last{};
   size_t out_len = 0;
   ~fsg_chain() {
     for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    for (auto& e : dl_ev)
       if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -1905,16 +1912,108 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   return FSG_OK;
 }
 
-// Host buffer for a downloaded batch, released with free(). Large outputs are
-// 2 MiB aligned and advised onto transparent huge pages: first touch of a
-// multi-GB malloc otherwise costs one page fault per 4 KiB inside the D2H copy.
+// Host buffers for downloaded batches.  Large ones (>= 4 MiB) are 2 MiB aligned,
+// advised onto transparent huge pages and recycled: host_free parks a large
+// buffer in a small process-wide cache and host_alloc takes it back for the
+// next output that fits, so a repeated multi-GB process_batch reuses memory
+// that is already faulted in (first touch zero-fills every page, which costs
+// as much as the D2H copy itself).
+constexpr size_t kHuge = 2u << 20;
+constexpr int kHostCache = 2;  // parked buffers, process-wide
+struct HostPool {
+  std::mutex mu;
+  std::map<void*, size_t> live;              // large buffers handed out -> capacity
+  std::vector<std::pair<void*, size_t>> parked;
+};
+HostPool& host_pool() {
+  static HostPool* p = new HostPool;  // never destroyed: frees may run at exit
+  return *p;
+}
+
 uint8_t* host_alloc(size_t n) {
-  constexpr size_t kHuge = 2u << 20;
   if (n < 2 * kHuge) return (uint8_t*)malloc(std::max<size_t>(n, 1));
+  HostPool& hp = host_pool();
+  {
+    std::lock_guard<std::mutex> g(hp.mu);
+    for (size_t i = 0; i < hp.parked.size(); i++) {
+      if (hp.parked[i].second >= n && hp.parked[i].second <= 2 * n) {
+        auto b = hp.parked[i];
+        hp.parked.erase(hp.parked.begin() + i);
+        hp.live[b.first] = b.second;
+        return (uint8_t*)b.first;
+      }
+    }
+  }
+  const size_t cap = (n + kHuge - 1) & ~(kHuge - 1);
   void* p = nullptr;
-  if (posix_memalign(&p, kHuge, n)) return nullptr;
-  (void)madvise(p, (n + kHuge - 1) & ~(kHuge - 1), MADV_HUGEPAGE);
+  if (posix_memalign(&p, kHuge, cap)) return nullptr;
+  (void)madvise(p, cap, MADV_HUGEPAGE);
+  std::lock_guard<std::mutex> g(hp.mu);
+  hp.live[p] = cap;
   return (uint8_t*)p;
+}
+
+void host_free(const void* q) {
+  if (!q) return;
+  void* p = const_cast<void*>(q);
+  HostPool& hp = host_pool();
+  {
+    std::lock_guard<std::mutex> g(hp.mu);
+    auto it = hp.live.find(p);
+    if (it != hp.live.end()) {
+      const size_t cap = it->second;
+      hp.live.erase(it);
+      hp.parked.emplace_back(p, cap);
+      if ((int)hp.parked.size() <= kHostCache) return;
+      p = hp.parked.front().first;  // evict the oldest parked buffer
+      hp.parked.erase(hp.parked.begin());
+    }
+  }
+  free(p);
+}
+
+constexpr size_t kDlChunk = 32u << 20;
+constexpr size_t kDlStaged = 128u << 20;  // outputs from here on take the staged download
+constexpr int kDlThreads = 4;
+
+// host copy of one staged chunk, split over kDlThreads threads
+void copy_out(uint8_t* dst, const uint8_t* src, size_t n) {
+  std::thread th[kDlThreads - 1];
+  const size_t part = (n / kDlThreads + 4095) & ~(size_t)4095;
+  for (int t = 1; t < kDlThreads; t++) {
+    const size_t a = std::min(n, part * t), b = std::min(n, part * (t + 1));
+    th[t - 1] = std::thread([=] {
+      if (b > a) memcpy(dst + a, src + a, b - a);
+    });
+  }
+  memcpy(dst, src, std::min(n, part));
+  for (auto& x : th) x.join();
+}
+
+// device -> pinned chunk k (alternating buffers) -> caller memory: the DMA of
+// chunk k+1 runs while the host copies chunk k out of the other buffer
+hipError_t staged_download(fsg_chain* c, uint8_t* dst, const uint8_t* src, size_t n) {
+  hipError_t e = c->hstage.ensure(2 * kDlChunk);
+  for (int k = 0; k < 2 && e == hipSuccess; k++)
+    if (!c->dl_ev[k]) e = hipEventCreateWithFlags(&c->dl_ev[k], hipEventDisableTiming);
+  if (e != hipSuccess) return e;
+  uint8_t* buf[2] = {(uint8_t*)c->hstage.p, (uint8_t*)c->hstage.p + kDlChunk};
+  const size_t nch = (n + kDlChunk - 1) / kDlChunk;
+  auto issue = [&](size_t k) -> hipError_t {
+    const size_t off = k * kDlChunk, len = std::min(kDlChunk, n - off);
+    hipError_t r = hipMemcpyAsync(buf[k & 1], src + off, len, hipMemcpyDeviceToHost, c->stream);
+    return r == hipSuccess ? hipEventRecord(c->dl_ev[k & 1], c->stream) : r;
+  };
+  for (size_t k = 0; k < std::min<size_t>(2, nch) && e == hipSuccess; k++) e = issue(k);
+  for (size_t k = 0; k < nch && e == hipSuccess; k++) {
+    e = hipEventSynchronize(c->dl_ev[k & 1]);
+    if (e != hipSuccess) break;
+    const size_t off = k * kDlChunk;
+    copy_out(dst + off, buf[k & 1], std::min(kDlChunk, n - off));
+    if (k + 2 < nch) e = issue(k + 2);
+  }
+  if (e != hipSuccess) (void)hipStreamSynchronize(c->stream);  // nothing left in flight into hstage
+  return e;
 }
 
 int download_output(fsg_chain* c, fsg_batch_output* res) {
@@ -1923,10 +2022,12 @@ int download_output(fsg_chain* c, fsg_batch_output* res) {
   hipError_t e = hipSuccess;
   if (c->out_pinned)
     memcpy(h, (const uint8_t*)c->hpin.p + kPinPlan, c->out_len);
+  else if (c->out_len >= kDlStaged)
+    e = staged_download(c, h, (const uint8_t*)c->out.p, c->out_len);
   else
     e = hipMemcpy(h, c->out.p, c->out_len, hipMemcpyDeviceToHost);
   if (e != hipSuccess) {
-    free(h);
+    host_free(h);
     return fail(FSG_E_DEVICE, hipGetErrorString(e));
   }
   res->batch = h;
@@ -2015,7 +2116,7 @@ extern "C" int fsg_chain_process(fsg_chain* c, const uint8_t* raw, size_t len, i
   else
     e = hipMemcpy(h, (uint8_t*)c->out.p + 57, rl, hipMemcpyDeviceToHost);
   if (e != hipSuccess) {
-    free(h);
+    host_free(h);
     free_error(r.error);
     return fail(FSG_E_DEVICE, hipGetErrorString(e));
   }
@@ -2135,13 +2236,13 @@ extern "C" int fsg_chain_last_timings(fsg_chain* c, fsg_timings* t) {
 
 extern "C" void fsg_output_free(fsg_output* o) {
   if (!o) return;
-  free((void*)o->records);
+  host_free(o->records);
   free_error(o->error);
   delete o;
 }
 extern "C" void fsg_batch_output_free(fsg_batch_output* o) {
   if (!o) return;
-  free((void*)o->batch);
+  host_free(o->batch);
   free_error(o->error);
   delete o;
 }

@@ -278,6 +278,21 @@ def test_ingest_slice_reused_across_calls(engine):
         assert_same_error(gout.error, oout["error"])
 
 
+def test_staged_download_large_output(engine):
+    """Outputs of 128 MiB and more come back through two pinned 32 MiB chunks
+    (DMA of one overlapping the host copy of the other): byte-exact with the
+    oracle over a ~150 MB decode-and-return batch (chunk count not a multiple of 2,
+    last chunk partial)."""
+    sl = synth.make_slice(2, 150_000, base_offset=77)
+    g, o = gpu_chain(engine, []), orc_chain([])
+    gout = g.process_batch(sl)
+    oout = o.process_batch(sl)
+    assert oout["status"] == 0
+    assert len(oout["bytes"]) >= 128 << 20
+    assert gout.raw == oout["bytes"]
+    del gout, oout
+
+
 def test_large_records_beyond_window(engine):
     """Records larger than the 17 KB LDS window take the global-memory path."""
     batches = b""
