@@ -544,14 +544,20 @@ def run_one_record(ctx, cpu):
     inp = SmartModuleInput.try_from_records([P.Record.new(b'{"level":"warn","message":"request timeout"}')])
     for _ in range(20):
         chain.process(inp)
-    n = 300
+    n = 2000
+    lat = []
     t0 = time.perf_counter()
     for _ in range(n):
+        t1 = time.perf_counter()
         out = chain.process(inp)
-    dt = (time.perf_counter() - t0) / n
+        lat.append(time.perf_counter() - t1)
+    mean = (time.perf_counter() - t0) / n
     assert len(out.successes) == 1
-    return {"metric": "latency per one-record process() call", "value": dt * 1e6, "unit": "us",
-            "higher_is_better": False, "calls": n, "records_per_s": 1.0 / dt, "ms_per_step": dt * 1e3,
+    lat.sort()
+    dt = lat[n // 2]  # p50: one slow call on a shared host does not move it
+    return {"metric": "latency per one-record process() call (p50)", "value": dt * 1e6, "unit": "us",
+            "higher_is_better": False, "calls": n, "mean_us": mean * 1e6, "p99_us": lat[n * 99 // 100] * 1e6,
+            "records_per_s": 1.0 / mean, "ms_per_step": dt * 1e3,
             "scaling": "weak", "dtype": "u8",
             "config": {"workload": "f3-one-record", "chain": ["filter_init"],
                        "description": "fsg_chain_process of a one-record SmartModuleInput (H2D upload, eval, "
