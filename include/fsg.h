@@ -211,6 +211,8 @@ int fsg_chain_get_accumulator(fsg_chain *c, size_t stage, uint8_t **acc, size_t 
 int fsg_chain_keyed_state(fsg_chain *c, size_t stage, uint64_t *dev_fp, uint32_t *dev_val, size_t cap, size_t *n);
 int fsg_chain_last_timings(fsg_chain *c, fsg_timings *t);
 void fsg_chain_free(fsg_chain *c);
+/* Release an output.  Large output buffers (>= 4 MiB) are parked for reuse by the
+ * next large output (at most two, process-wide) instead of being unmapped. */
 void fsg_output_free(fsg_output *o);
 void fsg_batch_output_free(fsg_batch_output *o);
 void fsg_free(void *p);
