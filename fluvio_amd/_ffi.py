@@ -73,7 +73,7 @@ class fsg_timings(ctypes.Structure):
     _fields_ = [("eval_ms", ctypes.c_float), ("plan_ms", ctypes.c_float), ("write_ms", ctypes.c_float),
                 ("crc_ms", ctypes.c_float), ("total_ms", ctypes.c_float), ("in_bytes", ctypes.c_uint64),
                 ("out_bytes", ctypes.c_uint64), ("n_batches", ctypes.c_uint64),
-                ("n_records_in", ctypes.c_uint64)]
+                ("n_records_in", ctypes.c_uint64), ("eval_path", ctypes.c_uint32), ("deferred", ctypes.c_uint32)]
 
 
 VP = ctypes.c_void_p

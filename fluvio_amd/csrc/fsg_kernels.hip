@@ -4447,12 +4447,15 @@ static uint32_t lean_grid(bool json) {
   return c;
 }
 
-void launch_eval(const EvalArgs& a, uint32_t ops, bool lean, hipStream_t s) {
+void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s) {
   if (!a.nbatches) return;
   const size_t dyn = (ops & opbit(OP_REGEX)) ? kDfaDyn : 0;
   EvalArgs e = a;
   uint32_t grid = a.nbatches;
-  if (lean) {
+  if (mode == EVAL_FLAT) {
+    launch_flat(a, s);  // k_flat_frame (k_chase + window descriptors) and k_flat
+    grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list
+  } else if (mode == EVAL_LEAN) {
     // persistent: as many workgroups as fit on the device at once
     const bool json = (ops & (opbit(OP_FILTER_JSON) | opbit(OP_PROJECT))) != 0;
     const uint32_t g = std::min<uint32_t>(a.nbatches, lean_grid(json));

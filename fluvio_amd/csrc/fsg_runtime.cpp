@@ -337,6 +337,19 @@ bool parse_acc_map(const std::vector<uint8_t>& s, AccMap& m) {
   return true;
 }
 
+// an environment switch (experiments: FSG_NO_FLAT=1 takes k_eval_lean instead of k_flat)
+bool getenv_flag(const char* name) {
+  static std::map<std::string, bool> cache;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(name);
+  if (it != cache.end()) return it->second;
+  const char* v = getenv(name);
+  const bool on = v && *v && strcmp(v, "0") != 0;
+  cache[name] = on;
+  return on;
+}
+
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -468,6 +481,7 @@ struct fsg_chain {
   DevBuf aj_bcnt, aj_brec, aj_rdesc, aj_rne, aj_rent, aj_rnew, aj_rnewb, aj_rlen, aj_roff, aj_ekid, aj_eval;
   DevBuf aj_sref, aj_sid, aj_state, aj_state2, aj_tsum;
   DevBuf rstart, rend;  // k_chase (lean path record starts)
+  DevBuf bwin;          // k_flat_frame: per-batch window descriptors
   // stateful last stage (filter_look_back / filter_hashset)
   int sf_stage = -1;
   std::shared_ptr<SfState> sf;
@@ -1583,8 +1597,14 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   HIPCHK(c->rend.ensure(((size_t)nb + 1) * sizeof(uint16_t)));
   ea.rstart = c->rstart.as<uint16_t>();
   ea.rend = c->rend.as<uint16_t>();
+  // substring filters / uppercase maps: the register-resident path (fsg_flat.hip)
+  const bool flat = lean && !getenv_flag("FSG_NO_FLAT") && flat_eligible(c->hdesc, ops);
   if (lean) HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
-  launch_eval(ea, ops, lean, st);
+  if (flat) {
+    HIPCHK(c->bwin.ensure((size_t)std::max<uint32_t>(nb, 1) * sizeof(BatchWin)));
+    ea.bwin = c->bwin.as<BatchWin>();
+  }
+  launch_eval(ea, ops, flat ? EVAL_FLAT : lean ? EVAL_LEAN : EVAL_EXACT, st);
   HIPCHK(hipGetLastError());
   if (c->timed) HIPCHK(hipEventRecord(c->ev[1], st));
   launch_mins(ea.bstat, nb, ea.mins, st);
@@ -1779,11 +1799,16 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   if (c->timed) HIPCHK(hipEventRecord(c->ev[2], st));
   HIPCHK(c->hpin.ensure(kPinPlan + kSmallOut));
   HIPCHK(hipMemcpyAsync(c->hpin.p, c->plan.p, sizeof(Plan), hipMemcpyDeviceToHost, st));
+  static_assert(sizeof(Plan) + sizeof(uint32_t) <= kPinPlan, "pinned plan block");
+  if (lean) HIPCHK(hipMemcpyAsync((uint8_t*)c->hpin.p + sizeof(Plan), ea.list, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   unsigned long long sfs[3] = {0, 0, 0};
   const bool dedup = has_sf && sfa.op == OP_DEDUP && nb;
   if (dedup) HIPCHK(hipMemcpyAsync(sfs, sfa.scal, sizeof sfs, hipMemcpyDeviceToHost, st));
   HIPCHK(wait_stream(st));
   memcpy(&c->hplan, c->hpin.p, sizeof(Plan));
+  c->last.eval_path = flat ? FSG_EVAL_FLAT : lean ? FSG_EVAL_LEAN : FSG_EVAL_EXACT;
+  c->last.deferred = 0;
+  if (lean) memcpy(&c->last.deferred, (const uint8_t*)c->hpin.p + sizeof(Plan), sizeof(uint32_t));
   if (dedup) {
     c->sf->n_ent = sfs[0];
     c->sf->arena_len = sfs[1];

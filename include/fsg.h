@@ -161,7 +161,12 @@ typedef struct fsg_timings {
   uint64_t out_bytes;     /* algorithmic bytes written (output batch) */
   uint64_t n_batches;
   uint64_t n_records_in;
+  uint32_t eval_path;     /* FSG_EVAL_EXACT / FSG_EVAL_LEAN / FSG_EVAL_FLAT: the first evaluation kernel */
+  uint32_t deferred;      /* batches that kernel handed to the exact kernel (non-ASCII, odd framing, ...) */
 } fsg_timings;
+#define FSG_EVAL_EXACT 0 /* k_eval over every batch */
+#define FSG_EVAL_LEAN 1  /* k_eval_lean (LDS windows), deferred batches through k_eval */
+#define FSG_EVAL_FLAT 2  /* k_flat (register-resident substring scan), deferred batches through k_eval */
 
 const char *fsg_last_error_message(void);
 int fsg_abi_version(void);

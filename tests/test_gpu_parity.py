@@ -1206,3 +1206,84 @@ def test_compressed_resident_and_errors(engine):
     z = bytearray(recompress(sl, [0]))
     z[22] = (z[22] & ~7) | 4
     check_batch(engine, modules, bytes(z))
+
+
+# ---------------------------------------------------------------------------
+# k_flat (fsg_flat.hip): the register-resident substring path.  Records with
+# keys, non-zero headers, long timestamp / offset varints, needles across
+# 16-byte chunks and 1 KiB wave loads, non-ASCII values (deferred batches)
+# ---------------------------------------------------------------------------
+def _flat_slice(seed=3, nbatches=60, words=None):
+    import random
+    rnd = random.Random(seed)
+    words = words or ["timeout", "time", "out", "level", "lev", "TIMEOUT", "eout", "xx", "y" * 13, "é"]
+    out = b""
+    base = 5
+    for bi in range(nbatches):
+        b = P.Batch(base_offset=base)
+        b.header.first_timestamp = rnd.choice([-1, 0, 1 << 40])
+        nrec = rnd.choice([1, 2, 15, 40, 64, 65]) if bi % 4 else rnd.randint(0, 8)
+        size = rnd.choice([0, 3, 16, 61, 250, 1000])
+        for i in range(nrec):
+            parts = []
+            while sum(len(p) + 1 for p in parts) < size:
+                pool = words if bi % 7 == 6 else words[:-1]  # every 7th batch may hold a non-ASCII value
+                parts.append(rnd.choice(pool))
+            v = rnd.choice(["", " ", "-"]).join(parts)[: size or None]
+            key = None if rnd.random() < 0.6 else rnd.choice([b"", b"timeout", b"k" * 40])
+            r = P.Record.new_key_value(key, v.encode())
+            if rnd.random() < 0.2:
+                r.headers = rnd.choice([1, -3, 60])
+            b.add_record(r)
+            if rnd.random() < 0.2:  # long varints: timestamp / offset deltas far from zero
+                r.preamble.timestamp_delta = rnd.choice([1 << 33, -(1 << 20), 300])
+        enc = b.encode()
+        if len(enc) - 57 > 16384:
+            continue
+        out += enc
+        base += max(nrec, 1) + rnd.randint(0, 3)
+    return out
+
+
+FLAT_CHAINS = [
+    [("filter_init", {"key": "timeout"}, None)],
+    [("filter_init", {"key": "level"}, None)],                     # 4..6 bytes: first 4-gram at every position
+    [("filter_init", {"key": "time"}, None)],
+    [("filter_init", {"key": "yyyyyyyyyyyyyyyyyyyyyyyyyy"}, None)],  # 26 bytes across chunks
+    [("map", {}, None), ("filter_init", {"key": "TIMEOUT"}, None)],
+    [("filter_init", {"key": "out"}, None)],                       # 3 bytes: k_eval_lean
+    [("filter_init", {"key": "timeout"}, None), ("map", {}, None), ("filter_init", {"key": "LEVEL"}, None)],
+    [("filter_init", {"key": ""}, None), ("map", {}, None)],
+    [("map", {}, None)],
+]
+
+
+@pytest.mark.parametrize("ci", range(len(FLAT_CHAINS)))
+@pytest.mark.parametrize("seed", [3, 4])
+def test_flat_path_parity(engine, ci, seed):
+    chain = FLAT_CHAINS[ci]
+    sl = _flat_slice(seed)
+    check_batch(engine, chain, sl)
+    g = gpu_chain(engine, chain)
+    g.process_batch(sl)
+    t = g.last_timings()
+    needles = [len(p.get("key", "")) for n, p, _ in chain if n == "filter_init"]
+    if all(m == 0 or 4 <= m <= 64 for m in needles):
+        assert t["eval_path"] == 2, t  # FSG_EVAL_FLAT
+        assert 0 < t["deferred"] < t["n_batches"], t  # the non-ASCII / 65-record batches
+    # the same chain over the synthetic C2 logs: nothing deferred
+    sl2 = synth.make_slice(2, 3000, base_offset=9)
+    check_batch(engine, chain, sl2)
+
+
+def test_flat_needle_at_window_edges(engine):
+    """A 7-byte needle at every offset around 16-byte chunks and 1 KiB loads."""
+    for shift in range(0, 40, 3):
+        b = P.Batch(base_offset=100 + shift)
+        for i in range(16):
+            pad = 1024 * (i % 3) - 40 + shift + i
+            v = ("x" * max(pad, 0) + "timeout" + "z" * (i * 7)).encode()
+            b.add_record(P.Record.new(v))
+        b2 = P.Batch(base_offset=200)
+        b2.add_record(P.Record.new(b"timeou"))
+        check_batch(engine, [("filter_init", {"key": "timeout"}, None)], b.encode() + b2.encode())
