@@ -66,7 +66,8 @@ C5K = {"partitions": 64, "records_per_partition": 50_000, "keys": 1024,
        "description": "aggregate-json over 64 partitions: records {\"repo-NNNN\": n} keyed by the repo name "
                       "(1024 keys routed by SipHash, ~16 per partition), per-key u32 sums, every record's output = "
                       "the pretty-printed map; each step the ranks' keyed states are merged topic-wide "
-                      "(all_gather over RCCL + per-key sum on the GPU)"}
+                      "through the C ABI (fsg_keyed_*: exact keys, RCCL all-gather of the key lists, union "
+                      "dictionary, dense u32 all-reduce)"}
 EXTRA = ["c1-regex", "c2-json", "c3-filter-map", "c4-array-map", "c5-keyed-agg", "c5-agg-sum", "f4-dedup",
          "f3-one-record"]
 C5_ALL = ("c5-keyed-agg", "c5-agg-sum")
@@ -365,7 +366,10 @@ def run_c5(ctx, cpu):
     engine.comm_init(ctx.broadcast_bytes(uid, 128), ctx.world, ctx.rank)
     owned = PT.owned_partitions(P, ctx.world, ctx.rank)
     t0 = time.time()
-    slices = {p: synth.make_slice_array(3, nrec, seed=synth.SEEDS[3] + p) for p in owned}
+    slices, vsum = {}, {}
+    for p in owned:
+        slices[p] = synth.make_slice_array(3, nrec, seed=synth.SEEDS[3] + p)
+        vsum[p] = synth.last_int_sum()  # the generator's ground truth (no GPU, no oracle)
     gen_s = time.time() - t0
     chains, rsl = {}, {}
     for p in owned:
@@ -378,6 +382,7 @@ def run_c5(ctx, cpu):
     nthreads = min(16, len(owned)) or 1
     groups = [owned[i::nthreads] for i in range(nthreads)]
     kms = {"eval_ms": 0.0, "write_ms": 0.0, "crc_ms": 0.0, "total_ms": 0.0}
+    out_bytes = [0]
     lock = threading.Lock()
 
     def work(ps):  # one host thread drives a group of partitions, each on its own chain stream
@@ -388,6 +393,7 @@ def run_c5(ctx, cpu):
             with lock:
                 for k in kms:
                     kms[k] += t[k]
+                out_bytes[0] += t["out_bytes"]
 
     def step():
         th = [threading.Thread(target=work, args=(g,)) for g in groups if g]
@@ -402,19 +408,25 @@ def run_c5(ctx, cpu):
     ctx.barrier()
     for k in kms:
         kms[k] = 0.0
+    out_bytes[0] = 0
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
     ctx.barrier()
     elapsed = ctx.max_over_ranks(time.perf_counter() - t0)
     total_recs = sum(rsl[p].n_records for p in owned)
-    if ctx.dist is not None:
-        import torch
-        tt = torch.tensor([total_recs], dtype=torch.float64)
-        ctx.dist.all_reduce(tt)
-        total_recs = int(tt.item())
     in_bytes = sum(chains[p].last_timings()["in_bytes"] for p in owned)
     vec = state.read()
+    # every partition's accumulator after warmup + steps calls over its slice:
+    # (calls x the generator's sum) wrapping i32, checked on the owned slots
+    calls = a.warmup + a.steps
+    bad = sum(1 for p in owned if vec[p] != PT.wrap_i32(calls * vsum[p]))
+    if ctx.dist is not None:
+        import torch
+        tt = torch.tensor([total_recs, bad], dtype=torch.float64)
+        ctx.dist.all_reduce(tt)
+        total_recs, bad = int(tt[0].item()), int(tt[1].item())
+    assert bad == 0, f"c5-agg-sum: {bad} partition accumulators differ from the generator's sums"
     per = {k: v / a.steps for k, v in kms.items()}
     res = {"metric": "records/s", "value": total_recs * a.steps / elapsed, "unit": "records/s",
            "ms_per_step": elapsed / a.steps * 1e3, "scaling": "strong", "dtype": "i32",
@@ -424,7 +436,14 @@ def run_c5(ctx, cpu):
                       "parallelism": f"partitions sharded p -> rank p mod {ctx.world}"},
            "kernel_ms_sum_over_partitions": per,
            "gbps_input_per_gpu": in_bytes * a.steps / elapsed / 1e9,
-           "state_checksum": sum(vec) & 0xFFFFFFFF, "setup_s": {"generate": gen_s}}
+           "state_checksum": sum(vec) & 0xFFFFFFFF,
+           "state_check": f"ok: all {P} partition accumulators == (warmup + steps) x the generator's sum of the "
+                          f"partition's integers (wrapping i32), merged by RCCL all-reduce",
+           "setup_s": {"generate": gen_s}}
+    # roofline over the partitions' launches: per step, the slices' bytes over
+    # the summed eval time of the 64 chains (each chain's launch reads its slice once)
+    res["roofline"] = roofline(per, {"in_bytes": in_bytes, "out_bytes": out_bytes[0] / a.steps}, "c5-agg-sum",
+                               total_recs, 0)
     res["cpu_baseline"] = cpu.get("c5-agg-sum")
     return res
 
@@ -440,15 +459,17 @@ def run_c5k(ctx, cpu):
     import torch
     from fluvio_amd import partitions as PT
     from fluvio_amd import synth
-    from fluvio_amd.smartengine import ResidentSlice, SmartEngine, SmartModuleChainBuilder, SmartModuleConfig, builtin
+    from fluvio_amd.smartengine import (KeyedState, ResidentSlice, SmartEngine, SmartModuleChainBuilder,
+                                        SmartModuleConfig, builtin, comm_unique_id)
     a = ctx.a
     P, nrec = C5K["partitions"], C5K["records_per_partition"]
     engine = SmartEngine(ctx.local)
-    torch.cuda.set_device(ctx.local)
-    group = ctx.nccl()
+    uid = comm_unique_id() if ctx.rank == 0 else bytes(128)
+    engine.comm_init(ctx.broadcast_bytes(uid, 128), ctx.world, ctx.rank)
     owned = PT.owned_partitions(P, ctx.world, ctx.rank)
     t0 = time.time()
-    raw = synth.make_keyed_slices(P, nrec, C5K["keys"], owned=owned)
+    ksum = {}
+    raw = synth.make_keyed_slices(P, nrec, C5K["keys"], owned=owned, key_sums=ksum)
     gen_s = time.time() - t0
     chains, rsl = {}, {}
     for p in owned:
@@ -459,28 +480,21 @@ def run_c5k(ctx, cpu):
         chains[p] = b.initialize(engine)
         rsl[p] = ResidentSlice(engine, raw[p])
     del raw
-    cap = C5K["keys"] + 64
-    fp = torch.zeros(len(owned) * cap, dtype=torch.int64, device=f"cuda:{ctx.local}")
-    val = torch.zeros(len(owned) * cap, dtype=torch.int32, device=f"cuda:{ctx.local}")
+    keyed = KeyedState(engine)
     nthreads = min(16, len(owned)) or 1
-    groups = [list(range(len(owned)))[i::nthreads] for i in range(nthreads)]
+    groups = [owned[i::nthreads] for i in range(nthreads)]
     kms = {"eval_ms": 0.0, "plan_ms": 0.0, "write_ms": 0.0, "crc_ms": 0.0, "total_ms": 0.0}
     out_bytes = [0]
     lock = threading.Lock()
-    counts = [0] * len(owned)
 
-    def work(idx):  # one host thread drives a group of partitions, each on its own chain stream
-        for i in idx:
-            p = owned[i]
+    def work(ps):  # one host thread drives a group of partitions, each on its own chain stream
+        for p in ps:
             chains[p].process_slice(rsl[p], download=False)
-            counts[i] = chains[p].keyed_state(0, fp.data_ptr() + i * cap * 8, val.data_ptr() + i * cap * 4, cap)
             t = chains[p].last_timings()
             with lock:
                 for k in kms:
                     kms[k] += t[k]
                 out_bytes[0] += t["out_bytes"]
-
-    merged = [None]
 
     def step():
         th = [threading.Thread(target=work, args=(g,)) for g in groups if g]
@@ -488,11 +502,12 @@ def run_c5k(ctx, cpu):
             x.start()
         for x in th:
             x.join()
-        assert max(counts) <= cap
-        sel = torch.cat([torch.arange(i * cap, i * cap + counts[i], device=fp.device) for i in range(len(owned))])
-        merged[0] = PT.merge_keyed_torch(fp[sel], val[sel].to(torch.int64) & 0xFFFFFFFF,
-                                         dist=ctx.dist, group=group)
-        torch.cuda.synchronize()
+        # the topic-wide totals: every owned partition's map (exact keys, in HBM)
+        # into the rank's table, then the union dictionary + dense u32 all-reduce over RCCL
+        keyed.reset()
+        for p in owned:
+            keyed.collect(chains[p])
+        keyed.allreduce()
 
     for _ in range(a.warmup):
         step()
@@ -506,12 +521,19 @@ def run_c5k(ctx, cpu):
     ctx.barrier()
     elapsed = ctx.max_over_ranks(time.perf_counter() - t0)
     total_recs = sum(rsl[p].n_records for p in owned)
-    if ctx.dist is not None:
-        tt = torch.tensor([total_recs], dtype=torch.float64)
-        ctx.dist.all_reduce(tt)
-        total_recs = int(tt.item())
     in_bytes = sum(chains[p].last_timings()["in_bytes"] for p in owned)
-    keys, sums = merged[0]
+    merged = keyed.read()
+    # the keys this rank's partitions own (SipHash routing: each key in one
+    # partition): topic total == (warmup + steps) x the generator's sum, u32 wrapping
+    calls = a.warmup + a.steps
+    bad = sum(1 for k, v in ksum.items() if merged.get(k) != (calls * v) & 0xFFFFFFFF)
+    nkeys_owned = len(ksum)
+    if ctx.dist is not None:
+        tt = torch.tensor([total_recs, bad, nkeys_owned], dtype=torch.float64)
+        ctx.dist.all_reduce(tt)
+        total_recs, bad, nkeys_owned = int(tt[0].item()), int(tt[1].item()), int(tt[2].item())
+    assert bad == 0 and len(merged) == nkeys_owned, \
+        f"c5-keyed-agg: {bad} keyed totals differ from the generator's sums ({len(merged)} vs {nkeys_owned} keys)"
     per = {k: v / a.steps for k, v in kms.items()}
     res = {"metric": "records/s", "value": total_recs * a.steps / elapsed, "unit": "records/s",
            "ms_per_step": elapsed / a.steps * 1e3, "scaling": "strong", "dtype": "u32",
@@ -523,8 +545,12 @@ def run_c5k(ctx, cpu):
            "kernel_ms_sum_over_partitions": per,
            "gbps_input_per_gpu": in_bytes * a.steps / elapsed / 1e9,
            "gbps_output_per_gpu": out_bytes[0] / elapsed / 1e9,
-           "merged_keys": int(keys.numel()), "state_checksum": int(sums.sum().item()) & 0xFFFFFFFF,
+           "merged_keys": len(merged), "state_checksum": sum(merged.values()) & 0xFFFFFFFF,
+           "state_check": f"ok: all {len(merged)} topic keys == (warmup + steps) x the generator's per-key sums "
+                          f"(u32 wrapping), merged through fsg_keyed_* (exact keys, RCCL)",
            "setup_s": {"generate": gen_s}}
+    res["roofline"] = roofline(per, {"in_bytes": in_bytes, "out_bytes": out_bytes[0] / a.steps}, "c5-keyed-agg",
+                               total_recs, 0)
     res["cpu_baseline"] = cpu.get("c5-keyed-agg")
     del rsl, chains
     return res

@@ -104,12 +104,12 @@ SIGNATURES = {
     "fsg_chain_builder_set_lookback": (ctypes.c_int, [VP, SZ, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint64]),
     "fsg_chain_get_accumulator": (ctypes.c_int, [VP, SZ, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
                                                  ctypes.POINTER(SZ)]),
-    "fsg_chain_keyed_state": (ctypes.c_int, [VP, SZ, VP, VP, SZ, ctypes.POINTER(SZ)]),
     "fsg_chain_last_timings": (ctypes.c_int, [VP, ctypes.POINTER(fsg_timings)]),
     "fsg_chain_free": (None, [VP]),
     "fsg_output_free": (None, [ctypes.POINTER(fsg_output)]),
     "fsg_batch_output_free": (None, [ctypes.POINTER(fsg_batch_output)]),
     "fsg_free": (None, [VP]),
+    "fsg_host_cache_trim": (None, []),
     "fsg_slice_upload": (ctypes.c_int, [VP, VP, SZ, PP]),
     "fsg_slice_info": (ctypes.c_int, [VP, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                       ctypes.POINTER(ctypes.c_uint64)]),
@@ -131,6 +131,14 @@ SIGNATURES = {
     "fsg_state_read": (ctypes.c_int, [VP, VP, SZ]),
     "fsg_state_device": (ctypes.c_int, [VP, PP]),
     "fsg_state_free": (None, [VP]),
+    "fsg_keyed_new": (ctypes.c_int, [VP, PP]),
+    "fsg_keyed_reset": (ctypes.c_int, [VP]),
+    "fsg_keyed_collect": (ctypes.c_int, [VP, VP, SZ]),
+    "fsg_keyed_allreduce": (ctypes.c_int, [VP, ctypes.POINTER(SZ), ctypes.POINTER(SZ)]),
+    "fsg_keyed_read": (ctypes.c_int, [VP, VP, SZ, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32),
+                                      SZ]),
+    "fsg_keyed_device": (ctypes.c_int, [VP, PP, PP, PP]),
+    "fsg_keyed_free": (None, [VP]),
 }
 
 FSG_DTYPE_I32, FSG_DTYPE_U32, FSG_DTYPE_I64, FSG_DTYPE_U64, FSG_DTYPE_F64 = range(5)
@@ -156,11 +164,27 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        L.fsg_debug_regex_match.restype = ctypes.c_int
-        L.fsg_debug_regex_match.argtypes = [ctypes.c_char_p, ctypes.c_char_p, SZ, ctypes.POINTER(ctypes.c_int),
-                                            ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         _lib = L
     return _lib
+
+
+_debug = None
+
+
+def debug_lib():
+    """The host-only test hook library (libfsg_debug.so: the regex -> DFA compiler
+    with no GPU); never part of libfsg.so or of any process call."""
+    global _debug
+    if _debug is None:
+        path = os.path.join(_HERE, "_lib", "libfsg_debug.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"libfsg_debug.so not built ({path}); run fluvio_amd._ffi.build()")
+        D = ctypes.CDLL(path)
+        D.fsg_debug_regex_match.restype = ctypes.c_int
+        D.fsg_debug_regex_match.argtypes = [ctypes.c_char_p, ctypes.c_char_p, SZ, ctypes.POINTER(ctypes.c_int),
+                                            ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+        _debug = D
+    return _debug
 
 
 def buf_ptr(data):

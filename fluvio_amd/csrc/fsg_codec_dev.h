@@ -293,11 +293,21 @@ __device__ bool snappy_frames_dev(const uint8_t* s, uint64_t n, DecOut& o, const
 }
 
 // ---- gzip member (RFC 1952) over inflate (RFC 1951)
+// The canonical-code construction (count / offs / sym) and the stored / fixed /
+// dynamic block walk follow the structure of Mark Adler's public-domain puff.c
+// (zlib contrib/puff); decoding is table-driven here (9-bit first-level table,
+// canonical walk only for longer codes).
 struct Bits {
   const uint8_t* s;
   uint64_t n, i;
   uint32_t buf, cnt;
   bool bad;
+  __device__ void fill(uint32_t k) {  // up to k (<= 24) bits buffered, fewer at the end of the stream
+    while (cnt < k && i < n) {
+      buf |= (uint32_t)s[i++] << cnt;
+      cnt += 8;
+    }
+  }
   __device__ uint32_t get(uint32_t k) {  // k <= 24
     while (cnt < k) {
       if (i >= n) {
@@ -313,9 +323,11 @@ struct Bits {
     return v;
   }
 };
+constexpr int kHuffFast = 9;  // first-level table bits
 struct Huff {
   uint16_t cnt[16];
   uint16_t sym[288];
+  uint16_t fast[1 << kHuffFast];  // stream bits (LSB first) -> sym << 4 | len, 0 = longer code
 };
 // canonical code lengths -> counts / symbols; false if over-subscribed
 // (incomplete codes are allowed, as zlib allows a single distance code)
@@ -334,9 +346,30 @@ __device__ bool huff_build(Huff& h, const uint8_t* len, int n) {
   for (int k = 1; k < 15; k++) offs[k + 1] = offs[k] + h.cnt[k];
   for (int s = 0; s < n; s++)
     if (len[s]) h.sym[offs[len[s]]++] = (uint16_t)s;
+  // first-level table: canonical codes in symbol order within each length,
+  // bit-reversed (deflate sends codes MSB first into an LSB-first stream)
+  for (int k = 0; k < (1 << kHuffFast); k++) h.fast[k] = 0;
+  int code = 0, idx = 0;
+  for (int L = 1; L <= kHuffFast; L++) {
+    for (int j = 0; j < h.cnt[L]; j++, code++) {
+      uint32_t r = 0;
+      for (int q = 0; q < L; q++) r |= (uint32_t)((code >> q) & 1) << (L - 1 - q);
+      const uint16_t e = (uint16_t)((h.sym[idx + j] << 4) | L);
+      for (uint32_t f = r; f < (1u << kHuffFast); f += 1u << L) h.fast[f] = e;
+    }
+    idx += h.cnt[L];
+    code <<= 1;
+  }
   return true;
 }
 __device__ int huff_decode(Bits& b, const Huff& h) {
+  b.fill(kHuffFast);
+  const uint32_t e = h.fast[b.buf & ((1u << kHuffFast) - 1u)];
+  if (e && (e & 15u) <= b.cnt) {
+    b.buf >>= e & 15u;
+    b.cnt -= e & 15u;
+    return (int)(e >> 4);
+  }
   int code = 0, first = 0, index = 0;
   for (int k = 1; k < 16; k++) {
     code |= (int)b.get(1);

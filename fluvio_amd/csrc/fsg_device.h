@@ -435,5 +435,67 @@ struct DecArgs {
 constexpr uint32_t kSkipEntry = 0xFFFFFFFFu;
 constexpr uint32_t kAjLds = 4096;  // k_aggj_text keeps up to this many values in LDS
 
+// aggregate-json state kept in HBM between calls (fsg_keyed.hip k_ajc_*): after
+// a call, the map as it stands after the last record folded through the stop
+// batch (process_batch's last processed batch) is rewritten into the chain's
+// other state buffer: per key id (insertion order) its match bytes and its
+// serialized text in one arena, and its u32 value.  The next call reads it as
+// its initial keys, so no accumulator text crosses PCIe and nothing is parsed
+// on the host after the first call.
+struct AjState {
+  uint8_t* arena;        // per key: match bytes, then text bytes
+  uint64_t* kptr;        // match bytes (device address)
+  uint32_t* klen;
+  uint64_t* tptr;        // serialized text ("..." with escapes)
+  uint32_t* tlen;
+  uint32_t* val;
+  uint32_t* blen;        // scratch: match + text bytes per key
+  uint64_t* boff;        // ... exclusive prefix
+};
+struct AjCommitArgs {
+  AggjArgs a;            // this call's dictionary, records, entries
+  int32_t stop;          // the last processed batch (plan.stop, >= 0)
+  uint32_t kmax;         // key ids of this call (n_init + new keys): the grid bound
+  AjState dst;
+  unsigned long long* out;  // [0] keys after the stop batch [1] records folded through it [2] arena bytes
+};
+
+// Topic-wide keyed totals (fsg_keyed_*, C5 keyed): a rank-local table of exact
+// keys (bytes in an arena, open addressing over key indices), values summed
+// u32-wrapping from the chains' aggregate-json states; the merge across ranks
+// all-gathers the key lists, builds the union dictionary (ids by first
+// occurrence in rank order: identical on every rank) and all-reduces a dense
+// K-slot u32 table.
+struct KdTable {
+  uint8_t* arena;
+  uint64_t* koff;        // key i: arena offset ...
+  uint32_t* klen;        // ... and length (kKdDead: a lost duplicate)
+  uint32_t* val;
+  uint32_t* slot;        // slot -> key index + 1 (0 empty)
+  uint32_t cap;          // slots (power of two)
+  unsigned long long* cnt;  // [0] keys [1] arena bytes
+};
+constexpr uint32_t kKdDead = 0xFFFFFFFFu;
+struct KdUnionArgs {
+  const uint64_t* gdesc;   // all-gathered descriptors: rank r's key i at r * maxn + i
+  const uint8_t* garena;   // all-gathered arenas: rank r's at r * maxb
+  uint64_t maxb;
+  uint32_t maxn, nitems;   // nitems = nranks * maxn
+  uint32_t me;             // this rank
+  const uint32_t* lval;    // this rank's local values (by local key index)
+  uint32_t* slot;          // union table
+  uint32_t cap;
+  uint32_t* gslot;         // per item: its slot
+  uint32_t* first;         // per item: 1 at a key's first occurrence
+  uint64_t* idpre;         // ... exclusive prefix = the union id
+  uint32_t* gid;           // per item: union id
+  uint32_t* ulen;          // per union id: key bytes
+  uint64_t* uoff;          // ... exclusive prefix
+  uint8_t* uarena;         // union keys, id order
+  uint32_t* dense;         // K-slot u32 table (this rank's values; summed by the all-reduce)
+  uint64_t* tsum;          // scan scratch
+  unsigned long long* tot; // [0] K [1] union arena bytes
+};
+
 
 }  // namespace fsg

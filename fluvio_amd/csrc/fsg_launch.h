@@ -35,6 +35,19 @@ void launch_aggj_kid(const AggjArgs& a, uint64_t n_ent, hipStream_t s);
 void launch_aggj_rows(const AggjArgs& a, hipStream_t s);
 void launch_aggj_size(const AggjArgs& a, uint64_t* tsum, hipStream_t s);
 void launch_aggj_write(const AggjArgs& a, hipStream_t s);
+void launch_xscan(const uint32_t* in, uint64_t* out, uint64_t* tsum, uint64_t n, unsigned long long* tot,
+                  hipStream_t s);
+// aggregate-json state kept in HBM (fsg_keyed.hip)
+// pass 0: out[0] keys, out[1] records, out[2] arena bytes (sizes the arena); pass 1: the state
+void launch_aggj_commit(const AjCommitArgs& c, uint64_t* tsum, int pass, hipStream_t s);
+// keyed tables and the union dictionary of the topic-wide merge (fsg_keyed.hip)
+void launch_kd_collect(const KdTable& t, const uint64_t* sptr, const uint32_t* slen, const uint32_t* sval, uint32_t n,
+                       hipStream_t s);
+void launch_kd_rehash(const KdTable& t, uint32_t n, hipStream_t s);
+void launch_kd_desc(const KdTable& t, uint32_t n, uint32_t maxn, uint64_t* desc, hipStream_t s);
+void launch_kd_union(const KdUnionArgs& u, hipStream_t s);       // tot[0] = K
+void launch_kd_ids(const KdUnionArgs& u, hipStream_t s);
+void launch_kd_place(const KdUnionArgs& u, uint64_t nkeys, hipStream_t s);  // tot[1] = union bytes
 // stateful last stages (SfArgs): filter_look_back / filter_hashset
 void launch_sf_lb(const SfArgs& a, hipStream_t s);
 void launch_sf_dedup(const SfArgs& a, hipStream_t s);      // decisions assuming no eviction; scal[3] = kept

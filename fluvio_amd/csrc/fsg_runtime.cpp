@@ -18,6 +18,7 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstdio>
@@ -337,7 +338,7 @@ bool parse_acc_map(const std::vector<uint8_t>& s, AccMap& m) {
   return true;
 }
 
-// an environment switch (experiments: FSG_NO_FLAT=1 takes k_eval_lean instead of k_flat)
+// an environment switch (experiments: FSG_FLAT=1 takes k_flat instead of k_eval_lean)
 bool getenv_flag(const char* name) {
   static std::map<std::string, bool> cache;
   static std::mutex mu;
@@ -454,6 +455,10 @@ struct fsg_slice {
   int64_t crc_first = -1;
   float crc_ms = 0;
   std::vector<uint64_t> hbpos, hrbase;  // host framing (kept: the H2D copies may still be reading them)
+  size_t dec_limit = 1000000000;  // largest decompressed batch (the store limit, engine.rs:24)
+  // framing / decompression scratch, grown and kept across uploads into this
+  // slice (hipFree synchronises the whole device)
+  DevBuf fr[12], dec[8];
 };
 
 constexpr size_t kPinPlan = 256;           // pinned block: Plan, then the small output
@@ -477,9 +482,21 @@ struct fsg_chain {
   DevBuf bstat, kept, rows, pre, aggpre, tiles, grand, mins, plan, out, crcparts, defer, elem, cat;
   DevBuf dstate;  // aggregate-sum accumulator (i32) after the last call, in HBM
   // aggregate-json: key dictionary, index, initial keys, per-batch accumulator text
-  DevBuf aj_kptr, aj_klen, aj_tptr, aj_tlen, aj_kup, aj_vinit, aj_arena, aj_out, aj_accoff, aj_acclen;  // aggregate-json
+  DevBuf aj_tptr, aj_tlen, aj_kup, aj_out, aj_accoff, aj_acclen;  // aggregate-json
   DevBuf aj_bcnt, aj_brec, aj_rdesc, aj_rne, aj_rent, aj_rnew, aj_rnewb, aj_rlen, aj_roff, aj_ekid, aj_eval;
   DevBuf aj_sref, aj_sid, aj_state, aj_state2, aj_tsum;
+  // the aggregate-json map between calls, in HBM (fsg_keyed.hip k_ajc_*):
+  // ajs[aj_cur] holds it, the commit after a call writes the other buffer
+  struct AjBuf {
+    DevBuf arena, kptr, klen, tptr, tlen, val, blen, boff;
+  } ajs[2];
+  int aj_cur = 0;
+  bool aj_dev = false;      // the state lives in ajs[aj_cur] (the initial accumulator was parsed once)
+  bool aj_touched = false;  // a record was folded: the accumulator is the map's text, not c->acc
+  uint32_t aj_K = 0;        // keys in the state
+  uint64_t aj_bytes = 0;    // its arena bytes
+  DevBuf aj_cout;           // commit scalars
+  hipEvent_t kd_ev[2] = {}; // keyed collect: chain stream -> collect stream -> chain stream
   DevBuf rstart, rend;  // k_chase (lean path record starts)
   DevBuf bwin;          // k_flat_frame: per-batch window descriptors
   // stateful last stage (filter_look_back / filter_hashset)
@@ -506,6 +523,8 @@ struct fsg_chain {
       if (e) (void)hipEventDestroy(e);
     for (auto& e : dl_ev)
       if (e) (void)hipEventDestroy(e);
+    for (auto& e : kd_ev)
+      if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -521,6 +540,8 @@ extern "C" int fsg_device_count(int* count) {
   return FSG_OK;
 }
 
+static std::atomic<int> g_engines{0};  // live engines: the last fsg_engine_free drains the host pool
+
 extern "C" int fsg_engine_new(int device, fsg_engine** out) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(FSG_E_DEVICE, "no HIP device available");
@@ -532,6 +553,7 @@ extern "C" int fsg_engine_new(int device, fsg_engine** out) {
   auto* e = new fsg_engine();
   e->device = device;
   e->coll = coll;
+  g_engines.fetch_add(1);
   *out = e;
   return FSG_OK;
 }
@@ -541,6 +563,7 @@ extern "C" void fsg_engine_free(fsg_engine* e) {
   if (e->comm) ncclCommDestroy(e->comm);
   if (e->coll) (void)hipStreamDestroy(e->coll);
   delete e;
+  if (g_engines.fetch_sub(1) == 1) fsg_host_cache_trim();
 }
 
 // ---------------------------------------------------------------------------
@@ -872,7 +895,7 @@ int frame_on_device(fsg_slice* sl, hipStream_t st, int* fallback) {
     return FSG_OK;
   }
   const uint32_t nchunks = (uint32_t)((len + kFrameChunk - 1) / kFrameChunk);
-  DevBuf cbuf, ccnt, coff, tsum, scal;
+  DevBuf &cbuf = sl->fr[0], &ccnt = sl->fr[1], &coff = sl->fr[2], &tsum = sl->fr[3], &scal = sl->fr[4];
   HIPCHK(cbuf.ensure((size_t)nchunks * kFrameCap * 2));
   HIPCHK(ccnt.ensure((size_t)nchunks * 4));
   HIPCHK(coff.ensure((size_t)nchunks * 8));
@@ -895,7 +918,8 @@ int frame_on_device(fsg_slice* sl, hipStream_t st, int* fallback) {
     *fallback = 1;
     return FSG_OK;
   }
-  DevBuf cand, jmp, term, mark, mpre, nrec, rpre;
+  DevBuf &cand = sl->fr[5], &jmp = sl->fr[6], &term = sl->fr[7], &mark = sl->fr[8], &mpre = sl->fr[9],
+         &nrec = sl->fr[10], &rpre = sl->fr[11];
   uint32_t levels = 1;
   while (levels < 40 && (1ull << (levels - 1)) < n) levels++;
   HIPCHK(cand.ensure(n * 8));
@@ -954,7 +978,8 @@ int frame_on_device(fsg_slice* sl, hipStream_t st, int* fallback) {
 int decompress_slice(fsg_slice* sl, const std::vector<uint64_t>& bpos, const std::vector<uint8_t>& codecs,
                      hipStream_t st) {
   const uint32_t nb = (uint32_t)bpos.size();
-  DevBuf dbpos, dcodec, dsize, npos, status, cnt;
+  DevBuf &dbpos = sl->dec[0], &dcodec = sl->dec[1], &dsize = sl->dec[2], &npos = sl->dec[3], &status = sl->dec[4],
+         &cnt = sl->dec[5];
   HIPCHK(dbpos.ensure(std::max<size_t>(nb, 1) * 8));
   HIPCHK(dcodec.ensure(std::max<size_t>(nb, 1)));
   HIPCHK(dsize.ensure(std::max<size_t>(nb, 1) * 8));
@@ -974,7 +999,7 @@ int decompress_slice(fsg_slice* sl, const std::vector<uint64_t>& bpos, const std
   a.status = status.as<int32_t>();
   a.cnt = cnt.as<uint64_t>();
   {  // the stored CRCs cover the compressed bytes: verify them before they go
-    DevBuf bad;
+    DevBuf& bad = sl->dec[6];
     HIPCHK(bad.ensure(16));
     const unsigned long long init[2] = {0, ~0ull};
     HIPCHK(hipMemcpyAsync(bad.p, init, sizeof init, hipMemcpyHostToDevice, st));
@@ -1011,7 +1036,31 @@ int decompress_slice(fsg_slice* sl, const std::vector<uint64_t>& bpos, const std
     np[b] = total;
     total += 57 + (uint64_t)ds[b];
   }
-  DevBuf nd;
+  // Bound what a small compressed slice may ask for before anything is
+  // allocated (gzip expands up to ~1000x, lz4 ~255x).  The reference hands one
+  // decompressed batch at a time to a guest whose memory is capped by the store
+  // limit (engine.rs:24, limiter.rs:18-35): a batch larger than the limit is
+  // StoreMemoryExceeded.  Here the whole decompressed slice is resident, so its
+  // total must also fit in half of the device's free memory.
+  {
+    uint64_t need = 0, big = 0;
+    for (uint32_t b = 0; b < keep; b++) big = std::max<uint64_t>(big, (uint64_t)ds[b]);
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
+    const uint64_t budget = fr / 2;
+    if (big > sl->dec_limit) need = big;
+    else if (total + kSlicePad + kWin > budget) need = total;
+    if (need) {
+      char b[200];
+      snprintf(b, sizeof b, "Requested memory %llub exceeded max allowed %llub (decompressed record sections)",
+               (unsigned long long)need, (unsigned long long)(big > sl->dec_limit ? sl->dec_limit : budget));
+      g_store_mem[0] = 0;
+      g_store_mem[1] = need;
+      g_store_mem[2] = big > sl->dec_limit ? sl->dec_limit : budget;
+      return fail(FSG_E_STORE_MEMORY, b);
+    }
+  }
+  DevBuf& nd = sl->dec[7];  // swapped with the compressed slice below: both stay for the next upload
   const size_t alloc = ((total + 15) & ~(size_t)15) + kSlicePad + kWin;
   HIPCHK(nd.ensure(alloc));
   HIPCHK(hipMemsetAsync(nd.p, 0, alloc, st));
@@ -1521,6 +1570,132 @@ int sf_run(fsg_chain* c, const fsg_slice* s, const EvalArgs& ea, SfArgs& sa, hip
   return FSG_OK;
 }
 
+// aggregate-json state in HBM.  The first call (or a keyed collect before any
+// call) parses the initial accumulator once (unwrap_or_default, as the guest's
+// serde_json::from_slice) into ajs[aj_cur]: per key its match bytes and its
+// serialized text in one arena, and its value.
+int aj_state_init(fsg_chain* c) {
+  if (c->aj_dev) return FSG_OK;
+  AccMap am;
+  parse_acc_map(c->acc, am);
+  const uint32_t n = (uint32_t)am.keys.size();
+  std::vector<uint8_t> arena;
+  std::vector<uint64_t> ko(n), to(n);
+  std::vector<uint32_t> kl(n), tl(n);
+  for (uint32_t k = 0; k < n; k++) {
+    ko[k] = arena.size();
+    arena.insert(arena.end(), am.keys[k].begin(), am.keys[k].end());
+    to[k] = arena.size();
+    arena.insert(arena.end(), am.text[k].begin(), am.text[k].end());
+    kl[k] = (uint32_t)am.keys[k].size();
+    tl[k] = (uint32_t)am.text[k].size();
+  }
+  fsg_chain::AjBuf& S = c->ajs[c->aj_cur];
+  const size_t n1 = std::max<uint32_t>(n, 1);
+  HIPCHK(S.arena.ensure(arena.size() + 16));
+  HIPCHK(S.kptr.ensure(n1 * 8));
+  HIPCHK(S.klen.ensure(n1 * 4));
+  HIPCHK(S.tptr.ensure(n1 * 8));
+  HIPCHK(S.tlen.ensure(n1 * 4));
+  HIPCHK(S.val.ensure(n1 * 4));
+  const uint64_t base = (uint64_t)S.arena.p;
+  for (uint32_t k = 0; k < n; k++) {
+    ko[k] += base;
+    to[k] += base;
+  }
+  hipStream_t st = c->stream;
+  if (n) {
+    HIPCHK(hipMemcpyAsync(S.arena.p, arena.data(), arena.size(), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.kptr.p, ko.data(), n * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.tptr.p, to.data(), n * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.klen.p, kl.data(), n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.tlen.p, tl.data(), n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.val.p, am.vals.data(), n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));  // the host vectors go out of scope
+  }
+  c->aj_K = n;
+  c->aj_bytes = arena.size();
+  c->aj_dev = true;
+  return FSG_OK;
+}
+
+// the map after the stop batch into the other state buffer (two phases: the
+// arena is sized by a scan), then it becomes the state
+int aj_commit(fsg_chain* c, const AggjArgs& aj, int32_t stop, uint32_t kmax) {
+  hipStream_t st = c->stream;
+  fsg_chain::AjBuf& D = c->ajs[1 - c->aj_cur];
+  const size_t k1 = std::max<uint32_t>(kmax, 1);
+  HIPCHK(D.kptr.ensure(k1 * 8));
+  HIPCHK(D.klen.ensure(k1 * 4));
+  HIPCHK(D.tptr.ensure(k1 * 8));
+  HIPCHK(D.tlen.ensure(k1 * 4));
+  HIPCHK(D.val.ensure(k1 * 4));
+  HIPCHK(D.blen.ensure(k1 * 4));
+  HIPCHK(D.boff.ensure(k1 * 8));
+  HIPCHK(D.arena.ensure(16));
+  HIPCHK(c->aj_cout.ensure(64));
+  HIPCHK(c->aj_tsum.ensure(xscan_tiles(k1) * 8));
+  AjCommitArgs ca{};
+  ca.a = aj;
+  ca.stop = stop;
+  ca.kmax = kmax;
+  ca.out = c->aj_cout.as<unsigned long long>();
+  ca.dst.arena = D.arena.as<uint8_t>();
+  ca.dst.kptr = D.kptr.as<uint64_t>();
+  ca.dst.klen = D.klen.as<uint32_t>();
+  ca.dst.tptr = D.tptr.as<uint64_t>();
+  ca.dst.tlen = D.tlen.as<uint32_t>();
+  ca.dst.val = D.val.as<uint32_t>();
+  ca.dst.blen = D.blen.as<uint32_t>();
+  ca.dst.boff = D.boff.as<uint64_t>();
+  launch_aggj_commit(ca, c->aj_tsum.as<uint64_t>(), 0, st);
+  unsigned long long o[3] = {0, 0, 0};
+  HIPCHK(hipMemcpyAsync(o, ca.out, sizeof o, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (o[1] == 0) return FSG_OK;  // no record folded through the stop batch: the state stands
+  HIPCHK(D.arena.ensure(o[2] + 16));
+  ca.dst.arena = D.arena.as<uint8_t>();
+  launch_aggj_commit(ca, c->aj_tsum.as<uint64_t>(), 1, st);
+  HIPCHK(hipGetLastError());
+  c->aj_cur = 1 - c->aj_cur;
+  c->aj_K = (uint32_t)o[0];
+  c->aj_bytes = o[2];
+  c->aj_touched = true;
+  return FSG_OK;
+}
+
+// serde_json::to_vec_pretty of the state (the text the guest's last record
+// carried): "{}" or "{\n  key: v,\n  ...\n}", keys in insertion order
+int aj_render(fsg_chain* c, std::vector<uint8_t>& out) {
+  const fsg_chain::AjBuf& S = c->ajs[c->aj_cur];
+  const uint32_t K = c->aj_K;
+  HIPCHK(hipSetDevice(c->eng->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  std::vector<uint64_t> tp(K);
+  std::vector<uint32_t> tl(K), v(K);
+  std::vector<uint8_t> ar(c->aj_bytes);
+  if (K) {
+    HIPCHK(hipMemcpy(tp.data(), S.tptr.p, (size_t)K * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(tl.data(), S.tlen.p, (size_t)K * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(v.data(), S.val.p, (size_t)K * 4, hipMemcpyDeviceToHost));
+    if (!ar.empty()) HIPCHK(hipMemcpy(ar.data(), S.arena.p, ar.size(), hipMemcpyDeviceToHost));
+  }
+  out.clear();
+  out.push_back('{');
+  for (uint32_t k = 0; k < K; k++) {
+    const char* sep = k ? ",\n  " : "\n  ";
+    out.insert(out.end(), sep, sep + strlen(sep));
+    const uint64_t off = tp[k] - (uint64_t)S.arena.p;
+    out.insert(out.end(), ar.begin() + off, ar.begin() + off + tl[k]);
+    char b[16];
+    const int n = snprintf(b, sizeof b, ": %u", v[k]);
+    out.insert(out.end(), b, b + n);
+  }
+  if (K) out.push_back('\n');
+  out.push_back('}');
+  return FSG_OK;
+}
+
 int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics* m, fsg_batch_output* res,
               bool empty_chain_io) {
   hipStream_t st = c->stream;
@@ -1598,7 +1773,9 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   ea.rstart = c->rstart.as<uint16_t>();
   ea.rend = c->rend.as<uint16_t>();
   // substring filters / uppercase maps: the register-resident path (fsg_flat.hip)
-  const bool flat = lean && !getenv_flag("FSG_NO_FLAT") && flat_eligible(c->hdesc, ops);
+  // is an experiment, opt-in with FSG_FLAT=1: measured on MI355X (C2, round 3)
+  // k_flat 2.56 ms against k_eval_lean 1.61 ms, parity-green both ways
+  const bool flat = lean && getenv_flag("FSG_FLAT") && flat_eligible(c->hdesc, ops);
   if (lean) HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
   if (flat) {
     HIPCHK(c->bwin.ensure((size_t)std::max<uint32_t>(nb, 1) * sizeof(BatchWin)));
@@ -1618,10 +1795,12 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   }
   // aggregate-json: fold the entries in stream order, size every record's map text
   AggjArgs aj{};
-  AccMap am;
+  uint64_t aj_nnew = 0;
   if (has_aggj) {
-    parse_acc_map(c->acc, am);  // unwrap_or_default
-    const uint32_t n_init = (uint32_t)am.keys.size();
+    int rc0 = aj_state_init(c);  // the initial accumulator, parsed once (unwrap_or_default)
+    if (rc0) return rc0;
+    const uint32_t n_init = c->aj_K;
+    const fsg_chain::AjBuf& S = c->ajs[c->aj_cur];
     const size_t nbb = std::max<uint32_t>(nb, 1);
     HIPCHK(c->aj_out.ensure(64));
     HIPCHK(c->aj_bcnt.ensure(nbb * 4));
@@ -1674,37 +1853,16 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     HIPCHK(c->aj_tptr.ensure(nkmax * 8));
     HIPCHK(c->aj_tlen.ensure(nkmax * 4));
     HIPCHK(c->aj_kup.ensure(nkmax * 4));
-    HIPCHK(c->aj_kptr.ensure((size_t)(n_init + 1) * 8));
-    HIPCHK(c->aj_klen.ensure((size_t)(n_init + 1) * 4));
-    HIPCHK(c->aj_vinit.ensure((size_t)(n_init + 1) * 4));
     HIPCHK(c->aj_tsum.ensure(xscan_tiles(std::max<uint64_t>(nrec, std::max<uint64_t>(nent, nb))) * 8));
     HIPCHK(hipMemsetAsync(c->aj_sref.p, 0, (size_t)cap * 8, st));
-    if (n_init) {  // the initial accumulator's keys: match bytes and serialized text in one arena
-      std::vector<uint8_t> arena;
-      std::vector<uint64_t> ko(n_init), to(n_init);
-      std::vector<uint32_t> kl(n_init), tl(n_init), zero(n_init, 0);
-      for (uint32_t k = 0; k < n_init; k++) {
-        ko[k] = arena.size();
-        arena.insert(arena.end(), am.keys[k].begin(), am.keys[k].end());
-        to[k] = arena.size();
-        arena.insert(arena.end(), am.text[k].begin(), am.text[k].end());
-        kl[k] = (uint32_t)am.keys[k].size();
-        tl[k] = (uint32_t)am.text[k].size();
-      }
-      HIPCHK(c->aj_arena.ensure(arena.size() + 16));
-      const uint64_t base = (uint64_t)c->aj_arena.p;
-      for (uint32_t k = 0; k < n_init; k++) {
-        ko[k] += base;
-        to[k] += base;
-      }
-      HIPCHK(hipMemcpyAsync(c->aj_arena.p, arena.data(), arena.size(), hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(c->aj_kptr.p, ko.data(), n_init * 8, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(c->aj_tptr.p, to.data(), n_init * 8, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(c->aj_klen.p, kl.data(), n_init * 4, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(c->aj_tlen.p, tl.data(), n_init * 4, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(c->aj_kup.p, zero.data(), n_init * 4, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(c->aj_vinit.p, am.vals.data(), n_init * 4, hipMemcpyHostToDevice, st));
+    if (n_init) {  // the state's keys (match bytes, text, values) straight from HBM
+      HIPCHK(hipMemcpyAsync(c->aj_tptr.p, S.tptr.p, (size_t)n_init * 8, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipMemcpyAsync(c->aj_tlen.p, S.tlen.p, (size_t)n_init * 4, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipMemsetAsync(c->aj_kup.p, 0, (size_t)n_init * 4, st));
     }
+    aj.kptr = S.kptr.as<uint64_t>();
+    aj.klen = S.klen.as<uint32_t>();
+    aj.val_init = S.val.as<uint32_t>();
     aj.n_rec = nrec;
     aj.rdesc = c->aj_rdesc.as<uint64_t>();
     aj.rne = c->aj_rne.as<uint32_t>();
@@ -1718,9 +1876,6 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     aj.slot_ref = c->aj_sref.as<unsigned long long>();
     aj.slot_id = c->aj_sid.as<uint32_t>();
     aj.cap = cap;
-    aj.kptr = c->aj_kptr.as<uint64_t>();
-    aj.klen = c->aj_klen.as<uint32_t>();
-    aj.val_init = c->aj_vinit.as<uint32_t>();
     aj.tptr = c->aj_tptr.as<uint64_t>();
     aj.tlen = c->aj_tlen.as<uint32_t>();
     aj.kup = c->aj_kup.as<uint32_t>();
@@ -1730,17 +1885,19 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     HIPCHK(hipMemcpyAsync(&nnew, aj.scal + 2, sizeof nnew, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     const uint64_t K = n_init + nnew;
+    aj_nnew = nnew;
     // blocks of rb records: ~4096 blocks (one wave each), the row table
     // nblk x K bounded to 64 Mi values
     uint64_t rb = std::max<uint64_t>(32, (nrec + 4095) / 4096);
     while (((nrec + rb - 1) / rb) * K > (64ull << 20) && rb < nrec) rb *= 2;
     const uint64_t nblk = nrec ? (nrec + rb - 1) / rb : 0;
     const size_t rows = (size_t)std::max<uint64_t>(nblk * K, 1) * 4;
-    if (dict + rows * (K > kAjLds ? 2 : 1) > c->limit) {
+    const size_t need_rows = dict + rows * (K > kAjLds ? 2 : 1);  // a copy of the rows when K > kAjLds
+    if (need_rows > c->limit) {
       char b[160];
-      snprintf(b, sizeof b, "Requested memory %zub exceeded max allowed %zub", dict + rows, c->limit);
+      snprintf(b, sizeof b, "Requested memory %zub exceeded max allowed %zub", need_rows, c->limit);
       g_store_mem[0] = dict;
-      g_store_mem[1] = dict + rows;
+      g_store_mem[1] = need_rows;
       g_store_mem[2] = c->limit;
       return fail(FSG_E_STORE_MEMORY, b);
     }
@@ -1912,16 +2069,9 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     if (rc) return rc;
     res->has_error = 1;
   }
-  if (has_aggj && p.stop >= 0) {  // the accumulator text after the last processed batch
-    uint64_t off = 0;
-    uint32_t len = 0xFFFFFFFFu;
-    HIPCHK(hipMemcpy(&off, c->aj_accoff.as<uint64_t>() + p.stop, sizeof off, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(&len, c->aj_acclen.as<uint32_t>() + p.stop, sizeof len, hipMemcpyDeviceToHost));
-    if (len != 0xFFFFFFFFu) {
-      std::vector<uint8_t> na(len);
-      if (len) HIPCHK(hipMemcpy(na.data(), c->cat.as<uint8_t>() + off, len, hipMemcpyDeviceToHost));
-      c->acc.swap(na);
-    }
+  if (has_aggj && p.stop >= 0) {  // the map after the last processed batch stays in HBM
+    int rc = aj_commit(c, aj, p.stop, (uint32_t)(aj.n_init + aj_nnew));
+    if (rc) return rc;
   }
   if (has_agg && !has_aggj && p.acc_touched) {
     if (has_cat) {
@@ -1997,6 +2147,20 @@ void host_free(const void* q) {
   free(p);
 }
 
+}  // namespace
+
+// frees every parked output buffer (buffers still held by the caller are untouched)
+extern "C" void fsg_host_cache_trim(void) {
+  HostPool& hp = host_pool();
+  std::vector<std::pair<void*, size_t>> v;
+  {
+    std::lock_guard<std::mutex> g(hp.mu);
+    v.swap(hp.parked);
+  }
+  for (auto& b : v) free(b.first);
+}
+
+namespace {
 constexpr size_t kDlChunk = 32u << 20;
 constexpr size_t kDlStaged = 128u << 20;  // outputs from here on take the staged download
 constexpr int kDlThreads = 4;
@@ -2093,6 +2257,7 @@ extern "C" int fsg_chain_output_device(fsg_chain* c, const void** dptr, size_t* 
 extern "C" int fsg_chain_process_batch(fsg_chain* c, const uint8_t* slice, size_t len, uint64_t max_bytes,
                                        fsg_metrics* m, fsg_batch_output** out) {
   HIPCHK(hipSetDevice(c->eng->device));
+  c->ingest.dec_limit = c->limit;
   int rc = upload_slice(c->eng, slice, len, &c->ingest, c->stream);
   if (rc) return rc;
   return fsg_chain_process_slice(c, &c->ingest, max_bytes, m, out);
@@ -2225,32 +2390,17 @@ extern "C" int fsg_chain_look_back(fsg_chain* c, fsg_read_fn read_fn, void* user
 
 extern "C" int fsg_chain_get_accumulator(fsg_chain* c, size_t stage, uint8_t** acc, size_t* len) {
   if ((int)stage != c->agg_stage) return fail(FSG_E_INVALID_ARG, "stage is not an aggregate");
-  *acc = (uint8_t*)malloc(std::max<size_t>(1, c->acc.size()));
-  memcpy(*acc, c->acc.data(), c->acc.size());
-  *len = c->acc.size();
-  return FSG_OK;
-}
-
-extern "C" int fsg_chain_keyed_state(fsg_chain* c, size_t stage, uint64_t* dev_fp, uint32_t* dev_val, size_t cap,
-                                     size_t* n) {
-  if ((int)stage != c->agg_stage || !(c->hdesc.flags & CF_AGG_JSON))
-    return fail(FSG_E_INVALID_ARG, "stage is not an aggregate-json aggregate");
-  AccMap m;
-  parse_acc_map(c->acc, m);  // the accumulator as the next record would read it
-  std::vector<uint64_t> fp(m.keys.size());
-  for (size_t k = 0; k < m.keys.size(); k++) {  // FNV-1a 64 of the key's bytes
-    uint64_t h = 14695981039346656037ull;
-    for (unsigned char ch : m.keys[k]) h = (h ^ ch) * 1099511628211ull;
-    fp[k] = h;
+  std::vector<uint8_t> txt;
+  const std::vector<uint8_t>* a = &c->acc;
+  if ((c->hdesc.flags & CF_AGG_JSON) && c->aj_touched) {  // rendered from the state in HBM
+    int rc = aj_render(c, txt);
+    if (rc) return rc;
+    a = &txt;
   }
-  *n = m.keys.size();
-  const size_t w = std::min(cap, m.keys.size());
-  HIPCHK(hipSetDevice(c->eng->device));
-  if (w) {
-    HIPCHK(hipMemcpyAsync(dev_fp, fp.data(), w * 8, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(dev_val, m.vals.data(), w * 4, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-  }
+  *acc = (uint8_t*)malloc(std::max<size_t>(1, a->size()));
+  if (!*acc) return fail(FSG_E_DEVICE, "host allocation failed");
+  if (!a->empty()) memcpy(*acc, a->data(), a->size());
+  *len = a->size();
   return FSG_OK;
 }
 
@@ -2329,6 +2479,7 @@ extern "C" int fsg_chain_allreduce_state(fsg_chain* c, void* dev_state, size_t c
 // ---------------------------------------------------------------------------
 struct fsg_state {
   fsg_engine* eng = nullptr;
+  std::mutex mu;
   DevBuf buf;
   size_t count = 0, esize = 4;
   int dtype = FSG_DTYPE_I32;
@@ -2357,9 +2508,14 @@ extern "C" int fsg_state_collect(fsg_state* s, size_t slot, fsg_chain* c) {
   if (c->eng->device != s->eng->device) return fail(FSG_E_INVALID_ARG, "chain and state on different devices");
   HIPCHK(hipSetDevice(s->eng->device));
   // device to device on the chain's stream, after its last k_state; chains of
-  // different partitions may collect from different host threads at once
+  // different partitions may collect from different host threads at once.  The
+  // merge stream waits for the copy on the device (no host wait per collect).
   HIPCHK(hipMemcpyAsync((uint8_t*)s->buf.p + slot * s->esize, c->dstate.p, 4, hipMemcpyDeviceToDevice, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  if (!c->kd_ev[0]) HIPCHK(hipEventCreateWithFlags(&c->kd_ev[0], hipEventDisableTiming));
+  if (!c->kd_ev[1]) HIPCHK(hipEventCreateWithFlags(&c->kd_ev[1], hipEventDisableTiming));
+  std::lock_guard<std::mutex> g(s->mu);  // hipStreamWaitEvent on the shared merge stream
+  HIPCHK(hipEventRecord(c->kd_ev[0], c->stream));
+  HIPCHK(hipStreamWaitEvent(s->eng->coll, c->kd_ev[0], 0));
   return FSG_OK;
 }
 extern "C" int fsg_state_allreduce(fsg_state* s) {
@@ -2376,3 +2532,266 @@ extern "C" int fsg_state_device(fsg_state* s, void** dptr) {
   return FSG_OK;
 }
 extern "C" void fsg_state_free(fsg_state* s) { delete s; }
+
+// ---------------------------------------------------------------------------
+// topic-wide keyed totals of aggregate-json states (C5 keyed, SURVEY §8 e)
+// ---------------------------------------------------------------------------
+struct fsg_keyed {
+  fsg_engine* eng = nullptr;
+  hipStream_t st = nullptr;
+  // rank-local table (KdTable)
+  DevBuf arena, koff, klen, val, slot, cnt;
+  uint32_t cap = 0;           // slots
+  uint64_t kcap = 0, acap = 0;  // key / arena capacity
+  uint64_t nb = 0, bb = 0;      // upper bounds of the keys / bytes in the table
+  // the merge
+  DevBuf gcnt, ldesc, gdesc, garena, uslot, gslot, first, idpre, gid, ulen, uoff, uarena, dense, tsum, tot;
+  uint64_t K = 0, ubytes = 0;
+  bool merged = false;
+  ~fsg_keyed() {
+    if (st) (void)hipStreamDestroy(st);
+  }
+  KdTable table() {
+    KdTable t;
+    t.arena = arena.as<uint8_t>();
+    t.koff = koff.as<uint64_t>();
+    t.klen = klen.as<uint32_t>();
+    t.val = val.as<uint32_t>();
+    t.slot = slot.as<uint32_t>();
+    t.cap = cap;
+    t.cnt = cnt.as<unsigned long long>();
+    return t;
+  }
+};
+
+namespace {
+uint32_t pow2_at_least(uint64_t n) {
+  uint32_t c = 16;
+  while (c < n) c <<= 1;
+  return c;
+}
+// room for `nk` more keys and `nbytes` more key bytes (grows and rehashes; rare)
+int kd_reserve(fsg_keyed* k, uint64_t nk, uint64_t nbytes) {
+  const uint64_t need_k = k->nb + nk, need_b = k->bb + nbytes;
+  if (need_k <= k->kcap && need_b + 16 <= k->acap && 2 * need_k <= k->cap) return FSG_OK;
+  hipStream_t st = k->st;
+  unsigned long long c[2] = {0, 0};
+  if (k->cnt.p) HIPCHK(hipMemcpyAsync(c, k->cnt.p, sizeof c, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const uint64_t kc = std::max<uint64_t>(2 * need_k, 1024), ac = std::max<uint64_t>(2 * need_b, 1 << 16);
+  DevBuf na, nko, nkl, nv, ns;
+  HIPCHK(na.ensure(ac + 16));
+  HIPCHK(nko.ensure(kc * 8));
+  HIPCHK(nkl.ensure(kc * 4));
+  HIPCHK(nv.ensure(kc * 4));
+  const uint32_t cap = pow2_at_least(2 * kc);
+  HIPCHK(ns.ensure((size_t)cap * 4));
+  HIPCHK(hipMemsetAsync(ns.p, 0, (size_t)cap * 4, st));
+  if (c[0]) {
+    HIPCHK(hipMemcpyAsync(na.p, k->arena.p, c[1], hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(nko.p, k->koff.p, c[0] * 8, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(nkl.p, k->klen.p, c[0] * 4, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(nv.p, k->val.p, c[0] * 4, hipMemcpyDeviceToDevice, st));
+  }
+  HIPCHK(k->cnt.ensure(16));
+  if (!k->kcap) HIPCHK(hipMemsetAsync(k->cnt.p, 0, 16, st));
+  HIPCHK(hipStreamSynchronize(st));
+  std::swap(k->arena.p, na.p);
+  std::swap(k->arena.cap, na.cap);
+  std::swap(k->koff.p, nko.p);
+  std::swap(k->koff.cap, nko.cap);
+  std::swap(k->klen.p, nkl.p);
+  std::swap(k->klen.cap, nkl.cap);
+  std::swap(k->val.p, nv.p);
+  std::swap(k->val.cap, nv.cap);
+  std::swap(k->slot.p, ns.p);
+  std::swap(k->slot.cap, ns.cap);
+  k->cap = cap;
+  k->kcap = kc;
+  k->acap = ac + 16;
+  launch_kd_rehash(k->table(), (uint32_t)c[0], st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));  // the old buffers are freed on return
+  return FSG_OK;
+}
+int kd_gather(fsg_keyed* k, const void* send, void* recv, size_t count, ncclDataType_t t, size_t esize) {
+  fsg_engine* e = k->eng;
+  if (!e->comm) {  // one rank without a communicator: the gather is a copy
+    if (count) HIPCHK(hipMemcpyAsync(recv, send, count * esize, hipMemcpyDeviceToDevice, k->st));
+    return FSG_OK;
+  }
+  ncclResult_t r = ncclAllGather(send, recv, count, t, e->comm, k->st);
+  if (r != ncclSuccess) return fail(FSG_E_DEVICE, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+  return FSG_OK;
+}
+}  // namespace
+
+extern "C" int fsg_keyed_new(fsg_engine* e, fsg_keyed** out) {
+  HIPCHK(hipSetDevice(e->device));
+  auto k = std::make_unique<fsg_keyed>();
+  k->eng = e;
+  HIPCHK(hipStreamCreateWithFlags(&k->st, hipStreamNonBlocking));
+  int rc = kd_reserve(k.get(), 1024, 1 << 16);
+  if (rc) return rc;
+  *out = k.release();
+  return FSG_OK;
+}
+
+extern "C" int fsg_keyed_reset(fsg_keyed* k) {
+  HIPCHK(hipSetDevice(k->eng->device));
+  HIPCHK(hipMemsetAsync(k->cnt.p, 0, 16, k->st));
+  HIPCHK(hipMemsetAsync(k->slot.p, 0, (size_t)k->cap * 4, k->st));
+  k->nb = k->bb = 0;
+  k->merged = false;
+  return FSG_OK;
+}
+
+extern "C" int fsg_keyed_collect(fsg_keyed* k, fsg_chain* c, size_t stage) {
+  if ((int)stage != c->agg_stage || !(c->hdesc.flags & CF_AGG_JSON))
+    return fail(FSG_E_INVALID_ARG, "stage is not an aggregate-json aggregate");
+  if (c->eng->device != k->eng->device) return fail(FSG_E_INVALID_ARG, "chain and keyed table on different devices");
+  HIPCHK(hipSetDevice(k->eng->device));
+  int rc = aj_state_init(c);  // a chain that has not processed anything yet: its initial accumulator
+  if (rc) return rc;
+  const uint32_t n = c->aj_K;
+  rc = kd_reserve(k, n, c->aj_bytes);
+  if (rc) return rc;
+  k->nb += n;
+  k->bb += c->aj_bytes;
+  k->merged = false;
+  for (auto& ev : c->kd_ev)
+    if (!ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  // the chain's state after its queued work; the chain's next commit waits
+  // for the collect (it may overwrite the other state buffer, never this one,
+  // but the one after it would)
+  HIPCHK(hipEventRecord(c->kd_ev[0], c->stream));
+  HIPCHK(hipStreamWaitEvent(k->st, c->kd_ev[0], 0));
+  const fsg_chain::AjBuf& S = c->ajs[c->aj_cur];
+  launch_kd_collect(k->table(), S.kptr.as<uint64_t>(), S.klen.as<uint32_t>(), S.val.as<uint32_t>(), n, k->st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->kd_ev[1], k->st));
+  HIPCHK(hipStreamWaitEvent(c->stream, c->kd_ev[1], 0));
+  return FSG_OK;
+}
+
+// The topic dictionary: every rank's key list all-gathered, the union built on
+// every rank (ids by first occurrence in rank order), then one all-reduce of
+// the dense K-slot u32 table.  World 1 (no communicator): the same steps with
+// device copies in place of the collectives.
+extern "C" int fsg_keyed_allreduce(fsg_keyed* k, size_t* n_keys, size_t* key_bytes) {
+  fsg_engine* e = k->eng;
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = k->st;
+  const int nr = e->comm ? e->nranks : 1, me = e->comm ? e->rank : 0;
+  HIPCHK(k->gcnt.ensure((size_t)nr * 16));
+  HIPCHK(k->tot.ensure(64));
+  int rc = kd_gather(k, k->cnt.p, k->gcnt.p, 2, ncclUint64, 8);
+  if (rc) return rc;
+  std::vector<unsigned long long> gc((size_t)nr * 2);
+  HIPCHK(hipMemcpyAsync(gc.data(), k->gcnt.p, gc.size() * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  uint64_t maxn = 1, maxb = 16;
+  for (int r = 0; r < nr; r++) {
+    maxn = std::max<uint64_t>(maxn, gc[2 * r]);
+    maxb = std::max<uint64_t>(maxb, gc[2 * r + 1]);
+  }
+  maxb = (maxb + 15) & ~15ull;
+  const uint64_t nloc = gc[2 * me];
+  if (maxn * (uint64_t)nr >= 0xFFFFFFF0ull) return fail(FSG_E_INVALID_ARG, "too many keys for the merge");
+  const uint32_t nitems = (uint32_t)(maxn * nr);
+  // the send buffers must hold maxn / maxb entries (all-gather counts are equal on every rank)
+  rc = kd_reserve(k, maxn > k->nb ? maxn - k->nb : 0, maxb > k->bb ? maxb - k->bb : 0);
+  if (rc) return rc;
+  HIPCHK(k->ldesc.ensure(maxn * 8));
+  HIPCHK(k->gdesc.ensure((size_t)nitems * 8));
+  HIPCHK(k->garena.ensure((size_t)nr * maxb + 16));
+  launch_kd_desc(k->table(), (uint32_t)nloc, (uint32_t)maxn, k->ldesc.as<uint64_t>(), st);
+  if (e->comm) ncclGroupStart();
+  rc = kd_gather(k, k->ldesc.p, k->gdesc.p, maxn, ncclUint64, 8);
+  if (!rc) rc = kd_gather(k, k->arena.p, k->garena.p, maxb, ncclUint8, 1);
+  if (e->comm) ncclGroupEnd();
+  if (rc) return rc;
+  const uint32_t ucap = pow2_at_least(2ull * nitems);
+  HIPCHK(k->uslot.ensure((size_t)ucap * 4));
+  HIPCHK(hipMemsetAsync(k->uslot.p, 0, (size_t)ucap * 4, st));
+  HIPCHK(k->gslot.ensure((size_t)nitems * 4));
+  HIPCHK(k->first.ensure((size_t)nitems * 4));
+  HIPCHK(k->idpre.ensure((size_t)nitems * 8));
+  HIPCHK(k->gid.ensure((size_t)nitems * 4));
+  HIPCHK(k->tsum.ensure(xscan_tiles(nitems) * 8));
+  KdUnionArgs u{};
+  u.gdesc = k->gdesc.as<uint64_t>();
+  u.garena = k->garena.as<uint8_t>();
+  u.maxb = maxb;
+  u.maxn = (uint32_t)maxn;
+  u.nitems = nitems;
+  u.me = (uint32_t)me;
+  u.lval = k->val.as<uint32_t>();
+  u.slot = k->uslot.as<uint32_t>();
+  u.cap = ucap;
+  u.gslot = k->gslot.as<uint32_t>();
+  u.first = k->first.as<uint32_t>();
+  u.idpre = k->idpre.as<uint64_t>();
+  u.gid = k->gid.as<uint32_t>();
+  u.tsum = k->tsum.as<uint64_t>();
+  u.tot = k->tot.as<unsigned long long>();
+  launch_kd_union(u, st);
+  unsigned long long K = 0;
+  HIPCHK(hipMemcpyAsync(&K, u.tot, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const size_t K1 = std::max<uint64_t>(K, 1);
+  HIPCHK(k->ulen.ensure(K1 * 4));
+  HIPCHK(k->uoff.ensure(K1 * 8));
+  HIPCHK(k->uarena.ensure((size_t)nr * maxb + 16));
+  HIPCHK(k->dense.ensure(K1 * 4));
+  HIPCHK(k->tsum.ensure(xscan_tiles(std::max<uint64_t>(nitems, K1)) * 8));
+  HIPCHK(hipMemsetAsync(k->dense.p, 0, K1 * 4, st));
+  u.ulen = k->ulen.as<uint32_t>();
+  u.uoff = k->uoff.as<uint64_t>();
+  u.uarena = k->uarena.as<uint8_t>();
+  u.dense = k->dense.as<uint32_t>();
+  u.tsum = k->tsum.as<uint64_t>();
+  launch_kd_ids(u, st);
+  launch_kd_place(u, K, st);
+  HIPCHK(hipGetLastError());
+  if (e->comm && K) {  // u32 sums wrap, like the guest's release-mode adds
+    ncclResult_t r = ncclAllReduce(k->dense.p, k->dense.p, K, ncclUint32, ncclSum, e->comm, st);
+    if (r != ncclSuccess) return fail(FSG_E_DEVICE, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  }
+  unsigned long long ub = 0;
+  HIPCHK(hipMemcpyAsync(&ub, u.tot + 1, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  k->K = K;
+  k->ubytes = ub;
+  k->merged = true;
+  if (n_keys) *n_keys = K;
+  if (key_bytes) *key_bytes = ub;
+  return FSG_OK;
+}
+
+extern "C" int fsg_keyed_read(fsg_keyed* k, uint8_t* keys, size_t key_bytes, uint64_t* offs, uint32_t* vals,
+                              size_t n) {
+  if (!k->merged) return fail(FSG_E_INVALID_ARG, "fsg_keyed_allreduce has not run since the last collect");
+  if (n < k->K || key_bytes < k->ubytes) return fail(FSG_E_INVALID_ARG, "buffers smaller than the merged table");
+  HIPCHK(hipSetDevice(k->eng->device));
+  HIPCHK(hipStreamSynchronize(k->st));
+  if (k->K) {
+    HIPCHK(hipMemcpy(offs, k->uoff.p, k->K * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(vals, k->dense.p, k->K * 4, hipMemcpyDeviceToHost));
+  }
+  if (offs) offs[k->K] = k->ubytes;
+  if (k->ubytes) HIPCHK(hipMemcpy(keys, k->uarena.p, k->ubytes, hipMemcpyDeviceToHost));
+  return FSG_OK;
+}
+
+extern "C" int fsg_keyed_device(fsg_keyed* k, const uint8_t** keys, const uint64_t** offs, const uint32_t** vals) {
+  if (!k->merged) return fail(FSG_E_INVALID_ARG, "fsg_keyed_allreduce has not run since the last collect");
+  HIPCHK(hipSetDevice(k->eng->device));
+  HIPCHK(hipStreamSynchronize(k->st));
+  if (keys) *keys = k->uarena.as<uint8_t>();
+  if (offs) *offs = k->uoff.as<uint64_t>();
+  if (vals) *vals = k->dense.as<uint32_t>();
+  return FSG_OK;
+}
+
+extern "C" void fsg_keyed_free(fsg_keyed* k) { delete k; }

@@ -70,7 +70,12 @@ def siphash24(data: bytes, k0: int = 0, k1: int = 0) -> int:
 def partition_siphash(key: bytes, partition_count: int) -> int:
     """partitioning.rs:70-83: `key.hash(&mut SipHasher::new())` % partitions.
     `<[u8] as Hash>::hash` writes the length as a native-endian usize (8 bytes on
-    the 64-bit client) before the bytes."""
+    the 64-bit client) before the bytes.
+
+    Parity unpinned: SipHash-2-4 itself is pinned by siphasher's test vectors
+    (tests/test_partitions.py), but no fixture in the reference tree holds a
+    key -> partition pair, so the length-prefix assumption above is a restatement
+    of std's `Hash for [u8]`, not checked against the reference client."""
     return siphash24(struct.pack("<Q", len(key)) + key) % partition_count
 
 
@@ -126,40 +131,35 @@ def merge_states_torch(vec: Sequence[int]) -> List[int]:
     return [int(x) for x in t.tolist()]
 
 
-def fnv1a64(key: bytes) -> int:
-    """The key fingerprint of fsg_chain_keyed_state (FNV-1a 64)."""
-    h = 14695981039346656037
-    for c in key:
-        h = ((h ^ c) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
-    return h
+def union_dictionary(key_lists: Sequence[Sequence[bytes]]) -> Dict[bytes, int]:
+    """The topic key dictionary of fsg_keyed_allreduce: the keys of every rank's
+    list in rank order, each id given at its first occurrence, so every rank that
+    holds the same gathered lists builds the same dictionary."""
+    ids: Dict[bytes, int] = {}
+    for keys in key_lists:
+        for k in keys:
+            if k not in ids:
+                ids[k] = len(ids)
+    return ids
 
 
-def merge_keyed_torch(fp, val, dist=None, group=None):
-    """Topic totals of aggregate-json states (C5 keyed): every rank's (key
-    fingerprint, u32 value) pairs gathered with one all_gather (RCCL on GPU
-    tensors, gloo on CPU ones), then summed per key (u32 wrapping) on the
-    tensors' device.  `fp` int64 (the u64 bits), `val` int64.  Returns
-    (fingerprints, sums) sorted by fingerprint, identical on every rank."""
+def merge_keyed(local: Dict[bytes, int], dist=None, group=None) -> Dict[bytes, int]:
+    """Topic-wide per-key totals of aggregate-json states with the shape of the
+    C ABI's merge (fsg_keyed_allreduce): every rank's exact key list all-gathered,
+    the union dictionary built in rank order, this rank's values scattered into a
+    dense K-slot table, one all-reduce (sum), u32 wrapping.  gloo on CPU ranks;
+    the GPU path runs the same steps on HBM with RCCL (smartengine.KeyedState)."""
     import torch
+    keys = list(local)
     if dist is not None and dist.is_initialized() and dist.get_world_size(group) > 1:
-        world = dist.get_world_size(group)
-        n = torch.tensor([fp.numel()], dtype=torch.int64, device=fp.device)
-        dist.all_reduce(n, op=dist.ReduceOp.MAX, group=group)
-        m = int(n.item())
-        pad = m - fp.numel()
-        fpp = torch.cat([fp, torch.zeros(pad, dtype=torch.int64, device=fp.device)])
-        valp = torch.cat([val, torch.zeros(pad, dtype=torch.int64, device=fp.device)])
-        okp = torch.cat([torch.ones(fp.numel(), dtype=torch.int64, device=fp.device),
-                         torch.zeros(pad, dtype=torch.int64, device=fp.device)])
-        packed = torch.stack([fpp, valp, okp])                   # one collective for the three rows
-        bufs = [torch.empty_like(packed) for _ in range(world)]
-        dist.all_gather(bufs, packed, group=group)
-        allp = torch.cat(bufs, dim=1)
-        keep = allp[2] == 1
-        fp, val = allp[0][keep], allp[1][keep]
-    if fp.numel() == 0:
-        return fp, val
-    keys, inv = torch.unique(fp, sorted=True, return_inverse=True)
-    sums = torch.zeros(keys.numel(), dtype=torch.int64, device=fp.device)
-    sums.index_add_(0, inv, val)
-    return keys, sums & 0xFFFFFFFF
+        gathered = [None] * dist.get_world_size(group)
+        dist.all_gather_object(gathered, keys, group=group)
+    else:
+        gathered = [keys]
+    ids = union_dictionary(gathered)
+    dense = torch.zeros(len(ids), dtype=torch.int64)
+    for k, v in local.items():
+        dense[ids[k]] += int(v)
+    if dist is not None and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(dense, op=dist.ReduceOp.SUM, group=group)
+    return {k: int(dense[i]) & 0xFFFFFFFF for k, i in ids.items()}

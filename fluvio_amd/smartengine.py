@@ -368,6 +368,54 @@ class PartitionState:
             self._h = None
 
 
+class KeyedState:
+    """Topic-wide keyed totals of aggregate-json chains (fsg_keyed_*): collect
+    each owned partition's map (exact keys, device side), then `allreduce()`
+    builds the topic key dictionary over the engine's communicator (RCCL
+    all-gather of the key lists, dense K-slot u32 all-reduce), or locally on one
+    rank.  `read()` -> {key bytes: u32 total}."""
+
+    def __init__(self, engine: "SmartEngine"):
+        h = ctypes.c_void_p()
+        _check(_ffi.lib().fsg_keyed_new(engine._h, ctypes.byref(h)))
+        self._h = h
+        self._engine = engine
+        self.n_keys = 0
+        self.key_bytes = 0
+
+    def reset(self) -> None:
+        _check(_ffi.lib().fsg_keyed_reset(self._h))
+
+    def collect(self, chain: "SmartModuleChainInstance", stage: int = 0) -> None:
+        _check(_ffi.lib().fsg_keyed_collect(self._h, chain._h, stage))
+
+    def allreduce(self) -> int:
+        n, b = ctypes.c_size_t(), ctypes.c_size_t()
+        _check(_ffi.lib().fsg_keyed_allreduce(self._h, ctypes.byref(n), ctypes.byref(b)))
+        self.n_keys, self.key_bytes = n.value, b.value
+        return n.value
+
+    def read(self) -> Dict[bytes, int]:
+        n = self.n_keys
+        keys = ctypes.create_string_buffer(max(self.key_bytes, 1))
+        offs = (ctypes.c_uint64 * (n + 1))()
+        vals = (ctypes.c_uint32 * max(n, 1))()
+        _check(_ffi.lib().fsg_keyed_read(self._h, keys, self.key_bytes, offs, vals, n))
+        raw = keys.raw
+        return {raw[offs[i]:offs[i + 1]]: int(vals[i]) for i in range(n)}
+
+    def close(self) -> None:
+        if self._h:
+            _ffi.lib().fsg_keyed_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def comm_unique_id() -> bytes:
     buf = ctypes.create_string_buffer(128)
     _check(_ffi.lib().fsg_comm_unique_id(buf))
@@ -480,14 +528,6 @@ class SmartModuleChainInstance:
         return data
 
 
-    def keyed_state(self, stage: int, dev_fp: int, dev_val: int, cap: int) -> int:
-        """aggregate-json: write the accumulator's (FNV-1a 64 key fingerprint, u32
-        value) pairs into device buffers (raw pointers, `cap` pairs); returns the
-        number of pairs in the state (fsg_chain_keyed_state)."""
-        n = ctypes.c_size_t()
-        _check(_ffi.lib().fsg_chain_keyed_state(self._h, stage, ctypes.c_void_p(dev_fp), ctypes.c_void_p(dev_val),
-                                                cap, ctypes.byref(n)))
-        return n.value
     def last_timings(self) -> Dict[str, float]:
         t = _ffi.fsg_timings()
         _check(_ffi.lib().fsg_chain_last_timings(self._h, ctypes.byref(t)))

@@ -51,8 +51,16 @@ def make_slice(kind: int, nrec: int, seed: int = None, base_offset: int = 0, max
     return make_slice_array(kind, nrec, seed, base_offset, max_section).tobytes()
 
 
+def last_int_sum() -> int:
+    """The sum of the integers of the last kind-3 slice generated (the
+    generator's own ground truth, for aggregate-sum checks without a GPU)."""
+    L = _l()
+    L.synth_last_sum.restype = ctypes.c_int64
+    return int(L.synth_last_sum())
+
+
 def make_keyed_slices(partitions: int = 64, nrec: int = 5000, nkeys: int = 10000, seed: int = 0xF106,
-                      owned=None) -> dict:
+                      owned=None, key_sums: dict = None) -> dict:
     """C5 keyed: records `{"repo-NNNN": n}` (aggregate-json input), the record
     key = the repo name, routed to partition SipHash(key) mod P exactly as
     fluvio's producer does (partitioning.rs:70-83), so every key lives in one
@@ -67,15 +75,24 @@ def make_keyed_slices(partitions: int = 64, nrec: int = 5000, nkeys: int = 10000
     L.synth_keyed.restype = ctypes.c_size_t
     L.synth_keyed.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
                               ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t]
+    L.synth_key_sums.argtypes = [ctypes.c_void_p]
+    L.synth_key_sums.restype = None
     out = {}
     for p in (owned if owned is not None else range(partitions)):
         ks = by_p.get(p) or [b"repo-none"]
+        sums = np.zeros(len(ks), dtype=np.uint64)
+        L.synth_key_sums(sums.ctypes.data if key_sums is not None else None)
         blob = b"".join(ks)
         off = np.zeros(len(ks) + 1, dtype=np.uint32)
         off[1:] = np.cumsum([len(k) for k in ks])
         cap = nrec * 80 + 65536
         buf = np.zeros(cap, dtype=np.uint8)
         n = L.synth_keyed(blob, off.ctypes.data, len(ks), nrec, seed * 1000003 + p, 0, buf.ctypes.data, cap)
+        L.synth_key_sums(None)
         assert n, "synth_keyed: buffer too small"
         out[p] = buf[:n].tobytes()
+        if key_sums is not None:  # the generator's ground truth: committed values per key
+            for k, v in zip(ks, sums.tolist()):
+                if v:
+                    key_sums[k] = key_sums.get(k, 0) + int(v)
     return out

@@ -142,8 +142,18 @@ static size_t gen_c2(uint8_t *v) {
   o[k++] = '}';
   return k;
 }
+/* ground truth of the last generated slice for the bench's state checks:
+ * kind 3 = the i64 sum of the committed records' integers; synth_keyed = per
+ * key index, the sum of its committed values (synth_key_sums, when set) */
+static int64_t g_vsum;
+static int g_last_c3;
+static uint64_t *g_ksum;
+int64_t synth_last_sum(void) { return g_vsum; }
+void synth_key_sums(uint64_t *sums) { g_ksum = sums; }
+
 static size_t gen_c3(uint8_t *v) {
   int x = (int)rnd_n(2001) - 1000;
+  g_last_c3 = x;
   return (size_t)sprintf((char *)v, "%d", x);
 }
 static size_t gen_c4(uint8_t *v, int *has_key, uint8_t *key, size_t *klen) {
@@ -202,6 +212,7 @@ size_t synth_slice(int kind, uint64_t nrec, uint64_t seed, int64_t base, uint8_t
                    uint32_t max_section) {
   rs = seed * 0x9E3779B97F4A7C15ull + 0x1234567ull;
   if (!rs) rs = 1;
+  g_vsum = 0;
   if (!max_section) max_section = 16384;
   size_t pos = 0;
   uint64_t done = 0;
@@ -250,6 +261,7 @@ size_t synth_slice(int kind, uint64_t nrec, uint64_t seed, int64_t base, uint8_t
       memcpy(out + q, rec, w);
       q += w;
       sec += w;
+      if (kind == 3) g_vsum += g_last_c3;
       cnt++;
     }
     const int64_t first_ts = 1700000000000LL + (int64_t)(done / 64);
@@ -300,7 +312,8 @@ size_t synth_keyed(const uint8_t *keys, const uint32_t *koff, uint32_t nkeys, ui
       val[vl++] = '"';
       memcpy(val + vl, kp, kl);
       vl += kl;
-      vl += (size_t)sprintf((char *)val + vl, "\":%u}", 1 + rnd_n(100));
+      const uint32_t nv = 1 + rnd_n(100);
+      vl += (size_t)sprintf((char *)val + vl, "\":%u}", nv);
       size_t inner = 1 + vsz(0) + vsz((int64_t)cnt) + 1 + vsz((int64_t)kl) + kl + vsz((int64_t)vl) + vl + 1;
       size_t rl = vsz((int64_t)inner) + inner;
       if (cnt > 0 && sec + rl > 16384) break;
@@ -320,6 +333,7 @@ size_t synth_keyed(const uint8_t *keys, const uint32_t *koff, uint32_t nkeys, ui
       memcpy(out + q, rec, w);
       q += w;
       sec += w;
+      if (g_ksum) g_ksum[k] += nv;
       cnt++;
     }
     const int64_t first_ts = 1700000000000LL + (int64_t)(done / 64);

@@ -208,19 +208,17 @@ int fsg_chain_look_back(fsg_chain *c, fsg_read_fn read_fn, void *user, fsg_metri
                         fsg_runtime_error *error);
 void fsg_runtime_error_free(fsg_runtime_error *e);
 int fsg_chain_get_accumulator(fsg_chain *c, size_t stage, uint8_t **acc, size_t *len);
-/* aggregate-json (C5 keyed): the accumulator's (key fingerprint, u32 value)
- * pairs for a cross-partition merge (FNV-1a 64 of each key's bytes) into device
- * buffers of `cap` pairs; *n = pairs in the state.  Merging per-GPU tables is
- * the caller's collective (RCCL all-gather + a keyed sum); no reference
- * counterpart (each partition's own state is the reference's). */
-int fsg_chain_keyed_state(fsg_chain *c, size_t stage, uint64_t *dev_fp, uint32_t *dev_val, size_t cap, size_t *n);
 int fsg_chain_last_timings(fsg_chain *c, fsg_timings *t);
 void fsg_chain_free(fsg_chain *c);
 /* Release an output.  Large output buffers (>= 4 MiB) are parked for reuse by the
- * next large output (at most two, process-wide) instead of being unmapped. */
+ * next large output (at most two, process-wide) instead of being unmapped; a
+ * parked buffer still holds earlier output bytes past its batch_len. */
 void fsg_output_free(fsg_output *o);
 void fsg_batch_output_free(fsg_batch_output *o);
 void fsg_free(void *p);
+/* Unmap every parked output buffer now (the last fsg_engine_free does it too).
+ * No reference counterpart: the host memory policy of this library. */
+void fsg_host_cache_trim(void);
 
 /* ---- HBM-resident path (batches ingested once, processed many times) --- */
 /* Ingest: copies the slice to HBM and frames its batches (FileBatchIterator). */
@@ -275,6 +273,28 @@ int fsg_state_allreduce(fsg_state *s);
 int fsg_state_read(fsg_state *s, void *host, size_t bytes);
 int fsg_state_device(fsg_state *s, void **dptr);
 void fsg_state_free(fsg_state *s);
+
+/* ---- topic-wide keyed totals of aggregate-json states (C5 keyed) ---------
+ * Each partition's chain keeps its aggregate-json map in HBM between calls
+ * (SmartModuleAggregate.accumulator, context.rs:25-30; the map of
+ * smartmodule/examples/aggregate-json/src/lib.rs:22-35).  A keyed table sums
+ * the maps of the chains collected into it by exact key bytes (u32 wrapping);
+ * fsg_keyed_allreduce builds the topic key dictionary across ranks (RCCL
+ * all-gather of every rank's key list; the union in rank order, so every rank
+ * holds the same dictionary) and sums one dense K-slot u32 table with an RCCL
+ * all-reduce.  Without a communicator (one rank) the same steps run locally.
+ * The key order of the result is the union's (first occurrence by rank, then
+ * by collect); no reference counterpart: each partition's own accumulator is
+ * the reference's (fsg_chain_get_accumulator). */
+typedef struct fsg_keyed fsg_keyed;
+int fsg_keyed_new(fsg_engine *engine, fsg_keyed **out);
+int fsg_keyed_reset(fsg_keyed *k);                                  /* empty the local table */
+int fsg_keyed_collect(fsg_keyed *k, fsg_chain *c, size_t stage);     /* add the chain's map (device side, async) */
+int fsg_keyed_allreduce(fsg_keyed *k, size_t *n_keys, size_t *key_bytes);
+/* keys: the union's key bytes (key i = keys[offs[i] .. offs[i + 1])), offs: n + 1 entries, vals: n */
+int fsg_keyed_read(fsg_keyed *k, uint8_t *keys, size_t key_bytes, uint64_t *offs, uint32_t *vals, size_t n);
+int fsg_keyed_device(fsg_keyed *k, const uint8_t **keys, const uint64_t **offs, const uint32_t **vals);
+void fsg_keyed_free(fsg_keyed *k);
 
 #ifdef __cplusplus
 }

@@ -115,27 +115,28 @@ def test_two_rank_state_merge(tmp_path):
 # ---------------------------------------------------------------------------
 # C5 keyed (aggregate-json): per-key u32 sums, keys routed by SipHash so a key
 # lives in one partition; the topic-wide table = all ranks' (fingerprint, value)
-# pairs gathered and summed per key (partitions.merge_keyed_torch)
+# key lists gathered, the union dictionary, a dense all-reduce (partitions.merge_keyed,
+# the shape of fsg_keyed_allreduce)
 # ---------------------------------------------------------------------------
 K_PART, K_REC, K_KEYS = 8, 1500, 64
 
 
 def keyed_pairs(owned):
-    """Per owned partition: the oracle's aggregate-json accumulator (the
-    pretty map after the partition's last record) as (FNV-1a 64, u32) pairs."""
+    """This rank's keyed table: the oracle's aggregate-json accumulator (the
+    pretty map after the partition's last record) of every owned partition,
+    summed by exact key (a key lives in one partition)."""
     import json
     from fluvio_amd import synth
     from oracle.oracle import OracleChain
     slices = synth.make_keyed_slices(K_PART, K_REC, K_KEYS, owned=list(owned))
-    fps, vals = [], []
+    local = {}
     for p in owned:
         ch = OracleChain([("aggregate-json", {}, None)])
         r = ch.process_batch(slices[p])
         assert r["status"] == 0 and r["error"] is None
         for k, v in json.loads(ch.accumulator(0)).items():
-            fps.append(PT.fnv1a64(k.encode()))
-            vals.append(v)
-    return fps, vals
+            local[k.encode()] = (local.get(k.encode(), 0) + v) & 0xFFFFFFFF
+    return local
 
 
 def keyed_expect():
@@ -148,7 +149,7 @@ def keyed_expect():
             for rec in b.memory_records():
                 for k, v in json.loads(rec.value).items():
                     assert PT.partition_siphash(k.encode(), K_PART) == p  # routed by key
-                    tot[PT.fnv1a64(k.encode())] = (tot.get(PT.fnv1a64(k.encode()), 0) + v) & 0xFFFFFFFF
+                    tot[k.encode()] = (tot.get(k.encode(), 0) + v) & 0xFFFFFFFF
     return tot
 
 
@@ -157,11 +158,9 @@ def _keyed_rank_main(rank, world, port, outdir):
     import torch
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    fps, vals = keyed_pairs(PT.owned_partitions(K_PART, world, rank))
-    fp = torch.tensor([f - (1 << 64) if f >= 1 << 63 else f for f in fps], dtype=torch.int64)
-    keys, sums = PT.merge_keyed_torch(fp, torch.tensor(vals, dtype=torch.int64), dist=dist)
+    merged = PT.merge_keyed(keyed_pairs(PT.owned_partitions(K_PART, world, rank)), dist=dist)
     with open(os.path.join(outdir, f"keyed{rank}.txt"), "w") as f:
-        f.write(" ".join(f"{k & 0xFFFFFFFFFFFFFFFF}:{v}" for k, v in zip(keys.tolist(), sums.tolist())))
+        f.write(" ".join(f"{k.decode()}:{v}" for k, v in merged.items()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -174,5 +173,5 @@ def test_two_rank_keyed_merge(tmp_path):
     expect = keyed_expect()
     assert len(expect) > K_PART
     for r in range(world):
-        got = dict(tuple(map(int, x.split(":"))) for x in open(tmp_path / f"keyed{r}.txt").read().split())
+        got = {k.encode(): int(v) for k, v in (x.split(":") for x in open(tmp_path / f"keyed{r}.txt").read().split())}
         assert got == expect

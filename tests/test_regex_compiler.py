@@ -11,7 +11,7 @@ from oracle import oracle as O
 
 def dfa_match(pattern, text):
     m, ml, ns = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-    rc = _ffi.lib().fsg_debug_regex_match(pattern.encode(), text, len(text), ctypes.byref(m),
+    rc = _ffi.debug_lib().fsg_debug_regex_match(pattern.encode(), text, len(text), ctypes.byref(m),
                                           ctypes.byref(ml), ctypes.byref(ns))
     if rc:
         raise ValueError(rc)
