@@ -308,6 +308,12 @@ struct Bits {
       cnt += 8;
     }
   }
+  // to the next byte boundary: whole bytes fill() read ahead go back to the stream
+  __device__ void align() {
+    i -= cnt >> 3;
+    buf = 0;
+    cnt = 0;
+  }
   __device__ uint32_t get(uint32_t k) {  // k <= 24
     while (cnt < k) {
       if (i >= n) {
@@ -334,6 +340,7 @@ struct Huff {
 __device__ bool huff_build(Huff& h, const uint8_t* len, int n) {
   for (int k = 0; k < 16; k++) h.cnt[k] = 0;
   for (int s = 0; s < n; s++) h.cnt[len[s]]++;
+  for (int k = 0; k < (1 << kHuffFast); k++) h.fast[k] = 0;
   if (h.cnt[0] == n) return true;
   int left = 1;
   for (int k = 1; k < 16; k++) {
@@ -348,7 +355,6 @@ __device__ bool huff_build(Huff& h, const uint8_t* len, int n) {
     if (len[s]) h.sym[offs[len[s]]++] = (uint16_t)s;
   // first-level table: canonical codes in symbol order within each length,
   // bit-reversed (deflate sends codes MSB first into an LSB-first stream)
-  for (int k = 0; k < (1 << kHuffFast); k++) h.fast[k] = 0;
   int code = 0, idx = 0;
   for (int L = 1; L <= kHuffFast; L++) {
     for (int j = 0; j < h.cnt[L]; j++, code++) {
@@ -415,8 +421,7 @@ __device__ bool inflate_dev(Bits& b, DecOut& o) {
     const uint32_t last = b.get(1), type = b.get(2);
     if (b.bad) return false;
     if (type == 0) {  // stored
-      b.buf = 0;
-      b.cnt = 0;  // to a byte boundary
+      b.align();  // to a byte boundary
       if (b.n - b.i < 4) return false;
       const uint32_t len = b.s[b.i] | (b.s[b.i + 1] << 8), nlen = b.s[b.i + 2] | (b.s[b.i + 3] << 8);
       b.i += 4;
@@ -497,6 +502,7 @@ __device__ bool gzip_dev(const uint8_t* s, uint64_t n, DecOut& o) {
   Bits b{s, n, i, 0, 0, false};
   const uint64_t o0 = o.n;
   if (!inflate_dev(b, o)) return false;
+  b.align();
   if (b.n - b.i < 8) return false;  // trailer after the byte-aligned end (unused bits dropped)
   const uint32_t crc = dec_le32(b.s + b.i), isize = dec_le32(b.s + b.i + 4);
   if ((uint32_t)(o.n - o0) != isize) return false;

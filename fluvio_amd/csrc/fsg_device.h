@@ -246,6 +246,8 @@ struct EvalArgs {
   uint16_t* rstart;    // k_chase: record n of batch b starts at window offset rstart[rbase[b] + n] ...
   uint16_t* rend;      // ... and the last one ends at rend[b] (0xFFFF: no lean framing, exact path)
   BatchWin* bwin;      // k_flat_frame -> k_flat: per-batch window (one scalar load per batch)
+  const uint8_t* pass; // per batch, 1: the records pass through unchanged (no stage runs on them:
+                       // an earlier segment's partial output before its error), nullptr: none
 };
 
 struct SizeArgs {
@@ -260,6 +262,7 @@ struct SizeArgs {
   int64_t acc0;
   const ElemRec* elem;
   uint64_t acc_len;        // aggregate (concat): initial accumulator bytes
+  uint32_t seg;            // 1: segment output (no offset rebase: rel = 0)
 };
 
 struct PlanArgs {
@@ -288,6 +291,24 @@ struct WriteArgs {
   const ElemRec* elem;
   const uint8_t* cat;      // aggregate (concat): kCatOff + accumulator stream
   uint64_t acc_len;
+  uint32_t seg;            // 1: segment output: batch b's records at 61 * (b + 1) + pre[b], rel = 0
+};
+// a chain segment's output as the next segment's input slice (k_seg_headers):
+// batch b in [0, nb) = the source batch's 57-byte header (base offset, last
+// offset delta, timestamps, attributes) with batch_len / the record count of
+// the records the segment produced for it, at 61 * b + pre[b].rec_bytes
+struct SegArgs {
+  const uint8_t* src;      // the segment's input slice
+  const uint64_t* bpos;    // its batch positions
+  const ScanRow* rows;     // per batch: rec_bytes / nrec of the segment's output
+  const ScanRow* pre;      // ... exclusive prefix
+  uint32_t nb;             // batches of the output slice
+  int32_t pass_batch;      // this segment's error batch (passes through the next segments), -1 none
+  const uint8_t* pass_in;  // the input slice's pass-through flags (nullptr: none)
+  uint8_t* dst;            // the output slice
+  uint64_t* dbpos;         // its batch positions ...
+  uint64_t* drbase;        // ... record-count prefix ...
+  uint8_t* dpass;          // ... and pass-through flags
 };
 constexpr uint64_t kCatOff = 64;  // the concat stream starts this far into its buffer (copy_seg margin)
 

@@ -1063,8 +1063,10 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
   const uint32_t rend_b = a.rend ? a.rend[b] : 0xFFFFu;
   const uint16_t* rsb = (a.rstart && rend_b != 0xFFFFu) ? a.rstart + a.rbase[b] : nullptr;
   const uint64_t rb = a.rbase[b];
-  // phase A: full chain; phase B (only if a record error occurred): truncated chain
-  int nst = (int)ch.nstages;
+  // phase A: full chain; phase B (only if a record error occurred): truncated
+  // chain.  A pass-through batch runs no stage: its records are kept as they are.
+  const bool passthru = a.pass && a.pass[b];
+  int nst = passthru ? 0 : (int)ch.nstages;
   uint32_t err_stage = 0xFFFFFFFFu, err_idx = 0xFFFFFFFFu;
   bool unsupported = false;
   uint32_t kcount = 0, nout = 0;
@@ -1267,14 +1269,14 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
   if (tid == 0) {
     if (!(flags & BF_DECODE) && err_stage != 0xFFFFFFFFu)
       flags |= (L.bs.err_code == EC_UNSUP) ? BF_UNSUPPORTED : BF_ERR;
-    if (err_stage == 0xFFFFFFFFu || err_stage + 1 == ch.nstages) flags |= BF_LAST_STAGE;
+    if (!passthru && (err_stage == 0xFFFFFFFFu || err_stage + 1 == ch.nstages)) flags |= BF_LAST_STAGE;
     if (unsupported) flags |= BF_UNSUPPORTED;
     BatchStat st = L.bs;
     st.flags = flags;
     st.nkeep = kcount;
     st.sec_len = sec_len;
     st.err_stage = err_stage;
-    const bool agg_ran = err_stage == 0xFFFFFFFFu || err_stage + 1 == ch.nstages;
+    const bool agg_ran = !passthru && (err_stage == 0xFFFFFFFFu || err_stage + 1 == ch.nstages);
     st.agg_sum = (ch.has_agg && agg_ran) ? aggsum : 0;
     st.nout = nout;
     st.pad = 0;
@@ -2419,7 +2421,7 @@ __global__ __launch_bounds__(256) void k_size(SizeArgs a) {
   row.agg = st.agg_sum;
   row.cat = st.cat_sum;
   if (f != 0xFFFFFFFFu && b >= f && !(st.flags & BF_DECODE)) {
-    const int64_t rel = a.bstat[f].base_offset - st.base_offset;
+    const int64_t rel = a.seg ? 0 : a.bstat[f].base_offset - st.base_offset;
     const int32_t agg_base = a.agg_pre ? (int32_t)((uint64_t)a.acc0 + (uint64_t)a.agg_pre[b].agg) : 0;
     const uint64_t cat_base = a.agg_pre ? a.acc_len + a.agg_pre[b].cat : 0;
     uint64_t sum = 0;
@@ -2645,6 +2647,41 @@ __global__ void k_state(const Plan* plan, int32_t* state) {
   if (threadIdx.x != 0) return;
   const Plan p = *plan;
   if (p.status == 0 && p.acc_touched) *state = (int32_t)p.acc_final;
+}
+
+// ---------------------------------------------------------------------------
+// k_seg_headers: a segment's output as the next segment's input slice: per
+// batch the source header with batch_len / count of the segment's records for
+// it (the records themselves were written by k_write / k_write_lean with
+// WriteArgs::seg), positions, record-count prefix and pass-through flags.  The
+// next segment decodes these records exactly as the reference's next stage
+// decodes SmartModuleInput::try_from_records (engine.rs:160-165).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_seg_headers(SegArgs a) {
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t l = lane_id();
+  if (b >= a.nb) return;
+  const uint64_t o = 61ull * b + a.pre[b].rec_bytes;
+  const uint8_t* h = a.src + a.bpos[b];
+  uint8_t* d = a.dst + o;
+  const uint64_t rb = a.rows[b].rec_bytes;
+  const uint32_t cnt = (uint32_t)a.rows[b].nrec;
+  const uint32_t blen = (uint32_t)(49 + rb);
+  if (l < 57) {
+    uint8_t x = h[l];
+    if (l >= 8 && l < 12) x = (uint8_t)(blen >> (8 * (11 - l)));
+    d[l] = x;
+  } else if (l < 61) {
+    d[l] = (uint8_t)(cnt >> (8 * (60 - l)));
+  }
+  if (l == 0) {
+    a.dbpos[b] = o;
+    a.drbase[b] = a.pre[b].nrec;
+    a.dpass[b] = ((int32_t)b == a.pass_batch || (a.pass_in && a.pass_in[b])) ? 1 : 0;
+  }
+}
+void launch_seg_headers(const SegArgs& a, hipStream_t s) {
+  if (a.nb) hipLaunchKernelGGL(k_seg_headers, dim3((a.nb + 3) / 4), dim3(256), 0, s, a);
 }
 
 // ---------------------------------------------------------------------------
@@ -2932,11 +2969,12 @@ __global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
   if (p.first < 0 || b > p.last) return;
   const uint32_t lane = lane_id();
   const BatchStat st = a.bstat[b];
-  const int64_t rel = a.bstat[p.first].base_offset - st.base_offset;
+  const int64_t rel = a.seg ? 0 : a.bstat[p.first].base_offset - st.base_offset;
   const int32_t agg_base = a.agg_pre ? (int32_t)((uint64_t)a.acc0 + (uint64_t)a.agg_pre[b].agg) : 0;
   const uint64_t cat_base = a.agg_pre ? a.acc_len + a.agg_pre[b].cat : 0;
   const KeptRec* d = a.desc + a.rbase[b];
-  const uint64_t obase = 61 + (a.pre[b].rec_bytes - a.pre[p.first].rec_bytes);
+  const uint64_t obase = a.seg ? 61ull * (uint64_t)(b + 1) + a.pre[b].rec_bytes
+                               : 61 + (a.pre[b].rec_bytes - a.pre[p.first].rec_bytes);
   uint8_t* out = a.out;
   if (st.nkeep && d[0].mode == KM_ARRAY) {  // a batch's descriptors share one mode
     write_array_batch(a, d, st.nkeep, rel, obase);
@@ -3895,9 +3933,10 @@ __global__ __launch_bounds__(kWlThreads) void k_write_lean(WriteArgs a) {
   if (p.first < 0 || b > p.last) return;
   const uint32_t t = threadIdx.x, lane = t & 63u;
   const BatchStat st = a.bstat[b];
-  const int64_t rel = a.bstat[p.first].base_offset - st.base_offset;
+  const int64_t rel = a.seg ? 0 : a.bstat[p.first].base_offset - st.base_offset;
   const KeptRec* d = a.desc + a.rbase[b];
-  const uint64_t obase = 61 + (a.pre[b].rec_bytes - a.pre[p.first].rec_bytes);
+  const uint64_t obase = a.seg ? 61ull * (uint64_t)(b + 1) + a.pre[b].rec_bytes
+                               : 61 + (a.pre[b].rec_bytes - a.pre[p.first].rec_bytes);
   const uint32_t d0 = (uint32_t)(obase & 15);
   const uint32_t nk = st.nkeep;
   // 1. headers and segments

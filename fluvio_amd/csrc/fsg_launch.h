@@ -23,6 +23,8 @@ void launch_scan(const ScanRow* rows, ScanRow* pre, ScanRow* tile_sums, ScanRow*
 void launch_plan(const PlanArgs& a, hipStream_t s);
 void launch_state(const Plan* plan, int32_t* state, hipStream_t s);
 void launch_header(const Plan* plan, uint8_t* out, hipStream_t s);
+// a chain segment's output as the next segment's input slice (SegArgs)
+void launch_seg_headers(const SegArgs& a, hipStream_t s);
 void launch_write(const WriteArgs& a, uint32_t nblocks, hipStream_t s);
 void launch_cat(const WriteArgs& a, uint32_t nbatches, hipStream_t s);
 void launch_crc(uint8_t* out, uint64_t off, uint64_t n, uint32_t* acc, hipStream_t s);

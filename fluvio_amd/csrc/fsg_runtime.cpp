@@ -456,6 +456,10 @@ struct fsg_slice {
   float crc_ms = 0;
   std::vector<uint64_t> hbpos, hrbase;  // host framing (kept: the H2D copies may still be reading them)
   size_t dec_limit = 1000000000;  // largest decompressed batch (the store limit, engine.rs:24)
+  // a chain segment's output (composed chains): batches whose records pass
+  // through the later segments unchanged (the partial output before an error)
+  DevBuf pass;
+  bool has_pass = false;
   // framing / decompression scratch, grown and kept across uploads into this
   // slice (hipFree synchronises the whole device)
   DevBuf fr[12], dec[8];
@@ -497,6 +501,18 @@ struct fsg_chain {
   uint64_t aj_bytes = 0;    // its arena bytes
   DevBuf aj_cout;           // commit scalars
   hipEvent_t kd_ev[2] = {}; // keyed collect: chain stream -> collect stream -> chain stream
+  // Composed chains (stages after an array_map, an aggregate or a stateful
+  // filter): the chain runs as segments, each ending at such a stage; segment
+  // k's per-batch output is segment k + 1's input slice (seg_io[k]).
+  std::vector<std::unique_ptr<fsg_chain>> segs;
+  std::vector<uint32_t> seg_stage0;  // global index of each segment's first stage
+  std::unique_ptr<fsg_slice[]> seg_io;
+  // what a segment run leaves for its deferred state commit
+  PlanArgs last_pa{};
+  SfArgs last_sfa{};
+  AggjArgs last_aj{};
+  uint32_t last_aj_kmax = 0;
+  bool last_has_aggj = false;
   DevBuf rstart, rend;  // k_chase (lean path record starts)
   DevBuf bwin;          // k_flat_frame: per-batch window descriptors
   // stateful last stage (filter_look_back / filter_hashset)
@@ -773,10 +789,50 @@ int add_stage(fsg_chain* c, const ModuleSpec& m, const std::string& name, uint8_
 }
 }  // namespace
 
+namespace {
+// stages whose output is the input of a new segment when more stages follow
+bool seg_boundary(const ModuleSpec& m) {
+  const auto& by = m.bytes;
+  if (by.size() < 4 || memcmp(by.data(), "\0fsg", 4)) return false;
+  const std::string name(by.begin() + 4, by.end());
+  return name == "array_map_json_array" || name == "aggregate-sum" || name == "aggregate" ||
+         name == "aggregate-json" || name == "filter_look_back" || name == "filter_hashset";
+}
+}  // namespace
+
 extern "C" int fsg_chain_builder_initialize(fsg_chain_builder* b, fsg_engine* e, fsg_chain** out) {
   std::unique_ptr<fsg_chain_builder> own(b);
   if (!e) return fail(FSG_E_INVALID_ARG, "null engine");
   HIPCHK(hipSetDevice(e->device));
+  {  // a stage after an array_map / aggregate / stateful filter: a composed chain of segments
+    std::vector<size_t> ends;
+    for (size_t i = 0; i + 1 < b->mods.size(); i++)
+      if (seg_boundary(b->mods[i])) ends.push_back(i);
+    if (!ends.empty()) {
+      ends.push_back(b->mods.size() - 1);
+      auto c = std::make_unique<fsg_chain>();
+      c->eng = e;
+      c->limit = b->limit;
+      size_t a0 = 0;
+      for (size_t ei : ends) {
+        auto* sb = new fsg_chain_builder();
+        sb->limit = b->limit;
+        sb->mods.assign(b->mods.begin() + a0, b->mods.begin() + ei + 1);
+        fsg_chain* g = nullptr;
+        int rc = fsg_chain_builder_initialize(sb, e, &g);  // takes sb
+        if (rc) return rc;
+        c->seg_stage0.push_back((uint32_t)a0);
+        for (auto& nm : g->names) c->names.push_back(nm);
+        c->segs.emplace_back(g);
+        a0 = ei + 1;
+      }
+      c->hdesc.nstages = (uint32_t)b->mods.size();
+      HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+      for (auto& ev : c->ev) HIPCHK(hipEventCreate(&ev));
+      *out = c.release();
+      return FSG_OK;
+    }
+  }
   auto c = std::make_unique<fsg_chain>();
   c->eng = e;
   c->limit = b->limit;
@@ -1696,11 +1752,38 @@ int aj_render(fsg_chain* c, std::vector<uint8_t>& out) {
   return FSG_OK;
 }
 
+// segment mode of run_slice (composed chains): the segment's per-batch output
+// becomes `out`, a slice of batches [0, stop] with the source headers; the
+// state commits wait for the final segment's stop (commit_deferred)
+struct SegOut {
+  fsg_slice* out;
+  int tail;        // the status of a failure right after the output's last batch (0: none)
+  int fail_batch;  // that batch (its process() call failed), -1: the input's own tail
+};
+
+// the host copy of an aggregate-sum / concat accumulator after a call that touched it
+int acc_update(fsg_chain* c, const Plan& p, bool cat) {
+  if (cat) {
+    std::vector<uint8_t> na(c->acc.size() + p.cat_final);
+    HIPCHK(hipMemcpy(na.data(), c->cat.as<uint8_t>() + kCatOff, na.size(), hipMemcpyDeviceToHost));
+    c->acc.swap(na);
+  } else {
+    char b[16];
+    int n = snprintf(b, sizeof b, "%d", (int32_t)p.acc_final);
+    c->acc.assign(b, b + n);
+  }
+  return FSG_OK;
+}
+
+int run_composed(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics* m, fsg_batch_output* res);
+
 int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics* m, fsg_batch_output* res,
-              bool empty_chain_io) {
+              bool empty_chain_io, SegOut* so = nullptr) {
+  if (!c->segs.empty()) return run_composed(c, s, max_bytes, m, res);
   hipStream_t st = c->stream;
   const uint32_t nb = s->nb;
   memset(res, 0, sizeof *res);
+  if (so) max_bytes = ~0ull;  // the SPU's max_bytes applies to the final segment's output only
   // scratch (StoreMemoryExceeded past the store limit, limiter.rs:18-35)
   const bool has_array = c->array_stage >= 0;
   const bool has_aggj = (c->hdesc.flags & CF_AGG_JSON) != 0;
@@ -1766,7 +1849,9 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   // through the exact kernel (list mode)
   const bool lean = (ops & ~((1u << OP_CONTAINS) | (1u << OP_MAP_UPPER) | (1u << OP_REGEX) |
                              (1u << OP_FILTER_JSON) | (1u << OP_PROJECT))) == 0 &&
-                    !has_agg && lean_stages && nb > 1;  // one batch: the exact kernel alone (1 launch, not 3)
+                    !has_agg && lean_stages && nb > 1 &&  // one batch: the exact kernel alone (1 launch, not 3)
+                    !s->has_pass;                         // pass-through batches: the exact kernel knows them
+  ea.pass = s->has_pass ? s->pass.as<uint8_t>() : nullptr;
   // record starts per batch (k_chase for the lean kernel, k_chase_x for the exact one)
   HIPCHK(c->rstart.ensure(((size_t)s->nrec + 64) * sizeof(uint16_t)));  // + a wave of over-read
   HIPCHK(c->rend.ensure(((size_t)nb + 1) * sizeof(uint16_t)));
@@ -1927,6 +2012,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   sa.acc0 = acc0;
   sa.elem = ea.elem;
   sa.acc_len = has_cat ? c->acc.size() : 0;
+  sa.seg = so ? 1u : 0u;
   if (has_agg) {
     sa.agg_only = 1;
     launch_size(sa, st);
@@ -1950,8 +2036,12 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   pa.has_agg = has_agg;
   pa.acc0 = acc0;
   launch_plan(pa, st);
-  if (c->hdesc.flags & CF_AGG_SUM) launch_state(pa.plan, c->dstate.as<int32_t>(), st);
-  if (has_sf) launch_sf_commit(sfa, st);  // the stage's state through plan.done
+  c->last_pa = pa;
+  c->last_sfa = sfa;
+  if (!so) {  // a segment's state commits wait for the final segment (commit_deferred)
+    if (c->hdesc.flags & CF_AGG_SUM) launch_state(pa.plan, c->dstate.as<int32_t>(), st);
+    if (has_sf) launch_sf_commit(sfa, st);  // the stage's state through plan.done
+  }
   HIPCHK(hipGetLastError());
   if (c->timed) HIPCHK(hipEventRecord(c->ev[2], st));
   HIPCHK(c->hpin.ensure(kPinPlan + kSmallOut));
@@ -1959,7 +2049,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   static_assert(sizeof(Plan) + sizeof(uint32_t) <= kPinPlan, "pinned plan block");
   if (lean) HIPCHK(hipMemcpyAsync((uint8_t*)c->hpin.p + sizeof(Plan), ea.list, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   unsigned long long sfs[3] = {0, 0, 0};
-  const bool dedup = has_sf && sfa.op == OP_DEDUP && nb;
+  const bool dedup = has_sf && sfa.op == OP_DEDUP && nb && !so;
   if (dedup) HIPCHK(hipMemcpyAsync(sfs, sfa.scal, sizeof sfs, hipMemcpyDeviceToHost, st));
   HIPCHK(wait_stream(st));
   memcpy(&c->hplan, c->hpin.p, sizeof(Plan));
@@ -1970,6 +2060,19 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     c->sf->n_ent = sfs[0];
     c->sf->arena_len = sfs[1];
     c->sf->n = sfs[2];
+  }
+  if (so && c->hplan.status != 0) {
+    // a segment: batches up to the failing one go on; the failure becomes the
+    // output slice's tail (the final segment reports it if it gets that far)
+    so->tail = c->hplan.status;
+    so->fail_batch = c->hplan.done + 1 < (int32_t)nb ? c->hplan.done + 1 : -1;
+    pa.nbatches = (uint32_t)(c->hplan.done + 1);
+    pa.tail_status = 0;
+    launch_plan(pa, st);
+    c->last_pa = pa;
+    HIPCHK(hipMemcpyAsync(c->hpin.p, c->plan.p, sizeof(Plan), hipMemcpyDeviceToHost, st));
+    HIPCHK(wait_stream(st));
+    memcpy(&c->hplan, c->hpin.p, sizeof(Plan));
   }
   const Plan p = c->hplan;
   if (m) {
@@ -1983,9 +2086,17 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
                                                     : "failed to decode SmartModule base input";
     return fail(p.status, why);
   }
-  // output batch: 61-byte header + records
-  const size_t out_len = 61 + p.rec_bytes;
-  HIPCHK(c->out.ensure(out_len + 64));
+  // output batch: 61-byte header + records (a segment: 61 bytes per batch + records)
+  const uint32_t seg_nb = so && p.stop >= 0 ? (uint32_t)p.stop + 1 : 0u;
+  const size_t out_len = so ? 61ull * seg_nb + p.rec_bytes : 61 + p.rec_bytes;
+  DevBuf& obuf = so ? so->out->data : c->out;
+  if (so) {
+    const size_t alloc = slice_alloc(out_len);
+    HIPCHK(obuf.ensure(alloc));
+    HIPCHK(hipMemsetAsync((uint8_t*)obuf.p + (out_len & ~(size_t)15), 0, alloc - (out_len & ~(size_t)15), st));
+  } else {
+    HIPCHK(c->out.ensure(out_len + 64));
+  }
   HIPCHK(c->crcparts.ensure(sizeof(uint32_t)));
   WriteArgs wa{};
   wa.slice = ea.slice;
@@ -1995,7 +2106,8 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   wa.pre = pa.pre;
   wa.agg_pre = has_agg ? c->aggpre.as<ScanRow>() : nullptr;
   wa.plan = pa.plan;
-  wa.out = c->out.as<uint8_t>();
+  wa.out = obuf.as<uint8_t>();
+  wa.seg = so ? 1u : 0u;
   wa.acc0 = acc0;
   wa.elem = ea.elem;
   wa.acc_len = sa.acc_len;
@@ -2023,7 +2135,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     launch_aggj_write(aj, st);
     wa.cat = aj.cat;
   }
-  launch_header(pa.plan, wa.out, st);
+  if (!so) launch_header(pa.plan, wa.out, st);
   if (c->timed) HIPCHK(hipEventRecord(c->ev[3], st));
   const uint32_t nblk = p.last >= p.first && p.first >= 0 ? (uint32_t)(p.last - p.first + 1) : 0u;
   // verbatim records (filters, uppercase, projections): staged in LDS
@@ -2037,10 +2149,39 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     launch_write(wa, nblk, st);
   HIPCHK(hipGetLastError());
   if (c->timed) HIPCHK(hipEventRecord(c->ev[4], st));
-  launch_crc(wa.out, 21, out_len - 21, c->crcparts.as<uint32_t>(), st);
+  if (so) {  // the next segment's input: headers, positions, record-count prefix, pass-through flags
+    fsg_slice* o = so->out;
+    HIPCHK(o->bpos.ensure(std::max<size_t>(seg_nb, 1) * 8));
+    HIPCHK(o->rbase.ensure(std::max<size_t>(seg_nb, 1) * 8));
+    HIPCHK(o->pass.ensure(std::max<size_t>(seg_nb, 1)));
+    SegArgs ga{};
+    ga.src = ea.slice;
+    ga.bpos = ea.bpos;
+    ga.rows = sa.rows;
+    ga.pre = pa.pre;
+    ga.nb = seg_nb;
+    ga.pass_batch = p.err_batch;
+    ga.pass_in = ea.pass;
+    ga.dst = obuf.as<uint8_t>();
+    ga.dbpos = o->bpos.as<uint64_t>();
+    ga.drbase = o->rbase.as<uint64_t>();
+    ga.dpass = o->pass.as<uint8_t>();
+    launch_seg_headers(ga, st);
+    o->eng = c->eng;
+    o->len = out_len;
+    o->nb = seg_nb;
+    o->nrec = p.n_records;
+    o->header_bytes = out_len;
+    o->tail_status = p.err_batch >= 0 ? 0 : so->tail;  // an error batch ends the slice
+    o->device_framed = true;
+    o->decompressed = s->decompressed;
+    o->has_pass = p.err_batch >= 0 || s->has_pass;
+  } else {
+    launch_crc(wa.out, 21, out_len - 21, c->crcparts.as<uint32_t>(), st);
+  }
   HIPCHK(hipGetLastError());
   if (c->timed) HIPCHK(hipEventRecord(c->ev[5], st));
-  c->out_pinned = out_len <= kSmallOut;
+  c->out_pinned = !so && out_len <= kSmallOut;
   if (c->out_pinned)
     HIPCHK(hipMemcpyAsync((uint8_t*)c->hpin.p + kPinPlan, wa.out, out_len, hipMemcpyDeviceToHost, st));
   HIPCHK(wait_stream(st));
@@ -2069,20 +2210,123 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     if (rc) return rc;
     res->has_error = 1;
   }
+  c->last_aj = aj;
+  c->last_aj_kmax = (uint32_t)(aj.n_init + aj_nnew);
+  c->last_has_aggj = has_aggj;
+  if (so) return FSG_OK;  // state commits: commit_deferred, once the final segment's stop is known
   if (has_aggj && p.stop >= 0) {  // the map after the last processed batch stays in HBM
     int rc = aj_commit(c, aj, p.stop, (uint32_t)(aj.n_init + aj_nnew));
     if (rc) return rc;
   }
-  if (has_agg && !has_aggj && p.acc_touched) {
-    if (has_cat) {
-      std::vector<uint8_t> na(c->acc.size() + p.cat_final);
-      HIPCHK(hipMemcpy(na.data(), c->cat.as<uint8_t>() + kCatOff, na.size(), hipMemcpyDeviceToHost));
-      c->acc.swap(na);
-    } else {
-      char b[16];
-      int n = snprintf(b, sizeof b, "%d", (int32_t)p.acc_final);
-      c->acc.assign(b, b + n);
+  if (has_agg && !has_aggj && p.acc_touched) return acc_update(c, p, has_cat);
+  return FSG_OK;
+}
+
+// the state commits of segment `c` of a composed chain through `done` (the
+// last batch whose process() call completed, as the final segment decided):
+// k_plan again with the cut at `done`, then the commits run_slice skipped
+int commit_deferred(fsg_chain* c, int32_t done) {
+  const bool has_agg = c->agg_stage >= 0, has_sf = (c->hdesc.flags & CF_STATEFUL) != 0;
+  if ((!has_agg && !has_sf) || done < 0) return FSG_OK;
+  hipStream_t st = c->stream;
+  HIPCHK(c->aj_cout.ensure(64));
+  const uint32_t cut = (uint32_t)done;
+  HIPCHK(hipMemcpyAsync(&c->mins.as<Mins>()->cut, &cut, sizeof cut, hipMemcpyHostToDevice, st));
+  launch_plan(c->last_pa, st);
+  if (c->hdesc.flags & CF_AGG_SUM) launch_state(c->last_pa.plan, c->dstate.as<int32_t>(), st);
+  const SfArgs& sfa = c->last_sfa;
+  const bool dedup = has_sf && sfa.op == OP_DEDUP && sfa.nbatches;
+  if (has_sf) launch_sf_commit(sfa, st);
+  HIPCHK(hipGetLastError());
+  unsigned long long sfs[3] = {0, 0, 0};
+  if (dedup) HIPCHK(hipMemcpyAsync(sfs, sfa.scal, sizeof sfs, hipMemcpyDeviceToHost, st));
+  Plan p;
+  HIPCHK(hipMemcpyAsync(&p, c->last_pa.plan, sizeof p, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (dedup) {
+    c->sf->n_ent = sfs[0];
+    c->sf->arena_len = sfs[1];
+    c->sf->n = sfs[2];
+  }
+  if (p.status != 0) return FSG_OK;
+  if (c->last_has_aggj) return p.stop >= 0 ? aj_commit(c, c->last_aj, p.stop, c->last_aj_kmax) : FSG_OK;
+  if (has_agg && p.acc_touched) return acc_update(c, p, (c->hdesc.flags & CF_AGG_CAT) != 0);
+  return FSG_OK;
+}
+
+// a composed chain: segment k's per-batch output (one batch per input batch,
+// the source headers) is segment k + 1's input, as the reference feeds each
+// stage's successes to the next one per SmartModuleInput (engine.rs:147-167).
+// A segment's error batch passes through the later segments unchanged (the
+// reference returns that stage's partial output at once) and its error is the
+// chain's if the final segment gets that far; the SPU's max_bytes and stop
+// rules run on the final segment's output; state commits run once the final
+// stop is known; metrics count the original input (engine.rs:139-141).
+int run_composed(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics* m, fsg_batch_output* res) {
+  const size_t n = c->segs.size();
+  if (!c->seg_io) c->seg_io.reset(new fsg_slice[n - 1]);
+  HIPCHK(hipStreamSynchronize(c->stream));  // the input was uploaded on the outer chain's stream
+  const fsg_slice* in = s;
+  fsg_runtime_error pend{};
+  int32_t pend_batch = -1;
+  int fail_status = 0, fail_batch = -1;
+  for (size_t k = 0; k + 1 < n; k++) {
+    fsg_chain* g = c->segs[k].get();
+    g->timed = c->timed;
+    SegOut so{&c->seg_io[k], 0, -1};
+    fsg_batch_output r;
+    int rc = run_slice(g, in, ~0ull, nullptr, &r, false, &so);
+    if (rc) {
+      free_error(r.error);
+      free_error(pend);
+      return rc;
     }
+    if (r.has_error) {  // ends this segment's output; an earlier pending error lay beyond it
+      free_error(pend);
+      pend = r.error;
+      pend_batch = g->hplan.err_batch;
+    } else {
+      free_error(r.error);
+    }
+    if (so.tail && so.fail_batch >= 0) {
+      fail_status = so.tail;
+      fail_batch = so.fail_batch;
+    }
+    in = &c->seg_io[k];
+  }
+  fsg_chain* f = c->segs.back().get();
+  f->timed = c->timed;
+  int rc = run_slice(f, in, max_bytes, nullptr, res, false);
+  const Plan pf = f->hplan;
+  // metrics of the original input: per process() call its raw bytes (segment 0's rows)
+  if (m) {
+    uint64_t inv = pf.invocations;
+    if (rc && fail_batch >= 0 && pf.status == fail_status && inv == (uint64_t)fail_batch) inv++;  // the failing call
+    uint64_t bin = 0;
+    if (inv) {
+      ScanRow r2[2];
+      fsg_chain* g0 = c->segs[0].get();
+      HIPCHK(hipMemcpy(&r2[0], g0->pre.as<ScanRow>() + (inv - 1), sizeof(ScanRow), hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(&r2[1], g0->rows.as<ScanRow>() + (inv - 1), sizeof(ScanRow), hipMemcpyDeviceToHost));
+      bin = r2[0].bytes_in + r2[1].bytes_in;
+    }
+    m->bytes_in += bin;
+    m->invocation_count += inv;
+    m->records_out += pf.records_out;
+  }
+  if (rc) {
+    free_error(pend);
+    return rc;
+  }
+  if (pend_batch >= 0 && pf.stop == pend_batch && !res->has_error) {
+    res->error = pend;
+    res->has_error = 1;
+    pend = fsg_runtime_error{};
+  }
+  free_error(pend);
+  for (size_t k = 0; k + 1 < n; k++) {
+    rc = commit_deferred(c->segs[k].get(), pf.done);
+    if (rc) return rc;
   }
   return FSG_OK;
 }
@@ -2205,7 +2449,11 @@ hipError_t staged_download(fsg_chain* c, uint8_t* dst, const uint8_t* src, size_
   return e;
 }
 
-int download_output(fsg_chain* c, fsg_batch_output* res) {
+// the chain holding the output of the last call (a composed chain: its final segment)
+fsg_chain* fin(fsg_chain* c) { return c->segs.empty() ? c : c->segs.back().get(); }
+
+int download_output(fsg_chain* c0, fsg_batch_output* res) {
+  fsg_chain* c = fin(c0);
   uint8_t* h = host_alloc(c->out_len);
   if (!h) return fail(FSG_E_DEVICE, "host allocation failed");
   hipError_t e = hipSuccess;
@@ -2248,7 +2496,8 @@ extern "C" int fsg_chain_process_slice(fsg_chain* c, const fsg_slice* s, uint64_
   return FSG_OK;
 }
 
-extern "C" int fsg_chain_output_device(fsg_chain* c, const void** dptr, size_t* len) {
+extern "C" int fsg_chain_output_device(fsg_chain* c0, const void** dptr, size_t* len) {
+  fsg_chain* c = fin(c0);
   *dptr = c->out.p;
   *len = c->out_len;
   return FSG_OK;
@@ -2294,6 +2543,7 @@ extern "C" int fsg_chain_process(fsg_chain* c, const uint8_t* raw, size_t len, i
   }
   auto o = std::make_unique<fsg_output>();
   memset(o.get(), 0, sizeof(fsg_output));
+  c = fin(c);
   const size_t rl = c->out_len - 57;  // u32 count + records
   uint8_t* h = host_alloc(rl);
   if (!h) {
@@ -2358,9 +2608,29 @@ int make_lookback_chain(fsg_chain* c) {
 // one SmartModuleInput (try_from_records: base offset 0), metrics.add_bytes_in,
 // and its look_back over them (derive generator/look_back.rs: stops at the
 // first Err with SmartModuleLookbackRuntimeError).
+namespace {
+// a composed chain's segment holding global stage `stage` (local index in *local)
+fsg_chain* seg_of(fsg_chain* c, size_t stage, size_t* local) {
+  for (size_t k = c->segs.size(); k-- > 0;)
+    if (stage >= c->seg_stage0[k]) {
+      *local = stage - c->seg_stage0[k];
+      return c->segs[k].get();
+    }
+  *local = stage;
+  return c;
+}
+}  // namespace
+
 extern "C" int fsg_chain_look_back(fsg_chain* c, fsg_read_fn read_fn, void* user, fsg_metrics* m,
                                    fsg_runtime_error* error) {
   if (error) memset(error, 0, sizeof *error);
+  if (!c->segs.empty()) {  // every segment's stateful stage with a Lookback, in chain order
+    for (auto& g : c->segs) {
+      int rc = fsg_chain_look_back(g.get(), read_fn, user, m, error);
+      if (rc) return rc;
+    }
+    return FSG_OK;
+  }
   if (c->sf_stage < 0 || c->lookback.kind == FSG_LOOKBACK_NONE) return FSG_OK;
   if (!read_fn) return fail(FSG_E_INVALID_ARG, "look_back needs a read_fn");
   HIPCHK(hipSetDevice(c->eng->device));
@@ -2388,7 +2658,9 @@ extern "C" int fsg_chain_look_back(fsg_chain* c, fsg_read_fn read_fn, void* user
   return FSG_OK;
 }
 
-extern "C" int fsg_chain_get_accumulator(fsg_chain* c, size_t stage, uint8_t** acc, size_t* len) {
+extern "C" int fsg_chain_get_accumulator(fsg_chain* c0, size_t stage0, uint8_t** acc, size_t* len) {
+  size_t stage = stage0;
+  fsg_chain* c = seg_of(c0, stage0, &stage);
   if ((int)stage != c->agg_stage) return fail(FSG_E_INVALID_ARG, "stage is not an aggregate");
   std::vector<uint8_t> txt;
   const std::vector<uint8_t>* a = &c->acc;
@@ -2405,7 +2677,21 @@ extern "C" int fsg_chain_get_accumulator(fsg_chain* c, size_t stage, uint8_t** a
 }
 
 extern "C" int fsg_chain_last_timings(fsg_chain* c, fsg_timings* t) {
-  *t = c->last;
+  *t = fin(c)->last;
+  if (!c->segs.empty()) {  // phases summed over the segments; the input as segment 0 saw it
+    const fsg_timings& t0 = c->segs[0]->last;
+    for (size_t k = 0; k + 1 < c->segs.size(); k++) {
+      const fsg_timings& g = c->segs[k]->last;
+      t->eval_ms += g.eval_ms;
+      t->plan_ms += g.plan_ms;
+      t->write_ms += g.write_ms;
+      t->crc_ms += g.crc_ms;
+      t->total_ms += g.total_ms;
+    }
+    t->in_bytes = t0.in_bytes;
+    t->n_batches = t0.n_batches;
+    t->n_records_in = t0.n_records_in;
+  }
   return FSG_OK;
 }
 
@@ -2502,6 +2788,8 @@ extern "C" int fsg_state_new(fsg_engine* e, size_t count, int dtype, fsg_state**
   return FSG_OK;
 }
 extern "C" int fsg_state_collect(fsg_state* s, size_t slot, fsg_chain* c) {
+  for (auto& g : c->segs)  // a composed chain: its aggregate-sum segment
+    if (g->hdesc.flags & CF_AGG_SUM) return fsg_state_collect(s, slot, g.get());
   if (slot >= s->count) return fail(FSG_E_INVALID_ARG, "state slot out of range");
   if (!(c->hdesc.flags & CF_AGG_SUM) || s->dtype != FSG_DTYPE_I32)
     return fail(FSG_E_INVALID_ARG, "collect needs an aggregate-sum chain and an i32 state vector");
@@ -2646,7 +2934,9 @@ extern "C" int fsg_keyed_reset(fsg_keyed* k) {
   return FSG_OK;
 }
 
-extern "C" int fsg_keyed_collect(fsg_keyed* k, fsg_chain* c, size_t stage) {
+extern "C" int fsg_keyed_collect(fsg_keyed* k, fsg_chain* c0, size_t stage0) {
+  size_t stage = stage0;
+  fsg_chain* c = seg_of(c0, stage0, &stage);
   if ((int)stage != c->agg_stage || !(c->hdesc.flags & CF_AGG_JSON))
     return fail(FSG_E_INVALID_ARG, "stage is not an aggregate-json aggregate");
   if (c->eng->device != k->eng->device) return fail(FSG_E_INVALID_ARG, "chain and keyed table on different devices");

@@ -219,6 +219,62 @@ def test_random_parity(engine, chain, kind, n):
     check_batch(engine, CHAINS[chain], sl)
 
 
+# ---------------------------------------------------------------------------
+# composed chains: stages after an array_map, an aggregate or a stateful
+# filter (engine.rs:147-167 feeds each stage's successes to the next); the
+# GPU runs them as segments (fsg_runtime.cpp run_composed)
+# ---------------------------------------------------------------------------
+COMPOSED = {
+    "array_map_filter": [("array_map_json_array", {}, None), ("filter_init", {"key": "a"}, None)],
+    "array_map_map": [("array_map_json_array", {}, None), ("map", {}, None)],
+    "array_map_filter_odd": [("array_map_json_array", {}, None), ("filter_odd", {}, None)],
+    "array_map_filter_map_double": [("array_map_json_array", {}, None), ("filter_map", {}, None),
+                                    ("map_double", {}, None)],
+    "filter_array_map_regex": [("filter_with_param", {"key": "1"}, None), ("array_map_json_array", {}, None),
+                               ("regex-filter", {"regex": r"^-?\d{2}$|[xyz]"}, None)],
+    "array_map_twice": [("array_map_json_array", {}, None), ("array_map_json_array", {}, None)],
+    "agg_sum_filter_odd": [("aggregate-sum", {}, b"7"), ("filter_odd", {}, None)],
+    "agg_sum_filter": [("aggregate-sum", {}, None), ("filter_init", {"key": "5"}, None), ("map", {}, None)],
+    "agg_sum_agg_sum": [("aggregate-sum", {}, None), ("aggregate-sum", {}, b"3")],
+    "hashset_map": [("filter_hashset", {}, None), ("map", {}, None)],
+    "hashset_filter_odd": [("filter_hashset", {"count": "50"}, None), ("filter_odd", {}, None)],
+    "look_back_filter_map": [("filter_look_back", {}, None), ("filter_map", {}, None)],
+    "aggj_filter": [("aggregate-json", {}, None), ("filter_init", {"key": "repo-0001"}, None)],
+    "map_agg_concat_filter": [("map", {}, None), ("aggregate", {}, b"x"), ("filter_init", {"key": "X"}, None)],
+}
+
+
+@pytest.mark.parametrize("kind,n", [(1, 800), (2, 600), (3, 2500), (4, 2500), (5, 1500)])
+@pytest.mark.parametrize("chain", sorted(COMPOSED))
+def test_composed_chain_parity(engine, chain, kind, n):
+    if chain == "map_agg_concat_filter":
+        n = min(n, 300)  # the concat output grows quadratically
+    sl = synth.make_slice(kind, n, base_offset=500)
+    check_batch(engine, COMPOSED[chain], sl, calls=2)
+
+
+@pytest.mark.parametrize("max_bytes", [0, 100, 5000, 60000])
+@pytest.mark.parametrize("chain", ["array_map_filter_odd", "agg_sum_filter_odd", "hashset_map"])
+def test_composed_chain_max_bytes(engine, chain, max_bytes):
+    sl = synth.make_slice(5 if chain.startswith("array") else 3, 2000, base_offset=9)
+    check_batch(engine, COMPOSED[chain], sl, max_bytes, calls=2)
+
+
+def test_composed_chain_keyed_errors(engine):
+    """aggregate-json then a filter over keyed records with bad values (the
+    aggregate's error batch passes through the filter), then process()."""
+    for seed in (1, 3):
+        check_batch(engine, COMPOSED["aggj_filter"], _keyed_slice(seed, bad=0.02), calls=2)
+    modules = COMPOSED["array_map_filter_odd"]
+    g, o = gpu_chain(engine, modules), orc_chain(modules)
+    for b in P.decode_batches(synth.make_slice(5, 400)):
+        gout = g.process(SmartModuleInput(b.records_bytes, b.base_offset, b.header.first_timestamp))
+        oout = o.process(b.records_bytes, b.base_offset, b.header.first_timestamp)
+        assert oout["status"] == 0
+        assert gout.raw_successes == oout["bytes"]
+        assert_same_error(gout.error, oout["error"])
+
+
 @pytest.mark.parametrize("max_bytes", [0, 1, 100, 5000, 40000, 300000])
 @pytest.mark.parametrize("chain", ["filter_init_timeout", "filter_then_map", "filter_map", "agg_sum"])
 def test_max_bytes_cut(engine, chain, max_bytes):
