@@ -514,8 +514,12 @@ __device__ bool gzip_dev(const uint8_t* s, uint64_t n, DecOut& o) {
   return true;  // bytes after the member are ignored
 }
 
-// Compression::uncompress of one record section: the output length, DEC_BAD
-// (io::Error "uncompress error") or DEC_UNSUP (zstd, not on the GPU path)
+}  // namespace fsg
+#include "fsg_zstd_dev.h"
+namespace fsg {
+
+// Compression::uncompress of one record section: the output length or DEC_BAD
+// (io::Error "uncompress error")
 __device__ int64_t dev_decompress(uint32_t codec, const uint8_t* s, uint64_t n, DecOut& o,
                                   const uint32_t* crc32c_tab) {
   bool ok;
@@ -523,7 +527,7 @@ __device__ int64_t dev_decompress(uint32_t codec, const uint8_t* s, uint64_t n, 
     case 1: ok = gzip_dev(s, n, o); break;
     case 2: ok = snappy_frames_dev(s, n, o, crc32c_tab); break;
     case 3: ok = lz4_frames_dev(s, n, o); break;
-    case 4: return DEC_UNSUP;
+    case 4: ok = zstd::zstd_frames_dev(s, n, o); break;
     default: return DEC_BAD;
   }
   return ok ? (int64_t)o.n : DEC_BAD;

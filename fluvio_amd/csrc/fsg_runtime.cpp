@@ -912,10 +912,10 @@ int frame(const uint8_t* s, size_t len, std::vector<uint64_t>& bpos, std::vector
       break;
     }
     const int comp = attrs & 7;
-    // gzip / snappy / lz4 sections are decompressed on the GPU after framing
-    // (decompress_slice); zstd is not restated (unsupported), codes > 4 are the
-    // iterator's "unknown compression value" io::Error
-    if (comp > 3 || (comp != 0 && !codecs)) {
+    // gzip / snappy / lz4 / zstd sections are decompressed on the GPU after
+    // framing (decompress_slice); codes > 4 are the iterator's "unknown
+    // compression value" io::Error
+    if (comp > 4 || (comp != 0 && !codecs)) {
       tail = comp <= 4 ? FSG_E_UNSUPPORTED : FSG_E_IO;
       break;
     }
@@ -1083,7 +1083,7 @@ int decompress_slice(fsg_slice* sl, const std::vector<uint64_t>& bpos, const std
   for (uint32_t b = 0; b < nb; b++)
     if (ds[b] < 0 || ds[b] > 0x7FFFFFFFll - 45) {
       keep = b;
-      tail = ds[b] == -2 ? FSG_E_UNSUPPORTED : FSG_E_IO;  // DEC_UNSUP: zstd
+      tail = ds[b] == -2 ? FSG_E_UNSUPPORTED : FSG_E_IO;  // DEC_UNSUP: a codec without a device decoder
       break;
     }
   std::vector<uint64_t> np(nb);

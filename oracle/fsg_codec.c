@@ -20,7 +20,10 @@
  *   snappy : stream identifier "sNaPpY", compressed (0x00) / uncompressed (0x01)
  *            chunks with masked CRC-32C of the uncompressed data, padding (0xfe)
  *            and skippable (0x80-0xfd) chunks; raw snappy blocks inside
- *   zstd   : not restated (the GPU path reports it unsupported)
+ *   zstd   : the zstd crate 0.13 (zstd-sys: libzstd) Decoder (zstd.rs:15-20):
+ *            concatenated frames and skippable frames, no dictionary; here the
+ *            system's libzstd itself (libzstd.so.1, loaded at first use), the
+ *            canonical implementation of RFC 8878, as zlib is for gzip
  * Parity of the formats is pinned by round trips with independent encoders:
  * Python's zlib (gzip) and this file's LZ4 / Snappy encoders, plus the xxhash
  * module for xxh32 (tests/test_codecs.py), and by produce_batch.rs:124-153's
@@ -29,6 +32,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <dlfcn.h>
 #include <zlib.h>
 
 #include "fsg_oracle.h"
@@ -475,8 +479,102 @@ static void snappy_encode(const uint8_t *s, size_t n, int flags, cbuf *o) {
   }
 }
 
-/* Compression::uncompress: 0 ok (*out malloc'd), -1 a decode error (io::Error),
- * ORC_E_UNSUPPORTED zstd */
+/* ---- zstd (zstd crate Decoder / Encoder level 1) through the system libzstd ----
+ * (prototypes of the stable API, zstd.h 1.4; no header in this image) */
+typedef struct { const void *src; size_t size; size_t pos; } zin_t;
+typedef struct { void *dst; size_t size; size_t pos; } zout_t;
+static struct {
+  int tried, ok;
+  void *(*createDStream)(void);
+  size_t (*freeDStream)(void *);
+  size_t (*initDStream)(void *);
+  size_t (*decompressStream)(void *, zout_t *, zin_t *);
+  unsigned (*isError)(size_t);
+  size_t (*compressBound)(size_t);
+  void *(*createCCtx)(void);
+  size_t (*freeCCtx)(void *);
+  size_t (*setParameter)(void *, int, int);
+  size_t (*compress2)(void *, void *, size_t, const void *, size_t);
+} Z;
+static int zstd_load(void) {
+  if (Z.tried) return Z.ok;
+  Z.tried = 1;
+  void *h = dlopen("libzstd.so.1", RTLD_NOW | RTLD_LOCAL);
+  if (!h) return 0;
+  *(void **)&Z.createDStream = dlsym(h, "ZSTD_createDStream");
+  *(void **)&Z.freeDStream = dlsym(h, "ZSTD_freeDStream");
+  *(void **)&Z.initDStream = dlsym(h, "ZSTD_initDStream");
+  *(void **)&Z.decompressStream = dlsym(h, "ZSTD_decompressStream");
+  *(void **)&Z.isError = dlsym(h, "ZSTD_isError");
+  *(void **)&Z.compressBound = dlsym(h, "ZSTD_compressBound");
+  *(void **)&Z.createCCtx = dlsym(h, "ZSTD_createCCtx");
+  *(void **)&Z.freeCCtx = dlsym(h, "ZSTD_freeCCtx");
+  *(void **)&Z.setParameter = dlsym(h, "ZSTD_CCtx_setParameter");
+  *(void **)&Z.compress2 = dlsym(h, "ZSTD_compress2");
+  Z.ok = Z.createDStream && Z.freeDStream && Z.initDStream && Z.decompressStream && Z.isError && Z.compressBound &&
+         Z.createCCtx && Z.freeCCtx && Z.setParameter && Z.compress2;
+  return Z.ok;
+}
+/* read_to_end of zstd::stream::read::Decoder: frames until the input ends; the
+ * input ending inside a frame, or bytes that are not a frame, is an error */
+static int zstd_decode(const uint8_t *s, size_t n, cbuf *o) {
+  if (!zstd_load()) return ORC_E_UNSUPPORTED;
+  void *d = Z.createDStream();
+  if (!d || Z.isError(Z.initDStream(d))) {
+    if (d) Z.freeDStream(d);
+    return -1;
+  }
+  zin_t in = {s, n, 0};
+  uint8_t tmp[1 << 16];
+  size_t hint = 1; /* zio::Reader starts with finished_frame = false: an empty input is an incomplete frame */
+  int rc = 0;
+  for (;;) {
+    zout_t out = {tmp, sizeof tmp, 0};
+    hint = Z.decompressStream(d, &out, &in);
+    if (Z.isError(hint)) {
+      rc = -1;
+      break;
+    }
+    cb_put(o, tmp, out.pos);
+    if (in.pos == in.size && out.pos < out.size) break; /* input consumed, output flushed */
+  }
+  if (!rc && hint) rc = -1; /* the input ended inside a frame ("incomplete frame") */
+  Z.freeDStream(d);
+  return rc;
+}
+/* flags: low byte = level (0 -> 1, the crate's Encoder::new(_, 1)); 0x100 content
+ * checksum; 0x200 no content size; 0x400 two concatenated frames; 0x800 a
+ * skippable frame first */
+static int zstd_encode(const uint8_t *s, size_t n, int flags, cbuf *o) {
+  if (!zstd_load()) return ORC_E_UNSUPPORTED;
+  const int level = (flags & 0xFF) ? (flags & 0xFF) : 1;
+  if (flags & 0x800) {
+    const uint8_t skip[12] = {0x53, 0x2A, 0x4D, 0x18, 4, 0, 0, 0, 'f', 's', 'g', '!'};
+    cb_put(o, skip, sizeof skip);
+  }
+  const int parts = (flags & 0x400) && n > 1 ? 2 : 1;
+  for (int k = 0; k < parts; k++) {
+    const size_t a = parts == 1 ? 0 : (k ? n / 2 : 0), b = parts == 1 ? n : (k ? n : n / 2);
+    void *c = Z.createCCtx();
+    if (!c) return -1;
+    Z.setParameter(c, 100, level);                        /* ZSTD_c_compressionLevel */
+    Z.setParameter(c, 201, (flags & 0x100) ? 1 : 0);      /* ZSTD_c_checksumFlag */
+    Z.setParameter(c, 200, (flags & 0x200) ? 0 : 1);      /* ZSTD_c_contentSizeFlag */
+    const size_t cap = Z.compressBound(b - a);
+    uint8_t *tmp = (uint8_t *)malloc(cap ? cap : 1);
+    const size_t r = Z.compress2(c, tmp, cap, s + a, b - a);
+    Z.freeCCtx(c);
+    if (Z.isError(r)) {
+      free(tmp);
+      return -1;
+    }
+    cb_put(o, tmp, r);
+    free(tmp);
+  }
+  return 0;
+}
+
+/* Compression::uncompress: 0 ok (*out malloc'd), -1 a decode error (io::Error) */
 int orc_decompress(int codec, const uint8_t *s, size_t n, uint8_t **out, size_t *out_len) {
   cbuf o = {0};
   int rc;
@@ -484,7 +582,7 @@ int orc_decompress(int codec, const uint8_t *s, size_t n, uint8_t **out, size_t 
     case 1: rc = gzip_decode(s, n, &o); break;
     case 2: rc = snappy_frames(s, n, &o); break;
     case 3: rc = lz4_frames(s, n, &o); break;
-    case 4: rc = ORC_E_UNSUPPORTED; break;
+    case 4: rc = zstd_decode(s, n, &o); break;
     default: rc = -1; break;
   }
   if (rc) {
@@ -495,7 +593,7 @@ int orc_decompress(int codec, const uint8_t *s, size_t n, uint8_t **out, size_t 
   *out_len = o.n;
   return 0;
 }
-/* test-data encoders: codec 1 gzip (flags = zlib level, 0 -> 6), 2 snappy, 3 lz4 */
+/* test-data encoders: codec 1 gzip (flags = zlib level, 0 -> 6), 2 snappy, 3 lz4, 4 zstd */
 int orc_compress(int codec, const uint8_t *s, size_t n, int flags, uint8_t **out, size_t *out_len) {
   cbuf o = {0};
   int rc = 0;
@@ -503,6 +601,7 @@ int orc_compress(int codec, const uint8_t *s, size_t n, int flags, uint8_t **out
     case 1: rc = gzip_encode(s, n, flags ? flags : 6, &o); break;
     case 2: snappy_encode(s, n, flags, &o); break;
     case 3: lz4_encode(s, n, flags, &o); break;
+    case 4: rc = zstd_encode(s, n, flags, &o); break;
     default: rc = -1;
   }
   if (rc) {

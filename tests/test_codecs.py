@@ -28,7 +28,7 @@ def test_produce_batch_iterator_kat():
 def test_lib_rs_round_trip_text():
     """fluvio-compression gzip.rs / snappy.rs / lz4.rs test_compress_decompress."""
     text = b"FLUVIO_AAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAA"
-    for codec in (1, 2, 3):
+    for codec in (1, 2, 3, 4):
         c = O.compress(codec, text)
         assert len(c) < len(text)
         assert O.decompress(codec, c) == text
@@ -38,7 +38,8 @@ def test_lib_rs_round_trip_text():
 def test_round_trips_and_independent_pins(n):
     rng = random.Random(n)
     data = bytes(rng.choice(b"abcdefgh  xyz0123{}\":,") for _ in range(n))
-    for codec, flags in ((1, [0, 1, 9]), (2, [0, 1, 2]), (3, [0, 1, 2, 3, 4, 8, 15, 16, 31])):
+    for codec, flags in ((1, [0, 1, 9]), (2, [0, 1, 2]), (3, [0, 1, 2, 3, 4, 8, 15, 16, 31]),
+                         (4, [0, 3, 19, 0x100, 0x200, 0x400, 0x800])):
         for f in flags:
             assert O.decompress(codec, O.compress(codec, data, f)) == data, (codec, f)
     assert O.decompress(1, gzip.compress(data)) == data          # Python's gzip encoder
@@ -49,7 +50,7 @@ def test_round_trips_and_independent_pins(n):
 
 def test_corrupt_inputs_are_errors():
     data = b"abcabcabcabcabcabc-" * 500
-    for codec, f in ((1, 0), (2, 0), (3, 3), (3, 0)):
+    for codec, f in ((1, 0), (2, 0), (3, 3), (3, 0), (4, 0x100)):
         c = bytearray(O.compress(codec, data, f))
         bad = 0
         for off in range(0, len(c), max(1, len(c) // 40)):
@@ -59,8 +60,12 @@ def test_corrupt_inputs_are_errors():
                 bad += 1
         assert bad > 0
         assert O.decompress(codec, bytes(c[:-3])) is None  # truncated
-    with pytest.raises(O.OracleError):
-        O.decompress(4, b"\x28\xb5\x2f\xfd")  # zstd: unsupported on the GPU path
+    # zstd (the crate's streaming Decoder): a bare magic, an empty input and
+    # bytes after the last frame are "incomplete frame" / unknown-frame errors
+    assert O.decompress(4, b"\x28\xb5\x2f\xfd") is None
+    assert O.decompress(4, b"") is None
+    assert O.decompress(4, O.compress(4, data) + b"\0\0") is None
+    assert O.decompress(4, O.compress(4, data, 0x800)) == data  # a skippable frame first
 
 
 @pytest.mark.parametrize("codecs", [[1], [2], [3], [0, 3, 2, 1]])

@@ -383,10 +383,9 @@ def test_edge_slices(engine):
     comp = bytearray(good)
     comp[22] |= 1
     check_batch(engine, chain, bytes(comp))
-    # zstd bits -> unsupported on the GPU path (zstd is not restated)
+    # zstd bits on a section that is not zstd -> io::Error, like the oracle
     comp[22] = (comp[22] & ~7) | 4
-    with pytest.raises(Unsupported):
-        gpu_chain(engine, chain).process_batch(bytes(comp))
+    check_batch(engine, chain, bytes(comp))
     # a record whose length claims more than the section -> decoding error (-11)
     bad = bytearray(good)
     bad[61] = 0x7E
@@ -1300,7 +1299,8 @@ COMPRESSED_CHAINS = ["filter_init_timeout", "filter_then_map", "regex_ssn", "fil
 
 
 @pytest.mark.parametrize("codecs,flags", [([1], 0), ([2], 0), ([3], 0), ([3], 15), ([2], 3), ([0, 3, 2, 1], {3: 7, 1: 9}),
-                                          ([1, 0], 1)])
+                                          ([1, 0], 1), ([4], 0), ([4], 0x100 | 19), ([4], 0x200 | 0x400 | 0x800),
+                                          ([0, 4, 2, 4, 1], {4: 0x100 | 7})])
 @pytest.mark.parametrize("chain", COMPRESSED_CHAINS)
 def test_compressed_slice_parity(engine, chain, codecs, flags):
     kind = 1 if chain == "regex_ssn" else 2
@@ -1336,7 +1336,18 @@ def test_decompression_bomb_is_store_memory(engine):
 @pytest.mark.parametrize("chain", ["filter_map", "agg_sum", "filter_odd"])
 def test_compressed_int_chains(engine, chain):
     sl = synth.make_slice(3, 20000, base_offset=7)
-    check_batch(engine, CHAINS[chain], recompress(sl, [3, 1, 2], {3: 3}))
+    check_batch(engine, CHAINS[chain], recompress(sl, [3, 1, 2, 4], {3: 3}))
+
+
+@pytest.mark.parametrize("level", [1, 3, 9, 19])
+def test_zstd_large_sections(engine, level):
+    """zstd over ~300 KiB record sections: several 128 KiB blocks per frame,
+    Huffman literals with 4 streams, FSE / repeat / predefined sequence tables,
+    repeat offsets across blocks; C2 JSON logs and C4 arrays."""
+    for kind, n in ((2, 1500), (5, 6000)):
+        sl = synth.make_slice(kind, n, base_offset=3, max_section=300000)
+        check_batch(engine, CHAINS["filter_init_timeout" if kind == 2 else "array_map"],
+                    recompress(sl, [4], 0x100 | level))
 
 
 def test_compressed_resident_and_errors(engine):
@@ -1359,10 +1370,14 @@ def test_compressed_resident_and_errors(engine):
         bad = recompress(sl, codecs, flags, corrupt={3: 50})
         check_batch(engine, modules, bad)
         assert orc_chain(modules).process_batch(bad)["status"] == -104  # FSG_E_IO
-    # zstd (codec 4): not restated on the GPU path -> Unsupported, like the oracle
+    # zstd bits on uncompressed sections: not zstd frames -> io::Error, like the oracle
     z = bytearray(recompress(sl, [0]))
     z[22] = (z[22] & ~7) | 4
     check_batch(engine, modules, bytes(z))
+    # corrupted zstd sections (content checksum on): both sides stop at that batch
+    for off in (5, 30, 60, 200):
+        bad = recompress(sl, [4], 0x100, corrupt={2: off})
+        check_batch(engine, modules, bad)
 
 
 # ---------------------------------------------------------------------------
