@@ -212,8 +212,11 @@ def cpu_baseline(kind, modules, per_proc):
 def roofline(per, t, workload, n_records, n_batches):
     # algorithmic bytes per launch: k_eval reads the slice once; k_write reads the
     # survivors' payloads (~ the output size) and writes the output batch once; the
-    # CRC reads the output once
-    kernels = {"k_eval": (per["eval_ms"], t["in_bytes"]), "k_write": (per["write_ms"], 2 * t["out_bytes"]),
+    # CRC reads the output once.  array_map (C4): the evaluation is
+    # priced on input + output bytes (it produces the element descriptors of a
+    # variable-size output)
+    ev_bytes = t["in_bytes"] + (t["out_bytes"] if workload == "c4-array-map" else 0)
+    kernels = {"k_eval": (per["eval_ms"], ev_bytes), "k_write": (per["write_ms"], 2 * t["out_bytes"]),
                "k_crc": (per["crc_ms"], t["out_bytes"])}
     dom = max(kernels, key=lambda k: kernels[k][0])
     dom_ms, dom_bytes = kernels[dom]
@@ -238,6 +241,28 @@ def get_slice(kind, nrec, rank):
     return _SLICES[key]
 
 
+def cpu_one_record():
+    """f3's CPU baseline: the scalar oracle's process() of the same one-record
+    SmartModuleInput (one host core, called through ctypes), p50 over 20000 calls."""
+    from fluvio_amd import protocol as P
+    from oracle.oracle import OracleChain
+    raw = P.encode_records([P.Record.new(b'{"level":"warn","message":"request timeout"}')])
+    oc = OracleChain([("filter_init", {"key": "timeout"}, None)])
+    for _ in range(200):
+        oc.process(raw, 0, -1)
+    n = 20000
+    lat = []
+    for _ in range(n):
+        t1 = time.perf_counter()
+        r = oc.process(raw, 0, -1)
+        lat.append(time.perf_counter() - t1)
+    assert r["status"] == 0 and r["n_records"] == 1
+    lat.sort()
+    return {"value": lat[n // 2] * 1e6, "unit": "us", "cores": 1, "kind": "port", "p99_us": lat[n * 99 // 100] * 1e6,
+            "sample": f"{n} calls of the scalar C oracle's process() on the same one-record input, p50 (includes "
+                      f"the ctypes call and result marshalling, ~a few us); wasmtime itself is not available here"}
+
+
 def cpu_baselines_first(ctx, names):
     """CPU baselines run before this process touches the GPU (the pool's
     processes are started from a GPU-free parent), rank 0 at N=1 only."""
@@ -247,6 +272,7 @@ def cpu_baselines_first(ctx, names):
     out = {}
     for w in names:
         if w == "f3-one-record":
+            out[w] = cpu_one_record()
             continue
         if w == "c5-agg-sum":
             out[w] = cpu_baseline(3, C5["modules"], min(a.cpu_sample, C5["records_per_partition"]))
@@ -587,7 +613,7 @@ def run_one_record(ctx, cpu):
             "scaling": "weak", "dtype": "u8",
             "config": {"workload": "f3-one-record", "chain": ["filter_init"],
                        "description": "fsg_chain_process of a one-record SmartModuleInput (H2D upload, eval, "
-                                      "plan with one host sync, write, CRC, D2H of the output)"}}
+                                      "plan with one host sync, write, CRC, D2H of the output)"}, "cpu_baseline": cpu.get("f3-one-record")}
 
 
 def run_workload(ctx, w, nrec, cpu):

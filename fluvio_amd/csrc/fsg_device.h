@@ -145,7 +145,9 @@ struct BatchStat {
 enum KeepMode : uint8_t { KM_COPY = 0, KM_UPPER = 1, KM_I32 = 2, KM_AGG = 3, KM_ARRAY = 4, KM_CONCAT = 5,
                          KM_AGGJ = 6 };  // KM_AGGJ: value = cat[vpos, vpos + vlen) (k_aggj's map text)
 // KeptRec::pad bits for KM_ARRAY / KM_CONCAT
-enum KeepFlags : uint8_t { KF_UPPER = 1, KF_I32 = 2 };
+enum KeepFlags : uint8_t { KF_UPPER = 1, KF_I32 = 2,
+                           KF_ESUM = 4 };  // KM_ARRAY from k_arr_lean: ts = Σ (varint + text) bytes of the
+                                           // elements, hdr = elements of >= 40 bytes (fsg_array.hip)
 struct KeptRec {
   uint64_t src;        // absolute slice offset of the source record (its length varint)
   uint64_t vpos;       // absolute slice offset of the source value bytes

@@ -2396,6 +2396,9 @@ __device__ __forceinline__ uint32_t elem_out_size(uint32_t len, int64_t rel) {
 }
 // Σ output record sizes of the elements of one KM_ARRAY record
 __device__ __forceinline__ uint64_t array_rec_bytes(const KeptRec& d, const ElemRec* elem, int64_t rel) {
+  // k_arr_lean's sums: every element shorter than 40 bytes has an inner length
+  // below 64 (one varint byte), so its record is 5 + vsize(rel) + vsize(len) + len
+  if ((d.pad & KF_ESUM) && d.hdr == 0) return (uint64_t)d.ival * (5 + vsize(rel)) + (uint64_t)d.ts;
   const ElemRec* e = elem + (d.vpos >> 1);
   uint64_t s = 0;
   for (int32_t j = 0; j < d.ival; j++) s += elem_out_size(e[j].out_len & 0x7FFFFFFFu, rel);
@@ -4493,6 +4496,11 @@ void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s) {
   uint32_t grid = a.nbatches;
   if (mode == EVAL_FLAT) {
     launch_flat(a, s);  // k_flat_frame (k_chase + window descriptors) and k_flat
+    grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list
+  } else if (mode == EVAL_ARRAY) {
+    // record starts (k_chase_x), then the lean array kernel (fsg_array.hip)
+    hipLaunchKernelGGL(k_chase_x, dim3(std::min<uint32_t>((a.nbatches + 255) / 256, 4096)), dim3(256), 0, s, a);
+    launch_array_lean(a, s);
     grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list
   } else if (mode == EVAL_LEAN) {
     // persistent: as many workgroups as fit on the device at once

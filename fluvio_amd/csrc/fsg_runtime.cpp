@@ -1861,12 +1861,15 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   // is an experiment, opt-in with FSG_FLAT=1: measured on MI355X (C2, round 3)
   // k_flat 2.56 ms against k_eval_lean 1.61 ms, parity-green both ways
   const bool flat = lean && getenv_flag("FSG_FLAT") && flat_eligible(c->hdesc, ops);
-  if (lean) HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
+  // array_map alone: the lean array kernel, unsupported shapes deferred to k_eval
+  const bool arr = !lean && nb > 1 && !s->has_pass && array_lean_eligible(c->hdesc, ops) &&
+                   !getenv_flag("FSG_NO_ARRAY_LEAN");
+  if (lean || arr) HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
   if (flat) {
     HIPCHK(c->bwin.ensure((size_t)std::max<uint32_t>(nb, 1) * sizeof(BatchWin)));
     ea.bwin = c->bwin.as<BatchWin>();
   }
-  launch_eval(ea, ops, flat ? EVAL_FLAT : lean ? EVAL_LEAN : EVAL_EXACT, st);
+  launch_eval(ea, ops, flat ? EVAL_FLAT : lean ? EVAL_LEAN : arr ? EVAL_ARRAY : EVAL_EXACT, st);
   HIPCHK(hipGetLastError());
   if (c->timed) HIPCHK(hipEventRecord(c->ev[1], st));
   launch_mins(ea.bstat, nb, ea.mins, st);
@@ -2047,15 +2050,16 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   HIPCHK(c->hpin.ensure(kPinPlan + kSmallOut));
   HIPCHK(hipMemcpyAsync(c->hpin.p, c->plan.p, sizeof(Plan), hipMemcpyDeviceToHost, st));
   static_assert(sizeof(Plan) + sizeof(uint32_t) <= kPinPlan, "pinned plan block");
-  if (lean) HIPCHK(hipMemcpyAsync((uint8_t*)c->hpin.p + sizeof(Plan), ea.list, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  if (lean || arr)
+    HIPCHK(hipMemcpyAsync((uint8_t*)c->hpin.p + sizeof(Plan), ea.list, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   unsigned long long sfs[3] = {0, 0, 0};
   const bool dedup = has_sf && sfa.op == OP_DEDUP && nb && !so;
   if (dedup) HIPCHK(hipMemcpyAsync(sfs, sfa.scal, sizeof sfs, hipMemcpyDeviceToHost, st));
   HIPCHK(wait_stream(st));
   memcpy(&c->hplan, c->hpin.p, sizeof(Plan));
-  c->last.eval_path = flat ? FSG_EVAL_FLAT : lean ? FSG_EVAL_LEAN : FSG_EVAL_EXACT;
+  c->last.eval_path = flat ? FSG_EVAL_FLAT : lean ? FSG_EVAL_LEAN : arr ? FSG_EVAL_ARRAY : FSG_EVAL_EXACT;
   c->last.deferred = 0;
-  if (lean) memcpy(&c->last.deferred, (const uint8_t*)c->hpin.p + sizeof(Plan), sizeof(uint32_t));
+  if (lean || arr) memcpy(&c->last.deferred, (const uint8_t*)c->hpin.p + sizeof(Plan), sizeof(uint32_t));
   if (dedup) {
     c->sf->n_ent = sfs[0];
     c->sf->arena_len = sfs[1];

@@ -167,6 +167,7 @@ typedef struct fsg_timings {
 #define FSG_EVAL_EXACT 0 /* k_eval over every batch */
 #define FSG_EVAL_LEAN 1  /* k_eval_lean (LDS windows), deferred batches through k_eval */
 #define FSG_EVAL_FLAT 2  /* k_flat (register-resident substring scan), deferred batches through k_eval */
+#define FSG_EVAL_ARRAY 3 /* k_arr_lean (array_map lane per record), deferred batches through k_eval */
 
 const char *fsg_last_error_message(void);
 int fsg_abi_version(void);

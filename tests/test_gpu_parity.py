@@ -220,6 +220,61 @@ def test_random_parity(engine, chain, kind, n):
 
 
 # ---------------------------------------------------------------------------
+# k_arr_lean (fsg_array.hip): array_map alone, lane per record; arrays outside
+# its grammar (floats, nested values, escapes, leading zeros, -0, long ints,
+# non-ASCII, errors) defer their batch to the exact kernel
+# ---------------------------------------------------------------------------
+def _array_slice(seed, nbatches=80, odd=0.1):
+    import random
+    rng = random.Random(seed)
+    good = ["1", "-7", "0", "123456789012345678", "true", "false", "null", '"ab c"', '""', '"x,]"', "-42"]
+    weird = ["1.5", "1e3", "01", "-0", "1234567890123456789012", "[1]", '{"a":1}', '"\\n"', '"\u00e9"', '"é"',
+             "tru", "nul", "-", "+1"]
+    out, base = b"", 0
+    for bi in range(nbatches):
+        b = P.Batch(base_offset=base)
+        nrec = rng.choice([1, 3, 40, 64, 65, 130, 200])
+        for _ in range(nrec):
+            els = [rng.choice(good) for _ in range(rng.randint(0, 12))]
+            if rng.random() < odd / nrec * 4:
+                els.insert(rng.randint(0, len(els)), rng.choice(weird))
+            sep = rng.choice([",", ", ", " ,", "\n,\t"])
+            v = rng.choice(["", " ", "\n"]) + "[" + rng.choice(["", " "]) + sep.join(els) + rng.choice(["", " "]) + "]"
+            if odd and rng.random() < 0.003:
+                v = rng.choice(["", "[1,2", "x", "[1,]", "[,]"])
+            key = None if rng.random() < 0.7 else b"k"
+            r = P.Record.new_key_value(key, v.encode())
+            if rng.random() < 0.1:
+                r.headers = 2
+            b.add_record(r)
+        enc = b.encode()
+        if len(enc) - 57 > 16000:
+            continue
+        out += enc
+        base += nrec + rng.randint(0, 5)
+    return out
+
+
+@pytest.mark.parametrize("seed,odd", [(1, 0.0), (2, 0.1), (3, 0.5)])
+def test_array_lean_parity(engine, seed, odd):
+    sl = _array_slice(seed, odd=odd)
+    check_batch(engine, CHAINS["array_map"], sl)
+    check_batch(engine, CHAINS["array_map"], sl, max_bytes=20000)
+    g = gpu_chain(engine, CHAINS["array_map"])
+    if orc_chain(CHAINS["array_map"]).process_batch(sl)["status"] == 0:  # (floats / -0: both unsupported)
+        g.process_batch(sl)
+        t = g.last_timings()
+        assert t["eval_path"] == 3, t  # FSG_EVAL_ARRAY
+        if odd == 0.0:
+            assert t["deferred"] < t["n_batches"] // 10, t
+    # the C4 synthetic arrays: every batch on the lean path
+    sl2 = synth.make_slice(5, 20000, base_offset=3)
+    check_batch(engine, CHAINS["array_map"], sl2)
+    g.process_batch(sl2)
+    assert g.last_timings()["deferred"] == 0
+
+
+# ---------------------------------------------------------------------------
 # composed chains: stages after an array_map, an aggregate or a stateful
 # filter (engine.rs:147-167 feeds each stage's successes to the next); the
 # GPU runs them as segments (fsg_runtime.cpp run_composed)
