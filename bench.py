@@ -129,16 +129,6 @@ class Ctx:
             dist.init_process_group("gloo")
             self.dist = dist
 
-    def nccl(self):
-        """RCCL group for GPU-tensor collectives (created on first use by every rank)."""
-        if self.dist is None:
-            return None
-        if self._nccl is None:
-            import torch
-            torch.cuda.set_device(self.local)
-            self._nccl = self.dist.new_group(backend="nccl")
-        return self._nccl
-
     def barrier(self):
         if self.dist is not None:
             self.dist.barrier()
@@ -632,13 +622,6 @@ def main():
     head = a.workload
     extra = [] if a.only else [w for w in EXTRA if w != head]
     cpu = cpu_baselines_first(ctx, [head] + extra)
-    if "c5-keyed-agg" in [head] + extra:
-        # torch's HIP runtime (the keyed-state merge) starts before the engine's
-        # large allocations: started after them it can find no device
-        import torch
-        torch.cuda.set_device(ctx.local)
-        torch.zeros(1, device=f"cuda:{ctx.local}")
-        ctx.nccl()
     line = dict(run_workload(ctx, head, a.records, cpu))
     workloads = {}
     for w in extra:

@@ -2049,7 +2049,13 @@ __global__ __launch_bounds__(256) void k_chase_x(EvalArgs a) {
 
 // four waves per SIMD (eight workgroups per CU, as many as the LDS holds)
 template <bool kJson>
-__global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJson ? 1 : 4))) void k_eval_lean(EvalArgs a) {
+#ifndef FSG_JSON_WPE
+#define FSG_JSON_WPE 1  // waves per SIMD of the JSON lean kernel (register budget)
+#endif
+#ifndef FSG_LEAN_WPE
+#define FSG_LEAN_WPE 4
+#endif
+__global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJson ? FSG_JSON_WPE : FSG_LEAN_WPE))) void k_eval_lean(EvalArgs a) {
   __shared__ typename std::conditional<kJson, LeanLdsJ, LeanLds>::type L;
   const uint32_t l = threadIdx.x;
   const uint32_t G = gridDim.x;

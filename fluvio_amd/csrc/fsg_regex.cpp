@@ -6,14 +6,19 @@
 // regex crate (1.6.0 / 1.8.1) is a third-party dependency that is not in the
 // reference tree; we restate its published semantics for the supported subset:
 // unanchored is_match over valid UTF-8, Unicode-aware `.` (any scalar but \n),
-// `\d` (Unicode Nd), `\s` (White_Space), `^`/`$` at value start/end (no
-// multi-line flag), `\A` / `\z`, `[[:name:]]` ASCII classes, inline flags i
-// (simple case folding, restated for ASCII letters + U+212A / U+017F), s and U.
-// `\w`, `\W`, `\b`, `\B` are exact on ASCII values only (the kernel reports
-// FSG_E_UNSUPPORTED for a non-ASCII value); word boundaries are DFA states that
-// remember whether the previous byte was a word byte.  \p{..}, the m / x / u
-// flags, nested classes and class set operations are rejected at init
-// (FSG_E_UNSUPPORTED).
+// `\d` (Unicode Nd), `\s` (White_Space), `\w` (Alphabetic + M + Nd + Pc +
+// Join_Control), `\p{..}` / `\P{..}` (General_Category values and groups, Any,
+// ASCII, Assigned, White_Space; fsg_unicode.h, generated from this image's
+// Unicode tables), `^`/`$` at value start/end or, under the m flag, at line
+// boundaries (DFA states that remember whether the previous byte was \n),
+// `\A` / `\z`, `[[:name:]]` ASCII classes, inline flags i (simple case folding,
+// restated for ASCII letters + U+212A / U+017F), s, U, m, x (whitespace and #
+// comments ignored) and u (off: ASCII \d \s \w; a negated class, `.` or \W that
+// could match invalid UTF-8 is the crate's init error).  `\b`, `\B` are exact on
+// ASCII values only (the kernel reports FSG_E_UNSUPPORTED for a non-ASCII value);
+// word boundaries are DFA states that remember whether the previous byte was a
+// word byte.  Scripts and other binary properties in \p{..}, nested classes and
+// class set operations are rejected at init (FSG_E_UNSUPPORTED).
 //
 // Output: a DFA over bytes with unanchored restart folded in, byte classes,
 // sticky acceptance, an end-of-value acceptance bit and the longest possible
@@ -21,6 +26,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <set>
@@ -28,6 +34,7 @@
 #include <vector>
 
 #include "fsg_regex.h"
+#include "fsg_unicode.h"
 
 namespace fsg {
 namespace {
@@ -53,6 +60,8 @@ const Range kNd[] = {
 const Range kWs[] = {{0x09, 0x0D}, {0x20, 0x20},     {0x85, 0x85},     {0xA0, 0xA0},     {0x1680, 0x1680},
                      {0x2000, 0x200A}, {0x2028, 0x2029}, {0x202F, 0x202F}, {0x205F, 0x205F}, {0x3000, 0x3000}};
 const Range kWordAscii[] = {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}};
+const Range kDigitAscii[] = {{'0', '9'}};
+const Range kSpaceAscii[] = {{'\t', '\r'}, {' ', ' '}};  // (?-u)\s: [\t\n\v\f\r ]
 
 using Set = std::vector<Range>;
 
@@ -83,8 +92,15 @@ Set table(const Range (&t)[N], bool neg) {
   return neg ? negate(s) : s;
 }
 
+Set urange(const fsg_urange* r, uint32_t n) {
+  Set o;
+  for (uint32_t k = 0; k < n; k++) o.push_back({r[k].lo, r[k].hi});
+  return o;
+}
+
 // ---------------- AST
-enum NodeT { N_EMPTY, N_SET, N_CAT, N_ALT, N_REP, N_BOL, N_EOL, N_WB, N_NWB };
+// N_MBOL / N_MEOL: ^ / $ under the m flag (after / before a \n, or at the ends)
+enum NodeT { N_EMPTY, N_SET, N_CAT, N_ALT, N_REP, N_BOL, N_EOL, N_WB, N_NWB, N_MBOL, N_MEOL };
 struct Node {
   NodeT t = N_EMPTY;
   Set set;
@@ -97,8 +113,92 @@ using NodeP = std::unique_ptr<Node>;
 struct Parser {
   std::vector<uint32_t> p;
   size_t i = 0;
-  bool err = false, unsup = false, word = false, wb = false;
+  bool err = false, unsup = false, word = false, wb = false, ml = false;
   bool fi = false, fs = false;  // inline flags i, s
+  bool fm = false, fx = false, fu = true;  // m (multi-line), x (verbose), u (Unicode, on by default)
+
+  // x: whitespace (char::is_whitespace) and # comments between tokens are ignored
+  static bool uspace(uint32_t c) {
+    for (const Range& r : kWs)
+      if (c >= r.lo && c <= r.hi) return true;
+    return false;
+  }
+  void skip_x() {
+    while (fx && i < p.size()) {
+      if (uspace(p[i])) {
+        i++;
+      } else if (p[i] == '#') {
+        while (i < p.size() && p[i] != '\n') i++;
+      } else {
+        break;
+      }
+    }
+  }
+  // \p{..} / \pX after the 'p' / 'P' (regex-syntax: names compared without case,
+  // spaces, '_' and '-'); 2 = a set, 0 = failure (err / unsup set)
+  int property(bool neg, Set* out) {
+    if (!fu) {  // Unicode classes need the u flag
+      err = true;
+      return 0;
+    }
+    std::string name;
+    if (at('{')) {
+      i++;
+      if (at('^')) {
+        neg = !neg;
+        i++;
+      }
+      while (i < p.size() && p[i] != '}') {
+        const uint32_t c = p[i++];
+        if (c == ' ' || c == '_' || c == '-') continue;
+        if (c >= 0x80) {
+          unsup = true;
+          return 0;
+        }
+        name += (char)(c >= 'A' && c <= 'Z' ? c + 32 : c);
+      }
+      if (!at('}')) {
+        err = true;
+        return 0;
+      }
+      i++;
+    } else {
+      if (i >= p.size()) {
+        err = true;
+        return 0;
+      }
+      const uint32_t c = p[i++];
+      if (c >= 0x80) {
+        err = true;
+        return 0;
+      }
+      name += (char)(c >= 'A' && c <= 'Z' ? c + 32 : c);
+    }
+    for (auto& ch : name)
+      if (ch == ':') ch = '=';
+    const long m = fsg_u_property(name.c_str());
+    Set st;
+    if (m == FSG_UPROP_ASCII) {
+      st.push_back({0, 0x7F});
+    } else if (m == FSG_UPROP_WSPACE) {
+      st.assign(std::begin(kWs), std::end(kWs));
+    } else if (m >= 0) {
+      for (uint32_t k = 0; k < fsg_u_ncats; k++)
+        if (m & (1L << k)) {
+          Set t = urange(fsg_u_cats[k].r, fsg_u_cats[k].n);
+          st.insert(st.end(), t.begin(), t.end());
+        }
+    } else {
+      unsup = true;  // scripts and other properties: not restated
+      return 0;
+    }
+    if (fi) {  // a Unicode class under (?i) would need full simple case folding
+      unsup = true;
+      return 0;
+    }
+    *out = neg ? negate(st) : norm(st);
+    return 2;
+  }
   int depth = 0;
 
   // (?i): simple case folding restated for ASCII letters (+ U+212A ~ k, U+017F ~ s);
@@ -159,12 +259,19 @@ struct Parser {
     }
     uint32_t e = p[i++];
     switch (e) {
-      case 'd': *s = table(kNd, false); return 2;
-      case 'D': *s = table(kNd, true); return 2;
-      case 's': *s = table(kWs, false); return 2;
-      case 'S': *s = table(kWs, true); return 2;
-      case 'w': *s = table(kWordAscii, false); word = true; return 2;
-      case 'W': *s = table(kWordAscii, true); word = true; return 2;
+      case 'd': case 'D': case 's': case 'S': case 'w': case 'W': {
+        const bool neg = e < 'a';
+        if (!fu && neg) {  // (?-u)\D \S \W can match invalid UTF-8 (Regex on &str)
+          err = true;
+          return 0;
+        }
+        Set t = (e | 0x20) == 'd' ? (fu ? table(kNd, false) : table(kDigitAscii, false))
+                : (e | 0x20) == 's' ? (fu ? table(kWs, false) : table(kSpaceAscii, false))
+                : (fu ? urange(fsg_u_word, fsg_u_word_n) : table(kWordAscii, false));
+        *s = neg ? negate(t) : norm(t);
+        return 2;
+      }
+      case 'p': case 'P': return property(e == 'P', s);
       case 'n': *c = '\n'; return 1;
       case 't': *c = '\t'; return 1;
       case 'r': *c = '\r'; return 1;
@@ -204,7 +311,7 @@ struct Parser {
         }
         if (e == 'b' || e == 'B') word = wb = true;
         return e == 'b' ? 3 : e == 'B' ? 4 : e == 'A' ? 5 : 6;
-      case 'p': case 'P': case 'u': case 'U':
+      case 'u': case 'U':
         unsup = true;
         return 0;
       default:
@@ -227,6 +334,7 @@ struct Parser {
     }
     bool first = true;
     for (;;) {
+      skip_x();
       if (i >= p.size()) {
         err = true;
         return n;
@@ -297,6 +405,10 @@ struct Parser {
       }
       add_folded(n->set, lo, hi);
     }
+    if (neg && !fu) {  // (?-u)[^..] can match invalid UTF-8 (Regex on &str)
+      err = true;
+      return n;
+    }
     n->set = neg ? negate(n->set) : norm(n->set);  // case folding applies before the negation
     return n;
   }
@@ -334,7 +446,7 @@ struct Parser {
           i++;
         } else {  // inline flags (?flags) / (?flags:re): i, s, U; m, x, u, R unsupported
           int neg = 0, nflags = 0;
-          bool nfi = fi, nfs = fs;
+          bool nfi = fi, nfs = fs, nfm = fm, nfx = fx, nfu = fu;
           for (;;) {
             if (i >= p.size()) {
               err = true;
@@ -349,6 +461,9 @@ struct Parser {
               if (f == ')') {  // until the end of the enclosing group
                 fi = nfi;
                 fs = nfs;
+                fm = nfm;
+                fx = nfx;
+                fu = nfu;
                 return n;  // N_EMPTY
               }
               break;
@@ -366,7 +481,13 @@ struct Parser {
             } else if (f == 's') {
               nfs = !neg;
             } else if (f == 'U') {  // greed only: same language for is_match
-            } else if (f == 'm' || f == 'x' || f == 'u' || f == 'R') {
+            } else if (f == 'm') {
+              nfm = !neg;
+            } else if (f == 'x') {
+              nfx = !neg;
+            } else if (f == 'u') {
+              nfu = !neg;
+            } else if (f == 'R') {  // CRLF mode (regex 1.8): not restated
               unsup = true;
               return n;
             } else {
@@ -376,9 +497,12 @@ struct Parser {
             nflags++;
             if (neg) neg = 2;
           }
-          const bool sfi = fi, sfs = fs;
+          const bool sfi = fi, sfs = fs, sfm = fm, sfx = fx, sfu = fu;
           fi = nfi;
           fs = nfs;
+          fm = nfm;
+          fx = nfx;
+          fu = nfu;
           if (++depth > 200) {
             err = true;
             return n;
@@ -387,6 +511,9 @@ struct Parser {
           depth--;
           fi = sfi;
           fs = sfs;
+          fm = sfm;
+          fx = sfx;
+          fu = sfu;
           if (!at(')')) {
             err = true;
             return g;
@@ -399,11 +526,14 @@ struct Parser {
         err = true;
         return n;
       }
-      const bool sfi = fi, sfs = fs;  // flags set inside a group end with it
+      const bool sfi = fi, sfs = fs, sfm = fm, sfx = fx, sfu = fu;  // flags set inside a group end with it
       NodeP g = alt();
       depth--;
       fi = sfi;
       fs = sfs;
+      fm = sfm;
+      fx = sfx;
+      fu = sfu;
       if (!at(')')) {
         err = true;
         return g;
@@ -413,6 +543,10 @@ struct Parser {
     }
     if (c == '[') return cls();
     if (c == '.') {
+      if (!fu) {  // (?-u:.) can match invalid UTF-8 (Regex on &str)
+        err = true;
+        return n;
+      }
       n->t = N_SET;
       if (fs)
         n->set = {{0, 0x10FFFF}};
@@ -421,11 +555,13 @@ struct Parser {
       return n;
     }
     if (c == '^') {
-      n->t = N_BOL;
+      n->t = fm ? N_MBOL : N_BOL;
+      ml |= fm;
       return n;
     }
     if (c == '$') {
-      n->t = N_EOL;
+      n->t = fm ? N_MEOL : N_EOL;
+      ml |= fm;
       return n;
     }
     if (c == '\\') {
@@ -456,9 +592,12 @@ struct Parser {
   NodeP cat() {
     auto n = std::make_unique<Node>();
     n->t = N_CAT;
-    while (i < p.size() && p[i] != '|' && p[i] != ')' && !err && !unsup) {
+    for (;;) {
+      skip_x();
+      if (!(i < p.size() && p[i] != '|' && p[i] != ')' && !err && !unsup)) break;
       NodeP a = atom();
       for (;;) {
+        skip_x();
         if (i >= p.size()) break;
         uint32_t q = p[i];
         int mn, mx;
@@ -526,7 +665,7 @@ struct Parser {
 int utf8_len(uint32_t c) { return c < 0x80 ? 1 : c < 0x800 ? 2 : c < 0x10000 ? 3 : 4; }
 int64_t max_len(const Node* n, bool ascii) {
   switch (n->t) {
-    case N_EMPTY: case N_BOL: case N_EOL: case N_WB: case N_NWB: return 0;
+    case N_EMPTY: case N_BOL: case N_EOL: case N_WB: case N_NWB: case N_MBOL: case N_MEOL: return 0;
     case N_SET: {
       int m = 0;
       for (auto& r : n->set) {
@@ -564,7 +703,7 @@ int64_t max_len(const Node* n, bool ascii) {
 }
 
 // ---------------- byte NFA
-enum NfaT { F_BYTE, F_SPLIT, F_EPS, F_BOT, F_EOT, F_MATCH, F_WB, F_NWB };
+enum NfaT { F_BYTE, F_SPLIT, F_EPS, F_BOT, F_EOT, F_MATCH, F_WB, F_NWB, F_MBOT, F_MEOT };
 struct NState {
   NfaT t;
   uint8_t lo, hi;
@@ -693,6 +832,11 @@ Frag build(Nfa& g, const Node* n, bool ascii) {
       int s = g.add(n->t == N_WB ? F_WB : F_NWB);
       return {s, {{s, 0}}};
     }
+    case N_MBOL:
+    case N_MEOL: {
+      int s = g.add(n->t == N_MBOL ? F_MBOT : F_MEOT);
+      return {s, {{s, 0}}};
+    }
     case N_SET: {
       std::vector<std::vector<std::pair<uint8_t, uint8_t>>> seqs;
       for (auto& r : n->set) {
@@ -706,8 +850,69 @@ Frag build(Nfa& g, const Node* n, bool ascii) {
         g.st[s].b = -2;
         return {s, {}};
       }
-      Frag f = bytes_seq(g, seqs[0]);
-      for (size_t k = 1; k < seqs.size(); k++) f = alt2(g, f, bytes_seq(g, seqs[k]));
+      // The sequences of a normalized set have, under a common prefix, byte
+      // ranges that are equal or disjoint: they form a deterministic trie.
+      // Equal subtrees are shared (hash-consed from the leaves), giving the
+      // minimal acyclic automaton of the class: \w is ~60 lead-byte edges
+      // into a handful of shared continuation chains, not ~700 alternatives.
+      struct TNode {
+        std::vector<std::pair<std::pair<uint8_t, uint8_t>, int>> kids;  // (range, child); leaf: none
+      };
+      std::vector<TNode> trie(1);
+      for (auto& sq : seqs) {
+        int at = 0;
+        for (auto& r : sq) {
+          int nx = -1;
+          for (auto& kd : trie[at].kids)
+            if (kd.first == r) nx = kd.second;
+          if (nx < 0) {
+            nx = (int)trie.size();
+            trie[at].kids.push_back({r, nx});
+            trie.emplace_back();
+          }
+          at = nx;
+        }
+      }
+      // canonical ids bottom-up (children have larger indices than parents)
+      std::vector<int> canon(trie.size());
+      std::map<std::vector<int>, int> sig;
+      for (size_t k = trie.size(); k-- > 0;) {
+        std::vector<int> key;
+        auto kids = trie[k].kids;
+        std::sort(kids.begin(), kids.end());
+        for (auto& kd : kids) {
+          key.push_back(kd.first.first);
+          key.push_back(kd.first.second);
+          key.push_back(canon[kd.second]);
+        }
+        canon[k] = sig.emplace(key, (int)sig.size()).first->second;
+      }
+      // emit each canonical node once: a balanced split tree over its edges
+      Frag f{-1, {}};
+      std::vector<int> entry(sig.size(), -1);
+      std::function<int(int)> emit = [&](int k) -> int {
+        if (entry[canon[k]] >= 0) return entry[canon[k]];
+        std::vector<int> edges;
+        for (auto& kd : trie[k].kids) {
+          int s = g.add(F_BYTE, kd.first.first, kd.first.second);
+          if (trie[kd.second].kids.empty())
+            f.outs.push_back({s, 0});
+          else
+            g.st[s].a = emit(kd.second);
+          edges.push_back(s);
+        }
+        std::function<int(size_t, size_t)> tree = [&](size_t a, size_t b) -> int {
+          if (b - a == 1) return edges[a];
+          int sp = g.add(F_SPLIT);
+          const size_t mid = (a + b) / 2;
+          const int l = tree(a, mid), r = tree(mid, b);
+          g.st[sp].a = l;
+          g.st[sp].b = r;
+          return sp;
+        };
+        return entry[canon[k]] = tree(0, edges.size());
+      };
+      f.start = emit(0);
       return f;
     }
     case N_CAT: {
@@ -750,12 +955,15 @@ struct Closure {
   const Nfa& g;
   std::vector<int> mark;
   int gen = 0;
+  int64_t work = 0;  // NFA states visited (the compile-time budget)
   explicit Closure(const Nfa& n) : g(n), mark(n.st.size(), 0) {}
   // closure of `seeds`; keeps BYTE, MATCH and (unfollowed) EOT states; word
   // boundaries are kept pending (resolve = false) or decided from the previous
   // and next byte's word-ness (resolve = true)
+  // multi-line anchors: ^ passes at the start or after a \n (pnl), $ at the
+  // end or before a \n (nnl); kept pending unless resolved like the boundaries
   std::vector<int> run(const std::vector<int>& seeds, bool bot, bool eot, bool resolve = false, bool pw = false,
-                       bool nw = false) {
+                       bool nw = false, bool pnl = false, bool nnl = false) {
     gen++;
     std::vector<int> out, stack(seeds.rbegin(), seeds.rend());
     while (!stack.empty()) {
@@ -763,6 +971,7 @@ struct Closure {
       stack.pop_back();
       if (s < 0 || mark[s] == gen) continue;
       mark[s] = gen;
+      work++;
       const NState& x = g.st[s];
       switch (x.t) {
         case F_BYTE: case F_MATCH: out.push_back(s); break;
@@ -787,6 +996,18 @@ struct Closure {
           else if ((pw != nw) == (x.t == F_WB))
             stack.push_back(x.a);
           break;
+        case F_MBOT:
+          if (bot || (resolve && pnl))
+            stack.push_back(x.a);
+          else if (!resolve)
+            out.push_back(s);
+          break;
+        case F_MEOT:
+          if (eot || (resolve && nnl))
+            stack.push_back(x.a);
+          else if (!resolve)
+            out.push_back(s);
+          break;
       }
     }
     std::sort(out.begin(), out.end());
@@ -796,7 +1017,7 @@ struct Closure {
 
 }  // namespace
 
-static int determinize(const Node* rootp, bool ascii, bool word, bool wb, Dfa& out, std::string& msg);
+static int determinize(const Node* rootp, bool ascii, bool word, bool wb, bool mlm, Dfa& out, std::string& msg);
 
 int compile_regex(const std::string& pattern, Dfa& out, Dfa& full, std::string& msg) {
   // pattern -> code points (must be valid UTF-8; Rust &str)
@@ -826,15 +1047,21 @@ int compile_regex(const std::string& pattern, Dfa& out, Dfa& full, std::string& 
     msg = "regex parse error";
     return -2;
   }
-  if (int rc = determinize(root.get(), true, P.word, P.wb, out, msg)) return rc;
-  return determinize(root.get(), false, P.word, P.wb, full, msg);
+  if (int rc = determinize(root.get(), true, P.word, P.wb, P.ml, out, msg)) return rc;
+  return determinize(root.get(), false, P.word, P.wb, P.ml, full, msg);
 }
+
+// ~0.5 s of subset construction on one core: a pattern whose DFA needs more is
+// one the GPU subset does not take (FSG_E_UNSUPPORTED), not a stalled chain build
+static const int64_t kCompileBudget = 60000000;
 
 static bool word_byte(int b) { return (b >= '0' && b <= '9') || (b >= 'A' && b <= 'Z') || (b >= 'a' && b <= 'z') || b == '_'; }
 
-int determinize(const Node* rootp, bool ascii, bool word, bool wb, Dfa& out, std::string& msg) {
-  // word boundaries need the previous byte: no chunk-parallel restarts (max_len -1)
-  const int64_t ml = wb ? -1 : max_len(rootp, ascii);
+int determinize(const Node* rootp, bool ascii, bool word, bool wb, bool mlm, Dfa& out, std::string& msg) {
+  // word boundaries and multi-line anchors need the previous byte: no
+  // chunk-parallel restarts (max_len -1)
+  const int64_t ml = (wb || mlm) ? -1 : max_len(rootp, ascii);
+  const bool resolve = wb || mlm;  // assertions decided at each transition from the previous / next byte
   Nfa g;
   Frag f = build(g, rootp, ascii);
   int m = g.add(F_MATCH);
@@ -851,6 +1078,7 @@ int determinize(const Node* rootp, bool ascii, bool word, bool wb, Dfa& out, std
   if (wb)  // word bytes form their own classes
     for (int b = 0; b < 256; b++)
       if (word_byte(b) != (b > 0 && word_byte(b - 1))) cut[b] = 1;
+  if (mlm) cut['\n'] = cut['\n' + 1] = 1;  // \n is its own class
   std::vector<uint8_t> cls(256);
   std::vector<int> rep;
   int nc = -1;
@@ -865,11 +1093,12 @@ int determinize(const Node* rootp, bool ascii, bool word, bool wb, Dfa& out, std
   Closure C(g);
   std::map<std::vector<int>, int> ids;
   std::vector<std::vector<int>> sets;
-  std::vector<uint8_t> bot_flag, pw_flag;
-  auto intern = [&](const std::vector<int>& s, bool is_bot, bool pw) {
+  std::vector<uint8_t> bot_flag, pw_flag, nl_flag;
+  auto intern = [&](const std::vector<int>& s, bool is_bot, bool pw, bool pnl = false) {
     auto key = s;
     if (is_bot) key.push_back(-7);  // the BOT state is distinct (EOT acceptance with ^ satisfied)
     if (pw) key.push_back(-8);      // the previous byte was a word byte (word boundaries)
+    if (pnl) key.push_back(-9);     // the previous byte was \n (multi-line anchors)
     auto it = ids.find(key);
     if (it != ids.end()) return it->second;
     int id = (int)sets.size();
@@ -877,31 +1106,69 @@ int determinize(const Node* rootp, bool ascii, bool word, bool wb, Dfa& out, std
     sets.push_back(s);
     bot_flag.push_back(is_bot);
     pw_flag.push_back(pw);
+    nl_flag.push_back(pnl);
     return id;
   };
-  const int s_bot = intern(C.run({start}, true, false), true, false);
-  const int s_mid = intern(C.run({start}, false, false), false, false);
+  auto has_match = [&](const std::vector<int>& v) {
+    return std::find_if(v.begin(), v.end(), [&](int s) { return g.st[s].t == F_MATCH; }) != v.end();
+  };
+  auto by_class = [&](const std::vector<int>& v, std::vector<std::vector<int>>& bucket) {
+    for (auto& b : bucket) b.clear();
+    for (int s : v) {
+      const NState& x = g.st[s];
+      if (x.t != F_BYTE) continue;
+      for (int c = cls[x.lo]; c <= cls[x.hi]; c++) bucket[c].push_back(x.a);
+    }
+  };
+  // Without assertions to resolve, every subset holds the restart closure S
+  // (the pattern started again at each position); a subset is kept as its
+  // members outside S, and S's successors per class are computed once.
+  const bool fast = !resolve;
+  std::vector<uint8_t> in_s(g.st.size(), 0);
+  std::vector<std::vector<int>> es(ncls), bucket(ncls);
+  bool s_has = false, s_eot = false;
+  auto strip = [&](std::vector<int> v) {
+    if (fast) v.erase(std::remove_if(v.begin(), v.end(), [&](int s) { return in_s[s] != 0; }), v.end());
+    return v;
+  };
+  std::vector<int> S;
+  if (fast) {
+    S = C.run({start}, false, false);
+    for (int s : S) in_s[s] = 1;
+    s_has = has_match(S);
+    s_eot = has_match(C.run(S, false, true));
+    by_class(S, es);
+    for (auto& e : es) e = strip(C.run(e, false, false));
+  }
+  const int s_bot = intern(strip(C.run({start}, true, false)), true, false);
+  const int s_mid = intern(strip(C.run({start}, false, false)), false, false);
   int s_acc = -1;  // sticky accept reached through a word boundary decided at a transition
   std::vector<std::vector<int>> trans;
   std::vector<uint8_t> acc;
   for (size_t k = 0; k < sets.size(); k++) {
-    if (sets.size() > (ascii ? 255u : 65535u)) {
+    // bounded chain-build cost: subsets before minimization and closure work
+    if (sets.size() > (ascii ? 1024u : 32768u) || C.work > kCompileBudget) {
       msg = "regex too large for the GPU DFA";
       return -103;
     }
     const auto cur = sets[k];
-    const bool pw = pw_flag[k];
-    auto has_match = [&](const std::vector<int>& v) {
-      return std::find_if(v.begin(), v.end(), [&](int s) { return g.st[s].t == F_MATCH; }) != v.end();
-    };
-    const bool is_acc = has_match(cur);
+    const bool pw = pw_flag[k], pnl = nl_flag[k];
+    const bool is_acc = has_match(cur) || s_has;
     uint8_t a = is_acc ? 1 : 0;
-    {
-      auto ce = C.run(cur, bot_flag[k], true, wb, pw, false);  // at the end: no next byte
-      if (is_acc || has_match(ce)) a |= 2;
+    if (!is_acc) {  // at the end: no next byte
+      std::vector<int> full = cur;
+      if (fast && bot_flag[k]) {
+        full.insert(full.end(), S.begin(), S.end());
+        std::sort(full.begin(), full.end());
+      }
+      auto ce = C.run(full, bot_flag[k], true, resolve, pw, false, pnl, false);
+      if (has_match(ce) || (fast && !bot_flag[k] && s_eot)) a |= 2;
+    } else {
+      a |= 2;
     }
     acc.push_back(a);
     std::vector<int> row(ncls);
+    if (fast && !is_acc) by_class(cur, bucket);  // targets of each byte state, by class (one pass)
     for (int c = 0; c < ncls; c++) {
       if (is_acc) {
         row[c] = (int)k;  // sticky: is_match is decided
@@ -909,26 +1176,78 @@ int determinize(const Node* rootp, bool ascii, bool word, bool wb, Dfa& out, std
       }
       const int byte = rep[c];
       const bool nw = wb && word_byte(byte);
-      const std::vector<int> res = wb ? C.run(cur, bot_flag[k], false, true, pw, nw) : cur;
-      if (wb && has_match(res)) {  // a boundary before this byte completed the match
+      const bool nnl = mlm && byte == '\n';
+      const std::vector<int> res = resolve ? C.run(cur, bot_flag[k], false, true, pw, nw, pnl, nnl) : cur;
+      if (resolve && has_match(res)) {  // an assertion before this byte completed the match
         if (s_acc < 0) s_acc = intern({m}, false, false);
         row[c] = s_acc;
         continue;
       }
       std::vector<int> nxt;
-      for (int s : res) {
-        const NState& x = g.st[s];
-        if (x.t == F_BYTE && byte >= x.lo && byte <= x.hi) nxt.push_back(x.a);
+      if (resolve) {
+        for (int s : res) {
+          const NState& x = g.st[s];
+          if (x.t == F_BYTE && byte >= x.lo && byte <= x.hi) nxt.push_back(x.a);
+        }
+        nxt.push_back(start);  // unanchored restart at the next position
+        row[c] = intern(C.run(nxt, false, false), false, nw, nnl);
+      } else {
+        nxt.swap(bucket[c]);
+        nxt.insert(nxt.end(), es[c].begin(), es[c].end());  // S is implied
+        row[c] = intern(strip(C.run(nxt, false, false)), false, false, false);
       }
-      nxt.push_back(start);  // unanchored restart at the next position
-      row[c] = intern(C.run(nxt, false, false), false, nw);
     }
     trans.push_back(row);
   }
-  out.nstates = (uint32_t)sets.size();
+  // Moore minimization: states with the same acceptance whose transitions
+  // lead to the same blocks are merged (suffix-equivalent subsets, the many
+  // sticky accepts); block ids renumbered in first-reached order from s_bot
+  const int n0 = (int)sets.size();
+  std::vector<int> blk(n0);
+  for (int k = 0; k < n0; k++) blk[k] = acc[k];
+  for (int nb = -1;;) {
+    std::map<std::vector<int>, int> sig;
+    std::vector<int> nblk(n0);
+    for (int k = 0; k < n0; k++) {
+      std::vector<int> key(ncls + 1);
+      key[0] = blk[k];
+      for (int c = 0; c < ncls; c++) key[c + 1] = blk[trans[k][c]];
+      nblk[k] = sig.emplace(std::move(key), (int)sig.size()).first->second;
+    }
+    blk.swap(nblk);
+    if ((int)sig.size() == nb) break;
+    nb = (int)sig.size();
+  }
+  std::vector<int> ren(n0, -1), rep_of;
+  {
+    std::vector<int> order{s_bot, s_mid};
+    for (size_t q = 0; q < order.size(); q++) {
+      const int k = order[q];
+      if (ren[blk[k]] >= 0) continue;
+      ren[blk[k]] = (int)rep_of.size();
+      rep_of.push_back(k);
+      for (int c = 0; c < ncls; c++)
+        if (ren[blk[trans[k][c]]] < 0) order.push_back(trans[k][c]);
+    }
+  }
+  {
+    std::vector<std::vector<int>> mt(rep_of.size(), std::vector<int>(ncls));
+    std::vector<uint8_t> ma(rep_of.size());
+    for (size_t q = 0; q < rep_of.size(); q++) {
+      ma[q] = acc[rep_of[q]];
+      for (int c = 0; c < ncls; c++) mt[q][c] = ren[blk[trans[rep_of[q]][c]]];
+    }
+    trans.swap(mt);
+    acc.swap(ma);
+  }
+  if (trans.size() > (ascii ? 255u : 65535u)) {
+    msg = "regex too large for the GPU DFA";
+    return -103;
+  }
+  out.nstates = (uint32_t)trans.size();
   out.nclasses = (uint32_t)ncls;
-  out.s_bot = (uint32_t)s_bot;
-  out.s_mid = (uint32_t)s_mid;
+  out.s_bot = (uint32_t)ren[blk[s_bot]];
+  out.s_mid = (uint32_t)ren[blk[s_mid]];
   out.max_len = ml < 0 || ml > (1 << 20) ? -1 : (int32_t)ml;
   out.unicode_word = word;
   out.classmap = cls;

@@ -24,6 +24,7 @@
  * cpu_baseline leg may load it.
  */
 #include "fsg_oracle.h"
+#include "fsg_unicode.h"
 
 #include <stdarg.h>
 #include <stdio.h>
@@ -490,6 +491,8 @@ static const cprange WS_TAB[] = {{0x09, 0x0D}, {0x20, 0x20},     {0x85, 0x85},  
                                  {0x1680, 0x1680}, {0x2000, 0x200A}, {0x2028, 0x2029}, {0x202F, 0x202F},
                                  {0x205F, 0x205F}, {0x3000, 0x3000}};
 static const cprange WORD_ASCII[] = {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}};
+static const cprange DIGIT_ASCII[] = {{'0', '9'}};
+static const cprange SPACE_ASCII[] = {{'\t', '\r'}, {' ', ' '}}; /* (?-u)\s */
 
 typedef struct {
   cprange *r;
@@ -556,7 +559,7 @@ static int cs_has(const cset *s, uint32_t c) {
   return 0;
 }
 
-enum { RX_CHAR, RX_CLASS, RX_SPLIT, RX_JMP, RX_BOL, RX_EOL, RX_MATCH, RX_WB, RX_NWB };
+enum { RX_CHAR, RX_CLASS, RX_SPLIT, RX_JMP, RX_BOL, RX_EOL, RX_MATCH, RX_WB, RX_NWB, RX_MBOL, RX_MEOL };
 typedef struct {
   int op;
   uint32_t c;
@@ -572,7 +575,7 @@ typedef struct {
 } rxprog;
 
 /* AST */
-enum { A_EMPTY, A_CHAR, A_CLASS, A_CAT, A_ALT, A_REP, A_BOL, A_EOL, A_WB, A_NWB };
+enum { A_EMPTY, A_CHAR, A_CLASS, A_CAT, A_ALT, A_REP, A_BOL, A_EOL, A_WB, A_NWB, A_MBOL, A_MEOL };
 typedef struct anode {
   int t;
   uint32_t c;
@@ -590,8 +593,88 @@ typedef struct {
   int unsupported;
   int depth;
   int fi, fs;   /* inline flags i (case-insensitive), s (. matches \n); U only swaps greed */
-  int word;     /* \w, \W, \b or \B used: exact on ASCII input only */
+  int fm, fx, fu; /* m: ^ $ at line boundaries; x: whitespace / # comments ignored; u: Unicode classes (on) */
+  int word;     /* \b or \B used: exact on ASCII input only */
 } rxparser;
+
+/* x: whitespace (White_Space) and # comments between tokens are skipped */
+static void rx_skip_x(rxparser *P) {
+  while (P->fx && P->i < P->n) {
+    uint32_t c = P->p[P->i];
+    int ws = 0;
+    for (size_t k = 0; k < sizeof WS_TAB / sizeof WS_TAB[0]; k++) ws |= c >= WS_TAB[k].lo && c <= WS_TAB[k].hi;
+    if (ws) {
+      P->i++;
+    } else if (c == '#') {
+      while (P->i < P->n && P->p[P->i] != '\n') P->i++;
+    } else {
+      break;
+    }
+  }
+}
+/* \p{name} / \pX (after the p / P): General_Category values and groups, Any,
+ * ASCII, Assigned, White_Space; names compared without case, ' ', '_', '-' */
+static int rx_property(rxparser *P, int neg, cset *set) {
+  if (!P->fu) {
+    P->err = 1;
+    return 0;
+  }
+  char name[64];
+  size_t nl = 0;
+  if (P->i < P->n && P->p[P->i] == '{') {
+    P->i++;
+    if (P->i < P->n && P->p[P->i] == '^') {
+      neg = !neg;
+      P->i++;
+    }
+    while (P->i < P->n && P->p[P->i] != '}') {
+      uint32_t c = P->p[P->i++];
+      if (c == ' ' || c == '_' || c == '-') continue;
+      if (c >= 0x80 || nl + 1 >= sizeof name) {
+        P->unsupported = 1;
+        return 0;
+      }
+      name[nl++] = (char)(c == ':' ? '=' : (c >= 'A' && c <= 'Z') ? c + 32 : c);
+    }
+    if (P->i >= P->n) {
+      P->err = 1;
+      return 0;
+    }
+    P->i++;
+  } else {
+    if (P->i >= P->n || P->p[P->i] >= 0x80) {
+      P->err = 1;
+      return 0;
+    }
+    uint32_t c = P->p[P->i++];
+    name[nl++] = (char)((c >= 'A' && c <= 'Z') ? c + 32 : c);
+  }
+  name[nl] = 0;
+  long m = fsg_u_property(name);
+  cset tmp = {0};
+  if (m == FSG_UPROP_ASCII) {
+    cs_add(&tmp, 0, 0x7F);
+  } else if (m == FSG_UPROP_WSPACE) {
+    cs_add_tab(&tmp, WS_TAB, sizeof WS_TAB / sizeof WS_TAB[0], 0);
+  } else if (m >= 0) {
+    for (uint32_t k = 0; k < fsg_u_ncats; k++)
+      if (m & (1L << k))
+        for (uint32_t q = 0; q < fsg_u_cats[k].n; q++) cs_add(&tmp, fsg_u_cats[k].r[q].lo, fsg_u_cats[k].r[q].hi);
+  } else {
+    P->unsupported = 1; /* scripts and other properties */
+    return 0;
+  }
+  if (P->fi) { /* a Unicode class under (?i) needs full simple case folding */
+    free(tmp.r);
+    P->unsupported = 1;
+    return 0;
+  }
+  cs_norm(&tmp);
+  if (neg) cs_negate(&tmp);
+  for (size_t q = 0; q < tmp.n; q++) cs_add(set, tmp.r[q].lo, tmp.r[q].hi);
+  free(tmp.r);
+  return 2;
+}
 
 /* (?i): regex-syntax's simple case folding, restated for ASCII letters: a-z <-> A-Z,
  * plus the two non-ASCII code points that fold to ASCII letters (U+212A KELVIN SIGN
@@ -673,12 +756,26 @@ static int rx_escape(rxparser *P, uint32_t *single, cset *set, int in_class) {
   }
   uint32_t c = P->p[P->i++];
   switch (c) {
-    case 'd': cs_add_tab(set, ND_TAB, sizeof ND_TAB / sizeof ND_TAB[0], 0); return 2;
-    case 'D': cs_add_tab(set, ND_TAB, sizeof ND_TAB / sizeof ND_TAB[0], 1); return 2;
-    case 's': cs_add_tab(set, WS_TAB, sizeof WS_TAB / sizeof WS_TAB[0], 0); return 2;
-    case 'S': cs_add_tab(set, WS_TAB, sizeof WS_TAB / sizeof WS_TAB[0], 1); return 2;
-    case 'w': cs_add_tab(set, WORD_ASCII, 4, 0); set->unicode_word = 1; return 2;
-    case 'W': cs_add_tab(set, WORD_ASCII, 4, 1); set->unicode_word = 1; return 2;
+    case 'd': case 'D': case 's': case 'S': case 'w': case 'W': {
+      const int neg = c < 'a', k = c | 0x20;
+      if (neg && !P->fu) { /* (?-u)\D \S \W can match invalid UTF-8 */
+        P->err = 1;
+        return 0;
+      }
+      if (k == 'd') {
+        if (P->fu) cs_add_tab(set, ND_TAB, sizeof ND_TAB / sizeof ND_TAB[0], neg);
+        else cs_add_tab(set, DIGIT_ASCII, 1, 0);
+      } else if (k == 's') {
+        if (P->fu) cs_add_tab(set, WS_TAB, sizeof WS_TAB / sizeof WS_TAB[0], neg);
+        else cs_add_tab(set, SPACE_ASCII, 2, 0);
+      } else if (P->fu) {
+        cs_add_tab(set, (const cprange *)fsg_u_word, fsg_u_word_n, neg); /* Alphabetic + M + Nd + Pc + Join_Control */
+      } else {
+        cs_add_tab(set, WORD_ASCII, 4, 0);
+      }
+      return 2;
+    }
+    case 'p': case 'P': return rx_property(P, c == 'P', set);
     case 'b': case 'B': /* word boundary assertions (Unicode \w: exact on ASCII input) */
       if (in_class) {
         P->err = 1;
@@ -721,7 +818,7 @@ static int rx_escape(rxparser *P, uint32_t *single, cset *set, int in_class) {
       *single = v;
       return 1;
     }
-    case 'p': case 'P': case 'u': case 'U':
+    case 'u': case 'U':
       P->unsupported = 1;
       return 0;
     default:
@@ -744,6 +841,7 @@ static anode *rx_parse_class(rxparser *P) {
   }
   int first = 1;
   for (;;) {
+    rx_skip_x(P);
     if (P->i >= P->n) {
       P->err = 1;
       return a;
@@ -824,6 +922,10 @@ static anode *rx_parse_class(rxparser *P) {
     }
     cs_add_folded(P, &a->cls, lo, hi);
   }
+  if (neg && !P->fu) { /* (?-u)[^..] can match invalid UTF-8 */
+    P->err = 1;
+    return a;
+  }
   if (neg) cs_negate(&a->cls); /* case folding applies before the negation */
   cs_norm(&a->cls);
   return a;
@@ -862,7 +964,7 @@ static anode *rx_parse_atom(rxparser *P) {
         P->i++;
       } else {
         /* inline flags (?flags) / (?flags:re): i, s, U supported; m, x, u, R not */
-        int neg = 0, nflags = 0, fi = P->fi, fs = P->fs;
+        int neg = 0, nflags = 0, fi = P->fi, fs = P->fs, fm = P->fm, fx = P->fx, fu = P->fu;
         for (;;) {
           if (P->i >= P->n) {
             P->err = 1;
@@ -877,6 +979,9 @@ static anode *rx_parse_atom(rxparser *P) {
             if (f == ')') { /* until the end of the enclosing group */
               P->fi = fi;
               P->fs = fs;
+              P->fm = fm;
+              P->fx = fx;
+              P->fu = fu;
               return an_new(A_EMPTY);
             }
             break;
@@ -892,7 +997,10 @@ static anode *rx_parse_atom(rxparser *P) {
           if (f == 'i') fi = !neg;
           else if (f == 's') fs = !neg;
           else if (f == 'U') { /* greed only: same language */ }
-          else if (f == 'm' || f == 'x' || f == 'u' || f == 'R') {
+          else if (f == 'm') fm = !neg;
+          else if (f == 'x') fx = !neg;
+          else if (f == 'u') fu = !neg;
+          else if (f == 'R') { /* CRLF mode (regex 1.8): not restated */
             P->unsupported = 1;
             return an_new(A_EMPTY);
           } else {
@@ -902,9 +1010,12 @@ static anode *rx_parse_atom(rxparser *P) {
           nflags++;
           if (neg) neg = 2;
         }
-        int sfi = P->fi, sfs = P->fs;
+        int sfi = P->fi, sfs = P->fs, sfm = P->fm, sfx = P->fx, sfu = P->fu;
         P->fi = fi;
         P->fs = fs;
+        P->fm = fm;
+        P->fx = fx;
+        P->fu = fu;
         if (++P->depth > 200) {
           P->err = 1;
           return an_new(A_EMPTY);
@@ -913,6 +1024,9 @@ static anode *rx_parse_atom(rxparser *P) {
         P->depth--;
         P->fi = sfi;
         P->fs = sfs;
+        P->fm = sfm;
+        P->fx = sfx;
+        P->fu = sfu;
         if (P->i >= P->n || P->p[P->i] != ')') {
           P->err = 1;
           return g;
@@ -925,11 +1039,14 @@ static anode *rx_parse_atom(rxparser *P) {
       P->err = 1;
       return an_new(A_EMPTY);
     }
-    int sfi = P->fi, sfs = P->fs; /* flags set inside a group end with it */
+    int sfi = P->fi, sfs = P->fs, sfm = P->fm, sfx = P->fx, sfu = P->fu; /* flags set inside a group end with it */
     anode *g = rx_parse_alt(P);
     P->depth--;
     P->fi = sfi;
     P->fs = sfs;
+    P->fm = sfm;
+    P->fx = sfx;
+    P->fu = sfu;
     if (P->i >= P->n || P->p[P->i] != ')') {
       P->err = 1;
       return g;
@@ -939,6 +1056,10 @@ static anode *rx_parse_atom(rxparser *P) {
   }
   if (c == '[') return rx_parse_class(P);
   if (c == '.') {
+    if (!P->fu) { /* (?-u:.) can match invalid UTF-8 */
+      P->err = 1;
+      return an_new(A_EMPTY);
+    }
     anode *a = an_new(A_CLASS);
     if (P->fs) {
       cs_add(&a->cls, 0, 0x10FFFF);
@@ -948,8 +1069,8 @@ static anode *rx_parse_atom(rxparser *P) {
     }
     return a;
   }
-  if (c == '^') return an_new(A_BOL);
-  if (c == '$') return an_new(A_EOL);
+  if (c == '^') return an_new(P->fm ? A_MBOL : A_BOL);
+  if (c == '$') return an_new(P->fm ? A_MEOL : A_EOL);
   if (c == '\\') {
     anode *a = an_new(A_CHAR);
     cset tmp = {0};
@@ -993,9 +1114,12 @@ static anode *rx_parse_atom(rxparser *P) {
 
 static anode *rx_parse_cat(rxparser *P) {
   anode *cat = an_new(A_CAT);
-  while (P->i < P->n && P->p[P->i] != '|' && P->p[P->i] != ')' && !P->err && !P->unsupported) {
+  for (;;) {
+    rx_skip_x(P);
+    if (!(P->i < P->n && P->p[P->i] != '|' && P->p[P->i] != ')' && !P->err && !P->unsupported)) break;
     anode *atom = rx_parse_atom(P);
     for (;;) {
+      rx_skip_x(P);
       if (P->i >= P->n) break;
       uint32_t q = P->p[P->i];
       int mn, mx;
@@ -1091,6 +1215,8 @@ static void rx_comp(rxprog *g, const anode *a) {
     case A_BOL: rx_emit(g, RX_BOL, 0, 0, 0); break;
     case A_EOL: rx_emit(g, RX_EOL, 0, 0, 0); break;
     case A_WB: rx_emit(g, RX_WB, 0, 0, 0); break;
+    case A_MBOL: rx_emit(g, RX_MBOL, 0, 0, 0); break;
+    case A_MEOL: rx_emit(g, RX_MEOL, 0, 0, 0); break;
     case A_NWB: rx_emit(g, RX_NWB, 0, 0, 0); break;
     case A_CAT:
       for (size_t i = 0; i < a->nk; i++) rx_comp(g, a->kids[i]);
@@ -1161,6 +1287,7 @@ static int rx_compile(const char *pat, rxprog *g) {
   memset(&P, 0, sizeof P);
   P.p = cps;
   P.n = ncp;
+  P.fu = 1; /* Unicode mode is the default */
   anode *root = rx_parse_alt(&P);
   if (P.word) g->unicode_word = 1;
   int rc = 0;
@@ -1206,6 +1333,12 @@ static void ss_add(const rxprog *g, sset *s, int pc, size_t pos, size_t n, int *
         break;
       case RX_EOL:
         if (pos == n) stack[sp++] = p + 1;
+        break;
+      case RX_MBOL: /* (?m)^ */
+        if (pos == 0 || cp[pos - 1] == '\n') stack[sp++] = p + 1;
+        break;
+      case RX_MEOL: /* (?m)$ */
+        if (pos == n || cp[pos] == '\n') stack[sp++] = p + 1;
         break;
       case RX_WB:
       case RX_NWB: {

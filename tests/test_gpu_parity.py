@@ -176,6 +176,10 @@ CHAINS = {
     "regex_word_boundary": [("regex-filter", {"regex": r"\btimeout\b|\b\d{3}\b"}, None)],
     "regex_case_insensitive": [("regex-filter", {"regex": r"(?i)TIMEOUT|(?i:ssn)\s"}, None)],
     "regex_posix": [("regex-filter", {"regex": r"[[:digit:]]{3}-[[:digit:]]{2}|^[[:upper:]]"}, None)],
+    "regex_unicode_word": [("regex-filter", {"regex": r"\w+é|\p{Lu}\p{Ll}+\d|\P{L}{4}$"}, None)],
+    "regex_multiline": [("regex-filter", {"regex": r"(?m)^\d+$|x$|^\{\x22level"}, None)],
+    "regex_verbose": [("regex-filter", {"regex": r"(?x) time out \s* \d  # the timeout records"}, None)],
+    "regex_ascii_only": [("regex-filter", {"regex": r"(?-u)\w\d{2}\s"}, None)],
     "map_then_regex_ci": [("map", {}, None), ("regex-filter", {"regex": r"(?i)error"}, None)],
     "map": [("map", {}, None)],
     "filter_json": [("filter_json", {}, None)],
@@ -521,9 +525,11 @@ def test_device_framing(engine):
 
 
 def test_unicode_word_is_loud(engine):
-    """\\w on a non-ASCII value is outside the GPU subset: FSG_E_UNSUPPORTED when
-    (and only when) such a record is reached in stream order, like the oracle."""
-    chain = [("regex-filter", {"regex": r"\w+"}, None)]
+    """\\b on a non-ASCII value is outside the GPU subset: FSG_E_UNSUPPORTED when
+    (and only when) such a record is reached in stream order, like the oracle.
+    (\\w itself is the Unicode class, decided by the full byte DFA.)"""
+    check_batch(engine, [("regex-filter", {"regex": r"\w+"}, None)], _one_record_slice("caf\u00e9".encode()))
+    chain = [("regex-filter", {"regex": r"\bx"}, None)]
     check_batch(engine, chain, synth.make_slice(4, 500))
     b = P.Batch()
     for v in ("abc", "caf\u00e9", "xyz"):

@@ -23,14 +23,16 @@ PATTERNS = [r"\d{3}-\d{2}-\d{4}", r"[A-Z]", r"^ab|cd$", r"a(b|c)*d", r"colou?r\s
             r"é+", r"[α-ω]{2}", r".{3}$", r"(a|ab)(c|bcd)(d*)", r"a?a?a?aaa", r"\x41\x{263A}", r"[\-\]a]",
             r"\bab", r"cd\b", r"\b\d+\b", r"\Ba\B", r"x\b|\by", r"\b", r"(?i)abcd", r"(?i)[a-c]x|D$",
             r"(?i:ab)c", r"(?i)[^a]", r"(?s)a.c", r"\Aab", r"cd\z", r"[[:alpha:]]{3}", r"[[:^digit:][:space:]]x",
-            r"(?i)[[:lower:]]{2}\b"]
-WORD = ("\\b", "\\B", "\\w", "\\W")
+            r"(?i)[[:lower:]]{2}\b", r"\w+é", r"^\w+$", r"\W\w", r"[\w-]{3}", r"\p{Lu}", r"\P{L}\pN",
+            r"\p{gc=Nd}", r"[\p{Sc}\d]", r"\p{^Ll}", r"(?m)^b$", r"(?m)a$|^c", r"(?m:^)x|y(?-m)$",
+            r"(?x) a b # comment", r"(?x)[ a ] c", r"(?x: \d \  \d )", r"(?-u)\w\d\s", r"(?u)\w(?-u:[a-z])"]
+WORD = ("\\b", "\\B")
 
 
 def texts(rng):
-    alpha = "abcdxyzABCD0123456789- \t\n.é☺αβω"
+    alpha = "abcdxyzABCD0123456789- \t\n.é☺αβωÉ٣€_#"
     out = ["", "a", "abc", "ac", "xxy", "123-45-6789", "my ssn 987-65-4321!", "colour  x", "☺A", "aé",
-           "abcd", "cd", "ab", "timeouts", "αβγ", "aaa", "abcbcd"]
+           "abcd", "cd", "ab", "timeouts", "αβγ", "aaa", "abcbcd", "a\nb\nc", "x\nb", "naïve", "9 ٣", "c\na"]
     for _ in range(60):
         out.append("".join(rng.choice(alpha) for _ in range(rng.randint(0, 24))))
     return out
@@ -42,7 +44,7 @@ def test_dfa_matches_oracle(pattern):
     word = any(w in pattern for w in WORD)
     for t in texts(rng):
         b = t.encode()
-        if word and not b.isascii():  # Unicode word semantics: the kernel reports UNSUPPORTED
+        if word and not b.isascii():  # Unicode \b semantics: the kernel reports UNSUPPORTED
             with pytest.raises(ValueError):
                 dfa_match(pattern, b)
             continue
@@ -57,8 +59,11 @@ def test_max_len():
 
 @pytest.mark.parametrize("bad,code", [("a(", _ffi.FSG_E_INIT), ("*a", _ffi.FSG_E_INIT), ("[z-a]", _ffi.FSG_E_INIT),
                                       ("(?)a", _ffi.FSG_E_INIT), ("(?z)a", _ffi.FSG_E_INIT), ("[\\b]", _ffi.FSG_E_INIT),
-                                      ("(?m)^a", _ffi.FSG_E_UNSUPPORTED), ("(?x)a b", _ffi.FSG_E_UNSUPPORTED),
-                                      (r"\pL", _ffi.FSG_E_UNSUPPORTED), ("(?i)é", _ffi.FSG_E_UNSUPPORTED),
+                                      ("(?-u:.)", _ffi.FSG_E_INIT), ("(?-u)[^a]", _ffi.FSG_E_INIT),
+                                      (r"(?-u)\W", _ffi.FSG_E_INIT), (r"(?-u)\pL", _ffi.FSG_E_INIT),
+                                      (r"\p{", _ffi.FSG_E_INIT), (r"\p{Nope}", _ffi.FSG_E_UNSUPPORTED),
+                                      (r"(?i)\p{Lu}", _ffi.FSG_E_UNSUPPORTED), ("(?R)a", _ffi.FSG_E_UNSUPPORTED),
+                                      (r"\p{Greek}", _ffi.FSG_E_UNSUPPORTED), ("(?i)é", _ffi.FSG_E_UNSUPPORTED),
                                       ("[[a]]", _ffi.FSG_E_UNSUPPORTED)])
 def test_errors_agree_with_oracle(bad, code):
     with pytest.raises(ValueError) as e:
@@ -66,3 +71,40 @@ def test_errors_agree_with_oracle(bad, code):
     assert e.value.args[0] == code
     with pytest.raises(ValueError):
         O.regex_is_match(bad, b"x")
+
+
+def _random_pattern(rng, depth=0):
+    atoms = ["a", "b", "é", "α", ".", r"\d", r"\w", r"\W", r"\s", r"\pL", r"\p{Lu}", r"\P{N}", "[a-cé]", "[^b]",
+             r"[\w-]", r"[α-ω\d]", "^", "$", r"\x{263A}", "(?m:^)", "(?m:$)", "(?i:ab)", "(?s:.)"]
+    if depth > 2 or rng.random() < 0.4:
+        a = rng.choice(atoms)
+    elif rng.random() < 0.5:
+        a = "(?:" + "|".join(_random_pattern(rng, depth + 1) for _ in range(rng.randint(1, 3))) + ")"
+    else:
+        a = "(?:" + "".join(_random_pattern(rng, depth + 1) for _ in range(rng.randint(1, 3))) + ")"
+    if a not in ("^", "$", "(?m:^)", "(?m:$)"):
+        a += rng.choice(["", "", "*", "+", "?", "{2}", "{1,3}", "*?"])
+    return a
+
+
+def test_random_patterns_match_oracle():
+    """Random patterns over Unicode classes, properties, multi-line anchors and
+    repeats: the minimized byte DFA decides exactly what the Pike VM decides.
+    A pattern whose DFA exceeds the chain-build budget is FSG_E_UNSUPPORTED
+    (loud, never a wrong answer); those must stay the exception."""
+    rng = random.Random(7)
+    alpha = "abéαβA1 \n-☺_٣É"
+    n = too_large = 0
+    for _ in range(150):
+        pat = "".join(_random_pattern(rng) for _ in range(rng.randint(1, 3)))
+        tx = ["".join(rng.choice(alpha) for _ in range(rng.randint(0, 10))).encode() for _ in range(12)]
+        try:
+            dfa_match(pat, b"")
+        except ValueError as e:
+            assert e.args[0] == _ffi.FSG_E_UNSUPPORTED, pat
+            too_large += 1
+            continue
+        for t in tx:
+            assert dfa_match(pat, t)[0] == O.regex_is_match(pat, t), (pat, t)
+            n += 1
+    assert n > 1000 and too_large < 20, (n, too_large)
