@@ -16,6 +16,7 @@
 #include <cstdint>
 
 #include "fsg_device.h"
+#include "fsg_float.h"
 
 namespace fsg {
 
@@ -34,6 +35,7 @@ enum JsonErr : uint8_t {
   JE_DEEP,             // ignored value nested deeper than the device frame stack (outside the restatement)
   JE_UNSUP,            // valid input outside the device restatement (array_map: floats, unsorted keys)
   JE_INVALID_VALUE,    // u32 visitor: sub = JU_UINT / JU_NINT, [a, b) = the digits ("invalid value: integer `N`, expected u32")
+  JE_RANGE,            // "number out of range" (f64_from_parts / parse_exponent_overflow), at pos
 };
 enum JsonUnexp : uint8_t { JU_UNIT = 0, JU_TRUE, JU_FALSE, JU_UINT, JU_NINT, JU_FLOAT, JU_STR, JU_SEQ, JU_MAP };
 enum JsonExp : uint8_t { JX_STRUCT = 0, JX_STRING, JX_VARIANT, JX_UNIT, JX_SEQ, JX_MAP, JX_U32 };
@@ -46,6 +48,299 @@ struct JRes {
   uint32_t pos;  // reader index the position is computed from
   uint32_t a, b;
 };
+
+// serde_json::to_string of a validated JSON value (Value: objects are
+// BTreeMap<String, Value>), from its source text s[0..n): whitespace dropped,
+// strings re-escaped (ser.rs format_escaped_str: \" \\ \b \t \n \f \r, other
+// control bytes \u00xx, the rest raw), numbers as serde_json reads them (u64 /
+// i64 keep their text, f64 through ryu), object members in key-byte order with
+// a repeated key keeping its last value (Map::insert).  Members are picked by
+// selection — the smallest key above the one emitted last — so no member list
+// is stored; one frame per open container.  o == nullptr counts only.
+// Returns the length, or ~0u past kCanonFrames nesting levels.  One lane; the
+// rare path (elements whose canonical text differs from their source text).
+constexpr uint32_t kCanonFrames = 128;  // serde_json's recursion limit bounds the depth
+template <typename P>
+struct JsonCanon {
+  P s;
+  uint32_t n;
+  bool upper;
+  uint8_t* o;
+  uint32_t w;
+  __device__ __forceinline__ uint32_t at(uint32_t k) const {
+    uint8_t c = s[k];
+    if (upper && c >= 'a' && c <= 'z') c -= 32;
+    return c;
+  }
+  __device__ __forceinline__ void put(uint32_t c) {
+    if (o) o[w] = (uint8_t)c;
+    w++;
+  }
+  static __device__ __forceinline__ uint32_t hexv(uint32_t c) { return c <= '9' ? c - '0' : (c | 0x20) - 'a' + 10; }
+  __device__ __forceinline__ uint32_t ws(uint32_t p) const {
+    while (p < n) {
+      const uint32_t c = at(p);
+      if (c != ' ' && c != '\n' && c != '\t' && c != '\r') break;
+      p++;
+    }
+    return p;
+  }
+  // one decoded code point of a validated string at p (p past the escape / bytes)
+  __device__ __forceinline__ uint32_t str_cp(uint32_t& p, uint32_t* nb) const {
+    uint32_t c = at(p++);
+    if (c != '\\') {
+      *nb = 1;  // raw byte (UTF-8 passes through byte by byte)
+      return c;
+    }
+    const uint32_t e = at(p++);
+    *nb = 0;
+    switch (e) {
+      case 'b': return 0x08;
+      case 'f': return 0x0C;
+      case 'n': return 0x0A;
+      case 'r': return 0x0D;
+      case 't': return 0x09;
+      case 'u': {
+        uint32_t cp = (hexv(at(p)) << 12) | (hexv(at(p + 1)) << 8) | (hexv(at(p + 2)) << 4) | hexv(at(p + 3));
+        p += 4;
+        if (cp >= 0xD800 && cp <= 0xDBFF) {  // validated pair
+          const uint32_t c2 = (hexv(at(p + 2)) << 12) | (hexv(at(p + 3)) << 8) | (hexv(at(p + 4)) << 4) | hexv(at(p + 5));
+          p += 6;
+          cp = (((cp - 0xD800) << 10) | (c2 - 0xDC00)) + 0x10000;
+        }
+        return cp;
+      }
+      default: return e;  // " \ /
+    }
+  }
+  // decoded key bytes one at a time (for the BTreeMap order)
+  struct KeyIt {
+    uint32_t p;
+    uint8_t b[4];
+    uint32_t nb, k;
+  };
+  __device__ __forceinline__ int key_next(KeyIt& it) const {  // -1 at the closing quote
+    if (it.k < it.nb) return it.b[it.k++];
+    if (at(it.p) == '"') return -1;
+    uint32_t raw;
+    const uint32_t cp = str_cp(it.p, &raw);
+    if (raw || cp < 0x80) return (int)cp;
+    it.k = 1;
+    if (cp < 0x800) {
+      it.nb = 2;
+      it.b[0] = (uint8_t)(0xC0 | (cp >> 6));
+      it.b[1] = (uint8_t)(0x80 | (cp & 0x3F));
+    } else if (cp < 0x10000) {
+      it.nb = 3;
+      it.b[0] = (uint8_t)(0xE0 | (cp >> 12));
+      it.b[1] = (uint8_t)(0x80 | ((cp >> 6) & 0x3F));
+      it.b[2] = (uint8_t)(0x80 | (cp & 0x3F));
+    } else {
+      it.nb = 4;
+      it.b[0] = (uint8_t)(0xF0 | (cp >> 18));
+      it.b[1] = (uint8_t)(0x80 | ((cp >> 12) & 0x3F));
+      it.b[2] = (uint8_t)(0x80 | ((cp >> 6) & 0x3F));
+      it.b[3] = (uint8_t)(0x80 | (cp & 0x3F));
+    }
+    return it.b[0];
+  }
+  // keys at a and b (positions after their opening quotes): <0, 0, >0
+  __device__ int key_cmp(uint32_t a, uint32_t b) const {
+    KeyIt x{a, {0, 0, 0, 0}, 0, 0}, y{b, {0, 0, 0, 0}, 0, 0};
+    for (;;) {
+      const int u = key_next(x), v = key_next(y);
+      if (u != v) return u < v ? -1 : 1;  // -1 (end) sorts first
+      if (u < 0) return 0;
+    }
+  }
+  __device__ __forceinline__ uint32_t skip_str(uint32_t p) const {  // p after the opening quote -> past the closing one
+    for (;;) {
+      const uint32_t c = at(p++);
+      if (c == '"') return p;
+      if (c == '\\') p++;
+    }
+  }
+  __device__ uint32_t skip_value(uint32_t p) const {  // validated value at p -> past it
+    const uint32_t c = at(p);
+    if (c == '"') return skip_str(p + 1);
+    if (c == '[' || c == '{') {
+      uint32_t d = 0;
+      for (;;) {
+        const uint32_t x = at(p++);
+        if (x == '"') {
+          p = skip_str(p);
+        } else if (x == '[' || x == '{') {
+          d++;
+        } else if (x == ']' || x == '}') {
+          if (--d == 0) return p;
+        }
+      }
+    }
+    while (p < n) {
+      const uint32_t x = at(p);
+      if (x == ',' || x == ']' || x == '}' || x == ' ' || x == '\n' || x == '\t' || x == '\r') break;
+      p++;
+    }
+    return p;
+  }
+  __device__ void emit_str(uint32_t p) {  // p after the opening quote
+    put('"');
+    for (;;) {
+      if (at(p) == '"') break;
+      uint32_t raw;
+      const uint32_t cp = str_cp(p, &raw);
+      if (raw && cp >= 0x80) {
+        put(cp);
+        continue;
+      }
+      if (cp < 0x80) {
+        switch (cp) {
+          case '"': put('\\'); put('"'); break;
+          case '\\': put('\\'); put('\\'); break;
+          case 0x08: put('\\'); put('b'); break;
+          case 0x09: put('\\'); put('t'); break;
+          case 0x0A: put('\\'); put('n'); break;
+          case 0x0C: put('\\'); put('f'); break;
+          case 0x0D: put('\\'); put('r'); break;
+          default:
+            if (cp < 0x20) {
+              const char* hx = "0123456789abcdef";
+              put('\\'); put('u'); put('0'); put('0');
+              put((uint8_t)hx[cp >> 4]);
+              put((uint8_t)hx[cp & 15]);
+            } else {
+              put(cp);
+            }
+        }
+      } else if (cp < 0x800) {
+        put(0xC0 | (cp >> 6));
+        put(0x80 | (cp & 0x3F));
+      } else if (cp < 0x10000) {
+        put(0xE0 | (cp >> 12));
+        put(0x80 | ((cp >> 6) & 0x3F));
+        put(0x80 | (cp & 0x3F));
+      } else {
+        put(0xF0 | (cp >> 18));
+        put(0x80 | ((cp >> 12) & 0x3F));
+        put(0x80 | ((cp >> 6) & 0x3F));
+        put(0x80 | (cp & 0x3F));
+      }
+    }
+    put('"');
+  }
+  // a scalar at p -> past it
+  __device__ uint32_t emit_scalar(uint32_t p) {
+    const uint32_t c = at(p);
+    if (c == '"') {
+      emit_str(p + 1);
+      return skip_str(p + 1);
+    }
+    if (c == '-' || (c >= '0' && c <= '9')) {
+      auto acc = [&](uint32_t k) -> int { return k < n ? (int)at(k) : -1; };
+      const flt::NumVal v = flt::num_value(acc, p, n);
+      if (v.kind == 1) {
+        w += flt::ryu_format(v.f, o ? o + w : nullptr);
+      } else {
+        for (uint32_t k = p; k < v.end; k++) put(at(k));
+      }
+      return v.end;
+    }
+    const uint32_t e = skip_value(p);  // true / false / null
+    for (uint32_t k = p; k < e; k++) put(at(k));
+    return e;
+  }
+  // the smallest member key above `last` (~0u: none yet) of the object whose
+  // members start at p; *kp = key position, *vp = its last value; false: none left
+  __device__ bool next_member(uint32_t p, uint32_t last, uint32_t* kp, uint32_t* vp) const {
+    bool any = false;
+    p = ws(p);
+    while (at(p) != '}') {
+      if (at(p) == ',') p = ws(p + 1);
+      const uint32_t k = p + 1;
+      p = ws(skip_str(k));  // ':'
+      const uint32_t v = ws(p + 1);
+      p = ws(skip_value(v));
+      if (last != ~0u && key_cmp(k, last) <= 0) continue;
+      const int c = any ? key_cmp(k, *kp) : -1;
+      if (c <= 0) {  // smaller, or the same key again (a later insert replaces the value)
+        *kp = k;
+        *vp = v;
+        any = true;
+      }
+    }
+    return any;
+  }
+  __device__ uint32_t run() {
+    uint32_t fpos[kCanonFrames], flast[kCanonFrames];  // '[': next element / 0|1 emitted; '{': first member / last key
+    uint64_t fkind[kCanonFrames / 64] = {};            // bit = 1: '['
+    uint32_t sn = 0;
+    w = 0;
+    uint32_t p = ws(0), vend = 0;
+    bool value = true;  // a value at p is to be emitted
+    for (;;) {
+      if (value) {
+        const uint32_t c = at(p);
+        if (c == '[' || c == '{') {
+          if (sn >= kCanonFrames) return ~0u;
+          put(c);
+          const uint64_t bit = 1ull << (sn & 63);
+          if (c == '[') fkind[sn >> 6] |= bit; else fkind[sn >> 6] &= ~bit;
+          fpos[sn] = p + 1;
+          flast[sn] = c == '[' ? 0u : ~0u;
+          sn++;
+        } else {
+          vend = emit_scalar(p);
+          if (sn == 0) return w;
+          if ((fkind[(sn - 1) >> 6] >> ((sn - 1) & 63)) & 1) fpos[sn - 1] = vend;
+        }
+        value = false;
+        continue;
+      }
+      const uint32_t f = sn - 1;
+      if ((fkind[f >> 6] >> (f & 63)) & 1) {  // '['
+        uint32_t q = ws(fpos[f]);
+        if (at(q) == ',') q = ws(q + 1);
+        if (at(q) == ']') {
+          put(']');
+          vend = q + 1;
+          sn--;
+          if (sn == 0) return w;
+          if ((fkind[(sn - 1) >> 6] >> ((sn - 1) & 63)) & 1) fpos[sn - 1] = vend;
+          continue;
+        }
+        if (flast[f]) put(',');
+        flast[f] = 1;
+        p = q;
+        value = true;
+      } else {  // '{'
+        uint32_t kp = 0, vp = 0;
+        if (!next_member(fpos[f], flast[f], &kp, &vp)) {
+          put('}');
+          sn--;
+          if (sn == 0) return w;
+          if ((fkind[(sn - 1) >> 6] >> ((sn - 1) & 63)) & 1) fpos[sn - 1] = skip_value(fpos[f] - 1);
+          continue;
+        }
+        if (flast[f] != ~0u) put(',');
+        flast[f] = kp;
+        emit_str(kp);
+        put(':');
+        p = vp;
+        value = true;
+      }
+    }
+  }
+};
+template <typename P>
+__device__ __noinline__ uint32_t json_canon(P s, uint32_t n, bool upper, uint8_t* o) {
+  JsonCanon<P> c;
+  c.s = s;
+  c.n = n;
+  c.upper = upper;
+  c.o = o;
+  c.w = 0;
+  return c.run();
+}
 
 constexpr uint32_t kJsonFrames = 64;  // ignore_value frame stack: one u64 ('[' = 1, '{' = 0)
 
@@ -389,12 +684,15 @@ struct JsonDev {
     if (c == 'e' || c == 'E') return exponent_syn();
     return 0;
   }
-  // parse_integer + parse_number syntax; *kind = JU_UINT / JU_NINT / JU_FLOAT
+  // parse_integer + parse_number syntax; *kind = JU_UINT / JU_NINT / JU_FLOAT.
+  // A float's value is read as serde_json reads it (fsg_float.h num_value):
+  // where f64_from_parts / parse_exponent_overflow fail, "number out of range".
   __device__ __forceinline__ int parse_integer(bool positive, uint8_t* kind) {
+    const uint32_t st = positive ? i : i - 1;  // the '-' was eaten by the caller
     const int c = next();
     if (c < 0) return error(JE_EOF_VALUE);
     uint64_t sig = 0;
-    bool flt = false;
+    bool flt = false, longi = false;
     if (c == '0') {
       if (dig(pnull())) return peek_error(JE_NUMBER);
     } else if (c >= '1' && c <= '9') {
@@ -405,11 +703,8 @@ struct JsonDev {
         const uint64_t dg = (uint64_t)(p - '0');
         if (sig > (~0ull - dg) / 10) {  // parse_long_integer
           while (dig(pnull())) eat();
-          const int q = pnull();
-          *kind = JU_FLOAT;
-          if (q == '.') return decimal_syn();
-          if (q == 'e' || q == 'E') return exponent_syn();
-          return 0;
+          flt = longi = true;
+          break;
         }
         eat();
         sig = sig * 10 + dg;
@@ -425,8 +720,13 @@ struct JsonDev {
       flt = true;
       if (exponent_syn()) return -1;
     }
-    if (!positive && (sig == 0 || sig > 0x8000000000000000ull)) flt = true;  // -0 / below i64::MIN -> f64
+    if (!longi && !positive && (sig == 0 || sig > 0x8000000000000000ull)) flt = true;  // -0 / below i64::MIN -> f64
     *kind = flt ? JU_FLOAT : (positive ? JU_UINT : JU_NINT);
+    if (flt) {
+      auto acc = [&](uint32_t k) -> int { return k < n ? at(k) : -1; };
+      const flt::NumVal v = flt::num_value(acc, st, n);
+      if (v.kind == 2) return fail_at(v.err, JE_RANGE);
+    }
     return 0;
   }
 
@@ -775,19 +1075,19 @@ struct JsonDev {
   // parse follows de.rs deserialize_seq / SeqAccess / deserialize_any /
   // MapAccess / parse_object_colon; instead of building Values it records,
   // per element, its source span and the length of its canonical
-  // serialization (ser.rs: compact, format_escaped_str, itoa).  Objects must
-  // already be in BTreeMap order (strictly increasing keys) and numbers must
-  // be integers (serde_json turns floats, -0 and integers beyond u64/i64 into
-  // f64, whose ryu Display is outside the restatement): a float stops the
-  // parse with JE_UNSUP at once (as the oracle does), an object that needs
-  // re-ordering only once the whole document has parsed (a later syntax error
-  // is still reported exactly).  The engine reports JE_UNSUP as
-  // FSG_E_UNSUPPORTED if that record is reached in stream order.
+  // serialization (ser.rs: compact, format_escaped_str, itoa, ryu).  An
+  // element holding a float (serde_json reads fractions, exponents, -0 and
+  // integers beyond u64/i64 as f64) or an object whose keys are not already
+  // in BTreeMap order, and one whose text differs from its canonical text
+  // (whitespace, escapes), is measured and written by json_canon in their own
+  // kernels (k_canon_len, k_write_canon: the canonicalizer's frame stack and
+  // bignums stay out of k_eval / k_write); a verbatim one is copied by k_write.
   // ------------------------------------------------------------------------
   uint32_t vcanon;  // canonical bytes of the element being parsed
   bool vhas_u;      // a \u escape was decoded (canonical form may differ in bytes)
   bool vhas_bs;     // the last string held a backslash
-  bool vunsup;      // an object needs re-ordering: unsupported unless a later syntax error decides
+  bool vunsup;      // outside the device restatement: unsupported unless a later syntax error decides
+  bool vcomplex;    // a float or an object out of key order: the canonical text comes from json_canon
   static __device__ __forceinline__ uint32_t canon_byte_len(uint32_t c) {
     if (c == '"' || c == '\\' || c == 0x08 || c == 0x09 || c == 0x0A || c == 0x0C || c == 0x0D) return 2;
     return c < 0x20 ? 6 : 1;
@@ -902,7 +1202,7 @@ struct JsonDev {
           if (c == '-') eat();
           uint8_t kind;
           if (parse_integer(c != '-', &kind)) return -1;
-          if (kind == JU_FLOAT) return fail_at(i, JE_UNSUP);
+          if (kind == JU_FLOAT) vcomplex = true;  // ryu's text
           vcanon += i - i0;  // an integer's canonical text is its source text (JSON has no + / leading 0)
           break;
         }
@@ -962,11 +1262,11 @@ struct JsonDev {
         const uint32_t lv = sn - 1;
         if (lv >= (uint32_t)kKeyFrames) {
           // deeper objects: only a single-member object is known to be in order
-          if (!first_member) vunsup = true;
+          if (!first_member) vcomplex = true;
         } else {
           if (pk1[lv] != 0xFFFFFFFFu) {
             const bool esc_prev = (pk0[lv] >> 31) != 0;
-            if (esc_prev || vhas_bs || key_cmp(pk0[lv] & 0x7FFFFFFFu, pk1[lv], k0, k1) >= 0) vunsup = true;
+            if (esc_prev || vhas_bs || key_cmp(pk0[lv] & 0x7FFFFFFFu, pk1[lv], k0, k1) >= 0) vcomplex = true;
           }
           pk0[lv] = k0 | (vhas_bs ? 0x80000000u : 0u);
           pk1[lv] = k1;
@@ -1028,12 +1328,15 @@ struct JsonDev {
         const uint32_t e0 = i;
         vcanon = 0;
         vhas_u = false;
+        vcomplex = false;
         if (any_value()) {
           rc = -1;
           break;
         }
         const uint32_t span = i - e0;
-        const bool verb = span == vcanon && !vhas_u;
+        if (vcomplex) vcanon = 0;  // floats / members out of key order: k_canon_len measures it
+        const bool verb = span == vcanon && !vhas_u && !vcomplex;
+        if (!verb) r.sub = 1;  // the batch has elements for k_canon_len / k_write_canon
         out[k].pos = abs0 + e0;
         out[k].src_len = span;
         out[k].out_len = vcanon | (verb ? 0x80000000u : 0u);
@@ -1050,7 +1353,7 @@ struct JsonDev {
     // a valid document whose objects need re-ordering: outside the restatement
     if (!rc && vunsup) rc = fail_at(i, JE_UNSUP);
     *count = k;
-    if (!rc) r.ok = 1;
+    if (!rc) r.ok = 1;  // (r.sub on success: some element is not verbatim)
     return r;
   }
 
@@ -1140,8 +1443,10 @@ struct JsonDev {
             break;
           }
           const uint32_t b = i;
-          if (kind == JU_FLOAT) {  // visit_f64: Rust float Display, outside the restatement
-            rc = fail_at(i, JE_UNSUP);
+          if (kind == JU_FLOAT) {  // visit_f64: the u32 visitor's default, invalid_type(Unexpected::Float)
+            custom(JE_INVALID_TYPE, a, b, (uint8_t)(JU_FLOAT | (JX_U32 << 4)));
+            fix_position();
+            rc = -1;
             break;
           }
           uint64_t mag = 0;
@@ -1182,8 +1487,9 @@ struct JsonDev {
   // unpinned): from_slice::<Map<String, Value>> (de.rs deserialize_map /
   // MapAccess), the last member whose key equals `field`.  *ps / *pl = its
   // value's span, *found, *verb = the span is already serde_json::to_string's
-  // text (else the projection is JE_UNSUP).  Keys with escapes, floats and
-  // unsorted objects inside the projected value are JE_UNSUP.
+  // text (else the projection is JE_UNSUP: the output is a span of the input).
+  // Keys with escapes, floats and unsorted objects inside the projected value
+  // are JE_UNSUP.
   __device__ __forceinline__ JRes run_project(const uint8_t* field, uint32_t fl, uint32_t* ps, uint32_t* pl,
                                               bool* found) {
     r = JRes{0, 0, 0, 0, 0, 0, 0};
@@ -1253,6 +1559,7 @@ struct JsonDev {
         }
         const bool un0 = vunsup;
         vunsup = false;
+        vcomplex = false;
         vcanon = 0;
         vhas_u = false;
         ws();
@@ -1266,7 +1573,7 @@ struct JsonDev {
           *ps = e0;
           *pl = i - e0;
           fverb = i - e0 == vcanon && !vhas_u;
-          funsup = vunsup;
+          funsup = vunsup || vcomplex;  // a projection is a span of its source: no generated text
         }
         vunsup = un0 || maybe;
       }

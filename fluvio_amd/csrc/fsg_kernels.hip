@@ -856,6 +856,7 @@ __device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int 
               }
             } else {
               L.r_ival[r] = (int32_t)ne;  // element count
+              if (jr.sub) L.bs.pad = 1u;  // non-verbatim elements (same value from every lane)
             }
             break;
           }
@@ -1029,6 +1030,7 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
     L.bs.err_aux = 0;
     L.bs.err_aux2 = 0;
     L.bs.err_aux3 = 0;
+    L.bs.pad = 0;  // set: array elements for k_canon_len / k_write_canon
   }
   const uint64_t sec0 = pos + 57;
   const uint64_t sec_end = pos + 12 + (uint64_t)(uint32_t)batch_len;  // framing validated at ingest
@@ -1279,7 +1281,6 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
     const bool agg_ran = !passthru && (err_stage == 0xFFFFFFFFu || err_stage + 1 == ch.nstages);
     st.agg_sum = (ch.has_agg && agg_ran) ? aggsum : 0;
     st.nout = nout;
-    st.pad = 0;
     st.cat_sum = (ch.has_agg && agg_ran) ? catsum : 0;
     a.bstat[b] = st;  // the cross-batch minima are reduced by k_mins
   }
@@ -2787,101 +2788,6 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t x, uint32_t lane) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// serde_json::to_string of a validated JSON value whose objects are already in
-// key order (checked by json_array_explode): drop whitespace outside strings,
-// re-escape strings (ser.rs format_escaped_str: \" \\ \b \t \n \f \r, other
-// control bytes \u00xx, everything else raw).  One lane, rare path (elements
-// whose canonical bytes differ from their source bytes).
-__device__ void json_canon_write(const uint8_t* __restrict__ s, uint32_t n, bool upper, uint8_t* __restrict__ o) {
-  auto at = [&](uint32_t k) -> uint32_t {
-    uint8_t c = s[k];
-    if (upper && c >= 'a' && c <= 'z') c -= 32;
-    return c;
-  };
-  auto hexv = [](uint32_t c) -> uint32_t { return c <= '9' ? c - '0' : (c | 0x20) - 'a' + 10; };
-  auto put_esc = [&](uint32_t c) {  // one decoded byte c < 0x80
-    const char* hx = "0123456789abcdef";
-    switch (c) {
-      case '"': *o++ = '\\'; *o++ = '"'; return;
-      case '\\': *o++ = '\\'; *o++ = '\\'; return;
-      case 0x08: *o++ = '\\'; *o++ = 'b'; return;
-      case 0x09: *o++ = '\\'; *o++ = 't'; return;
-      case 0x0A: *o++ = '\\'; *o++ = 'n'; return;
-      case 0x0C: *o++ = '\\'; *o++ = 'f'; return;
-      case 0x0D: *o++ = '\\'; *o++ = 'r'; return;
-      default:
-        if (c < 0x20) {
-          *o++ = '\\'; *o++ = 'u'; *o++ = '0'; *o++ = '0';
-          *o++ = (uint8_t)hx[c >> 4];
-          *o++ = (uint8_t)hx[c & 15];
-        } else {
-          *o++ = (uint8_t)c;
-        }
-    }
-  };
-  uint32_t i = 0;
-  while (i < n) {
-    const uint32_t c = at(i);
-    if (c == ' ' || c == '\n' || c == '\t' || c == '\r') {
-      i++;
-      continue;
-    }
-    if (c != '"') {
-      *o++ = (uint8_t)c;
-      i++;
-      continue;
-    }
-    *o++ = '"';
-    i++;
-    for (;;) {
-      const uint32_t d = at(i++);
-      if (d == '"') {
-        *o++ = '"';
-        break;
-      }
-      if (d != '\\') {
-        if (d < 0x80) put_esc(d); else *o++ = (uint8_t)d;
-        continue;
-      }
-      const uint32_t e = at(i++);
-      uint32_t cp;
-      switch (e) {
-        case 'b': cp = 0x08; break;
-        case 'f': cp = 0x0C; break;
-        case 'n': cp = 0x0A; break;
-        case 'r': cp = 0x0D; break;
-        case 't': cp = 0x09; break;
-        case 'u': {
-          cp = (hexv(at(i)) << 12) | (hexv(at(i + 1)) << 8) | (hexv(at(i + 2)) << 4) | hexv(at(i + 3));
-          i += 4;
-          if (cp >= 0xD800 && cp <= 0xDBFF) {  // validated pair
-            const uint32_t c2 = (hexv(at(i + 2)) << 12) | (hexv(at(i + 3)) << 8) | (hexv(at(i + 4)) << 4) | hexv(at(i + 5));
-            i += 6;
-            cp = (((cp - 0xD800) << 10) | (c2 - 0xDC00)) + 0x10000;
-          }
-          break;
-        }
-        default: cp = e; break;  // " \ /
-      }
-      if (cp < 0x80) {
-        put_esc(cp);
-      } else if (cp < 0x800) {
-        *o++ = (uint8_t)(0xC0 | (cp >> 6));
-        *o++ = (uint8_t)(0x80 | (cp & 0x3F));
-      } else if (cp < 0x10000) {
-        *o++ = (uint8_t)(0xE0 | (cp >> 12));
-        *o++ = (uint8_t)(0x80 | ((cp >> 6) & 0x3F));
-        *o++ = (uint8_t)(0x80 | (cp & 0x3F));
-      } else {
-        *o++ = (uint8_t)(0xF0 | (cp >> 18));
-        *o++ = (uint8_t)(0x80 | ((cp >> 12) & 0x3F));
-        *o++ = (uint8_t)(0x80 | ((cp >> 6) & 0x3F));
-        *o++ = (uint8_t)(0x80 | (cp & 0x3F));
-      }
-    }
-  }
-}
-
 constexpr uint32_t kElemLaneCopy = 48;  // array elements up to this size are copied by their own lane
 
 // array_map batch (derive generator/array_map.rs:17-42): the elements of the
@@ -2889,6 +2795,7 @@ constexpr uint32_t kElemLaneCopy = 48;  // array elements up to this size are co
 // size, wave scan, record header (default preamble + offset fix-up), payload
 // (short verbatim elements by the lane, long ones by the whole wave, the rest
 // through the canonicalizer).
+template <bool kCanon>  // kCanon: only the payloads of non-verbatim elements (k_write_canon)
 __device__ void write_array_batch(const WriteArgs& a, const KeptRec* d, uint32_t nkeep, int64_t rel, uint64_t obase) {
   const uint32_t lane = lane_id();
   uint8_t* out = a.out;
@@ -2929,7 +2836,13 @@ __device__ void write_array_batch(const WriteArgs& a, const KeptRec* d, uint32_t
       const uint64_t incl = wave_incl_scan((uint64_t)sz);
       const uint64_t my = obase + run + incl - sz;
       bool wave_copy = false;
-      if (ev) {
+      if (kCanon) {
+        if (ev && !verb) {  // the payload after the header k_write wrote
+          uint8_t t[16];
+          const uint32_t hw = venc((int64_t)elem_inner(len, rel), t) + 2 + venc(rel, t) + 1 + venc((int64_t)len, t);
+          json_canon<const uint8_t*>(a.slice + er.pos, er.src_len, upper, out + my + hw);
+        }
+      } else if (ev) {
         uint8_t* q = out + my;
         uint8_t t[16];
         uint32_t w = 0;
@@ -2943,7 +2856,7 @@ __device__ void write_array_batch(const WriteArgs& a, const KeptRec* d, uint32_t
         nn = venc((int64_t)len, t);
         for (uint32_t i = 0; i < nn; i++) q[w++] = t[i];
         if (!verb) {
-          json_canon_write(a.slice + er.pos, er.src_len, upper, q + w);
+          // floats, key order, whitespace, escapes: the payload by k_write_canon
         } else if (len <= kElemLaneCopy) {
           const uint8_t* src = a.slice + er.pos;
           for (uint32_t i = 0; i < len; i++) q[w + i] = upper ? up(src[i]) : src[i];
@@ -2986,7 +2899,7 @@ __global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
                                : 61 + (a.pre[b].rec_bytes - a.pre[p.first].rec_bytes);
   uint8_t* out = a.out;
   if (st.nkeep && d[0].mode == KM_ARRAY) {  // a batch's descriptors share one mode
-    write_array_batch(a, d, st.nkeep, rel, obase);
+    write_array_batch<false>(a, d, st.nkeep, rel, obase);
     return;
   }
   uint64_t run = 0;
@@ -3051,6 +2964,48 @@ __global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
     }
     run += readlane_u64(incl, 63);
   }
+}
+
+// Array elements whose canonical text differs from their source text (floats,
+// keys out of BTreeMap order, whitespace, escapes): json_canon measures them
+// after k_eval (k_canon_len, before k_size) and writes them after k_write
+// (k_write_canon, the same position walk as k_write), only in the batches
+// k_eval flagged (BatchStat::pad).  One wave per batch.
+__global__ __launch_bounds__(256) void k_canon_len(SizeArgs a, const uint8_t* __restrict__ slice) {
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= a.nbatches) return;
+  const BatchStat& st = a.bstat[b];
+  if (!st.pad || !st.nkeep) return;
+  const KeptRec* d = a.desc + a.rbase[b];
+  if (d[0].mode != KM_ARRAY) return;
+  for (uint32_t k = lane_id(); k < st.nkeep; k += 64) {
+    const KeptRec r = d[k];
+    const bool up = (r.pad & KF_UPPER) != 0;
+    ElemRec* e = const_cast<ElemRec*>(a.elem) + (r.vpos >> 1);
+    for (int32_t j = 0; j < r.ival; j++) {
+      const ElemRec x = e[j];
+      if (!(x.out_len >> 31)) e[j].out_len = json_canon<const uint8_t*>(slice + x.pos, x.src_len, up, nullptr);
+    }
+  }
+}
+__global__ __launch_bounds__(kWriteThreads) void k_write_canon(WriteArgs a) {
+  const Plan p = *a.plan;
+  const int32_t b = p.first + (int32_t)(blockIdx.x * (kWriteThreads / 64) + (threadIdx.x >> 6));
+  if (p.first < 0 || b > p.last) return;
+  const BatchStat st = a.bstat[b];
+  if (!st.pad || !st.nkeep) return;
+  const KeptRec* d = a.desc + a.rbase[b];
+  if (d[0].mode != KM_ARRAY) return;
+  const int64_t rel = a.seg ? 0 : a.bstat[p.first].base_offset - st.base_offset;
+  const uint64_t obase = a.seg ? 61ull * (uint64_t)(b + 1) + a.pre[b].rec_bytes
+                               : 61 + (a.pre[b].rec_bytes - a.pre[p.first].rec_bytes);
+  write_array_batch<true>(a, d, st.nkeep, rel, obase);
+}
+void launch_canon_len(const SizeArgs& a, const uint8_t* slice, hipStream_t s) {
+  if (a.nbatches) hipLaunchKernelGGL(k_canon_len, dim3((a.nbatches + 3) / 4), dim3(256), 0, s, a, slice);
+}
+void launch_write_canon(const WriteArgs& a, uint32_t nblk, hipStream_t s) {
+  if (nblk) hipLaunchKernelGGL(k_write_canon, dim3((nblk + 3) / 4), dim3(kWriteThreads), 0, s, a);
 }
 
 // k_cat — aggregate (concat) accumulator stream: cat[kCatOff..] = initial

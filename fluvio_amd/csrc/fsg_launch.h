@@ -30,6 +30,10 @@ void launch_header(const Plan* plan, uint8_t* out, hipStream_t s);
 // a chain segment's output as the next segment's input slice (SegArgs)
 void launch_seg_headers(const SegArgs& a, hipStream_t s);
 void launch_write(const WriteArgs& a, uint32_t nblocks, hipStream_t s);
+// array elements whose canonical text differs from their source (json_canon):
+// lengths before k_size, payloads after k_write, in the batches k_eval flagged
+void launch_canon_len(const SizeArgs& a, const uint8_t* slice, hipStream_t s);
+void launch_write_canon(const WriteArgs& a, uint32_t nblk, hipStream_t s);
 void launch_cat(const WriteArgs& a, uint32_t nbatches, hipStream_t s);
 void launch_crc(uint8_t* out, uint64_t off, uint64_t n, uint32_t* acc, hipStream_t s);
 void launch_write_lean(const WriteArgs& a, uint32_t nblocks, hipStream_t s);

@@ -1366,6 +1366,8 @@ bool json_hint(uint32_t code_word, uint32_t pos, uint32_t a, uint32_t b, const s
     std::string val;
     json_unescape(v, a, b, val);
     msg = "unknown variant `" + val + "`, expected one of `debug`, `info`, `warn`, `error`";
+  } else if (code == JE_RANGE) {
+    msg = "number out of range";
   } else if (code == JE_INVALID_VALUE) {  // the u32 visitor (aggregate-json): visit_u64 / visit_i64 out of range
     msg = std::string("invalid value: integer `") + ((sub & 15) == JU_NINT ? "-" : "") +
           std::string(v.begin() + a, v.begin() + b) + "`, expected u32";
@@ -1398,7 +1400,18 @@ bool json_hint(uint32_t code_word, uint32_t pos, uint32_t a, uint32_t b, const s
       }
       case JU_SEQ: un = "sequence"; break;
       case JU_MAP: un = "map"; break;
-      default: return false;  // JU_FLOAT
+      case JU_FLOAT: {  // serde Unexpected::Float: Rust Display behind WithDecimalPoint
+        const bool neg = a > 0 && a <= v.size() && v[a - 1] == '-';
+        const uint32_t st = neg ? a - 1 : a;
+        auto acc = [&](uint32_t k) -> int { return k < b && k < v.size() ? v[k] : -1; };
+        const flt::NumVal nv = flt::num_value(acc, st, b);
+        if (nv.kind != 1) return false;
+        uint8_t txt[400];
+        const uint32_t tl = flt::display_with_point(nv.f, txt);
+        un = "floating point `" + std::string((const char*)txt, tl) + "`";
+        break;
+      }
+      default: return false;
     }
     msg = "invalid type: " + un + ", expected " + kExp[(sub >> 4) & 7];
   } else {
@@ -2016,6 +2029,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   sa.elem = ea.elem;
   sa.acc_len = has_cat ? c->acc.size() : 0;
   sa.seg = so ? 1u : 0u;
+  if (has_array) launch_canon_len(sa, ea.slice, st);
   if (has_agg) {
     sa.agg_only = 1;
     launch_size(sa, st);
@@ -2151,6 +2165,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     launch_write_lean(wa, nblk, st);
   else
     launch_write(wa, nblk, st);
+  if (has_array) launch_write_canon(wa, nblk, st);
   HIPCHK(hipGetLastError());
   if (c->timed) HIPCHK(hipEventRecord(c->ev[4], st));
   if (so) {  // the next segment's input: headers, positions, record-count prefix, pass-through flags

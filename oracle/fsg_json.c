@@ -24,13 +24,16 @@
  * messages: invalid type / invalid length / unknown variant / duplicate field /
  * missing field (serde/src/de/mod.rs).
  *
+ * Floats: serde_json's f64 reading (f64_from_parts, no float_roundtrip) and
+ * Rust's shortest Display behind serde's WithDecimalPoint for "invalid type:
+ * floating point `..`"; ryu's format for Value::to_string.
  * Outside the restatement (status ORC_E_UNSUPPORTED, mirrored by the GPU path):
- * an "invalid type: floating point `..`" message (needs serde_json's f64
- * parse + Rust's shortest float Display), "invalid type: string ..." for a
+ * "invalid type: string ..." for a
  * string holding a byte outside printable ASCII (Rust's str Debug escaping),
  * an ignored value nested more than 64 levels below its first bracket, and an
  * error text holding a NUL byte.
  */
+#include <math.h>
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -410,51 +413,112 @@ static int ignore_integer(jde *d) {
   return 0;
 }
 
-/* parse_integer / parse_number / parse_decimal / parse_exponent: the syntax and
- * the reader movement exactly; a value that is a float (or -0, or an integer
- * beyond u64/i64) marks the number as float (message outside the restatement) */
+/* parse_integer / parse_number / parse_long_integer / parse_decimal(_overflow) /
+ * parse_exponent(_overflow) / f64_from_parts (de.rs, the default build without
+ * the float_roundtrip feature): the syntax, the reader movement and the value.
+ * A u64 significand collects the digits (past u64 they only move the decimal
+ * exponent); the f64 is significand * or / POW10[|exponent|] (1e0 ..= 1e308),
+ * "number out of range" where that overflows. */
 typedef struct {
   int is_float;
   int neg;
   uint64_t mag;
+  double f; /* is_float */
 } jnum;
 
-static int parse_exponent_syn(jde *d) {
+#define E_RANGE "number out of range"
+static const double ORC_POW10[309] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11, 1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22, 1e23, 1e24, 1e25, 1e26, 1e27, 1e28, 1e29, 1e30, 1e31, 1e32, 1e33, 1e34, 1e35, 1e36, 1e37, 1e38, 1e39, 1e40, 1e41, 1e42, 1e43, 1e44, 1e45, 1e46, 1e47, 1e48, 1e49, 1e50, 1e51, 1e52, 1e53, 1e54, 1e55, 1e56, 1e57, 1e58, 1e59, 1e60, 1e61, 1e62, 1e63, 1e64, 1e65, 1e66, 1e67, 1e68, 1e69, 1e70, 1e71, 1e72, 1e73, 1e74, 1e75, 1e76, 1e77, 1e78, 1e79, 1e80, 1e81, 1e82, 1e83, 1e84, 1e85, 1e86, 1e87, 1e88, 1e89, 1e90, 1e91, 1e92, 1e93, 1e94, 1e95, 1e96, 1e97, 1e98, 1e99, 1e100, 1e101, 1e102, 1e103, 1e104, 1e105, 1e106, 1e107, 1e108, 1e109, 1e110, 1e111, 1e112, 1e113, 1e114, 1e115, 1e116, 1e117, 1e118, 1e119, 1e120, 1e121, 1e122, 1e123, 1e124, 1e125, 1e126, 1e127, 1e128, 1e129, 1e130, 1e131, 1e132, 1e133, 1e134, 1e135, 1e136, 1e137, 1e138, 1e139, 1e140, 1e141, 1e142, 1e143, 1e144, 1e145, 1e146, 1e147, 1e148, 1e149, 1e150, 1e151, 1e152, 1e153, 1e154, 1e155, 1e156, 1e157, 1e158, 1e159, 1e160, 1e161, 1e162, 1e163, 1e164, 1e165, 1e166, 1e167, 1e168, 1e169, 1e170, 1e171, 1e172, 1e173, 1e174, 1e175, 1e176, 1e177, 1e178, 1e179, 1e180, 1e181, 1e182, 1e183, 1e184, 1e185, 1e186, 1e187, 1e188, 1e189, 1e190, 1e191, 1e192, 1e193, 1e194, 1e195, 1e196, 1e197, 1e198, 1e199, 1e200, 1e201, 1e202, 1e203, 1e204, 1e205, 1e206, 1e207, 1e208, 1e209, 1e210, 1e211, 1e212, 1e213, 1e214, 1e215, 1e216, 1e217, 1e218, 1e219, 1e220, 1e221, 1e222, 1e223, 1e224, 1e225, 1e226, 1e227, 1e228, 1e229, 1e230, 1e231, 1e232, 1e233, 1e234, 1e235, 1e236, 1e237, 1e238, 1e239, 1e240, 1e241, 1e242, 1e243, 1e244, 1e245, 1e246, 1e247, 1e248, 1e249, 1e250, 1e251, 1e252, 1e253, 1e254, 1e255, 1e256, 1e257, 1e258, 1e259, 1e260, 1e261, 1e262, 1e263, 1e264, 1e265, 1e266, 1e267, 1e268, 1e269, 1e270, 1e271, 1e272, 1e273, 1e274, 1e275, 1e276, 1e277, 1e278, 1e279, 1e280, 1e281, 1e282, 1e283, 1e284, 1e285, 1e286, 1e287, 1e288, 1e289, 1e290, 1e291, 1e292, 1e293, 1e294, 1e295, 1e296, 1e297, 1e298, 1e299, 1e300, 1e301, 1e302, 1e303, 1e304, 1e305, 1e306, 1e307, 1e308};
+
+static int f64_from_parts(jde *d, int positive, uint64_t significand, int32_t exponent, jnum *o) {
+  double f = (double)significand;
+  for (;;) {
+    uint32_t ae = exponent < 0 ? 0u - (uint32_t)exponent : (uint32_t)exponent; /* wrapping_abs as usize */
+    if (exponent != INT32_MIN && ae <= 308) {
+      if (exponent >= 0) {
+        f *= ORC_POW10[ae];
+        if (isinf(f)) return jerror(d, E_RANGE);
+      } else {
+        f /= ORC_POW10[ae];
+      }
+      break;
+    }
+    if (f == 0.0) break;
+    if (exponent >= 0) return jerror(d, E_RANGE);
+    f /= 1e308;
+    exponent += 308;
+  }
+  o->is_float = 1;
+  o->f = positive ? f : -f;
+  return 0;
+}
+static int sig_overflows(uint64_t sig, uint64_t dg) { return sig > UINT64_MAX / 10 || (sig == UINT64_MAX / 10 && dg > UINT64_MAX % 10); }
+
+static int parse_exponent(jde *d, int positive, uint64_t significand, int32_t starting_exp, jnum *o) {
   jeat(d);
+  int positive_exp = 1;
   int c = peek_or_null(d);
-  if (c == '+' || c == '-') jeat(d);
+  if (c == '+') {
+    jeat(d);
+  } else if (c == '-') {
+    jeat(d);
+    positive_exp = 0;
+  }
   int nx = jnext(d);
   if (nx < 0) return jerror(d, E_EOF_VALUE);
   if (!isdig(nx)) return jerror(d, E_NUMBER);
-  while (isdig(peek_or_null(d))) jeat(d);
-  return 0;
-}
-static int parse_decimal_syn(jde *d) {
-  jeat(d);
-  int any = 0;
+  int32_t exp = nx - '0';
   while (isdig(peek_or_null(d))) {
-    jeat(d);
-    any = 1;
+    int dg = jnext(d) - '0';
+    if (exp > INT32_MAX / 10 || (exp == INT32_MAX / 10 && dg > INT32_MAX % 10)) {
+      /* parse_exponent_overflow: error instead of +/- infinity */
+      if (significand != 0 && positive_exp) return jerror(d, E_RANGE);
+      while (isdig(peek_or_null(d))) jeat(d);
+      o->is_float = 1;
+      o->f = positive ? 0.0 : -0.0;
+      return 0;
+    }
+    exp = exp * 10 + dg;
   }
-  if (!any) {
+  int64_t fe = positive_exp ? (int64_t)starting_exp + exp : (int64_t)starting_exp - exp; /* saturating */
+  if (fe > INT32_MAX) fe = INT32_MAX;
+  if (fe < INT32_MIN) fe = INT32_MIN;
+  return f64_from_parts(d, positive, significand, (int32_t)fe, o);
+}
+static int parse_decimal(jde *d, int positive, uint64_t significand, int32_t exponent_before, jnum *o) {
+  jeat(d);
+  int32_t after = 0;
+  int overflow = 0;
+  while (isdig(peek_or_null(d))) {
+    uint64_t dg = (uint64_t)(peek_or_null(d) - '0');
+    if (sig_overflows(significand, dg)) { /* parse_decimal_overflow: further digits ignored */
+      overflow = 1;
+      while (isdig(peek_or_null(d))) jeat(d);
+      break;
+    }
+    jeat(d);
+    significand = significand * 10 + dg;
+    after--;
+  }
+  if (!overflow && after == 0) {
     if (jpeek(d) >= 0) return jpeek_error(d, E_NUMBER);
     return jpeek_error(d, E_EOF_VALUE);
   }
   int c = peek_or_null(d);
-  if (c == 'e' || c == 'E') return parse_exponent_syn(d);
-  return 0;
+  if (c == 'e' || c == 'E') return parse_exponent(d, positive, significand, exponent_before + after, o);
+  return f64_from_parts(d, positive, significand, exponent_before + after, o);
 }
-static int parse_number_tail(jde *d, jnum *o) {
+static int parse_number_tail(jde *d, int positive, uint64_t significand, jnum *o) {
   int c = peek_or_null(d);
-  if (c == '.') {
-    o->is_float = 1;
-    return parse_decimal_syn(d);
+  if (c == '.') return parse_decimal(d, positive, significand, 0, o);
+  if (c == 'e' || c == 'E') return parse_exponent(d, positive, significand, 0, o);
+  o->mag = significand;
+  if (!positive) {
+    int64_t neg = (int64_t)(0 - significand); /* (significand as i64).wrapping_neg() */
+    if (neg >= 0) {                           /* -0 / below i64::MIN: -(significand as f64) */
+      o->is_float = 1;
+      o->f = -(double)significand;
+    }
   }
-  if (c == 'e' || c == 'E') {
-    o->is_float = 1;
-    return parse_exponent_syn(d);
-  }
-  if (o->neg && (o->mag == 0 || o->mag > (uint64_t)INT64_MAX + 1ull)) o->is_float = 1; /* -0 / underflow -> f64 */
   return 0;
 }
 static int parse_integer(jde *d, int positive, jnum *o) {
@@ -464,7 +528,7 @@ static int parse_integer(jde *d, int positive, jnum *o) {
   if (c < 0) return jerror(d, E_EOF_VALUE);
   if (c == '0') {
     if (isdig(peek_or_null(d))) return jpeek_error(d, E_NUMBER);
-    return parse_number_tail(d, o);
+    return parse_number_tail(d, positive, 0, o);
   }
   if (c >= '1' && c <= '9') {
     uint64_t sig = (uint64_t)(c - '0');
@@ -472,22 +536,184 @@ static int parse_integer(jde *d, int positive, jnum *o) {
       int p = peek_or_null(d);
       if (!isdig(p)) break;
       uint64_t dg = (uint64_t)(p - '0');
-      if (sig > (UINT64_MAX - dg) / 10) {
-        /* parse_long_integer: the rest of the digits, then . / e as a float */
-        o->is_float = 1;
-        while (isdig(peek_or_null(d))) jeat(d);
+      if (sig_overflows(sig, dg)) {
+        /* parse_long_integer: every further integer digit raises the exponent */
+        int32_t exponent = 0;
+        while (isdig(peek_or_null(d))) {
+          jeat(d);
+          exponent++;
+        }
         int q = peek_or_null(d);
-        if (q == '.') return parse_decimal_syn(d);
-        if (q == 'e' || q == 'E') return parse_exponent_syn(d);
-        return 0;
+        if (q == '.') return parse_decimal(d, positive, sig, exponent, o);
+        if (q == 'e' || q == 'E') return parse_exponent(d, positive, sig, exponent, o);
+        return f64_from_parts(d, positive, sig, exponent, o);
       }
       jeat(d);
       sig = sig * 10 + dg;
     }
-    o->mag = sig;
-    return parse_number_tail(d, o);
+    return parse_number_tail(d, positive, sig, o);
   }
   return jerror(d, E_NUMBER);
+}
+
+/* Shortest round-trip digits of |v| > 0, found independently of the product's
+ * bignum generator: for p = 1..17 the correctly rounded p-digit decimal
+ * (glibc printf, exact, ties to even) and its two p-digit neighbours, the
+ * first that reads back (glibc strtod, correctly rounded) as v.  Among valid
+ * p-digit candidates the rounded one is the closest; when v lies exactly
+ * halfway and both round-trip, ryu keeps the even digit and Rust's Display
+ * (flt2dec dragon format_shortest) rounds up.  dig[0..n), v ~ 0.dig x 10^k. */
+static int orc_shortest(double v, int tie_up, char *dig, int *k) {
+  v = fabs(v);
+  char buf[64];
+  for (int p = 1; p <= 17; p++) {
+    snprintf(buf, sizeof buf, "%.*e", p - 1, v);
+    char ds[24];
+    int nd = 0;
+    const char *q = buf;
+    for (; *q && *q != 'e'; q++)
+      if (*q >= '0' && *q <= '9') ds[nd++] = *q;
+    int e10 = atoi(q + 1);
+    /* candidates: the rounded value, one unit above, one unit below (same length) */
+    for (int cand = 0; cand < 3; cand++) {
+      char cd[24];
+      memcpy(cd, ds, (size_t)nd);
+      int ce = e10, cn = nd;
+      if (cand) {
+        int j = nd - 1;
+        if (cand == 1) {
+          while (j >= 0 && cd[j] == '9') cd[j--] = '0';
+          if (j < 0) { /* 99..9 + 1 = 100..0: one more digit position */
+            cd[0] = '1';
+            for (int t = 1; t < nd; t++) cd[t] = '0';
+            ce++;
+          } else {
+            cd[j]++;
+          }
+        } else {
+          while (j >= 0 && cd[j] == '0') cd[j--] = '9';
+          if (j < 0 || (j == 0 && cd[0] == '1' && nd == 1)) continue;
+          cd[j]--;
+          if (cd[0] == '0') continue; /* would drop a digit: a shorter length covers it */
+        }
+      }
+      char t[48];
+      snprintf(t, sizeof t, "%c.%.*se%d", cd[0], cn - 1, cd + 1, ce);
+      if (cn == 1) snprintf(t, sizeof t, "%ce%d", cd[0], ce);
+      if (strtod(t, NULL) != v) continue;
+      if (cand == 0 && tie_up) {
+        /* exactly halfway (the exact expansion continues 5000..): take the upper one if valid */
+        char ex[1200];
+        snprintf(ex, sizeof ex, "%.*e", 800, v);
+        char xd[900];
+        int xn = 0;
+        for (const char *r = ex; *r && *r != 'e'; r++)
+          if (*r >= '0' && *r <= '9') xd[xn++] = *r;
+        int xe = atoi(strchr(ex, 'e') + 1);
+        int tie = 0;
+        /* the digits of v past the first p (relative to the rounded candidate's exponent) */
+        int off = p + (xe - e10);
+        if (xe == e10 && off < xn && xd[off] == '5') {
+          tie = 1;
+          for (int r = off + 1; r < xn; r++)
+            if (xd[r] != '0') tie = 0;
+        }
+        if (tie && memcmp(xd, cd, (size_t)p) == 0) { /* the rounded one went down: try up */
+          char ud[24];
+          memcpy(ud, cd, (size_t)cn);
+          int j = cn - 1, ue = ce;
+          while (j >= 0 && ud[j] == '9') ud[j--] = '0';
+          if (j < 0) {
+            ud[0] = '1';
+            ue++;
+          } else {
+            ud[j]++;
+          }
+          char u[48];
+          if (cn == 1)
+            snprintf(u, sizeof u, "%ce%d", ud[0], ue);
+          else
+            snprintf(u, sizeof u, "%c.%.*se%d", ud[0], cn - 1, ud + 1, ue);
+          if (strtod(u, NULL) == v) {
+            memcpy(cd, ud, (size_t)cn);
+            ce = ue;
+          }
+        }
+      }
+      memcpy(dig, cd, (size_t)cn);
+      *k = ce + 1;
+      return cn;
+    }
+  }
+  return 0; /* unreachable: 17 digits always round-trip */
+}
+
+/* ryu 1.0.13 Buffer::format_finite (pretty/mod.rs format64) */
+static void orc_ryu(double v, jbuf *out) {
+  if (signbit(v)) jb_byte(out, '-');
+  if (v == 0.0) {
+    jb_push(out, (const uint8_t *)"0.0", 3);
+    return;
+  }
+  char dig[24];
+  int kk;
+  int len = orc_shortest(v, 0, dig, &kk);
+  int e = kk - len;
+  char t[64];
+  if (e >= 0 && kk <= 16) { /* 1234e7 -> 12340000000.0 */
+    jb_push(out, (const uint8_t *)dig, (size_t)len);
+    for (int j = len; j < kk; j++) jb_byte(out, '0');
+    jb_push(out, (const uint8_t *)".0", 2);
+  } else if (kk > 0 && kk <= 16) { /* 1234e-2 -> 12.34 */
+    jb_push(out, (const uint8_t *)dig, (size_t)kk);
+    jb_byte(out, '.');
+    jb_push(out, (const uint8_t *)dig + kk, (size_t)(len - kk));
+  } else if (kk > -5 && kk <= 0) { /* 1234e-6 -> 0.001234 */
+    jb_push(out, (const uint8_t *)"0.", 2);
+    for (int j = kk; j < 0; j++) jb_byte(out, '0');
+    jb_push(out, (const uint8_t *)dig, (size_t)len);
+  } else if (len == 1) { /* 1e30 */
+    int m = snprintf(t, sizeof t, "%ce%d", dig[0], kk - 1);
+    jb_push(out, (const uint8_t *)t, (size_t)m);
+  } else { /* 1234e30 -> 1.234e33 */
+    jb_byte(out, (uint8_t)dig[0]);
+    jb_byte(out, '.');
+    jb_push(out, (const uint8_t *)dig + 1, (size_t)(len - 1));
+    int m = snprintf(t, sizeof t, "e%d", kk - 1);
+    jb_push(out, (const uint8_t *)t, (size_t)m);
+  }
+}
+
+/* serde 1.0.160 Unexpected::Float: `{}` of WithDecimalPoint(f) — Rust's f64
+ * Display (shortest digits, no exponent, "-0" for negative zero), ".0" added
+ * when it printed no '.' */
+static void orc_display_point(double v, char *o, size_t cap) {
+  jbuf b = {0};
+  if (signbit(v)) jb_byte(&b, '-');
+  if (v == 0.0) {
+    jb_byte(&b, '0');
+  } else {
+    char dig[24];
+    int kk;
+    int len = orc_shortest(v, 1, dig, &kk);
+    if (kk <= 0) {
+      jb_push(&b, (const uint8_t *)"0.", 2);
+      for (int j = kk; j < 0; j++) jb_byte(&b, '0');
+      jb_push(&b, (const uint8_t *)dig, (size_t)len);
+    } else if (kk < len) {
+      jb_push(&b, (const uint8_t *)dig, (size_t)kk);
+      jb_byte(&b, '.');
+      jb_push(&b, (const uint8_t *)dig + kk, (size_t)(len - kk));
+    } else {
+      jb_push(&b, (const uint8_t *)dig, (size_t)len);
+      for (int j = len; j < kk; j++) jb_byte(&b, '0');
+    }
+  }
+  if (!memchr(b.b, '.', b.n)) jb_push(&b, (const uint8_t *)".0", 2);
+  size_t m = b.n < cap - 1 ? b.n : cap - 1;
+  memcpy(o, b.b, m);
+  o[m] = 0;
+  free(b.b);
 }
 
 /* Rust `{:?}` of a str, restricted to printable ASCII plus the escapes Rust
@@ -519,7 +745,7 @@ static int str_debug(jde *d, const jbuf *s, jbuf *out) {
 static int peek_invalid_type(jde *d, const char *expected) {
   int c = jpeek(d);
   if (c < 0) c = 0;
-  char unexp[64];
+  char unexp[400];
   jbuf dbg = {0};
   switch (c) {
     case 'n':
@@ -543,8 +769,11 @@ static int peek_invalid_type(jde *d, const char *expected) {
       if (!pos) jeat(d);
       jnum num;
       if (parse_integer(d, pos, &num)) return -1;
-      if (num.is_float) return junsupported(d);
-      if (num.neg)
+      if (num.is_float) {
+        char fl[360];
+        orc_display_point(num.f, fl, sizeof fl);
+        snprintf(unexp, sizeof unexp, "floating point `%s`", fl);
+      } else if (num.neg)
         snprintf(unexp, sizeof unexp, "integer `-%llu`", (unsigned long long)num.mag);
       else
         snprintf(unexp, sizeof unexp, "integer `%llu`", (unsigned long long)num.mag);
@@ -572,7 +801,7 @@ static int peek_invalid_type(jde *d, const char *expected) {
   }
   char tail[160];
   snprintf(tail, sizeof tail, ", expected %s", expected);
-  char head[96];
+  char head[440];
   snprintf(head, sizeof head, "invalid type: %s", unexp);
   jcustom_parts(d, head, dbg.b, dbg.n, tail);
   free(dbg.b);
@@ -1019,10 +1248,9 @@ int orc_json_structured_log(const uint8_t *s, size_t n, int *level, char **msg, 
 /* itoa, ryu, serde only): objects are BTreeMap<String, Value>, so       */
 /* to_string emits members sorted by key bytes, a repeated key keeps its */
 /* last value (Map::insert).  Value parse = Deserializer::deserialize_any */
-/* (de.rs), serialization = ser.rs format_escaped_str + itoa.  Floats    */
+/* (de.rs), serialization = ser.rs format_escaped_str + itoa; floats    */
 /* (and -0 / integers beyond u64/i64, which serde_json parses as f64)    */
-/* need ryu's shortest round-trip Display: ORC_E_UNSUPPORTED on both     */
-/* sides ("parity unpinned" beyond the restatement).                     */
+/* through ryu's shortest round-trip format (orc_ryu).                   */
 /* ------------------------------------------------------------------ */
 
 /* ser.rs format_escaped_str_contents: ESCAPE table — '"' '\\', the short
@@ -1203,7 +1431,10 @@ static int value_canon(jde *d, jbuf *out) {
       if (!pos) jeat(d);
       jnum num;
       if (parse_integer(d, pos, &num)) return -1;
-      if (num.is_float) return junsupported(d);
+      if (num.is_float) { /* ser.rs serialize_f64 -> ryu format_finite (a parsed f64 is finite) */
+        orc_ryu(num.f, out);
+        break;
+      }
       char t[32];
       int k = snprintf(t, sizeof t, "%s%llu", num.neg ? "-" : "", (unsigned long long)num.mag);
       jb_push(out, (const uint8_t *)t, (size_t)k);
@@ -1538,7 +1769,13 @@ static int deserialize_u32(jde *d, uint32_t *out) {
     if (!pos) jeat(d);
     jnum num;
     if (parse_integer(d, pos, &num)) return -1;
-    if (num.is_float) return junsupported(d); /* visit_f64: float Display outside the restatement */
+    if (num.is_float) { /* visit_f64: the u32 visitor's default, invalid_type(Unexpected::Float) */
+      char fl[360];
+      orc_display_point(num.f, fl, sizeof fl);
+      jcustom(d, "invalid type: floating point `%s`, expected u32", fl);
+      jfix_position(d);
+      return -1;
+    }
     if (num.neg || num.mag > 0xFFFFFFFFull) {
       if (num.neg)
         jcustom(d, "invalid value: integer `-%llu`, expected u32", (unsigned long long)num.mag);

@@ -171,7 +171,7 @@ def json_structured_log(value: bytes):
 
 def json_array_map(value: bytes):
     """array_map_json_array: ("ok", [canonical element bytes]) / ("err", Display text);
-    raises OracleError(-103) outside the restatement (floats)."""
+    raises OracleError(-103) outside the restatement."""
     el = ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8))()
     ln = ctypes.POINTER(ctypes.c_size_t)()
     cnt = ctypes.c_size_t()

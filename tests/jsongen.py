@@ -105,7 +105,10 @@ def am_value(rng, depth=0, sorted_keys=True, ints_only=True):
     if depth > 3 or r < 0.45:
         nums = [str(rng.randrange(-10**6, 10**6)), "0", "18446744073709551615", "-9223372036854775808"]
         if not ints_only:
-            nums += [f"{rng.randrange(1000)}.{rng.randrange(1000)}", "-0", "18446744073709551616", "1e3"]
+            nums += [f"{rng.randrange(1000)}.{rng.randrange(1000)}", "-0", "18446744073709551616", "1e3",
+                     f"{rng.randrange(-99, 99)}.{rng.randrange(10**6)}e{rng.randrange(-330, 310)}", "-2.5E-4",
+                     "1e308", "4.9e-324", "0.1", "-0.0", "123456789012345678901234.5e-10", "1e16", "0.00001",
+                     repr(rng.uniform(-1e6, 1e6)), "1e400" if rng.random() < 0.05 else "2.0"]
         return rng.choice([rand_str(rng), rand_str(rng, 3, False), rng.choice(nums), "true", "false", "null",
                            '"\\u001f\\u0001\\u007F"', '"caf\\u00e9 \\ud83d\\ude00"', '"\\/\\b"', '"ü\x7f"'])
     if r < 0.75:

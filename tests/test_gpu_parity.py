@@ -4,6 +4,7 @@ error records, metrics and aggregate state.
 
 Every test here needs an MI355X (marked gpu).
 """
+import random
 import struct
 
 import os
@@ -265,7 +266,7 @@ def test_array_lean_parity(engine, seed, odd):
     check_batch(engine, CHAINS["array_map"], sl)
     check_batch(engine, CHAINS["array_map"], sl, max_bytes=20000)
     g = gpu_chain(engine, CHAINS["array_map"])
-    if orc_chain(CHAINS["array_map"]).process_batch(sl)["status"] == 0:  # (floats / -0: both unsupported)
+    if orc_chain(CHAINS["array_map"]).process_batch(sl)["status"] == 0:
         g.process_batch(sl)
         t = g.last_timings()
         assert t["eval_path"] == 3, t  # FSG_EVAL_ARRAY
@@ -762,53 +763,12 @@ def test_aggregate_concat_max_bytes(engine, max_bytes):
     check_batch(engine, CONCAT_CHAINS["agg_concat"], synth.make_slice(3, 900), max_bytes, calls=2)
 
 
-def _needs_reorder(doc: bytes) -> bool:
-    """True if some object of a valid JSON doc is not already in BTreeMap order
-    (keys strictly increasing), or orders keys holding escapes, or nests deeper
-    than the 8 levels whose order the device checks: the GPU reports those as
-    unsupported (fsg_json_dev.h any_value)."""
-    i, n = 0, len(doc)
-    stack = []  # per open container: None ('[') or list of raw keys ('{')
-    expect_key = False
-    while i < n:
-        c = doc[i:i + 1]
-        if c == b'"':
-            j = i + 1
-            while doc[j:j + 1] != b'"':
-                j += 2 if doc[j:j + 1] == b"\\" else 1
-            if expect_key and stack and stack[-1] is not None:
-                stack[-1].append(doc[i + 1:j])
-            expect_key = False
-            i = j + 1
-            continue
-        if c == b"{":
-            stack.append([])
-            expect_key = True
-        elif c == b"[":
-            stack.append(None)
-        elif c in (b"}", b"]"):
-            keys = stack.pop()
-            if keys is not None and len(keys) > 1:
-                if len(stack) > 8 or any(b"\\" in k for k in keys):
-                    return True
-                if any(keys[k] >= keys[k + 1] for k in range(len(keys) - 1)):
-                    return True
-        elif c == b",":
-            expect_key = bool(stack) and stack[-1] is not None
-        i += 1
-    return False
-
-
 def _check_array_doc(engine, doc):
     sl = _one_record_slice(doc, base=3)
     try:
         check_batch(engine, CHAINS["array_map"], sl)
     except AssertionError as e:
-        o = orc_chain(CHAINS["array_map"]).process_batch(sl)
-        if o["status"] != 0 or o["error"] is not None or not _needs_reorder(doc):
-            raise AssertionError(f"doc {doc!r}: {e}") from e
-        with pytest.raises(Unsupported):
-            gpu_chain(engine, CHAINS["array_map"]).process_batch(sl)
+        raise AssertionError(f"doc {doc!r}: {e}") from e
 
 
 def test_array_map_fuzz_one_record(engine):
@@ -817,8 +777,39 @@ def test_array_map_fuzz_one_record(engine):
     from tests import jsongen
     docs = jsongen.ARRAY_FIXED + jsongen.array_corpus(3, 250, 350)
     docs += jsongen.array_corpus(4, 60, 0, sorted_keys=False) + jsongen.array_corpus(6, 60, 0, ints_only=False)
+    docs += jsongen.array_corpus(8, 80, 40, sorted_keys=False, ints_only=False)
     for doc in docs:
         _check_array_doc(engine, doc)
+
+
+def _json_batches_slice(seed, nbatch=40, per=30):
+    """Many batches of array documents with floats, keys out of order, whitespace
+    and escapes (elements measured and written by k_canon_len / k_write_canon)
+    mixed with batches of verbatim integer arrays."""
+    from tests import jsongen
+    rng = random.Random(seed)
+    out = b""
+    off = 0
+    for k in range(nbatch):
+        b = P.Batch(base_offset=off)
+        for _ in range(per):
+            if k % 3 == 0:
+                doc = "[" + ",".join(str(rng.randrange(-999, 999)) for _ in range(rng.randrange(6))) + "]"
+            else:
+                doc = jsongen.array_doc(rng, sorted_keys=rng.random() < 0.5, ints_only=False)
+            b.add_record(P.Record.new(doc.encode()))
+        out += b.encode()
+        off += per
+    return out
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_array_map_canonical_batches(engine, seed):
+    sl = _json_batches_slice(seed)
+    check_batch(engine, CHAINS["array_map"], sl)
+    check_batch(engine, CHAINS["array_map"], sl, max_bytes=30000)
+    check_batch(engine, [("array_map_json_array", {}, None), ("filter_with_param", {"key": "."}, None)], sl)
+    check_batch(engine, [("map", {}, None), ("array_map_json_array", {}, None)], sl)
 
 
 def test_array_map_first_error_in_stream(engine):
