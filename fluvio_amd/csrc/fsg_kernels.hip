@@ -1540,20 +1540,30 @@ __device__ __forceinline__ uint32_t lean_scan(LeanLds& L, int nr, uint32_t lo, u
 // filter_regex with a <= 16-state ASCII DFA, smartmodule/regex-filter/src/lib.rs:
 // 24-28): the range is cut into one piece per thread; a thread runs the DFA
 // over its piece plus max_len - 1 bytes of overlap, so every match starting
-// in the piece ends inside the scan.  The DFA is register resident: the
-// state is 4 bits, one LDS read of tt[byte] gives the byte's whole row.
+// in the piece ends inside the scan.  Table-driven: the state is 4 bits, one
+// LDS read of tt[byte] gives the byte's whole row; FSG_RX_STEP bytes a step, their
+// row reads issued before the state chain consumes them (a byte at a time,
+// each read waited for at once: C1 eval 2.30 -> 1.36 ms at 8 bytes, 1.53 at 16
+// (128-VGPR cap of the lean kernel), 2.55 with two interleaved chains (spills)).
 // A value piece starts in s_bot at the value start and in s_mid elsewhere
 // (unanchored restart); accept bit0 is sticky (the DFA stays in an accepting
 // state), bit1 is checked where a value ends (`$`).  Returns the OR of every
 // scanned byte (bit 7 set <=> a non-ASCII value byte).
+#ifndef FSG_RX_STEP
+#define FSG_RX_STEP 8
+#endif
 __device__ __forceinline__ uint32_t lean_regex(LeanLds& L, int nr, uint32_t lo, uint32_t hi, uint32_t mlen,
                                                uint32_t s_bot, uint32_t s_mid, uint32_t acc1, uint32_t acc2) {
+  constexpr uint32_t kStep = FSG_RX_STEP;
   const uint32_t l = threadIdx.x;
-  const uint32_t q_len = (hi - lo + kLeanThreads - 1) / kLeanThreads;
+  // piece length: a multiple of 4 whose dword count is odd, so the lanes' window
+  // reads (ds_read_b32: bank (a/4) mod 32 per 32-lane group) fall on distinct banks
+  uint32_t q_len = ((hi - lo + kLeanThreads - 1) / kLeanThreads + 3u) & ~3u;
+  if (!((q_len >> 2) & 1u)) q_len += 4u;
   const uint32_t p0 = lo + l * q_len;
   uint32_t orw = 0;
   uint64_t mask = 0;
-  if (q_len && p0 < hi) {
+  if (p0 < hi) {
     const uint32_t p1 = p0 + q_len < hi ? p0 + q_len : hi;
     const uint32_t pe = p1 + mlen - (mlen ? 1u : 0u);
     const uint32_t pend = pe < hi ? pe : hi;
@@ -1566,6 +1576,20 @@ __device__ __forceinline__ uint32_t lean_regex(LeanLds& L, int nr, uint32_t lo, 
       if (q >= ve) continue;
       uint32_t st = q == vs ? s_bot : s_mid;
       const uint32_t end = ve < pend ? ve : pend;
+      while (q + kStep <= end) {
+        uint32_t w[kStep / 4];
+#pragma unroll
+        for (uint32_t j = 0; j < kStep / 4; j++) {
+          w[j] = lds_u32_at(L.win, q + 4u * j);
+          orw |= w[j];
+        }
+        uint64_t t[kStep];
+#pragma unroll
+        for (uint32_t k = 0; k < kStep; k++) t[k] = L.tt[(w[k >> 2] >> (8 * (k & 3))) & 0xFFu];
+#pragma unroll
+        for (uint32_t k = 0; k < kStep; k++) st = (uint32_t)(t[k] >> (4 * st)) & 15u;
+        q += kStep;
+      }
       while (q < end) {
         const uint32_t w = lds_u32_at(L.win, q);
         const uint32_t n = end - q < 4u ? end - q : 4u;
