@@ -1742,8 +1742,10 @@ __device__ bool lean_json_stage(LeanLdsJ& L, int nr, uint32_t& orpar, bool proj,
   const uint32_t c0 = L.r_vs[0] & ~15u, c1 = L.r_ve[nr - 1];
   const uint32_t nch = (c1 - c0 + 15) >> 4;
   if (nch > (uint32_t)kJsonChunks) return true;
-  // 1. masks; thread t owns the contiguous chunks [t*per, (t+1)*per)
-  const uint32_t per = (nch + kLeanThreads - 1) / kLeanThreads;
+  // 1. masks; thread t owns the contiguous chunks [t*per, (t+1)*per), per odd:
+  //    the lanes' jm[] dwords and 16-byte window reads then fall on distinct
+  //    banks (an even per put 4-8 lanes of a group on one bank)
+  const uint32_t per = ((nch + kLeanThreads - 1) / kLeanThreads) | 1u;
   const uint32_t k0 = l * per, k1 = k0 + per < nch ? k0 + per : nch;
   uint32_t par = 0;
   for (uint32_t k = k0; k < k1; k++) {  // byte classes, once: quote, special (< 0x20 incl. 0, '\\', >= 0x80), non-space

@@ -10,6 +10,9 @@ from fluvio_amd.smartengine import (ResidentSlice, SmartEngine, SmartModuleChain
 
 kind, nrec = int(sys.argv[1]), int(sys.argv[2])
 chains = {
+    "json": [("filter_json", {})],
+    "c3": [("filter_init", {"key": "timeout"}), ("map_json_project", {"field": "message"}), ("map", {})],
+} if kind == 2 else {
     "regex_ssn": [("regex-filter", {"regex": r"\d{3}-\d{2}-\d{4}"})],
     "regex_lit": [("regex-filter", {"regex": "zqzq"})],
     "regex_cls": [("regex-filter", {"regex": r"[0-9]-[0-9]"})],
