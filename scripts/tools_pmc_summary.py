@@ -3,7 +3,7 @@ import collections, csv, glob, sys
 for f in sorted(glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True)):
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(f)):
-        agg[r["Kernel_Name"].split("(")[0][:34]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        agg[r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:34]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     print(f)
     for k, d in agg.items():
         if "rocclr" in k:
@@ -16,4 +16,4 @@ for f in sorted(glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True)
     print(f)
     for r in csv.DictReader(open(f)):
         if "rocclr" not in r["Name"]:
-            print(f"  {r['Name'].split('(')[0][:34]:36s} calls={r['Calls']} avg_us={float(r['AverageNs'])/1000:.1f}")
+            print(f"  {r['Name'].replace('(anonymous namespace)::', '').split('(')[0][:34]:36s} calls={r['Calls']} avg_us={float(r['AverageNs'])/1000:.1f}")

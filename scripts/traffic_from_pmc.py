@@ -24,7 +24,7 @@ def per_kernel(d, counter):
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] == counter:
-                name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+                name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
                 vals[name].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
