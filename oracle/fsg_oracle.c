@@ -497,7 +497,6 @@ static const cprange SPACE_ASCII[] = {{'\t', '\r'}, {' ', ' '}}; /* (?-u)\s */
 typedef struct {
   cprange *r;
   size_t n, cap;
-  int unicode_word; /* \w / \W used: exact only on ASCII input */
 } cset;
 
 static void cs_add(cset *s, uint32_t lo, uint32_t hi) {
@@ -528,7 +527,6 @@ static void cs_norm(cset *s) {
 static void cs_negate(cset *s) {
   cs_norm(s);
   cset o = {0};
-  o.unicode_word = s->unicode_word;
   uint32_t next = 0;
   for (size_t i = 0; i < s->n; i++) {
     if (s->r[i].lo > next) cs_add(&o, next, s->r[i].lo - 1);
@@ -571,7 +569,7 @@ typedef struct {
   size_t n, cap;
   cset *classes;
   size_t ncls, ccap;
-  int unicode_word;
+  int unicode_word; /* \b / \B used: Unicode word boundaries, exact only on ASCII input */
 } rxprog;
 
 /* AST */
@@ -887,7 +885,6 @@ static anode *rx_parse_class(rxparser *P) {
       int k = rx_escape(P, &lo, &tmp, 1);
       if (k == 2) {
         for (size_t j = 0; j < tmp.n; j++) cs_add(&a->cls, tmp.r[j].lo, tmp.r[j].hi);
-        if (tmp.unicode_word) a->cls.unicode_word = 1;
         free(tmp.r);
         continue;
       }
@@ -1202,8 +1199,6 @@ static int rx_addcls(rxprog *g, const cset *s) {
   }
   cset c = {0};
   for (size_t i = 0; i < s->n; i++) cs_add(&c, s->r[i].lo, s->r[i].hi);
-  c.unicode_word = s->unicode_word;
-  if (s->unicode_word) g->unicode_word = 1;
   g->classes[g->ncls] = c;
   return (int)g->ncls++;
 }
