@@ -316,7 +316,7 @@ constexpr uint64_t kCatOff = 64;  // the concat stream starts this far into its 
 
 // aggregate-json (k_aggj_*): the folded records in stream order (records of
 // batches up to the first error batch), their entries, the key dictionary
-// (insertion order = id order) with an open-addressing index in HBM, and the
+// (ids by first occurrence) with an open-addressing index in HBM, and the
 // per-block state table (the map's values at every block's first record).
 // Keys point at their bytes: the slice for keys met in records, the uploaded
 // initial accumulator otherwise.
@@ -364,10 +364,32 @@ struct AggjArgs {
   uint32_t rb;
   uint32_t nblk;
   uint32_t* state;
-  unsigned long long* scal;  // [0] entries [1] records [2] new keys [3] text bytes
+  unsigned long long* scal;  // [0] entries [1] records [2] new keys [3] text bytes [4] [5] scan totals
+                             // [6] Σ keys over the records' maps (ord slots) [7] most entries of a record
   uint64_t* acc_off;       // per batch: the accumulator text after it (offset in cat) ...
   uint32_t* acc_len;       // ... and its length (0xFFFFFFFF: no record aggregated yet)
+  // the output key order (fsg_keyed.hip k_aggj_hash / k_aggj_order): record
+  // i's map is the guest's HashMap<String, u32> built from record i - 1's
+  // output text under RandomState k0 = k0_base + 2 i, plus the record's own
+  // map (k0 + 1) added in that map's bucket order; its text lists the keys in
+  // bucket order
+  uint32_t* nkr;           // per folded record: keys in the map after it
+  uint64_t* koff;          // ... exclusive prefix: the record's slots in `ord`
+  uint32_t* ord;           // per record, by key id: hash under its accumulator map's keys; then, by
+                           //   position: the key ids in output order (k_aggj_order writes in place)
+  uint32_t* hrec;          // per entry: its key's hash under the record map's keys
+  uint64_t k0_base;        // RandomState k0 of the first folded record's accumulator map
+  const uint32_t* iseq;    // record 0's accumulator keys in text order, kAjDup on a repeated key;
+  uint32_t n_iseq;         //   nullptr: the ids 0 .. n_init - 1
+  uint32_t agg_stage;      // the aggregate's stage index in this chain (its error draws a RandomState)
+  uint32_t in_i32;         // the stage reads an i32 view (never '{')
+  uint32_t* oscr;          // k_aggj_order: tables of maps past the register path (4 x obmax buckets)
+  uint32_t obmax;          // ... buckets per table (a power of two), 0: none
 };
+constexpr uint32_t kAjRegKeys = 55;  // k_aggj_order's register path: <= 55 keys / entries keep a map
+                                     // within 64 buckets (capacity 56: no reserve grows past it)
+constexpr uint32_t kAjDup = 0x80000000u;  // AggjArgs::iseq: the key appeared earlier in the text
+constexpr uint32_t kAjLdsBuckets = 2048;  // the general path's tables in LDS up to this many buckets
 // device framing of a stored slice (FileBatchIterator, iterators.rs:55-160):
 // every position whose magic byte (offset 16) is 2 is a candidate batch start;
 // each candidate's successor (pos + 57 + batch_len - 45) is found among the
@@ -461,7 +483,7 @@ constexpr uint32_t kAjLds = 4096;  // k_aggj_text keeps up to this many values i
 // aggregate-json state kept in HBM between calls (fsg_keyed.hip k_ajc_*): after
 // a call, the map as it stands after the last record folded through the stop
 // batch (process_batch's last processed batch) is rewritten into the chain's
-// other state buffer: per key id (insertion order) its match bytes and its
+// other state buffer: per key, in the order the last record's text lists them, its match bytes and its
 // serialized text in one arena, and its u32 value.  The next call reads it as
 // its initial keys, so no accumulator text crosses PCIe and nothing is parsed
 // on the host after the first call.
@@ -479,8 +501,10 @@ struct AjCommitArgs {
   AggjArgs a;            // this call's dictionary, records, entries
   int32_t stop;          // the last processed batch (plan.stop, >= 0)
   uint32_t kmax;         // key ids of this call (n_init + new keys): the grid bound
-  AjState dst;
+  AjState dst;           // keys in the output order of the last folded record (= its text's order)
+  uint32_t* inv;         // scratch: key id -> position in dst
   unsigned long long* out;  // [0] keys after the stop batch [1] records folded through it [2] arena bytes
+                            // [3] the stop batch ends at an aggregate error [4] ... whose value starts with '{'
 };
 
 // Topic-wide keyed totals (fsg_keyed_*, C5 keyed): a rank-local table of exact

@@ -3074,9 +3074,9 @@ __global__ __launch_bounds__(256) void k_cat(WriteArgs a, uint32_t nbatches) {
 // aggregate-json (smartmodule/examples/aggregate-json/src/lib.rs:22-36): per
 // record, `accumulated + new` (`entry().and_modify(+=).or_insert()`, u32
 // wrapping as in the release wasm) and the record's value = serde_json::
-// to_vec_pretty of the whole map.  HashMap's iteration order is random per
-// process; the device (and the oracle) use insertion order: the accumulator's
-// keys, then new keys in the order a record first names them.
+// to_vec_pretty of the whole map, its keys in the guest HashMap's bucket order
+// (deterministic on the wasm32 target: fsg_keyed.hip k_aggj_order).  Key ids
+// below are by first occurrence; the text pass lists them in that order.
 //
 // The fold is sequential in the reference; here it is data-parallel:
 //   1. k_aggj_bcount / scan / k_aggj_flat: the folded records in stream order
@@ -3091,7 +3091,8 @@ __global__ __launch_bounds__(256) void k_cat(WriteArgs a, uint32_t nbatches) {
 //      key, then per key an exclusive scan over blocks: the map's values at
 //      every block's first record
 //   5. k_aggj_text: one wave per block replays its records from that row
-//      (values in LDS), sizing (pass 0) or writing (pass 1) each record's text
+//      (values in LDS), sizing (pass 0; the length does not depend on the key
+//      order) or writing (pass 1, keys in k_aggj_order's order) each record's text
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t dec_digits_u32(uint32_t v) {
   uint32_t n = 1;
@@ -3181,19 +3182,24 @@ __device__ __forceinline__ uint32_t aggj_last(const AggjArgs& a) {
 // per batch: folded records and their entries (scal[1], scal[0])
 __global__ __launch_bounds__(256) void k_aggj_bcount(AggjArgs a) {
   const uint32_t last = aggj_last(a);
-  unsigned long long recs = 0, ents = 0;
+  unsigned long long recs = 0, ents = 0, most = 0;
   for (uint32_t b = blockIdx.x * 256 + threadIdx.x; b < a.nbatches; b += gridDim.x * 256) {
     const BatchStat st = a.bstat[b];
     const uint32_t n = (b <= last && !(st.flags & BF_DECODE)) ? st.nkeep : 0u;
     a.bcnt[b] = n;
     const KeptRec* d = a.desc + a.rbase[b];
-    for (uint32_t k = 0; k < n; k++) ents += (uint32_t)d[k].ival;
+    for (uint32_t k = 0; k < n; k++) {
+      const uint32_t e = (uint32_t)d[k].ival;
+      ents += e;
+      most = e > most ? e : most;
+    }
     recs += n;
   }
   recs = wave_sum(recs);
   ents = wave_sum(ents);
   if (lane_id() == 0 && recs) atomicAdd(&a.scal[1], recs);
   if (lane_id() == 0 && ents) atomicAdd(&a.scal[0], ents);
+  if (most) atomicMax(&a.scal[7], most);  // the most entries of one record (k_aggj_order's table sizes)
 }
 // one wave per batch: the stream's record table
 __global__ __launch_bounds__(256) void k_aggj_flat(AggjArgs a) {
@@ -3396,14 +3402,16 @@ __global__ __launch_bounds__(64) void k_aggj_text(AggjArgs a) {
       if (nk) o[len - 2] = '\n';
     }
     uint64_t q0 = 1;
+    const uint32_t* order = a.ord + a.koff[r];  // the keys in the guest HashMap's bucket order (k_aggj_order)
     for (uint32_t c0 = 0; c0 < nk; c0 += 64) {
-      const uint32_t k = c0 + l;
-      uint32_t v = k < nk ? vget(k) : 0u, tl = k < nk ? a.tlen[k] : 0u;
-      const uint32_t t = k < nk ? aggj_term(k, tl, v) : 0u;
+      const uint32_t p = c0 + l;
+      const uint32_t k = p < nk ? order[p] : 0u;
+      uint32_t v = p < nk ? vget(k) : 0u, tl = p < nk ? a.tlen[k] : 0u;
+      const uint32_t t = p < nk ? aggj_term(p, tl, v) : 0u;
       const uint32_t inc = wave_incl_scan(t);
-      if (k < nk) {
+      if (p < nk) {
         uint64_t q = q0 + inc - t;
-        if (k) o[q++] = ',';
+        if (p) o[q++] = ',';
         o[q++] = '\n';
         o[q++] = ' ';
         o[q++] = ' ';

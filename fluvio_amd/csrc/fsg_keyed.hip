@@ -27,48 +27,342 @@ __device__ __forceinline__ uint32_t grid_tid() { return blockIdx.x * blockDim.x 
 __device__ __forceinline__ uint32_t grid_n() { return gridDim.x * blockDim.x; }
 
 // ---------------------------------------------------------------------------
-// 1. aggregate-json commit
+// 0. aggregate-json output order.  The guest (examples/aggregate-json/src/
+//    lib.rs:22-36, Rust 1.75 for wasm32-unknown-unknown) builds every map as
+//    std's HashMap<String, u32>; its text lists the keys in the table's bucket
+//    order, which is deterministic on that target (AggjArgs; oracle/
+//    fsg_oracle.c hb_* restates it over control bytes):
+//    - RandomState::new() draws k0 = 1, 2, 3, ... (hashmap_random_keys() is the
+//      constant (1, 2) there; k1 stays 2): two maps per record;
+//    - SipHash-1-3 of the key's bytes and 0xFF; h1 = its low 32 bits;
+//    - hashbrown 0.14 with generic 8-byte control groups: the first free bucket
+//      of the 8-bucket window at the probe position (circular through the
+//      mirrored trailing group), triangular probing by 8; a 4-bucket table
+//      scans its own buckets circularly (the EMPTY padding then
+//      fix_insert_slot's rescan from bucket 0); growth 0 -> 4 -> 8 -> 2x when
+//      a reserve finds no room (HashMap::insert reserves before its lookup, the
+//      entry API only for a vacant key); resize re-inserts in bucket order.
+//    k_aggj_hash: every record's key hashes, data-parallel.  k_aggj_order: one
+//    wave per chain walks its records in stream order (record i's accumulator
+//    map is built from record i - 1's order), maps of <= kAjRegKeys keys as
+//    wave-uniform tables (occupancy in a 64-bit scalar mask, bucket s's key in
+//    lane s of a VGPR, hashes by key id in lanes), larger ones in LDS / HBM
+//    tables walked by lane 0.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int b) { return (x << b) | (x >> (64 - b)); }
+__device__ __forceinline__ void sip_round(uint64_t& v0, uint64_t& v1, uint64_t& v2, uint64_t& v3) {
+  v0 += v1;
+  v1 = rotl64(v1, 13) ^ v0;
+  v0 = rotl64(v0, 32);
+  v2 += v3;
+  v3 = rotl64(v3, 16) ^ v2;
+  v0 += v3;
+  v3 = rotl64(v3, 21) ^ v0;
+  v2 += v1;
+  v1 = rotl64(v1, 17) ^ v2;
+  v2 = rotl64(v2, 32);
+}
+// SipHash-1-3 under (k0, 2) of the key's bytes (ASCII-uppercased view when up)
+// followed by 0xFF: the low 32 bits
+__device__ uint32_t aj_sip13(uint64_t k0, const uint8_t* p, uint32_t n, bool up) {
+  constexpr uint64_t k1 = 2;
+  uint64_t v0 = k0 ^ 0x736f6d6570736575ull, v1 = k1 ^ 0x646f72616e646f6dull;
+  uint64_t v2 = k0 ^ 0x6c7967656e657261ull, v3 = k1 ^ 0x7465646279746573ull;
+  const uint32_t len = n + 1u;
+  uint64_t m = 0;
+  uint32_t fill = 0;
+  for (uint32_t i = 0; i < len; i++) {
+    const uint8_t c = i < n ? up_byte(p[i], up) : (uint8_t)0xFF;
+    m |= (uint64_t)c << (8u * fill);
+    if (++fill == 8u) {
+      v3 ^= m;
+      sip_round(v0, v1, v2, v3);
+      v0 ^= m;
+      m = 0;
+      fill = 0;
+    }
+  }
+  const uint64_t b = ((uint64_t)(len & 0xFFu) << 56) | m;
+  v3 ^= b;
+  sip_round(v0, v1, v2, v3);
+  v0 ^= b;
+  v2 ^= 0xFF;
+  sip_round(v0, v1, v2, v3);
+  sip_round(v0, v1, v2, v3);
+  sip_round(v0, v1, v2, v3);
+  return (uint32_t)(v0 ^ v1 ^ v2 ^ v3);
+}
+struct AjKeyRef {
+  const uint8_t* p;
+  uint32_t n;
+  bool up;
+};
+// key id k's bytes as the map holds them (initial keys decoded, new keys the
+// source span between the quotes, through the uppercase view)
+__device__ __forceinline__ AjKeyRef aj_key(const AggjArgs& a, uint32_t k) {
+  if (k < a.n_init) return {(const uint8_t*)a.kptr[k], a.klen[k], false};
+  return {(const uint8_t*)a.tptr[k] + 1, a.tlen[k] - 2u, a.kup[k] != 0};
+}
+__global__ __launch_bounds__(256) void k_aggj_nk(AggjArgs a) {
+  for (uint64_t r = grid_tid(); r < a.n_rec; r += grid_n()) a.nkr[r] = a.n_init + (uint32_t)(a.rnewb[r] + a.rnew[r]);
+}
+// one wave per record: its accumulator map's keys (ids < nk) under k0_base + 2 r,
+// its own entries under k0_base + 2 r + 1
+__global__ __launch_bounds__(256) void k_aggj_hash(AggjArgs a) {
+  const uint32_t l = threadIdx.x & 63u;
+  for (uint64_t r = grid_tid() >> 6; r < a.n_rec; r += grid_n() >> 6) {
+    const uint32_t nk = a.nkr[r];
+    const uint64_t ko = a.koff[r], k0 = a.k0_base + 2ull * r;
+    for (uint32_t k = l; k < nk; k += 64u) {
+      const AjKeyRef kr = aj_key(a, k);
+      a.ord[ko + k] = aj_sip13(k0, kr.p, kr.n, kr.up);
+    }
+    const uint32_t ne = a.rne[r];
+    const uint64_t g0 = a.rent[r];
+    for (uint32_t j = l; j < ne; j += 64u) {
+      const uint32_t kid = a.ekid[g0 + j];
+      if (kid == kSkipEntry) continue;
+      const AjKeyRef kr = aj_key(a, kid);
+      a.hrec[g0 + j] = aj_sip13(k0 + 1ull, kr.p, kr.n, kr.up);
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t hb_capacity(uint32_t B) { return B == 0 ? 0u : B <= 8u ? B - 1u : B / 8u * 7u; }
+// the register path: a table of at most 64 buckets, wave-uniform occupancy,
+// bucket s's payload in lane s of `pl`
+struct HbReg {
+  uint64_t occ;
+  uint32_t B, items, pl;
+};
+__device__ __forceinline__ uint64_t hb_rotr(uint64_t x, uint32_t p, uint32_t B) {
+  if (B == 64u) return p ? (x >> p) | (x << (64u - p)) : x;
+  return ((x >> p) | (x << (B - p))) & ((1ull << B) - 1ull);
+}
+__device__ __forceinline__ uint32_t hb_slot(uint64_t occ, uint32_t B, uint32_t h) {
+  const uint32_t mask = B - 1u, w = B < 8u ? B : 8u;
+  const uint64_t wm = (1ull << w) - 1ull;
+  uint32_t pos = h & mask, stride = 0;
+  for (;;) {
+    const uint64_t win = hb_rotr(occ, pos, B) & wm;
+    if (win != wm) return (pos + (uint32_t)__builtin_ctzll(~win)) & mask;
+    stride += 8u;
+    pos = (pos + stride) & mask;
+  }
+}
+__device__ __forceinline__ void hb_put(HbReg& t, uint32_t payload, uint32_t h) {
+  const uint32_t s = hb_slot(t.occ, t.B, h);
+  t.occ |= 1ull << s;
+  t.pl = (threadIdx.x & 63u) == s ? payload : t.pl;  // writelane
+  t.items++;
+}
+// reserve(1): no room -> capacity_to_buckets(capacity + 1) = 4, 8, 2B buckets,
+// the old buckets re-inserted in bucket order; hv: lane x = payload x's hash
+__device__ __forceinline__ void hb_reserve(HbReg& t, uint32_t hv) {
+  if (hb_capacity(t.B) != t.items) return;
+  HbReg n{0ull, t.B ? 2u * t.B : 4u, 0u, 0u};
+  for (uint64_t m = t.occ; m; m &= m - 1ull) {
+    const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)t.pl, (int)__builtin_ctzll(m));
+    hb_put(n, x, (uint32_t)__builtin_amdgcn_readlane((int)hv, (int)x));
+  }
+  t = n;
+}
+// the general path: a table in LDS or HBM (occupancy bits + payloads), lane 0
+struct HbMem {
+  uint32_t* occ;
+  uint32_t* pl;
+  uint32_t B, items;
+};
+__device__ __forceinline__ bool hbm_full(const HbMem& t, uint32_t i) { return (t.occ[i >> 5] >> (i & 31u)) & 1u; }
+__device__ void hbm_clear(HbMem& t, uint32_t B) {
+  t.B = B;
+  t.items = 0;
+  for (uint32_t w = 0; w < (B + 31u) / 32u; w++) t.occ[w] = 0;
+}
+__device__ void hbm_put(HbMem& t, uint32_t payload, uint32_t h) {
+  const uint32_t mask = t.B - 1u, w = t.B < 8u ? t.B : 8u;
+  uint32_t pos = h & mask, stride = 0, s = 0;
+  for (;;) {
+    uint32_t i = 0;
+    for (; i < w; i++)
+      if (!hbm_full(t, (pos + i) & mask)) break;
+    if (i < w) {
+      s = (pos + i) & mask;
+      break;
+    }
+    stride += 8u;
+    pos = (pos + stride) & mask;
+  }
+  t.occ[s >> 5] |= 1u << (s & 31u);
+  t.pl[s] = payload;
+  t.items++;
+}
+// hv[x] = payload x's hash
+__device__ void hbm_reserve(HbMem& t, HbMem& spare, const uint32_t* hv) {
+  if (hb_capacity(t.B) != t.items) return;
+  hbm_clear(spare, t.B ? 2u * t.B : 4u);
+  for (uint32_t i = 0; i < t.B; i++)
+    if (hbm_full(t, i)) hbm_put(spare, t.pl[i], hv[t.pl[i]]);
+  const HbMem o = t;
+  t = spare;
+  spare = o;
+}
+
+// one chain's records in stream order (one 64-lane workgroup)
+__device__ void aj_order_run(const AggjArgs& a, uint32_t* lds) {
+  const uint32_t l = threadIdx.x;
+  uint32_t seq = l;       // the previous record's order (lane p = key at position p) when in registers
+  bool seq_reg = true;    // ... else in ord at the previous record's slots
+  for (uint64_t r = 0; r < a.n_rec; r++) {
+    const uint32_t nk = a.nkr[r], ne = a.rne[r];
+    const uint32_t nkb = nk - a.rnew[r];  // keys of the accumulator map (the previous text's)
+    const uint64_t ko = a.koff[r], g0 = a.rent[r];
+    const bool first = r == 0;
+    const bool iseq = first && a.iseq != nullptr;
+    const uint32_t nseq = iseq ? a.n_iseq : nkb;
+    if (nk <= kAjRegKeys && ne <= kAjRegKeys && nseq <= kAjRegKeys) {
+      if (!seq_reg) {
+        __threadfence();  // lane 0 wrote the previous order
+        seq = l < nkb ? a.ord[a.koff[r - 1] + l] : 0u;
+      }
+      const uint32_t hk = l < nk ? a.ord[ko + l] : 0u;
+      const uint32_t ek = l < ne ? a.ekid[g0 + l] : kSkipEntry;
+      const uint32_t hr = l < ne ? a.hrec[g0 + l] : 0u;
+      const uint32_t is = iseq && l < nseq ? a.iseq[l] : 0u;
+      HbReg A{0ull, 0u, 0u, 0u};
+      for (uint32_t p = 0; p < nseq; p++) {  // the accumulator's text, HashMap::insert per entry
+        uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)(iseq ? is : seq), (int)p);
+        hb_reserve(A, hk);
+        if (k & kAjDup) continue;  // a repeated key: the value changes, the layout does not
+        hb_put(A, k, (uint32_t)__builtin_amdgcn_readlane((int)hk, (int)k));
+      }
+      HbReg R{0ull, 0u, 0u, 0u};
+      for (uint32_t j = 0; j < ne; j++) {  // the record's own map
+        hb_reserve(R, hr);
+        if ((uint32_t)__builtin_amdgcn_readlane((int)ek, (int)j) == kSkipEntry) continue;
+        hb_put(R, j, (uint32_t)__builtin_amdgcn_readlane((int)hr, (int)j));
+      }
+      for (uint64_t m = R.occ; m; m &= m - 1ull) {  // `for (repo, n) in next.0`: entry(repo) per vacant key
+        const uint32_t j = (uint32_t)__builtin_amdgcn_readlane((int)R.pl, (int)__builtin_ctzll(m));
+        const uint32_t kid = (uint32_t)__builtin_amdgcn_readlane((int)ek, (int)j);
+        if (kid < nkb) continue;
+        hb_reserve(A, hk);
+        hb_put(A, kid, (uint32_t)__builtin_amdgcn_readlane((int)hk, (int)kid));
+      }
+      const bool full = (A.occ >> l) & 1ull;
+      const uint32_t below = (uint32_t)__builtin_popcountll(A.occ & ((1ull << l) - 1ull));
+      const uint32_t pos = full ? below : nk + (l - below);
+      if (full) a.ord[ko + pos] = A.pl;
+      seq = (uint32_t)__builtin_amdgcn_ds_permute((int)(pos << 2), (int)A.pl);
+      seq_reg = true;
+      continue;
+    }
+    // a larger map: tables in LDS (kAjLdsBuckets) or the chain's HBM scratch, lane 0
+    if (l == 0) {
+      uint32_t* base = a.obmax <= kAjLdsBuckets ? lds : a.oscr;
+      const uint32_t bm = a.obmax <= kAjLdsBuckets ? kAjLdsBuckets : a.obmax, ow = (bm + 31u) / 32u;
+      HbMem T[4];
+      for (int q = 0; q < 4; q++) T[q] = HbMem{base + q * ow, base + 4u * ow + (uint64_t)q * bm, 0u, 0u};
+      const uint32_t* hk = a.ord + ko;  // by key id
+      const uint32_t* hr = a.hrec + g0;  // by entry
+      const uint32_t* prev = first ? nullptr : a.ord + a.koff[r - 1];
+      if (!first) __threadfence();  // the previous order, written by the whole wave
+      HbMem& A = T[0];
+      for (uint32_t p = 0; p < nseq; p++) {
+        const uint32_t k = iseq ? a.iseq[p] : first ? p : prev[p];
+        hbm_reserve(A, T[1], hk);
+        if (!(k & kAjDup)) hbm_put(A, k, hk[k]);
+      }
+      HbMem& R = T[2];
+      for (uint32_t j = 0; j < ne; j++) {
+        hbm_reserve(R, T[3], hr);
+        if (a.ekid[g0 + j] != kSkipEntry) hbm_put(R, j, hr[j]);
+      }
+      for (uint32_t i = 0; i < R.B; i++) {
+        if (!hbm_full(R, i)) continue;
+        const uint32_t kid = a.ekid[g0 + R.pl[i]];
+        if (kid < nkb) continue;
+        hbm_reserve(A, T[1], hk);
+        hbm_put(A, kid, hk[kid]);
+      }
+      // the hashes of this record are read: its order goes over them
+      uint32_t q = 0;
+      for (uint32_t i = 0; i < A.B; i++)
+        if (hbm_full(A, i)) a.ord[ko + q++] = A.pl[i];
+    }
+    seq_reg = false;
+  }
+}
+__global__ __launch_bounds__(64) void k_aggj_order(AggjArgs a) {
+  __shared__ uint32_t lds[4u * (kAjLdsBuckets + kAjLdsBuckets / 32u)];
+  aj_order_run(a, lds);
+}
+
+// ---------------------------------------------------------------------------
+// 1. aggregate-json commit: the map after the last record folded through the
+//    stop batch, keys in that record's output order (= the order its text
+//    lists them, which the next call's first record parses)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ const uint32_t* ajc_perm(const AjCommitArgs& c) {
+  const uint64_t n = c.out[1];
+  return n ? c.a.ord + c.a.koff[n - 1] : nullptr;
+}
 __global__ void k_ajc_head(AjCommitArgs c) {
   if (threadIdx.x || blockIdx.x) return;
   const AggjArgs& a = c.a;
   const uint64_t n = a.brec[c.stop] + a.bcnt[c.stop];  // records folded through the stop batch
-  uint32_t K = a.n_init;
-  if (n) K = a.n_init + (uint32_t)(a.rnewb[n - 1] + a.rnew[n - 1]);
-  c.out[0] = K;
+  c.out[0] = n ? a.nkr[n - 1] : a.n_init;
   c.out[1] = n;
+  // the stop batch ends at an aggregate-json error: that call drew its
+  // accumulator map and, when the value starts with '{', the record's map
+  const BatchStat& bs = a.bstat[c.stop];
+  const bool err = (bs.flags & BF_ERR) && bs.err_stage == a.agg_stage;
+  uint32_t brace = 0;
+  if (err && !a.in_i32) {
+    const uint8_t* v = a.slice + bs.err_vpos;
+    uint32_t i = 0;
+    while (i < bs.err_vlen && (v[i] == ' ' || v[i] == '\t' || v[i] == '\n' || v[i] == '\r')) i++;
+    brace = i < bs.err_vlen && v[i] == '{';
+  }
+  c.out[3] = err ? 1u : 0u;
+  c.out[4] = brace;
 }
 __global__ __launch_bounds__(256) void k_ajc_len(AjCommitArgs c) {
   const AggjArgs& a = c.a;
   const uint32_t K = (uint32_t)c.out[0];
-  for (uint32_t k = grid_tid(); k < c.kmax; k += grid_n()) {
-    if (k >= K) {
-      c.dst.blen[k] = 0;
+  const uint32_t* perm = ajc_perm(c);
+  for (uint32_t p = grid_tid(); p < c.kmax; p += grid_n()) {
+    if (p >= K) {
+      c.dst.blen[p] = 0;
       continue;
     }
+    const uint32_t k = perm ? perm[p] : p;
     const uint32_t tl = a.tlen[k];
     const uint32_t ml = k < a.n_init ? a.klen[k] : tl - 2u;  // a new key: its source bytes between the quotes
-    c.dst.blen[k] = ml + tl;
-    c.dst.val[k] = k < a.n_init ? a.val_init[k] : 0u;
+    c.dst.blen[p] = ml + tl;
+    c.dst.val[p] = k < a.n_init ? a.val_init[k] : 0u;
+    c.inv[k] = p;
   }
 }
 __global__ __launch_bounds__(256) void k_ajc_copy(AjCommitArgs c) {
   const AggjArgs& a = c.a;
   const uint32_t K = (uint32_t)c.out[0];
-  for (uint32_t k = grid_tid(); k < K; k += grid_n()) {
+  const uint32_t* perm = ajc_perm(c);
+  for (uint32_t p = grid_tid(); p < K; p += grid_n()) {
+    const uint32_t k = perm ? perm[p] : p;
     const bool init = k < a.n_init;
     const uint32_t tl = a.tlen[k];
     const uint8_t* t = (const uint8_t*)a.tptr[k];
     const uint8_t* m = init ? (const uint8_t*)a.kptr[k] : t + 1;
     const uint32_t ml = init ? a.klen[k] : tl - 2u;
     const bool up = !init && a.kup[k];  // committed keys are stored as the stage saw them
-    uint8_t* d = c.dst.arena + c.dst.boff[k];
+    uint8_t* d = c.dst.arena + c.dst.boff[p];
     for (uint32_t i = 0; i < ml; i++) d[i] = up_byte(m[i], up);
     for (uint32_t i = 0; i < tl; i++) d[ml + i] = up_byte(t[i], up);
-    c.dst.kptr[k] = (uint64_t)d;
-    c.dst.klen[k] = ml;
-    c.dst.tptr[k] = (uint64_t)(d + ml);
-    c.dst.tlen[k] = tl;
+    c.dst.kptr[p] = (uint64_t)d;
+    c.dst.klen[p] = ml;
+    c.dst.tptr[p] = (uint64_t)(d + ml);
+    c.dst.tlen[p] = tl;
   }
 }
 // the values: the initial ones plus every entry of the records folded through
@@ -81,7 +375,7 @@ __global__ __launch_bounds__(256) void k_ajc_vals(AjCommitArgs c) {
     const uint64_t g0 = a.rent[r];
     for (uint32_t j = 0; j < ne; j++) {
       const uint32_t k = a.ekid[g0 + j];
-      if (k != kSkipEntry) atomicAdd(&c.dst.val[k], a.eval[g0 + j]);
+      if (k != kSkipEntry) atomicAdd(&c.dst.val[c.inv[k]], a.eval[g0 + j]);
     }
   }
 }
@@ -262,6 +556,17 @@ uint32_t grid1(uint64_t n) {
 // ---------------------------------------------------------------------------
 // launchers (fsg_launch.h)
 // ---------------------------------------------------------------------------
+// keys per record's map and their slots in `ord` (scal[6] = total)
+void launch_aggj_nk(const AggjArgs& a, uint64_t* tsum, hipStream_t s) {
+  if (a.n_rec) hipLaunchKernelGGL(k_aggj_nk, dim3(grid1(a.n_rec)), dim3(256), 0, s, a);
+  launch_xscan(a.nkr, a.koff, tsum, a.n_rec, a.scal + 6, s);
+}
+// the hashes, then every record's output order (one wave, stream order)
+void launch_aggj_order(const AggjArgs& a, hipStream_t s) {
+  if (!a.n_rec) return;
+  hipLaunchKernelGGL(k_aggj_hash, dim3(grid1(a.n_rec * 64)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_aggj_order, dim3(1), dim3(64), 0, s, a);
+}
 void launch_aggj_commit(const AjCommitArgs& c, uint64_t* tsum, int pass, hipStream_t s) {
   if (pass == 0) {  // keys / records through the stop batch, arena bytes (out[0..2])
     hipLaunchKernelGGL(k_ajc_head, dim3(1), dim3(64), 0, s, c);

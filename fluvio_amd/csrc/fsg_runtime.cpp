@@ -181,7 +181,16 @@ int32_t acc_value(const std::vector<uint8_t>& a) {
 struct AccMap {
   std::vector<std::string> keys, text;
   std::vector<uint32_t> vals;
+  std::vector<uint32_t> seq;  // per entry in text order: its key's index, | kAjDup when the key came before
+  bool dups = false;
 };
+// serde_json's deserialize_map calls the map visitor (which draws the map's
+// RandomState) once the first non-whitespace byte is '{'
+bool json_starts_map(const std::vector<uint8_t>& s) {
+  size_t i = 0;
+  while (i < s.size() && (s[i] == ' ' || s[i] == '\t' || s[i] == '\n' || s[i] == '\r')) i++;
+  return i < s.size() && s[i] == '{';
+}
 bool parse_acc_map(const std::vector<uint8_t>& s, AccMap& m) {
   size_t i = 0;
   const size_t n = s.size();
@@ -293,7 +302,10 @@ bool parse_acc_map(const std::vector<uint8_t>& s, AccMap& m) {
       while (at < m.keys.size() && m.keys[at] != k) at++;
       if (at < m.keys.size()) {
         m.vals[at] = (uint32_t)v;
+        m.seq.push_back((uint32_t)at | kAjDup);
+        m.dups = true;
       } else {
+        m.seq.push_back((uint32_t)m.keys.size());
         m.keys.push_back(k);
         m.vals.push_back((uint32_t)v);
       }
@@ -497,7 +509,15 @@ struct fsg_chain {
   int aj_cur = 0;
   bool aj_dev = false;      // the state lives in ajs[aj_cur] (the initial accumulator was parsed once)
   bool aj_touched = false;  // a record was folded: the accumulator is the map's text, not c->acc
-  uint32_t aj_K = 0;        // keys in the state
+  uint32_t aj_K = 0;        // keys in the state (in the order the accumulator text lists them)
+  // the guest's RandomState sequence (fsg_keyed.hip k_aggj_order): the k0 the
+  // next map draws, and whether the initial accumulator draws twice (it starts
+  // with '{' but does not parse: the visitor's map, then HashMap::default())
+  uint64_t aj_k0 = 1;
+  bool aj_e0 = false;
+  DevBuf aj_iseq;           // the initial accumulator's entries with repeats (AggjArgs::iseq)
+  uint32_t aj_n_iseq = 0;   // 0: no repeated key (ids in order)
+  DevBuf aj_nkr, aj_koff, aj_ord, aj_hrec, aj_oscr, aj_inv;
   uint64_t aj_bytes = 0;    // its arena bytes
   DevBuf aj_cout;           // commit scalars
   hipEvent_t kd_ev[2] = {}; // keyed collect: chain stream -> collect stream -> chain stream
@@ -1646,8 +1666,14 @@ int sf_run(fsg_chain* c, const fsg_slice* s, const EvalArgs& ea, SfArgs& sa, hip
 int aj_state_init(fsg_chain* c) {
   if (c->aj_dev) return FSG_OK;
   AccMap am;
-  parse_acc_map(c->acc, am);
+  const bool ok = parse_acc_map(c->acc, am);
+  c->aj_e0 = !ok && json_starts_map(c->acc);
   const uint32_t n = (uint32_t)am.keys.size();
+  if (am.dups) {  // HashMap::insert reserves before it finds a repeated key: the layout sees it
+    HIPCHK(c->aj_iseq.ensure(am.seq.size() * 4));
+    HIPCHK(hipMemcpy(c->aj_iseq.p, am.seq.data(), am.seq.size() * 4, hipMemcpyHostToDevice));
+    c->aj_n_iseq = (uint32_t)am.seq.size();
+  }
   std::vector<uint8_t> arena;
   std::vector<uint64_t> ko(n), to(n);
   std::vector<uint32_t> kl(n), tl(n);
@@ -1704,10 +1730,12 @@ int aj_commit(fsg_chain* c, const AggjArgs& aj, int32_t stop, uint32_t kmax) {
   HIPCHK(D.arena.ensure(16));
   HIPCHK(c->aj_cout.ensure(64));
   HIPCHK(c->aj_tsum.ensure(xscan_tiles(k1) * 8));
+  HIPCHK(c->aj_inv.ensure(k1 * 4));
   AjCommitArgs ca{};
   ca.a = aj;
   ca.stop = stop;
   ca.kmax = kmax;
+  ca.inv = c->aj_inv.as<uint32_t>();
   ca.out = c->aj_cout.as<unsigned long long>();
   ca.dst.arena = D.arena.as<uint8_t>();
   ca.dst.kptr = D.kptr.as<uint64_t>();
@@ -1718,9 +1746,14 @@ int aj_commit(fsg_chain* c, const AggjArgs& aj, int32_t stop, uint32_t kmax) {
   ca.dst.blen = D.blen.as<uint32_t>();
   ca.dst.boff = D.boff.as<uint64_t>();
   launch_aggj_commit(ca, c->aj_tsum.as<uint64_t>(), 0, st);
-  unsigned long long o[3] = {0, 0, 0};
+  unsigned long long o[5] = {0, 0, 0, 0, 0};
   HIPCHK(hipMemcpyAsync(o, ca.out, sizeof o, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  // the RandomStates the guest drew through the stop batch: two per folded
+  // record from k0_base (which counts the initial accumulator's extra draw),
+  // and at a final aggregate error its accumulator map plus, when the value
+  // starts with '{', the record's map
+  if (o[1] + o[3] > 0) c->aj_k0 = aj.k0_base + 2ull * o[1] + (o[3] ? 1ull + o[4] : 0ull);
   if (o[1] == 0) return FSG_OK;  // no record folded through the stop batch: the state stands
   HIPCHK(D.arena.ensure(o[2] + 16));
   ca.dst.arena = D.arena.as<uint8_t>();
@@ -1729,12 +1762,13 @@ int aj_commit(fsg_chain* c, const AggjArgs& aj, int32_t stop, uint32_t kmax) {
   c->aj_cur = 1 - c->aj_cur;
   c->aj_K = (uint32_t)o[0];
   c->aj_bytes = o[2];
-  c->aj_touched = true;
+  c->aj_touched = true;  // the accumulator is now the last output text: no repeats, parses
+  c->aj_n_iseq = 0;
   return FSG_OK;
 }
 
 // serde_json::to_vec_pretty of the state (the text the guest's last record
-// carried): "{}" or "{\n  key: v,\n  ...\n}", keys in insertion order
+// carried): "{}" or "{\n  key: v,\n  ...\n}", keys in the state's order (that text's)
 int aj_render(fsg_chain* c, std::vector<uint8_t>& out) {
   const fsg_chain::AjBuf& S = c->ajs[c->aj_cur];
   const uint32_t K = c->aj_K;
@@ -1923,10 +1957,10 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     aj.acc_len = c->aj_acclen.as<uint32_t>();
     aj.n_init = n_init;
     launch_aggj_count(aj, st);
-    unsigned long long sc[2] = {0, 0};
+    unsigned long long sc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HIPCHK(hipMemcpyAsync(sc, c->aj_out.p, sizeof sc, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    const uint64_t nent = sc[0], nrec = sc[1];
+    const uint64_t nent = sc[0], nrec = sc[1], most_ent = sc[7];
     uint32_t cap = 16;
     while (cap < 2 * (n_init + nent) + 1) cap <<= 1;
     const size_t nkmax = (size_t)n_init + nent + 1;
@@ -1949,6 +1983,9 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     HIPCHK(c->aj_roff.ensure(nr1 * 8));
     HIPCHK(c->aj_ekid.ensure(ne1 * 4));
     HIPCHK(c->aj_eval.ensure(ne1 * 4));
+    HIPCHK(c->aj_hrec.ensure(ne1 * 4));
+    HIPCHK(c->aj_nkr.ensure(nr1 * 4));
+    HIPCHK(c->aj_koff.ensure(nr1 * 8));
     HIPCHK(c->aj_sref.ensure((size_t)cap * 8));
     HIPCHK(c->aj_sid.ensure((size_t)cap * 4));
     HIPCHK(c->aj_tptr.ensure(nkmax * 8));
@@ -1980,6 +2017,16 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     aj.tptr = c->aj_tptr.as<uint64_t>();
     aj.tlen = c->aj_tlen.as<uint32_t>();
     aj.kup = c->aj_kup.as<uint32_t>();
+    // the output order's inputs (k_aggj_order): RandomState k0 of the first
+    // record's accumulator map, the initial accumulator's entries with repeats
+    aj.nkr = c->aj_nkr.as<uint32_t>();
+    aj.koff = c->aj_koff.as<uint64_t>();
+    aj.hrec = c->aj_hrec.as<uint32_t>();
+    aj.k0_base = c->aj_k0 + (!c->aj_touched && c->aj_e0 ? 1u : 0u);
+    aj.iseq = !c->aj_touched && c->aj_n_iseq ? c->aj_iseq.as<uint32_t>() : nullptr;
+    aj.n_iseq = aj.iseq ? c->aj_n_iseq : 0u;
+    aj.agg_stage = (uint32_t)c->agg_stage;
+    aj.in_i32 = c->hdesc.st[c->agg_stage].in_type == VT_I32 ? 1u : 0u;
     launch_aggj_keys(aj, c->aj_tsum.as<uint64_t>(), st);
     launch_aggj_kid(aj, nent, st);
     unsigned long long nnew = 0;
@@ -2017,6 +2064,23 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     }
     a0.write = 0;
     launch_aggj_size(a0, c->aj_tsum.as<uint64_t>(), st);
+    launch_aggj_nk(aj, c->aj_tsum.as<uint64_t>(), st);
+    // general-path tables of k_aggj_order: the most keys / entries one map
+    // holds, one growth past it (a repeated key can reserve at capacity)
+    const uint64_t most = std::max<uint64_t>(std::max<uint64_t>(K, most_ent), aj.n_iseq);
+    uint32_t ob = 0;
+    if (most > kAjRegKeys) {
+      uint64_t b = 4;
+      while ((b <= 8 ? b - 1 : b / 8 * 7) < most + 1) b *= 2;
+      if (2 * b > (1ull << 31)) return fail(FSG_E_UNSUPPORTED, "aggregate-json map past 2^30 keys");
+      ob = (uint32_t)(2 * b);
+    }
+    aj.obmax = ob;
+    aj.oscr = nullptr;
+    if (ob > kAjLdsBuckets) {
+      HIPCHK(c->aj_oscr.ensure((size_t)4 * (ob / 32 + ob) * 4));
+      aj.oscr = c->aj_oscr.as<uint32_t>();
+    }
   }
   SizeArgs sa{};
   sa.bstat = ea.bstat;
@@ -2136,9 +2200,10 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     wa.cat = c->cat.as<uint8_t>();
     launch_cat(wa, nb, st);
   }
-  if (has_aggj) {  // pass 1: the map texts into cat (sized by pass 0)
-    uint64_t aj_total = 0;
-    HIPCHK(hipMemcpy(&aj_total, aj.scal + 3, sizeof aj_total, hipMemcpyDeviceToHost));
+  if (has_aggj) {  // pass 1: the map texts into cat (sized by pass 0), keys in the guest's order
+    unsigned long long sc[4] = {0, 0, 0, 0};  // scal[3] text bytes, scal[6] ord slots
+    HIPCHK(hipMemcpy(sc, aj.scal + 3, sizeof sc, hipMemcpyDeviceToHost));
+    const uint64_t aj_total = sc[0], n_ord = sc[3];
     if (aj_total + kCatOff > c->limit) {
       char b[160];
       snprintf(b, sizeof b, "Requested memory %zub exceeded max allowed %zub", (size_t)(aj_total + kCatOff), c->limit);
@@ -2148,6 +2213,9 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
       return fail(FSG_E_STORE_MEMORY, b);
     }
     HIPCHK(c->cat.ensure(kCatOff + aj_total + 64));
+    HIPCHK(c->aj_ord.ensure(std::max<uint64_t>(n_ord, 1) * 4));  // Σ keys <= text bytes / 8
+    aj.ord = c->aj_ord.as<uint32_t>();
+    launch_aggj_order(aj, st);
     aj.cat = c->cat.as<uint8_t>();
     aj.write = 1;
     launch_aggj_write(aj, st);

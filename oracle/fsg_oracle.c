@@ -1457,6 +1457,7 @@ typedef struct {
   size_t acc_len;
   int32_t prev; /* filter_look_back: static PREV (AtomicI32, starts at 0) */
   bhs_t *set;   /* filter_hashset: static SET */
+  uint64_t rs_k0; /* aggregate-json: the instance's next RandomState k0 (std's KEYS thread-local) */
 } stage_t;
 
 static uint64_t bhs_hash(const uint8_t *b, size_t n) {
@@ -1645,6 +1646,7 @@ int orc_chain_add(orc_chain *c, const char *module, const char **keys, const cha
   } else if (!strcmp(module, "aggregate-json")) {
     s.mod = M_AGG_JSON;
     s.kind = K_AGGREGATE;
+    s.rs_k0 = 1; /* hashmap_random_keys() = (1, 2) on wasm32-unknown-unknown */
   } else if (!strcmp(module, "map_json_project")) { /* param field, default "message" */
     v = param_get(keys, vals, n_params, "field");
     if (!v) v = "message";
@@ -1699,6 +1701,188 @@ static int mem_contains(const uint8_t *h, size_t hn, const uint8_t *n, size_t nn
 }
 
 static void i32_to_str(int32_t v, char *buf, size_t *len) { *len = (size_t)sprintf(buf, "%d", v); }
+
+/* ------------------------------------------------------------------------
+ * std::collections::HashMap<String, u32> as the aggregate-json guest builds it
+ * (examples/aggregate-json/src/lib.rs:22-36; Rust 1.75, examples/rust-toolchain,
+ * for wasm32-unknown-unknown), which fixes the key order of its output:
+ *  - RandomState::new() (std/src/hash/random.rs) hands out (k0, k1) from a
+ *    thread-local seeded by sys::hashmap_random_keys() = (1, 2) on this target
+ *    (std/src/sys/unsupported/common.rs) and bumps k0 per call (stage_t.rs_k0);
+ *  - DefaultHasher = SipHash-1-3 (core/src/hash/sip.rs), a String hashes as its
+ *    bytes then 0xFF (Hasher::write_str);
+ *  - the table is hashbrown 0.14 (std's backend): generic 8-byte control
+ *    groups (GroupWord = u64 on wasm32), h1 = the hash as a 32-bit usize, h2 =
+ *    its top 7 bits, triangular probing by groups over control bytes whose
+ *    trailing group mirrors the first, fix_insert_slot's rescan from bucket 0
+ *    for tables smaller than a group, growth by capacity_to_buckets
+ *    (0 -> 4 -> 8 -> 2x), resize re-inserting in bucket order, iteration in
+ *    bucket order.
+ * ---------------------------------------------------------------------- */
+uint64_t orc_siphash(int c_rounds, int d_rounds, uint64_t k0, uint64_t k1, const uint8_t *m, size_t n) {
+#define ORC_ROTL(x, b) (((x) << (b)) | ((x) >> (64 - (b))))
+#define ORC_SIPROUND                                                     \
+  do {                                                                   \
+    v0 += v1; v1 = ORC_ROTL(v1, 13); v1 ^= v0; v0 = ORC_ROTL(v0, 32);    \
+    v2 += v3; v3 = ORC_ROTL(v3, 16); v3 ^= v2;                           \
+    v0 += v3; v3 = ORC_ROTL(v3, 21); v3 ^= v0;                           \
+    v2 += v1; v1 = ORC_ROTL(v1, 17); v1 ^= v2; v2 = ORC_ROTL(v2, 32);    \
+  } while (0)
+  uint64_t v0 = k0 ^ 0x736f6d6570736575ull, v1 = k1 ^ 0x646f72616e646f6dull;
+  uint64_t v2 = k0 ^ 0x6c7967656e657261ull, v3 = k1 ^ 0x7465646279746573ull;
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w = 0;
+    for (int b = 0; b < 8; b++) w |= (uint64_t)m[i + b] << (8 * b);
+    v3 ^= w;
+    for (int r = 0; r < c_rounds; r++) ORC_SIPROUND;
+    v0 ^= w;
+  }
+  uint64_t b = (uint64_t)(n & 0xff) << 56;
+  for (size_t t = 0; i + t < n; t++) b |= (uint64_t)m[i + t] << (8 * t);
+  v3 ^= b;
+  for (int r = 0; r < c_rounds; r++) ORC_SIPROUND;
+  v0 ^= b;
+  v2 ^= 0xff;
+  for (int r = 0; r < d_rounds; r++) ORC_SIPROUND;
+  return v0 ^ v1 ^ v2 ^ v3;
+#undef ORC_SIPROUND
+#undef ORC_ROTL
+}
+
+static uint64_t hb_str_hash(uint64_t k0, const uint8_t *key, size_t n) {
+  uint8_t *t = (uint8_t *)malloc(n + 1);
+  if (n) memcpy(t, key, n);
+  t[n] = 0xff;
+  const uint64_t h = orc_siphash(1, 3, k0, 2, t, n + 1);
+  free(t);
+  return h;
+}
+
+enum { HB_GROUP = 8, HB_EMPTY = 0xff };
+typedef struct {
+  uint64_t k0;
+  size_t buckets; /* 0: the empty singleton */
+  size_t items;
+  uint8_t *ctrl;  /* buckets + HB_GROUP control bytes */
+  uint8_t **key;  /* per bucket (owned) */
+  size_t *klen;
+  uint32_t *val;
+  uint32_t *h1;   /* per bucket: the key's hash as usize */
+} hb_t;
+
+static size_t hb_capacity(size_t buckets) {
+  if (!buckets) return 0;
+  const size_t mask = buckets - 1;
+  return mask < 8 ? mask : ((mask + 1) / 8) * 7;
+}
+static size_t hb_cap_to_buckets(size_t cap) {
+  if (cap < 8) return cap < 4 ? 4 : 8;
+  size_t adj = cap * 8 / 7, b = 1;
+  while (b < adj) b <<= 1;
+  return b;
+}
+static void hb_alloc(hb_t *t, size_t buckets) {
+  t->buckets = buckets;
+  t->items = 0;
+  t->ctrl = (uint8_t *)malloc(buckets + HB_GROUP);
+  memset(t->ctrl, HB_EMPTY, buckets + HB_GROUP);
+  t->key = (uint8_t **)calloc(buckets, sizeof(uint8_t *));
+  t->klen = (size_t *)calloc(buckets, sizeof(size_t));
+  t->val = (uint32_t *)calloc(buckets, sizeof(uint32_t));
+  t->h1 = (uint32_t *)calloc(buckets, sizeof(uint32_t));
+}
+static void hb_free(hb_t *t) {
+  for (size_t i = 0; i < t->buckets; i++) free(t->key[i]);
+  free(t->ctrl);
+  free(t->key);
+  free(t->klen);
+  free(t->val);
+  free(t->h1);
+  memset(t, 0, sizeof *t);
+}
+static int hb_full(const hb_t *t, size_t i) { return !(t->ctrl[i] & 0x80); }
+/* set_ctrl: the byte and its mirror among the trailing HB_GROUP bytes */
+static void hb_set_ctrl(hb_t *t, size_t i, uint8_t c) {
+  t->ctrl[i] = c;
+  t->ctrl[((i - HB_GROUP) & (t->buckets - 1)) + HB_GROUP] = c;
+}
+/* find_insert_slot: the first EMPTY/DELETED byte of the group at the probe
+ * position, then fix_insert_slot */
+static size_t hb_find_insert_slot(const hb_t *t, uint32_t h1) {
+  const size_t mask = t->buckets - 1;
+  size_t pos = h1 & mask, stride = 0;
+  for (;;) {
+    for (size_t bit = 0; bit < HB_GROUP; bit++) {
+      if (!(t->ctrl[pos + bit] & 0x80)) continue;
+      size_t idx = (pos + bit) & mask;
+      if (hb_full(t, idx)) { /* a table smaller than a group: rescan the aligned first group */
+        idx = 0;
+        while (!(t->ctrl[idx] & 0x80)) idx++;
+      }
+      return idx;
+    }
+    stride += HB_GROUP;
+    pos = (pos + stride) & mask;
+  }
+}
+static void hb_place(hb_t *t, uint8_t *key, size_t klen, uint32_t val, uint64_t hash) {
+  const uint32_t h1 = (uint32_t)hash;
+  const size_t i = hb_find_insert_slot(t, h1);
+  hb_set_ctrl(t, i, (uint8_t)((h1 >> 25) & 0x7f));
+  t->key[i] = key;
+  t->klen[i] = klen;
+  t->val[i] = val;
+  t->h1[i] = h1;
+  t->items++;
+}
+/* reserve(1): reserve_rehash -> resize(max(items + 1, capacity + 1)), old
+ * buckets re-inserted in bucket order (no tombstones here: no removals) */
+static void hb_reserve1(hb_t *t) {
+  const size_t cap = hb_capacity(t->buckets);
+  if (cap - t->items >= 1) return;
+  hb_t n;
+  memset(&n, 0, sizeof n);
+  n.k0 = t->k0;
+  hb_alloc(&n, hb_cap_to_buckets(t->items + 1 > cap + 1 ? t->items + 1 : cap + 1));
+  for (size_t i = 0; i < t->buckets; i++) {
+    if (!hb_full(t, i)) continue;
+    hb_place(&n, t->key[i], t->klen[i], t->val[i], t->h1[i]);
+    t->key[i] = NULL;
+  }
+  hb_free(t);
+  *t = n;
+}
+static long hb_lookup(const hb_t *t, const uint8_t *key, size_t klen) {
+  for (size_t i = 0; i < t->buckets; i++)
+    if (hb_full(t, i) && t->klen[i] == klen && !memcmp(t->key[i], key, klen)) return (long)i;
+  return -1;
+}
+/* HashMap::insert: find_or_find_insert_slot reserves before the lookup */
+static void hb_insert(hb_t *t, const uint8_t *key, size_t klen, uint32_t val) {
+  hb_reserve1(t);
+  const long at = hb_lookup(t, key, klen);
+  if (at >= 0) {
+    t->val[at] = val;
+    return;
+  }
+  hb_place(t, dup_bytes(key, klen), klen, val, hb_str_hash(t->k0, key, klen));
+}
+/* entry(key).and_modify(+= v).or_insert(v): rustc_entry reserves for a vacant key only */
+static void hb_entry_add(hb_t *t, const uint8_t *key, size_t klen, uint32_t val) {
+  const long at = hb_lookup(t, key, klen);
+  if (at >= 0) {
+    t->val[at] += val; /* u32 wrapping (release wasm) */
+    return;
+  }
+  hb_reserve1(t);
+  hb_place(t, dup_bytes(key, klen), klen, val, hb_str_hash(t->k0, key, klen));
+}
+static int json_ws_first_is_brace(const uint8_t *s, size_t n) {
+  size_t i = 0;
+  while (i < n && (s[i] == ' ' || s[i] == '\t' || s[i] == '\n' || s[i] == '\r')) i++;
+  return i < n && s[i] == '{';
+}
 
 /* per-record user fn outcome */
 typedef struct {
@@ -1814,80 +1998,64 @@ static void stage_run(stage_t *s, recvec *in, int64_t base_offset, stage_out *o)
       case M_AGG_JSON: {
         /* aggregate-json/src/lib.rs:22-36: accumulated = from_slice(acc).unwrap_or_default();
          * new = from_slice(value)?; accumulated + new (per key `+=`, u32 wrapping in the
-         * release wasm); to_vec_pretty.  The map's iteration order is HashMap's (random per
-         * process): this restatement defines it as first insertion (the accumulator's keys
-         * first, then the record's new keys by first occurrence), the device does the same,
-         * and parity with the reference is on the map. */
+         * release wasm); to_vec_pretty of the accumulated map, in its iteration order
+         * (the hb_* restatement above).  RandomState draws: serde's map visitor once
+         * deserialize_map has seen '{', and HashMap::default() in unwrap_or_default. */
         uint8_t **ak = NULL, **nk = NULL;
         size_t *al = NULL, *nl = NULL, an = 0, nn = 0, ml;
         uint32_t *av = NULL, *nv = NULL;
         char *m = NULL;
+        hb_t acc, rec;
+        memset(&acc, 0, sizeof acc);
+        memset(&rec, 0, sizeof rec);
+        if (json_ws_first_is_brace(s->acc, s->acc_len)) acc.k0 = s->rs_k0++;
         if (orc_json_map_u32(s->acc, s->acc_len, &ak, &al, &av, &an, &m, &ml)) { /* unwrap_or_default */
           free(m);
           m = NULL;
           an = 0;
+          acc.k0 = s->rs_k0++;
         }
-        /* the accumulator's duplicate keys: the last value wins, at the first position */
-        size_t w = 0;
-        for (size_t k = 0; k < an; k++) {
-          size_t j = 0;
-          while (j < w && !(al[j] == al[k] && !memcmp(ak[j], ak[k], al[k]))) j++;
-          if (j < w) {
-            av[j] = av[k];
-            free(ak[k]);
-          } else {
-            ak[w] = ak[k];
-            al[w] = al[k];
-            av[w] = av[k];
-            w++;
-          }
+        for (size_t k = 0; k < an; k++) { /* the visitor's HashMap::insert per entry, text order */
+          hb_insert(&acc, ak[k], al[k], av[k]);
+          free(ak[k]);
         }
-        an = w;
+        free(ak); free(al); free(av);
+        if (json_ws_first_is_brace(r->val, r->val_len)) rec.k0 = s->rs_k0++;
         int jr = orc_json_map_u32(r->val, r->val_len, &nk, &nl, &nv, &nn, &m, &ml);
         if (jr == ORC_E_UNSUPPORTED) {
-          for (size_t k = 0; k < an; k++) free(ak[k]);
-          free(ak); free(al); free(av);
+          hb_free(&acc);
           o->unsupported = 1;
           return;
         }
         if (jr) {
-          for (size_t k = 0; k < an; k++) free(ak[k]);
-          free(ak); free(al); free(av);
+          hb_free(&acc);
           hint = m;
           break;
         }
-        /* the record's map: the last value of a key, at its first occurrence */
         for (size_t k = 0; k < nn; k++) {
-          size_t last = k;
-          int seen_before = 0;
-          for (size_t j = 0; j < nn; j++) {
-            if (nl[j] != nl[k] || memcmp(nk[j], nk[k], nl[k])) continue;
-            if (j < k) seen_before = 1;
-            last = j;
-          }
-          if (seen_before) continue;
-          const uint32_t v = nv[last];
-          size_t j = 0;
-          while (j < an && !(al[j] == nl[k] && !memcmp(ak[j], nk[k], nl[k]))) j++;
-          if (j < an) {
-            av[j] = av[j] + v; /* wrapping */
-          } else {
-            ak = (uint8_t **)realloc(ak, (an + 1) * sizeof(uint8_t *));
-            al = (size_t *)realloc(al, (an + 1) * sizeof(size_t));
-            av = (uint32_t *)realloc(av, (an + 1) * sizeof(uint32_t));
-            ak[an] = dup_bytes(nk[k], nl[k]);
-            al[an] = nl[k];
-            av[an] = v;
-            an++;
-          }
+          hb_insert(&rec, nk[k], nl[k], nv[k]);
+          free(nk[k]);
         }
-        for (size_t k = 0; k < nn; k++) free(nk[k]);
         free(nk); free(nl); free(nv);
+        for (size_t i = 0; i < rec.buckets; i++) /* `for (repo, new_stars) in next.0`: bucket order */
+          if (hb_full(&rec, i)) hb_entry_add(&acc, rec.key[i], rec.klen[i], rec.val[i]);
+        hb_free(&rec);
+        uint8_t **ok = (uint8_t **)malloc((acc.items + 1) * sizeof(uint8_t *));
+        size_t *ol = (size_t *)malloc((acc.items + 1) * sizeof(size_t));
+        uint32_t *ov = (uint32_t *)malloc((acc.items + 1) * sizeof(uint32_t));
+        size_t on = 0;
+        for (size_t i = 0; i < acc.buckets; i++) {
+          if (!hb_full(&acc, i)) continue;
+          ok[on] = acc.key[i];
+          ol[on] = acc.klen[i];
+          ov[on] = acc.val[i];
+          on++;
+        }
         uint8_t *pb;
         size_t pl;
-        orc_json_pretty_map(ak, al, av, an, &pb, &pl);
-        for (size_t k = 0; k < an; k++) free(ak[k]);
-        free(ak); free(al); free(av);
+        orc_json_pretty_map(ok, ol, ov, on, &pb, &pl);
+        free(ok); free(ol); free(ov);
+        hb_free(&acc);
         free(s->acc);
         s->acc = pb;
         s->acc_len = pl;

@@ -110,6 +110,9 @@ int orc_json_array_map(const uint8_t *s, size_t n, uint8_t ***elems, size_t **le
 /* aggregate-json: HashMap<String, u32> of one value (entries in text order) */
 int orc_json_map_u32(const uint8_t *s, size_t n, uint8_t ***keys, size_t **klens, uint32_t **vals, size_t *count,
                      char **msg, size_t *msg_len);
+/* SipHash-c-d (64-bit output) of m[0..n) under (k0, k1): SipHash-1-3 is std's
+ * DefaultHasher, which fixes aggregate-json's HashMap order (fsg_oracle.c hb_*) */
+uint64_t orc_siphash(int c_rounds, int d_rounds, uint64_t k0, uint64_t k1, const uint8_t *m, size_t n);
 void orc_json_pretty_map(uint8_t *const *keys, const size_t *klens, const uint32_t *vals, size_t n, uint8_t **out,
                          size_t *out_len);
 int orc_json_project(const uint8_t *s, size_t n, const char *field, uint8_t **out, size_t *out_len, int *found,

@@ -96,8 +96,15 @@ def lib():
         L.orc_xxh32.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32]
         L.orc_varint_encode.restype = ctypes.c_size_t
         L.orc_varint_encode.argtypes = [ctypes.c_int64, ctypes.c_char_p]
+        L.orc_siphash.restype = ctypes.c_uint64
+        L.orc_siphash.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_char_p,
+                                  ctypes.c_size_t]
         _lib = L
     return _lib
+
+
+def siphash(c_rounds: int, d_rounds: int, k0: int, k1: int, data: bytes) -> int:
+    return lib().orc_siphash(c_rounds, d_rounds, k0, k1, data, len(data))
 
 
 def crc32c(data: bytes) -> int:

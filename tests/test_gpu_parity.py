@@ -967,8 +967,10 @@ def test_project_c3_chain_errors_in_stream(engine):
 
 # ---------------------------------------------------------------------------
 # aggregate-json (examples/aggregate-json: HashMap<String, u32> += per key,
-# the C5 keyed aggregate): every record's output = the pretty map after it
-# (insertion order, as the oracle defines it), the stored accumulator, errors
+# the C5 keyed aggregate): every record's output = the pretty map after it, its
+# keys in the guest HashMap's bucket order (SipHash-1-3 under the wasm32
+# RandomState sequence, hashbrown's groups: oracle hb_*, tests/rust_hashmap.py),
+# the stored accumulator, errors; byte-for-byte against the oracle
 # ---------------------------------------------------------------------------
 def _keyed_slice(seed, nbatches=30, nkeys=40, bad=0.0, escapes=False):
     import json
@@ -1000,6 +1002,10 @@ AGGJ_CHAINS = {
     "aggj": [("aggregate-json", {}, None)],
     "aggj_acc": [("aggregate-json", {}, b'{\n  "repo-0003": 10,\n  "z\\"q": 1\n}')],
     "aggj_bad_acc": [("aggregate-json", {}, b"not json")],
+    # '{' then a failure: the visitor's map and HashMap::default() both draw a RandomState
+    "aggj_brace_bad_acc": [("aggregate-json", {}, b' {"repo-0002": "x"}')],
+    # a repeated key: HashMap::insert reserves before it finds the key (the layout can grow)
+    "aggj_dup_acc": [("aggregate-json", {}, b'{"a": 1, "b": 2, "c": 3, "a": 4, "d": 5, "e": 6, "f": 7, "a": 9}')],
     "filter_aggj": [("filter_init", {"key": "repo-000"}, None), ("aggregate-json", {}, None)],
     "map_aggj": [("map", {}, None), ("aggregate-json", {}, b'{"REPO-0001": 5}')],
 }
@@ -1152,7 +1158,8 @@ def test_aggregate_json_process_kat(engine):
     out = g.process(SmartModuleInput.try_from_records([P.Record.new(v) for v in vals]))
     ref = o.process(P.encode_records([P.Record.new(v) for v in vals]))
     assert [r.value for r in out.successes] == [r.value for r in P.decode_records(ref["bytes"])]
-    assert out.successes[-1].value == b'{\n  "a": 4,\n  "b": 2,\n  "c": 7\n}'
+    # bucket order under k0 = 7 (the fourth record's accumulator map): b, a, c (tests/rust_hashmap.py)
+    assert out.successes[-1].value == b'{\n  "b": 2,\n  "a": 4,\n  "c": 7\n}'
     assert g.accumulator(0) == o.accumulator(0)
 
 

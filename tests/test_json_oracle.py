@@ -282,34 +282,14 @@ def test_project_oracle_vs_python_json():
 
 # ---------------------------------------------------------------------------
 # aggregate-json (examples/aggregate-json: HashMap<String, u32> += per key,
-# to_vec_pretty): the oracle against a Python model of the same semantics
-# (insertion order for the map; the reference's HashMap order is random, so
-# parity with it is on the map)
+# to_vec_pretty): the oracle against the Python model of the guest's HashMap
+# (tests/rust_hashmap.py: SipHash-1-3 under the wasm32 RandomState sequence,
+# hashbrown's bucket order), including error hints
 # ---------------------------------------------------------------------------
-def _py_u32_map(doc: bytes):
-    """None if serde_json would reject `doc` as HashMap<String, u32>, else the
-    (key, value) pairs in text order.  Raises OverflowError for a float (outside
-    the restatement)."""
-    class _Pairs(list):
-        pass
-    try:
-        pairs = json.loads(doc, object_pairs_hook=_Pairs,
-                           parse_float=lambda x: (_ for _ in ()).throw(OverflowError()),
-                           parse_constant=lambda x: None)
-    except OverflowError:
-        raise
-    except (ValueError, RecursionError):
-        return None
-    if not isinstance(pairs, _Pairs):
-        return None
-    for k, v in pairs:
-        if isinstance(v, bool) or not isinstance(v, int) or not (0 <= v < 2 ** 32):
-            return None
-    return pairs
-
-
 def test_aggregate_json_oracle_vs_python_model():
     from fluvio_amd import protocol as P
+    from tests import rust_hashmap as H
+    from tests.test_hashmap_order import _py_u32_map
     import random
     rng = random.Random(12)
     keys = ["repo-%d" % i for i in range(12)] + ["é", 'q"uote', "tab\t"]
@@ -327,26 +307,14 @@ def test_aggregate_json_oracle_vs_python_model():
                 vals.append(rng.choice([b'{"a": -1}', b'{"a": "s"}', b"[1]", b'{"a": 4294967296}', b"{", b'{"a":1}x']))
         ch = O.OracleChain([("aggregate-json", {}, acc0)])
         out = ch.process(P.encode_records([P.Record.new(v) for v in vals]))
-        try:
-            init = _py_u32_map(acc0)
-        except OverflowError:
-            init = None
-        acc = {}
-        for k, v in (init or []):
-            acc[k] = v
+        model = H.AggregateJson(acc0, _py_u32_map)
         expect = []
-        err = False
         for v in vals:
-            pairs = _py_u32_map(v)
-            if pairs is None:
-                err = True
+            o = model.call(v)
+            if o is None:
                 break
-            rec = {}
-            for k, x in pairs:
-                rec[k] = x
-            for k, x in rec.items():
-                acc[k] = (acc.get(k, 0) + x) & 0xFFFFFFFF
-            expect.append(json.dumps(acc, indent=2, ensure_ascii=False).encode())
+            expect.append(o)
+        err = len(expect) < len(vals)
         got = [r.value for r in P.decode_records(out["bytes"])]
         assert got == expect, (acc0, vals)
         assert (out["error"] is not None) == err, (vals, out["error"])
