@@ -29,6 +29,7 @@ FSG_E_INVALID_ARG = -105
 FSG_E_LOOKBACK = -106
 FSG_LOOKBACK_NONE, FSG_LOOKBACK_LAST, FSG_LOOKBACK_AGE = 0, 1, 2
 FSG_E_DEVICE = -200
+ABI_VERSION = 4  # include/fsg.h FSG_ABI_VERSION: the struct layouts below
 
 
 class fsg_param(ctypes.Structure):
@@ -164,6 +165,9 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        got = L.fsg_abi_version()
+        if got != ABI_VERSION:  # a stale libfsg.so would write past these structs
+            raise RuntimeError(f"{LIB_PATH}: ABI version {got}, this binding expects {ABI_VERSION}; rebuild it")
         _lib = L
     return _lib
 

@@ -221,15 +221,6 @@ struct Plan {
   uint64_t cat_final;        // aggregate (concat): accumulator bytes appended through the stop batch
 };
 
-// k_flat_frame's per-batch window descriptor (fsg_flat.hip)
-struct BatchWin {
-  uint64_t al;         // 16-byte aligned window start (absolute slice offset)
-  uint64_t rb;         // rbase[b]
-  uint32_t wlen;       // window bytes (16-byte multiple, <= 16464)
-  uint32_t nr_re;      // records | end of the last record (window offset) << 16; nr = 0xFFFF: exact path
-  uint32_t pad[2];
-};
-
 struct EvalArgs {
   const uint8_t* slice;
   uint64_t slice_len;
@@ -247,7 +238,6 @@ struct EvalArgs {
   uint64_t nrec;       // records of the slice (rbase's total)
   uint16_t* rstart;    // k_chase: record n of batch b starts at window offset rstart[rbase[b] + n] ...
   uint16_t* rend;      // ... and the last one ends at rend[b] (0xFFFF: no lean framing, exact path)
-  BatchWin* bwin;      // k_flat_frame -> k_flat: per-batch window (one scalar load per batch)
   const uint8_t* pass; // per batch, 1: the records pass through unchanged (no stage runs on them:
                        // an earlier segment's partial output before its error), nullptr: none
 };

@@ -4489,10 +4489,7 @@ void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s) {
   const size_t dyn = (ops & opbit(OP_REGEX)) ? kDfaDyn : 0;
   EvalArgs e = a;
   uint32_t grid = a.nbatches;
-  if (mode == EVAL_FLAT) {
-    launch_flat(a, s);  // k_flat_frame (k_chase + window descriptors) and k_flat
-    grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list
-  } else if (mode == EVAL_ARRAY) {
+  if (mode == EVAL_ARRAY) {
     // record starts (k_chase_x), then the lean array kernel (fsg_array.hip)
     hipLaunchKernelGGL(k_chase_x, dim3(std::min<uint32_t>((a.nbatches + 255) / 256, 4096)), dim3(256), 0, s, a);
     launch_array_lean(a, s);

@@ -417,7 +417,9 @@ __global__ __launch_bounds__(256) void k_kd_collect(KdTable t, const uint64_t* s
     uint32_t s = kd_hash(p, len) & (t.cap - 1u);
     uint32_t mine = kKdDead;
     for (;;) {
-      uint32_t cur = ld_agent(&t.slot[s]);
+      // acquire: a published slot's key (klen / koff / arena, written before the
+      // publishing CAS behind a release fence) is visible once the slot is
+      uint32_t cur = __hip_atomic_load(&t.slot[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
       if (cur == 0) {
         if (mine == kKdDead) {
           mine = (uint32_t)atomicAdd(&t.cnt[0], 1ull);
@@ -433,6 +435,7 @@ __global__ __launch_bounds__(256) void k_kd_collect(KdTable t, const uint64_t* s
           atomicAdd(&t.val[mine], v);
           break;
         }
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);  // lost the CAS: read the winner's key after its slot
       }
       const uint32_t k = cur - 1u;
       const uint32_t kl = ld_agent(&t.klen[k]);

@@ -8,14 +8,9 @@ namespace fsg {
 hipError_t upload_crc_tables();
 // ops: bit per StageOp in the chain.  mode: EVAL_EXACT = k_eval over every
 // batch; EVAL_LEAN = k_chase + k_eval_lean, then k_eval over its deferred list;
-// EVAL_FLAT = k_chase + k_flat (fsg_flat.hip), then k_eval over its deferred list
 // EVAL_ARRAY = k_chase_x + k_arr_lean (fsg_array.hip), then k_eval over its deferred list
-enum EvalMode { EVAL_EXACT = 0, EVAL_LEAN = 1, EVAL_FLAT = 2, EVAL_ARRAY = 3 };
+enum EvalMode { EVAL_EXACT = 0, EVAL_LEAN = 1, EVAL_ARRAY = 3 };
 void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s);
-// the register-resident substring path (fsg_flat.hip): chains of contains
-// filters (needles of 4..64 bytes, at most two stages) and uppercase maps
-bool flat_eligible(const ChainDesc& ch, uint32_t ops);
-void launch_flat(const EvalArgs& a, hipStream_t s);
 // array_map_json_array alone over the source values (fsg_array.hip)
 bool array_lean_eligible(const ChainDesc& ch, uint32_t ops);
 void launch_array_lean(const EvalArgs& a, hipStream_t s);

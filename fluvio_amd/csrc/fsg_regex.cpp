@@ -201,8 +201,9 @@ struct Parser {
   }
   int depth = 0;
 
-  // (?i): simple case folding restated for ASCII letters (+ U+212A ~ k, U+017F ~ s);
-  // a literal outside ASCII under (?i) is unsupported
+  // (?i): simple case folding restated for ASCII letters, + U+212A ~ k and
+  // U+017F ~ s in Unicode mode only ((?-u) folds ASCII bytes: regex-syntax's
+  // byte classes); a literal outside ASCII under (?i) is unsupported
   void add_folded(Set& st, uint32_t lo, uint32_t hi) {
     st.push_back({lo, hi});
     if (!fi) return;
@@ -215,6 +216,7 @@ struct Parser {
     a = std::max<uint32_t>(lo, 'A');
     b = std::min<uint32_t>(hi, 'Z');
     if (a <= b) st.push_back({a + 32, b + 32});
+    if (!fu) return;
     if ((lo <= 'k' && 'k' <= hi) || (lo <= 'K' && 'K' <= hi)) st.push_back({0x212A, 0x212A});
     if ((lo <= 's' && 's' <= hi) || (lo <= 'S' && 'S' <= hi)) st.push_back({0x17F, 0x17F});
   }
@@ -385,8 +387,19 @@ struct Parser {
         lo = c;
       }
       uint32_t hi = lo;
-      if (i + 1 < p.size() && p[i] == '-' && p[i + 1] != ']') {
-        i++;
+      // parse_set_class_range: bump_space after the first item; a '-' makes a
+      // range unless the next non-space char is ']' or '-' (a difference)
+      skip_x();
+      size_t j = i + 1;
+      if (fx && i < p.size()) {
+        const size_t at_dash = i;
+        i = j;
+        skip_x();
+        j = i;
+        i = at_dash;
+      }
+      if (i < p.size() && p[i] == '-' && j < p.size() && p[j] != ']' && p[j] != '-') {
+        i = j;
         uint32_t c2 = p[i++];
         if (c2 == '\\') {
           Set s;
@@ -402,6 +415,10 @@ struct Parser {
           err = true;
           return n;
         }
+      }
+      if (!fu && hi >= 0x80) {  // class_literal_byte: UnicodeNotAllowed in a (?-u) class
+        err = true;
+        return n;
       }
       add_folded(n->set, lo, hi);
     }

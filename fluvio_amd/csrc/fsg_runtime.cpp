@@ -350,18 +350,6 @@ bool parse_acc_map(const std::vector<uint8_t>& s, AccMap& m) {
   return true;
 }
 
-// an environment switch (experiments: FSG_FLAT=1 takes k_flat instead of k_eval_lean)
-bool getenv_flag(const char* name) {
-  static std::map<std::string, bool> cache;
-  static std::mutex mu;
-  std::lock_guard<std::mutex> g(mu);
-  auto it = cache.find(name);
-  if (it != cache.end()) return it->second;
-  const char* v = getenv(name);
-  const bool on = v && *v && strcmp(v, "0") != 0;
-  cache[name] = on;
-  return on;
-}
 
 struct DevBuf {
   void* p = nullptr;
@@ -534,7 +522,6 @@ struct fsg_chain {
   uint32_t last_aj_kmax = 0;
   bool last_has_aggj = false;
   DevBuf rstart, rend;  // k_chase (lean path record starts)
-  DevBuf bwin;          // k_flat_frame: per-batch window descriptors
   // stateful last stage (filter_look_back / filter_hashset)
   int sf_stage = -1;
   std::shared_ptr<SfState> sf;
@@ -1116,24 +1103,30 @@ int decompress_slice(fsg_slice* sl, const std::vector<uint64_t>& bpos, const std
   // allocated (gzip expands up to ~1000x, lz4 ~255x).  The reference hands one
   // decompressed batch at a time to a guest whose memory is capped by the store
   // limit (engine.rs:24, limiter.rs:18-35): a batch larger than the limit is
-  // StoreMemoryExceeded.  Here the whole decompressed slice is resident, so its
-  // total must also fit in half of the device's free memory.
+  // StoreMemoryExceeded, exactly as there.  Here the whole decompressed slice
+  // is also resident: a slice that does not fit in the device's free memory
+  // (with half kept for the chain's scratch) is a device shortfall outside the
+  // reference's behaviour: FSG_E_DEVICE, not a StoreMemoryExceeded the
+  // reference would never raise for batches under the limit.
   {
-    uint64_t need = 0, big = 0;
+    uint64_t big = 0;
     for (uint32_t b = 0; b < keep; b++) big = std::max<uint64_t>(big, (uint64_t)ds[b]);
-    size_t fr = 0, tot = 0;
-    if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
-    const uint64_t budget = fr / 2;
-    if (big > sl->dec_limit) need = big;
-    else if (total + kSlicePad + kWin > budget) need = total;
-    if (need) {
+    if (big > sl->dec_limit) {
       char b[200];
       snprintf(b, sizeof b, "Requested memory %llub exceeded max allowed %llub (decompressed record sections)",
-               (unsigned long long)need, (unsigned long long)(big > sl->dec_limit ? sl->dec_limit : budget));
+               (unsigned long long)big, (unsigned long long)sl->dec_limit);
       g_store_mem[0] = 0;
-      g_store_mem[1] = need;
-      g_store_mem[2] = big > sl->dec_limit ? sl->dec_limit : budget;
+      g_store_mem[1] = big;
+      g_store_mem[2] = sl->dec_limit;
       return fail(FSG_E_STORE_MEMORY, b);
+    }
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
+    if (total + kSlicePad + kWin > fr / 2) {
+      char b[200];
+      snprintf(b, sizeof b, "decompressed slice of %llu bytes does not fit the device's free memory (%zu bytes)",
+               (unsigned long long)total, fr);
+      return fail(FSG_E_DEVICE, b);
     }
   }
   DevBuf& nd = sl->dec[7];  // swapped with the compressed slice below: both stay for the next upload
@@ -1904,19 +1897,10 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   HIPCHK(c->rend.ensure(((size_t)nb + 1) * sizeof(uint16_t)));
   ea.rstart = c->rstart.as<uint16_t>();
   ea.rend = c->rend.as<uint16_t>();
-  // substring filters / uppercase maps: the register-resident path (fsg_flat.hip)
-  // is an experiment, opt-in with FSG_FLAT=1: measured on MI355X (C2, round 3)
-  // k_flat 2.56 ms against k_eval_lean 1.61 ms, parity-green both ways
-  const bool flat = lean && getenv_flag("FSG_FLAT") && flat_eligible(c->hdesc, ops);
   // array_map alone: the lean array kernel, unsupported shapes deferred to k_eval
-  const bool arr = !lean && nb > 1 && !s->has_pass && array_lean_eligible(c->hdesc, ops) &&
-                   !getenv_flag("FSG_NO_ARRAY_LEAN");
+  const bool arr = !lean && nb > 1 && !s->has_pass && array_lean_eligible(c->hdesc, ops);
   if (lean || arr) HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
-  if (flat) {
-    HIPCHK(c->bwin.ensure((size_t)std::max<uint32_t>(nb, 1) * sizeof(BatchWin)));
-    ea.bwin = c->bwin.as<BatchWin>();
-  }
-  launch_eval(ea, ops, flat ? EVAL_FLAT : lean ? EVAL_LEAN : arr ? EVAL_ARRAY : EVAL_EXACT, st);
+  launch_eval(ea, ops, lean ? EVAL_LEAN : arr ? EVAL_ARRAY : EVAL_EXACT, st);
   HIPCHK(hipGetLastError());
   if (c->timed) HIPCHK(hipEventRecord(c->ev[1], st));
   launch_mins(ea.bstat, nb, ea.mins, st);
@@ -2135,7 +2119,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   if (dedup) HIPCHK(hipMemcpyAsync(sfs, sfa.scal, sizeof sfs, hipMemcpyDeviceToHost, st));
   HIPCHK(wait_stream(st));
   memcpy(&c->hplan, c->hpin.p, sizeof(Plan));
-  c->last.eval_path = flat ? FSG_EVAL_FLAT : lean ? FSG_EVAL_LEAN : arr ? FSG_EVAL_ARRAY : FSG_EVAL_EXACT;
+  c->last.eval_path = lean ? FSG_EVAL_LEAN : arr ? FSG_EVAL_ARRAY : FSG_EVAL_EXACT;
   c->last.deferred = 0;
   if (lean || arr) memcpy(&c->last.deferred, (const uint8_t*)c->hpin.p + sizeof(Plan), sizeof(uint32_t));
   if (dedup) {
@@ -2940,10 +2924,11 @@ struct fsg_keyed {
 };
 
 namespace {
+// table slots: a power of two >= n (callers bound n to 2^31, the u32 slot range)
 uint32_t pow2_at_least(uint64_t n) {
-  uint32_t c = 16;
+  uint64_t c = 16;
   while (c < n) c <<= 1;
-  return c;
+  return (uint32_t)c;
 }
 // room for `nk` more keys and `nbytes` more key bytes (grows and rehashes; rare)
 int kd_reserve(fsg_keyed* k, uint64_t nk, uint64_t nbytes) {
@@ -2959,6 +2944,7 @@ int kd_reserve(fsg_keyed* k, uint64_t nk, uint64_t nbytes) {
   HIPCHK(nko.ensure(kc * 8));
   HIPCHK(nkl.ensure(kc * 4));
   HIPCHK(nv.ensure(kc * 4));
+  if (2 * kc > (1ull << 31)) return fail(FSG_E_UNSUPPORTED, "keyed table past 2^30 keys");
   const uint32_t cap = pow2_at_least(2 * kc);
   HIPCHK(ns.ensure((size_t)cap * 4));
   HIPCHK(hipMemsetAsync(ns.p, 0, (size_t)cap * 4, st));
@@ -3088,6 +3074,7 @@ extern "C" int fsg_keyed_allreduce(fsg_keyed* k, size_t* n_keys, size_t* key_byt
   if (!rc) rc = kd_gather(k, k->arena.p, k->garena.p, maxb, ncclUint8, 1);
   if (e->comm) ncclGroupEnd();
   if (rc) return rc;
+  if (2ull * nitems > (1ull << 31)) return fail(FSG_E_UNSUPPORTED, "keyed merge past 2^30 gathered keys");
   const uint32_t ucap = pow2_at_least(2ull * nitems);
   HIPCHK(k->uslot.ensure((size_t)ucap * 4));
   HIPCHK(hipMemsetAsync(k->uslot.p, 0, (size_t)ucap * 4, st));

@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define FSG_ABI_VERSION 3
+#define FSG_ABI_VERSION 4 /* 4: fsg_timings gained eval_path / deferred; fsg_keyed_*, fsg_host_cache_trim */
 
 /* ---- status codes (mirror EngineError and the guest status enums) ---- */
 #define FSG_OK 0
@@ -166,7 +166,7 @@ typedef struct fsg_timings {
 } fsg_timings;
 #define FSG_EVAL_EXACT 0 /* k_eval over every batch */
 #define FSG_EVAL_LEAN 1  /* k_eval_lean (LDS windows), deferred batches through k_eval */
-#define FSG_EVAL_FLAT 2  /* k_flat (register-resident substring scan), deferred batches through k_eval */
+/* 2: retired (an opt-in register-resident substring path, slower than k_eval_lean on MI355X) */
 #define FSG_EVAL_ARRAY 3 /* k_arr_lean (array_map lane per record), deferred batches through k_eval */
 
 const char *fsg_last_error_message(void);

@@ -675,8 +675,9 @@ static int rx_property(rxparser *P, int neg, cset *set) {
 }
 
 /* (?i): regex-syntax's simple case folding, restated for ASCII letters: a-z <-> A-Z,
- * plus the two non-ASCII code points that fold to ASCII letters (U+212A KELVIN SIGN
- * ~ k, U+017F LONG S ~ s).  A literal outside ASCII under (?i) is unsupported. */
+ * plus, in Unicode mode only, the two non-ASCII code points that fold to ASCII
+ * letters (U+212A KELVIN SIGN ~ k, U+017F LONG S ~ s); (?-u) folds bytes (ASCII).
+ * A literal outside ASCII under (?i) is unsupported. */
 static void cs_add_folded(rxparser *P, cset *s, uint32_t lo, uint32_t hi) {
   cs_add(s, lo, hi);
   if (!P->fi) return;
@@ -689,6 +690,7 @@ static void cs_add_folded(rxparser *P, cset *s, uint32_t lo, uint32_t hi) {
   a = lo > 'A' ? lo : 'A';
   b = hi < 'Z' ? hi : 'Z';
   if (a <= b) cs_add(s, a + 32, b + 32);
+  if (!P->fu) return;
   if ((lo <= 'k' && 'k' <= hi) || (lo <= 'K' && 'K' <= hi)) cs_add(s, 0x212A, 0x212A);
   if ((lo <= 's' && 's' <= hi) || (lo <= 'S' && 'S' <= hi)) cs_add(s, 0x17F, 0x17F);
 }
@@ -899,8 +901,19 @@ static anode *rx_parse_class(rxparser *P) {
       lo = c;
     }
     uint32_t hi = lo;
-    if (P->i + 1 < P->n && P->p[P->i] == '-' && P->p[P->i + 1] != ']') {
-      P->i++;
+    /* parse_set_class_range: bump_space, then '-' starts a range unless the next
+     * non-space char is ']' or '-' */
+    rx_skip_x(P);
+    size_t nx = P->i + 1;
+    if (P->fx && P->i < P->n) {
+      const size_t at_dash = P->i;
+      P->i = nx;
+      rx_skip_x(P);
+      nx = P->i;
+      P->i = at_dash;
+    }
+    if (P->i < P->n && P->p[P->i] == '-' && nx < P->n && P->p[nx] != ']' && P->p[nx] != '-') {
+      P->i = nx;
       uint32_t c2 = P->p[P->i++];
       if (c2 == '\\') {
         cset tmp = {0};
@@ -916,6 +929,10 @@ static anode *rx_parse_class(rxparser *P) {
         P->err = 1;
         return a;
       }
+    }
+    if (!P->fu && hi >= 0x80) { /* class_literal_byte: UnicodeNotAllowed in a (?-u) class */
+      P->err = 1;
+      return a;
     }
     cs_add_folded(P, &a->cls, lo, hi);
   }

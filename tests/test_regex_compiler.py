@@ -108,3 +108,30 @@ def test_random_patterns_match_oracle():
             assert dfa_match(pat, t)[0] == O.regex_is_match(pat, t), (pat, t)
             n += 1
     assert n > 1000 and too_large < 20, (n, too_large)
+
+
+@pytest.mark.parametrize("pattern,text,expect", [
+    # (?i) folds KELVIN SIGN / LONG S to k / s only in Unicode mode; (?-u) folds ASCII bytes
+    (r"(?i)k", "K", True), (r"(?i-u)k", "K", False), (r"(?i)s", "ſ", True),
+    (r"(?i-u)s", "ſ", False), (r"(?i-u)[[:alpha:]]", "K", False), (r"(?i-u)K", "k", True),
+    (r"(?i)[[:alpha:]]", "K", True),
+    # (?x): whitespace around a class range's '-' is skipped (parse_set_class_range's bump_space)
+    (r"(?x)[a - z]", "m", True), (r"(?x)[a - z]", "-", False), (r"(?x)[a - ]", "-", True),
+    (r"(?x)[ a -z ]x", "qx", True), (r"[a - z]", "-", False), (r"[a - z]", " ", True), (r"[a - z]", "m", False),
+])
+def test_fold_and_x_ranges(pattern, text, expect):
+    b = text.encode()
+    assert O.regex_is_match(pattern, b) == expect
+    assert dfa_match(pattern, b)[0] == expect
+
+
+@pytest.mark.parametrize("bad", [r"(?-u)[é]", r"(?-u)[a-é]", r"(?-u)[é]"])
+def test_non_ascii_class_literal_without_unicode(bad):
+    """class_literal_byte: a literal outside ASCII in a (?-u) class is
+    UnicodeNotAllowed (an init error); outside a class it stays a literal."""
+    with pytest.raises(ValueError) as e:
+        dfa_match(bad, b"x")
+    assert e.value.args[0] == _ffi.FSG_E_INIT
+    with pytest.raises(ValueError):
+        O.regex_is_match(bad, b"x")
+    assert dfa_match(r"(?-u)é", "é".encode())[0] and O.regex_is_match(r"(?-u)é", "é".encode())
