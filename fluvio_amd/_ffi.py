@@ -140,6 +140,9 @@ SIGNATURES = {
                                       SZ]),
     "fsg_keyed_device": (ctypes.c_int, [VP, PP, PP, PP]),
     "fsg_keyed_free": (None, [VP]),
+    "fsg_keyed_allreduce_sim": (ctypes.c_int, [VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64),
+                                               PP, PP, ctypes.POINTER(ctypes.c_uint64), PP, ctypes.POINTER(SZ),
+                                               ctypes.POINTER(SZ)]),
 }
 
 FSG_DTYPE_I32, FSG_DTYPE_U32, FSG_DTYPE_I64, FSG_DTYPE_U64, FSG_DTYPE_F64 = range(5)

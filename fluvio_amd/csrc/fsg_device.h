@@ -513,6 +513,10 @@ struct KdTable {
   unsigned long long* cnt;  // [0] keys [1] arena bytes
 };
 constexpr uint32_t kKdDead = 0xFFFFFFFFu;
+// gathered key descriptors (k_kd_desc): arena offset | length << 40; this
+// length marks an entry with no key (a lost duplicate, or padding to maxn)
+constexpr uint64_t kKdLenDead = 0xFFFFFFull;
+constexpr uint64_t kKdLenDeadDesc = kKdLenDead << 40;
 struct KdUnionArgs {
   const uint64_t* gdesc;   // all-gathered descriptors: rank r's key i at r * maxn + i
   const uint8_t* garena;   // all-gathered arenas: rank r's at r * maxb

@@ -468,7 +468,6 @@ __device__ __forceinline__ const uint8_t* kd_item(const uint8_t* garena, uint64_
                                                   uint32_t g) {
   return garena + (uint64_t)(g / maxn) * maxb + (d & ((1ull << 40) - 1ull));
 }
-constexpr uint64_t kKdLenDead = 0xFFFFFFull;
 __global__ __launch_bounds__(256) void k_kd_union(uint32_t* slot, uint32_t cap, const uint64_t* gdesc,
                                                   const uint8_t* garena, uint64_t maxb, uint32_t maxn, uint32_t nitems,
                                                   uint32_t* gslot) {

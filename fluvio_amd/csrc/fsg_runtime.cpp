@@ -3037,22 +3037,44 @@ extern "C" int fsg_keyed_collect(fsg_keyed* k, fsg_chain* c0, size_t stage0) {
   return FSG_OK;
 }
 
+// the other ranks' send buffers, supplied by the caller (fsg_keyed_allreduce_sim)
+struct KdSim {
+  const uint64_t* n;
+  const uint64_t* const* desc;
+  const uint8_t* const* arena;
+  const uint64_t* arena_len;
+  const uint32_t* const* vals;
+};
+
 // The topic dictionary: every rank's key list all-gathered, the union built on
 // every rank (ids by first occurrence in rank order), then one all-reduce of
 // the dense K-slot u32 table.  World 1 (no communicator): the same steps with
-// device copies in place of the collectives.
-extern "C" int fsg_keyed_allreduce(fsg_keyed* k, size_t* n_keys, size_t* key_bytes) {
+// device copies in place of the collectives.  `sim`: this rank is `me` of `nr`
+// and the other ranks' gathered inputs come from the caller (uploads in place
+// of the all-gathers, their dense scatters summed in place of the all-reduce).
+static int kd_allreduce(fsg_keyed* k, int nr, int me, const KdSim* sim, size_t* n_keys, size_t* key_bytes) {
   fsg_engine* e = k->eng;
   HIPCHK(hipSetDevice(e->device));
   hipStream_t st = k->st;
-  const int nr = e->comm ? e->nranks : 1, me = e->comm ? e->rank : 0;
+  const bool nccl = e->comm && !sim;
   HIPCHK(k->gcnt.ensure((size_t)nr * 16));
   HIPCHK(k->tot.ensure(64));
-  int rc = kd_gather(k, k->cnt.p, k->gcnt.p, 2, ncclUint64, 8);
-  if (rc) return rc;
   std::vector<unsigned long long> gc((size_t)nr * 2);
-  HIPCHK(hipMemcpyAsync(gc.data(), k->gcnt.p, gc.size() * 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  int rc = FSG_OK;
+  if (sim) {
+    HIPCHK(hipMemcpyAsync(gc.data() + 2 * me, k->cnt.p, 16, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (int r = 0; r < nr; r++)
+      if (r != me) {
+        gc[2 * r] = sim->n[r];
+        gc[2 * r + 1] = sim->arena_len[r];
+      }
+  } else {
+    rc = kd_gather(k, k->cnt.p, k->gcnt.p, 2, ncclUint64, 8);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(gc.data(), k->gcnt.p, gc.size() * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
   uint64_t maxn = 1, maxb = 16;
   for (int r = 0; r < nr; r++) {
     maxn = std::max<uint64_t>(maxn, gc[2 * r]);
@@ -3069,11 +3091,29 @@ extern "C" int fsg_keyed_allreduce(fsg_keyed* k, size_t* n_keys, size_t* key_byt
   HIPCHK(k->gdesc.ensure((size_t)nitems * 8));
   HIPCHK(k->garena.ensure((size_t)nr * maxb + 16));
   launch_kd_desc(k->table(), (uint32_t)nloc, (uint32_t)maxn, k->ldesc.as<uint64_t>(), st);
-  if (e->comm) ncclGroupStart();
-  rc = kd_gather(k, k->ldesc.p, k->gdesc.p, maxn, ncclUint64, 8);
-  if (!rc) rc = kd_gather(k, k->arena.p, k->garena.p, maxb, ncclUint8, 1);
-  if (e->comm) ncclGroupEnd();
-  if (rc) return rc;
+  std::vector<uint64_t> hdesc;
+  std::vector<uint8_t> harena;
+  if (sim) {  // this rank's buffers at its slot, the others' uploaded padded to maxn / maxb
+    hdesc.assign((size_t)nr * maxn, kKdLenDeadDesc);
+    harena.assign((size_t)nr * maxb, 0);
+    for (int r = 0; r < nr; r++) {
+      if (r == me) continue;
+      for (uint64_t i = 0; i < sim->n[r]; i++) hdesc[(size_t)r * maxn + i] = sim->desc[r][i];
+      if (sim->arena_len[r]) memcpy(harena.data() + (size_t)r * maxb, sim->arena[r], sim->arena_len[r]);
+    }
+    HIPCHK(hipMemcpyAsync(k->gdesc.p, hdesc.data(), hdesc.size() * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(k->garena.p, harena.data(), harena.size(), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(k->gdesc.as<uint64_t>() + (size_t)me * maxn, k->ldesc.p, maxn * 8,
+                          hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(k->garena.as<uint8_t>() + (size_t)me * maxb, k->arena.p, maxb, hipMemcpyDeviceToDevice,
+                          st));
+  } else {
+    if (e->comm) ncclGroupStart();
+    rc = kd_gather(k, k->ldesc.p, k->gdesc.p, maxn, ncclUint64, 8);
+    if (!rc) rc = kd_gather(k, k->arena.p, k->garena.p, maxb, ncclUint8, 1);
+    if (e->comm) ncclGroupEnd();
+    if (rc) return rc;
+  }
   if (2ull * nitems > (1ull << 31)) return fail(FSG_E_UNSUPPORTED, "keyed merge past 2^30 gathered keys");
   const uint32_t ucap = pow2_at_least(2ull * nitems);
   HIPCHK(k->uslot.ensure((size_t)ucap * 4));
@@ -3118,7 +3158,25 @@ extern "C" int fsg_keyed_allreduce(fsg_keyed* k, size_t* n_keys, size_t* key_byt
   launch_kd_ids(u, st);
   launch_kd_place(u, K, st);
   HIPCHK(hipGetLastError());
-  if (e->comm && K) {  // u32 sums wrap, like the guest's release-mode adds
+  DevBuf sv;
+  if (sim && K) {  // the all-reduce: every other rank's values scattered by the same union ids
+    HIPCHK(sv.ensure((size_t)nr * maxn * 4));
+    std::vector<uint32_t> hv((size_t)nr * maxn, 0);
+    for (int r = 0; r < nr; r++)
+      if (r != me)
+        for (uint64_t i = 0; i < sim->n[r]; i++) hv[(size_t)r * maxn + i] = sim->vals[r][i];
+    HIPCHK(hipMemcpyAsync(sv.p, hv.data(), hv.size() * 4, hipMemcpyHostToDevice, st));
+    for (int r = 0; r < nr; r++) {
+      if (r == me) continue;
+      KdUnionArgs o = u;
+      o.me = (uint32_t)r;
+      o.lval = sv.as<uint32_t>() + (size_t)r * maxn;
+      launch_kd_place(o, K, st);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st));  // sv and the host vectors go out of scope
+  }
+  if (nccl && K) {  // u32 sums wrap, like the guest's release-mode adds
     ncclResult_t r = ncclAllReduce(k->dense.p, k->dense.p, K, ncclUint32, ncclSum, e->comm, st);
     if (r != ncclSuccess) return fail(FSG_E_DEVICE, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
   }
@@ -3131,6 +3189,22 @@ extern "C" int fsg_keyed_allreduce(fsg_keyed* k, size_t* n_keys, size_t* key_byt
   if (n_keys) *n_keys = K;
   if (key_bytes) *key_bytes = ub;
   return FSG_OK;
+}
+
+extern "C" int fsg_keyed_allreduce(fsg_keyed* k, size_t* n_keys, size_t* key_bytes) {
+  fsg_engine* e = k->eng;
+  return kd_allreduce(k, e->comm ? e->nranks : 1, e->comm ? e->rank : 0, nullptr, n_keys, key_bytes);
+}
+
+extern "C" int fsg_keyed_allreduce_sim(fsg_keyed* k, uint32_t nranks, uint32_t me, const uint64_t* rank_n,
+                                       const uint64_t* const* rank_desc, const uint8_t* const* rank_arena,
+                                       const uint64_t* rank_arena_len, const uint32_t* const* rank_vals,
+                                       size_t* n_keys, size_t* key_bytes) {
+  if (!nranks || me >= nranks || nranks > 1024 || !rank_n || !rank_desc || !rank_arena || !rank_arena_len ||
+      !rank_vals)
+    return fail(FSG_E_INVALID_ARG, "fsg_keyed_allreduce_sim: bad rank arguments");
+  const KdSim sim{rank_n, rank_desc, rank_arena, rank_arena_len, rank_vals};
+  return kd_allreduce(k, (int)nranks, (int)me, &sim, n_keys, key_bytes);
 }
 
 extern "C" int fsg_keyed_read(fsg_keyed* k, uint8_t* keys, size_t key_bytes, uint64_t* offs, uint32_t* vals,

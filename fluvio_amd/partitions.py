@@ -143,23 +143,91 @@ def union_dictionary(key_lists: Sequence[Sequence[bytes]]) -> Dict[bytes, int]:
     return ids
 
 
+KD_LEN_DEAD = 0xFFFFFF  # fsg_keyed.hip kKdLenDead: a descriptor with no key (a lost duplicate / padding)
+
+
+def keyed_desc(keys: Sequence[Optional[bytes]]):
+    """One rank's send buffers of fsg_keyed_allreduce (k_kd_desc): per key a u64
+    descriptor `arena offset | length << 40` (None = a dead entry) and the key
+    bytes packed in an arena."""
+    desc, arena = [], bytearray()
+    for k in keys:
+        if k is None:
+            desc.append(KD_LEN_DEAD << 40)
+            continue
+        desc.append(len(arena) | (len(k) << 40))
+        arena += k
+    return desc, bytes(arena)
+
+
+def gather_shape(counts: Sequence[Sequence[int]]):
+    """maxn / maxb of the all-gathers from every rank's (keys, arena bytes):
+    at least one entry and 16 bytes, bytes rounded up to 16."""
+    maxn = max([1] + [int(c[0]) for c in counts])
+    maxb = max([16] + [int(c[1]) for c in counts])
+    return maxn, (maxb + 15) & ~15
+
+
+def union_from_gathered(gdesc: Sequence[int], garena: bytes, maxn: int, maxb: int):
+    """k_kd_union / k_kd_first / k_kd_ids over the gathered buffers: item
+    g = rank * maxn + i, a live item's key at garena[rank * maxb + off ..], union
+    ids by first occurrence in item (rank-major) order.  -> (id per item or None,
+    union keys in id order)."""
+    ids: Dict[bytes, int] = {}
+    gid: List[Optional[int]] = []
+    for g, d in enumerate(gdesc):
+        ln = d >> 40
+        if ln == KD_LEN_DEAD:
+            gid.append(None)
+            continue
+        off = (g // maxn) * maxb + (d & ((1 << 40) - 1))
+        k = bytes(garena[off:off + ln])
+        if k not in ids:
+            ids[k] = len(ids)
+        gid.append(ids[k])
+    return gid, list(ids)
+
+
 def merge_keyed(local: Dict[bytes, int], dist=None, group=None) -> Dict[bytes, int]:
-    """Topic-wide per-key totals of aggregate-json states with the shape of the
-    C ABI's merge (fsg_keyed_allreduce): every rank's exact key list all-gathered,
-    the union dictionary built in rank order, this rank's values scattered into a
-    dense K-slot table, one all-reduce (sum), u32 wrapping.  gloo on CPU ranks;
-    the GPU path runs the same steps on HBM with RCCL (smartengine.KeyedState)."""
+    """Topic-wide per-key totals of aggregate-json states in the C ABI's shape
+    (fsg_keyed_allreduce, fsg_runtime.cpp): all-gather every rank's (keys, arena
+    bytes); all-gather the key descriptors (padded to maxn with dead entries) and
+    the arenas (padded to maxb); the union dictionary built identically on every
+    rank; this rank's values scattered into a dense K-slot table; one all-reduce
+    (sum, u32 wrapping).  gloo on CPU ranks; the GPU path runs the same steps on
+    HBM with RCCL (smartengine.KeyedState)."""
     import torch
     keys = list(local)
-    if dist is not None and dist.is_initialized() and dist.get_world_size(group) > 1:
-        gathered = [None] * dist.get_world_size(group)
-        dist.all_gather_object(gathered, keys, group=group)
+    desc, arena = keyed_desc(keys)
+    multi = dist is not None and dist.is_initialized() and dist.get_world_size(group) > 1
+    nr = dist.get_world_size(group) if multi else 1
+    me = dist.get_rank(group) if multi else 0
+    cnt = torch.tensor([len(desc), len(arena)], dtype=torch.int64)
+    gcnt = [torch.zeros(2, dtype=torch.int64) for _ in range(nr)]
+    if multi:
+        dist.all_gather(gcnt, cnt, group=group)
     else:
-        gathered = [keys]
-    ids = union_dictionary(gathered)
-    dense = torch.zeros(len(ids), dtype=torch.int64)
-    for k, v in local.items():
-        dense[ids[k]] += int(v)
-    if dist is not None and dist.is_initialized() and dist.get_world_size(group) > 1:
+        gcnt = [cnt]
+    maxn, maxb = gather_shape([c.tolist() for c in gcnt])
+    # u64 descriptors travel as int64 bit patterns
+    ld = torch.tensor([d - (1 << 64) if d >> 63 else d for d in desc + [KD_LEN_DEAD << 40] * (maxn - len(desc))],
+                      dtype=torch.int64)
+    la = torch.zeros(maxb, dtype=torch.uint8)
+    if arena:
+        la[:len(arena)] = torch.frombuffer(bytearray(arena), dtype=torch.uint8)
+    gd = [torch.zeros(maxn, dtype=torch.int64) for _ in range(nr)]
+    ga = [torch.zeros(maxb, dtype=torch.uint8) for _ in range(nr)]
+    if multi:
+        dist.all_gather(gd, ld, group=group)
+        dist.all_gather(ga, la, group=group)
+    else:
+        gd, ga = [ld], [la]
+    gdesc = [int(x) & _M64 for t in gd for x in t.tolist()]
+    garena = b"".join(bytes(t.tolist()) for t in ga)
+    gid, ukeys = union_from_gathered(gdesc, garena, maxn, maxb)
+    dense = torch.zeros(len(ukeys), dtype=torch.int64)
+    for i, k in enumerate(keys):  # k_kd_place: this rank's items
+        dense[gid[me * maxn + i]] += int(local[k])
+    if multi:
         dist.all_reduce(dense, op=dist.ReduceOp.SUM, group=group)
-    return {k: int(dense[i]) & 0xFFFFFFFF for k, i in ids.items()}
+    return {k: int(dense[i]) & 0xFFFFFFFF for i, k in enumerate(ukeys)}

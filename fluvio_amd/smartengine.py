@@ -395,6 +395,33 @@ class KeyedState:
         self.n_keys, self.key_bytes = n.value, b.value
         return n.value
 
+    def allreduce_simulated(self, me: int, ranks) -> int:
+        """fsg_keyed_allreduce_sim: this table as rank `me`, `ranks[r]` = rank r's
+        (key list with None for a dead entry, values) for r != me."""
+        from . import partitions as PT
+        nr = len(ranks)
+        n = (ctypes.c_uint64 * nr)()
+        alen = (ctypes.c_uint64 * nr)()
+        dptr, aptr, vptr = (ctypes.c_void_p * nr)(), (ctypes.c_void_p * nr)(), (ctypes.c_void_p * nr)()
+        keep = []
+        for r, item in enumerate(ranks):
+            if r == me or item is None:
+                continue
+            keys, vals = item
+            desc, arena = PT.keyed_desc(keys)
+            d = (ctypes.c_uint64 * max(len(desc), 1))(*desc)
+            a = ctypes.create_string_buffer(arena, max(len(arena), 1))
+            v = (ctypes.c_uint32 * max(len(vals), 1))(*vals)
+            keep += [d, a, v]
+            n[r], alen[r] = len(desc), len(arena)
+            dptr[r], aptr[r], vptr[r] = ctypes.cast(d, ctypes.c_void_p), ctypes.cast(a, ctypes.c_void_p), \
+                ctypes.cast(v, ctypes.c_void_p)
+        nk, b = ctypes.c_size_t(), ctypes.c_size_t()
+        _check(_ffi.lib().fsg_keyed_allreduce_sim(self._h, nr, me, n, dptr, aptr, alen, vptr, ctypes.byref(nk),
+                                                  ctypes.byref(b)))
+        self.n_keys, self.key_bytes = nk.value, b.value
+        return nk.value
+
     def read(self) -> Dict[bytes, int]:
         n = self.n_keys
         keys = ctypes.create_string_buffer(max(self.key_bytes, 1))

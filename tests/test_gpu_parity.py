@@ -1516,3 +1516,39 @@ def test_flat_needle_at_window_edges(engine):
         b2 = P.Batch(base_offset=200)
         b2.add_record(P.Record.new(b"timeou"))
         check_batch(engine, [("filter_init", {"key": "timeout"}, None)], b.encode() + b2.encode())
+
+
+@pytest.mark.parametrize("nr", range(2, 9))
+def test_keyed_merge_simulated_ranks(engine, nr):
+    """The multi-rank branch of fsg_keyed_allreduce (maxn / maxb padding,
+    rank-offset arenas, union ids by first occurrence in rank order, dense
+    placement per rank) on one GPU: this table is rank `me` of `nr`, the other
+    ranks' gathered key lists come from the host (unequal counts, shared and
+    disjoint keys, dead entries, empty ranks).  Totals against a host union."""
+    import json
+    import random
+    from fluvio_amd.smartengine import KeyedState
+    rng = random.Random(100 + nr)
+    pool = ["k%03d" % i for i in range(70)] + ["", "x" * 40, "é"]
+    me = rng.randrange(nr)
+    local = {}
+    ks = KeyedState(engine)
+    for c in range(rng.choice([1, 3])):  # this rank's table: chains that never ran (initial accumulators)
+        d = {k: rng.randint(0, 2 ** 32 - 1) for k in rng.sample(pool, rng.randint(0, 30))}
+        ks.collect(gpu_chain(engine, [("aggregate-json", {}, json.dumps(d).encode())]))
+        for k, v in d.items():
+            local[k.encode()] = (local.get(k.encode(), 0) + v) & 0xFFFFFFFF
+    ranks, expect = [], dict(local)
+    for r in range(nr):
+        if r == me:
+            ranks.append(None)
+            continue
+        keys = [k.encode() for k in rng.sample(pool, rng.choice([0, 1, 7, 40, 70]))]
+        keys = [None if rng.random() < 0.1 else k for k in keys]
+        vals = [rng.randint(0, 2 ** 32 - 1) for _ in keys]
+        for k, v in zip(keys, vals):
+            if k is not None:
+                expect[k] = (expect.get(k, 0) + v) & 0xFFFFFFFF
+        ranks.append((keys, vals))
+    assert ks.allreduce_simulated(me, ranks) == len(expect)
+    assert ks.read() == expect

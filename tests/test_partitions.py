@@ -175,3 +175,32 @@ def test_two_rank_keyed_merge(tmp_path):
     for r in range(world):
         got = {k.encode(): int(v) for k, v in (x.split(":") for x in open(tmp_path / f"keyed{r}.txt").read().split())}
         assert got == expect
+
+
+@pytest.mark.parametrize("nr", range(2, 9))
+def test_union_of_simulated_ranks(nr):
+    """The union step of fsg_keyed_allreduce on N = 2..8 simulated gathered key
+    lists (unequal counts, shared and disjoint keys, dead entries, padding to
+    maxn / maxb) against a host union built straight from the key lists."""
+    import random
+    rng = random.Random(nr)
+    pool = [b"k%03d" % i for i in range(60)] + [b"", b"x" * 40, "é".encode()]
+    lists = []
+    for r in range(nr):
+        n = rng.choice([0, 1, 5, 17, 40])
+        ks = rng.sample(pool, min(n, len(pool)))
+        lists.append([None if rng.random() < 0.1 else k for k in ks])
+    sends = [PT.keyed_desc(ks) for ks in lists]
+    maxn, maxb = PT.gather_shape([(len(d), len(a)) for d, a in sends])
+    gdesc, garena = [], b""
+    for d, a in sends:
+        gdesc += d + [PT.KD_LEN_DEAD << 40] * (maxn - len(d))
+        garena += a + bytes(maxb - len(a))
+    gid, ukeys = PT.union_from_gathered(gdesc, garena, maxn, maxb)
+    expect = PT.union_dictionary([[k for k in ks if k is not None] for ks in lists])
+    assert ukeys == list(expect)
+    for r, ks in enumerate(lists):
+        for i, k in enumerate(ks):
+            assert gid[r * maxn + i] == (None if k is None else expect[k])
+        for i in range(len(ks), maxn):
+            assert gid[r * maxn + i] is None
