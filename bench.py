@@ -30,7 +30,6 @@ import hashlib
 import json
 import os
 import sys
-import threading
 import time
 
 import numpy as np
@@ -376,7 +375,7 @@ def run_c5(ctx, cpu):
     from fluvio_amd import partitions as PT
     from fluvio_amd import synth
     from fluvio_amd.smartengine import (PartitionState, ResidentSlice, SmartEngine, SmartModuleChainBuilder,
-                                        SmartModuleConfig, builtin, comm_unique_id)
+                                        SmartModuleConfig, builtin, comm_unique_id, process_slices)
     a = ctx.a
     P, nrec = C5["partitions"], C5["records_per_partition"]
     engine = SmartEngine(ctx.local)
@@ -397,28 +396,18 @@ def run_c5(ctx, cpu):
         chains[p] = b.initialize(engine)
         rsl[p] = ResidentSlice(engine, slices[p])
     state = PartitionState(engine, P)
-    nthreads = min(16, len(owned)) or 1
-    groups = [owned[i::nthreads] for i in range(nthreads)]
     kms = {"eval_ms": 0.0, "write_ms": 0.0, "crc_ms": 0.0, "total_ms": 0.0}
     out_bytes = [0]
-    lock = threading.Lock()
-
-    def work(ps):  # one host thread drives a group of partitions, each on its own chain stream
-        for p in ps:
-            chains[p].process_slice(rsl[p], download=False)
-            state.collect(p, chains[p])
-            t = chains[p].last_timings()
-            with lock:
-                for k in kms:
-                    kms[k] += t[k]
-                out_bytes[0] += t["out_bytes"]
+    clist, slist = [chains[p] for p in owned], [rsl[p] for p in owned]
 
     def step():
-        th = [threading.Thread(target=work, args=(g,)) for g in groups if g]
-        for x in th:
-            x.start()
-        for x in th:
-            x.join()
+        process_slices(clist, slist)  # every owned partition's chain in one call, concurrently
+        for p in owned:
+            state.collect(p, chains[p])
+            t = chains[p].last_timings()
+            for k in kms:
+                kms[k] += t[k]
+            out_bytes[0] += t["out_bytes"]
         state.allreduce()  # RCCL sum over xGMI: the topic-wide per-partition table on every rank
 
     for _ in range(a.warmup):
@@ -450,7 +439,8 @@ def run_c5(ctx, cpu):
            "ms_per_step": elapsed / a.steps * 1e3, "scaling": "strong", "dtype": "i32",
            "config": {"workload": "c5-agg-sum", "description": C5["description"], "partitions": P,
                       "records_per_partition": nrec, "partitions_per_gpu": len(owned),
-                      "slice_bytes_this_gpu": in_bytes, "host_threads": nthreads,
+                      "slice_bytes_this_gpu": in_bytes,
+                      "host_call": "fsg_chain_group_process_slices (one call, every owned chain)",
                       "parallelism": f"partitions sharded p -> rank p mod {ctx.world}"},
            "kernel_ms_sum_over_partitions": per,
            "gbps_input_per_gpu": in_bytes * a.steps / elapsed / 1e9,
@@ -478,7 +468,7 @@ def run_c5k(ctx, cpu):
     from fluvio_amd import partitions as PT
     from fluvio_amd import synth
     from fluvio_amd.smartengine import (KeyedState, ResidentSlice, SmartEngine, SmartModuleChainBuilder,
-                                        SmartModuleConfig, builtin, comm_unique_id)
+                                        SmartModuleConfig, builtin, comm_unique_id, process_slices)
     a = ctx.a
     P, nrec = C5K["partitions"], C5K["records_per_partition"]
     engine = SmartEngine(ctx.local)
@@ -499,27 +489,19 @@ def run_c5k(ctx, cpu):
         rsl[p] = ResidentSlice(engine, raw[p])
     del raw
     keyed = KeyedState(engine)
-    nthreads = min(16, len(owned)) or 1
-    groups = [owned[i::nthreads] for i in range(nthreads)]
     kms = {"eval_ms": 0.0, "plan_ms": 0.0, "write_ms": 0.0, "crc_ms": 0.0, "total_ms": 0.0}
     out_bytes = [0]
-    lock = threading.Lock()
-
-    def work(ps):  # one host thread drives a group of partitions, each on its own chain stream
-        for p in ps:
-            chains[p].process_slice(rsl[p], download=False)
-            t = chains[p].last_timings()
-            with lock:
-                for k in kms:
-                    kms[k] += t[k]
-                out_bytes[0] += t["out_bytes"]
+    clist, slist = [chains[p] for p in owned], [rsl[p] for p in owned]
 
     def step():
-        th = [threading.Thread(target=work, args=(g,)) for g in groups if g]
-        for x in th:
-            x.start()
-        for x in th:
-            x.join()
+        # every owned partition's chain in one call (fsg_chain_group_process_slices:
+        # the chains run concurrently, their aggregate-json order walks as one launch)
+        process_slices(clist, slist)
+        for c in clist:
+            t = c.last_timings()
+            for k in kms:
+                kms[k] += t[k]
+            out_bytes[0] += t["out_bytes"]
         # the topic-wide totals: every owned partition's map (exact keys, in HBM)
         # into the rank's table, then the union dictionary + dense u32 all-reduce over RCCL
         keyed.reset()
@@ -558,7 +540,8 @@ def run_c5k(ctx, cpu):
            "config": {"workload": "c5-keyed-agg", "description": C5K["description"], "partitions": P,
                       "records_per_partition": nrec, "keys": C5K["keys"], "partitions_per_gpu": len(owned),
                       "slice_bytes_this_gpu": in_bytes, "output_bytes_this_gpu_per_step": out_bytes[0] / a.steps,
-                      "host_threads": nthreads, "chain": [m[0] for m in C5K["modules"]],
+                      "host_call": "fsg_chain_group_process_slices (one call, every owned chain)",
+                      "chain": [m[0] for m in C5K["modules"]],
                       "parallelism": f"partitions sharded p -> rank p mod {ctx.world}"},
            "kernel_ms_sum_over_partitions": per,
            "gbps_input_per_gpu": in_bytes * a.steps / elapsed / 1e9,

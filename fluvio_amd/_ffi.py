@@ -140,6 +140,9 @@ SIGNATURES = {
                                       SZ]),
     "fsg_keyed_device": (ctypes.c_int, [VP, PP, PP, PP]),
     "fsg_keyed_free": (None, [VP]),
+    "fsg_chain_group_process_slices": (ctypes.c_int, [PP, PP, SZ, ctypes.c_uint64, ctypes.POINTER(fsg_metrics),
+                                                      ctypes.POINTER(ctypes.POINTER(fsg_batch_output)),
+                                                      ctypes.POINTER(ctypes.c_int)]),
     "fsg_keyed_allreduce_sim": (ctypes.c_int, [VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64),
                                                PP, PP, ctypes.POINTER(ctypes.c_uint64), PP, ctypes.POINTER(SZ),
                                                ctypes.POINTER(SZ)]),

@@ -208,26 +208,76 @@ __device__ void hbm_reserve(HbMem& t, HbMem& spare, const uint32_t* hv) {
   spare = o;
 }
 
-// one chain's records in stream order (one 64-lane workgroup)
+// one chain's records in stream order (one 64-lane workgroup).  The walk is a
+// chain of dependent records, so its memory latency is hidden by prefetch: the
+// per-record scalars come 64 records at a time (lane i = record r0 + i, the
+// next tile in flight), and record r + 1's hashes and entries load while
+// record r is placed.
+struct AjTile {
+  uint32_t nk, ne, nnew;
+  uint64_t ko, g0;
+};
+__device__ __forceinline__ AjTile aj_tile(const AggjArgs& a, uint64_t r0) {
+  const uint64_t r = r0 + (threadIdx.x & 63u);
+  AjTile t{0u, 0u, 0u, 0ull, 0ull};
+  if (r < a.n_rec) {
+    t.nk = a.nkr[r];
+    t.ne = a.rne[r];
+    t.nnew = a.rnew[r];
+    t.ko = a.koff[r];
+    t.g0 = a.rent[r];
+  }
+  return t;
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t i) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)i) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)i) << 32);
+}
+struct AjRec {
+  uint32_t nk, ne, nnew;
+  uint64_t ko, g0;
+};
+__device__ __forceinline__ AjRec aj_rec(const AjTile& t, uint32_t i) {
+  return AjRec{(uint32_t)__builtin_amdgcn_readlane((int)t.nk, (int)i),
+               (uint32_t)__builtin_amdgcn_readlane((int)t.ne, (int)i),
+               (uint32_t)__builtin_amdgcn_readlane((int)t.nnew, (int)i), readlane64(t.ko, i), readlane64(t.g0, i)};
+}
 __device__ void aj_order_run(const AggjArgs& a, uint32_t* lds) {
   const uint32_t l = threadIdx.x;
   uint32_t seq = l;       // the previous record's order (lane p = key at position p) when in registers
   bool seq_reg = true;    // ... else in ord at the previous record's slots
+  AjTile cur = aj_tile(a, 0), nxt = aj_tile(a, 64);
+  AjRec q = aj_rec(cur, 0);
+  // record 0's data; then each record issues the next one's
+  uint32_t d_hk = l < q.nk ? a.ord[q.ko + l] : 0u;
+  uint32_t d_ek = l < q.ne ? a.ekid[q.g0 + l] : kSkipEntry;
+  uint32_t d_hr = l < q.ne ? a.hrec[q.g0 + l] : 0u;
+  uint64_t prev_ko = 0;
   for (uint64_t r = 0; r < a.n_rec; r++) {
-    const uint32_t nk = a.nkr[r], ne = a.rne[r];
-    const uint32_t nkb = nk - a.rnew[r];  // keys of the accumulator map (the previous text's)
-    const uint64_t ko = a.koff[r], g0 = a.rent[r];
+    const uint32_t i = (uint32_t)(r & 63u);
+    const uint32_t nk = q.nk, ne = q.ne;
+    const uint32_t nkb = nk - q.nnew;  // keys of the accumulator map (the previous text's)
+    const uint64_t ko = q.ko, g0 = q.g0;
+    const uint32_t hk = d_hk, ek = d_ek, hr = d_hr;
+    // the next record's scalars and data in flight
+    if (r + 1 < a.n_rec) {
+      if (i == 63u) {
+        cur = nxt;
+        nxt = aj_tile(a, r + 65);
+      }
+      q = aj_rec(cur, (uint32_t)((r + 1) & 63u));
+      d_hk = l < q.nk ? a.ord[q.ko + l] : 0u;
+      d_ek = l < q.ne ? a.ekid[q.g0 + l] : kSkipEntry;
+      d_hr = l < q.ne ? a.hrec[q.g0 + l] : 0u;
+    }
     const bool first = r == 0;
     const bool iseq = first && a.iseq != nullptr;
     const uint32_t nseq = iseq ? a.n_iseq : nkb;
     if (nk <= kAjRegKeys && ne <= kAjRegKeys && nseq <= kAjRegKeys) {
       if (!seq_reg) {
         __threadfence();  // lane 0 wrote the previous order
-        seq = l < nkb ? a.ord[a.koff[r - 1] + l] : 0u;
+        seq = l < nkb ? a.ord[prev_ko + l] : 0u;
       }
-      const uint32_t hk = l < nk ? a.ord[ko + l] : 0u;
-      const uint32_t ek = l < ne ? a.ekid[g0 + l] : kSkipEntry;
-      const uint32_t hr = l < ne ? a.hrec[g0 + l] : 0u;
       const uint32_t is = iseq && l < nseq ? a.iseq[l] : 0u;
       HbReg A{0ull, 0u, 0u, 0u};
       for (uint32_t p = 0; p < nseq; p++) {  // the accumulator's text, HashMap::insert per entry
@@ -255,6 +305,7 @@ __device__ void aj_order_run(const AggjArgs& a, uint32_t* lds) {
       if (full) a.ord[ko + pos] = A.pl;
       seq = (uint32_t)__builtin_amdgcn_ds_permute((int)(pos << 2), (int)A.pl);
       seq_reg = true;
+      prev_ko = ko;
       continue;
     }
     // a larger map: tables in LDS (kAjLdsBuckets) or the chain's HBM scratch, lane 0
@@ -262,40 +313,47 @@ __device__ void aj_order_run(const AggjArgs& a, uint32_t* lds) {
       uint32_t* base = a.obmax <= kAjLdsBuckets ? lds : a.oscr;
       const uint32_t bm = a.obmax <= kAjLdsBuckets ? kAjLdsBuckets : a.obmax, ow = (bm + 31u) / 32u;
       HbMem T[4];
-      for (int q = 0; q < 4; q++) T[q] = HbMem{base + q * ow, base + 4u * ow + (uint64_t)q * bm, 0u, 0u};
-      const uint32_t* hk = a.ord + ko;  // by key id
-      const uint32_t* hr = a.hrec + g0;  // by entry
-      const uint32_t* prev = first ? nullptr : a.ord + a.koff[r - 1];
+      for (int t = 0; t < 4; t++) T[t] = HbMem{base + t * ow, base + 4u * ow + (uint64_t)t * bm, 0u, 0u};
+      const uint32_t* hkp = a.ord + ko;  // by key id
+      const uint32_t* hrp = a.hrec + g0;  // by entry
+      const uint32_t* prev = first ? nullptr : a.ord + prev_ko;
       if (!first) __threadfence();  // the previous order, written by the whole wave
       HbMem& A = T[0];
       for (uint32_t p = 0; p < nseq; p++) {
         const uint32_t k = iseq ? a.iseq[p] : first ? p : prev[p];
-        hbm_reserve(A, T[1], hk);
-        if (!(k & kAjDup)) hbm_put(A, k, hk[k]);
+        hbm_reserve(A, T[1], hkp);
+        if (!(k & kAjDup)) hbm_put(A, k, hkp[k]);
       }
       HbMem& R = T[2];
       for (uint32_t j = 0; j < ne; j++) {
-        hbm_reserve(R, T[3], hr);
-        if (a.ekid[g0 + j] != kSkipEntry) hbm_put(R, j, hr[j]);
+        hbm_reserve(R, T[3], hrp);
+        if (a.ekid[g0 + j] != kSkipEntry) hbm_put(R, j, hrp[j]);
       }
-      for (uint32_t i = 0; i < R.B; i++) {
-        if (!hbm_full(R, i)) continue;
-        const uint32_t kid = a.ekid[g0 + R.pl[i]];
+      for (uint32_t b = 0; b < R.B; b++) {
+        if (!hbm_full(R, b)) continue;
+        const uint32_t kid = a.ekid[g0 + R.pl[b]];
         if (kid < nkb) continue;
-        hbm_reserve(A, T[1], hk);
-        hbm_put(A, kid, hk[kid]);
+        hbm_reserve(A, T[1], hkp);
+        hbm_put(A, kid, hkp[kid]);
       }
       // the hashes of this record are read: its order goes over them
-      uint32_t q = 0;
-      for (uint32_t i = 0; i < A.B; i++)
-        if (hbm_full(A, i)) a.ord[ko + q++] = A.pl[i];
+      uint32_t o = 0;
+      for (uint32_t b = 0; b < A.B; b++)
+        if (hbm_full(A, b)) a.ord[ko + o++] = A.pl[b];
     }
     seq_reg = false;
+    prev_ko = ko;
   }
 }
 __global__ __launch_bounds__(64) void k_aggj_order(AggjArgs a) {
   __shared__ uint32_t lds[4u * (kAjLdsBuckets + kAjLdsBuckets / 32u)];
   aj_order_run(a, lds);
+}
+// several chains' order passes in one launch (fsg_chain_group_*): workgroup
+// i walks chain i's records
+__global__ __launch_bounds__(64) void k_aggj_order_group(const AggjArgs* list) {
+  __shared__ uint32_t lds[4u * (kAjLdsBuckets + kAjLdsBuckets / 32u)];
+  aj_order_run(list[blockIdx.x], lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -563,11 +621,16 @@ void launch_aggj_nk(const AggjArgs& a, uint64_t* tsum, hipStream_t s) {
   if (a.n_rec) hipLaunchKernelGGL(k_aggj_nk, dim3(grid1(a.n_rec)), dim3(256), 0, s, a);
   launch_xscan(a.nkr, a.koff, tsum, a.n_rec, a.scal + 6, s);
 }
-// the hashes, then every record's output order (one wave, stream order)
+// every record's key hashes (data-parallel)
+void launch_aggj_hash(const AggjArgs& a, hipStream_t s) {
+  if (a.n_rec) hipLaunchKernelGGL(k_aggj_hash, dim3(grid1(a.n_rec * 64)), dim3(256), 0, s, a);
+}
+// every record's output order (one wave, stream order)
 void launch_aggj_order(const AggjArgs& a, hipStream_t s) {
-  if (!a.n_rec) return;
-  hipLaunchKernelGGL(k_aggj_hash, dim3(grid1(a.n_rec * 64)), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_aggj_order, dim3(1), dim3(64), 0, s, a);
+  if (a.n_rec) hipLaunchKernelGGL(k_aggj_order, dim3(1), dim3(64), 0, s, a);
+}
+void launch_aggj_order_group(const AggjArgs* list, uint32_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_aggj_order_group, dim3(n), dim3(64), 0, s, list);
 }
 void launch_aggj_commit(const AjCommitArgs& c, uint64_t* tsum, int pass, hipStream_t s) {
   if (pass == 0) {  // keys / records through the stop batch, arena bytes (out[0..2])

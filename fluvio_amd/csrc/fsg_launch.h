@@ -43,7 +43,9 @@ void launch_aggj_write(const AggjArgs& a, hipStream_t s);
 // the output key order (fsg_keyed.hip): nkr / koff + scal[6] = ord slots, then
 // (ord, hrec sized) the hashes and k_aggj_order
 void launch_aggj_nk(const AggjArgs& a, uint64_t* tsum, hipStream_t s);
+void launch_aggj_hash(const AggjArgs& a, hipStream_t s);
 void launch_aggj_order(const AggjArgs& a, hipStream_t s);
+void launch_aggj_order_group(const AggjArgs* list, uint32_t n, hipStream_t s);  // one workgroup per chain
 void launch_xscan(const uint32_t* in, uint64_t* out, uint64_t* tsum, uint64_t n, unsigned long long* tot,
                   hipStream_t s);
 // aggregate-json state kept in HBM (fsg_keyed.hip)

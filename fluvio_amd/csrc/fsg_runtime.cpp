@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -468,6 +469,33 @@ struct fsg_slice {
 constexpr size_t kPinPlan = 256;           // pinned block: Plan, then the small output
 constexpr size_t kSmallOut = 1u << 20;    // outputs up to 1 MiB come back through it
 
+// The chains of one fsg_chain_group_process_slices call (the partitions a
+// rank owns) meet once per call at aggregate-json's order pass: a walk over a
+// chain's records in stream order is one workgroup's work, so the group runs
+// every chain's walk in ONE launch (k_aggj_order_group) instead of one small
+// launch per chain serialised on the device's few hardware queues.  Each chain
+// arrives exactly once: with its walk, or empty (no aggregate-json records,
+// an earlier error, a composed chain).
+struct AjGroup {
+  std::mutex mu;
+  std::condition_variable cv;
+  size_t expected = 0, arrived = 0;
+  bool launched = false;
+  int rc = FSG_OK;
+  std::vector<AggjArgs> jobs;
+  std::vector<hipEvent_t> ready;  // per job: its chain's hashes are done
+  int device = 0;
+  hipStream_t st = nullptr;
+  hipEvent_t done = nullptr;
+  void* dlist = nullptr;
+  ~AjGroup() {
+    if (dlist) (void)hipFree(dlist);
+    if (done) (void)hipEventDestroy(done);
+    for (auto e : ready) (void)hipEventDestroy(e);
+    if (st) (void)hipStreamDestroy(st);
+  }
+};
+
 struct fsg_chain {
   fsg_engine* eng = nullptr;
   hipStream_t stream = nullptr;
@@ -506,6 +534,8 @@ struct fsg_chain {
   DevBuf aj_iseq;           // the initial accumulator's entries with repeats (AggjArgs::iseq)
   uint32_t aj_n_iseq = 0;   // 0: no repeated key (ids in order)
   DevBuf aj_nkr, aj_koff, aj_ord, aj_hrec, aj_oscr, aj_inv;
+  AjGroup* group = nullptr;  // set during a group call (fsg_chain_group_process_slices)
+  bool group_arrived = false;
   uint64_t aj_bytes = 0;    // its arena bytes
   DevBuf aj_cout;           // commit scalars
   hipEvent_t kd_ev[2] = {}; // keyed collect: chain stream -> collect stream -> chain stream
@@ -1817,6 +1847,53 @@ int acc_update(fsg_chain* c, const Plan& p, bool cat) {
 
 int run_composed(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics* m, fsg_batch_output* res);
 
+// the group's walks, once every chain has arrived (the last arrival launches)
+int group_launch(AjGroup* g) {
+  HIPCHK(hipSetDevice(g->device));
+  const size_t n = g->jobs.size();
+  if (!g->st) HIPCHK(hipStreamCreateWithFlags(&g->st, hipStreamNonBlocking));
+  if (!g->done) HIPCHK(hipEventCreateWithFlags(&g->done, hipEventDisableTiming));
+  if (n) {
+    for (auto e : g->ready) HIPCHK(hipStreamWaitEvent(g->st, e, 0));
+    HIPCHK(hipMalloc(&g->dlist, n * sizeof(AggjArgs)));
+    HIPCHK(hipMemcpyAsync(g->dlist, g->jobs.data(), n * sizeof(AggjArgs), hipMemcpyHostToDevice, g->st));
+    launch_aggj_order_group((const AggjArgs*)g->dlist, (uint32_t)n, g->st);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipEventRecord(g->done, g->st));
+  return FSG_OK;
+}
+// a chain's arrival (job = nullptr: nothing to walk); returns once the group's
+// launch is queued, with `st` ordered after it
+int group_arrive(fsg_chain* c, const AggjArgs* job, hipStream_t st) {
+  AjGroup* g = c->group;
+  if (!g || c->group_arrived) return FSG_OK;
+  c->group_arrived = true;
+  std::unique_lock<std::mutex> lk(g->mu);
+  if (job) {
+    hipEvent_t e = nullptr;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(e, st));
+    g->jobs.push_back(*job);
+    g->ready.push_back(e);
+  }
+  if (++g->arrived == g->expected) {
+    g->rc = group_launch(g);
+    g->launched = true;
+    g->cv.notify_all();
+  } else if (job) {
+    g->cv.wait(lk, [&] { return g->launched; });
+  }
+  if (job) {
+    if (g->rc) return g->rc;
+    HIPCHK(hipStreamWaitEvent(st, g->done, 0));
+  }
+  return FSG_OK;
+}
+int group_order(fsg_chain* c, const AggjArgs* aj, hipStream_t st) {
+  return group_arrive(c, aj->n_rec ? aj : nullptr, st);
+}
+
 int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics* m, fsg_batch_output* res,
               bool empty_chain_io, SegOut* so = nullptr) {
   if (!c->segs.empty()) return run_composed(c, s, max_bytes, m, res);
@@ -2199,7 +2276,13 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     HIPCHK(c->cat.ensure(kCatOff + aj_total + 64));
     HIPCHK(c->aj_ord.ensure(std::max<uint64_t>(n_ord, 1) * 4));  // Σ keys <= text bytes / 8
     aj.ord = c->aj_ord.as<uint32_t>();
-    launch_aggj_order(aj, st);
+    launch_aggj_hash(aj, st);
+    if (c->group) {
+      int rc = group_order(c, &aj, st);
+      if (rc) return rc;
+    } else {
+      launch_aggj_order(aj, st);
+    }
     aj.cat = c->cat.as<uint8_t>();
     aj.write = 1;
     launch_aggj_write(aj, st);
@@ -2565,6 +2648,54 @@ extern "C" int fsg_chain_process_slice(fsg_chain* c, const fsg_slice* s, uint64_
     free_error(res->error);
   }
   return FSG_OK;
+}
+
+extern "C" int fsg_chain_group_process_slices(fsg_chain* const* chains, const fsg_slice* const* slices, size_t n,
+                                              uint64_t max_bytes, fsg_metrics* metrics, fsg_batch_output** outs,
+                                              int* rcs) {
+  if (!chains || !slices || !rcs || n > 4096) return fail(FSG_E_INVALID_ARG, "fsg_chain_group_process_slices: bad arguments");
+  if (!n) return FSG_OK;
+  for (size_t i = 0; i < n; i++) {
+    if (!chains[i] || !slices[i]) return fail(FSG_E_INVALID_ARG, "fsg_chain_group_process_slices: null chain / slice");
+    for (size_t j = 0; j < i; j++)
+      if (chains[j] == chains[i]) return fail(FSG_E_INVALID_ARG, "fsg_chain_group_process_slices: a chain twice");
+    if (chains[i]->eng->device != chains[0]->eng->device)
+      return fail(FSG_E_INVALID_ARG, "fsg_chain_group_process_slices: chains on different devices");
+  }
+  AjGroup g;
+  g.device = chains[0]->eng->device;
+  g.expected = n;
+  for (size_t i = 0; i < n; i++) {
+    fsg_chain* c = chains[i];
+    // only plain aggregate-json chains walk in the group; the others arrive at once
+    const bool walks = (c->hdesc.flags & CF_AGG_JSON) && c->segs.empty();
+    c->group = &g;
+    c->group_arrived = false;
+    if (!walks) (void)group_arrive(c, nullptr, nullptr);
+  }
+  std::vector<std::thread> th;
+  std::vector<std::string> errs(n);
+  th.reserve(n);
+  for (size_t i = 0; i < n; i++)
+    th.emplace_back([&, i] {
+      fsg_chain* c = chains[i];
+      if (outs) outs[i] = nullptr;
+      rcs[i] = fsg_chain_process_slice(c, slices[i], max_bytes, metrics ? metrics + i : nullptr, outs ? outs + i : nullptr);
+      if (rcs[i]) errs[i] = g_err;
+      (void)group_arrive(c, nullptr, nullptr);  // a chain that failed before its walk
+    });
+  for (auto& t : th) t.join();
+  int rc = FSG_OK;
+  for (size_t i = 0; i < n; i++) {
+    chains[i]->group = nullptr;
+    if (rcs[i] && rc == FSG_OK) {
+      rc = rcs[i];
+      g_err = errs[i];
+    }
+  }
+  HIPCHK(hipSetDevice(g.device));
+  if (g.st) HIPCHK(hipStreamSynchronize(g.st));  // the list buffer is freed with g
+  return rc;
 }
 
 extern "C" int fsg_chain_output_device(fsg_chain* c0, const void** dptr, size_t* len) {

@@ -368,6 +368,33 @@ class PartitionState:
             self._h = None
 
 
+def process_slices(chains, slices, max_bytes: int = (1 << 64) - 1, metrics=None, download: bool = False):
+    """fsg_chain_group_process_slices: every chain over its resident slice in one
+    call (the partitions a rank owns), outputs left in HBM unless `download`;
+    aggregate-json's stream-order walks run as one launch over all chains.
+    Returns the BatchOutputs when downloading."""
+    n = len(chains)
+    assert len(slices) == n
+    ch = (ctypes.c_void_p * n)(*[c._h.value if isinstance(c._h, ctypes.c_void_p) else c._h for c in chains])
+    sl = (ctypes.c_void_p * n)(*[s._h.value if isinstance(s._h, ctypes.c_void_p) else s._h for s in slices])
+    rcs = (ctypes.c_int * max(n, 1))()
+    m = None
+    if metrics is not None:
+        m = (_ffi.fsg_metrics * n)()
+    outs = (ctypes.POINTER(_ffi.fsg_batch_output) * n)() if download else None
+    rc = _ffi.lib().fsg_chain_group_process_slices(ch, sl, n, max_bytes, m, outs, rcs)
+    if download:
+        res = [chains[i]._batch_result(outs[i]) if outs[i] else None for i in range(n)]
+    _check(rc)
+    if metrics is not None:
+        for i in range(n):
+            metrics[i]._m.bytes_in += m[i].bytes_in
+            metrics[i]._m.records_out += m[i].records_out
+            metrics[i]._m.invocation_count += m[i].invocation_count
+            metrics[i]._m.fuel_used += m[i].fuel_used
+    return res if download else None
+
+
 class KeyedState:
     """Topic-wide keyed totals of aggregate-json chains (fsg_keyed_*): collect
     each owned partition's map (exact keys, device side), then `allreduce()`

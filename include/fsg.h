@@ -243,6 +243,16 @@ void fsg_slice_free(fsg_slice *s);
  * fsg_chain_download_output (out may be NULL to keep it resident). */
 int fsg_chain_process_slice(fsg_chain *c, const fsg_slice *s, uint64_t max_bytes, fsg_metrics *metrics,
                             fsg_batch_output **out);
+/* process_slice of several chains at once: the partitions a rank owns, one
+ * chain instance each (crates/fluvio-spu/src/smartengine/context.rs:25-30),
+ * each over its own resident slice.  The chains run concurrently on their own
+ * streams; what walks a chain's records in stream order (aggregate-json's map
+ * order) runs as one launch over all of them.  metrics: n entries or NULL;
+ * outs: n entries or NULL (NULL keeps every output in HBM, as process_slice);
+ * rcs[i] = chain i's status (the call returns the first failure, its message
+ * in fsg_last_error_message). */
+int fsg_chain_group_process_slices(fsg_chain *const *chains, const fsg_slice *const *slices, size_t n,
+                                   uint64_t max_bytes, fsg_metrics *metrics, fsg_batch_output **outs, int *rcs);
 /* device pointer + size of the last resident output batch (valid until the next call) */
 int fsg_chain_output_device(fsg_chain *c, const void **dptr, size_t *len);
 

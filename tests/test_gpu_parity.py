@@ -1552,3 +1552,34 @@ def test_keyed_merge_simulated_ranks(engine, nr):
         ranks.append((keys, vals))
     assert ks.allreduce_simulated(me, ranks) == len(expect)
     assert ks.read() == expect
+
+
+def test_group_process_slices(comm_engine):
+    """fsg_chain_group_process_slices: 24 chains in one call (aggregate-json
+    partitions whose stream-order walks run as one launch, beside filter,
+    aggregate-sum and composed chains, an aggregate-json partition with record
+    errors, one with no records), two calls; every chain's output batch and
+    accumulator as the oracle has them."""
+    from fluvio_amd.smartengine import ResidentSlice, process_slices
+    keyed = synth.make_keyed_slices(16, 900, 300)
+    cases = []
+    for p in range(16):
+        acc = b'{"repo-0001": 7, "zz": 1}' if p == 5 else None
+        cases.append(([("aggregate-json", {}, acc)], keyed[p]))
+    cases.append((CHAINS["filter_init_timeout"], synth.make_slice(2, 500, seed=4)))
+    cases.append((CHAINS["agg_sum"], synth.make_slice(3, 2000, seed=5)))
+    cases.append(([("aggregate-json", {}, None), ("filter_init", {"key": "repo-000"}, None)], keyed[0]))
+    cases.append(([("filter_init", {"key": "repo"}, None), ("aggregate-json", {}, None)], keyed[1]))
+    cases.append(([("aggregate-json", {}, None)], P.Batch(base_offset=3).encode()))  # no records
+    cases.append(([("aggregate-json", {}, None)], keyed[2]))
+    cases.append(([("aggregate-json", {}, None)], _keyed_slice(7, nbatches=8, bad=0.05)))
+    cases.append(([("aggregate-json", {}, None)], _keyed_slice(8, nbatches=6)))
+    gs = [gpu_chain(comm_engine, m) for m, _ in cases]
+    os_ = [orc_chain(m) for m, _ in cases]
+    rs = [ResidentSlice(comm_engine, sl) for _, sl in cases]
+    for call in range(2):
+        outs = process_slices(gs, rs, download=True)
+        for i, (m, sl) in enumerate(cases):
+            _same_batch(outs[i], os_[i].process_batch(sl))
+            if m[-1][0] in ("aggregate-json", "aggregate-sum"):
+                assert gs[i].accumulator(len(m) - 1) == os_[i].accumulator(len(m) - 1), (call, i)
