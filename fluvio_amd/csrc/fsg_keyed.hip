@@ -130,38 +130,55 @@ __global__ __launch_bounds__(256) void k_aggj_hash(AggjArgs a) {
 
 __device__ __forceinline__ uint32_t hb_capacity(uint32_t B) { return B == 0 ? 0u : B <= 8u ? B - 1u : B / 8u * 7u; }
 // the register path: a table of at most 64 buckets, wave-uniform occupancy,
-// bucket s's payload in lane s of `pl`
+// bucket s's payload in lane s of `pl`.  The occupancy mask is kept TILED:
+// B-bit periods repeated over 64 bits (rep = bit 0 of every period), so the
+// group window at any probe position is one 64-bit rotate (period B divides
+// 64) whatever B is, and a table smaller than a group (B = 4) scans its own
+// buckets circularly, which is what its EMPTY padding plus fix_insert_slot's
+// rescan from bucket 0 amount to.
 struct HbReg {
-  uint64_t occ;
-  uint32_t B, items, pl;
+  uint64_t occ, rep;
+  uint32_t B, mask, wm, cap, items, pl;
 };
-__device__ __forceinline__ uint64_t hb_rotr(uint64_t x, uint32_t p, uint32_t B) {
-  if (B == 64u) return p ? (x >> p) | (x << (64u - p)) : x;
-  return ((x >> p) | (x << (B - p))) & ((1ull << B) - 1ull);
+__device__ __forceinline__ uint64_t rotr64(uint64_t x, uint32_t p) {
+  return (x >> (p & 63u)) | (x << ((64u - p) & 63u));  // p = 0: x | x
 }
-__device__ __forceinline__ uint32_t hb_slot(uint64_t occ, uint32_t B, uint32_t h) {
-  const uint32_t mask = B - 1u, w = B < 8u ? B : 8u;
-  const uint64_t wm = (1ull << w) - 1ull;
-  uint32_t pos = h & mask, stride = 0;
-  for (;;) {
-    const uint64_t win = hb_rotr(occ, pos, B) & wm;
-    if (win != wm) return (pos + (uint32_t)__builtin_ctzll(~win)) & mask;
-    stride += 8u;
-    pos = (pos + stride) & mask;
-  }
+__device__ __forceinline__ HbReg hb_new(uint32_t B) {  // B in {0, 4, 8, 16, 32, 64}
+  HbReg t;
+  t.occ = 0;
+  t.rep = B == 4u ? 0x1111111111111111ull : B == 8u ? 0x0101010101010101ull : B == 16u ? 0x0001000100010001ull
+          : B == 32u ? 0x0000000100000001ull : 1ull;
+  t.B = B;
+  t.mask = B - 1u;
+  t.wm = B < 8u ? 0xFu : 0xFFu;
+  t.cap = hb_capacity(B);
+  t.items = 0;
+  t.pl = 0;
+  return t;
 }
+// find_insert_slot: the first free bucket of the window at the probe
+// position; a full window (rare below 7/8 load) probes on by groups of 8
 __device__ __forceinline__ void hb_put(HbReg& t, uint32_t payload, uint32_t h) {
-  const uint32_t s = hb_slot(t.occ, t.B, h);
-  t.occ |= 1ull << s;
+  uint32_t pos = h & t.mask;
+  uint32_t win = (uint32_t)rotr64(t.occ, pos) & t.wm;
+  for (uint32_t stride = 8u; win == t.wm; stride += 8u) {
+    pos = (pos + stride) & t.mask;
+    win = (uint32_t)rotr64(t.occ, pos) & t.wm;
+  }
+  const uint32_t s = (pos + (uint32_t)__builtin_ctz(~win)) & t.mask;
+  t.occ |= t.rep << s;
   t.pl = (threadIdx.x & 63u) == s ? payload : t.pl;  // writelane
   t.items++;
+}
+__device__ __forceinline__ uint64_t hb_live(const HbReg& t) {
+  return t.B < 64u ? t.occ & ((1ull << t.B) - 1ull) : t.occ;
 }
 // reserve(1): no room -> capacity_to_buckets(capacity + 1) = 4, 8, 2B buckets,
 // the old buckets re-inserted in bucket order; hv: lane x = payload x's hash
 __device__ __forceinline__ void hb_reserve(HbReg& t, uint32_t hv) {
-  if (hb_capacity(t.B) != t.items) return;
-  HbReg n{0ull, t.B ? 2u * t.B : 4u, 0u, 0u};
-  for (uint64_t m = t.occ; m; m &= m - 1ull) {
+  if (t.cap != t.items) return;
+  HbReg n = hb_new(t.B ? 2u * t.B : 4u);
+  for (uint64_t m = hb_live(t); m; m &= m - 1ull) {
     const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)t.pl, (int)__builtin_ctzll(m));
     hb_put(n, x, (uint32_t)__builtin_amdgcn_readlane((int)hv, (int)x));
   }
@@ -279,28 +296,29 @@ __device__ void aj_order_run(const AggjArgs& a, uint32_t* lds) {
         seq = l < nkb ? a.ord[prev_ko + l] : 0u;
       }
       const uint32_t is = iseq && l < nseq ? a.iseq[l] : 0u;
-      HbReg A{0ull, 0u, 0u, 0u};
+      HbReg A = hb_new(0);
       for (uint32_t p = 0; p < nseq; p++) {  // the accumulator's text, HashMap::insert per entry
         uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)(iseq ? is : seq), (int)p);
         hb_reserve(A, hk);
         if (k & kAjDup) continue;  // a repeated key: the value changes, the layout does not
         hb_put(A, k, (uint32_t)__builtin_amdgcn_readlane((int)hk, (int)k));
       }
-      HbReg R{0ull, 0u, 0u, 0u};
+      HbReg R = hb_new(0);
       for (uint32_t j = 0; j < ne; j++) {  // the record's own map
         hb_reserve(R, hr);
         if ((uint32_t)__builtin_amdgcn_readlane((int)ek, (int)j) == kSkipEntry) continue;
         hb_put(R, j, (uint32_t)__builtin_amdgcn_readlane((int)hr, (int)j));
       }
-      for (uint64_t m = R.occ; m; m &= m - 1ull) {  // `for (repo, n) in next.0`: entry(repo) per vacant key
+      for (uint64_t m = hb_live(R); m; m &= m - 1ull) {  // `for (repo, n) in next.0`: entry(repo) per vacant key
         const uint32_t j = (uint32_t)__builtin_amdgcn_readlane((int)R.pl, (int)__builtin_ctzll(m));
         const uint32_t kid = (uint32_t)__builtin_amdgcn_readlane((int)ek, (int)j);
         if (kid < nkb) continue;
         hb_reserve(A, hk);
         hb_put(A, kid, (uint32_t)__builtin_amdgcn_readlane((int)hk, (int)kid));
       }
-      const bool full = (A.occ >> l) & 1ull;
-      const uint32_t below = (uint32_t)__builtin_popcountll(A.occ & ((1ull << l) - 1ull));
+      const uint64_t live = hb_live(A);
+      const bool full = (live >> l) & 1ull;
+      const uint32_t below = (uint32_t)__builtin_popcountll(live & ((1ull << l) - 1ull));
       const uint32_t pos = full ? below : nk + (l - below);
       if (full) a.ord[ko + pos] = A.pl;
       seq = (uint32_t)__builtin_amdgcn_ds_permute((int)(pos << 2), (int)A.pl);

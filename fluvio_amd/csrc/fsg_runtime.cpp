@@ -2665,6 +2665,7 @@ extern "C" int fsg_chain_group_process_slices(fsg_chain* const* chains, const fs
   AjGroup g;
   g.device = chains[0]->eng->device;
   g.expected = n;
+  std::vector<size_t> walkers, others;
   for (size_t i = 0; i < n; i++) {
     fsg_chain* c = chains[i];
     // only plain aggregate-json chains walk in the group; the others arrive at once
@@ -2672,17 +2673,27 @@ extern "C" int fsg_chain_group_process_slices(fsg_chain* const* chains, const fs
     c->group = &g;
     c->group_arrived = false;
     if (!walks) (void)group_arrive(c, nullptr, nullptr);
+    (walks ? walkers : others).push_back(i);
   }
-  std::vector<std::thread> th;
   std::vector<std::string> errs(n);
-  th.reserve(n);
-  for (size_t i = 0; i < n; i++)
-    th.emplace_back([&, i] {
-      fsg_chain* c = chains[i];
-      if (outs) outs[i] = nullptr;
-      rcs[i] = fsg_chain_process_slice(c, slices[i], max_bytes, metrics ? metrics + i : nullptr, outs ? outs + i : nullptr);
-      if (rcs[i]) errs[i] = g_err;
-      (void)group_arrive(c, nullptr, nullptr);  // a chain that failed before its walk
+  auto one = [&](size_t i) {
+    fsg_chain* c = chains[i];
+    if (outs) outs[i] = nullptr;
+    rcs[i] = fsg_chain_process_slice(c, slices[i], max_bytes, metrics ? metrics + i : nullptr, outs ? outs + i : nullptr);
+    if (rcs[i]) errs[i] = g_err;
+    (void)group_arrive(c, nullptr, nullptr);  // a chain that failed before its walk
+  };
+  // a walker blocks at the rendezvous until every walker has arrived: one
+  // thread each; the other chains share a pool (host launch and sync work
+  // does not scale past ~16 threads)
+  std::vector<std::thread> th;
+  th.reserve(walkers.size() + 16);
+  for (size_t i : walkers) th.emplace_back(one, i);
+  std::atomic<size_t> next{0};
+  const size_t pool = std::min<size_t>(others.size(), 16);
+  for (size_t k = 0; k < pool; k++)
+    th.emplace_back([&] {
+      for (size_t j = next++; j < others.size(); j = next++) one(others[j]);
     });
   for (auto& t : th) t.join();
   int rc = FSG_OK;
