@@ -2408,8 +2408,8 @@ struct __attribute__((aligned(16))) RlLds {
   uint16_t mst[kRlWaves][kRlMem + 2];
   uint32_t nst, out_upper, nd_res;
   LeanStage stg[kMaxStages];
-  uint8_t needles[kLeanNeedles];
-  uint8_t needle[kLeanNeedle + 8];  // a needle that does not fit in needles
+  alignas(16) uint8_t needles[kLeanNeedles];
+  alignas(16) uint8_t needle[kLeanNeedle + 8];  // a needle that does not fit in needles
   uint8_t dfa[kJsonStates * kJsonCls2];
   uint8_t bcls[256];
 };
@@ -2430,23 +2430,26 @@ __device__ __forceinline__ uint32_t rl_vmask(uint32_t c, uint32_t vs, uint32_t v
 }
 // bytes of a dword selected by a 4-bit mask
 __device__ __forceinline__ uint32_t rl_bytes(uint32_t nib) { return ((nib * 0x00204081u) & 0x01010101u) * 0xFFu; }
-__device__ __forceinline__ bool rl_verify(const uint8_t* win, uint32_t p, const uint8_t* nd, uint32_t m, bool upper) {
+// m needle bytes (at offset no of the 4-byte aligned LDS array nb) against the
+// window at p
+__device__ __forceinline__ bool rl_verify(const uint8_t* win, uint32_t p, const uint8_t* nb, uint32_t no, uint32_t m,
+                                          bool upper) {
   for (uint32_t t = 0; t < m; t += 4) {
     uint32_t x = lds_u32_at(win, p + t);
     if (upper) x = swar_upper(x);
     const uint32_t k = m - t >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (m - t))) - 1u);
-    if ((x ^ lds_u32_at(nd, t)) & k) return false;
+    if ((x ^ lds_u32_at(nb, no + t)) & k) return false;
   }
   return true;
 }
-// one record value [vs, ve) by one wave: bit 0 = the needle occurs, bit 1 = a
-// byte >= 0x80 (uniform)
-__device__ uint32_t rl_contains(const uint8_t* win, uint32_t vs, uint32_t ve, const uint8_t* nd, uint32_t m,
-                                bool upper) {
+// one record value [vs, ve) by one wave, the needle at offset no of nb: bit 0 =
+// the needle occurs, bit 1 = a byte >= 0x80 (uniform)
+__device__ uint32_t rl_contains(const uint8_t* win, uint32_t vs, uint32_t ve, const uint8_t* nb, uint32_t no,
+                                uint32_t m, bool upper) {
   const uint32_t l = threadIdx.x & 63u;
   const uint32_t m4 = m < 4 ? m : 4;
   uint32_t rot0 = 0;
-  for (uint32_t t = 0; t < m4; t++) rot0 |= (uint32_t)nd[t] << (8 * t);
+  for (uint32_t t = 0; t < m4; t++) rot0 |= (uint32_t)nb[no + t] << (8 * t);
   const uint32_t k4 = m4 == 4 ? 0xFFFFFFFFu : ((1u << (8 * m4)) - 1u);
   bool hit = false;
   uint32_t orw = 0;
@@ -2470,7 +2473,7 @@ __device__ uint32_t rl_contains(const uint8_t* win, uint32_t vs, uint32_t ve, co
     for (int j = 0; j < 16 && !hit; j++) {
       const uint32_t p = c + (uint32_t)j;
       if (((win5(wd, j) ^ rot0) & k4) == 0u && p >= vs && p + m <= ve &&
-          (m <= 4 || rl_verify(win, p + 4, nd + 4, m - 4, upper)))
+          (m <= 4 || rl_verify(win, p + 4, nb, no + 4, m - 4, upper)))
         hit = true;
     }
   }
@@ -2500,7 +2503,7 @@ __device__ __forceinline__ uint32_t rl_str_class(const uint8_t* win, uint32_t a)
 // is present), bit 1 = defer the batch; *span = the projected value's
 // [start, end) (uniform)
 template <bool kProj>
-__device__ uint32_t rl_json(RlLds& L, uint32_t w, uint32_t vs, uint32_t ve, const uint8_t* field, uint32_t fl,
+__device__ uint32_t rl_json(RlLds& L, uint32_t w, uint32_t vs, uint32_t ve, const uint8_t* fb, uint32_t fo, uint32_t fl,
                             uint32_t* span) {
   const uint32_t l = threadIdx.x & 63u;
   uint32_t* tok = L.tok[w];
@@ -2584,7 +2587,7 @@ __device__ uint32_t rl_json(RlLds& L, uint32_t w, uint32_t vs, uint32_t ve, cons
           khit = n == fl;
           for (uint32_t k = 0; khit && k < fl; k += 4) {
             const uint32_t mk = fl - k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (fl - k))) - 1u);
-            khit = ((lds_u32_at(L.win, pos + 1 + k) ^ lds_u32_at(field, k)) & mk) == 0u;
+            khit = ((lds_u32_at(L.win, pos + 1 + k) ^ lds_u32_at(fb, fo + k)) & mk) == 0u;
           }
         }
         if (st0 == JS_VAL_OTHER) {
@@ -2752,12 +2755,14 @@ __global__ __launch_bounds__(kRlThreads) void k_rec_lean(EvalArgs a) {
         defer = true;  // long needle / field name: exact kernel
         break;
       }
-      const uint8_t* nd = L.needles + __builtin_amdgcn_readfirstlane(sd.nd_off);
+      const uint8_t* nb = L.needles;  // the needle / field name: nb[no .. no + m)
+      uint32_t no = __builtin_amdgcn_readfirstlane(sd.nd_off);
       if (!__builtin_amdgcn_readfirstlane(L.nd_res)) {
         const uint8_t* gn = a.blob + __builtin_amdgcn_readfirstlane(sd.nd);
         for (uint32_t k = t; k < m; k += kRlThreads) L.needle[k] = gn[k];
         lean_sync();
-        nd = L.needle;
+        nb = L.needle;
+        no = 0;
       }
       const bool upper = sd.upper != 0;
       uint32_t* res = L.res[rsel];
@@ -2768,16 +2773,17 @@ __global__ __launch_bounds__(kRlThreads) void k_rec_lean(EvalArgs a) {
         if constexpr (kJson) {
           if (json) {
             uint32_t span[2] = {rvs, rve};
-            x = op == OP_PROJECT ? rl_json<true>(L, w, rvs, rve, nd, m, span) : rl_json<false>(L, w, rvs, rve, nullptr, 0, span);
+            x = op == OP_PROJECT ? rl_json<true>(L, w, rvs, rve, nb, no, m, span)
+                                 : rl_json<false>(L, w, rvs, rve, nb, 0, 0, span);
             if (op == OP_PROJECT && l == 0 && (x & 1u)) {  // the value narrows to the field's text
               L.r_vs[r] = span[0];
               L.r_ve[r] = span[1];
             }
           } else {
-            x = rl_contains(L.win, rvs, rve, nd, m, upper);
+            x = rl_contains(L.win, rvs, rve, nb, no, m, upper);
           }
         } else {
-          x = rl_contains(L.win, rvs, rve, nd, m, upper);
+          x = rl_contains(L.win, rvs, rve, nb, no, m, upper);
         }
         if (l == 0) res[r] = x;
       }
