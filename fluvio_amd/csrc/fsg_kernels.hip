@@ -2477,7 +2477,7 @@ __device__ uint32_t rl_contains(const uint8_t* win, uint32_t vs, uint32_t ve, co
         hit = true;
     }
   }
-  return (__ballot(hit) ? 1u : 0u) | (__ballot((orw & 0x80808080u) != 0u) ? 2u : 0u);
+  return (m == 0 || __ballot(hit) ? 1u : 0u) | (__ballot((orw & 0x80808080u) != 0u) ? 2u : 0u);  // "" is in every str
 }
 // the class of a string whose content starts at window offset a (its closing
 // quote within 8 bytes): "level" / "message" / a LogLevel variant / other
