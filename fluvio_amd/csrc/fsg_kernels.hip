@@ -2369,482 +2369,6 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
 }
 
 // ---------------------------------------------------------------------------
-// k_rec_lean — the lean path with one WAVE PER RECORD, for chains of
-// substring filters (filter / filter_init / filter_with_param), filter_json,
-// the field projection and uppercase maps (C2, C2-json, C3).  Persistent
-// workgroups of four waves walk the batches; a batch's window (57-B header +
-// record section, <= 16 KiB) lands in LDS by LDS-DMA, lanes < 64 parse the
-// records (k_chase found their starts), then each stage hands whole records
-// to the waves: wave w takes records w, w + 4, ... of those still alive, 64
-// lanes x 16 bytes = 1 KiB of the value per step.
-//   substring: the first (up to) 4 needle bytes compared at each of the
-//     lane's 16 positions (a min over XOR differences, VALU only), hits
-//     verified against the whole needle in LDS; the OR of the value bytes
-//     proves ASCII (from_utf8 cannot fail, filter.rs / derive filter.rs:14-40)
-//   filter_json / projection (serde_json::from_slice, filter_json/src/lib.rs:
-//     54-70): per 16-byte chunk the quote / special / non-space masks (SWAR),
-//     the in-string mask from a prefix XOR of the quotes carried across lanes
-//     by one ballot; the tokens (quotes, non-space bytes outside strings) go
-//     in order into the wave's list, each with its class and an "adjacent to
-//     the previous token" bit; then one lane per object member runs the token
-//     DFA of fsg_json_dfa.h over its tokens.  A record outside the DFA's flat
-//     grammar (or with escapes, control or non-ASCII bytes) sends the batch
-//     to the exact kernel.
-// A batch that cannot take this path (more than 64 records, a record that
-// does not frame exactly, a non-ASCII value, ...) is appended to a.list for
-// k_eval, as in k_eval_lean.
-// ---------------------------------------------------------------------------
-constexpr int kRlThreads = 256;
-constexpr int kRlWaves = kRlThreads / 64;
-constexpr int kRlTok = 256;  // tokens of one record value (more: exact kernel)
-constexpr int kRlMem = 63;   // object members of one record (more: exact kernel)
-struct __attribute__((aligned(16))) RlLds {
-  uint8_t win[kLeanWin + 64];  // + look-ahead of a record's last chunk
-  uint32_t r_vs[kLeanMaxR];
-  uint32_t r_ve[kLeanMaxR];
-  uint32_t res[2][kLeanMaxR];    // per record: the stage's result (alternating per stage)
-  uint32_t red[8];               // workgroup OR (two alternating quads)
-  uint32_t tok[kRlWaves][kRlTok];
-  uint16_t mst[kRlWaves][kRlMem + 2];
-  uint32_t nst, out_upper, nd_res;
-  LeanStage stg[kMaxStages];
-  alignas(16) uint8_t needles[kLeanNeedles];
-  alignas(16) uint8_t needle[kLeanNeedle + 8];  // a needle that does not fit in needles
-  uint8_t dfa[kJsonStates * kJsonCls2];
-  uint8_t bcls[256];
-};
-// workgroup OR of p over the four waves (one barrier; quads alternate)
-__device__ __forceinline__ bool rl_or(uint32_t* red, uint32_t& par, bool p) {
-  const uint64_t bl = __ballot(p);
-  uint32_t* r = red + 4 * par;
-  if ((threadIdx.x & 63u) == 0) r[threadIdx.x >> 6] = bl != 0 ? 1u : 0u;
-  lean_sync();
-  par ^= 1u;
-  return (r[0] | r[1] | r[2] | r[3]) != 0u;
-}
-// the 16-bit mask of chunk bytes [c, c + 16) inside [vs, ve)
-__device__ __forceinline__ uint32_t rl_vmask(uint32_t c, uint32_t vs, uint32_t ve) {
-  if (c >= ve) return 0u;
-  const uint32_t lo = vs > c ? vs - c : 0u, hi = ve - c < 16u ? ve - c : 16u;
-  return (hi >= 16u ? 0xFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
-}
-// bytes of a dword selected by a 4-bit mask
-__device__ __forceinline__ uint32_t rl_bytes(uint32_t nib) { return ((nib * 0x00204081u) & 0x01010101u) * 0xFFu; }
-// m needle bytes (at offset no of the 4-byte aligned LDS array nb) against the
-// window at p
-__device__ __forceinline__ bool rl_verify(const uint8_t* win, uint32_t p, const uint8_t* nb, uint32_t no, uint32_t m,
-                                          bool upper) {
-  for (uint32_t t = 0; t < m; t += 4) {
-    uint32_t x = lds_u32_at(win, p + t);
-    if (upper) x = swar_upper(x);
-    const uint32_t k = m - t >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (m - t))) - 1u);
-    if ((x ^ lds_u32_at(nb, no + t)) & k) return false;
-  }
-  return true;
-}
-// one record value [vs, ve) by one wave, the needle at offset no of nb: bit 0 =
-// the needle occurs, bit 1 = a byte >= 0x80 (uniform)
-__device__ uint32_t rl_contains(const uint8_t* win, uint32_t vs, uint32_t ve, const uint8_t* nb, uint32_t no,
-                                uint32_t m, bool upper) {
-  const uint32_t l = threadIdx.x & 63u;
-  const uint32_t m4 = m < 4 ? m : 4;
-  uint32_t rot0 = 0;
-  for (uint32_t t = 0; t < m4; t++) rot0 |= (uint32_t)nb[no + t] << (8 * t);
-  const uint32_t k4 = m4 == 4 ? 0xFFFFFFFFu : ((1u << (8 * m4)) - 1u);
-  bool hit = false;
-  uint32_t orw = 0;
-  for (uint32_t base = vs & ~15u; base < ve; base += 1024u) {
-    const uint32_t c = base + 16u * l;
-    const uint32_t vm = rl_vmask(c, vs, ve);
-    if (!vm) continue;
-    const uint4 v = *(const uint4*)(win + c);
-    uint32_t wd[5] = {v.x, v.y, v.z, v.w, *(const uint32_t*)(win + c + 16)};
-    orw |= (wd[0] & rl_bytes(vm & 15u)) | (wd[1] & rl_bytes((vm >> 4) & 15u)) | (wd[2] & rl_bytes((vm >> 8) & 15u)) |
-           (wd[3] & rl_bytes(vm >> 12));
-    if (m == 0) continue;
-    if (upper) {
-#pragma unroll
-      for (int k = 0; k < 5; k++) wd[k] = swar_upper(wd[k]);
-    }
-    uint32_t z = 0xFFFFFFFFu;
-#pragma unroll
-    for (int j = 0; j < 16; j += 2) z = min(z, min((win5(wd, j) ^ rot0) & k4, (win5(wd, j + 1) ^ rot0) & k4));
-    if (z != 0u || hit) continue;  // rare: a 4-gram (or the whole short needle) somewhere in the chunk
-    for (int j = 0; j < 16 && !hit; j++) {
-      const uint32_t p = c + (uint32_t)j;
-      if (((win5(wd, j) ^ rot0) & k4) == 0u && p >= vs && p + m <= ve &&
-          (m <= 4 || rl_verify(win, p + 4, nb, no + 4, m - 4, upper)))
-        hit = true;
-    }
-  }
-  return (m == 0 || __ballot(hit) ? 1u : 0u) | (__ballot((orw & 0x80808080u) != 0u) ? 2u : 0u);  // "" is in every str
-}
-// the class of a string whose content starts at window offset a (its closing
-// quote within 8 bytes): "level" / "message" / a LogLevel variant / other
-__device__ __forceinline__ uint32_t rl_str_class(const uint8_t* win, uint32_t a) {
-  const uint64_t w = (uint64_t)lds_u32_at(win, a) | ((uint64_t)lds_u32_at(win, a + 4) << 32);
-  const uint64_t x = w ^ 0x2222222222222222ull;
-  const uint64_t z = (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
-  if (!z) return JC_Q_OTHER;
-  const uint32_t n = (uint32_t)__builtin_ctzll(z) >> 3;  // content length
-  const uint64_t s = w & ((1ull << (8 * n)) - 1ull);
-  constexpr auto k = [](const char* t) {
-    uint64_t v = 0;
-    for (int i = 0; t[i]; i++) v |= (uint64_t)(uint8_t)t[i] << (8 * i);
-    return v;
-  };
-  if (n == 5) return s == k("level") ? JC_Q_LEVEL : s == k("debug") ? JC_Q_DEBUG : s == k("error") ? JC_Q_ERROR : JC_Q_OTHER;
-  if (n == 7) return s == k("message") ? JC_Q_MSG : JC_Q_OTHER;
-  if (n == 4) return s == k("info") ? JC_Q_INFO : s == k("warn") ? JC_Q_WARN : JC_Q_OTHER;
-  return JC_Q_OTHER;
-}
-// filter_json (kProj false) or the field projection (kProj true) of one record
-// value [vs, ve) by one wave.  Returns bit 0 = keep (level > Debug / the field
-// is present), bit 1 = defer the batch; *span = the projected value's
-// [start, end) (uniform)
-template <bool kProj>
-__device__ uint32_t rl_json(RlLds& L, uint32_t w, uint32_t vs, uint32_t ve, const uint8_t* fb, uint32_t fo, uint32_t fl,
-                            uint32_t* span) {
-  const uint32_t l = threadIdx.x & 63u;
-  uint32_t* tok = L.tok[w];
-  uint32_t ntok = 0, par = 0, hprev = 0;  // tokens so far, quote parity, last byte of the previous step a token
-  for (uint32_t base = vs & ~15u; base < ve; base += 1024u) {
-    const uint32_t c = base + 16u * l;
-    const uint32_t vm = rl_vmask(c, vs, ve);
-    uint32_t q = 0, sp = 0, sps = 0;
-    if (vm) {
-      const uint4 v = *(const uint4*)(L.win + c);
-#pragma unroll
-      for (int d = 0; d < 4; d++) {
-        const uint32_t x = d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
-        q |= nib4(zbytes(x ^ 0x22222222u)) << (4 * d);
-        sp |= nib4(zbytes(x & 0xE0E0E0E0u) | zbytes(x ^ 0x5C5C5C5Cu) | (x & 0x80808080u)) << (4 * d);
-        sps |= nib4(zbytes(x ^ 0x20202020u)) << (4 * d);
-      }
-      q &= vm;
-      sp &= vm;
-    }
-    const uint32_t ns = ~sps & vm;  // non-space value bytes
-    if (__ballot(sp != 0u)) return 2u;  // escapes, control or non-ASCII bytes: exact kernel
-    const uint64_t pb = __ballot(__builtin_popcount(q) & 1u);
-    const uint32_t pre = ((uint32_t)__builtin_popcountll(pb & ((1ull << l) - 1ull)) & 1u) ^ par;
-    par ^= (uint32_t)__builtin_popcountll(pb) & 1u;
-    const uint32_t instr = (pxor16(q) ^ q ^ (pre ? 0xFFFFu : 0u)) & 0xFFFFu;  // in a string (closing quotes too)
-    const uint32_t hot = q | (ns & ~instr);
-    const uint32_t hup = __shfl_up(hot, 1, 64);
-    const uint32_t adjm = ((hot << 1) | (l == 0 ? hprev : ((hup >> 15) & 1u))) & 0xFFFFu;
-    hprev = ((uint32_t)__shfl(hot, 63, 64) >> 15) & 1u;
-    const uint32_t cnt = (uint32_t)__builtin_popcount(hot);
-    const uint32_t incl = wave_incl_scan(cnt);
-    const uint32_t tot = (uint32_t)__shfl(incl, 63, 64);
-    if (ntok + tot > (uint32_t)kRlTok) return 2u;
-    uint32_t idx = ntok + incl - cnt;
-    for (uint32_t hm = hot; hm; hm &= hm - 1u) {
-      const uint32_t j = (uint32_t)__builtin_ctz(hm);
-      const uint32_t p = c + j;
-      const uint32_t b = L.win[p];
-      uint32_t cls = L.bcls[b];
-      if (b == '"') cls = ((instr >> j) & 1u) ? (uint32_t)JC_Q_CLOSE : kProj ? (uint32_t)JC_Q_OTHER : rl_str_class(L.win, p + 1);
-      tok[idx++] = p | (((adjm >> j) & 1u) << 15) | (cls << 16);
-    }
-    ntok += tot;
-  }
-  // members: token 0 and every token after a comma (the DFA admits flat objects only)
-  uint16_t* ms = L.mst[w];
-  uint32_t nm = 1;
-  if (l == 0) ms[0] = 0;
-  for (uint32_t t0 = 0; t0 < ntok; t0 += 64u) {
-    const uint32_t t = t0 + l;
-    const bool isc = t < ntok && ((tok[t] >> 16) & 0xFFu) == JC_COMMA;
-    const uint64_t bl = __ballot(isc);
-    if (isc) {
-      const uint32_t k = nm + (uint32_t)__builtin_popcountll(bl & ((1ull << l) - 1ull));
-      if (k <= (uint32_t)kRlMem) ms[k] = (uint16_t)(t + 1u);
-    }
-    nm += (uint32_t)__builtin_popcountll(bl);
-  }
-  if (nm > (uint32_t)kRlMem) return 2u;
-  if (l == 0) ms[nm] = (uint16_t)ntok;
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  // the token DFA, one lane per member
-  bool ok = true, found = false;
-  uint32_t nlv = 0, nmsg = 0, lv = 0, fs = 0, fe = 0;
-  if (l < nm) {
-    const uint32_t t0 = ms[l], t1 = ms[l + 1];
-    uint32_t st = l == 0 ? (uint32_t)JS_OBJ : (uint32_t)JS_KEY;
-    uint32_t prev = l == 0 ? 0xFFFFu : (tok[t0 - 1] & 0x7FFFu);
-    bool khit = false, inval = false, vneg = false, nbad = false;
-    uint32_t vstart = 0, ntv = 0;
-    for (uint32_t t = t0; t < t1; t++) {
-      const uint32_t en = tok[t];
-      const uint32_t pos = en & 0x7FFFu, cls = (en >> 16) & 0xFFu, adj = (en >> 15) & 1u;
-      const uint32_t st0 = st;
-      if (!kProj && st >= JS_INV_D && st <= JS_INV_E) lv = 1u << (st - JS_INV_D);
-      st = L.dfa[st * kJsonCls2 + cls * 2 + adj];
-      if constexpr (kProj) {
-        if (st == JS_INKEY_OTHER) {  // a key: the projected field?  (its closing quote is the next token)
-          const uint32_t n = t + 1 < ntok ? (tok[t + 1] & 0x7FFFu) - pos - 1u : 0xFFFFFFFFu;
-          khit = n == fl;
-          for (uint32_t k = 0; khit && k < fl; k += 4) {
-            const uint32_t mk = fl - k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (fl - k))) - 1u);
-            khit = ((lds_u32_at(L.win, pos + 1 + k) ^ lds_u32_at(fb, fo + k)) & mk) == 0u;
-          }
-        }
-        if (st0 == JS_VAL_OTHER) {
-          inval = true;
-          vstart = pos;
-          ntv = 0;
-          vneg = cls == JC_MINUS;
-        }
-        if (inval) {
-          if (st == JS_KEY || st == JS_END) {  // ',' / '}' after the value
-            inval = false;
-            if (st0 == JS_N_ZERO && vneg && ntv == 2) nbad = true;  // -0: serde_json prints it differently
-            if (khit) {
-              found = true;
-              fs = vstart;
-              fe = prev + 1u;
-            }
-          } else {
-            ntv++;
-            if (st == JS_N_DOT || st == JS_N_E || ntv > 18) nbad = true;  // floats: serde_json's text differs
-          }
-        }
-      } else {
-        nlv += st == JS_INKEY_LV ? 1u : 0u;
-        nmsg += st == JS_INKEY_MSG ? 1u : 0u;
-      }
-      prev = pos;
-      if (st == JS_FAIL) break;
-    }
-    ok = !nbad && (l + 1 < nm ? st == JS_KEY : st == JS_END);
-  }
-  if (__ballot(!ok)) return 2u;
-  if constexpr (kProj) {
-    const uint64_t fb = __ballot(found);
-    if (!fb) return 0u;  // filter_map: no such field, the record is dropped
-    const uint32_t m = 63u - (uint32_t)__builtin_clzll(fb);  // the last member with the key wins
-    span[0] = (uint32_t)__shfl(fs, (int)m, 64);
-    span[1] = (uint32_t)__shfl(fe, (int)m, 64);
-    return 1u;
-  } else {
-    if (wave_sum(nlv) != 1u || wave_sum(nmsg) != 1u) return 2u;  // each field exactly once (else a serde error)
-    return __ballot((lv & 0xEu) != 0u) ? 1u : 0u;               // level info / warn / error
-  }
-}
-// 1 KiB LDS-DMA pieces spread over the four waves
-__device__ __forceinline__ void rl_issue(const EvalArgs& a, const LeanWin& w, uint8_t* dst) {
-  const uint32_t l = threadIdx.x, lane = l & 63u;
-  const uint8_t* src = a.slice + w.al + lane * 16;
-  for (uint32_t k = __builtin_amdgcn_readfirstlane(l >> 6); k * 1024 < w.wlen; k += kRlWaves)
-    if (k * 1024 + lane * 16 < w.wlen)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + k * 1024),
-                                       (__attribute__((address_space(3))) void*)(dst + k * 1024), 16, 0, 0);
-}
-template <bool kJson>
-__global__ __launch_bounds__(kRlThreads) void k_rec_lean(EvalArgs a) {
-  __shared__ RlLds L;
-  const uint32_t t = threadIdx.x, l = t & 63u, w = t >> 6;
-  const uint32_t G = gridDim.x;
-  uint32_t b = blockIdx.x;
-  if (b >= a.nbatches) return;
-  {  // the chain's stages, needles and JSON tables: LDS, once
-    const ChainDesc& ch = *a.chain;
-    const uint32_t nst = ch.nstages;
-    uint32_t ndo = 0;
-    for (uint32_t s = 0; s < nst; s++)
-      if (ch.st[s].op == OP_CONTAINS || ch.st[s].op == OP_PROJECT) ndo += ch.st[s].needle_len;
-    const bool nd_res = ndo <= (uint32_t)kLeanNeedles;
-    ndo = 0;
-    for (uint32_t s = 0; s < nst; s++) {
-      const StageDesc& sd = ch.st[s];
-      if (t == 0) {
-        LeanStage g{};
-        g.op = sd.op;
-        g.upper = sd.in_type == VT_SRC_UPPER ? 1 : 0;
-        g.m = sd.needle_len;
-        g.nd = sd.needle;
-        g.nd_off = ndo;
-        L.stg[s] = g;
-      }
-      if ((sd.op == OP_CONTAINS || sd.op == OP_PROJECT) && nd_res) {
-        for (uint32_t k = t; k < sd.needle_len; k += kRlThreads) L.needles[ndo + k] = a.blob[sd.needle + k];
-        ndo += sd.needle_len;
-      }
-    }
-    if (t == 0) {
-      L.nst = nst;
-      L.out_upper = ch.out_type == VT_SRC_UPPER ? 1u : 0u;
-      L.nd_res = nd_res ? 1u : 0u;
-    }
-    if constexpr (kJson) {
-      for (uint32_t k = t; k < (uint32_t)(kJsonStates * kJsonCls2); k += kRlThreads) L.dfa[k] = g_json_tables.t[k];
-      for (uint32_t k = t; k < 256u; k += kRlThreads) L.bcls[k] = g_json_tables.bcls[k];
-    }
-  }
-  uint32_t par = 0;  // rl_or quad
-  for (uint32_t it = 0;; it++) {
-    lean_sync();  // every wave is done with the previous batch's window
-    const LeanWin W = lean_window(a, b);
-    const uint64_t pos = W.pos, al = W.al;
-    const uint64_t rb = a.rbase[b];
-    const uint32_t bn = b + G;
-    rl_issue(a, W, L.win);
-    const uint32_t rs = t < 64 ? a.rstart[rb + t] : 0u;  // record starts (k_chase)
-    const uint32_t re = a.rend[b];
-    __builtin_amdgcn_s_waitcnt(0);
-    lean_sync();
-    // batch header (batch.rs:163-180)
-    const uint8_t* h = L.win + (pos - al);
-    const int64_t base_offset = (int64_t)rd_be(h, 8);
-    const uint32_t batch_len = (uint32_t)rd_be(h + 8, 4);
-    const int32_t lod_in = (int32_t)rd_be(h + 23, 4);
-    const int64_t first_ts = (int64_t)rd_be(h + 27, 8);
-    const uint32_t comp = (uint32_t)h[22] & 7u;
-    const uint64_t sec0 = pos + 57, sec_end = pos + 12 + (uint64_t)batch_len;
-    const uint32_t sec_len = (uint32_t)(sec_end - sec0);
-    const int32_t count = sec_len >= 4 ? (int32_t)rd_be(L.win + (sec0 - al), 4) : -1;
-    bool defer = sec_len < 4 || sec_end - al > (uint64_t)W.wlen || count < 0 || count > kLeanMaxR || re == 0xFFFFu;
-    const int nr = defer ? 0 : count;
-    // lane r of wave 0 parses record r exactly (Record::decode, data.rs:534-562)
-    bool g = true;
-    int64_t ts = 0, od = 0, hdr = 0;
-    uint32_t vs = 0, vl = 0, kpos = 0, klen = 0;
-    uint8_t attr = 0, tag = 0;
-    const uint32_t rs_next = __shfl_down(rs, 1, 64);
-    if ((int)t < nr) {
-      uint32_t q = rs;
-      const uint32_t lim = (int)t + 1 == nr ? re : rs_next;
-      int64_t len, kl, vlen;
-      g = !wvarint((const uint8_t*)L.win, q, lim, &len);
-      if (g && q < lim) attr = L.win[q++]; else g = false;
-      g = g && !wvarint((const uint8_t*)L.win, q, lim, &ts) && !wvarint((const uint8_t*)L.win, q, lim, &od);
-      if (g && q < lim) tag = L.win[q++]; else g = false;
-      g = g && tag <= 1;
-      if (g && tag == 1) {
-        g = !wvarint((const uint8_t*)L.win, q, lim, &kl) && kl >= 0 && (uint64_t)q + (uint64_t)kl <= lim;
-        if (g) {
-          kpos = q;
-          klen = (uint32_t)kl;
-          q += klen;
-        }
-      }
-      g = g && !wvarint((const uint8_t*)L.win, q, lim, &vlen) && vlen >= 0 && (uint64_t)q + (uint64_t)vlen <= lim;
-      vs = q;
-      if (g) {
-        vl = (uint32_t)vlen;
-        q += vl;
-      }
-      g = g && !wvarint((const uint8_t*)L.win, q, lim, &hdr) && q == lim;
-      L.r_vs[t] = vs;
-      L.r_ve[t] = vs + vl;
-    }
-    defer = rl_or(L.red, par, defer || !g);  // a record that does not frame exactly; orders r_vs / r_ve
-    uint64_t alive = nr >= 64 ? ~0ull : ((1ull << nr) - 1ull);
-    bool checked = false;  // every value reaching a stage known ASCII
-    const uint32_t nst = __builtin_amdgcn_readfirstlane(L.nst);
-    uint32_t rsel = 0;  // L.res half of this stage
-    for (uint32_t s = 0; !defer && s < nst && alive; s++) {
-      const LeanStage sd = L.stg[s];
-      const uint32_t op = __builtin_amdgcn_readfirstlane((uint32_t)sd.op);
-      if (op == OP_MAP_UPPER) continue;  // representation only
-      const uint32_t m = __builtin_amdgcn_readfirstlane(sd.m);
-      const bool json = kJson && (op == OP_FILTER_JSON || op == OP_PROJECT);
-      if (!json && m == 0 && checked) continue;  // an empty needle keeps every (UTF-8) value
-      if (m > (uint32_t)kLeanNeedle) {
-        defer = true;  // long needle / field name: exact kernel
-        break;
-      }
-      const uint8_t* nb = L.needles;  // the needle / field name: nb[no .. no + m)
-      uint32_t no = __builtin_amdgcn_readfirstlane(sd.nd_off);
-      if (!__builtin_amdgcn_readfirstlane(L.nd_res)) {
-        const uint8_t* gn = a.blob + __builtin_amdgcn_readfirstlane(sd.nd);
-        for (uint32_t k = t; k < m; k += kRlThreads) L.needle[k] = gn[k];
-        lean_sync();
-        nb = L.needle;
-        no = 0;
-      }
-      const bool upper = sd.upper != 0;
-      uint32_t* res = L.res[rsel];
-      for (uint32_t r = w; r < (uint32_t)nr; r += kRlWaves) {
-        if (!((alive >> r) & 1ull)) continue;
-        const uint32_t rvs = L.r_vs[r], rve = L.r_ve[r];
-        uint32_t x;
-        if constexpr (kJson) {
-          if (json) {
-            uint32_t span[2] = {rvs, rve};
-            x = op == OP_PROJECT ? rl_json<true>(L, w, rvs, rve, nb, no, m, span)
-                                 : rl_json<false>(L, w, rvs, rve, nb, 0, 0, span);
-            if (op == OP_PROJECT && l == 0 && (x & 1u)) {  // the value narrows to the field's text
-              L.r_vs[r] = span[0];
-              L.r_ve[r] = span[1];
-            }
-          } else {
-            x = rl_contains(L.win, rvs, rve, nb, no, m, upper);
-          }
-        } else {
-          x = rl_contains(L.win, rvs, rve, nb, no, m, upper);
-        }
-        if (l == 0) res[r] = x;
-      }
-      lean_sync();
-      // every wave reads the results (records < 64: one per lane)
-      const uint32_t x = (l < (uint32_t)nr && ((alive >> l) & 1ull)) ? res[l] : 0u;
-      alive &= __ballot(x & 1u);
-      // contains: a non-ASCII value before from_utf8 was proven; JSON: the record left the DFA's grammar
-      if (__ballot(json ? (x & 2u) != 0u : (!checked && (x & 2u) != 0u))) defer = true;
-      if (!json) checked = true;
-      rsel ^= 1u;
-      if (json) lean_sync();  // r_vs / r_ve narrowed; tok / mst reused by the next stage
-    }
-    // survivors -> compaction descriptors, BatchStat (wave 0)
-    if (defer) {
-      if (t == 0) {
-        const uint32_t i = atomicAdd(&a.list[0], 1u);
-        a.list[1 + i] = b;
-      }
-    } else {
-      if (t < 64 && ((alive >> t) & 1ull)) {
-        KeptRec d;
-        const uint32_t fvs = L.r_vs[t];
-        d.src = al + rs;
-        d.vpos = al + fvs;
-        d.kpos = tag ? al + kpos : 0;
-        d.od = od;
-        d.ts = ts;
-        d.hdr = hdr;
-        d.vlen = L.r_ve[t] - fvs;
-        d.klen = klen;
-        d.ival = 0;
-        d.mode = L.out_upper ? KM_UPPER : KM_COPY;
-        d.has_key = tag;
-        d.attr = attr;
-        d.pad = 0;
-        a.desc[rb + __popcll(alive & ((1ull << t) - 1ull))] = d;
-      }
-      if (t == 0) {
-        BatchStat st = {};
-        st.base_offset = base_offset;
-        st.lod_in = lod_in;
-        st.first_ts = first_ts;
-        st.comp = comp;
-        st.flags = BF_LAST_STAGE;
-        st.nkeep = (uint32_t)__popcll(alive);
-        st.nout = st.nkeep;
-        st.sec_len = sec_len;
-        st.err_stage = 0xFFFFFFFFu;
-        a.bstat[b] = st;
-      }
-    }
-    (void)vs;
-    (void)vl;
-    (void)it;
-    if (bn >= a.nbatches) break;
-    b = bn;
-  }
-}
-
-// ---------------------------------------------------------------------------
 // k_mins: first surviving / erroring / undecodable / unsupported batch
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_mins(const BatchStat* bstat, uint32_t n, Mins* mins) {
@@ -4960,26 +4484,6 @@ static uint32_t lean_grid(bool json) {
   return c;
 }
 
-// resident workgroups of k_rec_lean on the current device
-static uint32_t rec_grid(bool json) {
-  static std::mutex mu;
-  static uint32_t cache[64][2];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-  std::lock_guard<std::mutex> lock(mu);
-  uint32_t& c = cache[dev][json ? 1 : 0];
-  if (!c) {
-    int cus = 0, per = 0;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (json)
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_rec_lean<true>, kRlThreads, 0);
-    else
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_rec_lean<false>, kRlThreads, 0);
-    c = (uint32_t)std::max(1, cus) * (uint32_t)std::max(1, per);
-  }
-  return c;
-}
-
 void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s) {
   if (!a.nbatches) return;
   const size_t dyn = (ops & opbit(OP_REGEX)) ? kDfaDyn : 0;
@@ -4989,16 +4493,6 @@ void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s) {
     // record starts (k_chase_x), then the lean array kernel (fsg_array.hip)
     hipLaunchKernelGGL(k_chase_x, dim3(std::min<uint32_t>((a.nbatches + 255) / 256, 4096)), dim3(256), 0, s, a);
     launch_array_lean(a, s);
-    grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list
-  } else if (mode == EVAL_LEAN && !(ops & opbit(OP_REGEX))) {
-    // a wave per record (substring / filter_json / projection / uppercase)
-    const bool json = (ops & (opbit(OP_FILTER_JSON) | opbit(OP_PROJECT))) != 0;
-    const uint32_t g = std::min<uint32_t>(a.nbatches, rec_grid(json));
-    hipLaunchKernelGGL(k_chase, dim3((a.nbatches + kChaseT - 1) / kChaseT), dim3(kChaseT), 0, s, a);
-    if (json)
-      hipLaunchKernelGGL(k_rec_lean<true>, dim3(g), dim3(kRlThreads), 0, s, a);
-    else
-      hipLaunchKernelGGL(k_rec_lean<false>, dim3(g), dim3(kRlThreads), 0, s, a);
     grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list
   } else if (mode == EVAL_LEAN) {
     // persistent: as many workgroups as fit on the device at once
