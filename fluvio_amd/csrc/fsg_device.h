@@ -114,7 +114,45 @@ enum BatchFlags : uint32_t {
   BF_DECODE = 2u,      // Vec<Record> decode failed -> the process() call returns Err
   BF_UNSUPPORTED = 4u, // input needs a feature the GPU path does not implement
   BF_LAST_STAGE = 8u,  // the error (if any) happened in the last stage -> records_out counted
+  BF_ARR_LEAN = 16u,   // array_map batch of k_arr_lean: sized from ArrBatch, written by k_arr_write
 };
+
+// varint size with the encoder quirk (varint.rs:68-80)
+__device__ __forceinline__ uint32_t vsize(int64_t num) {
+  int64_t v = (int64_t)(((uint64_t)num << 1) ^ (uint64_t)(num >> 31));
+  uint32_t n = 1;
+  while (v & (int64_t)0xffffff80) {
+    n++;
+    v >>= 7;
+  }
+  return n;
+}
+// variant_encode (varint.rs:43-66); returns bytes written
+__device__ __forceinline__ uint32_t venc(int64_t num, uint8_t* out) {
+  int64_t v = (int64_t)(((uint64_t)num << 1) ^ (uint64_t)(num >> 31));
+  uint32_t k = 0;
+  while (v & (int64_t)0xffffff80) {
+    out[k++] = (uint8_t)((v & 0x7f) | 0x80);
+    v >>= 7;
+  }
+  out[k++] = (uint8_t)v;
+  return k;
+}
+
+// k_arr_lean's per-batch element statistics (array_map, fsg_array.hip).  An
+// element's output record is 5 + vsize(rel) + L + [L >= 60 - vsize(rel)]
+// bytes, L = vsize(len) + len, so the batch's bytes follow from these counts
+// once k_size knows the offset rebase `rel`.
+struct ArrBatch {
+  uint32_t ne;         // elements
+  uint32_t esum;       // Σ L
+  uint32_t c59;        // elements with L >= 59
+  uint32_t cnt[9];     // elements with L = 50 .. 58
+};
+// per lean array batch, two bitmaps over its window offsets: element starts,
+// then element ends (exclusive); the k-th start pairs with the k-th end
+constexpr uint32_t kArrBmWords = kWin / 32;                // u32 words per bitmap
+constexpr uint32_t kArrBmBatch = 2 * kArrBmWords;          // per batch
 
 struct BatchStat {
   int64_t base_offset;
@@ -240,6 +278,8 @@ struct EvalArgs {
   uint16_t* rend;      // ... and the last one ends at rend[b] (0xFFFF: no lean framing, exact path)
   const uint8_t* pass; // per batch, 1: the records pass through unchanged (no stage runs on them:
                        // an earlier segment's partial output before its error), nullptr: none
+  ArrBatch* arr_b;     // array_map lean path: per batch element statistics ...
+  uint32_t* arr_bm;    // ... and element bitmaps (kArrBmBatch words per batch)
 };
 
 struct SizeArgs {
@@ -255,6 +295,7 @@ struct SizeArgs {
   const ElemRec* elem;
   uint64_t acc_len;        // aggregate (concat): initial accumulator bytes
   uint32_t seg;            // 1: segment output (no offset rebase: rel = 0)
+  const ArrBatch* arr_b;   // BF_ARR_LEAN batches: element statistics
 };
 
 struct PlanArgs {
@@ -284,6 +325,42 @@ struct WriteArgs {
   const uint8_t* cat;      // aggregate (concat): kCatOff + accumulator stream
   uint64_t acc_len;
   uint32_t seg;            // 1: segment output: batch b's records at 61 * (b + 1) + pre[b], rel = 0
+};
+// k_arr_write: the output records of the BF_ARR_LEAN batches of [plan.first,
+// plan.last], re-walked from the source window (fsg_array.hip)
+struct ArrWriteArgs {
+  const uint8_t* slice;
+  const uint64_t* bpos;
+  const uint64_t* rbase;
+  uint32_t nbatches;
+  uint32_t seg;            // WriteArgs::seg
+  uint64_t nrec;
+  const BatchStat* bstat;
+  const uint32_t* arr_bm;
+  const ScanRow* pre;
+  const Plan* plan;
+  uint8_t* out;
+  // fused CRC32C (nullptr acc: k_crc16 runs after): raw CRC partials of the
+  // bytes written, moved to crc_zend (the aligned end of the CRC region) and
+  // XOR-ed into *crc_acc
+  uint32_t* crc_acc;
+  uint64_t crc_zend;       // output offset
+  const uint32_t* crc_z16;    // g_crc_z16 [16][256]
+  const uint32_t* crc_shift;  // g_crc_shift [48][4][256]
+};
+// k_one: the whole process() of a one-batch input in one workgroup (the
+// producer's one-record path, f3): eval, minima, size, plan, header, write,
+// CRC32C.  Stateless chains only; an output past out_cap is left to the
+// host (the plan says how big it is).
+struct OneArgs {
+  EvalArgs ea;       // nbatches = 1; ea.bstat / ea.mins point into the read-back block
+  ScanRow* rows;     // [1]
+  ScanRow* pre;      // [1]
+  Plan* plan;
+  uint8_t* out;      // output batch, out_cap bytes
+  uint64_t out_cap;
+  int32_t empty_chain;
+  int32_t pad;
 };
 // a chain segment's output as the next segment's input slice (k_seg_headers):
 // batch b in [0, nb) = the source batch's 57-byte header (base offset, last

@@ -37,28 +37,6 @@ __device__ __forceinline__ uint64_t rd_be(const uint8_t* p, int n) {
   return v;
 }
 
-// varint size with the encoder quirk (varint.rs:68-80)
-__device__ __forceinline__ uint32_t vsize(int64_t num) {
-  int64_t v = (int64_t)(((uint64_t)num << 1) ^ (uint64_t)(num >> 31));
-  uint32_t n = 1;
-  while (v & (int64_t)0xffffff80) {
-    n++;
-    v >>= 7;
-  }
-  return n;
-}
-// variant_encode (varint.rs:43-66); returns bytes written
-__device__ __forceinline__ uint32_t venc(int64_t num, uint8_t* out) {
-  int64_t v = (int64_t)(((uint64_t)num << 1) ^ (uint64_t)(num >> 31));
-  uint32_t k = 0;
-  while (v & (int64_t)0xffffff80) {
-    out[k++] = (uint8_t)((v & 0x7f) | 0x80);
-    v >>= 7;
-  }
-  out[k++] = (uint8_t)v;
-  return k;
-}
-
 __device__ __forceinline__ uint32_t dec_len_i32(int32_t v) {
   uint32_t u = v < 0 ? (uint32_t)(-(int64_t)v) : (uint32_t)v;
   uint32_t n = 1;
@@ -93,6 +71,10 @@ __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o, 64);
   return v;
 }
 template <typename T>
@@ -404,7 +386,7 @@ __device__ bool walk_fast(WaveLds& L, const uint8_t* w, uint64_t wbase, uint32_t
   const uint64_t sec_lim64 = sec_end - wbase;
   const uint32_t have = wlen < sec_lim64 ? wlen : (uint32_t)sec_lim64;
   if (rsb) {
-    // record starts precomputed by k_chase_x (offsets from al0): every lane
+    // record starts precomputed by k_chase_w (offsets from al0): every lane
     // takes its records' bounds; the records that end inside the window are a prefix
     const uint32_t lim = rec_remaining < (uint32_t)kMaxR ? rec_remaining : (uint32_t)kMaxR;
     bool in = false;
@@ -1061,7 +1043,7 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
   }
   bool first_window = true;  // the window at al0 is already resident
   const uint32_t nrec_total = count > 0 ? (uint32_t)count : 0u;
-  // record starts from k_chase_x / k_chase when they framed this batch
+  // record starts from k_chase_w / k_chase when they framed this batch
   const uint32_t rend_b = a.rend ? a.rend[b] : 0xFFFFu;
   const uint16_t* rsb = (a.rstart && rend_b != 0xFFFFu) ? a.rstart + a.rbase[b] : nullptr;
   const uint64_t rb = a.rbase[b];
@@ -2037,14 +2019,24 @@ __global__ __launch_bounds__(kChaseT) void k_chase(EvalArgs a) {
   for (uint64_t i = tail0 + t; i < n; i += kChaseT) dst[i] = st[i];
 }
 
-// k_chase_x — the same record framing for the exact kernel: any record count
-// (batch up to 64 KiB from its aligned start), starts stored directly
-__global__ __launch_bounds__(256) void k_chase_x(EvalArgs a) {
-  for (uint32_t b = blockIdx.x * 256 + threadIdx.x; b < a.nbatches; b += gridDim.x * 256) {
+// k_chase_w — the same record framing for the exact kernel and the lean array
+// kernel: any record count, a batch up to 64 KiB from its aligned start.  One
+// wave per batch: the window streams through registers 16 KiB at a time (row
+// k = 1 KiB, lane = 16 bytes), and the wave-uniform walk reads each length
+// varint with two readlanes (no dependent memory loads on the chain); the
+// starts are gathered one per lane and stored 64 at a time.
+__device__ __forceinline__ uint32_t sel4(const uint4& v, uint32_t c) {
+  return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
+}
+constexpr int kChaseRows = 16;
+__global__ __launch_bounds__(256) void k_chase_w(EvalArgs a) {
+  const uint32_t lane = lane_id();
+  const uint32_t nw = gridDim.x * 4;
+  // the batch index is wave-uniform: readfirstlane keeps the whole walk scalar
+  for (uint32_t b = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); b < a.nbatches; b += nw) {
     const uint64_t pos = a.bpos[b];
     const uint64_t rb = a.rbase[b], rn = (b + 1 < a.nbatches ? a.rbase[b + 1] : a.nrec) - rb;
     const uint64_t al = pos & ~15ull;
-    const uint8_t* base = a.slice + al;
     const uint32_t batch_len = __builtin_bswap32(ld_u32_at(a.slice + pos + 8));
     const uint64_t sec0 = pos + 57, sec_end = pos + 12 + (uint64_t)batch_len;
     const uint64_t sec_len = sec_end - sec0;
@@ -2052,26 +2044,54 @@ __global__ __launch_bounds__(256) void k_chase_x(EvalArgs a) {
     uint32_t end = 0xFFFFu;
     if (sec_len >= 4 && sec_end - al < 0xFFFFu && count >= 0 && (uint64_t)count == rn) {
       const uint32_t have = (uint32_t)(sec_end - al);
+      const uint64_t lim = a.slice_len + kSlicePad;  // readable bytes of the slice buffer
       uint32_t q = (uint32_t)(sec0 + 4 - al);
-      int n = 0;
-      for (; n < count; n++) {
-        const uint32_t x = ld_u32_at(base + q);
-        const uint32_t term = ~x & 0x80808080u;
-        if (!term) break;
-        const uint32_t nb = (((uint32_t)__builtin_ctz(term)) >> 3) + 1;
-        if (q + nb > have) break;
-        const uint32_t y = nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u));
-        const uint32_t v = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
-        if (v & 1u) break;  // negative length (zigzag)
-        const uint32_t len = v >> 1;
-        if (have - (q + nb) < len) break;
-        a.rstart[rb + n] = (uint16_t)q;
-        q += nb + len;
+      uint32_t n = 0, acc = 0;
+      bool ok = true;
+      for (uint32_t blk = 0; ok && n < (uint32_t)count && blk * 1024u * kChaseRows < have; blk++) {
+        uint4 R[kChaseRows + 1];
+#pragma unroll
+        for (int k = 0; k <= kChaseRows; k++) {
+          const uint64_t o = al + (uint64_t)(blk * kChaseRows + k) * 1024 + lane * 16;
+          R[k] = o + 16 <= lim ? *(const uint4*)(a.slice + o) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < kChaseRows; k++) {
+          const uint32_t row_end = (blk * kChaseRows + k + 1) * 1024u;
+          while (ok && n < (uint32_t)count && q < row_end) {
+            q = __builtin_amdgcn_readfirstlane(q);  // uniform (the compiler cannot see it through the loop)
+            n = __builtin_amdgcn_readfirstlane(n);
+            const uint32_t d = (q & 1023u) >> 2;  // dword of the row
+            const uint32_t w0 = __builtin_amdgcn_readlane(sel4(R[k], d & 3u), d >> 2);
+            const uint32_t w1 = d == 255 ? __builtin_amdgcn_readlane(R[k + 1].x, 0)
+                                         : __builtin_amdgcn_readlane(sel4(R[k], (d + 1) & 3u), (d + 1) >> 2);
+            const uint32_t x = __builtin_amdgcn_alignbyte(w1, w0, q & 3u);
+            const uint32_t term = ~x & 0x80808080u;
+            const uint32_t nb = (((uint32_t)__builtin_ctz(term | 0x80000000u)) >> 3) + 1;
+            const uint32_t y = nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u));
+            const uint32_t v = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
+            const uint32_t len = v >> 1;
+            // no terminator in 4 bytes, past the section, a negative length, past the section
+            if (!term || q + nb > have || (v & 1u) || have - (q + nb) < len) {
+              ok = false;
+              break;
+            }
+            if (lane == (n & 63u)) acc = q;
+            if ((n & 63u) == 63u) a.rstart[rb + n - 63 + lane] = (uint16_t)acc;
+            n++;
+            q += nb + len;
+          }
+        }
       }
-      if (n == count) end = q;
+      if (n & 63u)
+        if (lane < (n & 63u)) a.rstart[rb + (n & ~63u) + lane] = (uint16_t)acc;
+      if (ok && n == (uint32_t)count) end = q;
     }
-    a.rend[b] = (uint16_t)end;
+    if (lane == 0) a.rend[b] = (uint16_t)end;
   }
+}
+void launch_chase_w(const EvalArgs& a, hipStream_t s) {
+  if (a.nbatches) hipLaunchKernelGGL(k_chase_w, dim3(std::min<uint32_t>((a.nbatches + 3) / 4, 8192)), dim3(256), 0, s, a);
 }
 
 // four waves per SIMD (eight workgroups per CU, as many as the LDS holds)
@@ -2439,10 +2459,8 @@ __device__ __forceinline__ uint64_t array_rec_bytes(const KeptRec& d, const Elem
 }
 
 // k_size: one wave per batch (4 batches per 256-thread block)
-__global__ __launch_bounds__(256) void k_size(SizeArgs a) {
-  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+__device__ void size_batch(const SizeArgs& a, uint32_t b) {
   const uint32_t l = lane_id();
-  if (b >= a.nbatches) return;
   const BatchStat st = a.bstat[b];
   const uint32_t f = a.mins->first_keep;
   ScanRow row = {};
@@ -2461,18 +2479,29 @@ __global__ __launch_bounds__(256) void k_size(SizeArgs a) {
     const int32_t agg_base = a.agg_pre ? (int32_t)((uint64_t)a.acc0 + (uint64_t)a.agg_pre[b].agg) : 0;
     const uint64_t cat_base = a.agg_pre ? a.acc_len + a.agg_pre[b].cat : 0;
     uint64_t sum = 0;
-    const KeptRec* d = a.desc + a.rbase[b];
-    for (uint32_t k = l; k < st.nkeep; k += 64) {
-      const KeptRec r = d[k];
-      sum += r.mode == KM_ARRAY ? array_rec_bytes(r, a.elem, rel) : rec_out_size(r, rel, agg_base, cat_base);
+    if (st.flags & BF_ARR_LEAN) {  // k_arr_lean's counts (fsg_array.hip): elements with L >= 60 - vsize(rel)
+      const ArrBatch& ab = a.arr_b[b];  // take one more inner-length varint byte
+      const uint32_t vr = vsize(rel);
+      sum = (uint64_t)ab.ne * (5 + vr) + ab.esum + ab.c59;
+      for (uint32_t L = 60 - vr < 50 ? 50 : 60 - vr; L <= 58; L++) sum += ab.cnt[L - 50];
+    } else {
+      const KeptRec* d = a.desc + a.rbase[b];
+      for (uint32_t k = l; k < st.nkeep; k += 64) {
+        const KeptRec r = d[k];
+        sum += r.mode == KM_ARRAY ? array_rec_bytes(r, a.elem, rel) : rec_out_size(r, rel, agg_base, cat_base);
+      }
+      sum = wave_sum(sum);
     }
-    sum = wave_sum(sum);
     row.rec_bytes = sum;
     row.nonempty = st.nout ? 1 : 0;
     row.lod = (uint64_t)(int64_t)(st.lod_in + 1);
     row.nrec = st.nout;
   }
   if (l == 0) a.rows[b] = row;
+}
+__global__ __launch_bounds__(256) void k_size(SizeArgs a) {
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b < a.nbatches) size_batch(a, b);
 }
 
 // ---------------------------------------------------------------------------
@@ -2591,8 +2620,7 @@ __device__ __forceinline__ ScanRow incl_at(const PlanArgs& a, uint32_t i) {
   return r;
 }
 
-__global__ void k_plan(PlanArgs a) {
-  if (threadIdx.x != 0) return;
+__device__ void plan_run(const PlanArgs& a) {
   const uint32_t NONE = 0xFFFFFFFFu;
   const uint32_t n = a.nbatches;
   const uint32_t f = a.mins->first_keep, e = a.mins->first_err, d = a.mins->first_dec, u = a.mins->first_unsup;
@@ -2675,6 +2703,9 @@ __global__ void k_plan(PlanArgs a) {
   }
   *a.plan = p;
 }
+__global__ void k_plan(PlanArgs a) {
+  if (threadIdx.x == 0) plan_run(a);
+}
 
 // k_state: the aggregate-sum accumulator after this call, kept in HBM
 // (SmartModuleAggregate.accumulator, transforms/aggregate.rs:95): unchanged
@@ -2723,8 +2754,7 @@ void launch_seg_headers(const SegArgs& a, hipStream_t s) {
 // ---------------------------------------------------------------------------
 // k_header: output batch header (Batch::default() + base offset, lod, count)
 // ---------------------------------------------------------------------------
-__global__ void k_header(const Plan* plan, uint8_t* out) {
-  if (threadIdx.x != 0) return;
+__device__ void header_run(const Plan* plan, uint8_t* out) {
   const Plan p = *plan;
   uint8_t h[61];
   auto be = [&](int off, uint64_t v, int nb) {
@@ -2744,6 +2774,9 @@ __global__ void k_header(const Plan* plan, uint8_t* out) {
   be(53, (uint32_t)-1, 4);  // first_sequence
   be(57, (uint32_t)p.n_records, 4);
   for (int i = 0; i < 61; i++) out[i] = h[i];
+}
+__global__ void k_header(const Plan* plan, uint8_t* out) {
+  if (threadIdx.x == 0) header_run(plan, out);
 }
 
 // ---------------------------------------------------------------------------
@@ -2911,10 +2944,7 @@ __device__ void write_array_batch(const WriteArgs& a, const KeptRec* d, uint32_t
 // each key/value payload with all 64 lanes (copy_seg).  aggregate (concat)
 // values are prefixes of the accumulator stream built by k_cat.
 constexpr int kWriteThreads = 256;
-__global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
-  const Plan p = *a.plan;
-  const int32_t b = p.first + (int32_t)(blockIdx.x * (kWriteThreads / 64) + (threadIdx.x >> 6));
-  if (p.first < 0 || b > p.last) return;
+__device__ void write_batch(const WriteArgs& a, const Plan& p, int32_t b) {
   const uint32_t lane = lane_id();
   const BatchStat st = a.bstat[b];
   const int64_t rel = a.seg ? 0 : a.bstat[p.first].base_offset - st.base_offset;
@@ -2924,6 +2954,7 @@ __global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
   const uint64_t obase = a.seg ? 61ull * (uint64_t)(b + 1) + a.pre[b].rec_bytes
                                : 61 + (a.pre[b].rec_bytes - a.pre[p.first].rec_bytes);
   uint8_t* out = a.out;
+  if (st.flags & BF_ARR_LEAN) return;  // k_arr_write (fsg_array.hip)
   if (st.nkeep && d[0].mode == KM_ARRAY) {  // a batch's descriptors share one mode
     write_array_batch<false>(a, d, st.nkeep, rel, obase);
     return;
@@ -2990,6 +3021,12 @@ __global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
     }
     run += readlane_u64(incl, 63);
   }
+}
+__global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
+  const Plan p = *a.plan;
+  const int32_t b = p.first + (int32_t)(blockIdx.x * (kWriteThreads / 64) + (threadIdx.x >> 6));
+  if (p.first < 0 || b > p.last) return;
+  write_batch(a, p, b);
 }
 
 // Array elements whose canonical text differs from their source text (floats,
@@ -3705,10 +3742,19 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc16(const uint8_t* __restrict
   }
 }
 
-// tail bytes [tail0, end) bytewise, init/xorout, big-endian CRC at out[17..21)
-__global__ void k_crc_final(uint8_t* out, const uint32_t* acc, uint64_t tail0, uint64_t end, uint64_t n) {
+// tail bytes [tail0, end) bytewise, init/xorout, big-endian CRC at out[17..21).
+// hdr_end > 0: the partials in *acc came from the writers (fused CRC), which
+// leave out the batch header's bytes [21, hdr_end): their raw CRC is added here,
+// moved to the end of the aligned region (tail0) with the shift tables.
+__global__ void k_crc_final(uint8_t* out, const uint32_t* acc, uint64_t tail0, uint64_t end, uint64_t n,
+                            uint64_t hdr_end) {
   if (threadIdx.x != 0) return;
   uint32_t c = *acc;
+  if (hdr_end) {
+    uint32_t h = 0;
+    for (uint64_t i = 21; i < hdr_end; i++) h = g_crc_z16[0][(h ^ out[i]) & 0xff] ^ (h >> 8);
+    c ^= crc_shift_bytes(h, tail0 - hdr_end);
+  }
   for (uint64_t i = tail0; i < end; i++) c = g_crc_z16[0][(c ^ out[i]) & 0xff] ^ (c >> 8);
   uint32_t crc = c ^ crc_shift_bytes(0xFFFFFFFFu, n) ^ 0xFFFFFFFFu;
   out[17] = (uint8_t)(crc >> 24);
@@ -4490,9 +4536,11 @@ void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s) {
   EvalArgs e = a;
   uint32_t grid = a.nbatches;
   if (mode == EVAL_ARRAY) {
-    // record starts (k_chase_x), then the lean array kernel (fsg_array.hip)
-    hipLaunchKernelGGL(k_chase_x, dim3(std::min<uint32_t>((a.nbatches + 255) / 256, 4096)), dim3(256), 0, s, a);
+    // the lean array kernel (fsg_array.hip) frames its own batches; the exact
+    // kernel chases the records of the batches it defers itself
     launch_array_lean(a, s);
+    e.rstart = nullptr;
+    e.rend = nullptr;
     grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list
   } else if (mode == EVAL_LEAN) {
     // persistent: as many workgroups as fit on the device at once
@@ -4506,13 +4554,12 @@ void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s) {
     grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list
   } else {
     e.list = nullptr;
-    // record starts for the exact kernel (no serial chase per window): a chain
-    // of dependent global loads per batch, so only where batches hold few
-    // records (measured on MI355X: C4 ~240 records/batch eval 6.6 -> 5.5 ms;
-    // ~2000 tiny records per batch over a few hundred batches is slower than the
-    // lane-0 chase through LDS; a handful of batches is not worth the launch)
+    // record starts for the exact kernel (no serial chase per window): k_chase_w
+    // where batches hold few records (~2000 tiny records per batch over a few
+    // hundred batches is left to the lane-0 chase through LDS; a handful of
+    // batches is not worth the launch)
     if (e.rstart && a.nbatches >= 64 && a.nrec <= 256ull * a.nbatches)
-      hipLaunchKernelGGL(k_chase_x, dim3(std::min<uint32_t>((a.nbatches + 255) / 256, 4096)), dim3(256), 0, s, e);
+      launch_chase_w(e, s);
     else
       e.rstart = nullptr, e.rend = nullptr;
   }
@@ -4663,7 +4710,130 @@ void launch_crc(uint8_t* out, uint64_t off, uint64_t n, uint32_t* acc, hipStream
     const uint32_t grid = (uint32_t)(nchunks < 768 ? nchunks : 768);  // 3 workgroups per CU (LDS)
     hipLaunchKernelGGL(k_crc16, dim3(grid), dim3(kCrcThreads), 0, s, (const uint8_t*)out, off - 16, nblocks, acc);
   }
-  hipLaunchKernelGGL(k_crc_final, dim3(1), dim3(64), 0, s, out, (const uint32_t*)acc, nblocks ? zend : off, end, n);
+  hipLaunchKernelGGL(k_crc_final, dim3(1), dim3(64), 0, s, out, (const uint32_t*)acc, nblocks ? zend : off, end, n,
+                     (uint64_t)0);
+}
+// the fused path: *acc already holds the raw CRC partials of out[hdr_end, zend)
+// (XOR-combined at zend by the writers); the header bytes and the tail here
+void launch_crc_fused(uint8_t* out, uint64_t hdr_end, uint64_t end, uint32_t* acc, hipStream_t s) {
+  const uint64_t zend = end & ~15ull;
+  hipLaunchKernelGGL(k_crc_final, dim3(1), dim3(64), 0, s, out, (const uint32_t*)acc, zend, end, end - 21, hdr_end);
+}
+void crc_table_ptrs(const uint32_t** z16, const uint32_t** shift) {
+  void* p = nullptr;
+  *z16 = hipGetSymbolAddress(&p, HIP_SYMBOL(g_crc_z16)) == hipSuccess ? (const uint32_t*)p : nullptr;
+  *shift = hipGetSymbolAddress(&p, HIP_SYMBOL(g_crc_shift)) == hipSuccess ? (const uint32_t*)p : nullptr;
+}
+
+// k_one — process() of a one-batch input in one 256-thread workgroup: the
+// exact evaluation (eval_batch), then the cross-batch passes collapsed to one
+// batch (minima, size row, plan, header, k_write's wave, CRC32C by one wave),
+// each phase behind a fence and a barrier.  One launch instead of ~12, and
+// no host wait between the plan and the write (the output is bounded by
+// out_cap: a larger one is left unwritten for the host to redo).
+__device__ void crc_wave(uint8_t* out, uint64_t end) {  // CRC32C of out[21, end) into out[17..21)
+  const uint32_t l = lane_id();
+  const uint64_t zend = end & ~15ull;
+  const uint64_t nb = zend > 16 ? (zend - 16) / 16 : 0;  // 16-byte units from out + 16
+  uint32_t c = 0;
+  int64_t lastu = -1;
+  for (uint64_t u = l; u < nb; u += 64) {
+    const uint4 v = ((const uint4*)(out + 16))[u];
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    if (u == 0) w[0] = 0, w[1] &= ~0xffu;  // out[16, 21) precede the CRC region
+    uint32_t r = 0;
+#pragma unroll
+    for (int q = 0; q < 16; q++) r ^= g_crc_z16[15 - q][(w[q >> 2] >> (8 * (q & 3))) & 0xff];
+    c = crc_shift_tab(g_crc_shift[10], c) ^ r;  // the lane's earlier units: 1 KiB back
+    lastu = (int64_t)u;
+  }
+  if (lastu >= 0) c = crc_shift_bytes(c, (nb - 1 - (uint64_t)lastu) * 16);
+  c = wave_xor(c);
+  if (l == 0) {
+    for (uint64_t i = nb ? zend : 21; i < end; i++) c = g_crc_z16[0][(c ^ out[i]) & 0xff] ^ (c >> 8);
+    const uint32_t crc = c ^ crc_shift_bytes(0xFFFFFFFFu, end - 21) ^ 0xFFFFFFFFu;
+    out[17] = (uint8_t)(crc >> 24);
+    out[18] = (uint8_t)(crc >> 16);
+    out[19] = (uint8_t)(crc >> 8);
+    out[20] = (uint8_t)crc;
+  }
+}
+template <uint32_t kOps>
+__global__ __launch_bounds__(kEvalThreads) void k_one(OneArgs o) {
+  __shared__ WaveLds L;
+  const uint32_t t = threadIdx.x;
+  const EvalArgs& a = o.ea;
+  eval_batch<kOps>(a, L, 0);
+  __threadfence();
+  __syncthreads();
+  if (t == 0) {  // k_mins over the one batch
+    const BatchStat st = a.bstat[0];
+    Mins m = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, {0, 0, 0}};
+    if (st.flags & BF_DECODE) m.first_dec = 0;
+    if (st.flags & BF_UNSUPPORTED) m.first_unsup = 0;
+    if (!(st.flags & BF_DECODE)) {
+      if (st.nout) m.first_keep = 0;
+      if (st.flags & BF_ERR) m.first_err = 0;
+    }
+    *a.mins = m;
+    o.pre[0] = ScanRow{};
+  }
+  __threadfence();
+  __syncthreads();
+  SizeArgs sa{};
+  sa.bstat = a.bstat;
+  sa.desc = a.desc;
+  sa.rbase = a.rbase;
+  sa.mins = a.mins;
+  sa.rows = o.rows;
+  sa.nbatches = 1;
+  if (t < 64) size_batch(sa, 0);
+  __threadfence();
+  __syncthreads();
+  if (t == 0) {  // one batch: the exclusive prefix is zero, no max_bytes cut
+    PlanArgs pa{};
+    pa.bstat = a.bstat;
+    pa.rows = o.rows;
+    pa.pre = o.pre;
+    pa.mins = a.mins;
+    pa.plan = o.plan;
+    pa.nbatches = 1;
+    pa.empty_chain = o.empty_chain;
+    plan_run(pa);
+  }
+  __threadfence();
+  __syncthreads();
+  const Plan p = *o.plan;
+  const uint64_t end = 61 + p.rec_bytes;
+  if (p.status != 0 || end > o.out_cap) return;
+  if (t == 0) header_run(o.plan, o.out);
+  if (t < 64 && p.first == 0 && p.last == 0) {
+    WriteArgs wa{};
+    wa.slice = a.slice;
+    wa.bstat = a.bstat;
+    wa.desc = a.desc;
+    wa.rbase = a.rbase;
+    wa.pre = o.pre;
+    wa.plan = o.plan;
+    wa.out = o.out;
+    write_batch(wa, p, 0);
+  }
+  __threadfence();
+  __syncthreads();
+  if (t < 64) crc_wave(o.out, end);
+}
+void launch_one(const OneArgs& o, uint32_t ops, hipStream_t s) {
+  const size_t dyn = (ops & opbit(OP_REGEX)) ? kDfaDyn : 0;
+  if ((ops & ~kOpsContains) == 0)
+    hipLaunchKernelGGL(k_one<kOpsContains>, dim3(1), dim3(kEvalThreads), dyn, s, o);
+  else if ((ops & ~kOpsRegex) == 0)
+    hipLaunchKernelGGL(k_one<kOpsRegex>, dim3(1), dim3(kEvalThreads), dyn, s, o);
+  else if ((ops & ~kOpsJson) == 0)
+    hipLaunchKernelGGL(k_one<kOpsJson>, dim3(1), dim3(kEvalThreads), dyn, s, o);
+  else if ((ops & ~kOpsInt) == 0)
+    hipLaunchKernelGGL(k_one<kOpsInt>, dim3(1), dim3(kEvalThreads), dyn, s, o);
+  else
+    hipLaunchKernelGGL(k_one<kOpsAll>, dim3(1), dim3(kEvalThreads), dyn, s, o);
 }
 
 // stateful last stage (k_sf_*), between the eval and the size passes

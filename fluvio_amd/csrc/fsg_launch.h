@@ -8,12 +8,16 @@ namespace fsg {
 hipError_t upload_crc_tables();
 // ops: bit per StageOp in the chain.  mode: EVAL_EXACT = k_eval over every
 // batch; EVAL_LEAN = k_chase + k_eval_lean, then k_eval over its deferred list;
-// EVAL_ARRAY = k_chase_x + k_arr_lean (fsg_array.hip), then k_eval over its deferred list
+// EVAL_ARRAY = k_chase_w + k_arr_lean (fsg_array.hip), then k_eval over its deferred list
 enum EvalMode { EVAL_EXACT = 0, EVAL_LEAN = 1, EVAL_ARRAY = 3 };
 void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s);
 // array_map_json_array alone over the source values (fsg_array.hip)
 bool array_lean_eligible(const ChainDesc& ch, uint32_t ops);
 void launch_array_lean(const EvalArgs& a, hipStream_t s);
+// the output records of its BF_ARR_LEAN batches among the nblk of the plan
+void launch_array_write(const ArrWriteArgs& a, uint32_t nblk, hipStream_t s);
+// record starts / ends of every batch (k_chase_w)
+void launch_chase_w(const EvalArgs& a, hipStream_t s);
 void launch_mins(const BatchStat* bstat, uint32_t n, Mins* mins, hipStream_t s);
 void launch_size(const SizeArgs& a, hipStream_t s);
 uint32_t scan_tiles(uint32_t n);
@@ -31,6 +35,12 @@ void launch_canon_len(const SizeArgs& a, const uint8_t* slice, hipStream_t s);
 void launch_write_canon(const WriteArgs& a, uint32_t nblk, hipStream_t s);
 void launch_cat(const WriteArgs& a, uint32_t nbatches, hipStream_t s);
 void launch_crc(uint8_t* out, uint64_t off, uint64_t n, uint32_t* acc, hipStream_t s);
+// process() of a one-batch input in one launch (k_one)
+void launch_one(const OneArgs& o, uint32_t ops, hipStream_t s);
+// CRC32C when the writers already folded out[hdr_end, end & ~15) into *acc
+void launch_crc_fused(uint8_t* out, uint64_t hdr_end, uint64_t end, uint32_t* acc, hipStream_t s);
+// device addresses of the CRC32C tables (slice-by-16 and the 2^k zero-byte shifts)
+void crc_table_ptrs(const uint32_t** z16, const uint32_t** shift);
 void launch_write_lean(const WriteArgs& a, uint32_t nblocks, hipStream_t s);
 // aggregate-json, in phases separated by host reads of AggjArgs::scal
 uint64_t xscan_tiles(uint64_t n);  // u64 scratch slots launch_xscan needs for n items

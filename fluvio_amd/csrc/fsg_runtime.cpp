@@ -512,6 +512,10 @@ struct fsg_chain {
   std::vector<uint8_t> acc;  // aggregate accumulator bytes (SmartModuleAggregate.accumulator)
   // scratch
   DevBuf bstat, kept, rows, pre, aggpre, tiles, grand, mins, plan, out, crcparts, defer, elem, cat;
+  DevBuf arr_b, arr_bm;  // lean array_map statistics and element bitmaps (per batch)
+  // the one-batch process() path (k_one): zeros for bpos / rbase, and one block
+  // read back with one copy: Plan | BatchStat | Mins | the output batch
+  DevBuf one_meta, one_blk;
   DevBuf dstate;  // aggregate-sum accumulator (i32) after the last call, in HBM
   // aggregate-json: key dictionary, index, initial keys, per-batch accumulator text
   DevBuf aj_tptr, aj_tlen, aj_kup, aj_out, aj_accoff, aj_acclen;  // aggregate-json
@@ -1906,7 +1910,8 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   const bool has_aggj = (c->hdesc.flags & CF_AGG_JSON) != 0;
   const size_t elem_cap = (has_array || has_aggj) ? (s->len / 2 + 2) : 0;  // ElemRec slots (fsg_device.h)
   const size_t need = (size_t)std::max<uint32_t>(nb, 1) * (sizeof(BatchStat) + 3 * sizeof(ScanRow)) +
-                      (size_t)std::max<uint64_t>(s->nrec, 1) * sizeof(KeptRec) + elem_cap * sizeof(ElemRec);
+                      (size_t)std::max<uint64_t>(s->nrec, 1) * sizeof(KeptRec) + elem_cap * sizeof(ElemRec) +
+                      (has_array ? (size_t)std::max<uint32_t>(nb, 1) * (sizeof(ArrBatch) + kArrBmBatch * 4) : 0);
   if (need > c->limit) {
     char b[160];
     snprintf(b, sizeof b, "Requested memory %zub exceeded max allowed %zub", need, c->limit);
@@ -1926,6 +1931,10 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   HIPCHK(c->mins.ensure(sizeof(Mins)));
   HIPCHK(c->plan.ensure(sizeof(Plan)));
   if (has_array || has_aggj) HIPCHK(c->elem.ensure(elem_cap * sizeof(ElemRec)));
+  if (has_array) {  // the lean array path's element statistics (fsg_array.hip)
+    HIPCHK(c->arr_b.ensure(std::max<uint32_t>(nb, 1) * sizeof(ArrBatch)));
+    HIPCHK(c->arr_bm.ensure(std::max<uint32_t>(nb, 1) * (size_t)kArrBmBatch * 4));
+  }
   const bool has_agg = c->agg_stage >= 0;
   const bool has_cat = has_agg && (c->hdesc.flags & CF_AGG_CAT);
   const int64_t acc0 = has_agg && !has_cat && !has_aggj ? acc_value(c->acc) : 0;
@@ -1945,6 +1954,8 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   ea.mins = c->mins.as<Mins>();
   ea.list = c->defer.as<uint32_t>();
   ea.elem = (has_array || has_aggj) ? c->elem.as<ElemRec>() : nullptr;
+  ea.arr_b = has_array ? c->arr_b.as<ArrBatch>() : nullptr;
+  ea.arr_bm = has_array ? c->arr_bm.as<uint32_t>() : nullptr;
   ea.nrec = s->nrec;
   uint32_t ops = 0;
   bool lean_stages = true;  // every stage has a lean form
@@ -1969,7 +1980,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
                     !has_agg && lean_stages && nb > 1 &&  // one batch: the exact kernel alone (1 launch, not 3)
                     !s->has_pass;                         // pass-through batches: the exact kernel knows them
   ea.pass = s->has_pass ? s->pass.as<uint8_t>() : nullptr;
-  // record starts per batch (k_chase for the lean kernel, k_chase_x for the exact one)
+  // record starts per batch (k_chase for the lean kernel, k_chase_w for the exact and array ones)
   HIPCHK(c->rstart.ensure(((size_t)s->nrec + 64) * sizeof(uint16_t)));  // + a wave of over-read
   HIPCHK(c->rend.ensure(((size_t)nb + 1) * sizeof(uint16_t)));
   ea.rstart = c->rstart.as<uint16_t>();
@@ -2154,6 +2165,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   sa.elem = ea.elem;
   sa.acc_len = has_cat ? c->acc.size() : 0;
   sa.seg = so ? 1u : 0u;
+  sa.arr_b = ea.arr_b;
   if (has_array) launch_canon_len(sa, ea.slice, st);
   if (has_agg) {
     sa.agg_only = 1;
@@ -2291,6 +2303,8 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   if (!so) launch_header(pa.plan, wa.out, st);
   if (c->timed) HIPCHK(hipEventRecord(c->ev[3], st));
   const uint32_t nblk = p.last >= p.first && p.first >= 0 ? (uint32_t)(p.last - p.first + 1) : 0u;
+  // array_map with every batch on the lean path: CRC32C folded into k_arr_write
+  const bool fused_crc = arr && !so && c->last.deferred == 0 && nblk && out_len >= 64;
   // verbatim records (filters, uppercase, projections): staged in LDS
   // (k_write_lean; a batch beyond its staging buffer or 64 survivors takes the
   // wave path inside it); measured on MI355X: C2 1 KB records write 1.33 -> 1.23
@@ -2300,6 +2314,27 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     launch_write_lean(wa, nblk, st);
   else
     launch_write(wa, nblk, st);
+  if (arr) {  // the lean batches' element records (k_write skips them)
+    ArrWriteArgs aw{};
+    aw.slice = ea.slice;
+    aw.bpos = ea.bpos;
+    aw.rbase = ea.rbase;
+    aw.nbatches = nb;
+    aw.seg = wa.seg;
+    aw.nrec = s->nrec;
+    aw.bstat = ea.bstat;
+    aw.arr_bm = ea.arr_bm;
+    aw.pre = pa.pre;
+    aw.plan = pa.plan;
+    aw.out = wa.out;
+    if (fused_crc) {  // every batch lean: the writer folds the output's CRC32C as it stores
+      HIPCHK(hipMemsetAsync(c->crcparts.p, 0, sizeof(uint32_t), st));
+      aw.crc_acc = c->crcparts.as<uint32_t>();
+      aw.crc_zend = out_len & ~(size_t)15;
+      crc_table_ptrs(&aw.crc_z16, &aw.crc_shift);
+    }
+    launch_array_write(aw, nblk, st);
+  }
   if (has_array) launch_write_canon(wa, nblk, st);
   HIPCHK(hipGetLastError());
   if (c->timed) HIPCHK(hipEventRecord(c->ev[4], st));
@@ -2330,6 +2365,8 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     o->device_framed = true;
     o->decompressed = s->decompressed;
     o->has_pass = p.err_batch >= 0 || s->has_pass;
+  } else if (fused_crc) {
+    launch_crc_fused(wa.out, 61, out_len, c->crcparts.as<uint32_t>(), st);
   } else {
     launch_crc(wa.out, 21, out_len - 21, c->crcparts.as<uint32_t>(), st);
   }
@@ -2727,9 +2764,138 @@ extern "C" int fsg_chain_process_batch(fsg_chain* c, const uint8_t* slice, size_
 
 // SmartModuleChainInstance::process: one SmartModuleInput{base_offset, raw_bytes,
 // base_timestamp} is one batch of the same pipeline (no offset fix-up applies).
+namespace {
+// process() of a stateless chain in one launch (k_one): upload, k_one, one
+// read-back of plan + batch result + output, one wait.  1 = not taken (the
+// general path runs: a stateful / aggregate / array chain, a composed chain,
+// an output beyond the block).
+constexpr size_t kOneHead = 512;  // Plan | BatchStat | Mins, then the output batch
+int process_one(fsg_chain* c, const uint8_t* raw, size_t len, int64_t base_offset, int64_t base_timestamp,
+                fsg_metrics* m, fsg_output** out) {
+  if (!c->segs.empty() || c->agg_stage >= 0 || c->array_stage >= 0 || c->sf_stage >= 0 ||
+      (c->hdesc.flags & (CF_AGG_JSON | CF_STATEFUL | CF_ARRAY)))
+    return 1;
+  static_assert(sizeof(Plan) <= 192 && sizeof(BatchStat) <= 192 && sizeof(Mins) <= 64, "k_one read-back head");
+  const size_t in_len = 57 + len, alloc = slice_alloc(in_len);
+  const size_t cap = 128 + 4 * len;  // stateless outputs stay within the input's size plus the i32 digits
+  if (alloc + kOneHead + cap > kPinPlan + kSmallOut) return 1;
+  HIPCHK(c->hpin.ensure(kPinPlan + kSmallOut));
+  HIPCHK(c->ingest.data.ensure(alloc));
+  HIPCHK(c->one_blk.ensure(kOneHead + cap));
+  HIPCHK(c->kept.ensure(std::max<size_t>(len / 7 + 1, 1) * sizeof(KeptRec)));
+  HIPCHK(c->rows.ensure(sizeof(ScanRow)));
+  HIPCHK(c->pre.ensure(sizeof(ScanRow)));
+  if (!c->one_meta.p) {
+    HIPCHK(c->one_meta.ensure(16));
+    HIPCHK(hipMemsetAsync(c->one_meta.p, 0, 16, c->stream));
+  }
+  // the batch (Batch::default() + base offset / timestamp, the records as given)
+  // in pinned memory, one copy up
+  uint8_t* b = (uint8_t*)c->hpin.p;
+  memset(b, 0, alloc);
+  auto be = [&](size_t off, uint64_t v, int n) {
+    for (int i = 0; i < n; i++) b[off + i] = (uint8_t)(v >> (8 * (n - 1 - i)));
+  };
+  be(0, (uint64_t)base_offset, 8);
+  be(8, (uint32_t)(45 + len), 4);
+  be(12, (uint32_t)-1, 4);
+  b[16] = 2;
+  be(27, (uint64_t)base_timestamp, 8);
+  if (len) memcpy(b + 57, raw, len);
+  uint64_t nrec = 0;  // frame(): the count, clamped by the bytes a record needs at least
+  if (len >= 4) {
+    const int32_t cnt = (int32_t)rd_be(raw, 4);
+    nrec = std::min<uint64_t>(cnt > 0 ? (uint64_t)cnt : 0, (len - 4) / 7);
+  }
+  hipStream_t st = c->stream;
+  HIPCHK(hipMemcpyAsync(c->ingest.data.p, b, alloc, hipMemcpyHostToDevice, st));
+  uint8_t* blk = c->one_blk.as<uint8_t>();
+  OneArgs o{};
+  EvalArgs& ea = o.ea;
+  ea.slice = c->ingest.data.as<uint8_t>();
+  ea.slice_len = in_len;
+  ea.bpos = c->one_meta.as<uint64_t>();
+  ea.rbase = c->one_meta.as<uint64_t>() + 1;
+  ea.nbatches = 1;
+  ea.chain = c->d_desc.as<ChainDesc>();
+  ea.blob = c->d_blob.as<uint8_t>();
+  ea.bstat = (BatchStat*)(blk + 192);
+  ea.desc = c->kept.as<KeptRec>();
+  ea.mins = (Mins*)(blk + 384);
+  ea.nrec = nrec;
+  o.rows = c->rows.as<ScanRow>();
+  o.pre = c->pre.as<ScanRow>();
+  o.plan = (Plan*)blk;
+  o.out = blk + kOneHead;
+  o.out_cap = cap;
+  o.empty_chain = c->hdesc.nstages == 0 ? 1 : 0;
+  uint32_t ops = 0;
+  for (uint32_t k = 0; k < c->hdesc.nstages; k++) ops |= 1u << c->hdesc.st[k].op;
+  launch_one(o, ops, st);
+  HIPCHK(hipGetLastError());
+  uint8_t* hb = (uint8_t*)c->hpin.p + kPinPlan;  // the input staging (at hpin.p) is free once the copy ran
+  HIPCHK(hipMemcpyAsync(hb, blk, kOneHead + cap, hipMemcpyDeviceToHost, st));
+  HIPCHK(wait_stream(st));
+  Plan p;
+  BatchStat bs;
+  memcpy(&p, hb, sizeof p);
+  memcpy(&bs, hb + 192, sizeof bs);
+  if (p.status != 0) {
+    if (m) {
+      m->bytes_in += p.bytes_in;
+      m->invocation_count += p.invocations;
+    }
+    const char* why = p.status == FSG_E_UNSUPPORTED ? "input needs a feature the GPU path does not implement"
+                      : p.status == FSG_E_IO        ? "io error while decoding batches"
+                                                    : "failed to decode SmartModule base input";
+    return fail(p.status, why);
+  }
+  const uint64_t out_len = 61 + p.rec_bytes;
+  if (out_len > cap) return 1;  // nothing was written: the general path redoes the call
+  if (m) {
+    m->bytes_in += p.bytes_in;
+    m->invocation_count += p.invocations;
+    if (c->hdesc.nstages) m->records_out += p.records_out;
+  }
+  auto o2 = std::make_unique<fsg_output>();
+  memset(o2.get(), 0, sizeof(fsg_output));
+  const size_t rl = out_len - 57;  // u32 count + records
+  uint8_t* h = host_alloc(rl);
+  if (!h) return fail(FSG_E_DEVICE, "host allocation failed");
+  memcpy(h, hb + kOneHead + 57, rl);
+  o2->records = h;
+  o2->records_len = rl;
+  o2->n_records = (uint32_t)p.n_records;
+  if (p.err_batch >= 0) {
+    c->ingest.eng = c->eng;
+    c->ingest.len = in_len;
+    c->ingest.nb = 1;
+    c->ingest.nrec = nrec;
+    int rc = build_error(c, &c->ingest, bs, o2->error);
+    if (rc) {
+      host_free(h);
+      return rc;
+    }
+    o2->has_error = 1;
+  }
+  c->out_len = out_len;
+  c->last = fsg_timings{};
+  c->last.in_bytes = in_len;
+  c->last.out_bytes = out_len;
+  c->last.n_batches = 1;
+  c->last.n_records_in = nrec;
+  *out = o2.release();
+  return FSG_OK;
+}
+}  // namespace
+
 extern "C" int fsg_chain_process(fsg_chain* c, const uint8_t* raw, size_t len, int64_t base_offset,
                                  int64_t base_timestamp, fsg_metrics* m, fsg_output** out) {
   HIPCHK(hipSetDevice(c->eng->device));
+  {
+    const int rc = process_one(c, raw, len, base_offset, base_timestamp, m, out);
+    if (rc != 1) return rc;
+  }
   std::vector<uint8_t> b(slice_alloc(57 + len));  // zero-padded: uploaded in one copy
   auto be = [&](size_t off, uint64_t v, int n) {
     for (int i = 0; i < n; i++) b[off + i] = (uint8_t)(v >> (8 * (n - 1 - i)));

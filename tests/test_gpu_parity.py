@@ -279,6 +279,38 @@ def test_array_lean_parity(engine, seed, odd):
     assert g.last_timings()["deferred"] == 0
 
 
+def test_array_lean_rebase_and_varint_edges(engine):
+    """k_arr_lean / k_arr_write edges: offset rebases of 1..5 varint bytes,
+    element varint + text lengths around the inner-length threshold (L = 50 .. 60
+    against 60 - vsize(rel)), texts of 64+ bytes (two-byte length varints),
+    batches of more than 256 records (the writer's record chunks) and outputs
+    spanning several 16 KiB staging rounds."""
+    rng = random.Random(7)
+    sl, base = b"", 0
+    jumps = [0, 70, 20000, 3_000_000, 2**31]
+    for k in range(15):
+        b = P.Batch(base_offset=base)
+        kind = k % 3
+        nrec = (40, 900, 3)[kind]
+        for j in range(nrec):
+            if kind == 1:
+                v = "[%d]" % j if j % 7 else "[]"
+            else:
+                els = ['"' + "s" * rng.randrange(44, 70) + '"' for _ in range(rng.randint(1, 4))]
+                els.append(str(rng.randint(-99, 99)))
+                rng.shuffle(els)
+                v = "[" + ",".join(els) + "]"
+            b.add_record(P.Record.new(v.encode()))
+        sl += b.encode()
+        base += nrec + jumps[k % 5]
+    check_batch(engine, CHAINS["array_map"], sl)
+    check_batch(engine, CHAINS["array_map"], sl, max_bytes=50000)
+    g = gpu_chain(engine, CHAINS["array_map"])
+    g.process_batch(sl)
+    t = g.last_timings()
+    assert t["eval_path"] == 3 and t["deferred"] == 0, t
+
+
 # ---------------------------------------------------------------------------
 # composed chains: stages after an array_map, an aggregate or a stateful
 # filter (engine.rs:147-167 feeds each stage's successes to the next); the
