@@ -283,6 +283,10 @@ __global__ __launch_bounds__(kArrT) void k_arr_lean(EvalArgs a) {
     }
     __syncthreads();
     if (!defer && t < 64) {  // framing (Batch decode: count, then each record's length varint)
+      // The chain of length varints is serial; a span of 256 bytes from the
+      // current record start is decoded speculatively, four candidate starts
+      // per lane (their successor offsets kept in registers), and the chain is
+      // followed through the span with one readlane per record.
       const uint32_t have = (uint32_t)(sec_end - al);
       const uint32_t c0 = (uint32_t)(pos + 57 - al);
       const uint32_t count = __builtin_bswap32(lds4(L.W, c0));
@@ -290,19 +294,36 @@ __global__ __launch_bounds__(kArrT) void k_arr_lean(EvalArgs a) {
       bool ok = count == rn;
       while (ok && n < count) {
         q = __builtin_amdgcn_readfirstlane(q);
-        const uint32_t x = __builtin_amdgcn_readfirstlane(lds4(L.W, q));
-        const uint32_t term = ~x & 0x80808080u;
-        const uint32_t nb = (((uint32_t)__builtin_ctz(term | 0x80000000u)) >> 3) + 1;
-        const uint32_t y = nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u));
-        const uint32_t v = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
-        const uint32_t len = v >> 1;
-        // no terminator in 4 bytes, past the section, a negative length, past the section
-        ok = term && q + nb <= have && !(v & 1u) && have - (q + nb) >= len;
-        if (ok) {
-          if (l == 0) L.rs[n] = (uint16_t)q;
-          n++;
-          q += nb + len;
+        // candidates p = q + 4 l + j: successor offset from q, or 0 when the
+        // record there cannot frame (no terminator in 4 bytes, past the section,
+        // a negative length)
+        const uint32_t p0 = q + 4 * l;
+        const uint64_t x8 = (uint64_t)lds4(L.W, p0) | ((uint64_t)lds4(L.W, p0 + 4) << 32);
+        uint32_t nx[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t x = (uint32_t)(x8 >> (8 * j));
+          const uint32_t term = ~x & 0x80808080u;
+          const uint32_t nb = (((uint32_t)__builtin_ctz(term | 0x80000000u)) >> 3) + 1;
+          const uint32_t y = nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u));
+          const uint32_t v = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
+          const uint32_t p = p0 + j, len = v >> 1;
+          const bool good = term && p + nb <= have && !(v & 1u) && have - (p + nb) >= len;
+          nx[j] = good ? 4 * l + j + nb + len : 0u;
         }
+        uint32_t cur = 0;  // offset from q of the record start being framed
+        while (n < count && cur < 256) {
+          const uint32_t ln = cur >> 2, j = cur & 3;
+          const uint32_t nxt = __builtin_amdgcn_readlane(j == 0 ? nx[0] : j == 1 ? nx[1] : j == 2 ? nx[2] : nx[3], ln);
+          if (!nxt) {
+            ok = false;
+            break;
+          }
+          if (l == 0) L.rs[n] = (uint16_t)(q + cur);
+          n++;
+          cur = nxt;
+        }
+        q += cur;
       }
       if (l == 0) {
         L.rs[n] = (uint16_t)q;
@@ -423,7 +444,6 @@ struct ArwLds {
   uint32_t bm[kArrBmBatch];
   uint16_t es[kEl], ee[kEl];  // element starts / ends of the current round
   uint32_t part[kArrT / 64][2];
-  uint32_t red[kArrT / 64];
 };
 
 __device__ __forceinline__ void put(uint8_t* O, int32_t j, uint32_t c) {
@@ -471,65 +491,17 @@ __device__ __forceinline__ void wg_scan2(uint32_t (*part)[2], uint32_t x, uint32
   }
   __syncthreads();  // part is reused by the next scan
 }
-// CRC32C tables (fsg_kernels.hip): raw CRC of a 16-byte unit by slice-by-16,
-// and "append 2^k zero bytes" as four byte-indexed tables
-__device__ __forceinline__ uint32_t crc_unit(const uint32_t* z16, const uint32_t w[4]) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int q = 0; q < 16; q++) r ^= z16[(15 - q) * 256 + ((w[q >> 2] >> (8 * (q & 3))) & 0xffu)];
-  return r;
-}
-__device__ __forceinline__ uint32_t crc_shift1(const uint32_t* T, uint32_t c) {  // T = one level's [4][256]
-  return T[c & 0xff] ^ T[256 + ((c >> 8) & 0xff)] ^ T[512 + ((c >> 16) & 0xff)] ^ T[768 + (c >> 24)];
-}
-__device__ __forceinline__ uint32_t crc_shift_n(const uint32_t* sh, uint32_t c, uint64_t n) {
-  for (int k = 0; n; k++, n >>= 1)
-    if (n & 1) c = crc_shift1(sh + (size_t)k * 1024, c);
-  return c;
-}
-// staged bytes of global addresses [lo, hi) to HBM (staging index = address - B);
-// with a.crc_acc, their raw CRC32C partial (other bytes zero) moved to the CRC
-// region's aligned end and XOR-ed into *crc_acc (every thread calls it)
-__device__ void stage_flush(const ArrWriteArgs& a, const uint8_t* O, uint32_t* red, uint64_t B, uint64_t lo,
-                            uint64_t hi) {
-  const uint32_t t = threadIdx.x;
-  const uint64_t zend = (uint64_t)(uintptr_t)a.out + a.crc_zend;
-  const uint64_t U0 = lo & ~15ull;
-  uint32_t c = 0;
-  uint64_t last = 0;
-  bool any = false;
-  for (uint64_t X = U0 + 16ull * t; X < hi; X += 16ull * kArrT) {
+// staged bytes of global addresses [lo, hi) to HBM (staging index = address - B)
+__device__ void stage_flush(const uint8_t* O, uint64_t B, uint64_t lo, uint64_t hi) {
+  for (uint64_t X = (lo & ~15ull) + 16ull * threadIdx.x; X < hi; X += 16ull * kArrT) {
     const uint8_t* src = O + (X - B);
-    const uint4 v = *(const uint4*)src;
     if (X >= lo && X + 16 <= hi) {
-      *(uint4*)(uintptr_t)X = v;
+      *(uint4*)(uintptr_t)X = *(const uint4*)src;
     } else {
       for (uint32_t k = 0; k < 16; k++)
         if (X + k >= lo && X + k < hi) *(uint8_t*)(uintptr_t)(X + k) = src[k];
     }
-    if (a.crc_acc && X < zend) {
-      uint32_t w[4] = {v.x, v.y, v.z, v.w};
-      if (X < lo || X + 16 > hi) {  // bytes outside [lo, hi) count as zeros
-#pragma unroll
-        for (int k = 0; k < 16; k++)
-          if (X + k < lo || X + k >= hi) w[k >> 2] &= ~(0xffu << (8 * (k & 3)));
-      }
-      c = crc_shift1(a.crc_shift + 12 * 1024, c) ^ crc_unit(a.crc_z16, w);  // earlier units: 4 KiB back
-      last = X;
-      any = true;
-    }
   }
-  if (!a.crc_acc) return;
-  if (any) c = crc_shift_n(a.crc_shift, c, zend - (last + 16));  // to the region's aligned end
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) c ^= __shfl_xor(c, o, 64);
-  if ((t & 63) == 0) red[t >> 6] = c;
-  __syncthreads();
-  if (t == 0) {
-    const uint32_t x = red[0] ^ red[1] ^ red[2] ^ red[3];
-    if (x) atomicXor(a.crc_acc, x);
-  }
-  __syncthreads();
 }
 
 __global__ __launch_bounds__(kArrT) void k_arr_write(ArrWriteArgs a) {
@@ -598,7 +570,7 @@ __global__ __launch_bounds__(kArrT) void k_arr_write(ArrWriteArgs a) {
         wg_scan2(L.part, sz, 0, off, z0, ttot, z1);
         const uint64_t tlo = F, thi = F + ttot;
         if (thi > B + kStage && F > done) {  // the tile does not fit after what is staged: store that first
-          stage_flush(a, L.O, L.red, B, done, F);
+          stage_flush(L.O, B, done, F);
           __syncthreads();
           done = F;
           B = F & ~15ull;
@@ -624,7 +596,7 @@ __global__ __launch_bounds__(kArrT) void k_arr_write(ArrWriteArgs a) {
             B = R;
             break;
           }
-          stage_flush(a, L.O, L.red, R, done, R + kStage);
+          stage_flush(L.O, R, done, R + kStage);
           __syncthreads();
           done = R + kStage;
         }
@@ -632,7 +604,7 @@ __global__ __launch_bounds__(kArrT) void k_arr_write(ArrWriteArgs a) {
       }
       __syncthreads();  // es / ee are rewritten by the next round
     }
-    if (F > done) stage_flush(a, L.O, L.red, B, done, F);
+    if (F > done) stage_flush(L.O, B, done, F);
   }
 }
 

@@ -340,13 +340,6 @@ struct ArrWriteArgs {
   const ScanRow* pre;
   const Plan* plan;
   uint8_t* out;
-  // fused CRC32C (nullptr acc: k_crc16 runs after): raw CRC partials of the
-  // bytes written, moved to crc_zend (the aligned end of the CRC region) and
-  // XOR-ed into *crc_acc
-  uint32_t* crc_acc;
-  uint64_t crc_zend;       // output offset
-  const uint32_t* crc_z16;    // g_crc_z16 [16][256]
-  const uint32_t* crc_shift;  // g_crc_shift [48][4][256]
 };
 // k_one: the whole process() of a one-batch input in one workgroup (the
 // producer's one-record path, f3): eval, minima, size, plan, header, write,
@@ -356,12 +349,15 @@ struct OneArgs {
   EvalArgs ea;       // nbatches = 1; ea.bstat / ea.mins point into the read-back block
   ScanRow* rows;     // [1]
   ScanRow* pre;      // [1]
-  Plan* plan;
-  uint8_t* out;      // output batch, out_cap bytes
+  Plan* plan;        // the read-back block: Plan at +0, BatchStat at +192, Mins at +384 ...
+  uint8_t* out;      // ... the output batch at +kOneHead (out_cap bytes)
   uint64_t out_cap;
+  const uint8_t* hin;  // the input batch in pinned host memory (copied into ea.slice first), in_len bytes
+  uint8_t* hout;       // pinned host memory: the read-back block is copied here last
+  uint32_t in_len;
   int32_t empty_chain;
-  int32_t pad;
 };
+constexpr uint32_t kOneHead = 512;  // Plan | BatchStat | Mins, then the output batch
 // a chain segment's output as the next segment's input slice (k_seg_headers):
 // batch b in [0, nb) = the source batch's 57-byte header (base offset, last
 // offset delta, timestamps, attributes) with batch_len / the record count of

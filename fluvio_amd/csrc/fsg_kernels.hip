@@ -3742,19 +3742,10 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc16(const uint8_t* __restrict
   }
 }
 
-// tail bytes [tail0, end) bytewise, init/xorout, big-endian CRC at out[17..21).
-// hdr_end > 0: the partials in *acc came from the writers (fused CRC), which
-// leave out the batch header's bytes [21, hdr_end): their raw CRC is added here,
-// moved to the end of the aligned region (tail0) with the shift tables.
-__global__ void k_crc_final(uint8_t* out, const uint32_t* acc, uint64_t tail0, uint64_t end, uint64_t n,
-                            uint64_t hdr_end) {
+// tail bytes [tail0, end) bytewise, init/xorout, big-endian CRC at out[17..21)
+__global__ void k_crc_final(uint8_t* out, const uint32_t* acc, uint64_t tail0, uint64_t end, uint64_t n) {
   if (threadIdx.x != 0) return;
   uint32_t c = *acc;
-  if (hdr_end) {
-    uint32_t h = 0;
-    for (uint64_t i = 21; i < hdr_end; i++) h = g_crc_z16[0][(h ^ out[i]) & 0xff] ^ (h >> 8);
-    c ^= crc_shift_bytes(h, tail0 - hdr_end);
-  }
   for (uint64_t i = tail0; i < end; i++) c = g_crc_z16[0][(c ^ out[i]) & 0xff] ^ (c >> 8);
   uint32_t crc = c ^ crc_shift_bytes(0xFFFFFFFFu, n) ^ 0xFFFFFFFFu;
   out[17] = (uint8_t)(crc >> 24);
@@ -3768,44 +3759,59 @@ __global__ void k_crc_final(uint8_t* out, const uint32_t* acc, uint64_t tail0, u
 // ingest (north_star "verify CRC32C").  The reference computes the CRC only on
 // encode and never checks it (protocol record/batch.rs:398-430), so this only
 // reports: process_batch never looks at the result.  One wave per batch
-// (persistent over the batches): 16-byte units counted back from the batch
-// end (the first unit zero-masked before the CRC start: leading zeros leave a
-// raw CRC unchanged), lane j takes units j, j + 64, ... (coalesced), folding
-// each round with the 1 KiB shift table, then its partial moves to the batch
-// end and the wave XORs the partials.
+// (persistent over the batches) over the 16-byte-ALIGNED units covering the
+// CRC range [pos + 21, end) (one dwordx4 load each; bytes outside the range
+// masked to zero).  Lane j takes units j, j + 64, ... four at a time (the four
+// loads in flight together), folding each with the 1 KiB shift table staged
+// in LDS beside the slice-by-16 tables; its partial then moves to the aligned
+// end E and the wave XORs the partials.  The raw CRC at E is the range's raw
+// CRC followed by E - end zero bytes, so the stored value is compared after
+// the same shift (x^8 is invertible mod the CRC32C polynomial: the comparison
+// is exact).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_verify_crc(const uint8_t* __restrict__ sl, const uint64_t* __restrict__ bpos,
                                                     uint32_t nb, unsigned long long* bad, uint32_t* flags) {
   __shared__ uint32_t z[16][256];
+  __shared__ uint32_t sh1k[4][256];
   for (uint32_t i = threadIdx.x; i < 16 * 256; i += 256) (&z[0][0])[i] = (&g_crc_z16[0][0])[i];
+  for (uint32_t i = threadIdx.x; i < 4 * 256; i += 256) (&sh1k[0][0])[i] = (&g_crc_shift[10][0][0])[i];
   __syncthreads();
   const uint32_t l = lane_id();
   const uint32_t W = gridDim.x * 4;
-  for (uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6); b < nb; b += W) {
+  for (uint32_t b = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); b < nb; b += W) {
     const uint64_t pos = bpos[b];
     const uint32_t blen = __builtin_bswap32(ld_u32_at(sl + pos + 8));
     const uint32_t stored = __builtin_bswap32(ld_u32_at(sl + pos + 17));
     const uint64_t a = pos + 21, e = pos + 12 + (uint64_t)blen;  // framing checked batch_len >= 45
-    const uint64_t n = e - a;
-    const uint32_t nu = (uint32_t)((n + 15) / 16);
-    const uint64_t b0 = e - 16ull * nu;  // unit u covers [b0 + 16u, b0 + 16u + 16)
-    uint32_t acc = 0, last = 0;
-    bool any = false;
-    for (uint32_t u = l; u < nu; u += 64) {
-      const uint8_t* p = sl + b0 + 16ull * u;
-      uint32_t w[4];
-#pragma unroll
-      for (int q = 0; q < 4; q++) w[q] = ld_u32_at(p + 4 * q);
-      if (u == 0 && b0 < a) {  // bytes before the CRC start
-        const uint32_t skip = (uint32_t)(a - b0);
+    const uint64_t U0 = a & ~15ull, E = (e + 15) & ~15ull;
+    const uint32_t nu = (uint32_t)((E - U0) / 16);
+    const uint4* units = (const uint4*)(sl + U0);
+    auto crc_of = [&](uint32_t u, uint4 v) {
+      uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      const uint64_t x = U0 + 16ull * u;
+      if (x < a || x + 16 > e) {  // the range's first / last unit
 #pragma unroll
         for (int q = 0; q < 16; q++)
-          if ((uint32_t)q < skip) w[q >> 2] &= ~(0xffu << (8 * (q & 3)));
+          if (x + q < a || x + q >= e) w[q >> 2] &= ~(0xffu << (8 * (q & 3)));
       }
       uint32_t r = 0;
 #pragma unroll
       for (int q = 0; q < 16; q++) r ^= z[15 - q][(w[q >> 2] >> (8 * (q & 3))) & 0xff];
-      acc = crc_shift_tab(g_crc_shift[10], acc) ^ r;  // earlier units of this lane: 1 KiB further back
+      return r;
+    };
+    auto fold = [&](uint32_t c) { return sh1k[0][c & 0xff] ^ sh1k[1][(c >> 8) & 0xff] ^ sh1k[2][(c >> 16) & 0xff] ^ sh1k[3][c >> 24]; };
+    uint32_t acc = 0, last = 0;
+    bool any = false;
+    uint32_t u = l;
+    for (; u + 192 < nu; u += 256) {  // four units per lane per round, loads first
+      const uint4 v0 = units[u], v1 = units[u + 64], v2 = units[u + 128], v3 = units[u + 192];
+      const uint32_t r0 = crc_of(u, v0), r1 = crc_of(u + 64, v1), r2 = crc_of(u + 128, v2), r3 = crc_of(u + 192, v3);
+      acc = fold(fold(fold(fold(acc) ^ r0) ^ r1) ^ r2) ^ r3;
+      last = u + 192;
+      any = true;
+    }
+    for (; u < nu; u += 64) {
+      acc = fold(acc) ^ crc_of(u, units[u]);  // earlier units of this lane: 1 KiB further back
       last = u;
       any = true;
     }
@@ -3813,8 +3819,8 @@ __global__ __launch_bounds__(256) void k_verify_crc(const uint8_t* __restrict__ 
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) acc ^= __shfl_xor(acc, o, 64);
     if (l == 0) {
-      const uint32_t crc = acc ^ crc_shift_bytes(0xFFFFFFFFu, n) ^ 0xFFFFFFFFu;
-      const bool ok = crc == stored;
+      const uint32_t want = crc_shift_bytes(stored ^ 0xFFFFFFFFu ^ crc_shift_bytes(0xFFFFFFFFu, e - a), E - e);
+      const bool ok = acc == want;
       if (flags) flags[b] = ok ? 0u : 1u;
       if (!ok) {
         atomicAdd(&bad[0], 1ull);
@@ -3896,8 +3902,10 @@ __global__ __launch_bounds__(256) void k_dec_count(DecArgs a) {
 //   3. LDS -> HBM: interior units dwordx4 stores, the two edge units bytewise
 // A batch with more than 64 survivors or more bytes than the staging buffer
 // is written by the generic wave path (write_batch_wave).
-// (A CRC computed from the staging buffer was measured: 64-byte pieces
-// combined with GF(2) multiplies cost more VALU than the separate k_crc16 pass.)
+// (A CRC computed from the staging buffer was measured twice and is not used:
+// 64-byte pieces combined with GF(2) multiplies (round 2), and the
+// slice-by-16 / shift tables read from global memory per unit (round 4: C2
+// write 1.24 -> 4.70 ms, against k_crc16's 0.52 ms).)
 // ---------------------------------------------------------------------------
 constexpr int kWlThreads = 256;
 constexpr int kObuf = 17408;  // staging bytes (one 16 KiB batch + re-encoding growth + alignment)
@@ -4710,19 +4718,7 @@ void launch_crc(uint8_t* out, uint64_t off, uint64_t n, uint32_t* acc, hipStream
     const uint32_t grid = (uint32_t)(nchunks < 768 ? nchunks : 768);  // 3 workgroups per CU (LDS)
     hipLaunchKernelGGL(k_crc16, dim3(grid), dim3(kCrcThreads), 0, s, (const uint8_t*)out, off - 16, nblocks, acc);
   }
-  hipLaunchKernelGGL(k_crc_final, dim3(1), dim3(64), 0, s, out, (const uint32_t*)acc, nblocks ? zend : off, end, n,
-                     (uint64_t)0);
-}
-// the fused path: *acc already holds the raw CRC partials of out[hdr_end, zend)
-// (XOR-combined at zend by the writers); the header bytes and the tail here
-void launch_crc_fused(uint8_t* out, uint64_t hdr_end, uint64_t end, uint32_t* acc, hipStream_t s) {
-  const uint64_t zend = end & ~15ull;
-  hipLaunchKernelGGL(k_crc_final, dim3(1), dim3(64), 0, s, out, (const uint32_t*)acc, zend, end, end - 21, hdr_end);
-}
-void crc_table_ptrs(const uint32_t** z16, const uint32_t** shift) {
-  void* p = nullptr;
-  *z16 = hipGetSymbolAddress(&p, HIP_SYMBOL(g_crc_z16)) == hipSuccess ? (const uint32_t*)p : nullptr;
-  *shift = hipGetSymbolAddress(&p, HIP_SYMBOL(g_crc_shift)) == hipSuccess ? (const uint32_t*)p : nullptr;
+  hipLaunchKernelGGL(k_crc_final, dim3(1), dim3(64), 0, s, out, (const uint32_t*)acc, nblocks ? zend : off, end, n);
 }
 
 // k_one — process() of a one-batch input in one 256-thread workgroup: the
@@ -4763,6 +4759,13 @@ __global__ __launch_bounds__(kEvalThreads) void k_one(OneArgs o) {
   __shared__ WaveLds L;
   const uint32_t t = threadIdx.x;
   const EvalArgs& a = o.ea;
+  {  // the input batch from pinned host memory (over PCIe) into the device slice
+    const uint4* src = (const uint4*)o.hin;
+    uint4* dst = (uint4*)a.slice;
+    for (uint32_t u = t; u < o.in_len / 16; u += kEvalThreads) dst[u] = src[u];
+  }
+  __threadfence();
+  __syncthreads();
   eval_batch<kOps>(a, L, 0);
   __threadfence();
   __syncthreads();
@@ -4805,8 +4808,9 @@ __global__ __launch_bounds__(kEvalThreads) void k_one(OneArgs o) {
   __syncthreads();
   const Plan p = *o.plan;
   const uint64_t end = 61 + p.rec_bytes;
-  if (p.status != 0 || end > o.out_cap) return;
-  if (t == 0) header_run(o.plan, o.out);
+  const bool written = p.status == 0 && end <= o.out_cap;
+  if (written) {
+    if (t == 0) header_run(o.plan, o.out);
   if (t < 64 && p.first == 0 && p.last == 0) {
     WriteArgs wa{};
     wa.slice = a.slice;
@@ -4821,6 +4825,14 @@ __global__ __launch_bounds__(kEvalThreads) void k_one(OneArgs o) {
   __threadfence();
   __syncthreads();
   if (t < 64) crc_wave(o.out, end);
+  }
+  __threadfence();
+  __syncthreads();
+  // the read-back block to pinned host memory (the host reads it after the wait)
+  const uint32_t n = kOneHead + (written ? (uint32_t)end : 0u);
+  const uint4* src = (const uint4*)o.plan;
+  uint4* dst = (uint4*)o.hout;
+  for (uint32_t u = t; u < (n + 15) / 16; u += kEvalThreads) dst[u] = src[u];
 }
 void launch_one(const OneArgs& o, uint32_t ops, hipStream_t s) {
   const size_t dyn = (ops & opbit(OP_REGEX)) ? kDfaDyn : 0;

@@ -37,10 +37,6 @@ void launch_cat(const WriteArgs& a, uint32_t nbatches, hipStream_t s);
 void launch_crc(uint8_t* out, uint64_t off, uint64_t n, uint32_t* acc, hipStream_t s);
 // process() of a one-batch input in one launch (k_one)
 void launch_one(const OneArgs& o, uint32_t ops, hipStream_t s);
-// CRC32C when the writers already folded out[hdr_end, end & ~15) into *acc
-void launch_crc_fused(uint8_t* out, uint64_t hdr_end, uint64_t end, uint32_t* acc, hipStream_t s);
-// device addresses of the CRC32C tables (slice-by-16 and the 2^k zero-byte shifts)
-void crc_table_ptrs(const uint32_t** z16, const uint32_t** shift);
 void launch_write_lean(const WriteArgs& a, uint32_t nblocks, hipStream_t s);
 // aggregate-json, in phases separated by host reads of AggjArgs::scal
 uint64_t xscan_tiles(uint64_t n);  // u64 scratch slots launch_xscan needs for n items

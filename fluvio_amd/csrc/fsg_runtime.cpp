@@ -379,6 +379,7 @@ struct DevBuf {
 struct PinBuf {
   void* p = nullptr;
   size_t cap = 0;
+  unsigned flags = hipHostMallocDefault;  // coherent + mapped: kernels read / write it directly (k_one)
   ~PinBuf() {
     if (p) (void)hipHostFree(p);
   }
@@ -387,7 +388,7 @@ struct PinBuf {
     if (p) (void)hipHostFree(p);
     p = nullptr;
     cap = 0;
-    hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(&p, n, flags);
     if (e == hipSuccess) cap = n;
     return e;
   }
@@ -513,9 +514,11 @@ struct fsg_chain {
   // scratch
   DevBuf bstat, kept, rows, pre, aggpre, tiles, grand, mins, plan, out, crcparts, defer, elem, cat;
   DevBuf arr_b, arr_bm;  // lean array_map statistics and element bitmaps (per batch)
-  // the one-batch process() path (k_one): zeros for bpos / rbase, and one block
-  // read back with one copy: Plan | BatchStat | Mins | the output batch
+  // the one-batch process() path (k_one): zeros for bpos / rbase, the device
+  // block Plan | BatchStat | Mins | output batch, and coherent pinned memory
+  // the kernel reads the input from and writes the block back to (no copies)
   DevBuf one_meta, one_blk;
+  PinBuf one_pin;
   DevBuf dstate;  // aggregate-sum accumulator (i32) after the last call, in HBM
   // aggregate-json: key dictionary, index, initial keys, per-batch accumulator text
   DevBuf aj_tptr, aj_tlen, aj_kup, aj_out, aj_accoff, aj_acclen;  // aggregate-json
@@ -1276,6 +1279,20 @@ extern "C" int fsg_slice_upload(fsg_engine* e, const uint8_t* s, size_t len, fsg
   return FSG_OK;
 }
 extern "C" int fsg_slice_device_framed(const fsg_slice* s) { return s->device_framed ? 1 : 0; }
+// frame the slice's resident bytes again on the device, as a freshly fetched
+// slice is framed (FileBatchIterator, iterators.rs:55-160): the fetch-shaped
+// measurement re-runs framing + CRC verify + process on HBM-resident bytes
+extern "C" int fsg_slice_reframe(fsg_slice* s) {
+  HIPCHK(hipSetDevice(s->eng->device));
+  if (s->decompressed) return fail(FSG_E_UNSUPPORTED, "the slice was decompressed at ingest: its stored bytes are gone");
+  int fallback = 0;
+  int rc = frame_on_device(s, 0, &fallback);
+  if (rc) return rc;
+  if (fallback) return fail(FSG_E_UNSUPPORTED, "this slice needs the host framing walk (no magic-2 framing)");
+  s->device_framed = true;
+  HIPCHK(hipStreamSynchronize(0));
+  return FSG_OK;
+}
 // CRC32C of every framed batch against its header (report only: the reference
 // never verifies, protocol record/batch.rs:398-430, so nothing else changes)
 extern "C" int fsg_slice_verify_crc(const fsg_slice* s, uint64_t* n_bad, int64_t* first_bad, float* ms) {
@@ -2303,8 +2320,6 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   if (!so) launch_header(pa.plan, wa.out, st);
   if (c->timed) HIPCHK(hipEventRecord(c->ev[3], st));
   const uint32_t nblk = p.last >= p.first && p.first >= 0 ? (uint32_t)(p.last - p.first + 1) : 0u;
-  // array_map with every batch on the lean path: CRC32C folded into k_arr_write
-  const bool fused_crc = arr && !so && c->last.deferred == 0 && nblk && out_len >= 64;
   // verbatim records (filters, uppercase, projections): staged in LDS
   // (k_write_lean; a batch beyond its staging buffer or 64 survivors takes the
   // wave path inside it); measured on MI355X: C2 1 KB records write 1.33 -> 1.23
@@ -2327,12 +2342,6 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     aw.pre = pa.pre;
     aw.plan = pa.plan;
     aw.out = wa.out;
-    if (fused_crc) {  // every batch lean: the writer folds the output's CRC32C as it stores
-      HIPCHK(hipMemsetAsync(c->crcparts.p, 0, sizeof(uint32_t), st));
-      aw.crc_acc = c->crcparts.as<uint32_t>();
-      aw.crc_zend = out_len & ~(size_t)15;
-      crc_table_ptrs(&aw.crc_z16, &aw.crc_shift);
-    }
     launch_array_write(aw, nblk, st);
   }
   if (has_array) launch_write_canon(wa, nblk, st);
@@ -2365,8 +2374,6 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     o->device_framed = true;
     o->decompressed = s->decompressed;
     o->has_pass = p.err_batch >= 0 || s->has_pass;
-  } else if (fused_crc) {
-    launch_crc_fused(wa.out, 61, out_len, c->crcparts.as<uint32_t>(), st);
   } else {
     launch_crc(wa.out, 21, out_len - 21, c->crcparts.as<uint32_t>(), st);
   }
@@ -2769,7 +2776,6 @@ namespace {
 // read-back of plan + batch result + output, one wait.  1 = not taken (the
 // general path runs: a stateful / aggregate / array chain, a composed chain,
 // an output beyond the block).
-constexpr size_t kOneHead = 512;  // Plan | BatchStat | Mins, then the output batch
 int process_one(fsg_chain* c, const uint8_t* raw, size_t len, int64_t base_offset, int64_t base_timestamp,
                 fsg_metrics* m, fsg_output** out) {
   if (!c->segs.empty() || c->agg_stage >= 0 || c->array_stage >= 0 || c->sf_stage >= 0 ||
@@ -2778,8 +2784,9 @@ int process_one(fsg_chain* c, const uint8_t* raw, size_t len, int64_t base_offse
   static_assert(sizeof(Plan) <= 192 && sizeof(BatchStat) <= 192 && sizeof(Mins) <= 64, "k_one read-back head");
   const size_t in_len = 57 + len, alloc = slice_alloc(in_len);
   const size_t cap = 128 + 4 * len;  // stateless outputs stay within the input's size plus the i32 digits
-  if (alloc + kOneHead + cap > kPinPlan + kSmallOut) return 1;
-  HIPCHK(c->hpin.ensure(kPinPlan + kSmallOut));
+  if (alloc > kSmallOut || kOneHead + cap > kSmallOut) return 1;
+  c->one_pin.flags = hipHostMallocMapped | hipHostMallocCoherent;
+  HIPCHK(c->one_pin.ensure(2 * kSmallOut));
   HIPCHK(c->ingest.data.ensure(alloc));
   HIPCHK(c->one_blk.ensure(kOneHead + cap));
   HIPCHK(c->kept.ensure(std::max<size_t>(len / 7 + 1, 1) * sizeof(KeptRec)));
@@ -2791,7 +2798,7 @@ int process_one(fsg_chain* c, const uint8_t* raw, size_t len, int64_t base_offse
   }
   // the batch (Batch::default() + base offset / timestamp, the records as given)
   // in pinned memory, one copy up
-  uint8_t* b = (uint8_t*)c->hpin.p;
+  uint8_t* b = (uint8_t*)c->one_pin.p;
   memset(b, 0, alloc);
   auto be = [&](size_t off, uint64_t v, int n) {
     for (int i = 0; i < n; i++) b[off + i] = (uint8_t)(v >> (8 * (n - 1 - i)));
@@ -2808,8 +2815,11 @@ int process_one(fsg_chain* c, const uint8_t* raw, size_t len, int64_t base_offse
     nrec = std::min<uint64_t>(cnt > 0 ? (uint64_t)cnt : 0, (len - 4) / 7);
   }
   hipStream_t st = c->stream;
-  HIPCHK(hipMemcpyAsync(c->ingest.data.p, b, alloc, hipMemcpyHostToDevice, st));
   uint8_t* blk = c->one_blk.as<uint8_t>();
+  uint8_t* hb = (uint8_t*)c->one_pin.p + kSmallOut;  // the read-back block lands here
+  void *din = nullptr, *dout = nullptr;  // the pinned buffers' device addresses (k_one reads / writes them)
+  HIPCHK(hipHostGetDevicePointer(&din, b, 0));
+  HIPCHK(hipHostGetDevicePointer(&dout, hb, 0));
   OneArgs o{};
   EvalArgs& ea = o.ea;
   ea.slice = c->ingest.data.as<uint8_t>();
@@ -2828,13 +2838,14 @@ int process_one(fsg_chain* c, const uint8_t* raw, size_t len, int64_t base_offse
   o.plan = (Plan*)blk;
   o.out = blk + kOneHead;
   o.out_cap = cap;
+  o.hin = (const uint8_t*)din;
+  o.hout = (uint8_t*)dout;
+  o.in_len = (uint32_t)alloc;
   o.empty_chain = c->hdesc.nstages == 0 ? 1 : 0;
   uint32_t ops = 0;
   for (uint32_t k = 0; k < c->hdesc.nstages; k++) ops |= 1u << c->hdesc.st[k].op;
-  launch_one(o, ops, st);
+  launch_one(o, ops, st);  // one launch: input over PCIe, process(), the block back to pinned memory
   HIPCHK(hipGetLastError());
-  uint8_t* hb = (uint8_t*)c->hpin.p + kPinPlan;  // the input staging (at hpin.p) is free once the copy ran
-  HIPCHK(hipMemcpyAsync(hb, blk, kOneHead + cap, hipMemcpyDeviceToHost, st));
   HIPCHK(wait_stream(st));
   Plan p;
   BatchStat bs;

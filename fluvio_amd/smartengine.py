@@ -645,6 +645,11 @@ class ResidentSlice:
         self.n_batches, self.n_records, self.bytes = nb.value, nr.value, by.value
         self.device_framed = bool(_ffi.lib().fsg_slice_device_framed(h))
 
+    def reframe(self):
+        """Frame the resident bytes again on the device, as a freshly fetched
+        slice (the fetch-shaped measurement: framing + verify + process)."""
+        _check(_ffi.lib().fsg_slice_reframe(self._h))
+
     def verify_crc(self):
         """CRC32C of every stored batch checked on the GPU (report only: the
         reference never verifies).  Returns (mismatches, first bad batch or -1,

@@ -230,6 +230,10 @@ int fsg_slice_info(const fsg_slice *s, uint64_t *n_batches, uint64_t *n_records,
  * without magic 2 on the chain, or candidates too dense).  Same result either
  * way (FileBatchIterator::next, crates/fluvio-storage/src/iterators.rs:55-160). */
 int fsg_slice_device_framed(const fsg_slice *s);
+/* Frame the slice's HBM-resident bytes again on the device (a freshly fetched
+ * slice: FileBatchIterator framing, iterators.rs:55-160); FSG_E_UNSUPPORTED
+ * for slices that needed the host walk or were decompressed at ingest. */
+int fsg_slice_reframe(fsg_slice *s);
 /* CRC32C (Castagnoli) of every framed batch, computed on the GPU over header
  * bytes 21.. + records and compared with the stored crc: *n_bad mismatches,
  * *first_bad the first such batch (-1 none), *ms the kernel time.  Reports

@@ -1381,6 +1381,22 @@ def test_verify_crc_large_batches(engine):
     assert rs.verify_crc()[:2] == (0, -1)
 
 
+def test_reframe_resident_slice(engine):
+    """fsg_slice_reframe (the fetch-shaped step): the HBM-resident bytes framed
+    again on the device give the same batches, CRC verdicts and process_batch
+    output, call after call."""
+    sl = synth.make_slice(2, 3000, base_offset=4)
+    rs = ResidentSlice(engine, sl)
+    nb, nr = rs.n_batches, rs.n_records
+    g = gpu_chain(engine, CHAINS["filter_init_timeout"])
+    ref = orc_chain(CHAINS["filter_init_timeout"]).process_batch(sl)["bytes"]
+    for _ in range(3):
+        rs.reframe()
+        assert rs.verify_crc()[:2] == (0, -1)
+        assert g.process_slice(rs).raw == ref
+    assert (rs.n_batches, rs.n_records) == (nb, nr)
+
+
 # ---------------------------------------------------------------------------
 # compressed record sections decompressed on the GPU at ingest (SURVEY §8 f2)
 # ---------------------------------------------------------------------------
