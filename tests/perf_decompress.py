@@ -1,6 +1,6 @@
 """Decompression-at-ingest throughput on the GPU (not a pytest test: run as
 `python tests/perf_decompress.py` on the GPU box).  C2 records re-stored with
-each codec (oracle/fsg_codec.c encoders, Python gzip), then ingested
+each codec (oracle/fsg_codec.c encoders, Python gzip, libzstd level 3), then ingested
 (fsg_slice_upload: framing, CRC check of the stored bytes, decompression
 sizing + writing passes, re-framing) and processed once for parity."""
 import json
@@ -23,8 +23,8 @@ def main():
     sl = synth.make_slice(2, n)
     engine = SmartEngine(0)
     out = {"records": n, "uncompressed_bytes": len(sl)}
-    for name, codec in (("gzip", 1), ("snappy", 2), ("lz4", 3)):
-        csl = recompress(sl, [codec])
+    for name, codec, flags in (("gzip", 1, 0), ("snappy", 2, 0), ("lz4", 3, 0), ("zstd", 4, 0x100 | 3)):
+        csl = recompress(sl, [codec], flags)
         ResidentSlice(engine, csl)  # warm
         t0 = time.perf_counter()
         rs = ResidentSlice(engine, csl)
