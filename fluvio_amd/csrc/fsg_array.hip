@@ -243,6 +243,51 @@ __device__ __forceinline__ void stage_window(const uint8_t* S, uint64_t al, uint
 }
 
 // ---------------------------------------------------------------------------
+// k_arr_frame — record framing of the batches for k_arr_lean: one THREAD per
+// batch (64-thread workgroups over every CU), so ~17 K independent
+// length-varint chains are in flight at once
+// (a wave per batch in LDS leaves too few to hide each step's latency).  Each
+// step reads the record's varint from global memory and also touches the line
+// 256 bytes ahead, so the chain's next steps hit L2 instead of HBM.  Starts to
+// rstart, the end to rend; 0xFFFF = not framed here (the exact kernel frames it).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kArrMaxRec = 2560;  // records per lean batch (a 17 KiB window holds ~2480 at most)
+__global__ __launch_bounds__(64) void k_arr_frame(EvalArgs a) {
+  const uint8_t* S = a.slice;
+  for (uint32_t b = blockIdx.x * 64 + threadIdx.x; b < a.nbatches; b += gridDim.x * 64) {
+    const uint64_t pos = a.bpos[b];
+    const uint64_t rb = a.rbase[b];
+    const uint32_t rn = (uint32_t)((b + 1 < a.nbatches ? a.rbase[b + 1] : a.nrec) - rb);
+    const uint64_t al = pos & ~15ull;
+    const uint8_t* base = S + al;
+    const uint32_t batch_len = __builtin_bswap32(ld4g(S + pos + 8));
+    const uint64_t sec_end = pos + 12 + (uint64_t)batch_len;
+    uint32_t end = 0xFFFFu;
+    if (sec_end - al <= (uint64_t)kWin && rn <= kArrMaxRec && batch_len >= 49 &&
+        __builtin_bswap32(ld4g(S + pos + 57)) == rn) {
+      const uint32_t have = (uint32_t)(sec_end - al);
+      uint32_t q = (uint32_t)(pos + 61 - al), n = 0, touch = 0;
+      for (; n < rn; n++) {
+        const uint32_t x = ld4g(base + q);
+        touch += ld4g(base + (q + 256 < have ? q + 256 : have - 4));  // the line a few records ahead
+        const uint32_t term = ~x & 0x80808080u;
+        const uint32_t nb = (((uint32_t)__builtin_ctz(term | 0x80000000u)) >> 3) + 1;
+        const uint32_t y = nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u));
+        const uint32_t v = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
+        const uint32_t len = v >> 1;
+        // no terminator in 4 bytes, past the section, a negative length, past the section
+        if (!term || q + nb > have || (v & 1u) || have - (q + nb) < len) break;
+        a.rstart[rb + n] = (uint16_t)q;
+        q += nb + len;
+      }
+      if (n == rn) end = q;
+      if (touch == 0x9E3779B9u && n > rn) end = 0;  // never true: keeps the look-ahead reads
+    }
+    a.rend[b] = (uint16_t)end;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_arr_lean — pass 1, one workgroup per batch (persistent).  Wave 0 frames
 // the batch's records in LDS (the length-varint chain, wave-uniform), then a
 // thread per record walks its value through the DFA: element starts / ends
@@ -250,7 +295,6 @@ __device__ __forceinline__ void stage_window(const uint8_t* S, uint64_t al, uint
 // k_size prices the batch's output with (ArrBatch).
 // ---------------------------------------------------------------------------
 constexpr int kArrT = 256;
-constexpr uint32_t kArrMaxRec = 2560;  // records per lean batch (a 17 KiB window holds ~2480 at most)
 struct ArrLds {
   uint8_t W[kWin + 16] __attribute__((aligned(16)));
   uint32_t bm[kArrBmBatch];  // starts, then ends
@@ -258,7 +302,6 @@ struct ArrLds {
   ArrTab T;
   uint32_t red[kArrT / 64][4];
   uint32_t cnt[9];
-  uint32_t nrs;  // records framed (0xFFFFFFFF: framing failed)
 };
 
 __global__ __launch_bounds__(kArrT) void k_arr_lean(EvalArgs a) {
@@ -273,6 +316,7 @@ __global__ __launch_bounds__(kArrT) void k_arr_lean(EvalArgs a) {
     const uint64_t al = pos & ~15ull;
     const uint32_t batch_len = __builtin_bswap32(ld4g(S + pos + 8));
     const uint64_t sec_end = pos + 12 + (uint64_t)batch_len;
+    const uint32_t rend = a.rend[b];
     // a batch beyond the window / the record slots / without a record count: the exact kernel
     bool defer = sec_end - al > (uint64_t)kWin || rn > kArrMaxRec || batch_len < 49;
     __syncthreads();  // the previous batch's window, bitmaps and counters are no longer read
@@ -282,56 +326,10 @@ __global__ __launch_bounds__(kArrT) void k_arr_lean(EvalArgs a) {
       stage_window(S, al, (uint32_t)((sec_end - al + 15) & ~15ull), L.W);
     }
     __syncthreads();
-    if (!defer && t < 64) {  // framing (Batch decode: count, then each record's length varint)
-      // The chain of length varints is serial; a span of 256 bytes from the
-      // current record start is decoded speculatively, four candidate starts
-      // per lane (their successor offsets kept in registers), and the chain is
-      // followed through the span with one readlane per record.
-      const uint32_t have = (uint32_t)(sec_end - al);
-      const uint32_t c0 = (uint32_t)(pos + 57 - al);
-      const uint32_t count = __builtin_bswap32(lds4(L.W, c0));
-      uint32_t q = c0 + 4, n = 0;
-      bool ok = count == rn;
-      while (ok && n < count) {
-        q = __builtin_amdgcn_readfirstlane(q);
-        // candidates p = q + 4 l + j: successor offset from q, or 0 when the
-        // record there cannot frame (no terminator in 4 bytes, past the section,
-        // a negative length)
-        const uint32_t p0 = q + 4 * l;
-        const uint64_t x8 = (uint64_t)lds4(L.W, p0) | ((uint64_t)lds4(L.W, p0 + 4) << 32);
-        uint32_t nx[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const uint32_t x = (uint32_t)(x8 >> (8 * j));
-          const uint32_t term = ~x & 0x80808080u;
-          const uint32_t nb = (((uint32_t)__builtin_ctz(term | 0x80000000u)) >> 3) + 1;
-          const uint32_t y = nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u));
-          const uint32_t v = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
-          const uint32_t p = p0 + j, len = v >> 1;
-          const bool good = term && p + nb <= have && !(v & 1u) && have - (p + nb) >= len;
-          nx[j] = good ? 4 * l + j + nb + len : 0u;
-        }
-        uint32_t cur = 0;  // offset from q of the record start being framed
-        while (n < count && cur < 256) {
-          const uint32_t ln = cur >> 2, j = cur & 3;
-          const uint32_t nxt = __builtin_amdgcn_readlane(j == 0 ? nx[0] : j == 1 ? nx[1] : j == 2 ? nx[2] : nx[3], ln);
-          if (!nxt) {
-            ok = false;
-            break;
-          }
-          if (l == 0) L.rs[n] = (uint16_t)(q + cur);
-          n++;
-          cur = nxt;
-        }
-        q += cur;
-      }
-      if (l == 0) {
-        L.rs[n] = (uint16_t)q;
-        L.nrs = ok ? n : 0xFFFFFFFFu;
-      }
-    }
+    if (!defer && rend == 0xFFFFu) defer = true;  // k_arr_frame could not frame it
+    if (!defer)
+      for (uint32_t r = t; r <= rn; r += kArrT) L.rs[r] = r < rn ? a.rstart[rb + r] : (uint16_t)rend;
     __syncthreads();
-    defer = defer || L.nrs != rn;
     uint32_t bne = 0, besum = 0, bc59 = 0;
     bool bad = false;
     for (uint32_t r = t; r < rn && !defer && !bad; r += kArrT) {
@@ -616,11 +614,12 @@ uint32_t resident(K kernel, int dev_threads) {
   (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, dev_threads, 0);
   return (uint32_t)(cus > 0 ? cus : 1) * (uint32_t)(per > 0 ? per : 1);
 }
-uint32_t arr_grid(uint32_t nb, int which) {
+uint32_t arr_grid(uint32_t nb, int which) {  // 0: k_arr_lean, 1: k_arr_write
   static uint32_t cache[64][2];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-  if (!cache[dev][which]) cache[dev][which] = which ? resident(k_arr_write, kArrT) : resident(k_arr_lean, kArrT);
+  if (!cache[dev][which])
+    cache[dev][which] = which == 1 ? resident(k_arr_write, kArrT) : resident(k_arr_lean, kArrT);
   return std::min<uint32_t>(nb, cache[dev][which]);
 }
 
@@ -632,6 +631,7 @@ bool array_lean_eligible(const ChainDesc& ch, uint32_t ops) {
 }
 void launch_array_lean(const EvalArgs& a, hipStream_t s) {
   if (!a.nbatches) return;
+  hipLaunchKernelGGL(k_arr_frame, dim3((a.nbatches + 63) / 64), dim3(64), 0, s, a);  // spread over every CU
   hipLaunchKernelGGL(k_arr_lean, dim3(arr_grid(a.nbatches, 0)), dim3(kArrT), 0, s, a);
 }
 void launch_array_write(const ArrWriteArgs& a, uint32_t nblk, hipStream_t s) {

@@ -354,8 +354,10 @@ struct OneArgs {
   uint64_t out_cap;
   const uint8_t* hin;  // the input batch in pinned host memory (copied into ea.slice first), in_len bytes
   uint8_t* hout;       // pinned host memory: the read-back block is copied here last
-  uint32_t in_len;
+  uint32_t in_len;     // the device slice's allocation (zeros behind the input)
+  uint32_t in_real;    // input bytes to read from hin (a multiple of 16)
   int32_t empty_chain;
+  int32_t pad;
 };
 constexpr uint32_t kOneHead = 512;  // Plan | BatchStat | Mins, then the output batch
 // a chain segment's output as the next segment's input slice (k_seg_headers):

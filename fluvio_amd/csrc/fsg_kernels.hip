@@ -4544,11 +4544,9 @@ void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s) {
   EvalArgs e = a;
   uint32_t grid = a.nbatches;
   if (mode == EVAL_ARRAY) {
-    // the lean array kernel (fsg_array.hip) frames its own batches; the exact
-    // kernel chases the records of the batches it defers itself
+    // k_arr_frame + the lean array kernel (fsg_array.hip); the exact kernel
+    // takes the deferred batches' record starts from k_arr_frame where it framed them
     launch_array_lean(a, s);
-    e.rstart = nullptr;
-    e.rend = nullptr;
     grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list
   } else if (mode == EVAL_LEAN) {
     // persistent: as many workgroups as fit on the device at once
@@ -4724,7 +4722,8 @@ void launch_crc(uint8_t* out, uint64_t off, uint64_t n, uint32_t* acc, hipStream
 // k_one — process() of a one-batch input in one 256-thread workgroup: the
 // exact evaluation (eval_batch), then the cross-batch passes collapsed to one
 // batch (minima, size row, plan, header, k_write's wave, CRC32C by one wave),
-// each phase behind a fence and a barrier.  One launch instead of ~12, and
+// each phase behind a workgroup-scope fence and a barrier (every byte one phase
+// reads was written by this workgroup: no device-scope L2 write-back).  One launch instead of ~12, and
 // no host wait between the plan and the write (the output is bounded by
 // out_cap: a larger one is left unwritten for the host to redo).
 __device__ void crc_wave(uint8_t* out, uint64_t end) {  // CRC32C of out[21, end) into out[17..21)
@@ -4754,21 +4753,35 @@ __device__ void crc_wave(uint8_t* out, uint64_t end) {  // CRC32C of out[21, end
     out[20] = (uint8_t)crc;
   }
 }
+#ifdef FSG_ONE_TIMING  // experiment builds: phase timestamps into the read-back head (bytes 416..511)
+#define ONE_MARK(k) if (threadIdx.x == 0 && (k) < 12) ((uint64_t*)((uint8_t*)o.plan + 416))[k] = __builtin_amdgcn_s_memrealtime()
+#else
+#define ONE_MARK(k)
+#endif
+constexpr uint32_t kOneSerialCrc = 1024;  // outputs up to this size: the CRC by one thread from LDS
+static_assert(kOneSerialCrc + 4 <= kWin + 64, "k_one's CRC copy reuses the window");
 template <uint32_t kOps>
 __global__ __launch_bounds__(kEvalThreads) void k_one(OneArgs o) {
   __shared__ WaveLds L;
+  __shared__ uint32_t zt[1024];  // g_crc_z16[0..3] for the small-output CRC, loaded with the input
   const uint32_t t = threadIdx.x;
   const EvalArgs& a = o.ea;
-  {  // the input batch from pinned host memory (over PCIe) into the device slice
+  ONE_MARK(0);
+  for (uint32_t i = t; i < 1024; i += kEvalThreads) zt[i] = (&g_crc_z16[0][0])[i];
+  {  // the input batch from pinned host memory (over PCIe) into the device slice,
+     // zeros behind it (the slice's over-read padding)
     const uint4* src = (const uint4*)o.hin;
     uint4* dst = (uint4*)a.slice;
-    for (uint32_t u = t; u < o.in_len / 16; u += kEvalThreads) dst[u] = src[u];
+    for (uint32_t u = t; u < o.in_len / 16; u += kEvalThreads)
+      dst[u] = u < o.in_real / 16 ? src[u] : make_uint4(0, 0, 0, 0);
   }
-  __threadfence();
+  __threadfence_block();
   __syncthreads();
+  ONE_MARK(1);
   eval_batch<kOps>(a, L, 0);
-  __threadfence();
+  __threadfence_block();
   __syncthreads();
+  ONE_MARK(2);
   if (t == 0) {  // k_mins over the one batch
     const BatchStat st = a.bstat[0];
     Mins m = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, {0, 0, 0}};
@@ -4781,8 +4794,9 @@ __global__ __launch_bounds__(kEvalThreads) void k_one(OneArgs o) {
     *a.mins = m;
     o.pre[0] = ScanRow{};
   }
-  __threadfence();
+  __threadfence_block();
   __syncthreads();
+  ONE_MARK(3);
   SizeArgs sa{};
   sa.bstat = a.bstat;
   sa.desc = a.desc;
@@ -4791,8 +4805,9 @@ __global__ __launch_bounds__(kEvalThreads) void k_one(OneArgs o) {
   sa.rows = o.rows;
   sa.nbatches = 1;
   if (t < 64) size_batch(sa, 0);
-  __threadfence();
+  __threadfence_block();
   __syncthreads();
+  ONE_MARK(4);
   if (t == 0) {  // one batch: the exclusive prefix is zero, no max_bytes cut
     PlanArgs pa{};
     pa.bstat = a.bstat;
@@ -4804,8 +4819,9 @@ __global__ __launch_bounds__(kEvalThreads) void k_one(OneArgs o) {
     pa.empty_chain = o.empty_chain;
     plan_run(pa);
   }
-  __threadfence();
+  __threadfence_block();
   __syncthreads();
+  ONE_MARK(5);
   const Plan p = *o.plan;
   const uint64_t end = 61 + p.rec_bytes;
   const bool written = p.status == 0 && end <= o.out_cap;
@@ -4822,12 +4838,35 @@ __global__ __launch_bounds__(kEvalThreads) void k_one(OneArgs o) {
     wa.out = o.out;
     write_batch(wa, p, 0);
   }
-  __threadfence();
+  __threadfence_block();
   __syncthreads();
-  if (t < 64) crc_wave(o.out, end);
+  ONE_MARK(6);
+  if (end <= kOneSerialCrc) {  // a small output: slice-by-4 from LDS by one thread
+    uint8_t* ob = L.win;  // the output bytes (eval is done with the window)
+    for (uint32_t i = t; i < (uint32_t)(end + 3) / 4; i += kEvalThreads) ((uint32_t*)ob)[i] = ((const uint32_t*)o.out)[i];
+    __syncthreads();
+    if (t == 0) {
+      uint32_t c = 0xFFFFFFFFu;
+      uint32_t i = 21;
+      for (; i < end && (i & 3u); i++) c = zt[(c ^ ob[i]) & 0xffu] ^ (c >> 8);
+      for (; i + 4 <= end; i += 4) {
+        const uint32_t x = c ^ *(const uint32_t*)(ob + i);
+        c = zt[768 + (x & 0xffu)] ^ zt[512 + ((x >> 8) & 0xffu)] ^ zt[256 + ((x >> 16) & 0xffu)] ^ zt[x >> 24];
+      }
+      for (; i < end; i++) c = zt[(c ^ ob[i]) & 0xffu] ^ (c >> 8);
+      c ^= 0xFFFFFFFFu;
+      o.out[17] = (uint8_t)(c >> 24);
+      o.out[18] = (uint8_t)(c >> 16);
+      o.out[19] = (uint8_t)(c >> 8);
+      o.out[20] = (uint8_t)c;
+    }
+  } else if (t < 64) {
+    crc_wave(o.out, end);
   }
-  __threadfence();
+  }
+  __threadfence_block();
   __syncthreads();
+  ONE_MARK(7);
   // the read-back block to pinned host memory (the host reads it after the wait)
   const uint32_t n = kOneHead + (written ? (uint32_t)end : 0u);
   const uint4* src = (const uint4*)o.plan;

@@ -8,7 +8,7 @@ namespace fsg {
 hipError_t upload_crc_tables();
 // ops: bit per StageOp in the chain.  mode: EVAL_EXACT = k_eval over every
 // batch; EVAL_LEAN = k_chase + k_eval_lean, then k_eval over its deferred list;
-// EVAL_ARRAY = k_chase_w + k_arr_lean (fsg_array.hip), then k_eval over its deferred list
+// EVAL_ARRAY = k_arr_frame + k_arr_lean (fsg_array.hip), then k_eval over its deferred list
 enum EvalMode { EVAL_EXACT = 0, EVAL_LEAN = 1, EVAL_ARRAY = 3 };
 void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s);
 // array_map_json_array alone over the source values (fsg_array.hip)

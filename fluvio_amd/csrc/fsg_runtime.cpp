@@ -2799,7 +2799,9 @@ int process_one(fsg_chain* c, const uint8_t* raw, size_t len, int64_t base_offse
   // the batch (Batch::default() + base offset / timestamp, the records as given)
   // in pinned memory, one copy up
   uint8_t* b = (uint8_t*)c->one_pin.p;
-  memset(b, 0, alloc);
+  const size_t in_real = (in_len + 15) & ~(size_t)15;  // k_one reads these, zero-fills the rest on the device
+  memset(b, 0, 57);
+  memset(b + in_len, 0, in_real - in_len);
   auto be = [&](size_t off, uint64_t v, int n) {
     for (int i = 0; i < n; i++) b[off + i] = (uint8_t)(v >> (8 * (n - 1 - i)));
   };
@@ -2841,6 +2843,7 @@ int process_one(fsg_chain* c, const uint8_t* raw, size_t len, int64_t base_offse
   o.hin = (const uint8_t*)din;
   o.hout = (uint8_t*)dout;
   o.in_len = (uint32_t)alloc;
+  o.in_real = (uint32_t)in_real;
   o.empty_chain = c->hdesc.nstages == 0 ? 1 : 0;
   uint32_t ops = 0;
   for (uint32_t k = 0; k < c->hdesc.nstages; k++) ops |= 1u << c->hdesc.st[k].op;
@@ -2851,6 +2854,17 @@ int process_one(fsg_chain* c, const uint8_t* raw, size_t len, int64_t base_offse
   BatchStat bs;
   memcpy(&p, hb, sizeof p);
   memcpy(&bs, hb + 192, sizeof bs);
+#ifdef FSG_ONE_TIMING
+  {
+    const uint64_t* tm = (const uint64_t*)(hb + 416);
+    static int calls = 0;
+    if (++calls % 500 == 0) {
+      fprintf(stderr, "k_one phases (10 ns ticks):");
+      for (int k = 1; k < 10 && tm[k]; k++) fprintf(stderr, " %d:%llu", k, (unsigned long long)(tm[k] - tm[k - 1]));
+      fprintf(stderr, "\n");
+    }
+  }
+#endif
   if (p.status != 0) {
     if (m) {
       m->bytes_in += p.bytes_in;
