@@ -2459,7 +2459,7 @@ __device__ __forceinline__ uint64_t array_rec_bytes(const KeptRec& d, const Elem
 }
 
 // k_size: one wave per batch (4 batches per 256-thread block)
-__device__ void size_batch(const SizeArgs& a, uint32_t b) {
+__device__ __forceinline__ void size_batch(const SizeArgs& a, uint32_t b) {
   const uint32_t l = lane_id();
   const BatchStat st = a.bstat[b];
   const uint32_t f = a.mins->first_keep;
@@ -2620,7 +2620,7 @@ __device__ __forceinline__ ScanRow incl_at(const PlanArgs& a, uint32_t i) {
   return r;
 }
 
-__device__ void plan_run(const PlanArgs& a) {
+__device__ __forceinline__ void plan_run(const PlanArgs& a) {
   const uint32_t NONE = 0xFFFFFFFFu;
   const uint32_t n = a.nbatches;
   const uint32_t f = a.mins->first_keep, e = a.mins->first_err, d = a.mins->first_dec, u = a.mins->first_unsup;
@@ -2754,7 +2754,7 @@ void launch_seg_headers(const SegArgs& a, hipStream_t s) {
 // ---------------------------------------------------------------------------
 // k_header: output batch header (Batch::default() + base offset, lod, count)
 // ---------------------------------------------------------------------------
-__device__ void header_run(const Plan* plan, uint8_t* out) {
+__device__ __forceinline__ void header_run(const Plan* plan, uint8_t* out) {
   const Plan p = *plan;
   uint8_t h[61];
   auto be = [&](int off, uint64_t v, int nb) {
@@ -2944,7 +2944,7 @@ __device__ void write_array_batch(const WriteArgs& a, const KeptRec* d, uint32_t
 // each key/value payload with all 64 lanes (copy_seg).  aggregate (concat)
 // values are prefixes of the accumulator stream built by k_cat.
 constexpr int kWriteThreads = 256;
-__device__ void write_batch(const WriteArgs& a, const Plan& p, int32_t b) {
+__device__ __forceinline__ void write_batch(const WriteArgs& a, const Plan& p, int32_t b) {
   const uint32_t lane = lane_id();
   const BatchStat st = a.bstat[b];
   const int64_t rel = a.seg ? 0 : a.bstat[p.first].base_offset - st.base_offset;
@@ -4764,6 +4764,7 @@ template <uint32_t kOps>
 __global__ __launch_bounds__(kEvalThreads) void k_one(OneArgs o) {
   __shared__ WaveLds L;
   __shared__ uint32_t zt[1024];  // g_crc_z16[0..3] for the small-output CRC, loaded with the input
+  __shared__ Plan sh_plan;
   const uint32_t t = threadIdx.x;
   const EvalArgs& a = o.ea;
   ONE_MARK(0);
@@ -4818,15 +4819,16 @@ __global__ __launch_bounds__(kEvalThreads) void k_one(OneArgs o) {
     pa.nbatches = 1;
     pa.empty_chain = o.empty_chain;
     plan_run(pa);
+    sh_plan = *o.plan;  // this thread's own store: the workgroup reads the plan from LDS
   }
   __threadfence_block();
   __syncthreads();
   ONE_MARK(5);
-  const Plan p = *o.plan;
+  const Plan p = sh_plan;
   const uint64_t end = 61 + p.rec_bytes;
   const bool written = p.status == 0 && end <= o.out_cap;
   if (written) {
-    if (t == 0) header_run(o.plan, o.out);
+    if (t == 0) header_run(&sh_plan, o.out);
   if (t < 64 && p.first == 0 && p.last == 0) {
     WriteArgs wa{};
     wa.slice = a.slice;

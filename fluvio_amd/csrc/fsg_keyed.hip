@@ -138,7 +138,7 @@ __device__ __forceinline__ uint32_t hb_capacity(uint32_t B) { return B == 0 ? 0u
 // rescan from bucket 0 amount to.
 struct HbReg {
   uint64_t occ, rep;
-  uint32_t B, mask, wm, cap, items, pl;
+  uint32_t B, mask, wm, cap, items, pl, ph;  // ph: lane s = the hash of bucket s's payload
 };
 __device__ __forceinline__ uint64_t rotr64(uint64_t x, uint32_t p) {
   return (x >> (p & 63u)) | (x << ((64u - p) & 63u));  // p = 0: x | x
@@ -154,6 +154,7 @@ __device__ __forceinline__ HbReg hb_new(uint32_t B) {  // B in {0, 4, 8, 16, 32,
   t.cap = hb_capacity(B);
   t.items = 0;
   t.pl = 0;
+  t.ph = 0;
   return t;
 }
 // find_insert_slot: the first free bucket of the window at the probe
@@ -167,20 +168,23 @@ __device__ __forceinline__ void hb_put(HbReg& t, uint32_t payload, uint32_t h) {
   }
   const uint32_t s = (pos + (uint32_t)__builtin_ctz(~win)) & t.mask;
   t.occ |= t.rep << s;
-  t.pl = (threadIdx.x & 63u) == s ? payload : t.pl;  // writelane
+  const bool mine = (threadIdx.x & 63u) == s;  // writelane
+  t.pl = mine ? payload : t.pl;
+  t.ph = mine ? h : t.ph;
   t.items++;
 }
 __device__ __forceinline__ uint64_t hb_live(const HbReg& t) {
   return t.B < 64u ? t.occ & ((1ull << t.B) - 1ull) : t.occ;
 }
 // reserve(1): no room -> capacity_to_buckets(capacity + 1) = 4, 8, 2B buckets,
-// the old buckets re-inserted in bucket order; hv: lane x = payload x's hash
-__device__ __forceinline__ void hb_reserve(HbReg& t, uint32_t hv) {
+// the old buckets re-inserted in bucket order (each bucket's payload and hash
+// read independently: no readlane feeds another's lane index)
+__device__ __forceinline__ void hb_reserve(HbReg& t) {
   if (t.cap != t.items) return;
   HbReg n = hb_new(t.B ? 2u * t.B : 4u);
   for (uint64_t m = hb_live(t); m; m &= m - 1ull) {
-    const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)t.pl, (int)__builtin_ctzll(m));
-    hb_put(n, x, (uint32_t)__builtin_amdgcn_readlane((int)hv, (int)x));
+    const uint32_t b = (uint32_t)__builtin_ctzll(m);
+    hb_put(n, (uint32_t)__builtin_amdgcn_readlane((int)t.pl, (int)b), (uint32_t)__builtin_amdgcn_readlane((int)t.ph, (int)b));
   }
   t = n;
 }
@@ -234,7 +238,36 @@ struct AjTile {
   uint32_t nk, ne, nnew;
   uint64_t ko, g0;
 };
-__device__ __forceinline__ AjTile aj_tile(const AggjArgs& a, uint64_t r0) {
+// the walk's arguments, copied into registers once: read through the group
+// launch's argument array (global memory), every field access would otherwise
+// be a load the compiler must repeat after each store to `ord` (aliasing), and
+// each of those loads' waits also waits for the records' prefetched data
+struct AjWalk {
+  uint32_t* ord;
+  const uint32_t *ekid, *hrec, *nkr, *rne, *rnew, *iseq;
+  const uint64_t *koff, *rent;
+  uint32_t* oscr;
+  uint64_t n_rec;
+  uint32_t n_iseq, obmax;
+};
+__device__ __forceinline__ AjWalk aj_walk_args(const AggjArgs& g) {
+  AjWalk w;
+  w.ord = g.ord;
+  w.ekid = g.ekid;
+  w.hrec = g.hrec;
+  w.nkr = g.nkr;
+  w.rne = g.rne;
+  w.rnew = g.rnew;
+  w.iseq = g.iseq;
+  w.koff = g.koff;
+  w.rent = g.rent;
+  w.oscr = g.oscr;
+  w.n_rec = g.n_rec;
+  w.n_iseq = g.n_iseq;
+  w.obmax = g.obmax;
+  return w;
+}
+__device__ __forceinline__ AjTile aj_tile(const AjWalk& a, uint64_t r0) {
   const uint64_t r = r0 + (threadIdx.x & 63u);
   AjTile t{0u, 0u, 0u, 0ull, 0ull};
   if (r < a.n_rec) {
@@ -259,7 +292,7 @@ __device__ __forceinline__ AjRec aj_rec(const AjTile& t, uint32_t i) {
                (uint32_t)__builtin_amdgcn_readlane((int)t.ne, (int)i),
                (uint32_t)__builtin_amdgcn_readlane((int)t.nnew, (int)i), readlane64(t.ko, i), readlane64(t.g0, i)};
 }
-__device__ void aj_order_run(const AggjArgs& a, uint32_t* lds) {
+__device__ void aj_order_run(const AjWalk a, uint32_t* lds) {
   const uint32_t l = threadIdx.x;
   uint32_t seq = l;       // the previous record's order (lane p = key at position p) when in registers
   bool seq_reg = true;    // ... else in ord at the previous record's slots
@@ -296,16 +329,21 @@ __device__ void aj_order_run(const AggjArgs& a, uint32_t* lds) {
         seq = l < nkb ? a.ord[prev_ko + l] : 0u;
       }
       const uint32_t is = iseq && l < nseq ? a.iseq[l] : 0u;
+      const uint32_t sq = iseq ? is : seq;
+      // lane p: the hash of the key inserted p-th (gathered once, so the
+      // insertion loop's two readlanes per key are independent)
+      const uint32_t hsq = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((sq & 63u) << 2), (int)hk);
       HbReg A = hb_new(0);
       for (uint32_t p = 0; p < nseq; p++) {  // the accumulator's text, HashMap::insert per entry
-        uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)(iseq ? is : seq), (int)p);
-        hb_reserve(A, hk);
+        const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)sq, (int)p);
+        const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)hsq, (int)p);
+        hb_reserve(A);
         if (k & kAjDup) continue;  // a repeated key: the value changes, the layout does not
-        hb_put(A, k, (uint32_t)__builtin_amdgcn_readlane((int)hk, (int)k));
+        hb_put(A, k, h);
       }
       HbReg R = hb_new(0);
       for (uint32_t j = 0; j < ne; j++) {  // the record's own map
-        hb_reserve(R, hr);
+        hb_reserve(R);
         if ((uint32_t)__builtin_amdgcn_readlane((int)ek, (int)j) == kSkipEntry) continue;
         hb_put(R, j, (uint32_t)__builtin_amdgcn_readlane((int)hr, (int)j));
       }
@@ -313,7 +351,7 @@ __device__ void aj_order_run(const AggjArgs& a, uint32_t* lds) {
         const uint32_t j = (uint32_t)__builtin_amdgcn_readlane((int)R.pl, (int)__builtin_ctzll(m));
         const uint32_t kid = (uint32_t)__builtin_amdgcn_readlane((int)ek, (int)j);
         if (kid < nkb) continue;
-        hb_reserve(A, hk);
+        hb_reserve(A);
         hb_put(A, kid, (uint32_t)__builtin_amdgcn_readlane((int)hk, (int)kid));
       }
       const uint64_t live = hb_live(A);
@@ -365,13 +403,13 @@ __device__ void aj_order_run(const AggjArgs& a, uint32_t* lds) {
 }
 __global__ __launch_bounds__(64) void k_aggj_order(AggjArgs a) {
   __shared__ uint32_t lds[4u * (kAjLdsBuckets + kAjLdsBuckets / 32u)];
-  aj_order_run(a, lds);
+  aj_order_run(aj_walk_args(a), lds);
 }
 // several chains' order passes in one launch (fsg_chain_group_*): workgroup
 // i walks chain i's records
 __global__ __launch_bounds__(64) void k_aggj_order_group(const AggjArgs* list) {
   __shared__ uint32_t lds[4u * (kAjLdsBuckets + kAjLdsBuckets / 32u)];
-  aj_order_run(list[blockIdx.x], lds);
+  aj_order_run(aj_walk_args(list[blockIdx.x]), lds);
 }
 
 // ---------------------------------------------------------------------------
