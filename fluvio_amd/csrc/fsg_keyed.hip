@@ -130,16 +130,19 @@ __global__ __launch_bounds__(256) void k_aggj_hash(AggjArgs a) {
 
 __device__ __forceinline__ uint32_t hb_capacity(uint32_t B) { return B == 0 ? 0u : B <= 8u ? B - 1u : B / 8u * 7u; }
 // the register path: a table of at most 64 buckets, wave-uniform occupancy,
-// bucket s's payload in lane s of `pl`.  The occupancy mask is kept TILED:
-// B-bit periods repeated over 64 bits (rep = bit 0 of every period), so the
-// group window at any probe position is one 64-bit rotate (period B divides
-// 64) whatever B is, and a table smaller than a group (B = 4) scans its own
-// buckets circularly, which is what its EMPTY padding plus fix_insert_slot's
-// rescan from bucket 0 amount to.
+// bucket s's entry in lane s of `v`.  An entry packs the low 6 bits of the
+// key's hash (all a table of <= 64 buckets probes with) under the payload:
+// e = h & 63 | payload << 6, so a put and a resize's re-insert each move one
+// lane.  The occupancy mask is kept TILED: B-bit periods repeated over 64 bits
+// (rep = bit 0 of every period), so the group window at any probe position is
+// one 64-bit shift (period B divides 64) whatever B is, and a table smaller
+// than a group (B = 4) scans its own buckets circularly, which is what its
+// EMPTY padding plus fix_insert_slot's rescan from bucket 0 amount to.
 struct HbReg {
   uint64_t occ, rep;
-  uint32_t B, mask, wm, cap, items, pl, ph;  // ph: lane s = the hash of bucket s's payload
+  uint32_t B, mask, wm, cap, items, v;
 };
+__device__ __forceinline__ uint32_t hb_entry(uint32_t payload, uint32_t h) { return (h & 63u) | payload << 6; }
 __device__ __forceinline__ uint64_t rotr64(uint64_t x, uint32_t p) {
   return (x >> (p & 63u)) | (x << ((64u - p) & 63u));  // p = 0: x | x
 }
@@ -153,40 +156,106 @@ __device__ __forceinline__ HbReg hb_new(uint32_t B) {  // B in {0, 4, 8, 16, 32,
   t.wm = B < 8u ? 0xFu : 0xFFu;
   t.cap = hb_capacity(B);
   t.items = 0;
-  t.pl = 0;
-  t.ph = 0;
+  t.v = 0;
   return t;
 }
 // find_insert_slot: the first free bucket of the window at the probe
-// position; a full window (rare below 7/8 load) probes on by groups of 8
-__device__ __forceinline__ void hb_put(HbReg& t, uint32_t payload, uint32_t h) {
-  uint32_t pos = h & t.mask;
-  uint32_t win = (uint32_t)rotr64(t.occ, pos) & t.wm;
-  for (uint32_t stride = 8u; win == t.wm; stride += 8u) {
+// position; a full window (rare below 7/8 load) probes on by groups of 8.
+// Below 64 buckets the tiled mask needs no rotate: pos + 8 <= 40 bits.
+template <bool Wide>
+__device__ __forceinline__ uint32_t hb_window(const HbReg& t, uint32_t pos) {
+  return (Wide ? (uint32_t)rotr64(t.occ, pos) : (uint32_t)(t.occ >> pos)) & t.wm;
+}
+template <bool Wide>
+__device__ __forceinline__ void hb_put(HbReg& t, uint32_t e) {
+  uint32_t pos = e & t.mask;
+  uint32_t win = hb_window<Wide>(t, pos);
+  for (uint32_t stride = 8u; __builtin_expect(win == t.wm, 0); stride += 8u) {
     pos = (pos + stride) & t.mask;
-    win = (uint32_t)rotr64(t.occ, pos) & t.wm;
+    win = hb_window<Wide>(t, pos);
   }
   const uint32_t s = (pos + (uint32_t)__builtin_ctz(~win)) & t.mask;
   t.occ |= t.rep << s;
-  const bool mine = (threadIdx.x & 63u) == s;  // writelane
-  t.pl = mine ? payload : t.pl;
-  t.ph = mine ? h : t.ph;
+  t.v = (threadIdx.x & 63u) == s ? e : t.v;  // writelane
   t.items++;
+}
+__device__ __forceinline__ void hb_put(HbReg& t, uint32_t e) {
+  if (t.B == 64u) hb_put<true>(t, e);
+  else hb_put<false>(t, e);
 }
 __device__ __forceinline__ uint64_t hb_live(const HbReg& t) {
   return t.B < 64u ? t.occ & ((1ull << t.B) - 1ull) : t.occ;
 }
+// s_ff1 of a 64-bit mask: the lowest set bit, 0xFFFFFFFF for none
+__device__ __forceinline__ uint32_t sff1_64(uint64_t x) {
+  uint32_t d;
+  asm("s_ff1_i32_b64 %0, %1" : "=s"(d) : "s"(x));
+  return d;
+}
+// A run of n puts (src(i) = the i-th entry) on the assumption that each key's
+// first free bucket at or after its probe position lies inside that window,
+// which is what find_insert_slot then picks: the per-put chain is shift, ff1,
+// add, and, shift, and-not, with no branch.  The largest distance found is
+// checked once at the end; false (t untouched) when some window was full, and
+// the caller re-runs the puts exactly.
+template <class Src>
+__device__ __forceinline__ bool hb_run_fast(HbReg& t, Src src, uint32_t n) {
+  uint64_t fr = ~t.occ;  // free buckets, tiled like occ
+  uint32_t v = t.v, dmax = 0;
+  const uint32_t mask = t.mask;
+  const uint64_t rep = t.rep;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t e = src(i);
+    const uint32_t pos = e & mask;
+    const uint32_t d = sff1_64(fr >> pos);
+    dmax = max(dmax, d);
+    const uint32_t sl = (pos + d) & mask;
+    fr &= ~(rep << sl);
+    v = (threadIdx.x & 63u) == sl ? e : v;  // writelane
+  }
+  if (dmax >= (t.B < 8u ? 4u : 8u)) return false;
+  t.occ = ~fr;
+  t.v = v;
+  t.items += n;
+  return true;
+}
+template <bool Wide, class Src>
+__device__ __forceinline__ void hb_run_exact(HbReg& t, Src src, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++) hb_put<Wide>(t, src(i));
+}
+template <class Mk>  // mk(): a fresh source of the run's entries
+__device__ __forceinline__ void hb_run(HbReg& t, Mk mk, uint32_t n) {
+  if (hb_run_fast(t, mk(), n)) return;
+  if (t.B == 64u) hb_run_exact<true>(t, mk(), n);
+  else hb_run_exact<false>(t, mk(), n);
+}
 // reserve(1): no room -> capacity_to_buckets(capacity + 1) = 4, 8, 2B buckets,
-// the old buckets re-inserted in bucket order (each bucket's payload and hash
-// read independently: no readlane feeds another's lane index)
+// the old buckets re-inserted in bucket order
 __device__ __forceinline__ void hb_reserve(HbReg& t) {
   if (t.cap != t.items) return;
   HbReg n = hb_new(t.B ? 2u * t.B : 4u);
-  for (uint64_t m = hb_live(t); m; m &= m - 1ull) {
-    const uint32_t b = (uint32_t)__builtin_ctzll(m);
-    hb_put(n, (uint32_t)__builtin_amdgcn_readlane((int)t.pl, (int)b), (uint32_t)__builtin_amdgcn_readlane((int)t.ph, (int)b));
-  }
+  const uint64_t live = hb_live(t);
+  const uint32_t tv = t.v;
+  hb_run(n, [=]() {
+    return [m = live, tv](uint32_t) mutable {
+      const uint32_t b = (uint32_t)__builtin_ctzll(m);
+      m &= m - 1ull;
+      return (uint32_t)__builtin_amdgcn_readlane((int)tv, (int)b);
+    };
+  }, t.items);
   t = n;
+}
+// HashMap::insert of the entries es[0..n) (lane p = the p-th key's entry),
+// none of them repeated: reserve(1) before each insert only acts when the
+// table is full, so the keys go in in runs up to the capacity
+__device__ __forceinline__ void hb_insert_run(HbReg& t, uint32_t es, uint32_t n) {
+  for (uint32_t p = 0; p < n;) {
+    hb_reserve(t);
+    const uint32_t e = min(n, p + (t.cap - t.items));
+    hb_run(t, [=]() { return [es, p](uint32_t i) { return (uint32_t)__builtin_amdgcn_readlane((int)es, (int)(p + i)); }; },
+           e - p);
+    p = e;
+  }
 }
 // the general path: a table in LDS or HBM (occupancy bits + payloads), lane 0
 struct HbMem {
@@ -242,42 +311,41 @@ struct AjTile {
 // launch's argument array (global memory), every field access would otherwise
 // be a load the compiler must repeat after each store to `ord` (aliasing), and
 // each of those loads' waits also waits for the records' prefetched data
+// The pointers are global-address-space ones: loads through generic pointers
+// become flat loads, which count against the LDS counter too, so the walk's
+// ds_bpermute / ds_permute waits would also wait for the next record's prefetch.
+template <class T>
+using gptr = __attribute__((address_space(1))) T*;
 struct AjWalk {
-  uint32_t* ord;
-  const uint32_t *ekid, *hrec, *nkr, *rne, *rnew, *iseq;
-  const uint64_t *koff, *rent;
+  gptr<uint32_t> ord;
+  gptr<const uint32_t> ekid, hrec, nkr, rne, rnew, iseq;
+  gptr<const uint64_t> koff, rent;
   uint32_t* oscr;
   uint64_t n_rec;
   uint32_t n_iseq, obmax;
 };
 __device__ __forceinline__ AjWalk aj_walk_args(const AggjArgs& g) {
   AjWalk w;
-  w.ord = g.ord;
-  w.ekid = g.ekid;
-  w.hrec = g.hrec;
-  w.nkr = g.nkr;
-  w.rne = g.rne;
-  w.rnew = g.rnew;
-  w.iseq = g.iseq;
-  w.koff = g.koff;
-  w.rent = g.rent;
+  w.ord = (gptr<uint32_t>)g.ord;
+  w.ekid = (gptr<const uint32_t>)g.ekid;
+  w.hrec = (gptr<const uint32_t>)g.hrec;
+  w.nkr = (gptr<const uint32_t>)g.nkr;
+  w.rne = (gptr<const uint32_t>)g.rne;
+  w.rnew = (gptr<const uint32_t>)g.rnew;
+  w.iseq = (gptr<const uint32_t>)g.iseq;
+  w.koff = (gptr<const uint64_t>)g.koff;
+  w.rent = (gptr<const uint64_t>)g.rent;
   w.oscr = g.oscr;
   w.n_rec = g.n_rec;
   w.n_iseq = g.n_iseq;
   w.obmax = g.obmax;
   return w;
 }
+// (lanes past the last record repeat it: unpredicated loads, so the tile lands
+// in its loop-carried registers without a wait at the branch that issues it)
 __device__ __forceinline__ AjTile aj_tile(const AjWalk& a, uint64_t r0) {
-  const uint64_t r = r0 + (threadIdx.x & 63u);
-  AjTile t{0u, 0u, 0u, 0ull, 0ull};
-  if (r < a.n_rec) {
-    t.nk = a.nkr[r];
-    t.ne = a.rne[r];
-    t.nnew = a.rnew[r];
-    t.ko = a.koff[r];
-    t.g0 = a.rent[r];
-  }
-  return t;
+  const uint64_t r = min(r0 + (threadIdx.x & 63u), a.n_rec - 1ull);
+  return AjTile{a.nkr[r], a.rne[r], a.rnew[r], a.koff[r], a.rent[r]};
 }
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t i) {
   return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)i) |
@@ -294,72 +362,94 @@ __device__ __forceinline__ AjRec aj_rec(const AjTile& t, uint32_t i) {
 }
 __device__ void aj_order_run(const AjWalk a, uint32_t* lds) {
   const uint32_t l = threadIdx.x;
-  uint32_t seq = l;       // the previous record's order (lane p = key at position p) when in registers
+  // the previous record's order (lane p = key at position p) when in registers;
+  // record 0's accumulator lists the initial keys in the stored state's order
+  uint32_t seq = a.iseq == nullptr ? l : l < a.n_iseq ? a.iseq[l] : 0u;
   bool seq_reg = true;    // ... else in ord at the previous record's slots
-  AjTile cur = aj_tile(a, 0), nxt = aj_tile(a, 64);
+  AjTile cur = aj_tile(a, 0);
   AjRec q = aj_rec(cur, 0);
   // record 0's data; then each record issues the next one's
   uint32_t d_hk = l < q.nk ? a.ord[q.ko + l] : 0u;
   uint32_t d_ek = l < q.ne ? a.ekid[q.g0 + l] : kSkipEntry;
   uint32_t d_hr = l < q.ne ? a.hrec[q.g0 + l] : 0u;
   uint64_t prev_ko = 0;
-  for (uint64_t r = 0; r < a.n_rec; r++) {
-    const uint32_t i = (uint32_t)(r & 63u);
+  // a register-path record's order is stored at the top of the next record,
+  // ahead of that record's prefetch: the wait for the prefetch then covers a
+  // store issued as early, not one issued just before it
+  gptr<uint32_t> st_ptr = nullptr;
+  uint32_t st_val = 0;
+  // record 0's data in hand: entering the loop with these loads pending would
+  // make every wait of the loop body a full drain
+  __builtin_amdgcn_s_waitcnt(0);
+  for (uint64_t t0 = 0; t0 < a.n_rec; t0 += 64u) {  // tiles of 64 records, the next one in flight
+   const AjTile nxt = aj_tile(a, t0 + 64u);
+   const uint32_t cnt = (uint32_t)min(a.n_rec - t0, (uint64_t)64u);
+   for (uint32_t i = 0; i < cnt; i++) {
+    const uint64_t r = t0 + i;
+    if (st_ptr != nullptr) *st_ptr = st_val;
+    st_ptr = nullptr;
     const uint32_t nk = q.nk, ne = q.ne;
     const uint32_t nkb = nk - q.nnew;  // keys of the accumulator map (the previous text's)
     const uint64_t ko = q.ko, g0 = q.g0;
     const uint32_t hk = d_hk, ek = d_ek, hr = d_hr;
+    const bool first = r == 0;
+    const bool iseq = first && a.iseq != nullptr;
+    const uint32_t nseq = iseq ? a.n_iseq : nkb;
+    const bool reg = nk <= kAjRegKeys && ne <= kAjRegKeys && nseq <= kAjRegKeys;
+    uint32_t sq = 0, hsq = 0;
+    if (reg) {  // the loads this record itself needs go out (and are waited for) before the prefetch
+      if (!seq_reg) {
+        __threadfence();  // lane 0 wrote the previous order
+        seq = l < nkb ? a.ord[prev_ko + l] : 0u;
+        asm volatile("" ::"v"(seq));  // waited for here, not on the common path
+      }
+      sq = seq;
+      // lane p: the hash of the key inserted p-th (gathered once, so the
+      // insertion loop's two readlanes per key are independent)
+      hsq = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((sq & 63u) << 2), (int)hk);
+    }
     // the next record's scalars and data in flight
     if (r + 1 < a.n_rec) {
-      if (i == 63u) {
-        cur = nxt;
-        nxt = aj_tile(a, r + 65);
-      }
-      q = aj_rec(cur, (uint32_t)((r + 1) & 63u));
+      q = i < 63u ? aj_rec(cur, i + 1u) : aj_rec(nxt, 0u);
       d_hk = l < q.nk ? a.ord[q.ko + l] : 0u;
       d_ek = l < q.ne ? a.ekid[q.g0 + l] : kSkipEntry;
       d_hr = l < q.ne ? a.hrec[q.g0 + l] : 0u;
     }
-    const bool first = r == 0;
-    const bool iseq = first && a.iseq != nullptr;
-    const uint32_t nseq = iseq ? a.n_iseq : nkb;
-    if (nk <= kAjRegKeys && ne <= kAjRegKeys && nseq <= kAjRegKeys) {
-      if (!seq_reg) {
-        __threadfence();  // lane 0 wrote the previous order
-        seq = l < nkb ? a.ord[prev_ko + l] : 0u;
-      }
-      const uint32_t is = iseq && l < nseq ? a.iseq[l] : 0u;
-      const uint32_t sq = iseq ? is : seq;
-      // lane p: the hash of the key inserted p-th (gathered once, so the
-      // insertion loop's two readlanes per key are independent)
-      const uint32_t hsq = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((sq & 63u) << 2), (int)hk);
+    if (reg) {
       HbReg A = hb_new(0);
-      for (uint32_t p = 0; p < nseq; p++) {  // the accumulator's text, HashMap::insert per entry
-        const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)sq, (int)p);
-        const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)hsq, (int)p);
-        hb_reserve(A);
-        if (k & kAjDup) continue;  // a repeated key: the value changes, the layout does not
-        hb_put(A, k, h);
+      // the accumulator's text, HashMap::insert per entry
+      if (__builtin_amdgcn_ballot_w64(l < nseq && (sq & kAjDup) != 0u) == 0ull) {
+        hb_insert_run(A, hb_entry(sq, hsq), nseq);
+      } else {
+        for (uint32_t p = 0; p < nseq; p++) {
+          const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)sq, (int)p);
+          const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)hsq, (int)p);
+          hb_reserve(A);
+          if (k & kAjDup) continue;  // a repeated key: the value changes, the layout does not
+          hb_put(A, hb_entry(k, h));
+        }
       }
       HbReg R = hb_new(0);
+      const uint32_t er = hb_entry(l, hr);
       for (uint32_t j = 0; j < ne; j++) {  // the record's own map
         hb_reserve(R);
         if ((uint32_t)__builtin_amdgcn_readlane((int)ek, (int)j) == kSkipEntry) continue;
-        hb_put(R, j, (uint32_t)__builtin_amdgcn_readlane((int)hr, (int)j));
+        hb_put(R, (uint32_t)__builtin_amdgcn_readlane((int)er, (int)j));
       }
       for (uint64_t m = hb_live(R); m; m &= m - 1ull) {  // `for (repo, n) in next.0`: entry(repo) per vacant key
-        const uint32_t j = (uint32_t)__builtin_amdgcn_readlane((int)R.pl, (int)__builtin_ctzll(m));
+        const uint32_t j = (uint32_t)__builtin_amdgcn_readlane((int)R.v, (int)__builtin_ctzll(m)) >> 6;
         const uint32_t kid = (uint32_t)__builtin_amdgcn_readlane((int)ek, (int)j);
         if (kid < nkb) continue;
         hb_reserve(A);
-        hb_put(A, kid, (uint32_t)__builtin_amdgcn_readlane((int)hk, (int)kid));
+        hb_put(A, hb_entry(kid, (uint32_t)__builtin_amdgcn_readlane((int)hk, (int)kid)));
       }
       const uint64_t live = hb_live(A);
       const bool full = (live >> l) & 1ull;
       const uint32_t below = (uint32_t)__builtin_popcountll(live & ((1ull << l) - 1ull));
       const uint32_t pos = full ? below : nk + (l - below);
-      if (full) a.ord[ko + pos] = A.pl;
-      seq = (uint32_t)__builtin_amdgcn_ds_permute((int)(pos << 2), (int)A.pl);
+      st_ptr = full ? a.ord + ko + pos : nullptr;
+      st_val = A.v >> 6;
+      seq = (uint32_t)__builtin_amdgcn_ds_permute((int)(pos << 2), (int)(A.v >> 6));
       seq_reg = true;
       prev_ko = ko;
       continue;
@@ -370,9 +460,9 @@ __device__ void aj_order_run(const AjWalk a, uint32_t* lds) {
       const uint32_t bm = a.obmax <= kAjLdsBuckets ? kAjLdsBuckets : a.obmax, ow = (bm + 31u) / 32u;
       HbMem T[4];
       for (int t = 0; t < 4; t++) T[t] = HbMem{base + t * ow, base + 4u * ow + (uint64_t)t * bm, 0u, 0u};
-      const uint32_t* hkp = a.ord + ko;  // by key id
-      const uint32_t* hrp = a.hrec + g0;  // by entry
-      const uint32_t* prev = first ? nullptr : a.ord + prev_ko;
+      const uint32_t* hkp = (const uint32_t*)(a.ord + ko);  // by key id
+      const uint32_t* hrp = (const uint32_t*)(a.hrec + g0);  // by entry
+      const uint32_t* prev = first ? nullptr : (const uint32_t*)(a.ord + prev_ko);
       if (!first) __threadfence();  // the previous order, written by the whole wave
       HbMem& A = T[0];
       for (uint32_t p = 0; p < nseq; p++) {
@@ -397,9 +487,16 @@ __device__ void aj_order_run(const AjWalk a, uint32_t* lds) {
       for (uint32_t b = 0; b < A.B; b++)
         if (hbm_full(A, b)) a.ord[ko + o++] = A.pl[b];
     }
+    // drain this path's flat (LDS-or-HBM) accesses: while one is pending the
+    // memory counters are out of order, and every later wait of the loop
+    // would be a full drain, the next record's prefetch and the last order store included
+    __builtin_amdgcn_s_waitcnt(0);
     seq_reg = false;
     prev_ko = ko;
+   }
+   cur = nxt;
   }
+  if (st_ptr != nullptr) *st_ptr = st_val;
 }
 __global__ __launch_bounds__(64) void k_aggj_order(AggjArgs a) {
   __shared__ uint32_t lds[4u * (kAjLdsBuckets + kAjLdsBuckets / 32u)];
