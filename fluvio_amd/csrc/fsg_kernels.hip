@@ -2847,6 +2847,71 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t x, uint32_t lane) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// Every lane's segment out[d0, d0 + n) <- src[s0, s0 + n) at once: the
+// segments' 16-byte destination units are numbered across the wave (a scan)
+// and dealt out 64 at a time, so the loads of many records are in flight
+// together instead of one record's per wave round trip.  Units a segment
+// shares with its neighbours are written bytewise inside the segment only.
+__device__ __forceinline__ void copy_segs(uint8_t* __restrict__ out, const uint8_t* __restrict__ src, uint64_t d0,
+                                          uint64_t s0, uint32_t n, bool upper) {
+  const uint64_t act = __ballot(n != 0u);
+  if (__builtin_popcountll(act) <= 1) {  // one segment (a one-record batch): no scan
+    if (act) {
+      const uint32_t i = (uint32_t)__builtin_ctzll(act);
+      copy_seg(out, src, readlane_u64(d0, i), readlane_u64(s0, i), __builtin_amdgcn_readlane(n, i),
+               __builtin_amdgcn_readlane((uint32_t)upper, i) != 0u);
+    }
+    return;
+  }
+  const uint32_t lane = lane_id();
+  const uint32_t units = n ? (uint32_t)(((d0 + n + 15) >> 4) - (d0 >> 4)) : 0u;
+  const uint32_t incl = wave_incl_scan(units), ex = incl - units;
+  const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+  for (uint32_t u0 = 0; u0 < tot; u0 += 64) {
+    const uint32_t u = u0 + lane;
+    // the segment of unit u: the last lane whose exclusive prefix <= u (empty
+    // segments share their successor's prefix and are passed over)
+    uint32_t rr = 0;
+#pragma unroll
+    for (uint32_t st = 32; st > 0; st >>= 1) {
+      const uint32_t c = rr + st;
+      const uint32_t pc = __shfl(ex, (int)(c & 63), 64);
+      if (c < 64 && pc <= u) rr = c;
+    }
+    const uint32_t rex = __shfl(ex, (int)rr, 64);
+    const uint64_t rd = ((uint64_t)__shfl((uint32_t)(d0 >> 32), (int)rr, 64) << 32) | __shfl((uint32_t)d0, (int)rr, 64);
+    const uint64_t rs = ((uint64_t)__shfl((uint32_t)(s0 >> 32), (int)rr, 64) << 32) | __shfl((uint32_t)s0, (int)rr, 64);
+    const uint32_t rn = __shfl(n, (int)rr, 64);
+    const bool rup = __shfl((uint32_t)upper, (int)rr, 64) != 0u;
+    if (u >= tot) continue;
+    const uint64_t D = ((rd >> 4) + (u - rex)) << 4;
+    const uint64_t A = rs + D - rd;  // the source of D (may start before rs: the unit's head is masked)
+    const uint4* sp = (const uint4*)(src + (A & ~15ull));
+    const uint4 x0 = sp[0], x1 = sp[1];
+    const uint32_t w[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    const uint32_t sh = (uint32_t)(A & 15), q = sh >> 2, bs = sh & 3u;
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t lo = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
+      const uint32_t hi = q == 0 ? w[k + 1] : q == 1 ? w[k + 2] : q == 2 ? w[k + 3] : w[k + 4];
+      v[k] = __builtin_amdgcn_alignbyte(hi, lo, bs);
+      if (rup) v[k] = swar_upper(v[k]);
+    }
+    const uint64_t e = rd + rn;
+    const uint64_t lo = D > rd ? D : rd;
+    const uint64_t hi = D + 16 < e ? D + 16 : e;
+    if (lo == D && hi == D + 16) {
+      *(uint4*)(out + D) = make_uint4(v[0], v[1], v[2], v[3]);
+    } else {
+      const uint32_t jl = (uint32_t)(lo - D), jh = (uint32_t)(hi - D);
+#pragma unroll
+      for (int jj = 0; jj < 16; jj++)
+        if ((uint32_t)jj >= jl && (uint32_t)jj < jh) out[D + jj] = (uint8_t)(v[jj >> 2] >> (8 * (jj & 3)));
+    }
+  }
+}
+
 constexpr uint32_t kElemLaneCopy = 48;  // array elements up to this size are copied by their own lane
 
 // array_map batch (derive generator/array_map.rs:17-42): the elements of the
@@ -3008,17 +3073,10 @@ __device__ __forceinline__ void write_batch(const WriteArgs& a, const Plan& p, i
       n = venc(r.hdr, t);
       for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
     }
-    // payloads, record by record, with the whole wave
-    const uint32_t nrec = st.nkeep - k0 < 64u ? st.nkeep - k0 : 64u;
+    // payloads: the chunk's keys, then its values, each spread over the wave
     const bool cat = st.nkeep && (d[0].mode == KM_CONCAT || d[0].mode == KM_AGGJ);
-    for (uint32_t i = 0; i < nrec; i++) {
-      const uint32_t rkl = __builtin_amdgcn_readlane(kl, i);
-      const uint32_t rvc = __builtin_amdgcn_readlane(vc, i);
-      if (rkl) copy_seg(out, a.slice, readlane_u64(kd, i), readlane_u64(r.kpos, i), rkl, false);
-      if (rvc)
-        copy_seg(out, cat ? a.cat : a.slice, readlane_u64(vd, i), readlane_u64(vsrc, i), rvc,
-                 __builtin_amdgcn_readlane((uint32_t)r.mode, i) == KM_UPPER);
-    }
+    if (__ballot(kl != 0u)) copy_segs(out, a.slice, kd, r.kpos, kl, false);
+    copy_segs(out, cat ? a.cat : a.slice, vd, vsrc, vc, r.mode == KM_UPPER);
     run += readlane_u64(incl, 63);
   }
 }
