@@ -1358,13 +1358,20 @@ __device__ __forceinline__ bool lean_or(uint32_t* red, uint32_t& par, bool p) {
 }
 // the filter_json variant: per-chunk quote / in-string masks, the token list,
 // the token DFA (fsg_json_dfa.h)
-constexpr int kJsonChunks = (kLeanWin + 48) / 16 + 2;
-constexpr int kJsonEnt = 2048;  // token entries per batch (more: exact kernel)
+// LDS of the JSON variant is sized for 5 workgroups per CU (<= 32 KiB): the
+// per-chunk words cover 16 KiB of values (a batch whose values span more takes
+// the exact kernel), the token list 1024 entries (a 16 KiB batch of ~1 KB log
+// records has ~600), and jn lives in the regex rows' space (LeanLds::tt; a
+// chain with regex and JSON stages reloads its rows per batch)
+constexpr int kJsonChunks = 1024;
+constexpr int kJsonEnt = 1024;  // token entries per batch (more: exact kernel)
 constexpr int kJsonSeg = kJsonChunks;  // object members per batch (LeanLdsJ::jn; more: exact kernel)
 __device__ constexpr JsonDfaTables g_json_tables{};
+static_assert(sizeof(LeanLds::tt) >= 2 * kJsonChunks, "jn overlays the regex rows");
 struct __attribute__((aligned(16))) LeanLdsJ : LeanLds {
   uint32_t jm[kJsonChunks];      // pass 1: quote16 | special16 << 16; pass 2: in-string16 | hot16 << 16
-  uint16_t jn[kJsonChunks];      // non-space16; then the object members: first token | record start << 15
+  // jn: non-space16 per chunk; then the object members: first token | record start << 15
+  __device__ __forceinline__ uint16_t* jn() { return reinterpret_cast<uint16_t*>(tt); }
   uint32_t ent[kJsonEnt];        // pos | in-string bit << 15 | byte << 16 | token class << 24
   uint32_t racc[kLeanMaxR];      // per record: level fields | message fields << 8 | bad << 16
   uint32_t rlvl[kLeanMaxR];      // per record: bit (LogLevel index) of its level value
@@ -1549,8 +1556,10 @@ __device__ __forceinline__ uint32_t lean_regex(LeanLds& L, int nr, uint32_t lo, 
     const uint32_t p1 = p0 + q_len < hi ? p0 + q_len : hi;
     const uint32_t pe = p1 + mlen - (mlen ? 1u : 0u);
     const uint32_t pend = pe < hi ? pe : hi;
-    int r = lean_rec_of(L, nr, p0);
-    if (r < 0) r = 0;
+    // the first record whose value ends after p0: the last value starting at or before p0
+    int r = 0;
+    for (int st = 64; st > 0; st >>= 1)
+      if (r + st < nr && L.r_vs[r + st] <= p0) r += st;
     for (; r < nr; r++) {
       const uint32_t vs = L.r_vs[r], ve = L.r_ve[r];
       if (vs >= p1) break;
@@ -1653,7 +1662,7 @@ __device__ __forceinline__ uint32_t json_str_class(const LdsT& L, uint32_t a, ui
 template <bool kProj>
 __device__ __forceinline__ void json_members(LeanLdsJ& L, int nr, uint32_t ntok, uint32_t nseg) {
   for (uint32_t k = threadIdx.x; k < nseg; k += kLeanThreads) {
-    const uint32_t sg = L.jn[k];
+    const uint32_t sg = L.jn()[k];
     const bool first = (sg & 0x8000u) != 0u;
     const uint32_t t0 = sg & 0x7FFFu;
     uint32_t t = t0;
@@ -1719,7 +1728,21 @@ __device__ __forceinline__ void json_members(LeanLdsJ& L, int nr, uint32_t ntok,
   }
 }
 
-__device__ bool lean_json_stage(LeanLdsJ& L, int nr, uint32_t& orpar, bool proj, uint32_t fl) {
+#ifdef FSG_LEAN_TIMING
+#define JT_PARAMS , uint64_t *lt_acc, uint64_t &lt_last
+#define JT_ARGS , lt_acc, lt_last
+#define JMARK(k)                                             \
+  {                                                          \
+    const uint64_t lt_now = __builtin_amdgcn_s_memtime();    \
+    lt_acc[k] += lt_now - lt_last;                           \
+    lt_last = lt_now;                                        \
+  }
+#else
+#define JT_PARAMS
+#define JT_ARGS
+#define JMARK(k)
+#endif
+__device__ bool lean_json_stage(LeanLdsJ& L, int nr, uint32_t& orpar, bool proj, uint32_t fl JT_PARAMS) {
   const uint32_t l = threadIdx.x;
   const uint32_t c0 = L.r_vs[0] & ~15u, c1 = L.r_ve[nr - 1];
   const uint32_t nch = (c1 - c0 + 15) >> 4;
@@ -1741,9 +1764,10 @@ __device__ bool lean_json_stage(LeanLdsJ& L, int nr, uint32_t& orpar, bool proj,
       ns |= nib4(zbytes(w ^ 0x20202020u)) << (4 * d);
     }
     L.jm[k] = q | (sp << 16);
-    L.jn[k] = (uint16_t)(~ns & 0xFFFFu);
+    L.jn()[k] = (uint16_t)(~ns & 0xFFFFu);
     par ^= __builtin_popcount(q) & 1u;
   }
+  JMARK(6);
   uint32_t tot;
   uint32_t carry = wg_excl_sum(par, L.wsum, &tot) & 1u;  // parity of all quotes before my chunks
   uint32_t cnt = 0;
@@ -1751,10 +1775,11 @@ __device__ bool lean_json_stage(LeanLdsJ& L, int nr, uint32_t& orpar, bool proj,
     const uint32_t m = L.jm[k], q = m & 0xFFFFu, sp = m >> 16;
     const uint32_t instr = (pxor16(q) ^ q ^ (carry ? 0xFFFFu : 0u)) & 0xFFFFu;
     carry ^= __builtin_popcount(q) & 1u;
-    const uint32_t hot = q | sp | ((uint32_t)L.jn[k] & ~instr);
+    const uint32_t hot = q | sp | ((uint32_t)L.jn()[k] & ~instr);
     L.jm[k] = instr | (hot << 16);
     cnt += __builtin_popcount(hot);
   }
+  JMARK(7);
   // 2. token list
   uint32_t ntok;
   uint32_t e = wg_excl_sum(cnt, L.wsum, &ntok);
@@ -1772,6 +1797,7 @@ __device__ bool lean_json_stage(LeanLdsJ& L, int nr, uint32_t& orpar, bool proj,
   }
   if (l == 0) L.nseg = 0;
   lean_sync();
+  JMARK(8);
   // classes; an opening quote takes the class of its string (the next token
   // closes it).  Bits 0..15 never change here, so a neighbour's position and
   // in-string bit can be read while it is being rewritten.
@@ -1804,10 +1830,11 @@ __device__ bool lean_json_stage(LeanLdsJ& L, int nr, uint32_t& orpar, bool proj,
     // members: the token after a comma starts one (of the comma's record)
     if (cls == JC_COMMA) {
       const uint32_t k = atomicAdd(&L.nseg, 1u);
-      if (k < (uint32_t)kJsonSeg) L.jn[k] = (uint16_t)(t + 1);
+      if (k < (uint32_t)kJsonSeg) L.jn()[k] = (uint16_t)(t + 1);
     }
   }
   lean_sync();
+  JMARK(9);
   // 3a. per record: balanced quotes at its ends, its first token (binary
   //     search on positions) = the start of its first member
   const uint32_t r = 2 * (l & 63u) + (l >> 6);
@@ -1834,7 +1861,7 @@ __device__ bool lean_json_stage(LeanLdsJ& L, int nr, uint32_t& orpar, bool proj,
     L.rbest[r] = 0;
     if (!bad) {
       const uint32_t k = atomicAdd(&L.nseg, 1u);
-      if (k < (uint32_t)kJsonSeg) L.jn[k] = (uint16_t)(lo | 0x8000u);
+      if (k < (uint32_t)kJsonSeg) L.jn()[k] = (uint16_t)(lo | 0x8000u);
     }
   }
   (void)t_first;
@@ -1850,11 +1877,13 @@ __device__ bool lean_json_stage(LeanLdsJ& L, int nr, uint32_t& orpar, bool proj,
   //     member whose key is the field; numbers whose serde_json text differs
   //     from the source (fractions, exponents, -0, more than 18 digits) are
   //     unsupported by the device restatement -> exact kernel
+  JMARK(10);
   if (proj)
     json_members<true>(L, nr, ntok, nseg);
   else
     json_members<false>(L, nr, ntok, nseg);
   lean_sync();
+  JMARK(11);
   if ((int)r < nr) {
     const uint32_t ac = L.racc[r];
     if (proj) {
@@ -2097,7 +2126,7 @@ void launch_chase_w(const EvalArgs& a, hipStream_t s) {
 // four waves per SIMD (eight workgroups per CU, as many as the LDS holds)
 template <bool kJson>
 #ifndef FSG_JSON_WPE
-#define FSG_JSON_WPE 1  // waves per SIMD of the JSON lean kernel (register budget)
+#define FSG_JSON_WPE 3  // waves per SIMD of the JSON lean kernel: <= 168 VGPRs, with <= 32 KiB LDS 5 workgroups per CU
 #endif
 #ifndef FSG_LEAN_WPE
 #define FSG_LEAN_WPE 4
@@ -2145,7 +2174,7 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
         ndo += sd.needle_len;
       }
     }
-    if (nrx == 1) {  // one regex stage: its rows stay resident
+    if (nrx == 1 && !kJson) {  // one regex stage: its rows stay resident (the JSON variant reuses them as jn)
       const StageDesc& sd = ch.st[rx];
       const uint64_t* tt = (const uint64_t*)(a.blob + (sd.in_type == VT_SRC_UPPER ? sd.dfa.tt_up : sd.dfa.tt));
       for (uint32_t t = l; t < 256; t += kLeanThreads) L.tt[t] = tt[t];
@@ -2153,7 +2182,7 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
     if (l == 0) {
       L.nst = nst;
       L.out_upper = ch.out_type == VT_SRC_UPPER ? 1u : 0u;
-      L.tt_stage = nrx == 1 ? rx : 0xFFu;
+      L.tt_stage = nrx == 1 && !kJson ? rx : 0xFFu;
       L.nd_res = nd_res ? 1u : 0u;
     }
     if constexpr (kJson) {
@@ -2162,6 +2191,17 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
     }
   }
   uint32_t par = 0;  // lean_or pair
+#ifdef FSG_LEAN_TIMING  // experiment builds: per-phase clock sums, printed by workgroup 0
+  uint64_t lt_acc[12] = {}, lt_last = __builtin_amdgcn_s_memtime(), lt_nb = 0;
+#define LEAN_MARK(k)                                         \
+  {                                                          \
+    const uint64_t lt_now = __builtin_amdgcn_s_memtime();    \
+    lt_acc[k] += lt_now - lt_last;                           \
+    lt_last = lt_now;                                        \
+  }
+#else
+#define LEAN_MARK(k)
+#endif
   // the previous batch's results, stored once the next window is in flight
   // (a store issued right before the wait for the next window would be waited for too)
   uint32_t p_b = 0xFFFFFFFFu;
@@ -2210,6 +2250,7 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
     const uint32_t re = a.rend[b];
     __builtin_amdgcn_s_waitcnt(0);  // this wave's pieces have landed
     lean_sync();                    // ... and the other wave's
+    LEAN_MARK(0);
     // batch header (file format, batch.rs:163-180), read before the gaps are cleared
     const uint8_t* h = L.win + (pos - al);
     const int64_t base_offset = (int64_t)rd_be(h, 8);
@@ -2259,6 +2300,7 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
       L.r_ve[l] = vs + vl;
     }
     defer = lean_or(L.red, par, defer || !g);  // a record that does not frame exactly
+    LEAN_MARK(1);
     uint64_t alive = __ballot((int)l < nr);
     // 3. stages.  Before the first scan every non-value byte of the scanned
     //    range is cleared (record headers, keys, lengths): then the OR of the
@@ -2291,10 +2333,12 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
           cleared = true;
         }
         lean_sync();
-        if (nr > 0 && lean_json_stage(L, nr, par, proj, fl)) {
+        LEAN_MARK(2);
+        if (nr > 0 && lean_json_stage(L, nr, par, proj, fl JT_ARGS)) {
           defer = true;
           break;
         }
+        LEAN_MARK(3);
         alive &= __ballot(l < 64 && ((L.match[(l >> 5) & 1] >> (l & 31)) & 1u));
         if (proj && (int)l < nr) {  // lane l keeps record l's (narrowed) value span
           vs = L.r_vs[l];
@@ -2308,7 +2352,9 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
       if (!rx && m == 0 && checked) continue;  // an empty needle keeps every (UTF-8) value
       if (nr == 0) break;
       const uint32_t lo = L.r_vs[0], hi = L.r_ve[nr - 1];
-      if (!cleared) {
+      // the regex scan runs over each value's own bytes only (its OR covers
+      // value bytes, its records come from a search of r_vs): no gap clearing
+      if (!cleared && !rx) {
         clear_gaps(L, nr, vs, vl);
         cleared = true;
       }
@@ -2324,8 +2370,10 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
           for (uint32_t t = l; t < 256; t += kLeanThreads) L.tt[t] = tt[t];
         }
         lean_sync();
+        LEAN_MARK(2);
         const uint32_t orw = lean_regex(L, nr, lo, hi, sd.max_len, sd.s_bot, sd.s_mid, sd.acc1, sd.acc2);
         const bool high = lean_or(L.red, par, (orw & 0x80808080u) != 0u);  // also orders the match bits
+        LEAN_MARK(3);
         if (!checked && high) defer = true;  // a non-ASCII value: exact UTF-8 / Unicode DFA path
         checked = true;
         const bool hit = l < 64 && ((L.match[(l >> 5) & 1] >> (l & 31)) & 1u);
@@ -2345,6 +2393,7 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
         for (uint32_t t = l; t < m; t += kLeanThreads) L.needle[t] = nd[t];
       }
       lean_sync();
+      LEAN_MARK(2);
       uint32_t orw;
       if (m >= 7) orw = lean_scan<0>(L, nr, lo, hi, nullptr, m, upper);
       else if (m >= 4) orw = lean_scan<1>(L, nr, lo, hi, nullptr, m, upper);
@@ -2354,6 +2403,7 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
       if (!checked && high) defer = true;  // a non-ASCII value: exact UTF-8 path
       checked = true;
       if (m > 0) alive &= __ballot(l < 64 && ((L.match[(l >> 5) & 1] >> (l & 31)) & 1u));
+      LEAN_MARK(3);
       lean_sync();  // match / needle are rewritten by the next stage
     }
     // 4. survivors -> descriptors (stored by the next iteration's flush)
@@ -2383,9 +2433,21 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
     p_nkeep = (uint32_t)__popcll(alive);
     p_sec = sec_len;
     flush();
+    LEAN_MARK(4);
+#ifdef FSG_LEAN_TIMING
+    lt_nb++;
+#endif
     if (bn >= a.nbatches) break;
     b = bn;
   }
+#ifdef FSG_LEAN_TIMING
+  if (blockIdx.x < 2 && (threadIdx.x & 63u) == 0)
+    printf("lean wg %u wave %u batches %lu wait %lu frame %lu gaps %lu scan %lu tail %lu | j1 %lu j1b %lu j2 %lu j2c %lu j3a %lu j3b %lu\n",
+           blockIdx.x, threadIdx.x >> 6, (unsigned long)lt_nb, (unsigned long)lt_acc[0], (unsigned long)lt_acc[1],
+           (unsigned long)lt_acc[2], (unsigned long)lt_acc[3], (unsigned long)lt_acc[4], (unsigned long)lt_acc[6],
+           (unsigned long)lt_acc[7], (unsigned long)lt_acc[8], (unsigned long)lt_acc[9], (unsigned long)lt_acc[10],
+           (unsigned long)lt_acc[11]);
+#endif
 }
 
 // ---------------------------------------------------------------------------
