@@ -357,7 +357,8 @@ struct OneArgs {
   uint32_t in_len;     // the device slice's allocation (zeros behind the input)
   uint32_t in_real;    // input bytes to read from hin (a multiple of 16)
   int32_t empty_chain;
-  int32_t pad;
+  uint32_t seq;        // written to *hflag (pinned) once the read-back block is in host memory
+  uint32_t* hflag;     // the host polls it instead of the stream
 };
 constexpr uint32_t kOneHead = 512;  // Plan | BatchStat | Mins, then the output batch
 // a chain segment's output as the next segment's input slice (k_seg_headers):

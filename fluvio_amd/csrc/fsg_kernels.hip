@@ -4994,6 +4994,11 @@ __global__ __launch_bounds__(kEvalThreads) void k_one(OneArgs o) {
   const uint4* src = (const uint4*)o.plan;
   uint4* dst = (uint4*)o.hout;
   for (uint32_t u = t; u < (n + 15) / 16; u += kEvalThreads) dst[u] = src[u];
+  // completion flag: every thread's block stores are made visible system-wide,
+  // then one store of the call's sequence number releases them to the host
+  __threadfence_system();
+  __syncthreads();
+  if (t == 0) __hip_atomic_store(o.hflag, o.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 void launch_one(const OneArgs& o, uint32_t ops, hipStream_t s) {
   const size_t dyn = (ops & opbit(OP_REGEX)) ? kDfaDyn : 0;

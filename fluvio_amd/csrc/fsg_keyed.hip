@@ -429,19 +429,30 @@ __device__ void aj_order_run(const AjWalk a, uint32_t* lds) {
           hb_put(A, hb_entry(k, h));
         }
       }
-      HbReg R = hb_new(0);
-      const uint32_t er = hb_entry(l, hr);
-      for (uint32_t j = 0; j < ne; j++) {  // the record's own map
-        hb_reserve(R);
-        if ((uint32_t)__builtin_amdgcn_readlane((int)ek, (int)j) == kSkipEntry) continue;
-        hb_put(R, (uint32_t)__builtin_amdgcn_readlane((int)er, (int)j));
-      }
-      for (uint64_t m = hb_live(R); m; m &= m - 1ull) {  // `for (repo, n) in next.0`: entry(repo) per vacant key
-        const uint32_t j = (uint32_t)__builtin_amdgcn_readlane((int)R.v, (int)__builtin_ctzll(m)) >> 6;
-        const uint32_t kid = (uint32_t)__builtin_amdgcn_readlane((int)ek, (int)j);
-        if (kid < nkb) continue;
+      // the record's own map only orders its keys that are new to the
+      // accumulator (entry(repo) inserts them in the map's bucket order): with
+      // none there is nothing to do, with one entry holding a new key its place
+      // in that order does not matter
+      const uint64_t vac = __builtin_amdgcn_ballot_w64(l < ne && ek != kSkipEntry && ek >= nkb);
+      if (vac != 0ull && (vac & (vac - 1ull)) == 0ull) {
+        const uint32_t kid = (uint32_t)__builtin_amdgcn_readlane((int)ek, (int)__builtin_ctzll(vac));
         hb_reserve(A);
         hb_put(A, hb_entry(kid, (uint32_t)__builtin_amdgcn_readlane((int)hk, (int)kid)));
+      } else if (vac != 0ull) {
+        HbReg R = hb_new(0);
+        const uint32_t er = hb_entry(l, hr);
+        for (uint32_t j = 0; j < ne; j++) {  // the record's own map
+          hb_reserve(R);
+          if ((uint32_t)__builtin_amdgcn_readlane((int)ek, (int)j) == kSkipEntry) continue;
+          hb_put(R, (uint32_t)__builtin_amdgcn_readlane((int)er, (int)j));
+        }
+        for (uint64_t m = hb_live(R); m; m &= m - 1ull) {  // `for (repo, n) in next.0`: entry(repo) per vacant key
+          const uint32_t j = (uint32_t)__builtin_amdgcn_readlane((int)R.v, (int)__builtin_ctzll(m)) >> 6;
+          const uint32_t kid = (uint32_t)__builtin_amdgcn_readlane((int)ek, (int)j);
+          if (kid < nkb) continue;
+          hb_reserve(A);
+          hb_put(A, hb_entry(kid, (uint32_t)__builtin_amdgcn_readlane((int)hk, (int)kid)));
+        }
       }
       const uint64_t live = hb_live(A);
       const bool full = (live >> l) & 1ull;

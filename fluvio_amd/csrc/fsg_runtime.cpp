@@ -519,6 +519,9 @@ struct fsg_chain {
   // the kernel reads the input from and writes the block back to (no copies)
   DevBuf one_meta, one_blk;
   PinBuf one_pin;
+  uint32_t one_seq = 0;  // k_one completion flag values
+  void* one_dev = nullptr;        // one_pin's device address
+  void* one_dev_for = nullptr;    // ... for this host allocation
   DevBuf dstate;  // aggregate-sum accumulator (i32) after the last call, in HBM
   // aggregate-json: key dictionary, index, initial keys, per-batch accumulator text
   DevBuf aj_tptr, aj_tlen, aj_kup, aj_out, aj_accoff, aj_acclen;  // aggregate-json
@@ -2786,7 +2789,7 @@ int process_one(fsg_chain* c, const uint8_t* raw, size_t len, int64_t base_offse
   const size_t cap = 128 + 4 * len;  // stateless outputs stay within the input's size plus the i32 digits
   if (alloc > kSmallOut || kOneHead + cap > kSmallOut) return 1;
   c->one_pin.flags = hipHostMallocMapped | hipHostMallocCoherent;
-  HIPCHK(c->one_pin.ensure(2 * kSmallOut));
+  HIPCHK(c->one_pin.ensure(2 * kSmallOut + 64));  // input | read-back block | completion flag
   HIPCHK(c->ingest.data.ensure(alloc));
   HIPCHK(c->one_blk.ensure(kOneHead + cap));
   HIPCHK(c->kept.ensure(std::max<size_t>(len / 7 + 1, 1) * sizeof(KeptRec)));
@@ -2819,9 +2822,14 @@ int process_one(fsg_chain* c, const uint8_t* raw, size_t len, int64_t base_offse
   hipStream_t st = c->stream;
   uint8_t* blk = c->one_blk.as<uint8_t>();
   uint8_t* hb = (uint8_t*)c->one_pin.p + kSmallOut;  // the read-back block lands here
-  void *din = nullptr, *dout = nullptr;  // the pinned buffers' device addresses (k_one reads / writes them)
-  HIPCHK(hipHostGetDevicePointer(&din, b, 0));
-  HIPCHK(hipHostGetDevicePointer(&dout, hb, 0));
+  // the pinned buffer's device address (k_one reads the input, writes the block
+  // and the flag through it), looked up once per allocation
+  if (c->one_dev_for != c->one_pin.p) {
+    HIPCHK(hipHostGetDevicePointer(&c->one_dev, c->one_pin.p, 0));
+    c->one_dev_for = c->one_pin.p;
+  }
+  void* din = c->one_dev;
+  void* dout = (uint8_t*)c->one_dev + kSmallOut;
   OneArgs o{};
   EvalArgs& ea = o.ea;
   ea.slice = c->ingest.data.as<uint8_t>();
@@ -2845,11 +2853,26 @@ int process_one(fsg_chain* c, const uint8_t* raw, size_t len, int64_t base_offse
   o.in_len = (uint32_t)alloc;
   o.in_real = (uint32_t)in_real;
   o.empty_chain = c->hdesc.nstages == 0 ? 1 : 0;
+  volatile uint32_t* flag = (volatile uint32_t*)((uint8_t*)c->one_pin.p + 2 * kSmallOut);
+  *flag = 0;
+  o.hflag = (uint32_t*)((uint8_t*)c->one_dev + 2 * kSmallOut);
+  o.seq = ++c->one_seq ? c->one_seq : ++c->one_seq;  // never 0
   uint32_t ops = 0;
   for (uint32_t k = 0; k < c->hdesc.nstages; k++) ops |= 1u << c->hdesc.st[k].op;
   launch_one(o, ops, st);  // one launch: input over PCIe, process(), the block back to pinned memory
   HIPCHK(hipGetLastError());
-  HIPCHK(wait_stream(st));
+  // the kernel's last act is the flag store (after a system-scope fence): poll
+  // host memory, no runtime call on the fast path; the stream is waited for
+  // only if the flag is late (an error or a slow device surfaces there)
+  {
+    const auto t0 = std::chrono::steady_clock::now();
+    bool seen = false;
+    while (!seen) {
+      seen = __atomic_load_n(flag, __ATOMIC_ACQUIRE) == o.seq;
+      if (!seen && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(500)) break;
+    }
+    if (!seen) HIPCHK(wait_stream(st));
+  }
   Plan p;
   BatchStat bs;
   memcpy(&p, hb, sizeof p);
