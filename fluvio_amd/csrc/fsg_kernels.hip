@@ -1556,10 +1556,8 @@ __device__ __forceinline__ uint32_t lean_regex(LeanLds& L, int nr, uint32_t lo, 
     const uint32_t p1 = p0 + q_len < hi ? p0 + q_len : hi;
     const uint32_t pe = p1 + mlen - (mlen ? 1u : 0u);
     const uint32_t pend = pe < hi ? pe : hi;
-    // the first record whose value ends after p0: the last value starting at or before p0
-    int r = 0;
-    for (int st = 64; st > 0; st >>= 1)
-      if (r + st < nr && L.r_vs[r + st] <= p0) r += st;
+    int r = lean_rec_of(L, nr, p0);
+    if (r < 0) r = 0;
     for (; r < nr; r++) {
       const uint32_t vs = L.r_vs[r], ve = L.r_ve[r];
       if (vs >= p1) break;
@@ -2352,9 +2350,7 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJ
       if (!rx && m == 0 && checked) continue;  // an empty needle keeps every (UTF-8) value
       if (nr == 0) break;
       const uint32_t lo = L.r_vs[0], hi = L.r_ve[nr - 1];
-      // the regex scan runs over each value's own bytes only (its OR covers
-      // value bytes, its records come from a search of r_vs): no gap clearing
-      if (!cleared && !rx) {
+      if (!cleared) {
         clear_gaps(L, nr, vs, vl);
         cleared = true;
       }
