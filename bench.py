@@ -87,8 +87,8 @@ def parse():
     return ap.parse_args()
 
 
-KERNEL_SOURCES = ("fsg_kernels.hip", "fsg_device.h", "fsg_codec_dev.h", "fsg_json_dev.h", "fsg_json_dfa.h",
-                  "fsg_launch.h")
+KERNEL_SOURCES = ("fsg_kernels.hip", "fsg_array.hip", "fsg_device.h", "fsg_codec_dev.h", "fsg_json_dev.h",
+                  "fsg_json_dfa.h", "fsg_launch.h")
 
 
 def lib_tag():
