@@ -56,7 +56,7 @@ WORKLOADS = {
                  "steady state: the state persists across steps, so after the first step every value is a "
                  "duplicate (the decisions, table build and compaction still run over every record)"),
 }
-C5 = {"partitions": 64, "records_per_partition": 500_000,
+C5 = {"partitions": 64, "records_per_partition": 1_000_000,
       "modules": [("aggregate-sum", {}, None)],
       "description": "aggregate-sum over 64 partitions (decimal i32 records), per-partition accumulators in HBM, "
                      "RCCL all-reduce of the partition state vector each step"}
@@ -84,7 +84,35 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="records per CPU-baseline process")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rank plumbing only (launch, rendezvous, barrier, max over ranks, the JSON line): no GPU work, "
+                         "for the CPU tests of --gpus N")
     return ap.parse_args()
+
+
+def launch_ranks(a):
+    """--gpus N without a torch.distributed launcher around us: start one process
+    per GPU under torch.distributed.run (127.0.0.1 rendezvous) as a CHILD of this
+    GPU-free process and exit with its code.  Returns None when this process is
+    already a rank (or N == 1).  A launcher's WORLD_SIZE that disagrees with
+    --gpus is an error: the line would report the wrong n_gpus."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        explicit = any(x == "--gpus" or x.startswith("--gpus=") for x in sys.argv[1:])
+        if explicit and int(ws) != a.gpus:
+            sys.stderr.write(f"bench.py: WORLD_SIZE={ws} but --gpus {a.gpus}\n")
+            return 2
+        return None
+    if a.gpus <= 1:
+        return None
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 KERNEL_SOURCES = ("fsg_kernels.hip", "fsg_array.hip", "fsg_device.h", "fsg_codec_dev.h", "fsg_json_dev.h",
@@ -200,28 +228,50 @@ def cpu_baseline(kind, modules, per_proc):
             "seconds": busy, "wall_s": wall}
 
 
-def roofline(per, t, workload, n_records, n_batches):
-    # algorithmic bytes per launch: k_eval reads the slice once; k_write reads the
-    # survivors' payloads (~ the output size) and writes the output batch once; the
-    # CRC reads the output once.  array_map (C4): SURVEY §8(d)'s unit is input +
-    # Σ output record bytes, and both of its passes are priced on it (k_arr_lean
-    # sizes the output from the input; k_arr_write reads the input and writes the
-    # output, the one kernel that moves exactly those bytes)
-    if workload == "c4-array-map":
-        ev_bytes = wr_bytes = t["in_bytes"] + t["out_bytes"]
-    else:
-        ev_bytes, wr_bytes = t["in_bytes"], 2 * t["out_bytes"]
-    kernels = {"k_eval": (per["eval_ms"], ev_bytes), "k_write": (per["write_ms"], wr_bytes),
-               "k_crc": (per["crc_ms"], t["out_bytes"])}
-    dom = max(kernels, key=lambda k: kernels[k][0])
-    dom_ms, dom_bytes = kernels[dom]
+def roofline(per, t, workload, n_records, n_batches, records_out, step_ms):
+    """The dominant phase of the step and its HBM roofline, plus the whole step.
+    Phases (HIP events on the chain's stream) and their algorithmic bytes per
+    launch: eval reads the slice once (k_chase + k_eval_lean /
+    k_arr_lean + deferred k_eval); plan reads a 64-B descriptor per surviving
+    record and ~300 B of scan rows per batch (k_mins, k_size, k_scan_*, k_plan);
+    text is the aggregate text / order phase (output bytes); write reads the
+    survivors' payloads and writes the output once (array_map: k_arr_write reads
+    the input and writes the output); crc reads the output once."""
+    ib, ob = t["in_bytes"], t["out_bytes"]
+    c4 = workload == "c4-array-map"
+    phases = {"k_eval": (per["eval_ms"], ib),
+              "k_plan": (per["plan_ms"], 64 * records_out + 300 * n_batches),
+              "k_text": (per.get("text_ms", 0.0), ob),
+              "k_write": (per["write_ms"], ib + ob if c4 else 2 * ob),
+              "k_crc": (per["crc_ms"], ob)}
+    dom = max(phases, key=lambda k: phases[k][0])
+    dom_ms, dom_bytes = phases[dom]
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     traffic, src = pmc_traffic(workload, dom, n_records, n_batches)
-    bound = "hbm"
-    return {"bound": bound, "kernel": dom, "achieved": achieved, "peak": PEAK_GBPS, "unit": "GB/s",
+    step_gbps = (ib + ob) / (step_ms * 1e-3) / 1e9 if step_ms > 0 else 0.0
+    return {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": PEAK_GBPS, "unit": "GB/s",
             "frac": achieved / PEAK_GBPS, "traffic": traffic, "traffic_source": src,
-            "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": dom_ms}
+            "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": dom_ms,
+            "phases_ms": {k: v[0] for k, v in phases.items()},
+            "step": {"bytes": ib + ob, "ms": step_ms, "achieved": step_gbps, "frac": step_gbps / PEAK_GBPS,
+                     "note": "whole step: input + output bytes / ms_per_step (every kernel of the step)"}}
 
+
+def roofline_step(bytes_per_step, step_ms, kernel, kernel_ms, note):
+    """C5: the partitions' chains run concurrently, so per-chain kernel times
+    summed over chains are no launch duration.  Priced on the step: the bytes
+    every owned partition moves per step / ms_per_step; `kernel` names the
+    dominant launch and its own duration (HIP events around it)."""
+    achieved = bytes_per_step / (step_ms * 1e-3) / 1e9 if step_ms > 0 else 0.0
+    return {"bound": "hbm", "kernel": kernel, "achieved": achieved, "peak": PEAK_GBPS, "unit": "GB/s",
+            "frac": achieved / PEAK_GBPS, "traffic": None, "traffic_source": None,
+            "algorithmic_bytes_per_launch": bytes_per_step, "avg_launch_ms": step_ms,
+            "priced_on": "step", "dominant_kernel_ms": kernel_ms, "note": note}
+
+
+PHASES = ("eval_ms", "plan_ms", "text_ms", "write_ms", "crc_ms", "total_ms")
+PHASE_KERNEL = {"eval_ms": "k_eval", "plan_ms": "k_plan", "text_ms": "k_text", "write_ms": "k_write",
+                "crc_ms": "k_crc", "total_ms": "step"}
 
 _SLICES = {}
 
@@ -304,7 +354,8 @@ def run_filter(ctx, name, nrec, cpu):
     for _ in range(a.warmup):
         chain.process_slice(rs, metrics=metrics, download=False)
     ctx.barrier()
-    acc = {"eval_ms": 0.0, "plan_ms": 0.0, "write_ms": 0.0, "crc_ms": 0.0, "total_ms": 0.0}
+    acc = {"eval_ms": 0.0, "plan_ms": 0.0, "text_ms": 0.0, "write_ms": 0.0, "crc_ms": 0.0, "total_ms": 0.0}
+    ro0 = metrics.records_out()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         chain.process_slice(rs, metrics=metrics, download=False)  # synchronizes its stream at the end
@@ -315,6 +366,7 @@ def run_filter(ctx, name, nrec, cpu):
     elapsed = ctx.max_over_ranks(time.perf_counter() - t0)
     t = chain.last_timings()
     per = {k: acc[k] / a.steps for k in acc}
+    rec_out = (metrics.records_out() - ro0) // a.steps
     recs = rs.n_records
     res = {"metric": "records/s", "value": recs * ctx.world * a.steps / elapsed, "unit": "records/s",
            "ms_per_step": elapsed / a.steps * 1e3, "scaling": "weak", "dtype": "u8",
@@ -323,7 +375,8 @@ def run_filter(ctx, name, nrec, cpu):
                       "output_bytes_per_gpu": t["out_bytes"], "chain": [m[0] for m in modules]},
            "gbps_input": t["in_bytes"] * ctx.world * a.steps / elapsed / 1e9,
            "gbps_pipeline": (t["in_bytes"] + t["out_bytes"]) / (per["total_ms"] * 1e-3) / 1e9,
-           "roofline": roofline(per, t, name, recs, rs.n_batches),
+           "records_out_per_gpu": rec_out,
+           "roofline": roofline(per, t, name, recs, rs.n_batches, rec_out, elapsed / a.steps * 1e3),
            "kernel_ms": per, "setup_s": {"generate": gen_s, "ingest_h2d": ingest_s},
            "crc_verify": {"ms": vms, "gbps": t["in_bytes"] / (vms * 1e-3) / 1e9 if vms > 0 else None,
                           "mismatches": vbad,
@@ -422,25 +475,30 @@ def run_c5(ctx, cpu):
         chains[p] = b.initialize(engine)
         rsl[p] = ResidentSlice(engine, slices[p])
     state = PartitionState(engine, P)
-    kms = {"eval_ms": 0.0, "write_ms": 0.0, "crc_ms": 0.0, "total_ms": 0.0}
+    kms = {k: 0.0 for k in PHASES}
+    kmax = {k: 0.0 for k in PHASES}
     out_bytes = [0]
     clist, slist = [chains[p] for p in owned], [rsl[p] for p in owned]
 
     def step():
         process_slices(clist, slist)  # every owned partition's chain in one call, concurrently
+        smax = {k: 0.0 for k in PHASES}
         for p in owned:
             state.collect(p, chains[p])
             t = chains[p].last_timings()
             for k in kms:
                 kms[k] += t[k]
+                smax[k] = max(smax[k], t[k])
             out_bytes[0] += t["out_bytes"]
+        for k in kmax:
+            kmax[k] += smax[k]
         state.allreduce()  # RCCL sum over xGMI: the topic-wide per-partition table on every rank
 
     for _ in range(a.warmup):
         step()
     ctx.barrier()
     for k in kms:
-        kms[k] = 0.0
+        kms[k] = kmax[k] = 0.0
     out_bytes[0] = 0
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -461,6 +519,7 @@ def run_c5(ctx, cpu):
         total_recs, bad = int(tt[0].item()), int(tt[1].item())
     assert bad == 0, f"c5-agg-sum: {bad} partition accumulators differ from the generator's sums"
     per = {k: v / a.steps for k, v in kms.items()}
+    pmax = {k: v / a.steps for k, v in kmax.items()}
     res = {"metric": "records/s", "value": total_recs * a.steps / elapsed, "unit": "records/s",
            "ms_per_step": elapsed / a.steps * 1e3, "scaling": "strong", "dtype": "i32",
            "config": {"workload": "c5-agg-sum", "description": C5["description"], "partitions": P,
@@ -469,15 +528,19 @@ def run_c5(ctx, cpu):
                       "host_call": "fsg_chain_group_process_slices (one call, every owned chain)",
                       "parallelism": f"partitions sharded p -> rank p mod {ctx.world}"},
            "kernel_ms_sum_over_partitions": per,
+           "kernel_ms_max_over_partitions": pmax,
            "gbps_input_per_gpu": in_bytes * a.steps / elapsed / 1e9,
            "state_checksum": sum(vec) & 0xFFFFFFFF,
            "state_check": f"ok: all {P} partition accumulators == (warmup + steps) x the generator's sum of the "
                           f"partition's integers (wrapping i32), merged by RCCL all-reduce",
            "setup_s": {"generate": gen_s}}
-    # roofline over the partitions' launches: per step, the slices' bytes over
-    # the summed eval time of the 64 chains (each chain's launch reads its slice once)
-    res["roofline"] = roofline(per, {"in_bytes": in_bytes, "out_bytes": out_bytes[0] / a.steps}, "c5-agg-sum",
-                               total_recs, 0)
+    # step-level roofline: every owned slice read once, every output batch written
+    # once, 4 B of state per partition; the dominant phase by its longest chain
+    dom = max(pmax, key=lambda k: pmax[k] if k != "total_ms" else -1.0)
+    res["roofline"] = roofline_step(in_bytes + out_bytes[0] / a.steps + 4 * len(owned), res["ms_per_step"],
+                                    PHASE_KERNEL[dom], pmax[dom],
+                                    "c5-agg-sum: input + output bytes of all owned partitions per step / ms_per_step; "
+                                    "the partitions' chains run concurrently (one group call)")
     res["cpu_baseline"] = cpu.get("c5-agg-sum")
     return res
 
@@ -485,11 +548,13 @@ def run_c5(ctx, cpu):
 def run_c5k(ctx, cpu):
     """C5 keyed: 64 partitions of {"repo-NNNN": n} records (key = repo name,
     SipHash-routed), aggregate-json per partition (every output record = the
-    partition's whole map), partitions sharded p -> rank p mod N.  Per step:
-    every owned partition's slice through its chain, then the topic-wide
-    per-key totals: each chain's state as (FNV-1a 64 key fingerprint, u32)
-    pairs written straight into HBM (fsg_chain_keyed_state), one all_gather
-    over RCCL, and a per-key sum on the GPU (partitions.merge_keyed_torch)."""
+    partition's whole map, keys in the guest HashMap's order), partitions
+    sharded p -> rank p mod N.  Per step: every owned partition's slice through
+    its chain (one group call: the order walks of all chains in one launch,
+    k_aggj_order_group), then the topic-wide per-key totals through the C ABI
+    (fsg_keyed_collect per chain: exact key bytes into the rank's table;
+    fsg_keyed_allreduce: RCCL all-gather of the key lists, the union
+    dictionary, one dense u32 all-reduce)."""
     import torch
     from fluvio_amd import partitions as PT
     from fluvio_amd import synth
@@ -515,7 +580,8 @@ def run_c5k(ctx, cpu):
         rsl[p] = ResidentSlice(engine, raw[p])
     del raw
     keyed = KeyedState(engine)
-    kms = {"eval_ms": 0.0, "plan_ms": 0.0, "write_ms": 0.0, "crc_ms": 0.0, "total_ms": 0.0}
+    kms = {k: 0.0 for k in PHASES + ("order_ms",)}
+    kmax = {k: 0.0 for k in PHASES + ("order_ms",)}
     out_bytes = [0]
     clist, slist = [chains[p] for p in owned], [rsl[p] for p in owned]
 
@@ -523,11 +589,15 @@ def run_c5k(ctx, cpu):
         # every owned partition's chain in one call (fsg_chain_group_process_slices:
         # the chains run concurrently, their aggregate-json order walks as one launch)
         process_slices(clist, slist)
+        smax = {k: 0.0 for k in kmax}
         for c in clist:
             t = c.last_timings()
             for k in kms:
                 kms[k] += t[k]
+                smax[k] = max(smax[k], t[k])
             out_bytes[0] += t["out_bytes"]
+        for k in kmax:
+            kmax[k] += smax[k]
         # the topic-wide totals: every owned partition's map (exact keys, in HBM)
         # into the rank's table, then the union dictionary + dense u32 all-reduce over RCCL
         keyed.reset()
@@ -539,7 +609,7 @@ def run_c5k(ctx, cpu):
         step()
     ctx.barrier()
     for k in kms:
-        kms[k] = 0.0
+        kms[k] = kmax[k] = 0.0
     out_bytes[0] = 0
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -561,6 +631,7 @@ def run_c5k(ctx, cpu):
     assert bad == 0 and len(merged) == nkeys_owned, \
         f"c5-keyed-agg: {bad} keyed totals differ from the generator's sums ({len(merged)} vs {nkeys_owned} keys)"
     per = {k: v / a.steps for k, v in kms.items()}
+    pmax = {k: v / a.steps for k, v in kmax.items()}
     res = {"metric": "records/s", "value": total_recs * a.steps / elapsed, "unit": "records/s",
            "ms_per_step": elapsed / a.steps * 1e3, "scaling": "strong", "dtype": "u32",
            "config": {"workload": "c5-keyed-agg", "description": C5K["description"], "partitions": P,
@@ -570,14 +641,20 @@ def run_c5k(ctx, cpu):
                       "chain": [m[0] for m in C5K["modules"]],
                       "parallelism": f"partitions sharded p -> rank p mod {ctx.world}"},
            "kernel_ms_sum_over_partitions": per,
+           "kernel_ms_max_over_partitions": pmax,
            "gbps_input_per_gpu": in_bytes * a.steps / elapsed / 1e9,
            "gbps_output_per_gpu": out_bytes[0] / elapsed / 1e9,
            "merged_keys": len(merged), "state_checksum": sum(merged.values()) & 0xFFFFFFFF,
            "state_check": f"ok: all {len(merged)} topic keys == (warmup + steps) x the generator's per-key sums "
                           f"(u32 wrapping), merged through fsg_keyed_* (exact keys, RCCL)",
            "setup_s": {"generate": gen_s}}
-    res["roofline"] = roofline(per, {"in_bytes": in_bytes, "out_bytes": out_bytes[0] / a.steps}, "c5-keyed-agg",
-                               total_recs, 0)
+    # step-level roofline; the dominant launch is the one order walk of all the
+    # rank's chains (k_aggj_order_group), timed with HIP events around it
+    res["roofline"] = roofline_step(in_bytes + out_bytes[0] / a.steps, res["ms_per_step"], "k_aggj_order_group",
+                                    pmax["order_ms"],
+                                    "c5-keyed-agg: input + output bytes of all owned partitions per step / "
+                                    "ms_per_step; the serial per-partition order walk (one workgroup per chain, "
+                                    "all chains in one launch) is latency-bound, not HBM-bound")
     res["cpu_baseline"] = cpu.get("c5-keyed-agg")
     del rsl, chains
     return res
@@ -627,9 +704,39 @@ def run_workload(ctx, w, nrec, cpu):
     return run_filter(ctx, w, nrec, cpu)
 
 
+def dry_run(ctx):
+    """--dry-run: the multi-rank plumbing of the real line without any GPU work
+    (each rank's "step" is a short sleep): barrier, timed steps, max over ranks,
+    rank 0 prints the line.  The CPU tests run it under --gpus 2."""
+    a = ctx.a
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        time.sleep(0.001 * (1 + ctx.rank))
+    ctx.barrier()
+    elapsed = ctx.max_over_ranks(time.perf_counter() - t0)
+    if ctx.rank == 0:
+        print(json.dumps({"metric": "records/sec + achieved HBM GB/s for SmartModule filter chain, 1/2/4/8 MI355X",
+                          "value": None, "unit": "records/s", "n_gpus": ctx.world, "steps": a.steps,
+                          "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "none (dry run)",
+                          "dry_run": True, "ranks": ctx.world,
+                          "config": {"workload": a.workload, "parallelism": f"partitions sharded over {ctx.world} GPU(s)"}}))
+    if ctx.dist is not None:
+        ctx.dist.destroy_process_group()
+
+
 def main():
     a = parse()
+    rc = launch_ranks(a)
+    if rc is not None:
+        sys.exit(rc)
     ctx = Ctx(a)
+    if a.dry_run:
+        dry_run(ctx)
+        return
+    assert ctx.world == a.gpus or (a.gpus == 1 and not any(x.startswith("--gpus") for x in sys.argv[1:])), \
+        f"--gpus {a.gpus} but {ctx.world} rank(s)"
     head = a.workload
     extra = [] if a.only else [w for w in EXTRA if w != head]
     cpu = cpu_baselines_first(ctx, [head] + extra)

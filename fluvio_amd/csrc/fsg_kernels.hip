@@ -3699,6 +3699,7 @@ __global__ __launch_bounds__(256) void k_frame_next(FrameArgs a) {
     a.nrec[c] = nrec;
     a.jmp[c] = nx < FN_END ? nx : (uint32_t)a.ncand;  // ends -> sink
     a.mark[c] = c == 0 && p == 0 ? 1u : 0u;
+    if (c == 0 && p != 0) atomicMax(&a.scal[0], 1ull);  // position 0 has no magic 2: the host walk decides
   }
 }
 __global__ __launch_bounds__(256) void k_frame_double(const uint32_t* src, uint32_t* dst, uint64_t n) {

@@ -18,6 +18,7 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -465,6 +466,16 @@ struct fsg_slice {
   // framing / decompression scratch, grown and kept across uploads into this
   // slice (hipFree synchronises the whole device)
   DevBuf fr[12], dec[8];
+  // fsg_slice_verify_crc: its stream, events and result word, kept across calls
+  // (a per-call hipMalloc / hipFree of the word synchronised the device)
+  mutable DevBuf vbad;
+  mutable hipStream_t vst = nullptr;
+  mutable hipEvent_t vev[2] = {};
+  ~fsg_slice() {
+    for (auto& e : vev)
+      if (e) (void)hipEventDestroy(e);
+    if (vst) (void)hipStreamDestroy(vst);
+  }
 };
 
 constexpr size_t kPinPlan = 256;           // pinned block: Plan, then the small output
@@ -488,10 +499,14 @@ struct AjGroup {
   int device = 0;
   hipStream_t st = nullptr;
   hipEvent_t done = nullptr;
+  hipEvent_t t0 = nullptr, t1 = nullptr;  // the walk's own duration (timed chains)
+  bool timed = false;
   void* dlist = nullptr;
   ~AjGroup() {
     if (dlist) (void)hipFree(dlist);
     if (done) (void)hipEventDestroy(done);
+    if (t0) (void)hipEventDestroy(t0);
+    if (t1) (void)hipEventDestroy(t1);
     for (auto e : ready) (void)hipEventDestroy(e);
     if (st) (void)hipStreamDestroy(st);
   }
@@ -579,10 +594,13 @@ struct fsg_chain {
   PinBuf hstage;
   hipEvent_t dl_ev[2] = {};
   hipEvent_t ev[6] = {};
+  hipEvent_t ev_order[2] = {};  // around a solo aggregate-json order walk
   fsg_timings last{};
   size_t out_len = 0;
   ~fsg_chain() {
     for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    for (auto& e : ev_order)
       if (e) (void)hipEventDestroy(e);
     for (auto& e : dl_ev)
       if (e) (void)hipEventDestroy(e);
@@ -911,6 +929,8 @@ extern "C" int fsg_chain_builder_initialize(fsg_chain_builder* b, fsg_engine* e,
   }
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   for (auto& ev : c->ev) HIPCHK(hipEventCreate(&ev));
+  if (c->hdesc.flags & CF_AGG_JSON)
+    for (auto& ev : c->ev_order) HIPCHK(hipEventCreate(&ev));
   HIPCHK(c->d_desc.ensure(sizeof(ChainDesc)));
   HIPCHK(hipMemcpy(c->d_desc.p, &c->hdesc, sizeof(ChainDesc), hipMemcpyHostToDevice));
   if (c->hblob.empty()) c->hblob.resize(16, 0);
@@ -1046,13 +1066,8 @@ int frame_on_device(fsg_slice* sl, hipStream_t st, int* fallback) {
   a.bpos = sl->bpos.as<uint64_t>();
   a.rbase = sl->rbase.as<uint64_t>();
   launch_frame_compact(a, nchunks, st);
-  uint64_t first = 1;
-  HIPCHK(hipMemcpyAsync(&first, cand.p, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  if (first != 0) {  // position 0 has no magic 2: the host walk decides
-    *fallback = 1;
-    return FSG_OK;
-  }
+  // position 0 without magic 2 (the host walk decides) is flagged in scal[0]
+  // by k_frame_next, read with the chain's results: one wait, not two
   launch_frame_chain(a, levels, tsum.as<uint64_t>(), st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(sc, scal.p, 64, hipMemcpyDeviceToHost, st));
@@ -1288,6 +1303,9 @@ extern "C" int fsg_slice_device_framed(const fsg_slice* s) { return s->device_fr
 extern "C" int fsg_slice_reframe(fsg_slice* s) {
   HIPCHK(hipSetDevice(s->eng->device));
   if (s->decompressed) return fail(FSG_E_UNSUPPORTED, "the slice was decompressed at ingest: its stored bytes are gone");
+  // a host-framed slice stays as it is: device framing would reset its batch
+  // table before finding that it needs the host walk again
+  if (!s->device_framed) return fail(FSG_E_UNSUPPORTED, "this slice needs the host framing walk (no magic-2 framing)");
   int fallback = 0;
   int rc = frame_on_device(s, 0, &fallback);
   if (rc) return rc;
@@ -1306,27 +1324,22 @@ extern "C" int fsg_slice_verify_crc(const fsg_slice* s, uint64_t* n_bad, int64_t
     return FSG_OK;
   }
   HIPCHK(hipSetDevice(s->eng->device));
-  hipStream_t st = nullptr;
-  HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  DevBuf bad;
-  HIPCHK(bad.ensure(16));
-  const unsigned long long init[2] = {0, ~0ull};
-  HIPCHK(hipMemcpyAsync(bad.p, init, sizeof init, hipMemcpyHostToDevice, st));
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  HIPCHK(hipEventCreate(&e0));
-  HIPCHK(hipEventCreate(&e1));
-  HIPCHK(hipEventRecord(e0, st));
-  launch_verify_crc((const uint8_t*)s->data.p, s->bpos.as<uint64_t>(), s->nb, bad.as<unsigned long long>(), nullptr, st);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(e1, st));
+  if (!s->vst) HIPCHK(hipStreamCreateWithFlags(&s->vst, hipStreamNonBlocking));
+  for (auto& e : s->vev)
+    if (!e) HIPCHK(hipEventCreate(&e));
+  hipStream_t st = s->vst;
+  HIPCHK(s->vbad.ensure(16));
   unsigned long long r[2] = {0, 0};
-  HIPCHK(hipMemcpyAsync(r, bad.p, sizeof r, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemsetAsync(s->vbad.p, 0, 8, st));  // [0] mismatches, [1] first mismatching batch (min)
+  HIPCHK(hipMemsetAsync((uint8_t*)s->vbad.p + 8, 0xFF, 8, st));
+  HIPCHK(hipEventRecord(s->vev[0], st));
+  launch_verify_crc((const uint8_t*)s->data.p, s->bpos.as<uint64_t>(), s->nb, s->vbad.as<unsigned long long>(), nullptr, st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(s->vev[1], st));
+  HIPCHK(hipMemcpyAsync(r, s->vbad.p, 16, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   float t = 0;
-  HIPCHK(hipEventElapsedTime(&t, e0, e1));
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  (void)hipStreamDestroy(st);
+  HIPCHK(hipEventElapsedTime(&t, s->vev[0], s->vev[1]));
   if (n_bad) *n_bad = r[0];
   if (first_bad) *first_bad = r[0] ? (int64_t)r[1] : -1;
   if (ms) *ms = t;
@@ -1881,8 +1894,14 @@ int group_launch(AjGroup* g) {
     for (auto e : g->ready) HIPCHK(hipStreamWaitEvent(g->st, e, 0));
     HIPCHK(hipMalloc(&g->dlist, n * sizeof(AggjArgs)));
     HIPCHK(hipMemcpyAsync(g->dlist, g->jobs.data(), n * sizeof(AggjArgs), hipMemcpyHostToDevice, g->st));
+    if (g->timed) {
+      if (!g->t0) HIPCHK(hipEventCreate(&g->t0));
+      if (!g->t1) HIPCHK(hipEventCreate(&g->t1));
+      HIPCHK(hipEventRecord(g->t0, g->st));
+    }
     launch_aggj_order_group((const AggjArgs*)g->dlist, (uint32_t)n, g->st);
     HIPCHK(hipGetLastError());
+    if (g->timed) HIPCHK(hipEventRecord(g->t1, g->st));
   }
   HIPCHK(hipEventRecord(g->done, g->st));
   return FSG_OK;
@@ -1892,15 +1911,25 @@ int group_launch(AjGroup* g) {
 int group_arrive(fsg_chain* c, const AggjArgs* job, hipStream_t st) {
   AjGroup* g = c->group;
   if (!g || c->group_arrived) return FSG_OK;
-  c->group_arrived = true;
   std::unique_lock<std::mutex> lk(g->mu);
+  // the arrival always counts, even when queueing this chain's walk fails:
+  // every other walker waits for the count to reach `expected`
+  int rc = FSG_OK;
   if (job) {
     hipEvent_t e = nullptr;
-    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIPCHK(hipEventRecord(e, st));
-    g->jobs.push_back(*job);
-    g->ready.push_back(e);
+    hipError_t he = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    if (he == hipSuccess) he = hipEventRecord(e, st);
+    if (he != hipSuccess) {
+      if (e) (void)hipEventDestroy(e);
+      rc = fail(FSG_E_DEVICE, std::string("group_arrive: ") + hipGetErrorString(he));
+      job = nullptr;
+    } else {
+      if (c->timed) g->timed = true;
+      g->jobs.push_back(*job);
+      g->ready.push_back(e);
+    }
   }
+  c->group_arrived = true;
   if (++g->arrived == g->expected) {
     g->rc = group_launch(g);
     g->launched = true;
@@ -1908,6 +1937,7 @@ int group_arrive(fsg_chain* c, const AggjArgs* job, hipStream_t st) {
   } else if (job) {
     g->cv.wait(lk, [&] { return g->launched; });
   }
+  if (rc) return rc;
   if (job) {
     if (g->rc) return g->rc;
     HIPCHK(hipStreamWaitEvent(st, g->done, 0));
@@ -1930,8 +1960,9 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   const bool has_aggj = (c->hdesc.flags & CF_AGG_JSON) != 0;
   const size_t elem_cap = (has_array || has_aggj) ? (s->len / 2 + 2) : 0;  // ElemRec slots (fsg_device.h)
   const size_t need = (size_t)std::max<uint32_t>(nb, 1) * (sizeof(BatchStat) + 3 * sizeof(ScanRow)) +
-                      (size_t)std::max<uint64_t>(s->nrec, 1) * sizeof(KeptRec) + elem_cap * sizeof(ElemRec) +
-                      (has_array ? (size_t)std::max<uint32_t>(nb, 1) * (sizeof(ArrBatch) + kArrBmBatch * 4) : 0);
+                      (size_t)std::max<uint64_t>(s->nrec, 1) * sizeof(KeptRec) + elem_cap * sizeof(ElemRec);
+  // (the lean array path's per-batch element bitmaps are device scratch of
+  // this engine, not guest memory: sized below only when that path is taken)
   if (need > c->limit) {
     char b[160];
     snprintf(b, sizeof b, "Requested memory %zub exceeded max allowed %zub", need, c->limit);
@@ -1951,10 +1982,6 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   HIPCHK(c->mins.ensure(sizeof(Mins)));
   HIPCHK(c->plan.ensure(sizeof(Plan)));
   if (has_array || has_aggj) HIPCHK(c->elem.ensure(elem_cap * sizeof(ElemRec)));
-  if (has_array) {  // the lean array path's element statistics (fsg_array.hip)
-    HIPCHK(c->arr_b.ensure(std::max<uint32_t>(nb, 1) * sizeof(ArrBatch)));
-    HIPCHK(c->arr_bm.ensure(std::max<uint32_t>(nb, 1) * (size_t)kArrBmBatch * 4));
-  }
   const bool has_agg = c->agg_stage >= 0;
   const bool has_cat = has_agg && (c->hdesc.flags & CF_AGG_CAT);
   const int64_t acc0 = has_agg && !has_cat && !has_aggj ? acc_value(c->acc) : 0;
@@ -1974,8 +2001,8 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   ea.mins = c->mins.as<Mins>();
   ea.list = c->defer.as<uint32_t>();
   ea.elem = (has_array || has_aggj) ? c->elem.as<ElemRec>() : nullptr;
-  ea.arr_b = has_array ? c->arr_b.as<ArrBatch>() : nullptr;
-  ea.arr_bm = has_array ? c->arr_bm.as<uint32_t>() : nullptr;
+  ea.arr_b = nullptr;
+  ea.arr_bm = nullptr;
   ea.nrec = s->nrec;
   uint32_t ops = 0;
   bool lean_stages = true;  // every stage has a lean form
@@ -2006,7 +2033,16 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   ea.rstart = c->rstart.as<uint16_t>();
   ea.rend = c->rend.as<uint16_t>();
   // array_map alone: the lean array kernel, unsupported shapes deferred to k_eval
-  const bool arr = !lean && nb > 1 && !s->has_pass && array_lean_eligible(c->hdesc, ops);
+  bool arr = !lean && nb > 1 && !s->has_pass && array_lean_eligible(c->hdesc, ops);
+  if (arr) {  // the lean array path's element statistics (fsg_array.hip); no room: the exact kernel
+    arr = c->arr_b.ensure((size_t)nb * sizeof(ArrBatch)) == hipSuccess &&
+          c->arr_bm.ensure((size_t)nb * kArrBmBatch * 4) == hipSuccess;
+    (void)hipGetLastError();
+    if (arr) {
+      ea.arr_b = c->arr_b.as<ArrBatch>();
+      ea.arr_bm = c->arr_bm.as<uint32_t>();
+    }
+  }
   if (lean || arr) HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
   launch_eval(ea, ops, lean ? EVAL_LEAN : arr ? EVAL_ARRAY : EVAL_EXACT, st);
   HIPCHK(hipGetLastError());
@@ -2313,7 +2349,9 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
       int rc = group_order(c, &aj, st);
       if (rc) return rc;
     } else {
+      if (c->timed) HIPCHK(hipEventRecord(c->ev_order[0], st));
       launch_aggj_order(aj, st);
+      if (c->timed) HIPCHK(hipEventRecord(c->ev_order[1], st));
     }
     aj.cat = c->cat.as<uint8_t>();
     aj.write = 1;
@@ -2395,7 +2433,16 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   c->last.plan_ms = t[1];
   c->last.write_ms = t[3];
   c->last.crc_ms = t[4];
+  c->last.text_ms = t[2];
   c->last.total_ms = t[0] + t[1] + t[2] + t[3] + t[4];
+  c->last.order_ms = 0;
+  if (c->timed && has_aggj && aj.n_rec) {  // the order walk alone (the group's launch for a group call)
+    AjGroup* g = c->group;
+    if (g && g->t0 && g->t1)
+      HIPCHK(hipEventElapsedTime(&c->last.order_ms, g->t0, g->t1));
+    else if (!g)
+      HIPCHK(hipEventElapsedTime(&c->last.order_ms, c->ev_order[0], c->ev_order[1]));
+  }
   c->last.in_bytes = s->header_bytes;
   c->last.out_bytes = out_len;
   c->last.n_batches = nb;
@@ -2723,11 +2770,15 @@ extern "C" int fsg_chain_group_process_slices(fsg_chain* const* chains, const fs
     (walks ? walkers : others).push_back(i);
   }
   std::vector<std::string> errs(n);
+  std::vector<std::array<uint64_t, 3>> smem(n);  // g_store_mem is thread-local too
   auto one = [&](size_t i) {
     fsg_chain* c = chains[i];
     if (outs) outs[i] = nullptr;
     rcs[i] = fsg_chain_process_slice(c, slices[i], max_bytes, metrics ? metrics + i : nullptr, outs ? outs + i : nullptr);
-    if (rcs[i]) errs[i] = g_err;
+    if (rcs[i]) {
+      errs[i] = g_err;
+      smem[i] = {g_store_mem[0], g_store_mem[1], g_store_mem[2]};
+    }
     (void)group_arrive(c, nullptr, nullptr);  // a chain that failed before its walk
   };
   // a walker blocks at the rendezvous until every walker has arrived: one
@@ -2749,6 +2800,7 @@ extern "C" int fsg_chain_group_process_slices(fsg_chain* const* chains, const fs
     if (rcs[i] && rc == FSG_OK) {
       rc = rcs[i];
       g_err = errs[i];
+      for (int k = 0; k < 3; k++) g_store_mem[k] = smem[i][k];
     }
   }
   HIPCHK(hipSetDevice(g.device));

@@ -1397,6 +1397,60 @@ def test_reframe_resident_slice(engine):
     assert (rs.n_batches, rs.n_records) == (nb, nr)
 
 
+
+def test_reframe_host_framed_slice_is_unsupported(engine):
+    """fsg_slice_reframe on a slice the host walk framed (no magic 2 at position
+    0): FSG_E_UNSUPPORTED before anything is reset, so the slice keeps its
+    batches and still processes exactly like the oracle."""
+    nomagic = bytearray(synth.make_slice(2, 1500))
+    nomagic[16] = 1
+    nomagic = bytes(nomagic)
+    rs = ResidentSlice(engine, nomagic)
+    assert not rs.device_framed
+    with pytest.raises(Unsupported):
+        rs.reframe()
+    g = gpu_chain(engine, CHAINS["filter_init_timeout"])
+    o = orc_chain(CHAINS["filter_init_timeout"]).process_batch(nomagic)
+    out = g.process_slice(rs)
+    assert out.raw == o["bytes"] and out.n_records == o["n_records"] > 0
+
+
+def test_array_map_many_tiny_batches_near_store_limit(engine):
+    """The lean array path's per-batch element bitmaps (~4.4 KB a batch) are this
+    engine's scratch, not guest memory: 3,000 one-record batches run under a
+    4 MB store limit, as the reference (limit per guest call = per batch)
+    runs them."""
+    out, base = b"", 0
+    for i in range(3000):
+        b = P.Batch(base_offset=base)
+        b.add_record(P.Record.new(b"[1,2]" if i % 3 else b'["a",7,null]'))
+        out += b.encode()
+        base += 1
+    g = gpu_chain(engine, CHAINS["array_map"], limit=4 << 20)
+    o = orc_chain(CHAINS["array_map"]).process_batch(out)
+    r = g.process_batch(out)
+    assert r.raw == o["bytes"] and r.n_records == o["n_records"]
+    assert g.last_timings()["eval_path"] == 3  # FSG_EVAL_ARRAY
+
+
+def test_group_order_walk_timing(engine):
+    """fsg_timings.order_ms: the aggregate-json order walk's own duration: the
+    group's one launch (the same for every chain of a group call), a chain's
+    own launch outside a group."""
+    from fluvio_amd.smartengine import process_slices
+    slices = synth.make_keyed_slices(4, 800, 64)
+    chains = [gpu_chain(engine, [("aggregate-json", {}, None)]) for _ in range(4)]
+    rs = [ResidentSlice(engine, slices[p]) for p in range(4)]
+    process_slices(chains, rs)
+    ts = [c.last_timings() for c in chains]
+    assert all(t["order_ms"] > 0 for t in ts), ts
+    assert len({t["order_ms"] for t in ts}) == 1
+    chains[0].process_slice(rs[0])
+    assert chains[0].last_timings()["order_ms"] > 0
+    g = gpu_chain(engine, CHAINS["filter_init_timeout"])
+    g.process_batch(synth.make_slice(2, 300))
+    assert g.last_timings()["order_ms"] == 0
+
 # ---------------------------------------------------------------------------
 # compressed record sections decompressed on the GPU at ingest (SURVEY §8 f2)
 # ---------------------------------------------------------------------------
