@@ -115,7 +115,7 @@ def launch_ranks(a):
     return subprocess.call(cmd)
 
 
-KERNEL_SOURCES = ("fsg_kernels.hip", "fsg_array.hip", "fsg_device.h", "fsg_codec_dev.h", "fsg_json_dev.h",
+KERNEL_SOURCES = ("fsg_kernels.hip", "fsg_lean.hip", "fsg_array.hip", "fsg_device.h", "fsg_dev_util.h", "fsg_codec_dev.h", "fsg_json_dev.h",
                   "fsg_json_dfa.h", "fsg_launch.h")
 
 

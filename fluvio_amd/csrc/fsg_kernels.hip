@@ -22,6 +22,7 @@
 #include <type_traits>
 
 #include "fsg_device.h"
+#include "fsg_dev_util.h"
 #include "fsg_codec_dev.h"
 #include "fsg_json_dev.h"
 #include "fsg_json_dfa.h"
@@ -31,12 +32,6 @@ namespace fsg {
 // ---------------------------------------------------------------------------
 // small device helpers
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t rd_be(const uint8_t* p, int n) {
-  uint64_t v = 0;
-  for (int i = 0; i < n; i++) v = (v << 8) | p[i];
-  return v;
-}
-
 __device__ __forceinline__ uint32_t dec_len_i32(int32_t v) {
   uint32_t u = v < 0 ? (uint32_t)(-(int64_t)v) : (uint32_t)v;
   uint32_t n = 1;
@@ -58,33 +53,6 @@ __device__ __forceinline__ uint32_t fmt_i32(int32_t v, uint8_t* out) {
   if (v < 0) out[k++] = '-';
   while (n) out[k++] = t[--n];
   return k;
-}
-
-__device__ __forceinline__ uint8_t up(uint8_t c) { return (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c; }
-
-// wave helpers (64 lanes)
-__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63; }
-__device__ __forceinline__ uint32_t lanemask_lt() {
-  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-}
-__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
-template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
-  for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o, 64);
-  return v;
-}
-template <typename T>
-__device__ __forceinline__ T wave_incl_scan(T v) {
-  const int l = lane_id();
-  for (int o = 1; o < 64; o <<= 1) {
-    T t = __shfl_up(v, o, 64);
-    if (l >= o) v += t;
-  }
-  return v;
 }
 
 // ---------------------------------------------------------------------------
@@ -253,24 +221,6 @@ struct __attribute__((aligned(16))) WaveLds {
   uint32_t next_cursor_lo, next_cursor_hi;
   BatchStat bs;             // the batch's result, assembled by lane 0 (keeps long-lived state out of VGPRs)
 };
-
-// decode a varint from window bytes [q, lim); lim_sec tells whether running
-// out of window bytes means "incomplete" (more section bytes) or EOF
-template <typename P>
-__device__ __forceinline__ int wvarint(P w, uint32_t& q, uint32_t wlim, int64_t* out) {
-  uint64_t num = 0;
-  uint32_t shift = 0;
-  for (;;) {
-    if (q >= wlim) return -1;
-    uint8_t b = w[q++];
-    num |= ((uint64_t)(b & 0x7f)) << (shift & 63);
-    shift += 7;
-    if (!(b & 0x80)) break;
-  }
-  int64_t sn = (int64_t)num;
-  *out = (int64_t)((uint64_t)(sn >> 1) ^ (uint64_t)(-(sn & 1)));
-  return 0;
-}
 
 // Serial exact walk of records (lane 0).  Window bytes w[0..wlen) map to
 // absolute offsets wbase..; the record section ends at absolute sec_end.
@@ -488,20 +438,6 @@ __device__ __forceinline__ int find_rec(const WaveLds& L, int nr, uint32_t p) {
   return r;
 }
 
-// exact zero-byte mask: 0x80 in each byte of x that is zero
-__device__ __forceinline__ uint32_t zbytes(uint32_t x) {
-  return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
-}
-
-// SWAR helpers (4 bytes per u32)
-__device__ __forceinline__ uint32_t swar_upper(uint32_t x) {
-  // make_ascii_uppercase on each byte: 'a'..'z' -> 'A'..'Z', other bytes unchanged
-  const uint32_t y = x & 0x7F7F7F7Fu;
-  const uint32_t ge_a = y + 0x1F1F1F1Fu;   // high bit set where y >= 'a'
-  const uint32_t gt_z = y + 0x05050505u;   // high bit set where y >= '{'
-  const uint32_t lower = ge_a & ~gt_z & ~x & 0x80808080u;
-  return x - (lower >> 2);
-}
 // Data-parallel substring scan + non-ASCII marking over the values of the window.
 // Marks RF_MATCH on records whose (optionally uppercased) value contains needle.
 // Each lane takes 16-byte chunks (32 bytes from two ds_read_b128 of the LDS
@@ -1278,1172 +1214,6 @@ __global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : (kOps ==
     eval_batch<kOps>(a, L, a.list ? a.list[1 + i] : i);
     __syncthreads();  // the window is reused by the next batch
   }
-}
-
-// ---------------------------------------------------------------------------
-// k_eval_lean — persistent workgroups of two waves for chains of substring /
-// bounded-regex / filter_json filters and ASCII-uppercase maps (filter /
-// filter_init / filter_with_param / regex-filter / filter_json / map), the
-// C1/C2 hot path.  Each workgroup walks the batches b = blockIdx.x + i * grid;
-// while batch i is evaluated, batch i + 1 is already streaming into a second
-// LDS window (LDS-DMA), so HBM latency hides behind the evaluation.  A batch
-// takes this path only when its records can neither error nor decode
-// unusually: record section inside the 16 KiB window, 1..64 records that frame
-// exactly, every value ASCII (then from_utf8 cannot fail, filter.rs / derive
-// filter.rs:14-40).  Any other batch is appended to a.list and evaluated
-// exactly by k_eval (list mode).
-//   1. LDS-DMA the batch (header + record section) into the prefetch window,
-//      copied to the evaluation window when its turn comes
-//   2. lane 0 chases the record length varints; lane r parses record r exactly
-//      (Record::decode, data.rs:534-562) and checks it ends where its length says
-//   3. per contains stage, a data-parallel 4-gram scan over the value bytes
-//      (16 B + 4 B look-ahead per lane, ballot-filtered); 4-gram hits are parked
-//      in registers and resolved after the scan (record lookup + full needle);
-//      before the first scan the bytes between values are cleared, so the OR
-//      of every scanned word has a high bit iff some value is non-ASCII
-//   4. survivors -> compaction descriptors (ballot prefix), BatchStat
-// ---------------------------------------------------------------------------
-constexpr int kLeanWin = 16464;  // 57-B header + 16 KiB section + 15 B alignment, 16-B multiple
-constexpr int kLeanMaxR = 64;    // one record per lane of wave 0
-constexpr int kLeanThreads = 128;  // two waves per batch: DMA issue and the scan are split over both
-constexpr int kLeanNeedle = 128; // longest needle of the lean path (longer: exact kernel)
-constexpr int kLeanBlk = (kLeanWin + 80) / 64 + 1;  // 64-byte blocks of the window
-constexpr int kLeanNeedles = 256;  // resident needle bytes of all contains stages
-// a stage as the lean kernel needs it, copied to LDS once per workgroup (no
-// global reads while a prefetch is in flight)
-struct LeanStage {
-  uint8_t op;
-  uint8_t upper;       // in_type == VT_SRC_UPPER
-  uint8_t keep_match;
-  uint8_t pad;
-  uint32_t m;          // needle_len
-  uint32_t max_len, s_bot, s_mid, acc1, acc2;
-  uint32_t tt;         // blob offset of the regex rows (tt or tt_up by the input case)
-  uint32_t nd;         // blob offset of the needle
-  uint32_t nd_off;     // its offset in LeanLds::needles (when resident)
-};
-struct __attribute__((aligned(16))) LeanLds {
-  uint8_t win[kLeanWin + 48];  // + look-ahead of the last scan chunk
-  uint32_t r_vs[kLeanMaxR];
-  uint32_t r_ve[kLeanMaxR];
-  uint32_t match[2];
-  uint32_t nst;
-  uint32_t red[4];                  // workgroup OR (two alternating pairs)
-  uint32_t out_upper;
-  uint32_t tt_stage;                // stage whose rows sit in tt for the whole launch (0xFF: reloaded)
-  uint32_t nd_res;                  // 1: every needle sits in needles (LeanStage::nd_off)
-  LeanStage stg[kMaxStages];
-  uint64_t tt[256];                 // the scanned regex stage's byte rows (DfaDesc::tt)
-  uint8_t needle[kLeanNeedle + 8];  // the scanned stage's needle
-  uint8_t needles[kLeanNeedles];    // the contains stages' needles, back to back (when they fit)
-  alignas(4) uint8_t blk[kLeanBlk + 4];  // blk[j] = last record whose value starts <= 64 j (0xFF none)
-};
-// Workgroup barrier over LDS only: the LDS-DMA of the next batch stays in
-// flight (__syncthreads would also wait for every outstanding global access).
-__device__ __forceinline__ void lean_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-// workgroup OR of p over the two waves; `par` alternates the LDS pair so one
-// barrier suffices (a pair is rewritten two calls later, after a barrier that
-// every reader of it has passed)
-__device__ __forceinline__ bool lean_or(uint32_t* red, uint32_t& par, bool p) {
-  const uint64_t bl = __ballot(p);
-  uint32_t* r = red + 2 * par;
-  if ((threadIdx.x & 63u) == 0) r[threadIdx.x >> 6] = bl != 0 ? 1u : 0u;
-  lean_sync();
-  par ^= 1u;
-  return (r[0] | r[1]) != 0u;
-}
-// the filter_json variant: per-chunk quote / in-string masks, the token list,
-// the token DFA (fsg_json_dfa.h)
-// LDS of the JSON variant is sized for 5 workgroups per CU (<= 32 KiB): the
-// per-chunk words cover 16 KiB of values (a batch whose values span more takes
-// the exact kernel), the token list 1024 entries (a 16 KiB batch of ~1 KB log
-// records has ~600), and jn lives in the regex rows' space (LeanLds::tt; a
-// chain with regex and JSON stages reloads its rows per batch)
-constexpr int kJsonChunks = 1024;
-constexpr int kJsonEnt = 1024;  // token entries per batch (more: exact kernel)
-constexpr int kJsonSeg = kJsonChunks;  // object members per batch (LeanLdsJ::jn; more: exact kernel)
-__device__ constexpr JsonDfaTables g_json_tables{};
-static_assert(sizeof(LeanLds::tt) >= 2 * kJsonChunks, "jn overlays the regex rows");
-struct __attribute__((aligned(16))) LeanLdsJ : LeanLds {
-  uint32_t jm[kJsonChunks];      // pass 1: quote16 | special16 << 16; pass 2: in-string16 | hot16 << 16
-  // jn: non-space16 per chunk; then the object members: first token | record start << 15
-  __device__ __forceinline__ uint16_t* jn() { return reinterpret_cast<uint16_t*>(tt); }
-  uint32_t ent[kJsonEnt];        // pos | in-string bit << 15 | byte << 16 | token class << 24
-  uint32_t racc[kLeanMaxR];      // per record: level fields | message fields << 8 | bad << 16
-  uint32_t rlvl[kLeanMaxR];      // per record: bit (LogLevel index) of its level value
-  unsigned long long rbest[kLeanMaxR];  // projection: (member + 1) << 32 | value span of the last matching member
-  uint32_t nseg;
-  uint32_t wsum[4];              // cross-wave scan carries
-  uint8_t dfa[kJsonStates * kJsonCls2];
-  uint8_t bcls[256];
-};
-
-__device__ __forceinline__ uint32_t win5(const uint32_t (&w)[5], int j) {
-  const int k = j >> 2, al = j & 3;
-  return al ? __builtin_amdgcn_alignbyte(w[k + 1], w[k], (uint32_t)al) : w[k];
-}
-// 4 window bytes starting at any offset q (two aligned LDS dwords)
-__device__ __forceinline__ uint32_t lds_u32_at(const uint8_t* win, uint32_t q) {
-  const uint32_t* w = (const uint32_t*)(win + (q & ~3u));
-  return __builtin_amdgcn_alignbyte(w[1], w[0], q & 3u);
-}
-// record whose value region holds window offset p: the last r with r_vs[r] <= p
-__device__ __forceinline__ int lean_rec_of(const LeanLds& L, int nr, uint32_t p) {
-  int r = (int)(int8_t)L.blk[p >> 6];
-  while (r + 1 < nr && L.r_vs[r + 1] <= p) r++;
-  return r;
-}
-// m needle bytes at window offset p (4 bytes per compare)
-__device__ __forceinline__ bool lean_verify(const LeanLds& L, uint32_t p, uint32_t m, bool upper) {
-  for (uint32_t t = 0; t < m; t += 4) {
-    uint32_t x = lds_u32_at(L.win, p + t);
-    if (upper) x = swar_upper(x);
-    const uint32_t k = m - t >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (m - t))) - 1u);
-    if ((x ^ lds_u32_at(L.needle, t)) & k) return false;
-  }
-  return true;
-}
-// a 4-gram hit at window offset p: the whole needle inside one value -> record bit
-__device__ __forceinline__ void lean_resolve(const LeanLds& L, int nr, uint32_t p, uint32_t m, bool upper,
-                                             uint64_t& mask) {
-  const int r = lean_rec_of(L, nr, p);
-  if (r < 0 || p < L.r_vs[r] || p + m > L.r_ve[r]) return;
-  if (lean_verify(L, p, m, upper)) mask |= 1ull << r;
-}
-__device__ __forceinline__ void lean_push(const LeanLds& L, int nr, uint32_t p, uint32_t m, bool upper,
-                                          uint32_t& s0, uint32_t& s1, uint32_t& nh, uint64_t& mask) {
-  if (nh == 0) s0 = p;
-  else if (nh == 1) s0 |= p << 16;
-  else if (nh == 2) s1 = p;
-  else if (nh == 3) s1 |= p << 16;
-  else lean_resolve(L, nr, p, m, upper, mask);  // more than 4 hits in one lane: resolve now
-  nh++;
-}
-// One contains stage over the value bytes [lo, hi) of a window whose non-value
-// bytes in [lo & ~15, hi + 16) are blanks (clear_gaps).  Returns the OR of the scanned words
-// (bit 7 of a byte set <=> some value byte >= 0x80, i.e. a non-ASCII value).
-//   kMode 0 (m >= 7): every occurrence covers an aligned word, so each aligned
-//           word is compared with the needle's 4-grams at offsets 0..3 (one
-//           compare per byte, no byte shifting)
-//   kMode 1 (4 <= m <= 6): the 4-gram at each of the 16 positions (alignbyte)
-//   kMode 2 (1 <= m <= 3): masked compare of the first m bytes at each position
-//   kMode 3 (m == 0): OR only
-template <int kMode>
-__device__ __forceinline__ uint32_t lean_scan(LeanLds& L, int nr, uint32_t lo, uint32_t hi, const uint8_t* nd,
-                                              uint32_t m, bool upper) {
-  const uint32_t l = threadIdx.x;
-  uint32_t rot[4] = {0, 0, 0, 0};
-  uint32_t k4 = 0xFFFFFFFFu;
-  if (kMode == 0) {
-    for (int d = 0; d < 4; d++)
-      for (int t = 0; t < 4; t++) rot[d] |= (uint32_t)L.needle[d + t] << (8 * t);
-  } else if (kMode != 3) {
-    const uint32_t m4 = m < 4 ? m : 4;
-    for (uint32_t t = 0; t < m4; t++) rot[0] |= (uint32_t)L.needle[t] << (8 * t);
-    if (kMode == 2) k4 = (1u << (8 * m4)) - 1u;
-  }
-  uint32_t acc = 0, s0 = 0, s1 = 0, nh = 0;
-  uint64_t mask = 0;  // records of this lane's verified hits
-  uint32_t c = (lo & ~15u) + l * 16;
-  uint4 nx = c < hi ? *(const uint4*)(&L.win[c]) : make_uint4(0, 0, 0, 0);
-  uint32_t nx4 = (kMode == 1 || kMode == 2) && c < hi ? *(const uint32_t*)(&L.win[c + 16]) : 0u;
-  constexpr uint32_t kStride = kLeanThreads * 16;
-  for (; c < hi; c += kStride) {
-    uint32_t wd[5] = {nx.x, nx.y, nx.z, nx.w, nx4};
-    if (c + kStride < hi) {  // next chunk's LDS read in flight during this one
-      nx = *(const uint4*)(&L.win[c + kStride]);
-      if (kMode == 1 || kMode == 2) nx4 = *(const uint32_t*)(&L.win[c + kStride + 16]);
-    }
-    acc |= wd[0] | wd[1] | wd[2] | wd[3];
-    if (kMode == 3) continue;
-    if (upper) {
-#pragma unroll
-      for (int k = 0; k < 5; k++) wd[k] = swar_upper(wd[k]);
-    }
-    // min over the compare differences: zero iff some 4-gram hits (vector ops
-    // only; a ballot per compare would cost a scalar OR each)
-    uint32_t z = 0xFFFFFFFFu;
-    if (kMode == 0) {
-#pragma unroll
-      for (int k = 0; k < 4; k++) z = min(z, min(min(wd[k] ^ rot[0], wd[k] ^ rot[1]), min(wd[k] ^ rot[2], wd[k] ^ rot[3])));
-    } else {
-#pragma unroll
-      for (int j = 0; j < 16; j += 2) z = min(z, min((win5(wd, j) ^ rot[0]) & k4, (win5(wd, j + 1) ^ rot[0]) & k4));
-    }
-    const bool hl = z == 0u;
-    if (!__ballot(hl)) continue;  // wave-uniform: no 4-gram hit in any lane
-    if (!hl) continue;            // none in this lane
-    if (kMode == 0) {
-      // rare hits: parked, resolved after the scan for all lanes at once
-#pragma unroll
-      for (int k = 0; k < 4; k++)
-#pragma unroll
-        for (int d = 0; d < 4; d++)
-          if (wd[k] == rot[d]) lean_push(L, nr, c + 4 * k - d, m, upper, s0, s1, nh, mask);
-    } else {
-      uint32_t cand = 0;
-#pragma unroll
-      for (int j = 0; j < 16; j++) cand |= (uint32_t)(((win5(wd, j) ^ rot[0]) & k4) == 0) << j;
-      if (kMode == 1) {
-        while (cand) {
-          lean_push(L, nr, c + (uint32_t)__builtin_ctz(cand), m, upper, s0, s1, nh, mask);
-          cand &= cand - 1;
-        }
-      } else {
-        // m <= 3: the masked compare is the whole needle and hits are dense;
-        // one record lookup per chunk, then register compares per hit
-        uint32_t p = c + (uint32_t)__builtin_ctz(cand);
-        int r = lean_rec_of(L, nr, p);
-        uint32_t rvs = r >= 0 ? L.r_vs[r] : 0u, rve = r >= 0 ? L.r_ve[r] : 0u;
-        uint32_t nvs = r + 1 < nr ? L.r_vs[r + 1] : 0xFFFFFFFFu;
-        while (cand) {
-          p = c + (uint32_t)__builtin_ctz(cand);
-          cand &= cand - 1;
-          while (p >= nvs) {
-            r++;
-            rvs = nvs;
-            rve = L.r_ve[r];
-            nvs = r + 1 < nr ? L.r_vs[r + 1] : 0xFFFFFFFFu;
-          }
-          if (r >= 0 && p >= rvs && p + m <= rve) mask |= 1ull << r;
-        }
-      }
-    }
-  }
-  if (nh > 0) lean_resolve(L, nr, s0 & 0xFFFFu, m, upper, mask);
-  if (nh > 1) lean_resolve(L, nr, s0 >> 16, m, upper, mask);
-  if (nh > 2) lean_resolve(L, nr, s1 & 0xFFFFu, m, upper, mask);
-  if (nh > 3) lean_resolve(L, nr, s1 >> 16, m, upper, mask);
-  if (mask) {
-    atomicOr(&L.match[0], (uint32_t)mask);
-    atomicOr(&L.match[1], (uint32_t)(mask >> 32));
-  }
-  return acc;
-}
-
-// One bounded-length regex stage over the value bytes [lo, hi) (regex-filter /
-// filter_regex with a <= 16-state ASCII DFA, smartmodule/regex-filter/src/lib.rs:
-// 24-28): the range is cut into one piece per thread; a thread runs the DFA
-// over its piece plus max_len - 1 bytes of overlap, so every match starting
-// in the piece ends inside the scan.  Table-driven: the state is 4 bits, one
-// LDS read of tt[byte] gives the byte's whole row; FSG_RX_STEP bytes a step, their
-// row reads issued before the state chain consumes them (a byte at a time,
-// each read waited for at once: C1 eval 2.30 -> 1.36 ms at 8 bytes, 1.53 at 16
-// (128-VGPR cap of the lean kernel), 2.55 with two interleaved chains (spills)).
-// A value piece starts in s_bot at the value start and in s_mid elsewhere
-// (unanchored restart); accept bit0 is sticky (the DFA stays in an accepting
-// state), bit1 is checked where a value ends (`$`).  Returns the OR of every
-// scanned byte (bit 7 set <=> a non-ASCII value byte).
-#ifndef FSG_RX_STEP
-#define FSG_RX_STEP 8
-#endif
-__device__ __forceinline__ uint32_t lean_regex(LeanLds& L, int nr, uint32_t lo, uint32_t hi, uint32_t mlen,
-                                               uint32_t s_bot, uint32_t s_mid, uint32_t acc1, uint32_t acc2) {
-  constexpr uint32_t kStep = FSG_RX_STEP;
-  const uint32_t l = threadIdx.x;
-  // piece length: a multiple of 4 whose dword count is odd, so the lanes' window
-  // reads (ds_read_b32: bank (a/4) mod 32 per 32-lane group) fall on distinct banks
-  uint32_t q_len = ((hi - lo + kLeanThreads - 1) / kLeanThreads + 3u) & ~3u;
-  if (!((q_len >> 2) & 1u)) q_len += 4u;
-  const uint32_t p0 = lo + l * q_len;
-  uint32_t orw = 0;
-  uint64_t mask = 0;
-  if (p0 < hi) {
-    const uint32_t p1 = p0 + q_len < hi ? p0 + q_len : hi;
-    const uint32_t pe = p1 + mlen - (mlen ? 1u : 0u);
-    const uint32_t pend = pe < hi ? pe : hi;
-    int r = lean_rec_of(L, nr, p0);
-    if (r < 0) r = 0;
-    for (; r < nr; r++) {
-      const uint32_t vs = L.r_vs[r], ve = L.r_ve[r];
-      if (vs >= p1) break;
-      uint32_t q = vs > p0 ? vs : p0;
-      if (q >= ve) continue;
-      uint32_t st = q == vs ? s_bot : s_mid;
-      const uint32_t end = ve < pend ? ve : pend;
-      while (q + kStep <= end) {
-        uint32_t w[kStep / 4];
-#pragma unroll
-        for (uint32_t j = 0; j < kStep / 4; j++) {
-          w[j] = lds_u32_at(L.win, q + 4u * j);
-          orw |= w[j];
-        }
-        uint64_t t[kStep];
-#pragma unroll
-        for (uint32_t k = 0; k < kStep; k++) t[k] = L.tt[(w[k >> 2] >> (8 * (k & 3))) & 0xFFu];
-#pragma unroll
-        for (uint32_t k = 0; k < kStep; k++) st = (uint32_t)(t[k] >> (4 * st)) & 15u;
-        q += kStep;
-      }
-      while (q < end) {
-        const uint32_t w = lds_u32_at(L.win, q);
-        const uint32_t n = end - q < 4u ? end - q : 4u;
-        orw |= n == 4 ? w : (w & ((1u << (8 * n)) - 1u));
-        for (uint32_t k = 0; k < n; k++) st = (uint32_t)(L.tt[(w >> (8 * k)) & 0xFFu] >> (4 * st)) & 15u;
-        q += n;
-      }
-      if (((acc1 >> st) & 1u) || (end == ve && ((acc2 >> st) & 1u))) mask |= 1ull << r;
-    }
-  }
-  // empty values: decided by the start state alone
-  if ((int)l < nr && L.r_vs[l] == L.r_ve[l] && (((acc1 | acc2) >> s_bot) & 1u)) mask |= 1ull << l;
-  if (mask) {
-    atomicOr(&L.match[0], (uint32_t)mask);
-    atomicOr(&L.match[1], (uint32_t)(mask >> 32));
-  }
-  return orw;
-}
-
-// 4 bits: which of the 4 bytes of a SWAR mask word carry 0x80
-__device__ __forceinline__ uint32_t nib4(uint32_t m80) { return ((((m80 >> 7) & 0x01010101u) * 0x01020408u) >> 24) & 15u; }
-// ---------------------------------------------------------------------------
-// filter_json in the lean kernel (smartmodule/examples/filter_json/src/lib.rs:
-// 54-70, serde_json::from_slice::<StructuredLog>), data-parallel:
-//   1. byte classes of every 16-byte chunk of the batch's values (quotes,
-//      spaces, "special" bytes: < 0x20, '\\', >= 0x80), one chunk per lane;
-//      the in-string mask from a prefix XOR of the quotes carried across the
-//      whole batch (a workgroup XOR scan)
-//   2. the token list: every quote, special byte and non-space byte outside
-//      strings, in order (workgroup prefix sum); opening quotes carry the class
-//      of their string ("level", "message", a LogLevel variant, other)
-//   3. one thread per record runs the table-driven token DFA of fsg_json_dfa.h
-//      over its tokens.  The DFA accepts exactly the flat objects whose
-//      outcome is certain: ASCII, no escapes / control bytes, level a variant
-//      string, message a string, other values strings / JSON numbers /
-//      literals, each field once.  Any other record (and any record starting
-//      inside an unbalanced string) sends the batch to the exact kernel.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t pxor16(uint32_t q) {  // inclusive prefix XOR of 16 bits
-  uint32_t px = q ^ (q << 1);
-  px ^= px << 2;
-  px ^= px << 4;
-  px ^= px << 8;
-  return px & 0xFFFFu;
-}
-// workgroup (128 threads) exclusive prefix of v; returns the exclusive value, *total
-__device__ __forceinline__ uint32_t wg_excl_sum(uint32_t v, uint32_t* wsum, uint32_t* total) {
-  const uint32_t l = threadIdx.x, lane = l & 63u, w = l >> 6;
-  const uint32_t incl = wave_incl_scan(v);
-  if (lane == 63) wsum[w] = incl;
-  lean_sync();
-  const uint32_t w0 = wsum[0];
-  *total = w0 + wsum[1];
-  lean_sync();
-  return incl - v + (w ? w0 : 0u);
-}
-// the class of the string of n bytes at window offset a: its (up to 8) bytes
-// as one little-endian word against immediate constants (string literals would
-// be global loads)
-template <typename LdsT>
-__device__ __forceinline__ uint32_t json_str_class(const LdsT& L, uint32_t a, uint32_t n) {
-  if (n < 4 || n > 7) return JC_Q_OTHER;
-  const uint64_t lo = lds_u32_at(L.win, a);
-  const uint64_t hi = lds_u32_at(L.win, a + 4);
-  const uint64_t w = (lo | (hi << 32)) & ((1ull << (8 * n)) - 1ull);
-  constexpr auto k = [](const char* t) {
-    uint64_t v = 0;
-    for (int i = 0; t[i]; i++) v |= (uint64_t)(uint8_t)t[i] << (8 * i);
-    return v;
-  };
-  if (n == 5) return w == k("level") ? JC_Q_LEVEL : w == k("debug") ? JC_Q_DEBUG : w == k("error") ? JC_Q_ERROR : JC_Q_OTHER;
-  if (n == 7) return w == k("message") ? JC_Q_MSG : JC_Q_OTHER;
-  if (n == 4) return w == k("info") ? JC_Q_INFO : w == k("warn") ? JC_Q_WARN : JC_Q_OTHER;
-  return JC_Q_OTHER;
-}
-// stages 1-3 for the records [0, nr); returns true if the batch must go to the
-// exact kernel; match bits of records whose level > Debug in L.match
-// lean_json_stage step 3b for the members [0, nseg) of L.jn
-template <bool kProj>
-__device__ __forceinline__ void json_members(LeanLdsJ& L, int nr, uint32_t ntok, uint32_t nseg) {
-  for (uint32_t k = threadIdx.x; k < nseg; k += kLeanThreads) {
-    const uint32_t sg = L.jn()[k];
-    const bool first = (sg & 0x8000u) != 0u;
-    const uint32_t t0 = sg & 0x7FFFu;
-    uint32_t t = t0;
-    // the member's record: that of its first token (a record start) or of the comma before it
-    const uint32_t anchor = L.ent[first ? t : t - 1] & 0x7FFFu;
-    const uint32_t rr = (uint32_t)lean_rec_of(L, nr, anchor);
-    const uint32_t ve = L.r_ve[rr];
-    uint32_t st = first ? (uint32_t)JS_OBJ : (uint32_t)JS_KEY;
-    uint32_t prev = first ? 0xFFFFu : anchor;
-    uint32_t nlv = 0, nmsg = 0, lv = 0;
-    bool ended = false, nbad = false;
-    bool khit = false, inval = false, found = false, vneg = false;
-    uint32_t vstart = 0, ntv = 0, fs = 0, fe = 0;
-    for (; t < ntok; t++) {
-      const uint32_t en = L.ent[t];
-      const uint32_t pos = en & 0x7FFFu;
-      if (pos >= ve) break;
-      uint32_t cls = en >> 24;
-      const uint32_t adj = pos == prev + 1 ? 1u : 0u;
-      const uint32_t st0 = st;
-      if constexpr (kProj) {
-        const bool q = cls == JC_Q_FIELD;
-        if (q) cls = JC_Q_OTHER;  // every string takes the "other" paths of the table
-        else if (cls >= JC_Q_LEVEL && cls <= JC_Q_ERROR) cls = JC_Q_OTHER;
-        st = L.dfa[st * kJsonCls2 + cls * 2 + adj];
-        if (st == JS_INKEY_OTHER) khit = q;
-        if (st0 == JS_VAL_OTHER) {
-          inval = true;
-          vstart = pos;
-          ntv = 0;
-          vneg = cls == JC_MINUS;
-        }
-        if (inval) {
-          if (st == JS_KEY || st == JS_END) {  // ',' / '}' after the value
-            inval = false;
-            if (st0 == JS_N_ZERO && vneg && ntv == 2) nbad = true;  // -0
-            if (khit) {
-              found = true;
-              fs = vstart;
-              fe = prev + 1;
-            }
-          } else {
-            ntv++;
-            if (st == JS_N_DOT || st == JS_N_E || ntv > 18) nbad = true;
-          }
-        }
-      } else {
-        if (st >= JS_INV_D && st <= JS_INV_E) lv = 1u << (st - JS_INV_D);
-        st = L.dfa[st * kJsonCls2 + cls * 2 + adj];
-        nlv += st == JS_INKEY_LV ? 1u : 0u;
-        nmsg += st == JS_INKEY_MSG ? 1u : 0u;
-      }
-      prev = pos;
-      if (cls == JC_COMMA || st == JS_FAIL) {
-        ended = true;
-        break;
-      }
-    }
-    const bool ok = !nbad && (ended ? st == JS_KEY : st == JS_END);
-    atomicAdd(&L.racc[rr], nlv | (nmsg << 8) | (ok ? 0u : 1u << 16));
-    if (lv) atomicOr(&L.rlvl[rr], lv);
-    if (found) atomicMax(&L.rbest[rr], ((unsigned long long)(t0 + 1) << 32) | (fs << 16) | fe);
-  }
-}
-
-#ifdef FSG_LEAN_TIMING
-#define JT_PARAMS , uint64_t *lt_acc, uint64_t &lt_last
-#define JT_ARGS , lt_acc, lt_last
-#define JMARK(k)                                             \
-  {                                                          \
-    const uint64_t lt_now = __builtin_amdgcn_s_memtime();    \
-    lt_acc[k] += lt_now - lt_last;                           \
-    lt_last = lt_now;                                        \
-  }
-#else
-#define JT_PARAMS
-#define JT_ARGS
-#define JMARK(k)
-#endif
-__device__ bool lean_json_stage(LeanLdsJ& L, int nr, uint32_t& orpar, bool proj, uint32_t fl JT_PARAMS) {
-  const uint32_t l = threadIdx.x;
-  const uint32_t c0 = L.r_vs[0] & ~15u, c1 = L.r_ve[nr - 1];
-  const uint32_t nch = (c1 - c0 + 15) >> 4;
-  if (nch > (uint32_t)kJsonChunks) return true;
-  // 1. masks; thread t owns the contiguous chunks [t*per, (t+1)*per), per odd:
-  //    the lanes' jm[] dwords and 16-byte window reads then fall on distinct
-  //    banks (an even per put 4-8 lanes of a group on one bank)
-  const uint32_t per = ((nch + kLeanThreads - 1) / kLeanThreads) | 1u;
-  const uint32_t k0 = l * per, k1 = k0 + per < nch ? k0 + per : nch;
-  uint32_t par = 0;
-  for (uint32_t k = k0; k < k1; k++) {  // byte classes, once: quote, special (< 0x20 incl. 0, '\\', >= 0x80), non-space
-    const uint4 v = *(const uint4*)(&L.win[c0 + 16 * k]);
-    uint32_t q = 0, sp = 0, ns = 0;
-#pragma unroll
-    for (int d = 0; d < 4; d++) {
-      const uint32_t w = d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
-      q |= nib4(zbytes(w ^ 0x22222222u)) << (4 * d);
-      sp |= nib4(zbytes(w & 0xE0E0E0E0u) | zbytes(w ^ 0x5C5C5C5Cu) | (w & 0x80808080u)) << (4 * d);
-      ns |= nib4(zbytes(w ^ 0x20202020u)) << (4 * d);
-    }
-    L.jm[k] = q | (sp << 16);
-    L.jn()[k] = (uint16_t)(~ns & 0xFFFFu);
-    par ^= __builtin_popcount(q) & 1u;
-  }
-  JMARK(6);
-  uint32_t tot;
-  uint32_t carry = wg_excl_sum(par, L.wsum, &tot) & 1u;  // parity of all quotes before my chunks
-  uint32_t cnt = 0;
-  for (uint32_t k = k0; k < k1; k++) {
-    const uint32_t m = L.jm[k], q = m & 0xFFFFu, sp = m >> 16;
-    const uint32_t instr = (pxor16(q) ^ q ^ (carry ? 0xFFFFu : 0u)) & 0xFFFFu;
-    carry ^= __builtin_popcount(q) & 1u;
-    const uint32_t hot = q | sp | ((uint32_t)L.jn()[k] & ~instr);
-    L.jm[k] = instr | (hot << 16);
-    cnt += __builtin_popcount(hot);
-  }
-  JMARK(7);
-  // 2. token list
-  uint32_t ntok;
-  uint32_t e = wg_excl_sum(cnt, L.wsum, &ntok);
-  if (ntok > (uint32_t)kJsonEnt) return true;  // uniform: every thread saw the same total
-  // positions in order (ALU only: the token count per thread is uneven, the
-  // records' heads are dense), then classes strided over the tokens
-  for (uint32_t k = k0; k < k1; k++) {
-    const uint32_t instr = L.jm[k] & 0xFFFFu;
-    uint32_t hot = L.jm[k] >> 16;
-    while (hot) {
-      const uint32_t j = (uint32_t)__builtin_ctz(hot);
-      hot &= hot - 1;
-      L.ent[e++] = (c0 + 16 * k + j) | (((instr >> j) & 1u) << 15);
-    }
-  }
-  if (l == 0) L.nseg = 0;
-  lean_sync();
-  JMARK(8);
-  // classes; an opening quote takes the class of its string (the next token
-  // closes it).  Bits 0..15 never change here, so a neighbour's position and
-  // in-string bit can be read while it is being rewritten.
-  for (uint32_t t = l; t < ntok; t += kLeanThreads) {
-    const uint32_t en = L.ent[t];
-    const uint32_t pos = en & 0x7FFFu;
-    const uint32_t b = L.win[pos];
-    uint32_t cls = L.bcls[b];
-    if (b == '"') {
-      cls = (en & 0x8000u) ? (uint32_t)JC_Q_CLOSE : (uint32_t)JC_Q_OTHER;
-      if (cls == JC_Q_OTHER && t + 1 < ntok) {
-        const uint32_t nx = L.ent[t + 1];
-        const uint32_t np = nx & 0x7FFFu;
-        if ((nx & 0x8000u) && L.win[np] == '"') {
-          const uint32_t a = pos + 1, n = np - a;
-          if (proj) {  // the projected field's name (L.needle) or another string
-            bool eq = n == fl;
-            for (uint32_t k = 0; eq && k < fl; k += 4) {
-              const uint32_t mk = fl - k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (fl - k))) - 1u);
-              eq = ((lds_u32_at(L.win, a + k) ^ lds_u32_at(L.needle, k)) & mk) == 0u;
-            }
-            cls = eq ? (uint32_t)JC_Q_FIELD : (uint32_t)JC_Q_OTHER;
-          } else {
-            cls = json_str_class(L, a, n);
-          }
-        }
-      }
-    }
-    L.ent[t] = (en & 0xFFFFu) | (b << 16) | (cls << 24);
-    // members: the token after a comma starts one (of the comma's record)
-    if (cls == JC_COMMA) {
-      const uint32_t k = atomicAdd(&L.nseg, 1u);
-      if (k < (uint32_t)kJsonSeg) L.jn()[k] = (uint16_t)(t + 1);
-    }
-  }
-  lean_sync();
-  JMARK(9);
-  // 3a. per record: balanced quotes at its ends, its first token (binary
-  //     search on positions) = the start of its first member
-  const uint32_t r = 2 * (l & 63u) + (l >> 6);
-  auto instr_at = [&](uint32_t p) {
-    const uint32_t k = (p - c0) >> 4, j = (p - c0) & 15u;
-    if (k >= nch) return 0u;
-    return (L.jm[k] >> j) & 1u;
-  };
-  uint32_t t_first = 0;
-  bool bad = false;
-  if ((int)r < nr) {
-    const uint32_t vs = L.r_vs[r], ve = L.r_ve[r];
-    if (instr_at(vs) || instr_at(ve)) bad = true;
-    uint32_t lo = 0, hi = ntok;
-    while (lo < hi) {
-      const uint32_t m = (lo + hi) >> 1;
-      if ((L.ent[m] & 0x7FFFu) < vs) lo = m + 1; else hi = m;
-    }
-    t_first = lo;
-    // no token inside the value: not an object (and no member may claim it)
-    if (lo >= ntok || (L.ent[lo] & 0x7FFFu) >= ve) bad = true;
-    L.racc[r] = bad ? 1u << 16 : 0u;
-    L.rlvl[r] = 0;
-    L.rbest[r] = 0;
-    if (!bad) {
-      const uint32_t k = atomicAdd(&L.nseg, 1u);
-      if (k < (uint32_t)kJsonSeg) L.jn()[k] = (uint16_t)(lo | 0x8000u);
-    }
-  }
-  (void)t_first;
-  lean_sync();
-  const uint32_t nseg = L.nseg;
-  if (nseg > (uint32_t)kJsonSeg) return lean_or(L.red, orpar, true);  // uniform
-  // 3b. the token DFA, one thread per object member: a member after a comma
-  //     starts in JS_KEY (the only state a comma leads to) and ends with the
-  //     next comma, which must lead to JS_KEY again, or at the record's end,
-  //     which must be JS_END.  filter_json, per record: each field exactly
-  //     once, the level value's variant.  Projection (map_json_project,
-  //     Map<String, Value>, last member wins): the value span of the last
-  //     member whose key is the field; numbers whose serde_json text differs
-  //     from the source (fractions, exponents, -0, more than 18 digits) are
-  //     unsupported by the device restatement -> exact kernel
-  JMARK(10);
-  if (proj)
-    json_members<true>(L, nr, ntok, nseg);
-  else
-    json_members<false>(L, nr, ntok, nseg);
-  lean_sync();
-  JMARK(11);
-  if ((int)r < nr) {
-    const uint32_t ac = L.racc[r];
-    if (proj) {
-      bad = (ac >> 16) != 0u;
-      const unsigned long long bst = L.rbest[r];
-      if (!bad && bst) {
-        atomicOr(&L.match[r >> 5], 1u << (r & 31));
-        L.r_vs[r] = (uint32_t)(bst >> 16) & 0xFFFFu;  // the value narrows to the field's text
-        L.r_ve[r] = (uint32_t)bst & 0xFFFFu;
-      }
-    } else {
-      // exactly one level and one message field (a duplicate is a serde error)
-      bad = (ac >> 16) != 0u || (ac & 0xFFu) != 1u || ((ac >> 8) & 0xFFu) != 1u;
-      if (!bad && (L.rlvl[r] & ~1u)) atomicOr(&L.match[r >> 5], 1u << (r & 31));
-    }
-  }
-  return lean_or(L.red, orpar, bad);
-}
-
-// blank every byte between values (record headers, keys, lengths) with
-// spaces and build the 64-byte block -> record table; thread l < nr owns
-// record l (value [vs, vs+vl)).  A space has no high bit (the scans' OR stays
-// an ASCII test), is no JSON token (the token list holds value bytes only) and
-// a needle hit that reaches into a gap fails its record range check.
-__device__ __forceinline__ void clear_gaps(LeanLds& L, int nr, uint32_t vs, uint32_t vl) {
-  const uint32_t l = threadIdx.x;
-  const uint32_t lo = L.r_vs[0], hi = L.r_ve[nr - 1];
-  // [s, e) <- ' ': whole aligned dwords inside the range, bytes at its edges (a
-  // dword at an edge may hold another record's value bytes)
-  auto zero = [&](uint32_t s, uint32_t e) {
-    const uint32_t s4 = (s + 3) & ~3u, e4 = e & ~3u;
-    if (s4 >= e4) {
-      for (uint32_t p = s; p < e; p++) L.win[p] = 0x20;
-      return;
-    }
-    for (uint32_t p = s; p < s4; p++) L.win[p] = 0x20;
-    for (uint32_t p = s4; p < e4; p += 4) *(uint32_t*)(L.win + p) = 0x20202020u;
-    for (uint32_t p = e4; p < e; p++) L.win[p] = 0x20;
-  };
-  if ((int)l < nr) zero(vs + vl, (int)l + 1 < nr ? L.r_vs[l + 1] : ((vs + vl + 15) & ~15u) + 16);
-  if (l == 0) zero(lo & ~15u, lo);
-  // blk[j] = l for the 64-byte blocks j starting in [vs, next value start)
-  if ((int)l < nr) {
-    const uint32_t e = (int)l + 1 < nr ? L.r_vs[l + 1] : hi + 80;
-    const uint32_t j0 = (vs + 63) >> 6, j1 = (e + 63) >> 6;
-    const uint32_t rep = l * 0x01010101u;
-    uint32_t j = j0;
-    for (; j < j1 && (j & 3u); j++) L.blk[j] = (uint8_t)l;
-    for (; j + 4 <= j1; j += 4) *(uint32_t*)(L.blk + j) = rep;
-    for (; j < j1; j++) L.blk[j] = (uint8_t)l;
-  }
-  if (l == 0)
-    for (uint32_t j = 0; (j << 6) < lo; j++) L.blk[j] = 0xFF;
-}
-
-// the 16-byte aligned window [al, al + wlen) of batch b
-struct LeanWin {
-  uint64_t pos, al;
-  uint32_t wlen;
-};
-__device__ __forceinline__ LeanWin lean_window(const EvalArgs& a, uint32_t b) {
-  LeanWin w;
-  w.pos = a.bpos[b];
-  const uint64_t nxt = b + 1 < a.nbatches ? a.bpos[b + 1] : a.slice_len;
-  w.al = w.pos & ~15ull;
-  uint64_t wl = nxt > w.al ? nxt - w.al : 0;
-  if (wl > (uint64_t)kLeanWin) wl = kLeanWin;
-  w.wlen = (uint32_t)((wl + 15) & ~15ull);
-  return w;
-}
-// 1 KiB LDS-DMA pieces (one 16-byte piece per lane), the last one partial;
-// the waves split the pieces
-__device__ __forceinline__ void lean_issue(const EvalArgs& a, const LeanWin& w, uint8_t* dst) {
-  const uint32_t l = threadIdx.x, lane = l & 63u;
-  const uint8_t* src = a.slice + w.al + lane * 16;
-  for (uint32_t k = __builtin_amdgcn_readfirstlane(l >> 6); k * 1024 < w.wlen; k += kLeanThreads / 64)
-    if (k * 1024 + lane * 16 < w.wlen)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + k * 1024),
-                                       (__attribute__((address_space(3))) void*)(dst + k * 1024), 16, 0, 0);
-}
-
-// k_chase — record framing of the lean path, one thread per batch: the chain
-// of record length varints (Record::decode's first field, data.rs:534-562)
-// walked with dependent global loads; thousands of batches in flight hide the
-// latency, and k_eval_lean gets every record's start with its window instead
-// of a serial walk through LDS.  Conservative: anything unusual (more than
-// kLeanMaxR records, a length varint over 4 bytes, a record past the window)
-// leaves rend[b] = 0xFFFF and the batch takes the exact path.
-__device__ __forceinline__ uint32_t ld_u32_at(const uint8_t* p) {  // 4 bytes at any address
-  const uint64_t a = (uint64_t)p;
-  const uint32_t* w = (const uint32_t*)(a & ~3ull);
-  return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3u));
-}
-// The starts are staged in LDS and written back as one contiguous span per
-// workgroup (batches b0 .. b0 + 255 own consecutive record slots), so the
-// stores are coalesced instead of one partial line per record.
-constexpr int kChaseT = 256;
-__global__ __launch_bounds__(kChaseT) void k_chase(EvalArgs a) {
-  __shared__ uint16_t st[kChaseT * kLeanMaxR];
-  const uint32_t t = threadIdx.x;
-  const uint32_t b0 = blockIdx.x * kChaseT;
-  const uint32_t b = b0 + t;
-  const uint32_t bl = b0 + kChaseT < a.nbatches ? b0 + kChaseT : a.nbatches;  // first batch past the block
-  const uint64_t R0 = a.rbase[b0];
-  const uint64_t R1 = bl < a.nbatches ? a.rbase[bl] : a.nrec;
-  const bool stage = R1 - R0 <= (uint64_t)(kChaseT * kLeanMaxR);
-  if (b < a.nbatches) {
-    const uint64_t pos = a.bpos[b];
-    const uint64_t nxt = b + 1 < a.nbatches ? a.bpos[b + 1] : a.slice_len;
-    const uint64_t rb = a.rbase[b], rn = (b + 1 < a.nbatches ? a.rbase[b + 1] : a.nrec) - rb;
-    const uint64_t al = pos & ~15ull;
-    uint64_t wl = nxt > al ? nxt - al : 0;
-    if (wl > (uint64_t)kLeanWin) wl = kLeanWin;
-    const uint64_t wlen = (wl + 15) & ~15ull;
-    const uint8_t* base = a.slice + al;
-    const uint32_t batch_len = __builtin_bswap32(ld_u32_at(a.slice + pos + 8));
-    const uint64_t sec0 = pos + 57, sec_end = pos + 12 + (uint64_t)batch_len;
-    const uint64_t sec_len = sec_end - sec0;
-    const int32_t count = sec_len >= 4 ? (int32_t)__builtin_bswap32(ld_u32_at(a.slice + sec0)) : -1;
-    uint32_t end = 0xFFFFu;
-    if (sec_len >= 4 && sec_end - al <= wlen && count >= 0 && count <= kLeanMaxR && (uint64_t)count == rn) {
-      const uint32_t have = (uint32_t)(sec_end - al);
-      uint32_t q = (uint32_t)(sec0 + 4 - al);
-      int n = 0;
-      for (; n < count; n++) {
-        const uint32_t x = ld_u32_at(base + q);
-        const uint32_t term = ~x & 0x80808080u;
-        if (!term) break;
-        const uint32_t nb = (((uint32_t)__builtin_ctz(term)) >> 3) + 1;
-        if (q + nb > have) break;
-        const uint32_t y = nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u));
-        const uint32_t v = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
-        if (v & 1u) break;  // negative length (zigzag)
-        const uint32_t len = v >> 1;
-        if (have - (q + nb) < len) break;
-        if (stage)
-          st[rb - R0 + n] = (uint16_t)q;
-        else
-          a.rstart[rb + n] = (uint16_t)q;
-        q += nb + len;
-      }
-      if (n == count) end = q;
-    }
-    a.rend[b] = (uint16_t)end;
-  }
-  if (!stage) return;  // uniform
-  __syncthreads();
-  // slots of failed chases hold garbage: the lean kernel never reads them (rend = 0xFFFF)
-  const uint64_t n = R1 - R0;
-  uint16_t* dst = a.rstart + R0;
-  const uint32_t head = (uint32_t)((8u - ((uintptr_t)dst & 15u) / 2u) & 7u);  // u16 slots to 16-B alignment
-  for (uint64_t i = t; i < n && i < head; i += kChaseT) dst[i] = st[i];
-  for (uint64_t i = head + 8ull * t; i + 8 <= n; i += 8ull * kChaseT) {
-    uint4 v;
-    v.x = st[i] | ((uint32_t)st[i + 1] << 16);
-    v.y = st[i + 2] | ((uint32_t)st[i + 3] << 16);
-    v.z = st[i + 4] | ((uint32_t)st[i + 5] << 16);
-    v.w = st[i + 6] | ((uint32_t)st[i + 7] << 16);
-    *(uint4*)(dst + i) = v;
-  }
-  const uint64_t tail0 = n > head ? head + ((n - head) & ~7ull) : n;
-  for (uint64_t i = tail0 + t; i < n; i += kChaseT) dst[i] = st[i];
-}
-
-// k_chase_w — the same record framing for the exact kernel and the lean array
-// kernel: any record count, a batch up to 64 KiB from its aligned start.  One
-// wave per batch: the window streams through registers 16 KiB at a time (row
-// k = 1 KiB, lane = 16 bytes), and the wave-uniform walk reads each length
-// varint with two readlanes (no dependent memory loads on the chain); the
-// starts are gathered one per lane and stored 64 at a time.
-__device__ __forceinline__ uint32_t sel4(const uint4& v, uint32_t c) {
-  return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
-}
-constexpr int kChaseRows = 16;
-__global__ __launch_bounds__(256) void k_chase_w(EvalArgs a) {
-  const uint32_t lane = lane_id();
-  const uint32_t nw = gridDim.x * 4;
-  // the batch index is wave-uniform: readfirstlane keeps the whole walk scalar
-  for (uint32_t b = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); b < a.nbatches; b += nw) {
-    const uint64_t pos = a.bpos[b];
-    const uint64_t rb = a.rbase[b], rn = (b + 1 < a.nbatches ? a.rbase[b + 1] : a.nrec) - rb;
-    const uint64_t al = pos & ~15ull;
-    const uint32_t batch_len = __builtin_bswap32(ld_u32_at(a.slice + pos + 8));
-    const uint64_t sec0 = pos + 57, sec_end = pos + 12 + (uint64_t)batch_len;
-    const uint64_t sec_len = sec_end - sec0;
-    const int32_t count = sec_len >= 4 ? (int32_t)__builtin_bswap32(ld_u32_at(a.slice + sec0)) : -1;
-    uint32_t end = 0xFFFFu;
-    if (sec_len >= 4 && sec_end - al < 0xFFFFu && count >= 0 && (uint64_t)count == rn) {
-      const uint32_t have = (uint32_t)(sec_end - al);
-      const uint64_t lim = a.slice_len + kSlicePad;  // readable bytes of the slice buffer
-      uint32_t q = (uint32_t)(sec0 + 4 - al);
-      uint32_t n = 0, acc = 0;
-      bool ok = true;
-      for (uint32_t blk = 0; ok && n < (uint32_t)count && blk * 1024u * kChaseRows < have; blk++) {
-        uint4 R[kChaseRows + 1];
-#pragma unroll
-        for (int k = 0; k <= kChaseRows; k++) {
-          const uint64_t o = al + (uint64_t)(blk * kChaseRows + k) * 1024 + lane * 16;
-          R[k] = o + 16 <= lim ? *(const uint4*)(a.slice + o) : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int k = 0; k < kChaseRows; k++) {
-          const uint32_t row_end = (blk * kChaseRows + k + 1) * 1024u;
-          while (ok && n < (uint32_t)count && q < row_end) {
-            q = __builtin_amdgcn_readfirstlane(q);  // uniform (the compiler cannot see it through the loop)
-            n = __builtin_amdgcn_readfirstlane(n);
-            const uint32_t d = (q & 1023u) >> 2;  // dword of the row
-            const uint32_t w0 = __builtin_amdgcn_readlane(sel4(R[k], d & 3u), d >> 2);
-            const uint32_t w1 = d == 255 ? __builtin_amdgcn_readlane(R[k + 1].x, 0)
-                                         : __builtin_amdgcn_readlane(sel4(R[k], (d + 1) & 3u), (d + 1) >> 2);
-            const uint32_t x = __builtin_amdgcn_alignbyte(w1, w0, q & 3u);
-            const uint32_t term = ~x & 0x80808080u;
-            const uint32_t nb = (((uint32_t)__builtin_ctz(term | 0x80000000u)) >> 3) + 1;
-            const uint32_t y = nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u));
-            const uint32_t v = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
-            const uint32_t len = v >> 1;
-            // no terminator in 4 bytes, past the section, a negative length, past the section
-            if (!term || q + nb > have || (v & 1u) || have - (q + nb) < len) {
-              ok = false;
-              break;
-            }
-            if (lane == (n & 63u)) acc = q;
-            if ((n & 63u) == 63u) a.rstart[rb + n - 63 + lane] = (uint16_t)acc;
-            n++;
-            q += nb + len;
-          }
-        }
-      }
-      if (n & 63u)
-        if (lane < (n & 63u)) a.rstart[rb + (n & ~63u) + lane] = (uint16_t)acc;
-      if (ok && n == (uint32_t)count) end = q;
-    }
-    if (lane == 0) a.rend[b] = (uint16_t)end;
-  }
-}
-void launch_chase_w(const EvalArgs& a, hipStream_t s) {
-  if (a.nbatches) hipLaunchKernelGGL(k_chase_w, dim3(std::min<uint32_t>((a.nbatches + 3) / 4, 8192)), dim3(256), 0, s, a);
-}
-
-// four waves per SIMD (eight workgroups per CU, as many as the LDS holds)
-template <bool kJson>
-#ifndef FSG_JSON_WPE
-#define FSG_JSON_WPE 3  // waves per SIMD of the JSON lean kernel: <= 168 VGPRs, with <= 32 KiB LDS 5 workgroups per CU
-#endif
-#ifndef FSG_LEAN_WPE
-#define FSG_LEAN_WPE 4
-#endif
-__global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kJson ? FSG_JSON_WPE : FSG_LEAN_WPE))) void k_eval_lean(EvalArgs a) {
-  __shared__ typename std::conditional<kJson, LeanLdsJ, LeanLds>::type L;
-  const uint32_t l = threadIdx.x;
-  const uint32_t G = gridDim.x;
-  uint32_t b = blockIdx.x;
-  if (b >= a.nbatches) return;
-  // the chain's stages, needles, regex rows and JSON tables: LDS, once
-  {
-    const ChainDesc& ch = *a.chain;
-    const uint32_t nst = ch.nstages;
-    uint32_t nrx = 0, rx = 0xFFu, ndo = 0;
-    for (uint32_t s = 0; s < nst; s++)
-      if (ch.st[s].op == OP_CONTAINS || ch.st[s].op == OP_PROJECT) ndo += ch.st[s].needle_len;
-    const bool nd_res = ndo <= (uint32_t)kLeanNeedles;
-    ndo = 0;
-    for (uint32_t s = 0; s < nst; s++) {
-      const StageDesc& sd = ch.st[s];
-      if (sd.op == OP_REGEX) {
-        nrx++;
-        rx = s;
-      }
-      if (l == 0) {
-        LeanStage g;
-        g.op = sd.op;
-        g.upper = sd.in_type == VT_SRC_UPPER ? 1 : 0;
-        g.keep_match = sd.keep_match;
-        g.pad = 0;
-        g.m = sd.needle_len;
-        g.max_len = (uint32_t)sd.dfa.max_len;
-        g.s_bot = sd.dfa.s_bot;
-        g.s_mid = sd.dfa.s_mid;
-        g.acc1 = sd.dfa.acc1;
-        g.acc2 = sd.dfa.acc2;
-        g.tt = sd.in_type == VT_SRC_UPPER ? sd.dfa.tt_up : sd.dfa.tt;
-        g.nd = sd.needle;
-        g.nd_off = ndo;
-        L.stg[s] = g;
-      }
-      if ((sd.op == OP_CONTAINS || sd.op == OP_PROJECT) && nd_res) {
-        for (uint32_t t = l; t < sd.needle_len; t += kLeanThreads) L.needles[ndo + t] = a.blob[sd.needle + t];
-        ndo += sd.needle_len;
-      }
-    }
-    if (nrx == 1 && !kJson) {  // one regex stage: its rows stay resident (the JSON variant reuses them as jn)
-      const StageDesc& sd = ch.st[rx];
-      const uint64_t* tt = (const uint64_t*)(a.blob + (sd.in_type == VT_SRC_UPPER ? sd.dfa.tt_up : sd.dfa.tt));
-      for (uint32_t t = l; t < 256; t += kLeanThreads) L.tt[t] = tt[t];
-    }
-    if (l == 0) {
-      L.nst = nst;
-      L.out_upper = ch.out_type == VT_SRC_UPPER ? 1u : 0u;
-      L.tt_stage = nrx == 1 && !kJson ? rx : 0xFFu;
-      L.nd_res = nd_res ? 1u : 0u;
-    }
-    if constexpr (kJson) {
-      for (uint32_t t = l; t < (uint32_t)(kJsonStates * kJsonCls2); t += kLeanThreads) L.dfa[t] = g_json_tables.t[t];
-      for (uint32_t t = l; t < 256; t += kLeanThreads) L.bcls[t] = g_json_tables.bcls[t];
-    }
-  }
-  uint32_t par = 0;  // lean_or pair
-#ifdef FSG_LEAN_TIMING  // experiment builds: per-phase clock sums, printed by workgroup 0
-  uint64_t lt_acc[12] = {}, lt_last = __builtin_amdgcn_s_memtime(), lt_nb = 0;
-#define LEAN_MARK(k)                                         \
-  {                                                          \
-    const uint64_t lt_now = __builtin_amdgcn_s_memtime();    \
-    lt_acc[k] += lt_now - lt_last;                           \
-    lt_last = lt_now;                                        \
-  }
-#else
-#define LEAN_MARK(k)
-#endif
-  // the previous batch's results, stored once the next window is in flight
-  // (a store issued right before the wait for the next window would be waited for too)
-  uint32_t p_b = 0xFFFFFFFFu;
-  bool p_defer = false, p_kept = false;
-  uint64_t p_idx = 0;
-  KeptRec p_d = {};
-  int64_t p_base = 0, p_ts0 = 0;
-  int32_t p_lod = 0;
-  uint32_t p_comp = 0;
-  uint32_t p_nkeep = 0, p_sec = 0;
-  auto flush = [&]() {
-    if (p_b == 0xFFFFFFFFu) return;
-    if (p_defer) {
-      if (l == 0) {
-        const uint32_t i = atomicAdd(&a.list[0], 1u);
-        a.list[1 + i] = p_b;
-      }
-    } else {
-      if (p_kept) a.desc[p_idx] = p_d;
-      if (l == 0) {
-        BatchStat st = {};
-        st.base_offset = p_base;
-        st.lod_in = p_lod;
-        st.first_ts = p_ts0;
-        st.comp = p_comp;
-        st.flags = BF_LAST_STAGE;
-        st.nkeep = p_nkeep;
-        st.nout = p_nkeep;
-        st.sec_len = p_sec;
-        st.err_stage = 0xFFFFFFFFu;
-        a.bstat[p_b] = st;
-      }
-    }
-    p_b = 0xFFFFFFFFu;
-  };
-  for (;;) {
-    lean_sync();  // every lane is done with the previous batch's window
-    const LeanWin W = lean_window(a, b);
-    const uint64_t pos = W.pos, al = W.al;
-    const uint32_t wlen = W.wlen;
-    const uint64_t rb = a.rbase[b];
-    const uint32_t bn = b + G;
-    lean_issue(a, W, L.win);
-    // the record starts (k_chase) ride along with the window
-    const uint32_t rs = l < 64 ? a.rstart[rb + l] : 0u;
-    const uint32_t re = a.rend[b];
-    __builtin_amdgcn_s_waitcnt(0);  // this wave's pieces have landed
-    lean_sync();                    // ... and the other wave's
-    LEAN_MARK(0);
-    // batch header (file format, batch.rs:163-180), read before the gaps are cleared
-    const uint8_t* h = L.win + (pos - al);
-    const int64_t base_offset = (int64_t)rd_be(h, 8);
-    const uint32_t batch_len = (uint32_t)rd_be(h + 8, 4);
-    const int32_t lod_in = (int32_t)rd_be(h + 23, 4);
-    const int64_t first_ts = (int64_t)rd_be(h + 27, 8);
-    const uint32_t comp = (uint32_t)h[22] & 7u;
-    const uint64_t sec0 = pos + 57;
-    const uint64_t sec_end = pos + 12 + (uint64_t)batch_len;  // framing validated at ingest
-    const uint32_t sec_len = (uint32_t)(sec_end - sec0);
-    const int32_t count = sec_len >= 4 ? (int32_t)rd_be(L.win + (sec0 - al), 4) : -1;
-    bool defer = sec_len < 4 || sec_end - al > (uint64_t)wlen || count < 0 || count > kLeanMaxR;
-    // 2. framing: the record starts k_chase found (rs, loaded with the window);
-    //    lane r parses record r.  No lean framing (rend 0xFFFF): exact path.
-    if (!defer) defer = re == 0xFFFFu;
-    const int nr = defer ? 0 : count;
-    bool g = true;
-    int64_t ts = 0, od = 0, hdr = 0;
-    uint32_t vs = 0, vl = 0, kpos = 0, klen = 0;
-    uint8_t attr = 0, tag = 0;
-    const uint32_t rs_next = __shfl_down(rs, 1, 64);
-    if ((int)l < nr) {
-      uint32_t q = rs;
-      const uint32_t lim = (int)l + 1 == nr ? re : rs_next;
-      int64_t len, kl, vlen;
-      g = !wvarint((const uint8_t*)L.win, q, lim, &len);
-      if (g && q < lim) attr = L.win[q++]; else g = false;
-      g = g && !wvarint((const uint8_t*)L.win, q, lim, &ts) && !wvarint((const uint8_t*)L.win, q, lim, &od);
-      if (g && q < lim) tag = L.win[q++]; else g = false;
-      g = g && tag <= 1;
-      if (g && tag == 1) {
-        g = !wvarint((const uint8_t*)L.win, q, lim, &kl) && kl >= 0 && (uint64_t)q + (uint64_t)kl <= lim;
-        if (g) {
-          kpos = q;
-          klen = (uint32_t)kl;
-          q += klen;
-        }
-      }
-      g = g && !wvarint((const uint8_t*)L.win, q, lim, &vlen) && vlen >= 0 && (uint64_t)q + (uint64_t)vlen <= lim;
-      vs = q;
-      if (g) {
-        vl = (uint32_t)vlen;
-        q += vl;
-      }
-      g = g && !wvarint((const uint8_t*)L.win, q, lim, &hdr) && q == lim;
-      L.r_vs[l] = vs;
-      L.r_ve[l] = vs + vl;
-    }
-    defer = lean_or(L.red, par, defer || !g);  // a record that does not frame exactly
-    LEAN_MARK(1);
-    uint64_t alive = __ballot((int)l < nr);
-    // 3. stages.  Before the first scan every non-value byte of the scanned
-    //    range is cleared (record headers, keys, lengths): then the OR of the
-    //    scanned words has a high bit iff some value is non-ASCII.
-    bool checked = false;  // every value known ASCII (from_utf8 cannot fail)
-    bool cleared = false;  // gap bytes zeroed, record block table built
-    const uint32_t nst = __builtin_amdgcn_readfirstlane(L.nst);
-    for (uint32_t s = 0; !defer && s < nst; s++) {
-      const LeanStage sd = L.stg[s];
-      const uint32_t op = __builtin_amdgcn_readfirstlane((uint32_t)sd.op);
-      if (op == OP_MAP_UPPER) continue;  // representation only
-      if constexpr (kJson) if (op == OP_FILTER_JSON || op == OP_PROJECT) {
-        const bool proj = op == OP_PROJECT;
-        const uint32_t fl = proj ? __builtin_amdgcn_readfirstlane(sd.m) : 0u;
-        if (l == 0) {
-          L.match[0] = 0;
-          L.match[1] = 0;
-        }
-        if (proj) {  // the field name (<= kLeanNeedle bytes: the runtime checks)
-          if (__builtin_amdgcn_readfirstlane(L.nd_res)) {
-            const uint32_t o = __builtin_amdgcn_readfirstlane(sd.nd_off);
-            for (uint32_t t = l; t < fl; t += kLeanThreads) L.needle[t] = L.needles[o + t];
-          } else {
-            const uint8_t* nd = a.blob + __builtin_amdgcn_readfirstlane(sd.nd);
-            for (uint32_t t = l; t < fl; t += kLeanThreads) L.needle[t] = nd[t];
-          }
-        }
-        if (!cleared && nr > 0) {
-          clear_gaps(L, nr, vs, vl);
-          cleared = true;
-        }
-        lean_sync();
-        LEAN_MARK(2);
-        if (nr > 0 && lean_json_stage(L, nr, par, proj, fl JT_ARGS)) {
-          defer = true;
-          break;
-        }
-        LEAN_MARK(3);
-        alive &= __ballot(l < 64 && ((L.match[(l >> 5) & 1] >> (l & 31)) & 1u));
-        if (proj && (int)l < nr) {  // lane l keeps record l's (narrowed) value span
-          vs = L.r_vs[l];
-          vl = L.r_ve[l] - vs;
-        }
-        lean_sync();
-        continue;
-      }
-      const bool rx = op == OP_REGEX;
-      const uint32_t m = __builtin_amdgcn_readfirstlane(sd.m);
-      if (!rx && m == 0 && checked) continue;  // an empty needle keeps every (UTF-8) value
-      if (nr == 0) break;
-      const uint32_t lo = L.r_vs[0], hi = L.r_ve[nr - 1];
-      if (!cleared) {
-        clear_gaps(L, nr, vs, vl);
-        cleared = true;
-      }
-      if (l == 0) {
-        L.match[0] = 0;
-        L.match[1] = 0;
-      }
-      const bool upper = sd.upper != 0;
-      if (rx) {
-        if (__builtin_amdgcn_readfirstlane(L.tt_stage) != s) {  // several regex stages: rows per stage
-          const uint64_t* tt = (const uint64_t*)(a.blob + __builtin_amdgcn_readfirstlane(sd.tt));
-          lean_sync();  // every lane is done with the previous rows
-          for (uint32_t t = l; t < 256; t += kLeanThreads) L.tt[t] = tt[t];
-        }
-        lean_sync();
-        LEAN_MARK(2);
-        const uint32_t orw = lean_regex(L, nr, lo, hi, sd.max_len, sd.s_bot, sd.s_mid, sd.acc1, sd.acc2);
-        const bool high = lean_or(L.red, par, (orw & 0x80808080u) != 0u);  // also orders the match bits
-        LEAN_MARK(3);
-        if (!checked && high) defer = true;  // a non-ASCII value: exact UTF-8 / Unicode DFA path
-        checked = true;
-        const bool hit = l < 64 && ((L.match[(l >> 5) & 1] >> (l & 31)) & 1u);
-        alive &= __ballot(sd.keep_match ? hit : !hit);
-        lean_sync();  // match is rewritten by the next stage
-        continue;
-      }
-      if (m > (uint32_t)kLeanNeedle) {
-        defer = true;  // long needle: exact kernel
-        break;
-      }
-      if (__builtin_amdgcn_readfirstlane(L.nd_res)) {
-        const uint32_t o = __builtin_amdgcn_readfirstlane(sd.nd_off);
-        for (uint32_t t = l; t < m; t += kLeanThreads) L.needle[t] = L.needles[o + t];
-      } else {
-        const uint8_t* nd = a.blob + __builtin_amdgcn_readfirstlane(sd.nd);
-        for (uint32_t t = l; t < m; t += kLeanThreads) L.needle[t] = nd[t];
-      }
-      lean_sync();
-      LEAN_MARK(2);
-      uint32_t orw;
-      if (m >= 7) orw = lean_scan<0>(L, nr, lo, hi, nullptr, m, upper);
-      else if (m >= 4) orw = lean_scan<1>(L, nr, lo, hi, nullptr, m, upper);
-      else if (m > 0) orw = lean_scan<2>(L, nr, lo, hi, nullptr, m, upper);
-      else orw = lean_scan<3>(L, nr, lo, hi, nullptr, m, upper);
-      const bool high = lean_or(L.red, par, (orw & 0x80808080u) != 0u);  // also orders the match bits
-      if (!checked && high) defer = true;  // a non-ASCII value: exact UTF-8 path
-      checked = true;
-      if (m > 0) alive &= __ballot(l < 64 && ((L.match[(l >> 5) & 1] >> (l & 31)) & 1u));
-      LEAN_MARK(3);
-      lean_sync();  // match / needle are rewritten by the next stage
-    }
-    // 4. survivors -> descriptors (stored by the next iteration's flush)
-    p_b = b;
-    p_defer = defer;
-    p_kept = !defer && l < 64 && ((alive >> (l & 63)) & 1ull);
-    if (p_kept) {
-      p_idx = rb + __popcll(alive & ((1ull << l) - 1ull));
-      p_d.src = al + rs;
-      p_d.vpos = al + vs;
-      p_d.kpos = tag ? al + kpos : 0;
-      p_d.od = od;
-      p_d.ts = ts;
-      p_d.hdr = hdr;
-      p_d.vlen = vl;
-      p_d.klen = klen;
-      p_d.ival = 0;
-      p_d.mode = L.out_upper ? KM_UPPER : KM_COPY;
-      p_d.has_key = tag;
-      p_d.attr = attr;
-      p_d.pad = 0;
-    }
-    p_base = base_offset;
-    p_ts0 = first_ts;
-    p_comp = comp;
-    p_lod = lod_in;
-    p_nkeep = (uint32_t)__popcll(alive);
-    p_sec = sec_len;
-    flush();
-    LEAN_MARK(4);
-#ifdef FSG_LEAN_TIMING
-    lt_nb++;
-#endif
-    if (bn >= a.nbatches) break;
-    b = bn;
-  }
-#ifdef FSG_LEAN_TIMING
-  if (blockIdx.x < 2 && (threadIdx.x & 63u) == 0)
-    printf("lean wg %u wave %u batches %lu wait %lu frame %lu gaps %lu scan %lu tail %lu | j1 %lu j1b %lu j2 %lu j2c %lu j3a %lu j3b %lu\n",
-           blockIdx.x, threadIdx.x >> 6, (unsigned long)lt_nb, (unsigned long)lt_acc[0], (unsigned long)lt_acc[1],
-           (unsigned long)lt_acc[2], (unsigned long)lt_acc[3], (unsigned long)lt_acc[4], (unsigned long)lt_acc[6],
-           (unsigned long)lt_acc[7], (unsigned long)lt_acc[8], (unsigned long)lt_acc[9], (unsigned long)lt_acc[10],
-           (unsigned long)lt_acc[11]);
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -4635,26 +3405,6 @@ hipError_t upload_crc_tables() {
   return e;
 }
 
-// resident workgroups of k_eval_lean on the current device (CUs x occupancy)
-static uint32_t lean_grid(bool json) {
-  static std::mutex mu;
-  static uint32_t cache[64][2];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-  std::lock_guard<std::mutex> lock(mu);
-  uint32_t& c = cache[dev][json ? 1 : 0];
-  if (!c) {
-    int cus = 0, per = 0;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (json)
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_eval_lean<true>, kLeanThreads, 0);
-    else
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_eval_lean<false>, kLeanThreads, 0);
-    c = (uint32_t)std::max(1, cus) * (uint32_t)std::max(1, per);
-  }
-  return c;
-}
-
 void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s) {
   if (!a.nbatches) return;
   const size_t dyn = (ops & opbit(OP_REGEX)) ? kDfaDyn : 0;
@@ -4666,14 +3416,8 @@ void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s) {
     launch_array_lean(a, s);
     grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list
   } else if (mode == EVAL_LEAN) {
-    // persistent: as many workgroups as fit on the device at once
-    const bool json = (ops & (opbit(OP_FILTER_JSON) | opbit(OP_PROJECT))) != 0;
-    const uint32_t g = std::min<uint32_t>(a.nbatches, lean_grid(json));
-    hipLaunchKernelGGL(k_chase, dim3((a.nbatches + kChaseT - 1) / kChaseT), dim3(kChaseT), 0, s, a);
-    if (json)
-      hipLaunchKernelGGL(k_eval_lean<true>, dim3(g), dim3(kLeanThreads), 0, s, a);
-    else
-      hipLaunchKernelGGL(k_eval_lean<false>, dim3(g), dim3(kLeanThreads), 0, s, a);
+    // k_chase + k_eval_lean (fsg_lean.hip)
+    launch_eval_lean(a, ops, s);
     grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list
   } else {
     e.list = nullptr;

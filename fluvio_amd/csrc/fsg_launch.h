@@ -11,6 +11,8 @@ hipError_t upload_crc_tables();
 // EVAL_ARRAY = k_arr_frame + k_arr_lean (fsg_array.hip), then k_eval over its deferred list
 enum EvalMode { EVAL_EXACT = 0, EVAL_LEAN = 1, EVAL_ARRAY = 3 };
 void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s);
+// k_chase + k_eval_lean (fsg_lean.hip), the kernel variant picked by the chain's stage ops
+void launch_eval_lean(const EvalArgs& a, uint32_t ops, hipStream_t s);
 // array_map_json_array alone over the source values (fsg_array.hip)
 bool array_lean_eligible(const ChainDesc& ch, uint32_t ops);
 void launch_array_lean(const EvalArgs& a, hipStream_t s);
