@@ -265,7 +265,7 @@ struct EvalArgs {
   const uint64_t* bpos;
   const uint64_t* rbase;
   uint32_t nbatches;
-  uint32_t pad;
+  uint32_t flat_st;    // EVAL_FLAT: the substring stage of the flat path
   const ChainDesc* chain;
   const uint8_t* blob;
   BatchStat* bstat;
@@ -280,6 +280,9 @@ struct EvalArgs {
                        // an earlier segment's partial output before its error), nullptr: none
   ArrBatch* arr_b;     // array_map lean path: per batch element statistics ...
   uint32_t* arr_bm;    // ... and element bitmaps (kArrBmBatch words per batch)
+  unsigned long long* fbm;  // flat substring path (fsg_lean.hip): a bit per 16-byte chunk of the slice,
+                            // occurrence starts [0, fbm_words), then bytes >= 0x80 [fbm_words, 2 fbm_words)
+  uint64_t fbm_words;
 };
 
 struct SizeArgs {

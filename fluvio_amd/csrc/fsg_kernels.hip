@@ -3415,9 +3415,12 @@ void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s) {
     // takes the deferred batches' record starts from k_arr_frame where it framed them
     launch_array_lean(a, s);
     grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list
-  } else if (mode == EVAL_LEAN) {
-    // k_chase + k_eval_lean (fsg_lean.hip)
-    launch_eval_lean(a, ops, s);
+  } else if (mode == EVAL_LEAN || mode == EVAL_FLAT) {
+    // k_chase + k_eval_lean, or the flat substring kernels (fsg_lean.hip)
+    if (mode == EVAL_FLAT)
+      launch_eval_flat(a, a.flat_st, s);
+    else
+      launch_eval_lean(a, ops, s);
     grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list
   } else {
     e.list = nullptr;

@@ -9,10 +9,15 @@ hipError_t upload_crc_tables();
 // ops: bit per StageOp in the chain.  mode: EVAL_EXACT = k_eval over every
 // batch; EVAL_LEAN = k_chase + k_eval_lean, then k_eval over its deferred list;
 // EVAL_ARRAY = k_arr_frame + k_arr_lean (fsg_array.hip), then k_eval over its deferred list
-enum EvalMode { EVAL_EXACT = 0, EVAL_LEAN = 1, EVAL_ARRAY = 3 };
+// EVAL_FLAT = k_chase + k_flat_scan + k_flat_decide (a.flat_st, a.fbm), then k_eval over the deferred list
+enum EvalMode { EVAL_EXACT = 0, EVAL_LEAN = 1, EVAL_ARRAY = 3, EVAL_FLAT = 4 };
 void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s);
 // k_chase + k_eval_lean (fsg_lean.hip), the kernel variant picked by the chain's stage ops
 void launch_eval_lean(const EvalArgs& a, uint32_t ops, hipStream_t s);
+// the flat substring path (fsg_lean.hip): the chain's one substring stage (needle 4..128 bytes, with
+// only uppercase maps beside it) or -1; k_chase + k_flat_scan + k_flat_decide over a.fbm
+int flat_stage(const ChainDesc& ch, uint32_t ops);
+void launch_eval_flat(const EvalArgs& a, uint32_t stage, hipStream_t s);
 // array_map_json_array alone over the source values (fsg_array.hip)
 bool array_lean_eligible(const ChainDesc& ch, uint32_t ops);
 void launch_array_lean(const EvalArgs& a, hipStream_t s);

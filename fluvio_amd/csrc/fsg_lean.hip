@@ -1286,6 +1286,277 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kK
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// Flat substring path: a chain whose one scanning stage is a substring filter
+// (filter / filter_init / filter_with_param: value.contains(needle), needle of
+// 4..128 bytes) decouples streaming from the batch structure:
+//   k_flat_scan   every byte of the slice once, as a flat array (headers and
+//                 gaps included): one 16-byte chunk a lane, 4 rounds of 1 KiB
+//                 per wave in flight; per chunk two bits: "a needle occurrence
+//                 starts here" (every position's 4-gram against the needle's
+//                 first 4 bytes, candidates verified in full) and "a byte
+//                 >= 0x80 here"; one 64-bit ballot store per bitmap per round
+//   k_flat_decide one wave per batch: lane r frames record r from its start
+//                 (k_chase) with the header in registers, then decides from
+//                 the bitmaps over its value [vs, ve): a start bit in a chunk
+//                 whose every start lies in [vs, ve - m] is a match; start
+//                 bits in the edge chunks and high bits in a chunk holding
+//                 gap bytes are re-checked on the bytes; any non-ASCII value,
+//                 unusual framing or batch shape defers the batch to k_eval
+// The batch results (BatchStat, KeptRec) are those k_eval_lean writes.
+// ---------------------------------------------------------------------------
+constexpr int kFlatRounds = 4;  // 1 KiB rounds per wave in flight
+__device__ __forceinline__ bool flat_verify(const uint8_t* s, uint64_t p, const uint8_t* nd, uint32_t m, bool upper) {
+  for (uint32_t t = 4; t < m; t += 4) {
+    uint32_t x = ld_u32_at(s + p + t);
+    if (upper) x = swar_upper(x);
+    const uint32_t k = m - t >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (m - t))) - 1u);
+    if ((x ^ ld_u32_at(nd + t)) & k) return false;
+  }
+  return true;
+}
+__global__ __launch_bounds__(256) void k_flat_scan(EvalArgs a, uint32_t stage) {
+  const StageDesc& sd = a.chain->st[stage];
+  const uint32_t m = sd.needle_len;
+  const bool upper = sd.in_type == VT_SRC_UPPER;
+  const uint8_t* nd = a.blob + sd.needle;
+  const uint32_t n4 = ld_u32_at(nd);
+  const uint32_t lane = lane_id();
+  const uint64_t nrounds = a.fbm_words;  // 1 KiB rounds of the slice
+  const uint64_t w0 = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  unsigned long long* hit_bm = a.fbm;
+  unsigned long long* hi_bm = a.fbm + a.fbm_words;
+  for (uint64_t r0 = w0 * kFlatRounds; r0 < nrounds; r0 += nw * kFlatRounds) {
+    uint4 v[kFlatRounds];
+    uint32_t nx[kFlatRounds];
+#pragma unroll
+    for (int i = 0; i < kFlatRounds; i++) {  // every round's loads in flight before the first use
+      const uint64_t c = (r0 + i) * 1024 + lane * 16;
+      v[i] = r0 + i < nrounds ? *(const uint4*)(a.slice + c) : make_uint4(0, 0, 0, 0);
+      nx[i] = r0 + i < nrounds ? *(const uint32_t*)(a.slice + c + 16) : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < kFlatRounds; i++) {
+      if (r0 + i >= nrounds) break;  // uniform
+      const uint64_t c = (r0 + i) * 1024 + lane * 16;
+      uint32_t w[5] = {v[i].x, v[i].y, v[i].z, v[i].w, nx[i]};
+      const bool high = ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) != 0u;
+      if (upper) {
+#pragma unroll
+        for (int k = 0; k < 5; k++) w[k] = swar_upper(w[k]);
+      }
+      uint32_t cand = 0;
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const uint32_t x = (j & 3) ? __builtin_amdgcn_alignbyte(w[(j >> 2) + 1], w[j >> 2], (uint32_t)(j & 3)) : w[j >> 2];
+        cand |= (uint32_t)(x == n4) << j;
+      }
+      bool hit = false;
+      while (cand && !hit) {  // rare: the rest of the needle
+        const uint32_t j = (uint32_t)__builtin_ctz(cand);
+        cand &= cand - 1;
+        hit = flat_verify(a.slice, c + j, nd, m, upper);
+      }
+      const uint64_t hb = __ballot(hit), hh = __ballot(high);
+      if (lane == 0) {
+        hit_bm[r0 + i] = hb;
+        hi_bm[r0 + i] = hh;
+      }
+    }
+  }
+}
+// bits [c0, c1) of a bitmap: any set
+__device__ __forceinline__ bool flat_any(const unsigned long long* bm, uint64_t c0, uint64_t c1) {
+  for (uint64_t c = c0; c < c1;) {
+    const uint64_t w = c >> 6, lo = c & 63;
+    const uint64_t hi = (c1 - (w << 6)) < 64 ? (c1 - (w << 6)) : 64;
+    const uint64_t mask = (hi == 64 ? ~0ull : ((1ull << hi) - 1ull)) & ~((1ull << lo) - 1ull);
+    if (bm[w] & mask) return true;
+    c = (w + 1) << 6;
+  }
+  return false;
+}
+__global__ __launch_bounds__(256) void k_flat_decide(EvalArgs a, uint32_t stage) {
+  const StageDesc& sd = a.chain->st[stage];
+  const uint32_t m = sd.needle_len;
+  const bool upper = sd.in_type == VT_SRC_UPPER;
+  const bool keep_match = sd.keep_match != 0;
+  const bool out_upper = a.chain->out_type == VT_SRC_UPPER;
+  const uint8_t* nd = a.blob + sd.needle;
+  const uint32_t n4 = ld_u32_at(nd);
+  const unsigned long long* hit_bm = a.fbm;
+  const unsigned long long* hi_bm = a.fbm + a.fbm_words;
+  const uint32_t l = lane_id();
+  const uint32_t nw = gridDim.x * 4;
+  for (uint32_t b = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); b < a.nbatches; b += nw) {
+    const uint64_t pos = a.bpos[b];
+    const uint64_t nxt = b + 1 < a.nbatches ? a.bpos[b + 1] : a.slice_len;
+    const uint64_t al = pos & ~15ull;
+    uint64_t wl = nxt > al ? nxt - al : 0;
+    if (wl > (uint64_t)kLeanWin) wl = kLeanWin;
+    const uint32_t wlen = (uint32_t)((wl + 15) & ~15ull);
+    const uint8_t* h = a.slice + pos;
+    const uint32_t batch_len = __builtin_bswap32(ld_u32_at(h + 8));
+    const uint64_t sec0 = pos + 57, sec_end = pos + 12 + (uint64_t)batch_len;
+    const uint32_t sec_len = (uint32_t)(sec_end - sec0);
+    const int32_t count = sec_len >= 4 ? (int32_t)__builtin_bswap32(ld_u32_at(a.slice + sec0)) : -1;
+    const uint32_t re = a.rend[b];
+    bool defer = sec_len < 4 || sec_end - al > (uint64_t)wlen || count < 0 || count > kLeanMaxR || re == 0xFFFFu;
+    const int nr = defer ? 0 : count;
+    const uint64_t rb = a.rbase[b];
+    const uint32_t rs = (int)l < nr ? a.rstart[rb + l] : 0u;
+    const uint32_t rs_next = __shfl_down(rs, 1, 64);
+    bool g = true, match = false;
+    int64_t ts = 0, od = 0, hdr = 0;
+    uint32_t vs = 0, vl = 0, kpos = 0, klen = 0;
+    uint8_t attr = 0, tag = 0;
+    if ((int)l < nr) {
+      // the record's header in registers: 24 bytes from its start (aligned dwords)
+      const uint32_t lim = (int)l + 1 == nr ? re : rs_next;
+      const uint64_t ra = al + rs, a0 = ra & ~3ull;
+      uint32_t x[6];
+#pragma unroll
+      for (int k = 0; k < 6; k++) x[k] = *(const uint32_t*)(a.slice + a0 + 4 * k);
+      uint32_t o = (uint32_t)(ra & 3), n;
+      int64_t len, kl = 0, vlen;
+      auto at = [&](uint32_t q) {  // bytes [q, q + 4) of x, q < 20
+        const uint32_t d = q >> 2;
+        uint32_t lo = x[0], hi = x[1];
+#pragma unroll
+        for (uint32_t k = 1; k < 5; k++)
+          if (d == k) {
+            lo = x[k];
+            hi = x[k + 1];
+          }
+        return __builtin_amdgcn_alignbyte(hi, lo, q & 3u);
+      };
+      auto var4 = [](uint32_t w, int64_t& val) {  // a varint of <= 4 bytes: its length (0: longer)
+        const uint32_t term = ~w & 0x80808080u;
+        const uint32_t nb = term ? (((uint32_t)__builtin_ctz(term)) >> 3) + 1 : 0u;
+        const uint32_t y = nb == 4 ? w : (w & ((1u << (8 * nb)) - 1u));
+        const uint32_t u = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
+        val = (int64_t)(u >> 1) ^ -(int64_t)(u & 1u);
+        return nb;
+      };
+      bool ok = true;
+      n = var4(at(o), len);
+      ok = ok && n != 0;
+      o += n;
+      attr = (uint8_t)at(o);
+      o += 1;
+      n = var4(at(o), ts);
+      ok = ok && n != 0;
+      o += n;
+      n = var4(at(o), od);
+      ok = ok && n != 0;
+      o += n;
+      tag = (uint8_t)at(o);
+      o += 1;
+      ok = ok && tag <= 1;
+      uint64_t q = a0 + o;  // absolute
+      if (ok && tag == 1) {
+        n = var4(at(o), kl);
+        ok = n != 0 && kl >= 0;
+        q += n;
+        kpos = (uint32_t)(q - al);
+        klen = (uint32_t)kl;
+        q += klen;
+      }
+      if (ok) {
+        n = var4(tag == 1 ? ld_u32_at(a.slice + q) : at(o), vlen);
+        ok = n != 0 && vlen >= 0;
+        q += n;
+        vs = (uint32_t)(q - al);
+        vl = (uint32_t)vlen;
+        ok = ok && (uint64_t)vs + vl <= lim;
+      }
+      if (ok) {
+        n = var4(ld_u32_at(a.slice + al + vs + vl), hdr);
+        ok = n != 0 && vs + vl + n == lim;
+      }
+      g = ok;
+      if (g) {
+        // bits over the value [va, ve): chunks c = byte >> 4
+        const uint64_t va = al + vs, ve = va + vl;
+        if (vl) {
+          const uint64_t c0 = va >> 4, c1 = (ve + 15) >> 4;   // chunks touching the value
+          const uint64_t i0 = (va + 15) >> 4, i1 = ve >> 4;  // chunks inside the value
+          bool hi = i0 < i1 && flat_any(hi_bm, i0, i1);
+          auto hi_exact = [&](uint64_t c) {  // the value bytes of chunk c
+            const uint64_t lo = c << 4 > va ? c << 4 : va, e = (c << 4) + 16 < ve ? (c << 4) + 16 : ve;
+            bool f = false;
+            for (uint64_t p = lo; p < e; p++) f |= a.slice[p] >= 0x80;
+            return f;
+          };
+          if (!hi && c0 < i0 && ((hi_bm[c0 >> 6] >> (c0 & 63)) & 1ull)) hi = hi_exact(c0);
+          if (!hi && i1 < c1 && (i1 >= i0 || c0 != i1) && ((hi_bm[i1 >> 6] >> (i1 & 63)) & 1ull)) hi = hi_exact(i1);
+          g = !hi;
+        }
+        if (g && vl >= m) {
+          // starts in [va, ve - m]: chunks whose every start is inside need no check
+          const uint64_t sl = ve - m;  // last valid start
+          const uint64_t j0 = (va + 15) >> 4, j1 = (sl + 1) >> 4;  // chunks fully inside [va, sl]
+          match = j0 < j1 && flat_any(hit_bm, j0, j1);
+          auto hit_exact = [&](uint64_t c) {  // starts of chunk c inside [va, sl]
+            const uint64_t lo = c << 4 > va ? c << 4 : va, e = (c << 4) + 15 < sl ? (c << 4) + 15 : sl;
+            bool f = false;
+            for (uint64_t p = lo; p <= e && !f; p++) {
+              uint32_t x0 = ld_u32_at(a.slice + p);
+              if (upper) x0 = swar_upper(x0);
+              f = x0 == n4 && flat_verify(a.slice, p, nd, m, upper);
+            }
+            return f;
+          };
+          const uint64_t e0 = va >> 4, e1 = sl >> 4;  // chunks holding some valid start
+          if (!match && e0 < j0 && ((hit_bm[e0 >> 6] >> (e0 & 63)) & 1ull)) match = hit_exact(e0);
+          if (!match && e1 >= j1 && e1 != (e0 < j0 ? e0 : ~0ull) && ((hit_bm[e1 >> 6] >> (e1 & 63)) & 1ull))
+            match = hit_exact(e1);
+        }
+      }
+    }
+    defer = defer || __ballot((int)l < nr && !g) != 0;
+    const bool keep = keep_match ? match : !match;
+    const uint64_t alive = __ballot((int)l < nr && keep);
+    if (defer) {
+      if (l == 0) {
+        const uint32_t i = atomicAdd(&a.list[0], 1u);
+        a.list[1 + i] = b;
+      }
+      continue;
+    }
+    if ((alive >> l) & 1ull) {
+      KeptRec d;
+      d.src = al + rs;
+      d.vpos = al + vs;
+      d.kpos = tag ? al + kpos : 0;
+      d.od = od;
+      d.ts = ts;
+      d.hdr = hdr;
+      d.vlen = vl;
+      d.klen = klen;
+      d.ival = 0;
+      d.mode = out_upper ? KM_UPPER : KM_COPY;
+      d.has_key = tag;
+      d.attr = attr;
+      d.pad = 0;
+      a.desc[rb + __popcll(alive & ((1ull << l) - 1ull))] = d;
+    }
+    if (l == 0) {  // batch header (file format, batch.rs:163-180)
+      BatchStat st = {};
+      st.base_offset = (int64_t)rd_be(h, 8);
+      st.lod_in = (int32_t)rd_be(h + 23, 4);
+      st.first_ts = (int64_t)rd_be(h + 27, 8);
+      st.comp = (uint32_t)h[22] & 7u;
+      st.flags = BF_LAST_STAGE;
+      st.nkeep = st.nout = (uint32_t)__popcll(alive);
+      st.sec_len = sec_len;
+      st.err_stage = 0xFFFFFFFFu;
+      a.bstat[b] = st;
+    }
+  }
+}
+
 // resident workgroups of k_eval_lean<kind> on the current device (CUs x occupancy)
 template <int kKind>
 static uint32_t lean_grid() {
@@ -1308,6 +1579,29 @@ static void launch_lean_kind(const EvalArgs& a, hipStream_t s) {
   // persistent: as many workgroups as fit on the device at once
   const uint32_t g = std::min<uint32_t>(a.nbatches, lean_grid<kKind>());
   hipLaunchKernelGGL(k_eval_lean<kKind>, dim3(g), dim3(kLeanThreads), 0, s, a);
+}
+
+int flat_stage(const ChainDesc& ch, uint32_t ops) {
+  if (ops & ~((1u << OP_CONTAINS) | (1u << OP_MAP_UPPER))) return -1;
+  int st = -1;
+  for (uint32_t k = 0; k < ch.nstages; k++)
+    if (ch.st[k].op == OP_CONTAINS) {
+      if (st >= 0) return -1;  // more than one substring stage: k_eval_lean
+      st = (int)k;
+    }
+  if (st < 0) return -1;
+  const uint32_t m = ch.st[st].needle_len;
+  return m >= 4 && m <= (uint32_t)kLeanNeedle ? st : -1;
+}
+
+void launch_eval_flat(const EvalArgs& a, uint32_t stage, hipStream_t s) {
+  if (!a.nbatches) return;
+  hipLaunchKernelGGL(k_chase, dim3((a.nbatches + kChaseT - 1) / kChaseT), dim3(kChaseT), 0, s, a);
+  const uint64_t waves = (a.fbm_words + kFlatRounds - 1) / kFlatRounds;
+  const uint32_t g1 = (uint32_t)std::min<uint64_t>((waves + 3) / 4, 4096);
+  hipLaunchKernelGGL(k_flat_scan, dim3(std::max<uint32_t>(g1, 1)), dim3(256), 0, s, a, stage);
+  const uint32_t g2 = std::min<uint32_t>((a.nbatches + 3) / 4, 8192);
+  hipLaunchKernelGGL(k_flat_decide, dim3(g2), dim3(256), 0, s, a, stage);
 }
 
 void launch_eval_lean(const EvalArgs& a, uint32_t ops, hipStream_t s) {

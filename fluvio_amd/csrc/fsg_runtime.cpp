@@ -529,6 +529,8 @@ struct fsg_chain {
   // scratch
   DevBuf bstat, kept, rows, pre, aggpre, tiles, grand, mins, plan, out, crcparts, defer, elem, cat;
   DevBuf arr_b, arr_bm;  // lean array_map statistics and element bitmaps (per batch)
+  DevBuf fbm;            // flat substring path: occurrence / high-byte bits per 16-byte chunk
+  bool no_flat = getenv("FSG_NO_FLAT") != nullptr;  // A/B: the flat path off (k_eval_lean instead)
   // the one-batch process() path (k_one): zeros for bpos / rbase, the device
   // block Plan | BatchStat | Mins | output batch, and coherent pinned memory
   // the kernel reads the input from and writes the block back to (no copies)
@@ -2043,8 +2045,21 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
       ea.arr_bm = c->arr_bm.as<uint32_t>();
     }
   }
+  // one substring stage: the flat path (the slice streamed once as bytes,
+  // per-16-byte-chunk occurrence / high-byte bits, then one wave per batch decides)
+  const int fst = lean ? flat_stage(c->hdesc, ops) : -1;
+  bool flat = false;
+  if (fst >= 0 && !c->no_flat) {
+    ea.fbm_words = (s->len + 1023) / 1024;
+    flat = c->fbm.ensure((size_t)ea.fbm_words * 16) == hipSuccess;
+    (void)hipGetLastError();
+    if (flat) {
+      ea.fbm = c->fbm.as<unsigned long long>();
+      ea.flat_st = (uint32_t)fst;
+    }
+  }
   if (lean || arr) HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
-  launch_eval(ea, ops, lean ? EVAL_LEAN : arr ? EVAL_ARRAY : EVAL_EXACT, st);
+  launch_eval(ea, ops, flat ? EVAL_FLAT : lean ? EVAL_LEAN : arr ? EVAL_ARRAY : EVAL_EXACT, st);
   HIPCHK(hipGetLastError());
   if (c->timed) HIPCHK(hipEventRecord(c->ev[1], st));
   launch_mins(ea.bstat, nb, ea.mins, st);
@@ -2264,7 +2279,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   if (dedup) HIPCHK(hipMemcpyAsync(sfs, sfa.scal, sizeof sfs, hipMemcpyDeviceToHost, st));
   HIPCHK(wait_stream(st));
   memcpy(&c->hplan, c->hpin.p, sizeof(Plan));
-  c->last.eval_path = lean ? FSG_EVAL_LEAN : arr ? FSG_EVAL_ARRAY : FSG_EVAL_EXACT;
+  c->last.eval_path = flat ? FSG_EVAL_FLAT : lean ? FSG_EVAL_LEAN : arr ? FSG_EVAL_ARRAY : FSG_EVAL_EXACT;
   c->last.deferred = 0;
   if (lean || arr) memcpy(&c->last.deferred, (const uint8_t*)c->hpin.p + sizeof(Plan), sizeof(uint32_t));
   if (dedup) {

@@ -161,7 +161,7 @@ typedef struct fsg_timings {
   uint64_t out_bytes;     /* algorithmic bytes written (output batch) */
   uint64_t n_batches;
   uint64_t n_records_in;
-  uint32_t eval_path;     /* FSG_EVAL_EXACT / FSG_EVAL_LEAN / FSG_EVAL_FLAT: the first evaluation kernel */
+  uint32_t eval_path;     /* FSG_EVAL_EXACT / _LEAN / _ARRAY / _FLAT: the first evaluation kernel */
   uint32_t deferred;      /* batches that kernel handed to the exact kernel (non-ASCII, odd framing, ...) */
   float text_ms;          /* plan end to write start: aggregate texts, the aggregate-json order walk, the header */
   float order_ms;         /* the aggregate-json order walk kernel alone (a group call: the group's one launch) */
@@ -170,6 +170,8 @@ typedef struct fsg_timings {
 #define FSG_EVAL_LEAN 1  /* k_eval_lean (LDS windows), deferred batches through k_eval */
 /* 2: retired (an opt-in register-resident substring path, slower than k_eval_lean on MI355X) */
 #define FSG_EVAL_ARRAY 3 /* k_arr_lean (array_map lane per record), deferred batches through k_eval */
+#define FSG_EVAL_FLAT 4  /* one substring stage: the slice streamed as bytes (k_flat_scan), a wave per batch
+                            decides (k_flat_decide), deferred batches through k_eval */
 
 const char *fsg_last_error_message(void);
 int fsg_abi_version(void);

@@ -1600,7 +1600,11 @@ def test_flat_path_parity(engine, ci, seed):
     g = gpu_chain(engine, chain)
     g.process_batch(sl)
     t = g.last_timings()
-    assert t["eval_path"] == 1, t  # FSG_EVAL_LEAN
+    # one substring stage with a needle of >= 4 bytes: the flat path (FSG_EVAL_FLAT),
+    # else k_eval_lean (FSG_EVAL_LEAN)
+    subs = [m for m in chain if m[0] == "filter_init"]
+    flat = len(subs) == 1 and len(subs[0][1]["key"]) >= 4
+    assert t["eval_path"] == (4 if flat else 1), t
     assert 0 < t["deferred"] < t["n_batches"], t  # the non-ASCII / 65-record batches go to k_eval
     # the same chain over the synthetic C2 logs: nothing deferred
     sl2 = synth.make_slice(2, 3000, base_offset=9)
@@ -1608,7 +1612,8 @@ def test_flat_path_parity(engine, ci, seed):
 
 
 def test_flat_needle_at_window_edges(engine):
-    """A 7-byte needle at every offset around 16-byte chunks and 1 KiB loads."""
+    """A 7-byte needle at every offset around 16-byte chunks and 1 KiB loads
+    (the flat path's edge chunks: starts before the value, ends past it)."""
     for shift in range(0, 40, 3):
         b = P.Batch(base_offset=100 + shift)
         for i in range(16):
@@ -1618,6 +1623,37 @@ def test_flat_needle_at_window_edges(engine):
         b2 = P.Batch(base_offset=200)
         b2.add_record(P.Record.new(b"timeou"))
         check_batch(engine, [("filter_init", {"key": "timeout"}, None)], b.encode() + b2.encode())
+
+
+def test_flat_edges_exhaustive(engine):
+    """The flat path's per-chunk bits against every value / chunk alignment:
+    values of 0..40 bytes at every offset, the needle at every position of the
+    value and just outside it (in the record header and trailer bytes), a
+    needle byte in the previous record's value, high bytes in the header
+    varints only (ASCII values) and in the value (deferred)."""
+    out, base = b"", 0
+    for vlen in list(range(0, 41)) + [255, 1000]:
+        b = P.Batch(base_offset=base)
+        for pos in range(-3, vlen + 2, 1 if vlen < 41 else 97):
+            v = bytearray(b"a" * vlen)
+            if 0 <= pos and pos + 4 <= vlen:
+                v[pos:pos + 4] = b"tiMe"
+            elif pos < 0 and vlen >= 4 + pos:
+                v[0:4 + pos] = b"tiMe"[-pos:]  # a partial needle at the value start
+            elif pos > vlen - 4 and pos < vlen:
+                v[pos:] = b"tiMe"[: vlen - pos]  # a partial needle at the value end
+            b.add_record(P.Record.new_key_value(b"ti" if pos % 5 == 0 else None, bytes(v)))
+        out += b.encode()
+        base += 200
+    hb = P.Batch(base_offset=base)
+    for i in range(20):
+        hb.add_record(P.Record.new(("x" * (i * 9) + "tiMe" + "\u00e9" * (i % 2)).encode()))
+    out += hb.encode()
+    for needle in ["tiMe", "tiMea", "atiMe"]:
+        g = gpu_chain(engine, [("filter_init", {"key": needle}, None)])
+        check_batch(engine, [("filter_init", {"key": needle}, None)], out)
+        g.process_batch(out)
+        assert g.last_timings()["eval_path"] == 4
 
 
 @pytest.mark.parametrize("nr", range(2, 9))
