@@ -265,7 +265,7 @@ struct EvalArgs {
   const uint64_t* bpos;
   const uint64_t* rbase;
   uint32_t nbatches;
-  uint32_t flat_st;    // EVAL_FLAT: the substring stage of the flat path
+  uint32_t flat_st;    // EVAL_FLAT: the substring stage of the flat path | its needle length << 8
   const ChainDesc* chain;
   const uint8_t* blob;
   BatchStat* bstat;

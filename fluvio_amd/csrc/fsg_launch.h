@@ -17,7 +17,7 @@ void launch_eval_lean(const EvalArgs& a, uint32_t ops, hipStream_t s);
 // the flat substring path (fsg_lean.hip): the chain's one substring stage (needle 4..128 bytes, with
 // only uppercase maps beside it) or -1; k_chase + k_flat_scan + k_flat_decide over a.fbm
 int flat_stage(const ChainDesc& ch, uint32_t ops);
-void launch_eval_flat(const EvalArgs& a, uint32_t stage, hipStream_t s);
+void launch_eval_flat(const EvalArgs& a, uint32_t flat_st, hipStream_t s);
 // array_map_json_array alone over the source values (fsg_array.hip)
 bool array_lean_eligible(const ChainDesc& ch, uint32_t ops);
 void launch_array_lean(const EvalArgs& a, hipStream_t s);

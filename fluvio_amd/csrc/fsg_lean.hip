@@ -1293,21 +1293,30 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kK
 //   k_flat_scan   every byte of the slice once, as a flat array (headers and
 //                 gaps included): one 16-byte chunk a lane, 4 rounds of 1 KiB
 //                 per wave in flight; per chunk two bits: "a needle occurrence
-//                 starts here" (every position's 4-gram against the needle's
-//                 first 4 bytes, candidates verified in full) and "a byte
-//                 >= 0x80 here"; one 64-bit ballot store per bitmap per round
-//   k_flat_decide one wave per batch: lane r frames record r from its start
-//                 (k_chase) with the header in registers, then decides from
-//                 the bitmaps over its value [vs, ve): a start bit in a chunk
-//                 whose every start lies in [vs, ve - m] is a match; start
-//                 bits in the edge chunks and high bits in a chunk holding
-//                 gap bytes are re-checked on the bytes; any non-ASCII value,
-//                 unusual framing or batch shape defers the batch to k_eval
+//                 is anchored here" and "a byte >= 0x80 here", stored as one
+//                 64-bit ballot per bitmap per round.  Needles of >= 7 bytes:
+//                 every occurrence covers an aligned dword; each aligned dword
+//                 is compared with the needle's 4-grams at offsets 0..3 and an
+//                 occurrence is anchored at the chunk of its first covered
+//                 aligned dword (starts in [16 C - 3, 16 C + 12]).  Needles of
+//                 4..6 bytes: the 4-gram at each of the 16 positions, anchored
+//                 at the chunk of its start.  Candidates are verified in full.
+//   k_flat_decide one thread per batch (the k_chase walk): each record framed
+//                 from its header bytes (one 24-byte read, varints decoded in
+//                 registers, the trailing headers varint checked where the
+//                 length says the record ends), then decided from the bits
+//                 over its value: anchors whose every start lies in [vs, ve - m]
+//                 match, edge chunks are re-checked on their bytes (the
+//                 record's own lines); a high bit in a chunk of the value
+//                 (exact at the edges: gap bytes hold varint continuation
+//                 bytes) defers the batch.  Anything unusual (more than 64
+//                 records, a varint over 4 bytes, framing that does not close)
+//                 defers the batch to k_eval.
 // The batch results (BatchStat, KeptRec) are those k_eval_lean writes.
 // ---------------------------------------------------------------------------
 constexpr int kFlatRounds = 4;  // 1 KiB rounds per wave in flight
 __device__ __forceinline__ bool flat_verify(const uint8_t* s, uint64_t p, const uint8_t* nd, uint32_t m, bool upper) {
-  for (uint32_t t = 4; t < m; t += 4) {
+  for (uint32_t t = 0; t < m; t += 4) {
     uint32_t x = ld_u32_at(s + p + t);
     if (upper) x = swar_upper(x);
     const uint32_t k = m - t >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (m - t))) - 1u);
@@ -1315,12 +1324,15 @@ __device__ __forceinline__ bool flat_verify(const uint8_t* s, uint64_t p, const 
   }
   return true;
 }
+template <bool kLong>  // kLong: m >= 7, aligned dwords against the 4 offsets
 __global__ __launch_bounds__(256) void k_flat_scan(EvalArgs a, uint32_t stage) {
   const StageDesc& sd = a.chain->st[stage];
   const uint32_t m = sd.needle_len;
   const bool upper = sd.in_type == VT_SRC_UPPER;
   const uint8_t* nd = a.blob + sd.needle;
-  const uint32_t n4 = ld_u32_at(nd);
+  uint32_t rot[4];
+#pragma unroll
+  for (int d = 0; d < 4; d++) rot[d] = ld_u32_at(nd + (kLong ? d : 0));
   const uint32_t lane = lane_id();
   const uint64_t nrounds = a.fbm_words;  // 1 KiB rounds of the slice
   const uint64_t w0 = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -1334,29 +1346,40 @@ __global__ __launch_bounds__(256) void k_flat_scan(EvalArgs a, uint32_t stage) {
     for (int i = 0; i < kFlatRounds; i++) {  // every round's loads in flight before the first use
       const uint64_t c = (r0 + i) * 1024 + lane * 16;
       v[i] = r0 + i < nrounds ? *(const uint4*)(a.slice + c) : make_uint4(0, 0, 0, 0);
-      nx[i] = r0 + i < nrounds ? *(const uint32_t*)(a.slice + c + 16) : 0u;
+      if (!kLong) nx[i] = r0 + i < nrounds ? *(const uint32_t*)(a.slice + c + 16) : 0u;
     }
 #pragma unroll
     for (int i = 0; i < kFlatRounds; i++) {
       if (r0 + i >= nrounds) break;  // uniform
       const uint64_t c = (r0 + i) * 1024 + lane * 16;
-      uint32_t w[5] = {v[i].x, v[i].y, v[i].z, v[i].w, nx[i]};
+      uint32_t w[5] = {v[i].x, v[i].y, v[i].z, v[i].w, kLong ? 0u : nx[i]};
       const bool high = ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) != 0u;
       if (upper) {
 #pragma unroll
         for (int k = 0; k < 5; k++) w[k] = swar_upper(w[k]);
       }
-      uint32_t cand = 0;
+      // min over the compare differences: zero iff some 4-gram hits
+      uint32_t z = 0xFFFFFFFFu;
+      if (kLong) {
 #pragma unroll
-      for (int j = 0; j < 16; j++) {
-        const uint32_t x = (j & 3) ? __builtin_amdgcn_alignbyte(w[(j >> 2) + 1], w[j >> 2], (uint32_t)(j & 3)) : w[j >> 2];
-        cand |= (uint32_t)(x == n4) << j;
+        for (int k = 0; k < 4; k++) z = min(z, min(min(w[k] ^ rot[0], w[k] ^ rot[1]), min(w[k] ^ rot[2], w[k] ^ rot[3])));
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+          z = min(z, ((j & 3) ? __builtin_amdgcn_alignbyte(w[(j >> 2) + 1], w[j >> 2], (uint32_t)(j & 3)) : w[j >> 2]) ^ rot[0]);
       }
       bool hit = false;
-      while (cand && !hit) {  // rare: the rest of the needle
-        const uint32_t j = (uint32_t)__builtin_ctz(cand);
-        cand &= cand - 1;
-        hit = flat_verify(a.slice, c + j, nd, m, upper);
+      if (z == 0u) {  // rare: find the candidates, verify the whole needle
+        if (kLong) {
+          for (int k = 0; k < 4 && !hit; k++)
+            for (int d = 0; d < 4 && !hit; d++)
+              if (w[k] == rot[d] && c + 4 * k >= (uint64_t)d) hit = flat_verify(a.slice, c + 4 * k - d, nd, m, upper);
+        } else {
+          for (int j = 0; j < 16 && !hit; j++) {
+            const uint32_t x = (j & 3) ? __builtin_amdgcn_alignbyte(w[(j >> 2) + 1], w[j >> 2], (uint32_t)(j & 3)) : w[j >> 2];
+            if (x == rot[0]) hit = flat_verify(a.slice, c + j, nd, m, upper);
+          }
+        }
       }
       const uint64_t hb = __ballot(hit), hh = __ballot(high);
       if (lane == 0) {
@@ -1366,6 +1389,7 @@ __global__ __launch_bounds__(256) void k_flat_scan(EvalArgs a, uint32_t stage) {
     }
   }
 }
+__device__ __forceinline__ bool bm_bit(const unsigned long long* bm, uint64_t c) { return (bm[c >> 6] >> (c & 63)) & 1ull; }
 // bits [c0, c1) of a bitmap: any set
 __device__ __forceinline__ bool flat_any(const unsigned long long* bm, uint64_t c0, uint64_t c1) {
   for (uint64_t c = c0; c < c1;) {
@@ -1377,184 +1401,172 @@ __device__ __forceinline__ bool flat_any(const unsigned long long* bm, uint64_t 
   }
   return false;
 }
+// a varint of at most 4 bytes at the start of w: its length (0: longer) and zigzag value (varint.rs:43-66)
+__device__ __forceinline__ uint32_t var4(uint32_t w, int64_t& val) {
+  const uint32_t term = ~w & 0x80808080u;
+  const uint32_t nb = term ? (((uint32_t)__builtin_ctz(term)) >> 3) + 1 : 0u;
+  const uint32_t y = nb == 4 ? w : (w & ((1u << (8 * nb)) - 1u));
+  const uint32_t u = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
+  val = (int64_t)(u >> 1) ^ -(int64_t)(u & 1u);
+  return nb;
+}
+template <bool kLong>
 __global__ __launch_bounds__(256) void k_flat_decide(EvalArgs a, uint32_t stage) {
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= a.nbatches) return;
   const StageDesc& sd = a.chain->st[stage];
   const uint32_t m = sd.needle_len;
   const bool upper = sd.in_type == VT_SRC_UPPER;
-  const bool keep_match = sd.keep_match != 0;
   const bool out_upper = a.chain->out_type == VT_SRC_UPPER;
   const uint8_t* nd = a.blob + sd.needle;
-  const uint32_t n4 = ld_u32_at(nd);
   const unsigned long long* hit_bm = a.fbm;
   const unsigned long long* hi_bm = a.fbm + a.fbm_words;
-  const uint32_t l = lane_id();
-  const uint32_t nw = gridDim.x * 4;
-  for (uint32_t b = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); b < a.nbatches; b += nw) {
-    const uint64_t pos = a.bpos[b];
-    const uint64_t nxt = b + 1 < a.nbatches ? a.bpos[b + 1] : a.slice_len;
-    const uint64_t al = pos & ~15ull;
-    uint64_t wl = nxt > al ? nxt - al : 0;
-    if (wl > (uint64_t)kLeanWin) wl = kLeanWin;
-    const uint32_t wlen = (uint32_t)((wl + 15) & ~15ull);
-    const uint8_t* h = a.slice + pos;
-    const uint32_t batch_len = __builtin_bswap32(ld_u32_at(h + 8));
-    const uint64_t sec0 = pos + 57, sec_end = pos + 12 + (uint64_t)batch_len;
-    const uint32_t sec_len = (uint32_t)(sec_end - sec0);
-    const int32_t count = sec_len >= 4 ? (int32_t)__builtin_bswap32(ld_u32_at(a.slice + sec0)) : -1;
-    const uint32_t re = a.rend[b];
-    bool defer = sec_len < 4 || sec_end - al > (uint64_t)wlen || count < 0 || count > kLeanMaxR || re == 0xFFFFu;
-    const int nr = defer ? 0 : count;
-    const uint64_t rb = a.rbase[b];
-    const uint32_t rs = (int)l < nr ? a.rstart[rb + l] : 0u;
-    const uint32_t rs_next = __shfl_down(rs, 1, 64);
-    bool g = true, match = false;
-    int64_t ts = 0, od = 0, hdr = 0;
-    uint32_t vs = 0, vl = 0, kpos = 0, klen = 0;
-    uint8_t attr = 0, tag = 0;
-    if ((int)l < nr) {
-      // the record's header in registers: 24 bytes from its start (aligned dwords)
-      const uint32_t lim = (int)l + 1 == nr ? re : rs_next;
-      const uint64_t ra = al + rs, a0 = ra & ~3ull;
-      uint32_t x[6];
+  const uint8_t* S = a.slice;
+  const uint64_t pos = a.bpos[b];
+  const uint64_t nxt = b + 1 < a.nbatches ? a.bpos[b + 1] : a.slice_len;
+  const uint64_t rb = a.rbase[b], rn = (b + 1 < a.nbatches ? a.rbase[b + 1] : a.nrec) - rb;
+  const uint64_t al = pos & ~15ull;
+  uint64_t wl = nxt > al ? nxt - al : 0;
+  if (wl > (uint64_t)kLeanWin) wl = kLeanWin;
+  const uint64_t wlen = (wl + 15) & ~15ull;
+  const uint32_t batch_len = __builtin_bswap32(ld_u32_at(S + pos + 8));
+  const uint64_t sec0 = pos + 57, sec_end = pos + 12 + (uint64_t)batch_len;
+  const uint64_t sec_len = sec_end - sec0;
+  const int32_t count = sec_len >= 4 ? (int32_t)__builtin_bswap32(ld_u32_at(S + sec0)) : -1;
+  bool ok = sec_len >= 4 && sec_end - al <= wlen && count >= 0 && count <= kLeanMaxR && (uint64_t)count == rn;
+  uint32_t nkeep = 0;
+  uint64_t q = sec0 + 4;  // absolute
+  for (int32_t n = 0; ok && n < count; n++) {
+    // the record's header: 24 bytes from its start, aligned dwords
+    const uint64_t a0 = q & ~3ull;
+    uint32_t x[6];
 #pragma unroll
-      for (int k = 0; k < 6; k++) x[k] = *(const uint32_t*)(a.slice + a0 + 4 * k);
-      uint32_t o = (uint32_t)(ra & 3), n;
-      int64_t len, kl = 0, vlen;
-      auto at = [&](uint32_t q) {  // bytes [q, q + 4) of x, q < 20
-        const uint32_t d = q >> 2;
-        uint32_t lo = x[0], hi = x[1];
+    for (int k = 0; k < 6; k++) x[k] = *(const uint32_t*)(S + a0 + 4 * k);
+    auto at = [&](uint32_t o) {  // bytes [o, o + 4) of x, o < 20
+      const uint32_t d = o >> 2;
+      uint32_t lo = x[0], hi = x[1];
 #pragma unroll
-        for (uint32_t k = 1; k < 5; k++)
-          if (d == k) {
-            lo = x[k];
-            hi = x[k + 1];
+      for (uint32_t k = 1; k < 5; k++)
+        if (d == k) {
+          lo = x[k];
+          hi = x[k + 1];
+        }
+      return __builtin_amdgcn_alignbyte(hi, lo, o & 3u);
+    };
+    uint32_t o = (uint32_t)(q & 3), nb;
+    int64_t len, ts, od, kl = 0, vlen, hdr;
+    nb = var4(at(o), len);
+    ok = nb != 0 && len >= 0;
+    const uint64_t end = q + nb + (uint64_t)len;  // where the record ends (Record::decode's length)
+    o += nb;
+    const uint8_t attr = (uint8_t)at(o);
+    o += 1;
+    nb = var4(at(o), ts);
+    ok = ok && nb != 0;
+    o += nb;
+    nb = var4(at(o), od);
+    ok = ok && nb != 0;
+    o += nb;
+    const uint8_t tag = (uint8_t)at(o);
+    o += 1;
+    ok = ok && tag <= 1 && end <= sec_end;
+    if (!ok) break;
+    uint64_t p = a0 + o, kpos = 0;
+    uint32_t klen = 0;
+    if (tag == 1) {
+      nb = var4(at(o), kl);
+      ok = nb != 0 && kl >= 0;
+      p += nb;
+      kpos = p;
+      klen = (uint32_t)kl;
+      p += klen;
+    }
+    nb = var4(tag == 1 ? ld_u32_at(S + p) : at(o), vlen);
+    ok = ok && nb != 0 && vlen >= 0;
+    const uint64_t va = p + nb, ve = va + (uint64_t)vlen;
+    ok = ok && ve <= end;
+    if (!ok) break;
+    nb = var4(ld_u32_at(S + ve), hdr);
+    ok = nb != 0 && ve + nb == end;
+    if (!ok) break;
+    // bytes >= 0x80 in the value: the chunks inside it by their bits, the
+    // edge chunks (which hold gap bytes) by their bytes
+    if (ve > va) {
+      const uint64_t c0 = va >> 4, c1 = (ve + 15) >> 4, i0 = (va + 15) >> 4, i1 = ve >> 4;
+      bool hi = i0 < i1 && flat_any(hi_bm, i0, i1);
+      auto hi_edge = [&](uint64_t c) {
+        const uint4 u = *(const uint4*)(S + (c << 4));
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+        uint32_t f = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) f |= w[k] & bytes_in((uint32_t)(((c << 4) + 4 * k) - al), (uint32_t)(va - al), (uint32_t)(ve - al));
+        return (f & 0x80808080u) != 0u;
+      };
+      if (!hi && c0 < i0 && bm_bit(hi_bm, c0)) hi = hi_edge(c0);
+      if (!hi && i1 < c1 && (i1 >= i0 || c0 != i1) && bm_bit(hi_bm, i1)) hi = hi_edge(i1);
+      ok = !hi;
+      if (!ok) break;
+    }
+    // an occurrence starting in [va, ve - m]
+    bool match = false;
+    if ((uint64_t)vlen >= m) {
+      const uint64_t sl = ve - m;  // last valid start
+      // anchors of chunk C: starts [16C - 3, 16C + 12] (kLong), [16C, 16C + 15]
+      const uint64_t blo = kLong ? 3 : 0, bhi = kLong ? 12 : 15;
+      const uint64_t j0 = (va + blo + 15) >> 4;  // first chunk whose every start is >= va
+      const uint64_t j1 = sl >= bhi ? ((sl - bhi) >> 4) + 1 : 0;  // chunks < j1: every start <= sl
+      match = j0 < j1 && flat_any(hit_bm, j0, j1);
+      if (!match) {  // chunks holding some valid start but not all: the bytes decide
+        const uint64_t e0 = va >= bhi ? (va - bhi + 15) >> 4 : 0, e1 = (sl + blo) >> 4;
+        for (uint64_t c = e0; c <= e1 && !match; c++) {
+          if (c >= j0 && c < j1) {
+            c = j1 - 1;
+            continue;
           }
-        return __builtin_amdgcn_alignbyte(hi, lo, q & 3u);
-      };
-      auto var4 = [](uint32_t w, int64_t& val) {  // a varint of <= 4 bytes: its length (0: longer)
-        const uint32_t term = ~w & 0x80808080u;
-        const uint32_t nb = term ? (((uint32_t)__builtin_ctz(term)) >> 3) + 1 : 0u;
-        const uint32_t y = nb == 4 ? w : (w & ((1u << (8 * nb)) - 1u));
-        const uint32_t u = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
-        val = (int64_t)(u >> 1) ^ -(int64_t)(u & 1u);
-        return nb;
-      };
-      bool ok = true;
-      n = var4(at(o), len);
-      ok = ok && n != 0;
-      o += n;
-      attr = (uint8_t)at(o);
-      o += 1;
-      n = var4(at(o), ts);
-      ok = ok && n != 0;
-      o += n;
-      n = var4(at(o), od);
-      ok = ok && n != 0;
-      o += n;
-      tag = (uint8_t)at(o);
-      o += 1;
-      ok = ok && tag <= 1;
-      uint64_t q = a0 + o;  // absolute
-      if (ok && tag == 1) {
-        n = var4(at(o), kl);
-        ok = n != 0 && kl >= 0;
-        q += n;
-        kpos = (uint32_t)(q - al);
-        klen = (uint32_t)kl;
-        q += klen;
-      }
-      if (ok) {
-        n = var4(tag == 1 ? ld_u32_at(a.slice + q) : at(o), vlen);
-        ok = n != 0 && vlen >= 0;
-        q += n;
-        vs = (uint32_t)(q - al);
-        vl = (uint32_t)vlen;
-        ok = ok && (uint64_t)vs + vl <= lim;
-      }
-      if (ok) {
-        n = var4(ld_u32_at(a.slice + al + vs + vl), hdr);
-        ok = n != 0 && vs + vl + n == lim;
-      }
-      g = ok;
-      if (g) {
-        // bits over the value [va, ve): chunks c = byte >> 4
-        const uint64_t va = al + vs, ve = va + vl;
-        if (vl) {
-          const uint64_t c0 = va >> 4, c1 = (ve + 15) >> 4;   // chunks touching the value
-          const uint64_t i0 = (va + 15) >> 4, i1 = ve >> 4;  // chunks inside the value
-          bool hi = i0 < i1 && flat_any(hi_bm, i0, i1);
-          auto hi_exact = [&](uint64_t c) {  // the value bytes of chunk c
-            const uint64_t lo = c << 4 > va ? c << 4 : va, e = (c << 4) + 16 < ve ? (c << 4) + 16 : ve;
-            bool f = false;
-            for (uint64_t p = lo; p < e; p++) f |= a.slice[p] >= 0x80;
-            return f;
-          };
-          if (!hi && c0 < i0 && ((hi_bm[c0 >> 6] >> (c0 & 63)) & 1ull)) hi = hi_exact(c0);
-          if (!hi && i1 < c1 && (i1 >= i0 || c0 != i1) && ((hi_bm[i1 >> 6] >> (i1 & 63)) & 1ull)) hi = hi_exact(i1);
-          g = !hi;
-        }
-        if (g && vl >= m) {
-          // starts in [va, ve - m]: chunks whose every start is inside need no check
-          const uint64_t sl = ve - m;  // last valid start
-          const uint64_t j0 = (va + 15) >> 4, j1 = (sl + 1) >> 4;  // chunks fully inside [va, sl]
-          match = j0 < j1 && flat_any(hit_bm, j0, j1);
-          auto hit_exact = [&](uint64_t c) {  // starts of chunk c inside [va, sl]
-            const uint64_t lo = c << 4 > va ? c << 4 : va, e = (c << 4) + 15 < sl ? (c << 4) + 15 : sl;
-            bool f = false;
-            for (uint64_t p = lo; p <= e && !f; p++) {
-              uint32_t x0 = ld_u32_at(a.slice + p);
-              if (upper) x0 = swar_upper(x0);
-              f = x0 == n4 && flat_verify(a.slice, p, nd, m, upper);
-            }
-            return f;
-          };
-          const uint64_t e0 = va >> 4, e1 = sl >> 4;  // chunks holding some valid start
-          if (!match && e0 < j0 && ((hit_bm[e0 >> 6] >> (e0 & 63)) & 1ull)) match = hit_exact(e0);
-          if (!match && e1 >= j1 && e1 != (e0 < j0 ? e0 : ~0ull) && ((hit_bm[e1 >> 6] >> (e1 & 63)) & 1ull))
-            match = hit_exact(e1);
+          if (!bm_bit(hit_bm, c)) continue;
+          const uint64_t lo = (c << 4) >= va + blo ? (c << 4) - blo : va;
+          const uint64_t hi = (c << 4) + bhi <= sl ? (c << 4) + bhi : sl;
+          for (uint64_t s0 = lo; s0 <= hi && !match; s0++) match = flat_verify(S, s0, nd, m, upper);
         }
       }
     }
-    defer = defer || __ballot((int)l < nr && !g) != 0;
-    const bool keep = keep_match ? match : !match;
-    const uint64_t alive = __ballot((int)l < nr && keep);
-    if (defer) {
-      if (l == 0) {
-        const uint32_t i = atomicAdd(&a.list[0], 1u);
-        a.list[1 + i] = b;
-      }
-      continue;
-    }
-    if ((alive >> l) & 1ull) {
+    if (match) {
       KeptRec d;
-      d.src = al + rs;
-      d.vpos = al + vs;
-      d.kpos = tag ? al + kpos : 0;
+      d.src = q;
+      d.vpos = va;
+      d.kpos = tag ? kpos : 0;
       d.od = od;
       d.ts = ts;
       d.hdr = hdr;
-      d.vlen = vl;
+      d.vlen = (uint32_t)vlen;
       d.klen = klen;
       d.ival = 0;
       d.mode = out_upper ? KM_UPPER : KM_COPY;
       d.has_key = tag;
       d.attr = attr;
       d.pad = 0;
-      a.desc[rb + __popcll(alive & ((1ull << l) - 1ull))] = d;
+      a.desc[rb + nkeep++] = d;
     }
-    if (l == 0) {  // batch header (file format, batch.rs:163-180)
-      BatchStat st = {};
-      st.base_offset = (int64_t)rd_be(h, 8);
-      st.lod_in = (int32_t)rd_be(h + 23, 4);
-      st.first_ts = (int64_t)rd_be(h + 27, 8);
-      st.comp = (uint32_t)h[22] & 7u;
-      st.flags = BF_LAST_STAGE;
-      st.nkeep = st.nout = (uint32_t)__popcll(alive);
-      st.sec_len = sec_len;
-      st.err_stage = 0xFFFFFFFFu;
-      a.bstat[b] = st;
-    }
+    q = end;
   }
+  ok = ok && q == sec_end;
+  if (!ok) {  // the exact kernel frames and evaluates this batch (no record starts from here)
+    a.rend[b] = 0xFFFFu;
+    const uint32_t i = atomicAdd(&a.list[0], 1u);
+    a.list[1 + i] = b;
+    return;
+  }
+  const uint8_t* h = S + pos;  // batch header (file format, batch.rs:163-180)
+  BatchStat st = {};
+  st.base_offset = (int64_t)rd_be(h, 8);
+  st.lod_in = (int32_t)rd_be(h + 23, 4);
+  st.first_ts = (int64_t)rd_be(h + 27, 8);
+  st.comp = (uint32_t)h[22] & 7u;
+  st.flags = BF_LAST_STAGE;
+  st.nkeep = st.nout = nkeep;
+  st.sec_len = (uint32_t)sec_len;
+  st.err_stage = 0xFFFFFFFFu;
+  a.bstat[b] = st;
 }
 
 // resident workgroups of k_eval_lean<kind> on the current device (CUs x occupancy)
@@ -1594,14 +1606,19 @@ int flat_stage(const ChainDesc& ch, uint32_t ops) {
   return m >= 4 && m <= (uint32_t)kLeanNeedle ? st : -1;
 }
 
-void launch_eval_flat(const EvalArgs& a, uint32_t stage, hipStream_t s) {
+void launch_eval_flat(const EvalArgs& a, uint32_t flat_st, hipStream_t s) {
   if (!a.nbatches) return;
-  hipLaunchKernelGGL(k_chase, dim3((a.nbatches + kChaseT - 1) / kChaseT), dim3(kChaseT), 0, s, a);
+  const uint32_t stage = flat_st & 0xFFu, m = flat_st >> 8;
   const uint64_t waves = (a.fbm_words + kFlatRounds - 1) / kFlatRounds;
-  const uint32_t g1 = (uint32_t)std::min<uint64_t>((waves + 3) / 4, 4096);
-  hipLaunchKernelGGL(k_flat_scan, dim3(std::max<uint32_t>(g1, 1)), dim3(256), 0, s, a, stage);
-  const uint32_t g2 = std::min<uint32_t>((a.nbatches + 3) / 4, 8192);
-  hipLaunchKernelGGL(k_flat_decide, dim3(g2), dim3(256), 0, s, a, stage);
+  const uint32_t g1 = (uint32_t)std::max<uint64_t>(std::min<uint64_t>((waves + 3) / 4, 4096), 1);
+  const uint32_t g2 = (a.nbatches + 255) / 256;
+  if (m >= 7) {
+    hipLaunchKernelGGL(k_flat_scan<true>, dim3(g1), dim3(256), 0, s, a, stage);
+    hipLaunchKernelGGL(k_flat_decide<true>, dim3(g2), dim3(256), 0, s, a, stage);
+  } else {
+    hipLaunchKernelGGL(k_flat_scan<false>, dim3(g1), dim3(256), 0, s, a, stage);
+    hipLaunchKernelGGL(k_flat_decide<false>, dim3(g2), dim3(256), 0, s, a, stage);
+  }
 }
 
 void launch_eval_lean(const EvalArgs& a, uint32_t ops, hipStream_t s) {

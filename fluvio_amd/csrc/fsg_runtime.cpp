@@ -2055,7 +2055,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     (void)hipGetLastError();
     if (flat) {
       ea.fbm = c->fbm.as<unsigned long long>();
-      ea.flat_st = (uint32_t)fst;
+      ea.flat_st = (uint32_t)fst | (c->hdesc.st[fst].needle_len << 8);
     }
   }
   if (lean || arr) HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
