@@ -1291,7 +1291,7 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kK
 // (filter / filter_init / filter_with_param: value.contains(needle), needle of
 // 4..128 bytes) decouples streaming from the batch structure:
 //   k_flat_scan   every byte of the slice once, as a flat array (headers and
-//                 gaps included): one 16-byte chunk a lane, 4 rounds of 1 KiB
+//                 gaps included): one 16-byte chunk a lane, 8 rounds of 1 KiB
 //                 per wave in flight; per chunk two bits: "a needle occurrence
 //                 is anchored here" and "a byte >= 0x80 here", stored as one
 //                 64-bit ballot per bitmap per round.  Needles of >= 7 bytes:
@@ -1314,7 +1314,7 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kK
 //                 defers the batch to k_eval.
 // The batch results (BatchStat, KeptRec) are those k_eval_lean writes.
 // ---------------------------------------------------------------------------
-constexpr int kFlatRounds = 4;  // 1 KiB rounds per wave in flight
+constexpr int kFlatRounds = 8;  // 1 KiB rounds per wave in flight
 __device__ __forceinline__ bool flat_verify(const uint8_t* s, uint64_t p, const uint8_t* nd, uint32_t m, bool upper) {
   for (uint32_t t = 0; t < m; t += 4) {
     uint32_t x = ld_u32_at(s + p + t);
@@ -1326,16 +1326,23 @@ __device__ __forceinline__ bool flat_verify(const uint8_t* s, uint64_t p, const 
 }
 template <bool kLong>  // kLong: m >= 7, aligned dwords against the 4 offsets
 __global__ __launch_bounds__(256) void k_flat_scan(EvalArgs a, uint32_t stage) {
+  // a wave's round staged in LDS when it holds candidates: the needle is
+  // verified from there (a global re-read per candidate stalled the stream)
+  __shared__ uint32_t rbuf[4][256 + 4];  // (+4: the alignbyte of the last dword reads one past)
+  __shared__ uint32_t ndw[kLeanNeedle / 4 + 1];
   const StageDesc& sd = a.chain->st[stage];
   const uint32_t m = sd.needle_len;
   const bool upper = sd.in_type == VT_SRC_UPPER;
   const uint8_t* nd = a.blob + sd.needle;
+  for (uint32_t t = threadIdx.x; t < (m + 3) / 4; t += 256) ndw[t] = ld_u32_at(nd + 4 * t);
+  __syncthreads();
   uint32_t rot[4];
 #pragma unroll
   for (int d = 0; d < 4; d++) rot[d] = ld_u32_at(nd + (kLong ? d : 0));
-  const uint32_t lane = lane_id();
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+  uint32_t* rb = rbuf[wv];
   const uint64_t nrounds = a.fbm_words;  // 1 KiB rounds of the slice
-  const uint64_t w0 = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t w0 = (uint64_t)blockIdx.x * 4 + wv;
   const uint64_t nw = (uint64_t)gridDim.x * 4;
   unsigned long long* hit_bm = a.fbm;
   unsigned long long* hi_bm = a.fbm + a.fbm_words;
@@ -1351,14 +1358,15 @@ __global__ __launch_bounds__(256) void k_flat_scan(EvalArgs a, uint32_t stage) {
 #pragma unroll
     for (int i = 0; i < kFlatRounds; i++) {
       if (r0 + i >= nrounds) break;  // uniform
-      const uint64_t c = (r0 + i) * 1024 + lane * 16;
+      const uint64_t R = (r0 + i) * 1024;
       uint32_t w[5] = {v[i].x, v[i].y, v[i].z, v[i].w, kLong ? 0u : nx[i]};
       const bool high = ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) != 0u;
       if (upper) {
 #pragma unroll
         for (int k = 0; k < 5; k++) w[k] = swar_upper(w[k]);
       }
-      // min over the compare differences: zero iff some 4-gram hits
+      // min over the compare differences: zero iff some 4-gram hits (the
+      // candidate masks are built only when a lane of the wave has one)
       uint32_t z = 0xFFFFFFFFu;
       if (kLong) {
 #pragma unroll
@@ -1369,16 +1377,43 @@ __global__ __launch_bounds__(256) void k_flat_scan(EvalArgs a, uint32_t stage) {
           z = min(z, ((j & 3) ? __builtin_amdgcn_alignbyte(w[(j >> 2) + 1], w[j >> 2], (uint32_t)(j & 3)) : w[j >> 2]) ^ rot[0]);
       }
       bool hit = false;
-      if (z == 0u) {  // rare: find the candidates, verify the whole needle
+      if (__ballot(z == 0u)) {  // rare: stage the round, verify every candidate from LDS
+        // candidates: bit (4k + d) = aligned dword k against the needle at
+        // offset d (kLong), bit j = the 4-gram at position j (else)
+        uint32_t cm = 0;
         if (kLong) {
-          for (int k = 0; k < 4 && !hit; k++)
-            for (int d = 0; d < 4 && !hit; d++)
-              if (w[k] == rot[d] && c + 4 * k >= (uint64_t)d) hit = flat_verify(a.slice, c + 4 * k - d, nd, m, upper);
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int d = 0; d < 4; d++) cm |= (uint32_t)(w[k] == rot[d]) << (4 * k + d);
         } else {
-          for (int j = 0; j < 16 && !hit; j++) {
-            const uint32_t x = (j & 3) ? __builtin_amdgcn_alignbyte(w[(j >> 2) + 1], w[j >> 2], (uint32_t)(j & 3)) : w[j >> 2];
-            if (x == rot[0]) hit = flat_verify(a.slice, c + j, nd, m, upper);
+#pragma unroll
+          for (int j = 0; j < 16; j++)
+            cm |= (uint32_t)(((j & 3) ? __builtin_amdgcn_alignbyte(w[(j >> 2) + 1], w[j >> 2], (uint32_t)(j & 3)) : w[j >> 2]) ==
+                             rot[0]) << j;
+        }
+        rb[4 * lane] = v[i].x;
+        rb[4 * lane + 1] = v[i].y;
+        rb[4 * lane + 2] = v[i].z;
+        rb[4 * lane + 3] = v[i].w;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        while (cm && !hit) {
+          const uint32_t j = (uint32_t)__builtin_ctz(cm);
+          cm &= cm - 1;
+          const int64_t rel = kLong ? (int64_t)(16 * lane + 4 * (j >> 2)) - (int64_t)(j & 3) : (int64_t)(16 * lane + j);
+          if (rel < 0 || rel + m > 1024) {  // beyond the staged round: from memory
+            hit = flat_verify(a.slice, R + rel, nd, m, upper);
+            continue;
           }
+          bool eq = true;
+          for (uint32_t t = 0; t < m && eq; t += 4) {
+            const uint32_t q = (uint32_t)rel + t;
+            uint32_t x = __builtin_amdgcn_alignbyte(rb[(q >> 2) + 1], rb[q >> 2], q & 3u);
+            if (upper) x = swar_upper(x);
+            const uint32_t k = m - t >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (m - t))) - 1u);
+            eq = ((x ^ ndw[t >> 2]) & k) == 0u;
+          }
+          hit = eq;
         }
       }
       const uint64_t hb = __ballot(hit), hh = __ballot(high);
@@ -1410,6 +1445,32 @@ __device__ __forceinline__ uint32_t var4(uint32_t w, int64_t& val) {
   val = (int64_t)(u >> 1) ^ -(int64_t)(u & 1u);
   return nb;
 }
+// the 24 header bytes of a record at absolute q, as aligned dwords from q & ~3
+struct FlatHdr {
+  uint32_t x[6];
+};
+__device__ __forceinline__ FlatHdr flat_hdr(const uint8_t* S, uint64_t q) {
+  FlatHdr h;
+  const uint64_t a0 = q & ~3ull;
+#pragma unroll
+  for (int k = 0; k < 6; k++) h.x[k] = *(const uint32_t*)(S + a0 + 4 * k);
+  return h;
+}
+__device__ __forceinline__ uint32_t flat_at(const FlatHdr& h, uint32_t o) {  // bytes [o, o + 4), o < 20
+  const uint32_t d = o >> 2;
+  uint32_t lo = h.x[0], hi = h.x[1];
+#pragma unroll
+  for (uint32_t k = 1; k < 5; k++)
+    if (d == k) {
+      lo = h.x[k];
+      hi = h.x[k + 1];
+    }
+  return __builtin_amdgcn_alignbyte(hi, lo, o & 3u);
+}
+// Software-pipelined walk: record n + 1's header load is issued as soon as
+// record n's length varint says where it starts, together with record n's
+// trailer, bitmap words and edge chunks, so one memory round trip per record
+// sits on the thread's critical path (the plain walk had five).
 template <bool kLong>
 __global__ __launch_bounds__(256) void k_flat_decide(EvalArgs a, uint32_t stage) {
   const uint32_t b = blockIdx.x * 256 + threadIdx.x;
@@ -1435,75 +1496,85 @@ __global__ __launch_bounds__(256) void k_flat_decide(EvalArgs a, uint32_t stage)
   const int32_t count = sec_len >= 4 ? (int32_t)__builtin_bswap32(ld_u32_at(S + sec0)) : -1;
   bool ok = sec_len >= 4 && sec_end - al <= wlen && count >= 0 && count <= kLeanMaxR && (uint64_t)count == rn;
   uint32_t nkeep = 0;
-  uint64_t q = sec0 + 4;  // absolute
+  uint64_t q = sec0 + 4;  // absolute start of record n
+  FlatHdr H = flat_hdr(S, ok && count > 0 ? q : sec0);
   for (int32_t n = 0; ok && n < count; n++) {
-    // the record's header: 24 bytes from its start, aligned dwords
-    const uint64_t a0 = q & ~3ull;
-    uint32_t x[6];
-#pragma unroll
-    for (int k = 0; k < 6; k++) x[k] = *(const uint32_t*)(S + a0 + 4 * k);
-    auto at = [&](uint32_t o) {  // bytes [o, o + 4) of x, o < 20
-      const uint32_t d = o >> 2;
-      uint32_t lo = x[0], hi = x[1];
-#pragma unroll
-      for (uint32_t k = 1; k < 5; k++)
-        if (d == k) {
-          lo = x[k];
-          hi = x[k + 1];
-        }
-      return __builtin_amdgcn_alignbyte(hi, lo, o & 3u);
-    };
     uint32_t o = (uint32_t)(q & 3), nb;
     int64_t len, ts, od, kl = 0, vlen, hdr;
-    nb = var4(at(o), len);
+    nb = var4(flat_at(H, o), len);
     ok = nb != 0 && len >= 0;
     const uint64_t end = q + nb + (uint64_t)len;  // where the record ends (Record::decode's length)
-    o += nb;
-    const uint8_t attr = (uint8_t)at(o);
-    o += 1;
-    nb = var4(at(o), ts);
-    ok = ok && nb != 0;
-    o += nb;
-    nb = var4(at(o), od);
-    ok = ok && nb != 0;
-    o += nb;
-    const uint8_t tag = (uint8_t)at(o);
-    o += 1;
-    ok = ok && tag <= 1 && end <= sec_end;
+    ok = ok && end <= sec_end;
     if (!ok) break;
-    uint64_t p = a0 + o, kpos = 0;
+    const FlatHdr Hn = flat_hdr(S, n + 1 < count ? end : q);  // the next record's header, in flight now
+    o += nb;
+    const uint8_t attr = (uint8_t)flat_at(H, o);
+    o += 1;
+    nb = var4(flat_at(H, o), ts);
+    ok = nb != 0;
+    o += nb;
+    nb = var4(flat_at(H, o), od);
+    ok = ok && nb != 0;
+    o += nb;
+    const uint8_t tag = (uint8_t)flat_at(H, o);
+    o += 1;
+    ok = ok && tag <= 1;
+    if (!ok) break;
+    uint64_t p = (q & ~3ull) + o, kpos = 0;
     uint32_t klen = 0;
     if (tag == 1) {
-      nb = var4(at(o), kl);
+      nb = var4(flat_at(H, o), kl);
       ok = nb != 0 && kl >= 0;
       p += nb;
       kpos = p;
       klen = (uint32_t)kl;
       p += klen;
     }
-    nb = var4(tag == 1 ? ld_u32_at(S + p) : at(o), vlen);
+    nb = var4(tag == 1 ? ld_u32_at(S + p) : flat_at(H, o), vlen);
     ok = ok && nb != 0 && vlen >= 0;
     const uint64_t va = p + nb, ve = va + (uint64_t)vlen;
     ok = ok && ve <= end;
     if (!ok) break;
-    nb = var4(ld_u32_at(S + ve), hdr);
+    // every load of this record at once: trailer, bitmap words, edge chunks
+    const uint32_t tw = ld_u32_at(S + ve);
+    const uint64_t c0 = va >> 4, c1 = (ve + 15) >> 4, i0 = (va + 15) >> 4, i1 = ve >> 4;
+    const uint64_t wb = c0 >> 6;  // first bitmap word touching the value
+    const unsigned long long hb0 = hi_bm[wb], hb1 = hi_bm[wb + 1];
+    const unsigned long long mb0 = hit_bm[wb], mb1 = hit_bm[wb + 1];
+    const uint4 ea = *(const uint4*)(S + (c0 << 4));
+    const uint4 eb = *(const uint4*)(S + (((ve ? ve - 1 : 0) >> 4) << 4));
+    nb = var4(tw, hdr);
     ok = nb != 0 && ve + nb == end;
     if (!ok) break;
-    // bytes >= 0x80 in the value: the chunks inside it by their bits, the
-    // edge chunks (which hold gap bytes) by their bytes
+    // bits [x0, x1) of a bitmap from the two loaded words (a longer range reads more)
+    auto bits_any = [&](const unsigned long long* bm, unsigned long long w0v, unsigned long long w1v, uint64_t x0,
+                        uint64_t x1) {
+      if (x1 <= x0) return false;
+      if (x1 > (wb + 2) << 6) return flat_any(bm, x0, x1);
+      const uint64_t lo = x0 - (wb << 6), hi = x1 - (wb << 6);  // in [0, 128]
+      const unsigned long long m0 = (lo < 64 ? (~0ull << lo) : 0ull) & (hi >= 64 ? ~0ull : ((1ull << hi) - 1ull));
+      const unsigned long long m1 = (hi > 64 ? (hi >= 128 ? ~0ull : ((1ull << (hi - 64)) - 1ull)) : 0ull) &
+                                    (lo > 64 ? (~0ull << (lo - 64)) : ~0ull);
+      return ((w0v & m0) | (w1v & m1)) != 0ull;
+    };
+    auto bit = [&](unsigned long long w0v, unsigned long long w1v, uint64_t c) {
+      const uint64_t r = c - (wb << 6);
+      return r < 64 ? ((w0v >> r) & 1ull) != 0ull : r < 128 ? ((w1v >> (r - 64)) & 1ull) != 0ull : false;
+    };
+    // bytes >= 0x80 in the value: chunks inside it by their bits, the edge
+    // chunks (which hold gap bytes) by their bytes
     if (ve > va) {
-      const uint64_t c0 = va >> 4, c1 = (ve + 15) >> 4, i0 = (va + 15) >> 4, i1 = ve >> 4;
-      bool hi = i0 < i1 && flat_any(hi_bm, i0, i1);
-      auto hi_edge = [&](uint64_t c) {
-        const uint4 u = *(const uint4*)(S + (c << 4));
+      bool hi = bits_any(hi_bm, hb0, hb1, i0, i1);
+      auto hi_edge = [&](const uint4& u, uint64_t c) {
         const uint32_t w[4] = {u.x, u.y, u.z, u.w};
         uint32_t f = 0;
 #pragma unroll
-        for (int k = 0; k < 4; k++) f |= w[k] & bytes_in((uint32_t)(((c << 4) + 4 * k) - al), (uint32_t)(va - al), (uint32_t)(ve - al));
+        for (int k = 0; k < 4; k++)
+          f |= w[k] & bytes_in((uint32_t)(((c << 4) + 4 * k) - al), (uint32_t)(va - al), (uint32_t)(ve - al));
         return (f & 0x80808080u) != 0u;
       };
-      if (!hi && c0 < i0 && bm_bit(hi_bm, c0)) hi = hi_edge(c0);
-      if (!hi && i1 < c1 && (i1 >= i0 || c0 != i1) && bm_bit(hi_bm, i1)) hi = hi_edge(i1);
+      if (!hi && c0 < i0) hi = hi_edge(ea, c0);
+      if (!hi && i1 < c1 && (i1 >= i0 || c0 != i1)) hi = hi_edge(eb, i1);
       ok = !hi;
       if (!ok) break;
     }
@@ -1513,9 +1584,9 @@ __global__ __launch_bounds__(256) void k_flat_decide(EvalArgs a, uint32_t stage)
       const uint64_t sl = ve - m;  // last valid start
       // anchors of chunk C: starts [16C - 3, 16C + 12] (kLong), [16C, 16C + 15]
       const uint64_t blo = kLong ? 3 : 0, bhi = kLong ? 12 : 15;
-      const uint64_t j0 = (va + blo + 15) >> 4;  // first chunk whose every start is >= va
+      const uint64_t j0 = (va + blo + 15) >> 4;                   // first chunk whose every start is >= va
       const uint64_t j1 = sl >= bhi ? ((sl - bhi) >> 4) + 1 : 0;  // chunks < j1: every start <= sl
-      match = j0 < j1 && flat_any(hit_bm, j0, j1);
+      match = j0 < j1 && bits_any(hit_bm, mb0, mb1, j0, j1);
       if (!match) {  // chunks holding some valid start but not all: the bytes decide
         const uint64_t e0 = va >= bhi ? (va - bhi + 15) >> 4 : 0, e1 = (sl + blo) >> 4;
         for (uint64_t c = e0; c <= e1 && !match; c++) {
@@ -1523,7 +1594,7 @@ __global__ __launch_bounds__(256) void k_flat_decide(EvalArgs a, uint32_t stage)
             c = j1 - 1;
             continue;
           }
-          if (!bm_bit(hit_bm, c)) continue;
+          if (c >= wb && c < wb + 128 ? !bit(mb0, mb1, c) : !bm_bit(hit_bm, c)) continue;
           const uint64_t lo = (c << 4) >= va + blo ? (c << 4) - blo : va;
           const uint64_t hi = (c << 4) + bhi <= sl ? (c << 4) + bhi : sl;
           for (uint64_t s0 = lo; s0 <= hi && !match; s0++) match = flat_verify(S, s0, nd, m, upper);
@@ -1548,6 +1619,7 @@ __global__ __launch_bounds__(256) void k_flat_decide(EvalArgs a, uint32_t stage)
       a.desc[rb + nkeep++] = d;
     }
     q = end;
+    H = Hn;
   }
   ok = ok && q == sec_end;
   if (!ok) {  // the exact kernel frames and evaluates this batch (no record starts from here)
