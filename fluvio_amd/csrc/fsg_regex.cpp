@@ -17,8 +17,9 @@
 // could match invalid UTF-8 is the crate's init error).  `\b`, `\B` are exact on
 // ASCII values only (the kernel reports FSG_E_UNSUPPORTED for a non-ASCII value);
 // word boundaries are DFA states that remember whether the previous byte was a
-// word byte.  Scripts and other binary properties in \p{..}, nested classes and
-// class set operations are rejected at init (FSG_E_UNSUPPORTED).
+// word byte.  Nested classes and the class set operations && -- ~~, escapes
+// \x \u \U (fixed digits or braces).  Scripts and other binary properties in
+// \p{..} are rejected at init (FSG_E_UNSUPPORTED).
 //
 // Output: a DFA over bytes with unanchored restart folded in, byte classes,
 // sticky acceptance, an end-of-value acceptance bit and the longest possible
@@ -86,6 +87,14 @@ Set negate(const Set& s0) {
   if (next <= 0x10FFFF) o.push_back({next, 0x10FFFF});
   return o;
 }
+// class set operations (regex-syntax ClassSetBinaryOpKind): &&, --, ~~
+Set set_union(Set a, const Set& b) {
+  a.insert(a.end(), b.begin(), b.end());
+  return norm(a);
+}
+Set set_inter(const Set& a, const Set& b) { return negate(set_union(negate(a), negate(b))); }
+Set set_diff(const Set& a, const Set& b) { return set_inter(a, negate(b)); }
+Set set_symdiff(const Set& a, const Set& b) { return set_union(set_diff(a, b), set_diff(b, a)); }
 template <size_t N>
 Set table(const Range (&t)[N], bool neg) {
   Set s(t, t + N);
@@ -280,7 +289,8 @@ struct Parser {
       case 'f': *c = '\f'; return 1;
       case 'v': *c = '\v'; return 1;
       case 'a': *c = 7; return 1;
-      case 'x': {
+      case 'x': case 'u': case 'U': {  // \x7F \x{..}, \u007F \u{..}, \U0000007F \U{..} (regex-syntax parse_hex)
+        const int fixed = e == 'x' ? 2 : e == 'u' ? 4 : 8;
         uint32_t v = 0;
         if (at('{')) {
           i++;
@@ -295,12 +305,16 @@ struct Parser {
           }
           i++;
         } else {
-          for (int k = 0; k < 2; k++) {
+          for (int k = 0; k < fixed; k++) {
             if (i >= p.size() || !hex(p[i])) {
               err = true;
               return 0;
             }
             v = v * 16 + hv(p[i++]);
+          }
+          if (v > 0x10FFFF || (v >= 0xD800 && v <= 0xDFFF)) {
+            err = true;
+            return 0;
           }
         }
         *c = v;
@@ -313,9 +327,6 @@ struct Parser {
         }
         if (e == 'b' || e == 'B') word = wb = true;
         return e == 'b' ? 3 : e == 'B' ? 4 : e == 'A' ? 5 : 6;
-      case 'u': case 'U':
-        unsup = true;
-        return 0;
       default:
         if (e < 0x80 && !((e >= '0' && e <= '9') || (e >= 'a' && e <= 'z') || (e >= 'A' && e <= 'Z'))) {
           *c = e;
@@ -326,23 +337,50 @@ struct Parser {
     }
   }
 
-  NodeP cls() {
-    auto n = std::make_unique<Node>();
-    n->t = N_SET;
+  // a bracketed class after its '[' through the matching ']' (regex-syntax
+  // parse_set_class): items are unions; nested brackets are items; the binary
+  // operators && (intersection), -- (difference) and ~~ (symmetric difference)
+  // are left-associative and bind looser than the union; a leading ']' and
+  // leading '-'s are literals; negation applies to the whole result
+  Set bracket() {
     bool neg = false;
     if (at('^')) {
       neg = true;
       i++;
     }
+    Set uni, lhs;
+    int op = 0;  // 0 none, 1 &&, 2 --, 3 ~~
     bool first = true;
+    auto literal = [&](uint32_t lo, uint32_t hi) {
+      if (!fu && hi >= 0x80) {  // class_literal_byte: UnicodeNotAllowed in a (?-u) class
+        err = true;
+        return;
+      }
+      add_folded(uni, lo, hi);
+    };
     for (;;) {
       skip_x();
       if (i >= p.size()) {
         err = true;
-        return n;
+        return uni;
       }
       uint32_t c = p[i];
-      if (c == ']' && !first) {
+      if (first) {  // parse_set_class_open: a leading ']' and any leading '-' are literals
+        first = false;
+        if (c == ']') {
+          i++;
+          literal(']', ']');
+          continue;
+        }
+        if (c == '-') {
+          while (at('-')) {
+            i++;
+            literal('-', '-');
+          }
+          continue;
+        }
+      }
+      if (c == ']') {
         i++;
         break;
       }
@@ -358,31 +396,40 @@ struct Parser {
         Set ps;
         if (k + 1 < p.size() && posix(std::vector<uint32_t>(p.begin() + j, p.begin() + k), ps)) {
           if (pneg) ps = negate(ps);
-          for (auto& r : ps) add_folded(n->set, r.lo, r.hi);
+          for (auto& r : ps) add_folded(uni, r.lo, r.hi);
           i = k + 2;
-          first = false;
           continue;
         }
       }
-      if (c == '[') {
-        unsup = true;
-        return n;
+      if (c == '[') {  // a nested class: one item of the union
+        i++;
+        if (++depth > 64) {
+          unsup = true;
+          return uni;
+        }
+        Set in = bracket();
+        depth--;
+        if (err || unsup) return uni;
+        uni.insert(uni.end(), in.begin(), in.end());
+        continue;
       }
-      if ((c == '&' || c == '-' || c == '~') && i + 1 < p.size() && p[i + 1] == c && !first) {
-        unsup = true;
-        return n;
+      if ((c == '&' || c == '-' || c == '~') && i + 1 < p.size() && p[i + 1] == c) {
+        i += 2;
+        lhs = op == 0 ? norm(uni) : op == 1 ? set_inter(lhs, uni) : op == 2 ? set_diff(lhs, uni) : set_symdiff(lhs, uni);
+        uni.clear();
+        op = c == '&' ? 1 : c == '-' ? 2 : 3;
+        continue;
       }
-      first = false;
       i++;
       uint32_t lo;
       if (c == '\\') {
         Set s;
         int k = escape(&lo, &s, true);
         if (k == 2) {
-          n->set.insert(n->set.end(), s.begin(), s.end());
+          uni.insert(uni.end(), s.begin(), s.end());
           continue;
         }
-        if (k == 0) return n;
+        if (k == 0) return uni;
       } else {
         lo = c;
       }
@@ -406,27 +453,28 @@ struct Parser {
           int k = escape(&hi, &s);
           if (k != 1) {
             if (k == 2) err = true;
-            return n;
+            return uni;
           }
         } else {
           hi = c2;
         }
         if (hi < lo) {
           err = true;
-          return n;
+          return uni;
         }
       }
-      if (!fu && hi >= 0x80) {  // class_literal_byte: UnicodeNotAllowed in a (?-u) class
-        err = true;
-        return n;
-      }
-      add_folded(n->set, lo, hi);
+      literal(lo, hi);
+      if (err) return uni;
     }
-    if (neg && !fu) {  // (?-u)[^..] can match invalid UTF-8 (Regex on &str)
-      err = true;
-      return n;
-    }
-    n->set = neg ? negate(n->set) : norm(n->set);  // case folding applies before the negation
+    Set r = op == 0 ? norm(uni) : op == 1 ? set_inter(lhs, uni) : op == 2 ? set_diff(lhs, uni) : set_symdiff(lhs, uni);
+    return neg ? negate(r) : r;  // case folding applies before the negation
+  }
+  NodeP cls() {
+    auto n = std::make_unique<Node>();
+    n->t = N_SET;
+    n->set = bracket();
+    // (?-u): a class that can match a byte >= 0x80 can match invalid UTF-8 (Regex on &str)
+    if (!fu && !err && !unsup && !n->set.empty() && n->set.back().hi >= 0x80) err = true;
     return n;
   }
 

@@ -857,13 +857,37 @@ int add_stage(fsg_chain* c, const ModuleSpec& m, const std::string& name, uint8_
 }  // namespace
 
 namespace {
+std::string builtin_name(const ModuleSpec& m) {
+  const auto& by = m.bytes;
+  if (by.size() < 4 || memcmp(by.data(), "\0fsg", 4)) return std::string();
+  return std::string(by.begin() + 4, by.end());
+}
 // stages whose output is the input of a new segment when more stages follow
 bool seg_boundary(const ModuleSpec& m) {
-  const auto& by = m.bytes;
-  if (by.size() < 4 || memcmp(by.data(), "\0fsg", 4)) return false;
-  const std::string name(by.begin() + 4, by.end());
+  const std::string name = builtin_name(m);
   return name == "array_map_json_array" || name == "aggregate-sum" || name == "aggregate" ||
          name == "aggregate-json" || name == "filter_look_back" || name == "filter_hashset";
+}
+// the segment ends of a chain: after every seg_boundary stage that has a
+// successor, and before a filter_hashset whose input is an integer stage's
+// output (map_double / filter_map: the dedup set holds the records' text, so
+// that segment's output is materialized as the text records the reference's
+// next stage receives, engine.rs:147-167)
+std::vector<size_t> seg_ends(const std::vector<ModuleSpec>& mods) {
+  std::vector<size_t> ends;
+  bool int_out = false;  // the value after stage i is an i32 (VT_I32)
+  for (size_t i = 0; i + 1 < mods.size(); i++) {
+    const std::string name = builtin_name(mods[i]);
+    if (name == "map_double" || name == "filter_map") int_out = true;
+    if (seg_boundary(mods[i])) {
+      ends.push_back(i);
+      int_out = false;
+    } else if (int_out && builtin_name(mods[i + 1]) == "filter_hashset") {
+      ends.push_back(i);
+      int_out = false;
+    }
+  }
+  return ends;
 }
 }  // namespace
 
@@ -872,9 +896,7 @@ extern "C" int fsg_chain_builder_initialize(fsg_chain_builder* b, fsg_engine* e,
   if (!e) return fail(FSG_E_INVALID_ARG, "null engine");
   HIPCHK(hipSetDevice(e->device));
   {  // a stage after an array_map / aggregate / stateful filter: a composed chain of segments
-    std::vector<size_t> ends;
-    for (size_t i = 0; i + 1 < b->mods.size(); i++)
-      if (seg_boundary(b->mods[i])) ends.push_back(i);
+    std::vector<size_t> ends = seg_ends(b->mods);
     if (!ends.empty()) {
       ends.push_back(b->mods.size() - 1);
       auto c = std::make_unique<fsg_chain>();

@@ -543,6 +543,45 @@ static void cs_add_tab(cset *s, const cprange *t, size_t n, int neg) {
   for (size_t i = 0; i < tmp.n; i++) cs_add(s, tmp.r[i].lo, tmp.r[i].hi);
   free(tmp.r);
 }
+/* class set operations (regex-syntax ClassSetBinaryOpKind): *a = *a op *b;
+ * op 1 intersection (&&), 2 difference (--), 3 symmetric difference (~~) */
+static void cs_copy(cset *d, const cset *s) {
+  for (size_t i = 0; i < s->n; i++) cs_add(d, s->r[i].lo, s->r[i].hi);
+}
+static void cs_binop(cset *a, const cset *b, int op) {
+  cset na = {0}, nb = {0}, t = {0};
+  cs_copy(&na, a);
+  cs_copy(&nb, b);
+  if (op == 1) { /* a & b = ~(~a | ~b) */
+    cs_negate(&na);
+    cs_negate(&nb);
+    cs_copy(&na, &nb);
+    cs_negate(&na);
+    free(a->r);
+    *a = na;
+    free(nb.r);
+    return;
+  }
+  if (op == 2) { /* a - b = ~(~a | b) */
+    cs_negate(&na);
+    cs_copy(&na, b);
+    cs_negate(&na);
+    free(a->r);
+    *a = na;
+    free(nb.r);
+    return;
+  }
+  /* a ^ b = (a - b) | (b - a) */
+  cs_binop(&na, b, 2);
+  cs_binop(&nb, a, 2);
+  cs_copy(&t, &na);
+  cs_copy(&t, &nb);
+  cs_norm(&t);
+  free(na.r);
+  free(nb.r);
+  free(a->r);
+  *a = t;
+}
 static int cs_has(const cset *s, uint32_t c) {
   size_t lo = 0, hi = s->n;
   while (lo < hi) {
@@ -791,7 +830,8 @@ static int rx_escape(rxparser *P, uint32_t *single, cset *set, int in_class) {
     case 'f': *single = '\f'; return 1;
     case 'v': *single = '\v'; return 1;
     case 'a': *single = 7; return 1;
-    case 'x': {
+    case 'x': case 'u': case 'U': { /* \x7F \x{..}, \u007F \u{..}, \U0000007F \U{..} (regex-syntax parse_hex) */
+      const int fixed = c == 'x' ? 2 : c == 'u' ? 4 : 8;
       uint32_t v = 0;
       if (P->i < P->n && P->p[P->i] == '{') {
         P->i++;
@@ -807,20 +847,21 @@ static int rx_escape(rxparser *P, uint32_t *single, cset *set, int in_class) {
         }
         P->i++;
       } else {
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < fixed; k++) {
           if (P->i >= P->n || !is_hex(P->p[P->i])) {
             P->err = 1;
             return 0;
           }
           v = v * 16 + hexv(P->p[P->i++]);
         }
+        if (v > 0x10FFFF || (v >= 0xD800 && v <= 0xDFFF)) {
+          P->err = 1;
+          return 0;
+        }
       }
       *single = v;
       return 1;
     }
-    case 'u': case 'U':
-      P->unsupported = 1;
-      return 0;
     default:
       if (c < 0x80 && !((c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'))) {
         *single = c; /* escaped punctuation / meta */
@@ -831,23 +872,50 @@ static int rx_escape(rxparser *P, uint32_t *single, cset *set, int in_class) {
   }
 }
 
-static anode *rx_parse_class(rxparser *P) {
-  /* after '[' */
-  anode *a = an_new(A_CLASS);
+/* a bracketed class after its '[' through the matching ']' (regex-syntax
+ * parse_set_class): the items of a union; a nested bracket is an item; the
+ * operators && -- ~~ are left-associative and bind looser than the union; a
+ * leading ']' and leading '-'s are literals; the negation applies last.
+ * Returns 0 ok (the set in *out), -1 on err / unsupported (flags in P). */
+static int rx_parse_bracket(rxparser *P, cset *out) {
   int neg = 0;
   if (P->i < P->n && P->p[P->i] == '^') {
     neg = 1;
     P->i++;
   }
-  int first = 1;
+  cset uni = {0}, lhs = {0};
+  int op = 0, first = 1;
+#define RX_LIT(lo_, hi_)                                                                     \
+  do {                                                                                       \
+    if (!P->fu && (hi_) >= 0x80) { /* class_literal_byte: UnicodeNotAllowed in a (?-u) class */ \
+      P->err = 1;                                                                            \
+      goto fail;                                                                             \
+    }                                                                                        \
+    cs_add_folded(P, &uni, (lo_), (hi_));                                                    \
+  } while (0)
   for (;;) {
     rx_skip_x(P);
     if (P->i >= P->n) {
       P->err = 1;
-      return a;
+      goto fail;
     }
     uint32_t c = P->p[P->i];
-    if (c == ']' && !first) {
+    if (first) { /* parse_set_class_open: a leading ']' and any leading '-' are literals */
+      first = 0;
+      if (c == ']') {
+        P->i++;
+        RX_LIT(']', ']');
+        continue;
+      }
+      if (c == '-') {
+        while (P->i < P->n && P->p[P->i] == '-') {
+          P->i++;
+          RX_LIT('-', '-');
+        }
+        continue;
+      }
+    }
+    if (c == ']') {
       P->i++;
       break;
     }
@@ -863,40 +931,56 @@ static anode *rx_parse_class(rxparser *P) {
       cset tmp = {0};
       if (k + 1 < P->n && posix_class(P->p + j, k - j, &tmp)) {
         if (pneg) cs_negate(&tmp);
-        for (size_t q = 0; q < tmp.n; q++) cs_add_folded(P, &a->cls, tmp.r[q].lo, tmp.r[q].hi);
+        for (size_t q = 0; q < tmp.n; q++) cs_add_folded(P, &uni, tmp.r[q].lo, tmp.r[q].hi);
         free(tmp.r);
         P->i = k + 2;
-        first = 0;
         continue;
       }
       free(tmp.r);
     }
-    if (c == '[') {
-      P->unsupported = 1; /* nested classes */
-      return a;
+    if (c == '[') { /* a nested class: one item of the union */
+      P->i++;
+      cset in = {0};
+      if (++P->depth > 64) {
+        P->unsupported = 1;
+        goto fail;
+      }
+      int r = rx_parse_bracket(P, &in);
+      P->depth--;
+      if (r) {
+        free(in.r);
+        goto fail;
+      }
+      cs_copy(&uni, &in);
+      free(in.r);
+      continue;
     }
-    if ((c == '&' || c == '-' || c == '~') && P->i + 1 < P->n && P->p[P->i + 1] == c && !first) {
-      P->unsupported = 1; /* set operations */
-      return a;
+    if ((c == '&' || c == '-' || c == '~') && P->i + 1 < P->n && P->p[P->i + 1] == c) {
+      P->i += 2;
+      if (op == 0) {
+        cs_copy(&lhs, &uni);
+        cs_norm(&lhs);
+      } else {
+        cs_binop(&lhs, &uni, op);
+      }
+      free(uni.r);
+      memset(&uni, 0, sizeof uni);
+      op = c == '&' ? 1 : c == '-' ? 2 : 3;
+      continue;
     }
-    first = 0;
     uint32_t lo;
     P->i++;
     if (c == '\\') {
       cset tmp = {0};
       int k = rx_escape(P, &lo, &tmp, 1);
       if (k == 2) {
-        for (size_t j = 0; j < tmp.n; j++) cs_add(&a->cls, tmp.r[j].lo, tmp.r[j].hi);
+        cs_copy(&uni, &tmp);
         free(tmp.r);
         continue;
       }
-      if (k >= 3) {
-        P->err = 1;
-        free(tmp.r);
-        return a;
-      }
       free(tmp.r);
-      if (k == 0) return a;
+      if (k >= 3) P->err = 1;
+      if (k != 1) goto fail;
     } else {
       lo = c;
     }
@@ -921,27 +1005,42 @@ static anode *rx_parse_class(rxparser *P) {
         free(tmp.r);
         if (k != 1) {
           if (k == 2) P->err = 1;
-          return a;
+          goto fail;
         }
       } else
         hi = c2;
       if (hi < lo) {
         P->err = 1;
-        return a;
+        goto fail;
       }
     }
-    if (!P->fu && hi >= 0x80) { /* class_literal_byte: UnicodeNotAllowed in a (?-u) class */
-      P->err = 1;
-      return a;
-    }
-    cs_add_folded(P, &a->cls, lo, hi);
+    RX_LIT(lo, hi);
   }
-  if (neg && !P->fu) { /* (?-u)[^..] can match invalid UTF-8 */
-    P->err = 1;
-    return a;
+#undef RX_LIT
+  if (op == 0) {
+    cs_norm(&uni);
+    *out = uni;
+  } else {
+    cs_binop(&lhs, &uni, op);
+    free(uni.r);
+    *out = lhs;
+    memset(&lhs, 0, sizeof lhs);
   }
-  if (neg) cs_negate(&a->cls); /* case folding applies before the negation */
-  cs_norm(&a->cls);
+  free(lhs.r);
+  if (neg) cs_negate(out); /* case folding applies before the negation */
+  cs_norm(out);
+  return 0;
+fail:
+  free(uni.r);
+  free(lhs.r);
+  return -1;
+}
+static anode *rx_parse_class(rxparser *P) {
+  /* after '[' */
+  anode *a = an_new(A_CLASS);
+  if (rx_parse_bracket(P, &a->cls)) return a;
+  /* (?-u): a class that can match a byte >= 0x80 can match invalid UTF-8 (Regex on &str) */
+  if (!P->fu && a->cls.n && a->cls.r[a->cls.n - 1].hi >= 0x80) P->err = 1;
   return a;
 }
 

@@ -1261,6 +1261,10 @@ SF_CHAINS = {
     "dedup_zero": [("filter_hashset", {"count": "0"}, None)],
     "map_dedup": [("map", {}, None), ("filter_hashset", {"count": "500"}, None)],
     "filter_dedup": [("filter_with_param", {"key": "1"}, None), ("filter_hashset", {}, None)],
+    # an integer stage before the dedup: the set holds the records' text (a segment boundary)
+    "map_double_dedup": [("map_double", {}, None), ("filter_hashset", {"count": "300"}, None)],
+    "filter_map_dedup": [("filter_map", {}, None), ("filter_hashset", {}, None)],
+    "map_double_odd_dedup": [("map_double", {}, None), ("filter_odd", {}, None), ("filter_hashset", {}, None)],
 }
 
 

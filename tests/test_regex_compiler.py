@@ -25,7 +25,12 @@ PATTERNS = [r"\d{3}-\d{2}-\d{4}", r"[A-Z]", r"^ab|cd$", r"a(b|c)*d", r"colou?r\s
             r"(?i:ab)c", r"(?i)[^a]", r"(?s)a.c", r"\Aab", r"cd\z", r"[[:alpha:]]{3}", r"[[:^digit:][:space:]]x",
             r"(?i)[[:lower:]]{2}\b", r"\w+é", r"^\w+$", r"\W\w", r"[\w-]{3}", r"\p{Lu}", r"\P{L}\pN",
             r"\p{gc=Nd}", r"[\p{Sc}\d]", r"\p{^Ll}", r"(?m)^b$", r"(?m)a$|^c", r"(?m:^)x|y(?-m)$",
-            r"(?x) a b # comment", r"(?x)[ a ] c", r"(?x: \d \  \d )", r"(?-u)\w\d\s", r"(?u)\w(?-u:[a-z])"]
+            r"(?x) a b # comment", r"(?x)[ a ] c", r"(?x: \d \  \d )", r"(?-u)\w\d\s", r"(?u)\w(?-u:[a-z])",
+            # nested classes, class set operations, \u / \U escapes
+            r"[a-z&&[^aeiou]]{2}", r"[\w--\d]+x", r"[a-g~~c-j]", r"[0-9--4]", r"[[a-c][x-z]]", r"[^[a-c]d]",
+            r"[a-z&&b-y&&[^m]]", r"[\pL&&\p{Ll}]é", r"[\p{L}--[a-zé]]", r"[a-c~~b-d~~c-e]", r"[--a]", r"[]a]",
+            r"[a-c--b]d", r"\u0041\U0001F600?\u{263a}", r"[\u00e9-\u00ea\U000003b1]", r"(?i)[a-z--k]",
+            r"(?-u)[[^a]&&[b-c]]", r"(?x)[ a-z && [^ x ] ]"]
 WORD = ("\\b", "\\B")
 
 
@@ -64,7 +69,9 @@ def test_max_len():
                                       (r"\p{", _ffi.FSG_E_INIT), (r"\p{Nope}", _ffi.FSG_E_UNSUPPORTED),
                                       (r"(?i)\p{Lu}", _ffi.FSG_E_UNSUPPORTED), ("(?R)a", _ffi.FSG_E_UNSUPPORTED),
                                       (r"\p{Greek}", _ffi.FSG_E_UNSUPPORTED), ("(?i)é", _ffi.FSG_E_UNSUPPORTED),
-                                      ("[[a]]", _ffi.FSG_E_UNSUPPORTED)])
+                                      ("[a-c", _ffi.FSG_E_INIT), ("[a[b]", _ffi.FSG_E_INIT), (r"\u12", _ffi.FSG_E_INIT),
+                                      (r"\u{110000}", _ffi.FSG_E_INIT), (r"\ud800", _ffi.FSG_E_INIT),
+                                      (r"(?-u)[[^a]--b]", _ffi.FSG_E_INIT)])
 def test_errors_agree_with_oracle(bad, code):
     with pytest.raises(ValueError) as e:
         dfa_match(bad, b"x")
@@ -75,7 +82,8 @@ def test_errors_agree_with_oracle(bad, code):
 
 def _random_pattern(rng, depth=0):
     atoms = ["a", "b", "é", "α", ".", r"\d", r"\w", r"\W", r"\s", r"\pL", r"\p{Lu}", r"\P{N}", "[a-cé]", "[^b]",
-             r"[\w-]", r"[α-ω\d]", "^", "$", r"\x{263A}", "(?m:^)", "(?m:$)", "(?i:ab)", "(?s:.)"]
+             r"[\w-]", r"[α-ω\d]", "^", "$", r"\x{263A}", "(?m:^)", "(?m:$)", "(?i:ab)", "(?s:.)",
+             r"[\w&&[^a\d]]", r"[[a-c]--b]", r"[é~~\pL]", r"[^[α-ω]&&\pL]", r"\u00e9"]
     if depth > 2 or rng.random() < 0.4:
         a = rng.choice(atoms)
     elif rng.random() < 0.5:
@@ -135,3 +143,19 @@ def test_non_ascii_class_literal_without_unicode(bad):
     with pytest.raises(ValueError):
         O.regex_is_match(bad, b"x")
     assert dfa_match(r"(?-u)é", "é".encode())[0] and O.regex_is_match(r"(?-u)é", "é".encode())
+
+
+@pytest.mark.parametrize("pattern", [r"[a-z&&[^aeiou]]", r"[a-y&&xyz]", r"[0-9--4]", r"[a-g~~b-h]", r"[\w--\d]",
+                                     r"[[a-c][x-z]]x", r"[^[a-c]d]", r"[a-z--[b-y]&&[^z]]", r"[a-c~~b-d~~c-e]",
+                                     r"[0-9&&[^4]]{2}", r"\u0041b", r"[\u0061-\u0063]z"])
+def test_set_operations_against_python_regex(pattern):
+    """regex-syntax's class set operations / nested classes / \\u escapes on ASCII
+    text, against Python's `regex` module (V1 set syntax, the same grammar on
+    these patterns): the DFA and the oracle agree with it."""
+    regex = pytest.importorskip("regex")
+    rng = random.Random(hash(pattern) & 0xFFFF)
+    for _ in range(200):
+        t = "".join(rng.choice("abcdefghmxyz0459AZ_-") for _ in range(rng.randint(0, 6)))
+        want = regex.search("(?V1)" + pattern, t) is not None
+        assert dfa_match(pattern, t.encode())[0] == want, (pattern, t)
+        assert O.regex_is_match(pattern, t.encode()) == want, (pattern, t)
