@@ -138,9 +138,10 @@ def pmc_traffic(workload, kernel, n_records, n_batches):
     db = json.load(open(path)).get(workload)
     if not db or db.get("lib") != lib_tag() or db.get("n_records") != n_records or db.get("n_batches") != n_batches:
         return None, None
-    # the eval bracket covers k_eval_lean / k_arr_lean + the deferred exact k_eval<N>; crc: k_crc16 +
-    # k_crc_final; write: k_write(_lean) + k_write_canon
-    pre = ("fsg::" + kernel,) + (("fsg::k_arr_lean",) if kernel == "k_eval" else ())
+    # the eval bracket covers k_chase + k_eval_lean, the flat path's k_flat_scan + k_flat_decide,
+    # k_arr_frame + k_arr_lean, and the deferred exact k_eval<N>; crc: k_crc16 + k_crc_final;
+    # write: k_write(_lean) + k_write_canon
+    pre = ("fsg::" + kernel,) + (("fsg::k_arr_", "fsg::k_flat_", "fsg::k_chase") if kernel == "k_eval" else ())
     hits = [v["total"] for k, v in db["kernels"].items() if k.split("<")[0].startswith(pre)]
     return (sum(hits), db["source"]) if hits else (None, None)
 

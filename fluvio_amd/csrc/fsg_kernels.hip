@@ -2806,7 +2806,7 @@ struct __attribute__((aligned(16))) WlLds {
 };
 
 // the generic writer of one batch (k_write's body), wave-wide
-__device__ void write_batch_wave(const WriteArgs& a, const KeptRec* d, uint32_t nkeep, int64_t rel, uint64_t obase) {
+__device__ __forceinline__ void write_batch_wave(const WriteArgs& a, const KeptRec* d, uint32_t nkeep, int64_t rel, uint64_t obase) {
   const uint32_t lane = lane_id();
   uint8_t* out = a.out;
   uint64_t run = 0;

@@ -10,7 +10,7 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 for W in c2-substring c1-regex c2-json c3-filter-map; do
   timeout -k 10 300 python -u bench.py --workload $W --only --steps 10 --warmup 2 --no-cpu-baseline --no-e2e > $O/$W.json 2> $O/$W.err || exit $?
 done
-FSG_NO_FLAT=1 timeout -k 10 300 python -u bench.py --workload c2-substring --only --steps 10 --warmup 2 --no-cpu-baseline --no-e2e > $O/c2-noflat.json 2> $O/c2-noflat.err || exit $?
+FSG_WRITE_LDS=1 timeout -k 10 300 python -u bench.py --workload c2-substring --only --steps 10 --warmup 2 --no-cpu-baseline --no-e2e > $O/c2-noflat.json 2> $O/c2-noflat.err || exit $?
 B="python3 $GRAFT_REPO_ROOT/bench.py --workload c2-substring --only --steps 5 --warmup 1 --no-cpu-baseline --no-e2e"
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o kt -- $B > "$O/kt.log" 2>&1 || exit $?
