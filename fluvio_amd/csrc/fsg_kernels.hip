@@ -424,6 +424,92 @@ __device__ bool walk_fast(WaveLds& L, const uint8_t* w, uint64_t wbase, uint32_t
   return ok;
 }
 
+// ---------------------------------------------------------------------------
+// Parallel framing of a batch of many small records (k_eval<kOpsInt / kOpsAll>,
+// a batch whose section is resident in the window and holds more than kMaxR
+// records: aggregate-sum, filter_hashset, integer maps over decimal values).
+// The lane-0 chase costs one dependent LDS round trip per record and a window
+// reload per kMaxR records; here every byte position p of the section gets
+// nx(p) = where a record starting at p would end (its length varint decoded as
+// walk_fast decodes it), J = nx^32 by five in-place squarings, lane 0 follows
+// J from the first record (one hop per 32 records), and one lane per hop fills
+// in its 32 record starts with nx.  Any position whose length does not decode,
+// a chain that does not end exactly at the section end, or a record count
+// other than the header's leaves the batch to the exact walk (nothing is
+// decided from here: walk_fast re-parses every record it is given).
+// ---------------------------------------------------------------------------
+constexpr int kParMaxR = 4096;  // record starts held (a 16 KiB section of 7-byte records: ~2,340)
+constexpr int kParHop = 32;     // J = nx^kParHop
+constexpr uint32_t kParBad = 0xFFFFu;
+struct __attribute__((aligned(16))) ParLds {
+  uint16_t J[kWin + 16];               // section-relative successor^32 (n = exact end, kParBad = undecodable)
+  uint16_t rs[kParMaxR];               // record starts (window offsets)
+  uint16_t lead[kParMaxR / kParHop];   // every kParHop-th record start (section-relative)
+  uint32_t nlead, total, ok;
+};
+// where a record starting at window offset q would end (section-relative to c0), or kParBad
+__device__ __forceinline__ uint32_t par_next(const uint8_t* w, uint32_t q, uint32_t c0, uint32_t lim) {
+  int64_t len;
+  if (wvarint(w, q, lim, &len)) return kParBad;
+  if (len < 0 || (int64_t)(lim - q) < len) return kParBad;
+  return q + (uint32_t)len - c0;
+}
+// record starts of the section [c0, lim) (window offsets) into P.rs; true when
+// exactly `count` records tile it
+__device__ bool par_frame(const uint8_t* w, ParLds& P, uint32_t c0, uint32_t lim, uint32_t count) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t n = lim - c0;
+  for (uint32_t i = tid; i < n; i += kEvalThreads) P.J[i] = (uint16_t)par_next(w, c0 + i, c0, lim);
+  __syncthreads();
+  // five squarings in place: a chunk's successors-of-successors are read before any is written
+  constexpr int kC = 16;
+  for (int r = 0; r < 5; r++) {
+    for (uint32_t base = 0; base < n; base += kEvalThreads * kC) {
+      uint16_t v[kC];
+#pragma unroll
+      for (int k = 0; k < kC; k++) {
+        const uint32_t i = base + (uint32_t)k * kEvalThreads + tid;
+        const uint32_t j = i < n ? P.J[i] : kParBad;
+        v[k] = (uint16_t)(j >= n ? j : P.J[j]);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < kC; k++) {
+        const uint32_t i = base + (uint32_t)k * kEvalThreads + tid;
+        if (i < n) P.J[i] = v[k];
+      }
+      __syncthreads();
+    }
+  }
+  if (tid == 0) {
+    uint32_t p = 0, k = 0;
+    bool ok = true;
+    while (p < n) {
+      if (k >= (uint32_t)(kParMaxR / kParHop)) {
+        ok = false;
+        break;
+      }
+      P.lead[k++] = (uint16_t)p;
+      p = P.J[p];
+    }
+    P.nlead = k;
+    P.ok = ok && p == n;
+  }
+  __syncthreads();
+  if (!P.ok) return false;
+  const uint32_t nl = P.nlead;
+  if (tid < nl) {  // hop t: records [32 t, 32 t + 32)
+    uint32_t p = P.lead[tid], s = 0;
+    for (; s < (uint32_t)kParHop && p < n; s++) {
+      P.rs[tid * kParHop + s] = (uint16_t)(c0 + p);
+      p = par_next(w, c0 + p, c0, lim);
+    }
+    if (tid + 1 == nl) P.total = tid * kParHop + s;
+  }
+  __syncthreads();
+  return P.total == count;
+}
+
 // find the record whose [start, ...) region contains window offset p (largest r with r_vs[r] <= p)
 __device__ __forceinline__ int find_rec(const WaveLds& L, int nr, uint32_t p) {
   int lo = 0, hi = nr - 1, r = -1;
@@ -922,7 +1008,7 @@ __device__ __forceinline__ void load_window(WaveLds& L, const uint8_t* slice, ui
 // walk and the ordered emission run on wave 0
 // ---------------------------------------------------------------------------
 template <uint32_t kOps>
-__device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const uint32_t b) {
+__device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const uint32_t b, ParLds* PL = nullptr) {
   const uint32_t l = lane_id();
   const uint32_t tid = threadIdx.x;
   const bool wave0 = tid < 64;
@@ -980,9 +1066,20 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
   bool first_window = true;  // the window at al0 is already resident
   const uint32_t nrec_total = count > 0 ? (uint32_t)count : 0u;
   // record starts from k_chase_w / k_chase when they framed this batch
-  const uint32_t rend_b = a.rend ? a.rend[b] : 0xFFFFu;
+  uint32_t rend_b = a.rend ? a.rend[b] : 0xFFFFu;
   const uint16_t* rsb = (a.rstart && rend_b != 0xFFFFu) ? a.rstart + a.rbase[b] : nullptr;
   const uint64_t rb = a.rbase[b];
+  // many small records in a resident section: framed in parallel (par_frame),
+  // the window kept for every group of kMaxR records
+  bool resident = false;
+  if (PL && !rsb && nrec_total > (uint32_t)kMaxR && nrec_total <= (uint32_t)kParMaxR &&
+      sec_end + 16 <= al0 + (uint64_t)kWin) {
+    if (par_frame((const uint8_t*)L.win, *PL, (uint32_t)(sec0 + 4 - al0), (uint32_t)(sec_end - al0), nrec_total)) {
+      rsb = PL->rs;
+      rend_b = (uint32_t)(sec_end - al0);
+      resident = true;
+    }
+  }
   // phase A: full chain; phase B (only if a record error occurred): truncated
   // chain.  A pass-through batch runs no stage: its records are kept as they are.
   const bool passthru = a.pass && a.pass[b];
@@ -1014,13 +1111,13 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
     const uint8_t out_type = (nst == (int)ch.nstages) ? (uint8_t)ch.out_type : ch.st[nst].in_type;
     while (done_recs < nrec_total && done_recs < (phase == 1 ? rec_cap + 1 : nrec_total)) {
       // window [al, al + wlen)
-      const uint64_t al = first_window ? al0 : (cursor & ~15ull);
+      const uint64_t al = (first_window || resident) ? al0 : (cursor & ~15ull);
       uint64_t wend = al + kWin;
       const uint64_t sec_end16 = (sec_end + 15) & ~15ull;
       if (wend > sec_end16) wend = sec_end16;
       const uint32_t wlen = (uint32_t)(wend - al);
       __syncthreads();
-      if (!first_window) load_window(L, S, al, wlen);
+      if (!first_window && !resident) load_window(L, S, al, wlen);
       first_window = false;
       if (!walk_fast(L, (const uint8_t*)L.win, al, wlen, sec_end, cursor, nrec_total - done_recs, rsb, al0, done_recs,
                      rend_b)) {
@@ -1210,9 +1307,17 @@ template <uint32_t kOps>
 __global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : (kOps == kOpsArray ? 3 : 2)) void k_eval(EvalArgs a) {
   __shared__ WaveLds L;
   const uint32_t n = a.list ? a.list[0] : a.nbatches;
-  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-    eval_batch<kOps>(a, L, a.list ? a.list[1 + i] : i);
-    __syncthreads();  // the window is reused by the next batch
+  if constexpr (kOps == kOpsInt || kOps == kOpsAll) {  // batches of many small records: parallel framing
+    __shared__ ParLds P;
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+      eval_batch<kOps>(a, L, a.list ? a.list[1 + i] : i, &P);
+      __syncthreads();
+    }
+  } else {
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+      eval_batch<kOps>(a, L, a.list ? a.list[1 + i] : i);
+      __syncthreads();  // the window is reused by the next batch
+    }
   }
 }
 
@@ -1496,6 +1601,16 @@ __device__ __forceinline__ void plan_run(const PlanArgs& a) {
       p.bytes_in = r.bytes_in;
       p.invocations = m + 1;
     }
+    if (a.has_agg && p.done >= 0) {
+      // the aggregate's accumulator after the completed calls: the chain
+      // instance keeps it although process_batch returns the error
+      // (smartengine batch loop: `process(input)?` per batch)
+      const ScanRow rd = incl_at(a, (uint32_t)p.done);
+      p.acc_final = (int64_t)(int32_t)((uint64_t)a.acc0 + (uint64_t)rd.agg);
+      p.cat_final = rd.cat;
+      p.acc_touched = rd.recs_out > 0;
+      p.stop = p.done;  // k_cat appends through it
+    }
     *a.plan = p;
     return;
   }
@@ -1541,7 +1656,7 @@ __global__ void k_plan(PlanArgs a) {
 __global__ void k_state(const Plan* plan, int32_t* state) {
   if (threadIdx.x != 0) return;
   const Plan p = *plan;
-  if (p.status == 0 && p.acc_touched) *state = (int32_t)p.acc_final;
+  if (p.acc_touched) *state = (int32_t)p.acc_final;  // also through `done` when the call fails
 }
 
 // ---------------------------------------------------------------------------

@@ -2328,6 +2328,44 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     m->invocation_count += p.invocations;
     if (c->hdesc.nstages) m->records_out += p.records_out;  // the empty chain adds none (engine.rs:179-184)
   }
+  if (p.status != 0 && !so && p.done >= 0) {
+    // process() completed for batches 0..done before the failing one: their
+    // state stands (the reference's chain instance keeps it), as on success
+    int rc = FSG_OK;
+    if (has_aggj) {
+      // the commit lists the keys in the last folded record's output order:
+      // this chain's order walk alone (a group call's walks do not wait for it)
+      unsigned long long sc[4] = {0, 0, 0, 0};  // scal[6] ord slots
+      HIPCHK(hipMemcpy(sc, aj.scal + 3, sizeof sc, hipMemcpyDeviceToHost));
+      HIPCHK(c->aj_ord.ensure(std::max<uint64_t>(sc[3], 1) * 4));
+      aj.ord = c->aj_ord.as<uint32_t>();
+      launch_aggj_hash(aj, st);
+      launch_aggj_order(aj, st);
+      HIPCHK(hipGetLastError());
+      rc = aj_commit(c, aj, p.done, (uint32_t)(aj.n_init + aj_nnew));
+    } else if (has_agg && p.acc_touched) {
+      if (has_cat) {  // the accumulator stream through `done` (k_cat reads plan.stop = done)
+        HIPCHK(c->cat.ensure(kCatOff + c->acc.size() + p.cat_final + 64));
+        if (!c->acc.empty())
+          HIPCHK(hipMemcpyAsync(c->cat.as<uint8_t>() + kCatOff, c->acc.data(), c->acc.size(), hipMemcpyHostToDevice, st));
+        WriteArgs wc{};
+        wc.slice = ea.slice;
+        wc.bstat = ea.bstat;
+        wc.desc = ea.desc;
+        wc.rbase = ea.rbase;
+        wc.pre = pa.pre;
+        wc.agg_pre = c->aggpre.as<ScanRow>();
+        wc.plan = pa.plan;
+        wc.acc_len = sa.acc_len;
+        wc.cat = c->cat.as<uint8_t>();
+        launch_cat(wc, nb, st);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(st));
+      }
+      rc = acc_update(c, p, has_cat);
+    }
+    if (rc) return rc;
+  }
   if (p.status != 0) {
     const char* why = p.status == FSG_E_UNSUPPORTED ? "input needs a feature the GPU path does not implement"
                       : p.status == FSG_E_IO        ? "io error while decoding batches"

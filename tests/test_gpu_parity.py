@@ -1725,3 +1725,142 @@ def test_group_process_slices(comm_engine):
             _same_batch(outs[i], os_[i].process_batch(sl))
             if m[-1][0] in ("aggregate-json", "aggregate-sum"):
                 assert gs[i].accumulator(len(m) - 1) == os_[i].accumulator(len(m) - 1), (call, i)
+
+
+# ---------------------------------------------------------------------------
+# par_frame (k_eval<kOpsInt / kOpsAll>): batches of more than 128 small records
+# framed in parallel (successor^32 by squaring, one lane per 32 records); a
+# malformed length, a header count other than the records present, or any
+# record whose fields do not tile it leaves the batch to the serial walk
+# ---------------------------------------------------------------------------
+def _raw_batch(base, raws, count=None):
+    h = P.BatchHeader()
+    h.last_offset_delta = len(raws) - 1
+    body = struct.pack(">hiqqqhi", h.attributes, h.last_offset_delta, h.first_timestamp, h.max_time_stamp,
+                       h.producer_id, h.producer_epoch, h.first_sequence)
+    recs = struct.pack(">I", len(raws) if count is None else count & 0xFFFFFFFF) + b"".join(raws)
+    body += recs
+    return struct.pack(">qiibI", base, P.BATCH_HEADER_SIZE + len(recs), h.partition_leader_epoch, h.magic,
+                       P.crc32c(body)) + body
+
+
+def _small_records(rnd, n, bad_value=None, keys=True, hi=99999):
+    out = []
+    for i in range(n):
+        v = str(rnd.randint(-hi, hi)).encode() if rnd.random() < 0.9 else str(rnd.randint(0, 9)).encode()
+        if bad_value is not None and i == bad_value:
+            v = b"12x"
+        k = None if (not keys or rnd.random() < 0.8) else rnd.choice([b"", b"k", b"key7"])
+        r = P.Record.new_key_value(k, v)
+        r.preamble.offset_delta = i
+        out.append(r.encode())
+    return out
+
+
+def _noncanonical_len(raw):
+    ln, pos = P.varint_decode(raw, 0)
+    z = (ln << 1) & 0xFF  # zigzag of a small non-negative length, one byte
+    assert z < 0x80
+    return bytes([z | 0x80, 0x00]) + raw[pos:]
+
+
+def _par_slices():
+    rnd = random.Random(5)
+    good = b""
+    base = 0
+    for n in (129, 200, 700, 1000, 1500, 2000):
+        good += _raw_batch(base, _small_records(rnd, n))
+        base += n + 2
+    cases = {"good": good}
+    recs = _small_records(rnd, 900)
+    r = bytearray(recs[611])  # key tag 2: Record::decode fails ("not valid bool value")
+    ln, pos = P.varint_decode(bytes(r), 0)
+    i = pos + 1
+    _, i = P.varint_decode(bytes(r), i)
+    _, i = P.varint_decode(bytes(r), i)
+    r[i] = 2
+    cases["bad_tag"] = good + _raw_batch(base, recs[:611] + [bytes(r)] + recs[612:])
+    recs = _small_records(rnd, 800)
+    cases["count_low"] = _raw_batch(0, recs[:400]) + _raw_batch(400, recs, count=799)
+    cases["count_high"] = _raw_batch(0, recs[:300]) + _raw_batch(300, recs, count=801)
+    recs = _small_records(rnd, 1200)
+    cases["noncanonical"] = _raw_batch(0, [_noncanonical_len(x) if j % 97 == 5 else x for j, x in enumerate(recs)])
+    cases["parse_error"] = good + _raw_batch(base, _small_records(rnd, 1300, bad_value=1000))
+    cases["unkeyed_2300"] = _raw_batch(0, _small_records(rnd, 2300, keys=False))  # beyond the window: serial walk
+    short = b""
+    for j, n in enumerate((1800, 1500, 1100, 130)):  # resident sections of up to ~1,800 records
+        short += _raw_batch(j * 2000, _small_records(rnd, n, keys=False, hi=9 if n > 1500 else 999))
+    cases["short"] = short
+    return cases
+
+
+@pytest.mark.parametrize("chain", [
+    [("filter_odd", {}, None)],
+    [("map_double", {}, None)],
+    [("filter_map", {}, None)],
+    [("aggregate-sum", {}, b"7")],
+    [("filter_with_param", {"key": "1"}, None), ("aggregate-sum", {}, None)],
+    [("filter_hashset", {}, None)],
+    [("map_double", {}, None), ("filter_map", {}, None)],
+    [("regex-filter", {"regex": r"\d"}, None), ("filter_odd", {}, None)],  # k_eval<kOpsAll>
+])
+def test_par_frame_many_small_records(engine, chain):
+    for name, sl in _par_slices().items():
+        try:
+            check_batch(engine, chain, sl)
+        except AssertionError as e:
+            raise AssertionError(f"slice {name}: {e}") from e
+
+
+def _bad_tag_batch(base, n=20, at=7):
+    raws = []
+    for i in range(n):
+        r = P.Record.new_key_value(None, str(i * 3 + 1).encode())
+        r.preamble.offset_delta = i
+        raws.append(bytearray(r.encode()))
+    r = raws[at]  # len, attr, ts, od, then the key tag
+    _, i = P.varint_decode(bytes(r), 0)
+    i += 1
+    _, i = P.varint_decode(bytes(r), i)
+    _, i = P.varint_decode(bytes(r), i)
+    r[i] = 2
+    return _raw_batch(base, [bytes(x) for x in raws])
+
+
+@pytest.mark.parametrize("chain,kind", [
+    ([("aggregate-sum", {}, b"7")], "int"),
+    ([("filter_with_param", {"key": "1"}, None), ("aggregate-sum", {}, None)], "int"),
+    ([("aggregate", {}, b"A")], "int"),
+    ([("aggregate-json", {}, None)], "json"),
+    ([("filter_hashset", {}, None)], "int"),
+    ([("filter_look_back", {}, None)], "int"),
+])
+def test_state_kept_before_decode_error(engine, chain, kind):
+    """A batch that fails to decode ends process_batch with the error, but the
+    calls that completed before it changed the chain's state (the reference's
+    batch loop returns at `process(input)?`): the next call sees that state."""
+    if kind == "int":
+        rnd = random.Random(9)
+        good = b"".join(_raw_batch(j * 100, _small_records(rnd, 40, keys=False, hi=500)) for j in range(3))
+        later = _raw_batch(1000, _small_records(rnd, 30, keys=False, hi=500))
+    else:
+        good = _keyed_slice(4, nbatches=5)
+        later = _keyed_slice(5, nbatches=3)
+    g = gpu_chain(engine, chain)
+    o = orc_chain(chain)
+    bad = good + _bad_tag_batch(5000)
+    oo = o.process_batch(bad, (1 << 64) - 1)
+    assert oo["status"] != 0
+    with pytest.raises(Exception) as ei:
+        g.process_batch(bad, (1 << 64) - 1, SmartModuleChainMetrics())
+    assert getattr(ei.value, "code", None) == oo["status"]
+    for i, m in enumerate(chain):
+        if m[0] in ("aggregate-sum", "aggregate", "aggregate-json"):
+            assert g.accumulator(i) == o.accumulator(i)
+    gout = g.process_batch(later, (1 << 64) - 1, SmartModuleChainMetrics())
+    oo = o.process_batch(later, (1 << 64) - 1)
+    assert oo["status"] == 0
+    assert gout.raw == oo["bytes"]
+    for i, m in enumerate(chain):
+        if m[0] in ("aggregate-sum", "aggregate", "aggregate-json"):
+            assert g.accumulator(i) == o.accumulator(i)
