@@ -328,6 +328,8 @@ struct WriteArgs {
   const uint8_t* cat;      // aggregate (concat): kCatOff + accumulator stream
   uint64_t acc_len;
   uint32_t seg;            // 1: segment output: batch b's records at 61 * (b + 1) + pre[b], rel = 0
+  int32_t first, last;     // plan.first / plan.last as the host read them (k_write_lean: no plan load
+                           // ahead of the batch rows)
 };
 // k_arr_write: the output records of the BF_ARR_LEAN batches of [plan.first,
 // plan.last], re-walked from the source window (fsg_array.hip)

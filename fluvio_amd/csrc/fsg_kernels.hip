@@ -137,7 +137,7 @@ __device__ void utf8_trim(P s, uint32_t n, uint32_t* b, uint32_t* e) {
 
 // <i32 as FromStr>::from_str — 0 ok, 1 Empty, 2 InvalidDigit, 3 PosOverflow, 4 NegOverflow
 template <typename P>
-__device__ int parse_i32(P s, uint32_t n, int32_t* out) {
+__device__ __forceinline__ int parse_i32(P s, uint32_t n, int32_t* out) {
   if (n == 0) return 1;
   uint32_t i = 0;
   bool pos = true;
@@ -329,7 +329,7 @@ done:
 // parses its own records exactly (Record::decode) and checks that the fields end
 // where the length said.  Any inconsistency -> caller runs the exact serial walk.
 // Returns true when the window was walked.
-__device__ bool walk_fast(WaveLds& L, const uint8_t* w, uint64_t wbase, uint32_t wlen, uint64_t sec_end,
+__device__ __forceinline__ bool walk_fast(WaveLds& L, const uint8_t* w, uint64_t wbase, uint32_t wlen, uint64_t sec_end,
                           uint64_t cursor, uint32_t rec_remaining, const uint16_t* rsb = nullptr, uint64_t al0 = 0,
                           uint32_t done = 0, uint32_t rend = 0) {
   const uint32_t tid = threadIdx.x;
@@ -456,7 +456,7 @@ __device__ __forceinline__ uint32_t par_next(const uint8_t* w, uint32_t q, uint3
 }
 // record starts of the section [c0, lim) (window offsets) into P.rs; true when
 // exactly `count` records tile it
-__device__ bool par_frame(const uint8_t* w, ParLds& P, uint32_t c0, uint32_t lim, uint32_t count) {
+__device__ __forceinline__ bool par_frame(const uint8_t* w, ParLds& P, uint32_t c0, uint32_t lim, uint32_t count) {
   const uint32_t tid = threadIdx.x;
   const uint32_t n = lim - c0;
   for (uint32_t i = tid; i < n; i += kEvalThreads) P.J[i] = (uint16_t)par_next(w, c0 + i, c0, lim);
@@ -1007,6 +1007,15 @@ __device__ __forceinline__ void load_window(WaveLds& L, const uint8_t* slice, ui
 // shared, the scans and per-record work spread over the 4 waves, the serial
 // walk and the ordered emission run on wave 0
 // ---------------------------------------------------------------------------
+#ifdef FSG_EVAL_TIMING  // experiment builds: per-phase clock sums of workgroup 0, printed at its end
+__shared__ unsigned long long et_acc[6];
+#define ET_MARK(v) const unsigned long long v = (threadIdx.x == 0) ? (unsigned long long)clock64() : 0ull
+#define ET_ADD(i, a0, a1) \
+  if (threadIdx.x == 0) et_acc[i] += (a1) - (a0)
+#else
+#define ET_MARK(v)
+#define ET_ADD(i, a0, a1)
+#endif
 template <uint32_t kOps>
 __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const uint32_t b, ParLds* PL = nullptr) {
   const uint32_t l = lane_id();
@@ -1072,6 +1081,7 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
   // many small records in a resident section: framed in parallel (par_frame),
   // the window kept for every group of kMaxR records
   bool resident = false;
+  ET_MARK(tp0);
   if (PL && !rsb && nrec_total > (uint32_t)kMaxR && nrec_total <= (uint32_t)kParMaxR &&
       sec_end + 16 <= al0 + (uint64_t)kWin) {
     if (par_frame((const uint8_t*)L.win, *PL, (uint32_t)(sec0 + 4 - al0), (uint32_t)(sec_end - al0), nrec_total)) {
@@ -1080,6 +1090,11 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
       resident = true;
     }
   }
+  ET_MARK(tp1);
+  ET_ADD(0, tp0, tp1);
+#ifdef FSG_EVAL_TIMING
+  if (threadIdx.x == 0) et_acc[5] += resident ? 1000000ull : 1ull;
+#endif
   // phase A: full chain; phase B (only if a record error occurred): truncated
   // chain.  A pass-through batch runs no stage: its records are kept as they are.
   const bool passthru = a.pass && a.pass[b];
@@ -1119,6 +1134,7 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
       __syncthreads();
       if (!first_window && !resident) load_window(L, S, al, wlen);
       first_window = false;
+      ET_MARK(tw0);
       if (!walk_fast(L, (const uint8_t*)L.win, al, wlen, sec_end, cursor, nrec_total - done_recs, rsb, al0, done_recs,
                      rend_b)) {
         if (tid == 0)
@@ -1155,6 +1171,8 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
       else
         eval_window<kOps, true>(L, (const uint8_t*)L.win, wlen, nr_eval, ch, a.blob, nst, lds_stage,
                           unsupported, al, a.elem);
+      ET_MARK(tw2);
+      ET_ADD(1, tw0, tw2);
       const uint64_t wbase = global_mode ? gbase : al;
       // ---- error tracking (phase A) and descriptor emission: wave 0, in record order
       for (int r0 = 0; wave0 && r0 < nr_eval; r0 += 64) {
@@ -1278,6 +1296,11 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
       err_idx = L.err_idx_b;
       done_recs += (uint32_t)nr;
       cursor = ((uint64_t)L.next_cursor_hi << 32) | L.next_cursor_lo;
+      ET_MARK(tw3);
+      ET_ADD(2, tw2, tw3);
+#ifdef FSG_EVAL_TIMING
+      if (threadIdx.x == 0) et_acc[3] += 1;
+#endif
       (void)last;
     }
     if (phase == 0 && err_stage == 0xFFFFFFFFu) break;
@@ -1309,10 +1332,20 @@ __global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : (kOps ==
   const uint32_t n = a.list ? a.list[0] : a.nbatches;
   if constexpr (kOps == kOpsInt || kOps == kOpsAll) {  // batches of many small records: parallel framing
     __shared__ ParLds P;
+#ifdef FSG_EVAL_TIMING
+    if (threadIdx.x < 6) et_acc[threadIdx.x] = 0;
+    __syncthreads();
+    const unsigned long long tk0 = clock64();
+#endif
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
       eval_batch<kOps>(a, L, a.list ? a.list[1 + i] : i, &P);
       __syncthreads();
     }
+#ifdef FSG_EVAL_TIMING
+    if (threadIdx.x == 0 && blockIdx.x == 0)
+      printf("k_eval timing wg0: total %llu par %llu walk+eval %llu emit %llu windows %llu resident %llu\n",
+             (unsigned long long)(clock64() - tk0), et_acc[0], et_acc[1], et_acc[2], et_acc[3], et_acc[5]);
+#endif
   } else {
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
       eval_batch<kOps>(a, L, a.list ? a.list[1 + i] : i);
@@ -2982,15 +3015,14 @@ __device__ __forceinline__ void write_batch_wave(const WriteArgs& a, const KeptR
 
 __global__ __launch_bounds__(kWlThreads) void k_write_lean(WriteArgs a) {
   __shared__ WlLds L;
-  const Plan p = *a.plan;
-  const int32_t b = p.first + (int32_t)blockIdx.x;
-  if (p.first < 0 || b > p.last) return;
+  const int32_t b = a.first + (int32_t)blockIdx.x;
+  if (a.first < 0 || b > a.last) return;
   const uint32_t t = threadIdx.x, lane = t & 63u;
   const BatchStat st = a.bstat[b];
-  const int64_t rel = a.seg ? 0 : a.bstat[p.first].base_offset - st.base_offset;
+  const int64_t rel = a.seg ? 0 : a.bstat[a.first].base_offset - st.base_offset;
   const KeptRec* d = a.desc + a.rbase[b];
   const uint64_t obase = a.seg ? 61ull * (uint64_t)(b + 1) + a.pre[b].rec_bytes
-                               : 61 + (a.pre[b].rec_bytes - a.pre[p.first].rec_bytes);
+                               : 61 + (a.pre[b].rec_bytes - a.pre[a.first].rec_bytes);
   const uint32_t d0 = (uint32_t)(obase & 15);
   const uint32_t nk = st.nkeep;
   // 1. headers and segments

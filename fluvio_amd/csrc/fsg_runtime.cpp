@@ -436,6 +436,13 @@ struct fsg_engine {
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
   hipStream_t coll = nullptr;  // collective stream (state merges)
+  // aggregate-json group walks (AjGroup): created on the first group call that
+  // walks and kept (a stream create + destroy per call cost ~3 ms of host time)
+  std::mutex gmu;              // one group call at a time uses them
+  hipStream_t gst = nullptr;
+  hipEvent_t gdone = nullptr, gt0 = nullptr, gt1 = nullptr;
+  void* gdlist = nullptr;
+  size_t gdcap = 0;
 };
 
 struct fsg_chain_builder {
@@ -497,18 +504,13 @@ struct AjGroup {
   std::vector<AggjArgs> jobs;
   std::vector<hipEvent_t> ready;  // per job: its chain's hashes are done
   int device = 0;
+  fsg_engine* eng = nullptr;  // owns the stream, events and job list below
   hipStream_t st = nullptr;
   hipEvent_t done = nullptr;
   hipEvent_t t0 = nullptr, t1 = nullptr;  // the walk's own duration (timed chains)
   bool timed = false;
-  void* dlist = nullptr;
   ~AjGroup() {
-    if (dlist) (void)hipFree(dlist);
-    if (done) (void)hipEventDestroy(done);
-    if (t0) (void)hipEventDestroy(t0);
-    if (t1) (void)hipEventDestroy(t1);
     for (auto e : ready) (void)hipEventDestroy(e);
-    if (st) (void)hipStreamDestroy(st);
   }
 };
 
@@ -645,6 +647,11 @@ extern "C" void fsg_engine_free(fsg_engine* e) {
   if (!e) return;
   if (e->comm) ncclCommDestroy(e->comm);
   if (e->coll) (void)hipStreamDestroy(e->coll);
+  if (e->gst) (void)hipStreamDestroy(e->gst);
+  if (e->gdone) (void)hipEventDestroy(e->gdone);
+  if (e->gt0) (void)hipEventDestroy(e->gt0);
+  if (e->gt1) (void)hipEventDestroy(e->gt1);
+  if (e->gdlist) (void)hipFree(e->gdlist);
   delete e;
   if (g_engines.fetch_sub(1) == 1) fsg_host_cache_trim();
 }
@@ -1910,23 +1917,34 @@ int run_composed(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metri
 
 // the group's walks, once every chain has arrived (the last arrival launches)
 int group_launch(AjGroup* g) {
-  HIPCHK(hipSetDevice(g->device));
   const size_t n = g->jobs.size();
-  if (!g->st) HIPCHK(hipStreamCreateWithFlags(&g->st, hipStreamNonBlocking));
-  if (!g->done) HIPCHK(hipEventCreateWithFlags(&g->done, hipEventDisableTiming));
-  if (n) {
-    for (auto e : g->ready) HIPCHK(hipStreamWaitEvent(g->st, e, 0));
-    HIPCHK(hipMalloc(&g->dlist, n * sizeof(AggjArgs)));
-    HIPCHK(hipMemcpyAsync(g->dlist, g->jobs.data(), n * sizeof(AggjArgs), hipMemcpyHostToDevice, g->st));
-    if (g->timed) {
-      if (!g->t0) HIPCHK(hipEventCreate(&g->t0));
-      if (!g->t1) HIPCHK(hipEventCreate(&g->t1));
-      HIPCHK(hipEventRecord(g->t0, g->st));
-    }
-    launch_aggj_order_group((const AggjArgs*)g->dlist, (uint32_t)n, g->st);
-    HIPCHK(hipGetLastError());
-    if (g->timed) HIPCHK(hipEventRecord(g->t1, g->st));
+  if (!n) return FSG_OK;  // nothing walks: no chain waits for the group
+  HIPCHK(hipSetDevice(g->device));
+  fsg_engine* e = g->eng;
+  if (!e->gst) HIPCHK(hipStreamCreateWithFlags(&e->gst, hipStreamNonBlocking));
+  if (!e->gdone) HIPCHK(hipEventCreateWithFlags(&e->gdone, hipEventDisableTiming));
+  g->st = e->gst;
+  g->done = e->gdone;
+  const size_t need = n * sizeof(AggjArgs);
+  if (need > e->gdcap) {  // grow-only (the previous group's walk was waited for by its chains)
+    if (e->gdlist) HIPCHK(hipFree(e->gdlist));
+    e->gdlist = nullptr;
+    e->gdcap = 0;
+    HIPCHK(hipMalloc(&e->gdlist, need));
+    e->gdcap = need;
   }
+  for (auto ev : g->ready) HIPCHK(hipStreamWaitEvent(g->st, ev, 0));
+  HIPCHK(hipMemcpyAsync(e->gdlist, g->jobs.data(), need, hipMemcpyHostToDevice, g->st));
+  if (g->timed) {
+    if (!e->gt0) HIPCHK(hipEventCreate(&e->gt0));
+    if (!e->gt1) HIPCHK(hipEventCreate(&e->gt1));
+    g->t0 = e->gt0;
+    g->t1 = e->gt1;
+    HIPCHK(hipEventRecord(g->t0, g->st));
+  }
+  launch_aggj_order_group((const AggjArgs*)e->gdlist, (uint32_t)n, g->st);
+  HIPCHK(hipGetLastError());
+  if (g->timed) HIPCHK(hipEventRecord(g->t1, g->st));
   HIPCHK(hipEventRecord(g->done, g->st));
   return FSG_OK;
 }
@@ -2397,6 +2415,8 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   wa.acc0 = acc0;
   wa.elem = ea.elem;
   wa.acc_len = sa.acc_len;
+  wa.first = p.first;
+  wa.last = p.last;
   if (has_cat) {  // the accumulator stream: initial accumulator ++ appended values (k_cat)
     HIPCHK(c->cat.ensure(kCatOff + c->acc.size() + p.cat_final + 64));
     if (!c->acc.empty())
@@ -2831,8 +2851,10 @@ extern "C" int fsg_chain_group_process_slices(fsg_chain* const* chains, const fs
     if (chains[i]->eng->device != chains[0]->eng->device)
       return fail(FSG_E_INVALID_ARG, "fsg_chain_group_process_slices: chains on different devices");
   }
+  std::unique_lock<std::mutex> glk(chains[0]->eng->gmu);
   AjGroup g;
   g.device = chains[0]->eng->device;
+  g.eng = chains[0]->eng;
   g.expected = n;
   std::vector<size_t> walkers, others;
   for (size_t i = 0; i < n; i++) {
@@ -2879,7 +2901,7 @@ extern "C" int fsg_chain_group_process_slices(fsg_chain* const* chains, const fs
     }
   }
   HIPCHK(hipSetDevice(g.device));
-  if (g.st) HIPCHK(hipStreamSynchronize(g.st));  // the list buffer is freed with g
+  if (g.st) HIPCHK(hipStreamSynchronize(g.st));  // the job list is rewritten by the next group call
   return rc;
 }
 

@@ -1864,3 +1864,53 @@ def test_state_kept_before_decode_error(engine, chain, kind):
     for i, m in enumerate(chain):
         if m[0] in ("aggregate-sum", "aggregate", "aggregate-json"):
             assert g.accumulator(i) == o.accumulator(i)
+
+
+# ---------------------------------------------------------------------------
+# long verbatim records (k_write_lean's staged units and its wave path for
+# batches beyond the staging buffer): keys up to 210 B, values of 0..2000 B,
+# uppercase maps, offset-delta rebasing across batches with gaps
+# ---------------------------------------------------------------------------
+def _long_slice(seed, nbatches=50):
+    rnd = random.Random(seed)
+    words = ["timeout", "level", "warn", "x", "é", "abc", "TIME", "out"]
+    out, base = b"", 0
+    for bi in range(nbatches):
+        b = P.Batch(base_offset=base)
+        n = rnd.choice([1, 2, 7, 13, 40, 64, 70])
+        for i in range(n):
+            if rnd.random() < 0.75:
+                size = rnd.randint(128, 2000)
+            else:
+                size = rnd.randint(0, 127)
+            v = ""
+            while len(v) < size:
+                v += rnd.choice(words) + rnd.choice(["", " ", "-"])
+            enc = v.encode()[:size] if rnd.random() < 0.5 else v.encode()
+            if bi >= nbatches - 3 and rnd.random() < 0.05:
+                enc = enc + b"\xff"  # invalid UTF-8 near the end: the filters' error path
+            key = None if rnd.random() < 0.7 else rnd.choice([b"", b"k", b"timeout" * 30])
+            r = P.Record.new_key_value(key, enc)
+            r.preamble.offset_delta = i
+            r.preamble.timestamp_delta = rnd.choice([0, 5, 300, 1 << 20])
+            b.records.append(r)
+        b.header.last_offset_delta = n - 1
+        enc_b = b.encode()
+        out += enc_b
+        base += n + rnd.choice([0, 0, 1, 100, 5000])
+    return out
+
+
+@pytest.mark.parametrize("chain", [
+    [("filter_init", {"key": "timeout"}, None)],
+    [("filter_init", {"key": "out"}, None)],
+    [("map", {}, None)],
+    [("map", {}, None), ("filter_init", {"key": "TIMEOUT"}, None)],
+    [],
+    [("regex-filter", {"regex": r"warn|x"}, None)],
+])
+def test_writer_long_records(engine, chain):
+    for seed in (1, 2, 3):
+        sl = _long_slice(seed)
+        check_batch(engine, chain, sl)
+        check_batch(engine, chain, sl, max_bytes=len(sl) // 3)
