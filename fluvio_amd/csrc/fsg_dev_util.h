@@ -59,6 +59,37 @@ __device__ __forceinline__ int wvarint(P w, uint32_t& q, uint32_t wlim, int64_t*
   return 0;
 }
 
+// <i32 as FromStr>::from_str — 0 ok, 1 Empty, 2 InvalidDigit, 3 PosOverflow, 4 NegOverflow
+template <typename P>
+__device__ __forceinline__ int parse_i32(P s, uint32_t n, int32_t* out) {
+  if (n == 0) return 1;
+  uint32_t i = 0;
+  bool pos = true;
+  uint8_t c0 = s[0];
+  if ((c0 == '+' || c0 == '-') && n == 1) return 2;
+  if (c0 == '+')
+    i = 1;
+  else if (c0 == '-') {
+    pos = false;
+    i = 1;
+  }
+  int64_t acc = 0;
+  for (; i < n; i++) {
+    uint32_t c = s[i];
+    if (c < '0' || c > '9') return 2;
+    int d = (int)c - '0';
+    if (pos) {
+      acc = acc * 10 + d;
+      if (acc > 2147483647LL) return 3;
+    } else {
+      acc = acc * 10 - d;
+      if (acc < -2147483648LL) return 4;
+    }
+  }
+  *out = (int32_t)acc;
+  return 0;
+}
+
 // exact zero-byte mask: 0x80 in each byte of x that is zero
 __device__ __forceinline__ uint32_t zbytes(uint32_t x) {
   return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);

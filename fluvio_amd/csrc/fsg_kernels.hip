@@ -135,36 +135,6 @@ __device__ void utf8_trim(P s, uint32_t n, uint32_t* b, uint32_t* e) {
   *e = j;
 }
 
-// <i32 as FromStr>::from_str — 0 ok, 1 Empty, 2 InvalidDigit, 3 PosOverflow, 4 NegOverflow
-template <typename P>
-__device__ __forceinline__ int parse_i32(P s, uint32_t n, int32_t* out) {
-  if (n == 0) return 1;
-  uint32_t i = 0;
-  bool pos = true;
-  uint8_t c0 = s[0];
-  if ((c0 == '+' || c0 == '-') && n == 1) return 2;
-  if (c0 == '+')
-    i = 1;
-  else if (c0 == '-') {
-    pos = false;
-    i = 1;
-  }
-  int64_t acc = 0;
-  for (; i < n; i++) {
-    uint32_t c = s[i];
-    if (c < '0' || c > '9') return 2;
-    int d = (int)c - '0';
-    if (pos) {
-      acc = acc * 10 + d;
-      if (acc > 2147483647LL) return 3;
-    } else {
-      acc = acc * 10 - d;
-      if (acc < -2147483648LL) return 4;
-    }
-  }
-  *out = (int32_t)acc;
-  return 0;
-}
 
 // ---------------------------------------------------------------------------
 // k_eval: per-wave LDS state
@@ -3562,6 +3532,10 @@ void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s) {
     // takes the deferred batches' record starts from k_arr_frame where it framed them
     launch_array_lean(a, s);
     grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list
+  } else if (mode == EVAL_INT) {
+    // k_eval_int over every batch (starts from k_chase_w, kept with the slice), then the deferred list
+    launch_eval_int(a, (ops & opbit(OP_AGG_SUM)) != 0, s);
+    grid = a.nbatches < 2048u ? a.nbatches : 2048u;
   } else if (mode == EVAL_LEAN || mode == EVAL_FLAT) {
     // k_chase + k_eval_lean, or the flat substring kernels (fsg_lean.hip)
     if (mode == EVAL_FLAT)

@@ -1665,6 +1665,217 @@ static void launch_lean_kind(const EvalArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_eval_lean<kKind>, dim3(g), dim3(kLeanThreads), 0, s, a);
 }
 
+// ---------------------------------------------------------------------------
+// k_eval_int — chains of integer stages over decimal values (filter_odd,
+// map_double, filter_map, aggregate-sum: from_utf8 + parse::<i32>, the
+// aggregate after str::trim) on batches of many small records.  One
+// 256-thread workgroup per batch: the window in LDS by LDS-DMA, the record
+// starts from k_chase_w (kept with the slice), thread t takes the contiguous
+// records [t R, t R + R) (R <= kIntR, unrolled: no indexed registers).
+//   pass 1  every field of each record parsed from LDS (Record::decode, the
+//           same checks walk_fast makes), the value parsed and the stages
+//           run in registers: a keep bit and the output integer per record
+//   scans   kept records and the aggregate's wrapping i32 sum, in record order
+//           (thread runs are contiguous): wave scans + the four wave totals
+//   pass 2  the kept records' fields again, their descriptors at the prefix
+// A batch with a byte >= 0x80 in a value, a value that does not parse, a
+// record that does not tile its span, more than 256 kIntR records or starts
+// k_chase_w could not find is deferred whole to k_eval (list mode), which
+// reports its error exactly.
+// ---------------------------------------------------------------------------
+constexpr int kIntR = 8;
+struct __attribute__((aligned(16))) IntLds {
+  uint8_t win[kLeanWin + 64];
+  uint32_t wk[4], wa[4];
+  uint32_t defer;
+};
+struct IntRec {  // one record's fields (window offsets)
+  uint32_t vs, vl, kpos, klen;
+  int64_t ts, od, hdr;
+  uint8_t attr, tag;
+};
+// Record::decode of the record spanning window offsets [s, e): false unless it tiles the span
+__device__ __forceinline__ bool int_rec(const uint8_t* w, uint32_t s, uint32_t e, IntRec& r) {
+  uint32_t q = s;
+  int64_t len, kl, vl;
+  bool g = !wvarint(w, q, e, &len) && len >= 0 && (uint64_t)q + (uint64_t)len == e;
+  if (g && q < e) r.attr = w[q++]; else g = false;
+  g = g && !wvarint(w, q, e, &r.ts) && !wvarint(w, q, e, &r.od);
+  if (g && q < e) r.tag = w[q++]; else g = false;
+  g = g && r.tag <= 1;
+  r.kpos = 0;
+  r.klen = 0;
+  if (g && r.tag == 1) {
+    g = !wvarint(w, q, e, &kl) && kl >= 0 && (uint64_t)q + (uint64_t)kl <= e;
+    if (g) {
+      r.kpos = q;
+      r.klen = (uint32_t)kl;
+      q += r.klen;
+    }
+  }
+  g = g && !wvarint(w, q, e, &vl) && vl >= 0 && (uint64_t)q + (uint64_t)vl <= e;
+  r.vs = q;
+  r.vl = g ? (uint32_t)vl : 0u;
+  if (g) q += r.vl;
+  g = g && !wvarint(w, q, e, &r.hdr) && q == e;
+  return g;
+}
+__device__ __forceinline__ bool int_ws(uint32_t c) { return c == 0x20 || (c >= 0x09 && c <= 0x0D); }
+template <int kAgg>  // kAgg: the chain ends in aggregate-sum
+__global__ __launch_bounds__(256) void k_eval_int(EvalArgs a) {
+  __shared__ IntLds L;
+  const uint32_t b = blockIdx.x;
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const ChainDesc& ch = *a.chain;
+  const uint8_t* S = a.slice;
+  const uint64_t pos = a.bpos[b];
+  const uint64_t nxt = b + 1 < a.nbatches ? a.bpos[b + 1] : a.slice_len;
+  const uint64_t rb = a.rbase[b], rn = (b + 1 < a.nbatches ? a.rbase[b + 1] : a.nrec) - rb;
+  const uint32_t rend = a.rend[b];
+  const uint64_t al = pos & ~15ull;
+  uint64_t wl = nxt > al ? nxt - al : 0;
+  if (wl > (uint64_t)kLeanWin) wl = kLeanWin;
+  const uint32_t wlen = (uint32_t)((wl + 15) & ~15ull);
+  // the window (every byte of the batch when it fits) by LDS-DMA
+  for (uint32_t k = wv; k * 1024u < wlen; k += 4)
+    if (k * 1024u + lane * 16u < wlen)  // (an inactive lane writes nothing)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(S + al + k * 1024u + lane * 16u),
+                                       (__attribute__((address_space(3))) void*)(L.win + k * 1024u), 16, 0, 0);
+  if (t == 0) L.defer = 0;
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  const uint32_t batch_len = (uint32_t)rd_be(L.win + (pos - al) + 8, 4);
+  const uint64_t sec0 = pos + 57, sec_end = pos + 12 + (uint64_t)batch_len;
+  const uint32_t count = (uint32_t)rn;
+  bool ok = rend != 0xFFFFu && sec_end - al <= wlen && sec_end - al == rend && count > 0 &&
+            count <= 256u * (uint32_t)kIntR && sec_end >= sec0 + 4 &&
+            (uint32_t)rd_be(L.win + (sec0 - al), 4) == count;
+  const uint16_t* rs = a.rstart + rb;
+  const uint32_t R = (count + 255u) >> 8;
+  const uint32_t r0 = t * R;
+  uint32_t keep = 0, kc = 0, asum = 0;
+  int32_t xv[kIntR];
+  const bool src_out = ch.out_type != VT_I32;
+  // pass 1: fields, value, stages
+#pragma unroll
+  for (int i = 0; i < kIntR; i++) {
+    xv[i] = 0;
+    const uint32_t k = r0 + (uint32_t)i;
+    if (!ok || i >= (int)R || k >= count) continue;
+    const uint32_t s = rs[k], e = k + 1 < count ? rs[k + 1] : rend;
+    IntRec r;
+    ok = s < e && e <= rend && int_rec(L.win, s, e, r);
+    if (!ok) continue;
+    // from_utf8: ASCII only here; the aggregate trims (str::trim) before parsing
+    uint32_t vb = r.vs, ve = r.vs + r.vl;
+    for (uint32_t j = vb; j < ve; j++) ok = ok && L.win[j] < 0x80u;
+    if (!ok) continue;
+    if (ch.st[0].op == OP_AGG_SUM) {
+      while (vb < ve && int_ws(L.win[vb])) vb++;
+      while (ve > vb && int_ws(L.win[ve - 1])) ve--;
+    }
+    int32_t x = 0;
+    ok = parse_i32(L.win + vb, ve - vb, &x) == 0;
+    if (!ok) continue;
+    bool alive = true;
+    for (uint32_t st = 0; st < ch.nstages && alive; st++) {
+      const uint8_t op = ch.st[st].op;
+      if (op == OP_FILTER_ODD) {
+        alive = x % 2 == 0;
+      } else if (op == OP_MAP_DOUBLE) {
+        x = (int32_t)((uint32_t)x * 2u);
+      } else if (op == OP_FILTER_MAP) {
+        if (x % 2 == 0) x /= 2; else alive = false;
+      }
+    }
+    xv[i] = x;
+    if (alive) {
+      keep |= 1u << i;
+      kc++;
+      if (kAgg) asum += (uint32_t)x;
+    }
+  }
+  if (__syncthreads_or(!ok)) {  // the exact kernel takes the whole batch
+    if (t == 0) {
+      const uint32_t j = atomicAdd(&a.list[0], 1u);
+      a.list[1 + j] = b;
+    }
+    return;
+  }
+  // record-order prefixes: kept records, aggregate sum (wrapping)
+  const uint32_t ik = wave_incl_scan(kc), ia = wave_incl_scan(asum);
+  if (lane == 63) {
+    L.wk[wv] = ik;
+    L.wa[wv] = ia;
+  }
+  __syncthreads();
+  uint32_t kbase = ik - kc, abase = ia - asum;
+  for (uint32_t w2 = 0; w2 < wv; w2++) {
+    kbase += L.wk[w2];
+    abase += L.wa[w2];
+  }
+  // pass 2: the kept records' descriptors
+  const uint8_t mode = kAgg ? (uint8_t)KM_AGG : src_out ? (ch.out_type == VT_SRC_UPPER ? (uint8_t)KM_UPPER : (uint8_t)KM_COPY)
+                                                        : (uint8_t)KM_I32;
+  uint32_t kn = 0, run = abase;
+#pragma unroll
+  for (int i = 0; i < kIntR; i++) {
+    if (!((keep >> i) & 1u)) continue;
+    const uint32_t k = r0 + (uint32_t)i;
+    const uint32_t s = rs[k], e = k + 1 < count ? rs[k + 1] : rend;
+    IntRec r;
+    (void)int_rec(L.win, s, e, r);
+    run += (uint32_t)xv[i];
+    KeptRec d;
+    d.src = al + s;
+    d.vpos = al + r.vs;
+    d.kpos = r.tag ? al + r.kpos : 0;
+    d.od = r.od;
+    d.ts = r.ts;
+    d.hdr = r.hdr;
+    d.vlen = r.vl;
+    d.klen = r.klen;
+    d.ival = kAgg ? (int32_t)run : xv[i];
+    d.mode = mode;
+    d.has_key = r.tag;
+    d.attr = r.attr;
+    d.pad = 0;
+    a.desc[rb + kbase + kn++] = d;
+  }
+  if (t == 0) {
+    const uint8_t* h = L.win + (pos - al);  // batch header (file format, batch.rs:163-180)
+    BatchStat st = {};
+    st.base_offset = (int64_t)rd_be(h, 8);
+    st.lod_in = (int32_t)rd_be(h + 23, 4);
+    st.first_ts = (int64_t)rd_be(h + 27, 8);
+    st.comp = (uint32_t)h[22] & 7u;
+    st.flags = BF_LAST_STAGE;
+    st.nkeep = st.nout = L.wk[0] + L.wk[1] + L.wk[2] + L.wk[3];
+    st.sec_len = (uint32_t)(sec_end - sec0);
+    st.err_stage = 0xFFFFFFFFu;
+    st.agg_sum = kAgg ? (int64_t)(int32_t)(L.wa[0] + L.wa[1] + L.wa[2] + L.wa[3]) : 0;
+    a.bstat[b] = st;
+  }
+}
+
+bool int_lean_eligible(const ChainDesc& ch, uint32_t ops) {
+  if (!ch.nstages) return false;
+  if (ops & ~((1u << OP_FILTER_ODD) | (1u << OP_MAP_DOUBLE) | (1u << OP_FILTER_MAP) | (1u << OP_AGG_SUM))) return false;
+  if (ch.st[0].in_type != VT_SRC) return false;
+  for (uint32_t k = 0; k < ch.nstages; k++) {
+    const StageDesc& sd = ch.st[k];
+    if (sd.op == OP_AGG_SUM && (k + 1 != ch.nstages || sd.acc_bad || !(ch.flags & CF_AGG_SUM))) return false;
+  }
+  return true;
+}
+void launch_eval_int(const EvalArgs& a, bool agg, hipStream_t s) {
+  if (!a.nbatches) return;
+  if (agg)
+    hipLaunchKernelGGL(k_eval_int<1>, dim3(a.nbatches), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_eval_int<0>, dim3(a.nbatches), dim3(256), 0, s, a);
+}
+
 int flat_stage(const ChainDesc& ch, uint32_t ops) {
   if (ops & ~((1u << OP_CONTAINS) | (1u << OP_MAP_UPPER))) return -1;
   int st = -1;

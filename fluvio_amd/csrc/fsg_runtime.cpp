@@ -460,6 +460,12 @@ struct fsg_slice {
   uint64_t header_bytes = 0;  // 57 B per framed batch + the record sections
   bool device_framed = false; // framed by k_frame_* (else by the host walk)
   bool decompressed = false;  // compressed sections were decompressed on the GPU at ingest
+  // record starts / ends per batch (k_chase_w) for k_eval_int, computed on first
+  // use and kept while the slice is unchanged (every framing resets rs_ok)
+  mutable std::mutex rs_mu;
+  mutable DevBuf rs_start, rs_end;
+  mutable hipEvent_t rs_ev = nullptr;  // recorded after the framing: another stream waits for it
+  mutable bool rs_ok = false;
   // CRC32C verify of the stored (compressed) batches, run before decompression
   uint64_t crc_bad = 0;
   int64_t crc_first = -1;
@@ -479,6 +485,7 @@ struct fsg_slice {
   mutable hipStream_t vst = nullptr;
   mutable hipEvent_t vev[2] = {};
   ~fsg_slice() {
+    if (rs_ev) (void)hipEventDestroy(rs_ev);
     for (auto& e : vev)
       if (e) (void)hipEventDestroy(e);
     if (vst) (void)hipStreamDestroy(vst);
@@ -533,6 +540,7 @@ struct fsg_chain {
   DevBuf arr_b, arr_bm;  // lean array_map statistics and element bitmaps (per batch)
   DevBuf fbm;            // flat substring path: occurrence / high-byte bits per 16-byte chunk
   bool no_flat = getenv("FSG_NO_FLAT") != nullptr;  // A/B: the flat path off (k_eval_lean instead)
+  bool no_int = getenv("FSG_NO_INT") != nullptr;    // A/B: integer chains through k_eval alone
   // the one-batch process() path (k_one): zeros for bpos / rbase, the device
   // block Plan | BatchStat | Mins | output batch, and coherent pinned memory
   // the kernel reads the input from and writes the block back to (no copies)
@@ -1039,6 +1047,7 @@ int frame(const uint8_t* s, size_t len, std::vector<uint64_t>& bpos, std::vector
 int frame_on_device(fsg_slice* sl, hipStream_t st, int* fallback) {
   const uint64_t len = sl->len;
   *fallback = 0;
+  sl->rs_ok = false;
   sl->nb = 0;
   sl->nrec = 0;
   sl->tail_status = 0;
@@ -1253,6 +1262,7 @@ int decompress_slice(fsg_slice* sl, const std::vector<uint64_t>& bpos, const std
   std::swap(sl->data.p, nd.p);
   std::swap(sl->data.cap, nd.cap);
   sl->len = total;
+  sl->rs_ok = false;
   sl->nb = keep;
   sl->nrec = nrec;
   sl->tail_status = tail;
@@ -1271,6 +1281,7 @@ int upload_slice(fsg_engine* e, const uint8_t* s, size_t len, fsg_slice* sl, hip
                  bool device_frame = true, bool sync = true, bool padded = false) {
   sl->eng = e;
   sl->len = len;
+  sl->rs_ok = false;
   sl->nb = 0;
   sl->nrec = 0;
   sl->tail_status = 0;
@@ -2098,8 +2109,35 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
       ea.flat_st = (uint32_t)fst | (c->hdesc.st[fst].needle_len << 8);
     }
   }
-  if (lean || arr) HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
-  launch_eval(ea, ops, flat ? EVAL_FLAT : lean ? EVAL_LEAN : arr ? EVAL_ARRAY : EVAL_EXACT, st);
+  // integer stages over decimal values (filter_odd / map_double / filter_map /
+  // aggregate-sum): k_eval_int with the slice's record starts (k_chase_w once per slice)
+  bool ints = !lean && !arr && nb > 1 && !s->has_pass && !c->no_int && int_lean_eligible(c->hdesc, ops);
+  if (ints) {  // (chains of one group call may share the slice: one framing, the others wait for its event)
+    std::lock_guard<std::mutex> lk(s->rs_mu);
+    if (!s->rs_ok) {
+      ints = s->rs_start.ensure(((size_t)s->nrec + 64) * sizeof(uint16_t)) == hipSuccess &&
+             s->rs_end.ensure(((size_t)nb + 1) * sizeof(uint16_t)) == hipSuccess &&
+             (s->rs_ev || hipEventCreateWithFlags(&s->rs_ev, hipEventDisableTiming) == hipSuccess);
+      (void)hipGetLastError();
+      if (ints) {
+        EvalArgs ca = ea;
+        ca.rstart = s->rs_start.as<uint16_t>();
+        ca.rend = s->rs_end.as<uint16_t>();
+        launch_chase_w(ca, st);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(s->rs_ev, st));
+        s->rs_ok = true;
+      }
+    } else {
+      HIPCHK(hipStreamWaitEvent(st, s->rs_ev, 0));
+    }
+    if (ints) {
+      ea.rstart = s->rs_start.as<uint16_t>();
+      ea.rend = s->rs_end.as<uint16_t>();
+    }
+  }
+  if (lean || arr || ints) HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
+  launch_eval(ea, ops, flat ? EVAL_FLAT : lean ? EVAL_LEAN : arr ? EVAL_ARRAY : ints ? EVAL_INT : EVAL_EXACT, st);
   HIPCHK(hipGetLastError());
   if (c->timed) HIPCHK(hipEventRecord(c->ev[1], st));
   launch_mins(ea.bstat, nb, ea.mins, st);
@@ -2312,16 +2350,16 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   HIPCHK(c->hpin.ensure(kPinPlan + kSmallOut));
   HIPCHK(hipMemcpyAsync(c->hpin.p, c->plan.p, sizeof(Plan), hipMemcpyDeviceToHost, st));
   static_assert(sizeof(Plan) + sizeof(uint32_t) <= kPinPlan, "pinned plan block");
-  if (lean || arr)
+  if (lean || arr || ints)
     HIPCHK(hipMemcpyAsync((uint8_t*)c->hpin.p + sizeof(Plan), ea.list, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   unsigned long long sfs[3] = {0, 0, 0};
   const bool dedup = has_sf && sfa.op == OP_DEDUP && nb && !so;
   if (dedup) HIPCHK(hipMemcpyAsync(sfs, sfa.scal, sizeof sfs, hipMemcpyDeviceToHost, st));
   HIPCHK(wait_stream(st));
   memcpy(&c->hplan, c->hpin.p, sizeof(Plan));
-  c->last.eval_path = flat ? FSG_EVAL_FLAT : lean ? FSG_EVAL_LEAN : arr ? FSG_EVAL_ARRAY : FSG_EVAL_EXACT;
+  c->last.eval_path = flat ? FSG_EVAL_FLAT : lean ? FSG_EVAL_LEAN : arr ? FSG_EVAL_ARRAY : ints ? FSG_EVAL_INT : FSG_EVAL_EXACT;
   c->last.deferred = 0;
-  if (lean || arr) memcpy(&c->last.deferred, (const uint8_t*)c->hpin.p + sizeof(Plan), sizeof(uint32_t));
+  if (lean || arr || ints) memcpy(&c->last.deferred, (const uint8_t*)c->hpin.p + sizeof(Plan), sizeof(uint32_t));
   if (dedup) {
     c->sf->n_ent = sfs[0];
     c->sf->arena_len = sfs[1];
@@ -2503,6 +2541,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     launch_seg_headers(ga, st);
     o->eng = c->eng;
     o->len = out_len;
+    o->rs_ok = false;
     o->nb = seg_nb;
     o->nrec = p.n_records;
     o->header_bytes = out_len;

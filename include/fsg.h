@@ -172,6 +172,8 @@ typedef struct fsg_timings {
 #define FSG_EVAL_ARRAY 3 /* k_arr_lean (array_map lane per record), deferred batches through k_eval */
 #define FSG_EVAL_FLAT 4  /* one substring stage: the slice streamed as bytes (k_flat_scan), a wave per batch
                             decides (k_flat_decide), deferred batches through k_eval */
+#define FSG_EVAL_INT 5   /* integer stages over decimal values: k_eval_int (workgroup per batch, record starts
+                            kept with the slice), deferred batches through k_eval */
 
 const char *fsg_last_error_message(void);
 int fsg_abi_version(void);

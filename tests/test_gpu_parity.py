@@ -1914,3 +1914,35 @@ def test_writer_long_records(engine, chain):
         sl = _long_slice(seed)
         check_batch(engine, chain, sl)
         check_batch(engine, chain, sl, max_bytes=len(sl) // 3)
+
+
+@pytest.mark.parametrize("chain", [
+    [("aggregate-sum", {}, b"7")],
+    [("filter_odd", {}, None)],
+    [("map_double", {}, None), ("filter_map", {}, None)],
+    [("filter_map", {}, None), ("aggregate-sum", {}, None)],
+])
+def test_int_path_taken_and_exact(engine, chain):
+    """k_eval_int (FSG_EVAL_INT) runs for integer chains over many small records:
+    the C5 generator's slice (1,000+ decimal records per batch) decides every
+    batch there (no deferral) and matches the oracle; a malformed batch in the
+    stream is deferred to k_eval and still matches; the slice's record starts
+    are computed once and reused by the next call."""
+    sl = synth.make_slice(3, 20000, seed=11)
+    g = gpu_chain(engine, chain)
+    o = orc_chain(chain)
+    rs = ResidentSlice(engine, sl)
+    for _ in range(2):  # the second call reuses the slice's record starts
+        gout = g.process_slice(rs)
+        oo = o.process_batch(sl, (1 << 64) - 1)
+        assert oo["status"] == 0
+        assert gout.raw == oo["bytes"]
+        t = g.last_timings()
+        assert t["eval_path"] == 5 and t["deferred"] == 0, t  # FSG_EVAL_INT
+    for i, m in enumerate(chain):
+        if m[0] == "aggregate-sum":
+            assert g.accumulator(i) == o.accumulator(i)
+    # a batch the lean kernel defers (a non-digit value mid-stream; a key tag of 2 at the end)
+    rnd = random.Random(3)
+    mixed = sl + _raw_batch(10 ** 6, _small_records(rnd, 900, bad_value=450, hi=999)) + _bad_tag_batch(2 * 10 ** 6)
+    check_batch(engine, chain, mixed)
