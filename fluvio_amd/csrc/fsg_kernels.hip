@@ -2033,6 +2033,105 @@ __global__ __launch_bounds__(kWriteThreads) void k_write(WriteArgs a) {
   write_batch(a, p, b);
 }
 
+// k_write_gen — batches of records whose values are generated integers
+// (KM_I32: map_double / filter_map outputs; KM_AGG: aggregate-sum's running
+// sum): one 256-thread workgroup per included batch, thread t the contiguous
+// kept records [t R, t R + R) (R <= 8, unrolled); output sizes, a block scan,
+// every record's bytes assembled in LDS (varint fields, key, decimal value,
+// trailer), then 16-byte stores.  Batches of another mode, more than 2048
+// records or more output than the stage holds take write_batch on wave 0.
+constexpr int kWgObuf = 32768;
+constexpr int kWgR = 8;
+struct __attribute__((aligned(16))) WgLds {
+  uint8_t ob[kWgObuf + 16];
+  uint32_t wt[4];
+};
+__global__ __launch_bounds__(256) void k_write_gen(WriteArgs a) {
+  __shared__ WgLds L;
+  const int32_t b = a.first + (int32_t)blockIdx.x;
+  if (a.first < 0 || b > a.last) return;
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const BatchStat st = a.bstat[b];
+  const uint32_t nk = st.nkeep;
+  if (!nk) return;
+  const int64_t rel = a.seg ? 0 : a.bstat[a.first].base_offset - st.base_offset;
+  const int32_t agg_base = a.agg_pre ? (int32_t)((uint64_t)a.acc0 + (uint64_t)a.agg_pre[b].agg) : 0;
+  const KeptRec* d = a.desc + a.rbase[b];
+  const uint64_t obase = a.seg ? 61ull * (uint64_t)(b + 1) + a.pre[b].rec_bytes
+                               : 61 + (a.pre[b].rec_bytes - a.pre[a.first].rec_bytes);
+  const uint8_t mode0 = d[0].mode;  // a batch's descriptors share one mode
+  const uint32_t R = (nk + 255u) >> 8;
+  const bool gen = (mode0 == KM_I32 || mode0 == KM_AGG) && R <= (uint32_t)kWgR && !(st.flags & BF_ARR_LEAN);
+  Plan p = {};
+  p.first = a.first;
+  if (!gen) {
+    if (t < 64) write_batch(a, p, b);
+    return;
+  }
+  const uint32_t k0 = t * R;
+  uint32_t sz[kWgR], mine = 0;
+#pragma unroll
+  for (int i = 0; i < kWgR; i++) {
+    sz[i] = 0;
+    if (i < (int)R && k0 + i < nk) {
+      sz[i] = rec_out_size(d[k0 + i], rel, agg_base, 0);
+      mine += sz[i];
+    }
+  }
+  const uint32_t incl = wave_incl_scan(mine);
+  if (lane == 63) L.wt[wv] = incl;
+  __syncthreads();
+  uint32_t off = incl - mine;
+  for (uint32_t w2 = 0; w2 < wv; w2++) off += L.wt[w2];
+  const uint32_t total = L.wt[0] + L.wt[1] + L.wt[2] + L.wt[3];
+  const uint32_t d0 = (uint32_t)(obase & 15);
+  if (d0 + total > (uint32_t)kWgObuf) {  // uniform
+    if (t < 64) write_batch(a, p, b);
+    return;
+  }
+  uint32_t q = d0 + off;
+#pragma unroll
+  for (int i = 0; i < kWgR; i++) {
+    if (!sz[i]) continue;
+    const KeptRec r = d[k0 + i];
+    const int32_t x = r.mode == KM_I32 ? r.ival : (int32_t)((uint32_t)agg_base + (uint32_t)r.ival);
+    const uint32_t vl = dec_len_i32(x);
+    const uint32_t inner = 1 + vsize(r.ts) + vsize(r.od + rel) + 1 +
+                           (r.has_key ? vsize((int64_t)r.klen) + r.klen : 0) + vsize((int64_t)vl) + vl + vsize(r.hdr);
+    uint8_t* o = L.ob + q;
+    uint32_t w = venc((int64_t)inner, o);
+    o[w++] = r.attr;
+    w += venc(r.ts, o + w);
+    w += venc(r.od + rel, o + w);
+    o[w++] = r.has_key ? 1 : 0;
+    if (r.has_key) {
+      w += venc((int64_t)r.klen, o + w);
+      const uint8_t* ks = a.slice + r.kpos;
+      for (uint32_t j = 0; j < r.klen; j++) o[w + j] = ks[j];
+      w += r.klen;
+    }
+    w += venc((int64_t)vl, o + w);
+    w += fmt_i32(x, o + w);
+    w += venc(r.hdr, o + w);
+    q += w;
+  }
+  __syncthreads();
+  const uint32_t E = d0 + total;
+  uint8_t* og = a.out + obase - d0;
+  for (uint32_t u = t; u < (E + 15) >> 4; u += 256) {
+    const uint32_t D = u << 4;
+    if (D >= d0 && D + 16 <= E) {
+      *(uint4*)(og + D) = *(const uint4*)(L.ob + D);
+    } else {
+      const uint32_t lo = D > d0 ? D : d0, hi = D + 16 < E ? D + 16 : E;
+      for (uint32_t j = lo; j < hi; j++) og[j] = L.ob[j];
+    }
+  }
+}
+void launch_write_gen(const WriteArgs& a, uint32_t nblocks, hipStream_t s) {
+  if (nblocks) hipLaunchKernelGGL(k_write_gen, dim3(nblocks), dim3(256), 0, s, a);
+}
+
 // Array elements whose canonical text differs from their source text (floats,
 // keys out of BTreeMap order, whitespace, escapes): json_canon measures them
 // after k_eval (k_canon_len, before k_size) and writes them after k_write

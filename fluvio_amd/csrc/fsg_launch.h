@@ -50,6 +50,8 @@ void launch_crc(uint8_t* out, uint64_t off, uint64_t n, uint32_t* acc, hipStream
 // process() of a one-batch input in one launch (k_one)
 void launch_one(const OneArgs& o, uint32_t ops, hipStream_t s);
 void launch_write_lean(const WriteArgs& a, uint32_t nblocks, hipStream_t s);
+// generated integer values (KM_I32 / KM_AGG) staged per batch in LDS (other batches: the wave path)
+void launch_write_gen(const WriteArgs& a, uint32_t nblocks, hipStream_t s);
 // aggregate-json, in phases separated by host reads of AggjArgs::scal
 uint64_t xscan_tiles(uint64_t n);  // u64 scratch slots launch_xscan needs for n items
 void launch_aggj_count(const AggjArgs& a, hipStream_t s);

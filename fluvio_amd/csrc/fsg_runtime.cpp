@@ -2499,8 +2499,14 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   // wave path inside it); measured on MI355X: C2 1 KB records write 1.33 -> 1.23
   // ms, C2-json 1.89 -> 1.39 ms against k_write's record-by-record wave copies
   const bool verbatim = !has_agg && !has_array && c->hdesc.out_type != VT_I32;
+  // generated integer values (map_double / filter_map outputs, aggregate-sum's
+  // running sums): staged per batch in LDS (k_write_gen)
+  const bool gen_int = !has_array && !has_aggj && !has_cat &&
+                       (c->hdesc.out_type == VT_I32 || (c->hdesc.flags & CF_AGG_SUM));
   if (verbatim && nblk && p.n_records)
     launch_write_lean(wa, nblk, st);
+  else if (gen_int && nblk && p.n_records)
+    launch_write_gen(wa, nblk, st);
   else
     launch_write(wa, nblk, st);
   if (arr) {  // the lean batches' element records (k_write skips them)
