@@ -8,18 +8,19 @@
 // unanchored is_match over valid UTF-8, Unicode-aware `.` (any scalar but \n),
 // `\d` (Unicode Nd), `\s` (White_Space), `\w` (Alphabetic + M + Nd + Pc +
 // Join_Control), `\p{..}` / `\P{..}` (General_Category values and groups, Any,
-// ASCII, Assigned, White_Space; fsg_unicode.h, generated from this image's
-// Unicode tables), `^`/`$` at value start/end or, under the m flag, at line
+// ASCII, Assigned, regex-syntax's binary properties, Script and
+// Script_Extensions values; fsg_unicode.h, generated from this image's Unicode
+// tables), `^`/`$` at value start/end or, under the m flag, at line
 // boundaries (DFA states that remember whether the previous byte was \n),
-// `\A` / `\z`, `[[:name:]]` ASCII classes, inline flags i (simple case folding,
-// restated for ASCII letters + U+212A / U+017F), s, U, m, x (whitespace and #
+// `\A` / `\z`, `[[:name:]]` ASCII classes, inline flags i (simple case folding:
+// the CaseFolding C + S orbits, on literals, ranges and Unicode classes), s, U, m, x (whitespace and #
 // comments ignored) and u (off: ASCII \d \s \w; a negated class, `.` or \W that
 // could match invalid UTF-8 is the crate's init error).  `\b`, `\B` are exact on
 // ASCII values only (the kernel reports FSG_E_UNSUPPORTED for a non-ASCII value);
 // word boundaries are DFA states that remember whether the previous byte was a
 // word byte.  Nested classes and the class set operations && -- ~~, escapes
-// \x \u \U (fixed digits or braces).  Scripts and other binary properties in
-// \p{..} are rejected at init (FSG_E_UNSUPPORTED).
+// \x \u \U (fixed digits or braces).  Other enumerated properties in \p{..}
+// (Age, the break properties, ...) are rejected at init (FSG_E_UNSUPPORTED).
 //
 // Output: a DFA over bytes with unanchored restart folded in, byte classes,
 // sticky acceptance, an end-of-value acceptance bit and the longest possible
@@ -198,24 +199,36 @@ struct Parser {
           st.insert(st.end(), t.begin(), t.end());
         }
     } else {
-      unsup = true;  // scripts and other properties: not restated
-      return 0;
+      // binary properties, Script / Script_Extensions values (sc= / scx=)
+      const fsg_urange* pr = nullptr;
+      uint32_t pn = 0;
+      if (!fsg_u_lookup(name.c_str(), &pr, &pn)) {
+        unsup = true;  // other properties (Age, Grapheme_Cluster_Break, ...): not restated
+        return 0;
+      }
+      st = urange(pr, pn);
     }
-    if (fi) {  // a Unicode class under (?i) would need full simple case folding
-      unsup = true;
-      return 0;
-    }
+    if (fi) fold_set(st);  // (?i): simple case folding, before the negation
     *out = neg ? negate(st) : norm(st);
     return 2;
   }
   int depth = 0;
 
-  // (?i): simple case folding restated for ASCII letters, + U+212A ~ k and
-  // U+017F ~ s in Unicode mode only ((?-u) folds ASCII bytes: regex-syntax's
-  // byte classes); a literal outside ASCII under (?i) is unsupported
+  // (?i): regex-syntax's simple case folding (CaseFolding.txt C + S orbits,
+  // fsg_unicode.h) in Unicode mode; (?-u) folds ASCII letters only (its byte
+  // classes)
+  static void fold_add(void* ctx, uint32_t c) { static_cast<Set*>(ctx)->push_back({c, c}); }
+  void fold_set(Set& st) {
+    const Set base = st;
+    for (const auto& r : base) fsg_u_fold_range(r.lo, r.hi, fold_add, &st);
+  }
   void add_folded(Set& st, uint32_t lo, uint32_t hi) {
     st.push_back({lo, hi});
     if (!fi) return;
+    if (fu) {
+      fsg_u_fold_range(lo, hi, fold_add, &st);
+      return;
+    }
     if (hi >= 0x80) {
       unsup = true;
       return;
@@ -225,9 +238,6 @@ struct Parser {
     a = std::max<uint32_t>(lo, 'A');
     b = std::min<uint32_t>(hi, 'Z');
     if (a <= b) st.push_back({a + 32, b + 32});
-    if (!fu) return;
-    if ((lo <= 'k' && 'k' <= hi) || (lo <= 'K' && 'K' <= hi)) st.push_back({0x212A, 0x212A});
-    if ((lo <= 's' && 's' <= hi) || (lo <= 'S' && 'S' <= hi)) st.push_back({0x17F, 0x17F});
   }
   // [:name:] ASCII classes (regex-syntax ClassAsciiKind)
   static bool posix(const std::vector<uint32_t>& name, Set& st) {

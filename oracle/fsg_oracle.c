@@ -649,8 +649,10 @@ static void rx_skip_x(rxparser *P) {
     }
   }
 }
+static void cs_fold_add(void *ctx, uint32_t c) { cs_add((cset *)ctx, c, c); }
 /* \p{name} / \pX (after the p / P): General_Category values and groups, Any,
- * ASCII, Assigned, White_Space; names compared without case, ' ', '_', '-' */
+ * ASCII, Assigned, White_Space, binary properties, Script / Script_Extensions
+ * values; names compared without case, ' ', '_', '-' */
 static int rx_property(rxparser *P, int neg, cset *set) {
   if (!P->fu) {
     P->err = 1;
@@ -697,14 +699,18 @@ static int rx_property(rxparser *P, int neg, cset *set) {
     for (uint32_t k = 0; k < fsg_u_ncats; k++)
       if (m & (1L << k))
         for (uint32_t q = 0; q < fsg_u_cats[k].n; q++) cs_add(&tmp, fsg_u_cats[k].r[q].lo, fsg_u_cats[k].r[q].hi);
-  } else {
-    P->unsupported = 1; /* scripts and other properties */
-    return 0;
+  } else { /* binary properties, Script / Script_Extensions values */
+    const fsg_urange *pr = NULL;
+    uint32_t pn = 0;
+    if (!fsg_u_lookup(name, &pr, &pn)) {
+      P->unsupported = 1; /* other enumerated properties (Age, the break properties, ...) */
+      return 0;
+    }
+    for (uint32_t q = 0; q < pn; q++) cs_add(&tmp, pr[q].lo, pr[q].hi);
   }
-  if (P->fi) { /* a Unicode class under (?i) needs full simple case folding */
-    free(tmp.r);
-    P->unsupported = 1;
-    return 0;
+  if (P->fi) { /* (?i): simple case folding before the negation */
+    size_t n0 = tmp.n;
+    for (size_t q = 0; q < n0; q++) fsg_u_fold_range(tmp.r[q].lo, tmp.r[q].hi, cs_fold_add, &tmp);
   }
   cs_norm(&tmp);
   if (neg) cs_negate(&tmp);
@@ -713,13 +719,15 @@ static int rx_property(rxparser *P, int neg, cset *set) {
   return 2;
 }
 
-/* (?i): regex-syntax's simple case folding, restated for ASCII letters: a-z <-> A-Z,
- * plus, in Unicode mode only, the two non-ASCII code points that fold to ASCII
- * letters (U+212A KELVIN SIGN ~ k, U+017F LONG S ~ s); (?-u) folds bytes (ASCII).
- * A literal outside ASCII under (?i) is unsupported. */
+/* (?i): regex-syntax's simple case folding (CaseFolding.txt C + S orbits,
+ * fsg_unicode.h) in Unicode mode; (?-u) folds ASCII letters only (bytes). */
 static void cs_add_folded(rxparser *P, cset *s, uint32_t lo, uint32_t hi) {
   cs_add(s, lo, hi);
   if (!P->fi) return;
+  if (P->fu) {
+    fsg_u_fold_range(lo, hi, cs_fold_add, s);
+    return;
+  }
   if (hi >= 0x80) {
     P->unsupported = 1;
     return;
@@ -729,9 +737,6 @@ static void cs_add_folded(rxparser *P, cset *s, uint32_t lo, uint32_t hi) {
   a = lo > 'A' ? lo : 'A';
   b = hi < 'Z' ? hi : 'Z';
   if (a <= b) cs_add(s, a + 32, b + 32);
-  if (!P->fu) return;
-  if ((lo <= 'k' && 'k' <= hi) || (lo <= 'K' && 'K' <= hi)) cs_add(s, 0x212A, 0x212A);
-  if ((lo <= 's' && 's' <= hi) || (lo <= 'S' && 'S' <= hi)) cs_add(s, 0x17F, 0x17F);
 }
 /* [[:name:]] ASCII classes (regex-syntax ast ClassAsciiKind) */
 static int posix_class(const uint32_t *p, size_t n, cset *s) {

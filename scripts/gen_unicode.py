@@ -28,6 +28,174 @@ def ranges(pred):
     return out
 
 
+# regex-syntax's binary properties (property_bool.rs: PropList, DerivedCoreProperties,
+# emoji-data) with their PropertyAliases.txt names; Changes_When_NFKC_Casefolded is
+# left out (the Python regex module has no table for it: \p{CWKCF} stays unsupported)
+BOOLS = [("ASCII_Hex_Digit", "AHex"), ("Alphabetic", "Alpha"), ("Bidi_Control", "Bidi_C"),
+         ("Bidi_Mirrored", "Bidi_M"), ("Case_Ignorable", "CI"), ("Cased",), ("Changes_When_Casefolded", "CWCF"),
+         ("Changes_When_Casemapped", "CWCM"), ("Changes_When_Lowercased", "CWL"), ("Changes_When_Titlecased", "CWT"),
+         ("Changes_When_Uppercased", "CWU"), ("Dash",), ("Default_Ignorable_Code_Point", "DI"), ("Deprecated", "Dep"),
+         ("Diacritic", "Dia"), ("Emoji",), ("Emoji_Component", "EComp"), ("Emoji_Modifier", "EMod"),
+         ("Emoji_Modifier_Base", "EBase"), ("Emoji_Presentation", "EPres"), ("Extended_Pictographic", "ExtPict"),
+         ("Extender", "Ext"), ("Grapheme_Base", "Gr_Base"), ("Grapheme_Extend", "Gr_Ext"), ("Grapheme_Link", "Gr_Link"),
+         ("Hex_Digit", "Hex"), ("Hyphen",), ("IDS_Binary_Operator", "IDSB"), ("IDS_Trinary_Operator", "IDST"),
+         ("ID_Continue", "IDC"), ("ID_Start", "IDS"), ("Ideographic", "Ideo"), ("Join_Control", "Join_C"),
+         ("Logical_Order_Exception", "LOE"), ("Lowercase", "Lower"), ("Math",), ("Noncharacter_Code_Point", "NChar"),
+         ("Other_Alphabetic", "OAlpha"), ("Other_Default_Ignorable_Code_Point", "ODI"),
+         ("Other_Grapheme_Extend", "OGr_Ext"), ("Other_ID_Continue", "OIDC"), ("Other_ID_Start", "OIDS"),
+         ("Other_Lowercase", "OLower"), ("Other_Math", "OMath"), ("Other_Uppercase", "OUpper"),
+         ("Pattern_Syntax", "Pat_Syn"), ("Pattern_White_Space", "Pat_WS"), ("Prepended_Concatenation_Mark", "PCM"),
+         ("Quotation_Mark", "QMark"), ("Radical",), ("Regional_Indicator", "RI"), ("Sentence_Terminal", "STerm"),
+         ("Soft_Dotted", "SD"), ("Terminal_Punctuation", "Term"), ("Unified_Ideograph", "UIdeo"),
+         ("Uppercase", "Upper"), ("Variation_Selector", "VS"), ("White_Space", "WSpace", "space"),
+         ("XID_Continue", "XIDC"), ("XID_Start", "XIDS")]
+# scripts the reference's Unicode 15 tables do not have (added in Unicode 16 / 17)
+NEW_SCRIPTS = {"GARAY", "GURUNGKHEMA", "KIRATRAI", "OLONAL", "SUNUWAR", "TODHRI", "TULUTIGALARI", "BERIAERFE",
+               "SIDETIC", "TAIYO", "TOLONGSIKI"}
+
+
+def norm(name):
+    return "".join(ch for ch in name.lower() if ch not in " _-")
+
+
+def collapse(cps):
+    out = []
+    for c in cps:
+        if out and out[-1][1] + 1 == c:
+            out[-1][1] = c
+        else:
+            out.append([c, c])
+    return [tuple(r) for r in out]
+
+
+def props_and_folds():
+    """Binary properties and Script / Script_Extensions values from the Python
+    regex module (its UCD is newer than the reference's Unicode 15: code points
+    assigned since differ, parity unpinned for them); simple case folding from
+    this Python's str case mappings (Unicode 13)."""
+    import regex
+    import regex._regex_core as rc
+    allc = "".join(chr(c) for c in range(0x110000))
+
+    def cps_of(pat):
+        return collapse(m.start() for m in regex.finditer(pat, allc))
+
+    lines, sets, names = [], [], []
+    gc_names = set()
+    for i, k in enumerate(CATS):
+        gc_names.add(k.lower())
+    for b in BOOLS:
+        rs = cps_of(r"\p{%s}" % b[0])
+        idx = len(sets)
+        sets.append(("b_" + b[0], rs))
+        for a in b:
+            n = norm(a)
+            assert n not in gc_names or n == "space", n
+            names.append((n, 1, idx))
+    by_id = {}
+    for nm, i in rc.PROPERTIES["SCRIPT"][1].items():
+        by_id.setdefault(i, []).append(nm)
+    for i, nms in sorted(by_id.items()):
+        if any(n in NEW_SCRIPTS for n in nms):
+            continue
+        canon = max(nms, key=len)
+        sc = cps_of(r"\p{Script=%s}" % canon)
+        scx = cps_of(r"\p{Script_Extensions=%s}" % canon)
+        si = len(sets)
+        sets.append(("sc_" + canon, sc))
+        sets.append(("scx_" + canon, scx))
+        for n in nms:
+            names.append((n.lower(), 2, si))
+            names.append((n.lower(), 3, si + 1))
+    for nm, rs in sets:
+        lines.append("static const fsg_urange fsg_u_%s[] = {%s};" % (nm, ", ".join("{0x%X, 0x%X}" % r for r in rs) or "{1, 0}"))
+    lines.append("static const fsg_urange* const fsg_u_psets[] = {%s};" % ", ".join("fsg_u_" + nm for nm, _ in sets))
+    lines.append("static const uint32_t fsg_u_psets_n[] = {%s};" % ", ".join(str(len(rs)) for _, rs in sets))
+    names.sort()
+    lines.append("/* normalized name, kind (1 binary property, 2 Script value, 3 Script_Extensions value), set */")
+    lines.append("static const struct { const char *n; int k, s; } fsg_u_pnames[] = {" +
+                 ", ".join('{"%s", %d, %d}' % t for t in names) + "};")
+    lines.append("""/* a normalized \\p{..} name that is not a General_Category value: a binary
+ * property, a Script value (bare or sc= / script=) or a Script_Extensions value
+ * (scx= / scriptextensions=), in regex-syntax's order; 1 found, 0 unknown */
+static int fsg_u_lookup(const char *name, const fsg_urange **r, uint32_t *n) {
+  const char *eq = strchr(name, '=');
+  int want = 0;
+  const char *v = name;
+  if (eq) {
+    size_t pl = (size_t)(eq - name);
+    if ((pl == 2 && !strncmp(name, "sc", 2)) || (pl == 6 && !strncmp(name, "script", 6))) want = 2;
+    else if ((pl == 3 && !strncmp(name, "scx", 3)) || (pl == 16 && !strncmp(name, "scriptextensions", 16))) want = 3;
+    else return 0;
+    v = eq + 1;
+  } else if (!strcmp(name, "cf") || !strcmp(name, "sc") || !strcmp(name, "lc")) {
+    return 0;
+  }
+  for (int pass = eq ? want : 1; pass <= (eq ? want : 2); pass++)
+    for (size_t i = 0; i < sizeof fsg_u_pnames / sizeof fsg_u_pnames[0]; i++)
+      if (fsg_u_pnames[i].k == pass && !strcmp(fsg_u_pnames[i].n, v)) {
+        *r = fsg_u_psets[fsg_u_pnames[i].s];
+        *n = fsg_u_psets_n[fsg_u_pnames[i].s];
+        return 1;
+      }
+  return 0;
+}""")
+    # simple case folding (CaseFolding.txt statuses C + S, as ucd-generate builds
+    # regex-syntax's table): a code point's simple fold is its casefold() when
+    # that is one character (status C), else its lowercase when that is one
+    # character (the S entry of an F code point: U+1E9E -> U+00DF, U+1F88 ->
+    # U+1F80), else itself; the orbits are the classes of equal folds (Turkic T
+    # entries stay out: U+0131 and U+0130 have none)
+    def sfold(c):
+        ch = chr(c)
+        f = ch.casefold()
+        if len(f) == 1:
+            return ord(f)
+        lo = ch.lower()
+        return ord(lo) if len(lo) == 1 else c
+    groups = {}
+    for c in range(0x110000):
+        if 0xD800 <= c <= 0xDFFF:
+            continue
+        groups.setdefault(sfold(c), set()).add(c)
+    orbits = []
+    for k, mem in groups.items():
+        mem.add(k)
+        if len(mem) > 1:
+            orbits.append(sorted(mem))
+    orbits.sort()
+    cp_orb = []
+    for oi, mem in enumerate(orbits):
+        for c in mem:
+            cp_orb.append((c, oi))
+    cp_orb.sort()
+    offs, flat = [], []
+    for mem in orbits:
+        offs.append(len(flat))
+        flat += mem
+    offs.append(len(flat))
+    lines.append("/* simple case folding: code points with case-fold equivalents, their orbit, the orbits' members */")
+    lines.append("static const uint32_t fsg_u_fold_cp[] = {%s};" % ", ".join("0x%X" % c for c, _ in cp_orb))
+    lines.append("static const uint16_t fsg_u_fold_orb[] = {%s};" % ", ".join(str(o) for _, o in cp_orb))
+    lines.append("static const uint16_t fsg_u_orb_off[] = {%s};" % ", ".join(str(o) for o in offs))
+    lines.append("static const uint32_t fsg_u_orb_mem[] = {%s};" % ", ".join("0x%X" % c for c in flat))
+    lines.append("static const uint32_t fsg_u_fold_n = %d;" % len(cp_orb))
+    lines.append("""/* every case-fold equivalent of the code points in [lo, hi] (their orbits' members) */
+static void fsg_u_fold_range(uint32_t lo, uint32_t hi, void (*add)(void *, uint32_t), void *ctx) {
+  uint32_t a = 0, b = fsg_u_fold_n;
+  while (a < b) {
+    uint32_t m = (a + b) / 2;
+    if (fsg_u_fold_cp[m] < lo) a = m + 1; else b = m;
+  }
+  for (uint32_t i = a; i < fsg_u_fold_n && fsg_u_fold_cp[i] <= hi; i++) {
+    uint32_t o = fsg_u_fold_orb[i];
+    for (uint32_t j = fsg_u_orb_off[o]; j < fsg_u_orb_off[o + 1]; j++) add(ctx, fsg_u_orb_mem[j]);
+  }
+}""")
+    print(f"{len(sets)} property sets ({sum(len(r) for _, r in sets)} ranges), {len(orbits)} fold orbits", file=sys.stderr)
+    return lines
+
+
 def main():
     cat = [unicodedata.category(chr(c)) for c in range(0x110000)]
     oalpha = set()
@@ -36,7 +204,8 @@ def main():
     tabs = {k: ranges(lambda c, k=k: cat[c] == k) for k in CATS}
     word = ranges(lambda c: cat[c][0] in "LM" or cat[c] in ("Nd", "Nl", "Pc") or c in (0x200C, 0x200D) or c in oalpha)
     lines = ["/* generated by scripts/gen_unicode.py from Python unicodedata %s: General_Category" % unicodedata.unidata_version,
-             " * ranges and regex-syntax's Perl \\\\w (Alphabetic + M + Nd + Pc + Join_Control).  Do not edit. */",
+             " * ranges and regex-syntax's Perl \\\\w (Alphabetic + M + Nd + Pc + Join_Control); binary properties,",
+             " * scripts from the Python regex module, simple case folding from str case mappings.  Do not edit. */",
              "#pragma once", "#include <stdint.h>", "#include <string.h>", "#include <stddef.h>",
              "typedef struct { uint32_t lo, hi; } fsg_urange;",
              "#define FSG_UNICODE_VERSION \"%s\"" % unicodedata.unidata_version]
@@ -92,6 +261,7 @@ def main():
     lines.append("    if (!strcmp(T[i].n, nm)) return T[i].m;")
     lines.append("  return -1;")
     lines.append("}")
+    lines += props_and_folds()
     text = "\n".join(lines) + "\n"
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for d in ("fluvio_amd/csrc", "oracle"):

@@ -181,6 +181,7 @@ CHAINS = {
     "regex_multiline": [("regex-filter", {"regex": r"(?m)^\d+$|x$|^\{\x22level"}, None)],
     "regex_verbose": [("regex-filter", {"regex": r"(?x) time out \s* \d  # the timeout records"}, None)],
     "regex_ascii_only": [("regex-filter", {"regex": r"(?-u)\w\d{2}\s"}, None)],
+    "regex_script_fold": [("regex-filter", {"regex": r"(?i)\p{Greek}|É\p{Alphabetic}|\p{Emoji_Presentation}|TIME\p{Ll}"}, None)],
     "map_then_regex_ci": [("map", {}, None), ("regex-filter", {"regex": r"(?i)error"}, None)],
     "map": [("map", {}, None)],
     "filter_json": [("filter_json", {}, None)],

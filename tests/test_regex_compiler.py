@@ -30,12 +30,17 @@ PATTERNS = [r"\d{3}-\d{2}-\d{4}", r"[A-Z]", r"^ab|cd$", r"a(b|c)*d", r"colou?r\s
             r"[a-z&&[^aeiou]]{2}", r"[\w--\d]+x", r"[a-g~~c-j]", r"[0-9--4]", r"[[a-c][x-z]]", r"[^[a-c]d]",
             r"[a-z&&b-y&&[^m]]", r"[\pL&&\p{Ll}]é", r"[\p{L}--[a-zé]]", r"[a-c~~b-d~~c-e]", r"[--a]", r"[]a]",
             r"[a-c--b]d", r"\u0041\U0001F600?\u{263a}", r"[\u00e9-\u00ea\U000003b1]", r"(?i)[a-z--k]",
-            r"(?-u)[[^a]&&[b-c]]", r"(?x)[ a-z && [^ x ] ]"]
+            r"(?-u)[[^a]&&[b-c]]", r"(?x)[ a-z && [^ x ] ]",
+            # binary properties, scripts, Script_Extensions; (?i) on Unicode literals and classes
+            r"\p{Greek}+", r"\p{sc=Cyrillic}\w", r"\p{scx=Grek}", r"\p{Alphabetic}{2}", r"\p{Emoji}",
+            r"\P{Greek}$", r"[\p{Greek}&&\p{Ll}]", r"\p{Script_Extensions=Arabic}", r"\p{Upper}\p{Lower}",
+            r"\p{White_Space}", r"(?i)\p{Lu}", r"(?i)é", r"(?i)Σ", r"(?i)[α-γ]x?", r"(?i)ǆ", r"(?i)\P{Ll}",
+            r"(?i)[^σ]", r"(?i)ж+", r"(?i)[\p{Greek}--α]"]
 WORD = ("\\b", "\\B")
 
 
 def texts(rng):
-    alpha = "abcdxyzABCD0123456789- \t\n.é☺αβωÉ٣€_#"
+    alpha = "abcdxyzABCD0123456789- \t\n.é☺αβωÉ٣€_#ΣσςЖжǄǅǆΑΓ"
     out = ["", "a", "abc", "ac", "xxy", "123-45-6789", "my ssn 987-65-4321!", "colour  x", "☺A", "aé",
            "abcd", "cd", "ab", "timeouts", "αβγ", "aaa", "abcbcd", "a\nb\nc", "x\nb", "naïve", "9 ٣", "c\na"]
     for _ in range(60):
@@ -67,8 +72,8 @@ def test_max_len():
                                       ("(?-u:.)", _ffi.FSG_E_INIT), ("(?-u)[^a]", _ffi.FSG_E_INIT),
                                       (r"(?-u)\W", _ffi.FSG_E_INIT), (r"(?-u)\pL", _ffi.FSG_E_INIT),
                                       (r"\p{", _ffi.FSG_E_INIT), (r"\p{Nope}", _ffi.FSG_E_UNSUPPORTED),
-                                      (r"(?i)\p{Lu}", _ffi.FSG_E_UNSUPPORTED), ("(?R)a", _ffi.FSG_E_UNSUPPORTED),
-                                      (r"\p{Greek}", _ffi.FSG_E_UNSUPPORTED), ("(?i)é", _ffi.FSG_E_UNSUPPORTED),
+                                      (r"\p{Age=3.0}", _ffi.FSG_E_UNSUPPORTED), ("(?R)a", _ffi.FSG_E_UNSUPPORTED),
+                                      (r"\p{CWKCF}", _ffi.FSG_E_UNSUPPORTED), (r"\p{Garay}", _ffi.FSG_E_UNSUPPORTED),
                                       ("[a-c", _ffi.FSG_E_INIT), ("[a[b]", _ffi.FSG_E_INIT), (r"\u12", _ffi.FSG_E_INIT),
                                       (r"\u{110000}", _ffi.FSG_E_INIT), (r"\ud800", _ffi.FSG_E_INIT),
                                       (r"(?-u)[[^a]--b]", _ffi.FSG_E_INIT)])
@@ -123,14 +128,45 @@ def test_random_patterns_match_oracle():
     (r"(?i)k", "K", True), (r"(?i-u)k", "K", False), (r"(?i)s", "ſ", True),
     (r"(?i-u)s", "ſ", False), (r"(?i-u)[[:alpha:]]", "K", False), (r"(?i-u)K", "k", True),
     (r"(?i)[[:alpha:]]", "K", True),
+    # simple case folding (CaseFolding C + S): orbits, no full folding, no Turkic entries
+    (r"(?i)σ", "ς", True), (r"(?i)Σ", "σ", True), (r"(?i)ß", "ẞ", True), (r"(?i)^ß$", "ss", False),
+    (r"(?i)i", "ı", False), (r"(?i)i", "İ", False), (r"(?i)I", "i", True), (r"(?i)ǆ", "ǅ", True),
+    (r"(?i)ǆ", "Ǆ", True), (r"(?i)θ", "ϑ", True), (r"(?i)\p{Lu}", "a", True), (r"\p{Lu}", "a", False),
+    (r"(?i)[^a]", "A", False), (r"(?i)\P{Lu}", "A", False), (r"(?i)\P{Lu}", "a", False), (r"(?i)\P{Lu}", "1", True), (r"(?i)ω", "Ω", True), (r"(?i)µ", "Μ", True),
+    (r"\p{Greek}", "ω", True), (r"\p{Greek}", "w", False), (r"\p{sc=Latin}", "é", True),
+    (r"\p{isGreek}", "ω", None),
     # (?x): whitespace around a class range's '-' is skipped (parse_set_class_range's bump_space)
     (r"(?x)[a - z]", "m", True), (r"(?x)[a - z]", "-", False), (r"(?x)[a - ]", "-", True),
     (r"(?x)[ a -z ]x", "qx", True), (r"[a - z]", "-", False), (r"[a - z]", " ", True), (r"[a - z]", "m", False),
 ])
 def test_fold_and_x_ranges(pattern, text, expect):
     b = text.encode()
+    if expect is None:  # a property name outside the tables: FSG_E_UNSUPPORTED on both sides (loud)
+        with pytest.raises(ValueError):
+            O.regex_is_match(pattern, b)
+        with pytest.raises(ValueError) as e:
+            dfa_match(pattern, b)
+        assert e.value.args[0] == _ffi.FSG_E_UNSUPPORTED
+        return
     assert O.regex_is_match(pattern, b) == expect
     assert dfa_match(pattern, b)[0] == expect
+
+
+@pytest.mark.parametrize("pattern", [r"\p{Greek}", r"\p{Cyrillic}+", r"\p{scx=Arabic}", r"\p{Emoji}", r"\p{Alphabetic}",
+                                     r"\p{Uppercase}", r"\p{Dash}", r"\p{Han}", r"\P{Latin}", r"[\p{Greek}\p{Cyrillic}]{2}",
+                                     r"\p{Extended_Pictographic}", r"\p{Math}"])
+def test_properties_against_python_regex(pattern):
+    """Binary properties, scripts and Script_Extensions over random text of
+    Greek, Cyrillic, Latin, Arabic, CJK and symbols, against Python's `regex`
+    module (the tables' source: the same UCD values)."""
+    regex = pytest.importorskip("regex")
+    rng = random.Random(hash(pattern) & 0xFFFF)
+    alpha = "aZé-ωΣж٣ب漢☺€+𝟘😀́ 1_"
+    for _ in range(200):
+        t = "".join(rng.choice(alpha) for _ in range(rng.randint(0, 6)))
+        want = regex.search(pattern, t) is not None
+        assert dfa_match(pattern, t.encode())[0] == want, (pattern, t)
+        assert O.regex_is_match(pattern, t.encode()) == want, (pattern, t)
 
 
 @pytest.mark.parametrize("bad", [r"(?-u)[é]", r"(?-u)[a-é]", r"(?-u)[é]"])
