@@ -17,8 +17,10 @@ extern "C" int fsg_debug_regex_match(const char* pattern, const uint8_t* text, s
   bool ascii = true;
   for (size_t i = 0; i < n; i++) ascii &= text[i] < 0x80;
   // the kernel's choice: ASCII DFA for ASCII-only values, full DFA otherwise
-  *is_match = fsg::dfa_is_match(ascii ? a : d, text, n) ? 1 : 0;
-  if (!ascii && a.unicode_word) return -103;
+  // (the marked walk for Unicode word boundaries)
+  if (!ascii && a.unicode_word && !d.marked) return -103;
+  *is_match = (ascii ? fsg::dfa_is_match(a, text, n) : d.marked ? fsg::dfa_is_match_marked(d, text, n)
+                                                                : fsg::dfa_is_match(d, text, n)) ? 1 : 0;
   if (max_len) *max_len = a.max_len;
   if (nstates) *nstates = (int)d.nstates;
   return 0;

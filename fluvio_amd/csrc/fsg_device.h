@@ -75,6 +75,12 @@ struct DfaDesc {
   uint32_t f_trans;    // blob offset: u16[f_nstates * f_nclasses]
   uint32_t f_accept;   // blob offset: u8[f_nstates]
   uint32_t unicode_word;
+  // f_marked: the full DFA expects a marker byte before every code point
+  // (0xFC word / 0xFD other / 0xFE \n: Unicode word boundaries); wtab: blob
+  // offset of the Unicode \w ranges (u32 lo, hi pairs), wtab_n of them
+  uint32_t f_marked;
+  uint32_t wtab;
+  uint32_t wtab_n;
   // register-resident form for the lean kernel (ASCII DFA with <= 16 states):
   // tt[b] = the row of byte b, next state of s in bits [4s, 4s+4); acc1/acc2 =
   // states with accept bit0 / bit1

@@ -670,6 +670,47 @@ __device__ bool dfa_run_full(P s, uint32_t n, const uint8_t* blob, const DfaDesc
   return (acc[st] & 2) != 0;
 }
 
+// the marked walk (Unicode \b / \B, fsg_regex.h): before each code point the
+// marker of its class (0xFC a \w code point, 0xFE \n, 0xFD any other), then
+// its bytes; \w membership by binary search over the blob's ranges.  The
+// value is valid UTF-8 here (checked before the stage).
+template <typename P>
+__device__ bool dfa_run_marked(P s, uint32_t n, const uint8_t* blob, const DfaDesc& f, bool upper) {
+  const uint8_t* cls = blob + (upper ? f.f_classmap_up : f.f_classmap);
+  const uint8_t* mcls = blob + f.f_classmap;  // the markers' classes (uppercasing leaves them)
+  const uint16_t* tr = (const uint16_t*)(blob + f.f_trans);
+  const uint8_t* acc = blob + f.f_accept;
+  const uint32_t* wt = (const uint32_t*)(blob + f.wtab);
+  uint32_t st = f.f_s_bot;
+  if (acc[st] & 1) return true;
+  for (uint32_t i = 0; i < n;) {
+    const uint32_t c0 = s[i];
+    const uint32_t w = c0 < 0x80 ? 1u : c0 < 0xE0 ? 2u : c0 < 0xF0 ? 3u : 4u;
+    uint32_t cp = w == 1 ? c0 : w == 2 ? (c0 & 0x1Fu) : w == 3 ? (c0 & 0x0Fu) : (c0 & 0x07u);
+    for (uint32_t k = 1; k < w && i + k < n; k++) cp = (cp << 6) | (s[i + k] & 0x3Fu);
+    bool word;
+    if (cp < 0x80) {
+      word = (cp >= '0' && cp <= '9') || (cp >= 'A' && cp <= 'Z') || (cp >= 'a' && cp <= 'z') || cp == '_';
+    } else {
+      uint32_t lo = 0, hi = f.wtab_n;
+      while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (wt[2 * m + 1] < cp) lo = m + 1; else hi = m;
+      }
+      word = lo < f.wtab_n && wt[2 * lo] <= cp;
+    }
+    const uint32_t mk = cp == '\n' ? 0xFEu : word ? 0xFCu : 0xFDu;
+    st = tr[st * f.f_nclasses + mcls[mk]];
+    if (acc[st] & 1) return true;
+    for (uint32_t k = 0; k < w && i + k < n; k++) {
+      st = tr[st * f.f_nclasses + cls[s[i + k]]];
+      if (acc[st] & 1) return true;
+    }
+    i += w;
+  }
+  return (acc[st] & 2) != 0;
+}
+
 // ---------------------------------------------------------------------------
 // evaluate the chain (stages [0, nst)) over the records of one window
 // ---------------------------------------------------------------------------
@@ -762,12 +803,13 @@ __device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int 
             bool m;
             if (src) {
               if (f & RF_NONASCII) {
-                if (sd.dfa.unicode_word) {
-                  err = true;  // \w on a non-ASCII value: surfaces only if this record is reached
+                if (sd.dfa.unicode_word && !sd.dfa.f_marked) {
+                  err = true;  // (?-u) \b on a non-ASCII value: surfaces only if this record is reached
                   ec = EC_UNSUP;
                   break;
                 }
-                m = dfa_run_full(w + vs, vl, blob, sd.dfa, upper);
+                m = sd.dfa.f_marked ? dfa_run_marked(w + vs, vl, blob, sd.dfa, upper)
+                                    : dfa_run_full(w + vs, vl, blob, sd.dfa, upper);
               } else if (sd.dfa.max_len >= 0) {
                 m = (f & RF_MATCH) != 0;
                 // an empty value is never visited by the chunk scan

@@ -15,10 +15,12 @@
 // `\A` / `\z`, `[[:name:]]` ASCII classes, inline flags i (simple case folding:
 // the CaseFolding C + S orbits, on literals, ranges and Unicode classes), s, U, m, x (whitespace and #
 // comments ignored) and u (off: ASCII \d \s \w; a negated class, `.` or \W that
-// could match invalid UTF-8 is the crate's init error).  `\b`, `\B` are exact on
-// ASCII values only (the kernel reports FSG_E_UNSUPPORTED for a non-ASCII value);
-// word boundaries are DFA states that remember whether the previous byte was a
-// word byte.  Nested classes and the class set operations && -- ~~, escapes
+// could match invalid UTF-8 is the crate's init error).  `\b`, `\B`: word
+// boundaries are DFA states that remember whether the previous byte was a word
+// byte (ASCII values); for values with non-ASCII bytes the full DFA is built
+// over the bytes with a marker before each code point carrying its Unicode \w
+// class (determinize's marker mode); a (?-u) \b keeps non-ASCII values
+// FSG_E_UNSUPPORTED.  Nested classes and the class set operations && -- ~~, escapes
 // \x \u \U (fixed digits or braces).  Other enumerated properties in \p{..}
 // (Age, the break properties, ...) are rejected at init (FSG_E_UNSUPPORTED).
 //
@@ -124,6 +126,7 @@ struct Parser {
   std::vector<uint32_t> p;
   size_t i = 0;
   bool err = false, unsup = false, word = false, wb = false, ml = false;
+  bool wbu = false, wba = false;  // \b / \B seen in Unicode mode / under (?-u)
   bool fi = false, fs = false;  // inline flags i, s
   bool fm = false, fx = false, fu = true;  // m (multi-line), x (verbose), u (Unicode, on by default)
 
@@ -335,7 +338,10 @@ struct Parser {
           err = true;
           return 0;
         }
-        if (e == 'b' || e == 'B') word = wb = true;
+        if (e == 'b' || e == 'B') {
+          word = wb = true;
+          (fu ? wbu : wba) = true;
+        }
         return e == 'b' ? 3 : e == 'B' ? 4 : e == 'A' ? 5 : 6;
       default:
         if (e < 0x80 && !((e >= '0' && e <= '9') || (e >= 'a' && e <= 'z') || (e >= 'A' && e <= 'Z'))) {
@@ -1092,7 +1098,8 @@ struct Closure {
 
 }  // namespace
 
-static int determinize(const Node* rootp, bool ascii, bool word, bool wb, bool mlm, Dfa& out, std::string& msg);
+static int determinize(const Node* rootp, bool ascii, bool word, bool wb, bool mlm, Dfa& out, std::string& msg,
+                       bool marker = false);
 
 int compile_regex(const std::string& pattern, Dfa& out, Dfa& full, std::string& msg) {
   // pattern -> code points (must be valid UTF-8; Rust &str)
@@ -1123,7 +1130,18 @@ int compile_regex(const std::string& pattern, Dfa& out, Dfa& full, std::string& 
     return -2;
   }
   if (int rc = determinize(root.get(), true, P.word, P.wb, P.ml, out, msg)) return rc;
-  return determinize(root.get(), false, P.word, P.wb, P.ml, full, msg);
+  // Unicode word boundaries: the full DFA is the marked one (a (?-u) \b among
+  // them keeps non-ASCII values FSG_E_UNSUPPORTED: bytes inside a code point)
+  return determinize(root.get(), false, P.word, P.wb, P.ml, full, msg, P.wbu && !P.wba);
+}
+
+static bool word_cp(uint32_t c) {
+  uint32_t a = 0, b = fsg_u_word_n;
+  while (a < b) {
+    const uint32_t m = (a + b) / 2;
+    if (fsg_u_word[m].hi < c) a = m + 1; else b = m;
+  }
+  return a < fsg_u_word_n && fsg_u_word[a].lo <= c;
 }
 
 // ~0.5 s of subset construction on one core: a pattern whose DFA needs more is
@@ -1132,11 +1150,14 @@ static const int64_t kCompileBudget = 60000000;
 
 static bool word_byte(int b) { return (b >= '0' && b <= '9') || (b >= 'A' && b <= 'Z') || (b >= 'a' && b <= 'z') || b == '_'; }
 
-int determinize(const Node* rootp, bool ascii, bool word, bool wb, bool mlm, Dfa& out, std::string& msg) {
+int determinize(const Node* rootp, bool ascii, bool word, bool wb, bool mlm, Dfa& out, std::string& msg, bool marker) {
   // word boundaries and multi-line anchors need the previous byte: no
   // chunk-parallel restarts (max_len -1)
   const int64_t ml = (wb || mlm) ? -1 : max_len(rootp, ascii);
   const bool resolve = wb || mlm;  // assertions decided at each transition from the previous / next byte
+  // marker mode (Unicode \b): the assertions are decided at the marker before
+  // each code point (its word-ness / \n), the unanchored restart added there;
+  // the code point's bytes only move the NFA (pending assertions wait)
   Nfa g;
   Frag f = build(g, rootp, ascii);
   int m = g.add(F_MATCH);
@@ -1154,6 +1175,8 @@ int determinize(const Node* rootp, bool ascii, bool word, bool wb, bool mlm, Dfa
     for (int b = 0; b < 256; b++)
       if (word_byte(b) != (b > 0 && word_byte(b - 1))) cut[b] = 1;
   if (mlm) cut['\n'] = cut['\n' + 1] = 1;  // \n is its own class
+  if (marker)  // each marker its own class
+    for (int b = kMarkWord; b <= kMarkNl + 1; b++) cut[b] = 1;
   std::vector<uint8_t> cls(256);
   std::vector<int> rep;
   int nc = -1;
@@ -1236,6 +1259,7 @@ int determinize(const Node* rootp, bool ascii, bool word, bool wb, bool mlm, Dfa
         full.insert(full.end(), S.begin(), S.end());
         std::sort(full.begin(), full.end());
       }
+      if (marker) full.push_back(start);  // a match may start at the end position
       auto ce = C.run(full, bot_flag[k], true, resolve, pw, false, pnl, false);
       if (has_match(ce) || (fast && !bot_flag[k] && s_eot)) a |= 2;
     } else {
@@ -1250,9 +1274,33 @@ int determinize(const Node* rootp, bool ascii, bool word, bool wb, bool mlm, Dfa
         continue;
       }
       const int byte = rep[c];
-      const bool nw = wb && word_byte(byte);
-      const bool nnl = mlm && byte == '\n';
-      const std::vector<int> res = resolve ? C.run(cur, bot_flag[k], false, true, pw, nw, pnl, nnl) : cur;
+      if (marker && byte < kMarkWord) {  // a byte of the code point: no assertion decided, no restart
+        std::vector<int> nxt;
+        for (int s : cur) {
+          const NState& x = g.st[s];
+          if (x.t == F_BYTE && byte >= x.lo && byte <= x.hi) nxt.push_back(x.a);
+        }
+        row[c] = intern(C.run(nxt, false, false), false, pw, pnl);
+        continue;
+      }
+      if (marker && byte > kMarkNl) {  // never fed
+        row[c] = (int)k;
+        continue;
+      }
+      const bool nw = marker ? byte == kMarkWord : wb && word_byte(byte);
+      const bool nnl = marker ? (mlm && byte == kMarkNl) : mlm && byte == '\n';
+      std::vector<int> seeds = cur;
+      if (marker) seeds.push_back(start);  // the unanchored restart at this code point
+      const std::vector<int> res = resolve ? C.run(seeds, bot_flag[k], false, true, pw, nw, pnl, nnl) : cur;
+      if (marker) {  // the marker consumes nothing: the resolved set waits for the code point's bytes
+        if (has_match(res)) {
+          if (s_acc < 0) s_acc = intern({m}, false, false);
+          row[c] = s_acc;
+        } else {
+          row[c] = intern(res, false, nw, nnl);
+        }
+        continue;
+      }
       if (resolve && has_match(res)) {  // an assertion before this byte completed the match
         if (s_acc < 0) s_acc = intern({m}, false, false);
         row[c] = s_acc;
@@ -1325,6 +1373,7 @@ int determinize(const Node* rootp, bool ascii, bool word, bool wb, bool mlm, Dfa
   out.s_mid = (uint32_t)ren[blk[s_mid]];
   out.max_len = ml < 0 || ml > (1 << 20) ? -1 : (int32_t)ml;
   out.unicode_word = word;
+  out.marked = marker;
   out.classmap = cls;
   out.classmap_up.resize(256);
   for (int b = 0; b < 256; b++) out.classmap_up[b] = cls[(b >= 'a' && b <= 'z') ? b - 32 : b];
@@ -1333,6 +1382,35 @@ int determinize(const Node* rootp, bool ascii, bool word, bool wb, bool mlm, Dfa
     for (uint32_t c = 0; c < out.nclasses; c++) out.trans[s * out.nclasses + c] = (uint16_t)trans[s][c];
   out.accept = acc;
   return 0;
+}
+
+std::vector<uint32_t> unicode_word_ranges() {
+  std::vector<uint32_t> v;
+  for (uint32_t q = 0; q < fsg_u_word_n; q++) {
+    v.push_back(fsg_u_word[q].lo);
+    v.push_back(fsg_u_word[q].hi);
+  }
+  return v;
+}
+
+bool dfa_is_match_marked(const Dfa& d, const uint8_t* s, size_t n) {
+  uint32_t st = d.s_bot;
+  if (d.accept[st] & 1) return true;
+  auto step = [&](uint8_t b) {
+    st = d.trans[st * d.nclasses + d.classmap[b]];
+    return (d.accept[st] & 1) != 0;
+  };
+  for (size_t i = 0; i < n;) {
+    const uint32_t c0 = s[i];
+    const size_t w = c0 < 0x80 ? 1 : c0 < 0xE0 ? 2 : c0 < 0xF0 ? 3 : 4;
+    uint32_t cp = w == 1 ? c0 : w == 2 ? (c0 & 0x1F) : w == 3 ? (c0 & 0x0F) : (c0 & 0x07);
+    for (size_t k = 1; k < w && i + k < n; k++) cp = (cp << 6) | (s[i + k] & 0x3F);
+    if (step(cp == '\n' ? kMarkNl : word_cp(cp) ? kMarkWord : kMarkOther)) return true;
+    for (size_t k = 0; k < w && i + k < n; k++)
+      if (step(s[i + k])) return true;
+    i += w;
+  }
+  return (d.accept[st] & 2) != 0;
 }
 
 bool dfa_is_match(const Dfa& d, const uint8_t* s, size_t n) {

@@ -10,6 +10,11 @@ struct Dfa {
   uint32_t nstates = 0, nclasses = 0, s_bot = 0, s_mid = 0;
   int32_t max_len = -1;  // longest match in bytes, -1 unbounded
   bool unicode_word = false;
+  // the full DFA of a pattern with Unicode \b / \B runs over the value's bytes
+  // with a marker before every code point (kMarkWord / kMarkOther / kMarkNl:
+  // bytes that never occur in UTF-8) carrying that code point's word-ness, so
+  // the boundaries are decided between code points (dfa_is_match_marked)
+  bool marked = false;
   std::vector<uint8_t> classmap, classmap_up, accept;
   std::vector<uint16_t> trans;
 };
@@ -19,7 +24,12 @@ struct Dfa {
 // Unicode (<= 65535 states, read through L1/L2 for values with non-ASCII bytes).
 // 0 ok; -2 (FSG_E_INIT) syntax error; -103 (FSG_E_UNSUPPORTED) outside the supported subset
 int compile_regex(const std::string& pattern, Dfa& ascii, Dfa& full, std::string& msg);
+constexpr uint8_t kMarkWord = 0xFC, kMarkOther = 0xFD, kMarkNl = 0xFE;
 // host walk of the compiled DFA — used only by the compiler's unit tests
 bool dfa_is_match(const Dfa& d, const uint8_t* s, size_t n);
+// the marked walk over valid UTF-8 (isword: regex-syntax's Unicode \w)
+bool dfa_is_match_marked(const Dfa& d, const uint8_t* s, size_t n);
+// regex-syntax's Unicode \w as (lo, hi) pairs (the marked walk's table on the device)
+std::vector<uint32_t> unicode_word_ranges();
 
 }  // namespace fsg

@@ -771,6 +771,12 @@ int add_stage(fsg_chain* c, const ModuleSpec& m, const std::string& name, uint8_
     sd.dfa.f_classmap_up = put_blob(fd.classmap_up.data(), 256);
     sd.dfa.f_trans = put_blob(fd.trans.data(), fd.trans.size() * 2);
     sd.dfa.f_accept = put_blob(fd.accept.data(), fd.accept.size());
+    if (fd.marked) {  // Unicode word boundaries: the marked walk classifies each code point with \w
+      sd.dfa.f_marked = 1;
+      const std::vector<uint32_t> wt = unicode_word_ranges();
+      sd.dfa.wtab = put_blob(wt.data(), wt.size() * 4);
+      sd.dfa.wtab_n = (uint32_t)(wt.size() / 2);
+    }
     if (d.nstates <= 16) {  // the lean kernel's byte-row tables (fsg_device.h DfaDesc)
       std::vector<uint64_t> tt(256, 0), ttu(256, 0);
       for (uint32_t b = 0; b < 256; b++)

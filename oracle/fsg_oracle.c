@@ -608,7 +608,8 @@ typedef struct {
   size_t n, cap;
   cset *classes;
   size_t ncls, ccap;
-  int unicode_word; /* \b / \B used: Unicode word boundaries, exact only on ASCII input */
+  int unicode_word; /* \b / \B used */
+  int ascii_wb;     /* a (?-u) \b / \B among them: bytes inside a code point, exact only on ASCII input */
 } rxprog;
 
 /* AST */
@@ -631,7 +632,8 @@ typedef struct {
   int depth;
   int fi, fs;   /* inline flags i (case-insensitive), s (. matches \n); U only swaps greed */
   int fm, fx, fu; /* m: ^ $ at line boundaries; x: whitespace / # comments ignored; u: Unicode classes (on) */
-  int word;     /* \b or \B used: exact on ASCII input only */
+  int word;     /* \b or \B used */
+  int wba;      /* \b or \B under (?-u) */
 } rxparser;
 
 /* x: whitespace (White_Space) and # comments between tokens are skipped */
@@ -826,6 +828,7 @@ static int rx_escape(rxparser *P, uint32_t *single, cset *set, int in_class) {
         return 0;
       }
       P->word = 1;
+      if (!P->fu) P->wba = 1;
       return c == 'b' ? 3 : 4;
     case 'A': return in_class ? (P->err = 1, 0) : 5; /* start of text (= ^ without m) */
     case 'z': return in_class ? (P->err = 1, 0) : 6; /* end of text (= $ without m) */
@@ -1406,6 +1409,7 @@ static int rx_compile(const char *pat, rxprog *g) {
   P.fu = 1; /* Unicode mode is the default */
   anode *root = rx_parse_alt(&P);
   if (P.word) g->unicode_word = 1;
+  if (P.wba) g->ascii_wb = 1;
   int rc = 0;
   if (P.unsupported)
     rc = ORC_E_UNSUPPORTED;
@@ -1420,13 +1424,21 @@ static int rx_compile(const char *pat, rxprog *g) {
   return rc;
 }
 
-/* Pike VM.  returns 1 match, 0 no match, -1 unsupported (\w with non-ASCII) */
+/* Pike VM.  returns 1 match, 0 no match, -1 unsupported ((?-u) \b with non-ASCII) */
 typedef struct {
   int *dense, *sparse;
   int n;
 } sset;
+/* \b / \B on code points: regex-syntax's Unicode \w (fsg_u_word), which is
+ * [0-9A-Za-z_] on ASCII */
 static int rx_is_word(uint32_t c) {
-  return (c >= '0' && c <= '9') || (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || c == '_';
+  if (c < 0x80) return (c >= '0' && c <= '9') || (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || c == '_';
+  uint32_t a = 0, b = fsg_u_word_n;
+  while (a < b) {
+    uint32_t m = (a + b) / 2;
+    if (fsg_u_word[m].hi < c) a = m + 1; else b = m;
+  }
+  return a < fsg_u_word_n && fsg_u_word[a].lo <= c;
 }
 static void ss_add(const rxprog *g, sset *s, int pc, size_t pos, size_t n, int *match, int *stack,
                    const uint32_t *cp) {
@@ -1468,7 +1480,7 @@ static void ss_add(const rxprog *g, sset *s, int pc, size_t pos, size_t n, int *
   }
 }
 static int rx_run(const rxprog *g, const uint32_t *cp, size_t n) {
-  if (g->unicode_word)
+  if (g->unicode_word && g->ascii_wb)
     for (size_t i = 0; i < n; i++)
       if (cp[i] >= 0x80) return -1;
   int np = (int)g->n;

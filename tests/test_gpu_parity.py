@@ -558,16 +558,20 @@ def test_device_framing(engine):
             check_batch(engine, CHAINS["filter_init_timeout"], sl)
 
 
-def test_unicode_word_is_loud(engine):
-    """\\b on a non-ASCII value is outside the GPU subset: FSG_E_UNSUPPORTED when
-    (and only when) such a record is reached in stream order, like the oracle.
-    (\\w itself is the Unicode class, decided by the full byte DFA.)"""
+def test_unicode_word_boundaries(engine):
+    """\\b / \\B on non-ASCII values: Unicode word boundaries between code points
+    (the marked full DFA, a marker with each code point's \\w class before its
+    bytes), like the oracle's Pike VM; a (?-u) \\b stays outside the GPU subset:
+    FSG_E_UNSUPPORTED when (and only when) such a record is reached in stream order."""
     check_batch(engine, [("regex-filter", {"regex": r"\w+"}, None)], _one_record_slice("caf\u00e9".encode()))
-    chain = [("regex-filter", {"regex": r"\bx"}, None)]
-    check_batch(engine, chain, synth.make_slice(4, 500))
     b = P.Batch()
-    for v in ("abc", "caf\u00e9", "xyz"):
+    for v in ("abc", "caf\u00e9", "xyz", "x\u00e9", "\u00e9x", "\u03c9 x", "\u263a\u263ax", "na\u0301x"):
         b.add_record(P.Record.new(v))
+    for pat in (r"\bx", r"x\b", r"\Bx", r"\b\w+\b", r"(?i)\bCAF\u00c9\b", r"\b\u03c9\b"):
+        chain = [("regex-filter", {"regex": pat}, None)]
+        check_batch(engine, chain, synth.make_slice(4, 500))
+        check_batch(engine, chain, b.encode())
+    chain = [("regex-filter", {"regex": r"(?-u:\b)x"}, None)]
     with pytest.raises(Unsupported):
         gpu_chain(engine, chain).process_batch(b.encode())
     check_batch(engine, chain, b.encode())

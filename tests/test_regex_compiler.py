@@ -35,7 +35,9 @@ PATTERNS = [r"\d{3}-\d{2}-\d{4}", r"[A-Z]", r"^ab|cd$", r"a(b|c)*d", r"colou?r\s
             r"\p{Greek}+", r"\p{sc=Cyrillic}\w", r"\p{scx=Grek}", r"\p{Alphabetic}{2}", r"\p{Emoji}",
             r"\P{Greek}$", r"[\p{Greek}&&\p{Ll}]", r"\p{Script_Extensions=Arabic}", r"\p{Upper}\p{Lower}",
             r"\p{White_Space}", r"(?i)\p{Lu}", r"(?i)é", r"(?i)Σ", r"(?i)[α-γ]x?", r"(?i)ǆ", r"(?i)\P{Ll}",
-            r"(?i)[^σ]", r"(?i)ж+", r"(?i)[\p{Greek}--α]"]
+            r"(?i)[^σ]", r"(?i)ж+", r"(?i)[\p{Greek}--α]",
+            # Unicode word boundaries on non-ASCII text (the marked full DFA)
+            r"\bαβ", r"ω\b", r"\b\w+\b", r"é\B", r"\B☺", r"(?m)^\bЖ|ж\b$", r"(?i)\bσ\b", r"\b[α-ω]{2}\b"]
 WORD = ("\\b", "\\B")
 
 
@@ -54,7 +56,7 @@ def test_dfa_matches_oracle(pattern):
     word = any(w in pattern for w in WORD)
     for t in texts(rng):
         b = t.encode()
-        if word and not b.isascii():  # Unicode \b semantics: the kernel reports UNSUPPORTED
+        if word and not b.isascii() and "(?-u" in pattern:  # a (?-u) \b: UNSUPPORTED on non-ASCII values
             with pytest.raises(ValueError):
                 dfa_match(pattern, b)
             continue
@@ -193,5 +195,20 @@ def test_set_operations_against_python_regex(pattern):
     for _ in range(200):
         t = "".join(rng.choice("abcdefghmxyz0459AZ_-") for _ in range(rng.randint(0, 6)))
         want = regex.search("(?V1)" + pattern, t) is not None
+        assert dfa_match(pattern, t.encode())[0] == want, (pattern, t)
+        assert O.regex_is_match(pattern, t.encode()) == want, (pattern, t)
+
+
+@pytest.mark.parametrize("pattern", [r"\bαβ", r"ω\b", r"\b\w+\b", r"é\B", r"\B☺", r"\b[α-ω]{2}\b", r"\bx", r"x\b",
+                                     r"\b٣", r"\B\d"])
+def test_unicode_word_boundaries_against_python_regex(pattern):
+    """\\b / \\B between code points by Unicode \\w (the marked DFA, and the
+    oracle's Pike VM over code points), against Python's `regex` module."""
+    regex = pytest.importorskip("regex")
+    rng = random.Random(hash(pattern) & 0xFFFF)
+    alpha = "xaé ωαβ☺٣-_ж́.1"
+    for _ in range(300):
+        t = "".join(rng.choice(alpha) for _ in range(rng.randint(0, 7)))
+        want = regex.search(pattern, t) is not None
         assert dfa_match(pattern, t.encode())[0] == want, (pattern, t)
         assert O.regex_is_match(pattern, t.encode()) == want, (pattern, t)
