@@ -145,9 +145,6 @@ SIGNATURES = {
     "fsg_chain_group_process_slices": (ctypes.c_int, [PP, PP, SZ, ctypes.c_uint64, ctypes.POINTER(fsg_metrics),
                                                       ctypes.POINTER(ctypes.POINTER(fsg_batch_output)),
                                                       ctypes.POINTER(ctypes.c_int)]),
-    "fsg_keyed_allreduce_sim": (ctypes.c_int, [VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64),
-                                               PP, PP, ctypes.POINTER(ctypes.c_uint64), PP, ctypes.POINTER(SZ),
-                                               ctypes.POINTER(SZ)]),
 }
 
 FSG_DTYPE_I32, FSG_DTYPE_U32, FSG_DTYPE_I64, FSG_DTYPE_U64, FSG_DTYPE_F64 = range(5)
@@ -197,6 +194,27 @@ def debug_lib():
                                             ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         _debug = D
     return _debug
+
+
+_hooks = None
+
+
+def hooks_lib():
+    """The GPU test-hook library (libfsg_hooks.so, linked against libfsg.so):
+    the keyed merge over simulated ranks; never part of libfsg.so's C ABI."""
+    global _hooks
+    if _hooks is None:
+        lib()  # libfsg.so first (the hooks library resolves against it)
+        path = os.path.join(_HERE, "_lib", "libfsg_hooks.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"libfsg_hooks.so not built ({path}); run fluvio_amd._ffi.build()")
+        H = ctypes.CDLL(path)
+        H.fsg_keyed_allreduce_sim.restype = ctypes.c_int
+        H.fsg_keyed_allreduce_sim.argtypes = [VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64),
+                                               PP, PP, ctypes.POINTER(ctypes.c_uint64), PP, ctypes.POINTER(SZ),
+                                               ctypes.POINTER(SZ)]
+        _hooks = H
+    return _hooks
 
 
 def buf_ptr(data):

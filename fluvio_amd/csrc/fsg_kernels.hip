@@ -1339,7 +1339,7 @@ __device__ __forceinline__ void eval_batch(const EvalArgs& a, WaveLds& L, const 
 // k_eval: batches blockIdx.x (direct mode) or the deferred list written by
 // k_eval_lean (list mode: a.list[0] = count, a.list[1..] = batch indices)
 template <uint32_t kOps>
-__global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : (kOps == kOpsArray ? 3 : 2)) void k_eval(EvalArgs a) {
+__global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : 2) void k_eval(EvalArgs a) {
   __shared__ WaveLds L;
   const uint32_t n = a.list ? a.list[0] : a.nbatches;
   if constexpr (kOps == kOpsInt || kOps == kOpsAll) {  // batches of many small records: parallel framing
@@ -2633,44 +2633,61 @@ __global__ __launch_bounds__(256) void k_aggj_place(AggjArgs a) {
 // ---------------------------------------------------------------------------
 // 1. candidates: one workgroup per 64 KiB chunk, 16 coalesced 16-byte rounds;
 //    positions p with s[p + 16] == 2, kept in ascending order per chunk
+// every 16-byte unit's loads in flight before the first use (16 per thread),
+// the candidates of each round placed by wave scans and one exchange of the
+// wave totals (one barrier, not two per round)
+constexpr int kFrameRounds = kFrameChunk / (256 * 16);
 __global__ __launch_bounds__(256) void k_frame_cand(FrameArgs a) {
-  __shared__ uint64_t sh[4];
-  __shared__ uint32_t base;
-  const uint32_t t = threadIdx.x;
+  __shared__ uint32_t wt[kFrameRounds][4];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   const uint64_t c0 = (uint64_t)blockIdx.x * kFrameChunk;
-  if (t == 0) base = 0;
-  __syncthreads();
-  for (uint32_t i = 0; i < kFrameChunk / (256 * 16); i++) {
+  uint4 v[kFrameRounds];
+#pragma unroll
+  for (int i = 0; i < kFrameRounds; i++) {
+    const uint64_t u = c0 + ((uint64_t)i * 256 + t) * 16;
+    v[i] = u < a.len ? *(const uint4*)(a.s + u) : make_uint4(0, 0, 0, 0);  // the slice buffer is padded (kSlicePad)
+  }
+  uint32_t m[kFrameRounds], ex[kFrameRounds];
+#pragma unroll
+  for (int i = 0; i < kFrameRounds; i++) {
     const uint64_t u = c0 + ((uint64_t)i * 256 + t) * 16;  // the 16 bytes [u, u + 16) hold magic bytes of p = u - 16 + j
-    uint32_t m = 0;
+    uint32_t mm = 0;
     if (u < a.len) {
-      const uint4 v = *(const uint4*)(a.s + u);  // the slice buffer is padded (kSlicePad)
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
 #pragma unroll
       for (int d = 0; d < 4; d++) {
         const uint32_t z = zbytes(w[d] ^ 0x02020202u);
 #pragma unroll
         for (int k = 0; k < 4; k++)
-          if ((z >> (8 * k + 7)) & 1u) m |= 1u << (4 * d + k);
+          if ((z >> (8 * k + 7)) & 1u) mm |= 1u << (4 * d + k);
       }
       // magic byte at u + j: candidate p = u + j - 16 (>= 0, inside the slice)
       const uint32_t lo = u < 16 ? (uint32_t)(16 - u) : 0u;
       const uint64_t lim = a.len + 16 - u;  // p < len
-      m &= (0xFFFFu << lo) & 0xFFFFu;
-      if (lim < 16) m &= (1u << lim) - 1u;
+      mm &= (0xFFFFu << lo) & 0xFFFFu;
+      if (lim < 16) mm &= (1u << lim) - 1u;
     }
-    uint64_t tot;
-    const uint32_t ex = (uint32_t)block_excl_u64((uint64_t)__builtin_popcount(m), sh, tot);
-    uint32_t k = base + ex;
-    while (m) {
-      const uint32_t j = (uint32_t)__builtin_ctz(m);
-      m &= m - 1;
+    m[i] = mm;
+    const uint32_t c = (uint32_t)__builtin_popcount(mm);
+    const uint32_t inc = wave_incl_scan(c);
+    ex[i] = inc - c;
+    if (lane == 63) wt[i][wv] = inc;
+  }
+  __syncthreads();
+  uint32_t base = 0;
+#pragma unroll
+  for (int i = 0; i < kFrameRounds; i++) {
+    uint32_t k = base + ex[i];
+    for (uint32_t w2 = 0; w2 < wv; w2++) k += wt[i][w2];
+    base += wt[i][0] + wt[i][1] + wt[i][2] + wt[i][3];
+    const uint64_t u = c0 + ((uint64_t)i * 256 + t) * 16;
+    uint32_t mm = m[i];
+    while (mm) {
+      const uint32_t j = (uint32_t)__builtin_ctz(mm);
+      mm &= mm - 1;
       if (k < kFrameCap) a.cbuf[(uint64_t)blockIdx.x * kFrameCap + k] = (uint16_t)(u + j - 16 - c0 + 16);
       k++;
     }
-    __syncthreads();
-    if (t == 0) base += (uint32_t)tot;
-    __syncthreads();
   }
   if (t == 0) {
     a.ccnt[blockIdx.x] = base < kFrameCap ? base : kFrameCap;

@@ -3752,16 +3752,20 @@ extern "C" int fsg_keyed_allreduce(fsg_keyed* k, size_t* n_keys, size_t* key_byt
   return kd_allreduce(k, e->comm ? e->nranks : 1, e->comm ? e->rank : 0, nullptr, n_keys, key_bytes);
 }
 
-extern "C" int fsg_keyed_allreduce_sim(fsg_keyed* k, uint32_t nranks, uint32_t me, const uint64_t* rank_n,
-                                       const uint64_t* const* rank_desc, const uint8_t* const* rank_arena,
-                                       const uint64_t* rank_arena_len, const uint32_t* const* rank_vals,
-                                       size_t* n_keys, size_t* key_bytes) {
+// the merge over simulated gathered lists (C++ linkage, not part of the C ABI:
+// its C entry lives in the test-hook library libfsg_hooks.so, fsg_hooks.cpp)
+namespace fsg {
+int keyed_allreduce_sim(fsg_keyed* k, uint32_t nranks, uint32_t me, const uint64_t* rank_n,
+                        const uint64_t* const* rank_desc, const uint8_t* const* rank_arena,
+                        const uint64_t* rank_arena_len, const uint32_t* const* rank_vals, size_t* n_keys,
+                        size_t* key_bytes) {
   if (!nranks || me >= nranks || nranks > 1024 || !rank_n || !rank_desc || !rank_arena || !rank_arena_len ||
       !rank_vals)
     return fail(FSG_E_INVALID_ARG, "fsg_keyed_allreduce_sim: bad rank arguments");
   const KdSim sim{rank_n, rank_desc, rank_arena, rank_arena_len, rank_vals};
   return kd_allreduce(k, (int)nranks, (int)me, &sim, n_keys, key_bytes);
 }
+}  // namespace fsg
 
 extern "C" int fsg_keyed_read(fsg_keyed* k, uint8_t* keys, size_t key_bytes, uint64_t* offs, uint32_t* vals,
                               size_t n) {

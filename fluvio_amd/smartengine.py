@@ -444,7 +444,7 @@ class KeyedState:
             dptr[r], aptr[r], vptr[r] = ctypes.cast(d, ctypes.c_void_p), ctypes.cast(a, ctypes.c_void_p), \
                 ctypes.cast(v, ctypes.c_void_p)
         nk, b = ctypes.c_size_t(), ctypes.c_size_t()
-        _check(_ffi.lib().fsg_keyed_allreduce_sim(self._h, nr, me, n, dptr, aptr, alen, vptr, ctypes.byref(nk),
+        _check(_ffi.hooks_lib().fsg_keyed_allreduce_sim(self._h, nr, me, n, dptr, aptr, alen, vptr, ctypes.byref(nk),
                                                   ctypes.byref(b)))
         self.n_keys, self.key_bytes = nk.value, b.value
         return nk.value

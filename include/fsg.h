@@ -316,16 +316,8 @@ int fsg_keyed_allreduce(fsg_keyed *k, size_t *n_keys, size_t *key_bytes);
 int fsg_keyed_read(fsg_keyed *k, uint8_t *keys, size_t key_bytes, uint64_t *offs, uint32_t *vals, size_t n);
 int fsg_keyed_device(fsg_keyed *k, const uint8_t **keys, const uint64_t **offs, const uint32_t **vals);
 void fsg_keyed_free(fsg_keyed *k);
-/* Test hook: fsg_keyed_allreduce as rank `me` of `nranks` on one device, the
- * other ranks' all-gathered inputs supplied by the caller: rank r's rank_n[r]
- * key descriptors (arena offset | length << 40; length 0xFFFFFF = no key),
- * its arena (rank_arena_len[r] bytes) and values.  The same union, id and
- * placement kernels run over them; the all-reduce becomes the sum of every
- * rank's dense scatter.  Entry `me` of the arrays is ignored (the local table). */
-int fsg_keyed_allreduce_sim(fsg_keyed *k, uint32_t nranks, uint32_t me, const uint64_t *rank_n,
-                            const uint64_t *const *rank_desc, const uint8_t *const *rank_arena,
-                            const uint64_t *rank_arena_len, const uint32_t *const *rank_vals, size_t *n_keys,
-                            size_t *key_bytes);
+/* (The merge over simulated ranks, fsg_keyed_allreduce_sim, is a GPU test hook
+ * in libfsg_hooks.so, outside this ABI.) */
 
 #ifdef __cplusplus
 }

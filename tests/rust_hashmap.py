@@ -4,7 +4,9 @@ smartmodule/examples/aggregate-json/src/lib.rs:22-36 deserializes the
 accumulator and the record into `HashMap<String, u32>` (std), adds the record's
 map into the accumulator's with the entry API and writes `to_vec_pretty` of
 the accumulator's map: the output keys come in the map's iteration order.  The
-module is built with Rust 1.75 (smartmodule/examples/rust-toolchain) for
+module is built with Rust 1.75 (the repository root's rust-toolchain.toml; a
+guest built from smartmodule/cargo_template, which pins `stable`, may carry a
+newer hashbrown whose order differs: a known limit) for
 wasm32-unknown-unknown, where that order is deterministic:
 
 * `RandomState::new()` (std/src/hash/random.rs) takes its keys from a
