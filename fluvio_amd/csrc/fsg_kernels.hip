@@ -3141,79 +3141,62 @@ __device__ __forceinline__ void write_batch_wave(const WriteArgs& a, const KeptR
   }
 }
 
-__global__ __launch_bounds__(kWlThreads) void k_write_lean(WriteArgs a) {
-  __shared__ WlLds L;
-  const int32_t b = a.first + (int32_t)blockIdx.x;
-  if (a.first < 0 || b > a.last) return;
-  const uint32_t t = threadIdx.x, lane = t & 63u;
-  const BatchStat st = a.bstat[b];
-  const int64_t rel = a.seg ? 0 : a.bstat[a.first].base_offset - st.base_offset;
-  const KeptRec* d = a.desc + a.rbase[b];
-  const uint64_t obase = a.seg ? 61ull * (uint64_t)(b + 1) + a.pre[b].rec_bytes
-                               : 61 + (a.pre[b].rec_bytes - a.pre[a.first].rec_bytes);
-  const uint32_t d0 = (uint32_t)(obase & 15);
-  const uint32_t nk = st.nkeep;
-  // 1. headers and segments
-  if (t < 64) {
-    const bool v = lane < nk && nk <= 64;
-    KeptRec r = {};
-    uint32_t sz = 0;
-    if (v) {
-      r = d[lane];
-      sz = rec_out_size(r, rel, 0, 0);
+// phase 1 on wave 0 (lane = record, `r` its descriptor when v): sizes, the
+// varint fields into the staging buffer, the segment table, L.total / nunits / big
+__device__ __forceinline__ void wl_phase1(WlLds& L, const KeptRec& r, bool v, int64_t rel, uint32_t d0, uint32_t nk) {
+  const uint32_t lane = lane_id();
+  uint32_t sz = 0;
+  if (v) sz = rec_out_size(r, rel, 0, 0);
+  const uint32_t incl = wave_incl_scan(sz);
+  const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+  const bool big = nk > 64 || d0 + total > (uint32_t)kObuf;
+  uint32_t uk = 0, uv = 0;
+  if (v && !big) {
+    const uint32_t off = d0 + incl - sz;
+    uint8_t* q = L.ob + off;
+    const uint32_t vl = r.vlen;
+    const uint32_t inner = 1 + vsize(r.ts) + vsize(r.od + rel) + 1 +
+                           (r.has_key ? vsize((int64_t)r.klen) + r.klen : 0) + vsize((int64_t)vl) + vl + vsize(r.hdr);
+    uint32_t w = venc((int64_t)inner, q);  // varints straight into the staging buffer
+    q[w++] = r.attr;
+    w += venc(r.ts, q + w);
+    w += venc(r.od + rel, q + w);
+    q[w++] = r.has_key ? 1 : 0;
+    uint32_t kdst = off + w;
+    if (r.has_key) {
+      w += venc((int64_t)r.klen, q + w);
+      kdst = off + w;
+      w += r.klen;
     }
-    const uint32_t incl = wave_incl_scan(sz);
-    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-    const bool big = nk > 64 || d0 + total > (uint32_t)kObuf;
-    uint32_t uk = 0, uv = 0;
-    if (v && !big) {
-      const uint32_t off = d0 + incl - sz;
-      uint8_t* q = L.ob + off;
-      const uint32_t vl = r.vlen;
-      const uint32_t inner = 1 + vsize(r.ts) + vsize(r.od + rel) + 1 +
-                             (r.has_key ? vsize((int64_t)r.klen) + r.klen : 0) + vsize((int64_t)vl) + vl + vsize(r.hdr);
-      uint32_t w = venc((int64_t)inner, q);  // varints straight into the staging buffer
-      q[w++] = r.attr;
-      w += venc(r.ts, q + w);
-      w += venc(r.od + rel, q + w);
-      q[w++] = r.has_key ? 1 : 0;
-      uint32_t kdst = off + w;
-      if (r.has_key) {
-        w += venc((int64_t)r.klen, q + w);
-        kdst = off + w;
-        w += r.klen;
-      }
-      w += venc((int64_t)vl, q + w);
-      const uint32_t vdst = off + w;
-      w += vl;
-      w += venc(r.hdr, q + w);
-      const uint32_t kl = r.has_key ? r.klen : 0u;
-      L.s_src[2 * lane] = r.kpos;
-      L.s_dst[2 * lane] = kdst;
-      L.s_len[2 * lane] = kl;
-      L.s_src[2 * lane + 1] = r.vpos;
-      L.s_dst[2 * lane + 1] = vdst;
-      L.s_len[2 * lane + 1] = vl | (r.mode == KM_UPPER ? 0x80000000u : 0u);
-      uk = kl ? ((kdst + kl + 15) >> 4) - (kdst >> 4) : 0u;
-      uv = vl ? ((vdst + vl + 15) >> 4) - (vdst >> 4) : 0u;
-    }
-    const uint32_t ui = wave_incl_scan(uk + uv);
-    if (v && !big) {
-      L.s_upre[2 * lane] = ui - uk - uv;
-      L.s_upre[2 * lane + 1] = ui - uv;
-    }
-    if (lane == 0) {
-      L.total = total;
-      L.nunits = __builtin_amdgcn_readlane(ui, 63);
-      L.big = big ? 1u : 0u;
-    }
-    if (lane == 0 && !big) L.s_upre[2 * (nk < 64 ? nk : 64)] = __builtin_amdgcn_readlane(ui, 63);
+    w += venc((int64_t)vl, q + w);
+    const uint32_t vdst = off + w;
+    w += vl;
+    w += venc(r.hdr, q + w);
+    const uint32_t kl = r.has_key ? r.klen : 0u;
+    L.s_src[2 * lane] = r.kpos;
+    L.s_dst[2 * lane] = kdst;
+    L.s_len[2 * lane] = kl;
+    L.s_src[2 * lane + 1] = r.vpos;
+    L.s_dst[2 * lane + 1] = vdst;
+    L.s_len[2 * lane + 1] = vl | (r.mode == KM_UPPER ? 0x80000000u : 0u);
+    uk = kl ? ((kdst + kl + 15) >> 4) - (kdst >> 4) : 0u;
+    uv = vl ? ((vdst + vl + 15) >> 4) - (vdst >> 4) : 0u;
   }
-  __syncthreads();
-  if (L.big) {  // generic path for this batch
-    if (t < 64) write_batch_wave(a, d, nk, rel, obase);
-    return;
+  const uint32_t ui = wave_incl_scan(uk + uv);
+  if (v && !big) {
+    L.s_upre[2 * lane] = ui - uk - uv;
+    L.s_upre[2 * lane + 1] = ui - uv;
   }
+  if (lane == 0) {
+    L.total = total;
+    L.nunits = __builtin_amdgcn_readlane(ui, 63);
+    L.big = big ? 1u : 0u;
+  }
+  if (lane == 0 && !big) L.s_upre[2 * (nk < 64 ? nk : 64)] = __builtin_amdgcn_readlane(ui, 63);
+}
+// phases 2 and 3 on every thread (after phase 1 and a barrier; L.big clear)
+__device__ __forceinline__ void wl_phase23(const WriteArgs& a, WlLds& L, uint64_t obase, uint32_t d0, uint32_t nk) {
+  const uint32_t t = threadIdx.x;
   const uint32_t total = L.total, nunits = L.nunits, nseg = 2 * nk;
   // 2. segments -> staging, thread t copies the contiguous units [u0, u1)
   {
@@ -3292,6 +3275,33 @@ __global__ __launch_bounds__(kWlThreads) void k_write_lean(WriteArgs a) {
     }
   }
 }
+
+__global__ __launch_bounds__(kWlThreads) void k_write_lean(WriteArgs a) {
+  __shared__ WlLds L;
+  const int32_t b = a.first + (int32_t)blockIdx.x;
+  if (a.first < 0 || b > a.last) return;
+  const uint32_t t = threadIdx.x, lane = t & 63u;
+  const BatchStat st = a.bstat[b];
+  const int64_t rel = a.seg ? 0 : a.bstat[a.first].base_offset - st.base_offset;
+  const KeptRec* d = a.desc + a.rbase[b];
+  const uint64_t obase = a.seg ? 61ull * (uint64_t)(b + 1) + a.pre[b].rec_bytes
+                               : 61 + (a.pre[b].rec_bytes - a.pre[a.first].rec_bytes);
+  const uint32_t d0 = (uint32_t)(obase & 15);
+  const uint32_t nk = st.nkeep;
+  if (t < 64) {  // 1. headers and segments
+    const bool v = lane < nk && nk <= 64;
+    KeptRec r = {};
+    if (v) r = d[lane];
+    wl_phase1(L, r, v, rel, d0, nk);
+  }
+  __syncthreads();
+  if (L.big) {  // generic path for this batch
+    if (t < 64) write_batch_wave(a, d, nk, rel, obase);
+    return;
+  }
+  wl_phase23(a, L, obase, d0, nk);
+}
+
 
 // ---------------------------------------------------------------------------
 // stateful last stages (k_sf_*): filter_look_back (examples/filter_look_back:
@@ -3846,6 +3856,9 @@ void launch_write(const WriteArgs& a, uint32_t nblocks, hipStream_t s) {
                                   dim3(kWriteThreads), 0, s, a);
 }
 void launch_write_lean(const WriteArgs& a, uint32_t nblocks, hipStream_t s) {
+  // one workgroup per batch: a persistent variant that loads batch i + grid's
+  // rows and descriptors while batch i is written measured slower on MI355X
+  // (C2 write 1.37 -> 1.99 ms), as did round 4's LDS-DMA prefetching one
   if (nblocks) hipLaunchKernelGGL(k_write_lean, dim3(nblocks), dim3(kWlThreads), 0, s, a);
 }
 // CRC32C of out[off, off + n) into out[17..21); `acc` is one u32 of scratch
