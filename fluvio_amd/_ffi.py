@@ -118,6 +118,7 @@ SIGNATURES = {
     "fsg_slice_free": (None, [VP]),
     "fsg_slice_device_framed": (ctypes.c_int, [VP]),
     "fsg_slice_reframe": (ctypes.c_int, [VP]),
+    "fsg_slice_verify_crc_start": (ctypes.c_int, [VP]),
     "fsg_slice_verify_crc": (ctypes.c_int, [VP, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int64),
                                             ctypes.POINTER(ctypes.c_float)]),
     "fsg_chain_process_slice": (ctypes.c_int, [VP, VP, ctypes.c_uint64, ctypes.POINTER(fsg_metrics),

@@ -484,7 +484,17 @@ struct fsg_slice {
   mutable DevBuf vbad;
   mutable hipStream_t vst = nullptr;
   mutable hipEvent_t vev[2] = {};
+  // fsg_slice_verify_crc_start: a verify in flight on vst (its result lands in
+  // the pinned words vres); anything that rewrites the batch table or the
+  // bytes waits for it first (verify_drain)
+  mutable unsigned long long* vres = nullptr;
+  mutable bool v_pending = false;
+  void verify_drain() const {
+    if (v_pending) (void)hipStreamSynchronize(vst);
+  }
   ~fsg_slice() {
+    verify_drain();
+    if (vres) (void)hipHostFree(vres);
     if (rs_ev) (void)hipEventDestroy(rs_ev);
     for (auto& e : vev)
       if (e) (void)hipEventDestroy(e);
@@ -1053,6 +1063,7 @@ int frame(const uint8_t* s, size_t len, std::vector<uint64_t>& bpos, std::vector
 int frame_on_device(fsg_slice* sl, hipStream_t st, int* fallback) {
   const uint64_t len = sl->len;
   *fallback = 0;
+  sl->verify_drain();
   sl->rs_ok = false;
   sl->nb = 0;
   sl->nrec = 0;
@@ -1285,6 +1296,8 @@ size_t slice_alloc(size_t len) { return ((len + 15) & ~(size_t)15) + kSlicePad +
 // padded: `s` already holds slice_alloc(len) bytes, zeros behind the slice
 int upload_slice(fsg_engine* e, const uint8_t* s, size_t len, fsg_slice* sl, hipStream_t stream,
                  bool device_frame = true, bool sync = true, bool padded = false) {
+  sl->verify_drain();
+  sl->v_pending = false;  // the verified bytes are being replaced
   sl->eng = e;
   sl->len = len;
   sl->rs_ok = false;
@@ -1364,6 +1377,29 @@ extern "C" int fsg_slice_reframe(fsg_slice* s) {
 }
 // CRC32C of every framed batch against its header (report only: the reference
 // never verifies, protocol record/batch.rs:398-430, so nothing else changes)
+// Started on the slice's own stream, so a fetch can verify while the chain
+// processes the same batches (both only read the stored bytes); the result is
+// collected by fsg_slice_verify_crc.
+extern "C" int fsg_slice_verify_crc_start(const fsg_slice* s) {
+  if (s->decompressed) return FSG_OK;  // checked on the stored bytes at ingest
+  HIPCHK(hipSetDevice(s->eng->device));
+  s->verify_drain();
+  if (!s->vst) HIPCHK(hipStreamCreateWithFlags(&s->vst, hipStreamNonBlocking));
+  for (auto& e : s->vev)
+    if (!e) HIPCHK(hipEventCreate(&e));
+  if (!s->vres) HIPCHK(hipHostMalloc((void**)&s->vres, 16, hipHostMallocDefault));
+  hipStream_t st = s->vst;
+  HIPCHK(s->vbad.ensure(16));
+  HIPCHK(hipMemsetAsync(s->vbad.p, 0, 8, st));  // [0] mismatches, [1] first mismatching batch (min)
+  HIPCHK(hipMemsetAsync((uint8_t*)s->vbad.p + 8, 0xFF, 8, st));
+  HIPCHK(hipEventRecord(s->vev[0], st));
+  launch_verify_crc((const uint8_t*)s->data.p, s->bpos.as<uint64_t>(), s->nb, s->vbad.as<unsigned long long>(), nullptr, st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(s->vev[1], st));
+  HIPCHK(hipMemcpyAsync(s->vres, s->vbad.p, 16, hipMemcpyDeviceToHost, st));
+  s->v_pending = true;
+  return FSG_OK;
+}
 extern "C" int fsg_slice_verify_crc(const fsg_slice* s, uint64_t* n_bad, int64_t* first_bad, float* ms) {
   if (s->decompressed) {  // checked on the stored bytes at ingest, before decompression
     if (n_bad) *n_bad = s->crc_bad;
@@ -1371,25 +1407,17 @@ extern "C" int fsg_slice_verify_crc(const fsg_slice* s, uint64_t* n_bad, int64_t
     if (ms) *ms = s->crc_ms;
     return FSG_OK;
   }
+  if (!s->v_pending) {
+    int rc = fsg_slice_verify_crc_start(s);
+    if (rc) return rc;
+  }
   HIPCHK(hipSetDevice(s->eng->device));
-  if (!s->vst) HIPCHK(hipStreamCreateWithFlags(&s->vst, hipStreamNonBlocking));
-  for (auto& e : s->vev)
-    if (!e) HIPCHK(hipEventCreate(&e));
-  hipStream_t st = s->vst;
-  HIPCHK(s->vbad.ensure(16));
-  unsigned long long r[2] = {0, 0};
-  HIPCHK(hipMemsetAsync(s->vbad.p, 0, 8, st));  // [0] mismatches, [1] first mismatching batch (min)
-  HIPCHK(hipMemsetAsync((uint8_t*)s->vbad.p + 8, 0xFF, 8, st));
-  HIPCHK(hipEventRecord(s->vev[0], st));
-  launch_verify_crc((const uint8_t*)s->data.p, s->bpos.as<uint64_t>(), s->nb, s->vbad.as<unsigned long long>(), nullptr, st);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(s->vev[1], st));
-  HIPCHK(hipMemcpyAsync(r, s->vbad.p, 16, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  HIPCHK(hipStreamSynchronize(s->vst));
+  s->v_pending = false;
   float t = 0;
   HIPCHK(hipEventElapsedTime(&t, s->vev[0], s->vev[1]));
-  if (n_bad) *n_bad = r[0];
-  if (first_bad) *first_bad = r[0] ? (int64_t)r[1] : -1;
+  if (n_bad) *n_bad = s->vres[0];
+  if (first_bad) *first_bad = s->vres[0] ? (int64_t)s->vres[1] : -1;
   if (ms) *ms = t;
   return FSG_OK;
 }

@@ -650,6 +650,11 @@ class ResidentSlice:
         slice (the fetch-shaped measurement: framing + verify + process)."""
         _check(_ffi.lib().fsg_slice_reframe(self._h))
 
+    def verify_crc_start(self):
+        """Start the CRC32C check on the slice's own stream and return at
+        once; the next verify_crc() returns its result."""
+        _check(_ffi.lib().fsg_slice_verify_crc_start(self._h))
+
     def verify_crc(self):
         """CRC32C of every stored batch checked on the GPU (report only: the
         reference never verifies).  Returns (mismatches, first bad batch or -1,

@@ -248,6 +248,11 @@ int fsg_slice_reframe(fsg_slice *s);
  * For a slice with compressed batches the check runs on the stored bytes at
  * ingest (before decompression) and this returns that result. */
 int fsg_slice_verify_crc(const fsg_slice *s, uint64_t *n_bad, int64_t *first_bad, float *ms);
+/* Starts the same check on the slice's own stream and returns at once, so a
+ * fetch verifies while fsg_chain_process_slice runs on the same (read-only)
+ * bytes; the next fsg_slice_verify_crc returns its result.  Reframing or
+ * re-uploading the slice waits for it first. */
+int fsg_slice_verify_crc_start(const fsg_slice *s);
 void fsg_slice_free(fsg_slice *s);
 /* process_batch over a resident slice; the output batch stays in HBM until
  * fsg_chain_download_output (out may be NULL to keep it resident). */

@@ -1375,6 +1375,12 @@ def test_verify_crc_on_ingest(engine):
         rs2 = ResidentSlice(engine, bytes(corrupt))
         bad, first, _ms = rs2.verify_crc()
         assert (bad, first) == (len(picks), picks[0]), kind
+        # started on the slice's stream, processed beside it, collected after
+        modules = [("filter_init", {"key": "timeout"}, None)]
+        rs2.verify_crc_start()
+        out = gpu_chain(engine, modules).process_slice(rs2).raw
+        assert rs2.verify_crc()[:2] == (len(picks), picks[0]), kind
+        assert out == orc_chain(modules).process_batch(bytes(corrupt))["bytes"], kind
     # the reference never checks: a corrupted CRC field does not change process_batch
     sl = synth.make_slice(2, 2000)
     c = bytearray(sl)
@@ -1399,10 +1405,18 @@ def test_reframe_resident_slice(engine):
     nb, nr = rs.n_batches, rs.n_records
     g = gpu_chain(engine, CHAINS["filter_init_timeout"])
     ref = orc_chain(CHAINS["filter_init_timeout"]).process_batch(sl)["bytes"]
-    for _ in range(3):
+    for i in range(4):
         rs.reframe()
-        assert rs.verify_crc()[:2] == (0, -1)
-        assert g.process_slice(rs).raw == ref
+        if i % 2:  # the bench's fetch step: the verify beside process_batch
+            rs.verify_crc_start()
+            assert g.process_slice(rs).raw == ref
+            assert rs.verify_crc()[:2] == (0, -1)
+        else:
+            assert rs.verify_crc()[:2] == (0, -1)
+            assert g.process_slice(rs).raw == ref
+    rs.verify_crc_start()
+    rs.reframe()  # waits for the verify in flight; its result stays collectable
+    assert rs.verify_crc()[:2] == (0, -1)
     assert (rs.n_batches, rs.n_records) == (nb, nr)
 
 
