@@ -4097,7 +4097,9 @@ void launch_verify_crc(const uint8_t* slice, const uint64_t* bpos, uint32_t nb, 
   int dev = 0, cus = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const uint32_t g = std::min<uint32_t>((nb + 3) / 4, (uint32_t)std::max(1, cus) * 8u);
+  // about 64 batches per workgroup (at least 8 workgroups per CU): blocks
+  // retire while a concurrent process_batch waits for slots
+  const uint32_t g = std::min<uint32_t>((nb + 3) / 4, std::max((uint32_t)std::max(1, cus) * 8u, (nb + 63) / 64));
   hipLaunchKernelGGL(k_verify_crc, dim3(g), dim3(256), 0, s, slice, bpos, nb, bad, flags);
 }
 void launch_decompress(const DecArgs& a, int pass, hipStream_t s) {

@@ -1384,7 +1384,11 @@ extern "C" int fsg_slice_verify_crc_start(const fsg_slice* s) {
   if (s->decompressed) return FSG_OK;  // checked on the stored bytes at ingest
   HIPCHK(hipSetDevice(s->eng->device));
   s->verify_drain();
-  if (!s->vst) HIPCHK(hipStreamCreateWithFlags(&s->vst, hipStreamNonBlocking));
+  if (!s->vst) {  // the lowest priority: process_batch's workgroups go first as verify blocks retire
+    int lo = 0, hi = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIPCHK(hipStreamCreateWithPriority(&s->vst, hipStreamNonBlocking, lo));
+  }
   for (auto& e : s->vev)
     if (!e) HIPCHK(hipEventCreate(&e));
   if (!s->vres) HIPCHK(hipHostMalloc((void**)&s->vres, 16, hipHostMallocDefault));

@@ -1396,6 +1396,49 @@ def test_verify_crc_large_batches(engine):
     assert rs.verify_crc()[:2] == (0, -1)
 
 
+def test_verify_blocks_every_shape(engine):
+    """k_verify_crc over batches of every size class (a few units, a few
+    KiB, beyond one wave's 1 KiB round) at every alignment, with corruptions
+    in the first and last units, the middle and the stored CRC; the count
+    and first bad batch match the CPU check, also when started beside
+    process_batch after a reframe."""
+    rnd = random.Random(11)
+    sizes = [rnd.randint(1, 6) for _ in range(300)] + [rnd.randint(20, 200) for _ in range(60)] + \
+        [rnd.randint(1500, 4000) for _ in range(8)] + [9000]
+    rnd.shuffle(sizes)
+    raw, starts, base = b"", [], 0
+    for n in sizes:
+        recs = []
+        for i in range(n):
+            r = P.Record.new_key_value(None, bytes(rnd.choice(b"abcdefgh") for _ in range(rnd.randint(2, 90))))
+            r.preamble.offset_delta = i
+            recs.append(r.encode())
+        starts.append(len(raw))
+        raw += _raw_batch(base, recs)
+        base += n
+    rs = ResidentSlice(engine, raw)
+    assert rs.n_batches == len(sizes) and rs.device_framed
+    assert rs.verify_crc()[:2] == (0, -1)
+    c = bytearray(raw)
+    picks = sorted(rnd.sample(range(len(sizes)), 40))
+    for bi in picks:
+        p0 = starts[bi]
+        end = p0 + 12 + struct.unpack(">i", raw[p0 + 8:p0 + 12])[0]
+        # (header bytes the framing reads stay intact: batch length, magic, attributes, record count)
+        off = rnd.choice([p0 + 17 + rnd.randint(0, 3), p0 + 27 + rnd.randint(0, 29), max(p0 + 61, end - 1 - rnd.randint(0, 40)),
+                          rnd.randint(p0 + 61, end - 1)])
+        c[off] ^= 1 << rnd.randint(0, 7)
+    want = sum(1 for i, p0 in enumerate(starts)
+               if O.crc32c(bytes(c[p0 + 21:p0 + 12 + struct.unpack(">i", raw[p0 + 8:p0 + 12])[0]]))
+               != struct.unpack(">I", bytes(c[p0 + 17:p0 + 21]))[0])
+    assert want == len(picks)
+    rs2 = ResidentSlice(engine, bytes(c))
+    assert rs2.verify_crc()[:2] == (len(picks), picks[0])
+    rs2.reframe()
+    rs2.verify_crc_start()
+    assert rs2.verify_crc()[:2] == (len(picks), picks[0])
+
+
 def test_reframe_resident_slice(engine):
     """fsg_slice_reframe (the fetch-shaped step): the HBM-resident bytes framed
     again on the device give the same batches, CRC verdicts and process_batch
