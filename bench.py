@@ -26,6 +26,7 @@ merged over RCCL each step.  Rank 0 prints ONE JSON line.
 """
 import argparse
 import ctypes
+import gc
 import hashlib
 import json
 import os
@@ -751,6 +752,9 @@ def main():
     line = dict(run_workload(ctx, head, a.records, cpu))
     workloads = {}
     for w in extra:
+        # the previous workload's engines, slices and streams go before the next
+        # one is timed (their buffers and streams otherwise stay until exit)
+        gc.collect()
         workloads[w] = run_workload(ctx, w, 0, cpu)
     if ctx.rank == 0:
         out = {
