@@ -1423,4 +1423,42 @@ bool dfa_is_match(const Dfa& d, const uint8_t* s, size_t n) {
   return (d.accept[st] & 2) != 0;
 }
 
+bool rust_str_debug(const std::string& raw, std::string& out) {
+  out += '"';
+  for (size_t i = 0; i < raw.size();) {
+    const uint8_t c = (uint8_t)raw[i];
+    uint32_t cp = c;
+    size_t len = 1;
+    if (c >= 0x80) {
+      len = c >= 0xF0 ? 4 : c >= 0xE0 ? 3 : 2;
+      if (c < 0xC2 || c > 0xF4 || i + len > raw.size()) return false;
+      cp = c & (0x7Fu >> len);
+      for (size_t k = 1; k < len; k++) {
+        const uint8_t t = (uint8_t)raw[i + k];
+        if ((t & 0xC0) != 0x80) return false;
+        cp = (cp << 6) | (t & 0x3Fu);
+      }
+    }
+    switch (cp) {
+      case '"': out += "\\\""; break;
+      case '\\': out += "\\\\"; break;
+      case '\n': out += "\\n"; break;
+      case '\r': out += "\\r"; break;
+      case '\t': out += "\\t"; break;
+      case 0: out += "\\0"; break;
+      default:
+        if (fsg_u_dbg_escaped(cp)) {
+          char u[16];
+          snprintf(u, sizeof u, "\\u{%x}", cp);
+          out += u;
+        } else {
+          out.append(raw, i, len);
+        }
+    }
+    i += len;
+  }
+  out += '"';
+  return true;
+}
+
 }  // namespace fsg

@@ -31,5 +31,10 @@ bool dfa_is_match(const Dfa& d, const uint8_t* s, size_t n);
 bool dfa_is_match_marked(const Dfa& d, const uint8_t* s, size_t n);
 // regex-syntax's Unicode \w as (lo, hi) pairs (the marked walk's table on the device)
 std::vector<uint32_t> unicode_word_ranges();
+// <str as Debug>::fmt of Rust 1.75 (serde's "invalid type: string \"..\""):
+// \0 \t \r \n \\ \" escaped, Grapheme_Extend and non-printable chars as
+// \u{hex} (this image's Unicode 13 categories; parity unpinned for code points
+// assigned later); false when `raw` is not UTF-8
+bool rust_str_debug(const std::string& raw, std::string& out);
 
 }  // namespace fsg

@@ -1543,18 +1543,8 @@ bool json_hint(uint32_t code_word, uint32_t pos, uint32_t a, uint32_t b, const s
       case JU_STR: {
         std::string raw;
         json_unescape(v, a, b, raw);
-        un = "string \"";
-        for (unsigned char c : raw) {  // Rust str Debug, printable-ASCII subset
-          if (c == '"') un += "\\\"";
-          else if (c == '\\') un += "\\\\";
-          else if (c == '\n') un += "\\n";
-          else if (c == '\r') un += "\\r";
-          else if (c == '\t') un += "\\t";
-          else if (c == 0) un += "\\0";
-          else if (c >= 0x20 && c < 0x7f) un += (char)c;
-          else return false;
-        }
-        un += "\"";
+        un = "string ";
+        if (!rust_str_debug(raw, un)) return false;
         break;
       }
       case JU_SEQ: un = "sequence"; break;

@@ -27,9 +27,10 @@
  * Floats: serde_json's f64 reading (f64_from_parts, no float_roundtrip) and
  * Rust's shortest Display behind serde's WithDecimalPoint for "invalid type:
  * floating point `..`"; ryu's format for Value::to_string.
+ * "invalid type: string ..." renders the string with Rust's str Debug
+ * (str_debug: Unicode escapes from this image's Unicode 13 categories and
+ * Grapheme_Extend, parity unpinned for code points assigned later).
  * Outside the restatement (status ORC_E_UNSUPPORTED, mirrored by the GPU path):
- * "invalid type: string ..." for a
- * string holding a byte outside printable ASCII (Rust's str Debug escaping),
  * an ignored value nested more than 64 levels below its first bracket, and an
  * error text holding a NUL byte.
  */
@@ -718,24 +719,47 @@ static void orc_display_point(double v, char *o, size_t cap) {
 
 /* Rust `{:?}` of a str, restricted to printable ASCII plus the escapes Rust
  * uses for \t \r \n \" \\ and \0 (anything else: unsupported) */
+/* <str as Debug>::fmt (core/src/fmt/mod.rs, Rust 1.75): each char through
+ * char::escape_debug_ext with escape_grapheme_extended and escape_double_quote
+ * (not the single quote): \0 \t \r \n \\ \" as backslash escapes, a
+ * Grapheme_Extend or non-printable char (core/src/unicode/printable.rs) as
+ * \u{hex}, lowercase hex without leading zeros; anything else as is */
 static int str_debug(jde *d, const jbuf *s, jbuf *out) {
   memset(out, 0, sizeof *out);
   jb_byte(out, '"');
-  for (size_t i = 0; i < s->n; i++) {
+  for (size_t i = 0; i < s->n;) {
     uint8_t c = s->b[i];
+    uint32_t cp;
+    size_t len;
+    if (c < 0x80) {
+      cp = c;
+      len = 1;
+    } else {  /* the string is valid UTF-8 (parse_str checked it) */
+      len = c >= 0xF0 ? 4 : c >= 0xE0 ? 3 : 2;
+      if (c < 0xC2 || c > 0xF4 || i + len > s->n) return junsupported(d);
+      cp = c & (0x7F >> len);
+      for (size_t k = 1; k < len; k++) {
+        if ((s->b[i + k] & 0xC0) != 0x80) return junsupported(d);
+        cp = (cp << 6) | (s->b[i + k] & 0x3F);
+      }
+    }
     const char *e = NULL;
-    if (c == '"') e = "\\\"";
-    else if (c == '\\') e = "\\\\";
-    else if (c == '\n') e = "\\n";
-    else if (c == '\r') e = "\\r";
-    else if (c == '\t') e = "\\t";
-    else if (c == 0) e = "\\0";
-    if (e)
+    if (cp == '"') e = "\\\"";
+    else if (cp == '\\') e = "\\\\";
+    else if (cp == '\n') e = "\\n";
+    else if (cp == '\r') e = "\\r";
+    else if (cp == '\t') e = "\\t";
+    else if (cp == 0) e = "\\0";
+    if (e) {
       jb_push(out, (const uint8_t *)e, strlen(e));
-    else if (c >= 0x20 && c < 0x7f)
-      jb_byte(out, c);
-    else
-      return junsupported(d);
+    } else if (orc_u_dbg_escaped(cp)) {
+      char u[16];
+      int k = snprintf(u, sizeof u, "\\u{%x}", cp);
+      jb_push(out, (const uint8_t *)u, (size_t)k);
+    } else {
+      jb_push(out, s->b + i, len);
+    }
+    i += len;
   }
   jb_byte(out, '"');
   return 0;

@@ -31,6 +31,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+int orc_u_dbg_escaped(uint32_t cp) { return fsg_u_dbg_escaped(cp); }
+
 /* ------------------------------------------------------------------ */
 /* growable byte buffer                                                 */
 /* ------------------------------------------------------------------ */

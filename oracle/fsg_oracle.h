@@ -66,6 +66,8 @@ uint32_t orc_crc32c(const uint8_t *p, size_t n);
 size_t orc_varint_encode(int64_t v, uint8_t *out);
 size_t orc_varint_size(int64_t v);
 int orc_varint_decode(const uint8_t *p, size_t n, int64_t *v, size_t *used);
+/* 1: Rust's str Debug (toolchain 1.75) writes code point cp as \u{..}: not printable or Grapheme_Extend */
+int orc_u_dbg_escaped(uint32_t cp);
 
 orc_chain *orc_chain_new(void);
 void orc_chain_free(orc_chain *c);

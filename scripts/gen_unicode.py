@@ -215,6 +215,28 @@ def main():
     for k in CATS:
         arr(k, tabs[k])
     arr("word", word)
+    # Rust's str Debug (core fmt, toolchain 1.75): a char is written as \u{..}
+    # when it is not printable (printable.py: General_Category Cc Cf Cs Co Cn Zl
+    # Zp Zs, the space excepted) or Grapheme_Extend (escape_grapheme_extended);
+    # Grapheme_Extend from the Python regex module, on code points unicodedata
+    # assigns (later ones are Cn here: parity unpinned for them)
+    import regex
+    gext = regex.compile(r"\p{Grapheme_Extend}")
+    dbg = ranges(lambda c: (cat[c] in ("Cc", "Cf", "Cs", "Co", "Cn", "Zl", "Zp", "Zs") and c != 0x20) or
+                 (cat[c] != "Cn" and gext.match(chr(c)) is not None))
+    arr("dbgesc", dbg)
+    lines.append("static const uint32_t fsg_u_dbgesc_n = %d;" % len(dbg))
+    lines.append("/* 1: Rust's str Debug writes code point cp as \\u{..} (fsg_u_dbgesc) */")
+    lines.append("static int fsg_u_dbg_escaped(uint32_t cp) {")
+    lines.append("  uint32_t lo = 0, hi = fsg_u_dbgesc_n;")
+    lines.append("  while (lo < hi) {")
+    lines.append("    const uint32_t m = (lo + hi) / 2;")
+    lines.append("    if (cp < fsg_u_dbgesc[m].lo) hi = m;")
+    lines.append("    else if (cp > fsg_u_dbgesc[m].hi) lo = m + 1;")
+    lines.append("    else return 1;")
+    lines.append("  }")
+    lines.append("  return 0;")
+    lines.append("}")
     lines.append("typedef struct { const char *name; const fsg_urange *r; uint32_t n; } fsg_ucat;")
     lines.append("static const fsg_ucat fsg_u_cats[] = {" + ", ".join(
         '{"%s", fsg_u_%s, %d}' % (k, k, len(tabs[k])) for k in CATS) + "};")

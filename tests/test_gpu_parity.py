@@ -614,6 +614,24 @@ def _one_record_slice(value: bytes, base: int = 0) -> bytes:
     return b.encode()
 
 
+def test_filter_json_string_debug_texts(engine):
+    """serde's "invalid type: string .." with Rust's str Debug of any string
+    (control / format / separator / private-use / unassigned chars and
+    combining marks as \\u{..}): error hint bit-exact with the oracle, as one
+    record and as the first error in a batch."""
+    import json as _json
+    from tests.test_json_oracle import DEBUG_STRINGS
+    for s in DEBUG_STRINGS:
+        for ascii_only in (True, False):
+            doc = _json.dumps(s, ensure_ascii=ascii_only).encode()
+            check_batch(engine, CHAINS["filter_json"], _one_record_slice(doc))
+    b = P.Batch()
+    for v in (b'{"level":"info","message":"a"}', b'{"level":"warn","message":"b"}',
+              _json.dumps("x\u200d\u0301\x1b y").encode(), b'{"level":"info","message":"c"}'):
+        b.add_record(P.Record.new(v))
+    check_batch(engine, CHAINS["filter_json"], b.encode())
+
+
 def test_filter_json_fuzz_one_record(engine):
     """Every document of the corpus (valid, mutated, hand-picked error cases) as a
     one-record batch: output, error hint text, offset and value bit-exact."""

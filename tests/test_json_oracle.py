@@ -123,6 +123,47 @@ def test_oracle_error_texts():
         assert O.json_structured_log(doc) == ("err", want), doc
 
 
+# strings serde reports with Rust's str Debug ("invalid type: string ...")
+DEBUG_STRINGS = ["tab\there", "esc\x1b[31m", "del\x7f", "bel\u0007", "nul\u0000x", "caf\u00e9", "na\u0301x",
+                 "zwj\u200dx", "nbsp\u00a0x", "ls\u2028x", "shy\u00adx", "pua\ue000", "nonchar\uffff",
+                 "last\U0010ffff", "emoji\U0001f600", "quote'\"s", "back\\slash", "\u0300lead", "cjk\u4e2d",
+                 "arabic\u0645\u0631\u062d\u0628\u0627", "vs\ufe0f", "tag\U000e0041", "\u0085nel"]
+
+
+def _rust_str_debug(s):
+    """<str as Debug>::fmt restated from its documented rules (Rust 1.75
+    core::fmt / char::escape_debug_ext): independent of the oracle's C."""
+    import unicodedata
+    import regex
+    out = ['"']
+    for ch in s:
+        cp = ord(ch)
+        esc = {0: "\\0", 9: "\\t", 10: "\\n", 13: "\\r", 0x5C: "\\\\", 0x22: '\\"'}.get(cp)
+        cat = unicodedata.category(ch)
+        if esc is not None:
+            out.append(esc)
+        elif (cat != "Cn" and regex.match(r"\p{Grapheme_Extend}", ch)) or \
+                (cat in ("Cc", "Cf", "Cs", "Co", "Cn", "Zl", "Zp", "Zs") and ch != " "):
+            out.append("\\u{%x}" % cp)
+        else:
+            out.append(ch)
+    return "".join(out) + '"'
+
+
+def test_oracle_string_debug_texts():
+    """serde's Unexpected::Str through Rust's str Debug: control, format,
+    separator, private-use and unassigned chars and combining marks as
+    \\u{..}; printable non-ASCII as is (parity unpinned: no reference fixture;
+    checked against a separate restatement of the rules)."""
+    import json as _json
+    for s, ascii_only in [(s, a) for s in DEBUG_STRINGS for a in (True, False)]:
+        doc = _json.dumps(s, ensure_ascii=ascii_only).encode()  # \\u escapes, or raw UTF-8
+        col = len(doc)
+        want = "invalid type: string %s, expected struct StructuredLog at line 1 column %d" % (_rust_str_debug(s), col)
+        got = O.json_structured_log(doc)
+        assert got == ("err", want), (s, got, want)
+
+
 # ---------------------------------------------------------------------------
 # array_map_json_array: from_slice::<Vec<Value>> + to_string per element
 # ---------------------------------------------------------------------------
