@@ -31,8 +31,9 @@
  * (str_debug: Unicode escapes from this image's Unicode 13 categories and
  * Grapheme_Extend, parity unpinned for code points assigned later).
  * Outside the restatement (status ORC_E_UNSUPPORTED, mirrored by the GPU path):
- * an ignored value nested more than 64 levels below its first bracket, and an
- * error text holding a NUL byte.
+ * an ignored value nested more than 64 levels below its first bracket.  (An
+ * error text holding a NUL byte, from "unknown variant" of StructuredLog, is
+ * carried with its length.)
  */
 #include <math.h>
 #include <stdarg.h>
@@ -1240,13 +1241,8 @@ static int from_slice_struct(const uint8_t *s, size_t n, const jstruct *st, int 
     free(d.msg);
     return ORC_E_UNSUPPORTED;
   }
-  *msg = render(&d, msg_len);
+  *msg = render(&d, msg_len); /* may hold a NUL ("unknown variant" of a raw string): *msg_len carries it */
   free(d.msg);
-  if (memchr(*msg, 0, *msg_len)) { /* a NUL inside the text: the C-string hint plumbing cannot carry it */
-    free(*msg);
-    *msg = NULL;
-    return ORC_E_UNSUPPORTED;
-  }
   return 1;
 }
 

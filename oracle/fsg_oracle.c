@@ -2032,6 +2032,7 @@ typedef struct {
   int has_error;
   rec_t err_rec; /* owned clone of the failing record */
   char *hint;
+  size_t hint_len; /* 0: strlen(hint) (a serde_json text may hold a NUL: its length is kept) */
   int64_t err_offset;
   int kind;
   int unsupported;
@@ -2043,6 +2044,7 @@ static void stage_run(stage_t *s, recvec *in, int64_t base_offset, stage_out *o)
   for (size_t i = 0; i < in->n; i++) {
     rec_t *r = &in->r[i];
     char *hint = NULL;
+    size_t hint_len = 0;
     size_t vut;
     int el;
     int keep = 0;
@@ -2082,7 +2084,8 @@ static void stage_run(stage_t *s, recvec *in, int64_t base_offset, stage_out *o)
           return;
         }
         if (jr) {
-          hint = m; /* serde_json::Error Display */
+          hint = m; /* serde_json::Error Display (may hold a NUL: "unknown variant `..`" of the raw string) */
+          hint_len = ml;
           break;
         }
         keep = level > 0;
@@ -2353,6 +2356,7 @@ static void stage_run(stage_t *s, recvec *in, int64_t base_offset, stage_out *o)
       /* SmartModuleTransformRuntimeError::new(record, base_offset, kind, err) */
       o->has_error = 1;
       o->hint = hint;
+      o->hint_len = hint_len;
       o->err_offset = base_offset + r->off_delta;
       o->err_rec = rec_clone(r);
       return; /* break */
@@ -2369,7 +2373,7 @@ static void res_set_error(orc_result *out, stage_out *so) {
   out->has_error = 1;
   out->hint = so->hint;
   so->hint = NULL;
-  out->hint_len = strlen(out->hint);
+  out->hint_len = so->hint_len ? so->hint_len : strlen(out->hint);
   out->err_offset = so->err_offset;
   out->err_kind = so->kind;
   out->has_key = so->err_rec.has_key;

@@ -25,7 +25,7 @@ class _Result(ctypes.Structure):
         ("base_offset", ctypes.c_int64),
         ("last_offset_delta", ctypes.c_int32),
         ("has_error", ctypes.c_int),
-        ("hint", ctypes.c_char_p),
+        ("hint", ctypes.POINTER(ctypes.c_char)),  # hint_len bytes (a serde text may hold a NUL)
         ("hint_len", ctypes.c_size_t),
         ("err_offset", ctypes.c_int64),
         ("err_kind", ctypes.c_int32),

@@ -625,6 +625,8 @@ def test_filter_json_string_debug_texts(engine):
         for ascii_only in (True, False):
             doc = _json.dumps(s, ensure_ascii=ascii_only).encode()
             check_batch(engine, CHAINS["filter_json"], _one_record_slice(doc))
+    # a NUL inside the error text (unknown variant of the raw string) crosses with hint_len
+    check_batch(engine, CHAINS["filter_json"], _one_record_slice(b'{"level":"in\\u0000fo","message":"m"}'))
     b = P.Batch()
     for v in (b'{"level":"info","message":"a"}', b'{"level":"warn","message":"b"}',
               _json.dumps("x\u200d\u0301\x1b y").encode(), b'{"level":"info","message":"c"}'):

@@ -118,6 +118,9 @@ def test_oracle_error_texts():
         b'{"level":"info","message":"x"} x': "trailing characters at line 1 column 32",
         b'{"level":"info","message":"x",}': "trailing comma at line 1 column 31",
         b'\n\n  {"level"\n:\n"info"}': "missing field `message` at line 5 column 7",
+        # a NUL in the text (the raw variant string): carried with its length
+        b'{"level":"in\\u0000fo","message":"m"}':
+            "unknown variant `in\x00fo`, expected one of `debug`, `info`, `warn`, `error` at line 1 column 21",
     }
     for doc, want in cases.items():
         assert O.json_structured_log(doc) == ("err", want), doc
