@@ -161,15 +161,43 @@ struct Parser {
         neg = !neg;
         i++;
       }
+      // the raw text splits at its first ':' / '=' and each part is normalized
+      // on its own (symbolic_name_normalize, UAX44-LM3): an "is" prefix of the
+      // raw part dropped ("isc" kept), then ' ', '_', '-' removed, lowercased
+      std::string part;
+      bool is_pfx = false, start = true, split = false;
+      auto finish = [&]() {
+        if (is_pfx && part == "c") part = "isc";
+        name += part;
+        part.clear();
+      };
       while (i < p.size() && p[i] != '}') {
         const uint32_t c = p[i++];
-        if (c == ' ' || c == '_' || c == '-') continue;
         if (c >= 0x80) {
           unsup = true;
           return 0;
         }
-        name += (char)(c >= 'A' && c <= 'Z' ? c + 32 : c);
+        if (!split && (c == ':' || c == '=')) {
+          finish();
+          name += '=';
+          split = true;
+          start = true;
+          continue;
+        }
+        if (start) {
+          start = false;
+          const uint32_t c2 = i < p.size() ? p[i] : 0;
+          if ((c | 0x20) == 'i' && (c2 | 0x20) == 's') {
+            is_pfx = true;
+            i++;
+            continue;
+          }
+          is_pfx = false;
+        }
+        if (c == ' ' || c == '_' || c == '-') continue;
+        part += (char)(c >= 'A' && c <= 'Z' ? c + 32 : c);
       }
+      finish();
       if (!at('}')) {
         err = true;
         return 0;
@@ -187,8 +215,6 @@ struct Parser {
       }
       name += (char)(c >= 'A' && c <= 'Z' ? c + 32 : c);
     }
-    for (auto& ch : name)
-      if (ch == ':') ch = '=';
     const long m = fsg_u_property(name.c_str());
     Set st;
     if (m == FSG_UPROP_ASCII) {

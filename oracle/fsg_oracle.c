@@ -670,15 +670,39 @@ static int rx_property(rxparser *P, int neg, cset *set) {
       neg = !neg;
       P->i++;
     }
+    /* regex-syntax: the raw text splits at its first ':' / '='; each part is
+     * normalized alone (symbolic_name_normalize): a raw "is" prefix dropped
+     * ("isc" kept), ' ', '_', '-' removed, ASCII lowercased */
+    int split = 0, start = 1, is_pfx = 0;
+    size_t p0 = 0; /* where the current part starts in name */
     while (P->i < P->n && P->p[P->i] != '}') {
       uint32_t c = P->p[P->i++];
-      if (c == ' ' || c == '_' || c == '-') continue;
-      if (c >= 0x80 || nl + 1 >= sizeof name) {
+      if (c >= 0x80 || nl + 4 >= sizeof name) {
         P->unsupported = 1;
         return 0;
       }
-      name[nl++] = (char)(c == ':' ? '=' : (c >= 'A' && c <= 'Z') ? c + 32 : c);
+      if (!split && (c == ':' || c == '=')) {
+        if (is_pfx && nl - p0 == 1 && name[p0] == 'c') nl = p0 + (size_t)sprintf(name + p0, "isc");
+        name[nl++] = '=';
+        split = 1;
+        start = 1;
+        p0 = nl;
+        continue;
+      }
+      if (start) {
+        start = 0;
+        uint32_t c2 = P->i < P->n ? P->p[P->i] : 0;
+        if ((c | 0x20) == 'i' && (c2 | 0x20) == 's') {
+          is_pfx = 1;
+          P->i++;
+          continue;
+        }
+        is_pfx = 0;
+      }
+      if (c == ' ' || c == '_' || c == '-') continue;
+      name[nl++] = (char)((c >= 'A' && c <= 'Z') ? c + 32 : c);
     }
+    if (is_pfx && nl - p0 == 1 && name[p0] == 'c') nl = p0 + (size_t)sprintf(name + p0, "isc");
     if (P->i >= P->n) {
       P->err = 1;
       return 0;

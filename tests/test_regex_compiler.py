@@ -136,10 +136,13 @@ def test_random_patterns_match_oracle():
     (r"(?i)ǆ", "Ǆ", True), (r"(?i)θ", "ϑ", True), (r"(?i)\p{Lu}", "a", True), (r"\p{Lu}", "a", False),
     (r"(?i)[^a]", "A", False), (r"(?i)\P{Lu}", "A", False), (r"(?i)\P{Lu}", "a", False), (r"(?i)\P{Lu}", "1", True), (r"(?i)ω", "Ω", True), (r"(?i)µ", "Μ", True),
     (r"\p{Greek}", "ω", True), (r"\p{Greek}", "w", False), (r"\p{sc=Latin}", "é", True),
-    (r"\p{isGreek}", "ω", None),
+    (r"\p{isGreek}", "ω", True),
     # (?x): whitespace around a class range's '-' is skipped (parse_set_class_range's bump_space)
     (r"(?x)[a - z]", "m", True), (r"(?x)[a - z]", "-", False), (r"(?x)[a - ]", "-", True),
     (r"(?x)[ a -z ]x", "qx", True), (r"[a - z]", "-", False), (r"[a - z]", " ", True), (r"[a - z]", "m", False),
+    # the "is" prefix is dropped from the raw part only ("I_s" is not a prefix; "isc" = ISO_Comment, not "c")
+    (r"\p{IsLu}", "A", True), (r"\p{IsLu}", "a", False), (r"\p{sc=IsArabic}", "\u0628", True),
+    (r"\p{sc=IsArabic}", "b", False), (r"\p{IsScript:Greek}", "\u03c9", True), (r"\p{I_sGreek}", "x", None), (r"\p{Isc}", "x", None),
 ])
 def test_fold_and_x_ranges(pattern, text, expect):
     b = text.encode()
@@ -156,7 +159,10 @@ def test_fold_and_x_ranges(pattern, text, expect):
 
 @pytest.mark.parametrize("pattern", [r"\p{Greek}", r"\p{Cyrillic}+", r"\p{scx=Arabic}", r"\p{Emoji}", r"\p{Alphabetic}",
                                      r"\p{Uppercase}", r"\p{Dash}", r"\p{Han}", r"\P{Latin}", r"[\p{Greek}\p{Cyrillic}]{2}",
-                                     r"\p{Extended_Pictographic}", r"\p{Math}"])
+                                     r"\p{Extended_Pictographic}", r"\p{Math}",
+                                     # symbolic_name_normalize's "is" prefix, per part of name=value
+                                     r"\p{IsGreek}", r"\p{Is_Cyrillic}", r"\p{IsAlphabetic}",
+                                     r"\p{IsHan}+"])
 def test_properties_against_python_regex(pattern):
     """Binary properties, scripts and Script_Extensions over random text of
     Greek, Cyrillic, Latin, Arabic, CJK and symbols, against Python's `regex`
