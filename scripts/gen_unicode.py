@@ -107,17 +107,32 @@ def props_and_folds():
         for n in nms:
             names.append((n.lower(), 2, si))
             names.append((n.lower(), 3, si + 1))
+    # Grapheme_Cluster_Break / Word_Break / Sentence_Break values (gcb= / wb= /
+    # sb=; regex-syntax's property_values; the value sets are Unicode 15's)
+    for kind, (prop, short) in enumerate([("GRAPHEMECLUSTERBREAK", "gcb"), ("WORDBREAK", "wb"),
+                                          ("SENTENCEBREAK", "sb")], start=4):
+        by_id = {}
+        for nm, i in rc.PROPERTIES[prop][1].items():
+            by_id.setdefault(i, []).append(nm)
+        for i, nms in sorted(by_id.items()):
+            canon = max(nms, key=len)
+            si = len(sets)
+            sets.append(("%s_%s" % (short, canon), cps_of(r"\p{%s=%s}" % (prop, canon))))
+            for n in nms:
+                names.append((n.lower(), kind, si))
     for nm, rs in sets:
         lines.append("static const fsg_urange fsg_u_%s[] = {%s};" % (nm, ", ".join("{0x%X, 0x%X}" % r for r in rs) or "{1, 0}"))
     lines.append("static const fsg_urange* const fsg_u_psets[] = {%s};" % ", ".join("fsg_u_" + nm for nm, _ in sets))
     lines.append("static const uint32_t fsg_u_psets_n[] = {%s};" % ", ".join(str(len(rs)) for _, rs in sets))
     names.sort()
-    lines.append("/* normalized name, kind (1 binary property, 2 Script value, 3 Script_Extensions value), set */")
+    lines.append("/* normalized name, kind (1 binary property, 2 Script value, 3 Script_Extensions value, 4 / 5 / 6 "
+                 "Grapheme_Cluster_Break / Word_Break / Sentence_Break value), set */")
     lines.append("static const struct { const char *n; int k, s; } fsg_u_pnames[] = {" +
                  ", ".join('{"%s", %d, %d}' % t for t in names) + "};")
     lines.append("""/* a normalized \\p{..} name that is not a General_Category value: a binary
- * property, a Script value (bare or sc= / script=) or a Script_Extensions value
- * (scx= / scriptextensions=), in regex-syntax's order; 1 found, 0 unknown */
+ * property, a Script value (bare or sc= / script=), a Script_Extensions value
+ * (scx= / scriptextensions=) or a gcb= / wb= / sb= value, in regex-syntax's
+ * order; 1 found, 0 unknown */
 static int fsg_u_lookup(const char *name, const fsg_urange **r, uint32_t *n) {
   const char *eq = strchr(name, '=');
   int want = 0;
@@ -126,6 +141,9 @@ static int fsg_u_lookup(const char *name, const fsg_urange **r, uint32_t *n) {
     size_t pl = (size_t)(eq - name);
     if ((pl == 2 && !strncmp(name, "sc", 2)) || (pl == 6 && !strncmp(name, "script", 6))) want = 2;
     else if ((pl == 3 && !strncmp(name, "scx", 3)) || (pl == 16 && !strncmp(name, "scriptextensions", 16))) want = 3;
+    else if ((pl == 3 && !strncmp(name, "gcb", 3)) || (pl == 20 && !strncmp(name, "graphemeclusterbreak", 20))) want = 4;
+    else if ((pl == 2 && !strncmp(name, "wb", 2)) || (pl == 9 && !strncmp(name, "wordbreak", 9))) want = 5;
+    else if ((pl == 2 && !strncmp(name, "sb", 2)) || (pl == 13 && !strncmp(name, "sentencebreak", 13))) want = 6;
     else return 0;
     v = eq + 1;
   } else if (!strcmp(name, "cf") || !strcmp(name, "sc") || !strcmp(name, "lc")) {

@@ -571,7 +571,8 @@ def test_unicode_word_boundaries(engine):
         chain = [("regex-filter", {"regex": pat}, None)]
         check_batch(engine, chain, synth.make_slice(4, 500))
         check_batch(engine, chain, b.encode())
-    for pat in (r"\p{IsGreek}", r"\p{sc=IsGreek}\s", r"\p{Is_L}{3}"):  # symbolic_name_normalize's "is" prefix
+    for pat in (r"\p{IsGreek}", r"\p{sc=IsGreek}\s", r"\p{Is_L}{3}",  # symbolic_name_normalize's "is" prefix
+                r"\p{GCB=Extend}", r"\p{WB=ALetter}{2}\p{SB=Lower}"):  # break property values
         check_batch(engine, [("regex-filter", {"regex": pat}, None)], b.encode())
     chain = [("regex-filter", {"regex": r"(?-u:\b)x"}, None)]
     with pytest.raises(Unsupported):

@@ -162,7 +162,11 @@ def test_fold_and_x_ranges(pattern, text, expect):
                                      r"\p{Extended_Pictographic}", r"\p{Math}",
                                      # symbolic_name_normalize's "is" prefix, per part of name=value
                                      r"\p{IsGreek}", r"\p{Is_Cyrillic}", r"\p{IsAlphabetic}",
-                                     r"\p{IsHan}+"])
+                                     r"\p{IsHan}+",
+                                     # Grapheme_Cluster_Break / Word_Break / Sentence_Break values
+                                     r"\p{GCB=Extend}", r"\p{Grapheme_Cluster_Break=Other}{2}", r"\p{WB=ALetter}+",
+                                     r"\p{Word_Break=Numeric}", r"\p{SB=Upper}", r"\P{Sentence_Break=Lower}",
+                                     r"\p{gcb=EB}", r"[\p{WB=MidLetter}\p{WB=Katakana}]"])
 def test_properties_against_python_regex(pattern):
     """Binary properties, scripts and Script_Extensions over random text of
     Greek, Cyrillic, Latin, Arabic, CJK and symbols, against Python's `regex`
