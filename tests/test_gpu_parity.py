@@ -1606,6 +1606,8 @@ def test_compressed_resident_and_errors(engine):
     rs = ResidentSlice(engine, csl)
     assert not rs.device_framed and rs.n_records == 2000
     assert rs.verify_crc()[:2] == (0, -1)  # checked on the stored (compressed) bytes at ingest
+    rs.verify_crc_start()  # nothing to start: the ingest result is returned
+    assert rs.verify_crc()[:2] == (0, -1)
     from tests.compressed_slices import batches
     crc_bad = bytearray(csl)
     crc_bad[list(batches(csl))[4][0] + 18] ^= 1  # batch 4's stored CRC
