@@ -287,7 +287,7 @@ struct EvalArgs {
   ArrBatch* arr_b;     // array_map lean path: per batch element statistics ...
   uint32_t* arr_bm;    // ... and element bitmaps (kArrBmBatch words per batch)
   unsigned long long* fbm;  // flat substring path (fsg_lean.hip): a bit per 16-byte chunk of the slice,
-                            // occurrence starts [0, fbm_words), then bytes >= 0x80 [fbm_words, 2 fbm_words)
+                            // per 1 KiB round the occurrence-start word then the bytes >= 0x80 word
   uint64_t fbm_words;
 };
 

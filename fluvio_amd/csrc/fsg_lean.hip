@@ -1344,8 +1344,9 @@ __global__ __launch_bounds__(256) void k_flat_scan(EvalArgs a, uint32_t stage) {
   const uint64_t nrounds = a.fbm_words;  // 1 KiB rounds of the slice
   const uint64_t w0 = (uint64_t)blockIdx.x * 4 + wv;
   const uint64_t nw = (uint64_t)gridDim.x * 4;
-  unsigned long long* hit_bm = a.fbm;
-  unsigned long long* hi_bm = a.fbm + a.fbm_words;
+  // the two bitmaps interleaved per 1 KiB round: occurrence word r at fbm[2r],
+  // high-byte word at fbm[2r + 1] (k_flat_decide reads both from one line)
+  ulonglong2* bm2 = (ulonglong2*)a.fbm;
   for (uint64_t r0 = w0 * kFlatRounds; r0 < nrounds; r0 += nw * kFlatRounds) {
     uint4 v[kFlatRounds];
     uint32_t nx[kFlatRounds];
@@ -1417,21 +1418,19 @@ __global__ __launch_bounds__(256) void k_flat_scan(EvalArgs a, uint32_t stage) {
         }
       }
       const uint64_t hb = __ballot(hit), hh = __ballot(high);
-      if (lane == 0) {
-        hit_bm[r0 + i] = hb;
-        hi_bm[r0 + i] = hh;
-      }
+      if (lane == 0) bm2[r0 + i] = make_ulonglong2(hb, hh);
     }
   }
 }
-__device__ __forceinline__ bool bm_bit(const unsigned long long* bm, uint64_t c) { return (bm[c >> 6] >> (c & 63)) & 1ull; }
+// bm: the interleaved bitmaps offset by the one wanted (0 occurrences, 1 high bytes): word w at bm[2 w]
+__device__ __forceinline__ bool bm_bit(const unsigned long long* bm, uint64_t c) { return (bm[2 * (c >> 6)] >> (c & 63)) & 1ull; }
 // bits [c0, c1) of a bitmap: any set
 __device__ __forceinline__ bool flat_any(const unsigned long long* bm, uint64_t c0, uint64_t c1) {
   for (uint64_t c = c0; c < c1;) {
     const uint64_t w = c >> 6, lo = c & 63;
     const uint64_t hi = (c1 - (w << 6)) < 64 ? (c1 - (w << 6)) : 64;
     const uint64_t mask = (hi == 64 ? ~0ull : ((1ull << hi) - 1ull)) & ~((1ull << lo) - 1ull);
-    if (bm[w] & mask) return true;
+    if (bm[2 * w] & mask) return true;
     c = (w + 1) << 6;
   }
   return false;
@@ -1480,8 +1479,8 @@ __global__ __launch_bounds__(256) void k_flat_decide(EvalArgs a, uint32_t stage)
   const bool upper = sd.in_type == VT_SRC_UPPER;
   const bool out_upper = a.chain->out_type == VT_SRC_UPPER;
   const uint8_t* nd = a.blob + sd.needle;
-  const unsigned long long* hit_bm = a.fbm;
-  const unsigned long long* hi_bm = a.fbm + a.fbm_words;
+  const unsigned long long* hit_bm = a.fbm;  // interleaved (k_flat_scan): hit word w at [2 w], high at [2 w + 1]
+  const unsigned long long* hi_bm = a.fbm + 1;
   const uint8_t* S = a.slice;
   const uint64_t pos = a.bpos[b];
   const uint64_t nxt = b + 1 < a.nbatches ? a.bpos[b + 1] : a.slice_len;
@@ -1539,8 +1538,8 @@ __global__ __launch_bounds__(256) void k_flat_decide(EvalArgs a, uint32_t stage)
     const uint32_t tw = ld_u32_at(S + ve);
     const uint64_t c0 = va >> 4, c1 = (ve + 15) >> 4, i0 = (va + 15) >> 4, i1 = ve >> 4;
     const uint64_t wb = c0 >> 6;  // first bitmap word touching the value
-    const unsigned long long hb0 = hi_bm[wb], hb1 = hi_bm[wb + 1];
-    const unsigned long long mb0 = hit_bm[wb], mb1 = hit_bm[wb + 1];
+    const ulonglong2 bw0 = *(const ulonglong2*)(a.fbm + 2 * wb), bw1 = *(const ulonglong2*)(a.fbm + 2 * wb + 2);
+    const unsigned long long mb0 = bw0.x, hb0 = bw0.y, mb1 = bw1.x, hb1 = bw1.y;
     const uint4 ea = *(const uint4*)(S + (c0 << 4));
     const uint4 eb = *(const uint4*)(S + (((ve ? ve - 1 : 0) >> 4) << 4));
     nb = var4(tw, hdr);
@@ -1594,7 +1593,7 @@ __global__ __launch_bounds__(256) void k_flat_decide(EvalArgs a, uint32_t stage)
             c = j1 - 1;
             continue;
           }
-          if (c >= wb && c < wb + 128 ? !bit(mb0, mb1, c) : !bm_bit(hit_bm, c)) continue;
+          if (c >= (wb << 6) && c < ((wb + 2) << 6) ? !bit(mb0, mb1, c) : !bm_bit(hit_bm, c)) continue;  // the loaded words
           const uint64_t lo = (c << 4) >= va + blo ? (c << 4) - blo : va;
           const uint64_t hi = (c << 4) + bhi <= sl ? (c << 4) + bhi : sl;
           for (uint64_t s0 = lo; s0 <= hi && !match; s0++) match = flat_verify(S, s0, nd, m, upper);

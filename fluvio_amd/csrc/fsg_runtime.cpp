@@ -2128,7 +2128,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   bool flat = false;
   if (fst >= 0 && !c->no_flat) {
     ea.fbm_words = (s->len + 1023) / 1024;
-    flat = c->fbm.ensure((size_t)ea.fbm_words * 16) == hipSuccess;
+    flat = c->fbm.ensure((size_t)ea.fbm_words * 16 + 32) == hipSuccess;  // + the pair past the last (k_flat_decide)
     (void)hipGetLastError();
     if (flat) {
       ea.fbm = c->fbm.as<unsigned long long>();
