@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="records per CPU-baseline process")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--detail", default=os.path.join(ROOT, "bench_detail.json"),
+                    help="the full result (phases, prose, fetch, e2e) is written here; stdout gets the compact line")
     ap.add_argument("--dry-run", action="store_true",
                     help="rank plumbing only (launch, rendezvous, barrier, max over ranks, the JSON line): no GPU work, "
                          "for the CPU tests of --gpus N")
@@ -142,7 +144,7 @@ def pmc_traffic(workload, kernel, n_records, n_batches):
     # the eval bracket covers k_chase + k_eval_lean, the flat path's k_flat_scan + k_flat_decide,
     # k_arr_frame + k_arr_lean, and the deferred exact k_eval<N>; crc: k_crc16 + k_crc_final;
     # write: k_write(_lean) + k_write_canon
-    pre = ("fsg::" + kernel,) + (("fsg::k_arr_", "fsg::k_flat_", "fsg::k_chase") if kernel == "k_eval" else ())
+    pre = ("fsg::" + kernel,) + (("fsg::k_arr_frame", "fsg::k_arr_lean", "fsg::k_flat_", "fsg::k_chase") if kernel == "k_eval" else ())
     hits = [v["total"] for k, v in db["kernels"].items() if k.split("<")[0].startswith(pre)]
     return (sum(hits), db["source"]) if hits else (None, None)
 
@@ -725,14 +727,97 @@ def dry_run(ctx):
     ctx.barrier()
     elapsed = ctx.max_over_ranks(time.perf_counter() - t0)
     if ctx.rank == 0:
-        print(json.dumps({"metric": "records/sec + achieved HBM GB/s for SmartModule filter chain, 1/2/4/8 MI355X",
-                          "value": None, "unit": "records/s", "n_gpus": ctx.world, "steps": a.steps,
-                          "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
-                          "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "none (dry run)",
-                          "dry_run": True, "ranks": ctx.world,
-                          "config": {"workload": a.workload, "parallelism": f"partitions sharded over {ctx.world} GPU(s)"}}))
+        full = {"metric": "records/sec + achieved HBM GB/s for SmartModule filter chain, 1/2/4/8 MI355X",
+                "value": None, "unit": "records/s", "n_gpus": ctx.world, "steps": a.steps,
+                "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "none (dry run)",
+                "config": {"workload": a.workload, "parallelism": f"partitions sharded over {ctx.world} GPU(s)"}}
+        j = json.loads(compact_line(full))
+        j.update(dry_run=True, ranks=ctx.world)
+        print(json.dumps(j, allow_nan=False, separators=(",", ":")), flush=True)
     if ctx.dist is not None:
         ctx.dist.destroy_process_group()
+
+
+LINE_MAX = 8192  # the driver parses one stdout line; everything else goes to the detail file
+
+
+def _finite(v):
+    """JSON-safe: NaN / Infinity become null (json.dumps would print bare NaN)."""
+    if isinstance(v, float):
+        return v if v == v and v not in (float("inf"), float("-inf")) else None
+    if isinstance(v, dict):
+        return {k: _finite(x) for k, x in v.items()}
+    if isinstance(v, (list, tuple)):
+        return [_finite(x) for x in v]
+    return v
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if isinstance(d, dict) and k in d}
+
+
+def _rnd(v, nd=4):
+    """Significant-digit rounding for the compact line (values stay exact in the detail file)."""
+    if isinstance(v, float) and v == v and v not in (float("inf"), float("-inf")) and v != 0.0:
+        from math import floor, log10
+        return round(v, max(0, nd - 1 - int(floor(log10(abs(v))))))
+    if isinstance(v, dict):
+        return {k: _rnd(x, nd) for k, x in v.items()}
+    return v
+
+
+def compact_line(full):
+    """The ONE line the driver parses (< LINE_MAX bytes, no NaN / Infinity): the
+    headline keys, its roofline and cpu_baseline, and per workload a summary
+    {value, unit, ms_per_step, roofline {kernel, frac, achieved}, cpu_baseline
+    {value, cores}}.  Phases, prose, fetch and e2e details live in the detail file."""
+    head = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data")
+    out = _pick(full, head)
+    cfg = full.get("config") or {}
+    out["config"] = _pick(cfg, ("workload", "records_per_gpu", "batches_per_gpu", "slice_bytes_per_gpu",
+                                "output_bytes_per_gpu", "chain", "partitions", "records_per_partition",
+                                "parallelism"))
+    rf = full.get("roofline")
+    if rf:
+        r = _pick(rf, ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic",
+                       "algorithmic_bytes_per_launch", "avg_launch_ms", "priced_on"))
+        if isinstance(rf.get("step"), dict):
+            r["step_frac"] = rf["step"].get("frac")
+        out["roofline"] = r
+    cb = full.get("cpu_baseline")
+    out["cpu_baseline"] = None if not cb else dict(
+        _pick(cb, ("value", "unit", "cores", "kind", "cpu_model")),
+        sample=f"{cb.get('cores')} partitions x bounded sample through the scalar C oracle (port); see detail file"
+        if cb.get("unit") != "us" else "20000 one-record calls of the scalar C oracle, p50")
+    for k in ("fetch", "e2e"):
+        if isinstance(full.get(k), dict):
+            out[k] = _pick(full[k], ("value", "unit", "ms_per_step"))
+    wl = {}
+    for name, w in (full.get("workloads") or {}).items():
+        s = _pick(w, ("value", "unit", "ms_per_step", "higher_is_better", "scaling", "dtype"))
+        if isinstance(w.get("roofline"), dict):
+            s["roofline"] = _pick(w["roofline"], ("kernel", "frac", "achieved", "traffic", "priced_on"))
+            if isinstance(w["roofline"].get("step"), dict):
+                s["roofline"]["step_frac"] = w["roofline"]["step"].get("frac")
+        if isinstance(w.get("cpu_baseline"), dict):
+            s["cpu_baseline"] = _pick(w["cpu_baseline"], ("value", "unit", "cores", "kind"))
+        wl[name] = s
+    if wl:
+        out["workloads"] = wl
+    out["detail"] = "bench_detail.json"
+    out = _finite(_rnd(out))
+    line = json.dumps(out, allow_nan=False, separators=(",", ":"))
+    if len(line) >= LINE_MAX:  # drop per-workload extras before anything the contract names
+        for s in out.get("workloads", {}).values():
+            for k in ("higher_is_better", "scaling", "dtype"):
+                s.pop(k, None)
+        out.pop("fetch", None)
+        out.pop("e2e", None)
+        line = json.dumps(out, allow_nan=False, separators=(",", ":"))
+    assert len(line) < LINE_MAX, len(line)
+    return line
 
 
 def main():
@@ -779,7 +864,9 @@ def main():
             out["workloads"] = workloads
         if head == "f3-one-record":  # a latency line, not the headline metric
             out["metric"] = line["metric"]
-        print(json.dumps(out))
+        with open(a.detail, "w") as fh:
+            json.dump(_finite(out), fh, indent=1, allow_nan=False)
+        print(compact_line(out), flush=True)
     if ctx.dist is not None:
         ctx.dist.destroy_process_group()
 
