@@ -317,6 +317,7 @@ struct PlanArgs {
   int32_t tail_status;  // framing status of the batch after the last framed one (0 = clean end)
   int32_t empty_chain;
   int32_t has_agg;
+  int32_t seg;  // a segment of a composed chain: `done` locates the failure for the next segment
   int64_t acc0;
 };
 

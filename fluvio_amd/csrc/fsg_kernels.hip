@@ -1640,6 +1640,10 @@ __device__ __forceinline__ void plan_run(const PlanArgs& a) {
     // process() completed for the batches before the failing one (all of them
     // when the iterator failed after the last framed batch)
     p.done = fail_at != NONE ? (int32_t)fail_at - 1 : (int32_t)n - 1;
+    // FSG_E_UNSUPPORTED: the input is valid for the reference and the caller
+    // falls back (e.g. to wasm) and replays it, so no state moves; a segment
+    // keeps `done` (its output slice ends there, the final stop decides)
+    if (status == -103 && !a.seg) p.done = -1;
     const uint32_t m = fail_at != NONE ? fail_at : (n ? n - 1 : NONE);
     if (m != NONE) {
       ScanRow r = incl_at(a, m);
@@ -3704,10 +3708,12 @@ void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s) {
     // k_eval_int over every batch (starts from k_chase_w, kept with the slice), then the deferred list
     launch_eval_int(a, (ops & opbit(OP_AGG_SUM)) != 0, s);
     grid = a.nbatches < 2048u ? a.nbatches : 2048u;
-  } else if (mode == EVAL_LEAN || mode == EVAL_FLAT) {
-    // k_chase + k_eval_lean, or the flat substring kernels (fsg_lean.hip)
+  } else if (mode == EVAL_LEAN || mode == EVAL_FLAT || mode == EVAL_FJSON) {
+    // k_chase + k_eval_lean, or the flat substring / JSON kernels (fsg_lean.hip)
     if (mode == EVAL_FLAT)
       launch_eval_flat(a, a.flat_st, s);
+    else if (mode == EVAL_FJSON)
+      launch_eval_fjson(a, s);
     else
       launch_eval_lean(a, ops, s);
     grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list

@@ -1324,21 +1324,30 @@ __device__ __forceinline__ bool flat_verify(const uint8_t* s, uint64_t p, const 
   }
   return true;
 }
-template <bool kLong>  // kLong: m >= 7, aligned dwords against the 4 offsets
+// JSON-interesting bytes of a dword (0x80 per byte): '"', '\\', < 0x20, >= 0x80
+__device__ __forceinline__ uint32_t fj_bytes(uint32_t w) {
+  return zbytes(w ^ 0x22222222u) | zbytes(w ^ 0x5C5C5C5Cu) | zbytes(w & 0xE0E0E0E0u) | (w & 0x80808080u);
+}
+// kLong: m >= 7, aligned dwords against the 4 offsets.  kJson: the second word
+// of a round holds the chunks with a JSON-interesting byte (fj_bytes) instead
+// of the high bytes (the flat JSON path); kNone: no substring stage (occurrence word 0)
+template <bool kLong, bool kJson = false, bool kNone = false>
 __global__ __launch_bounds__(256) void k_flat_scan(EvalArgs a, uint32_t stage) {
   // a wave's round staged in LDS when it holds candidates: the needle is
   // verified from there (a global re-read per candidate stalled the stream)
   __shared__ uint32_t rbuf[4][256 + 4];  // (+4: the alignbyte of the last dword reads one past)
   __shared__ uint32_t ndw[kLeanNeedle / 4 + 1];
-  const StageDesc& sd = a.chain->st[stage];
-  const uint32_t m = sd.needle_len;
-  const bool upper = sd.in_type == VT_SRC_UPPER;
+  const StageDesc& sd = a.chain->st[kNone ? 0 : stage];
+  const uint32_t m = kNone ? 4u : sd.needle_len;
+  const bool upper = !kNone && sd.in_type == VT_SRC_UPPER;
   const uint8_t* nd = a.blob + sd.needle;
-  for (uint32_t t = threadIdx.x; t < (m + 3) / 4; t += 256) ndw[t] = ld_u32_at(nd + 4 * t);
-  __syncthreads();
-  uint32_t rot[4];
+  uint32_t rot[4] = {0, 0, 0, 0};
+  if (!kNone) {
+    for (uint32_t t = threadIdx.x; t < (m + 3) / 4; t += 256) ndw[t] = ld_u32_at(nd + 4 * t);
+    __syncthreads();
 #pragma unroll
-  for (int d = 0; d < 4; d++) rot[d] = ld_u32_at(nd + (kLong ? d : 0));
+    for (int d = 0; d < 4; d++) rot[d] = ld_u32_at(nd + (kLong ? d : 0));
+  }
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   uint32_t* rb = rbuf[wv];
   const uint64_t nrounds = a.fbm_words;  // 1 KiB rounds of the slice
@@ -1361,7 +1370,13 @@ __global__ __launch_bounds__(256) void k_flat_scan(EvalArgs a, uint32_t stage) {
       if (r0 + i >= nrounds) break;  // uniform
       const uint64_t R = (r0 + i) * 1024;
       uint32_t w[5] = {v[i].x, v[i].y, v[i].z, v[i].w, kLong ? 0u : nx[i]};
-      const bool high = ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) != 0u;
+      const bool high = kJson ? ((fj_bytes(w[0]) | fj_bytes(w[1]) | fj_bytes(w[2]) | fj_bytes(w[3])) != 0u)
+                              : ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) != 0u;
+      if (kNone) {
+        const uint64_t hh = __ballot(high);
+        if (lane == 0) bm2[r0 + i] = make_ulonglong2(0ull, hh);
+        continue;
+      }
       if (upper) {
 #pragma unroll
         for (int k = 0; k < 5; k++) w[k] = swar_upper(w[k]);
@@ -1403,6 +1418,7 @@ __global__ __launch_bounds__(256) void k_flat_scan(EvalArgs a, uint32_t stage) {
           cm &= cm - 1;
           const int64_t rel = kLong ? (int64_t)(16 * lane + 4 * (j >> 2)) - (int64_t)(j & 3) : (int64_t)(16 * lane + j);
           if (rel < 0 || rel + m > 1024) {  // beyond the staged round: from memory
+            if ((int64_t)R + rel < 0) continue;  // a start before the slice (round 0): no occurrence
             hit = flat_verify(a.slice, R + rel, nd, m, upper);
             continue;
           }
@@ -1622,6 +1638,384 @@ __global__ __launch_bounds__(256) void k_flat_decide(EvalArgs a, uint32_t stage)
   }
   ok = ok && q == sec_end;
   if (!ok) {  // the exact kernel frames and evaluates this batch (no record starts from here)
+    a.rend[b] = 0xFFFFu;
+    const uint32_t i = atomicAdd(&a.list[0], 1u);
+    a.list[1 + i] = b;
+    return;
+  }
+  const uint8_t* h = S + pos;  // batch header (file format, batch.rs:163-180)
+  BatchStat st = {};
+  st.base_offset = (int64_t)rd_be(h, 8);
+  st.lod_in = (int32_t)rd_be(h + 23, 4);
+  st.first_ts = (int64_t)rd_be(h + 27, 8);
+  st.comp = (uint32_t)h[22] & 7u;
+  st.flags = BF_LAST_STAGE;
+  st.nkeep = st.nout = nkeep;
+  st.sec_len = (uint32_t)sec_len;
+  st.err_stage = 0xFFFFFFFFu;
+  a.bstat[b] = st;
+}
+
+// ---------------------------------------------------------------------------
+// Flat JSON path: filter_json (serde_json::from_slice::<StructuredLog>,
+// smartmodule/examples/filter_json/src/lib.rs:54-70) and the field projection
+// (map_json_project), with at most one substring stage and uppercase maps
+// beside them.  k_flat_scan<., kJson> streams the slice once and marks every
+// 16-byte chunk holding a JSON-interesting byte ('"', '\\', < 0x20, >= 0x80),
+// beside the needle's occurrence anchors when there is a substring stage;
+// k_fj_decide walks each batch's records with one thread (k_flat_decide's
+// pipelined framing) and parses every value as a flat object: bytes outside
+// strings one by one, strings by their first interesting byte, the clean
+// chunks between skipped with the bitmap (a clean chunk holds no quote, so the
+// string goes on through it).  Accepted is what the lean kernel's token DFA
+// accepts (fsg_json_dfa.h): { "key": value (, "key": value)* } with ' ' as the
+// only whitespace, keys and strings without escapes / control / high bytes,
+// level a LogLevel variant string, message a string, other values a string, a
+// JSON number or true / false / null, each field once; with a projection
+// (Map<String, Value>: every number is parsed) numbers are integers of at most
+// 18 characters other than -0, and the last member named by the field is the
+// output span.  Every byte of an accepted value was either examined or lies in
+// a clean chunk, so the value is ASCII (from_utf8 cannot fail).  Any other
+// record, and framing k_flat_decide would not take, defers the batch to k_eval.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t u4_dw(const uint4& v, uint32_t k) {
+  return (k & 2u) ? ((k & 1u) ? v.w : v.z) : ((k & 1u) ? v.y : v.x);
+}
+// 16 bits: the JSON-interesting bytes of a chunk
+__device__ __forceinline__ uint32_t fj_mask(const uint4& v) {
+  return nib4(fj_bytes(v.x)) | (nib4(fj_bytes(v.y)) << 4) | (nib4(fj_bytes(v.z)) << 8) | (nib4(fj_bytes(v.w)) << 12);
+}
+// a record's value seen through two cached chunks (the current one and the
+// value's last, loaded up front) and the interesting-chunk bitmap
+struct FjCur {
+  const uint8_t* S;
+  const unsigned long long* fbm;  // interleaved: the JSON word of round r at fbm[2 r + 1]
+  uint64_t c, tc;                 // chunk indices of v and tv
+  uint4 v, tv;
+  uint64_t wb;                    // the rounds wb, wb + 1 preloaded as j0, j1
+  unsigned long long j0, j1;
+  __device__ __forceinline__ uint4 chunk(uint64_t ci) {
+    if (ci == tc) return tv;
+    if (ci != c) {
+      v = *(const uint4*)(S + (ci << 4));
+      c = ci;
+    }
+    return v;
+  }
+  __device__ __forceinline__ uint32_t at(uint64_t p) {
+    const uint4 u = chunk(p >> 4);
+    return (u4_dw(u, (uint32_t)(p >> 2) & 3u) >> (8u * (uint32_t)(p & 3u))) & 0xFFu;
+  }
+  // the first chunk in [ci, lim) with an interesting byte, or lim
+  __device__ __forceinline__ uint64_t next(uint64_t ci, uint64_t lim) {
+    while (ci < lim) {
+      const uint64_t r = ci >> 6;
+      unsigned long long w = r == wb ? j0 : r == wb + 1 ? j1 : fbm[2 * r + 1];
+      w &= ~0ull << (ci & 63u);
+      if (w) {
+        const uint64_t x = (r << 6) + (uint64_t)__builtin_ctzll(w);
+        return x < lim ? x : lim;
+      }
+      ci = (r + 1) << 6;
+    }
+    return lim;
+  }
+};
+// the closing quote of the string whose bytes start at s (before ve), or ~0:
+// an escape, a control or high byte, or no quote before ve
+__device__ __forceinline__ uint64_t fj_str_end(FjCur& C, uint64_t s, uint64_t ve) {
+  uint64_t ci = s >> 4;
+  uint32_t m = fj_mask(C.chunk(ci)) & (0xFFFFu << (uint32_t)(s & 15u));
+  const uint64_t lim = (ve + 15) >> 4;
+  while (!m) {
+    ci = C.next(ci + 1, lim);
+    if (ci >= lim) return ~0ull;
+    m = fj_mask(C.chunk(ci));
+  }
+  const uint64_t x = (ci << 4) + (uint64_t)__builtin_ctz(m);
+  if (x >= ve || C.at(x) != 0x22u) return ~0ull;
+  return x;
+}
+__device__ __forceinline__ uint64_t fj_word(const uint8_t* S, uint64_t p, uint32_t n) {  // n <= 8 bytes at p
+  const uint64_t w = (uint64_t)ld_u32_at(S + p) | ((uint64_t)ld_u32_at(S + p + 4) << 32);
+  return n >= 8 ? w : (w & ((1ull << (8 * n)) - 1ull));
+}
+constexpr uint64_t fj_k(const char* t) {
+  uint64_t v = 0;
+  for (int i = 0; t[i]; i++) v |= (uint64_t)(uint8_t)t[i] << (8 * i);
+  return v;
+}
+__device__ __forceinline__ bool fj_digit(uint32_t c) { return c - 0x30u < 10u; }
+// one record's value [va, ve); false: the batch goes to k_eval.  fj: the
+// StructuredLog filter (lvl = 1 << LogLevel index); proj: the field fld[0, fl),
+// its last member's value span [fs, fe) when found
+__device__ bool fj_walk(FjCur& C, uint64_t va, uint64_t ve, bool fj, bool proj, const uint8_t* fld, uint32_t fl,
+                        uint32_t& lvl, bool& found, uint64_t& fs, uint64_t& fe) {
+  const uint8_t* S = C.S;
+  uint64_t p = va;
+  uint32_t nlv = 0, nmsg = 0;
+  lvl = 0;
+  found = false;
+  auto sp = [&]() {
+    while (p < ve && C.at(p) == 0x20u) p++;
+  };
+  sp();
+  if (p >= ve || C.at(p) != '{') return false;
+  p++;
+  for (;;) {
+    sp();
+    if (p >= ve || C.at(p) != '"') return false;  // (an empty object goes to k_eval too)
+    const uint64_t k0 = p + 1, k1 = fj_str_end(C, k0, ve);
+    if (k1 == ~0ull) return false;
+    const uint32_t kn = (uint32_t)(k1 - k0);
+    p = k1 + 1;
+    sp();
+    if (p >= ve || C.at(p) != ':') return false;
+    p++;
+    sp();
+    if (p >= ve) return false;
+    uint32_t key = 0;  // 1 level, 2 message
+    if (fj && (kn == 5 || kn == 7)) {
+      const uint64_t w = fj_word(S, k0, kn);
+      key = kn == 5 && w == fj_k("level") ? 1u : kn == 7 && w == fj_k("message") ? 2u : 0u;
+    }
+    bool fhit = false;
+    if (proj && kn == fl) {
+      fhit = true;
+      for (uint32_t t = 0; fhit && t < fl; t += 4) {
+        const uint32_t mk = fl - t >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (fl - t))) - 1u);
+        fhit = ((ld_u32_at(S + k0 + t) ^ ld_u32_at(fld + t)) & mk) == 0u;
+      }
+    }
+    const uint64_t v0 = p;
+    const uint32_t c = C.at(p);
+    if (c == '"') {
+      const uint64_t s1 = fj_str_end(C, p + 1, ve);
+      if (s1 == ~0ull) return false;
+      if (key == 1) {
+        const uint32_t n = (uint32_t)(s1 - p - 1);
+        const uint64_t w = n == 4 || n == 5 ? fj_word(S, p + 1, n) : 0ull;
+        const uint32_t v = n == 5 && w == fj_k("debug") ? 1u : n == 4 && w == fj_k("info") ? 2u
+                         : n == 4 && w == fj_k("warn") ? 4u : n == 5 && w == fj_k("error") ? 8u : 0u;
+        if (!v || nlv++) return false;  // unknown variant / duplicate field: serde errors
+        lvl = v;
+      } else if (key == 2) {
+        if (nmsg++) return false;
+      }
+      p = s1 + 1;
+    } else {
+      if (key) return false;  // level / message not a string: invalid type
+      if (c == '-' || fj_digit(c)) {
+        const bool neg = c == '-';
+        if (neg) p++;
+        if (p >= ve) return false;
+        const uint32_t d = C.at(p);
+        if (d == '0') {
+          p++;
+          if (p < ve && fj_digit(C.at(p))) return false;  // a leading zero
+        } else if (fj_digit(d)) {
+          while (++p < ve && fj_digit(C.at(p))) {
+          }
+        } else {
+          return false;
+        }
+        bool real = false;
+        if (p < ve && C.at(p) == '.') {
+          real = true;
+          if (++p >= ve || !fj_digit(C.at(p))) return false;
+          while (++p < ve && fj_digit(C.at(p))) {
+          }
+        }
+        if (p < ve && (C.at(p) | 0x20u) == 'e') {
+          real = true;
+          if (++p < ve && (C.at(p) == '+' || C.at(p) == '-')) p++;
+          if (p >= ve || !fj_digit(C.at(p))) return false;
+          while (++p < ve && fj_digit(C.at(p))) {
+          }
+        }
+        // a projection parses every number into a Value: integers of <= 18
+        // characters only (no f64 reading, no -0)
+        if (proj && (real || p - v0 > 18 || (neg && p - v0 == 2 && d == '0'))) return false;
+      } else {
+        const uint32_t n = c == 'f' ? 5u : 4u;
+        if (p + n > ve) return false;
+        const uint64_t w = fj_word(S, p, n);
+        if (!(c == 't' ? w == fj_k("true") : c == 'f' ? w == fj_k("false") : c == 'n' && w == fj_k("null")))
+          return false;
+        p += n;
+      }
+    }
+    if (fhit) {
+      found = true;
+      fs = v0;
+      fe = p;
+    }
+    sp();
+    if (p >= ve) return false;
+    const uint32_t e = C.at(p++);
+    if (e == '}') break;
+    if (e != ',') return false;
+  }
+  sp();
+  if (p != ve) return false;                       // trailing characters
+  return !fj || (nlv == 1 && nmsg == 1);           // a missing field: serde error
+}
+__global__ __launch_bounds__(256) void k_fj_decide(EvalArgs a) {
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= a.nbatches) return;
+  // a.flat_st: substring stage (0xFF none) | needle length << 8 | filter_json << 16 | projection << 17 | its stage << 24
+  const uint32_t fst = a.flat_st;
+  const uint32_t sub = fst & 0xFFu, m = (fst >> 8) & 0xFFu;
+  const bool has_sub = sub != 0xFFu, fj = (fst >> 16) & 1u, proj = (fst >> 17) & 1u;
+  const bool kLong = m >= 7;
+  const StageDesc& sd = a.chain->st[has_sub ? sub : 0];
+  const bool upper = has_sub && sd.in_type == VT_SRC_UPPER;
+  const bool out_upper = a.chain->out_type == VT_SRC_UPPER;
+  const uint8_t* nd = a.blob + sd.needle;
+  const StageDesc& pd = a.chain->st[fst >> 24];
+  const uint8_t* fld = a.blob + pd.needle;
+  const uint32_t fl = proj ? pd.needle_len : 0u;
+  const unsigned long long* hit_bm = a.fbm;  // interleaved (k_flat_scan): occurrence word w at [2 w], JSON word at [2 w + 1]
+  const uint8_t* S = a.slice;
+  const uint64_t pos = a.bpos[b];
+  const uint64_t nxt = b + 1 < a.nbatches ? a.bpos[b + 1] : a.slice_len;
+  const uint64_t rb = a.rbase[b], rn = (b + 1 < a.nbatches ? a.rbase[b + 1] : a.nrec) - rb;
+  const uint64_t al = pos & ~15ull;
+  uint64_t wl = nxt > al ? nxt - al : 0;
+  if (wl > (uint64_t)kLeanWin) wl = kLeanWin;
+  const uint64_t wlen = (wl + 15) & ~15ull;
+  const uint32_t batch_len = __builtin_bswap32(ld_u32_at(S + pos + 8));
+  const uint64_t sec0 = pos + 57, sec_end = pos + 12 + (uint64_t)batch_len;
+  const uint64_t sec_len = sec_end - sec0;
+  const int32_t count = sec_len >= 4 ? (int32_t)__builtin_bswap32(ld_u32_at(S + sec0)) : -1;
+  bool ok = sec_len >= 4 && sec_end - al <= wlen && count >= 0 && count <= kLeanMaxR && (uint64_t)count == rn;
+  uint32_t nkeep = 0;
+  uint64_t q = sec0 + 4;  // absolute start of record n
+  FlatHdr H = flat_hdr(S, ok && count > 0 ? q : sec0);
+  FjCur C;
+  C.S = S;
+  C.fbm = a.fbm;
+  C.c = ~0ull;
+  for (int32_t n = 0; ok && n < count; n++) {
+    uint32_t o = (uint32_t)(q & 3), nb;
+    int64_t len, ts, od, kl = 0, vlen, hdr;
+    nb = var4(flat_at(H, o), len);
+    ok = nb != 0 && len >= 0;
+    const uint64_t end = q + nb + (uint64_t)len;  // where the record ends (Record::decode's length)
+    ok = ok && end <= sec_end;
+    if (!ok) break;
+    const FlatHdr Hn = flat_hdr(S, n + 1 < count ? end : q);  // the next record's header, in flight now
+    o += nb;
+    const uint8_t attr = (uint8_t)flat_at(H, o);
+    o += 1;
+    nb = var4(flat_at(H, o), ts);
+    ok = nb != 0;
+    o += nb;
+    nb = var4(flat_at(H, o), od);
+    ok = ok && nb != 0;
+    o += nb;
+    const uint8_t tag = (uint8_t)flat_at(H, o);
+    o += 1;
+    ok = ok && tag <= 1;
+    if (!ok) break;
+    uint64_t p = (q & ~3ull) + o, kpos = 0;
+    uint32_t klen = 0;
+    if (tag == 1) {
+      nb = var4(flat_at(H, o), kl);
+      ok = nb != 0 && kl >= 0;
+      p += nb;
+      kpos = p;
+      klen = (uint32_t)kl;
+      p += klen;
+    }
+    nb = var4(tag == 1 ? ld_u32_at(S + p) : flat_at(H, o), vlen);
+    ok = ok && nb != 0 && vlen >= 0;
+    const uint64_t va = p + nb, ve = va + (uint64_t)vlen;
+    ok = ok && ve <= end && ve > va;  // (an empty value is a serde error: k_eval)
+    if (!ok) break;
+    // every load of this record at once: trailer, bitmap words, the value's first and last chunks
+    const uint32_t tw = ld_u32_at(S + ve);
+    const uint64_t c0 = va >> 4;
+    const uint64_t wb = c0 >> 6;  // first bitmap round touching the value
+    const ulonglong2 bw0 = *(const ulonglong2*)(a.fbm + 2 * wb), bw1 = *(const ulonglong2*)(a.fbm + 2 * wb + 2);
+    C.tc = (ve - 1) >> 4;
+    C.tv = *(const uint4*)(S + (C.tc << 4));
+    if (C.c != c0 && c0 != C.tc) {
+      C.v = *(const uint4*)(S + (c0 << 4));
+      C.c = c0;
+    }
+    C.wb = wb;
+    C.j0 = bw0.y;
+    C.j1 = bw1.y;
+    nb = var4(tw, hdr);
+    ok = nb != 0 && ve + nb == end;
+    if (!ok) break;
+    bool keep = true;
+    if (has_sub) {  // an occurrence starting in [va, ve - m] (k_flat_decide's anchors)
+      const unsigned long long mb0 = bw0.x, mb1 = bw1.x;
+      auto bits_any = [&](uint64_t x0, uint64_t x1) {
+        if (x1 <= x0) return false;
+        if (x1 > (wb + 2) << 6) return flat_any(hit_bm, x0, x1);
+        const uint64_t lo = x0 - (wb << 6), hi = x1 - (wb << 6);  // in [0, 128]
+        const unsigned long long m0 = (lo < 64 ? (~0ull << lo) : 0ull) & (hi >= 64 ? ~0ull : ((1ull << hi) - 1ull));
+        const unsigned long long m1 = (hi > 64 ? (hi >= 128 ? ~0ull : ((1ull << (hi - 64)) - 1ull)) : 0ull) &
+                                      (lo > 64 ? (~0ull << (lo - 64)) : ~0ull);
+        return ((mb0 & m0) | (mb1 & m1)) != 0ull;
+      };
+      bool match = false;
+      if ((uint64_t)vlen >= m) {
+        const uint64_t sl = ve - m;
+        const uint64_t blo = kLong ? 3 : 0, bhi = kLong ? 12 : 15;
+        const uint64_t j0 = (va + blo + 15) >> 4;
+        const uint64_t j1 = sl >= bhi ? ((sl - bhi) >> 4) + 1 : 0;
+        match = j0 < j1 && bits_any(j0, j1);
+        if (!match) {
+          const uint64_t e0 = va >= bhi ? (va - bhi + 15) >> 4 : 0, e1 = (sl + blo) >> 4;
+          for (uint64_t c = e0; c <= e1 && !match; c++) {
+            if (c >= j0 && c < j1) {
+              c = j1 - 1;
+              continue;
+            }
+            const uint64_t r = c - (wb << 6);
+            const bool bt = c >= (wb << 6) && r < 128 ? (((r < 64 ? mb0 : mb1) >> (r & 63)) & 1ull) != 0ull
+                                                      : bm_bit(hit_bm, c);
+            if (!bt) continue;
+            const uint64_t lo = (c << 4) >= va + blo ? (c << 4) - blo : va;
+            const uint64_t hi = (c << 4) + bhi <= sl ? (c << 4) + bhi : sl;
+            for (uint64_t s0 = lo; s0 <= hi && !match; s0++) match = flat_verify(S, s0, nd, m, upper);
+          }
+        }
+      }
+      keep = match;
+    }
+    uint32_t lvl = 0;
+    bool found = false;
+    uint64_t fs = va, fe = ve;
+    ok = fj_walk(C, va, ve, fj, proj, fld, fl, lvl, found, fs, fe);
+    if (!ok) break;
+    keep = keep && (!fj || lvl > 1u) && (!proj || found);  // level > Debug
+    if (keep) {
+      KeptRec d;
+      d.src = q;
+      d.vpos = fs;
+      d.kpos = tag ? kpos : 0;
+      d.od = od;
+      d.ts = ts;
+      d.hdr = hdr;
+      d.vlen = (uint32_t)(fe - fs);
+      d.klen = klen;
+      d.ival = 0;
+      d.mode = out_upper ? KM_UPPER : KM_COPY;
+      d.has_key = tag;
+      d.attr = attr;
+      d.pad = 0;
+      a.desc[rb + nkeep++] = d;
+    }
+    q = end;
+    H = Hn;
+  }
+  ok = ok && q == sec_end;
+  if (!ok) {  // the exact kernel frames and evaluates this batch
     a.rend[b] = 0xFFFFu;
     const uint32_t i = atomicAdd(&a.list[0], 1u);
     a.list[1 + i] = b;
@@ -1901,6 +2295,51 @@ void launch_eval_flat(const EvalArgs& a, uint32_t flat_st, hipStream_t s) {
     hipLaunchKernelGGL(k_flat_scan<false>, dim3(g1), dim3(256), 0, s, a, stage);
     hipLaunchKernelGGL(k_flat_decide<false>, dim3(g2), dim3(256), 0, s, a, stage);
   }
+}
+
+int fjson_flags(const ChainDesc& ch, uint32_t ops) {
+  const uint32_t jops = (1u << OP_FILTER_JSON) | (1u << OP_PROJECT);
+  if (!(ops & jops) || (ops & ~((1u << OP_CONTAINS) | (1u << OP_MAP_UPPER) | jops))) return -1;
+  int sub = -1, fjs = -1, pjs = -1;
+  for (uint32_t k = 0; k < ch.nstages; k++) {
+    const StageDesc& sd = ch.st[k];
+    if (pjs >= 0 && sd.op != OP_MAP_UPPER) return -1;  // after a projection: uppercase maps only
+    if (sd.op == OP_CONTAINS) {
+      if (sub >= 0) return -1;
+      sub = (int)k;
+    } else if (sd.op == OP_FILTER_JSON || sd.op == OP_PROJECT) {
+      if (sd.in_type != VT_SRC) return -1;
+      if (sd.op == OP_FILTER_JSON) {
+        if (fjs >= 0) return -1;
+        fjs = (int)k;
+      } else {
+        if (sd.needle_len > (uint32_t)kLeanNeedle) return -1;
+        pjs = (int)k;
+      }
+    }
+  }
+  uint32_t m = 0;
+  if (sub >= 0) {
+    m = ch.st[sub].needle_len;
+    if (m < 4 || m > (uint32_t)kLeanNeedle) return -1;
+  }
+  return (int)((sub >= 0 ? (uint32_t)sub : 0xFFu) | (m << 8) | ((fjs >= 0 ? 1u : 0u) << 16) |
+               ((pjs >= 0 ? 1u : 0u) << 17) | ((uint32_t)(pjs >= 0 ? pjs : 0) << 24));
+}
+
+void launch_eval_fjson(const EvalArgs& a, hipStream_t s) {
+  if (!a.nbatches) return;
+  const uint32_t sub = a.flat_st & 0xFFu, m = (a.flat_st >> 8) & 0xFFu;
+  const uint64_t waves = (a.fbm_words + kFlatRounds - 1) / kFlatRounds;
+  const uint32_t g1 = (uint32_t)std::max<uint64_t>(std::min<uint64_t>((waves + 3) / 4, 4096), 1);
+  const uint32_t g2 = (a.nbatches + 255) / 256;
+  if (sub == 0xFFu)
+    hipLaunchKernelGGL((k_flat_scan<true, true, true>), dim3(g1), dim3(256), 0, s, a, 0u);
+  else if (m >= 7)
+    hipLaunchKernelGGL((k_flat_scan<true, true, false>), dim3(g1), dim3(256), 0, s, a, sub);
+  else
+    hipLaunchKernelGGL((k_flat_scan<false, true, false>), dim3(g1), dim3(256), 0, s, a, sub);
+  hipLaunchKernelGGL(k_fj_decide, dim3(g2), dim3(256), 0, s, a);
 }
 
 void launch_eval_lean(const EvalArgs& a, uint32_t ops, hipStream_t s) {

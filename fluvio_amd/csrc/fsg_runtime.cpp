@@ -550,6 +550,7 @@ struct fsg_chain {
   DevBuf arr_b, arr_bm;  // lean array_map statistics and element bitmaps (per batch)
   DevBuf fbm;            // flat substring path: occurrence / high-byte bits per 16-byte chunk
   bool no_flat = getenv("FSG_NO_FLAT") != nullptr;  // A/B: the flat path off (k_eval_lean instead)
+  bool no_fjson = getenv("FSG_NO_FJSON") != nullptr;  // A/B: the flat JSON path off (k_eval_lean instead)
   bool no_int = getenv("FSG_NO_INT") != nullptr;    // A/B: integer chains through k_eval alone
   // the one-batch process() path (k_one): zeros for bpos / rbase, the device
   // block Plan | BatchStat | Mins | output batch, and coherent pinned memory
@@ -2125,14 +2126,22 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   // one substring stage: the flat path (the slice streamed once as bytes,
   // per-16-byte-chunk occurrence / high-byte bits, then one wave per batch decides)
   const int fst = lean ? flat_stage(c->hdesc, ops) : -1;
-  bool flat = false;
-  if (fst >= 0 && !c->no_flat) {
+  // filter_json / projection (with at most one substring stage): the flat JSON path
+  const int fjf = lean && fst < 0 && !c->no_fjson ? fjson_flags(c->hdesc, ops) : -1;
+  bool flat = false, fjson = false;
+  if ((fst >= 0 || fjf >= 0) && !c->no_flat) {
     ea.fbm_words = (s->len + 1023) / 1024;
-    flat = c->fbm.ensure((size_t)ea.fbm_words * 16 + 32) == hipSuccess;  // + the pair past the last (k_flat_decide)
+    const bool have = c->fbm.ensure((size_t)ea.fbm_words * 16 + 32) == hipSuccess;  // + the pair past the last
     (void)hipGetLastError();
-    if (flat) {
+    if (have) {
       ea.fbm = c->fbm.as<unsigned long long>();
-      ea.flat_st = (uint32_t)fst | (c->hdesc.st[fst].needle_len << 8);
+      if (fst >= 0) {
+        flat = true;
+        ea.flat_st = (uint32_t)fst | (c->hdesc.st[fst].needle_len << 8);
+      } else {
+        fjson = true;
+        ea.flat_st = (uint32_t)fjf;
+      }
     }
   }
   // integer stages over decimal values (filter_odd / map_double / filter_map /
@@ -2163,7 +2172,8 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     }
   }
   if (lean || arr || ints) HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
-  launch_eval(ea, ops, flat ? EVAL_FLAT : lean ? EVAL_LEAN : arr ? EVAL_ARRAY : ints ? EVAL_INT : EVAL_EXACT, st);
+  launch_eval(ea, ops, flat ? EVAL_FLAT : fjson ? EVAL_FJSON : lean ? EVAL_LEAN : arr ? EVAL_ARRAY : ints ? EVAL_INT : EVAL_EXACT,
+              st);
   HIPCHK(hipGetLastError());
   if (c->timed) HIPCHK(hipEventRecord(c->ev[1], st));
   launch_mins(ea.bstat, nb, ea.mins, st);
@@ -2363,6 +2373,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   pa.tail_status = s->tail_status;
   pa.empty_chain = empty_chain_io ? 1 : 0;
   pa.has_agg = has_agg;
+  pa.seg = so ? 1 : 0;
   pa.acc0 = acc0;
   launch_plan(pa, st);
   c->last_pa = pa;
@@ -2383,7 +2394,8 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   if (dedup) HIPCHK(hipMemcpyAsync(sfs, sfa.scal, sizeof sfs, hipMemcpyDeviceToHost, st));
   HIPCHK(wait_stream(st));
   memcpy(&c->hplan, c->hpin.p, sizeof(Plan));
-  c->last.eval_path = flat ? FSG_EVAL_FLAT : lean ? FSG_EVAL_LEAN : arr ? FSG_EVAL_ARRAY : ints ? FSG_EVAL_INT : FSG_EVAL_EXACT;
+  c->last.eval_path = flat ? FSG_EVAL_FLAT : fjson ? FSG_EVAL_FJSON : lean ? FSG_EVAL_LEAN : arr ? FSG_EVAL_ARRAY
+                    : ints ? FSG_EVAL_INT : FSG_EVAL_EXACT;
   c->last.deferred = 0;
   if (lean || arr || ints) memcpy(&c->last.deferred, (const uint8_t*)c->hpin.p + sizeof(Plan), sizeof(uint32_t));
   if (dedup) {

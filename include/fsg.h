@@ -161,7 +161,7 @@ typedef struct fsg_timings {
   uint64_t out_bytes;     /* algorithmic bytes written (output batch) */
   uint64_t n_batches;
   uint64_t n_records_in;
-  uint32_t eval_path;     /* FSG_EVAL_EXACT / _LEAN / _ARRAY / _FLAT: the first evaluation kernel */
+  uint32_t eval_path;     /* FSG_EVAL_*: the first evaluation kernel */
   uint32_t deferred;      /* batches that kernel handed to the exact kernel (non-ASCII, odd framing, ...) */
   float text_ms;          /* plan end to write start: aggregate texts, the aggregate-json order walk, the header */
   float order_ms;         /* the aggregate-json order walk kernel alone (a group call: the group's one launch) */
@@ -174,6 +174,9 @@ typedef struct fsg_timings {
                             decides (k_flat_decide), deferred batches through k_eval */
 #define FSG_EVAL_INT 5   /* integer stages over decimal values: k_eval_int (workgroup per batch, record starts
                             kept with the slice), deferred batches through k_eval */
+#define FSG_EVAL_FJSON 6 /* filter_json / field projection (+ one substring stage): the slice streamed as bytes
+                            (k_flat_scan<., kJson>: JSON-interesting chunks), a thread per batch parses the
+                            records' values as flat objects (k_fj_decide), deferred batches through k_eval */
 
 const char *fsg_last_error_message(void);
 int fsg_abi_version(void);

@@ -580,6 +580,37 @@ def test_unicode_word_boundaries(engine):
     check_batch(engine, chain, b.encode())
 
 
+def test_unsupported_mid_stream_leaves_state(engine):
+    """FSG_E_UNSUPPORTED in batch 1 of 3 (a (?-u) \\b on a non-ASCII value):
+    the caller falls back and replays the input, so the aggregate accumulator
+    and the dedup set must not move past batch 0 (the advisor's round-5 case)."""
+    rx = ("regex-filter", {"regex": r"(?-u:\b)\d"}, None)
+    sl = b""
+    for base, vals in ((0, ["5", "7"]), (10, ["8", "\u00e95"]), (20, ["9"])):
+        b = P.Batch(base_offset=base)
+        for v in vals:
+            b.add_record(P.Record.new(v.encode()))
+        sl += b.encode()
+    b0 = P.Batch(base_offset=0)
+    for v in ("5", "7"):
+        b0.add_record(P.Record.new(v.encode()))
+    first = b0.encode()
+    assert sl.startswith(first)
+    g = gpu_chain(engine, [rx, ("aggregate-sum", {}, b"100")])
+    with pytest.raises(Unsupported):
+        g.process_batch(sl)
+    assert g.accumulator(1) == b"100"
+    o = orc_chain([rx, ("aggregate-sum", {}, b"100")])
+    assert g.process_batch(first).raw == o.process_batch(first)["bytes"]
+    assert g.accumulator(1) == o.accumulator(1) == b"112"
+    h = gpu_chain(engine, [rx, ("filter_hashset", {}, None)])
+    with pytest.raises(Unsupported):
+        h.process_batch(sl)
+    oh = orc_chain([rx, ("filter_hashset", {}, None)])
+    r = h.process_batch(first)
+    assert r.raw == oh.process_batch(first)["bytes"] and r.n_records == 2
+
+
 def test_resident_slice_matches_process_batch(engine):
     sl = synth.make_slice(2, 4000)
     ch = gpu_chain(engine, CHAINS["filter_then_map"])
@@ -1745,6 +1776,27 @@ def test_flat_edges_exhaustive(engine):
         check_batch(engine, [("filter_init", {"key": needle}, None)], out)
         g.process_batch(out)
         assert g.last_timings()["eval_path"] == 4
+
+
+@pytest.mark.parametrize("d", [1, 2, 3])
+def test_flat_scan_slice_start_candidate(engine, d):
+    """The slice's first aligned dword (the first batch's base offset, big
+    endian) equals the needle's 4-gram at offset d: the long-needle candidate
+    would start d bytes before the slice.  No occurrence, no read before it."""
+    needle =("wvu"[: d] + "ABCD" + "qrstu")[: max(7, d + 4)]
+    assert needle[d:d + 4] == "ABCD"
+    b = P.Batch(base_offset=0x41424344 << 32)
+    for i in range(20):
+        b.add_record(P.Record.new(("ABCD" + "z" * i + (needle if i % 3 == 0 else "")).encode()))
+    b2 = P.Batch(base_offset=(0x41424344 << 32) + 100)  # two batches: the flat path (one takes k_eval)
+    b2.add_record(P.Record.new(needle.encode()))
+    sl = b.encode() + b2.encode()
+    assert sl[:4] == b"ABCD"
+    chain = [("filter_init", {"key": needle}, None)]
+    check_batch(engine, chain, sl)
+    g = gpu_chain(engine, chain)
+    g.process_batch(sl)
+    assert g.last_timings()["eval_path"] == 4
 
 
 @pytest.mark.parametrize("nr", range(2, 9))
