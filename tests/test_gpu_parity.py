@@ -777,6 +777,106 @@ def test_filter_json_synthetic_logs(engine):
     assert 0 < out.n_records < 3000
 
 
+FJ_CHAINS = [
+    [("filter_json", {}, None)],
+    [("filter_json", {}, None), ("map", {}, None)],
+    [("filter_init", {"key": "timeout"}, None), ("filter_json", {}, None)],
+    [("filter_json", {}, None), ("filter_init", {"key": "tim"}, None)],  # short needle: lean kernel, not flat
+    [("filter_init", {"key": "timeout"}, None), ("map_json_project", {"field": "message"}, None), ("map", {}, None)],
+    [("map_json_project", {}, None)],
+    [("map_json_project", {"field": "ts"}, None)],
+    [("filter_init", {"key": "warn"}, None), ("map_json_project", {"field": "level"}, None)],
+    [("filter_json", {}, None), ("map_json_project", {"field": "host"}, None)],
+]
+
+
+def _fj_docs(rng):
+    """Values for the flat JSON path: ones it decides (flat objects, ' ' only,
+    every value kind, strings across 16-byte chunks and 1 KiB rounds) beside
+    ones it must hand to k_eval (escapes, tabs, nesting, floats under a
+    projection, duplicates, missing fields, bad variants, trailing bytes,
+    non-ASCII, unterminated strings)."""
+    lv = ["debug", "info", "warn", "error"]
+    good, odd = [], []
+    for i in range(400):
+        msg = "".join(rng.choice("abcdefgh ij") for _ in range(rng.choice([0, 1, 5, 14, 15, 16, 17, 31, 63, 200,
+                                                                              1000, 1100, 2500])))
+        if rng.random() < 0.4:
+            msg = msg[: len(msg) // 2] + "timeout" + msg[len(msg) // 2:]
+        sp = " " * rng.choice([0, 0, 0, 1, 3])
+        extra = rng.choice(['"ts":%d' % rng.randrange(10**9), '"ok":true', '"no":false', '"z":null',
+                            '"n":-%d' % rng.randrange(1, 10**6), '"s":"svc-%02d"' % rng.randrange(100), '"e":""'])
+        members = ['"level"%s:%s"%s"' % (sp, sp, rng.choice(lv)), '"message":%s"%s"' % (sp, msg), extra,
+                   '"host":"h-%04d"' % rng.randrange(10**4)]
+        rng.shuffle(members)
+        pre = " " * rng.randrange(0, 18)
+        good.append((pre + "{" + sp + ("," + sp).join(members) + sp + "}" + sp).encode())
+    odd += [b'{"level":"info","message":"a\\nb"}', b'{"level":"info","message":"a\tb"}',
+            b'{"level":"info","message":"x","n":1.5}', b'{"level":"info","message":"x","n":2e3}',
+            b'{"level":"info","message":"x","n":-0}', b'{"level":"info","message":"x","n":01}',
+            b'{"level":"info","message":"x","o":{"a":1}}', b'{"level":"info","message":"x","a":[1,2]}',
+            b'{"level":"info","level":"warn","message":"x"}', b'{"message":"x"}', b'{"level":"info"}',
+            b'{"level":"INFO","message":"x"}', b'{"level":1,"message":"x"}', b'{"level":"info","message":5}',
+            b'{"level":"info","message":"x"} x', b'{"level":"info","message":"x"}}', b'{}', b'',
+            b'["info","x"]', b'{"level":"info","message":"caf\xc3\xa9"}', b'{"level":"info","message":"x',
+            b'{"level":"info","message":"x","t":tru}', b'{"level":"info","message":"x","t":truex}',
+            b'{"level":"info","message":"x","n":12345678901234567890}', b'{"level":"info","message":"x",}',
+            b'{"level":"info" "message":"x"}', b'{"level":"info","message":"x"\n}', b'{"\xff":1}',
+            b'{"level":"info","message":"x","n":-}', b'{"level":"info","message":"x","n":1.}',
+            b'{"level":"info","message":"x","n":1e}', b'{"message":"timeout","message":"again"}']
+    return good, odd
+
+
+@pytest.mark.parametrize("ci", range(len(FJ_CHAINS)))
+def test_fjson_path_parity(engine, ci):
+    """The flat JSON path (FSG_EVAL_FJSON: k_flat_scan's JSON-interesting
+    chunks + k_fj_decide) against the oracle: clean batches it decides alone,
+    batches with one odd document (deferred whole to k_eval), strings that end
+    at every offset of a 16-byte chunk and messages longer than the two
+    preloaded bitmap rounds."""
+    import random
+    rng = random.Random(77 + ci)
+    good, odd = _fj_docs(rng)
+    sl, base = b"", 0
+    for k in range(90):
+        b = P.Batch(base_offset=base)
+        n = rng.choice([1, 2, 9, 16, 33, 64])
+        for j in range(n):
+            doc = rng.choice(odd) if (k % 5 == 4 and j == n // 2) else rng.choice(good)
+            b.add_record(P.Record.new_key_value(b"k%d" % j if j % 3 == 0 else None, doc))
+        sl += b.encode()
+        base += n
+    chain = FJ_CHAINS[ci]
+    check_batch(engine, chain, sl)
+    g = gpu_chain(engine, chain)
+    g.process_batch(sl)
+    t = g.last_timings()
+    short = any(m[0] == "filter_init" and len(m[1]["key"]) < 4 for m in chain)
+    assert t["eval_path"] == (1 if short else 6), t
+    if not short:
+        assert 0 < t["deferred"] < t["n_batches"], t
+
+
+def test_fjson_string_ends_every_offset(engine):
+    """Strings ending at each byte of a chunk, keys and values straddling
+    chunk and 1 KiB round edges, values starting at every alignment."""
+    sl, base = b"", 0
+    for shift in range(0, 48):
+        b = P.Batch(base_offset=base)
+        for i in range(20):
+            msg = "m" * (i * 7 + shift)
+            doc = ('{"level":"%s","message":"%s","n":%d}' % (["debug", "info"][i % 2], msg, i)).encode()
+            b.add_record(P.Record.new(b" " * (shift % 5) + doc))
+        sl += b.encode()
+        base += 20
+    for chain in ([("filter_json", {}, None)], [("map_json_project", {}, None), ("map", {}, None)]):
+        check_batch(engine, chain, sl)
+        g = gpu_chain(engine, chain)
+        g.process_batch(sl)
+        t = g.last_timings()
+        assert t["eval_path"] == 6 and t["deferred"] == 0, t
+
+
 # ---------------------------------------------------------------------------
 # k_eval_lean (one wave per batch) vs the exact path: every needle-length mode,
 # upper-cased scans, keys, empty values, needles at value edges or spanning
