@@ -1678,33 +1678,91 @@ __global__ __launch_bounds__(256) void k_flat_decide(EvalArgs a, uint32_t stage)
 // a clean chunk, so the value is ASCII (from_utf8 cannot fail).  Any other
 // record, and framing k_flat_decide would not take, defers the batch to k_eval.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t u4_dw(const uint4& v, uint32_t k) {
-  return (k & 2u) ? ((k & 1u) ? v.w : v.z) : ((k & 1u) ? v.y : v.x);
+__device__ __forceinline__ uint32_t u4_dw(uint4 v, uint32_t k) {  // (values, not lvalues: no memory select)
+  const uint32_t x = v.x, y = v.y, z = v.z, w = v.w;
+  return (k & 2u) ? ((k & 1u) ? w : z) : ((k & 1u) ? y : x);
 }
 // 16 bits: the JSON-interesting bytes of a chunk
 __device__ __forceinline__ uint32_t fj_mask(const uint4& v) {
   return nib4(fj_bytes(v.x)) | (nib4(fj_bytes(v.y)) << 4) | (nib4(fj_bytes(v.z)) << 8) | (nib4(fj_bytes(v.w)) << 12);
 }
-// a record's value seen through two cached chunks (the current one and the
-// value's last, loaded up front) and the interesting-chunk bitmap
+__device__ __forceinline__ uint4 sel4(uint4 a0, uint4 a1, uint4 a2, uint4 a3, uint32_t k) {
+  uint4 r;
+  r.x = u4_dw(make_uint4(a0.x, a1.x, a2.x, a3.x), k);
+  r.y = u4_dw(make_uint4(a0.y, a1.y, a2.y, a3.y), k);
+  r.z = u4_dw(make_uint4(a0.z, a1.z, a2.z, a3.z), k);
+  r.w = u4_dw(make_uint4(a0.w, a1.w, a2.w, a3.w), k);
+  return r;
+}
+// a record's value seen through registers: the 64 bytes from its first chunk
+// (hd), the 64 bytes up to its last chunk (tl), both loaded with the record's
+// header, and one more chunk loaded on demand; plus the interesting-chunk bitmap
 struct FjCur {
   const uint8_t* S;
   const unsigned long long* fbm;  // interleaved: the JSON word of round r at fbm[2 r + 1]
-  uint64_t c, tc;                 // chunk indices of v and tv
-  uint4 v, tv;
+  uint64_t hc, tc;                // first chunk of hd / tl
+  uint4 h0, h1, h2, h3, t0, t1, t2, t3;
+  uint64_t c;                     // chunk index of v (the current chunk) and m its interesting bytes
+  uint4 v;
+  uint32_t m;
+  bool mv;                        // m computed
   uint64_t wb;                    // the rounds wb, wb + 1 preloaded as j0, j1
   unsigned long long j0, j1;
   __device__ __forceinline__ uint4 chunk(uint64_t ci) {
-    if (ci == tc) return tv;
     if (ci != c) {
-      v = *(const uint4*)(S + (ci << 4));
+      if (ci - hc < 4) v = sel4(h0, h1, h2, h3, (uint32_t)(ci - hc));
+      else if (ci - tc < 4) v = sel4(t0, t1, t2, t3, (uint32_t)(ci - tc));
+      else v = *(const uint4*)(S + (ci << 4));
       c = ci;
+      mv = false;
     }
     return v;
+  }
+  __device__ __forceinline__ uint32_t mask(uint64_t ci) {  // interesting bytes of chunk ci
+    chunk(ci);
+    if (!mv) {
+      m = fj_mask(v);
+      mv = true;
+    }
+    return m;
   }
   __device__ __forceinline__ uint32_t at(uint64_t p) {
     const uint4 u = chunk(p >> 4);
     return (u4_dw(u, (uint32_t)(p >> 2) & 3u) >> (8u * (uint32_t)(p & 3u))) & 0xFFu;
+  }
+  // the n <= 8 bytes at p as a little-endian word (from registers)
+  __device__ __forceinline__ uint64_t word(uint64_t p, uint32_t n) {
+    const uint4 u = chunk(p >> 4);
+    const uint32_t o = (uint32_t)(p & 15u);
+    const uint4 u2 = o + n > 16 ? chunk((p >> 4) + 1) : u;
+    const uint32_t k = o >> 2;
+    const uint32_t e0 = u4_dw(u, k);
+    const uint32_t e1 = k < 3 ? u4_dw(u, k + 1) : u2.x;
+    const uint32_t e2 = k < 2 ? u4_dw(u, k + 2) : u4_dw(u2, k - 2);
+    const uint32_t sh = o & 3u;
+    const uint64_t w = (uint64_t)__builtin_amdgcn_alignbyte(e1, e0, sh) |
+                       ((uint64_t)__builtin_amdgcn_alignbyte(e2, e1, sh) << 32);
+    return n >= 8 ? w : (w & ((1ull << (8 * n)) - 1ull));
+  }
+  // the first position >= p holding a byte that is not an ASCII digit
+  __device__ __forceinline__ uint64_t digits_end(uint64_t p, uint64_t ve) {
+    for (;;) {
+      const uint4 u = chunk(p >> 4);
+      uint32_t nd = 0;
+#pragma unroll
+      for (int d = 0; d < 4; d++) {
+        const uint32_t w = u4_dw(u, (uint32_t)d), x = w & 0x7F7F7F7Fu;
+        const uint32_t dig = (x + 0x50505050u) & ~(x + 0x46464646u) & ~w & 0x80808080u;  // 0x30 <= b <= 0x39
+        nd |= nib4(~dig & 0x80808080u) << (4 * d);
+      }
+      nd &= 0xFFFFu << (uint32_t)(p & 15u);
+      if (nd) {
+        const uint64_t x = (p & ~15ull) + (uint64_t)__builtin_ctz(nd);
+        return x < ve ? x : ve;
+      }
+      p = (p | 15ull) + 1;
+      if (p >= ve) return ve;
+    }
   }
   // the first chunk in [ci, lim) with an interesting byte, or lim
   __device__ __forceinline__ uint64_t next(uint64_t ci, uint64_t lim) {
@@ -1725,20 +1783,16 @@ struct FjCur {
 // an escape, a control or high byte, or no quote before ve
 __device__ __forceinline__ uint64_t fj_str_end(FjCur& C, uint64_t s, uint64_t ve) {
   uint64_t ci = s >> 4;
-  uint32_t m = fj_mask(C.chunk(ci)) & (0xFFFFu << (uint32_t)(s & 15u));
+  uint32_t m = C.mask(ci) & (0xFFFFu << (uint32_t)(s & 15u));
   const uint64_t lim = (ve + 15) >> 4;
   while (!m) {
     ci = C.next(ci + 1, lim);
     if (ci >= lim) return ~0ull;
-    m = fj_mask(C.chunk(ci));
+    m = C.mask(ci);
   }
   const uint64_t x = (ci << 4) + (uint64_t)__builtin_ctz(m);
   if (x >= ve || C.at(x) != 0x22u) return ~0ull;
   return x;
-}
-__device__ __forceinline__ uint64_t fj_word(const uint8_t* S, uint64_t p, uint32_t n) {  // n <= 8 bytes at p
-  const uint64_t w = (uint64_t)ld_u32_at(S + p) | ((uint64_t)ld_u32_at(S + p + 4) << 32);
-  return n >= 8 ? w : (w & ((1ull << (8 * n)) - 1ull));
 }
 constexpr uint64_t fj_k(const char* t) {
   uint64_t v = 0;
@@ -1749,8 +1803,8 @@ __device__ __forceinline__ bool fj_digit(uint32_t c) { return c - 0x30u < 10u; }
 // one record's value [va, ve); false: the batch goes to k_eval.  fj: the
 // StructuredLog filter (lvl = 1 << LogLevel index); proj: the field fld[0, fl),
 // its last member's value span [fs, fe) when found
-__device__ bool fj_walk(FjCur& C, uint64_t va, uint64_t ve, bool fj, bool proj, const uint8_t* fld, uint32_t fl,
-                        uint32_t& lvl, bool& found, uint64_t& fs, uint64_t& fe) {
+__device__ __forceinline__ bool fj_walk(FjCur& C, uint64_t va, uint64_t ve, bool fj, bool proj, const uint8_t* fld, uint32_t fl,
+                        uint64_t fw, uint32_t& lvl, bool& found, uint64_t& fs, uint64_t& fe) {
   const uint8_t* S = C.S;
   uint64_t p = va;
   uint32_t nlv = 0, nmsg = 0;
@@ -1776,11 +1830,13 @@ __device__ bool fj_walk(FjCur& C, uint64_t va, uint64_t ve, bool fj, bool proj, 
     if (p >= ve) return false;
     uint32_t key = 0;  // 1 level, 2 message
     if (fj && (kn == 5 || kn == 7)) {
-      const uint64_t w = fj_word(S, k0, kn);
+      const uint64_t w = C.word(k0, kn);
       key = kn == 5 && w == fj_k("level") ? 1u : kn == 7 && w == fj_k("message") ? 2u : 0u;
     }
     bool fhit = false;
-    if (proj && kn == fl) {
+    if (proj && kn == fl && fl <= 8) {
+      fhit = C.word(k0, fl) == fw;
+    } else if (proj && kn == fl) {
       fhit = true;
       for (uint32_t t = 0; fhit && t < fl; t += 4) {
         const uint32_t mk = fl - t >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (fl - t))) - 1u);
@@ -1794,7 +1850,7 @@ __device__ bool fj_walk(FjCur& C, uint64_t va, uint64_t ve, bool fj, bool proj, 
       if (s1 == ~0ull) return false;
       if (key == 1) {
         const uint32_t n = (uint32_t)(s1 - p - 1);
-        const uint64_t w = n == 4 || n == 5 ? fj_word(S, p + 1, n) : 0ull;
+        const uint64_t w = n == 4 || n == 5 ? C.word(p + 1, n) : 0ull;
         const uint32_t v = n == 5 && w == fj_k("debug") ? 1u : n == 4 && w == fj_k("info") ? 2u
                          : n == 4 && w == fj_k("warn") ? 4u : n == 5 && w == fj_k("error") ? 8u : 0u;
         if (!v || nlv++) return false;  // unknown variant / duplicate field: serde errors
@@ -1814,8 +1870,7 @@ __device__ bool fj_walk(FjCur& C, uint64_t va, uint64_t ve, bool fj, bool proj, 
           p++;
           if (p < ve && fj_digit(C.at(p))) return false;  // a leading zero
         } else if (fj_digit(d)) {
-          while (++p < ve && fj_digit(C.at(p))) {
-          }
+          p = C.digits_end(p + 1, ve);
         } else {
           return false;
         }
@@ -1823,15 +1878,13 @@ __device__ bool fj_walk(FjCur& C, uint64_t va, uint64_t ve, bool fj, bool proj, 
         if (p < ve && C.at(p) == '.') {
           real = true;
           if (++p >= ve || !fj_digit(C.at(p))) return false;
-          while (++p < ve && fj_digit(C.at(p))) {
-          }
+          p = C.digits_end(p + 1, ve);
         }
         if (p < ve && (C.at(p) | 0x20u) == 'e') {
           real = true;
           if (++p < ve && (C.at(p) == '+' || C.at(p) == '-')) p++;
           if (p >= ve || !fj_digit(C.at(p))) return false;
-          while (++p < ve && fj_digit(C.at(p))) {
-          }
+          p = C.digits_end(p + 1, ve);
         }
         // a projection parses every number into a Value: integers of <= 18
         // characters only (no f64 reading, no -0)
@@ -1839,7 +1892,7 @@ __device__ bool fj_walk(FjCur& C, uint64_t va, uint64_t ve, bool fj, bool proj, 
       } else {
         const uint32_t n = c == 'f' ? 5u : 4u;
         if (p + n > ve) return false;
-        const uint64_t w = fj_word(S, p, n);
+        const uint64_t w = C.word(p, n);
         if (!(c == 't' ? w == fj_k("true") : c == 'f' ? w == fj_k("false") : c == 'n' && w == fj_k("null")))
           return false;
         p += n;
@@ -1875,6 +1928,8 @@ __global__ __launch_bounds__(256) void k_fj_decide(EvalArgs a) {
   const StageDesc& pd = a.chain->st[fst >> 24];
   const uint8_t* fld = a.blob + pd.needle;
   const uint32_t fl = proj ? pd.needle_len : 0u;
+  uint64_t fw = 0;  // a field name of <= 8 bytes as a word
+  for (uint32_t t = 0; t < fl && fl <= 8; t++) fw |= (uint64_t)fld[t] << (8 * t);
   const unsigned long long* hit_bm = a.fbm;  // interleaved (k_flat_scan): occurrence word w at [2 w], JSON word at [2 w + 1]
   const uint8_t* S = a.slice;
   const uint64_t pos = a.bpos[b];
@@ -1895,7 +1950,6 @@ __global__ __launch_bounds__(256) void k_fj_decide(EvalArgs a) {
   FjCur C;
   C.S = S;
   C.fbm = a.fbm;
-  C.c = ~0ull;
   for (int32_t n = 0; ok && n < count; n++) {
     uint32_t o = (uint32_t)(q & 3), nb;
     int64_t len, ts, od, kl = 0, vlen, hdr;
@@ -1938,11 +1992,21 @@ __global__ __launch_bounds__(256) void k_fj_decide(EvalArgs a) {
     const uint64_t c0 = va >> 4;
     const uint64_t wb = c0 >> 6;  // first bitmap round touching the value
     const ulonglong2 bw0 = *(const ulonglong2*)(a.fbm + 2 * wb), bw1 = *(const ulonglong2*)(a.fbm + 2 * wb + 2);
-    C.tc = (ve - 1) >> 4;
-    C.tv = *(const uint4*)(S + (C.tc << 4));
-    if (C.c != c0 && c0 != C.tc) {
-      C.v = *(const uint4*)(S + (c0 << 4));
-      C.c = c0;
+    {
+      const uint4* hp = (const uint4*)(S + (c0 << 4));
+      const uint64_t tc = ((ve - 1) >> 4) >= c0 + 3 ? ((ve - 1) >> 4) - 3 : c0;
+      const uint4* tp = (const uint4*)(S + (tc << 4));
+      C.h0 = hp[0];
+      C.h1 = hp[1];
+      C.h2 = hp[2];
+      C.h3 = hp[3];
+      C.t0 = tp[0];
+      C.t1 = tp[1];
+      C.t2 = tp[2];
+      C.t3 = tp[3];
+      C.hc = c0;
+      C.tc = tc;
+      C.c = ~0ull;
     }
     C.wb = wb;
     C.j0 = bw0.y;
@@ -1991,7 +2055,7 @@ __global__ __launch_bounds__(256) void k_fj_decide(EvalArgs a) {
     uint32_t lvl = 0;
     bool found = false;
     uint64_t fs = va, fe = ve;
-    ok = fj_walk(C, va, ve, fj, proj, fld, fl, lvl, found, fs, fe);
+    ok = fj_walk(C, va, ve, fj, proj, fld, fl, fw, lvl, found, fs, fe);
     if (!ok) break;
     keep = keep && (!fj || lvl > 1u) && (!proj || found);  // level > Debug
     if (keep) {
