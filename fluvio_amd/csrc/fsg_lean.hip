@@ -1324,10 +1324,12 @@ __device__ __forceinline__ bool flat_verify(const uint8_t* s, uint64_t p, const 
   }
   return true;
 }
-// JSON-interesting bytes of a dword (0x80 per byte): '"', '\\', < 0x20, >= 0x80
-__device__ __forceinline__ uint32_t fj_bytes(uint32_t w) {
-  return zbytes(w ^ 0x22222222u) | zbytes(w ^ 0x5C5C5C5Cu) | zbytes(w & 0xE0E0E0E0u) | (w & 0x80808080u);
+// JSON-interesting bytes of a dword (0x80 per byte): '"', '\\', < 0x20, >= 0x80;
+// special: the same without the quote
+__device__ __forceinline__ uint32_t fj_special(uint32_t w) {
+  return zbytes(w ^ 0x5C5C5C5Cu) | zbytes(w & 0xE0E0E0E0u) | (w & 0x80808080u);
 }
+__device__ __forceinline__ uint32_t fj_bytes(uint32_t w) { return zbytes(w ^ 0x22222222u) | fj_special(w); }
 // kLong: m >= 7, aligned dwords against the 4 offsets.  kJson: the second word
 // of a round holds the chunks with a JSON-interesting byte (fj_bytes) instead
 // of the high bytes (the flat JSON path); kNone: no substring stage (occurrence word 0)
@@ -1370,11 +1372,17 @@ __global__ __launch_bounds__(256) void k_flat_scan(EvalArgs a, uint32_t stage) {
       if (r0 + i >= nrounds) break;  // uniform
       const uint64_t R = (r0 + i) * 1024;
       uint32_t w[5] = {v[i].x, v[i].y, v[i].z, v[i].w, kLong ? 0u : nx[i]};
-      const bool high = kJson ? ((fj_bytes(w[0]) | fj_bytes(w[1]) | fj_bytes(w[2]) | fj_bytes(w[3])) != 0u)
+      // kJson: high = a JSON-interesting byte, spec = one that is not a quote
+      const bool spec = kJson && ((fj_special(w[0]) | fj_special(w[1]) | fj_special(w[2]) | fj_special(w[3])) != 0u);
+      const bool high = kJson ? (spec || ((zbytes(w[0] ^ 0x22222222u) | zbytes(w[1] ^ 0x22222222u) |
+                                           zbytes(w[2] ^ 0x22222222u) | zbytes(w[3] ^ 0x22222222u)) != 0u))
                               : ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) != 0u;
       if (kNone) {
-        const uint64_t hh = __ballot(high);
-        if (lane == 0) bm2[r0 + i] = make_ulonglong2(0ull, hh);
+        const uint64_t hh = __ballot(high), xx = __ballot(spec);
+        if (lane == 0) {
+          bm2[2 * (r0 + i)] = make_ulonglong2(0ull, hh);
+          bm2[2 * (r0 + i) + 1] = make_ulonglong2(xx, 0ull);
+        }
         continue;
       }
       if (upper) {
@@ -1434,19 +1442,30 @@ __global__ __launch_bounds__(256) void k_flat_scan(EvalArgs a, uint32_t stage) {
         }
       }
       const uint64_t hb = __ballot(hit), hh = __ballot(high);
-      if (lane == 0) bm2[r0 + i] = make_ulonglong2(hb, hh);
+      if (kJson) {  // four words per round: occurrences, interesting, special, 0
+        const uint64_t xx = __ballot(spec);
+        if (lane == 0) {
+          bm2[2 * (r0 + i)] = make_ulonglong2(hb, hh);
+          bm2[2 * (r0 + i) + 1] = make_ulonglong2(xx, 0ull);
+        }
+      } else if (lane == 0) {
+        bm2[r0 + i] = make_ulonglong2(hb, hh);
+      }
     }
   }
 }
-// bm: the interleaved bitmaps offset by the one wanted (0 occurrences, 1 high bytes): word w at bm[2 w]
-__device__ __forceinline__ bool bm_bit(const unsigned long long* bm, uint64_t c) { return (bm[2 * (c >> 6)] >> (c & 63)) & 1ull; }
+// bm: the interleaved bitmaps offset by the one wanted (0 occurrences, 1 high bytes): word w at bm[kS w]
+// (kS = 2; the flat JSON path interleaves four words per round)
+template <int kS = 2>
+__device__ __forceinline__ bool bm_bit(const unsigned long long* bm, uint64_t c) { return (bm[kS * (c >> 6)] >> (c & 63)) & 1ull; }
 // bits [c0, c1) of a bitmap: any set
+template <int kS = 2>
 __device__ __forceinline__ bool flat_any(const unsigned long long* bm, uint64_t c0, uint64_t c1) {
   for (uint64_t c = c0; c < c1;) {
     const uint64_t w = c >> 6, lo = c & 63;
     const uint64_t hi = (c1 - (w << 6)) < 64 ? (c1 - (w << 6)) : 64;
     const uint64_t mask = (hi == 64 ? ~0ull : ((1ull << hi) - 1ull)) & ~((1ull << lo) - 1ull);
-    if (bm[2 * w] & mask) return true;
+    if (bm[kS * w] & mask) return true;
     c = (w + 1) << 6;
   }
   return false;
@@ -1694,58 +1713,75 @@ __device__ __forceinline__ uint4 sel4(uint4 a0, uint4 a1, uint4 a2, uint4 a3, ui
   r.w = u4_dw(make_uint4(a0.w, a1.w, a2.w, a3.w), k);
   return r;
 }
-// a record's value seen through registers: the 64 bytes from its first chunk
-// (hd), the 64 bytes up to its last chunk (tl), both loaded with the record's
-// header, and one more chunk loaded on demand; plus the interesting-chunk bitmap
+// A record's value as the walk sees it: the 64 bytes from its first chunk (the
+// head window) and the 80 bytes up to its last chunk (the tail window), staged
+// in this thread's LDS slot, every other byte from memory (rare: members in the
+// middle of a long value), and the interesting-chunk bitmap for strings that
+// run between the windows.  Positions are 32-bit offsets from B (the batch's
+// 16-aligned start); the windows start at chunk boundaries.
+constexpr uint32_t kFjHead = 64, kFjTail = 80, kFjSlot = kFjHead + kFjTail;  // bytes per thread in LDS
 struct FjCur {
-  const uint8_t* S;
-  const unsigned long long* fbm;  // interleaved: the JSON word of round r at fbm[2 r + 1]
-  uint64_t hc, tc;                // first chunk of hd / tl
-  uint4 h0, h1, h2, h3, t0, t1, t2, t3;
-  uint64_t c;                     // chunk index of v (the current chunk) and m its interesting bytes
+  const uint8_t* B;
+  uint8_t* W;                     // this thread's LDS slot: head window, then tail window
+  const unsigned long long* fbm;  // four words per round r: occurrences, interesting, special at fbm[4 r + 0..2]
+  uint64_t cb;                    // B's chunk index in the slice
+  uint32_t hb, tb;                // offsets of the head / tail windows
+  uint32_t c;                     // chunk of v (the current chunk) and m its interesting bytes
   uint4 v;
   uint32_t m;
   bool mv;                        // m computed
-  uint64_t wb;                    // the rounds wb, wb + 1 preloaded as j0, j1
-  unsigned long long j0, j1;
-  __device__ __forceinline__ uint4 chunk(uint64_t ci) {
+  uint64_t wb;                    // the slice rounds wb, wb + 1 preloaded: interesting j0, j1; special x0, x1
+  unsigned long long j0, j1, x0, x1;
+  // the slot offset of position p, or >= kFjSlot outside both windows
+  __device__ __forceinline__ uint32_t loff(uint32_t p) const {
+    const uint32_t dh = p - hb, dt = p - tb;
+    return dh < kFjHead ? dh : dt < kFjTail ? kFjHead + dt : kFjSlot;
+  }
+  __device__ __forceinline__ uint4 chunk(uint32_t ci) {
     if (ci != c) {
-      if (ci - hc < 4) v = sel4(h0, h1, h2, h3, (uint32_t)(ci - hc));
-      else if (ci - tc < 4) v = sel4(t0, t1, t2, t3, (uint32_t)(ci - tc));
-      else v = *(const uint4*)(S + (ci << 4));
+      const uint32_t o = loff(16u * ci);
+      if (o < kFjSlot) v = *(const uint4*)(W + o);
+      else v = *(const uint4*)(B + 16u * ci);
       c = ci;
       mv = false;
     }
     return v;
   }
-  __device__ __forceinline__ uint32_t mask(uint64_t ci) {  // interesting bytes of chunk ci
+  __device__ __forceinline__ uint32_t mask(uint32_t ci) {  // interesting bytes of chunk ci
     chunk(ci);
     if (!mv) {
-      m = fj_mask(v);
+      const uint64_t ac = cb + ci, r = ac >> 6;
+      const unsigned long long xw = r == wb ? x0 : r == wb + 1 ? x1 : fbm[4 * r + 2];
+      if ((xw >> (ac & 63u)) & 1ull) {
+        m = fj_mask(v);
+      } else {  // no special byte in the chunk (the scan's bitmap): its quotes only
+        m = nib4(zbytes(v.x ^ 0x22222222u)) | (nib4(zbytes(v.y ^ 0x22222222u)) << 4) |
+            (nib4(zbytes(v.z ^ 0x22222222u)) << 8) | (nib4(zbytes(v.w ^ 0x22222222u)) << 12);
+      }
       mv = true;
     }
     return m;
   }
-  __device__ __forceinline__ uint32_t at(uint64_t p) {
-    const uint4 u = chunk(p >> 4);
-    return (u4_dw(u, (uint32_t)(p >> 2) & 3u) >> (8u * (uint32_t)(p & 3u))) & 0xFFu;
+  __device__ __forceinline__ uint32_t at(uint32_t p) {
+    const uint32_t o = loff(p);
+    if (o < kFjSlot) return W[o];
+    return B[p];
   }
-  // the n <= 8 bytes at p as a little-endian word (from registers)
-  __device__ __forceinline__ uint64_t word(uint64_t p, uint32_t n) {
-    const uint4 u = chunk(p >> 4);
-    const uint32_t o = (uint32_t)(p & 15u);
-    const uint4 u2 = o + n > 16 ? chunk((p >> 4) + 1) : u;
-    const uint32_t k = o >> 2;
-    const uint32_t e0 = u4_dw(u, k);
-    const uint32_t e1 = k < 3 ? u4_dw(u, k + 1) : u2.x;
-    const uint32_t e2 = k < 2 ? u4_dw(u, k + 2) : u4_dw(u2, k - 2);
-    const uint32_t sh = o & 3u;
-    const uint64_t w = (uint64_t)__builtin_amdgcn_alignbyte(e1, e0, sh) |
-                       ((uint64_t)__builtin_amdgcn_alignbyte(e2, e1, sh) << 32);
+  // the n <= 8 bytes at p as a little-endian word
+  __device__ __forceinline__ uint64_t word(uint32_t p, uint32_t n) {
+    const uint32_t o = loff(p);
+    uint64_t w = 0;
+    if (o < kFjHead ? o + n <= kFjHead : o + n <= kFjSlot) {  // inside one window: three aligned dwords
+      const uint32_t* d = (const uint32_t*)(W + (o & ~3u));
+      const uint32_t e0 = d[0], e1 = d[1], e2 = d[2], sh = o & 3u;
+      w = (uint64_t)__builtin_amdgcn_alignbyte(e1, e0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(e2, e1, sh) << 32);
+    } else {
+      for (uint32_t i = 0; i < n; i++) w |= (uint64_t)at(p + i) << (8 * i);
+    }
     return n >= 8 ? w : (w & ((1ull << (8 * n)) - 1ull));
   }
-  // the first position >= p holding a byte that is not an ASCII digit
-  __device__ __forceinline__ uint64_t digits_end(uint64_t p, uint64_t ve) {
+  // the first position >= p (< ve) holding a byte that is not an ASCII digit, or ve
+  __device__ __forceinline__ uint32_t digits_end(uint32_t p, uint32_t ve) {
     for (;;) {
       const uint4 u = chunk(p >> 4);
       uint32_t nd = 0;
@@ -1755,43 +1791,43 @@ struct FjCur {
         const uint32_t dig = (x + 0x50505050u) & ~(x + 0x46464646u) & ~w & 0x80808080u;  // 0x30 <= b <= 0x39
         nd |= nib4(~dig & 0x80808080u) << (4 * d);
       }
-      nd &= 0xFFFFu << (uint32_t)(p & 15u);
+      nd &= 0xFFFFu << (p & 15u);
       if (nd) {
-        const uint64_t x = (p & ~15ull) + (uint64_t)__builtin_ctz(nd);
+        const uint32_t x = (p & ~15u) + (uint32_t)__builtin_ctz(nd);
         return x < ve ? x : ve;
       }
-      p = (p | 15ull) + 1;
+      p = (p | 15u) + 1;
       if (p >= ve) return ve;
     }
   }
   // the first chunk in [ci, lim) with an interesting byte, or lim
-  __device__ __forceinline__ uint64_t next(uint64_t ci, uint64_t lim) {
+  __device__ __forceinline__ uint32_t next(uint32_t ci, uint32_t lim) {
     while (ci < lim) {
-      const uint64_t r = ci >> 6;
-      unsigned long long w = r == wb ? j0 : r == wb + 1 ? j1 : fbm[2 * r + 1];
-      w &= ~0ull << (ci & 63u);
+      const uint64_t ac = cb + ci, r = ac >> 6;
+      unsigned long long w = r == wb ? j0 : r == wb + 1 ? j1 : fbm[4 * r + 1];
+      w &= ~0ull << (ac & 63u);
       if (w) {
-        const uint64_t x = (r << 6) + (uint64_t)__builtin_ctzll(w);
+        const uint32_t x = ci + (uint32_t)__builtin_ctzll(w) - (uint32_t)(ac & 63u);
         return x < lim ? x : lim;
       }
-      ci = (r + 1) << 6;
+      ci += 64u - (uint32_t)(ac & 63u);
     }
     return lim;
   }
 };
-// the closing quote of the string whose bytes start at s (before ve), or ~0:
+// the closing quote of the string whose bytes start at s (before ve), or ~0u:
 // an escape, a control or high byte, or no quote before ve
-__device__ __forceinline__ uint64_t fj_str_end(FjCur& C, uint64_t s, uint64_t ve) {
-  uint64_t ci = s >> 4;
-  uint32_t m = C.mask(ci) & (0xFFFFu << (uint32_t)(s & 15u));
-  const uint64_t lim = (ve + 15) >> 4;
+__device__ __forceinline__ uint32_t fj_str_end(FjCur& C, uint32_t s, uint32_t ve) {
+  uint32_t ci = s >> 4;
+  uint32_t m = C.mask(ci) & (0xFFFFu << (s & 15u));
+  const uint32_t lim = (ve + 15) >> 4;
   while (!m) {
     ci = C.next(ci + 1, lim);
-    if (ci >= lim) return ~0ull;
+    if (ci >= lim) return ~0u;
     m = C.mask(ci);
   }
-  const uint64_t x = (ci << 4) + (uint64_t)__builtin_ctz(m);
-  if (x >= ve || C.at(x) != 0x22u) return ~0ull;
+  const uint32_t x = (ci << 4) + (uint32_t)__builtin_ctz(m);
+  if (x >= ve || ((u4_dw(C.v, (x >> 2) & 3u) >> (8u * (x & 3u))) & 0xFFu) != 0x22u) return ~0u;
   return x;
 }
 constexpr uint64_t fj_k(const char* t) {
@@ -1800,13 +1836,14 @@ constexpr uint64_t fj_k(const char* t) {
   return v;
 }
 __device__ __forceinline__ bool fj_digit(uint32_t c) { return c - 0x30u < 10u; }
-// one record's value [va, ve); false: the batch goes to k_eval.  fj: the
-// StructuredLog filter (lvl = 1 << LogLevel index); proj: the field fld[0, fl),
-// its last member's value span [fs, fe) when found
-__device__ __forceinline__ bool fj_walk(FjCur& C, uint64_t va, uint64_t ve, bool fj, bool proj, const uint8_t* fld, uint32_t fl,
-                        uint64_t fw, uint32_t& lvl, bool& found, uint64_t& fs, uint64_t& fe) {
-  const uint8_t* S = C.S;
-  uint64_t p = va;
+// one record's value [va, ve) (offsets from C.B); false: the batch goes to
+// k_eval.  fj: the StructuredLog filter (lvl = 1 << LogLevel index); proj: the
+// field fld[0, fl) (fw: as a word when fl <= 8), its last member's value span
+// [fs, fe) when found
+__device__ __forceinline__ bool fj_walk(FjCur& C, uint32_t va, uint32_t ve, bool fj, bool proj, const uint8_t* fld,
+                                        uint32_t fl, uint64_t fw, uint32_t& lvl, bool& found, uint32_t& fs,
+                                        uint32_t& fe) {
+  uint32_t p = va;
   uint32_t nlv = 0, nmsg = 0;
   lvl = 0;
   found = false;
@@ -1819,15 +1856,19 @@ __device__ __forceinline__ bool fj_walk(FjCur& C, uint64_t va, uint64_t ve, bool
   for (;;) {
     sp();
     if (p >= ve || C.at(p) != '"') return false;  // (an empty object goes to k_eval too)
-    const uint64_t k0 = p + 1, k1 = fj_str_end(C, k0, ve);
-    if (k1 == ~0ull) return false;
-    const uint32_t kn = (uint32_t)(k1 - k0);
+    const uint32_t k0 = p + 1, k1 = fj_str_end(C, k0, ve);
+    if (k1 == ~0u) return false;
+    const uint32_t kn = k1 - k0;
     p = k1 + 1;
-    sp();
-    if (p >= ve || C.at(p) != ':') return false;
-    p++;
-    sp();
-    if (p >= ve) return false;
+    if (p + 2 <= ve && (uint32_t)C.word(p, 2) == 0x223Au) {  // `:"` (the common layout): one word
+      p++;
+    } else {
+      sp();
+      if (p >= ve || C.at(p) != ':') return false;
+      p++;
+      sp();
+      if (p >= ve) return false;
+    }
     uint32_t key = 0;  // 1 level, 2 message
     if (fj && (kn == 5 || kn == 7)) {
       const uint64_t w = C.word(k0, kn);
@@ -1840,16 +1881,16 @@ __device__ __forceinline__ bool fj_walk(FjCur& C, uint64_t va, uint64_t ve, bool
       fhit = true;
       for (uint32_t t = 0; fhit && t < fl; t += 4) {
         const uint32_t mk = fl - t >= 4 ? 0xFFFFFFFFu : ((1u << (8 * (fl - t))) - 1u);
-        fhit = ((ld_u32_at(S + k0 + t) ^ ld_u32_at(fld + t)) & mk) == 0u;
+        fhit = ((ld_u32_at(C.B + k0 + t) ^ ld_u32_at(fld + t)) & mk) == 0u;
       }
     }
-    const uint64_t v0 = p;
+    const uint32_t v0 = p;
     const uint32_t c = C.at(p);
     if (c == '"') {
-      const uint64_t s1 = fj_str_end(C, p + 1, ve);
-      if (s1 == ~0ull) return false;
+      const uint32_t s1 = fj_str_end(C, p + 1, ve);
+      if (s1 == ~0u) return false;
       if (key == 1) {
-        const uint32_t n = (uint32_t)(s1 - p - 1);
+        const uint32_t n = s1 - p - 1;
         const uint64_t w = n == 4 || n == 5 ? C.word(p + 1, n) : 0ull;
         const uint32_t v = n == 5 && w == fj_k("debug") ? 1u : n == 4 && w == fj_k("info") ? 2u
                          : n == 4 && w == fj_k("warn") ? 4u : n == 5 && w == fj_k("error") ? 8u : 0u;
@@ -1903,6 +1944,10 @@ __device__ __forceinline__ bool fj_walk(FjCur& C, uint64_t va, uint64_t ve, bool
       fs = v0;
       fe = p;
     }
+    if (p + 2 <= ve && (uint32_t)C.word(p, 2) == 0x222Cu) {  // `,"` (the common layout): the next key
+      p++;
+      continue;
+    }
     sp();
     if (p >= ve) return false;
     const uint32_t e = C.at(p++);
@@ -1913,7 +1958,90 @@ __device__ __forceinline__ bool fj_walk(FjCur& C, uint64_t va, uint64_t ve, bool
   if (p != ve) return false;                       // trailing characters
   return !fj || (nlv == 1 && nmsg == 1);           // a missing field: serde error
 }
+// one record's framing (Record::decode, data.rs:534-562) from its header bytes
+struct FjRec {
+  uint64_t q, end, va, ve, kpos;
+  int64_t ts, od;
+  uint32_t klen;
+  uint8_t attr, tag;
+  bool ok;
+};
+__device__ __forceinline__ FjRec fj_frame(const uint8_t* S, const FlatHdr& H, uint64_t q, uint64_t sec_end) {
+  FjRec r;
+  r.q = q;
+  r.kpos = 0;
+  r.klen = 0;
+  r.ts = r.od = 0;
+  r.attr = r.tag = 0;
+  r.va = r.ve = r.end = q;
+  uint32_t o = (uint32_t)(q & 3), nb;
+  int64_t len, kl = 0, vlen;
+  nb = var4(flat_at(H, o), len);
+  r.ok = nb != 0 && len >= 0;
+  r.end = q + nb + (uint64_t)len;  // where the record ends (Record::decode's length)
+  r.ok = r.ok && r.end <= sec_end;
+  if (!r.ok) return r;
+  o += nb;
+  r.attr = (uint8_t)flat_at(H, o);
+  o += 1;
+  nb = var4(flat_at(H, o), r.ts);
+  r.ok = nb != 0;
+  o += nb;
+  nb = var4(flat_at(H, o), r.od);
+  r.ok = r.ok && nb != 0;
+  o += nb;
+  r.tag = (uint8_t)flat_at(H, o);
+  o += 1;
+  r.ok = r.ok && r.tag <= 1;
+  if (!r.ok) return r;
+  uint64_t p = (q & ~3ull) + o;
+  if (r.tag == 1) {
+    nb = var4(flat_at(H, o), kl);
+    r.ok = nb != 0 && kl >= 0;
+    p += nb;
+    r.kpos = p;
+    r.klen = (uint32_t)kl;
+    p += r.klen;
+  }
+  nb = var4(r.tag == 1 ? ld_u32_at(S + p) : flat_at(H, o), vlen);
+  r.ok = r.ok && nb != 0 && vlen >= 0;
+  r.va = p + nb;
+  r.ve = r.va + (uint64_t)vlen;
+  r.ok = r.ok && r.ve <= r.end && r.ve > r.va;  // (an empty value is a serde error: k_eval)
+  return r;
+}
+// a record's loads, issued together: its value's head and tail windows, the
+// bitmap rounds over its first chunk, its trailer (the headers varint)
+struct FjLoads {
+  uint4 h0, h1, h2, h3, t0, t1, t2, t3, t4;
+  ulonglong2 bw0, bw1, bx0, bx1;  // rounds wb, wb + 1: (occurrences, interesting), (special, 0)
+  uint32_t tw;
+  uint64_t tc;
+};
+__device__ __forceinline__ FjLoads fj_issue(const uint8_t* S, const unsigned long long* fbm, const FjRec& r) {
+  FjLoads L;
+  const uint64_t c0 = r.va >> 4, wb = c0 >> 6;
+  const uint4* hp = (const uint4*)(S + (c0 << 4));
+  L.tc = ((r.ve - 1) >> 4) >= c0 + 4 ? ((r.ve - 1) >> 4) - 4 : c0;
+  const uint4* tp = (const uint4*)(S + (L.tc << 4));
+  L.h0 = hp[0];
+  L.h1 = hp[1];
+  L.h2 = hp[2];
+  L.h3 = hp[3];
+  L.t0 = tp[0];
+  L.t1 = tp[1];
+  L.t2 = tp[2];
+  L.t3 = tp[3];
+  L.t4 = tp[4];
+  L.bw0 = *(const ulonglong2*)(fbm + 4 * wb);
+  L.bx0 = *(const ulonglong2*)(fbm + 4 * wb + 2);
+  L.bw1 = *(const ulonglong2*)(fbm + 4 * wb + 4);
+  L.bx1 = *(const ulonglong2*)(fbm + 4 * wb + 6);
+  L.tw = ld_u32_at(S + r.ve);
+  return L;
+}
 __global__ __launch_bounds__(256) void k_fj_decide(EvalArgs a) {
+  __shared__ uint4 slots[256 * (kFjSlot / 16) + 1];  // (+1: a word read past the last slot's end)
   const uint32_t b = blockIdx.x * 256 + threadIdx.x;
   if (b >= a.nbatches) return;
   // a.flat_st: substring stage (0xFF none) | needle length << 8 | filter_json << 16 | projection << 17 | its stage << 24
@@ -1930,7 +2058,7 @@ __global__ __launch_bounds__(256) void k_fj_decide(EvalArgs a) {
   const uint32_t fl = proj ? pd.needle_len : 0u;
   uint64_t fw = 0;  // a field name of <= 8 bytes as a word
   for (uint32_t t = 0; t < fl && fl <= 8; t++) fw |= (uint64_t)fld[t] << (8 * t);
-  const unsigned long long* hit_bm = a.fbm;  // interleaved (k_flat_scan): occurrence word w at [2 w], JSON word at [2 w + 1]
+  const unsigned long long* hit_bm = a.fbm;  // k_flat_scan<., kJson>: occurrence word w at [4 w]
   const uint8_t* S = a.slice;
   const uint64_t pos = a.bpos[b];
   const uint64_t nxt = b + 1 < a.nbatches ? a.bpos[b + 1] : a.slice_len;
@@ -1945,81 +2073,72 @@ __global__ __launch_bounds__(256) void k_fj_decide(EvalArgs a) {
   const int32_t count = sec_len >= 4 ? (int32_t)__builtin_bswap32(ld_u32_at(S + sec0)) : -1;
   bool ok = sec_len >= 4 && sec_end - al <= wlen && count >= 0 && count <= kLeanMaxR && (uint64_t)count == rn;
   uint32_t nkeep = 0;
-  uint64_t q = sec0 + 4;  // absolute start of record n
-  FlatHdr H = flat_hdr(S, ok && count > 0 ? q : sec0);
   FjCur C;
-  C.S = S;
+  C.B = S + al;
+  C.W = (uint8_t*)&slots[threadIdx.x * (kFjSlot / 16)];
+  C.cb = al >> 4;
   C.fbm = a.fbm;
+  // software pipeline: record n + 1's header is framed and its loads issued
+  // before record n is walked; record n + 2's header is in flight meanwhile
+  FjRec R = {};
+  FjLoads L = {};
+  FlatHdr H = flat_hdr(S, sec0);
+  uint64_t q = sec0 + 4;  // absolute start of the next record to frame
+  if (ok && count > 0) {
+    H = flat_hdr(S, q);
+    R = fj_frame(S, H, q, sec_end);
+    ok = R.ok;
+    if (ok) {
+      L = fj_issue(S, a.fbm, R);
+      q = R.end;
+      if (count > 1) H = flat_hdr(S, q);
+    }
+  }
   for (int32_t n = 0; ok && n < count; n++) {
-    uint32_t o = (uint32_t)(q & 3), nb;
-    int64_t len, ts, od, kl = 0, vlen, hdr;
-    nb = var4(flat_at(H, o), len);
-    ok = nb != 0 && len >= 0;
-    const uint64_t end = q + nb + (uint64_t)len;  // where the record ends (Record::decode's length)
-    ok = ok && end <= sec_end;
-    if (!ok) break;
-    const FlatHdr Hn = flat_hdr(S, n + 1 < count ? end : q);  // the next record's header, in flight now
-    o += nb;
-    const uint8_t attr = (uint8_t)flat_at(H, o);
-    o += 1;
-    nb = var4(flat_at(H, o), ts);
-    ok = nb != 0;
-    o += nb;
-    nb = var4(flat_at(H, o), od);
-    ok = ok && nb != 0;
-    o += nb;
-    const uint8_t tag = (uint8_t)flat_at(H, o);
-    o += 1;
-    ok = ok && tag <= 1;
-    if (!ok) break;
-    uint64_t p = (q & ~3ull) + o, kpos = 0;
-    uint32_t klen = 0;
-    if (tag == 1) {
-      nb = var4(flat_at(H, o), kl);
-      ok = nb != 0 && kl >= 0;
-      p += nb;
-      kpos = p;
-      klen = (uint32_t)kl;
-      p += klen;
-    }
-    nb = var4(tag == 1 ? ld_u32_at(S + p) : flat_at(H, o), vlen);
-    ok = ok && nb != 0 && vlen >= 0;
-    const uint64_t va = p + nb, ve = va + (uint64_t)vlen;
-    ok = ok && ve <= end && ve > va;  // (an empty value is a serde error: k_eval)
-    if (!ok) break;
-    // every load of this record at once: trailer, bitmap words, the value's first and last chunks
-    const uint32_t tw = ld_u32_at(S + ve);
-    const uint64_t c0 = va >> 4;
-    const uint64_t wb = c0 >> 6;  // first bitmap round touching the value
-    const ulonglong2 bw0 = *(const ulonglong2*)(a.fbm + 2 * wb), bw1 = *(const ulonglong2*)(a.fbm + 2 * wb + 2);
+    // record n's loads have landed: its windows into the slot
     {
-      const uint4* hp = (const uint4*)(S + (c0 << 4));
-      const uint64_t tc = ((ve - 1) >> 4) >= c0 + 3 ? ((ve - 1) >> 4) - 3 : c0;
-      const uint4* tp = (const uint4*)(S + (tc << 4));
-      C.h0 = hp[0];
-      C.h1 = hp[1];
-      C.h2 = hp[2];
-      C.h3 = hp[3];
-      C.t0 = tp[0];
-      C.t1 = tp[1];
-      C.t2 = tp[2];
-      C.t3 = tp[3];
-      C.hc = c0;
-      C.tc = tc;
-      C.c = ~0ull;
+      uint4* w = (uint4*)C.W;
+      w[0] = L.h0;
+      w[1] = L.h1;
+      w[2] = L.h2;
+      w[3] = L.h3;
+      w[4] = L.t0;
+      w[5] = L.t1;
+      w[6] = L.t2;
+      w[7] = L.t3;
+      w[8] = L.t4;
     }
+    const FjRec cur = R;
+    const uint64_t va = cur.va, ve = cur.ve;
+    const uint64_t c0 = va >> 4, wb = c0 >> 6;
+    const ulonglong2 bw0 = L.bw0, bw1 = L.bw1;
+    int64_t hdr;
+    uint32_t nb = var4(L.tw, hdr);
+    ok = nb != 0 && ve + nb == cur.end;
+    if (!ok) break;
+    C.hb = (uint32_t)(va - al) & ~15u;
+    C.tb = (uint32_t)((L.tc << 4) - al);
+    C.c = ~0u;
     C.wb = wb;
     C.j0 = bw0.y;
     C.j1 = bw1.y;
-    nb = var4(tw, hdr);
-    ok = nb != 0 && ve + nb == end;
-    if (!ok) break;
+    C.x0 = L.bx0.x;
+    C.x1 = L.bx1.x;
+    // the next record: framed now, its loads in flight during this walk
+    if (n + 1 < count) {
+      R = fj_frame(S, H, q, sec_end);
+      ok = R.ok;
+      if (!ok) break;
+      L = fj_issue(S, a.fbm, R);
+      q = R.end;
+      if (n + 2 < count) H = flat_hdr(S, q);
+    }
     bool keep = true;
     if (has_sub) {  // an occurrence starting in [va, ve - m] (k_flat_decide's anchors)
       const unsigned long long mb0 = bw0.x, mb1 = bw1.x;
       auto bits_any = [&](uint64_t x0, uint64_t x1) {
         if (x1 <= x0) return false;
-        if (x1 > (wb + 2) << 6) return flat_any(hit_bm, x0, x1);
+        if (x1 > (wb + 2) << 6) return flat_any<4>(hit_bm, x0, x1);
         const uint64_t lo = x0 - (wb << 6), hi = x1 - (wb << 6);  // in [0, 128]
         const unsigned long long m0 = (lo < 64 ? (~0ull << lo) : 0ull) & (hi >= 64 ? ~0ull : ((1ull << hi) - 1ull));
         const unsigned long long m1 = (hi > 64 ? (hi >= 128 ? ~0ull : ((1ull << (hi - 64)) - 1ull)) : 0ull) &
@@ -2027,7 +2146,8 @@ __global__ __launch_bounds__(256) void k_fj_decide(EvalArgs a) {
         return ((mb0 & m0) | (mb1 & m1)) != 0ull;
       };
       bool match = false;
-      if ((uint64_t)vlen >= m) {
+      const uint64_t vlen = ve - va;
+      if (vlen >= m) {
         const uint64_t sl = ve - m;
         const uint64_t blo = kLong ? 3 : 0, bhi = kLong ? 12 : 15;
         const uint64_t j0 = (va + blo + 15) >> 4;
@@ -2042,7 +2162,7 @@ __global__ __launch_bounds__(256) void k_fj_decide(EvalArgs a) {
             }
             const uint64_t r = c - (wb << 6);
             const bool bt = c >= (wb << 6) && r < 128 ? (((r < 64 ? mb0 : mb1) >> (r & 63)) & 1ull) != 0ull
-                                                      : bm_bit(hit_bm, c);
+                                                      : bm_bit<4>(hit_bm, c);
             if (!bt) continue;
             const uint64_t lo = (c << 4) >= va + blo ? (c << 4) - blo : va;
             const uint64_t hi = (c << 4) + bhi <= sl ? (c << 4) + bhi : sl;
@@ -2052,33 +2172,36 @@ __global__ __launch_bounds__(256) void k_fj_decide(EvalArgs a) {
       }
       keep = match;
     }
-    uint32_t lvl = 0;
+    uint32_t lvl = 0, fs = (uint32_t)(va - al), fe = (uint32_t)(ve - al);
     bool found = false;
-    uint64_t fs = va, fe = ve;
-    ok = fj_walk(C, va, ve, fj, proj, fld, fl, fw, lvl, found, fs, fe);
+#ifdef FSG_FJ_NOWALK  // experiment builds: the decide without the JSON walk (framing, loads and staging only)
+    lvl = 2u;
+    found = true;
+    (void)fw;
+#else
+    ok = fj_walk(C, fs, fe, fj, proj, fld, fl, fw, lvl, found, fs, fe);
+#endif
     if (!ok) break;
     keep = keep && (!fj || lvl > 1u) && (!proj || found);  // level > Debug
     if (keep) {
       KeptRec d;
-      d.src = q;
-      d.vpos = fs;
-      d.kpos = tag ? kpos : 0;
-      d.od = od;
-      d.ts = ts;
+      d.src = cur.q;
+      d.vpos = al + fs;
+      d.kpos = cur.tag ? cur.kpos : 0;
+      d.od = cur.od;
+      d.ts = cur.ts;
       d.hdr = hdr;
-      d.vlen = (uint32_t)(fe - fs);
-      d.klen = klen;
+      d.vlen = fe - fs;
+      d.klen = cur.klen;
       d.ival = 0;
       d.mode = out_upper ? KM_UPPER : KM_COPY;
-      d.has_key = tag;
-      d.attr = attr;
+      d.has_key = cur.tag;
+      d.attr = cur.attr;
       d.pad = 0;
       a.desc[rb + nkeep++] = d;
     }
-    q = end;
-    H = Hn;
   }
-  ok = ok && q == sec_end;
+  ok = ok && q == sec_end;  // (q: the end of the last record framed)
   if (!ok) {  // the exact kernel frames and evaluates this batch
     a.rend[b] = 0xFFFFu;
     const uint32_t i = atomicAdd(&a.list[0], 1u);
