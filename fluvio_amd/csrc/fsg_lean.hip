@@ -1372,17 +1372,11 @@ __global__ __launch_bounds__(256) void k_flat_scan(EvalArgs a, uint32_t stage) {
       if (r0 + i >= nrounds) break;  // uniform
       const uint64_t R = (r0 + i) * 1024;
       uint32_t w[5] = {v[i].x, v[i].y, v[i].z, v[i].w, kLong ? 0u : nx[i]};
-      // kJson: high = a JSON-interesting byte, spec = one that is not a quote
-      const bool spec = kJson && ((fj_special(w[0]) | fj_special(w[1]) | fj_special(w[2]) | fj_special(w[3])) != 0u);
-      const bool high = kJson ? (spec || ((zbytes(w[0] ^ 0x22222222u) | zbytes(w[1] ^ 0x22222222u) |
-                                           zbytes(w[2] ^ 0x22222222u) | zbytes(w[3] ^ 0x22222222u)) != 0u))
+      const bool high = kJson ? ((fj_bytes(w[0]) | fj_bytes(w[1]) | fj_bytes(w[2]) | fj_bytes(w[3])) != 0u)
                               : ((w[0] | w[1] | w[2] | w[3]) & 0x80808080u) != 0u;
       if (kNone) {
-        const uint64_t hh = __ballot(high), xx = __ballot(spec);
-        if (lane == 0) {
-          bm2[2 * (r0 + i)] = make_ulonglong2(0ull, hh);
-          bm2[2 * (r0 + i) + 1] = make_ulonglong2(xx, 0ull);
-        }
+        const uint64_t hh = __ballot(high);
+        if (lane == 0) bm2[r0 + i] = make_ulonglong2(0ull, hh);
         continue;
       }
       if (upper) {
@@ -1442,15 +1436,7 @@ __global__ __launch_bounds__(256) void k_flat_scan(EvalArgs a, uint32_t stage) {
         }
       }
       const uint64_t hb = __ballot(hit), hh = __ballot(high);
-      if (kJson) {  // four words per round: occurrences, interesting, special, 0
-        const uint64_t xx = __ballot(spec);
-        if (lane == 0) {
-          bm2[2 * (r0 + i)] = make_ulonglong2(hb, hh);
-          bm2[2 * (r0 + i) + 1] = make_ulonglong2(xx, 0ull);
-        }
-      } else if (lane == 0) {
-        bm2[r0 + i] = make_ulonglong2(hb, hh);
-      }
+      if (lane == 0) bm2[r0 + i] = make_ulonglong2(hb, hh);
     }
   }
 }
@@ -1723,15 +1709,15 @@ constexpr uint32_t kFjHead = 64, kFjTail = 80, kFjSlot = kFjHead + kFjTail;  // 
 struct FjCur {
   const uint8_t* B;
   uint8_t* W;                     // this thread's LDS slot: head window, then tail window
-  const unsigned long long* fbm;  // four words per round r: occurrences, interesting, special at fbm[4 r + 0..2]
+  const unsigned long long* fbm;  // two words per round r: occurrences, interesting at fbm[2 r], fbm[2 r + 1]
   uint64_t cb;                    // B's chunk index in the slice
   uint32_t hb, tb;                // offsets of the head / tail windows
   uint32_t c;                     // chunk of v (the current chunk) and m its interesting bytes
   uint4 v;
   uint32_t m;
   bool mv;                        // m computed
-  uint64_t wb;                    // the slice rounds wb, wb + 1 preloaded: interesting j0, j1; special x0, x1
-  unsigned long long j0, j1, x0, x1;
+  uint64_t wb;                    // the slice rounds wb, wb + 1 preloaded: interesting words j0, j1
+  unsigned long long j0, j1;
   // the slot offset of position p, or >= kFjSlot outside both windows
   __device__ __forceinline__ uint32_t loff(uint32_t p) const {
     const uint32_t dh = p - hb, dt = p - tb;
@@ -1750,14 +1736,7 @@ struct FjCur {
   __device__ __forceinline__ uint32_t mask(uint32_t ci) {  // interesting bytes of chunk ci
     chunk(ci);
     if (!mv) {
-      const uint64_t ac = cb + ci, r = ac >> 6;
-      const unsigned long long xw = r == wb ? x0 : r == wb + 1 ? x1 : fbm[4 * r + 2];
-      if ((xw >> (ac & 63u)) & 1ull) {
-        m = fj_mask(v);
-      } else {  // no special byte in the chunk (the scan's bitmap): its quotes only
-        m = nib4(zbytes(v.x ^ 0x22222222u)) | (nib4(zbytes(v.y ^ 0x22222222u)) << 4) |
-            (nib4(zbytes(v.z ^ 0x22222222u)) << 8) | (nib4(zbytes(v.w ^ 0x22222222u)) << 12);
-      }
+      m = fj_mask(v);
       mv = true;
     }
     return m;
@@ -1804,7 +1783,7 @@ struct FjCur {
   __device__ __forceinline__ uint32_t next(uint32_t ci, uint32_t lim) {
     while (ci < lim) {
       const uint64_t ac = cb + ci, r = ac >> 6;
-      unsigned long long w = r == wb ? j0 : r == wb + 1 ? j1 : fbm[4 * r + 1];
+      unsigned long long w = r == wb ? j0 : r == wb + 1 ? j1 : fbm[2 * r + 1];
       w &= ~0ull << (ac & 63u);
       if (w) {
         const uint32_t x = ci + (uint32_t)__builtin_ctzll(w) - (uint32_t)(ac & 63u);
@@ -2014,7 +1993,7 @@ __device__ __forceinline__ FjRec fj_frame(const uint8_t* S, const FlatHdr& H, ui
 // bitmap rounds over its first chunk, its trailer (the headers varint)
 struct FjLoads {
   uint4 h0, h1, h2, h3, t0, t1, t2, t3, t4;
-  ulonglong2 bw0, bw1, bx0, bx1;  // rounds wb, wb + 1: (occurrences, interesting), (special, 0)
+  ulonglong2 bw0, bw1;  // rounds wb, wb + 1: (occurrences, interesting)
   uint32_t tw;
   uint64_t tc;
 };
@@ -2033,14 +2012,15 @@ __device__ __forceinline__ FjLoads fj_issue(const uint8_t* S, const unsigned lon
   L.t2 = tp[2];
   L.t3 = tp[3];
   L.t4 = tp[4];
-  L.bw0 = *(const ulonglong2*)(fbm + 4 * wb);
-  L.bx0 = *(const ulonglong2*)(fbm + 4 * wb + 2);
-  L.bw1 = *(const ulonglong2*)(fbm + 4 * wb + 4);
-  L.bx1 = *(const ulonglong2*)(fbm + 4 * wb + 6);
+  L.bw0 = *(const ulonglong2*)(fbm + 2 * wb);
+  L.bw1 = *(const ulonglong2*)(fbm + 2 * wb + 2);
   L.tw = ld_u32_at(S + r.ve);
   return L;
 }
-__global__ __launch_bounds__(256) void k_fj_decide(EvalArgs a) {
+#ifndef FSG_FJ_WPE
+#define FSG_FJ_WPE 3  // waves per SIMD of k_fj_decide (<= 168 VGPRs, no scratch)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FSG_FJ_WPE))) void k_fj_decide(EvalArgs a) {
   __shared__ uint4 slots[256 * (kFjSlot / 16) + 1];  // (+1: a word read past the last slot's end)
   const uint32_t b = blockIdx.x * 256 + threadIdx.x;
   if (b >= a.nbatches) return;
@@ -2058,7 +2038,7 @@ __global__ __launch_bounds__(256) void k_fj_decide(EvalArgs a) {
   const uint32_t fl = proj ? pd.needle_len : 0u;
   uint64_t fw = 0;  // a field name of <= 8 bytes as a word
   for (uint32_t t = 0; t < fl && fl <= 8; t++) fw |= (uint64_t)fld[t] << (8 * t);
-  const unsigned long long* hit_bm = a.fbm;  // k_flat_scan<., kJson>: occurrence word w at [4 w]
+  const unsigned long long* hit_bm = a.fbm;  // k_flat_scan<., kJson>: occurrence word w at [2 w]
   const uint8_t* S = a.slice;
   const uint64_t pos = a.bpos[b];
   const uint64_t nxt = b + 1 < a.nbatches ? a.bpos[b + 1] : a.slice_len;
@@ -2122,8 +2102,6 @@ __global__ __launch_bounds__(256) void k_fj_decide(EvalArgs a) {
     C.wb = wb;
     C.j0 = bw0.y;
     C.j1 = bw1.y;
-    C.x0 = L.bx0.x;
-    C.x1 = L.bx1.x;
     // the next record: framed now, its loads in flight during this walk
     if (n + 1 < count) {
       R = fj_frame(S, H, q, sec_end);
@@ -2138,7 +2116,7 @@ __global__ __launch_bounds__(256) void k_fj_decide(EvalArgs a) {
       const unsigned long long mb0 = bw0.x, mb1 = bw1.x;
       auto bits_any = [&](uint64_t x0, uint64_t x1) {
         if (x1 <= x0) return false;
-        if (x1 > (wb + 2) << 6) return flat_any<4>(hit_bm, x0, x1);
+        if (x1 > (wb + 2) << 6) return flat_any(hit_bm, x0, x1);
         const uint64_t lo = x0 - (wb << 6), hi = x1 - (wb << 6);  // in [0, 128]
         const unsigned long long m0 = (lo < 64 ? (~0ull << lo) : 0ull) & (hi >= 64 ? ~0ull : ((1ull << hi) - 1ull));
         const unsigned long long m1 = (hi > 64 ? (hi >= 128 ? ~0ull : ((1ull << (hi - 64)) - 1ull)) : 0ull) &
@@ -2162,7 +2140,7 @@ __global__ __launch_bounds__(256) void k_fj_decide(EvalArgs a) {
             }
             const uint64_t r = c - (wb << 6);
             const bool bt = c >= (wb << 6) && r < 128 ? (((r < 64 ? mb0 : mb1) >> (r & 63)) & 1ull) != 0ull
-                                                      : bm_bit<4>(hit_bm, c);
+                                                      : bm_bit(hit_bm, c);
             if (!bt) continue;
             const uint64_t lo = (c << 4) >= va + blo ? (c << 4) - blo : va;
             const uint64_t hi = (c << 4) + bhi <= sl ? (c << 4) + bhi : sl;

@@ -2131,8 +2131,8 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   bool flat = false, fjson = false;
   if ((fst >= 0 || fjf >= 0) && !c->no_flat) {
     ea.fbm_words = (s->len + 1023) / 1024;
-    // (two words per 1 KiB round, four on the JSON path; + the rounds past the last)
-    const bool have = c->fbm.ensure((size_t)ea.fbm_words * (fst >= 0 ? 16 : 32) + 64) == hipSuccess;
+    // (two words per 1 KiB round; + the rounds past the last)
+    const bool have = c->fbm.ensure((size_t)ea.fbm_words * 16 + 64) == hipSuccess;
     (void)hipGetLastError();
     if (have) {
       ea.fbm = c->fbm.as<unsigned long long>();
