@@ -254,7 +254,10 @@ int fsg_slice_verify_crc(const fsg_slice *s, uint64_t *n_bad, int64_t *first_bad
 /* Starts the same check on the slice's own stream and returns at once, so a
  * fetch verifies while fsg_chain_process_slice runs on the same (read-only)
  * bytes; the next fsg_slice_verify_crc returns its result.  Reframing or
- * re-uploading the slice waits for it first. */
+ * re-uploading the slice waits for it first.  The slice must be fully framed
+ * when this is called: nothing on the device orders the verify after the
+ * framing, which holds because fsg_slice_upload and fsg_slice_reframe return
+ * only once their framing (and the batch table it writes) is complete. */
 int fsg_slice_verify_crc_start(const fsg_slice *s);
 void fsg_slice_free(fsg_slice *s);
 /* process_batch over a resident slice; the output batch stays in HBM until

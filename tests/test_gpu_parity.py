@@ -2157,6 +2157,46 @@ def test_writer_long_records(engine, chain):
 
 @pytest.mark.parametrize("chain", [
     [("aggregate-sum", {}, b"7")],
+    [("aggregate-sum", {}, b" -5 ")],
+    [("filter_odd", {}, None)],
+    [("map_double", {}, None)],
+    [("map_double", {}, None), ("filter_map", {}, None)],
+    [("filter_map", {}, None), ("aggregate-sum", {}, None)],
+])
+def test_int_path_edge_values(engine, chain):
+    """k_eval_int on the values its branches special-case, with no deferral:
+    '+' signs, -0, the i32 bounds, map_double / the aggregate's sum wrapping,
+    and (aggregate-sum alone, which trims) surrounding whitespace; batches of
+    more than 128 records, every output record and accumulator vs the oracle."""
+    rnd = random.Random(5)
+    agg_only = chain[0][0] == "aggregate-sum"
+    pool = ["+7", "-0", "0", "2147483647", "-2147483648", "1073741824", "-1073741825", "+0", "-1", "12"]
+    if agg_only:
+        pool += [" 12\t", "\t-3", "+4 ", "\n2147483647\r", " 0 ", "\x0b9\x0c"]
+    sl, base = b"", 0
+    for k in range(12):
+        n = rnd.choice([129, 200, 300])
+        b = P.Batch(base_offset=base)
+        for j in range(n):
+            b.add_record(P.Record.new(rnd.choice(pool).encode()))
+        sl += b.encode()
+        base += n
+    g = gpu_chain(engine, chain)
+    o = orc_chain(chain)
+    for _ in range(2):
+        gout = g.process_batch(sl)
+        oo = o.process_batch(sl, (1 << 64) - 1)
+        assert oo["status"] == 0
+        assert gout.raw == oo["bytes"]
+        t = g.last_timings()
+        assert t["eval_path"] == 5 and t["deferred"] == 0, t  # FSG_EVAL_INT
+        for i, m in enumerate(chain):
+            if m[0] == "aggregate-sum":
+                assert g.accumulator(i) == o.accumulator(i)
+
+
+@pytest.mark.parametrize("chain", [
+    [("aggregate-sum", {}, b"7")],
     [("filter_odd", {}, None)],
     [("map_double", {}, None), ("filter_map", {}, None)],
     [("filter_map", {}, None), ("aggregate-sum", {}, None)],
