@@ -272,6 +272,7 @@ struct EvalArgs {
   const uint64_t* rbase;
   uint32_t nbatches;
   uint32_t flat_st;    // EVAL_FLAT: the substring stage of the flat path | its needle length << 8
+  int32_t chain_host_max_len;  // EVAL_RX: the regex stage's max_len (host copy for the launch)
   const ChainDesc* chain;
   const uint8_t* blob;
   BatchStat* bstat;

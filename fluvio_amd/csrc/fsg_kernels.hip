@@ -3708,12 +3708,14 @@ void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s) {
     // k_eval_int over every batch (starts from k_chase_w, kept with the slice), then the deferred list
     launch_eval_int(a, (ops & opbit(OP_AGG_SUM)) != 0, s);
     grid = a.nbatches < 2048u ? a.nbatches : 2048u;
-  } else if (mode == EVAL_LEAN || mode == EVAL_FLAT || mode == EVAL_FJSON) {
-    // k_chase + k_eval_lean, or the flat substring / JSON kernels (fsg_lean.hip)
+  } else if (mode == EVAL_LEAN || mode == EVAL_FLAT || mode == EVAL_FJSON || mode == EVAL_RX) {
+    // k_chase + k_eval_lean, or the flat substring / JSON / regex kernels (fsg_lean.hip)
     if (mode == EVAL_FLAT)
       launch_eval_flat(a, a.flat_st, s);
     else if (mode == EVAL_FJSON)
       launch_eval_fjson(a, s);
+    else if (mode == EVAL_RX)
+      launch_eval_rx(a, a.flat_st, s);
     else
       launch_eval_lean(a, ops, s);
     grid = a.nbatches < 2048u ? a.nbatches : 2048u;  // persistent over the deferred list

@@ -13,7 +13,8 @@ hipError_t upload_crc_tables();
 // EVAL_INT = k_eval_int over every batch (record starts in a.rstart / a.rend from k_chase_w), then k_eval over
 // its deferred list
 // EVAL_FJSON = k_flat_scan<., kJson> + k_fj_decide (a.flat_st = fjson_flags, a.fbm), then k_eval over the deferred list
-enum EvalMode { EVAL_EXACT = 0, EVAL_LEAN = 1, EVAL_ARRAY = 3, EVAL_FLAT = 4, EVAL_INT = 5, EVAL_FJSON = 6 };
+// EVAL_RX = k_rx_scan + k_rx_decide (a.flat_st = the regex stage, a.fbm), then k_eval over the deferred list
+enum EvalMode { EVAL_EXACT = 0, EVAL_LEAN = 1, EVAL_ARRAY = 3, EVAL_FLAT = 4, EVAL_INT = 5, EVAL_FJSON = 6, EVAL_RX = 7 };
 void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s);
 // k_chase + k_eval_lean (fsg_lean.hip), the kernel variant picked by the chain's stage ops
 void launch_eval_lean(const EvalArgs& a, uint32_t ops, hipStream_t s);
@@ -25,6 +26,10 @@ void launch_eval_flat(const EvalArgs& a, uint32_t flat_st, hipStream_t s);
 // (needle 4..128 bytes) and uppercase maps beside them; its launch flags for a.flat_st, or -1
 int fjson_flags(const ChainDesc& ch, uint32_t ops);
 void launch_eval_fjson(const EvalArgs& a, hipStream_t s);
+// the flat regex path (fsg_lean.hip): one bounded regex stage (ASCII DFA <= 16 states, max_len <= 17) and
+// uppercase maps; the stage or -1
+int rx_flat_stage(const ChainDesc& ch, uint32_t ops);
+void launch_eval_rx(const EvalArgs& a, uint32_t stage, hipStream_t s);
 // integer-stage chains (filter_odd, map_double, filter_map, a final aggregate-sum) over decimal values (fsg_lean.hip)
 bool int_lean_eligible(const ChainDesc& ch, uint32_t ops);
 void launch_eval_int(const EvalArgs& a, bool agg, hipStream_t s);

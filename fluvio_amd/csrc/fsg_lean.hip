@@ -1945,7 +1945,8 @@ struct FjRec {
   uint8_t attr, tag;
   bool ok;
 };
-__device__ __forceinline__ FjRec fj_frame(const uint8_t* S, const FlatHdr& H, uint64_t q, uint64_t sec_end) {
+__device__ __forceinline__ FjRec fj_frame(const uint8_t* S, const FlatHdr& H, uint64_t q, uint64_t sec_end,
+                                          bool allow_empty = false) {
   FjRec r;
   r.q = q;
   r.kpos = 0;
@@ -1986,9 +1987,228 @@ __device__ __forceinline__ FjRec fj_frame(const uint8_t* S, const FlatHdr& H, ui
   r.ok = r.ok && nb != 0 && vlen >= 0;
   r.va = p + nb;
   r.ve = r.va + (uint64_t)vlen;
-  r.ok = r.ok && r.ve <= r.end && r.ve > r.va;  // (an empty value is a serde error: k_eval)
+  r.ok = r.ok && r.ve <= r.end && (allow_empty || r.ve > r.va);  // (JSON: an empty value is a serde error, k_eval)
   return r;
 }
+// ---------------------------------------------------------------------------
+// Flat regex path: a chain whose one scanning stage is a bounded regex filter
+// (regex-filter / filter_regex, smartmodule/regex-filter/src/lib.rs:24-28:
+// Regex::is_match on the value) whose ASCII DFA has <= 16 states and a longest
+// match of <= 17 bytes (no word boundaries, no multi-line anchors: the compiler
+// then gives a restart state s_mid that needs no previous byte).
+//   k_rx_scan    every 16-byte chunk C of the slice once, as a flat array: the
+//                DFA from s_mid over the chunk's window [16 C - ctx, 16 C + 16)
+//                (ctx = 4 ceil((max_len - 1) / 4) bytes of the previous chunk);
+//                bit "the sticky accept was reached in the window" and bit "a
+//                byte >= 0x80 in the chunk", one 64-bit ballot each per 1 KiB
+//                round (k_flat_scan's interleaved layout)
+//   k_rx_decide  one thread per batch (k_flat_decide's framing): a record
+//                matches when an interior chunk (window inside the value) has
+//                the bit; the chunks whose windows leave the value (its first
+//                chunks, its last) are decided by an exact scan of their bytes
+//                (from s_bot at the value start, acceptance at its end), which
+//                an anchor-free pattern (s_bot = s_mid, no end-only accept)
+//                skips when their bits are clear.  Every match of at most
+//                max_len bytes lies in the window of the chunk holding its last
+//                byte, so the bits plus the edge scans see every match.
+// ---------------------------------------------------------------------------
+template <int kCtx>  // context dwords before each chunk: ceil((max_len - 1) / 4)
+__global__ __launch_bounds__(256) void k_rx_scan(EvalArgs a, uint32_t stage) {
+  __shared__ unsigned long long T[256];
+  const StageDesc& sd = a.chain->st[stage];
+  const bool upper = sd.in_type == VT_SRC_UPPER;
+  T[threadIdx.x] = ((const unsigned long long*)(a.blob + (upper ? sd.dfa.tt_up : sd.dfa.tt)))[threadIdx.x];
+  __syncthreads();
+  const uint32_t s0 = sd.dfa.s_mid, acc1 = sd.dfa.acc1;
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+  const uint64_t nrounds = a.fbm_words;
+  const uint64_t w0 = (uint64_t)blockIdx.x * 4 + wv;
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  ulonglong2* bm2 = (ulonglong2*)a.fbm;
+  for (uint64_t r0 = w0 * kFlatRounds; r0 < nrounds; r0 += nw * kFlatRounds) {
+    uint4 v[kFlatRounds], pv[kFlatRounds];
+#pragma unroll
+    for (int i = 0; i < kFlatRounds; i++) {  // every round's loads in flight before the first use
+      const uint64_t c = (r0 + i) * 1024 + lane * 16;
+      v[i] = r0 + i < nrounds ? *(const uint4*)(a.slice + c) : make_uint4(0, 0, 0, 0);
+      if (kCtx) pv[i] = r0 + i < nrounds && c >= 16 ? *(const uint4*)(a.slice + c - 16) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < kFlatRounds; i++) {
+      if (r0 + i >= nrounds) break;  // uniform
+      uint32_t w[4 + kCtx];
+#pragma unroll
+      for (int d = 0; d < kCtx; d++) w[d] = u4_dw(pv[i], (uint32_t)(4 - kCtx + d));
+      w[kCtx] = v[i].x;
+      w[kCtx + 1] = v[i].y;
+      w[kCtx + 2] = v[i].z;
+      w[kCtx + 3] = v[i].w;
+      unsigned long long row[4 * (4 + kCtx)];
+#pragma unroll
+      for (int k = 0; k < 4 * (4 + kCtx); k++) row[k] = T[(w[k >> 2] >> (8 * (k & 3))) & 0xFFu];  // rows ahead of the chain
+      uint32_t st = s0;
+#pragma unroll
+      for (int k = 0; k < 4 * (4 + kCtx); k++) st = (uint32_t)(row[k] >> (4 * st)) & 15u;
+      const bool hit = (acc1 >> st) & 1u;
+      const bool high = ((v[i].x | v[i].y | v[i].z | v[i].w) & 0x80808080u) != 0u;
+      const uint64_t hb = __ballot(hit), hh = __ballot(high);
+      if (lane == 0) bm2[r0 + i] = make_ulonglong2(hb, hh);
+    }
+  }
+}
+// the DFA over bytes [p0, p1) of S from state st (the rows in T); the sticky accept, or acceptance at the end
+__device__ __forceinline__ uint32_t rx_run(const unsigned long long* T, const uint8_t* S, uint64_t p0, uint64_t p1, uint32_t st) {
+  for (uint64_t p = p0; p < p1; p++) st = (uint32_t)(T[S[p]] >> (4 * st)) & 15u;
+  return st;
+}
+__global__ __launch_bounds__(256) void k_rx_decide(EvalArgs a, uint32_t stage) {
+  __shared__ unsigned long long T[256];
+  const StageDesc& sd = a.chain->st[stage];
+  const bool upper = sd.in_type == VT_SRC_UPPER;
+  T[threadIdx.x] = ((const unsigned long long*)(a.blob + (upper ? sd.dfa.tt_up : sd.dfa.tt)))[threadIdx.x];
+  __syncthreads();
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= a.nbatches) return;
+  const uint32_t s_bot = sd.dfa.s_bot, s_mid = sd.dfa.s_mid, acc1 = sd.dfa.acc1, acc2 = sd.dfa.acc2;
+  const uint32_t ml = (uint32_t)sd.dfa.max_len;
+  const uint64_t ctx = 4 * ((ml + 2) / 4);  // context bytes of a chunk's window (k_rx_scan's kCtx dwords)
+  const bool free_ = s_bot == s_mid && (acc2 & ~acc1) == 0u;  // no begin / end anchors: clear bits decide edges
+  const bool keep_match = sd.keep_match != 0;
+  const bool out_upper = a.chain->out_type == VT_SRC_UPPER;
+  const unsigned long long* hit_bm = a.fbm;  // interleaved: window bits of round w at [2 w], high bytes at [2 w + 1]
+  const unsigned long long* hi_bm = a.fbm + 1;
+  const uint8_t* S = a.slice;
+  const uint64_t pos = a.bpos[b];
+  const uint64_t nxt = b + 1 < a.nbatches ? a.bpos[b + 1] : a.slice_len;
+  const uint64_t rb = a.rbase[b], rn = (b + 1 < a.nbatches ? a.rbase[b + 1] : a.nrec) - rb;
+  const uint64_t al = pos & ~15ull;
+  uint64_t wl = nxt > al ? nxt - al : 0;
+  if (wl > (uint64_t)kLeanWin) wl = kLeanWin;
+  const uint64_t wlen = (wl + 15) & ~15ull;
+  const uint32_t batch_len = __builtin_bswap32(ld_u32_at(S + pos + 8));
+  const uint64_t sec0 = pos + 57, sec_end = pos + 12 + (uint64_t)batch_len;
+  const uint64_t sec_len = sec_end - sec0;
+  const int32_t count = sec_len >= 4 ? (int32_t)__builtin_bswap32(ld_u32_at(S + sec0)) : -1;
+  bool ok = sec_len >= 4 && sec_end - al <= wlen && count >= 0 && count <= kLeanMaxR && (uint64_t)count == rn;
+  uint32_t nkeep = 0;
+  uint64_t q = sec0 + 4;  // absolute start of record n
+  FlatHdr H = flat_hdr(S, ok && count > 0 ? q : sec0);
+  for (int32_t n = 0; ok && n < count; n++) {
+    const FjRec R = fj_frame(S, H, q, sec_end, true);
+    ok = R.ok;
+    if (!ok) break;
+    const uint64_t end = R.end;
+    const FlatHdr Hn = flat_hdr(S, n + 1 < count ? end : q);  // the next record's header, in flight now
+    const uint64_t va = R.va, ve = R.ve;
+    // every load of this record at once: trailer, bitmap words, edge chunks
+    const uint32_t tw = ld_u32_at(S + ve);
+    const uint64_t c0 = va >> 4, c1 = (ve + 15) >> 4, i0 = (va + 15) >> 4, i1 = ve >> 4;
+    const uint64_t wb = c0 >> 6;  // first bitmap word touching the value
+    const ulonglong2 bw0 = *(const ulonglong2*)(a.fbm + 2 * wb), bw1 = *(const ulonglong2*)(a.fbm + 2 * wb + 2);
+    const unsigned long long mb0 = bw0.x, hb0 = bw0.y, mb1 = bw1.x, hb1 = bw1.y;
+    const uint4 ea = *(const uint4*)(S + (c0 << 4));
+    const uint4 eb = *(const uint4*)(S + (((ve ? ve - 1 : 0) >> 4) << 4));
+    int64_t hdr;
+    uint32_t nb = var4(tw, hdr);
+    ok = nb != 0 && ve + nb == end;
+    if (!ok) break;
+    auto bits_any = [&](const unsigned long long* bm, unsigned long long w0v, unsigned long long w1v, uint64_t x0,
+                        uint64_t x1) {
+      if (x1 <= x0) return false;
+      if (x1 > (wb + 2) << 6) return flat_any(bm, x0, x1);
+      const uint64_t lo = x0 - (wb << 6), hi = x1 - (wb << 6);  // in [0, 128]
+      const unsigned long long m0 = (lo < 64 ? (~0ull << lo) : 0ull) & (hi >= 64 ? ~0ull : ((1ull << hi) - 1ull));
+      const unsigned long long m1 = (hi > 64 ? (hi >= 128 ? ~0ull : ((1ull << (hi - 64)) - 1ull)) : 0ull) &
+                                    (lo > 64 ? (~0ull << (lo - 64)) : ~0ull);
+      return ((w0v & m0) | (w1v & m1)) != 0ull;
+    };
+    // bytes >= 0x80 in the value: chunks inside it by their bits, the edge
+    // chunks (which hold gap bytes) by their bytes
+    if (ve > va) {
+      bool hi = bits_any(hi_bm, hb0, hb1, i0, i1);
+      auto hi_edge = [&](const uint4& u, uint64_t c) {
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+        uint32_t f = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          f |= w[k] & bytes_in((uint32_t)(((c << 4) + 4 * k) - al), (uint32_t)(va - al), (uint32_t)(ve - al));
+        return (f & 0x80808080u) != 0u;
+      };
+      if (!hi && c0 < i0) hi = hi_edge(ea, c0);
+      if (!hi && i1 < c1 && (i1 >= i0 || c0 != i1)) hi = hi_edge(eb, i1);
+      ok = !hi;
+      if (!ok) break;
+    }
+    bool match;
+    if (ve == va) {
+      match = (((acc1 | acc2) >> s_bot) & 1u) != 0u;
+    } else {
+      const uint64_t l1 = (ve - 1) >> 4;                      // the value's last chunk
+      const uint64_t j0 = (va + ctx + 15) >> 4, j1 = ve >> 4;  // interior chunks [j0, j1): window inside the value
+      match = j0 < j1 && bits_any(hit_bm, mb0, mb1, j0, j1);
+      if (!match) {
+        // head chunks [c0, h1) hold the matches ending near the value start,
+        // tail chunks [t0, l1] those ending near its end; an anchored pattern
+        // scans both always (a ^ match can end in an interior chunk, a $ match
+        // at an aligned end has no tail chunk)
+        const uint64_t h1 = j0 < l1 + 1 ? j0 : l1 + 1, t0 = j1 > j0 ? j1 : j0;
+        const bool head = !free_ || bits_any(hit_bm, mb0, mb1, c0, h1);
+        const bool tail = free_ ? t0 <= l1 && bits_any(hit_bm, mb0, mb1, t0, l1 + 1) : true;
+        uint64_t he = (h1 << 4) < ve ? (h1 << 4) : ve;  // the head scan's end
+        if (!free_ && he < va + ml) he = va + ml < ve ? va + ml : ve;
+        if (head) {  // from the value start
+          const uint32_t st = rx_run(T, S, va, he, s_bot);
+          match = ((acc1 >> st) & 1u) || (he == ve && ((acc2 >> st) & 1u));
+        }
+        if (!match && tail && !(head && he == ve)) {
+          const uint64_t e = t0 <= l1 ? (t0 << 4) : ve - 1;  // the earliest end of a match left to see
+          const uint64_t back = ml ? ml - 1 : 0;
+          const uint64_t st0 = e > va + back ? e - back : va;
+          const uint32_t st = rx_run(T, S, st0, ve, st0 == va ? s_bot : s_mid);
+          match = ((acc1 >> st) & 1u) || ((acc2 >> st) & 1u);
+        }
+      }
+    }
+    if (match == keep_match) {
+      KeptRec d;
+      d.src = q;
+      d.vpos = va;
+      d.kpos = R.tag ? R.kpos : 0;
+      d.od = R.od;
+      d.ts = R.ts;
+      d.hdr = hdr;
+      d.vlen = (uint32_t)(ve - va);
+      d.klen = R.klen;
+      d.ival = 0;
+      d.mode = out_upper ? KM_UPPER : KM_COPY;
+      d.has_key = R.tag;
+      d.attr = R.attr;
+      d.pad = 0;
+      a.desc[rb + nkeep++] = d;
+    }
+    q = end;
+    H = Hn;
+  }
+  ok = ok && q == sec_end;
+  if (!ok) {  // the exact kernel frames and evaluates this batch
+    a.rend[b] = 0xFFFFu;
+    const uint32_t i = atomicAdd(&a.list[0], 1u);
+    a.list[1 + i] = b;
+    return;
+  }
+  const uint8_t* h = S + pos;  // batch header (file format, batch.rs:163-180)
+  BatchStat st = {};
+  st.base_offset = (int64_t)rd_be(h, 8);
+  st.lod_in = (int32_t)rd_be(h + 23, 4);
+  st.first_ts = (int64_t)rd_be(h + 27, 8);
+  st.comp = (uint32_t)h[22] & 7u;
+  st.flags = BF_LAST_STAGE;
+  st.nkeep = st.nout = nkeep;
+  st.sec_len = (uint32_t)sec_len;
+  st.err_stage = 0xFFFFFFFFu;
+  a.bstat[b] = st;
+}
+
 // a record's loads, issued together: its value's head and tail windows, the
 // bitmap rounds over its first chunk, its trailer (the headers varint)
 struct FjLoads {
@@ -2505,6 +2725,34 @@ void launch_eval_fjson(const EvalArgs& a, hipStream_t s) {
   else
     hipLaunchKernelGGL((k_flat_scan<false, true, false>), dim3(g1), dim3(256), 0, s, a, sub);
   hipLaunchKernelGGL(k_fj_decide, dim3(g2), dim3(256), 0, s, a);
+}
+
+int rx_flat_stage(const ChainDesc& ch, uint32_t ops) {
+  if (ops & ~((1u << OP_REGEX) | (1u << OP_MAP_UPPER))) return -1;
+  int st = -1;
+  for (uint32_t k = 0; k < ch.nstages; k++)
+    if (ch.st[k].op == OP_REGEX) {
+      if (st >= 0) return -1;  // several regex stages: k_eval_lean
+      st = (int)k;
+    }
+  if (st < 0) return -1;
+  const DfaDesc& d = ch.st[st].dfa;
+  return d.lean && d.max_len >= 0 && d.max_len <= 17 ? st : -1;
+}
+void launch_eval_rx(const EvalArgs& a, uint32_t stage, hipStream_t s) {
+  if (!a.nbatches) return;
+  const uint32_t ml = (uint32_t)a.chain_host_max_len;
+  const uint64_t waves = (a.fbm_words + kFlatRounds - 1) / kFlatRounds;
+  const uint32_t g1 = (uint32_t)std::max<uint64_t>(std::min<uint64_t>((waves + 3) / 4, 4096), 1);
+  const uint32_t g2 = (a.nbatches + 255) / 256;
+  switch ((ml + 2) / 4) {  // context dwords of a chunk's window
+    case 0: hipLaunchKernelGGL(k_rx_scan<0>, dim3(g1), dim3(256), 0, s, a, stage); break;
+    case 1: hipLaunchKernelGGL(k_rx_scan<1>, dim3(g1), dim3(256), 0, s, a, stage); break;
+    case 2: hipLaunchKernelGGL(k_rx_scan<2>, dim3(g1), dim3(256), 0, s, a, stage); break;
+    case 3: hipLaunchKernelGGL(k_rx_scan<3>, dim3(g1), dim3(256), 0, s, a, stage); break;
+    default: hipLaunchKernelGGL(k_rx_scan<4>, dim3(g1), dim3(256), 0, s, a, stage); break;
+  }
+  hipLaunchKernelGGL(k_rx_decide, dim3(g2), dim3(256), 0, s, a, stage);
 }
 
 void launch_eval_lean(const EvalArgs& a, uint32_t ops, hipStream_t s) {

@@ -551,6 +551,7 @@ struct fsg_chain {
   DevBuf fbm;            // flat substring path: occurrence / high-byte bits per 16-byte chunk
   bool no_flat = getenv("FSG_NO_FLAT") != nullptr;  // A/B: the flat path off (k_eval_lean instead)
   bool no_fjson = getenv("FSG_NO_FJSON") != nullptr;  // A/B: the flat JSON path off (k_eval_lean instead)
+  bool no_frx = getenv("FSG_NO_FRX") != nullptr;      // A/B: the flat regex path off (k_eval_lean instead)
   bool no_int = getenv("FSG_NO_INT") != nullptr;    // A/B: integer chains through k_eval alone
   // the one-batch process() path (k_one): zeros for bpos / rbase, the device
   // block Plan | BatchStat | Mins | output batch, and coherent pinned memory
@@ -2128,8 +2129,10 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   const int fst = lean ? flat_stage(c->hdesc, ops) : -1;
   // filter_json / projection (with at most one substring stage): the flat JSON path
   const int fjf = lean && fst < 0 && !c->no_fjson ? fjson_flags(c->hdesc, ops) : -1;
-  bool flat = false, fjson = false;
-  if ((fst >= 0 || fjf >= 0) && !c->no_flat) {
+  // one bounded regex stage: the flat regex path
+  const int rxs = lean && fst < 0 && fjf < 0 && !c->no_frx ? rx_flat_stage(c->hdesc, ops) : -1;
+  bool flat = false, fjson = false, frx = false;
+  if ((fst >= 0 || fjf >= 0 || rxs >= 0) && !c->no_flat) {
     ea.fbm_words = (s->len + 1023) / 1024;
     // (two words per 1 KiB round; + the rounds past the last)
     const bool have = c->fbm.ensure((size_t)ea.fbm_words * 16 + 64) == hipSuccess;
@@ -2139,9 +2142,13 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
       if (fst >= 0) {
         flat = true;
         ea.flat_st = (uint32_t)fst | (c->hdesc.st[fst].needle_len << 8);
-      } else {
+      } else if (fjf >= 0) {
         fjson = true;
         ea.flat_st = (uint32_t)fjf;
+      } else {
+        frx = true;
+        ea.flat_st = (uint32_t)rxs;
+        ea.chain_host_max_len = c->hdesc.st[rxs].dfa.max_len;
       }
     }
   }
@@ -2173,7 +2180,9 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     }
   }
   if (lean || arr || ints) HIPCHK(hipMemsetAsync(ea.list, 0, sizeof(uint32_t), st));
-  launch_eval(ea, ops, flat ? EVAL_FLAT : fjson ? EVAL_FJSON : lean ? EVAL_LEAN : arr ? EVAL_ARRAY : ints ? EVAL_INT : EVAL_EXACT,
+  launch_eval(ea, ops,
+              flat ? EVAL_FLAT : fjson ? EVAL_FJSON : frx ? EVAL_RX : lean ? EVAL_LEAN : arr ? EVAL_ARRAY
+              : ints ? EVAL_INT : EVAL_EXACT,
               st);
   HIPCHK(hipGetLastError());
   if (c->timed) HIPCHK(hipEventRecord(c->ev[1], st));
@@ -2395,7 +2404,8 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   if (dedup) HIPCHK(hipMemcpyAsync(sfs, sfa.scal, sizeof sfs, hipMemcpyDeviceToHost, st));
   HIPCHK(wait_stream(st));
   memcpy(&c->hplan, c->hpin.p, sizeof(Plan));
-  c->last.eval_path = flat ? FSG_EVAL_FLAT : fjson ? FSG_EVAL_FJSON : lean ? FSG_EVAL_LEAN : arr ? FSG_EVAL_ARRAY
+  c->last.eval_path = flat ? FSG_EVAL_FLAT : fjson ? FSG_EVAL_FJSON : frx ? FSG_EVAL_RX : lean ? FSG_EVAL_LEAN
+                    : arr ? FSG_EVAL_ARRAY
                     : ints ? FSG_EVAL_INT : FSG_EVAL_EXACT;
   c->last.deferred = 0;
   if (lean || arr || ints) memcpy(&c->last.deferred, (const uint8_t*)c->hpin.p + sizeof(Plan), sizeof(uint32_t));

@@ -177,6 +177,9 @@ typedef struct fsg_timings {
 #define FSG_EVAL_FJSON 6 /* filter_json / field projection (+ one substring stage): the slice streamed as bytes
                             (k_flat_scan<., kJson>: JSON-interesting chunks), a thread per batch parses the
                             records' values as flat objects (k_fj_decide), deferred batches through k_eval */
+#define FSG_EVAL_RX 7    /* one bounded regex stage: the DFA over every 16-byte chunk's window of the flat slice
+                            (k_rx_scan), a thread per batch decides from the bits and the values' edges
+                            (k_rx_decide), deferred batches through k_eval */
 
 const char *fsg_last_error_message(void);
 int fsg_abi_version(void);

@@ -938,6 +938,65 @@ def test_lean_path_parity(engine, chain):
     check_batch(engine, chain, _lean_slice(seed=11, nbatches=25))
 
 
+RX_FLAT_CHAINS = [
+    [("regex-filter", {"regex": r"\d{3}-\d{2}-\d{4}"}, None)],          # C1: max_len 11, anchor-free
+    [("filter_regex", {}, None)],                                          # the same DFA, keep non-matches
+    [("regex-filter", {"regex": r"^\d{2}"}, None)],                      # begin anchor: head scans
+    [("regex-filter", {"regex": r"\d-\d$"}, None)],                      # end anchor: tail scans
+    [("regex-filter", {"regex": r"x?"}, None)],                           # matches the empty string
+    [("map", {}, None), ("regex-filter", {"regex": r"AB\d"}, None)],     # upper-cased rows
+    [("regex-filter", {"regex": r"\d{14}"}, None)],                        # max_len 14: four context dwords
+    [("regex-filter", {"regex": r"[a-c]b{5}"}, None)],                     # max_len 6: two context dwords
+    [("regex-filter", {"regex": r"q"}, None)],                            # max_len 1: no context
+]
+
+
+def _rx_slice(seed):
+    """Values of every length 0..70 and a few long ones, an SSN (or other
+    digit runs) at every offset around the value's start, end and 16-byte
+    chunk edges, digits in the record headers around it, some non-ASCII
+    batches (deferred) and keys."""
+    rnd = random.Random(seed)
+    out, base = b"", 0
+    for bi in range(60):
+        b = P.Batch(base_offset=base)
+        n = rnd.choice([1, 5, 17, 40, 64])
+        for j in range(n):
+            L = rnd.choice(list(range(0, 71)) + [200, 1000, 3000])
+            v = bytearray(rnd.choice(b"abcxyzAB ,.;:") for _ in range(L))
+            if L >= 11 and rnd.random() < 0.6:
+                p = rnd.choice([0, 1, L - 11, L - 12, rnd.randrange(L - 10)])
+                v[p:p + 11] = b"%03d-%02d-%04d" % (rnd.randrange(1000), rnd.randrange(100), rnd.randrange(10000))
+            elif L >= 3 and rnd.random() < 0.3:
+                v[0:2] = b"%02d" % rnd.randrange(100)
+                v[-3:] = b"%d-%d" % (rnd.randrange(10), rnd.randrange(10))
+            if L >= 14 and rnd.random() < 0.2:
+                p = rnd.randrange(L - 13)
+                v[p:p + 14] = b"%014d" % rnd.randrange(10 ** 14) if rnd.random() < 0.5 else b"cbbbbb12345678"
+            if bi % 13 == 12 and j == 0:
+                v += "é".encode()
+            b.add_record(P.Record.new_key_value(b"123-45-6789" if j % 7 == 3 else None, bytes(v)))
+        out += b.encode()
+        base += n
+    return out
+
+
+@pytest.mark.parametrize("ci", range(len(RX_FLAT_CHAINS)))
+def test_rx_flat_path(engine, ci):
+    """The flat regex path (FSG_EVAL_RX: k_rx_scan window bits + k_rx_decide
+    with the edge scans) against the oracle's Pike VM."""
+    chain = RX_FLAT_CHAINS[ci]
+    for seed in (1, 2):
+        sl = _rx_slice(seed)
+        check_batch(engine, chain, sl)
+        g = gpu_chain(engine, chain)
+        g.process_batch(sl)
+        t = g.last_timings()
+        assert t["eval_path"] == 7 and 0 < t["deferred"] < t["n_batches"], t  # FSG_EVAL_RX
+    sl = synth.make_slice(1, 3000)
+    check_batch(engine, chain, sl)
+
+
 # ---------------------------------------------------------------------------
 # string-concatenating aggregate (examples/aggregate) and array_map
 # (examples/array_map_json_array): variable-size outputs
