@@ -2012,18 +2012,28 @@ __device__ __forceinline__ FjRec fj_frame(const uint8_t* S, const FlatHdr& H, ui
 //                max_len bytes lies in the window of the chunk holding its last
 //                byte, so the bits plus the edge scans see every match.
 // ---------------------------------------------------------------------------
+// The rows sit in LDS as 32 interleaved copies (row b of copy k at u64 index
+// 32 b + k, lane l reads copy l mod 32): a 32-lane group's ds_read_b64 then
+// touches banks 2 k, 2 k + 1 whatever the bytes, no conflicts (one copy had
+// ~3.2 conflict cycles per lookup on C1 text).  64 KiB per 512-thread workgroup.
+constexpr int kRxThreads = 512;
 template <int kCtx>  // context dwords before each chunk: ceil((max_len - 1) / 4)
-__global__ __launch_bounds__(256) void k_rx_scan(EvalArgs a, uint32_t stage) {
-  __shared__ unsigned long long T[256];
+__global__ __launch_bounds__(kRxThreads) void k_rx_scan(EvalArgs a, uint32_t stage) {
+  __shared__ unsigned long long T32[256 * 32];
   const StageDesc& sd = a.chain->st[stage];
   const bool upper = sd.in_type == VT_SRC_UPPER;
-  T[threadIdx.x] = ((const unsigned long long*)(a.blob + (upper ? sd.dfa.tt_up : sd.dfa.tt)))[threadIdx.x];
+  {
+    const unsigned long long* tt = (const unsigned long long*)(a.blob + (upper ? sd.dfa.tt_up : sd.dfa.tt));
+    for (uint32_t i = threadIdx.x; i < 256 * 32; i += kRxThreads) T32[i] = tt[i >> 5];
+  }
   __syncthreads();
+  const unsigned long long* T = T32 + (threadIdx.x & 31u);  // this lane's copy: row b at T[32 b]
   const uint32_t s0 = sd.dfa.s_mid, acc1 = sd.dfa.acc1;
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   const uint64_t nrounds = a.fbm_words;
-  const uint64_t w0 = (uint64_t)blockIdx.x * 4 + wv;
-  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  constexpr uint32_t kW = kRxThreads / 64;  // waves per workgroup
+  const uint64_t w0 = (uint64_t)blockIdx.x * kW + wv;
+  const uint64_t nw = (uint64_t)gridDim.x * kW;
   ulonglong2* bm2 = (ulonglong2*)a.fbm;
   for (uint64_t r0 = w0 * kFlatRounds; r0 < nrounds; r0 += nw * kFlatRounds) {
     uint4 v[kFlatRounds], pv[kFlatRounds];
@@ -2045,7 +2055,7 @@ __global__ __launch_bounds__(256) void k_rx_scan(EvalArgs a, uint32_t stage) {
       w[kCtx + 3] = v[i].w;
       unsigned long long row[4 * (4 + kCtx)];
 #pragma unroll
-      for (int k = 0; k < 4 * (4 + kCtx); k++) row[k] = T[(w[k >> 2] >> (8 * (k & 3))) & 0xFFu];  // rows ahead of the chain
+      for (int k = 0; k < 4 * (4 + kCtx); k++) row[k] = T[32u * ((w[k >> 2] >> (8 * (k & 3))) & 0xFFu)];  // rows ahead of the chain
       uint32_t st = s0;
 #pragma unroll
       for (int k = 0; k < 4 * (4 + kCtx); k++) st = (uint32_t)(row[k] >> (4 * st)) & 15u;
@@ -2056,9 +2066,35 @@ __global__ __launch_bounds__(256) void k_rx_scan(EvalArgs a, uint32_t stage) {
     }
   }
 }
-// the DFA over bytes [p0, p1) of S from state st (the rows in T); the sticky accept, or acceptance at the end
-__device__ __forceinline__ uint32_t rx_run(const unsigned long long* T, const uint8_t* S, uint64_t p0, uint64_t p1, uint32_t st) {
-  for (uint64_t p = p0; p < p1; p++) st = (uint32_t)(T[S[p]] >> (4 * st)) & 15u;
+// the DFA over the bytes [p0, p1) of the three chunks from chunk cb (every
+// position stepped in order, inactive ones predicated off: no divergent loop)
+__device__ __noinline__ uint32_t rx_win(const unsigned long long* T, const uint8_t* S, uint64_t cb, uint64_t p0,
+                                           uint64_t p1, uint32_t st) {
+  const uint4* src = (const uint4*)(S + (cb << 4));
+  const uint4 u[3] = {src[0], src[1], src[2]};
+  const uint64_t base = cb << 4;
+  const uint32_t lo = p0 > base ? (uint32_t)(p0 - base) : 0u, hi = p1 > base ? (uint32_t)(p1 - base) : 0u;
+#pragma unroll
+  for (uint32_t k = 0; k < 48; k++) {
+    const uint32_t w = k < 16 ? u4_dw(u[0], (k >> 2) & 3u) : k < 32 ? u4_dw(u[1], (k >> 2) & 3u) : u4_dw(u[2], (k >> 2) & 3u);
+    const uint32_t nx = (uint32_t)(T[(w >> (8 * (k & 3u))) & 0xFFu] >> (4 * st)) & 15u;
+    st = k >= lo && k < hi ? nx : st;
+  }
+  return st;
+}
+// the DFA over bytes [p0, p1) of S from state st (the rows in T); the
+// sticky accept, or acceptance at the end.  The bytes arrive 64 at a time
+// (four 16-byte loads in flight together), the steps run from registers.
+__device__ __noinline__ uint32_t rx_run(const unsigned long long* T, const uint8_t* S, uint64_t p0, uint64_t p1, uint32_t st) {
+  for (uint64_t a0 = p0 & ~15ull; a0 < p1; a0 += 64) {
+    const uint4* src = (const uint4*)(S + a0);
+    const uint4 u0 = src[0], u1 = src[1], u2 = src[2], u3 = src[3];
+    const uint64_t lo = p0 > a0 ? p0 - a0 : 0, hi = p1 - a0 < 64 ? p1 - a0 : 64;
+    for (uint32_t k = (uint32_t)lo; k < (uint32_t)hi; k++) {
+      const uint32_t w = u4_dw(sel4(u0, u1, u2, u3, k >> 4), (k >> 2) & 3u);
+      st = (uint32_t)(T[(w >> (8 * (k & 3u))) & 0xFFu] >> (4 * st)) & 15u;
+    }
+  }
   return st;
 }
 __global__ __launch_bounds__(256) void k_rx_decide(EvalArgs a, uint32_t stage) {
@@ -2093,23 +2129,52 @@ __global__ __launch_bounds__(256) void k_rx_decide(EvalArgs a, uint32_t stage) {
   uint32_t nkeep = 0;
   uint64_t q = sec0 + 4;  // absolute start of record n
   FlatHdr H = flat_hdr(S, ok && count > 0 ? q : sec0);
-  for (int32_t n = 0; ok && n < count; n++) {
-    const FjRec R = fj_frame(S, H, q, sec_end, true);
+  // software pipeline: record n + 1 is framed and its loads are issued before
+  // record n is decided; record n + 2's header is in flight meanwhile
+  struct RxLoads {
+    uint32_t tw;
+    ulonglong2 bw0, bw1;
+    uint4 ea, eb;
+  };
+  auto issue = [&](const FjRec& r) {
+    RxLoads L;
+    L.tw = ld_u32_at(S + r.ve);
+    const uint64_t wb0 = (r.va >> 4) >> 6;
+    L.bw0 = *(const ulonglong2*)(a.fbm + 2 * wb0);
+    L.bw1 = *(const ulonglong2*)(a.fbm + 2 * wb0 + 2);
+    L.ea = *(const uint4*)(S + ((r.va >> 4) << 4));
+    L.eb = *(const uint4*)(S + (((r.ve ? r.ve - 1 : 0) >> 4) << 4));
+    return L;
+  };
+  FjRec R = {};
+  RxLoads LD = {};
+  if (ok && count > 0) {
+    R = fj_frame(S, H, q, sec_end, true);
     ok = R.ok;
-    if (!ok) break;
-    const uint64_t end = R.end;
-    const FlatHdr Hn = flat_hdr(S, n + 1 < count ? end : q);  // the next record's header, in flight now
-    const uint64_t va = R.va, ve = R.ve;
-    // every load of this record at once: trailer, bitmap words, edge chunks
-    const uint32_t tw = ld_u32_at(S + ve);
+    if (ok) {
+      LD = issue(R);
+      q = R.end;
+      if (count > 1) H = flat_hdr(S, q);
+    }
+  }
+  for (int32_t n = 0; ok && n < count; n++) {
+    const FjRec cur = R;
+    const RxLoads CL = LD;
+    if (n + 1 < count) {
+      R = fj_frame(S, H, q, sec_end, true);
+      ok = R.ok;
+      if (!ok) break;
+      LD = issue(R);
+      q = R.end;
+      if (n + 2 < count) H = flat_hdr(S, q);
+    }
+    const uint64_t va = cur.va, ve = cur.ve, end = cur.end;
     const uint64_t c0 = va >> 4, c1 = (ve + 15) >> 4, i0 = (va + 15) >> 4, i1 = ve >> 4;
     const uint64_t wb = c0 >> 6;  // first bitmap word touching the value
-    const ulonglong2 bw0 = *(const ulonglong2*)(a.fbm + 2 * wb), bw1 = *(const ulonglong2*)(a.fbm + 2 * wb + 2);
-    const unsigned long long mb0 = bw0.x, hb0 = bw0.y, mb1 = bw1.x, hb1 = bw1.y;
-    const uint4 ea = *(const uint4*)(S + (c0 << 4));
-    const uint4 eb = *(const uint4*)(S + (((ve ? ve - 1 : 0) >> 4) << 4));
+    const unsigned long long mb0 = CL.bw0.x, hb0 = CL.bw0.y, mb1 = CL.bw1.x, hb1 = CL.bw1.y;
+    const uint4 ea = CL.ea, eb = CL.eb;
     int64_t hdr;
-    uint32_t nb = var4(tw, hdr);
+    uint32_t nb = var4(CL.tw, hdr);
     ok = nb != 0 && ve + nb == end;
     if (!ok) break;
     auto bits_any = [&](const unsigned long long* bm, unsigned long long w0v, unsigned long long w1v, uint64_t x0,
@@ -2157,39 +2222,39 @@ __global__ __launch_bounds__(256) void k_rx_decide(EvalArgs a, uint32_t stage) {
         uint64_t he = (h1 << 4) < ve ? (h1 << 4) : ve;  // the head scan's end
         if (!free_ && he < va + ml) he = va + ml < ve ? va + ml : ve;
         if (head) {  // from the value start
-          const uint32_t st = rx_run(T, S, va, he, s_bot);
+          const uint32_t st = he - (c0 << 4) <= 48 ? rx_win(T, S, c0, va, he, s_bot) : rx_run(T, S, va, he, s_bot);
           match = ((acc1 >> st) & 1u) || (he == ve && ((acc2 >> st) & 1u));
         }
         if (!match && tail && !(head && he == ve)) {
           const uint64_t e = t0 <= l1 ? (t0 << 4) : ve - 1;  // the earliest end of a match left to see
           const uint64_t back = ml ? ml - 1 : 0;
           const uint64_t st0 = e > va + back ? e - back : va;
-          const uint32_t st = rx_run(T, S, st0, ve, st0 == va ? s_bot : s_mid);
+          const uint64_t cs = st0 >> 4;
+          const uint32_t s1 = st0 == va ? s_bot : s_mid;
+          const uint32_t st = ve - (cs << 4) <= 48 ? rx_win(T, S, cs, st0, ve, s1) : rx_run(T, S, st0, ve, s1);
           match = ((acc1 >> st) & 1u) || ((acc2 >> st) & 1u);
         }
       }
     }
     if (match == keep_match) {
       KeptRec d;
-      d.src = q;
+      d.src = cur.q;
       d.vpos = va;
-      d.kpos = R.tag ? R.kpos : 0;
-      d.od = R.od;
-      d.ts = R.ts;
+      d.kpos = cur.tag ? cur.kpos : 0;
+      d.od = cur.od;
+      d.ts = cur.ts;
       d.hdr = hdr;
       d.vlen = (uint32_t)(ve - va);
-      d.klen = R.klen;
+      d.klen = cur.klen;
       d.ival = 0;
       d.mode = out_upper ? KM_UPPER : KM_COPY;
-      d.has_key = R.tag;
-      d.attr = R.attr;
+      d.has_key = cur.tag;
+      d.attr = cur.attr;
       d.pad = 0;
       a.desc[rb + nkeep++] = d;
     }
-    q = end;
-    H = Hn;
   }
-  ok = ok && q == sec_end;
+  ok = ok && q == sec_end;  // (q: the end of the last record framed)
   if (!ok) {  // the exact kernel frames and evaluates this batch
     a.rend[b] = 0xFFFFu;
     const uint32_t i = atomicAdd(&a.list[0], 1u);
@@ -2743,14 +2808,15 @@ void launch_eval_rx(const EvalArgs& a, uint32_t stage, hipStream_t s) {
   if (!a.nbatches) return;
   const uint32_t ml = (uint32_t)a.chain_host_max_len;
   const uint64_t waves = (a.fbm_words + kFlatRounds - 1) / kFlatRounds;
-  const uint32_t g1 = (uint32_t)std::max<uint64_t>(std::min<uint64_t>((waves + 3) / 4, 4096), 1);
+  constexpr uint32_t kW = kRxThreads / 64;
+  const uint32_t g1 = (uint32_t)std::max<uint64_t>(std::min<uint64_t>((waves + kW - 1) / kW, 2048), 1);
   const uint32_t g2 = (a.nbatches + 255) / 256;
   switch ((ml + 2) / 4) {  // context dwords of a chunk's window
-    case 0: hipLaunchKernelGGL(k_rx_scan<0>, dim3(g1), dim3(256), 0, s, a, stage); break;
-    case 1: hipLaunchKernelGGL(k_rx_scan<1>, dim3(g1), dim3(256), 0, s, a, stage); break;
-    case 2: hipLaunchKernelGGL(k_rx_scan<2>, dim3(g1), dim3(256), 0, s, a, stage); break;
-    case 3: hipLaunchKernelGGL(k_rx_scan<3>, dim3(g1), dim3(256), 0, s, a, stage); break;
-    default: hipLaunchKernelGGL(k_rx_scan<4>, dim3(g1), dim3(256), 0, s, a, stage); break;
+    case 0: hipLaunchKernelGGL(k_rx_scan<0>, dim3(g1), dim3(kRxThreads), 0, s, a, stage); break;
+    case 1: hipLaunchKernelGGL(k_rx_scan<1>, dim3(g1), dim3(kRxThreads), 0, s, a, stage); break;
+    case 2: hipLaunchKernelGGL(k_rx_scan<2>, dim3(g1), dim3(kRxThreads), 0, s, a, stage); break;
+    case 3: hipLaunchKernelGGL(k_rx_scan<3>, dim3(g1), dim3(kRxThreads), 0, s, a, stage); break;
+    default: hipLaunchKernelGGL(k_rx_scan<4>, dim3(g1), dim3(kRxThreads), 0, s, a, stage); break;
   }
   hipLaunchKernelGGL(k_rx_decide, dim3(g2), dim3(256), 0, s, a, stage);
 }

@@ -552,6 +552,12 @@ struct fsg_chain {
   bool no_flat = getenv("FSG_NO_FLAT") != nullptr;  // A/B: the flat path off (k_eval_lean instead)
   bool no_fjson = getenv("FSG_NO_FJSON") != nullptr;  // A/B: the flat JSON path off (k_eval_lean instead)
   bool no_frx = getenv("FSG_NO_FRX") != nullptr;      // A/B: the flat regex path off (k_eval_lean instead)
+  // the flat regex path for slices of records averaging at least this many
+  // bytes: its per-record framing walk re-reads a line per record, which for
+  // short records costs more than k_eval_lean's batch windows (C1, 256-B
+  // records: k_rx_scan 0.56 + k_rx_decide 0.82 ms against k_chase +
+  // k_eval_lean's 1.33 ms on MI355X)
+  uint64_t frx_min_rec = getenv("FSG_FRX_MIN_REC") ? strtoull(getenv("FSG_FRX_MIN_REC"), nullptr, 10) : 512;
   bool no_int = getenv("FSG_NO_INT") != nullptr;    // A/B: integer chains through k_eval alone
   // the one-batch process() path (k_one): zeros for bpos / rbase, the device
   // block Plan | BatchStat | Mins | output batch, and coherent pinned memory
@@ -2130,7 +2136,8 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   // filter_json / projection (with at most one substring stage): the flat JSON path
   const int fjf = lean && fst < 0 && !c->no_fjson ? fjson_flags(c->hdesc, ops) : -1;
   // one bounded regex stage: the flat regex path
-  const int rxs = lean && fst < 0 && fjf < 0 && !c->no_frx ? rx_flat_stage(c->hdesc, ops) : -1;
+  const int rxs = lean && fst < 0 && fjf < 0 && !c->no_frx && s->len >= c->frx_min_rec * std::max<uint64_t>(s->nrec, 1)
+                      ? rx_flat_stage(c->hdesc, ops) : -1;
   bool flat = false, fjson = false, frx = false;
   if ((fst >= 0 || fjf >= 0 || rxs >= 0) && !c->no_flat) {
     ea.fbm_words = (s->len + 1023) / 1024;

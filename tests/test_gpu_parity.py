@@ -982,9 +982,12 @@ def _rx_slice(seed):
 
 
 @pytest.mark.parametrize("ci", range(len(RX_FLAT_CHAINS)))
-def test_rx_flat_path(engine, ci):
+def test_rx_flat_path(engine, ci, monkeypatch):
     """The flat regex path (FSG_EVAL_RX: k_rx_scan window bits + k_rx_decide
-    with the edge scans) against the oracle's Pike VM."""
+    with the edge scans) against the oracle's Pike VM, taken whatever the
+    record sizes (FSG_FRX_MIN_REC=0: by default only slices of records
+    averaging >= 512 bytes take it)."""
+    monkeypatch.setenv("FSG_FRX_MIN_REC", "0")
     chain = RX_FLAT_CHAINS[ci]
     for seed in (1, 2):
         sl = _rx_slice(seed)
