@@ -1369,10 +1369,10 @@ __global__ __launch_bounds__(kEvalThreads, (kOps == kOpsContains) ? 4 : 2) void 
 // ---------------------------------------------------------------------------
 // k_mins: first surviving / erroring / undecodable / unsupported batch
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_mins(const BatchStat* bstat, uint32_t n, Mins* mins) {
+__device__ __forceinline__ void mins_body(const BatchStat* bstat, uint32_t n, Mins* mins, uint32_t bid, uint32_t gdim) {
   __shared__ uint32_t sh[4][4];
   uint32_t fk = 0xFFFFFFFFu, fe = 0xFFFFFFFFu, fd = 0xFFFFFFFFu, fu = 0xFFFFFFFFu;
-  for (uint32_t b = blockIdx.x * 256 + threadIdx.x; b < n; b += gridDim.x * 256) {
+  for (uint32_t b = bid * 256 + threadIdx.x; b < n; b += gdim * 256) {
     const uint32_t f = bstat[b].flags;
     const uint32_t nk = bstat[b].nout;  // batches whose stage output is non-empty
     if (f & BF_DECODE) fd = fd < b ? fd : b;
@@ -1399,6 +1399,9 @@ __global__ __launch_bounds__(256) void k_mins(const BatchStat* bstat, uint32_t n
     for (int k = 1; k < 4; k++) m = sh[k][threadIdx.x] < m ? sh[k][threadIdx.x] : m;
     if (m != 0xFFFFFFFFu) atomicMin(&((uint32_t*)mins)[threadIdx.x], m);  // first_keep, first_err, first_dec, first_unsup
   }
+}
+__global__ __launch_bounds__(256) void k_mins(const BatchStat* bstat, uint32_t n, Mins* mins) {
+  mins_body(bstat, n, mins, blockIdx.x, gridDim.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -1560,9 +1563,9 @@ struct ScanDownArgs {
   const BatchStat* bstat;
 };
 
-__global__ __launch_bounds__(256) void k_scan_down(ScanDownArgs a) {
+__device__ __forceinline__ void scan_down_body(const ScanDownArgs& a, uint32_t bid) {
   __shared__ ScanRow sh[kScanBlock];
-  const uint32_t base = blockIdx.x * kScanTile;
+  const uint32_t base = bid * kScanTile;
   ScanRow acc = {};
   for (int k = 0; k < kScanPer; k++) {
     uint32_t i = base + threadIdx.x * kScanPer + k;
@@ -1570,7 +1573,7 @@ __global__ __launch_bounds__(256) void k_scan_down(ScanDownArgs a) {
   }
   ScanRow total;
   block_excl_scan(acc, sh, total);
-  ScanRow run = a.tile_sums ? a.tile_sums[blockIdx.x] : ScanRow{};  // null: the slice is one tile
+  ScanRow run = a.tile_sums ? a.tile_sums[bid] : ScanRow{};  // null: the slice is one tile
   row_add(run, acc);
   const uint32_t f = a.mins->first_keep;
   for (int k = 0; k < kScanPer; k++) {
@@ -1586,6 +1589,7 @@ __global__ __launch_bounds__(256) void k_scan_down(ScanDownArgs a) {
     }
   }
 }
+__global__ __launch_bounds__(256) void k_scan_down(ScanDownArgs a) { scan_down_body(a, blockIdx.x); }
 
 // ---------------------------------------------------------------------------
 // k_plan: the process_batch stop rules (batch.rs:41-142), one thread
@@ -2092,9 +2096,9 @@ struct __attribute__((aligned(16))) WgLds {
   uint8_t ob[kWgObuf + 16];
   uint32_t wt[4];
 };
-__global__ __launch_bounds__(256) void k_write_gen(WriteArgs a) {
+__device__ __forceinline__ void write_gen_body(const WriteArgs& a, uint32_t bid) {
   __shared__ WgLds L;
-  const int32_t b = a.first + (int32_t)blockIdx.x;
+  const int32_t b = a.first + (int32_t)bid;
   if (a.first < 0 || b > a.last) return;
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   const BatchStat st = a.bstat[b];
@@ -2174,6 +2178,7 @@ __global__ __launch_bounds__(256) void k_write_gen(WriteArgs a) {
     }
   }
 }
+__global__ __launch_bounds__(256) void k_write_gen(WriteArgs a) { write_gen_body(a, blockIdx.x); }
 void launch_write_gen(const WriteArgs& a, uint32_t nblocks, hipStream_t s) {
   if (nblocks) hipLaunchKernelGGL(k_write_gen, dim3(nblocks), dim3(256), 0, s, a);
 }
@@ -2829,15 +2834,15 @@ __device__ __forceinline__ uint32_t crc_shift_bytes(uint32_t c, uint64_t n) {
 // One 64 KiB chunk per workgroup iteration; the next chunk's blocks are loaded
 // (into registers) while this one is folded, and the barriers wait for LDS
 // only, so the loads stay in flight.
-__global__ __launch_bounds__(kCrcThreads) void k_crc16(const uint8_t* __restrict__ out, uint64_t skip,
-                                                        uint64_t nblocks, uint32_t* acc) {
+__device__ __forceinline__ void crc16_body(const uint8_t* __restrict__ out, uint64_t skip, uint64_t nblocks,
+                                           uint32_t* acc, uint32_t bid, uint32_t gdim) {
   __shared__ uint32_t z[16][256];
   __shared__ uint32_t sh[9][4][256];  // shifts by 16 B .. 4 KiB (2^4 .. 2^12 bytes)
   __shared__ uint32_t red[2][kCrcThreads / 64];
   const uint32_t t = threadIdx.x;
   const uint4* base = (const uint4*)(out + 16);
   const uint64_t nchunks = (nblocks + kCrcChunkBlocks - 1) / kCrcChunkBlocks;
-  uint64_t ch = blockIdx.x;
+  uint64_t ch = bid;
   if (ch >= nchunks) return;
   // blocks of chunk c: unconditional loads, clamped to the last block (a
   // conditional load would be waited for at once)
@@ -2856,7 +2861,7 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc16(const uint8_t* __restrict
   __syncthreads();
   uint32_t par = 0;
   for (;;) {
-    const uint64_t chn = ch + gridDim.x;
+    const uint64_t chn = ch + gdim;
     fetch(chn < nchunks ? chn : ch, nv);  // the last iteration re-reads its own chunk
     const uint64_t b0 = ch * kCrcChunkBlocks;
     const uint32_t nb = (uint32_t)(nblocks - b0 < kCrcChunkBlocks ? nblocks - b0 : kCrcChunkBlocks);
@@ -2907,6 +2912,10 @@ __global__ __launch_bounds__(kCrcThreads) void k_crc16(const uint8_t* __restrict
 #pragma unroll
     for (int i = 0; i < kCrcIters; i++) v[i] = nv[i];
   }
+}
+__global__ __launch_bounds__(kCrcThreads) void k_crc16(const uint8_t* __restrict__ out, uint64_t skip,
+                                                        uint64_t nblocks, uint32_t* acc) {
+  crc16_body(out, skip, nblocks, acc, blockIdx.x, gridDim.x);
 }
 
 // tail bytes [tail0, end) bytewise, init/xorout, big-endian CRC at out[17..21)
@@ -3743,6 +3752,120 @@ void launch_eval(const EvalArgs& a, uint32_t ops, int mode, hipStream_t s) {
   else
     hipLaunchKernelGGL(k_eval<kOpsAll>, dim3(grid), dim3(kEvalThreads), dyn, s, e);
 }
+// ---------------------------------------------------------------------------
+// the aggregate-sum group path (fsg_launch.h GaJob): one launch per phase
+// over every chain of a group call; the per-batch phases find their job by
+// a binary search of the grid offsets, the per-chain ones take a block each
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t ga_job(const uint32_t* off, uint32_t n, uint32_t bid) {
+  uint32_t lo = 0, hi = n - 1;  // the last job with off[j] <= bid
+  while (lo < hi) {
+    const uint32_t m = (lo + hi + 1) >> 1;
+    if (off[m] <= bid) lo = m; else hi = m - 1;
+  }
+  return lo;
+}
+__global__ void k_ga_init(const GaJob* J, uint32_t n) {  // mins = none, no deferred batch, CRC partials 0
+  const uint32_t j = blockIdx.x * 64 + threadIdx.x;
+  if (j >= n) return;
+  uint32_t* m = (uint32_t*)J[j].ea.mins;
+  for (int k = 0; k < (int)(sizeof(Mins) / 4); k++) m[k] = 0xFFFFFFFFu;
+  J[j].ea.list[0] = 0;
+  *J[j].crc_acc = 0;
+}
+// deferred batches are not evaluated on this path: an unsupported stand-in
+// keeps the later phases inside the batch's bounds; the host re-runs the chain
+__global__ void k_ga_defer_mark(const GaJob* J, uint32_t n) {
+  const GaJob& g = J[blockIdx.x];
+  const uint32_t nd = g.ea.list[0];
+  for (uint32_t i = threadIdx.x; i < nd; i += 64) {
+    BatchStat st = {};
+    st.flags = BF_UNSUPPORTED;
+    st.err_stage = 0xFFFFFFFFu;
+    g.ea.bstat[g.ea.list[1 + i]] = st;
+  }
+}
+__global__ __launch_bounds__(256) void k_ga_mins(const GaJob* J, const uint32_t* off, uint32_t n) {
+  const uint32_t j = ga_job(off, n, blockIdx.x);
+  mins_body(J[j].ea.bstat, J[j].ea.nbatches, J[j].ea.mins, blockIdx.x - off[j], off[j + 1] - off[j]);
+}
+__global__ __launch_bounds__(256) void k_ga_size(const GaJob* J, const uint32_t* off, uint32_t n, uint32_t agg_only) {
+  const uint32_t j = ga_job(off, n, blockIdx.x);
+  SizeArgs a = J[j].sa;
+  a.agg_only = agg_only;
+  a.agg_pre = agg_only ? nullptr : J[j].aggpre;
+  const uint32_t b = (blockIdx.x - off[j]) * 4 + (threadIdx.x >> 6);
+  if (b < a.nbatches) size_batch(a, b);
+}
+__global__ __launch_bounds__(256) void k_ga_scan(const GaJob* J, uint32_t cut) {  // one tile per chain
+  const GaJob& g = J[blockIdx.x];
+  ScanDownArgs d{g.sa.rows, cut ? g.pre : g.aggpre, nullptr, g.sa.nbatches, cut, cut ? g.max_bytes : 0,
+                 g.ea.mins, g.ea.bstat};
+  scan_down_body(d, 0);
+}
+__global__ void k_ga_plan(const GaJob* J, GaResult* res) {  // the plan, the accumulator, the read-back row
+  if (threadIdx.x != 0) return;
+  const GaJob& g = J[blockIdx.x];
+  plan_run(g.pa);
+  const Plan p = *g.pa.plan;
+  const uint32_t nd = g.ea.list[0];
+  if (!nd && p.acc_touched) *g.state = (int32_t)p.acc_final;  // (k_state; a re-run chain commits there)
+  res[blockIdx.x].plan = p;
+  res[blockIdx.x].deferred = nd;
+}
+__global__ void k_ga_header(const GaJob* J) {
+  if (threadIdx.x == 0 && J[blockIdx.x].out_len) header_run(J[blockIdx.x].wa.plan, J[blockIdx.x].wa.out);
+}
+__global__ __launch_bounds__(256) void k_ga_write(const GaJob* J, const uint32_t* off, uint32_t n) {
+  const uint32_t j = ga_job(off, n, blockIdx.x);
+  write_gen_body(J[j].wa, blockIdx.x - off[j]);
+}
+__global__ __launch_bounds__(kCrcThreads) void k_ga_crc(const GaJob* J, const uint32_t* off, uint32_t n) {
+  const uint32_t j = ga_job(off, n, blockIdx.x);
+  const uint64_t end = J[j].out_len, zend = end & ~15ull, nblocks = zend > 16 ? (zend - 16) / 16 : 0;
+  crc16_body(J[j].wa.out, 21 - 16, nblocks, J[j].crc_acc, blockIdx.x - off[j], off[j + 1] - off[j]);
+}
+__global__ void k_ga_crc_final(const GaJob* J) {
+  const GaJob& g = J[blockIdx.x];
+  if (threadIdx.x != 0 || !g.out_len) return;
+  const uint64_t end = g.out_len, zend = end & ~15ull, nblocks = zend > 16 ? (zend - 16) / 16 : 0;
+  // (k_crc_final's body: tail bytes, init / xorout, the big-endian CRC at out[17..21))
+  uint8_t* out = g.wa.out;
+  const uint64_t n = end - 21;
+  uint32_t c = *g.crc_acc;
+  for (uint64_t i = nblocks ? zend : 21; i < end; i++) c = g_crc_z16[0][(c ^ out[i]) & 0xff] ^ (c >> 8);
+  const uint32_t crc = c ^ crc_shift_bytes(0xFFFFFFFFu, n) ^ 0xFFFFFFFFu;
+  out[17] = (uint8_t)(crc >> 24);
+  out[18] = (uint8_t)(crc >> 16);
+  out[19] = (uint8_t)(crc >> 8);
+  out[20] = (uint8_t)crc;
+}
+uint32_t ga_mins_blocks(uint32_t nb) { return std::min<uint32_t>((nb + 255) / 256, 1024u); }
+uint32_t ga_crc_blocks(uint64_t out_len) {
+  const uint64_t zend = out_len & ~15ull, nblocks = zend > 16 ? (zend - 16) / 16 : 0;
+  const uint64_t nchunks = (nblocks + kCrcChunkBlocks - 1) / kCrcChunkBlocks;
+  return (uint32_t)std::min<uint64_t>(nchunks, 768);
+}
+void launch_ga_phase1(const GaJob* J, uint32_t n, const GaOffsets& o, GaResult* res, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_ga_init, dim3((n + 63) / 64), dim3(64), 0, s, J, n);
+  launch_ga_eval_int(J, n, o.eval, o.t_eval, s);
+  hipLaunchKernelGGL(k_ga_defer_mark, dim3(n), dim3(64), 0, s, J, n);
+  if (o.t_mins) hipLaunchKernelGGL(k_ga_mins, dim3(o.t_mins), dim3(256), 0, s, J, o.mins, n);
+  if (o.t_size) hipLaunchKernelGGL(k_ga_size, dim3(o.t_size), dim3(256), 0, s, J, o.size, n, 1u);
+  hipLaunchKernelGGL(k_ga_scan, dim3(n), dim3(kScanBlock), 0, s, J, 0u);
+  if (o.t_size) hipLaunchKernelGGL(k_ga_size, dim3(o.t_size), dim3(256), 0, s, J, o.size, n, 0u);
+  hipLaunchKernelGGL(k_ga_scan, dim3(n), dim3(kScanBlock), 0, s, J, 1u);
+  hipLaunchKernelGGL(k_ga_plan, dim3(n), dim3(64), 0, s, J, res);
+}
+void launch_ga_phase2(const GaJob* J, uint32_t n, const GaOffsets& o, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_ga_header, dim3(n), dim3(64), 0, s, J);
+  if (o.t_write) hipLaunchKernelGGL(k_ga_write, dim3(o.t_write), dim3(256), 0, s, J, o.write, n);
+  if (o.t_crc) hipLaunchKernelGGL(k_ga_crc, dim3(o.t_crc), dim3(kCrcThreads), 0, s, J, o.crc, n);
+  hipLaunchKernelGGL(k_ga_crc_final, dim3(n), dim3(64), 0, s, J);
+}
+
 void launch_mins(const BatchStat* bstat, uint32_t n, Mins* mins, hipStream_t s) {
   if (!n) return;
   uint32_t g = (n + 255) / 256;

@@ -41,6 +41,38 @@ void launch_array_write(const ArrWriteArgs& a, uint32_t nblk, hipStream_t s);
 // record starts / ends of every batch (k_chase_w)
 void launch_chase_w(const EvalArgs& a, hipStream_t s);
 void launch_mins(const BatchStat* bstat, uint32_t n, Mins* mins, hipStream_t s);
+// ---------------------------------------------------------------------------
+// The aggregate-sum group path (fsg_chain_group_process_slices): one launch
+// per phase over every chain of the group instead of ~13 launches and two
+// host waits per chain.  GaJob = one chain's arguments; the grid offsets of
+// the per-batch phases (job j owns the virtual blocks [off[j], off[j + 1]))
+// live beside the jobs in device memory.
+struct GaJob {
+  EvalArgs ea;        // k_eval_int<1> over the batches (record starts kept with the slice)
+  SizeArgs sa;        // k_size, agg_only set by the phase
+  ScanRow* aggpre;    // exclusive aggregate prefix (first scan)
+  ScanRow* pre;       // exclusive output prefix + max_bytes cut (second scan)
+  uint64_t max_bytes;
+  PlanArgs pa;
+  int32_t* state;     // the accumulator in HBM (k_state)
+  uint32_t* crc_acc;
+  WriteArgs wa;       // phase 2: k_header, k_write_gen over [wa.first, wa.last]
+  uint64_t out_len;
+};
+struct GaResult {     // per job, read back after phase 1
+  Plan plan;
+  uint32_t deferred;  // batches k_eval_int left to the exact kernel (the chain is re-run on the general path)
+  uint32_t pad[3];
+};
+struct GaOffsets {    // device pointers to the n + 1 grid offsets per phase, and the totals
+  const uint32_t *eval, *mins, *size, *write, *crc;
+  uint32_t t_eval, t_mins, t_size, t_write, t_crc;
+};
+uint32_t ga_mins_blocks(uint32_t nb);
+uint32_t ga_crc_blocks(uint64_t out_len);
+void launch_ga_phase1(const GaJob* jobs, uint32_t n, const GaOffsets& o, GaResult* res, hipStream_t s);
+void launch_ga_phase2(const GaJob* jobs, uint32_t n, const GaOffsets& o, hipStream_t s);
+void launch_ga_eval_int(const GaJob* jobs, uint32_t n, const uint32_t* off, uint32_t total, hipStream_t s);
 void launch_size(const SizeArgs& a, hipStream_t s);
 uint32_t scan_tiles(uint32_t n);
 void launch_scan(const ScanRow* rows, ScanRow* pre, ScanRow* tile_sums, ScanRow* grand, uint32_t n, bool cut,

@@ -2565,9 +2565,9 @@ __device__ __forceinline__ bool int_rec(const uint8_t* w, uint32_t s, uint32_t e
 }
 __device__ __forceinline__ bool int_ws(uint32_t c) { return c == 0x20 || (c >= 0x09 && c <= 0x0D); }
 template <int kAgg>  // kAgg: the chain ends in aggregate-sum
-__global__ __launch_bounds__(256) void k_eval_int(EvalArgs a) {
+__device__ __forceinline__ void eval_int_body(const EvalArgs& a, uint32_t bid) {
   __shared__ IntLds L;
-  const uint32_t b = blockIdx.x;
+  const uint32_t b = bid;
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   const ChainDesc& ch = *a.chain;
   const uint8_t* S = a.slice;
@@ -2699,6 +2699,24 @@ __global__ __launch_bounds__(256) void k_eval_int(EvalArgs a) {
     st.agg_sum = kAgg ? (int64_t)(int32_t)(L.wa[0] + L.wa[1] + L.wa[2] + L.wa[3]) : 0;
     a.bstat[b] = st;
   }
+}
+template <int kAgg>
+__global__ __launch_bounds__(256) void k_eval_int(EvalArgs a) { eval_int_body<kAgg>(a, blockIdx.x); }
+// the aggregate-sum group path: every chain's batches in one grid (fsg_launch.h GaJob)
+__device__ __forceinline__ uint32_t ga_find(const uint32_t* off, uint32_t n, uint32_t bid) {
+  uint32_t lo = 0, hi = n - 1;  // the last job with off[j] <= bid
+  while (lo < hi) {
+    const uint32_t m = (lo + hi + 1) >> 1;
+    if (off[m] <= bid) lo = m; else hi = m - 1;
+  }
+  return lo;
+}
+__global__ __launch_bounds__(256) void k_ga_eval_int(const GaJob* J, const uint32_t* off, uint32_t n) {
+  const uint32_t j = ga_find(off, n, blockIdx.x);
+  eval_int_body<1>(J[j].ea, blockIdx.x - off[j]);
+}
+void launch_ga_eval_int(const GaJob* jobs, uint32_t n, const uint32_t* off, uint32_t total, hipStream_t s) {
+  if (total) hipLaunchKernelGGL(k_ga_eval_int, dim3(total), dim3(256), 0, s, jobs, off, n);
 }
 
 bool int_lean_eligible(const ChainDesc& ch, uint32_t ops) {

@@ -443,6 +443,11 @@ struct fsg_engine {
   hipEvent_t gdone = nullptr, gt0 = nullptr, gt1 = nullptr;
   void* gdlist = nullptr;
   size_t gdcap = 0;
+  // the aggregate-sum group path (group_agg_fast): jobs + offsets in HBM and
+  // their pinned host image, the read-back rows, phase events
+  DevBuf ga_dev;
+  PinBuf ga_pin;
+  hipEvent_t ga_ev[5] = {};
 };
 
 struct fsg_chain_builder {
@@ -2632,11 +2637,11 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   c->last.text_ms = t[2];
   c->last.total_ms = t[0] + t[1] + t[2] + t[3] + t[4];
   c->last.order_ms = 0;
-  if (c->timed && has_aggj && aj.n_rec) {  // the order walk alone (the group's launch for a group call)
+  if (has_aggj && aj.n_rec) {  // the order walk alone (the group's launch for a group call: timed when its first chain is)
     AjGroup* g = c->group;
-    if (g && g->t0 && g->t1)
+    if (g && g->timed && g->t0 && g->t1)
       HIPCHK(hipEventElapsedTime(&c->last.order_ms, g->t0, g->t1));
-    else if (!g)
+    else if (!g && c->timed)
       HIPCHK(hipEventElapsedTime(&c->last.order_ms, c->ev_order[0], c->ev_order[1]));
   }
   c->last.in_bytes = s->header_bytes;
@@ -2940,6 +2945,235 @@ extern "C" int fsg_chain_process_slice(fsg_chain* c, const fsg_slice* s, uint64_
   return FSG_OK;
 }
 
+// The aggregate-sum group path: chains that are one aggregate-sum stage over
+// a resident slice of decimal records (k_eval_int's chains, C5) run as ONE
+// launch per phase over the whole group (fsg_launch.h GaJob): jobs uploaded
+// once, phase 1 (eval, minima, sizes, scans, plan, accumulator) and its
+// read-back with one wait, the host sizes the outputs, phase 2 (header,
+// records, CRC32C) with one wait.  A chain whose batches the integer kernel
+// defers, or whose call ends in an error, is re-run on the general path (its
+// accumulator depends only on the host accumulator and its input, so the
+// re-run commits the same state).  Returns the indices left to the general path.
+int group_agg_fast(fsg_chain* const* chains, const fsg_slice* const* slices, size_t n, uint64_t max_bytes,
+                   fsg_metrics* metrics, fsg_batch_output** outs, int* rcs, std::vector<size_t>& rest) {
+  std::vector<size_t> fast;
+  rest.clear();
+  static const bool disabled = getenv("FSG_NO_GROUP_FAST") != nullptr;
+  for (size_t i = 0; i < n; i++) {
+    fsg_chain* c = chains[i];
+    const fsg_slice* s = slices[i];
+    const ChainDesc& h = c->hdesc;
+    const bool ok = !disabled && c->segs.empty() && h.nstages == 1 && h.st[0].op == OP_AGG_SUM && (h.flags & CF_AGG_SUM) &&
+                    !h.st[0].acc_bad && h.st[0].in_type == VT_SRC && !c->no_int && s->nb > 1 &&
+                    scan_tiles(s->nb) == 1 && !s->has_pass && s->rs_ok && c->dstate.p &&
+                    (size_t)s->nb * (sizeof(BatchStat) + 3 * sizeof(ScanRow)) + (size_t)s->nrec * sizeof(KeptRec) <=
+                        c->limit;
+    (ok ? fast : rest).push_back(i);
+  }
+  if (fast.size() < 2) {  // one chain: the general path
+    if (!fast.empty()) rest.insert(rest.begin(), fast[0]);
+    return FSG_OK;
+  }
+  auto bail = [&](const char*) {  // an allocation failed: every chain takes the general path
+    rest.resize(n);
+    for (size_t i = 0; i < n; i++) rest[i] = i;
+    (void)hipGetLastError();
+    return FSG_OK;
+  };
+  fsg_engine* e = chains[0]->eng;
+  if (!e->gst && hipStreamCreateWithFlags(&e->gst, hipStreamNonBlocking) != hipSuccess) return bail("stream");
+  for (auto& ev : e->ga_ev)
+    if (!ev && hipEventCreate(&ev) != hipSuccess) return bail("event");
+  hipStream_t gs = e->gst;
+  const uint32_t m = (uint32_t)fast.size();
+  // buffers of each chain (grow-only; after the first call nothing is allocated)
+  for (size_t i : fast) {
+    fsg_chain* c = chains[i];
+    const fsg_slice* s = slices[i];
+    const uint32_t nb = s->nb;
+    if (c->bstat.ensure(nb * sizeof(BatchStat)) || c->kept.ensure(std::max<uint64_t>(s->nrec, 1) * sizeof(KeptRec)) ||
+        c->rows.ensure(nb * sizeof(ScanRow)) || c->pre.ensure(nb * sizeof(ScanRow)) ||
+        c->aggpre.ensure(nb * sizeof(ScanRow)) || c->defer.ensure(((size_t)nb + 1) * sizeof(uint32_t)) ||
+        c->mins.ensure(sizeof(Mins)) || c->plan.ensure(sizeof(Plan)) || c->crcparts.ensure(sizeof(uint32_t)))
+      return bail("buffers");
+  }
+  // jobs | 5 offset tables | read-back rows
+  const size_t jb = (size_t)m * sizeof(GaJob), ob = (size_t)5 * (m + 1) * sizeof(uint32_t);
+  const size_t rb_off = (jb + ob + 255) & ~(size_t)255, total = rb_off + (size_t)m * sizeof(GaResult);
+  if (e->ga_dev.ensure(total) || e->ga_pin.ensure(total)) return bail("job buffers");
+  uint8_t* hp = (uint8_t*)e->ga_pin.p;
+  GaJob* J = (GaJob*)hp;
+  uint32_t* off = (uint32_t*)(hp + jb);
+  uint32_t* oe = off, *om = off + (m + 1), *os = off + 2 * (m + 1), *ow = off + 3 * (m + 1), *oc = off + 4 * (m + 1);
+  oe[0] = om[0] = os[0] = ow[0] = oc[0] = 0;
+  // the chains' earlier work (a collect, the record starts) before the group stream reads their buffers
+  for (size_t i : fast) {
+    fsg_chain* c = chains[i];
+    if (hipStreamQuery(c->stream) == hipErrorNotReady) (void)hipStreamSynchronize(c->stream);
+    if (slices[i]->rs_ev) (void)hipEventSynchronize(slices[i]->rs_ev);
+  }
+  (void)hipGetLastError();
+  for (uint32_t k = 0; k < m; k++) {
+    fsg_chain* c = chains[fast[k]];
+    const fsg_slice* s = slices[fast[k]];
+    const uint32_t nb = s->nb;
+    GaJob g{};
+    EvalArgs& ea = g.ea;
+    ea.slice = (const uint8_t*)s->data.p;
+    ea.slice_len = s->len;
+    ea.bpos = s->bpos.as<uint64_t>();
+    ea.rbase = s->rbase.as<uint64_t>();
+    ea.nbatches = nb;
+    ea.chain = c->d_desc.as<ChainDesc>();
+    ea.blob = c->d_blob.as<uint8_t>();
+    ea.bstat = c->bstat.as<BatchStat>();
+    ea.desc = c->kept.as<KeptRec>();
+    ea.mins = c->mins.as<Mins>();
+    ea.list = c->defer.as<uint32_t>();
+    ea.nrec = s->nrec;
+    ea.rstart = s->rs_start.as<uint16_t>();
+    ea.rend = s->rs_end.as<uint16_t>();
+    const int64_t acc0 = acc_value(c->acc);
+    SizeArgs& sa = g.sa;
+    sa.bstat = ea.bstat;
+    sa.desc = ea.desc;
+    sa.rbase = ea.rbase;
+    sa.mins = ea.mins;
+    sa.rows = c->rows.as<ScanRow>();
+    sa.nbatches = nb;
+    sa.acc0 = acc0;
+    g.aggpre = c->aggpre.as<ScanRow>();
+    g.pre = c->pre.as<ScanRow>();
+    g.max_bytes = max_bytes;
+    PlanArgs& pa = g.pa;
+    pa.bstat = ea.bstat;
+    pa.rows = sa.rows;
+    pa.pre = g.pre;
+    pa.mins = ea.mins;
+    pa.plan = c->plan.as<Plan>();
+    pa.nbatches = nb;
+    pa.tail_status = s->tail_status;
+    pa.has_agg = 1;
+    pa.acc0 = acc0;
+    g.state = c->dstate.as<int32_t>();
+    g.crc_acc = c->crcparts.as<uint32_t>();
+    J[k] = g;
+    oe[k + 1] = oe[k] + nb;
+    om[k + 1] = om[k] + ga_mins_blocks(nb);
+    os[k + 1] = os[k] + (nb + 3) / 4;
+  }
+  GaJob* dJ = e->ga_dev.as<GaJob>();
+  const uint32_t* doff = (const uint32_t*)((uint8_t*)e->ga_dev.p + jb);
+  GaResult* dres = (GaResult*)((uint8_t*)e->ga_dev.p + rb_off);
+  GaOffsets o{doff, doff + (m + 1), doff + 2 * (m + 1), doff + 3 * (m + 1), doff + 4 * (m + 1),
+              oe[m], om[m], os[m], 0, 0};
+  const bool timed = chains[fast[0]]->timed;
+  HIPCHK(hipMemcpyAsync(e->ga_dev.p, hp, jb + ob, hipMemcpyHostToDevice, gs));
+  if (timed) HIPCHK(hipEventRecord(e->ga_ev[0], gs));
+  launch_ga_phase1(dJ, m, o, dres, gs);
+  if (timed) HIPCHK(hipEventRecord(e->ga_ev[1], gs));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(hp + rb_off, dres, (size_t)m * sizeof(GaResult), hipMemcpyDeviceToHost, gs));
+  HIPCHK(wait_stream(gs));
+  const GaResult* R = (const GaResult*)(hp + rb_off);
+  // the plans: outputs sized, abnormal chains back to the general path
+  std::vector<uint8_t> done(m, 0);
+  for (uint32_t k = 0; k < m; k++) {
+    fsg_chain* c = chains[fast[k]];
+    const Plan& p = R[k].plan;
+    if (R[k].deferred || p.status != 0 || p.err_batch >= 0) {
+      J[k].out_len = 0;
+      J[k].wa = WriteArgs{};
+      J[k].wa.first = -1;
+      ow[k + 1] = ow[k];
+      oc[k + 1] = oc[k];
+      continue;
+    }
+    done[k] = 1;
+    const size_t out_len = 61 + p.rec_bytes;
+    if (c->out.ensure(out_len + 64)) return bail("output");
+    WriteArgs& wa = J[k].wa;
+    wa = WriteArgs{};
+    wa.slice = J[k].ea.slice;
+    wa.bstat = J[k].ea.bstat;
+    wa.desc = J[k].ea.desc;
+    wa.rbase = J[k].ea.rbase;
+    wa.pre = J[k].pre;
+    wa.agg_pre = J[k].aggpre;
+    wa.plan = J[k].pa.plan;
+    wa.out = c->out.as<uint8_t>();
+    wa.acc0 = J[k].pa.acc0;
+    wa.first = p.first;
+    wa.last = p.last;
+    J[k].out_len = out_len;
+    const uint32_t nblk = p.last >= p.first && p.first >= 0 && p.n_records ? (uint32_t)(p.last - p.first + 1) : 0u;
+    ow[k + 1] = ow[k] + nblk;
+    oc[k + 1] = oc[k] + ga_crc_blocks(out_len);
+  }
+  o.t_write = ow[m];
+  o.t_crc = oc[m];
+  HIPCHK(hipMemcpyAsync(e->ga_dev.p, hp, jb + ob, hipMemcpyHostToDevice, gs));
+  launch_ga_phase2(dJ, m, o, gs);
+  if (timed) {
+    HIPCHK(hipEventRecord(e->ga_ev[2], gs));
+    HIPCHK(hipEventRecord(e->ga_ev[3], gs));
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(wait_stream(gs));
+  float t1 = 0, t2 = 0;
+  if (timed) {
+    HIPCHK(hipEventElapsedTime(&t1, e->ga_ev[0], e->ga_ev[1]));
+    HIPCHK(hipEventElapsedTime(&t2, e->ga_ev[1], e->ga_ev[2]));
+  }
+  for (uint32_t k = 0; k < m; k++) {
+    const size_t i = fast[k];
+    fsg_chain* c = chains[i];
+    const fsg_slice* s = slices[i];
+    if (!done[k]) {
+      rest.push_back(i);
+      continue;
+    }
+    const Plan& p = R[k].plan;
+    c->hplan = p;
+    c->last_pa = J[k].pa;
+    c->out_len = J[k].out_len;
+    c->out_pinned = false;
+    c->last_has_aggj = false;
+    fsg_timings& t = c->last;
+    t = fsg_timings{};
+    if (k == 0) {  // the group's phase times on its first chain (the phases are one launch each for every chain)
+      t.eval_ms = t1;
+      t.write_ms = t2;
+      t.total_ms = t1 + t2;
+    }
+    t.in_bytes = s->header_bytes;
+    t.out_bytes = J[k].out_len;
+    t.n_batches = s->nb;
+    t.n_records_in = s->nrec;
+    t.eval_path = FSG_EVAL_INT;
+    if (metrics) {
+      metrics[i].bytes_in += p.bytes_in;
+      metrics[i].invocation_count += p.invocations;
+      metrics[i].records_out += p.records_out;
+    }
+    rcs[i] = FSG_OK;
+    if (p.acc_touched) (void)acc_update(c, p, false);
+    if (outs) {
+      auto res = std::make_unique<fsg_batch_output>();
+      res->base_offset = p.base_offset;
+      res->last_offset_delta = p.lod;
+      res->n_records = (uint32_t)p.n_records;
+      const int rc = download_output(c, res.get());
+      if (rc) {
+        rcs[i] = rc;
+        continue;
+      }
+      outs[i] = res.release();
+    }
+  }
+  return FSG_OK;
+}
+
 extern "C" int fsg_chain_group_process_slices(fsg_chain* const* chains, const fsg_slice* const* slices, size_t n,
                                               uint64_t max_bytes, fsg_metrics* metrics, fsg_batch_output** outs,
                                               int* rcs) {
@@ -2953,12 +3187,19 @@ extern "C" int fsg_chain_group_process_slices(fsg_chain* const* chains, const fs
       return fail(FSG_E_INVALID_ARG, "fsg_chain_group_process_slices: chains on different devices");
   }
   std::unique_lock<std::mutex> glk(chains[0]->eng->gmu);
+  HIPCHK(hipSetDevice(chains[0]->eng->device));
+  if (outs)
+    for (size_t i = 0; i < n; i++) outs[i] = nullptr;
+  // aggregate-sum chains over decimal records: one launch per phase for all of them
+  std::vector<size_t> todo;
+  const int frc = group_agg_fast(chains, slices, n, max_bytes, metrics, outs, rcs, todo);
+  if (frc) return frc;
   AjGroup g;
   g.device = chains[0]->eng->device;
   g.eng = chains[0]->eng;
-  g.expected = n;
+  g.expected = todo.size();
   std::vector<size_t> walkers, others;
-  for (size_t i = 0; i < n; i++) {
+  for (size_t i : todo) {
     fsg_chain* c = chains[i];
     // only plain aggregate-json chains walk in the group; the others arrive at once
     const bool walks = (c->hdesc.flags & CF_AGG_JSON) && c->segs.empty();
@@ -2969,6 +3210,13 @@ extern "C" int fsg_chain_group_process_slices(fsg_chain* const* chains, const fs
   }
   std::vector<std::string> errs(n);
   std::vector<std::array<uint64_t, 3>> smem(n);  // g_store_mem is thread-local too
+  // per-phase timing events on the first chain only: ~8 event calls per chain
+  // and call contend for the runtime's locks with every other chain's launches
+  std::vector<uint8_t> was_timed(n);
+  for (size_t i = 0; i < n; i++) {
+    was_timed[i] = chains[i]->timed ? 1 : 0;
+    if (i) chains[i]->timed = false;
+  }
   auto one = [&](size_t i) {
     fsg_chain* c = chains[i];
     if (outs) outs[i] = nullptr;
@@ -2986,7 +3234,8 @@ extern "C" int fsg_chain_group_process_slices(fsg_chain* const* chains, const fs
   th.reserve(walkers.size() + 16);
   for (size_t i : walkers) th.emplace_back(one, i);
   std::atomic<size_t> next{0};
-  const size_t pool = std::min<size_t>(others.size(), 16);
+  static const size_t kPool = getenv("FSG_GROUP_THREADS") ? std::max(1, atoi(getenv("FSG_GROUP_THREADS"))) : 16;
+  const size_t pool = std::min<size_t>(others.size(), kPool);
   for (size_t k = 0; k < pool; k++)
     th.emplace_back([&] {
       for (size_t j = next++; j < others.size(); j = next++) one(others[j]);
@@ -2995,6 +3244,7 @@ extern "C" int fsg_chain_group_process_slices(fsg_chain* const* chains, const fs
   int rc = FSG_OK;
   for (size_t i = 0; i < n; i++) {
     chains[i]->group = nullptr;
+    chains[i]->timed = was_timed[i] != 0;
     if (rcs[i] && rc == FSG_OK) {
       rc = rcs[i];
       g_err = errs[i];
