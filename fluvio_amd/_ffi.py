@@ -193,6 +193,8 @@ def debug_lib():
         D.fsg_debug_regex_match.restype = ctypes.c_int
         D.fsg_debug_regex_match.argtypes = [ctypes.c_char_p, ctypes.c_char_p, SZ, ctypes.POINTER(ctypes.c_int),
                                             ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+        D.fsg_debug_regex_error.restype = ctypes.c_int
+        D.fsg_debug_regex_error.argtypes = [ctypes.c_char_p, ctypes.c_char_p, SZ]
         _debug = D
     return _debug
 

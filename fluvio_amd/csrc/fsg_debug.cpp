@@ -2,6 +2,7 @@
 // the chain-build-time regex -> DFA compiler and the JSON float arithmetic the
 // kernels share with the host (fsg_float.h).  Not part of the data path: no
 // record of a process call ever goes through these.
+#include <algorithm>
 #include <cstring>
 #include <string>
 
@@ -19,11 +20,26 @@ extern "C" int fsg_debug_regex_match(const char* pattern, const uint8_t* text, s
   // the kernel's choice: ASCII DFA for ASCII-only values, full DFA otherwise
   // (the marked walk for Unicode word boundaries)
   if (!ascii && a.unicode_word && !d.marked) return -103;
+  if (!ascii && d.utab && fsg::utf8_has_newer(text, n)) return -103;  // k_eval's version check
   *is_match = (ascii ? fsg::dfa_is_match(a, text, n) : d.marked ? fsg::dfa_is_match_marked(d, text, n)
                                                                 : fsg::dfa_is_match(d, text, n)) ? 1 : 0;
   if (max_len) *max_len = a.max_len;
   if (nstates) *nstates = (int)d.nstates;
   return 0;
+}
+
+// the chain-build message of a pattern (compile_regex's msg: the init error
+// text for FSG_E_INIT); returns compile_regex's code, msg NUL-terminated in cap
+extern "C" int fsg_debug_regex_error(const char* pattern, char* msg, size_t cap) {
+  fsg::Dfa a, d;
+  std::string m;
+  const int rc = fsg::compile_regex(pattern, a, d, m);
+  if (cap) {
+    const size_t k = std::min(cap - 1, m.size());
+    memcpy(msg, m.data(), k);
+    msg[k] = 0;
+  }
+  return rc;
 }
 
 // serde_json's reading of the JSON number text[0..n) (fsg_float.h num_value):

@@ -89,6 +89,11 @@ struct DfaDesc {
   uint32_t tt_up;      // blob offset: u64[256], rows of toupper(byte)
   uint32_t acc1;
   uint32_t acc2;
+  // version-uncertain code points (fsg_unicode.h fsg_u_newer): blob offset of
+  // (lo, hi) u32 pairs, vtab_n of them; 0 when the pattern uses no
+  // version-dependent table (a value holding one is then FSG_E_UNSUPPORTED)
+  uint32_t vtab;
+  uint32_t vtab_n;
 };
 
 struct StageDesc {

@@ -670,6 +670,32 @@ __device__ bool dfa_run_full(P s, uint32_t n, const uint8_t* blob, const DfaDesc
   return (acc[st] & 2) != 0;
 }
 
+// a code point of the valid UTF-8 value in the DFA's version-uncertain ranges
+// (fsg_u_newer: assigned, or recategorized, after this build's Unicode 13
+// tables; binary search over the blob's (lo, hi) pairs)
+template <typename P>
+__device__ bool utf8_has_newer(P s, uint32_t n, const uint8_t* blob, const DfaDesc& f) {
+  const uint32_t* vt = (const uint32_t*)(blob + f.vtab);
+  for (uint32_t i = 0; i < n;) {
+    const uint32_t c0 = s[i];
+    if (c0 < 0x80) {
+      i++;
+      continue;
+    }
+    const uint32_t w = c0 < 0xE0 ? 2u : c0 < 0xF0 ? 3u : 4u;
+    uint32_t cp = w == 2 ? (c0 & 0x1Fu) : w == 3 ? (c0 & 0x0Fu) : (c0 & 0x07u);
+    for (uint32_t k = 1; k < w && i + k < n; k++) cp = (cp << 6) | (s[i + k] & 0x3Fu);
+    uint32_t lo = 0, hi = f.vtab_n;
+    while (lo < hi) {
+      const uint32_t m = (lo + hi) >> 1;
+      if (vt[2 * m + 1] < cp) lo = m + 1; else hi = m;
+    }
+    if (lo < f.vtab_n && vt[2 * lo] <= cp) return true;
+    i += w;
+  }
+  return false;
+}
+
 // the marked walk (Unicode \b / \B, fsg_regex.h): before each code point the
 // marker of its class (0xFC a \w code point, 0xFE \n, 0xFD any other), then
 // its bytes; \w membership by binary search over the blob's ranges.  The
@@ -803,8 +829,12 @@ __device__ __forceinline__ void eval_window(WaveLds& L, P w, uint32_t wlen, int 
             bool m;
             if (src) {
               if (f & RF_NONASCII) {
-                if (sd.dfa.unicode_word && !sd.dfa.f_marked) {
-                  err = true;  // (?-u) \b on a non-ASCII value: surfaces only if this record is reached
+                if ((sd.dfa.unicode_word && !sd.dfa.f_marked) ||
+                    (sd.dfa.vtab_n && utf8_has_newer(w + vs, vl, blob, sd.dfa))) {
+                  // (?-u) \b on a non-ASCII value, or a code point whose class
+                  // membership differs between Unicode versions: surfaces only if
+                  // this record is reached
+                  err = true;
                   ec = EC_UNSUP;
                   break;
                 }

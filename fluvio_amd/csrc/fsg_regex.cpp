@@ -129,6 +129,13 @@ struct Parser {
   bool wbu = false, wba = false;  // \b / \B seen in Unicode mode / under (?-u)
   bool fi = false, fs = false;  // inline flags i, s
   bool fm = false, fx = false, fu = true;  // m (multi-line), x (verbose), u (Unicode, on by default)
+  // utab: a class built from version-dependent Unicode tables (\d \w, \p, (?i)
+  // folding, Unicode \b) — values holding a fsg_u_newer code point are
+  // FSG_E_UNSUPPORTED; perr: the first \p name regex-syntax rejects at
+  // Regex::new (fsg_u_unresolved 2 / 3) and its span [perr_lo, perr_hi)
+  bool utab = false;
+  int perr = 0;
+  size_t perr_lo = 0, perr_hi = 0;
 
   // x: whitespace (char::is_whitespace) and # comments between tokens are ignored
   static bool uspace(uint32_t c) {
@@ -154,6 +161,7 @@ struct Parser {
       err = true;
       return 0;
     }
+    const size_t at0 = i - 2;  // the escape's '\'
     std::string name;
     if (at('{')) {
       i++;
@@ -232,11 +240,22 @@ struct Parser {
       const fsg_urange* pr = nullptr;
       uint32_t pn = 0;
       if (!fsg_u_lookup(name.c_str(), &pr, &pn)) {
-        unsup = true;  // other properties (Age, Grapheme_Cluster_Break, ...): not restated
-        return 0;
+        const int k = fsg_u_unresolved(name.c_str());
+        if (k == 1) {
+          unsup = true;  // Age values, CWKCF: regex-syntax has them, not restated here
+          return 0;
+        }
+        if (!perr) {  // rejected at Regex::new: reported once the whole pattern parsed
+          perr = k;
+          perr_lo = at0;
+          perr_hi = i;
+        }
+        *out = Set{};
+        return 2;
       }
       st = urange(pr, pn);
     }
+    if (m != FSG_UPROP_ASCII && m != FSG_UPROP_WSPACE) utab = true;
     if (fi) fold_set(st);  // (?i): simple case folding, before the negation
     *out = neg ? negate(st) : norm(st);
     return 2;
@@ -248,6 +267,7 @@ struct Parser {
   // classes)
   static void fold_add(void* ctx, uint32_t c) { static_cast<Set*>(ctx)->push_back({c, c}); }
   void fold_set(Set& st) {
+    utab = true;
     const Set base = st;
     for (const auto& r : base) fsg_u_fold_range(r.lo, r.hi, fold_add, &st);
   }
@@ -255,6 +275,7 @@ struct Parser {
     st.push_back({lo, hi});
     if (!fi) return;
     if (fu) {
+      utab = true;
       fsg_u_fold_range(lo, hi, fold_add, &st);
       return;
     }
@@ -315,6 +336,7 @@ struct Parser {
           err = true;
           return 0;
         }
+        if (fu && (e | 0x20) != 's') utab = true;  // White_Space is the same in every version
         Set t = (e | 0x20) == 'd' ? (fu ? table(kNd, false) : table(kDigitAscii, false))
                 : (e | 0x20) == 's' ? (fu ? table(kWs, false) : table(kSpaceAscii, false))
                 : (fu ? urange(fsg_u_word, fsg_u_word_n) : table(kWordAscii, false));
@@ -1147,6 +1169,11 @@ int compile_regex(const std::string& pattern, Dfa& out, Dfa& full, std::string& 
     }
   }
   NodeP root = P.alt();
+  if (P.perr && !P.err && P.i == P.p.size()) {
+    msg = syntax_error_text(P.p, P.perr_lo, P.perr_hi,
+                            P.perr == 2 ? "Unicode property value not found" : "Unicode property not found");
+    return -2;
+  }
   if (P.unsup) {
     msg = "unsupported regex syntax";
     return -103;
@@ -1158,7 +1185,84 @@ int compile_regex(const std::string& pattern, Dfa& out, Dfa& full, std::string& 
   if (int rc = determinize(root.get(), true, P.word, P.wb, P.ml, out, msg)) return rc;
   // Unicode word boundaries: the full DFA is the marked one (a (?-u) \b among
   // them keeps non-ASCII values FSG_E_UNSUPPORTED: bytes inside a code point)
-  return determinize(root.get(), false, P.word, P.wb, P.ml, full, msg, P.wbu && !P.wba);
+  const int rc = determinize(root.get(), false, P.word, P.wb, P.ml, full, msg, P.wbu && !P.wba);
+  out.utab = full.utab = P.utab || P.wbu;
+  return rc;
+}
+
+// regex-syntax's error Display (error.rs Formatter / Spans::notate, the same in
+// 0.6.27 and 0.7.1): "regex parse error:", the pattern's lines (4 spaces in
+// front, or a right-aligned line number and ": " when the pattern has a '\n',
+// between two lines of 79 '~'), a line of '^' under a one-line span, "on line
+// .. through line .." for a span over lines, then "error: <kind>".  Columns
+// count code points; [lo, hi) are code-point offsets into the pattern.
+static void put_utf8(std::string& s, uint32_t c) {
+  if (c < 0x80) {
+    s += (char)c;
+  } else if (c < 0x800) {
+    s += (char)(0xC0 | (c >> 6));
+    s += (char)(0x80 | (c & 0x3F));
+  } else if (c < 0x10000) {
+    s += (char)(0xE0 | (c >> 12));
+    s += (char)(0x80 | ((c >> 6) & 0x3F));
+    s += (char)(0x80 | (c & 0x3F));
+  } else {
+    s += (char)(0xF0 | (c >> 18));
+    s += (char)(0x80 | ((c >> 12) & 0x3F));
+    s += (char)(0x80 | ((c >> 6) & 0x3F));
+    s += (char)(0x80 | (c & 0x3F));
+  }
+}
+
+std::string syntax_error_text(const std::vector<uint32_t>& p, size_t lo, size_t hi, const char* kind) {
+  // str::lines: split at '\n', one trailing '\r' dropped per line, no empty last line
+  std::vector<std::pair<size_t, size_t>> lines;
+  for (size_t s = 0, k = 0; k <= p.size(); k++)
+    if (k == p.size() || p[k] == '\n') {
+      if (k < p.size() || k > s) lines.push_back({s, k < p.size() && k > s && p[k - 1] == '\r' ? k - 1 : k});
+      s = k + 1;
+    }
+  const bool multi = std::find(p.begin(), p.end(), (uint32_t)'\n') != p.end();
+  size_t line_count = lines.size() + (!p.empty() && p.back() == '\n' ? 1 : 0);
+  const size_t lnw = line_count <= 1 ? 0 : std::to_string(line_count).size();
+  auto pos = [&](size_t off, size_t& line, size_t& col) {  // 1-based line / column of offset off
+    line = 1;
+    size_t ls = 0;
+    for (size_t k = 0; k < off; k++)
+      if (p[k] == '\n') {
+        line++;
+        ls = k + 1;
+      }
+    col = off - ls + 1;
+  };
+  size_t l0, c0, l1, c1;
+  pos(lo, l0, c0);
+  pos(hi, l1, c1);
+  std::string notated;
+  for (size_t n = 0; n < lines.size(); n++) {
+    if (lnw) {
+      const std::string num = std::to_string(n + 1);
+      notated += std::string(lnw - num.size(), ' ') + num + ": ";
+    } else {
+      notated += "    ";
+    }
+    for (size_t k = lines[n].first; k < lines[n].second; k++) put_utf8(notated, p[k]);
+    notated += '\n';
+    if (l0 == l1 && l0 == n + 1) {
+      notated += std::string(lnw ? 2 + lnw : 4, ' ');
+      notated += std::string(c0 - 1, ' ');
+      notated += std::string(std::max<size_t>(1, c1 > c0 ? c1 - c0 : 0), '^');
+      notated += '\n';
+    }
+  }
+  std::string out = "regex parse error:\n";
+  if (!multi) return out + notated + "error: " + kind;
+  const std::string div(79, '~');
+  out += div + "\n" + notated + div + "\n";
+  if (l0 != l1)
+    out += "on line " + std::to_string(l0) + " (column " + std::to_string(c0) + ") through line " +
+           std::to_string(l1) + " (column " + std::to_string(c1 - 1) + ")\n";
+  return out + "error: " + kind;
 }
 
 static bool word_cp(uint32_t c) {
@@ -1408,6 +1512,27 @@ int determinize(const Node* rootp, bool ascii, bool word, bool wb, bool mlm, Dfa
     for (uint32_t c = 0; c < out.nclasses; c++) out.trans[s * out.nclasses + c] = (uint16_t)trans[s][c];
   out.accept = acc;
   return 0;
+}
+
+std::vector<uint32_t> unicode_newer_ranges() {
+  std::vector<uint32_t> v;
+  for (uint32_t q = 0; q < fsg_u_newer_n; q++) {
+    v.push_back(fsg_u_newer[q].lo);
+    v.push_back(fsg_u_newer[q].hi);
+  }
+  return v;
+}
+
+bool utf8_has_newer(const uint8_t* s, size_t n) {
+  for (size_t i = 0; i < n;) {
+    const uint32_t c0 = s[i];
+    const size_t w = c0 < 0x80 ? 1 : c0 < 0xE0 ? 2 : c0 < 0xF0 ? 3 : 4;
+    uint32_t cp = w == 1 ? c0 : w == 2 ? (c0 & 0x1F) : w == 3 ? (c0 & 0x0F) : (c0 & 0x07);
+    for (size_t k = 1; k < w && i + k < n; k++) cp = (cp << 6) | (s[i + k] & 0x3F);
+    if (cp >= 0x80 && fsg_u_is_newer(cp)) return true;
+    i += w;
+  }
+  return false;
 }
 
 std::vector<uint32_t> unicode_word_ranges() {

@@ -800,6 +800,11 @@ int add_stage(fsg_chain* c, const ModuleSpec& m, const std::string& name, uint8_
       sd.dfa.wtab = put_blob(wt.data(), wt.size() * 4);
       sd.dfa.wtab_n = (uint32_t)(wt.size() / 2);
     }
+    if (d.utab) {  // regex-syntax 0.6.27 / 0.7.1 tables differ from this build's on these
+      const std::vector<uint32_t> vt = unicode_newer_ranges();
+      sd.dfa.vtab = put_blob(vt.data(), vt.size() * 4);
+      sd.dfa.vtab_n = (uint32_t)(vt.size() / 2);
+    }
     if (d.nstates <= 16) {  // the lean kernel's byte-row tables (fsg_device.h DfaDesc)
       std::vector<uint64_t> tt(256, 0), ttu(256, 0);
       for (uint32_t b = 0; b < 256; b++)

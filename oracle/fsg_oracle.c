@@ -612,6 +612,7 @@ typedef struct {
   size_t ncls, ccap;
   int unicode_word; /* \b / \B used */
   int ascii_wb;     /* a (?-u) \b / \B among them: bytes inside a code point, exact only on ASCII input */
+  int utab;         /* version-dependent tables: a fsg_u_newer code point in the text is unsupported */
 } rxprog;
 
 /* AST */
@@ -636,6 +637,9 @@ typedef struct {
   int fm, fx, fu; /* m: ^ $ at line boundaries; x: whitespace / # comments ignored; u: Unicode classes (on) */
   int word;     /* \b or \B used */
   int wba;      /* \b or \B under (?-u) */
+  int utab;     /* a version-dependent Unicode table used (\d \w \p, (?i) folding, Unicode \b) */
+  int perr;     /* the first \p name regex-syntax rejects: 2 value not found, 3 property not found */
+  size_t perr_lo, perr_hi; /* its span, code-point offsets [lo, hi) */
 } rxparser;
 
 /* x: whitespace (White_Space) and # comments between tokens are skipped */
@@ -662,6 +666,7 @@ static int rx_property(rxparser *P, int neg, cset *set) {
     P->err = 1;
     return 0;
   }
+  const size_t at0 = P->i - 2; /* the escape's backslash */
   char name[64];
   size_t nl = 0;
   if (P->i < P->n && P->p[P->i] == '{') {
@@ -731,12 +736,23 @@ static int rx_property(rxparser *P, int neg, cset *set) {
     const fsg_urange *pr = NULL;
     uint32_t pn = 0;
     if (!fsg_u_lookup(name, &pr, &pn)) {
-      P->unsupported = 1; /* other enumerated properties (Age, the break properties, ...) */
-      return 0;
+      const int k = fsg_u_unresolved(name);
+      if (k == 1) {
+        P->unsupported = 1; /* Age values, CWKCF: known to regex-syntax, not restated */
+        return 0;
+      }
+      if (!P->perr) { /* Regex::new fails; reported after the whole pattern parsed */
+        P->perr = k;
+        P->perr_lo = at0;
+        P->perr_hi = P->i;
+      }
+      return 2;
     }
     for (uint32_t q = 0; q < pn; q++) cs_add(&tmp, pr[q].lo, pr[q].hi);
   }
+  if (m != FSG_UPROP_ASCII && m != FSG_UPROP_WSPACE) P->utab = 1;
   if (P->fi) { /* (?i): simple case folding before the negation */
+    P->utab = 1;
     size_t n0 = tmp.n;
     for (size_t q = 0; q < n0; q++) fsg_u_fold_range(tmp.r[q].lo, tmp.r[q].hi, cs_fold_add, &tmp);
   }
@@ -753,6 +769,7 @@ static void cs_add_folded(rxparser *P, cset *s, uint32_t lo, uint32_t hi) {
   cs_add(s, lo, hi);
   if (!P->fi) return;
   if (P->fu) {
+    P->utab = 1;
     fsg_u_fold_range(lo, hi, cs_fold_add, s);
     return;
   }
@@ -834,6 +851,7 @@ static int rx_escape(rxparser *P, uint32_t *single, cset *set, int in_class) {
         P->err = 1;
         return 0;
       }
+      if (P->fu && k != 's') P->utab = 1; /* White_Space is the same in every version */
       if (k == 'd') {
         if (P->fu) cs_add_tab(set, ND_TAB, sizeof ND_TAB / sizeof ND_TAB[0], neg);
         else cs_add_tab(set, DIGIT_ASCII, 1, 0);
@@ -855,6 +873,7 @@ static int rx_escape(rxparser *P, uint32_t *single, cset *set, int in_class) {
       }
       P->word = 1;
       if (!P->fu) P->wba = 1;
+      else P->utab = 1;
       return c == 'b' ? 3 : 4;
     case 'A': return in_class ? (P->err = 1, 0) : 5; /* start of text (= ^ without m) */
     case 'z': return in_class ? (P->err = 1, 0) : 6; /* end of text (= $ without m) */
@@ -1420,12 +1439,112 @@ static void rxprog_free(rxprog *g) {
   memset(g, 0, sizeof *g);
 }
 
-/* 0 ok, ORC_E_INIT on syntax error, ORC_E_UNSUPPORTED on unsupported syntax */
-static int rx_compile(const char *pat, rxprog *g) {
+/* regex-syntax's error Display (error.rs Formatter / Spans::notate, the same in
+ * 0.6.27 and 0.7.1) for the span [lo, hi) of the pattern's code points cp[0..n):
+ * "regex parse error:", the pattern's lines (4 spaces in front, or a
+ * right-aligned line number and ": " when the pattern holds a '\n', between
+ * two lines of 79 '~'), '^' under a one-line span, "on line .. through line .."
+ * for a span over lines, then "error: <kind>".  Columns count code points. */
+static void sb_put(char **b, size_t *len, size_t *cap, const char *s, size_t n) {
+  if (*len + n + 1 > *cap) {
+    *cap = (*len + n + 1) * 2;
+    *b = (char *)realloc(*b, *cap);
+  }
+  memcpy(*b + *len, s, n);
+  *len += n;
+  (*b)[*len] = 0;
+}
+static void sb_rep(char **b, size_t *len, size_t *cap, char c, size_t n) {
+  for (size_t k = 0; k < n; k++) sb_put(b, len, cap, &c, 1);
+}
+static void sb_cp(char **b, size_t *len, size_t *cap, uint32_t c) {
+  char u[4];
+  size_t w;
+  if (c < 0x80) { u[0] = (char)c; w = 1; }
+  else if (c < 0x800) { u[0] = (char)(0xC0 | (c >> 6)); u[1] = (char)(0x80 | (c & 0x3F)); w = 2; }
+  else if (c < 0x10000) { u[0] = (char)(0xE0 | (c >> 12)); u[1] = (char)(0x80 | ((c >> 6) & 0x3F)); u[2] = (char)(0x80 | (c & 0x3F)); w = 3; }
+  else { u[0] = (char)(0xF0 | (c >> 18)); u[1] = (char)(0x80 | ((c >> 12) & 0x3F)); u[2] = (char)(0x80 | ((c >> 6) & 0x3F)); u[3] = (char)(0x80 | (c & 0x3F)); w = 4; }
+  sb_put(b, len, cap, u, w);
+}
+static void rx_pos(const uint32_t *cp, size_t off, size_t *line, size_t *col) {
+  size_t ls = 0;
+  *line = 1;
+  for (size_t k = 0; k < off; k++)
+    if (cp[k] == '\n') {
+      ++*line;
+      ls = k + 1;
+    }
+  *col = off - ls + 1;
+}
+static char *rx_error_text(const uint32_t *cp, size_t n, size_t lo, size_t hi, const char *kind) {
+  char *b = NULL, num[32];
+  size_t len = 0, cap = 0;
+  int multi = 0;
+  size_t nlines = 0, l0, c0, l1, c1;
+  for (size_t k = 0; k < n; k++) multi |= cp[k] == '\n';
+  /* str::lines: split at '\n' (a "\r\n" ending dropped whole), no empty last line */
+  for (size_t s = 0, k = 0; k <= n; k++)
+    if (k == n || cp[k] == '\n') {
+      if (k < n || k > s) nlines++;
+      s = k + 1;
+    }
+  size_t count = nlines + (n && cp[n - 1] == '\n' ? 1 : 0), lnw = 0;
+  if (count > 1) lnw = (size_t)sprintf(num, "%zu", count);
+  rx_pos(cp, lo, &l0, &c0);
+  rx_pos(cp, hi, &l1, &c1);
+  sb_put(&b, &len, &cap, "regex parse error:\n", 19);
+  if (multi) {
+    sb_rep(&b, &len, &cap, '~', 79);
+    sb_put(&b, &len, &cap, "\n", 1);
+  }
+  size_t line = 0;
+  for (size_t s = 0, k = 0; k <= n; k++) {
+    if (!(k == n || cp[k] == '\n')) continue;
+    if (k == n && k <= s) break; /* no empty last line */
+    size_t e = (k < n && k > s && cp[k - 1] == '\r') ? k - 1 : k;
+    line++;
+    if (lnw) {
+      int w = sprintf(num, "%zu", line);
+      sb_rep(&b, &len, &cap, ' ', lnw - (size_t)w);
+      sb_put(&b, &len, &cap, num, (size_t)w);
+      sb_put(&b, &len, &cap, ": ", 2);
+    } else {
+      sb_put(&b, &len, &cap, "    ", 4);
+    }
+    for (size_t q = s; q < e; q++) sb_cp(&b, &len, &cap, cp[q]);
+    sb_put(&b, &len, &cap, "\n", 1);
+    if (l0 == l1 && l0 == line) {
+      sb_rep(&b, &len, &cap, ' ', lnw ? 2 + lnw : 4);
+      sb_rep(&b, &len, &cap, ' ', c0 - 1);
+      sb_rep(&b, &len, &cap, '^', c1 > c0 ? c1 - c0 : 1);
+      sb_put(&b, &len, &cap, "\n", 1);
+    }
+    s = k + 1;
+  }
+  if (multi) {
+    sb_rep(&b, &len, &cap, '~', 79);
+    sb_put(&b, &len, &cap, "\n", 1);
+    if (l0 != l1) {
+      char t[160];
+      int w = sprintf(t, "on line %zu (column %zu) through line %zu (column %zu)\n", l0, c0, l1, c1 - 1);
+      sb_put(&b, &len, &cap, t, (size_t)w);
+    }
+  }
+  sb_put(&b, &len, &cap, "error: ", 7);
+  sb_put(&b, &len, &cap, kind, strlen(kind));
+  return b;
+}
+
+/* 0 ok, ORC_E_INIT on syntax error, ORC_E_UNSUPPORTED on unsupported syntax;
+ * *msg (when msg is not NULL): the error text, malloc'd */
+static int rx_compile(const char *pat, rxprog *g, char **msg) {
   memset(g, 0, sizeof *g);
   size_t plen = strlen(pat), vut;
   int el;
-  if (!utf8_check((const uint8_t *)pat, plen, &vut, &el)) return ORC_E_INIT;
+  if (!utf8_check((const uint8_t *)pat, plen, &vut, &el)) {
+    if (msg) *msg = dup_str("regex parse error");
+    return ORC_E_INIT;
+  }
   size_t ncp;
   uint32_t *cps = utf8_decode((const uint8_t *)pat, plen, &ncp);
   rxparser P;
@@ -1436,11 +1555,20 @@ static int rx_compile(const char *pat, rxprog *g) {
   anode *root = rx_parse_alt(&P);
   if (P.word) g->unicode_word = 1;
   if (P.wba) g->ascii_wb = 1;
+  g->utab = P.utab;
   int rc = 0;
-  if (P.unsupported)
-    rc = ORC_E_UNSUPPORTED;
-  else if (P.err || P.i != P.n)
+  if (P.perr && !P.err && P.i == P.n) {
     rc = ORC_E_INIT;
+    if (msg)
+      *msg = rx_error_text(cps, ncp, P.perr_lo, P.perr_hi,
+                           P.perr == 2 ? "Unicode property value not found" : "Unicode property not found");
+  } else if (P.unsupported) {
+    rc = ORC_E_UNSUPPORTED;
+    if (msg) *msg = dup_str("unsupported regex syntax");
+  } else if (P.err || P.i != P.n) {
+    rc = ORC_E_INIT;
+    if (msg) *msg = dup_str("regex parse error");
+  }
   if (!rc) {
     rx_comp(g, root);
     rx_emit(g, RX_MATCH, 0, 0, 0);
@@ -1509,6 +1637,11 @@ static int rx_run(const rxprog *g, const uint32_t *cp, size_t n) {
   if (g->unicode_word && g->ascii_wb)
     for (size_t i = 0; i < n; i++)
       if (cp[i] >= 0x80) return -1;
+  /* a code point whose class membership differs between this build's Unicode 13
+   * tables and regex-syntax 0.6.27 / 0.7.1's (Unicode 14 / 15): not decided */
+  if (g->utab)
+    for (size_t i = 0; i < n; i++)
+      if (cp[i] >= 0x80 && fsg_u_is_newer(cp[i])) return -1;
   int np = (int)g->n;
   sset a = {(int *)malloc(np * sizeof(int)), (int *)calloc(np, sizeof(int)), 0};
   sset b = {(int *)malloc(np * sizeof(int)), (int *)calloc(np, sizeof(int)), 0};
@@ -1544,7 +1677,7 @@ static int rx_run(const rxprog *g, const uint32_t *cp, size_t n) {
 
 int orc_regex_is_match(const char *pattern, const uint8_t *text, size_t n, int *is_match) {
   rxprog g;
-  int rc = rx_compile(pattern, &g);
+  int rc = rx_compile(pattern, &g, NULL);
   if (rc) return rc;
   size_t vut;
   int el;
@@ -1770,12 +1903,22 @@ int orc_chain_add(orc_chain *c, const char *module, const char **keys, const cha
       pat = "\\d{3}-\\d{2}-\\d{4}";
       s.rx_keep_match = 0;
     }
-    int rc = rx_compile(pat, &s.rx);
+    char *em = NULL;
+    int rc = rx_compile(pat, &s.rx, &em);
     if (rc) {
       rxprog_free(&s.rx);
-      if (msg_out) *msg_out = dup_str(rc == ORC_E_UNSUPPORTED ? "unsupported regex syntax" : "regex parse error");
+      if (msg_out && rc == ORC_E_INIT) { /* the init error Display (SmartModuleInitError) */
+        size_t k = strlen(em);
+        char *t = (char *)malloc(k + 32);
+        sprintf(t, "%s\n\nSmartModule Init Error: \n", em);
+        *msg_out = t;
+      } else if (msg_out) {
+        *msg_out = dup_str(em);
+      }
+      free(em);
       return rc;
     }
+    free(em);
     s.mod = M_FILTER_REGEX;
     s.kind = K_FILTER;
   } else if (!strcmp(module, "filter_json")) {

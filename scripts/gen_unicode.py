@@ -1,9 +1,11 @@
 """Generate the Unicode class tables the regex compiler (fluvio_amd/csrc) and the
 oracle's Pike VM (oracle/) share: General_Category ranges and the Perl \\w set
 of regex-syntax (Alphabetic + M + Nd + Pc + Join_Control), from this image's
-Python unicodedata.  The reference's regex crate (1.6 / 1.8) carries Unicode
-14 / 15 tables; code points assigned after unicodedata's version differ
-(parity unpinned for them).  Usage: python scripts/gen_unicode.py"""
+Python unicodedata.  The reference's regex crate carries Unicode 14
+(regex-filter: regex-syntax 0.6.27) / 15 (examples: 0.7.1) tables, neither of
+which is in the image: the code points whose General_Category differs between
+unicodedata and the regex module's newer UCD (fsg_u_newer) make a
+table-dependent pattern FSG_E_UNSUPPORTED.  Usage: python scripts/gen_unicode.py"""
 import os
 import sys
 import unicodedata
@@ -255,6 +257,49 @@ def main():
     lines.append("  }")
     lines.append("  return 0;")
     lines.append("}")
+    # version-uncertain code points: General_Category differs between this
+    # image's unicodedata and the regex module's UCD (every code point assigned
+    # after unicodedata's version, plus gc changes such as U+0295 Ll -> Lo).
+    # regex-filter emulates regex-syntax 0.6.27 (Unicode 14), filter_regex
+    # regex-syntax 0.7.1 (Unicode 15); neither version's tables are in the
+    # image, so a table-dependent pattern meeting one of these code points is
+    # FSG_E_UNSUPPORTED (device and oracle alike) rather than a guess
+    allc = "".join(chr(c) for c in range(0x110000))
+    rgc = ["Cn"] * 0x110000
+    for k in CATS:
+        for m in regex.finditer(r"\p{gc=%s}" % k, allc):
+            rgc[m.start()] = k
+    newer = ranges(lambda c: rgc[c] != cat[c])
+    arr("newer", newer)
+    lines.append("static const uint32_t fsg_u_newer_n = %d;" % len(newer))
+    lines.append("/* 1: code point cp is version-uncertain (fsg_u_newer) */")
+    lines.append("static int fsg_u_is_newer(uint32_t cp) {")
+    lines.append("  uint32_t lo = 0, hi = fsg_u_newer_n;")
+    lines.append("  while (lo < hi) {")
+    lines.append("    const uint32_t m = (lo + hi) / 2;")
+    lines.append("    if (cp < fsg_u_newer[m].lo) hi = m;")
+    lines.append("    else if (cp > fsg_u_newer[m].hi) lo = m + 1;")
+    lines.append("    else return 1;")
+    lines.append("  }")
+    lines.append("  return 0;")
+    lines.append("}")
+    lines.append("""/* a normalized \\p{..} name neither fsg_u_property nor fsg_u_lookup resolves,
+ * as regex-syntax's unicode.rs canonicalizes it: 1 a property it supports that
+ * is not restated here (Age values, Changes_When_NFKC_Casefolded:
+ * FSG_E_UNSUPPORTED), 2 a known enumerated property with an unknown value
+ * ("Unicode property value not found"), 3 anything else, a Unicode 16+ script
+ * included ("Unicode property not found") */
+static int fsg_u_unresolved(const char *name) {
+  static const char *const enumerated[] = {"gc", "generalcategory", "sc", "script", "scx", "scriptextensions",
+                                           "gcb", "graphemeclusterbreak", "wb", "wordbreak", "sb", "sentencebreak"};
+  const char *eq = strchr(name, '=');
+  if (!eq) return (!strcmp(name, "cwkcf") || !strcmp(name, "changeswhennfkccasefolded")) ? 1 : 3;
+  const size_t pl = (size_t)(eq - name);
+  if (pl == 3 && !strncmp(name, "age", 3)) return 1;
+  for (size_t i = 0; i < sizeof enumerated / sizeof enumerated[0]; i++)
+    if (strlen(enumerated[i]) == pl && !strncmp(name, enumerated[i], pl)) return 2;
+  return 3;
+}""")
     lines.append("typedef struct { const char *name; const fsg_urange *r; uint32_t n; } fsg_ucat;")
     lines.append("static const fsg_ucat fsg_u_cats[] = {" + ", ".join(
         '{"%s", fsg_u_%s, %d}' % (k, k, len(tabs[k])) for k in CATS) + "};")

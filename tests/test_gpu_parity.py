@@ -580,6 +580,30 @@ def test_unicode_word_boundaries(engine):
     check_batch(engine, chain, b.encode())
 
 
+def test_version_uncertain_code_points(engine):
+    """regex-filter emulates regex-syntax 0.6.27 (Unicode 14) and filter_regex
+    0.7.1 (Unicode 15); this build's tables are Unicode 13 (unicodedata) and
+    the regex module's newer UCD.  A table-dependent pattern (\\d \\w \\p,
+    (?i), Unicode \\b) meeting a code point whose class differs between them
+    (U+1FAE8, assigned in 15; U+0295, Ll -> Lo in 14) is FSG_E_UNSUPPORTED on
+    the GPU and in the oracle; literal / '.' patterns decide it."""
+    b = P.Batch()
+    for v in ("abc", "café", "x \U0001FAE8 y", "zz ʕ"):
+        b.add_record(P.Record.new(v))
+    for pat in (r"\w+é", r"\d", r"(?i)ZZ", r"\p{Ll}", r"\bq"):
+        chain = [("regex-filter", {"regex": pat}, None)]
+        with pytest.raises(Unsupported):
+            gpu_chain(engine, chain).process_batch(b.encode())
+        check_batch(engine, chain, b.encode())
+    for pat in (r"zz", r"é", r"x . y", r"[^a]"):
+        check_batch(engine, [("regex-filter", {"regex": pat}, None)], b.encode())
+    # a \p name regex-syntax rejects (a Unicode 16 script): the regex crate's error Display
+    with pytest.raises(SmartModuleInitError) as e:
+        gpu_chain(engine, [("regex-filter", {"regex": r"a\p{Garay}"}, None)])
+    assert str(e.value) == ("regex parse error:\n    a\\p{Garay}\n     ^^^^^^^^^\nerror: Unicode property not found"
+                            "\n\nSmartModule Init Error: \n")
+
+
 def test_unsupported_mid_stream_leaves_state(engine):
     """FSG_E_UNSUPPORTED in batch 1 of 3 (a (?-u) \\b on a non-ASCII value):
     the caller falls back and replays the input, so the aggregate accumulator
