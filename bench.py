@@ -446,11 +446,14 @@ def run_filter(ctx, name, nrec, cpu):
         out = chain.process_batch(raw)
         py_s = time.perf_counter() - t0
         assert len(out.raw) == n_out
+        chunks = chain.last_timings()["chunks"]
         res["e2e"] = {"value": recs * ctx.world / e2e, "unit": "records/s", "ms_per_step": e2e * 1e3,
                       "gbps_h2d_plus_d2h": (src.nbytes + n_out) / e2e / 1e9,
                       "includes": "fsg_chain_process_batch: H2D of the slice (pageable host memory), device "
-                                  "batch framing, the GPU process_batch, D2H of the output batch",
-                      "output_bytes": n_out, "python_binding_ms": py_s * 1e3}
+                                  "batch framing, the GPU process_batch, D2H of the output batch into host "
+                                  "memory; pipelined over `chunks` slice chunks (upload of one piece, processing "
+                                  "of chunk k, download of chunk k-1 overlap; 0 = serial)",
+                      "chunks": chunks, "output_bytes": n_out, "python_binding_ms": py_s * 1e3}
         del raw, out, src
     res["cpu_baseline"] = cpu.get(name)
     del rs, chain

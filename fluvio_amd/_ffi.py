@@ -29,7 +29,7 @@ FSG_E_INVALID_ARG = -105
 FSG_E_LOOKBACK = -106
 FSG_LOOKBACK_NONE, FSG_LOOKBACK_LAST, FSG_LOOKBACK_AGE = 0, 1, 2
 FSG_E_DEVICE = -200
-ABI_VERSION = 5  # include/fsg.h FSG_ABI_VERSION: the struct layouts below
+ABI_VERSION = 6  # include/fsg.h FSG_ABI_VERSION: the struct layouts below
 
 
 class fsg_param(ctypes.Structure):
@@ -75,7 +75,8 @@ class fsg_timings(ctypes.Structure):
                 ("crc_ms", ctypes.c_float), ("total_ms", ctypes.c_float), ("in_bytes", ctypes.c_uint64),
                 ("out_bytes", ctypes.c_uint64), ("n_batches", ctypes.c_uint64),
                 ("n_records_in", ctypes.c_uint64), ("eval_path", ctypes.c_uint32), ("deferred", ctypes.c_uint32),
-                ("text_ms", ctypes.c_float), ("order_ms", ctypes.c_float)]
+                ("text_ms", ctypes.c_float), ("order_ms", ctypes.c_float), ("chunks", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
 
 
 VP = ctypes.c_void_p

@@ -513,7 +513,7 @@ __global__ __launch_bounds__(kArrT) void k_arr_write(ArrWriteArgs a) {
     const uint32_t b = (uint32_t)p.first + j;
     const BatchStat bs = a.bstat[b];
     if (!(bs.flags & BF_ARR_LEAN)) continue;  // written by k_write (the exact kernel's descriptors)
-    const int64_t rel = a.seg ? 0 : a.bstat[p.first].base_offset - bs.base_offset;
+    const int64_t rel = a.seg ? 0 : p.base_offset - bs.base_offset;
     uint8_t rv[16];
     const uint32_t vr = venc(rel, rv);
     const uint64_t G = (uint64_t)(uintptr_t)a.out + (a.seg ? 61ull * (uint64_t)(b + 1) + a.pre[b].rec_bytes

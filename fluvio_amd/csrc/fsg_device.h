@@ -245,7 +245,12 @@ struct Mins {
   uint32_t first_dec;
   uint32_t first_unsup;
   uint32_t cut;
-  uint32_t pad[3];
+  // a continuation (fsg_chain_process_batch's pipelined chunks): the output
+  // batch was started by an earlier chunk, so every batch of this one counts
+  // from its first (first_keep = 0) and records rebase to carry_base; carry =
+  // that batch's compression bits, 0xFFFFFFFF (the 0xFF fill) = none
+  uint32_t carry;
+  int64_t carry_base;
 };
 
 struct Plan {
@@ -266,7 +271,7 @@ struct Plan {
   int32_t acc_touched;       // accumulator changed by this call
   int32_t done;              // last batch whose process() call completed (-1 none): state commits through it
   int32_t comp;              // compression bits of the first surviving batch (set_compression, batch.rs:144-153)
-  int32_t pad_;
+  int32_t nonempty;          // batches of [first, last] with records (each adds 4 to records.write_size)
   uint64_t cat_final;        // aggregate (concat): accumulator bytes appended through the stop batch
 };
 
@@ -343,6 +348,7 @@ struct WriteArgs {
   uint32_t seg;            // 1: segment output: batch b's records at 61 * (b + 1) + pre[b], rel = 0
   int32_t first, last;     // plan.first / plan.last as the host read them (k_write_lean: no plan load
                            // ahead of the batch rows)
+  int64_t base;            // plan.base_offset as the host read it: records rebase to it (batch.rs:95-100)
 };
 // k_arr_write: the output records of the BF_ARR_LEAN batches of [plan.first,
 // plan.last], re-walked from the source window (fsg_array.hip)

@@ -1486,7 +1486,8 @@ __device__ __forceinline__ void size_batch(const SizeArgs& a, uint32_t b) {
   row.agg = st.agg_sum;
   row.cat = st.cat_sum;
   if (f != 0xFFFFFFFFu && b >= f && !(st.flags & BF_DECODE)) {
-    const int64_t rel = a.seg ? 0 : a.bstat[f].base_offset - st.base_offset;
+    const int64_t first_base = a.mins->carry != 0xFFFFFFFFu ? a.mins->carry_base : a.bstat[f].base_offset;
+    const int64_t rel = a.seg ? 0 : first_base - st.base_offset;
     const int32_t agg_base = a.agg_pre ? (int32_t)((uint64_t)a.acc0 + (uint64_t)a.agg_pre[b].agg) : 0;
     const uint64_t cat_base = a.agg_pre ? a.acc_len + a.agg_pre[b].cat : 0;
     uint64_t sum = 0;
@@ -1716,8 +1717,11 @@ __device__ __forceinline__ void plan_run(const PlanArgs& a) {
   if (err) p.err_batch = (int32_t)e;
   if (f != NONE && f <= stop) {
     p.first = (int32_t)f;
-    p.base_offset = a.bstat[f].base_offset;  // set before the max_bytes check (batch.rs:85-91)
-    p.comp = (int32_t)a.bstat[f].comp;       // set_compression of the first surviving batch
+    // set before the max_bytes check (batch.rs:85-91); set_compression of the
+    // first surviving batch — a continuation carries both from an earlier chunk
+    const bool carry = a.mins->carry != 0xFFFFFFFFu;
+    p.base_offset = carry ? a.mins->carry_base : a.bstat[f].base_offset;
+    p.comp = carry ? (int32_t)(a.mins->carry & 7u) : (int32_t)a.bstat[f].comp;
     if ((int64_t)f <= last) {
       p.last = (int32_t)last;
       const ScanRow rl = incl_at(a, (uint32_t)last);
@@ -1725,6 +1729,7 @@ __device__ __forceinline__ void plan_run(const PlanArgs& a) {
       p.lod = (int32_t)(-1 + (int64_t)(rl.lod - rf.lod));
       p.n_records = rl.nrec - rf.nrec;
       p.rec_bytes = rl.rec_bytes - rf.rec_bytes;
+      p.nonempty = (int32_t)(rl.nonempty - rf.nonempty);
     }
   }
   *a.plan = p;
@@ -2038,7 +2043,7 @@ constexpr int kWriteThreads = 256;
 __device__ __forceinline__ void write_batch(const WriteArgs& a, const Plan& p, int32_t b) {
   const uint32_t lane = lane_id();
   const BatchStat st = a.bstat[b];
-  const int64_t rel = a.seg ? 0 : a.bstat[p.first].base_offset - st.base_offset;
+  const int64_t rel = a.seg ? 0 : a.base - st.base_offset;
   const int32_t agg_base = a.agg_pre ? (int32_t)((uint64_t)a.acc0 + (uint64_t)a.agg_pre[b].agg) : 0;
   const uint64_t cat_base = a.agg_pre ? a.acc_len + a.agg_pre[b].cat : 0;
   const KeptRec* d = a.desc + a.rbase[b];
@@ -2134,7 +2139,7 @@ __device__ __forceinline__ void write_gen_body(const WriteArgs& a, uint32_t bid)
   const BatchStat st = a.bstat[b];
   const uint32_t nk = st.nkeep;
   if (!nk) return;
-  const int64_t rel = a.seg ? 0 : a.bstat[a.first].base_offset - st.base_offset;
+  const int64_t rel = a.seg ? 0 : a.base - st.base_offset;
   const int32_t agg_base = a.agg_pre ? (int32_t)((uint64_t)a.acc0 + (uint64_t)a.agg_pre[b].agg) : 0;
   const KeptRec* d = a.desc + a.rbase[b];
   const uint64_t obase = a.seg ? 61ull * (uint64_t)(b + 1) + a.pre[b].rec_bytes
@@ -2243,7 +2248,7 @@ __global__ __launch_bounds__(kWriteThreads) void k_write_canon(WriteArgs a) {
   if (!st.pad || !st.nkeep) return;
   const KeptRec* d = a.desc + a.rbase[b];
   if (d[0].mode != KM_ARRAY) return;
-  const int64_t rel = a.seg ? 0 : a.bstat[p.first].base_offset - st.base_offset;
+  const int64_t rel = a.seg ? 0 : a.base - st.base_offset;
   const uint64_t obase = a.seg ? 61ull * (uint64_t)(b + 1) + a.pre[b].rec_bytes
                                : 61 + (a.pre[b].rec_bytes - a.pre[p.first].rec_bytes);
   write_array_batch<true>(a, d, st.nkeep, rel, obase);
@@ -3325,7 +3330,7 @@ __global__ __launch_bounds__(kWlThreads) void k_write_lean(WriteArgs a) {
   if (a.first < 0 || b > a.last) return;
   const uint32_t t = threadIdx.x, lane = t & 63u;
   const BatchStat st = a.bstat[b];
-  const int64_t rel = a.seg ? 0 : a.bstat[a.first].base_offset - st.base_offset;
+  const int64_t rel = a.seg ? 0 : a.base - st.base_offset;
   const KeptRec* d = a.desc + a.rbase[b];
   const uint64_t obase = a.seg ? 61ull * (uint64_t)(b + 1) + a.pre[b].rec_bytes
                                : 61 + (a.pre[b].rec_bytes - a.pre[a.first].rec_bytes);
@@ -4102,7 +4107,7 @@ __global__ __launch_bounds__(kEvalThreads) void k_one(OneArgs o) {
   ONE_MARK(2);
   if (t == 0) {  // k_mins over the one batch
     const BatchStat st = a.bstat[0];
-    Mins m = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, {0, 0, 0}};
+    Mins m = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, -1};
     if (st.flags & BF_DECODE) m.first_dec = 0;
     if (st.flags & BF_UNSUPPORTED) m.first_unsup = 0;
     if (!(st.flags & BF_DECODE)) {
@@ -4155,6 +4160,7 @@ __global__ __launch_bounds__(kEvalThreads) void k_one(OneArgs o) {
     wa.pre = o.pre;
     wa.plan = o.plan;
     wa.out = o.out;
+    wa.base = p.base_offset;
     write_batch(wa, p, 0);
   }
   __threadfence_block();

@@ -356,6 +356,13 @@ bool parse_acc_map(const std::vector<uint8_t>& s, AccMap& m) {
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;  // owns p: no copies (a copy's destructor would free it)
+  DevBuf& operator=(const DevBuf&) = delete;
+  void swap(DevBuf& o) {
+    std::swap(p, o.p);
+    std::swap(cap, o.cap);
+  }
   ~DevBuf() {
     if (p) (void)hipFree(p);
   }
@@ -632,6 +639,17 @@ struct fsg_chain {
   hipEvent_t ev_order[2] = {};  // around a solo aggregate-json order walk
   fsg_timings last{};
   size_t out_len = 0;
+  // pipelined process_batch (process_pipelined): the host slice uploaded in
+  // pieces into pipe_in while chunks of it are processed; chunk outputs
+  // alternate between out and pipe_out, downloaded on pipe_dl beside the next
+  // chunk's processing
+  DevBuf pipe_in, pipe_out;
+  fsg_slice pipe_chunk;
+  PinBuf pipe_pin;
+  hipStream_t pipe_up = nullptr, pipe_dl = nullptr;
+  hipEvent_t pipe_ev[2] = {};
+  bool no_pipe = getenv("FSG_NO_PIPE") != nullptr;  // A/B: the serial H2D -> process -> D2H path
+  size_t pipe_bytes = getenv("FSG_PIPE_CHUNK") ? strtoull(getenv("FSG_PIPE_CHUNK"), nullptr, 10) : (size_t)256 << 20;
   ~fsg_chain() {
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
@@ -641,7 +659,11 @@ struct fsg_chain {
       if (e) (void)hipEventDestroy(e);
     for (auto& e : kd_ev)
       if (e) (void)hipEventDestroy(e);
+    for (auto& e : pipe_ev)
+      if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
+    if (pipe_up) (void)hipStreamDestroy(pipe_up);
+    if (pipe_dl) (void)hipStreamDestroy(pipe_dl);
   }
 };
 
@@ -1969,6 +1991,17 @@ int acc_update(fsg_chain* c, const Plan& p, bool cat) {
 }
 
 int run_composed(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics* m, fsg_batch_output* res);
+// one chunk of a pipelined fsg_chain_process_batch (process_pipelined): the
+// output batch an earlier chunk started (its base offset, compression bits)
+// and the max_bytes budget the earlier chunks used; out: the chunk output's
+// CRC32C over [21, out_len) (its own header, then its records)
+struct Carry {
+  bool cont = false;
+  int64_t base = -1;
+  int32_t comp = 0;
+  uint64_t spent = 0;
+  uint32_t crc = 0;
+};
 
 // the group's walks, once every chain has arrived (the last arrival launches)
 int group_launch(AjGroup* g) {
@@ -2046,7 +2079,7 @@ int group_order(fsg_chain* c, const AggjArgs* aj, hipStream_t st) {
 }
 
 int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics* m, fsg_batch_output* res,
-              bool empty_chain_io, SegOut* so = nullptr) {
+              bool empty_chain_io, SegOut* so = nullptr, Carry* cy = nullptr) {
   if (!c->segs.empty()) return run_composed(c, s, max_bytes, m, res);
   hipStream_t st = c->stream;
   const uint32_t nb = s->nb;
@@ -2084,6 +2117,15 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   const int64_t acc0 = has_agg && !has_cat && !has_aggj ? acc_value(c->acc) : 0;
 
   HIPCHK(hipMemsetAsync(c->mins.p, 0xFF, sizeof(Mins), st));
+  if (cy && cy->cont) {  // a continuation: every batch counts, records rebase to the carried base
+    Mins m0;
+    memset(&m0, 0xFF, sizeof m0);
+    m0.first_keep = 0;
+    m0.carry = (uint32_t)cy->comp & 7u;
+    m0.carry_base = cy->base;
+    HIPCHK(hipMemcpyAsync(c->mins.p, &m0, sizeof m0, hipMemcpyHostToDevice, st));
+  }
+  if (cy) max_bytes -= cy->spent;  // the budget the earlier chunks left (they stayed within it)
   if (c->timed) HIPCHK(hipEventRecord(c->ev[0], st));
   EvalArgs ea{};
   ea.slice = (const uint8_t*)s->data.p;
@@ -2521,6 +2563,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   wa.acc_len = sa.acc_len;
   wa.first = p.first;
   wa.last = p.last;
+  wa.base = p.base_offset;
   if (has_cat) {  // the accumulator stream: initial accumulator ++ appended values (k_cat)
     HIPCHK(c->cat.ensure(kCatOff + c->acc.size() + p.cat_final + 64));
     if (!c->acc.empty())
@@ -2631,6 +2674,11 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
     HIPCHK(hipMemcpyAsync((uint8_t*)c->hpin.p + kPinPlan, wa.out, out_len, hipMemcpyDeviceToHost, st));
   HIPCHK(wait_stream(st));
   c->out_len = out_len;
+  if (cy) {  // CRC32C of [21, out_len) as k_crc_final stored it (big-endian at 17)
+    uint8_t b4[4];
+    HIPCHK(hipMemcpy(b4, wa.out + 17, 4, hipMemcpyDeviceToHost));
+    cy->crc = (uint32_t)b4[0] << 24 | (uint32_t)b4[1] << 16 | (uint32_t)b4[2] << 8 | b4[3];
+  }
   // timings
   float t[5] = {0};
   if (c->timed)
@@ -2642,6 +2690,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   c->last.text_ms = t[2];
   c->last.total_ms = t[0] + t[1] + t[2] + t[3] + t[4];
   c->last.order_ms = 0;
+  c->last.chunks = 0;
   if (has_aggj && aj.n_rec) {  // the order walk alone (the group's launch for a group call: timed when its first chain is)
     AjGroup* g = c->group;
     if (g && g->timed && g->t0 && g->t1)
@@ -2879,28 +2928,31 @@ void copy_out(uint8_t* dst, const uint8_t* src, size_t n) {
 
 // device -> pinned chunk k (alternating buffers) -> caller memory: the DMA of
 // chunk k+1 runs while the host copies chunk k out of the other buffer
-hipError_t staged_download(fsg_chain* c, uint8_t* dst, const uint8_t* src, size_t n) {
-  hipError_t e = c->hstage.ensure(2 * kDlChunk);
+hipError_t staged_copy(PinBuf& pin, hipEvent_t* ev, hipStream_t st, uint8_t* dst, const uint8_t* src, size_t n) {
+  hipError_t e = pin.ensure(2 * kDlChunk);
   for (int k = 0; k < 2 && e == hipSuccess; k++)
-    if (!c->dl_ev[k]) e = hipEventCreateWithFlags(&c->dl_ev[k], hipEventDisableTiming);
+    if (!ev[k]) e = hipEventCreateWithFlags(&ev[k], hipEventDisableTiming);
   if (e != hipSuccess) return e;
-  uint8_t* buf[2] = {(uint8_t*)c->hstage.p, (uint8_t*)c->hstage.p + kDlChunk};
+  uint8_t* buf[2] = {(uint8_t*)pin.p, (uint8_t*)pin.p + kDlChunk};
   const size_t nch = (n + kDlChunk - 1) / kDlChunk;
   auto issue = [&](size_t k) -> hipError_t {
     const size_t off = k * kDlChunk, len = std::min(kDlChunk, n - off);
-    hipError_t r = hipMemcpyAsync(buf[k & 1], src + off, len, hipMemcpyDeviceToHost, c->stream);
-    return r == hipSuccess ? hipEventRecord(c->dl_ev[k & 1], c->stream) : r;
+    hipError_t r = hipMemcpyAsync(buf[k & 1], src + off, len, hipMemcpyDeviceToHost, st);
+    return r == hipSuccess ? hipEventRecord(ev[k & 1], st) : r;
   };
   for (size_t k = 0; k < std::min<size_t>(2, nch) && e == hipSuccess; k++) e = issue(k);
   for (size_t k = 0; k < nch && e == hipSuccess; k++) {
-    e = hipEventSynchronize(c->dl_ev[k & 1]);
+    e = hipEventSynchronize(ev[k & 1]);
     if (e != hipSuccess) break;
     const size_t off = k * kDlChunk;
     copy_out(dst + off, buf[k & 1], std::min(kDlChunk, n - off));
     if (k + 2 < nch) e = issue(k + 2);
   }
-  if (e != hipSuccess) (void)hipStreamSynchronize(c->stream);  // nothing left in flight into hstage
+  if (e != hipSuccess) (void)hipStreamSynchronize(st);  // nothing left in flight into the pinned chunks
   return e;
+}
+hipError_t staged_download(fsg_chain* c, uint8_t* dst, const uint8_t* src, size_t n) {
+  return staged_copy(c->hstage, c->dl_ev, c->stream, dst, src, n);
 }
 
 // the chain holding the output of the last call (a composed chain: its final segment)
@@ -3110,6 +3162,7 @@ int group_agg_fast(fsg_chain* const* chains, const fsg_slice* const* slices, siz
     wa.acc0 = J[k].pa.acc0;
     wa.first = p.first;
     wa.last = p.last;
+    wa.base = p.base_offset;
     J[k].out_len = out_len;
     const uint32_t nblk = p.last >= p.first && p.first >= 0 && p.n_records ? (uint32_t)(p.last - p.first + 1) : 0u;
     ow[k + 1] = ow[k] + nblk;
@@ -3268,9 +3321,370 @@ extern "C" int fsg_chain_output_device(fsg_chain* c0, const void** dptr, size_t*
   return FSG_OK;
 }
 
+
+// ---------------------------------------------------------------------------
+// Pipelined process_batch: for a host slice of at least two chunks, H2D of
+// the slice (64 MiB pieces, an upload thread on its own stream), processing of
+// chunk k (whole batches, framed on the device) and D2H of chunk k - 1's
+// records (a download thread: pinned pieces, copied out) overlap.  The output
+// is the one batch the serial path returns: chunk k > 0 continues the batch an
+// earlier chunk started (Mins::carry: records rebase to its base offset, the
+// max_bytes budget goes on), the host writes the 61-byte header, and the
+// CRC32C is combined from the chunks' (GF(2) shift of the CRC so far by the
+// next chunk's length).  Stateless chains of verbatim / uppercased /
+// projected records (their output stays within len + 10 B per record), and
+// only when the call wants the output; 1 = not taken.
+// ---------------------------------------------------------------------------
+uint32_t crc32c_host(const uint8_t* p, size_t n) {  // standard init / xorout, bitwise (a header's 40 bytes)
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; i++) {
+    c ^= p[i];
+    for (int k = 0; k < 8; k++) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+  }
+  return c ^ 0xFFFFFFFFu;
+}
+// a GF(2) 32 x 32 matrix (word k = the image of bit k) applied to v
+uint32_t gf2_apply(const uint32_t* mat, uint32_t v) {
+  uint32_t r = 0;
+  for (int k = 0; v; k++, v >>= 1)
+    if (v & 1u) r ^= mat[k];
+  return r;
+}
+void gf2_sq(uint32_t* out, const uint32_t* mat) {
+  for (int k = 0; k < 32; k++) out[k] = gf2_apply(mat, mat[k]);
+}
+// CRC32C of A ++ B from crc(A), crc(B) and |B|: crc(A) moved past |B| zero
+// bytes (the one-zero-bit operator squared up to bytes, then by the bits of
+// |B|), xor crc(B); the init / xorout terms cancel
+uint32_t crc32c_combine(uint32_t a, uint32_t b, uint64_t nb) {
+  if (nb == 0) return a ^ b;
+  uint32_t odd[32], even[32];
+  odd[0] = 0x82F63B78u;
+  for (int k = 1; k < 32; k++) odd[k] = 1u << (k - 1);
+  gf2_sq(even, odd);  // two zero bits
+  gf2_sq(odd, even);  // four
+  for (;;) {
+    gf2_sq(even, odd);  // eight, then 32, 128 ...
+    if (nb & 1) a = gf2_apply(even, a);
+    nb >>= 1;
+    if (!nb) break;
+    gf2_sq(odd, even);
+    if (nb & 1) a = gf2_apply(odd, a);
+    nb >>= 1;
+    if (!nb) break;
+  }
+  return a ^ b;
+}
+// the output batch header k_header writes (Batch::default() + base offset, lod, count)
+void host_header(uint8_t* h, int64_t base, uint64_t rec_bytes, int32_t comp, int32_t lod, uint64_t nrec) {
+  auto be = [&](int off, uint64_t v, int nb) {
+    for (int i = 0; i < nb; i++) h[off + i] = (uint8_t)(v >> (8 * (nb - 1 - i)));
+  };
+  be(0, (uint64_t)base, 8);
+  be(8, (uint32_t)(45 + 4 + rec_bytes), 4);
+  be(12, (uint32_t)-1, 4);
+  h[16] = 2;
+  be(17, 0, 4);
+  be(21, (uint32_t)comp & 7u, 2);
+  be(23, (uint32_t)lod, 4);
+  be(27, (uint64_t)-1, 8);
+  be(35, (uint64_t)-1, 8);
+  be(43, (uint64_t)-1, 8);
+  be(51, (uint16_t)-1, 2);
+  be(53, (uint32_t)-1, 4);
+  be(57, (uint32_t)nrec, 4);
+}
+
+bool pipe_eligible(const fsg_chain* c) {
+  if (c->no_pipe || !c->segs.empty() || c->agg_stage >= 0 || c->array_stage >= 0 || c->sf_stage >= 0) return false;
+  if ((c->hdesc.flags & (CF_AGG_JSON | CF_STATEFUL | CF_ARRAY | CF_AGG_SUM)) || c->hdesc.out_type == VT_I32) return false;
+  for (uint32_t k = 0; k < c->hdesc.nstages; k++) {
+    const uint32_t op = c->hdesc.st[k].op;
+    if (op != OP_CONTAINS && op != OP_REGEX && op != OP_FILTER_JSON && op != OP_MAP_UPPER && op != OP_PROJECT)
+      return false;
+  }
+  return true;
+}
+
+// chunk bytes [src, src + n) of the resident slice into `sl` (zero padding
+// behind them) and framed on the device; *fallback: the host walk would decide
+int load_chunk(fsg_engine* e, fsg_slice* sl, const uint8_t* src, size_t n, hipStream_t st, int* fallback) {
+  sl->verify_drain();
+  sl->v_pending = false;
+  sl->eng = e;
+  sl->len = n;
+  sl->rs_ok = false;
+  sl->nb = 0;
+  sl->nrec = 0;
+  sl->tail_status = 0;
+  sl->header_bytes = 0;
+  sl->device_framed = false;
+  sl->decompressed = false;
+  sl->has_pass = false;
+  const size_t alloc = slice_alloc(n);
+  HIPCHK(sl->data.ensure(alloc));
+  HIPCHK(hipMemsetAsync((uint8_t*)sl->data.p + (n & ~(size_t)15), 0, alloc - (n & ~(size_t)15), st));
+  HIPCHK(hipMemcpyAsync(sl->data.p, src, n, hipMemcpyDeviceToDevice, st));
+  int rc = frame_on_device(sl, st, fallback);
+  if (rc) return rc;
+  sl->device_framed = !*fallback;
+  HIPCHK(sl->bpos.ensure(8));
+  HIPCHK(sl->rbase.ensure(8));
+  return FSG_OK;
+}
+
+int process_pipelined(fsg_chain* c, const uint8_t* s, size_t len, uint64_t max_bytes, fsg_metrics* m,
+                      fsg_batch_output** out) {
+  const size_t C = std::max<size_t>(c->pipe_bytes, 1 << 16);
+  if (!out || len < 2 * C || !pipe_eligible(c)) return 1;
+  constexpr size_t kPiece = 64u << 20;
+  const int dev = c->eng->device;
+  hipStream_t st = c->stream;
+  if (!c->pipe_up) HIPCHK(hipStreamCreateWithFlags(&c->pipe_up, hipStreamNonBlocking));
+  if (!c->pipe_dl) HIPCHK(hipStreamCreateWithFlags(&c->pipe_dl, hipStreamNonBlocking));
+  HIPCHK(c->pipe_in.ensure(len + 64));
+  // the output: header + records within len + 10 B per record (>= 7 B each)
+  const size_t bound = 61 + len + 10 * (len / 7) + 64;
+  uint8_t* h = host_alloc(bound);
+  if (!h) return fail(FSG_E_DEVICE, "host allocation failed");
+  // upload thread: pieces in order, progress = bytes resident
+  std::mutex mu;
+  std::condition_variable cv;
+  size_t up_done = 0;
+  bool up_fin = false, stop = false;
+  hipError_t up_err = hipSuccess;
+  uint8_t* big = c->pipe_in.as<uint8_t>();
+  std::thread up([&] {
+    hipError_t e = hipSetDevice(dev);
+    for (size_t off = 0; off < len && e == hipSuccess; off += kPiece) {
+      {
+        std::lock_guard<std::mutex> g(mu);
+        if (stop) break;
+      }
+      const size_t n = std::min(kPiece, len - off);
+      e = hipMemcpyAsync(big + off, s + off, n, hipMemcpyHostToDevice, c->pipe_up);
+      if (e == hipSuccess) e = hipStreamSynchronize(c->pipe_up);
+      std::lock_guard<std::mutex> g(mu);
+      if (e == hipSuccess) up_done = off + n;
+      cv.notify_all();
+    }
+    std::lock_guard<std::mutex> g(mu);
+    up_err = e;
+    up_fin = true;
+    cv.notify_all();
+  });
+  // download thread: jobs (device records -> h + offset) in order
+  struct Job {
+    const uint8_t* src;
+    uint8_t* dst;
+    size_t n;
+  };
+  std::vector<Job> jobs;
+  size_t dl_next = 0, dl_done = 0;
+  bool dl_quit = false;
+  hipError_t dl_err = hipSuccess;
+  std::thread dl([&] {
+    hipError_t e = hipSetDevice(dev);
+    for (;;) {
+      Job j;
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return dl_next < jobs.size() || dl_quit; });
+        if (dl_next >= jobs.size()) break;
+        j = jobs[dl_next++];
+      }
+      if (e == hipSuccess && j.n) e = staged_copy(c->pipe_pin, c->pipe_ev, c->pipe_dl, j.dst, j.src, j.n);
+      std::lock_guard<std::mutex> g(mu);
+      dl_done++;
+      if (e != hipSuccess) dl_err = e;
+      cv.notify_all();
+    }
+  });
+  auto finish = [&]() {  // both threads drained and joined (every exit path)
+    {
+      std::lock_guard<std::mutex> g(mu);
+      stop = true;
+      dl_quit = true;
+    }
+    cv.notify_all();
+    up.join();
+    dl.join();
+  };
+  fsg_metrics mloc{};
+  Carry cy;
+  fsg_batch_output res{};
+  uint64_t rec_total = 0, nrec_total = 0, in_bytes = 0;
+  int32_t lod = -1, comp = 0;
+  int64_t base = -1;
+  uint32_t crc_rec = 0;
+  size_t X = 0, want = std::min(len, C);
+  int rc = FSG_OK;
+  bool fell_back = false;
+  // chunk outputs alternate between two device buffers (c->out is the one
+  // run_slice writes; physical buffer `cur`); buf_job: the download reading each
+  const size_t NOJOB = ~(size_t)0;
+  size_t buf_job[2] = {NOJOB, NOJOB};
+  int cur = 0;
+  uint32_t nchunk = 0;
+  for (;;) {
+    {
+      std::unique_lock<std::mutex> g(mu);
+      cv.wait(g, [&] { return up_done >= want || up_fin; });
+      if (up_done < want) {
+        rc = fail(FSG_E_DEVICE, up_err != hipSuccess ? hipGetErrorString(up_err) : "upload stopped");
+        break;
+      }
+    }
+    bool last = want == len;
+    int fb = 0;
+    rc = load_chunk(c->eng, &c->pipe_chunk, big + X, want - X, st, &fb);
+    if (rc) break;
+    if (fb) {  // the host walk decides this slice (no magic 2, compressed batches): the serial path
+      fell_back = true;
+      break;
+    }
+    fsg_slice& cs = c->pipe_chunk;
+    const uint64_t E = cs.header_bytes;
+    if (!last && E < want - X) {
+      // framing stopped inside the chunk: a batch the chunk's end cuts (the
+      // full slice holds it: the next chunk starts there), or the framing
+      // failure the serial path meets at the same position
+      const size_t q = X + E, rem = len - q;
+      bool cut_batch = false;
+      if (rem >= 57) {
+        const int32_t bl = (int32_t)rd_be(s + q + 8, 4);
+        const int comp_q = (int)(rd_be(s + q + 21, 2) & 7);
+        if (bl >= 45 && rem - 57 >= (size_t)bl - 45) {
+          if (comp_q != 0) {  // compressed: the serial path decompresses it
+            fell_back = true;
+            break;
+          }
+          cut_batch = true;
+        }
+      }
+      if (cut_batch) {
+        cs.tail_status = 0;
+        if (E == 0) {  // no whole batch yet: a longer chunk
+          want = std::min(len, want + C);
+          continue;
+        }
+      } else {
+        last = true;
+      }
+    }
+    const int tgt = (int)(nchunk & 1u);
+    if (cur != tgt) {
+      c->out.swap(c->pipe_out);
+      cur = tgt;
+    }
+    if (buf_job[tgt] != NOJOB) {  // its previous chunk's records are downloaded first
+      std::unique_lock<std::mutex> g(mu);
+      cv.wait(g, [&] { return dl_done > buf_job[tgt]; });
+      buf_job[tgt] = NOJOB;
+    }
+    fsg_batch_output rk{};
+    rc = run_slice(c, &cs, max_bytes, &mloc, &rk, c->hdesc.nstages == 0, nullptr, &cy);
+    in_bytes += cs.header_bytes;
+    if (rc) {
+      free_error(rk.error);
+      break;
+    }
+    nchunk++;
+    const Plan p = c->hplan;
+    if (p.first >= 0) {
+      if (!cy.cont) {
+        cy.cont = true;
+        cy.base = base = p.base_offset;
+        cy.comp = comp = p.comp;
+        lod = p.lod;
+      } else {
+        lod += p.lod + 1;
+      }
+      if (p.rec_bytes) {
+        uint8_t hc[61];
+        host_header(hc, p.base_offset, p.rec_bytes, p.comp, p.lod, p.n_records);
+        // the chunk's records: crc(header ++ records) with the header's CRC taken out
+        const uint32_t crc_k = crc32c_combine(crc32c_host(hc + 21, 40), cy.crc, p.rec_bytes);
+        crc_rec = rec_total ? crc32c_combine(crc_rec, crc_k, p.rec_bytes) : crc_k;
+        if (61 + rec_total + p.rec_bytes > bound) {
+          rc = fail(FSG_E_DEVICE, "pipelined output past its bound");
+          free_error(rk.error);
+          break;
+        }
+        {
+          std::lock_guard<std::mutex> g(mu);
+          jobs.push_back({c->out.as<uint8_t>() + 61, h + 61 + rec_total, p.rec_bytes});
+          buf_job[tgt] = jobs.size() - 1;
+        }
+        cv.notify_all();
+      }
+      rec_total += p.rec_bytes;
+      nrec_total += p.n_records;
+      cy.spent += p.rec_bytes + 4ull * (uint64_t)p.nonempty;
+    }
+    // an error batch, or the max_bytes cut (last < stop; at the chunk's last batch too)
+    const bool stopped = rk.has_error || p.stop + 1 < (int32_t)cs.nb || (p.first >= 0 && p.last < p.stop);
+    if (rk.has_error) {
+      res.has_error = 1;
+      res.error = rk.error;
+    } else {
+      free_error(rk.error);
+    }
+    if (stopped || last) break;
+    X += E;
+    want = std::min(len, X + C);
+  }
+  // the downloads before the header goes in
+  {
+    std::unique_lock<std::mutex> g(mu);
+    cv.wait(g, [&] { return dl_done >= jobs.size(); });
+  }
+  const hipError_t de = dl_err;
+  finish();
+  if (rc == FSG_OK && !fell_back && de != hipSuccess) rc = fail(FSG_E_DEVICE, hipGetErrorString(de));
+  if (rc != FSG_OK || fell_back) {
+    if (res.has_error) free_error(res.error);
+    host_free(h);
+    if (rc != FSG_OK) {  // a status error: the metrics of the batches before it stand, as on the serial path
+      if (m) {
+        m->bytes_in += mloc.bytes_in;
+        m->invocation_count += mloc.invocation_count;
+        m->records_out += mloc.records_out;
+      }
+      return rc;
+    }
+    return 1;  // nothing of this call is visible: the serial path runs it
+  }
+  host_header(h, base, rec_total, comp, lod, nrec_total);
+  const uint32_t crc = crc32c_combine(crc32c_host(h + 21, 40), crc_rec, rec_total);
+  h[17] = (uint8_t)(crc >> 24);
+  h[18] = (uint8_t)(crc >> 16);
+  h[19] = (uint8_t)(crc >> 8);
+  h[20] = (uint8_t)crc;
+  if (m) {
+    m->bytes_in += mloc.bytes_in;
+    m->invocation_count += mloc.invocation_count;
+    m->records_out += mloc.records_out;
+  }
+  c->out_len = 0;  // the device holds only the last chunk's output
+  c->last.chunks = nchunk;
+  c->last.in_bytes = in_bytes;
+  c->last.out_bytes = 61 + rec_total;
+  auto r = std::make_unique<fsg_batch_output>(res);
+  r->batch = h;
+  r->batch_len = 61 + rec_total;
+  r->base_offset = base;
+  r->last_offset_delta = lod;
+  r->n_records = (uint32_t)nrec_total;
+  *out = r.release();
+  return FSG_OK;
+}
+
 extern "C" int fsg_chain_process_batch(fsg_chain* c, const uint8_t* slice, size_t len, uint64_t max_bytes,
                                        fsg_metrics* m, fsg_batch_output** out) {
   HIPCHK(hipSetDevice(c->eng->device));
+  const int pr = process_pipelined(c, slice, len, max_bytes, m, out);
+  if (pr != 1) return pr;
   c->ingest.dec_limit = c->limit;
   int rc = upload_slice(c->eng, slice, len, &c->ingest, c->stream);
   if (rc) return rc;

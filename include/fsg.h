@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define FSG_ABI_VERSION 5 /* 5: fsg_timings gained text_ms / order_ms; 4: eval_path / deferred, fsg_keyed_*, fsg_host_cache_trim */
+#define FSG_ABI_VERSION 6 /* 6: fsg_timings gained chunks; 5: fsg_timings gained text_ms / order_ms; 4: eval_path / deferred, fsg_keyed_*, fsg_host_cache_trim */
 
 /* ---- status codes (mirror EngineError and the guest status enums) ---- */
 #define FSG_OK 0
@@ -165,6 +165,9 @@ typedef struct fsg_timings {
   uint32_t deferred;      /* batches that kernel handed to the exact kernel (non-ASCII, odd framing, ...) */
   float text_ms;          /* plan end to write start: aggregate texts, the aggregate-json order walk, the header */
   float order_ms;         /* the aggregate-json order walk kernel alone (a group call: the group's one launch) */
+  uint32_t chunks;        /* fsg_chain_process_batch pipelined over this many slice chunks (0: serial); the
+                             per-phase times and eval_path are then the last chunk's */
+  uint32_t reserved;
 } fsg_timings;
 #define FSG_EVAL_EXACT 0 /* k_eval over every batch */
 #define FSG_EVAL_LEAN 1  /* k_eval_lean (LDS windows), deferred batches through k_eval */

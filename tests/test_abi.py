@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _ffi.lib().fsg_abi_version() == _ffi.ABI_VERSION == 5
+    assert _ffi.lib().fsg_abi_version() == _ffi.ABI_VERSION == 6
 
 
 def test_gfx950_code_object_embedded():

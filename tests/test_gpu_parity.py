@@ -2311,3 +2311,41 @@ def test_int_path_taken_and_exact(engine, chain):
     rnd = random.Random(3)
     mixed = sl + _raw_batch(10 ** 6, _small_records(rnd, 900, bad_value=450, hi=999)) + _bad_tag_batch(2 * 10 ** 6)
     check_batch(engine, chain, mixed)
+
+
+PIPE_CHAINS = ["filter_init_timeout", "regex_ssn", "filter_json", "filter_project_map", "map", "empty"]
+
+
+def _pipe_slices():
+    """Host slices of many 48 KiB chunks: batches straddling chunk ends, a
+    batch larger than a chunk (a longer chunk), a leading run of batches no
+    filter keeps (the output batch starts in a later chunk), and a tail of
+    edge-case records (invalid UTF-8, odd JSON: errors in a late chunk)."""
+    logs = synth.make_slice(2, 1500) + synth.make_slice(2, 150, seed=5, base_offset=10_000, max_section=200_000) + \
+        synth.make_slice(2, 1500, seed=6, base_offset=20_000)
+    ints_first = synth.make_slice(3, 30_000, base_offset=0) + synth.make_slice(2, 1500, seed=8, base_offset=100_000)
+    edge_tail = synth.make_slice(2, 2000, seed=9) + synth.make_slice(4, 3000, base_offset=50_000)
+    return {"logs": logs, "ints_first": ints_first, "edge_tail": edge_tail}
+
+
+@pytest.mark.parametrize("name", PIPE_CHAINS)
+def test_pipelined_process_batch(engine, monkeypatch, name):
+    """fsg_chain_process_batch of a host slice larger than two chunks runs
+    pipelined (upload of piece k+1, processing of chunk k and download of chunk
+    k-1 overlap; chunk k > 0 continues the output batch an earlier chunk
+    started, the CRC32C combined on the host): the output batch, its header,
+    error and metrics equal the oracle's process_batch of the whole slice, for
+    an unlimited max_bytes and cuts in the first and in a later chunk."""
+    monkeypatch.setenv("FSG_PIPE_CHUNK", str(48 << 10))  # read when the chain is built
+    for key, sl in _pipe_slices().items():
+        for max_bytes in ((1 << 64) - 1, len(sl) // 3, 5000):
+            check_batch(engine, CHAINS[name], sl, max_bytes=max_bytes)
+        g = gpu_chain(engine, CHAINS[name])
+        try:
+            g.process_batch(sl)
+        except Exception:  # noqa: BLE001 (a status error: check_batch compared it)
+            continue
+        assert g.last_timings()["chunks"] >= 1, key
+    g = gpu_chain(engine, CHAINS[name])
+    g.process_batch(_pipe_slices()["logs"])
+    assert g.last_timings()["chunks"] > 4
