@@ -1314,7 +1314,15 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kK
 //                 defers the batch to k_eval.
 // The batch results (BatchStat, KeptRec) are those k_eval_lean writes.
 // ---------------------------------------------------------------------------
-constexpr int kFlatRounds = 8;  // 1 KiB rounds per wave in flight
+#ifndef FSG_FLAT_ROUNDS
+#define FSG_FLAT_ROUNDS 8
+#endif
+// a workgroup per 4 x kFlatRounds KiB (no cap: measured on MI355X, c2 eval
+// 1.142 -> 1.067 ms with the nontemporal loads below, against 4096 workgroups)
+#ifndef FSG_FLAT_GRID
+#define FSG_FLAT_GRID 1000000
+#endif
+constexpr int kFlatRounds = FSG_FLAT_ROUNDS;  // 1 KiB rounds per wave in flight
 __device__ __forceinline__ bool flat_verify(const uint8_t* s, uint64_t p, const uint8_t* nd, uint32_t m, bool upper) {
   for (uint32_t t = 0; t < m; t += 4) {
     uint32_t x = ld_u32_at(s + p + t);
@@ -1364,7 +1372,16 @@ __global__ __launch_bounds__(256) void k_flat_scan(EvalArgs a, uint32_t stage) {
 #pragma unroll
     for (int i = 0; i < kFlatRounds; i++) {  // every round's loads in flight before the first use
       const uint64_t c = (r0 + i) * 1024 + lane * 16;
+#ifndef FSG_FLAT_NO_NT  // streamed once: nontemporal, the later kernels' lines stay cached
+      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+      v[i] = make_uint4(0, 0, 0, 0);
+      if (r0 + i < nrounds) {
+        const v4u t = __builtin_nontemporal_load((const v4u*)(a.slice + c));
+        v[i] = make_uint4(t.x, t.y, t.z, t.w);
+      }
+#else
       v[i] = r0 + i < nrounds ? *(const uint4*)(a.slice + c) : make_uint4(0, 0, 0, 0);
+#endif
       if (!kLong) nx[i] = r0 + i < nrounds ? *(const uint32_t*)(a.slice + c + 16) : 0u;
     }
 #pragma unroll
@@ -2754,7 +2771,7 @@ void launch_eval_flat(const EvalArgs& a, uint32_t flat_st, hipStream_t s) {
   if (!a.nbatches) return;
   const uint32_t stage = flat_st & 0xFFu, m = flat_st >> 8;
   const uint64_t waves = (a.fbm_words + kFlatRounds - 1) / kFlatRounds;
-  const uint32_t g1 = (uint32_t)std::max<uint64_t>(std::min<uint64_t>((waves + 3) / 4, 4096), 1);
+  const uint32_t g1 = (uint32_t)std::max<uint64_t>(std::min<uint64_t>((waves + 3) / 4, FSG_FLAT_GRID), 1);
   const uint32_t g2 = (a.nbatches + 255) / 256;
   if (m >= 7) {
     hipLaunchKernelGGL(k_flat_scan<true>, dim3(g1), dim3(256), 0, s, a, stage);

@@ -213,6 +213,13 @@ void fsg_chain_builder_free(fsg_chain_builder *b);
 /* ---- chain ------------------------------------------------------------- */
 int fsg_chain_process(fsg_chain *c, const uint8_t *raw_records, size_t len, int64_t base_offset,
                       int64_t base_timestamp, fsg_metrics *metrics, fsg_output **out);
+/* process_batch over a host slice.  A slice of at least two chunks (256 MiB;
+ * FSG_PIPE_CHUNK bytes) through a stateless chain of filters / uppercase maps /
+ * projections, with `out` given, runs pipelined: the slice is uploaded in
+ * pieces on one thread while whole-batch chunks of it are processed and the
+ * previous chunk's records are downloaded on another; the result is the same
+ * one output batch (fsg_timings.chunks says how many chunks; the device copy
+ * of fsg_chain_output_device is then not kept).  FSG_NO_PIPE=1: serial. */
 int fsg_chain_process_batch(fsg_chain *c, const uint8_t *slice, size_t len, uint64_t max_bytes,
                             fsg_metrics *metrics, fsg_batch_output **out);
 /* look_back (engine.rs:187-218): for every stage with a look_back function
