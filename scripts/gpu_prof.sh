@@ -17,7 +17,7 @@ if [ -n "${3:-}" ]; then
   step tests $?
 fi
 if [ -n "${4:-}" ]; then
-  timeout -k 10 900 python -u bench.py > "$O/bench_full.log" 2>&1
+  timeout -k 10 900 python -u bench.py --detail "$O/bench_detail.json" > "$O/bench_full.log" 2>&1
   step bench_full $?
 fi
 for WL in $WLS; do
