@@ -646,10 +646,11 @@ struct fsg_chain {
   DevBuf pipe_in, pipe_out;
   fsg_slice pipe_chunk;
   PinBuf pipe_pin;
-  hipStream_t pipe_up = nullptr, pipe_dl = nullptr;
+  hipStream_t pipe_upv[4] = {}, pipe_dl = nullptr;
+  int pipe_up_threads = getenv("FSG_PIPE_UP") ? std::max(1, std::min(4, atoi(getenv("FSG_PIPE_UP")))) : 1;
   hipEvent_t pipe_ev[2] = {};
   bool no_pipe = getenv("FSG_NO_PIPE") != nullptr;  // A/B: the serial H2D -> process -> D2H path
-  size_t pipe_bytes = getenv("FSG_PIPE_CHUNK") ? strtoull(getenv("FSG_PIPE_CHUNK"), nullptr, 10) : (size_t)256 << 20;
+  size_t pipe_bytes = getenv("FSG_PIPE_CHUNK") ? strtoull(getenv("FSG_PIPE_CHUNK"), nullptr, 10) : (size_t)128 << 20;
   ~fsg_chain() {
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
@@ -662,7 +663,8 @@ struct fsg_chain {
     for (auto& e : pipe_ev)
       if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
-    if (pipe_up) (void)hipStreamDestroy(pipe_up);
+    for (auto& u : pipe_upv)
+      if (u) (void)hipStreamDestroy(u);
     if (pipe_dl) (void)hipStreamDestroy(pipe_dl);
   }
 };
@@ -3440,7 +3442,8 @@ int process_pipelined(fsg_chain* c, const uint8_t* s, size_t len, uint64_t max_b
   constexpr size_t kPiece = 64u << 20;
   const int dev = c->eng->device;
   hipStream_t st = c->stream;
-  if (!c->pipe_up) HIPCHK(hipStreamCreateWithFlags(&c->pipe_up, hipStreamNonBlocking));
+  for (int t = 0; t < c->pipe_up_threads; t++)
+    if (!c->pipe_upv[t]) HIPCHK(hipStreamCreateWithFlags(&c->pipe_upv[t], hipStreamNonBlocking));
   if (!c->pipe_dl) HIPCHK(hipStreamCreateWithFlags(&c->pipe_dl, hipStreamNonBlocking));
   HIPCHK(c->pipe_in.ensure(len + 64));
   // the output: header + records within len + 10 B per record (>= 7 B each)
@@ -3454,25 +3457,38 @@ int process_pipelined(fsg_chain* c, const uint8_t* s, size_t len, uint64_t max_b
   bool up_fin = false, stop = false;
   hipError_t up_err = hipSuccess;
   uint8_t* big = c->pipe_in.as<uint8_t>();
-  std::thread up([&] {
+  // (pieces k = t mod T on upload thread t, each on its own stream; up_done =
+  // the bytes of the resident prefix of pieces)
+  const int T = c->pipe_up_threads;
+  const size_t npieces = (len + kPiece - 1) / kPiece;
+  std::vector<uint8_t> pdone(npieces, 0);
+  size_t upk = 0;
+  int up_exited = 0;
+  auto upf = [&](int t) {
     hipError_t e = hipSetDevice(dev);
-    for (size_t off = 0; off < len && e == hipSuccess; off += kPiece) {
+    for (size_t k = (size_t)t; k < npieces && e == hipSuccess; k += (size_t)T) {
       {
         std::lock_guard<std::mutex> g(mu);
         if (stop) break;
       }
-      const size_t n = std::min(kPiece, len - off);
-      e = hipMemcpyAsync(big + off, s + off, n, hipMemcpyHostToDevice, c->pipe_up);
-      if (e == hipSuccess) e = hipStreamSynchronize(c->pipe_up);
+      const size_t off = k * kPiece, n = std::min(kPiece, len - off);
+      e = hipMemcpyAsync(big + off, s + off, n, hipMemcpyHostToDevice, c->pipe_upv[t]);
+      if (e == hipSuccess) e = hipStreamSynchronize(c->pipe_upv[t]);
       std::lock_guard<std::mutex> g(mu);
-      if (e == hipSuccess) up_done = off + n;
+      if (e == hipSuccess) {
+        pdone[k] = 1;
+        while (upk < npieces && pdone[upk]) upk++;
+        up_done = std::min(len, upk * kPiece);
+      }
       cv.notify_all();
     }
     std::lock_guard<std::mutex> g(mu);
-    up_err = e;
-    up_fin = true;
+    if (e != hipSuccess) up_err = e;
+    if (++up_exited == T) up_fin = true;
     cv.notify_all();
-  });
+  };
+  std::vector<std::thread> ups;
+  for (int t = 0; t < T; t++) ups.emplace_back(upf, t);
   // download thread: jobs (device records -> h + offset) in order
   struct Job {
     const uint8_t* src;
@@ -3507,7 +3523,7 @@ int process_pipelined(fsg_chain* c, const uint8_t* s, size_t len, uint64_t max_b
       dl_quit = true;
     }
     cv.notify_all();
-    up.join();
+    for (auto& u : ups) u.join();
     dl.join();
   };
   fsg_metrics mloc{};

@@ -213,7 +213,7 @@ void fsg_chain_builder_free(fsg_chain_builder *b);
 /* ---- chain ------------------------------------------------------------- */
 int fsg_chain_process(fsg_chain *c, const uint8_t *raw_records, size_t len, int64_t base_offset,
                       int64_t base_timestamp, fsg_metrics *metrics, fsg_output **out);
-/* process_batch over a host slice.  A slice of at least two chunks (256 MiB;
+/* process_batch over a host slice.  A slice of at least two chunks (128 MiB;
  * FSG_PIPE_CHUNK bytes) through a stateless chain of filters / uppercase maps /
  * projections, with `out` given, runs pipelined: the slice is uploaded in
  * pieces on one thread while whole-batch chunks of it are processed and the
