@@ -126,6 +126,7 @@ enum BatchFlags : uint32_t {
   BF_UNSUPPORTED = 4u, // input needs a feature the GPU path does not implement
   BF_LAST_STAGE = 8u,  // the error (if any) happened in the last stage -> records_out counted
   BF_ARR_LEAN = 16u,   // array_map batch of k_arr_lean: sized from ArrBatch, written by k_arr_write
+  BF_COMPACT = 32u,    // the batch's descriptors are 16-byte KeptC (k_eval_int's aggregate-sum batches)
 };
 
 // varint size with the encoder quirk (varint.rs:68-80)
@@ -214,6 +215,30 @@ struct KeptRec {
   uint8_t pad;         // KeepFlags
 };
 static_assert(sizeof(KeptRec) == 64, "KeptRec is one 64-byte line");
+// the compact descriptor of a generated-integer record without key or headers
+// and with 32-bit deltas (k_eval_int's aggregate-sum batches, BF_COMPACT): a
+// quarter of the KeptRec traffic its eval, size and write passes move; the
+// batch's KeptC array starts where its KeptRec array would
+struct KeptC {
+  int32_t od;
+  int32_t ts;
+  int32_t ival;
+  uint8_t mode;
+  uint8_t attr;
+  uint16_t pad;
+};
+static_assert(sizeof(KeptC) == 16, "KeptC is 16 bytes");
+__device__ __forceinline__ KeptRec kept_at(const KeptRec* d, uint32_t k, bool compact) {
+  if (!compact) return d[k];
+  const KeptC c = ((const KeptC*)d)[k];
+  KeptRec r = {};
+  r.od = c.od;
+  r.ts = c.ts;
+  r.ival = c.ival;
+  r.mode = c.mode;
+  r.attr = c.attr;
+  return r;
+}
 
 // one array_map output element: the source span of a JSON array element and
 // the length of its serde_json::to_string form.  The elements of a record with

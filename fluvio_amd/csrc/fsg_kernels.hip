@@ -1498,8 +1498,9 @@ __device__ __forceinline__ void size_batch(const SizeArgs& a, uint32_t b) {
       for (uint32_t L = 60 - vr < 50 ? 50 : 60 - vr; L <= 58; L++) sum += ab.cnt[L - 50];
     } else {
       const KeptRec* d = a.desc + a.rbase[b];
+      const bool compact = (st.flags & BF_COMPACT) != 0;
       for (uint32_t k = l; k < st.nkeep; k += 64) {
-        const KeptRec r = d[k];
+        const KeptRec r = kept_at(d, k, compact);
         sum += r.mode == KM_ARRAY ? array_rec_bytes(r, a.elem, rel) : rec_out_size(r, rel, agg_base, cat_base);
       }
       sum = wave_sum(sum);
@@ -2051,7 +2052,9 @@ __device__ __forceinline__ void write_batch(const WriteArgs& a, const Plan& p, i
                                : 61 + (a.pre[b].rec_bytes - a.pre[p.first].rec_bytes);
   uint8_t* out = a.out;
   if (st.flags & BF_ARR_LEAN) return;  // k_arr_write (fsg_array.hip)
-  if (st.nkeep && d[0].mode == KM_ARRAY) {  // a batch's descriptors share one mode
+  const bool compact = (st.flags & BF_COMPACT) != 0;
+  const uint8_t mode0 = st.nkeep ? (compact ? (uint8_t)KM_AGG : d[0].mode) : (uint8_t)0;
+  if (mode0 == KM_ARRAY) {  // a batch's descriptors share one mode
     write_array_batch<false>(a, d, st.nkeep, rel, obase);
     return;
   }
@@ -2062,7 +2065,7 @@ __device__ __forceinline__ void write_batch(const WriteArgs& a, const Plan& p, i
     KeptRec r = {};
     uint32_t sz = 0;
     if (v) {
-      r = d[k];
+      r = kept_at(d, k, compact);
       sz = rec_out_size(r, rel, agg_base, cat_base);
     }
     const uint64_t incl = wave_incl_scan((uint64_t)sz);
@@ -2105,7 +2108,7 @@ __device__ __forceinline__ void write_batch(const WriteArgs& a, const Plan& p, i
       for (uint32_t i = 0; i < n; i++) q[w++] = t[i];
     }
     // payloads: the chunk's keys, then its values, each spread over the wave
-    const bool cat = st.nkeep && (d[0].mode == KM_CONCAT || d[0].mode == KM_AGGJ);
+    const bool cat = mode0 == KM_CONCAT || mode0 == KM_AGGJ;
     if (__ballot(kl != 0u)) copy_segs(out, a.slice, kd, r.kpos, kl, false);
     copy_segs(out, cat ? a.cat : a.slice, vd, vsrc, vc, r.mode == KM_UPPER);
     run += readlane_u64(incl, 63);
@@ -2144,7 +2147,8 @@ __device__ __forceinline__ void write_gen_body(const WriteArgs& a, uint32_t bid)
   const KeptRec* d = a.desc + a.rbase[b];
   const uint64_t obase = a.seg ? 61ull * (uint64_t)(b + 1) + a.pre[b].rec_bytes
                                : 61 + (a.pre[b].rec_bytes - a.pre[a.first].rec_bytes);
-  const uint8_t mode0 = d[0].mode;  // a batch's descriptors share one mode
+  const bool compact = (st.flags & BF_COMPACT) != 0;
+  const uint8_t mode0 = compact ? (uint8_t)KM_AGG : d[0].mode;  // a batch's descriptors share one mode
   const uint32_t R = (nk + 255u) >> 8;
   const bool gen = (mode0 == KM_I32 || mode0 == KM_AGG) && R <= (uint32_t)kWgR && !(st.flags & BF_ARR_LEAN);
   Plan p = {};
@@ -2159,7 +2163,7 @@ __device__ __forceinline__ void write_gen_body(const WriteArgs& a, uint32_t bid)
   for (int i = 0; i < kWgR; i++) {
     sz[i] = 0;
     if (i < (int)R && k0 + i < nk) {
-      sz[i] = rec_out_size(d[k0 + i], rel, agg_base, 0);
+      sz[i] = rec_out_size(kept_at(d, k0 + i, compact), rel, agg_base, 0);
       mine += sz[i];
     }
   }
@@ -2178,7 +2182,7 @@ __device__ __forceinline__ void write_gen_body(const WriteArgs& a, uint32_t bid)
 #pragma unroll
   for (int i = 0; i < kWgR; i++) {
     if (!sz[i]) continue;
-    const KeptRec r = d[k0 + i];
+    const KeptRec r = kept_at(d, k0 + i, compact);
     const int32_t x = r.mode == KM_I32 ? r.ival : (int32_t)((uint32_t)agg_base + (uint32_t)r.ival);
     const uint32_t vl = dec_len_i32(x);
     const uint32_t inner = 1 + vsize(r.ts) + vsize(r.od + rel) + 1 +

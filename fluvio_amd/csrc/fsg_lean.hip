@@ -2614,6 +2614,7 @@ __device__ __forceinline__ void eval_int_body(const EvalArgs& a, uint32_t bid) {
   const uint32_t R = (count + 255u) >> 8;
   const uint32_t r0 = t * R;
   uint32_t keep = 0, kc = 0, asum = 0;
+  bool simple = true;  // every kept record fits a KeptC (no key, no headers, 32-bit deltas)
   int32_t xv[kIntR];
   const bool src_out = ch.out_type != VT_I32;
   // pass 1: fields, value, stages
@@ -2653,6 +2654,7 @@ __device__ __forceinline__ void eval_int_body(const EvalArgs& a, uint32_t bid) {
       keep |= 1u << i;
       kc++;
       if (kAgg) asum += (uint32_t)x;
+      simple = simple && r.tag == 0 && r.hdr == 0 && r.od == (int64_t)(int32_t)r.od && r.ts == (int64_t)(int32_t)r.ts;
     }
   }
   if (__syncthreads_or(!ok)) {  // the exact kernel takes the whole batch
@@ -2662,6 +2664,7 @@ __device__ __forceinline__ void eval_int_body(const EvalArgs& a, uint32_t bid) {
     }
     return;
   }
+  const bool compact = kAgg && __syncthreads_and(simple);
   // record-order prefixes: kept records, aggregate sum (wrapping)
   const uint32_t ik = wave_incl_scan(kc), ia = wave_incl_scan(asum);
   if (lane == 63) {
@@ -2686,6 +2689,17 @@ __device__ __forceinline__ void eval_int_body(const EvalArgs& a, uint32_t bid) {
     IntRec r;
     (void)int_rec(L.win, s, e, r);
     run += (uint32_t)xv[i];
+    if (compact) {
+      KeptC c;
+      c.od = (int32_t)r.od;
+      c.ts = (int32_t)r.ts;
+      c.ival = (int32_t)run;
+      c.mode = mode;
+      c.attr = r.attr;
+      c.pad = 0;
+      ((KeptC*)(a.desc + rb))[kbase + kn++] = c;
+      continue;
+    }
     KeptRec d;
     d.src = al + s;
     d.vpos = al + r.vs;
@@ -2709,7 +2723,7 @@ __device__ __forceinline__ void eval_int_body(const EvalArgs& a, uint32_t bid) {
     st.lod_in = (int32_t)rd_be(h + 23, 4);
     st.first_ts = (int64_t)rd_be(h + 27, 8);
     st.comp = (uint32_t)h[22] & 7u;
-    st.flags = BF_LAST_STAGE;
+    st.flags = BF_LAST_STAGE | (compact ? BF_COMPACT : 0u);
     st.nkeep = st.nout = L.wk[0] + L.wk[1] + L.wk[2] + L.wk[3];
     st.sec_len = (uint32_t)(sec_end - sec0);
     st.err_stage = 0xFFFFFFFFu;
