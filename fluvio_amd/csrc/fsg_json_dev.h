@@ -342,7 +342,7 @@ __device__ __noinline__ uint32_t json_canon(P s, uint32_t n, bool upper, uint8_t
   return c.run();
 }
 
-constexpr uint32_t kJsonFrames = 64;  // ignore_value frame stack: one u64 ('[' = 1, '{' = 0)
+constexpr uint32_t kJsonFrames = 256;  // ignore_value frame stack: four u64 words of bits ('[' = 1, '{' = 0)
 
 template <typename P>
 struct JsonDev {
@@ -776,10 +776,17 @@ struct JsonDev {
     return -1;
   }
 
-  // de.rs ignore_value (frames as a bit stack: 1 = '[', 0 = '{')
+  // de.rs ignore_value (frames as a bit stack: 1 = '[', 0 = '{'; serde keeps
+  // them in a Vec with no limit, here 256 levels in four words selected by
+  // value, not by an indexed array, so they stay in registers)
   __device__ __forceinline__ int ignore_value() {
-    uint64_t stk = 0;
+    uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
     uint32_t sn = 0;
+    auto top = [&](uint32_t n) -> int {
+      const uint32_t w = n >> 6;
+      const uint64_t x = w == 0 ? s0 : w == 1 ? s1 : w == 2 ? s2 : s3;
+      return ((x >> (n & 63)) & 1) ? '[' : '{';
+    };
     int enclosing = 0;
     for (;;) {
       const int peek_c = ws();
@@ -798,11 +805,12 @@ struct JsonDev {
         case '{':
           if (enclosing) {
             if (sn >= kJsonFrames) return fail_at(i, JE_DEEP);
-            const uint64_t bit = 1ull << sn;
-            if (enclosing == '[')
-              stk |= bit;
-            else
-              stk &= ~bit;
+            const uint64_t bit = 1ull << (sn & 63), set = enclosing == '[' ? bit : 0ull;
+            const uint32_t w = sn >> 6;
+            s0 = w == 0 ? (s0 & ~bit) | set : s0;
+            s1 = w == 1 ? (s1 & ~bit) | set : s1;
+            s2 = w == 2 ? (s2 & ~bit) | set : s2;
+            s3 = w == 3 ? (s3 & ~bit) | set : s3;
             sn++;
           }
           enclosing = 0;
@@ -820,7 +828,7 @@ struct JsonDev {
         accept_comma = true;
       } else if (sn) {
         sn--;
-        frame = ((stk >> sn) & 1) ? '[' : '{';
+        frame = top(sn);
         accept_comma = true;
       } else {
         return 0;
@@ -841,7 +849,7 @@ struct JsonDev {
         eat();
         if (!sn) return 0;
         sn--;
-        frame = ((stk >> sn) & 1) ? '[' : '{';
+        frame = top(sn);
         accept_comma = true;
       }
       if (frame == '{') {

@@ -31,7 +31,7 @@
  * (str_debug: Unicode escapes from this image's Unicode 13 categories and
  * Grapheme_Extend, parity unpinned for code points assigned later).
  * Outside the restatement (status ORC_E_UNSUPPORTED, mirrored by the GPU path):
- * an ignored value nested more than 64 levels below its first bracket.  (An
+ * an ignored value nested more than 256 levels below its first bracket.  (An
  * error text holding a NUL byte, from "unknown variant" of StructuredLog, is
  * carried with its length.)
  */
@@ -866,9 +866,9 @@ static int ignore_value(jde *d) {
       case '"': jeat(d); if (ignore_str(d)) goto out; break;
       case '[':
       case '{':
-        /* the device path keeps ignore_value's frames in a 256-entry bit stack:
-         * deeper nesting is outside both restatements */
-        if (enclosing && sn >= 64) {
+        /* the device path keeps ignore_value's frames in a 256-entry bit stack
+         * (serde's Vec has no limit): deeper nesting is outside both restatements */
+        if (enclosing && sn >= 256) {
           junsupported(d);
           goto out;
         }

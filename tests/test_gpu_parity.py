@@ -2349,3 +2349,25 @@ def test_pipelined_process_batch(engine, monkeypatch, name):
     g = gpu_chain(engine, CHAINS[name])
     g.process_batch(_pipe_slices()["logs"])
     assert g.last_timings()["chunks"] > 4
+
+
+def test_filter_json_deeply_nested_ignored_values(engine):
+    """serde_json skips a field StructuredLog does not name with ignore_value,
+    whose frame stack is a Vec with no depth limit (de.rs): on the GPU the
+    exact kernel keeps 256 levels of frames in registers (the round-5 stack had
+    64), so an ignored value nested 65..256 deep is decided like the oracle's
+    restatement (and its syntax errors found at the same position)."""
+    b = P.Batch()
+    for depth in (1, 63, 64, 65, 100, 128, 129, 200, 255, 256):
+        for opener, closer in (("[", "]"), ('{"a":', "}")):
+            inner = "1" if opener == "[" else "2"
+            v = '{"level":"warn","extra":' + opener * depth + inner + closer * depth + ',"message":"m"}'
+            b.add_record(P.Record.new(v.encode()))
+    for depth in (70, 250):  # unbalanced: the EOF / comma errors at the same byte
+        b.add_record(P.Record.new(('{"level":"error","x":' + "[" * depth + "1" + "]" * (depth - 1) + "}").encode()))
+    sl = b.encode()
+    check_batch(engine, CHAINS["filter_json"], sl)
+    # one record per batch, so each error stops only its own call
+    for depth in (65, 256):
+        check_batch(engine, CHAINS["filter_json"], _one_record_slice(
+            ('{"level":"info","extra":' + "[" * depth + "]" * depth + "}").encode()))
