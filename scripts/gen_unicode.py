@@ -216,6 +216,11 @@ static void fsg_u_fold_range(uint32_t lo, uint32_t hi, void (*add)(void *, uint3
     return lines
 
 
+def regex_version():
+    import regex
+    return regex.__version__
+
+
 def main():
     cat = [unicodedata.category(chr(c)) for c in range(0x110000)]
     oalpha = set()
@@ -228,7 +233,12 @@ def main():
              " * scripts from the Python regex module, simple case folding from str case mappings.  Do not edit. */",
              "#pragma once", "#include <stdint.h>", "#include <string.h>", "#include <stddef.h>",
              "typedef struct { uint32_t lo, hi; } fsg_urange;",
-             "#define FSG_UNICODE_VERSION \"%s\"" % unicodedata.unidata_version]
+             "#define FSG_UNICODE_VERSION \"%s\"" % unicodedata.unidata_version,
+             "/* binary properties, scripts, break properties: the Python regex module %s (Unicode 17 by its"
+             " assigned-character count); the reference: regex-syntax 0.6.27 (Unicode 14, regex-filter) and"
+             " 0.7.1 (Unicode 15, filter_regex) */" % regex_version(),
+             "#define FSG_UNICODE_PROPS_SOURCE \"regex %s\"" % regex_version(),
+             "#define FSG_UNICODE_REFERENCE \"14.0 (regex-syntax 0.6.27) / 15.0 (regex-syntax 0.7.1)\""]
     def arr(name, rs):
         body = ", ".join("{0x%X, 0x%X}" % r for r in rs)
         lines.append("static const fsg_urange fsg_u_%s[] = {%s};" % (name, body))
