@@ -126,6 +126,7 @@ enum BatchFlags : uint32_t {
   BF_UNSUPPORTED = 4u, // input needs a feature the GPU path does not implement
   BF_LAST_STAGE = 8u,  // the error (if any) happened in the last stage -> records_out counted
   BF_ARR_LEAN = 16u,   // array_map batch of k_arr_lean: sized from ArrBatch, written by k_arr_write
+  BF_ROWDONE = 64u,    // the flat decide wrote the batch's ScanRow for first_keep = 0 (k_size skips it then)
   BF_COMPACT = 32u,    // the batch's descriptors are 16-byte KeptC (k_eval_int's aggregate-sum batches)
 };
 
@@ -215,6 +216,14 @@ struct KeptRec {
   uint8_t pad;         // KeepFlags
 };
 static_assert(sizeof(KeptRec) == 64, "KeptRec is one 64-byte line");
+// output size of a verbatim kept record (KM_COPY / KM_UPPER) after the offset
+// fix-up: k_size's rec_out_size for those modes (the flat decides' rows)
+__device__ __forceinline__ uint32_t copy_out_size(const KeptRec& d, int64_t rel) {
+  const uint32_t inner = 1 + vsize(d.ts) + vsize(d.od + rel) + 1 +
+                         (d.has_key ? vsize((int64_t)d.klen) + d.klen : 0) + vsize((int64_t)d.vlen) + d.vlen +
+                         vsize(d.hdr);
+  return vsize((int64_t)inner) + inner;
+}
 // the compact descriptor of a generated-integer record without key or headers
 // and with 32-bit deltas (k_eval_int's aggregate-sum batches, BF_COMPACT): a
 // quarter of the KeptRec traffic its eval, size and write passes move; the
@@ -325,6 +334,7 @@ struct EvalArgs {
   unsigned long long* fbm;  // flat substring path (fsg_lean.hip): a bit per 16-byte chunk of the slice,
                             // per 1 KiB round the occurrence-start word then the bytes >= 0x80 word
   uint64_t fbm_words;
+  struct ScanRow* rows;     // the flat decides' rows for a first surviving batch 0 (BF_ROWDONE), nullptr: none
 };
 
 struct SizeArgs {

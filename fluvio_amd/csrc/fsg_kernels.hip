@@ -1474,6 +1474,8 @@ __device__ __forceinline__ void size_batch(const SizeArgs& a, uint32_t b) {
   const uint32_t l = lane_id();
   const BatchStat st = a.bstat[b];
   const uint32_t f = a.mins->first_keep;
+  // a flat decide already wrote this row for f = 0 (the offset fix-up against batch 0)
+  if ((st.flags & BF_ROWDONE) && f == 0 && a.mins->carry == 0xFFFFFFFFu && !a.seg && !a.agg_only) return;
   ScanRow row = {};
   if (a.agg_only) {
     row.agg = st.agg_sum;

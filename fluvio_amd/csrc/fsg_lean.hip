@@ -1521,6 +1521,9 @@ __global__ __launch_bounds__(256) void k_flat_decide(EvalArgs a, uint32_t stage)
   const unsigned long long* hi_bm = a.fbm + 1;
   const uint8_t* S = a.slice;
   const uint64_t pos = a.bpos[b];
+  // output sizes for a first surviving batch 0 (k_size skips BF_ROWDONE batches then)
+  const int64_t rel0 = (int64_t)rd_be(S + a.bpos[0], 8) - (int64_t)rd_be(S + pos, 8);
+  uint64_t rbytes = 0;
   const uint64_t nxt = b + 1 < a.nbatches ? a.bpos[b + 1] : a.slice_len;
   const uint64_t rb = a.rbase[b], rn = (b + 1 < a.nbatches ? a.rbase[b + 1] : a.nrec) - rb;
   const uint64_t al = pos & ~15ull;
@@ -1653,6 +1656,7 @@ __global__ __launch_bounds__(256) void k_flat_decide(EvalArgs a, uint32_t stage)
       d.has_key = tag;
       d.attr = attr;
       d.pad = 0;
+      rbytes += copy_out_size(d, rel0);
       a.desc[rb + nkeep++] = d;
     }
     q = end;
@@ -1672,6 +1676,17 @@ __global__ __launch_bounds__(256) void k_flat_decide(EvalArgs a, uint32_t stage)
   st.first_ts = (int64_t)rd_be(h + 27, 8);
   st.comp = (uint32_t)h[22] & 7u;
   st.flags = BF_LAST_STAGE;
+  if (a.rows) {
+    ScanRow row = {};
+    row.rec_bytes = rbytes;
+    row.nonempty = nkeep ? 1 : 0;
+    row.lod = (uint64_t)(int64_t)(st.lod_in + 1);
+    row.nrec = nkeep;
+    row.bytes_in = sec_len;
+    row.recs_out = nkeep;
+    a.rows[b] = row;
+    st.flags |= BF_ROWDONE;
+  }
   st.nkeep = st.nout = nkeep;
   st.sec_len = (uint32_t)sec_len;
   st.err_stage = 0xFFFFFFFFu;
@@ -2132,6 +2147,9 @@ __global__ __launch_bounds__(256) void k_rx_decide(EvalArgs a, uint32_t stage) {
   const unsigned long long* hi_bm = a.fbm + 1;
   const uint8_t* S = a.slice;
   const uint64_t pos = a.bpos[b];
+  // output sizes for a first surviving batch 0 (k_size skips BF_ROWDONE batches then)
+  const int64_t rel0 = (int64_t)rd_be(S + a.bpos[0], 8) - (int64_t)rd_be(S + pos, 8);
+  uint64_t rbytes = 0;
   const uint64_t nxt = b + 1 < a.nbatches ? a.bpos[b + 1] : a.slice_len;
   const uint64_t rb = a.rbase[b], rn = (b + 1 < a.nbatches ? a.rbase[b + 1] : a.nrec) - rb;
   const uint64_t al = pos & ~15ull;
@@ -2268,6 +2286,7 @@ __global__ __launch_bounds__(256) void k_rx_decide(EvalArgs a, uint32_t stage) {
       d.has_key = cur.tag;
       d.attr = cur.attr;
       d.pad = 0;
+      rbytes += copy_out_size(d, rel0);
       a.desc[rb + nkeep++] = d;
     }
   }
@@ -2285,6 +2304,17 @@ __global__ __launch_bounds__(256) void k_rx_decide(EvalArgs a, uint32_t stage) {
   st.first_ts = (int64_t)rd_be(h + 27, 8);
   st.comp = (uint32_t)h[22] & 7u;
   st.flags = BF_LAST_STAGE;
+  if (a.rows) {
+    ScanRow row = {};
+    row.rec_bytes = rbytes;
+    row.nonempty = nkeep ? 1 : 0;
+    row.lod = (uint64_t)(int64_t)(st.lod_in + 1);
+    row.nrec = nkeep;
+    row.bytes_in = sec_len;
+    row.recs_out = nkeep;
+    a.rows[b] = row;
+    st.flags |= BF_ROWDONE;
+  }
   st.nkeep = st.nout = nkeep;
   st.sec_len = (uint32_t)sec_len;
   st.err_stage = 0xFFFFFFFFu;
@@ -2343,6 +2373,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FSG_FJ_WPE)
   const unsigned long long* hit_bm = a.fbm;  // k_flat_scan<., kJson>: occurrence word w at [2 w]
   const uint8_t* S = a.slice;
   const uint64_t pos = a.bpos[b];
+  // output sizes for a first surviving batch 0 (k_size skips BF_ROWDONE batches then)
+  const int64_t rel0 = (int64_t)rd_be(S + a.bpos[0], 8) - (int64_t)rd_be(S + pos, 8);
+  uint64_t rbytes = 0;
   const uint64_t nxt = b + 1 < a.nbatches ? a.bpos[b + 1] : a.slice_len;
   const uint64_t rb = a.rbase[b], rn = (b + 1 < a.nbatches ? a.rbase[b + 1] : a.nrec) - rb;
   const uint64_t al = pos & ~15ull;
@@ -2478,6 +2511,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FSG_FJ_WPE)
       d.has_key = cur.tag;
       d.attr = cur.attr;
       d.pad = 0;
+      rbytes += copy_out_size(d, rel0);
       a.desc[rb + nkeep++] = d;
     }
   }
@@ -2495,6 +2529,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FSG_FJ_WPE)
   st.first_ts = (int64_t)rd_be(h + 27, 8);
   st.comp = (uint32_t)h[22] & 7u;
   st.flags = BF_LAST_STAGE;
+  if (a.rows) {
+    ScanRow row = {};
+    row.rec_bytes = rbytes;
+    row.nonempty = nkeep ? 1 : 0;
+    row.lod = (uint64_t)(int64_t)(st.lod_in + 1);
+    row.nrec = nkeep;
+    row.bytes_in = sec_len;
+    row.recs_out = nkeep;
+    a.rows[b] = row;
+    st.flags |= BF_ROWDONE;
+  }
   st.nkeep = st.nout = nkeep;
   st.sec_len = (uint32_t)sec_len;
   st.err_stage = 0xFFFFFFFFu;

@@ -2144,6 +2144,7 @@ int run_slice(fsg_chain* c, const fsg_slice* s, uint64_t max_bytes, fsg_metrics*
   ea.elem = (has_array || has_aggj) ? c->elem.as<ElemRec>() : nullptr;
   ea.arr_b = nullptr;
   ea.arr_bm = nullptr;
+  ea.rows = c->rows.as<ScanRow>();  // (rows is sized above; k_size fills what the flat decides leave)
   ea.nrec = s->nrec;
   uint32_t ops = 0;
   bool lean_stages = true;  // every stage has a lean form
