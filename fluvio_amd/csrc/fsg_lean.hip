@@ -988,6 +988,10 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kK
   // the previous batch's results, stored once the next window is in flight
   // (a store issued right before the wait for the next window would be waited for too)
   uint32_t p_b = 0xFFFFFFFFu;
+  // the regex variant also writes each batch's scan row (BF_ROWDONE); the
+  // others would spill for it (measured: 20 / 8 more bytes of scratch)
+  const bool kRows = kKind == 1 && a.rows != nullptr;
+  const int64_t base0 = kRows ? (int64_t)rd_be(a.slice + a.bpos[0], 8) : 0;  // batch 0's base offset
   bool p_defer = false, p_kept = false;
   uint64_t p_idx = 0;
   KeptRec p_d = {};
@@ -1004,6 +1008,8 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kK
       }
     } else {
       if (p_kept) a.desc[p_idx] = p_d;
+      // the batch's scan row for a first surviving batch 0 (k_size skips BF_ROWDONE batches then)
+      const uint64_t rbytes = kRows ? wave_sum((uint64_t)(p_kept ? copy_out_size(p_d, base0 - p_base) : 0u)) : 0ull;
       if (l == 0) {
         BatchStat st = {};
         st.base_offset = p_base;
@@ -1011,6 +1017,17 @@ __global__ __launch_bounds__(kLeanThreads) __attribute__((amdgpu_waves_per_eu(kK
         st.first_ts = p_ts0;
         st.comp = p_comp;
         st.flags = BF_LAST_STAGE;
+        if (kRows) {
+          ScanRow row = {};
+          row.rec_bytes = rbytes;
+          row.nonempty = p_nkeep ? 1 : 0;
+          row.lod = (uint64_t)(int64_t)(p_lod + 1);
+          row.nrec = p_nkeep;
+          row.bytes_in = p_sec;
+          row.recs_out = p_nkeep;
+          a.rows[p_b] = row;
+          st.flags |= BF_ROWDONE;
+        }
         st.nkeep = p_nkeep;
         st.nout = p_nkeep;
         st.sec_len = p_sec;
